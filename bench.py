@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched OR-Set join (lasp_orset:merge/2) on MI355X.
+
+Workload (BASELINE.json configs[1], SURVEY.md §8d cfg 2): per GPU, 2^20 replica pairs
+x 4096 element slots x 64 token slots, synthetic.  One step = one
+`laspj_orset_join` launch computing C = A ⊔ B over the whole batch (3 x 64 GiB
+resident in HBM).  Multi-GPU: one process per GPU, each joins its own replica shard
+(no data-path collective; weak scaling); a gloo barrier + max-over-ranks brackets the
+timed region.
+
+Output: one JSON line (rank 0).  `roofline.achieved` = 48 algorithmic bytes per
+(replica, element) join x cells per launch / average launch time measured with HIP
+events on the engine's stream; `roofline.traffic` = HBM bytes per launch from the
+rocprofv3 PMC passes committed under profiles/ (null if absent);  `cpu_baseline` =
+the C restatement of lasp_orset:merge/2 (oracle/laspj_oracle.c, kind "port") timed on
+this host's cores on a bounded sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "merged lattice elements/sec (node) + % HBM roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+BYTES_PER_JOIN = 48         # read 2 x 16 B cells, write 16 B
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--replicas", type=int, default=1 << 20, help="replica pairs per GPU")
+    ap.add_argument("--elements", type=int, default=4096)
+    ap.add_argument("--cpu-budget", type=float, default=12.0,
+                    help="seconds of CPU baseline work (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--nt", type=int, default=-1)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_join.json"),
+                    help="PMC summary giving HBM traffic per join launch")
+    return ap.parse_args()
+
+
+def host_cores() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))       # the GPU box grants 16 CPUs per GPU
+
+
+def cpu_baseline(elements: int, budget: float):
+    from oracle import columnar as orc    # cpu_baseline leg: the oracle is the timed port
+    cores = host_cores()
+    eps, merges, secs = orc.bench_orset_merge(elements, 2, cores, 2, budget)
+    return {
+        "value": eps, "unit": "merged elements/s", "cores": cores, "kind": "port",
+        "sample": (f"C restatement of lasp_orset:merge/2 (nested orddict two-finger merge, "
+                   f"20-byte tokens) on {cores} threads x 2 synthetic replica pairs "
+                   f"(E={elements}, T<=64), {merges} merges in {secs:.1f} s"),
+    }
+
+
+def load_traffic(path: str, replicas: int, elements: int):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("replicas") != replicas or d.get("elements") != elements:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+
+    from lasp_amd import engine
+    from lasp_amd._lib import TUNE_STREAM_GRID, TUNE_STREAM_NT, TUNE_STREAM_UNROLL
+
+    R, E = args.replicas, args.elements
+    ctx = engine.Context(local)
+    if args.grid:
+        ctx.set_tuning(TUNE_STREAM_GRID, args.grid)
+    if args.unroll:
+        ctx.set_tuning(TUNE_STREAM_UNROLL, args.unroll)
+    if args.nt >= 0:
+        ctx.set_tuning(TUNE_STREAM_NT, args.nt)
+    a, b, c = ctx.orset_batch(R, E), ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+    a.fill_synthetic(2, replica_base=rank * R)
+    b.fill_synthetic(3, replica_base=rank * R)
+    ctx.synchronize()
+
+    for _ in range(args.warmup):
+        c.join(a, b)
+    ctx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ev0, ev1 = ctx.event(), ctx.event()
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        c.join(a, b)
+    ev1.record()
+    ctx.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_ms(ev1) / args.steps
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    if rank != 0:
+        dist.barrier()
+        return
+
+    cells = R * E
+    ms_per_step = wall * 1000.0 / args.steps
+    value = cells * world / (wall / args.steps)
+    achieved = BYTES_PER_JOIN * cells / (kern_ms / 1000.0) / 1e9
+    traffic = load_traffic(args.pmc, R, E)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "merged elements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded splitmix64 replicas, DESIGN.md §5)",
+        "config": {
+            "workload": "batched OR-Set join lasp_orset:merge/2 (BASELINE configs[1])",
+            "replicas_per_gpu": R, "elements": E, "token_slots": 64,
+            "global_replicas": R * world, "parallelism": f"replica shards x{world}",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": BYTES_PER_JOIN * cells,
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

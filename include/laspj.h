@@ -1,0 +1,202 @@
+/*
+ * laspj.h — C ABI of the MI355X lattice-join engine (liblaspj.so).
+ *
+ * This is the drop-in boundary for Lasp's CRDT hot path.  In the reference every
+ * CRDT is an Erlang module dispatched as `Type:Fun(...)` (the riak_dt behaviour,
+ * SURVEY.md §8b); an Erlang NIF module that keeps those signatures binds exactly the
+ * entry points below (INTEGRATION.md shows the binding).  Each entry point cites the
+ * reference function it replaces (paths relative to the reference checkout).
+ *
+ * Conventions
+ *   - every function returns an int status: LASPJ_OK (0) or a negative LASPJ_E_*;
+ *     the message of the last failure on a context is laspj_ctx_last_error(ctx).
+ *     No C++ exception crosses this ABI.
+ *   - handles are opaque; sizes are explicit; no torch / HIP types in signatures.
+ *   - device work is enqueued on the context's own HIP stream and is asynchronous,
+ *     except *_download / *_upload and laspj_ctx_synchronize, which return after the
+ *     copy (resp. all queued work) has completed.  Results written to a laspj_buf are
+ *     valid after the next synchronising call on the same context.
+ *   - a context serialises its own calls with a mutex (many BEAM schedulers may call
+ *     one context); use one context per scheduler for concurrency.
+ *
+ * Data layout in HBM
+ *   OR-Set batch: R replicas x E element slots; per (replica, slot) one 16-byte cell
+ *     { uint64 p; uint64 r; } — bit k of p: token slot k of that element is present
+ *     in the replica's orddict; bit k of r: that token's removed flag is `true`.
+ *     r ⊆ p.  The element is present in the replica's orddict iff p != 0.
+ *     Replica-major: cell (i, e) at byte offset (i*E + e)*16.
+ *   G-Set batch: R replicas x W = ceil(E/64) uint64 words; bit e%64 of word e/64.
+ *   Element slots and token slots are dictionary positions owned by the host (the NIF
+ *   keeps the terms); every batch that meets in one call shares those dictionaries.
+ */
+#ifndef LASPJ_H
+#define LASPJ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LASPJ_ABI_VERSION 1
+
+/* status codes */
+#define LASPJ_OK               0
+#define LASPJ_E_INVAL         -1   /* bad argument / null handle (NIF: badarg)          */
+#define LASPJ_E_NOMEM         -2   /* device or host allocation failed                  */
+#define LASPJ_E_DEVICE        -3   /* HIP runtime / kernel error                         */
+#define LASPJ_E_SHAPE         -4   /* operand shapes do not agree (NIF: badarg)          */
+#define LASPJ_E_KIND          -5   /* OR-Set batch where a G-Set batch was expected ...  */
+#define LASPJ_E_RANGE         -6   /* replica / offset / byte range out of bounds        */
+#define LASPJ_E_COMM          -7   /* RCCL communicator error                            */
+#define LASPJ_E_UNSUPPORTED   -8   /* built without the feature                          */
+
+#define LASPJ_KIND_ORSET 1
+#define LASPJ_KIND_GSET  2
+
+typedef struct laspj_ctx   laspj_ctx;
+typedef struct laspj_buf   laspj_buf;
+typedef struct laspj_batch laspj_batch;
+typedef struct laspj_event laspj_event;
+typedef struct laspj_comm  laspj_comm;
+
+typedef struct laspj_batch_info {
+    int32_t  kind;               /* LASPJ_KIND_*                                       */
+    uint32_t elements;           /* E: element slots per replica                       */
+    uint64_t replicas;           /* R                                                  */
+    uint64_t bytes_per_replica;  /* 16*E (OR-Set) or 8*ceil(E/64) (G-Set)              */
+    uint64_t bytes;              /* R * bytes_per_replica                              */
+} laspj_batch_info;
+
+/* One update operation (lasp_orset:update/3, lasp_orset.erl:99-117;
+ * lasp_gset:update/3, lasp_gset.erl:84-88), applied by laspj_*_apply_ops. */
+#define LASPJ_OP_ADD     1  /* add / add_by_token: token slot `slot` of `element` := false */
+#define LASPJ_OP_REMOVE  2  /* remove: every token of `element` := true, or
+                               {error,{precondition,{not_present,E}}} if absent       */
+#define LASPJ_OP_FLAG_NEW_CALL 1  /* this op starts a new update/3 call; ops of one call
+                                     are all-or-nothing ({update, Ops}, remove_all)   */
+typedef struct laspj_op {
+    uint64_t replica;
+    uint32_t element;
+    uint8_t  kind;
+    uint8_t  slot;               /* token slot 0..63 (ADD on an OR-Set)                */
+    uint8_t  flags;
+    uint8_t  pad;
+} laspj_op;
+/* per-op status written by apply_ops */
+#define LASPJ_OPST_APPLIED   0
+#define LASPJ_OPST_NOT_PRESENT 1   /* this op's precondition failed; call rolled back */
+#define LASPJ_OPST_ROLLED_BACK 2   /* another op of the same call failed              */
+
+/* ------------------------------------------------------------------ library / context */
+int         laspj_abi_version(void);
+const char* laspj_strerror(int status);
+int         laspj_device_count(int* n);
+int         laspj_ctx_create(int device, laspj_ctx** out);
+int         laspj_ctx_destroy(laspj_ctx* ctx);
+const char* laspj_ctx_last_error(const laspj_ctx* ctx);
+int         laspj_ctx_synchronize(laspj_ctx* ctx);
+/* tuning knobs for the streaming kernels (bench sweeps); 0 = built-in default */
+#define LASPJ_TUNE_STREAM_GRID   1   /* workgroups for grid-stride streaming kernels    */
+#define LASPJ_TUNE_STREAM_UNROLL 2   /* 16-B cells per lane per iteration: 1,2,4,8      */
+#define LASPJ_TUNE_STREAM_NT     3   /* 1 = non-temporal loads/stores, 0 = default      */
+int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
+
+/* ------------------------------------------------------------------ device buffers */
+int      laspj_buf_create(laspj_ctx* ctx, uint64_t bytes, laspj_buf** out);
+int      laspj_buf_destroy(laspj_buf* buf);
+uint64_t laspj_buf_bytes(const laspj_buf* buf);
+int      laspj_buf_upload(laspj_ctx* ctx, laspj_buf* buf, uint64_t offset,
+                          const void* src, uint64_t bytes);
+int      laspj_buf_download(laspj_ctx* ctx, const laspj_buf* buf, uint64_t offset,
+                            void* dst, uint64_t bytes);
+
+/* ------------------------------------------------------------------ batches */
+/* lasp_orset:new/0 (lasp_orset.erl:63-65) for R replicas over E element slots */
+int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                             laspj_batch** out);
+/* lasp_gset:new/0 (lasp_gset.erl:70-72) */
+int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                            laspj_batch** out);
+int laspj_batch_destroy(laspj_batch* batch);
+int laspj_batch_info_get(const laspj_batch* batch, laspj_batch_info* out);
+/* host <-> device, replicas [first, first+count), host layout = device layout */
+int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* batch, uint64_t first, uint64_t count,
+                       const void* host);
+int laspj_batch_download(laspj_ctx* ctx, const laspj_batch* batch, uint64_t first,
+                         uint64_t count, void* host);
+/* every replica := new() */
+int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* batch);
+/* deterministic synthetic replicas (oracle/laspj_oracle.c restates it):
+ * replica i of the batch is synthetic replica (replica_base + i) of stream `seed` */
+int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed,
+                               uint64_t replica_base);
+
+/* ------------------------------------------------------------------ lasp_orset */
+/* merge/2 — lasp_orset.erl:128-134: dst[i] = a[i] ⊔ b[i]  (p|p', r|r').
+ * dst may alias a or b (the bind path merges in place, lasp_core.erl:300-303). */
+int laspj_orset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b);
+/* foldl(merge, new(), Replies) over groups of `group` consecutive replicas —
+ * lasp_update_fsm.erl:189-192 / lasp_bind_fsm.erl:185-188: dst[g] = ⊔ src[g*group+j] */
+int laspj_orset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       uint32_t group);
+/* value/1 — lasp_orset.erl:67-73: bit e of replica i set iff element e has a token
+ * with flag false.  out: R * ceil(E/64) uint64 words. */
+int laspj_orset_value(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
+/* value(removed, S) — lasp_orset.erl:90-95: elements with a token flagged true */
+int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
+/* stats/1 — lasp_orset.erl:156-192: per replica {element_count, adds_count,
+ * removes_count} as 3 uint64 (waste_pct = round(removes/(adds+removes)*100) host-side) */
+int laspj_orset_stats(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_counts);
+/* equal/2 — lasp_orset.erl:136-138: out[i] = (a[i] == b[i]) as one byte */
+int laspj_orset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                      laspj_buf* out);
+/* is_inflation/3 (strict = 0) — lasp_lattice.erl:97-98,153-161,277-285 — and
+ * is_strict_inflation/3 (strict = 1) — lasp_lattice.erl:105-106,235-253.
+ * prev has R replicas or 1 (broadcast); out[i] = one byte per cur replica.
+ * threshold_met(lasp_orset, V, T) (lasp_lattice.erl:72-75) is inflation(T, V). */
+int laspj_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                          int strict, laspj_buf* out);
+/* update/3 — lasp_orset.erl:99-117 (add_elem :222-230, remove_elem :232-241).
+ * ops: host array sorted by replica (stable within a replica); status: nops int32 */
+int laspj_orset_apply_ops(laspj_ctx* ctx, laspj_batch* batch, const laspj_op* ops,
+                          uint64_t nops, int32_t* status);
+/* union body for lasp_orset — lasp_core.erl:616-618: orddict:merge keep-left:
+ * dst[i][e] = (l[i][e].p != 0) ? l[i][e] : r[i][e] */
+int laspj_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                      const laspj_batch* r);
+/* filter body — lasp_core.erl:681-712: keep element e iff bit e of `keep` (the
+ * predicate F(X) evaluated once per element slot, ceil(E/64) words); tombstoned
+ * elements are kept like live ones. */
+int laspj_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       const laspj_buf* keep);
+
+/* ------------------------------------------------------------------ lasp_gset */
+/* merge/2 — lasp_gset.erl:99-101 (ordsets:union on canonical sets = OR) */
+int laspj_gset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                    const laspj_batch* b);
+int laspj_gset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      uint32_t group);
+/* stat(element_count) — lasp_gset.erl:135-136: one uint64 per replica */
+int laspj_gset_stats(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_counts);
+int laspj_gset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                     laspj_buf* out);
+/* is_inflation — lasp_lattice.erl:137-140; strict — :212-215 */
+int laspj_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                         int strict, laspj_buf* out);
+/* update/3 add / add_all — lasp_gset.erl:84-88 (LASPJ_OP_ADD only) */
+int laspj_gset_apply_ops(laspj_ctx* ctx, laspj_batch* batch, const laspj_op* ops,
+                         uint64_t nops, int32_t* status);
+
+/* ------------------------------------------------------------------ timing */
+int laspj_event_create(laspj_ctx* ctx, laspj_event** out);
+int laspj_event_destroy(laspj_event* ev);
+int laspj_event_record(laspj_ctx* ctx, laspj_event* ev);
+int laspj_event_elapsed_ms(laspj_event* start, laspj_event* stop, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LASPJ_H */

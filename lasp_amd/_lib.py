@@ -1,0 +1,131 @@
+"""ctypes binding of liblaspj.so (include/laspj.h).
+
+This is the Python stand-in for the Erlang NIF that would bind the same entry points
+(INTEGRATION.md).  It fails loudly: if the HIP library is missing or does not load,
+every caller gets LaspjUnavailable — there is no CPU fallback anywhere in lasp_amd.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblaspj.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "laspj.h")
+
+OK = 0
+E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
+    -1, -2, -3, -4, -5, -6, -7, -8)
+KIND_ORSET, KIND_GSET = 1, 2
+OP_ADD, OP_REMOVE = 1, 2
+OP_FLAG_NEW_CALL = 1
+OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK = 0, 1, 2
+TUNE_STREAM_GRID, TUNE_STREAM_UNROLL, TUNE_STREAM_NT = 1, 2, 3
+
+
+class LaspjUnavailable(RuntimeError):
+    """liblaspj.so is not built / not loadable: the engine has no fallback."""
+
+
+class LaspjError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"laspj status {status}: {msg}")
+        self.status = status
+
+
+class BatchInfo(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("elements", C.c_uint32), ("replicas", C.c_uint64),
+                ("bytes_per_replica", C.c_uint64), ("bytes", C.c_uint64)]
+
+
+class Op(C.Structure):
+    _fields_ = [("replica", C.c_uint64), ("element", C.c_uint32), ("kind", C.c_uint8),
+                ("slot", C.c_uint8), ("flags", C.c_uint8), ("pad", C.c_uint8)]
+
+
+vp = C.c_void_p
+vpp = C.POINTER(C.c_void_p)
+i = C.c_int
+u32 = C.c_uint32
+u64 = C.c_uint64
+
+# name -> (restype, argtypes); mirrors include/laspj.h one to one
+SIGNATURES = {
+    "laspj_abi_version": (i, []),
+    "laspj_strerror": (C.c_char_p, [i]),
+    "laspj_device_count": (i, [C.POINTER(i)]),
+    "laspj_ctx_create": (i, [i, vpp]),
+    "laspj_ctx_destroy": (i, [vp]),
+    "laspj_ctx_last_error": (C.c_char_p, [vp]),
+    "laspj_ctx_synchronize": (i, [vp]),
+    "laspj_ctx_set_tuning": (i, [vp, i, C.c_int64]),
+    "laspj_buf_create": (i, [vp, u64, vpp]),
+    "laspj_buf_destroy": (i, [vp]),
+    "laspj_buf_bytes": (u64, [vp]),
+    "laspj_buf_upload": (i, [vp, vp, u64, vp, u64]),
+    "laspj_buf_download": (i, [vp, vp, u64, vp, u64]),
+    "laspj_orset_batch_create": (i, [vp, u64, u32, vpp]),
+    "laspj_gset_batch_create": (i, [vp, u64, u32, vpp]),
+    "laspj_batch_destroy": (i, [vp]),
+    "laspj_batch_info_get": (i, [vp, C.POINTER(BatchInfo)]),
+    "laspj_batch_upload": (i, [vp, vp, u64, u64, vp]),
+    "laspj_batch_download": (i, [vp, vp, u64, u64, vp]),
+    "laspj_batch_clear": (i, [vp, vp]),
+    "laspj_batch_fill_synthetic": (i, [vp, vp, u64, u64]),
+    "laspj_orset_join": (i, [vp, vp, vp, vp]),
+    "laspj_orset_reduce": (i, [vp, vp, vp, u32]),
+    "laspj_orset_value": (i, [vp, vp, vp]),
+    "laspj_orset_removed": (i, [vp, vp, vp]),
+    "laspj_orset_stats": (i, [vp, vp, vp]),
+    "laspj_orset_equal": (i, [vp, vp, vp, vp]),
+    "laspj_orset_inflation": (i, [vp, vp, vp, i, vp]),
+    "laspj_orset_apply_ops": (i, [vp, vp, C.POINTER(Op), u64, C.POINTER(C.c_int32)]),
+    "laspj_orset_union": (i, [vp, vp, vp, vp]),
+    "laspj_orset_filter": (i, [vp, vp, vp, vp]),
+    "laspj_gset_join": (i, [vp, vp, vp, vp]),
+    "laspj_gset_reduce": (i, [vp, vp, vp, u32]),
+    "laspj_gset_stats": (i, [vp, vp, vp]),
+    "laspj_gset_equal": (i, [vp, vp, vp, vp]),
+    "laspj_gset_inflation": (i, [vp, vp, vp, i, vp]),
+    "laspj_gset_apply_ops": (i, [vp, vp, C.POINTER(Op), u64, C.POINTER(C.c_int32)]),
+    "laspj_event_create": (i, [vp, vpp]),
+    "laspj_event_destroy": (i, [vp]),
+    "laspj_event_record": (i, [vp, vp]),
+    "laspj_event_elapsed_ms": (i, [vp, vp, C.POINTER(C.c_float)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load liblaspj.so (built in-tree by __graft_entry__.build()) or raise."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LaspjUnavailable(
+            f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise LaspjUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.laspj_abi_version() != 1:
+        raise LaspjUnavailable("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(status: int, ctx=None) -> None:
+    if status != OK:
+        L = load()
+        msg = L.laspj_strerror(status).decode()
+        if ctx is not None:
+            detail = L.laspj_ctx_last_error(ctx)
+            if detail:
+                msg += f": {detail.decode()}"
+        raise LaspjError(status, msg)

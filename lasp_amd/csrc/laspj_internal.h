@@ -1,0 +1,101 @@
+// Internal definitions shared by the liblaspj translation units (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <string>
+
+#include "../../include/laspj.h"
+
+struct laspj_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    int cus = 256;
+    // tuning knobs (LASPJ_TUNE_*); 0 = default
+    int64_t tune_grid = 0;
+    int64_t tune_unroll = 0;
+    int64_t tune_nt = -1;
+    // device scratch for apply_ops (grown on demand)
+    void* scratch = nullptr;
+    uint64_t scratch_bytes = 0;
+};
+
+struct laspj_buf {
+    laspj_ctx* ctx = nullptr;
+    void* dev = nullptr;
+    uint64_t bytes = 0;
+};
+
+struct laspj_batch {
+    laspj_ctx* ctx = nullptr;
+    int32_t kind = 0;
+    uint32_t elements = 0;      // E
+    uint64_t replicas = 0;      // R
+    uint64_t words_per_replica = 0;  // u64 words: 2E (OR-Set) or ceil(E/64) (G-Set)
+    uint64_t* dev = nullptr;
+};
+
+struct laspj_event {
+    laspj_ctx* ctx = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+namespace laspj {
+
+int fail(laspj_ctx* ctx, int code, const char* fmt, ...);
+
+inline uint64_t bytes_of(const laspj_batch* b) { return b->replicas * b->words_per_replica * 8ull; }
+
+#define LJ_HIP(ctx, call)                                                              \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return ::laspj::fail((ctx), LASPJ_E_DEVICE, "%s: %s (%s:%d)", #call,        \
+                                 hipGetErrorString(e_), __FILE__, __LINE__);           \
+    } while (0)
+
+#define LJ_LAUNCHED(ctx)                                                               \
+    do {                                                                               \
+        hipError_t e_ = hipGetLastError();                                             \
+        if (e_ != hipSuccess)                                                          \
+            return ::laspj::fail((ctx), LASPJ_E_DEVICE, "kernel launch: %s (%s:%d)",   \
+                                 hipGetErrorString(e_), __FILE__, __LINE__);           \
+    } while (0)
+
+// Launch wrappers implemented in laspj_kernels.hip.  All take validated shapes.
+struct StreamTune {
+    int grid;
+    int unroll;
+    bool nt;
+};
+StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16);
+
+hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                     uint64_t words);
+hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                            uint64_t groups, uint32_t group, uint64_t words_per_replica);
+hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
+                                 uint64_t replica_base);
+hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
+                              bool removed);
+hipError_t launch_orset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out);
+hipError_t launch_gset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out);
+hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                        uint8_t* out);
+hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                  const laspj_batch* cur, bool strict, uint8_t* out);
+hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                 const laspj_batch* cur, bool strict, uint8_t* out);
+hipError_t launch_apply_ops(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops,
+                            uint64_t nops, int32_t* status);
+hipError_t launch_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                              const laspj_batch* r);
+hipError_t launch_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                               const uint64_t* keep);
+
+}  // namespace laspj

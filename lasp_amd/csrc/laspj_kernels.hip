@@ -1,0 +1,558 @@
+// CDNA4 (gfx950) kernels of the lattice-join engine.
+//
+// Everything on this path is integer/boolean and HBM-bound: no MFMA.
+// Design rules applied (cdna_hip_programming.md §6, MI355X_MICROARCH.md §HBM):
+//   * 16 B per lane per access (global_load/store_dwordx4): one wave-instruction moves
+//     1 KiB of consecutive bytes; cells are {p, r} u64 pairs so one load = one cell.
+//   * grid-stride loops over ~8 workgroups per CU with U cells in flight per lane,
+//     non-temporal loads/stores for once-touched streams (206 GB per join batch never
+//     fits the 256 MiB Infinity Cache).
+//   * per-replica predicates use one wave64 per replica: lanes walk the replica's
+//     cells with a 64-cell stride (coalesced), and the reduction is a __ballot or a
+//     __shfl_xor tree — no LDS, no __syncthreads.
+//
+// Layout (include/laspj.h): OR-Set cell (i, e) = words [2(iE+e), 2(iE+e)+1] = {p, r};
+// G-Set replica i = words [iW, (i+1)W), W = ceil(E/64).
+
+#include "laspj_internal.h"
+
+namespace laspj {
+
+typedef unsigned long long u64;
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kBlock = 256;
+
+template <bool NT>
+__device__ __forceinline__ u64x2 ld2(const u64x2* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st2(u64x2* p, u64x2 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ tuning
+
+StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16) {
+    StreamTune t;
+    t.grid = ctx->tune_grid > 0 ? (int)ctx->tune_grid : ctx->cus * 8;
+    t.unroll = ctx->tune_unroll > 0 ? (int)ctx->tune_unroll : 4;
+    t.nt = ctx->tune_nt < 0 ? true : ctx->tune_nt != 0;
+    uint64_t need = (n16 + kBlock - 1) / kBlock;
+    if (need < (uint64_t)t.grid) t.grid = need > 0 ? (int)need : 1;
+    return t;
+}
+
+static int wave_grid(const laspj_ctx* ctx, uint64_t items) {
+    // one wave per item, 4 waves per 256-thread block
+    uint64_t blocks = (items + 3) / 4;
+    uint64_t cap = (uint64_t)ctx->cus * 8;
+    if (blocks > cap) blocks = cap;
+    return blocks ? (int)blocks : 1;
+}
+
+// ------------------------------------------------------------------ join: d = a | b
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_or16(u64x2* d, const u64x2* a, const u64x2* b,
+                                                 uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        u64x2 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld2<NT>(a + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[u] = ld2<NT>(b + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st2<NT>(d + i + u * stride, x[u] | y[u]);
+    }
+    for (; i < n; i += stride) st2<NT>(d + i, ld2<NT>(a + i) | ld2<NT>(b + i));
+}
+
+__global__ void k_or_tail(u64* d, const u64* a, const u64* b, uint64_t idx) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) d[idx] = a[idx] | b[idx];
+}
+
+template <int U, bool NT>
+static void launch_or16_t(laspj_ctx* ctx, int grid, u64x2* d, const u64x2* a, const u64x2* b,
+                          uint64_t n) {
+    hipLaunchKernelGGL((k_or16<U, NT>), dim3(grid), dim3(kBlock), 0, ctx->stream, d, a, b, n);
+}
+
+template <bool NT>
+static void launch_or16_u(laspj_ctx* ctx, const StreamTune& t, u64x2* d, const u64x2* a,
+                          const u64x2* b, uint64_t n) {
+    switch (t.unroll) {
+        case 1: launch_or16_t<1, NT>(ctx, t.grid, d, a, b, n); break;
+        case 2: launch_or16_t<2, NT>(ctx, t.grid, d, a, b, n); break;
+        case 8: launch_or16_t<8, NT>(ctx, t.grid, d, a, b, n); break;
+        default: launch_or16_t<4, NT>(ctx, t.grid, d, a, b, n); break;
+    }
+}
+
+hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                     uint64_t words) {
+    uint64_t n16 = words / 2;
+    if (n16) {
+        StreamTune t = stream_tune(ctx, n16);
+        auto* d2 = reinterpret_cast<u64x2*>(dst);
+        auto* a2 = reinterpret_cast<const u64x2*>(a);
+        auto* b2 = reinterpret_cast<const u64x2*>(b);
+        if (t.nt) launch_or16_u<true>(ctx, t, d2, a2, b2, n16);
+        else launch_or16_u<false>(ctx, t, d2, a2, b2, n16);
+    }
+    if (words & 1)
+        hipLaunchKernelGGL(k_or_tail, dim3(1), dim3(64), 0, ctx->stream, (u64*)dst,
+                           (const u64*)a, (const u64*)b, words - 1);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ reduce over groups
+
+// dst replica g = OR_{j<group} src replica (g*group + j); vectorised over word pairs
+template <bool VEC2>
+__global__ __launch_bounds__(kBlock) void k_reduce_or(u64* dst, const u64* src, uint64_t groups,
+                                                      uint32_t group, uint64_t wr) {
+    const uint64_t per = VEC2 ? wr / 2 : wr;          // items per replica
+    const uint64_t n = groups * per;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t g = i / per, w = i - g * per;
+        uint64_t base = g * group * per + w;
+        if constexpr (VEC2) {
+            const u64x2* s = reinterpret_cast<const u64x2*>(src);
+            u64x2 acc = ld2<true>(s + base);
+            for (uint32_t j = 1; j < group; ++j) acc |= ld2<true>(s + base + j * per);
+            st2<true>(reinterpret_cast<u64x2*>(dst) + i, acc);
+        } else {
+            u64 acc = src[base];
+            for (uint32_t j = 1; j < group; ++j) acc |= src[base + j * per];
+            dst[i] = acc;
+        }
+    }
+}
+
+hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                            uint64_t groups, uint32_t group, uint64_t wr) {
+    bool vec2 = (wr % 2) == 0;
+    uint64_t n = groups * (vec2 ? wr / 2 : wr);
+    StreamTune t = stream_tune(ctx, n);
+    if (vec2)
+        hipLaunchKernelGGL((k_reduce_or<true>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           (u64*)dst, (const u64*)src, groups, group, wr);
+    else
+        hipLaunchKernelGGL((k_reduce_or<false>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           (u64*)dst, (const u64*)src, groups, group, wr);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ synthetic replicas
+// DESIGN.md §5; restated in oracle/laspj_oracle.c (orc_synth_*).
+
+__device__ __forceinline__ u64 sm64(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ u64 synth_replica_key(u64 seed, u64 grep) {
+    return sm64(sm64(seed ^ 0x4C41535000000000ull) ^ grep);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_orset(u64x2* cells, uint64_t R, uint32_t E,
+                                                       u64 seed, u64 base) {
+    const uint64_t n = R * E;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t rep = i / E;
+        uint32_t e = (uint32_t)(i - rep * E);
+        u64 h = synth_replica_key(seed, base + rep);
+        u64 x = sm64(h + (u64)e * 0xD1B54A32D192ED03ull);
+        u64 y = sm64(x ^ 0xA5A5A5A5A5A5A5A5ull);
+        u64 z = sm64(y ^ 0x5A5A5A5A5A5A5A5Aull);
+        u64 w = sm64(z);
+        u64 p = (z % 20ull) == 0 ? 0ull : x;
+        u64x2 c;
+        c.x = p;
+        c.y = p & y & w;
+        cells[i] = c;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_gset(u64* words, uint64_t R, uint32_t E,
+                                                      u64 seed, u64 base) {
+    const uint64_t W = (E + 63ull) / 64ull;
+    const uint64_t n = R * W;
+    const u64 last_mask = (E % 64) ? ((1ull << (E % 64)) - 1ull) : ~0ull;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t rep = i / W;
+        uint64_t wi = i - rep * W;
+        u64 h = synth_replica_key(seed, base + rep);
+        u64 x = sm64(h + wi * 0xD1B54A32D192ED03ull);
+        words[i] = (wi == W - 1) ? (x & last_mask) : x;
+    }
+}
+
+hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
+                                 uint64_t base) {
+    StreamTune t = stream_tune(ctx, b->replicas * b->words_per_replica / 2 + 1);
+    if (b->kind == LASPJ_KIND_ORSET)
+        hipLaunchKernelGGL(k_fill_orset, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<u64x2*>(b->dev), b->replicas, b->elements,
+                           (u64)seed, (u64)base);
+    else
+        hipLaunchKernelGGL(k_fill_gset, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           (u64*)b->dev, b->replicas, b->elements, (u64)seed, (u64)base);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ value / removed
+// One wave per 64-element word: lane l tests element 64*w + l, __ballot packs the bits.
+
+template <bool REMOVED>
+__global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64* out,
+                                                        uint64_t R, uint32_t E) {
+    const uint32_t W = (E + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t total = R * W;
+    for (uint64_t w = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w < total;
+         w += nwaves) {
+        uint64_t rep = w / W;
+        uint32_t e = (uint32_t)(w - rep * W) * 64u + lane;
+        bool pred = false;
+        if (e < E) {
+            u64x2 c = ld2<true>(cells + rep * E + e);
+            pred = REMOVED ? (c.y != 0) : ((c.x & ~c.y) != 0);
+        }
+        u64 m = __ballot(pred);
+        if (lane == 0) out[w] = m;
+    }
+}
+
+hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
+                              bool removed) {
+    uint64_t words = b->replicas * ((b->elements + 63ull) / 64ull);
+    int grid = wave_grid(ctx, words);
+    auto* cells = reinterpret_cast<const u64x2*>(b->dev);
+    if (removed)
+        hipLaunchKernelGGL(k_orset_value<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           cells, (u64*)out, b->replicas, b->elements);
+    else
+        hipLaunchKernelGGL(k_orset_value<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           cells, (u64*)out, b->replicas, b->elements);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ stats (wave/replica)
+
+__global__ __launch_bounds__(kBlock) void k_orset_stats(const u64x2* cells, u64* out,
+                                                        uint64_t R, uint32_t E) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        const u64x2* c = cells + rep * E;
+        u64 elems = 0, adds = 0, rems = 0;
+#pragma unroll 8
+        for (uint32_t e = lane; e < E; e += 64) {
+            u64x2 v = ld2<true>(c + e);
+            elems += v.x != 0;
+            adds += __popcll(v.x & ~v.y);
+            rems += __popcll(v.y);
+        }
+        elems = wave_sum(elems);
+        adds = wave_sum(adds);
+        rems = wave_sum(rems);
+        if (lane == 0) {
+            out[rep * 3 + 0] = elems;
+            out[rep * 3 + 1] = adds;
+            out[rep * 3 + 2] = rems;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gset_stats(const u64* words, u64* out, uint64_t R,
+                                                       uint64_t W) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        u64 n = 0;
+        for (uint64_t w = lane; w < W; w += 64) n += __popcll(words[rep * W + w]);
+        n = wave_sum(n);
+        if (lane == 0) out[rep] = n;
+    }
+}
+
+hipError_t launch_orset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
+    hipLaunchKernelGGL(k_orset_stats, dim3(wave_grid(ctx, b->replicas)), dim3(kBlock), 0,
+                       ctx->stream, reinterpret_cast<const u64x2*>(b->dev), (u64*)out,
+                       b->replicas, b->elements);
+    return hipGetLastError();
+}
+
+hipError_t launch_gset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
+    hipLaunchKernelGGL(k_gset_stats, dim3(wave_grid(ctx, b->replicas)), dim3(kBlock), 0,
+                       ctx->stream, (const u64*)b->dev, (u64*)out, b->replicas,
+                       b->words_per_replica);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ equal (wave/replica)
+
+__global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, uint8_t* out,
+                                                  uint64_t R, uint64_t wr) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        bool diff = false;
+        if ((wr & 1) == 0) {
+            const u64x2* a2 = reinterpret_cast<const u64x2*>(a + rep * wr);
+            const u64x2* b2 = reinterpret_cast<const u64x2*>(b + rep * wr);
+#pragma unroll 4
+            for (uint64_t w = lane; w < wr / 2; w += 64) {
+                u64x2 x = ld2<true>(a2 + w), y = ld2<true>(b2 + w);
+                diff |= (x.x != y.x) | (x.y != y.y);
+            }
+        } else {
+            for (uint64_t w = lane; w < wr; w += 64) diff |= a[rep * wr + w] != b[rep * wr + w];
+        }
+        bool any = __ballot(diff) != 0;
+        if (lane == 0) out[rep] = any ? 0 : 1;
+    }
+}
+
+hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                        uint8_t* out) {
+    hipLaunchKernelGGL(k_equal, dim3(wave_grid(ctx, a->replicas)), dim3(kBlock), 0,
+                       ctx->stream, (const u64*)a->dev, (const u64*)b->dev, out, a->replicas,
+                       a->words_per_replica);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ inflation
+
+// lasp_lattice.erl:153-161 (non-strict): every Prev element is in Cur with every Prev
+// token  <=>  for all e: (pP & ~pC) == 0   (an absent Cur element has pC == 0).
+// lasp_lattice.erl:235-253 (strict): [] -> non-empty is true; otherwise
+// inflation && (some element of Prev found in Cur with a different token dict
+//               || length(Prev) < length(Cur)).
+template <bool STRICT>
+__global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
+                                                            const u64x2* cur, uint8_t* out,
+                                                            uint64_t R, uint32_t E,
+                                                            bool prev_bcast) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        const u64x2* P = prev + (prev_bcast ? 0 : rep * E);
+        const u64x2* C = cur + rep * E;
+        bool viol = false, changed = false;
+        u64 np = 0, nc = 0;
+#pragma unroll 4
+        for (uint32_t e = lane; e < E; e += 64) {
+            u64x2 p = ld2<false>(P + e), c = ld2<true>(C + e);
+            viol |= (p.x & ~c.x) != 0;
+            if constexpr (STRICT) {
+                changed |= (p.x != 0) & (c.x != 0) & ((p.x != c.x) | (p.y != c.y));
+                np += p.x != 0;
+                nc += c.x != 0;
+            }
+        }
+        bool infl = __ballot(viol) == 0;
+        bool res = infl;
+        if constexpr (STRICT) {
+            bool any_changed = __ballot(changed) != 0;
+            np = wave_sum(np);
+            nc = wave_sum(nc);
+            res = infl && (any_changed || np < nc);
+        }
+        if (lane == 0) out[rep] = res ? 1 : 0;
+    }
+}
+
+// lasp_lattice.erl:137-140 / :212-215: subset, and strict adds "sets differ".
+template <bool STRICT>
+__global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, const u64* cur,
+                                                           uint8_t* out, uint64_t R,
+                                                           uint64_t W, bool prev_bcast) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        const u64* P = prev + (prev_bcast ? 0 : rep * W);
+        const u64* C = cur + rep * W;
+        bool viol = false, diff = false;
+        for (uint64_t w = lane; w < W; w += 64) {
+            u64 p = P[w], c = C[w];
+            viol |= (p & ~c) != 0;
+            diff |= p != c;
+        }
+        bool res = __ballot(viol) == 0;
+        if constexpr (STRICT) res = res && (__ballot(diff) != 0);
+        if (lane == 0) out[rep] = res ? 1 : 0;
+    }
+}
+
+hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                  const laspj_batch* cur, bool strict, uint8_t* out) {
+    int grid = wave_grid(ctx, cur->replicas);
+    bool bc = prev->replicas == 1 && cur->replicas != 1;
+    auto* P = reinterpret_cast<const u64x2*>(prev->dev);
+    auto* C = reinterpret_cast<const u64x2*>(cur->dev);
+    if (strict)
+        hipLaunchKernelGGL(k_orset_inflation<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, P,
+                           C, out, cur->replicas, cur->elements, bc);
+    else
+        hipLaunchKernelGGL(k_orset_inflation<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           P, C, out, cur->replicas, cur->elements, bc);
+    return hipGetLastError();
+}
+
+hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                 const laspj_batch* cur, bool strict, uint8_t* out) {
+    int grid = wave_grid(ctx, cur->replicas);
+    bool bc = prev->replicas == 1 && cur->replicas != 1;
+    if (strict)
+        hipLaunchKernelGGL(k_gset_inflation<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)prev->dev, (const u64*)cur->dev, out, cur->replicas,
+                           cur->words_per_replica, bc);
+    else
+        hipLaunchKernelGGL(k_gset_inflation<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)prev->dev, (const u64*)cur->dev, out, cur->replicas,
+                           cur->words_per_replica, bc);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ update ops
+// lasp_orset:update/3 (lasp_orset.erl:99-117).  The op list is grouped by replica
+// (validated on the host); the thread owning the first op of a replica's run applies
+// that run in order, one update/3 call at a time: a call whose remove finds its
+// element absent (and not added earlier in the same call) is rolled back as a whole —
+// the reference returns {error,{precondition,{not_present,E}}} and keeps the state.
+
+__global__ __launch_bounds__(kBlock) void k_apply_ops(u64* state, uint64_t wr, int32_t kind,
+                                                      const laspj_op* ops, uint64_t nops,
+                                                      int32_t* status) {
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nops) return;
+    const uint64_t rep = ops[i].replica;
+    if (i > 0 && ops[i - 1].replica == rep) return;
+    uint64_t end = i + 1;
+    while (end < nops && ops[end].replica == rep) ++end;
+    u64* s = state + rep * wr;
+    uint64_t c0 = i;
+    while (c0 < end) {
+        uint64_t c1 = c0 + 1;
+        while (c1 < end && !(ops[c1].flags & LASPJ_OP_FLAG_NEW_CALL)) ++c1;
+        uint64_t bad = ~0ull;
+        if (kind == LASPJ_KIND_ORSET) {
+            for (uint64_t k = c0; k < c1 && bad == ~0ull; ++k) {
+                if (ops[k].kind != LASPJ_OP_REMOVE) continue;
+                uint32_t e = ops[k].element;
+                bool present = s[2ull * e] != 0;
+                for (uint64_t j = c0; j < k && !present; ++j)
+                    present = ops[j].kind == LASPJ_OP_ADD && ops[j].element == e;
+                if (!present) bad = k;
+            }
+        }
+        if (bad != ~0ull) {
+            for (uint64_t k = c0; k < c1; ++k)
+                status[k] = k == bad ? LASPJ_OPST_NOT_PRESENT : LASPJ_OPST_ROLLED_BACK;
+        } else {
+            for (uint64_t k = c0; k < c1; ++k) {
+                const laspj_op& o = ops[k];
+                if (kind == LASPJ_KIND_ORSET) {
+                    u64* cell = s + 2ull * o.element;
+                    if (o.kind == LASPJ_OP_ADD) {
+                        // orddict:store(Token, false, Tokens) — present, flag false
+                        cell[0] |= 1ull << o.slot;
+                        cell[1] &= ~(1ull << o.slot);
+                    } else {
+                        cell[1] = cell[0];  // every token of Elem := true
+                    }
+                } else {
+                    s[o.element >> 6] |= 1ull << (o.element & 63u);
+                }
+                status[k] = LASPJ_OPST_APPLIED;
+            }
+        }
+        c0 = c1;
+    }
+}
+
+hipError_t launch_apply_ops(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
+                            int32_t* status) {
+    uint64_t grid = (nops + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_apply_ops, dim3((unsigned)grid), dim3(kBlock), 0, ctx->stream,
+                       (u64*)b->dev, b->words_per_replica, b->kind, ops, nops, status);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ combinators
+
+// union (lasp_core.erl:616-618): keep-left select per cell
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_orset_union(u64x2* d, const u64x2* l,
+                                                        const u64x2* r, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        u64x2 x = ld2<NT>(l + i), y = ld2<NT>(r + i);
+        st2<NT>(d + i, x.x != 0 ? x : y);
+    }
+}
+
+hipError_t launch_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                              const laspj_batch* r) {
+    uint64_t n = l->replicas * l->elements;
+    StreamTune t = stream_tune(ctx, n);
+    hipLaunchKernelGGL(k_orset_union<true>, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
+                       reinterpret_cast<const u64x2*>(r->dev), n);
+    return hipGetLastError();
+}
+
+// filter (lasp_core.erl:681-712): keep cell iff the element's predicate bit is set
+__global__ __launch_bounds__(kBlock) void k_orset_filter(u64x2* d, const u64x2* s,
+                                                         const u64* keep, uint64_t R,
+                                                         uint32_t E) {
+    const uint64_t n = R * E;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t rep = i / E;
+        uint32_t e = (uint32_t)(i - rep * E);
+        bool k = (keep[e >> 6] >> (e & 63u)) & 1ull;
+        u64x2 v = ld2<true>(s + i);
+        u64x2 z;
+        z.x = 0;
+        z.y = 0;
+        st2<true>(d + i, k ? v : z);
+    }
+}
+
+hipError_t launch_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                               const uint64_t* keep) {
+    uint64_t n = src->replicas * src->elements;
+    StreamTune t = stream_tune(ctx, n);
+    hipLaunchKernelGGL(k_orset_filter, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(src->dev),
+                       (const u64*)keep, src->replicas, src->elements);
+    return hipGetLastError();
+}
+
+}  // namespace laspj

@@ -1,0 +1,617 @@
+// liblaspj runtime: contexts, device buffers, batches, events and the C-ABI entry
+// points (include/laspj.h).  Kernels live in laspj_kernels.hip.
+//
+// Every entry point validates handles and shapes on the host before anything is
+// launched, locks the context mutex (the NIF calls one context from many BEAM
+// schedulers, SURVEY.md §8b "Threading"), and reports failures through an int status
+// plus ctx->err.  No C++ exception escapes: allocation failures surface as
+// LASPJ_E_NOMEM via the nothrow paths below.
+
+#include <cstdarg>
+#include <new>
+#include <vector>
+
+#include "laspj_internal.h"
+
+namespace laspj {
+
+int fail(laspj_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+}  // namespace laspj
+
+using laspj::fail;
+
+namespace {
+
+struct Guard {
+    laspj_ctx* ctx;
+    std::lock_guard<std::mutex> lk;
+    explicit Guard(laspj_ctx* c) : ctx(c), lk(c->mu) { hipSetDevice(c->device); }
+};
+
+bool same_ctx(const laspj_ctx* ctx, const laspj_batch* b) { return b && b->ctx == ctx; }
+
+int check_pair(laspj_ctx* ctx, const laspj_batch* x, const laspj_batch* y, int32_t kind,
+               const char* what) {
+    if (!same_ctx(ctx, x) || !same_ctx(ctx, y))
+        return fail(ctx, LASPJ_E_INVAL, "%s: null batch or batch of another context", what);
+    if (x->kind != kind || y->kind != kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind (%d, %d; want %d)", what, x->kind,
+                    y->kind, kind);
+    if (x->elements != y->elements || x->replicas != y->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: shapes differ (%llu x %u vs %llu x %u)", what,
+                    (unsigned long long)x->replicas, x->elements,
+                    (unsigned long long)y->replicas, y->elements);
+    return LASPJ_OK;
+}
+
+int check_buf(laspj_ctx* ctx, const laspj_buf* buf, uint64_t need, const char* what) {
+    if (!buf || buf->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: null output buffer or buffer of another context",
+                    what);
+    if (buf->bytes < need)
+        return fail(ctx, LASPJ_E_RANGE, "%s: output buffer holds %llu bytes, needs %llu", what,
+                    (unsigned long long)buf->bytes, (unsigned long long)need);
+    return LASPJ_OK;
+}
+
+uint64_t words_per(int32_t kind, uint32_t elements) {
+    return kind == LASPJ_KIND_ORSET ? 2ull * elements : (elements + 63ull) / 64ull;
+}
+
+int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t elements,
+                 laspj_batch** out) {
+    if (!ctx || !out) return fail(ctx, LASPJ_E_INVAL, "batch_create: null argument");
+    *out = nullptr;
+    if (replicas == 0 || elements == 0)
+        return fail(ctx, LASPJ_E_SHAPE, "batch_create: replicas and elements must be > 0");
+    Guard g(ctx);
+    auto* b = new (std::nothrow) laspj_batch;
+    if (!b) return fail(ctx, LASPJ_E_NOMEM, "batch_create: host allocation");
+    b->ctx = ctx;
+    b->kind = kind;
+    b->elements = elements;
+    b->replicas = replicas;
+    b->words_per_replica = words_per(kind, elements);
+    uint64_t bytes = laspj::bytes_of(b);
+    if (replicas > (~0ull / 8ull) / b->words_per_replica) {
+        delete b;
+        return fail(ctx, LASPJ_E_SHAPE, "batch_create: size overflow");
+    }
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dev), bytes);
+    if (e != hipSuccess) {
+        delete b;
+        hipGetLastError();
+        return fail(ctx, LASPJ_E_NOMEM, "batch_create: hipMalloc(%llu) failed: %s",
+                    (unsigned long long)bytes, hipGetErrorString(e));
+    }
+    e = hipMemsetAsync(b->dev, 0, bytes, ctx->stream);  // new/0 for every replica
+    if (e != hipSuccess) {
+        hipFree(b->dev);
+        delete b;
+        return fail(ctx, LASPJ_E_DEVICE, "batch_create: memset: %s", hipGetErrorString(e));
+    }
+    *out = b;
+    return LASPJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int laspj_abi_version(void) { return LASPJ_ABI_VERSION; }
+
+const char* laspj_strerror(int s) {
+    switch (s) {
+        case LASPJ_OK: return "ok";
+        case LASPJ_E_INVAL: return "invalid argument";
+        case LASPJ_E_NOMEM: return "out of memory";
+        case LASPJ_E_DEVICE: return "device error";
+        case LASPJ_E_SHAPE: return "shape mismatch";
+        case LASPJ_E_KIND: return "wrong batch kind";
+        case LASPJ_E_RANGE: return "out of range";
+        case LASPJ_E_COMM: return "communicator error";
+        case LASPJ_E_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+int laspj_device_count(int* n) {
+    if (!n) return LASPJ_E_INVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        hipGetLastError();
+        c = 0;
+    }
+    *n = c;
+    return LASPJ_OK;
+}
+
+int laspj_ctx_create(int device, laspj_ctx** out) {
+    if (!out) return LASPJ_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        hipGetLastError();
+        return LASPJ_E_DEVICE;
+    }
+    auto* ctx = new (std::nothrow) laspj_ctx;
+    if (!ctx) return LASPJ_E_NOMEM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return LASPJ_E_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->cus = prop.multiProcessorCount;
+    *out = ctx;
+    return LASPJ_OK;
+}
+
+int laspj_ctx_destroy(laspj_ctx* ctx) {
+    if (!ctx) return LASPJ_E_INVAL;
+    {
+        Guard g(ctx);
+        hipStreamSynchronize(ctx->stream);
+        if (ctx->scratch) hipFree(ctx->scratch);
+        hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+    return LASPJ_OK;
+}
+
+const char* laspj_ctx_last_error(const laspj_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int laspj_ctx_synchronize(laspj_ctx* ctx) {
+    if (!ctx) return LASPJ_E_INVAL;
+    Guard g(ctx);
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
+    if (!ctx) return LASPJ_E_INVAL;
+    Guard g(ctx);
+    switch (knob) {
+        case LASPJ_TUNE_STREAM_GRID:
+            if (value < 0 || value > (1 << 20))
+                return fail(ctx, LASPJ_E_INVAL, "tuning: grid out of range");
+            ctx->tune_grid = value;
+            return LASPJ_OK;
+        case LASPJ_TUNE_STREAM_UNROLL:
+            if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8))
+                return fail(ctx, LASPJ_E_INVAL, "tuning: unroll must be 0,1,2,4,8");
+            ctx->tune_unroll = value;
+            return LASPJ_OK;
+        case LASPJ_TUNE_STREAM_NT:
+            ctx->tune_nt = value;
+            return LASPJ_OK;
+        default:
+            return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
+    }
+}
+
+// ------------------------------------------------------------------------- buffers
+
+int laspj_buf_create(laspj_ctx* ctx, uint64_t bytes, laspj_buf** out) {
+    if (!ctx || !out) return fail(ctx, LASPJ_E_INVAL, "buf_create: null argument");
+    *out = nullptr;
+    Guard g(ctx);
+    auto* b = new (std::nothrow) laspj_buf;
+    if (!b) return fail(ctx, LASPJ_E_NOMEM, "buf_create: host allocation");
+    b->ctx = ctx;
+    b->bytes = bytes;
+    if (bytes) {
+        hipError_t e = hipMalloc(&b->dev, bytes);
+        if (e != hipSuccess) {
+            delete b;
+            hipGetLastError();
+            return fail(ctx, LASPJ_E_NOMEM, "buf_create: hipMalloc(%llu): %s",
+                        (unsigned long long)bytes, hipGetErrorString(e));
+        }
+        e = hipMemsetAsync(b->dev, 0, bytes, ctx->stream);
+        if (e != hipSuccess) {
+            hipFree(b->dev);
+            delete b;
+            return fail(ctx, LASPJ_E_DEVICE, "buf_create: memset: %s", hipGetErrorString(e));
+        }
+    }
+    *out = b;
+    return LASPJ_OK;
+}
+
+int laspj_buf_destroy(laspj_buf* b) {
+    if (!b) return LASPJ_E_INVAL;
+    {
+        Guard g(b->ctx);
+        hipStreamSynchronize(b->ctx->stream);
+        if (b->dev) hipFree(b->dev);
+    }
+    delete b;
+    return LASPJ_OK;
+}
+
+uint64_t laspj_buf_bytes(const laspj_buf* b) { return b ? b->bytes : 0; }
+
+int laspj_buf_upload(laspj_ctx* ctx, laspj_buf* b, uint64_t off, const void* src,
+                     uint64_t bytes) {
+    if (!ctx || !b || b->ctx != ctx || (!src && bytes))
+        return fail(ctx, LASPJ_E_INVAL, "buf_upload: bad argument");
+    if (off > b->bytes || bytes > b->bytes - off)
+        return fail(ctx, LASPJ_E_RANGE, "buf_upload: range out of bounds");
+    Guard g(ctx);
+    if (!bytes) return LASPJ_OK;
+    LJ_HIP(ctx, hipMemcpyAsync(static_cast<char*>(b->dev) + off, src, bytes,
+                               hipMemcpyHostToDevice, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_buf_download(laspj_ctx* ctx, const laspj_buf* b, uint64_t off, void* dst,
+                       uint64_t bytes) {
+    if (!ctx || !b || b->ctx != ctx || (!dst && bytes))
+        return fail(ctx, LASPJ_E_INVAL, "buf_download: bad argument");
+    if (off > b->bytes || bytes > b->bytes - off)
+        return fail(ctx, LASPJ_E_RANGE, "buf_download: range out of bounds");
+    Guard g(ctx);
+    if (!bytes) return LASPJ_OK;
+    LJ_HIP(ctx, hipMemcpyAsync(dst, static_cast<const char*>(b->dev) + off, bytes,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+// ------------------------------------------------------------------------- batches
+
+int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                             laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_ORSET, replicas, elements, out);
+}
+
+int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                            laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_GSET, replicas, elements, out);
+}
+
+int laspj_batch_destroy(laspj_batch* b) {
+    if (!b) return LASPJ_E_INVAL;
+    {
+        Guard g(b->ctx);
+        hipStreamSynchronize(b->ctx->stream);
+        hipFree(b->dev);
+    }
+    delete b;
+    return LASPJ_OK;
+}
+
+int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
+    if (!b || !out) return LASPJ_E_INVAL;
+    out->kind = b->kind;
+    out->elements = b->elements;
+    out->replicas = b->replicas;
+    out->bytes_per_replica = b->words_per_replica * 8ull;
+    out->bytes = laspj::bytes_of(b);
+    return LASPJ_OK;
+}
+
+int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t first, uint64_t count,
+                       const void* host) {
+    if (!same_ctx(ctx, b) || (!host && count))
+        return fail(ctx, LASPJ_E_INVAL, "batch_upload: bad argument");
+    if (first > b->replicas || count > b->replicas - first)
+        return fail(ctx, LASPJ_E_RANGE, "batch_upload: replicas [%llu, +%llu) out of %llu",
+                    (unsigned long long)first, (unsigned long long)count,
+                    (unsigned long long)b->replicas);
+    Guard g(ctx);
+    uint64_t rb = b->words_per_replica * 8ull;
+    LJ_HIP(ctx, hipMemcpyAsync(reinterpret_cast<char*>(b->dev) + first * rb, host, count * rb,
+                               hipMemcpyHostToDevice, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_batch_download(laspj_ctx* ctx, const laspj_batch* b, uint64_t first,
+                         uint64_t count, void* host) {
+    if (!same_ctx(ctx, b) || (!host && count))
+        return fail(ctx, LASPJ_E_INVAL, "batch_download: bad argument");
+    if (first > b->replicas || count > b->replicas - first)
+        return fail(ctx, LASPJ_E_RANGE, "batch_download: replicas out of range");
+    Guard g(ctx);
+    uint64_t rb = b->words_per_replica * 8ull;
+    LJ_HIP(ctx, hipMemcpyAsync(host, reinterpret_cast<const char*>(b->dev) + first * rb,
+                               count * rb, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* b) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "batch_clear: bad argument");
+    Guard g(ctx);
+    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, laspj::bytes_of(b), ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
+                               uint64_t replica_base) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base));
+    return LASPJ_OK;
+}
+
+// ------------------------------------------------------------------------- joins
+
+static int join_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b, int32_t kind, const char* what) {
+    if (int s = check_pair(ctx, a, b, kind, what)) return s;
+    if (int s = check_pair(ctx, dst, a, kind, what)) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_or(ctx, dst->dev, a->dev, b->dev,
+                                 a->replicas * a->words_per_replica));
+    return LASPJ_OK;
+}
+
+int laspj_orset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b) {
+    return join_impl(ctx, dst, a, b, LASPJ_KIND_ORSET, "orset_join");
+}
+
+int laspj_gset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                    const laspj_batch* b) {
+    return join_impl(ctx, dst, a, b, LASPJ_KIND_GSET, "gset_join");
+}
+
+static int reduce_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       uint32_t group, int32_t kind, const char* what) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    if (dst->kind != kind || src->kind != kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
+    if (group == 0 || dst->elements != src->elements ||
+        dst->replicas * (uint64_t)group != src->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: need src replicas = dst replicas * group", what);
+    if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "%s: dst aliases src", what);
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_reduce_or(ctx, dst->dev, src->dev, dst->replicas, group,
+                                        src->words_per_replica));
+    return LASPJ_OK;
+}
+
+int laspj_orset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       uint32_t group) {
+    return reduce_impl(ctx, dst, src, group, LASPJ_KIND_ORSET, "orset_reduce");
+}
+
+int laspj_gset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      uint32_t group) {
+    return reduce_impl(ctx, dst, src, group, LASPJ_KIND_GSET, "gset_reduce");
+}
+
+// ------------------------------------------------------------------------- predicates
+
+static int value_impl(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out, bool removed) {
+    const char* what = removed ? "orset_removed" : "orset_value";
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "%s: not an OR-Set", what);
+    uint64_t need = b->replicas * ((b->elements + 63ull) / 64ull) * 8ull;
+    if (int s = check_buf(ctx, out, need, what)) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_value(ctx, b, static_cast<uint64_t*>(out->dev), removed));
+    return LASPJ_OK;
+}
+
+int laspj_orset_value(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
+    return value_impl(ctx, b, out, false);
+}
+
+int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
+    return value_impl(ctx, b, out, true);
+}
+
+int laspj_orset_stats(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "orset_stats: bad batch");
+    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "orset_stats: not an OR-Set");
+    if (int s = check_buf(ctx, out, b->replicas * 24ull, "orset_stats")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_stats(ctx, b, static_cast<uint64_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gset_stats(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "gset_stats: bad batch");
+    if (b->kind != LASPJ_KIND_GSET) return fail(ctx, LASPJ_E_KIND, "gset_stats: not a G-Set");
+    if (int s = check_buf(ctx, out, b->replicas * 8ull, "gset_stats")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gset_stats(ctx, b, static_cast<uint64_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+static int equal_impl(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                      laspj_buf* out, int32_t kind, const char* what) {
+    if (int s = check_pair(ctx, a, b, kind, what)) return s;
+    if (int s = check_buf(ctx, out, a->replicas, what)) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_equal(ctx, a, b, static_cast<uint8_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_orset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                      laspj_buf* out) {
+    return equal_impl(ctx, a, b, out, LASPJ_KIND_ORSET, "orset_equal");
+}
+
+int laspj_gset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                     laspj_buf* out) {
+    return equal_impl(ctx, a, b, out, LASPJ_KIND_GSET, "gset_equal");
+}
+
+static int inflation_impl(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                          int strict, laspj_buf* out, int32_t kind, const char* what) {
+    if (!same_ctx(ctx, prev) || !same_ctx(ctx, cur))
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    if (prev->kind != kind || cur->kind != kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
+    if (prev->elements != cur->elements ||
+        !(prev->replicas == cur->replicas || prev->replicas == 1))
+        return fail(ctx, LASPJ_E_SHAPE, "%s: prev must have cur's replicas or 1", what);
+    if (int s = check_buf(ctx, out, cur->replicas, what)) return s;
+    Guard g(ctx);
+    if (kind == LASPJ_KIND_ORSET)
+        LJ_HIP(ctx, laspj::launch_orset_inflation(ctx, prev, cur, strict != 0,
+                                                  static_cast<uint8_t*>(out->dev)));
+    else
+        LJ_HIP(ctx, laspj::launch_gset_inflation(ctx, prev, cur, strict != 0,
+                                                 static_cast<uint8_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                          int strict, laspj_buf* out) {
+    return inflation_impl(ctx, prev, cur, strict, out, LASPJ_KIND_ORSET, "orset_inflation");
+}
+
+int laspj_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                         int strict, laspj_buf* out) {
+    return inflation_impl(ctx, prev, cur, strict, out, LASPJ_KIND_GSET, "gset_inflation");
+}
+
+// ------------------------------------------------------------------------- updates
+
+static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
+                          int32_t* status, int32_t kind, const char* what) {
+    if (!same_ctx(ctx, b) || (!ops && nops) || (!status && nops))
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad argument", what);
+    if (b->kind != kind) return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
+    // Host-side validation: every op addresses a real cell and the list is grouped by
+    // replica, which is what the one-thread-per-replica-run kernel relies on.
+    for (uint64_t i = 0; i < nops; ++i) {
+        const laspj_op& o = ops[i];
+        if (o.replica >= b->replicas || o.element >= b->elements)
+            return fail(ctx, LASPJ_E_RANGE, "%s: op %llu addresses (%llu, %u) outside %llu x %u",
+                        what, (unsigned long long)i, (unsigned long long)o.replica, o.element,
+                        (unsigned long long)b->replicas, b->elements);
+        if (o.slot >= 64) return fail(ctx, LASPJ_E_RANGE, "%s: op %llu token slot >= 64", what,
+                                      (unsigned long long)i);
+        bool ok_kind = kind == LASPJ_KIND_ORSET
+                           ? (o.kind == LASPJ_OP_ADD || o.kind == LASPJ_OP_REMOVE)
+                           : o.kind == LASPJ_OP_ADD;
+        if (!ok_kind) return fail(ctx, LASPJ_E_INVAL, "%s: op %llu has kind %u", what,
+                                  (unsigned long long)i, o.kind);
+        if (i && ops[i - 1].replica > o.replica)
+            return fail(ctx, LASPJ_E_INVAL, "%s: ops not sorted by replica at %llu", what,
+                        (unsigned long long)i);
+    }
+    if (!nops) return LASPJ_OK;
+    Guard g(ctx);
+    uint64_t need = nops * (sizeof(laspj_op) + sizeof(int32_t));
+    if (ctx->scratch_bytes < need) {
+        if (ctx->scratch) {
+            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            hipFree(ctx->scratch);
+            ctx->scratch = nullptr;
+            ctx->scratch_bytes = 0;
+        }
+        if (hipMalloc(&ctx->scratch, need) != hipSuccess) {
+            hipGetLastError();
+            return fail(ctx, LASPJ_E_NOMEM, "%s: scratch allocation", what);
+        }
+        ctx->scratch_bytes = need;
+    }
+    auto* dops = static_cast<laspj_op*>(ctx->scratch);
+    auto* dst = reinterpret_cast<int32_t*>(dops + nops);
+    LJ_HIP(ctx, hipMemcpyAsync(dops, ops, nops * sizeof(laspj_op), hipMemcpyHostToDevice,
+                               ctx->stream));
+    LJ_HIP(ctx, laspj::launch_apply_ops(ctx, b, dops, nops, dst));
+    LJ_HIP(ctx, hipMemcpyAsync(status, dst, nops * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_orset_apply_ops(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
+                          int32_t* status) {
+    return apply_ops_impl(ctx, b, ops, nops, status, LASPJ_KIND_ORSET, "orset_apply_ops");
+}
+
+int laspj_gset_apply_ops(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
+                         int32_t* status) {
+    return apply_ops_impl(ctx, b, ops, nops, status, LASPJ_KIND_GSET, "gset_apply_ops");
+}
+
+// ------------------------------------------------------------------------- combinators
+
+int laspj_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                      const laspj_batch* r) {
+    if (int s = check_pair(ctx, l, r, LASPJ_KIND_ORSET, "orset_union")) return s;
+    if (int s = check_pair(ctx, dst, l, LASPJ_KIND_ORSET, "orset_union")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_union(ctx, dst, l, r));
+    return LASPJ_OK;
+}
+
+int laspj_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       const laspj_buf* keep) {
+    if (int s = check_pair(ctx, dst, src, LASPJ_KIND_ORSET, "orset_filter")) return s;
+    if (int s = check_buf(ctx, keep, (src->elements + 63ull) / 64ull * 8ull, "orset_filter"))
+        return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_filter(ctx, dst, src, static_cast<const uint64_t*>(keep->dev)));
+    return LASPJ_OK;
+}
+
+// ------------------------------------------------------------------------- events
+
+int laspj_event_create(laspj_ctx* ctx, laspj_event** out) {
+    if (!ctx || !out) return LASPJ_E_INVAL;
+    *out = nullptr;
+    Guard g(ctx);
+    auto* ev = new (std::nothrow) laspj_event;
+    if (!ev) return LASPJ_E_NOMEM;
+    ev->ctx = ctx;
+    if (hipEventCreate(&ev->ev) != hipSuccess) {
+        delete ev;
+        return fail(ctx, LASPJ_E_DEVICE, "event_create failed");
+    }
+    *out = ev;
+    return LASPJ_OK;
+}
+
+int laspj_event_destroy(laspj_event* ev) {
+    if (!ev) return LASPJ_E_INVAL;
+    {
+        Guard g(ev->ctx);
+        hipEventDestroy(ev->ev);
+    }
+    delete ev;
+    return LASPJ_OK;
+}
+
+int laspj_event_record(laspj_ctx* ctx, laspj_event* ev) {
+    if (!ctx || !ev || ev->ctx != ctx) return LASPJ_E_INVAL;
+    Guard g(ctx);
+    LJ_HIP(ctx, hipEventRecord(ev->ev, ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_event_elapsed_ms(laspj_event* start, laspj_event* stop, float* ms) {
+    if (!start || !stop || !ms || start->ctx != stop->ctx) return LASPJ_E_INVAL;
+    laspj_ctx* ctx = start->ctx;
+    Guard g(ctx);
+    LJ_HIP(ctx, hipEventSynchronize(stop->ev));
+    LJ_HIP(ctx, hipEventElapsedTime(ms, start->ev, stop->ev));
+    return LASPJ_OK;
+}
+
+}  // extern "C"

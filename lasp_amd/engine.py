@@ -1,0 +1,268 @@
+"""Device-resident batches over the C ABI: the batched lattice-join engine.
+
+`Context` owns one HIP stream on one GPU; `ORSetBatch` / `GSetBatch` hold R replicas of
+one CRDT in the columnar layout of include/laspj.h; `Buffer` holds kernel outputs.
+Every method is one C-ABI call (and, for the *_host helpers, one download).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, load
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.L = load()
+        h = C.c_void_p()
+        check(self.L.laspj_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.laspj_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def synchronize(self):
+        check(self.L.laspj_ctx_synchronize(self.h), self.h)
+
+    def set_tuning(self, knob: int, value: int):
+        check(self.L.laspj_ctx_set_tuning(self.h, knob, value), self.h)
+
+    # -- factories
+    def orset_batch(self, replicas: int, elements: int) -> "ORSetBatch":
+        return ORSetBatch(self, replicas, elements)
+
+    def gset_batch(self, replicas: int, elements: int) -> "GSetBatch":
+        return GSetBatch(self, replicas, elements)
+
+    def buffer(self, nbytes: int) -> "Buffer":
+        return Buffer(self, nbytes)
+
+    def event(self) -> "Event":
+        return Event(self)
+
+
+def device_count() -> int:
+    L = load()
+    n = C.c_int()
+    check(L.laspj_device_count(C.byref(n)))
+    return n.value
+
+
+class Buffer:
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(ctx.L.laspj_buf_create(ctx.h, nbytes, C.byref(h)), ctx.h)
+        self.h = h
+        self.nbytes = nbytes
+
+    def __del__(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_buf_destroy(self.h)
+            self.h = None
+
+    def download(self, dtype=np.uint8, count: Optional[int] = None, offset: int = 0) -> np.ndarray:
+        itemsize = np.dtype(dtype).itemsize
+        if count is None:
+            count = (self.nbytes - offset) // itemsize
+        out = np.empty((count,), dtype=dtype)
+        check(self.ctx.L.laspj_buf_download(self.ctx.h, self.h, offset, out.ctypes.data,
+                                            count * itemsize), self.ctx.h)
+        return out
+
+    def upload(self, arr: np.ndarray, offset: int = 0):
+        arr = np.ascontiguousarray(arr)
+        check(self.ctx.L.laspj_buf_upload(self.ctx.h, self.h, offset, arr.ctypes.data,
+                                          arr.nbytes), self.ctx.h)
+
+
+class Event:
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(ctx.L.laspj_event_create(ctx.h, C.byref(h)), ctx.h)
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_event_destroy(self.h)
+            self.h = None
+
+    def record(self):
+        check(self.ctx.L.laspj_event_record(self.ctx.h, self.h), self.ctx.h)
+
+    def elapsed_ms(self, stop: "Event") -> float:
+        ms = C.c_float()
+        check(self.ctx.L.laspj_event_elapsed_ms(self.h, stop.h, C.byref(ms)), self.ctx.h)
+        return ms.value
+
+
+class _Batch:
+    kind = 0
+    _create = ""
+
+    def __init__(self, ctx: Context, replicas: int, elements: int):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(getattr(ctx.L, self._create)(ctx.h, replicas, elements, C.byref(h)), ctx.h)
+        self.h = h
+        self.replicas = replicas
+        self.elements = elements
+        info = _lib.BatchInfo()
+        check(ctx.L.laspj_batch_info_get(self.h, C.byref(info)))
+        self.bytes_per_replica = info.bytes_per_replica
+        self.nbytes = info.bytes
+
+    def __del__(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_batch_destroy(self.h)
+            self.h = None
+
+    @property
+    def words_per_replica(self) -> int:
+        return self.bytes_per_replica // 8
+
+    def upload(self, host: np.ndarray, first: int = 0):
+        host = np.ascontiguousarray(host, dtype=np.uint64)
+        count = host.nbytes // self.bytes_per_replica
+        if count * self.bytes_per_replica != host.nbytes:
+            raise ValueError("host array is not a whole number of replicas")
+        check(self.ctx.L.laspj_batch_upload(self.ctx.h, self.h, first, count, host.ctypes.data),
+              self.ctx.h)
+
+    def download_words(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        if count is None:
+            count = self.replicas - first
+        out = np.empty((count, self.words_per_replica), dtype=np.uint64)
+        check(self.ctx.L.laspj_batch_download(self.ctx.h, self.h, first, count,
+                                              out.ctypes.data), self.ctx.h)
+        return out
+
+    def clear(self):
+        check(self.ctx.L.laspj_batch_clear(self.ctx.h, self.h), self.ctx.h)
+
+    def fill_synthetic(self, seed: int, replica_base: int = 0):
+        check(self.ctx.L.laspj_batch_fill_synthetic(self.ctx.h, self.h, seed, replica_base),
+              self.ctx.h)
+
+    def _bool_out(self, fn, *args) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas)
+        check(fn(self.ctx.h, *args, buf.h), self.ctx.h)
+        return buf.download(np.uint8).astype(bool)
+
+    def _apply_ops(self, fn, ops: Sequence[tuple]) -> np.ndarray:
+        n = len(ops)
+        arr = (_lib.Op * max(n, 1))()
+        for k, (rep, elem, kind, slot, flags) in enumerate(ops):
+            arr[k].replica, arr[k].element, arr[k].kind = rep, elem, kind
+            arr[k].slot, arr[k].flags, arr[k].pad = slot, flags, 0
+        status = np.zeros((max(n, 1),), dtype=np.int32)
+        check(fn(self.ctx.h, self.h, arr, n, status.ctypes.data_as(C.POINTER(C.c_int32))),
+              self.ctx.h)
+        return status[:n]
+
+
+class ORSetBatch(_Batch):
+    """R replicas of an OR-Set over E element slots (16-byte {p, r} cells)."""
+
+    kind = _lib.KIND_ORSET
+    _create = "laspj_orset_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """(count, E, 2) uint64 array of {p, r} cells."""
+        w = self.download_words(first, count)
+        return w.reshape(w.shape[0], self.elements, 2)
+
+    # lasp_orset:merge/2
+    def join(self, a: "ORSetBatch", b: "ORSetBatch"):
+        check(self.ctx.L.laspj_orset_join(self.ctx.h, self.h, a.h, b.h), self.ctx.h)
+        return self
+
+    def reduce_from(self, src: "ORSetBatch", group: int):
+        check(self.ctx.L.laspj_orset_reduce(self.ctx.h, self.h, src.h, group), self.ctx.h)
+        return self
+
+    def value_bits(self, removed: bool = False) -> np.ndarray:
+        W = (self.elements + 63) // 64
+        buf = self.ctx.buffer(self.replicas * W * 8)
+        fn = self.ctx.L.laspj_orset_removed if removed else self.ctx.L.laspj_orset_value
+        check(fn(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, W)
+
+    def stats(self) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas * 24)
+        check(self.ctx.L.laspj_orset_stats(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, 3)
+
+    def equal(self, other: "ORSetBatch") -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_orset_equal, self.h, other.h)
+
+    def is_inflation_of(self, prev: "ORSetBatch", strict: bool = False) -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_orset_inflation, prev.h, self.h, int(strict))
+
+    def apply_ops(self, ops: Sequence[tuple]) -> np.ndarray:
+        """ops: (replica, element_slot, OP_ADD|OP_REMOVE, token_slot, flags)."""
+        return self._apply_ops(self.ctx.L.laspj_orset_apply_ops, ops)
+
+    def union(self, l: "ORSetBatch", r: "ORSetBatch"):
+        check(self.ctx.L.laspj_orset_union(self.ctx.h, self.h, l.h, r.h), self.ctx.h)
+        return self
+
+    def filter(self, src: "ORSetBatch", keep_bits: np.ndarray):
+        keep = self.ctx.buffer(((self.elements + 63) // 64) * 8)
+        keep.upload(np.ascontiguousarray(keep_bits, dtype=np.uint64))
+        check(self.ctx.L.laspj_orset_filter(self.ctx.h, self.h, src.h, keep.h), self.ctx.h)
+        self.ctx.synchronize()
+        return self
+
+
+class GSetBatch(_Batch):
+    """R replicas of a G-Set over E element slots (ceil(E/64) u64 words)."""
+
+    kind = _lib.KIND_GSET
+    _create = "laspj_gset_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        return self.download_words(first, count)
+
+    def join(self, a: "GSetBatch", b: "GSetBatch"):
+        check(self.ctx.L.laspj_gset_join(self.ctx.h, self.h, a.h, b.h), self.ctx.h)
+        return self
+
+    def reduce_from(self, src: "GSetBatch", group: int):
+        check(self.ctx.L.laspj_gset_reduce(self.ctx.h, self.h, src.h, group), self.ctx.h)
+        return self
+
+    def stats(self) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas * 8)
+        check(self.ctx.L.laspj_gset_stats(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64)
+
+    def equal(self, other: "GSetBatch") -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_gset_equal, self.h, other.h)
+
+    def is_inflation_of(self, prev: "GSetBatch", strict: bool = False) -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_gset_inflation, prev.h, self.h, int(strict))
+
+    def apply_ops(self, ops: Sequence[tuple]) -> np.ndarray:
+        return self._apply_ops(self.ctx.L.laspj_gset_apply_ops, ops)

@@ -1,0 +1,303 @@
+"""GPU parity of the HIP engine against the oracle (run with -m gpu on an MI355X).
+
+Every engine result is compared bit-for-bit with the C restatement of the reference
+(oracle/laspj_oracle.c: orddict merge, keyfind-based inflation, ...) on seeded
+synthetic replicas, decoded token for token where the reference returns terms.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import columnar as orc
+
+pytestmark = pytest.mark.gpu
+
+E = 256          # element slots per replica in the mid-size cases
+R = 512          # replicas per batch in the mid-size cases
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from lasp_amd import engine
+    c = engine.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def tokens():
+    return orc.synth_tokens(E)
+
+
+def _synth(seed, n, e, base=0):
+    return np.stack([orc.synth_orset(seed, base + i, e) for i in range(n)])
+
+
+def test_fill_synthetic_matches_oracle(ctx):
+    b = ctx.orset_batch(R, E)
+    b.fill_synthetic(7, replica_base=1000)
+    got = b.download()
+    assert np.array_equal(got, _synth(7, R, E, 1000))
+    g = ctx.gset_batch(64, 1000)          # E not a multiple of 64: padding bits stay 0
+    g.fill_synthetic(9, 5)
+    want = np.stack([orc.synth_gset(9, 5 + i, 1000) for i in range(64)])
+    assert np.array_equal(g.download(), want)
+
+
+def test_orset_join_token_for_token(ctx, tokens):
+    """lasp_orset:merge/2 (lasp_orset.erl:128-134) vs the C orddict merge."""
+    a, b, c = ctx.orset_batch(R, E), ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    c.join(a, b)
+    got = c.download()
+    ha, hb = a.download(), b.download()
+    for i in range(0, R, 37):
+        A = orc.ORDict.from_cells(ha[i], tokens)
+        B = orc.ORDict.from_cells(hb[i], tokens)
+        M = A.merge(B)
+        G = orc.ORDict.from_cells(got[i], tokens)
+        assert G.equal(M), f"replica {i}"
+    # whole-batch property: the columnar join is p|p', r|r'
+    assert np.array_equal(got, ha | hb)
+
+
+def test_orset_join_in_place_and_idempotent(ctx):
+    a, b = ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    want = a.download() | b.download()
+    a.join(a, b)                       # bind merges in place (lasp_core.erl:300-303)
+    assert np.array_equal(a.download(), want)
+    a.join(a, a)                       # idempotence
+    assert np.array_equal(a.download(), want)
+    a.join(a, b)                       # absorbing
+    assert np.array_equal(a.download(), want)
+
+
+def test_orset_join_edge_cases(ctx, tokens):
+    """empty, identical, disjoint and all-removed replicas (SURVEY.md §8d cfg 2)."""
+    n = 4
+    host = np.zeros((n, E, 2), dtype=np.uint64)
+    other = np.zeros_like(host)
+    full = _synth(4, 1, E)[0]
+    host[1] = full                                 # identical
+    other[1] = full
+    host[2, : E // 2] = full[: E // 2]             # disjoint halves
+    other[2, E // 2:] = full[E // 2:]
+    host[3] = full
+    host[3, :, 1] = full[:, 0]                     # all removed
+    other[3] = full
+    a, b, c = ctx.orset_batch(n, E), ctx.orset_batch(n, E), ctx.orset_batch(n, E)
+    a.upload(host)
+    b.upload(other)
+    c.join(a, b)
+    got = c.download()
+    for i in range(n):
+        M = orc.ORDict.from_cells(host[i], tokens).merge(orc.ORDict.from_cells(other[i], tokens))
+        assert orc.ORDict.from_cells(got[i], tokens).equal(M)
+    assert not got[0].any()
+
+
+def test_orset_value_removed_stats(ctx, tokens):
+    b = ctx.orset_batch(R, E)
+    b.fill_synthetic(11)
+    h = b.download()
+    vis = b.value_bits()
+    rem = b.value_bits(removed=True)
+    st = b.stats()
+    for i in range(0, R, 29):
+        D = orc.ORDict.from_cells(h[i], tokens)
+        want_vis = D.value()
+        got_vis = np.nonzero(np.unpackbits(vis[i].view(np.uint8), bitorder="little")[:E])[0]
+        assert np.array_equal(got_vis, want_vis)
+        assert tuple(int(x) for x in st[i]) == D.stats()
+        want_rem = [e for e in range(E) if h[i, e, 1] != 0]
+        got_rem = np.nonzero(np.unpackbits(rem[i].view(np.uint8), bitorder="little")[:E])[0]
+        assert list(got_rem) == want_rem
+
+
+def test_orset_inflation_vs_keyfind_oracle(ctx, tokens):
+    """is_inflation / is_strict_inflation (lasp_lattice.erl:153-161, 235-253)."""
+    n = 64
+    prev = _synth(21, n, E)
+    cur = prev.copy()
+    rng = np.random.default_rng(0)
+    for i in range(n):
+        kind = i % 6
+        if kind == 1:       # merge-style inflation
+            cur[i] |= _synth(22, 1, E, i)[0]
+        elif kind == 2:     # drop a token -> not an inflation
+            e = int(np.nonzero(cur[i, :, 0])[0][0])
+            low = cur[i, e, 0] & (~cur[i, e, 0] + np.uint64(1))
+            cur[i, e, 0] ^= low
+            cur[i, e, 1] &= cur[i, e, 0]
+        elif kind == 3:     # remove an element (tombstone all) -> strict inflation
+            e = int(np.nonzero(cur[i, :, 0])[0][0])
+            cur[i, e, 1] = cur[i, e, 0]
+        elif kind == 4:     # un-remove only (flags ignored by is_inflation)
+            prev[i, :, 1] = prev[i, :, 0]
+        elif kind == 5:     # empty prev
+            prev[i] = 0
+        if i == n - 1:      # empty both
+            prev[i] = 0
+            cur[i] = 0
+        _ = rng
+    P, Cb = ctx.orset_batch(n, E), ctx.orset_batch(n, E)
+    P.upload(prev)
+    Cb.upload(cur)
+    infl = Cb.is_inflation_of(P)
+    strict = Cb.is_inflation_of(P, strict=True)
+    for i in range(n):
+        Dp = orc.ORDict.from_cells(prev[i], tokens)
+        Dc = orc.ORDict.from_cells(cur[i], tokens)
+        assert infl[i] == Dc.is_inflation_of(Dp), i
+        assert strict[i] == Dc.is_strict_inflation_of(Dp), i
+
+
+def test_orset_threshold_broadcast(ctx, tokens):
+    """threshold_met with one threshold against many values (prev replicas = 1)."""
+    n = 32
+    cur = _synth(31, n, E)
+    th = cur[0].copy()
+    th[:, 1] = 0
+    T, Cb = ctx.orset_batch(1, E), ctx.orset_batch(n, E)
+    T.upload(th[None])
+    Cb.upload(cur)
+    got = Cb.is_inflation_of(T)
+    Dt = orc.ORDict.from_cells(th, tokens)
+    for i in range(n):
+        assert got[i] == orc.ORDict.from_cells(cur[i], tokens).is_inflation_of(Dt)
+
+
+def test_orset_equal(ctx):
+    a, b = ctx.orset_batch(8, E), ctx.orset_batch(8, E)
+    a.fill_synthetic(5)
+    b.fill_synthetic(5)
+    h = b.download()
+    h[3, 7, 1] ^= np.uint64(1) << np.uint64(63)
+    b.upload(h)
+    eq = a.equal(b)
+    assert list(eq) == [True, True, True, False, True, True, True, True]
+
+
+def test_orset_reduce_fsm_merge(ctx, tokens):
+    """foldl(merge, new(), Replies) — lasp_update_fsm.erl:189-192, N=3."""
+    groups, N = 50, 3
+    src, dst = ctx.orset_batch(groups * N, E), ctx.orset_batch(groups, E)
+    src.fill_synthetic(41)
+    dst.reduce_from(src, N)
+    hs = src.download()
+    got = dst.download()
+    for g in range(0, groups, 7):
+        acc = orc.ORDict.from_cells(np.zeros((E, 2), np.uint64), tokens)
+        for j in range(N):
+            acc = orc.ORDict.from_cells(hs[g * N + j], tokens).merge(acc)
+        assert orc.ORDict.from_cells(got[g], tokens).equal(acc)
+
+
+def test_orset_apply_ops_vs_python_oracle(ctx):
+    """update/3 add_by_token / remove / {update, Ops} (lasp_orset.erl:99-117)."""
+    from lasp_amd._lib import OP_ADD, OP_REMOVE, OP_FLAG_NEW_CALL, OPST_APPLIED, \
+        OPST_NOT_PRESENT, OPST_ROLLED_BACK
+    from oracle import orset as oo
+    e_n = 8
+    toks = [bytes([k]) * 20 for k in range(64)]
+    b = ctx.orset_batch(3, e_n)
+    # replica 0: add e1/t3, add e1/t5, remove e1 (one call each), add e1/t3 again
+    # replica 1: call {update, [add e2/t0, remove e4]} -> rolled back (e4 absent)
+    # replica 2: call {update, [add e4/t1, remove e4]} -> ok (added earlier in call)
+    ops = [(0, 1, OP_ADD, 3, OP_FLAG_NEW_CALL), (0, 1, OP_ADD, 5, OP_FLAG_NEW_CALL),
+           (0, 1, OP_REMOVE, 0, OP_FLAG_NEW_CALL), (0, 1, OP_ADD, 3, OP_FLAG_NEW_CALL),
+           (1, 2, OP_ADD, 0, OP_FLAG_NEW_CALL), (1, 4, OP_REMOVE, 0, 0),
+           (2, 4, OP_ADD, 1, OP_FLAG_NEW_CALL), (2, 4, OP_REMOVE, 0, 0)]
+    st = b.apply_ops(ops)
+    assert list(st) == [OPST_APPLIED] * 4 + [OPST_ROLLED_BACK, OPST_NOT_PRESENT] + [OPST_APPLIED] * 2
+    got = b.download()
+    # oracle
+    s0 = oo.new()
+    for op in [("add_by_token", toks[3], 1), ("add_by_token", toks[5], 1), ("remove", 1),
+               ("add_by_token", toks[3], 1)]:
+        s0 = oo.update(op, None, s0)[1]
+    assert oo.update(("update", [("add_by_token", toks[0], 2), ("remove", 4)]), None, [])[0] == "error"
+    s2 = oo.update(("update", [("add_by_token", toks[1], 4), ("remove", 4)]), None, [])[1]
+
+    def enc(s):
+        out = np.zeros((e_n, 2), np.uint64)
+        for elem, tl in s:
+            for t, rm in tl:
+                k = toks.index(t)
+                out[elem, 0] |= np.uint64(1) << np.uint64(k)
+                if rm:
+                    out[elem, 1] |= np.uint64(1) << np.uint64(k)
+        return out
+    assert np.array_equal(got[0], enc(s0))
+    assert not got[1].any()
+    assert np.array_equal(got[2], enc(s2))
+
+
+def test_orset_union_filter_vs_bodies(ctx):
+    """union (lasp_core.erl:616-618) and filter (:681-712) bodies."""
+    from oracle import core
+    e_n = 70
+    toks = [bytes([k]) * 20 for k in range(64)]
+    l = _synth(51, 4, e_n)
+    r = _synth(52, 4, e_n)
+    l[:, ::3] = 0              # some elements only on the right
+
+    def dec(cells):
+        out = []
+        for e in range(e_n):
+            p, rr = int(cells[e, 0]), int(cells[e, 1])
+            if p:
+                out.append((e, [(toks[k], bool((rr >> k) & 1)) for k in range(64) if (p >> k) & 1]))
+        return out
+    L, Rb, U, F = (ctx.orset_batch(4, e_n) for _ in range(4))
+    L.upload(l)
+    Rb.upload(r)
+    U.union(L, Rb)
+    keep = np.zeros(((e_n + 63) // 64,), np.uint64)
+    for e in range(e_n):
+        if e % 2 == 0:
+            keep[e // 64] |= np.uint64(1) << np.uint64(e % 64)
+    F.filter(L, keep)
+    gu, gf = U.download(), F.download()
+    for i in range(4):
+        assert dec(gu[i]) == core.union_body("lasp_orset", dec(l[i]), dec(r[i]))
+        assert dec(gf[i]) == core.filter_body("lasp_orset", lambda x: x % 2 == 0, dec(l[i]))
+
+
+def test_gset_join_inflation_stats(ctx):
+    n, e_n = 128, 1000
+    a, b, c = (ctx.gset_batch(n, e_n) for _ in range(3))
+    a.fill_synthetic(61)
+    b.fill_synthetic(62)
+    c.join(a, b)
+    ha, hb, hc = a.download(), b.download(), c.download()
+    for i in range(0, n, 13):
+        want = orc.gset_merge(ha[i], hb[i], e_n)
+        assert np.array_equal(orc.gset_members(hc[i], e_n), want)
+    assert np.array_equal(c.stats(), np.array([len(orc.gset_members(x, e_n)) for x in hc]))
+    assert c.is_inflation_of(a).all()
+    assert c.is_inflation_of(a, strict=True).all()
+    assert not c.is_inflation_of(c, strict=True).any()
+    assert c.is_inflation_of(c).all()
+    assert c.equal(c).all()
+
+
+def test_large_join_property(ctx):
+    """A 4 GiB-per-operand batch (2^16 replicas x 4096 elements): join equals p|p' on
+    sampled replicas regenerated by the oracle, and the join is idempotent."""
+    n, e_n = 1 << 16, 4096
+    a, b, c = (ctx.orset_batch(n, e_n) for _ in range(3))
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    c.join(a, b)
+    for i in (0, 1, 12345, n - 1):
+        got = c.download(i, 1)[0]
+        want = orc.synth_orset(2, i, e_n) | orc.synth_orset(3, i, e_n)
+        assert np.array_equal(got, want)
+    assert c.equal(c).all()
+    d = ctx.orset_batch(n, e_n)
+    d.join(c, a)
+    assert d.equal(c).all()
