@@ -1,0 +1,201 @@
+"""Dictionaries and the orddict <-> columnar codec (host side of the boundary).
+
+The device never sees terms.  A `Domain` owns
+  * the element dictionary: element term -> element slot (append-only), and
+  * one token dictionary per element slot: token term -> token slot 0..63 (append-only).
+Every batch of a domain uses those slots, so joins / predicates / combinators between
+its batches are pure bit operations.  Slots are assigned in first-seen order; the
+term order needed for decoding (orddict keys and token keys ascend in Erlang term
+order) is a per-dictionary permutation cached on the host.
+
+Canonical states only: the device layout expresses an orddict whose keys are unique
+and ascending, whose token lists are unique, ascending and non-empty — which is every
+state lasp_orset:new/update/merge can produce (lasp_orset.erl:63-134).  Anything else
+(the unsorted / duplicated outputs of the map and fold combinators, SURVEY.md
+Appendix B) raises NonCanonical instead of being silently canonicalised.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Sequence
+
+import numpy as np
+
+from .terms import hkey, term_cmp, term_key
+
+TOKEN_SLOTS = 64
+
+
+class NonCanonical(ValueError):
+    """The orddict is not expressible in the columnar layout (see module doc)."""
+
+
+class CapacityError(ValueError):
+    """An element needs more than 64 token slots, or the batch has too few slots."""
+
+
+class _Dict:
+    def __init__(self, cap: int):
+        self.cap = cap
+        self.terms: List = []
+        self.index: Dict = {}
+        self._order = None
+
+    def __len__(self):
+        return len(self.terms)
+
+    def slot(self, term, create: bool = True) -> int:
+        k = hkey(term)
+        s = self.index.get(k)
+        if s is None:
+            if not create:
+                return -1
+            if len(self.terms) >= self.cap:
+                raise CapacityError(f"dictionary full ({self.cap} slots)")
+            s = len(self.terms)
+            self.terms.append(term)
+            self.index[k] = s
+            self._order = None
+        return s
+
+    def order(self) -> np.ndarray:
+        """Slots in ascending term order."""
+        if self._order is None or len(self._order) != len(self.terms):
+            idx = sorted(range(len(self.terms)), key=lambda i: term_key(self.terms[i]))
+            self._order = np.asarray(idx, dtype=np.int64)
+        return self._order
+
+
+class Domain:
+    """Element + token dictionaries shared by all batches of one engine domain."""
+
+    def __init__(self, element_capacity: int = 1 << 30):
+        self.elements = _Dict(element_capacity)
+        self.tokens: List[_Dict] = []
+
+    def element_slot(self, elem, create: bool = True) -> int:
+        s = self.elements.slot(elem, create)
+        while create and len(self.tokens) < len(self.elements):
+            self.tokens.append(_Dict(TOKEN_SLOTS))
+        return s
+
+    def token_slot(self, eslot: int, tok, create: bool = True) -> int:
+        try:
+            return self.tokens[eslot].slot(tok, create)
+        except CapacityError as e:
+            raise CapacityError(
+                f"element {self.elements.terms[eslot]!r} has more than {TOKEN_SLOTS} tokens") from e
+
+    @property
+    def size(self) -> int:
+        return len(self.elements)
+
+    # ------------------------------------------------------------------ OR-Set
+    def register_orset(self, s) -> None:
+        for elem, toks in s:
+            es = self.element_slot(elem)
+            for tok, _rm in toks:
+                self.token_slot(es, tok)
+
+    def encode_orset(self, states: Sequence, E: int) -> np.ndarray:
+        """orddicts -> (len(states), E, 2) uint64 {p, r} cells."""
+        for s in states:
+            self.register_orset(s)
+        if self.size > E:
+            raise CapacityError(f"{self.size} elements do not fit {E} slots")
+        out = np.zeros((len(states), E, 2), dtype=np.uint64)
+        for i, s in enumerate(states):
+            _check_canonical_orset(s)
+            for elem, toks in s:
+                es = self.element_slot(elem, create=False)
+                p = r = 0
+                for tok, rm in toks:
+                    bit = 1 << self.token_slot(es, tok, create=False)
+                    p |= bit
+                    if rm is True:
+                        r |= bit
+                    elif rm is not False:
+                        raise NonCanonical(f"token flag {rm!r} is not a boolean")
+                out[i, es, 0] = p
+                out[i, es, 1] = r
+        return out
+
+    def decode_orset(self, cells: np.ndarray) -> list:
+        """(E, 2) cells -> orddict (keys and tokens ascending in term order)."""
+        out = []
+        p_col = cells[:, 0]
+        for es in self.elements.order():
+            if es >= cells.shape[0]:
+                continue
+            p = int(p_col[es])
+            if not p:
+                continue
+            r = int(cells[es, 1])
+            td = self.tokens[es]
+            toks = [(td.terms[k], bool((r >> k) & 1)) for k in td.order() if (p >> int(k)) & 1]
+            out.append((self.elements.terms[es], toks))
+        return out
+
+    def decode_value_bits(self, words: np.ndarray) -> list:
+        """value/1 bitmap -> element terms in term order."""
+        out = []
+        for es in self.elements.order():
+            if (int(words[es >> 6]) >> int(es & 63)) & 1:
+                out.append(self.elements.terms[es])
+        return out
+
+    # ------------------------------------------------------------------ G-Set
+    def encode_gset(self, states: Sequence, E: int) -> np.ndarray:
+        for s in states:
+            for elem in s:
+                self.element_slot(elem)
+        if self.size > E:
+            raise CapacityError(f"{self.size} elements do not fit {E} slots")
+        W = (E + 63) // 64
+        out = np.zeros((len(states), W), dtype=np.uint64)
+        for i, s in enumerate(states):
+            _check_canonical_gset(s)
+            for elem in s:
+                es = self.element_slot(elem, create=False)
+                out[i, es >> 6] |= np.uint64(1) << np.uint64(es & 63)
+        return out
+
+    def decode_gset(self, words: np.ndarray) -> list:
+        return self.decode_value_bits(words)
+
+    def keep_bits(self, pred, E: int) -> np.ndarray:
+        """Evaluate a filter predicate once per element slot (lasp_core.erl:697)."""
+        W = (E + 63) // 64
+        out = np.zeros((W,), dtype=np.uint64)
+        for es, elem in enumerate(self.elements.terms):
+            if pred(elem) is True:
+                out[es >> 6] |= np.uint64(1) << np.uint64(es & 63)
+        return out
+
+
+def _check_canonical_orset(s) -> None:
+    prev = None
+    for item in s:
+        if not (isinstance(item, tuple) and len(item) == 2):
+            raise NonCanonical(f"orddict entry {item!r} is not a 2-tuple")
+        elem, toks = item
+        if prev is not None and term_cmp(prev, elem) >= 0:
+            raise NonCanonical("orddict keys are not strictly ascending")
+        prev = elem
+        if not isinstance(toks, list) or not toks:
+            raise NonCanonical(f"element {elem!r} has an empty or non-list token orddict")
+        tprev = None
+        for t in toks:
+            if not (isinstance(t, tuple) and len(t) == 2):
+                raise NonCanonical("token orddict entry is not a 2-tuple")
+            if tprev is not None and term_cmp(tprev, t[0]) >= 0:
+                raise NonCanonical("token keys are not strictly ascending")
+            tprev = t[0]
+
+
+def _check_canonical_gset(s: Iterable) -> None:
+    prev = None
+    for e in s:
+        if prev is not None and term_cmp(prev, e) >= 0:
+            raise NonCanonical("ordset is not strictly ascending")
+        prev = e

@@ -4,7 +4,7 @@
 // Design rules applied (cdna_hip_programming.md §6, MI355X_MICROARCH.md §HBM):
 //   * 16 B per lane per access (global_load/store_dwordx4): one wave-instruction moves
 //     1 KiB of consecutive bytes; cells are {p, r} u64 pairs so one load = one cell.
-//   * grid-stride loops over ~8 workgroups per CU with U cells in flight per lane,
+//   * grid-stride loops over 64 workgroups per CU with U cells in flight per lane,
 //     non-temporal loads/stores for once-touched streams (206 GB per join batch never
 //     fits the 256 MiB Infinity Cache).
 //   * per-replica predicates use one wave64 per replica: lanes walk the replica's
@@ -44,8 +44,11 @@ __device__ __forceinline__ u64 wave_sum(u64 v) {
 
 StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16) {
     StreamTune t;
-    t.grid = ctx->tune_grid > 0 ? (int)ctx->tune_grid : ctx->cus * 8;
-    t.unroll = ctx->tune_unroll > 0 ? (int)ctx->tune_unroll : 4;
+    // defaults from the bench-size sweep (profiles/r01_sweep_join.log): 64 workgroups
+    // per CU x 2 cells in flight per lane reached 6.1 TB/s; 8/CU (persistent-style)
+    // stayed at 5.6-5.8 TB/s.
+    t.grid = ctx->tune_grid > 0 ? (int)ctx->tune_grid : ctx->cus * 64;
+    t.unroll = ctx->tune_unroll > 0 ? (int)ctx->tune_unroll : 2;
     t.nt = ctx->tune_nt < 0 ? true : ctx->tune_nt != 0;
     uint64_t need = (n16 + kBlock - 1) / kBlock;
     if (need < (uint64_t)t.grid) t.grid = need > 0 ? (int)need : 1;

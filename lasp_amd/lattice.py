@@ -1,0 +1,46 @@
+"""lasp_lattice mirror: threshold_met / is_inflation / is_strict_inflation for the
+lasp_orset and lasp_gset clauses (src/lasp_lattice.erl:62-75, 137-161, 212-253),
+computed by the wave64 ballot kernels on the device."""
+
+from __future__ import annotations
+
+from .codec import Domain
+from .orset import context
+from . import gset as _gset
+
+
+def _pair(type_, prev, cur):
+    dom = Domain()
+    ctx = context()
+    if type_ == "lasp_orset":
+        dom.register_orset(prev)
+        dom.register_orset(cur)
+        E = max(1, dom.size)
+        P, C = ctx.orset_batch(1, E), ctx.orset_batch(1, E)
+        P.upload(dom.encode_orset([prev], E))
+        C.upload(dom.encode_orset([cur], E))
+        return P, C
+    if type_ == "lasp_gset":
+        for e in list(prev) + list(cur):
+            dom.element_slot(e)
+        return _gset._batch(dom, [prev]), _gset._batch(dom, [cur])
+    raise ValueError(f"type {type_!r} is not on the device path (lasp_orset | lasp_gset)")
+
+
+def is_inflation(type_, prev, cur) -> bool:
+    """is_inflation/3 — lasp_lattice.erl:97-98."""
+    P, C = _pair(type_, prev, cur)
+    return bool(C.is_inflation_of(P)[0])
+
+
+def is_strict_inflation(type_, prev, cur) -> bool:
+    """is_strict_inflation/3 — lasp_lattice.erl:105-106."""
+    P, C = _pair(type_, prev, cur)
+    return bool(C.is_inflation_of(P, strict=True)[0])
+
+
+def threshold_met(type_, value, threshold) -> bool:
+    """threshold_met/3 — lasp_lattice.erl:62-75: {strict, T} -> strict inflation of T."""
+    if isinstance(threshold, tuple) and len(threshold) == 2 and threshold[0] == "strict":
+        return is_strict_inflation(type_, threshold[1], value)
+    return is_inflation(type_, threshold, value)

@@ -1,0 +1,192 @@
+"""lasp_orset mirror over the MI355X engine (the NIF module's behaviour, in Python).
+
+Same names, argument meaning and error behaviour as src/lasp_orset.erl; states are
+Erlang-shaped orddicts (see lasp_amd.terms).  Each call encodes its operands into a
+batch of a per-call Domain, runs the HIP kernel through the C ABI and decodes the
+result — the single-object path of the drop-in.  Throughput callers batch many
+objects per call (`merge_many`, or lasp_amd.engine directly).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib, engine
+from .codec import Domain, NonCanonical  # noqa: F401  (re-exported error type)
+from .terms import Atom
+
+_CTX = None
+
+
+def context() -> engine.Context:
+    """The process-wide engine context (device $LASPJ_DEVICE, default 0)."""
+    global _CTX
+    if _CTX is None:
+        _CTX = engine.Context(int(os.environ.get("LASPJ_DEVICE", "0")))
+    return _CTX
+
+
+def _batch(dom: Domain, states: Sequence) -> Tuple[engine.ORSetBatch, int]:
+    for s in states:
+        dom.register_orset(s)
+    E = max(1, dom.size)
+    b = context().orset_batch(len(states), E)
+    b.upload(dom.encode_orset(states, E))
+    return b, E
+
+
+# --------------------------------------------------------------------------- API
+
+def new():
+    """new/0 — lasp_orset.erl:63-65."""
+    return []
+
+
+def merge(a, b):
+    """merge/2 — lasp_orset.erl:128-134 (device join)."""
+    return merge_many([(a, b)])[0]
+
+
+def merge_many(pairs: Sequence[Tuple[list, list]]) -> List[list]:
+    """merge/2 over many independent pairs in one launch."""
+    if not pairs:
+        return []
+    dom = Domain()
+    A, E = _batch(dom, [p[0] for p in pairs])
+    B, _ = _batch(dom, [p[1] for p in pairs])
+    if B.elements != E:             # B registered more elements: re-encode A at B's size
+        A, E = _batch(dom, [p[0] for p in pairs])
+    C = context().orset_batch(len(pairs), E)
+    C.join(A, B)
+    out = C.download()
+    return [dom.decode_orset(out[i]) for i in range(len(pairs))]
+
+
+def value(s):
+    """value/1 — lasp_orset.erl:67-73 (device value bitmap)."""
+    dom = Domain()
+    b, _ = _batch(dom, [s])
+    return dom.decode_value_bits(b.value_bits()[0])
+
+
+def value2(query, s):
+    """value/2 — lasp_orset.erl:75-97."""
+    if isinstance(query, tuple) and len(query) == 2 and query[0] == "fragment":
+        toks = value2(("tokens", query[1]), s)
+        return [] if toks == [] else [(query[1], toks)]
+    if isinstance(query, tuple) and len(query) == 2 and query[0] == "tokens":
+        dom = Domain()
+        b, _ = _batch(dom, [s])
+        es = dom.element_slot(query[1], create=False)
+        if es < 0:
+            return []
+        cells = b.download()[0]
+        return dict(dom.decode_orset(cells)).get(dom.elements.terms[es], [])
+    if query == "removed":
+        dom = Domain()
+        b, _ = _batch(dom, [s])
+        return dom.decode_value_bits(b.value_bits(removed=True)[0])
+    return value(s)
+
+
+def update(op, actor, s):
+    """update/3 — lasp_orset.erl:99-117.  Returns ("ok", S1) or
+    ("error", ("precondition", ("not_present", Elem)))."""
+    dom = Domain()
+    dom.register_orset(s)
+    ops = []
+    _compile(op, dom, ops, new_call=True)
+    E = max(1, dom.size)
+    b = context().orset_batch(1, E)
+    b.upload(dom.encode_orset([s], E))
+    st = b.apply_ops(ops)
+    bad = np.nonzero(st == _lib.OPST_NOT_PRESENT)[0]
+    if len(bad):
+        return ("error", ("precondition", ("not_present", dom.elements.terms[ops[bad[0]][1]])))
+    return ("ok", dom.decode_orset(b.download()[0]))
+
+
+def update4(op, actor, s, _ctx=None):
+    """update/4 — lasp_orset.erl:119-122 (context ignored)."""
+    return update(op, actor, s)
+
+
+def _unique(_actor) -> bytes:
+    """unique/1 — lasp_orset.erl:261-262: 20 random bytes."""
+    return os.urandom(20)
+
+
+def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
+    kind = op[0]
+    flag = _lib.OP_FLAG_NEW_CALL if new_call else 0
+    if kind in ("add", "add_by_token"):
+        elem = op[1] if kind == "add" else op[2]
+        tok = _unique(None) if kind == "add" else op[1]
+        es = dom.element_slot(elem)
+        ops.append((0, es, _lib.OP_ADD, dom.token_slot(es, tok), flag))
+    elif kind == "add_all":
+        # foldl of update({add, E}) (:106-111): every add is its own call
+        for e in op[1]:
+            es = dom.element_slot(e)
+            ops.append((0, es, _lib.OP_ADD, dom.token_slot(es, _unique(None)),
+                        _lib.OP_FLAG_NEW_CALL))
+    elif kind == "remove":
+        ops.append((0, dom.element_slot(op[1]), _lib.OP_REMOVE, 0, flag))
+    elif kind == "remove_all":
+        # remove_elems/2 (:244-250): one all-or-nothing call
+        for k, e in enumerate(op[1]):
+            ops.append((0, dom.element_slot(e), _lib.OP_REMOVE, 0, flag if k == 0 else 0))
+    elif kind == "update":
+        # apply_ops/3 (:253-259): the whole list is one all-or-nothing call
+        first = len(ops)
+        for sub in op[1]:
+            _compile(sub, dom, ops, new_call=False)
+        if len(ops) > first:
+            r, e, k, sl, _f = ops[first]
+            ops[first] = (r, e, k, sl, flag)
+        for j in range(first + 1, len(ops)):
+            r, e, k, sl, _f = ops[j]
+            ops[j] = (r, e, k, sl, 0)
+    else:
+        raise ValueError(f"function_clause: {op!r}")
+
+
+def equal(a, b) -> bool:
+    """equal/2 — lasp_orset.erl:136-138."""
+    dom = Domain()
+    dom.register_orset(a)
+    dom.register_orset(b)
+    E = max(1, dom.size)
+    A = context().orset_batch(1, E)
+    B = context().orset_batch(1, E)
+    A.upload(dom.encode_orset([a], E))
+    B.upload(dom.encode_orset([b], E))
+    return bool(A.equal(B)[0])
+
+
+def stats(s):
+    """stats/1 — lasp_orset.erl:156-161."""
+    dom = Domain()
+    b, _ = _batch(dom, [s])
+    elems, adds, rems = (int(x) for x in b.stats()[0])
+    return [("element_count", elems), ("adds_count", adds), ("removes_count", rems),
+            ("waste_pct", _waste_pct(adds, rems))]
+
+
+def stat(name, s):
+    """stat/2 — lasp_orset.erl:163-192 (unknown stat -> undefined)."""
+    for k, v in stats(s):
+        if k == name:
+            return v
+    return Atom("undefined")
+
+
+def _waste_pct(adds: int, rems: int) -> int:
+    # case Tags of 0 -> 0; _ -> round(Tombs / AllTags * 100) end  (erlang:round: half away)
+    if adds == 0:
+        return 0
+    import math
+    return int(math.floor(rems / (adds + rems) * 100 + 0.5))

@@ -34,7 +34,7 @@ _NUM, _ATOM, _TUPLE, _MAP, _NIL, _LIST, _BIN = 0, 1, 6, 7, 8, 9, 10
 
 
 def _rank(t) -> int:
-    if isinstance(t, bool) or isinstance(t, Atom):
+    if isinstance(t, (bool, str)):      # any str subclass is an atom (product's too)
         return _ATOM
     if isinstance(t, (int, float)):
         return _NUM

@@ -1,0 +1,73 @@
+"""The C-ABI library loads and exports every entry point include/laspj.h declares, and
+the ctypes binding (the NIF stand-in) binds each of them.  No compute without a GPU."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from lasp_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    src = open(os.path.join(ROOT, "include", "laspj.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(laspj_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from lasp_amd import build
+    build.build()
+    return _lib.load()
+
+
+def test_header_parses():
+    names = declared()
+    assert "laspj_orset_join" in names and "laspj_orset_inflation" in names
+    assert len(names) >= 40
+
+
+def test_every_declared_symbol_is_exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (laspj_\w+)", out))
+    missing = [n for n in declared() if n not in exported]
+    assert not missing, missing
+    for n in declared():
+        assert hasattr(lib, n)
+
+
+def test_binding_covers_header():
+    assert sorted(_lib.SIGNATURES) == declared()
+
+
+def test_abi_calls_without_gpu(lib):
+    assert lib.laspj_abi_version() == 1
+    assert lib.laspj_strerror(_lib.E_SHAPE) == b"shape mismatch"
+    n = ctypes.c_int(-1)
+    assert lib.laspj_device_count(ctypes.byref(n)) == 0
+    assert n.value >= 0
+    # null handles are rejected with LASPJ_E_INVAL, never a crash
+    assert lib.laspj_orset_join(None, None, None, None) == _lib.E_INVAL
+    assert lib.laspj_ctx_destroy(None) == _lib.E_INVAL
+    assert lib.laspj_ctx_create(0, None) == _lib.E_INVAL
+    if n.value == 0:
+        h = ctypes.c_void_p()
+        assert lib.laspj_ctx_create(0, ctypes.byref(h)) == _lib.E_DEVICE
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(_lib.Op) == 16
+    assert ctypes.sizeof(_lib.BatchInfo) == 32
+
+
+def test_engine_fails_loudly_without_library(monkeypatch):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/liblaspj.so")
+    with pytest.raises(_lib.LaspjUnavailable):
+        _lib.load()
