@@ -52,8 +52,14 @@ extern "C" {
 #define LASPJ_E_COMM          -7   /* RCCL communicator error                            */
 #define LASPJ_E_UNSUPPORTED   -8   /* built without the feature                          */
 
-#define LASPJ_KIND_ORSET 1
-#define LASPJ_KIND_GSET  2
+#define LASPJ_KIND_ORSET         1
+#define LASPJ_KIND_GSET          2
+/* combinator outputs whose reference list is not an orddict of the input shape:     */
+#define LASPJ_KIND_ORSET_CONCAT  3  /* intersection: 32 B/cell {pL, rL, pR, rR}; the
+                                       element's token list decodes as Cx ++ Cy       */
+#define LASPJ_KIND_ORSET_PRODUCT 4  /* product: EL x ER cells of uint32
+                                       {pX:8, rX:8, pY:8, rY:8}, cell (x,y) at x*ER+y  */
+#define LASPJ_KIND_GSET_PRODUCT  5  /* product: EL rows x ceil(ER/64) words           */
 
 typedef struct laspj_ctx   laspj_ctx;
 typedef struct laspj_buf   laspj_buf;
@@ -63,10 +69,13 @@ typedef struct laspj_comm  laspj_comm;
 
 typedef struct laspj_batch_info {
     int32_t  kind;               /* LASPJ_KIND_*                                       */
-    uint32_t elements;           /* E: element slots per replica                       */
+    uint32_t elements;           /* E: element slots per replica (EL for products)     */
     uint64_t replicas;           /* R                                                  */
-    uint64_t bytes_per_replica;  /* 16*E (OR-Set) or 8*ceil(E/64) (G-Set)              */
+    uint64_t bytes_per_replica;  /* 16*E (OR-Set) or 8*ceil(E/64) (G-Set) ...          */
     uint64_t bytes;              /* R * bytes_per_replica                              */
+    uint32_t elements_r;         /* ER for product batches, else 0                     */
+    uint32_t reserved;
+    uint64_t cells_per_replica;  /* E, or EL*ER for products                           */
 } laspj_batch_info;
 
 /* One update operation (lasp_orset:update/3, lasp_orset.erl:99-117;
@@ -143,7 +152,9 @@ int laspj_orset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
 int laspj_orset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                        uint32_t group);
 /* value/1 — lasp_orset.erl:67-73: bit e of replica i set iff element e has a token
- * with flag false.  out: R * ceil(E/64) uint64 words. */
+ * with flag false.  out: R * ceil(C/64) uint64 words, C = cells per replica.
+ * Also accepts combinator outputs: a CONCAT cell is visible if Cx ++ Cy has a false
+ * flag, a PRODUCT cell (x, y) iff both x and y have one. */
 int laspj_orset_value(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
 /* value(removed, S) — lasp_orset.erl:90-95: elements with a token flagged true */
 int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
@@ -173,6 +184,29 @@ int laspj_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
 int laspj_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                        const laspj_buf* keep);
 
+/* intersection body for lasp_orset — lasp_core.erl:546-589 with
+ * lasp_lattice:orset_causal_union/2 (:311-312): element e of L that keyfind-s in R
+ * becomes {e, Cx ++ Cy}.  l, r: OR-Set batches over the same element slots;
+ * dst: LASPJ_KIND_ORSET_CONCAT batch of the same shape. */
+int laspj_orset_concat_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                                    laspj_batch** out);
+int laspj_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                             const laspj_batch* r);
+/* product body for lasp_orset — lasp_core.erl:499-533 with
+ * lasp_lattice:orset_causal_product/2 (:303-308): cell (x, y) holds the 8-bit token
+ * masks of x and y (the token set is Tx x Ty, flag = Dx orelse Dy).  Token slots must
+ * be < 8 (else LASPJ_E_RANGE, checked on the device).  l has EL slots, r ER slots. */
+int laspj_orset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                     uint32_t er, laspj_batch** out);
+int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                        const laspj_batch* r);
+/* map / fold bodies — lasp_core.erl:641-667, :460-486: output slot o takes the cell of
+ * input slot index[o] (uint32 per dst slot; 0xFFFFFFFF = empty).  The host builds the
+ * index from F over the element dictionary (a map is one slot per input slot, a fold
+ * one slot per F(X) entry, in list order). */
+int laspj_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       const laspj_buf* index);
+
 /* ------------------------------------------------------------------ lasp_gset */
 /* merge/2 — lasp_gset.erl:99-101 (ordsets:union on canonical sets = OR) */
 int laspj_gset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
@@ -189,6 +223,26 @@ int laspj_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
 /* update/3 add / add_all — lasp_gset.erl:84-88 (LASPJ_OP_ADD only) */
 int laspj_gset_apply_ops(laspj_ctx* ctx, laspj_batch* batch, const laspj_op* ops,
                          uint64_t nops, int32_t* status);
+
+/* union body for lasp_gset — lasp_core.erl:620 binds `L ++ R`; on ordsets that are
+ * disjoint and ordered this is their union, which is what this computes (bitwise OR);
+ * an overlapping L ++ R is not a set and is not produced. */
+int laspj_gset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                     const laspj_batch* r);
+/* intersection body for lasp_gset — lasp_core.erl:569-576 (lists:member) */
+int laspj_gset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                            const laspj_batch* r);
+/* filter body for lasp_gset — lasp_core.erl:681-712 */
+int laspj_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* keep);
+/* product body for lasp_gset — lasp_core.erl:518-520: bit (x, y) = x in L and y in R */
+int laspj_gset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                    uint32_t er, laspj_batch** out);
+int laspj_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                       const laspj_batch* r);
+/* map / fold bodies for lasp_gset: dst bit o = src bit index[o] */
+int laspj_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* index);
 
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);

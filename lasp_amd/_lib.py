@@ -17,7 +17,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "laspj.h")
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
     -1, -2, -3, -4, -5, -6, -7, -8)
-KIND_ORSET, KIND_GSET = 1, 2
+KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 OP_ADD, OP_REMOVE = 1, 2
 OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK = 0, 1, 2
@@ -36,7 +36,9 @@ class LaspjError(RuntimeError):
 
 class BatchInfo(C.Structure):
     _fields_ = [("kind", C.c_int32), ("elements", C.c_uint32), ("replicas", C.c_uint64),
-                ("bytes_per_replica", C.c_uint64), ("bytes", C.c_uint64)]
+                ("bytes_per_replica", C.c_uint64), ("bytes", C.c_uint64),
+                ("elements_r", C.c_uint32), ("reserved", C.c_uint32),
+                ("cells_per_replica", C.c_uint64)]
 
 
 class Op(C.Structure):
@@ -83,6 +85,17 @@ SIGNATURES = {
     "laspj_orset_apply_ops": (i, [vp, vp, C.POINTER(Op), u64, C.POINTER(C.c_int32)]),
     "laspj_orset_union": (i, [vp, vp, vp, vp]),
     "laspj_orset_filter": (i, [vp, vp, vp, vp]),
+    "laspj_orset_concat_batch_create": (i, [vp, u64, u32, vpp]),
+    "laspj_orset_intersection": (i, [vp, vp, vp, vp]),
+    "laspj_orset_product_batch_create": (i, [vp, u64, u32, u32, vpp]),
+    "laspj_orset_product": (i, [vp, vp, vp, vp]),
+    "laspj_orset_gather": (i, [vp, vp, vp, vp]),
+    "laspj_gset_union": (i, [vp, vp, vp, vp]),
+    "laspj_gset_intersection": (i, [vp, vp, vp, vp]),
+    "laspj_gset_filter": (i, [vp, vp, vp, vp]),
+    "laspj_gset_product_batch_create": (i, [vp, u64, u32, u32, vpp]),
+    "laspj_gset_product": (i, [vp, vp, vp, vp]),
+    "laspj_gset_gather": (i, [vp, vp, vp, vp]),
     "laspj_gset_join": (i, [vp, vp, vp, vp]),
     "laspj_gset_reduce": (i, [vp, vp, vp, u32]),
     "laspj_gset_stats": (i, [vp, vp, vp]),

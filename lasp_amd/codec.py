@@ -132,7 +132,7 @@ class Domain:
                 continue
             r = int(cells[es, 1])
             td = self.tokens[es]
-            toks = [(td.terms[k], bool((r >> k) & 1)) for k in td.order() if (p >> int(k)) & 1]
+            toks = [(td.terms[k], bool((r >> int(k)) & 1)) for k in td.order() if (p >> int(k)) & 1]
             out.append((self.elements.terms[es], toks))
         return out
 
@@ -199,3 +199,102 @@ def _check_canonical_gset(s: Iterable) -> None:
         if prev is not None and term_cmp(prev, e) >= 0:
             raise NonCanonical("ordset is not strictly ascending")
         prev = e
+
+
+# ---------------------------------------------------------------------- combinator outputs
+
+def decode_concat(dom: Domain, cells: np.ndarray) -> list:
+    """CONCAT cells (E, 4) {pL, rL, pR, rR} -> the intersection body's list
+    [{X, Cx ++ Cy}] in L's (term) order (lasp_core.erl:559-583, lasp_lattice.erl:311-312)."""
+    out = []
+    for es in dom.elements.order():
+        if es >= cells.shape[0]:
+            continue
+        pl, rl, pr, rr = (int(v) for v in cells[es])
+        if not pl:
+            continue
+        td = dom.tokens[es]
+        cx = [(td.terms[k], bool((rl >> int(k)) & 1)) for k in td.order() if (pl >> int(k)) & 1]
+        cy = [(td.terms[k], bool((rr >> int(k)) & 1)) for k in td.order() if (pr >> int(k)) & 1]
+        out.append((dom.elements.terms[es], cx + cy))
+    return out
+
+
+def decode_product(dl: Domain, dr: Domain, cells: np.ndarray) -> list:
+    """PRODUCT cells (EL, ER) uint32 -> the product body's list, X-major, each with
+    orset_causal_product's fully reversed token order (lasp_lattice.erl:303-308)."""
+    out = []
+    xs = [int(x) for x in dl.elements.order() if x < cells.shape[0]]
+    ys = [int(y) for y in dr.elements.order() if y < cells.shape[1]]
+    for x in xs:
+        row = cells[x]
+        for y in ys:
+            c = int(row[y])
+            if not c:
+                continue
+            px, rx, py, ry = c & 0xFF, (c >> 8) & 0xFF, (c >> 16) & 0xFF, (c >> 24) & 0xFF
+            tdx, tdy = dl.tokens[x], dr.tokens[y]
+            tx = [(tdx.terms[k], bool((rx >> int(k)) & 1)) for k in tdx.order() if (px >> int(k)) & 1]
+            ty = [(tdy.terms[k], bool((ry >> int(k)) & 1)) for k in tdy.order() if (py >> int(k)) & 1]
+            toks = [([a, b], da or db) for a, da in reversed(tx) for b, db in reversed(ty)]
+            out.append(((dl.elements.terms[x], dr.elements.terms[y]), toks))
+    return out
+
+
+def decode_gset_product(dl: Domain, dr: Domain, rows: np.ndarray) -> list:
+    """G-Set product rows (EL, ceil(ER/64)) -> [{X, Y}] X-major (lasp_core.erl:518-520)."""
+    out = []
+    ys = [int(y) for y in dr.elements.order()]
+    for x in dl.elements.order():
+        x = int(x)
+        if x >= rows.shape[0]:
+            continue
+        for y in ys:
+            if (int(rows[x, y >> 6]) >> (y & 63)) & 1:
+                out.append((dl.elements.terms[x], dr.elements.terms[y]))
+    return out
+
+
+class SeqOutput:
+    """Output of the map / fold bodies (lasp_core.erl:641-667, 460-486): a list whose
+    slot s holds key keys[s] with the causality of input slot src[s].  Slots are laid
+    out in the input's list order, so decoding in slot order reproduces the reference's
+    list exactly — unsorted or duplicated keys included."""
+
+    def __init__(self, dom: Domain, keys: list, src: list):
+        self.dom, self.keys, self.src = dom, keys, src
+
+    @classmethod
+    def map(cls, dom: Domain, fun) -> "SeqOutput":
+        order = [int(s) for s in dom.elements.order()]
+        return cls(dom, [fun(dom.elements.terms[s]) for s in order], order)
+
+    @classmethod
+    def fold(cls, dom: Domain, fun) -> "SeqOutput":
+        keys, src = [], []
+        for s in dom.elements.order():
+            for v in fun(dom.elements.terms[int(s)]):
+                keys.append(v)
+                src.append(int(s))
+        return cls(dom, keys, src)
+
+    @property
+    def size(self) -> int:
+        return len(self.keys)
+
+    def index(self) -> np.ndarray:
+        return np.asarray(self.src if self.src else [0xFFFFFFFF], dtype=np.uint32)
+
+    def decode_orset(self, cells: np.ndarray) -> list:
+        out = []
+        for o, (key, s) in enumerate(zip(self.keys, self.src)):
+            p, r = int(cells[o, 0]), int(cells[o, 1])
+            if not p:
+                continue
+            td = self.dom.tokens[s]
+            out.append((key, [(td.terms[k], bool((r >> int(k)) & 1))
+                              for k in td.order() if (p >> int(k)) & 1]))
+        return out
+
+    def decode_bits(self, words: np.ndarray) -> list:
+        return [key for o, key in enumerate(self.keys) if (int(words[o >> 6]) >> (o & 63)) & 1]

@@ -1,0 +1,315 @@
+// Combinator kernels: the bodies lasp_core re-runs on every bind (src/lasp_core.erl:
+// 460-712) over device-resident replicas.  All HBM-bound integer work (no MFMA).
+//
+//   intersection  per-slot select into 32-byte CONCAT cells {pL, rL, pR, rR}: the
+//                 reference's token list for a kept element is Cx ++ Cy
+//                 (lasp_lattice:orset_causal_union/2), so both halves are kept as is.
+//   product       LDS-tiled outer product: a 64-row x 1024-column tile stages the two
+//                 input strips once as packed 16-bit {p8, r8} words, then every lane
+//                 writes 4 cells (16 B, dwordx4, non-temporal) per row; output is 4 B
+//                 per (x, y) cell, i.e. the product is write-bound at |L|*|R|*4 B.
+//   gather        map / fold: output slot o copies input slot index[o].
+//   G-Set         AND / filter / outer product / bit gather on bitmaps.
+
+#include "laspj_internal.h"
+
+namespace laspj {
+
+typedef unsigned long long u64;
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kB = 256;
+
+__device__ __forceinline__ u64x2 ldnt(const u64x2* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void stnt(u64x2* p, u64x2 v) { __builtin_nontemporal_store(v, p); }
+
+static int grid_for(const laspj_ctx* ctx, uint64_t items, int per_cu = 64) {
+    uint64_t g = (items + kB - 1) / kB;
+    uint64_t cap = (uint64_t)ctx->cus * per_cu;
+    if (g > cap) g = cap;
+    return g ? (int)g : 1;
+}
+
+// ------------------------------------------------------------------ intersection
+
+__global__ __launch_bounds__(kB) void k_orset_intersection(u64x2* out, const u64x2* l,
+                                                           const u64x2* r, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        u64x2 a = ldnt(l + i), b = ldnt(r + i);
+        bool keep = (a.x != 0) & (b.x != 0);   // X in L and lists:keyfind(X, R) found
+        u64x2 z = {0, 0};
+        stnt(out + 2 * i, keep ? a : z);
+        stnt(out + 2 * i + 1, keep ? b : z);
+    }
+}
+
+hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                     const laspj_batch* r) {
+    uint64_t n = l->replicas * l->elements;
+    hipLaunchKernelGGL(k_orset_intersection, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
+                       reinterpret_cast<const u64x2*>(r->dev), n);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ product (OR-Set)
+
+constexpr int kPX = 64;     // rows per tile
+constexpr int kPY = 1024;   // columns per tile = 4 per lane
+
+__device__ __forceinline__ uint32_t pack8(u64x2 c, uint32_t* flag) {
+    if (c.x >> 8) atomicOr(flag, 1u);          // token slot >= 8: not expressible in 4 B
+    return c.x ? (uint32_t)((c.x & 0xFFull) | ((c.y & 0xFFull) << 8)) : 0u;
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(kB) void k_orset_product(uint32_t* out, const u64x2* L,
+                                                      const u64x2* R, uint64_t reps,
+                                                      uint32_t EL, uint32_t ER,
+                                                      uint64_t cstride, uint32_t* flag) {
+    __shared__ __attribute__((aligned(16))) uint32_t ry[kPY];
+    __shared__ uint32_t lx[kPX];
+    const uint64_t tx_n = (EL + kPX - 1) / kPX, ty_n = (ER + kPY - 1) / kPY;
+    const uint64_t tiles = reps * tx_n * ty_n;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        uint64_t rep = t / (tx_n * ty_n);
+        uint64_t rem = t - rep * tx_n * ty_n;
+        uint32_t tx = (uint32_t)(rem / ty_n), ty = (uint32_t)(rem - (uint64_t)tx * ty_n);
+        uint32_t x0 = tx * kPX, y0 = ty * kPY;
+        for (int i = threadIdx.x; i < kPY; i += kB) {
+            uint32_t y = y0 + i;
+            ry[i] = y < ER ? pack8(ldnt(R + rep * ER + y), flag) << 16 : 0u;
+        }
+        for (int i = threadIdx.x; i < kPX; i += kB) {
+            uint32_t x = x0 + i;
+            lx[i] = x < EL ? pack8(ldnt(L + rep * EL + x), flag) : 0u;
+        }
+        __syncthreads();
+        const uint32_t yl = threadIdx.x * 4;
+        u32x4 ryv = *reinterpret_cast<const u32x4*>(&ry[yl]);
+        const uint32_t rows = min((uint32_t)kPX, EL - x0);
+        for (uint32_t rr = 0; rr < rows; ++rr) {
+            uint32_t lv = lx[rr];
+            u32x4 v;
+            v.x = (lv && ryv.x) ? lv | ryv.x : 0u;
+            v.y = (lv && ryv.y) ? lv | ryv.y : 0u;
+            v.z = (lv && ryv.z) ? lv | ryv.z : 0u;
+            v.w = (lv && ryv.w) ? lv | ryv.w : 0u;
+            uint64_t base = rep * cstride + (uint64_t)(x0 + rr) * ER + y0 + yl;
+            if (ALIGNED && y0 + yl + 3 < ER) {
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + base));
+            } else {
+                uint32_t y = y0 + yl;
+                if (y < ER) out[base] = v.x;
+                if (y + 1 < ER) out[base + 1] = v.y;
+                if (y + 2 < ER) out[base + 2] = v.z;
+                if (y + 3 < ER) out[base + 3] = v.w;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                const laspj_batch* r, uint32_t* flag) {
+    uint64_t tiles = l->replicas * ((l->elements + kPX - 1) / kPX) *
+                     ((r->elements + kPY - 1) / kPY);
+    uint64_t g = tiles < (uint64_t)ctx->cus * 32 ? tiles : (uint64_t)ctx->cus * 32;
+    auto* o = reinterpret_cast<uint32_t*>(dst->dev);
+    auto* L = reinterpret_cast<const u64x2*>(l->dev);
+    auto* R = reinterpret_cast<const u64x2*>(r->dev);
+    if (r->elements % 4 == 0)
+        hipLaunchKernelGGL(k_orset_product<true>, dim3((unsigned)g), dim3(kB), 0, ctx->stream, o,
+                           L, R, l->replicas, l->elements, r->elements,
+                           2 * dst->words_per_replica, flag);
+    else
+        hipLaunchKernelGGL(k_orset_product<false>, dim3((unsigned)g), dim3(kB), 0, ctx->stream,
+                           o, L, R, l->replicas, l->elements, r->elements,
+                           2 * dst->words_per_replica, flag);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ gather (map / fold)
+
+__global__ __launch_bounds__(kB) void k_orset_gather(u64x2* out, const u64x2* src,
+                                                     const uint32_t* index, uint64_t reps,
+                                                     uint32_t E_out, uint32_t E_in) {
+    const uint64_t n = reps * E_out;
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        uint64_t rep = i / E_out;
+        uint32_t o = (uint32_t)(i - rep * E_out);
+        uint32_t s = index[o];
+        u64x2 v = {0, 0};
+        if (s < E_in) v = src[rep * E_in + s];
+        stnt(out + i, v);
+    }
+}
+
+hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                               const uint32_t* index) {
+    uint64_t n = dst->replicas * dst->elements;
+    hipLaunchKernelGGL(k_orset_gather, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(src->dev),
+                       index, dst->replicas, dst->elements, src->elements);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ G-Set
+
+__global__ __launch_bounds__(kB) void k_and16(u64x2* d, const u64x2* a, const u64x2* b,
+                                              uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride)
+        stnt(d + i, ldnt(a + i) & ldnt(b + i));
+}
+
+__global__ void k_and_tail(u64* d, const u64* a, const u64* b, uint64_t idx) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) d[idx] = a[idx] & b[idx];
+}
+
+hipError_t launch_and(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                      uint64_t words) {
+    uint64_t n = words / 2;
+    if (n)
+        hipLaunchKernelGGL(k_and16, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                           reinterpret_cast<u64x2*>(dst), reinterpret_cast<const u64x2*>(a),
+                           reinterpret_cast<const u64x2*>(b), n);
+    if (words & 1)
+        hipLaunchKernelGGL(k_and_tail, dim3(1), dim3(64), 0, ctx->stream, (u64*)dst,
+                           (const u64*)a, (const u64*)b, words - 1);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kB) void k_gset_filter(u64* d, const u64* s, const u64* keep,
+                                                    uint64_t reps, uint64_t W) {
+    const uint64_t n = reps * W;
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride)
+        d[i] = s[i] & keep[i % W];
+}
+
+hipError_t launch_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              const uint64_t* keep) {
+    uint64_t n = src->replicas * src->words_per_replica;
+    hipLaunchKernelGGL(k_gset_filter, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                       (u64*)dst->dev, (const u64*)src->dev, (const u64*)keep, src->replicas,
+                       src->words_per_replica);
+    return hipGetLastError();
+}
+
+// dst replica i: EL rows of WR words; row x = R's bitmap if x in L, else 0
+__global__ __launch_bounds__(kB) void k_gset_product(u64* d, const u64* L, const u64* R,
+                                                     uint64_t reps, uint32_t EL, uint64_t WL,
+                                                     uint64_t WR) {
+    const uint64_t n = reps * EL * WR;
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+        uint64_t row = i / WR, w = i - row * WR;
+        uint64_t rep = row / EL;
+        uint32_t x = (uint32_t)(row - rep * EL);
+        bool in_l = (L[rep * WL + (x >> 6)] >> (x & 63u)) & 1ull;
+        d[i] = in_l ? R[rep * WR + w] : 0ull;
+    }
+}
+
+hipError_t launch_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                               const laspj_batch* r) {
+    uint64_t WR = r->words_per_replica;
+    uint64_t n = l->replicas * (uint64_t)l->elements * WR;
+    hipLaunchKernelGGL(k_gset_product, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                       (u64*)dst->dev, (const u64*)l->dev, (const u64*)r->dev, l->replicas,
+                       l->elements, l->words_per_replica, WR);
+    return hipGetLastError();
+}
+
+// wave per destination word: lane = bit, __ballot packs
+__global__ __launch_bounds__(kB) void k_gset_gather(u64* d, const u64* s, const uint32_t* index,
+                                                    uint64_t reps, uint32_t E_out,
+                                                    uint32_t E_in) {
+    const uint64_t Wo = (E_out + 63u) / 64u, Wi = (E_in + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kB / 64);
+    for (uint64_t w = ((uint64_t)blockIdx.x * kB + threadIdx.x) >> 6; w < reps * Wo;
+         w += nwaves) {
+        uint64_t rep = w / Wo;
+        uint32_t o = (uint32_t)(w - rep * Wo) * 64u + lane;
+        bool bit = false;
+        if (o < E_out) {
+            uint32_t src = index[o];
+            if (src < E_in) bit = (s[rep * Wi + (src >> 6)] >> (src & 63u)) & 1ull;
+        }
+        u64 m = __ballot(bit);
+        if (lane == 0) d[w] = m;
+    }
+}
+
+hipError_t launch_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              const uint32_t* index) {
+    uint64_t words = dst->replicas * dst->words_per_replica;
+    hipLaunchKernelGGL(k_gset_gather, dim3(grid_for(ctx, words * 64)), dim3(kB), 0, ctx->stream,
+                       (u64*)dst->dev, (const u64*)src->dev, index, dst->replicas, dst->elements,
+                       src->elements);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ value of outputs
+
+// CONCAT: visible iff the element is present and Cx ++ Cy holds a {Token, false}
+__global__ __launch_bounds__(kB) void k_concat_value(const u64x2* cells, u64* out, uint64_t reps,
+                                                     uint32_t E) {
+    const uint32_t W = (E + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kB / 64);
+    for (uint64_t w = ((uint64_t)blockIdx.x * kB + threadIdx.x) >> 6; w < reps * W;
+         w += nwaves) {
+        uint64_t rep = w / W;
+        uint32_t e = (uint32_t)(w - rep * W) * 64u + lane;
+        bool vis = false;
+        if (e < E) {
+            u64x2 a = ldnt(cells + 2 * (rep * E + e)), b = ldnt(cells + 2 * (rep * E + e) + 1);
+            vis = (a.x != 0) && (((a.x & ~a.y) | (b.x & ~b.y)) != 0);
+        }
+        u64 m = __ballot(vis);
+        if (lane == 0) out[w] = m;
+    }
+}
+
+// PRODUCT: visible iff x and y both hold a live token (the pair flag is Dx orelse Dy)
+__global__ __launch_bounds__(kB) void k_product_value(const uint32_t* cells, u64* out,
+                                                      uint64_t reps, uint64_t C,
+                                                      uint64_t cstride) {
+    const uint64_t W = (C + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kB / 64);
+    for (uint64_t w = ((uint64_t)blockIdx.x * kB + threadIdx.x) >> 6; w < reps * W;
+         w += nwaves) {
+        uint64_t rep = w / W;
+        uint64_t c = (w - rep * W) * 64u + lane;
+        bool vis = false;
+        if (c < C) {
+            uint32_t v = cells[rep * cstride + c];
+            vis = ((v & ~(v >> 8)) & 0xFFu) && (((v >> 16) & ~(v >> 24)) & 0xFFu);
+        }
+        u64 m = __ballot(vis);
+        if (lane == 0) out[w] = m;
+    }
+}
+
+hipError_t launch_combinator_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
+    uint64_t words = b->replicas * ((b->cells + 63ull) / 64ull);
+    int grid = grid_for(ctx, words * 64, 8);
+    if (b->kind == LASPJ_KIND_ORSET_CONCAT)
+        hipLaunchKernelGGL(k_concat_value, dim3(grid), dim3(kB), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), (u64*)out, b->replicas,
+                           b->elements);
+    else
+        hipLaunchKernelGGL(k_product_value, dim3(grid), dim3(kB), 0, ctx->stream,
+                           reinterpret_cast<const uint32_t*>(b->dev), (u64*)out, b->replicas,
+                           b->cells, 2 * b->words_per_replica);
+    return hipGetLastError();
+}
+
+}  // namespace laspj

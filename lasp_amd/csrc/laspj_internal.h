@@ -23,6 +23,8 @@ struct laspj_ctx {
     // device scratch for apply_ops (grown on demand)
     void* scratch = nullptr;
     uint64_t scratch_bytes = 0;
+    // one device word for kernel-detected argument violations (product token slots)
+    uint32_t* flag = nullptr;
 };
 
 struct laspj_buf {
@@ -36,7 +38,9 @@ struct laspj_batch {
     int32_t kind = 0;
     uint32_t elements = 0;      // E
     uint64_t replicas = 0;      // R
-    uint64_t words_per_replica = 0;  // u64 words: 2E (OR-Set) or ceil(E/64) (G-Set)
+    uint64_t words_per_replica = 0;  // u64 words: 2E (OR-Set) or ceil(E/64) (G-Set) ...
+    uint32_t elements_r = 0;    // ER of product batches
+    uint64_t cells = 0;         // cells per replica: E, or EL*ER for products
     uint64_t* dev = nullptr;
 };
 
@@ -97,5 +101,19 @@ hipError_t launch_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batc
                               const laspj_batch* r);
 hipError_t launch_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                const uint64_t* keep);
+hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                     const laspj_batch* r);
+hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                const laspj_batch* r, uint32_t* flag);
+hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                               const uint32_t* index);
+hipError_t launch_and(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                      uint64_t words);
+hipError_t launch_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              const uint64_t* keep);
+hipError_t launch_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                               const laspj_batch* r);
+hipError_t launch_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              const uint32_t* index);
 
 }  // namespace laspj

@@ -245,8 +245,11 @@ __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64*
     }
 }
 
+hipError_t launch_combinator_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out);
+
 hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
                               bool removed) {
+    if (b->kind != LASPJ_KIND_ORSET) return launch_combinator_value(ctx, b, out);
     uint64_t words = b->replicas * ((b->elements + 63ull) / 64ull);
     int grid = wave_grid(ctx, words);
     auto* cells = reinterpret_cast<const u64x2*>(b->dev);

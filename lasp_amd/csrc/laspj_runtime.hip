@@ -65,15 +65,26 @@ int check_buf(laspj_ctx* ctx, const laspj_buf* buf, uint64_t need, const char* w
     return LASPJ_OK;
 }
 
-uint64_t words_per(int32_t kind, uint32_t elements) {
-    return kind == LASPJ_KIND_ORSET ? 2ull * elements : (elements + 63ull) / 64ull;
+uint64_t words_per(int32_t kind, uint32_t elements, uint32_t er) {
+    switch (kind) {
+        case LASPJ_KIND_ORSET: return 2ull * elements;
+        case LASPJ_KIND_GSET: return (elements + 63ull) / 64ull;
+        case LASPJ_KIND_ORSET_CONCAT: return 4ull * elements;
+        case LASPJ_KIND_ORSET_PRODUCT: return ((uint64_t)elements * er + 1ull) / 2ull;
+        case LASPJ_KIND_GSET_PRODUCT: return (uint64_t)elements * ((er + 63ull) / 64ull);
+    }
+    return 0;
+}
+
+bool is_product(int32_t kind) {
+    return kind == LASPJ_KIND_ORSET_PRODUCT || kind == LASPJ_KIND_GSET_PRODUCT;
 }
 
 int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t elements,
-                 laspj_batch** out) {
+                 laspj_batch** out, uint32_t er = 0) {
     if (!ctx || !out) return fail(ctx, LASPJ_E_INVAL, "batch_create: null argument");
     *out = nullptr;
-    if (replicas == 0 || elements == 0)
+    if (replicas == 0 || elements == 0 || (is_product(kind) && er == 0))
         return fail(ctx, LASPJ_E_SHAPE, "batch_create: replicas and elements must be > 0");
     Guard g(ctx);
     auto* b = new (std::nothrow) laspj_batch;
@@ -81,8 +92,10 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
     b->ctx = ctx;
     b->kind = kind;
     b->elements = elements;
+    b->elements_r = is_product(kind) ? er : 0;
+    b->cells = is_product(kind) ? (uint64_t)elements * er : elements;
     b->replicas = replicas;
-    b->words_per_replica = words_per(kind, elements);
+    b->words_per_replica = words_per(kind, elements, er);
     uint64_t bytes = laspj::bytes_of(b);
     if (replicas > (~0ull / 8ull) / b->words_per_replica) {
         delete b;
@@ -156,6 +169,11 @@ int laspj_ctx_create(int device, laspj_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->cus = prop.multiProcessorCount;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->flag), 256) != hipSuccess) {
+        hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return LASPJ_E_NOMEM;
+    }
     *out = ctx;
     return LASPJ_OK;
 }
@@ -166,6 +184,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         Guard g(ctx);
         hipStreamSynchronize(ctx->stream);
         if (ctx->scratch) hipFree(ctx->scratch);
+        if (ctx->flag) hipFree(ctx->flag);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -303,6 +322,9 @@ int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
     out->replicas = b->replicas;
     out->bytes_per_replica = b->words_per_replica * 8ull;
     out->bytes = laspj::bytes_of(b);
+    out->elements_r = b->elements_r;
+    out->reserved = 0;
+    out->cells_per_replica = b->cells;
     return LASPJ_OK;
 }
 
@@ -346,6 +368,8 @@ int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* b) {
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                uint64_t replica_base) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
+    if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_GSET)
+        return fail(ctx, LASPJ_E_KIND, "fill_synthetic: OR-Set or G-Set batches only");
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base));
     return LASPJ_OK;
@@ -404,8 +428,11 @@ int laspj_gset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
 static int value_impl(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out, bool removed) {
     const char* what = removed ? "orset_removed" : "orset_value";
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
-    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "%s: not an OR-Set", what);
-    uint64_t need = b->replicas * ((b->elements + 63ull) / 64ull) * 8ull;
+    bool ok_kind = b->kind == LASPJ_KIND_ORSET ||
+                   (!removed && (b->kind == LASPJ_KIND_ORSET_CONCAT ||
+                                 b->kind == LASPJ_KIND_ORSET_PRODUCT));
+    if (!ok_kind) return fail(ctx, LASPJ_E_KIND, "%s: not an OR-Set batch", what);
+    uint64_t need = b->replicas * ((b->cells + 63ull) / 64ull) * 8ull;
     if (int s = check_buf(ctx, out, need, what)) return s;
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_orset_value(ctx, b, static_cast<uint64_t*>(out->dev), removed));
@@ -568,6 +595,125 @@ int laspj_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
         return s;
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_orset_filter(ctx, dst, src, static_cast<const uint64_t*>(keep->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_orset_concat_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                                    laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_ORSET_CONCAT, replicas, elements, out);
+}
+
+int laspj_orset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                     uint32_t er, laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_ORSET_PRODUCT, replicas, el, out, er);
+}
+
+int laspj_gset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                    uint32_t er, laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_GSET_PRODUCT, replicas, el, out, er);
+}
+
+int laspj_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                             const laspj_batch* r) {
+    if (int s = check_pair(ctx, l, r, LASPJ_KIND_ORSET, "orset_intersection")) return s;
+    if (!same_ctx(ctx, dst)) return fail(ctx, LASPJ_E_INVAL, "orset_intersection: bad dst");
+    if (dst->kind != LASPJ_KIND_ORSET_CONCAT)
+        return fail(ctx, LASPJ_E_KIND, "orset_intersection: dst must be a CONCAT batch");
+    if (dst->replicas != l->replicas || dst->elements != l->elements)
+        return fail(ctx, LASPJ_E_SHAPE, "orset_intersection: dst shape differs");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_intersection(ctx, dst, l, r));
+    return LASPJ_OK;
+}
+
+static int product_check(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                         const laspj_batch* r, int32_t in_kind, int32_t out_kind,
+                         const char* what) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, l) || !same_ctx(ctx, r))
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    if (l->kind != in_kind || r->kind != in_kind || dst->kind != out_kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kinds", what);
+    if (l->replicas != r->replicas || dst->replicas != l->replicas ||
+        dst->elements != l->elements || dst->elements_r != r->elements)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: dst must be replicas x EL x ER of l, r", what);
+    return LASPJ_OK;
+}
+
+int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                        const laspj_batch* r) {
+    if (int s = product_check(ctx, dst, l, r, LASPJ_KIND_ORSET, LASPJ_KIND_ORSET_PRODUCT,
+                              "orset_product"))
+        return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
+    LJ_HIP(ctx, laspj::launch_orset_product(ctx, dst, l, r, ctx->flag));
+    uint32_t flag = 0;
+    LJ_HIP(ctx, hipMemcpyAsync(&flag, ctx->flag, 4, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (flag)
+        return fail(ctx, LASPJ_E_RANGE,
+                    "orset_product: an input element uses token slot >= 8 (4-byte cells)");
+    return LASPJ_OK;
+}
+
+int laspj_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                       const laspj_buf* index) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "orset_gather: bad batch");
+    if (dst->kind != LASPJ_KIND_ORSET || src->kind != LASPJ_KIND_ORSET)
+        return fail(ctx, LASPJ_E_KIND, "orset_gather: OR-Set batches expected");
+    if (dst->replicas != src->replicas || dst->dev == src->dev)
+        return fail(ctx, LASPJ_E_SHAPE, "orset_gather: replicas differ or dst aliases src");
+    if (int s = check_buf(ctx, index, 4ull * dst->elements, "orset_gather")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_gather(ctx, dst, src, static_cast<const uint32_t*>(index->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                     const laspj_batch* r) {
+    return join_impl(ctx, dst, l, r, LASPJ_KIND_GSET, "gset_union");
+}
+
+int laspj_gset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                            const laspj_batch* r) {
+    if (int s = check_pair(ctx, l, r, LASPJ_KIND_GSET, "gset_intersection")) return s;
+    if (int s = check_pair(ctx, dst, l, LASPJ_KIND_GSET, "gset_intersection")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_and(ctx, dst->dev, l->dev, r->dev, l->replicas * l->words_per_replica));
+    return LASPJ_OK;
+}
+
+int laspj_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* keep) {
+    if (int s = check_pair(ctx, dst, src, LASPJ_KIND_GSET, "gset_filter")) return s;
+    if (int s = check_buf(ctx, keep, src->words_per_replica * 8ull, "gset_filter")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gset_filter(ctx, dst, src, static_cast<const uint64_t*>(keep->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                       const laspj_batch* r) {
+    if (int s = product_check(ctx, dst, l, r, LASPJ_KIND_GSET, LASPJ_KIND_GSET_PRODUCT,
+                              "gset_product"))
+        return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gset_product(ctx, dst, l, r));
+    return LASPJ_OK;
+}
+
+int laspj_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* index) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "gset_gather: bad batch");
+    if (dst->kind != LASPJ_KIND_GSET || src->kind != LASPJ_KIND_GSET)
+        return fail(ctx, LASPJ_E_KIND, "gset_gather: G-Set batches expected");
+    if (dst->replicas != src->replicas || dst->dev == src->dev)
+        return fail(ctx, LASPJ_E_SHAPE, "gset_gather: replicas differ or dst aliases src");
+    if (int s = check_buf(ctx, index, 4ull * dst->elements, "gset_gather")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gset_gather(ctx, dst, src, static_cast<const uint32_t*>(index->dev)));
     return LASPJ_OK;
 }
 

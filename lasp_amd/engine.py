@@ -235,6 +235,87 @@ class ORSetBatch(_Batch):
         self.ctx.synchronize()
         return self
 
+    # intersection body (lasp_core.erl:546-589): returns a CONCAT batch
+    def intersection(self, r: "ORSetBatch") -> "ConcatBatch":
+        out = ConcatBatch(self.ctx, self.replicas, self.elements)
+        check(self.ctx.L.laspj_orset_intersection(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
+        return out
+
+    # product body (lasp_core.erl:499-533): returns a PRODUCT batch (EL x ER cells)
+    def product(self, r: "ORSetBatch", out: Optional["ORSetProductBatch"] = None):
+        if out is None:
+            out = ORSetProductBatch(self.ctx, self.replicas, self.elements, r.elements)
+        check(self.ctx.L.laspj_orset_product(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
+        return out
+
+    # map / fold bodies: self <- src gathered through index (one u32 per slot of self)
+    def gather(self, src: "ORSetBatch", index: np.ndarray):
+        idx = self.ctx.buffer(4 * self.elements)
+        idx.upload(np.ascontiguousarray(index, dtype=np.uint32))
+        check(self.ctx.L.laspj_orset_gather(self.ctx.h, self.h, src.h, idx.h), self.ctx.h)
+        self.ctx.synchronize()
+        return self
+
+
+class ConcatBatch(_Batch):
+    """Intersection output: per slot {pL, rL, pR, rR} (tokens decode as Cx ++ Cy)."""
+
+    kind = _lib.KIND_ORSET_CONCAT
+    _create = "laspj_orset_concat_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        w = self.download_words(first, count)
+        return w.reshape(w.shape[0], self.elements, 4)
+
+    def value_bits(self) -> np.ndarray:
+        W = (self.elements + 63) // 64
+        buf = self.ctx.buffer(self.replicas * W * 8)
+        check(self.ctx.L.laspj_orset_value(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, W)
+
+
+class _ProductBatch(_Batch):
+    def __init__(self, ctx: Context, replicas: int, el: int, er: int):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(getattr(ctx.L, self._create)(ctx.h, replicas, el, er, C.byref(h)), ctx.h)
+        self.h = h
+        self.replicas, self.elements, self.elements_r = replicas, el, er
+        info = _lib.BatchInfo()
+        check(ctx.L.laspj_batch_info_get(self.h, C.byref(info)))
+        self.bytes_per_replica = info.bytes_per_replica
+        self.nbytes = info.bytes
+        self.cells = info.cells_per_replica
+
+
+class ORSetProductBatch(_ProductBatch):
+    """Product output: EL x ER uint32 cells {pX:8, rX:8, pY:8, rY:8}."""
+
+    kind = _lib.KIND_ORSET_PRODUCT
+    _create = "laspj_orset_product_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        w = self.download_words(first, count)
+        return w.view(np.uint32)[:, : self.cells].reshape(w.shape[0], self.elements,
+                                                           self.elements_r)
+
+    def value_bits(self) -> np.ndarray:
+        W = (self.cells + 63) // 64
+        buf = self.ctx.buffer(self.replicas * W * 8)
+        check(self.ctx.L.laspj_orset_value(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, W)
+
+
+class GSetProductBatch(_ProductBatch):
+    """G-Set product output: EL rows x ceil(ER/64) words."""
+
+    kind = _lib.KIND_GSET_PRODUCT
+    _create = "laspj_gset_product_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        w = self.download_words(first, count)
+        return w.reshape(w.shape[0], self.elements, (self.elements_r + 63) // 64)
+
 
 class GSetBatch(_Batch):
     """R replicas of a G-Set over E element slots (ceil(E/64) u64 words)."""
@@ -266,3 +347,30 @@ class GSetBatch(_Batch):
 
     def apply_ops(self, ops: Sequence[tuple]) -> np.ndarray:
         return self._apply_ops(self.ctx.L.laspj_gset_apply_ops, ops)
+
+    def union(self, l: "GSetBatch", r: "GSetBatch"):
+        check(self.ctx.L.laspj_gset_union(self.ctx.h, self.h, l.h, r.h), self.ctx.h)
+        return self
+
+    def intersection(self, l: "GSetBatch", r: "GSetBatch"):
+        check(self.ctx.L.laspj_gset_intersection(self.ctx.h, self.h, l.h, r.h), self.ctx.h)
+        return self
+
+    def filter(self, src: "GSetBatch", keep_bits: np.ndarray):
+        keep = self.ctx.buffer(self.words_per_replica * 8)
+        keep.upload(np.ascontiguousarray(keep_bits, dtype=np.uint64))
+        check(self.ctx.L.laspj_gset_filter(self.ctx.h, self.h, src.h, keep.h), self.ctx.h)
+        self.ctx.synchronize()
+        return self
+
+    def product(self, r: "GSetBatch") -> "GSetProductBatch":
+        out = GSetProductBatch(self.ctx, self.replicas, self.elements, r.elements)
+        check(self.ctx.L.laspj_gset_product(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
+        return out
+
+    def gather(self, src: "GSetBatch", index: np.ndarray):
+        idx = self.ctx.buffer(4 * self.elements)
+        idx.upload(np.ascontiguousarray(index, dtype=np.uint32))
+        check(self.ctx.L.laspj_gset_gather(self.ctx.h, self.h, src.h, idx.h), self.ctx.h)
+        self.ctx.synchronize()
+        return self

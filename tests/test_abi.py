@@ -63,7 +63,7 @@ def test_abi_calls_without_gpu(lib):
 
 def test_struct_layouts():
     assert ctypes.sizeof(_lib.Op) == 16
-    assert ctypes.sizeof(_lib.BatchInfo) == 32
+    assert ctypes.sizeof(_lib.BatchInfo) == 48
 
 
 def test_engine_fails_loudly_without_library(monkeypatch):

@@ -182,3 +182,41 @@ def test_gpu_orset_update_matches_oracle():
     st = do.stats(sd)
     assert [list(x) for x in st] == [list(x) for x in orset.stats(so)]
     np.testing.assert_equal(len(do.value(sd)), len(orset.value(so)))
+
+
+@pytest.mark.gpu
+def test_gpu_orset_combinator_bodies_match_vectors():
+    """intersection / product / map / fold bodies (lasp_core.erl:460-667) on the device,
+    decoded list-faithfully (Cx ++ Cy, descending product tokens, duplicates kept)."""
+    from lasp_amd import orset as do
+    from lasp_amd.codec import Domain, SeqOutput, decode_concat, decode_product
+    from lasp_amd.terms import Atom
+    ctx = do.context()
+    for c in OR:
+        a, b = dec(c["a"], Atom), dec(c["b"], Atom)
+        dom = Domain()
+        dom.register_orset(a)
+        dom.register_orset(b)
+        E = max(1, dom.size)
+        L, R = ctx.orset_batch(1, E), ctx.orset_batch(1, E)
+        L.upload(dom.encode_orset([a], E))
+        R.upload(dom.encode_orset([b], E))
+        X = L.intersection(R)
+        assert _eq(decode_concat(dom, X.download()[0]), dec(c["intersection"]))
+        # product of the first 4 elements of each side, each in its own domain
+        dl, dr = Domain(), Domain()
+        dl.register_orset(a[:4])
+        dr.register_orset(b[:4])
+        PL, PR = ctx.orset_batch(1, max(1, dl.size)), ctx.orset_batch(1, max(1, dr.size))
+        PL.upload(dl.encode_orset([a[:4]], PL.elements))
+        PR.upload(dr.encode_orset([b[:4]], PR.elements))
+        P = PL.product(PR)
+        assert _eq(decode_product(dl, dr, P.download()[0]), dec(c["product"]))
+        # fold X -> [X, X, X] and map X -> 2X over the dictionary, gathered on device
+        fo = SeqOutput.fold(dom, lambda x: [x, x, x])
+        F = ctx.orset_batch(1, max(1, fo.size)).gather(L, fo.index())
+        assert _eq(fo.decode_orset(F.download()[0]), dec(c["fold_x3"]))
+        if c["map_x2"] is not None:
+            mo = SeqOutput.map(dom, lambda x: x * 2)
+            M = ctx.orset_batch(1, max(1, mo.size)).gather(L, mo.index())
+            assert _eq(mo.decode_orset(M.download()[0]), dec(c["map_x2"]))

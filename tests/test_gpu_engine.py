@@ -301,3 +301,83 @@ def test_large_join_property(ctx):
     d = ctx.orset_batch(n, e_n)
     d.join(c, a)
     assert d.equal(c).all()
+
+
+def test_orset_product_tiles_and_tails(ctx):
+    """Outer-product tiling: EL and ER off the 64 x 1024 tile, several replicas; every
+    cell equals {pX8, rX8, pY8, rY8} of its row / column (0 where either is absent)."""
+    n, el, er = 3, 130, 1027
+    l = _synth(71, n, el)
+    r = _synth(72, n, er)
+    l &= np.uint64(0x7)          # 3 token slots, as in BASELINE config 5
+    r &= np.uint64(0x7)
+    L, Rb = ctx.orset_batch(n, el), ctx.orset_batch(n, er)
+    L.upload(l)
+    Rb.upload(r)
+    P = L.product(Rb)
+    got = P.download()
+    lx = np.where(l[:, :, 0] != 0, l[:, :, 0] | (l[:, :, 1] << np.uint64(8)), 0).astype(np.uint32)
+    ry = np.where(r[:, :, 0] != 0, (r[:, :, 0] << np.uint64(16)) | (r[:, :, 1] << np.uint64(24)), 0
+                  ).astype(np.uint32)
+    want = np.where((lx[:, :, None] != 0) & (ry[:, None, :] != 0),
+                    lx[:, :, None] | ry[:, None, :], 0).astype(np.uint32)
+    assert np.array_equal(got, want)
+    vis = P.value_bits()
+    live_l = (l[:, :, 0] & ~l[:, :, 1]) != 0
+    live_r = (r[:, :, 0] & ~r[:, :, 1]) != 0
+    want_vis = (live_l[:, :, None] & live_r[:, None, :]).reshape(n, -1)
+    bits = np.unpackbits(vis.view(np.uint8), axis=1, bitorder="little")[:, : el * er].astype(bool)
+    assert np.array_equal(bits, want_vis)
+
+
+def test_orset_product_rejects_wide_token_slots(ctx):
+    from lasp_amd import LaspjError
+    from lasp_amd._lib import E_RANGE
+    L, Rb = ctx.orset_batch(1, 4), ctx.orset_batch(1, 4)
+    h = np.zeros((1, 4, 2), np.uint64)
+    h[0, 1, 0] = np.uint64(1) << np.uint64(9)      # token slot 9
+    L.upload(h)
+    Rb.upload(h)
+    with pytest.raises(LaspjError) as ei:
+        L.product(Rb)
+    assert ei.value.status == E_RANGE
+
+
+def test_orset_intersection_concat(ctx):
+    l, r = _synth(81, 8, E), _synth(82, 8, E)
+    L, Rb = ctx.orset_batch(8, E), ctx.orset_batch(8, E)
+    L.upload(l)
+    Rb.upload(r)
+    got = L.intersection(Rb).download()
+    keep = (l[:, :, 0] != 0) & (r[:, :, 0] != 0)
+    want = np.concatenate([l, r], axis=2) * keep[:, :, None].astype(np.uint64)
+    assert np.array_equal(got, want)
+
+
+def test_gset_combinators(ctx):
+    """G-Set union / intersection / filter / product / gather bodies vs oracle lists."""
+    from oracle import core
+    n, e_n = 4, 150
+    a = np.stack([orc.synth_gset(91, i, e_n) for i in range(n)])
+    b = np.stack([orc.synth_gset(92, i, e_n) for i in range(n)])
+    A, B = ctx.gset_batch(n, e_n), ctx.gset_batch(n, e_n)
+    A.upload(a)
+    B.upload(b)
+    mem = lambda w: [int(x) for x in orc.gset_members(w, e_n)]   # noqa: E731
+    I = ctx.gset_batch(n, e_n).intersection(A, B).download()
+    keep = np.zeros(((e_n + 63) // 64,), np.uint64)
+    for e in range(0, e_n, 3):
+        keep[e // 64] |= np.uint64(1) << np.uint64(e % 64)
+    Fl = ctx.gset_batch(n, e_n).filter(A, keep).download()
+    P = A.product(B).download()
+    idx = np.array([e // 2 for e in range(e_n)], np.uint32)          # a map onto slots
+    G = ctx.gset_batch(n, e_n).gather(A, idx).download()
+    for i in range(n):
+        la, lb = mem(a[i]), mem(b[i])
+        assert mem(I[i]) == core.intersection_body("lasp_gset", la, lb)
+        assert mem(Fl[i]) == core.filter_body("lasp_gset", lambda x: x % 3 == 0, la)
+        pairs = [(x, y) for x in range(e_n) for y in range(e_n)
+                 if (int(P[i, x, y >> 6]) >> (y & 63)) & 1]
+        assert pairs == core.product_body("lasp_gset", la, lb)
+        got_g = [o for o in range(e_n) if (int(G[i, o >> 6]) >> (o & 63)) & 1]
+        assert got_g == [o for o in range(e_n) if (o // 2) in set(la)]
