@@ -142,6 +142,12 @@ int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* batch);
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed,
                                uint64_t replica_base);
 
+/* Slot-wise join of two batches of the same kind and shape (any kind): dst = a | b
+ * word by word.  For OR-Set / G-Set batches this is merge/2; for combinator outputs
+ * it ORs both halves of CONCAT cells and the packed masks of PRODUCT cells. */
+int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b);
+
 /* ------------------------------------------------------------------ lasp_orset */
 /* merge/2 — lasp_orset.erl:128-134: dst[i] = a[i] ⊔ b[i]  (p|p', r|r').
  * dst may alias a or b (the bind path merges in place, lasp_core.erl:300-303). */

@@ -75,6 +75,7 @@ SIGNATURES = {
     "laspj_batch_download": (i, [vp, vp, u64, u64, vp]),
     "laspj_batch_clear": (i, [vp, vp]),
     "laspj_batch_fill_synthetic": (i, [vp, vp, u64, u64]),
+    "laspj_batch_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_reduce": (i, [vp, vp, vp, u32]),
     "laspj_orset_value": (i, [vp, vp, vp]),

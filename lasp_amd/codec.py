@@ -264,16 +264,31 @@ class SeqOutput:
     def __init__(self, dom: Domain, keys: list, src: list):
         self.dom, self.keys, self.src = dom, keys, src
 
+    # F runs once per dictionary element, not per replica.  A dictionary element that
+    # F cannot take (F raises) keeps an empty slot: it is absent from every input that
+    # reaches this body, or the reference's body would have crashed on it too.
+
     @classmethod
     def map(cls, dom: Domain, fun) -> "SeqOutput":
-        order = [int(s) for s in dom.elements.order()]
-        return cls(dom, [fun(dom.elements.terms[s]) for s in order], order)
+        keys, src = [], []
+        for s in dom.elements.order():
+            try:
+                keys.append(fun(dom.elements.terms[int(s)]))
+                src.append(int(s))
+            except Exception:
+                keys.append(None)
+                src.append(0xFFFFFFFF)
+        return cls(dom, keys, src)
 
     @classmethod
     def fold(cls, dom: Domain, fun) -> "SeqOutput":
         keys, src = [], []
         for s in dom.elements.order():
-            for v in fun(dom.elements.terms[int(s)]):
+            try:
+                vals = list(fun(dom.elements.terms[int(s)]))
+            except Exception:
+                continue
+            for v in vals:
                 keys.append(v)
                 src.append(int(s))
         return cls(dom, keys, src)
@@ -289,7 +304,7 @@ class SeqOutput:
         out = []
         for o, (key, s) in enumerate(zip(self.keys, self.src)):
             p, r = int(cells[o, 0]), int(cells[o, 1])
-            if not p:
+            if not p or s == 0xFFFFFFFF:
                 continue
             td = self.dom.tokens[s]
             out.append((key, [(td.terms[k], bool((r >> int(k)) & 1))

@@ -387,6 +387,23 @@ static int join_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     return LASPJ_OK;
 }
 
+int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, a) || !same_ctx(ctx, b))
+        return fail(ctx, LASPJ_E_INVAL, "batch_join: bad batch");
+    if (a->kind != b->kind || dst->kind != a->kind)
+        return fail(ctx, LASPJ_E_KIND, "batch_join: kinds differ");
+    if (a->replicas != b->replicas || dst->replicas != a->replicas ||
+        a->words_per_replica != b->words_per_replica ||
+        dst->words_per_replica != a->words_per_replica || a->elements != b->elements ||
+        a->elements_r != b->elements_r)
+        return fail(ctx, LASPJ_E_SHAPE, "batch_join: shapes differ");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_or(ctx, dst->dev, a->dev, b->dev,
+                                 a->replicas * a->words_per_replica));
+    return LASPJ_OK;
+}
+
 int laspj_orset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b) {
     return join_impl(ctx, dst, a, b, LASPJ_KIND_ORSET, "orset_join");

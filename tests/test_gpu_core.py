@@ -1,0 +1,119 @@
+"""lasp_core on the device (lasp_amd.core.Store) against the reference's riak_test known
+answers and against the oracle's Store on the same scenario (values compared as terms).
+"""
+
+import pytest
+
+from oracle import core as ocore
+from oracle.terms import exact_eq
+
+pytestmark = pytest.mark.gpu
+
+
+def _stores():
+    from lasp_amd import core as dcore
+    from lasp_amd.terms import Atom
+    return dcore.Store(capacity=256), ocore.Store(), Atom
+
+
+def _both(fn):
+    """Run the same scenario on the device store and the oracle store."""
+    ds, os_, Atom = _stores()
+    return fn(ds, Atom), fn(os_, Atom), ds, os_
+
+
+@pytest.mark.parametrize("t", ["lasp_gset", "lasp_orset"])
+@pytest.mark.parametrize("comb,expected", [
+    ("union", lambda A: [1, 2, 3, A("a"), A("b"), A("c")]),
+    ("intersection", lambda A: [3, A("a")]),
+    ("product", lambda A: [(1, A("a")), (1, A("b")), (1, A("c")), (2, A("a")), (2, A("b")),
+                           (2, A("c")), (3, A("a")), (3, A("b")), (3, A("c"))]),
+])
+def test_two_input_kats(t, comb, expected):
+    """riak_test/lasp_{union,intersection,product}_test.erl."""
+    def scen(st, A):
+        _, s1 = st.declare(t)
+        _, s2 = st.declare(t)
+        _, s3 = st.declare(t)
+        left = [1, 2, 3, A("a")] if comb == "intersection" else [1, 2, 3]
+        right = [A("a"), A("b"), A("c"), 3] if comb == "intersection" else [A("a"), A("b"), A("c")]
+        st.update(s1, ("add_all", left), A("a"))
+        st.update(s2, ("add_all", right), A("a"))
+        getattr(st, comb)(s1, s2, s3)
+        return s3
+    ds, _, Atom = _stores()
+    s3 = scen(ds, Atom)
+    assert ds.type_value(s3) == expected(Atom)
+
+
+@pytest.mark.parametrize("t", ["lasp_gset", "lasp_orset"])
+@pytest.mark.parametrize("comb,fun,expected", [
+    ("map", lambda x: x * 2, [2, 4, 6, 8, 10, 12]),
+    ("filter", lambda x: x % 2 == 0, [2, 4, 6]),
+    ("fold", lambda x: [x, x, x], [1, 1, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6]),
+])
+def test_one_input_kats(t, comb, fun, expected):
+    """riak_test/lasp_{map,filter,fold}_test.erl: bind [1,2,3], run, bind [4,5,6]."""
+    from lasp_amd import core as dcore
+    from lasp_amd.terms import Atom
+    st = dcore.Store(capacity=64)
+    _, s1 = st.declare(t)
+    st.update(s1, ("add_all", [1, 2, 3]), Atom("a"))
+    _, s2 = st.declare(t)
+    getattr(st, comb)(s1, fun, s2)
+    st.update(s1, ("add_all", [4, 5, 6]), Atom("a"))
+    assert st.type_value(s1) == [1, 2, 3, 4, 5, 6]
+    assert st.type_value(s2) == expected
+
+
+def test_monotonic_read_kat():
+    """riak_test/lasp_monotonic_read_test.erl:62-86 (threshold reads on the device)."""
+    from lasp_amd import core as dcore
+    st = dcore.Store(capacity=64)
+    _, g = st.declare("lasp_gset")
+    assert st.read(g, [1, 2, 3]) is None
+    st.bind(g, [1])
+    st.bind(g, [1, 2])
+    assert st.read(g, [1, 2, 3]) is None
+    st.bind(g, [1, 2, 3])
+    assert st.read(g, [1, 2, 3])[1][2] == [1, 2, 3]
+    assert st.read(g, [1, 2, 3, 4]) is None
+    assert st.read(g, ("strict", [1, 2, 3])) is None
+    st.bind(g, [1, 2, 3, 4])
+    assert st.read(g, [1, 2, 3, 4])[1][2] == [1, 2, 3, 4]
+    assert st.read(g, ("strict", [1, 2, 3]))[1][2] == [1, 2, 3, 4]
+
+
+def test_store_values_match_oracle_store():
+    """A mixed scenario: the device store's variables decode to exactly the oracle
+    store's values (token lists, flags and list order included)."""
+    toks = [bytes([k + 1]) * 20 for k in range(40)]
+
+    def scen(st, A):
+        _, a = st.declare("lasp_orset")
+        _, b = st.declare("lasp_orset")
+        _, u = st.declare("lasp_orset")
+        _, x = st.declare("lasp_orset")
+        _, f = st.declare("lasp_orset")
+        _, m = st.declare("lasp_orset")
+        _, fo = st.declare("lasp_orset")
+        st.update(a, ("add_by_token", toks[0], 1), None)
+        st.update(a, ("add_by_token", toks[1], 2), None)
+        st.update(b, ("add_by_token", toks[2], 2), None)
+        st.update(b, ("add_by_token", toks[3], 5), None)
+        st.union(a, b, u)
+        st.intersection(a, b, x)
+        st.filter(a, lambda v: v % 2 == 1, f)
+        st.map(a, lambda v: v * 10, m)
+        st.fold(a, lambda v: [v, v], fo)
+        st.update(a, ("add_by_token", toks[4], 3), None)
+        st.update(a, ("remove", 1), None)
+        st.update(a, ("add_by_token", toks[5], 7), None)
+        st.bind(b, [(2, [(toks[2], True)]), (9, [(toks[6], False)])])
+        return [a, b, u, x, f, m, fo]
+
+    ds, os_, Atom = _stores()
+    ids_d = scen(ds, Atom)
+    ids_o = scen(os_, Atom)
+    for i_d, i_o in zip(ids_d, ids_o):
+        assert exact_eq(ds.value(i_d), os_.value(i_o)), (i_d, ds.value(i_d), os_.value(i_o))
