@@ -47,7 +47,50 @@ def parse():
     ap.add_argument("--nt", type=int, default=-1)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_join.json"),
                     help="PMC summary giving HBM traffic per join launch")
+    ap.add_argument("--antientropy", choices=["auto", "on", "off"], default="auto",
+                    help="config-3 gossip anti-entropy leg (auto: when N > 1)")
+    ap.add_argument("--ae-objects", type=int, default=1 << 18,
+                    help="objects per GPU for the anti-entropy leg (2^18 x 4096 = 16 GiB)")
+    ap.add_argument("--ae-rounds", type=int, default=3)
     return ap.parse_args()
+
+
+XGMI_LINK_GBS = 153.0        # per link per direction
+
+
+def antientropy_leg(ctx, args, rank, world, barrier):
+    """BASELINE config 3: every rank holds one replica of `objects` OR-Sets; a round
+    leaves every rank with the join of all ranks' replicas (lasp_amd.gossip)."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    from lasp_amd.gossip import DeviceAntiEntropy
+    g = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+    O, E = args.ae_objects, args.elements
+    ae = DeviceAntiEntropy(ctx, O, E, group=g)
+    ae.fill(10 + rank)
+    ae.round()                                   # warm-up (RCCL connection setup)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.ae_rounds):
+        ae.round()
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per_round = float(t.item()) / args.ae_rounds
+    S = ae.bytes
+    xgmi = 2.0 * (world - 1) / world * S / per_round / 1e9 if world > 1 else 0.0
+    return {
+        "workload": "gossip anti-entropy (BASELINE configs[2]): all_to_all + HIP OR + all_gather",
+        "objects_per_gpu": O, "elements": E, "state_bytes_per_gpu": S,
+        "rounds": args.ae_rounds, "ms_per_round": per_round * 1e3,
+        "merged_elements_per_s": (world - 1) * O * E / per_round,
+        "xgmi_GBps_per_gpu": xgmi,
+        "frac_mesh": xgmi / (XGMI_LINK_GBS * 7), "frac_ring": xgmi / XGMI_LINK_GBS,
+    }
 
 
 def host_cores() -> int:
@@ -87,9 +130,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    ae_on = args.antientropy == "on" or (args.antientropy == "auto" and world > 1)
+    if world > 1 or ae_on:
+        # torch first: its bundled HIP runtime is then the one liblaspj binds to
         import torch
         import torch.distributed as dist
+        torch.cuda.set_device(local)
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 
     from lasp_amd import engine
@@ -135,6 +181,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
+    ae = None
+    if ae_on:
+        del a, b, c                      # free the 192 GiB of join operands first
+        ctx.synchronize()
+        try:
+            ae = antientropy_leg(ctx, args, rank, world, barrier)
+        except Exception as e:           # reported, never fatal to the headline line
+            ae = {"error": f"{type(e).__name__}: {e}"}
+
     if rank != 0:
         dist.barrier()
         return
@@ -169,6 +224,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if ae is not None:
+        out["antientropy"] = ae
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
     print(json.dumps(out), flush=True)

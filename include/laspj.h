@@ -129,6 +129,11 @@ int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t element
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out);
 int laspj_batch_destroy(laspj_batch* batch);
+/* A non-owning OR-Set / G-Set batch over caller device memory (e.g. a buffer another
+ * allocator or a collective library owns; the bytes must stay valid until destroy).
+ * `kind` is LASPJ_KIND_ORSET or LASPJ_KIND_GSET; `bytes` must equal the batch size. */
+int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* device_ptr, uint64_t bytes,
+                     uint64_t replicas, uint32_t elements, laspj_batch** out);
 int laspj_batch_info_get(const laspj_batch* batch, laspj_batch_info* out);
 /* host <-> device, replicas [first, first+count), host layout = device layout */
 int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* batch, uint64_t first, uint64_t count,
@@ -147,6 +152,12 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed
  * it ORs both halves of CONCAT cells and the packed masks of PRODUCT cells. */
 int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b);
+
+/* Anti-entropy reduce step: src holds nchunks copies of dst's replica
+ * range laid out chunk-major (what an all-to-all delivers); dst[i] = ⊔_j src[j*R + i].
+ * Any kind; src.replicas = nchunks * dst.replicas. */
+int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              uint32_t nchunks);
 
 /* ------------------------------------------------------------------ lasp_orset */
 /* merge/2 — lasp_orset.erl:128-134: dst[i] = a[i] ⊔ b[i]  (p|p', r|r').

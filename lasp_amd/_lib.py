@@ -70,6 +70,8 @@ SIGNATURES = {
     "laspj_orset_batch_create": (i, [vp, u64, u32, vpp]),
     "laspj_gset_batch_create": (i, [vp, u64, u32, vpp]),
     "laspj_batch_destroy": (i, [vp]),
+    "laspj_batch_wrap": (i, [vp, C.c_int32, vp, u64, u64, u32, vpp]),
+    "laspj_batch_reduce_chunks": (i, [vp, vp, vp, u32]),
     "laspj_batch_info_get": (i, [vp, C.POINTER(BatchInfo)]),
     "laspj_batch_upload": (i, [vp, vp, u64, u64, vp]),
     "laspj_batch_download": (i, [vp, vp, u64, u64, vp]),

@@ -42,6 +42,7 @@ struct laspj_batch {
     uint32_t elements_r = 0;    // ER of product batches
     uint64_t cells = 0;         // cells per replica: E, or EL*ER for products
     uint64_t* dev = nullptr;
+    bool owns = true;           // false for laspj_batch_wrap
 };
 
 struct laspj_event {
@@ -81,6 +82,8 @@ StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16);
 
 hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
                      uint64_t words);
+hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                                uint64_t words, uint32_t nchunks);
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t words_per_replica);
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,

@@ -159,6 +159,42 @@ hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
     return hipGetLastError();
 }
 
+// dst[w] = OR_j src[j*n + w]: the reduce of an all-to-all receive buffer
+__global__ __launch_bounds__(kBlock) void k_reduce_chunks(u64x2* dst, const u64x2* src,
+                                                          uint64_t n, uint32_t nchunks) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        u64x2 acc = ld2<true>(src + i);
+        for (uint32_t j = 1; j < nchunks; ++j) acc |= ld2<true>(src + (uint64_t)j * n + i);
+        st2<true>(dst + i, acc);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce_chunks_scalar(u64* dst, const u64* src,
+                                                                 uint64_t n, uint32_t nchunks) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        u64 acc = src[i];
+        for (uint32_t j = 1; j < nchunks; ++j) acc |= src[(uint64_t)j * n + i];
+        dst[i] = acc;
+    }
+}
+
+hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                                uint64_t words, uint32_t nchunks) {
+    if ((words & 1) == 0) {
+        StreamTune t = stream_tune(ctx, words / 2);
+        hipLaunchKernelGGL(k_reduce_chunks, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<u64x2*>(dst), reinterpret_cast<const u64x2*>(src),
+                           words / 2, nchunks);
+    } else {    // odd word count: chunk starts are only 8-byte aligned
+        StreamTune t = stream_tune(ctx, words);
+        hipLaunchKernelGGL(k_reduce_chunks_scalar, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           (u64*)dst, (const u64*)src, words, nchunks);
+    }
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ synthetic replicas
 // DESIGN.md §5; restated in oracle/laspj_oracle.c (orc_synth_*).
 

@@ -309,9 +309,52 @@ int laspj_batch_destroy(laspj_batch* b) {
     {
         Guard g(b->ctx);
         hipStreamSynchronize(b->ctx->stream);
-        hipFree(b->dev);
+        if (b->owns) hipFree(b->dev);
     }
     delete b;
+    return LASPJ_OK;
+}
+
+int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* dev, uint64_t bytes,
+                     uint64_t replicas, uint32_t elements, laspj_batch** out) {
+    if (!ctx || !out || !dev) return fail(ctx, LASPJ_E_INVAL, "batch_wrap: null argument");
+    *out = nullptr;
+    if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET)
+        return fail(ctx, LASPJ_E_KIND, "batch_wrap: OR-Set or G-Set only");
+    if (replicas == 0 || elements == 0)
+        return fail(ctx, LASPJ_E_SHAPE, "batch_wrap: empty shape");
+    uint64_t wpr = words_per(kind, elements, 0);
+    if (replicas > (~0ull / 8ull) / wpr || replicas * wpr * 8ull != bytes)
+        return fail(ctx, LASPJ_E_SHAPE, "batch_wrap: %llu bytes do not hold %llu x %u",
+                    (unsigned long long)bytes, (unsigned long long)replicas, elements);
+    if (reinterpret_cast<uintptr_t>(dev) % 16)
+        return fail(ctx, LASPJ_E_INVAL, "batch_wrap: device pointer not 16-byte aligned");
+    auto* b = new (std::nothrow) laspj_batch;
+    if (!b) return fail(ctx, LASPJ_E_NOMEM, "batch_wrap: host allocation");
+    b->ctx = ctx;
+    b->kind = kind;
+    b->elements = elements;
+    b->cells = elements;
+    b->replicas = replicas;
+    b->words_per_replica = wpr;
+    b->dev = static_cast<uint64_t*>(dev);
+    b->owns = false;
+    *out = b;
+    return LASPJ_OK;
+}
+
+int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                              uint32_t nchunks) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "reduce_chunks: bad batch");
+    if (dst->kind != src->kind) return fail(ctx, LASPJ_E_KIND, "reduce_chunks: kinds differ");
+    if (nchunks == 0 || dst->words_per_replica != src->words_per_replica ||
+        dst->elements != src->elements || dst->replicas * (uint64_t)nchunks != src->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "reduce_chunks: need src replicas = nchunks x dst");
+    if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "reduce_chunks: dst aliases src");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_reduce_chunks(ctx, dst->dev, src->dev,
+                                            dst->replicas * dst->words_per_replica, nchunks));
     return LASPJ_OK;
 }
 

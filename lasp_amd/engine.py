@@ -165,6 +165,12 @@ class _Batch:
         check(self.ctx.L.laspj_batch_fill_synthetic(self.ctx.h, self.h, seed, replica_base),
               self.ctx.h)
 
+    def reduce_chunks(self, src: "_Batch", nchunks: int):
+        """self[i] = join over j of src[j*R + i] (laspj_batch_reduce_chunks)."""
+        check(self.ctx.L.laspj_batch_reduce_chunks(self.ctx.h, self.h, src.h, nchunks),
+              self.ctx.h)
+        return self
+
     def _bool_out(self, fn, *args) -> np.ndarray:
         buf = self.ctx.buffer(self.replicas)
         check(fn(self.ctx.h, *args, buf.h), self.ctx.h)
@@ -255,6 +261,23 @@ class ORSetBatch(_Batch):
         check(self.ctx.L.laspj_orset_gather(self.ctx.h, self.h, src.h, idx.h), self.ctx.h)
         self.ctx.synchronize()
         return self
+
+
+class WrappedORSetBatch(ORSetBatch):
+    """An OR-Set batch over device memory owned by someone else (e.g. a torch tensor
+    that RCCL collectives write into); laspj_batch_wrap, non-owning."""
+
+    def __init__(self, ctx: Context, tensor, replicas: int, elements: int):
+        self.ctx = ctx
+        self._keep = tensor
+        nbytes = tensor.numel() * tensor.element_size()
+        h = C.c_void_p()
+        check(ctx.L.laspj_batch_wrap(ctx.h, _lib.KIND_ORSET, C.c_void_p(tensor.data_ptr()),
+                                     nbytes, replicas, elements, C.byref(h)), ctx.h)
+        self.h = h
+        self.replicas, self.elements = replicas, elements
+        self.bytes_per_replica = 16 * elements
+        self.nbytes = nbytes
 
 
 class ConcatBatch(_Batch):

@@ -1,0 +1,74 @@
+"""World-size-2 CPU coverage of the multi-GPU paths (gloo): the anti-entropy
+orchestration (lasp_amd.gossip.anti_entropy_round) and the bench's shard layout."""
+
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path.insert(0, %(root)r)
+    import numpy as np
+    import torch, torch.distributed as dist
+    from lasp_amd.gossip import anti_entropy_round
+    from oracle import columnar as orc
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    objects, E = 6, 33            # chunk = 3 objects per rank; odd E
+    # this rank's replica of every object: synthetic stream 100 + rank
+    mine = np.stack([orc.synth_orset(100 + rank, o, E) for o in range(objects)])
+    state = torch.from_numpy(mine.reshape(-1).view(np.int64).copy())
+    recv = torch.empty_like(state)
+    chunk = torch.empty(state.numel() // world, dtype=torch.int64)
+
+    def reduce_fn():     # CPU stand-in for laspj_batch_reduce_chunks (tested on GPU)
+        r = recv.numpy().view(np.uint64).reshape(world, -1)
+        chunk.numpy().view(np.uint64)[:] = np.bitwise_or.reduce(r, axis=0)
+
+    anti_entropy_round(state, recv, chunk, reduce_fn)
+    got = state.numpy().view(np.uint64).reshape(objects, E, 2)
+    want = np.zeros_like(mine)
+    for r in range(world):
+        want |= np.stack([orc.synth_orset(100 + r, o, E) for o in range(objects)])
+    assert np.array_equal(got, want), "anti-entropy did not converge to the join"
+    # a second round is idempotent (the join is already everywhere)
+    anti_entropy_round(state, recv, chunk, reduce_fn)
+    assert np.array_equal(state.numpy().view(np.uint64).reshape(objects, E, 2), want)
+    # bench shard layout: rank r's join shard is synthetic replicas [r*R, (r+1)*R)
+    R = 4
+    bases = [None] * world
+    dist.all_gather_object(bases, rank * R)
+    assert bases == [r * R for r in range(world)]
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)        # bench takes the max wall time
+    assert t.item() == float(world)
+    print("ok", rank)
+""")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_anti_entropy_gloo_world2(tmp_path):
+    from oracle import columnar
+    columnar.lib()
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER % {"root": ROOT})
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    assert res.stdout.count("ok") == 2
