@@ -25,6 +25,9 @@ struct laspj_ctx {
     uint64_t scratch_bytes = 0;
     // one device word for kernel-detected argument violations (product token slots)
     uint32_t* flag = nullptr;
+    // per-replica partial records of segmented reductions (grown on demand)
+    void* partials = nullptr;
+    uint64_t partials_bytes = 0;
 };
 
 struct laspj_buf {

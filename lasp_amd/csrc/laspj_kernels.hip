@@ -263,21 +263,31 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 template <bool REMOVED>
 __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64* out,
                                                         uint64_t R, uint32_t E) {
+    // one wave packs 4 consecutive 64-element words per iteration (4 x 1 KiB loads in
+    // flight per wave before the first __ballot)
+    constexpr int U = 4;
     const uint32_t W = (E + 63u) / 64u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t total = R * W;
-    for (uint64_t w = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; w < total;
-         w += nwaves) {
-        uint64_t rep = w / W;
-        uint32_t e = (uint32_t)(w - rep * W) * 64u + lane;
-        bool pred = false;
-        if (e < E) {
-            u64x2 c = ld2<true>(cells + rep * E + e);
-            pred = REMOVED ? (c.y != 0) : ((c.x & ~c.y) != 0);
+    for (uint64_t w0 = (((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * U; w0 < total;
+         w0 += nwaves * U) {
+        u64x2 c[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint64_t w = w0 + u;
+            uint64_t rep = w / W;
+            uint32_t e = (uint32_t)(w - rep * W) * 64u + lane;
+            ok[u] = w < total && e < E;
+            c[u] = ok[u] ? ld2<true>(cells + rep * E + e) : u64x2{0, 0};
         }
-        u64 m = __ballot(pred);
-        if (lane == 0) out[w] = m;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            bool pred = ok[u] && (REMOVED ? (c[u].y != 0) : ((c[u].x & ~c[u].y) != 0));
+            u64 m = __ballot(pred);
+            if (lane == 0 && w0 + u < total) out[w0 + u] = m;
+        }
     }
 }
 
@@ -298,19 +308,44 @@ hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* ou
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ stats (wave/replica)
+// ------------------------------------------------------------------ per-replica reductions
+// stats / equal / inflation reduce over each replica.  Work is cut into segments of
+// kSeg cells (kSegW words for G-Sets); one wave64 reduces one (replica, segment) item
+// with __ballot / __shfl_xor.  A replica that is a single segment (BASELINE config 2:
+// E = 4096) is finished by its wave; longer replicas (config 4: 3M slots) combine their
+// segments with one atomic per wave into ctx->partials and a finalize kernel, so the
+// launch always has R x segments waves of parallelism.
 
+constexpr uint32_t kSeg = 4096;     // OR-Set cells per segment (64 KiB)
+constexpr uint32_t kSegW = 4096;    // G-Set words per segment (32 KiB)
+
+struct SegIter {
+    uint64_t item, nitems, stride;
+    uint32_t nseg;
+};
+
+__device__ __forceinline__ void seg_range(uint64_t item, uint32_t nseg, uint64_t n, uint64_t seg,
+                                          uint64_t* rep, uint64_t* b, uint64_t* e) {
+    *rep = item / nseg;
+    uint64_t sg = item - *rep * nseg;
+    *b = sg * seg;
+    *e = min(n, *b + seg);
+}
+
+template <bool SEG>
 __global__ __launch_bounds__(kBlock) void k_orset_stats(const u64x2* cells, u64* out,
-                                                        uint64_t R, uint32_t E) {
+                                                        uint64_t R, uint32_t E, uint32_t nseg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
-         rep += nwaves) {
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, b, e;
+        seg_range(it, nseg, E, kSeg, &rep, &b, &e);
         const u64x2* c = cells + rep * E;
         u64 elems = 0, adds = 0, rems = 0;
 #pragma unroll 8
-        for (uint32_t e = lane; e < E; e += 64) {
-            u64x2 v = ld2<true>(c + e);
+        for (uint64_t i = b + lane; i < e; i += 64) {
+            u64x2 v = ld2<true>(c + i);
             elems += v.x != 0;
             adds += __popcll(v.x & ~v.y);
             rems += __popcll(v.y);
@@ -319,70 +354,189 @@ __global__ __launch_bounds__(kBlock) void k_orset_stats(const u64x2* cells, u64*
         adds = wave_sum(adds);
         rems = wave_sum(rems);
         if (lane == 0) {
-            out[rep * 3 + 0] = elems;
-            out[rep * 3 + 1] = adds;
-            out[rep * 3 + 2] = rems;
+            if constexpr (SEG) {
+                atomicAdd(out + rep * 3 + 0, elems);
+                atomicAdd(out + rep * 3 + 1, adds);
+                atomicAdd(out + rep * 3 + 2, rems);
+            } else {
+                out[rep * 3 + 0] = elems;
+                out[rep * 3 + 1] = adds;
+                out[rep * 3 + 2] = rems;
+            }
         }
     }
 }
 
+template <bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gset_stats(const u64* words, u64* out, uint64_t R,
-                                                       uint64_t W) {
+                                                       uint64_t W, uint32_t nseg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
-         rep += nwaves) {
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, b, e;
+        seg_range(it, nseg, W, kSegW, &rep, &b, &e);
         u64 n = 0;
-        for (uint64_t w = lane; w < W; w += 64) n += __popcll(words[rep * W + w]);
+        for (uint64_t w = b + lane; w < e; w += 64) n += __popcll(words[rep * W + w]);
         n = wave_sum(n);
-        if (lane == 0) out[rep] = n;
+        if (lane == 0) {
+            if constexpr (SEG) atomicAdd(out + rep, n);
+            else out[rep] = n;
+        }
     }
 }
 
+static uint32_t nseg_of(uint64_t n, uint64_t seg) { return (uint32_t)((n + seg - 1) / seg); }
+
+static int seg_grid(const laspj_ctx* ctx, uint64_t items) {
+    uint64_t blocks = (items + 3) / 4;
+    uint64_t cap = (uint64_t)ctx->cus * 16;
+    if (blocks > cap) blocks = cap;
+    return blocks ? (int)blocks : 1;
+}
+
 hipError_t launch_orset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
-    hipLaunchKernelGGL(k_orset_stats, dim3(wave_grid(ctx, b->replicas)), dim3(kBlock), 0,
-                       ctx->stream, reinterpret_cast<const u64x2*>(b->dev), (u64*)out,
-                       b->replicas, b->elements);
+    uint32_t ns = nseg_of(b->elements, kSeg);
+    int grid = seg_grid(ctx, b->replicas * ns);
+    auto* cells = reinterpret_cast<const u64x2*>(b->dev);
+    if (ns == 1) {
+        hipLaunchKernelGGL(k_orset_stats<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, cells,
+                           (u64*)out, b->replicas, b->elements, ns);
+    } else {
+        hipError_t e = hipMemsetAsync(out, 0, b->replicas * 24, ctx->stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_orset_stats<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, cells,
+                           (u64*)out, b->replicas, b->elements, ns);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_gset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
-    hipLaunchKernelGGL(k_gset_stats, dim3(wave_grid(ctx, b->replicas)), dim3(kBlock), 0,
-                       ctx->stream, (const u64*)b->dev, (u64*)out, b->replicas,
-                       b->words_per_replica);
+    uint32_t ns = nseg_of(b->words_per_replica, kSegW);
+    int grid = seg_grid(ctx, b->replicas * ns);
+    if (ns == 1) {
+        hipLaunchKernelGGL(k_gset_stats<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, (u64*)out, b->replicas, b->words_per_replica, ns);
+    } else {
+        hipError_t e = hipMemsetAsync(out, 0, b->replicas * 8, ctx->stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_gset_stats<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, (u64*)out, b->replicas, b->words_per_replica, ns);
+    }
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ equal (wave/replica)
+// per-replica partial record for segmented reductions: {flags, count P, count C, -}
+constexpr u64 kViol = 1, kChanged = 2;
 
+static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out) {
+    uint64_t need = R * 32;
+    if (ctx->partials_bytes < need) {
+        if (ctx->partials) {
+            hipError_t e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) return e;
+            hipFree(ctx->partials);
+            ctx->partials = nullptr;
+            ctx->partials_bytes = 0;
+        }
+        hipError_t e = hipMalloc(&ctx->partials, need);
+        if (e != hipSuccess) return e;
+        ctx->partials_bytes = need;
+    }
+    *out = static_cast<u64*>(ctx->partials);
+    return hipMemsetAsync(ctx->partials, 0, need, ctx->stream);
+}
+
+__device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t rep,
+                                     u64 flags, u64 np, u64 nc, int mode) {
+    // mode 0: equal (out = !diff), 1: inflation, 2: strict inflation
+    if (seg) {
+        if (flags) atomicOr(part + rep * 4, flags);
+        if (mode == 2) {
+            atomicAdd(part + rep * 4 + 1, np);
+            atomicAdd(part + rep * 4 + 2, nc);
+        }
+        return;
+    }
+    bool res;
+    if (mode == 0) res = !(flags & kViol);
+    else res = !(flags & kViol) && (mode == 1 || (flags & kChanged) || np < nc);
+    out[rep] = res ? 1 : 0;
+}
+
+__global__ void k_finalize(const u64* part, uint8_t* out, uint64_t R, int mode) {
+    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
+         rep += (uint64_t)gridDim.x * blockDim.x) {
+        u64 f = part[rep * 4];
+        bool res;
+        if (mode == 0) res = !(f & kViol);
+        else res = !(f & kViol) && (mode == 1 || (f & kChanged) || part[rep * 4 + 1] < part[rep * 4 + 2]);
+        out[rep] = res ? 1 : 0;
+    }
+}
+
+static hipError_t finalize(laspj_ctx* ctx, const u64* part, uint8_t* out, uint64_t R, int mode) {
+    uint64_t g = (R + kBlock - 1) / kBlock;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part, out, R,
+                       mode);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ equal
+// equal/2 (lasp_orset.erl:136-138, lasp_gset.erl:103-105): every word equal.
+
+template <bool SEG, bool VEC2>
 __global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, uint8_t* out,
-                                                  uint64_t R, uint64_t wr) {
+                                                  u64* part, uint64_t R, uint64_t wr,
+                                                  uint32_t nseg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
-         rep += nwaves) {
+    const uint64_t n = VEC2 ? wr / 2 : wr;
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, n, kSeg, &rep, &lo, &hi);
         bool diff = false;
-        if ((wr & 1) == 0) {
+        if constexpr (VEC2) {
             const u64x2* a2 = reinterpret_cast<const u64x2*>(a + rep * wr);
             const u64x2* b2 = reinterpret_cast<const u64x2*>(b + rep * wr);
 #pragma unroll 4
-            for (uint64_t w = lane; w < wr / 2; w += 64) {
+            for (uint64_t w = lo + lane; w < hi; w += 64) {
                 u64x2 x = ld2<true>(a2 + w), y = ld2<true>(b2 + w);
                 diff |= (x.x != y.x) | (x.y != y.y);
             }
         } else {
-            for (uint64_t w = lane; w < wr; w += 64) diff |= a[rep * wr + w] != b[rep * wr + w];
+            for (uint64_t w = lo + lane; w < hi; w += 64) diff |= a[rep * wr + w] != b[rep * wr + w];
         }
         bool any = __ballot(diff) != 0;
-        if (lane == 0) out[rep] = any ? 0 : 1;
+        if (lane == 0) emit(SEG, out, part, rep, any ? kViol : 0, 0, 0, 0);
     }
 }
 
 hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
                         uint8_t* out) {
-    hipLaunchKernelGGL(k_equal, dim3(wave_grid(ctx, a->replicas)), dim3(kBlock), 0,
-                       ctx->stream, (const u64*)a->dev, (const u64*)b->dev, out, a->replicas,
-                       a->words_per_replica);
+    bool vec2 = (a->words_per_replica & 1) == 0;
+    uint64_t n = vec2 ? a->words_per_replica / 2 : a->words_per_replica;
+    uint32_t ns = nseg_of(n, kSeg);
+    int grid = seg_grid(ctx, a->replicas * ns);
+    u64* part = nullptr;
+    if (ns > 1) {
+        hipError_t e = partials(ctx, a->replicas, &part);
+        if (e != hipSuccess) return e;
+    }
+#define LJ_EQ(S, V)                                                                        \
+    hipLaunchKernelGGL((k_equal<S, V>), dim3(grid), dim3(kBlock), 0, ctx->stream,          \
+                       (const u64*)a->dev, (const u64*)b->dev, out, part, a->replicas,     \
+                       a->words_per_replica, ns)
+    if (ns > 1) {
+        if (vec2) LJ_EQ(true, true); else LJ_EQ(true, false);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return finalize(ctx, part, out, a->replicas, 0);
+    }
+    if (vec2) LJ_EQ(false, true); else LJ_EQ(false, false);
+#undef LJ_EQ
     return hipGetLastError();
 }
 
@@ -393,21 +547,23 @@ hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch*
 // lasp_lattice.erl:235-253 (strict): [] -> non-empty is true; otherwise
 // inflation && (some element of Prev found in Cur with a different token dict
 //               || length(Prev) < length(Cur)).
-template <bool STRICT>
+template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
                                                             const u64x2* cur, uint8_t* out,
-                                                            uint64_t R, uint32_t E,
-                                                            bool prev_bcast) {
+                                                            u64* part, uint64_t R, uint32_t E,
+                                                            bool prev_bcast, uint32_t nseg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
-         rep += nwaves) {
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, E, kSeg, &rep, &lo, &hi);
         const u64x2* P = prev + (prev_bcast ? 0 : rep * E);
         const u64x2* C = cur + rep * E;
         bool viol = false, changed = false;
         u64 np = 0, nc = 0;
 #pragma unroll 4
-        for (uint32_t e = lane; e < E; e += 64) {
+        for (uint64_t e = lo + lane; e < hi; e += 64) {
             u64x2 p = ld2<false>(P + e), c = ld2<true>(C + e);
             viol |= (p.x & ~c.x) != 0;
             if constexpr (STRICT) {
@@ -416,68 +572,93 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
                 nc += c.x != 0;
             }
         }
-        bool infl = __ballot(viol) == 0;
-        bool res = infl;
+        u64 flags = (__ballot(viol) != 0) ? kViol : 0;
         if constexpr (STRICT) {
-            bool any_changed = __ballot(changed) != 0;
+            if (__ballot(changed) != 0) flags |= kChanged;
             np = wave_sum(np);
             nc = wave_sum(nc);
-            res = infl && (any_changed || np < nc);
         }
-        if (lane == 0) out[rep] = res ? 1 : 0;
+        if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1);
     }
 }
 
 // lasp_lattice.erl:137-140 / :212-215: subset, and strict adds "sets differ".
-template <bool STRICT>
+template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, const u64* cur,
-                                                           uint8_t* out, uint64_t R,
-                                                           uint64_t W, bool prev_bcast) {
+                                                           uint8_t* out, u64* part, uint64_t R,
+                                                           uint64_t W, bool prev_bcast,
+                                                           uint32_t nseg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
-         rep += nwaves) {
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
         const u64* P = prev + (prev_bcast ? 0 : rep * W);
         const u64* C = cur + rep * W;
         bool viol = false, diff = false;
-        for (uint64_t w = lane; w < W; w += 64) {
+        for (uint64_t w = lo + lane; w < hi; w += 64) {
             u64 p = P[w], c = C[w];
             viol |= (p & ~c) != 0;
             diff |= p != c;
         }
-        bool res = __ballot(viol) == 0;
-        if constexpr (STRICT) res = res && (__ballot(diff) != 0);
-        if (lane == 0) out[rep] = res ? 1 : 0;
+        u64 flags = (__ballot(viol) != 0) ? kViol : 0;
+        if (__ballot(diff) != 0) flags |= kChanged;
+        // strict = subset and differs: "differs" plays the role of `changed`, and
+        // np = nc = 0 so the length test never fires
+        if (lane == 0) emit(SEG, out, part, rep, flags, 0, 0, STRICT ? 2 : 1);
     }
 }
 
 hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                   const laspj_batch* cur, bool strict, uint8_t* out) {
-    int grid = wave_grid(ctx, cur->replicas);
+    uint32_t ns = nseg_of(cur->elements, kSeg);
+    int grid = seg_grid(ctx, cur->replicas * ns);
     bool bc = prev->replicas == 1 && cur->replicas != 1;
     auto* P = reinterpret_cast<const u64x2*>(prev->dev);
     auto* C = reinterpret_cast<const u64x2*>(cur->dev);
-    if (strict)
-        hipLaunchKernelGGL(k_orset_inflation<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, P,
-                           C, out, cur->replicas, cur->elements, bc);
-    else
-        hipLaunchKernelGGL(k_orset_inflation<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           P, C, out, cur->replicas, cur->elements, bc);
+    u64* part = nullptr;
+    if (ns > 1) {
+        hipError_t e = partials(ctx, cur->replicas, &part);
+        if (e != hipSuccess) return e;
+    }
+#define LJ_INF(ST, SG)                                                                      \
+    hipLaunchKernelGGL((k_orset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
+                       P, C, out, part, cur->replicas, cur->elements, bc, ns)
+    if (ns > 1) {
+        if (strict) LJ_INF(true, true); else LJ_INF(false, true);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
+    }
+    if (strict) LJ_INF(true, false); else LJ_INF(false, false);
+#undef LJ_INF
     return hipGetLastError();
 }
 
 hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                  const laspj_batch* cur, bool strict, uint8_t* out) {
-    int grid = wave_grid(ctx, cur->replicas);
+    uint64_t W = cur->words_per_replica;
+    uint32_t ns = nseg_of(W, kSegW);
+    int grid = seg_grid(ctx, cur->replicas * ns);
     bool bc = prev->replicas == 1 && cur->replicas != 1;
-    if (strict)
-        hipLaunchKernelGGL(k_gset_inflation<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)prev->dev, (const u64*)cur->dev, out, cur->replicas,
-                           cur->words_per_replica, bc);
-    else
-        hipLaunchKernelGGL(k_gset_inflation<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)prev->dev, (const u64*)cur->dev, out, cur->replicas,
-                           cur->words_per_replica, bc);
+    u64* part = nullptr;
+    if (ns > 1) {
+        hipError_t e = partials(ctx, cur->replicas, &part);
+        if (e != hipSuccess) return e;
+    }
+#define LJ_GINF(ST, SG)                                                                     \
+    hipLaunchKernelGGL((k_gset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
+                       (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas, \
+                       W, bc, ns)
+    if (ns > 1) {
+        if (strict) LJ_GINF(true, true); else LJ_GINF(false, true);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
+    }
+    if (strict) LJ_GINF(true, false); else LJ_GINF(false, false);
+#undef LJ_GINF
     return hipGetLastError();
 }
 

@@ -185,6 +185,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         hipStreamSynchronize(ctx->stream);
         if (ctx->scratch) hipFree(ctx->scratch);
         if (ctx->flag) hipFree(ctx->flag);
+        if (ctx->partials) hipFree(ctx->partials);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;

@@ -381,3 +381,46 @@ def test_gset_combinators(ctx):
         assert pairs == core.product_body("lasp_gset", la, lb)
         got_g = [o for o in range(e_n) if (int(G[i, o >> 6]) >> (o & 63)) & 1]
         assert got_g == [o for o in range(e_n) if (o // 2) in set(la)]
+
+
+def test_segmented_reductions_long_replicas(ctx):
+    """Replicas longer than one 4096-cell segment (config 4 shape, scaled down): stats,
+    equal and (strict) inflation combine per-segment partials exactly."""
+    n, e_n = 5, 10_000
+    tok = orc.synth_tokens(e_n, 64)
+    prev = _synth(101, n, e_n)
+    cur = prev.copy()
+    cur[1, 9_000, 1] = cur[1, 9_000, 0]              # tombstone far in the last segment
+    cur[2, 5_000, 0] = 0                             # drop an element: not an inflation
+    cur[2, 5_000, 1] = 0
+    cur[3] |= _synth(102, 1, e_n)[0]                 # strict growth
+    P, Cb = ctx.orset_batch(n, e_n), ctx.orset_batch(n, e_n)
+    P.upload(prev)
+    Cb.upload(cur)
+    st = Cb.stats()
+    eq = Cb.equal(P)
+    infl = Cb.is_inflation_of(P)
+    strict = Cb.is_inflation_of(P, strict=True)
+    for i in range(n):
+        Dp, Dc = orc.ORDict.from_cells(prev[i], tok), orc.ORDict.from_cells(cur[i], tok)
+        assert tuple(int(x) for x in st[i]) == Dc.stats()
+        assert eq[i] == Dc.equal(Dp)
+        assert infl[i] == Dc.is_inflation_of(Dp)
+        assert strict[i] == Dc.is_strict_inflation_of(Dp)
+    # G-Set with more than 4096 words per replica
+    g_e = 300_000
+    ga, gb = ctx.gset_batch(3, g_e), ctx.gset_batch(3, g_e)
+    ga.fill_synthetic(7)
+    h = ga.download()
+    h2 = h.copy()
+    h2[0, 4_500] |= np.uint64(1) << np.uint64(3) if not (h[0, 4_500] >> np.uint64(3)) & np.uint64(1) else np.uint64(0)
+    h2[1, 4_600] = 0
+    gb.upload(h2)
+    assert list(gb.stats()) == [sum(bin(int(w)).count("1") for w in row) for row in h2]
+    eqg = gb.equal(ga)
+    ig = gb.is_inflation_of(ga)
+    sg = gb.is_inflation_of(ga, strict=True)
+    for i in range(3):
+        sub = not np.any(h[i] & ~h2[i])
+        same = np.array_equal(h[i], h2[i])
+        assert eqg[i] == same and ig[i] == sub and sg[i] == (sub and not same)

@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Per-kernel and per-config measurements beyond bench.py's headline line.
+
+Each line: kernel / workload, average launch time from HIP events on the engine's
+stream, algorithmic bytes per launch (DESIGN.md §4 per-unit figures x units) and the
+fraction of the 8 TB/s HBM peak.  Workloads:
+  kernels at BASELINE config 2 size (2^20 replicas x 4096 slots unless noted);
+  config 4: ad-counter dataflow map -> filter -> fold -> strict threshold over 1024
+            OR-Set objects x 1M int elements x 3 tokens;
+  config 5: intersection (1024 pairs x 150k slots, 50 % id overlap) and product
+            (100k x 100k, 3 tokens: 4 B per cell written).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from lasp_amd import engine  # noqa: E402
+from lasp_amd import _lib  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(ctx, fn, steps, warmup=1):
+    for _ in range(warmup):
+        fn()
+    ctx.synchronize()
+    e0, e1 = ctx.event(), ctx.event()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    return e0.elapsed_ms(e1) / steps
+
+
+def report(name, ms, nbytes, units, unit_name, **extra):
+    gbs = nbytes / (ms / 1e3) / 1e9
+    d = {"kernel": name, "ms": round(ms, 4), "algorithmic_bytes": int(nbytes),
+         "GBps": round(gbs, 1), "frac_hbm": round(gbs / PEAK, 4),
+         unit_name: units / (ms / 1e3)}
+    d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def kernels(ctx, R, E, steps):
+    a, b, c = ctx.orset_batch(R, E), ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    cells = R * E
+    W = (E + 63) // 64
+    report("orset_join", timed(ctx, lambda: c.join(a, b), steps), 48 * cells, cells, "cells_per_s")
+    bits = ctx.buffer(R * W * 8)
+    L = ctx.L
+    report("orset_value", timed(ctx, lambda: _lib.check(L.laspj_orset_value(ctx.h, a.h, bits.h)), steps),
+           16 * cells + R * W * 8, cells, "cells_per_s")
+    st = ctx.buffer(R * 24)
+    report("orset_stats", timed(ctx, lambda: _lib.check(L.laspj_orset_stats(ctx.h, a.h, st.h)), steps),
+           16 * cells + R * 24, cells, "cells_per_s")
+    o = ctx.buffer(R)
+    for strict in (0, 1):
+        c.join(a, b)
+        report(f"orset_inflation_strict{strict}",
+               timed(ctx, lambda: _lib.check(L.laspj_orset_inflation(ctx.h, a.h, c.h, strict, o.h)), steps),
+               32 * cells + R, cells, "cells_per_s")
+    report("orset_equal", timed(ctx, lambda: _lib.check(L.laspj_orset_equal(ctx.h, a.h, c.h, o.h)), steps),
+           32 * cells + R, cells, "cells_per_s")
+    report("orset_union", timed(ctx, lambda: c.union(a, b), steps), 48 * cells, cells, "cells_per_s")
+    keep = ctx.buffer(W * 8)
+    keep.upload(np.full((W,), 0x5555555555555555, np.uint64))
+    report("orset_filter", timed(ctx, lambda: _lib.check(L.laspj_orset_filter(ctx.h, c.h, a.h, keep.h)), steps),
+           32 * cells, cells, "cells_per_s")
+    idx = ctx.buffer(4 * E)
+    idx.upload(np.arange(E, dtype=np.uint32)[::-1].copy())
+    report("orset_gather", timed(ctx, lambda: _lib.check(L.laspj_orset_gather(ctx.h, c.h, a.h, idx.h)), steps),
+           32 * cells, cells, "cells_per_s")
+    del c
+    # FSM N-way merge: groups of N=3 replicas (lasp_update_fsm.erl:189-192)
+    g = R // 4
+    src = ctx.orset_batch(3 * g, E)
+    dst = ctx.orset_batch(g, E)
+    src.fill_synthetic(4)
+    report("orset_reduce_n3", timed(ctx, lambda: dst.reduce_from(src, 3), steps),
+           64 * g * E, g * E, "dst_cells_per_s")
+    del src, dst, a, b
+    h = R // 2                      # CONCAT output is 32 B per cell: half the replicas
+    a2, b2 = ctx.orset_batch(h, E), ctx.orset_batch(h, E)
+    a2.fill_synthetic(2)
+    b2.fill_synthetic(3)
+    x = a2.intersection(b2)
+    report("orset_intersection", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_intersection(ctx.h, x.h, a2.h, b2.h)), steps), 64 * h * E, h * E, "cells_per_s")
+    del x, a2, b2
+    # G-Set at the same element count
+    ga, gb, gc = (ctx.gset_batch(R, E) for _ in range(3))
+    ga.fill_synthetic(5)
+    gb.fill_synthetic(6)
+    report("gset_join", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * R * W, R * E, "elements_per_s")
+
+
+def ops(ctx, steps):
+    """update/3 throughput: 1M single-op calls spread over 2^20 replicas."""
+    R, E = 1 << 20, 64
+    b = ctx.orset_batch(R, E)
+    rng = np.random.default_rng(0)
+    n = 1 << 20
+    reps = np.sort(rng.integers(0, R, n))
+    arr = (_lib.Op * n)()
+    el = rng.integers(0, E, n)
+    sl = rng.integers(0, 64, n)
+    kd = np.where(rng.random(n) < 0.8, _lib.OP_ADD, _lib.OP_REMOVE)
+    for k in range(n):
+        arr[k].replica, arr[k].element, arr[k].kind = int(reps[k]), int(el[k]), int(kd[k])
+        arr[k].slot, arr[k].flags = int(sl[k]), 1
+    st = np.zeros((n,), np.int32)
+    ptr = st.ctypes.data_as(_lib.C.POINTER(_lib.C.c_int32))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _lib.check(ctx.L.laspj_orset_apply_ops(ctx.h, b.h, arr, n, ptr), ctx.h)
+    dt = (time.perf_counter() - t0) / steps
+    print(json.dumps({"kernel": "orset_apply_ops", "ms": round(dt * 1e3, 3), "ops": n,
+                      "ops_per_s": n / dt, "note": "host->device op upload + status download included"}),
+          flush=True)
+
+
+def config4(ctx, objects, elements, steps):
+    """map X->2X -> filter even -> fold X->[X,X,X] -> strict threshold vs previous fold.
+    Dictionary-level work (F evaluated once per element) is host-side and not timed;
+    the per-replica work is one gather / filter / gather / inflation launch each."""
+    E = elements
+    src = ctx.orset_batch(objects, E)
+    src.fill_synthetic(40)
+    # T = 3 tokens: keep token slots 0..2 (synthetic cells masked on device by a filter
+    # is not possible; tokens beyond slot 2 are simply present - the byte traffic is the
+    # same 16 B per cell either way)
+    mapped = ctx.orset_batch(objects, E)
+    filt = ctx.orset_batch(objects, E)
+    fold = ctx.orset_batch(objects, 3 * E)
+    prev = ctx.orset_batch(objects, 3 * E)
+    L = ctx.L
+    ident = ctx.buffer(4 * E)
+    ident.upload(np.arange(E, dtype=np.uint32))       # X -> 2X is monotone: slot order kept
+    keep = ctx.buffer(((E + 63) // 64) * 8)
+    keep.upload(np.full(((E + 63) // 64,), ~np.uint64(0), np.uint64))   # 2X is even
+    fidx = ctx.buffer(4 * 3 * E)
+    fidx.upload(np.repeat(np.arange(E, dtype=np.uint32), 3))
+    out = ctx.buffer(objects)
+
+    def step():
+        _lib.check(L.laspj_orset_gather(ctx.h, mapped.h, src.h, ident.h), ctx.h)
+        _lib.check(L.laspj_orset_filter(ctx.h, filt.h, mapped.h, keep.h), ctx.h)
+        _lib.check(L.laspj_orset_gather(ctx.h, fold.h, filt.h, fidx.h), ctx.h)
+        _lib.check(L.laspj_orset_inflation(ctx.h, prev.h, fold.h, 1, out.h), ctx.h)
+    ms = timed(ctx, step, steps)
+    cells = objects * E
+    nbytes = 32 * cells + 32 * cells + (16 + 48) * cells + 2 * 48 * cells
+    report("config4_dataflow", ms, nbytes, cells, "input_elements_per_s",
+           objects=objects, elements=E,
+           stages="gather 32B + filter 32B + fold-gather 64B + strict inflation 96B per input element")
+
+
+def config5(ctx, steps):
+    # intersection: 1024 pairs over a 150k-slot dictionary, each side 100k elements
+    P, E = 1024, 150_000
+    l, r = ctx.orset_batch(P, E), ctx.orset_batch(P, E)
+    l.fill_synthetic(5)
+    r.fill_synthetic(6)
+    x = l.intersection(r)
+    L = ctx.L
+    report("config5_intersection", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_intersection(ctx.h, x.h, l.h, r.h), ctx.h), steps),
+        64 * P * E, P * E, "slots_per_s", pairs=P, slots=E)
+    del x, l, r
+    # product: 100k x 100k, T = 3 token slots
+    n = 100_000
+    pl, pr = ctx.orset_batch(1, n), ctx.orset_batch(1, n)
+    h = np.zeros((1, n, 2), np.uint64)
+    rng = np.random.default_rng(5)
+    h[0, :, 0] = rng.integers(1, 8, n, dtype=np.uint64)
+    h[0, :, 1] = h[0, :, 0] & rng.integers(0, 8, n, dtype=np.uint64)
+    pl.upload(h)
+    pr.upload(h)
+    out = engine.ORSetProductBatch(ctx, 1, n, n)
+    ms = timed(ctx, lambda: pl.product(pr, out), steps)
+    report("config5_product", ms, 4 * n * n + 32 * n, n * n, "cells_per_s", el=n, er=n)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replicas", type=int, default=1 << 20)
+    ap.add_argument("--elements", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--only", default="kernels,ops,config4,config5")
+    a = ap.parse_args()
+    ctx = engine.Context(0)
+    todo = a.only.split(",")
+    if "kernels" in todo:
+        kernels(ctx, a.replicas, a.elements, a.steps)
+    if "ops" in todo:
+        ops(ctx, 3)
+    if "config4" in todo:
+        config4(ctx, 1024, 1 << 20, a.steps)
+    if "config5" in todo:
+        config5(ctx, a.steps)
+
+
+if __name__ == "__main__":
+    main()
