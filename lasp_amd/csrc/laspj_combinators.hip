@@ -33,22 +33,25 @@ static int grid_for(const laspj_ctx* ctx, uint64_t items, int per_cu = 64) {
 
 // ------------------------------------------------------------------ intersection
 
+// One lane per 16-byte output half: lanes 2i and 2i+1 write cell i's L and R halves, so
+// every store instruction covers 1 KiB of consecutive bytes; the pair reads the same two
+// input cells (one cache line fetch serves both lanes).
 __global__ __launch_bounds__(kB) void k_orset_intersection(u64x2* out, const u64x2* l,
                                                            const u64x2* r, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * kB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
+    for (uint64_t u = (uint64_t)blockIdx.x * kB + threadIdx.x; u < 2 * n; u += stride) {
+        uint64_t i = u >> 1;
         u64x2 a = ldnt(l + i), b = ldnt(r + i);
         bool keep = (a.x != 0) & (b.x != 0);   // X in L and lists:keyfind(X, R) found
         u64x2 z = {0, 0};
-        stnt(out + 2 * i, keep ? a : z);
-        stnt(out + 2 * i + 1, keep ? b : z);
+        stnt(out + u, keep ? ((u & 1) ? b : a) : z);
     }
 }
 
 hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                      const laspj_batch* r) {
     uint64_t n = l->replicas * l->elements;
-    hipLaunchKernelGGL(k_orset_intersection, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_orset_intersection, dim3(grid_for(ctx, 2 * n)), dim3(kB), 0, ctx->stream,
                        reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
                        reinterpret_cast<const u64x2*>(r->dev), n);
     return hipGetLastError();

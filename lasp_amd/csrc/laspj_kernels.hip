@@ -122,22 +122,40 @@ hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uin
 
 // ------------------------------------------------------------------ reduce over groups
 
-// dst replica g = OR_{j<group} src replica (g*group + j); vectorised over word pairs
+// dst replica g = OR_{j<group} src replica (g*group + j); vectorised over word pairs,
+// two destination items per lane per iteration so 2*group loads are in flight
 template <bool VEC2>
 __global__ __launch_bounds__(kBlock) void k_reduce_or(u64* dst, const u64* src, uint64_t groups,
                                                       uint32_t group, uint64_t wr) {
     const uint64_t per = VEC2 ? wr / 2 : wr;          // items per replica
     const uint64_t n = groups * per;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        uint64_t g = i / per, w = i - g * per;
-        uint64_t base = g * group * per + w;
-        if constexpr (VEC2) {
-            const u64x2* s = reinterpret_cast<const u64x2*>(src);
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (VEC2) {
+        const u64x2* s = reinterpret_cast<const u64x2*>(src);
+        u64x2* d = reinterpret_cast<u64x2*>(dst);
+        for (; i + stride < n; i += 2 * stride) {
+            uint64_t i1 = i + stride;
+            uint64_t g0 = i / per, g1 = i1 / per;
+            uint64_t b0 = g0 * group * per + (i - g0 * per), b1 = g1 * group * per + (i1 - g1 * per);
+            u64x2 a0 = ld2<true>(s + b0), a1 = ld2<true>(s + b1);
+            for (uint32_t j = 1; j < group; ++j) {
+                a0 |= ld2<true>(s + b0 + j * per);
+                a1 |= ld2<true>(s + b1 + j * per);
+            }
+            st2<true>(d + i, a0);
+            st2<true>(d + i1, a1);
+        }
+        for (; i < n; i += stride) {
+            uint64_t g = i / per, base = g * group * per + (i - g * per);
             u64x2 acc = ld2<true>(s + base);
             for (uint32_t j = 1; j < group; ++j) acc |= ld2<true>(s + base + j * per);
-            st2<true>(reinterpret_cast<u64x2*>(dst) + i, acc);
-        } else {
+            st2<true>(d + i, acc);
+        }
+    } else {
+        for (; i < n; i += stride) {
+            uint64_t g = i / per, w = i - g * per;
+            uint64_t base = g * group * per + w;
             u64 acc = src[base];
             for (uint32_t j = 1; j < group; ++j) acc |= src[base + j * per];
             dst[i] = acc;
