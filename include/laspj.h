@@ -60,6 +60,8 @@ extern "C" {
 #define LASPJ_KIND_ORSET_PRODUCT 4  /* product: EL x ER cells of uint32
                                        {pX:8, rX:8, pY:8, rY:8}, cell (x,y) at x*ER+y  */
 #define LASPJ_KIND_GSET_PRODUCT  5  /* product: EL rows x ceil(ER/64) words           */
+#define LASPJ_KIND_GCOUNTER      6  /* riak_dt_gcounter: R x E actor slots, uint64 count
+                                       per slot (0 = actor absent from the orddict)   */
 
 typedef struct laspj_ctx   laspj_ctx;
 typedef struct laspj_buf   laspj_buf;
@@ -260,6 +262,40 @@ int laspj_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
 /* map / fold bodies for lasp_gset: dst bit o = src bit index[o] */
 int laspj_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                       const laspj_buf* index);
+
+/* ------------------------------------------------------------------ riak_dt_gcounter */
+/* The G-Counter the ad counter's threshold reads use.  State is
+ * the orddict Actor -> Count of riak_dt_gcounter (third-party riak_dt, not vendored;
+ * its merge is the per-actor max, its value the sum).  Actor slots are host
+ * dictionary positions, like element slots. */
+typedef struct laspj_incr {
+    uint64_t replica;
+    uint32_t actor;              /* actor slot */
+    uint32_t amount;             /* increment / {increment, N} */
+} laspj_incr;
+int laspj_gcounter_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t actors,
+                                laspj_batch** out);
+/* merge/2: per-actor max */
+int laspj_gcounter_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                        const laspj_batch* b);
+/* value/1: one uint64 sum per replica */
+int laspj_gcounter_value(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_sums);
+/* threshold_met(riak_dt_gcounter, V, T) — lasp_lattice.erl:87-90:
+ * T =< value(V) (strict = 0) or T < value(V) (strict = 1); one byte per replica */
+int laspj_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* batch, uint64_t threshold,
+                             int strict, laspj_buf* out);
+/* is_inflation — lasp_lattice.erl:169-179 (every Prev actor in Cur with Count =< Count1);
+ * strict — :273-275 (value(Prev) < value(Cur)); prev may be one broadcast replica */
+int laspj_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                             int strict, laspj_buf* out);
+int laspj_gcounter_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                         laspj_buf* out);
+/* update(increment | {increment, N}, Actor, C): counts are commutative, any order */
+int laspj_gcounter_apply_increments(laspj_ctx* ctx, laspj_batch* batch,
+                                    const laspj_incr* incs, uint64_t n);
+/* FSM N-way merge over groups of `group` replicas (per-actor max) */
+int laspj_gcounter_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                          uint32_t group);
 
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);

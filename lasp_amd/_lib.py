@@ -18,6 +18,7 @@ OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
     -1, -2, -3, -4, -5, -6, -7, -8)
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
+KIND_GCOUNTER = 6
 OP_ADD, OP_REMOVE = 1, 2
 OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK = 0, 1, 2
@@ -44,6 +45,10 @@ class BatchInfo(C.Structure):
 class Op(C.Structure):
     _fields_ = [("replica", C.c_uint64), ("element", C.c_uint32), ("kind", C.c_uint8),
                 ("slot", C.c_uint8), ("flags", C.c_uint8), ("pad", C.c_uint8)]
+
+
+class Incr(C.Structure):
+    _fields_ = [("replica", C.c_uint64), ("actor", C.c_uint32), ("amount", C.c_uint32)]
 
 
 vp = C.c_void_p
@@ -105,6 +110,14 @@ SIGNATURES = {
     "laspj_gset_equal": (i, [vp, vp, vp, vp]),
     "laspj_gset_inflation": (i, [vp, vp, vp, i, vp]),
     "laspj_gset_apply_ops": (i, [vp, vp, C.POINTER(Op), u64, C.POINTER(C.c_int32)]),
+    "laspj_gcounter_batch_create": (i, [vp, u64, u32, vpp]),
+    "laspj_gcounter_join": (i, [vp, vp, vp, vp]),
+    "laspj_gcounter_value": (i, [vp, vp, vp]),
+    "laspj_gcounter_threshold": (i, [vp, vp, u64, i, vp]),
+    "laspj_gcounter_inflation": (i, [vp, vp, vp, i, vp]),
+    "laspj_gcounter_equal": (i, [vp, vp, vp, vp]),
+    "laspj_gcounter_apply_increments": (i, [vp, vp, C.POINTER(Incr), u64]),
+    "laspj_gcounter_reduce": (i, [vp, vp, vp, u32]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

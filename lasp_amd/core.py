@@ -61,6 +61,7 @@ class Store:
         self.cap = capacity
         self.odom = Domain(element_capacity=capacity)
         self.gdom = Domain(element_capacity=capacity)
+        self.cdom = Domain(element_capacity=capacity)      # G-Counter actors
         self.vars: Dict = {}
         self.procs: List[dict] = []
         self._n = 0
@@ -73,14 +74,21 @@ class Store:
             return self.ctx.orset_batch(1, self.cap)
         if type_ == "lasp_gset":
             return self.ctx.gset_batch(1, self.cap)
+        if type_ == "riak_dt_gcounter":
+            return self.ctx.gcounter_batch(1, self.cap)
         raise Unsupported(type_)
 
     def _encode(self, type_, term):
         b = self._new_batch(type_)
         if type_ == "lasp_orset":
             b.upload(self.odom.encode_orset([term], self.cap))
-        else:
+        elif type_ == "lasp_gset":
             b.upload(self.gdom.encode_gset([term], self.cap))
+        else:
+            host = np.zeros((1, self.cap), dtype=np.uint64)
+            for actor, n in term:
+                host[0, self.cdom.element_slot(actor)] = n
+            b.upload(host)
         return b
 
     def _copy(self, b):
@@ -195,7 +203,10 @@ class Store:
             raise ValueError("badmatch: update on a combinator output")
         from . import orset as _o
         cur = self._copy(v.val)
-        if v.type == "lasp_orset":
+        if v.type == "riak_dt_gcounter":
+            n = 1 if op == "increment" else op[1]
+            cur.increment([(0, self.cdom.element_slot(actor), n)])
+        elif v.type == "lasp_orset":
             ops = []
             _o._compile(op, self.odom, ops, new_call=True)
             st = cur.apply_ops(ops)
@@ -225,6 +236,12 @@ class Store:
         """lasp_lattice:threshold_met/3 on the device (lasp_lattice.erl:62-75)."""
         strict = isinstance(threshold, tuple) and threshold[0] == "strict"
         term = threshold[1] if strict else threshold
+        if v.type == "riak_dt_gcounter":
+            # Threshold =< value(V) (lasp_lattice.erl:87-90); an integer threshold is
+            # compared on the device; new() = [] is never below a number in term order
+            if not isinstance(term, int) or isinstance(term, bool):
+                return False
+            return bool(v.val.threshold_met(term, strict)[0])
         if v.rep != "canonical":
             # combinator outputs are only read with the bottom threshold
             if term not in ([],):
@@ -237,6 +254,9 @@ class Store:
         """The variable's value as the reference would hold it (decoded from HBM)."""
         v = self.vars[id_]
         cells = v.val.download()[0]
+        if v.type == "riak_dt_gcounter":
+            return [(self.cdom.elements.terms[int(a)], int(cells[int(a)]))
+                    for a in self.cdom.elements.order() if int(cells[int(a)])]
         if v.rep == "canonical":
             return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
                 self.gdom.decode_gset(cells)
@@ -250,6 +270,8 @@ class Store:
     def type_value(self, id_):
         """Type:value(Value) of the variable (value/1 kernel + decode)."""
         v = self.vars[id_]
+        if v.type == "riak_dt_gcounter":
+            return int(v.val.values()[0])
         if v.type == "lasp_gset":
             return self.value(id_)
         bits = v.val.value_bits()[0]
@@ -372,8 +394,12 @@ class _DeviceValue:
 
 
 def _or_into(ctx, dst, a, b):
-    """dst := a ⊔ b slot-wise for any representation (one k_or16 launch)."""
-    _lib.check(ctx.L.laspj_batch_join(ctx.h, dst.h, a.h, b.h), ctx.h)
+    """dst := a ⊔ b slot-wise for any representation: one k_or16 launch, or the
+    per-actor max for G-Counters."""
+    if isinstance(dst, engine.GCounterBatch):
+        _lib.check(ctx.L.laspj_gcounter_join(ctx.h, dst.h, a.h, b.h), ctx.h)
+    else:
+        _lib.check(ctx.L.laspj_batch_join(ctx.h, dst.h, a.h, b.h), ctx.h)
 
 
 def _concat_visible(dom: Domain, bits) -> list:

@@ -85,6 +85,17 @@ StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16);
 
 hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
                      uint64_t words);
+hipError_t launch_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                      uint64_t words);
+hipError_t launch_reduce_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                             uint64_t groups, uint32_t group, uint64_t wr);
+hipError_t launch_gcounter_sums(laspj_ctx* ctx, const laspj_batch* b, uint64_t* sums);
+hipError_t launch_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* b, uint64_t t,
+                                     bool strict, uint8_t* out);
+hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                     const laspj_batch* cur, bool strict, uint8_t* out);
+hipError_t launch_gcounter_incr(laspj_ctx* ctx, laspj_batch* b, const laspj_incr* incs,
+                                uint64_t n);
 hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                                 uint64_t words, uint32_t nchunks);
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,

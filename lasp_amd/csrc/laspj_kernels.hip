@@ -337,11 +337,6 @@ hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* ou
 constexpr uint32_t kSeg = 4096;     // OR-Set cells per segment (64 KiB)
 constexpr uint32_t kSegW = 4096;    // G-Set words per segment (32 KiB)
 
-struct SegIter {
-    uint64_t item, nitems, stride;
-    uint32_t nseg;
-};
-
 __device__ __forceinline__ void seg_range(uint64_t item, uint32_t nseg, uint64_t n, uint64_t seg,
                                           uint64_t* rep, uint64_t* b, uint64_t* e) {
     *rep = item / nseg;
@@ -470,7 +465,7 @@ __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t
     // mode 0: equal (out = !diff), 1: inflation, 2: strict inflation
     if (seg) {
         if (flags) atomicOr(part + rep * 4, flags);
-        if (mode == 2) {
+        if (mode >= 2) {
             atomicAdd(part + rep * 4 + 1, np);
             atomicAdd(part + rep * 4 + 2, nc);
         }
@@ -478,6 +473,7 @@ __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t
     }
     bool res;
     if (mode == 0) res = !(flags & kViol);
+    else if (mode == 3) res = np < nc;
     else res = !(flags & kViol) && (mode == 1 || (flags & kChanged) || np < nc);
     out[rep] = res ? 1 : 0;
 }
@@ -488,6 +484,7 @@ __global__ void k_finalize(const u64* part, uint8_t* out, uint64_t R, int mode) 
         u64 f = part[rep * 4];
         bool res;
         if (mode == 0) res = !(f & kViol);
+        else if (mode == 3) res = part[rep * 4 + 1] < part[rep * 4 + 2];
         else res = !(f & kViol) && (mode == 1 || (f & kChanged) || part[rep * 4 + 1] < part[rep * 4 + 2]);
         out[rep] = res ? 1 : 0;
     }
@@ -677,6 +674,208 @@ hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
     }
     if (strict) LJ_GINF(true, false); else LJ_GINF(false, false);
 #undef LJ_GINF
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ riak_dt_gcounter
+// merge = per-actor max; value = sum (riak_dt, restated in oracle/core.py _GCounter)
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_max16(u64x2* d, const u64x2* a, const u64x2* b,
+                                                  uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        u64x2 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld2<true>(a + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[u] = ld2<true>(b + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            u64x2 m;
+            m.x = x[u].x > y[u].x ? x[u].x : y[u].x;
+            m.y = x[u].y > y[u].y ? x[u].y : y[u].y;
+            st2<true>(d + i + u * stride, m);
+        }
+    }
+    for (; i < n; i += stride) {
+        u64x2 x = ld2<true>(a + i), y = ld2<true>(b + i), m;
+        m.x = x.x > y.x ? x.x : y.x;
+        m.y = x.y > y.y ? x.y : y.y;
+        st2<true>(d + i, m);
+    }
+}
+
+__global__ void k_max_tail(u64* d, const u64* a, const u64* b, uint64_t idx) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) d[idx] = a[idx] > b[idx] ? a[idx] : b[idx];
+}
+
+hipError_t launch_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
+                      uint64_t words) {
+    uint64_t n16 = words / 2;
+    if (n16) {
+        StreamTune t = stream_tune(ctx, n16);
+        hipLaunchKernelGGL(k_max16<2>, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<u64x2*>(dst), reinterpret_cast<const u64x2*>(a),
+                           reinterpret_cast<const u64x2*>(b), n16);
+    }
+    if (words & 1)
+        hipLaunchKernelGGL(k_max_tail, dim3(1), dim3(64), 0, ctx->stream, (u64*)dst,
+                           (const u64*)a, (const u64*)b, words - 1);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce_max(u64* dst, const u64* src, uint64_t groups,
+                                                       uint32_t group, uint64_t wr) {
+    const uint64_t n = groups * wr;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t g = i / wr, w = i - g * wr;
+        uint64_t base = g * group * wr + w;
+        u64 acc = src[base];
+        for (uint32_t j = 1; j < group; ++j) {
+            u64 v = src[base + j * wr];
+            acc = v > acc ? v : acc;
+        }
+        dst[i] = acc;
+    }
+}
+
+hipError_t launch_reduce_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                             uint64_t groups, uint32_t group, uint64_t wr) {
+    StreamTune t = stream_tune(ctx, groups * wr);
+    hipLaunchKernelGGL(k_reduce_max, dim3(t.grid), dim3(kBlock), 0, ctx->stream, (u64*)dst,
+                       (const u64*)src, groups, group, wr);
+    return hipGetLastError();
+}
+
+// per replica: sum of counts (mode 3 partial np/nc or plain sums)
+template <bool SEG>
+__global__ __launch_bounds__(kBlock) void k_gcounter_sums(const u64* c, u64* sums, uint64_t R,
+                                                          uint64_t W, uint32_t nseg) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
+        u64 s = 0;
+        for (uint64_t w = lo + lane; w < hi; w += 64) s += c[rep * W + w];
+        s = wave_sum(s);
+        if (lane == 0) {
+            if constexpr (SEG) atomicAdd(sums + rep, s);
+            else sums[rep] = s;
+        }
+    }
+}
+
+hipError_t launch_gcounter_sums(laspj_ctx* ctx, const laspj_batch* b, uint64_t* sums) {
+    uint32_t ns = nseg_of(b->words_per_replica, kSegW);
+    int grid = seg_grid(ctx, b->replicas * ns);
+    if (ns == 1) {
+        hipLaunchKernelGGL(k_gcounter_sums<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, (u64*)sums, b->replicas, b->words_per_replica, ns);
+    } else {
+        hipError_t e = hipMemsetAsync(sums, 0, b->replicas * 8, ctx->stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_gcounter_sums<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, (u64*)sums, b->replicas, b->words_per_replica, ns);
+    }
+    return hipGetLastError();
+}
+
+__global__ void k_threshold_cmp(const u64* sums, uint8_t* out, uint64_t R, u64 t, bool strict) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = (strict ? t < sums[i] : t <= sums[i]) ? 1 : 0;
+}
+
+hipError_t launch_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* b, uint64_t t,
+                                     bool strict, uint8_t* out) {
+    u64* part = nullptr;
+    hipError_t e = partials(ctx, b->replicas, &part);   // R x 32 B >= R sums
+    if (e != hipSuccess) return e;
+    e = launch_gcounter_sums(ctx, b, reinterpret_cast<uint64_t*>(part));
+    if (e != hipSuccess) return e;
+    uint64_t g = (b->replicas + kBlock - 1) / kBlock;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_threshold_cmp, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part,
+                       out, b->replicas, (u64)t, strict);
+    return hipGetLastError();
+}
+
+// lasp_lattice.erl:169-179: for all actors Count(Prev) =< Count(Cur) (absent = 0);
+// :273-275 strict: value(Prev) < value(Cur) only (the reference's "massive shortcut")
+template <bool STRICT, bool SEG>
+__global__ __launch_bounds__(kBlock) void k_gcounter_inflation(const u64* prev, const u64* cur,
+                                                               uint8_t* out, u64* part,
+                                                               uint64_t R, uint64_t W,
+                                                               bool bcast, uint32_t nseg) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
+        const u64* P = prev + (bcast ? 0 : rep * W);
+        const u64* C = cur + rep * W;
+        bool viol = false;
+        u64 sp = 0, sc = 0;
+        for (uint64_t w = lo + lane; w < hi; w += 64) {
+            u64 p = P[w], c = C[w];
+            viol |= p > c;
+            sp += p;
+            sc += c;
+        }
+        u64 flags = __ballot(viol) != 0 ? kViol : 0;
+        if constexpr (STRICT) {
+            sp = wave_sum(sp);
+            sc = wave_sum(sc);
+        }
+        if (lane == 0) emit(SEG, out, part, rep, flags, sp, sc, STRICT ? 3 : 1);
+    }
+}
+
+hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
+                                     const laspj_batch* cur, bool strict, uint8_t* out) {
+    uint64_t W = cur->words_per_replica;
+    uint32_t ns = nseg_of(W, kSegW);
+    int grid = seg_grid(ctx, cur->replicas * ns);
+    bool bc = prev->replicas == 1 && cur->replicas != 1;
+    u64* part = nullptr;
+    if (ns > 1) {
+        hipError_t e = partials(ctx, cur->replicas, &part);
+        if (e != hipSuccess) return e;
+    }
+#define LJ_GC(ST, SG)                                                                          \
+    hipLaunchKernelGGL((k_gcounter_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
+                       (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas,    \
+                       W, bc, ns)
+    if (ns > 1) {
+        if (strict) LJ_GC(true, true); else LJ_GC(false, true);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return finalize(ctx, part, out, cur->replicas, strict ? 3 : 1);
+    }
+    if (strict) LJ_GC(true, false); else LJ_GC(false, false);
+#undef LJ_GC
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_gcounter_incr(u64* c, uint64_t W,
+                                                          const laspj_incr* incs, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock)
+        atomicAdd(c + incs[i].replica * W + incs[i].actor, (u64)incs[i].amount);
+}
+
+hipError_t launch_gcounter_incr(laspj_ctx* ctx, laspj_batch* b, const laspj_incr* incs,
+                                uint64_t n) {
+    uint64_t g = (n + kBlock - 1) / kBlock;
+    if (g > (uint64_t)ctx->cus * 16) g = (uint64_t)ctx->cus * 16;
+    hipLaunchKernelGGL(k_gcounter_incr, dim3((unsigned)(g ? g : 1)), dim3(kBlock), 0, ctx->stream,
+                       (u64*)b->dev, b->words_per_replica, incs, n);
     return hipGetLastError();
 }
 

@@ -72,6 +72,7 @@ uint64_t words_per(int32_t kind, uint32_t elements, uint32_t er) {
         case LASPJ_KIND_ORSET_CONCAT: return 4ull * elements;
         case LASPJ_KIND_ORSET_PRODUCT: return ((uint64_t)elements * er + 1ull) / 2ull;
         case LASPJ_KIND_GSET_PRODUCT: return (uint64_t)elements * ((er + 63ull) / 64ull);
+        case LASPJ_KIND_GCOUNTER: return elements;
     }
     return 0;
 }
@@ -775,6 +776,112 @@ int laspj_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
     if (int s = check_buf(ctx, index, 4ull * dst->elements, "gset_gather")) return s;
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_gset_gather(ctx, dst, src, static_cast<const uint32_t*>(index->dev)));
+    return LASPJ_OK;
+}
+
+// ------------------------------------------------------------------------- riak_dt_gcounter
+
+int laspj_gcounter_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t actors,
+                                laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_GCOUNTER, replicas, actors, out);
+}
+
+int laspj_gcounter_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                        const laspj_batch* b) {
+    if (int s = check_pair(ctx, a, b, LASPJ_KIND_GCOUNTER, "gcounter_join")) return s;
+    if (int s = check_pair(ctx, dst, a, LASPJ_KIND_GCOUNTER, "gcounter_join")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_max(ctx, dst->dev, a->dev, b->dev, a->replicas * a->words_per_replica));
+    return LASPJ_OK;
+}
+
+int laspj_gcounter_value(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "gcounter_value: bad batch");
+    if (b->kind != LASPJ_KIND_GCOUNTER) return fail(ctx, LASPJ_E_KIND, "gcounter_value: kind");
+    if (int s = check_buf(ctx, out, b->replicas * 8ull, "gcounter_value")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gcounter_sums(ctx, b, static_cast<uint64_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* b, uint64_t threshold,
+                             int strict, laspj_buf* out) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "gcounter_threshold: bad batch");
+    if (b->kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "gcounter_threshold: kind");
+    if (int s = check_buf(ctx, out, b->replicas, "gcounter_threshold")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gcounter_threshold(ctx, b, threshold, strict != 0,
+                                                 static_cast<uint8_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                             int strict, laspj_buf* out) {
+    if (!same_ctx(ctx, prev) || !same_ctx(ctx, cur))
+        return fail(ctx, LASPJ_E_INVAL, "gcounter_inflation: bad batch");
+    if (prev->kind != LASPJ_KIND_GCOUNTER || cur->kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "gcounter_inflation: kind");
+    if (prev->elements != cur->elements ||
+        !(prev->replicas == cur->replicas || prev->replicas == 1))
+        return fail(ctx, LASPJ_E_SHAPE, "gcounter_inflation: prev must have cur's replicas or 1");
+    if (int s = check_buf(ctx, out, cur->replicas, "gcounter_inflation")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gcounter_inflation(ctx, prev, cur, strict != 0,
+                                                 static_cast<uint8_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
+int laspj_gcounter_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                         laspj_buf* out) {
+    return equal_impl(ctx, a, b, out, LASPJ_KIND_GCOUNTER, "gcounter_equal");
+}
+
+int laspj_gcounter_apply_increments(laspj_ctx* ctx, laspj_batch* b, const laspj_incr* incs,
+                                    uint64_t n) {
+    if (!same_ctx(ctx, b) || (!incs && n))
+        return fail(ctx, LASPJ_E_INVAL, "gcounter_apply_increments: bad argument");
+    if (b->kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "gcounter_apply_increments: kind");
+    for (uint64_t i = 0; i < n; ++i)
+        if (incs[i].replica >= b->replicas || incs[i].actor >= b->elements)
+            return fail(ctx, LASPJ_E_RANGE, "gcounter_apply_increments: op %llu out of range",
+                        (unsigned long long)i);
+    if (!n) return LASPJ_OK;
+    Guard g(ctx);
+    uint64_t need = n * sizeof(laspj_incr);
+    if (ctx->scratch_bytes < need) {
+        if (ctx->scratch) {
+            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            hipFree(ctx->scratch);
+            ctx->scratch = nullptr;
+            ctx->scratch_bytes = 0;
+        }
+        if (hipMalloc(&ctx->scratch, need) != hipSuccess) {
+            hipGetLastError();
+            return fail(ctx, LASPJ_E_NOMEM, "gcounter_apply_increments: scratch");
+        }
+        ctx->scratch_bytes = need;
+    }
+    LJ_HIP(ctx, hipMemcpyAsync(ctx->scratch, incs, need, hipMemcpyHostToDevice, ctx->stream));
+    LJ_HIP(ctx, laspj::launch_gcounter_incr(ctx, b, static_cast<const laspj_incr*>(ctx->scratch), n));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_gcounter_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                          uint32_t group) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "gcounter_reduce: bad batch");
+    if (dst->kind != LASPJ_KIND_GCOUNTER || src->kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "gcounter_reduce: kind");
+    if (group == 0 || dst->elements != src->elements ||
+        dst->replicas * (uint64_t)group != src->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "gcounter_reduce: need src replicas = dst x group");
+    if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "gcounter_reduce: aliasing");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_reduce_max(ctx, dst->dev, src->dev, dst->replicas, group,
+                                         src->words_per_replica));
     return LASPJ_OK;
 }
 

@@ -54,6 +54,9 @@ class Context:
     def gset_batch(self, replicas: int, elements: int) -> "GSetBatch":
         return GSetBatch(self, replicas, elements)
 
+    def gcounter_batch(self, replicas: int, actors: int) -> "GCounterBatch":
+        return GCounterBatch(self, replicas, actors)
+
     def buffer(self, nbytes: int) -> "Buffer":
         return Buffer(self, nbytes)
 
@@ -396,4 +399,46 @@ class GSetBatch(_Batch):
         idx.upload(np.ascontiguousarray(index, dtype=np.uint32))
         check(self.ctx.L.laspj_gset_gather(self.ctx.h, self.h, src.h, idx.h), self.ctx.h)
         self.ctx.synchronize()
+        return self
+
+
+class GCounterBatch(_Batch):
+    """R replicas of a riak_dt_gcounter over E actor slots (uint64 count per slot)."""
+
+    kind = _lib.KIND_GCOUNTER
+    _create = "laspj_gcounter_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        return self.download_words(first, count)
+
+    def join(self, a: "GCounterBatch", b: "GCounterBatch"):
+        check(self.ctx.L.laspj_gcounter_join(self.ctx.h, self.h, a.h, b.h), self.ctx.h)
+        return self
+
+    def reduce_from(self, src: "GCounterBatch", group: int):
+        check(self.ctx.L.laspj_gcounter_reduce(self.ctx.h, self.h, src.h, group), self.ctx.h)
+        return self
+
+    def values(self) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas * 8)
+        check(self.ctx.L.laspj_gcounter_value(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64)
+
+    def threshold_met(self, threshold: int, strict: bool = False) -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_gcounter_threshold, self.h, int(threshold),
+                              int(strict))
+
+    def is_inflation_of(self, prev: "GCounterBatch", strict: bool = False) -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_gcounter_inflation, prev.h, self.h, int(strict))
+
+    def equal(self, other: "GCounterBatch") -> np.ndarray:
+        return self._bool_out(self.ctx.L.laspj_gcounter_equal, self.h, other.h)
+
+    def increment(self, incs: Sequence[tuple]):
+        """incs: (replica, actor_slot, amount)."""
+        n = len(incs)
+        arr = (_lib.Incr * max(n, 1))()
+        for k, (rep, actor, amount) in enumerate(incs):
+            arr[k].replica, arr[k].actor, arr[k].amount = rep, actor, amount
+        check(self.ctx.L.laspj_gcounter_apply_increments(self.ctx.h, self.h, arr, n), self.ctx.h)
         return self

@@ -24,7 +24,15 @@ def _pair(type_, prev, cur):
         for e in list(prev) + list(cur):
             dom.element_slot(e)
         return _gset._batch(dom, [prev]), _gset._batch(dom, [cur])
-    raise ValueError(f"type {type_!r} is not on the device path (lasp_orset | lasp_gset)")
+    if type_ == "riak_dt_gcounter":
+        from . import gcounter as _gc
+        dom = Domain()
+        P = _gc._batch(dom, [prev])
+        C = _gc._batch(dom, [cur])
+        if P.elements != C.elements:
+            P = _gc._batch(dom, [prev])
+        return P, C
+    raise ValueError(f"type {type_!r} is not on the device path")
 
 
 def is_inflation(type_, prev, cur) -> bool:
@@ -40,7 +48,14 @@ def is_strict_inflation(type_, prev, cur) -> bool:
 
 
 def threshold_met(type_, value, threshold) -> bool:
-    """threshold_met/3 — lasp_lattice.erl:62-75: {strict, T} -> strict inflation of T."""
+    """threshold_met/3 — lasp_lattice.erl:62-75: {strict, T} -> strict inflation of T;
+    riak_dt_gcounter (:87-90): T =< value(V), strict T < value(V)."""
+    if type_ == "riak_dt_gcounter":
+        from . import gcounter as _gc
+        strict = isinstance(threshold, tuple) and threshold[0] == "strict"
+        t = threshold[1] if strict else threshold
+        b = _gc._batch(Domain(), [value])
+        return bool(b.threshold_met(t, strict)[0])
     if isinstance(threshold, tuple) and len(threshold) == 2 and threshold[0] == "strict":
         return is_strict_inflation(type_, threshold[1], value)
     return is_inflation(type_, threshold, value)

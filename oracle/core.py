@@ -36,11 +36,20 @@ class _GCounter:
 
     @staticmethod
     def update(op, actor, c, tokens=None):
+        # riak_dt_gcounter:update(increment | {increment, N}, Actor, C): orddict
+        # update_counter(Actor, N, C)
         if op == "increment":
+            op = ("increment", 1)
+        if isinstance(op, tuple) and op[0] == "increment" and op[1] > 0:
             found = otp.orddict_find(actor, c)
             n = 0 if found is None else found[1]
-            return ("ok", otp.orddict_store(actor, n + 1, c))
+            return ("ok", otp.orddict_store(actor, n + op[1], c))
         raise ValueError(op)
+
+    @staticmethod
+    def equal(a, b):
+        from .terms import eq
+        return eq(list(a), list(b))
 
     @staticmethod
     def merge(a, b):

@@ -117,3 +117,55 @@ def test_store_values_match_oracle_store():
     ids_o = scen(os_, Atom)
     for i_d, i_o in zip(ids_d, ids_o):
         assert exact_eq(ds.value(i_d), os_.value(i_o)), (i_d, ds.value(i_d), os_.value(i_o))
+
+
+def test_gcounter_lattice_kats_on_device():
+    """lasp_lattice.erl:386-443 riak_dt_gcounter inflation KATs through the device."""
+    from lasp_amd import gcounter as dg
+    from lasp_amd import lattice as dl
+    from lasp_amd.terms import Atom
+    a, b = Atom("a"), Atom("b")
+    a1, b1 = dg.new(), dg.new()
+    a2 = dg.update("increment", a, a1)[1]
+    a3 = dg.update("increment", a, a2)[1]
+    b2 = dg.update("increment", b, b1)[1]
+    t = "riak_dt_gcounter"
+    assert dl.is_inflation(t, a1, b1) and not dl.is_inflation(t, a2, b1)
+    assert dl.is_inflation(t, a1, a2) and dl.is_inflation(t, b1, a2)
+    assert not dl.is_inflation(t, a2, b2)
+    assert not dl.is_strict_inflation(t, a1, b1) and not dl.is_strict_inflation(t, a2, b1)
+    assert dl.is_strict_inflation(t, a1, a2) and dl.is_strict_inflation(t, b1, a2)
+    assert not dl.is_strict_inflation(t, a2, b2) and not dl.is_strict_inflation(t, a2, a2)
+    assert dl.is_strict_inflation(t, a2, a3)
+    assert dg.value(dg.merge(a3, b2)) == 3
+    assert dl.threshold_met(t, a3, 2) and not dl.threshold_met(t, a3, ("strict", 2))
+
+
+def test_adcounter_orset_kat_on_device():
+    """riak_test/lasp_adcounter_orset_test.erl:57-137 on the device store: 5 G-Counter
+    ads in an OR-Set, 100 views, each ad removed once its threshold-5 read fires; the
+    final value is [] and every counter holds exactly 5."""
+    import random
+    from lasp_amd import core as dcore
+    from lasp_amd.terms import Atom
+    st = dcore.Store(capacity=64)
+    _, ads = st.declare("lasp_orset")
+    ad_ids = []
+    for i in range(5):
+        _, ad = st.declare("riak_dt_gcounter", f"ad{i}".encode())
+        st.update(ads, ("add", ad), None)
+        ad_ids.append(ad)
+    removed = set()
+    rng = random.Random(7)
+    for _ in range(100):
+        live = st.type_value(ads)
+        if not live:
+            break
+        ad = live[rng.randrange(len(live))]
+        st.update(ad, "increment", Atom("client"))
+        for x in ad_ids:
+            if x not in removed and st.read(x, 5) is not None:
+                st.update(ads, ("remove", x), x)
+                removed.add(x)
+    assert st.type_value(ads) == []
+    assert [st.type_value(x) for x in ad_ids] == [5] * 5

@@ -424,3 +424,38 @@ def test_segmented_reductions_long_replicas(ctx):
         sub = not np.any(h[i] & ~h2[i])
         same = np.array_equal(h[i], h2[i])
         assert eqg[i] == same and ig[i] == sub and sg[i] == (sub and not same)
+
+
+def test_gcounter_batch_kernels(ctx):
+    """riak_dt_gcounter join (per-actor max), value (sum), threshold, inflation, FSM
+    reduce, increments — against the oracle's _GCounter restatement."""
+    from oracle import core as oc
+    from oracle import lattice as ol
+    rng = np.random.default_rng(3)
+    n, actors = 40, 5000           # > one 4096-word segment per replica
+    a = rng.integers(0, 4, (n, actors)).astype(np.uint64) * (rng.random((n, actors)) < 0.3)
+    b = rng.integers(0, 4, (n, actors)).astype(np.uint64) * (rng.random((n, actors)) < 0.3)
+    b[5] = a[5]
+    b[6] = a[6] + np.uint64(1)
+    A, B, Cc = (ctx.gcounter_batch(n, actors) for _ in range(3))
+    A.upload(a.astype(np.uint64))
+    B.upload(b.astype(np.uint64))
+    Cc.join(A, B)
+    assert np.array_equal(Cc.download(), np.maximum(a, b))
+    assert np.array_equal(A.values(), a.sum(axis=1))
+    t = int(np.median(a.sum(axis=1)))
+    assert list(A.threshold_met(t)) == [t <= int(x) for x in a.sum(axis=1)]
+    assert list(A.threshold_met(t, strict=True)) == [t < int(x) for x in a.sum(axis=1)]
+    od = lambda row: [(k, int(v)) for k, v in enumerate(row) if v]     # noqa: E731
+    infl = B.is_inflation_of(A)
+    strict = B.is_inflation_of(A, strict=True)
+    for i in range(n):
+        assert infl[i] == ol.is_inflation("riak_dt_gcounter", od(a[i]), od(b[i]))
+        assert strict[i] == ol.is_strict_inflation("riak_dt_gcounter", od(a[i]), od(b[i]))
+        assert oc._GCounter.merge(od(a[i]), od(b[i])) == od(np.maximum(a[i], b[i]))
+    assert list(B.equal(A)) == [bool(np.array_equal(a[i], b[i])) for i in range(n)]
+    G = ctx.gcounter_batch(n // 4, actors).reduce_from(A, 4)
+    assert np.array_equal(G.download(), a.reshape(n // 4, 4, actors).max(axis=1))
+    A.increment([(0, 3, 7), (0, 3, 1), (39, 4999, 2)])
+    h = A.download()
+    assert h[0, 3] == a[0, 3] + 8 and h[39, 4999] == a[39, 4999] + 2
