@@ -229,7 +229,8 @@ class Store:
             threshold = ("strict", [])
         if self._threshold_met(v, threshold):
             return ("ok", (id_, v.type, self.value(id_)))
-        v.waiting.append(threshold)
+        if threshold not in v.waiting:       # one pending entry per distinct threshold
+            v.waiting.append(threshold)
         return None
 
     def _threshold_met(self, v: _Var, threshold) -> bool:
