@@ -136,27 +136,38 @@ hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_ba
 
 // ------------------------------------------------------------------ gather (map / fold)
 
+// one block per (replica, 4096-slot segment of the output)
+constexpr uint32_t kGSeg = 4096;
+
 __global__ __launch_bounds__(kB) void k_orset_gather(u64x2* out, const u64x2* src,
                                                      const uint32_t* index, uint64_t reps,
-                                                     uint32_t E_out, uint32_t E_in) {
-    const uint64_t n = reps * E_out;
-    const uint64_t stride = (uint64_t)gridDim.x * kB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += stride) {
-        uint64_t rep = i / E_out;
-        uint32_t o = (uint32_t)(i - rep * E_out);
-        uint32_t s = index[o];
-        u64x2 v = {0, 0};
-        if (s < E_in) v = src[rep * E_in + s];
-        stnt(out + i, v);
+                                                     uint32_t E_out, uint32_t E_in,
+                                                     uint32_t nseg) {
+    for (uint64_t it = blockIdx.x; it < reps * nseg; it += gridDim.x) {
+        uint64_t rep = it / nseg;
+        uint32_t o0 = (uint32_t)(it - rep * nseg) * kGSeg;
+        uint32_t o1 = min(E_out, o0 + kGSeg);
+        const u64x2* s = src + rep * E_in;
+        u64x2* d = out + rep * E_out;
+#pragma unroll 4
+        for (uint32_t o = o0 + threadIdx.x; o < o1; o += kB) {
+            uint32_t si = index[o];
+            u64x2 v = {0, 0};
+            if (si < E_in) v = s[si];
+            stnt(d + o, v);
+        }
     }
 }
 
 hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                const uint32_t* index) {
-    uint64_t n = dst->replicas * dst->elements;
-    hipLaunchKernelGGL(k_orset_gather, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+    uint32_t ns = (dst->elements + kGSeg - 1) / kGSeg;
+    uint64_t items = dst->replicas * ns;
+    uint64_t cap = (uint64_t)ctx->cus * 32;
+    uint64_t g = items < cap ? items : cap;
+    hipLaunchKernelGGL(k_orset_gather, dim3((unsigned)(g ? g : 1)), dim3(kB), 0, ctx->stream,
                        reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(src->dev),
-                       index, dst->replicas, dst->elements, src->elements);
+                       index, dst->replicas, dst->elements, src->elements, ns);
     return hipGetLastError();
 }
 

@@ -122,43 +122,35 @@ hipError_t launch_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uin
 
 // ------------------------------------------------------------------ reduce over groups
 
-// dst replica g = OR_{j<group} src replica (g*group + j); vectorised over word pairs,
-// two destination items per lane per iteration so 2*group loads are in flight
+// dst replica g = OR_{j<group} src replica (g*group + j): one block per (dst replica,
+// 8192-word segment); lanes stride the segment, `group` independent loads per step.
+constexpr uint64_t kRSeg = 8192;
+
 template <bool VEC2>
 __global__ __launch_bounds__(kBlock) void k_reduce_or(u64* dst, const u64* src, uint64_t groups,
-                                                      uint32_t group, uint64_t wr) {
+                                                      uint32_t group, uint64_t wr,
+                                                      uint32_t nseg) {
     const uint64_t per = VEC2 ? wr / 2 : wr;          // items per replica
-    const uint64_t n = groups * per;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if constexpr (VEC2) {
-        const u64x2* s = reinterpret_cast<const u64x2*>(src);
-        u64x2* d = reinterpret_cast<u64x2*>(dst);
-        for (; i + stride < n; i += 2 * stride) {
-            uint64_t i1 = i + stride;
-            uint64_t g0 = i / per, g1 = i1 / per;
-            uint64_t b0 = g0 * group * per + (i - g0 * per), b1 = g1 * group * per + (i1 - g1 * per);
-            u64x2 a0 = ld2<true>(s + b0), a1 = ld2<true>(s + b1);
-            for (uint32_t j = 1; j < group; ++j) {
-                a0 |= ld2<true>(s + b0 + j * per);
-                a1 |= ld2<true>(s + b1 + j * per);
+    for (uint64_t it = blockIdx.x; it < groups * nseg; it += gridDim.x) {
+        uint64_t g = it / nseg;
+        uint64_t lo = (it - g * nseg) * kRSeg, hi = min(per, lo + kRSeg);
+        if constexpr (VEC2) {
+            const u64x2* s = reinterpret_cast<const u64x2*>(src) + g * group * per;
+            u64x2* d = reinterpret_cast<u64x2*>(dst) + g * per;
+#pragma unroll 2
+            for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+                u64x2 acc = ld2<true>(s + i);
+                for (uint32_t j = 1; j < group; ++j) acc |= ld2<true>(s + j * per + i);
+                st2<true>(d + i, acc);
             }
-            st2<true>(d + i, a0);
-            st2<true>(d + i1, a1);
-        }
-        for (; i < n; i += stride) {
-            uint64_t g = i / per, base = g * group * per + (i - g * per);
-            u64x2 acc = ld2<true>(s + base);
-            for (uint32_t j = 1; j < group; ++j) acc |= ld2<true>(s + base + j * per);
-            st2<true>(d + i, acc);
-        }
-    } else {
-        for (; i < n; i += stride) {
-            uint64_t g = i / per, w = i - g * per;
-            uint64_t base = g * group * per + w;
-            u64 acc = src[base];
-            for (uint32_t j = 1; j < group; ++j) acc |= src[base + j * per];
-            dst[i] = acc;
+        } else {
+            const u64* s = src + g * group * per;
+            u64* d = dst + g * per;
+            for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+                u64 acc = s[i];
+                for (uint32_t j = 1; j < group; ++j) acc |= s[j * per + i];
+                d[i] = acc;
+            }
         }
     }
 }
@@ -166,14 +158,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or(u64* dst, const u64* src, 
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t wr) {
     bool vec2 = (wr % 2) == 0;
-    uint64_t n = groups * (vec2 ? wr / 2 : wr);
-    StreamTune t = stream_tune(ctx, n);
+    uint64_t per = vec2 ? wr / 2 : wr;
+    uint32_t ns = (uint32_t)((per + kRSeg - 1) / kRSeg);
+    uint64_t items = groups * ns, cap = (uint64_t)ctx->cus * 32;
+    unsigned g = (unsigned)(items < cap ? (items ? items : 1) : cap);
     if (vec2)
-        hipLaunchKernelGGL((k_reduce_or<true>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
-                           (u64*)dst, (const u64*)src, groups, group, wr);
+        hipLaunchKernelGGL((k_reduce_or<true>), dim3(g), dim3(kBlock), 0, ctx->stream,
+                           (u64*)dst, (const u64*)src, groups, group, wr, ns);
     else
-        hipLaunchKernelGGL((k_reduce_or<false>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
-                           (u64*)dst, (const u64*)src, groups, group, wr);
+        hipLaunchKernelGGL((k_reduce_or<false>), dim3(g), dim3(kBlock), 0, ctx->stream,
+                           (u64*)dst, (const u64*)src, groups, group, wr, ns);
     return hipGetLastError();
 }
 
@@ -278,33 +272,37 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 // ------------------------------------------------------------------ value / removed
 // One wave per 64-element word: lane l tests element 64*w + l, __ballot packs the bits.
 
+// One wave per (replica, 4096-cell segment): it walks the segment's 64 words, 4 words
+// (4 x 1 KiB loads) in flight before each group of __ballot packs; no per-cell division.
+constexpr uint32_t kVSeg = 4096;
+
 template <bool REMOVED>
 __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64* out,
-                                                        uint64_t R, uint32_t E) {
-    // one wave packs 4 consecutive 64-element words per iteration (4 x 1 KiB loads in
-    // flight per wave before the first __ballot)
+                                                        uint64_t R, uint32_t E, uint32_t nseg) {
     constexpr int U = 4;
     const uint32_t W = (E + 63u) / 64u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    const uint64_t total = R * W;
-    for (uint64_t w0 = (((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * U; w0 < total;
-         w0 += nwaves * U) {
-        u64x2 c[U];
-        bool ok[U];
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep = it / nseg;
+        uint32_t e0 = (uint32_t)(it - rep * nseg) * kVSeg;
+        uint32_t e1 = min(E, e0 + kVSeg);
+        const u64x2* c = cells + rep * E;
+        u64* o = out + rep * W;
+        for (uint32_t e = e0; e < e1; e += 64 * U) {
+            u64x2 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint64_t w = w0 + u;
-            uint64_t rep = w / W;
-            uint32_t e = (uint32_t)(w - rep * W) * 64u + lane;
-            ok[u] = w < total && e < E;
-            c[u] = ok[u] ? ld2<true>(cells + rep * E + e) : u64x2{0, 0};
-        }
+            for (int u = 0; u < U; ++u) {
+                uint32_t x = e + u * 64 + lane;
+                v[u] = x < e1 ? ld2<true>(c + x) : u64x2{0, 0};
+            }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            bool pred = ok[u] && (REMOVED ? (c[u].y != 0) : ((c[u].x & ~c[u].y) != 0));
-            u64 m = __ballot(pred);
-            if (lane == 0 && w0 + u < total) out[w0 + u] = m;
+            for (int u = 0; u < U; ++u) {
+                bool pred = REMOVED ? (v[u].y != 0) : ((v[u].x & ~v[u].y) != 0);
+                u64 m = __ballot(pred);
+                if (lane == 0 && e + u * 64 < e1) o[(e + u * 64) >> 6] = m;
+            }
         }
     }
 }
@@ -314,15 +312,17 @@ hipError_t launch_combinator_value(laspj_ctx* ctx, const laspj_batch* b, uint64_
 hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
                               bool removed) {
     if (b->kind != LASPJ_KIND_ORSET) return launch_combinator_value(ctx, b, out);
-    uint64_t words = b->replicas * ((b->elements + 63ull) / 64ull);
-    int grid = wave_grid(ctx, words);
+    uint32_t ns = (b->elements + kVSeg - 1) / kVSeg;
+    uint64_t items = b->replicas * ns;
+    uint64_t blocks = (items + 3) / 4, cap = (uint64_t)ctx->cus * 16;
+    int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
     auto* cells = reinterpret_cast<const u64x2*>(b->dev);
     if (removed)
         hipLaunchKernelGGL(k_orset_value<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements);
+                           cells, (u64*)out, b->replicas, b->elements, ns);
     else
         hipLaunchKernelGGL(k_orset_value<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements);
+                           cells, (u64*)out, b->replicas, b->elements, ns);
     return hipGetLastError();
 }
 
@@ -968,30 +968,38 @@ hipError_t launch_orset_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batc
 }
 
 // filter (lasp_core.erl:681-712): keep cell iff the element's predicate bit is set
+// one block per (replica, 4096-cell segment); lanes stride the segment by 256 cells
 __global__ __launch_bounds__(kBlock) void k_orset_filter(u64x2* d, const u64x2* s,
                                                          const u64* keep, uint64_t R,
-                                                         uint32_t E) {
-    const uint64_t n = R * E;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        uint64_t rep = i / E;
-        uint32_t e = (uint32_t)(i - rep * E);
-        bool k = (keep[e >> 6] >> (e & 63u)) & 1ull;
-        u64x2 v = ld2<true>(s + i);
-        u64x2 z;
-        z.x = 0;
-        z.y = 0;
-        st2<true>(d + i, k ? v : z);
+                                                         uint32_t E, uint32_t nseg) {
+    for (uint64_t it = blockIdx.x; it < R * nseg; it += gridDim.x) {
+        uint64_t rep = it / nseg;
+        uint32_t e0 = (uint32_t)(it - rep * nseg) * kVSeg;
+        uint32_t e1 = min(E, e0 + kVSeg);
+        const u64x2* src = s + rep * E;
+        u64x2* dst = d + rep * E;
+#pragma unroll 4
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+            bool k = (keep[e >> 6] >> (e & 63u)) & 1ull;
+            u64x2 v = ld2<true>(src + e);
+            u64x2 z = {0, 0};
+            st2<true>(dst + e, k ? v : z);
+        }
     }
+}
+
+static int seg_blocks(const laspj_ctx* ctx, uint64_t items) {
+    uint64_t cap = (uint64_t)ctx->cus * 32;
+    return (int)(items < cap ? (items ? items : 1) : cap);
 }
 
 hipError_t launch_orset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                const uint64_t* keep) {
-    uint64_t n = src->replicas * src->elements;
-    StreamTune t = stream_tune(ctx, n);
-    hipLaunchKernelGGL(k_orset_filter, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
-                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(src->dev),
-                       (const u64*)keep, src->replicas, src->elements);
+    uint32_t ns = (src->elements + kVSeg - 1) / kVSeg;
+    hipLaunchKernelGGL(k_orset_filter, dim3(seg_blocks(ctx, src->replicas * ns)), dim3(kBlock), 0,
+                       ctx->stream, reinterpret_cast<u64x2*>(dst->dev),
+                       reinterpret_cast<const u64x2*>(src->dev), (const u64*)keep, src->replicas,
+                       src->elements, ns);
     return hipGetLastError();
 }
 
