@@ -105,12 +105,41 @@ def cpu_baseline(elements: int, budget: float):
     from oracle import columnar as orc    # cpu_baseline leg: the oracle is the timed port
     cores = host_cores()
     eps, merges, secs = orc.bench_orset_merge(elements, 2, cores, 2, budget)
+    m, u, f = orc.bench_config1(10_000, 200)
     return {
         "value": eps, "unit": "merged elements/s", "cores": cores, "kind": "port",
         "sample": (f"C restatement of lasp_orset:merge/2 (nested orddict two-finger merge, "
                    f"20-byte tokens) on {cores} threads x 2 synthetic replica pairs "
                    f"(E={elements}, T<=64), {merges} merges in {secs:.1f} s"),
+        "config1": {"workload": "2 replicas x 10k elements (BASELINE configs[0]), 1 thread",
+                    "us_merge": m, "us_union": u, "us_filter": f},
     }
+
+
+def config1_gpu(ctx):
+    """BASELINE configs[0] on the device: one 10k-slot replica pair; per-call latency of
+    merge, the union body and the filter body (launch + kernel, inputs resident)."""
+    import numpy as np
+    n, iters = 10_000, 200
+    a, b, c = ctx.orset_batch(1, 2 * n), ctx.orset_batch(1, 2 * n), ctx.orset_batch(1, 2 * n)
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    keep = ctx.buffer(((2 * n + 63) // 64) * 8)
+    keep.upload(np.full(((2 * n + 63) // 64,), 0x5555555555555555, np.uint64))
+    L = ctx.L
+    from lasp_amd._lib import check
+    out = {}
+    for name, fn in (("merge", lambda: c.join(a, b)), ("union", lambda: c.union(a, b)),
+                     ("filter", lambda: check(L.laspj_orset_filter(ctx.h, c.h, a.h, keep.h)))):
+        fn()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        ctx.synchronize()
+        out["us_" + name] = (time.perf_counter() - t0) * 1e6 / iters
+    out["workload"] = "1 replica pair x 20k element slots, inputs resident in HBM"
+    return out
 
 
 def load_traffic(path: str, replicas: int, elements: int):
@@ -181,6 +210,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
+    cfg1 = config1_gpu(ctx) if rank == 0 else None
+
     ae = None
     if ae_on:
         del a, b, c                      # free the 192 GiB of join operands first
@@ -226,6 +257,8 @@ def main():
     }
     if ae is not None:
         out["antientropy"] = ae
+    if cfg1 is not None:
+        out["config1_gpu"] = cfg1
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
     print(json.dumps(out), flush=True)

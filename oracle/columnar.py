@@ -55,6 +55,8 @@ def lib():
         L.orc_gset_from_words.restype = C.c_uint32
         L.orc_gset_merge.argtypes = [i64p, C.c_uint32, i64p, C.c_uint32, i64p]
         L.orc_gset_merge.restype = C.c_uint32
+        L.orc_bench_config1.argtypes = [C.c_uint32, C.c_int, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.orc_bench_orset_merge.argtypes = [C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
                                             C.c_double, C.POINTER(C.c_double), u64p,
                                             C.POINTER(C.c_double)]
@@ -172,3 +174,11 @@ def bench_orset_merge(E: int, seed: int, threads: int, pairs: int, budget_s: flo
     if rc != 0:
         raise RuntimeError("orc_bench_orset_merge failed")
     return eps.value, merges.value, secs.value
+
+
+def bench_config1(n: int = 10_000, iters: int = 200):
+    """BASELINE config 1 on the C restatement: (us per merge, union, filter)."""
+    m, u, f = C.c_double(), C.c_double(), C.c_double()
+    if lib().orc_bench_config1(n, iters, C.byref(m), C.byref(u), C.byref(f)) != 0:
+        raise RuntimeError("orc_bench_config1 failed")
+    return m.value, u.value, f.value

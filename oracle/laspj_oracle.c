@@ -33,6 +33,8 @@
 
 typedef uint64_t u64;
 
+static double now_s(void);
+
 /* ------------------------------------------------------------------ synthetic inputs */
 
 static inline u64 sm64(u64 x) {
@@ -326,6 +328,101 @@ int orc_orset_is_strict(const orc_orset* prev, const orc_orset* cur) {
     }
     int new_elems = prev->nelem < cur->nelem;
     return infl && (deleted || new_elems);
+}
+
+/* union body for lasp_orset — lasp_core.erl:616-618: orddict:merge(fun(_, L, _R) -> L)
+ * (keep-left: on a common element the left token list is kept as is) */
+int orc_orset_union(const orc_orset* l, const orc_orset* r, orc_orset* out) {
+    uint32_t i = 0, j = 0;
+    out->nelem = out->ntok = 0;
+    if (out->cap_elem < l->nelem + r->nelem || out->cap_tok < l->ntok + r->ntok) return -1;
+    while (i < l->nelem || j < r->nelem) {
+        const orc_elem* el = i < l->nelem ? &l->elems[i] : NULL;
+        const orc_elem* er = j < r->nelem ? &r->elems[j] : NULL;
+        const orc_elem* src;
+        const orc_orset* from;
+        if (er == NULL || (el && el->key < er->key)) {
+            src = el, from = l, ++i;
+        } else if (el == NULL || el->key > er->key) {
+            src = er, from = r, ++j;
+        } else {
+            src = el, from = l, ++i, ++j;
+        }
+        orc_elem* eo = &out->elems[out->nelem++];
+        eo->key = src->key;
+        eo->off = out->ntok;
+        eo->n = src->n;
+        memcpy(&out->toks[out->ntok], &from->toks[src->off], (size_t)src->n * sizeof(orc_tok));
+        out->ntok += src->n;
+    }
+    return 0;
+}
+
+/* filter body — lasp_core.erl:681-712 with fun(X) -> X rem 2 == 0 end
+ * (lasp_filter_test.erl:70); `Acc ++ [Element]` keeps list order and tombstones */
+int orc_orset_filter_even(const orc_orset* s, orc_orset* out) {
+    out->nelem = out->ntok = 0;
+    if (out->cap_elem < s->nelem || out->cap_tok < s->ntok) return -1;
+    for (uint32_t i = 0; i < s->nelem; ++i) {
+        const orc_elem* el = &s->elems[i];
+        if (el->key % 2 != 0) continue;
+        orc_elem* eo = &out->elems[out->nelem++];
+        eo->key = el->key;
+        eo->off = out->ntok;
+        eo->n = el->n;
+        memcpy(&out->toks[out->ntok], &s->toks[el->off], (size_t)el->n * sizeof(orc_tok));
+        out->ntok += el->n;
+    }
+    return 0;
+}
+
+/* BASELINE config 1: two replicas of 10k integer elements — A adds all
+ * with one token each, B adds all with its own token and removes a 10 % subset; time
+ * merge/2, the union body (against a second 10k set with 5k overlap) and the filter
+ * body, single-threaded, averaged over `iters` calls.  Results in microseconds. */
+int orc_bench_config1(uint32_t n, int iters, double* us_merge, double* us_union,
+                      double* us_filter) {
+    uint32_t E = 2 * n;
+    orc_orset *a = orc_orset_alloc(E, E), *b = orc_orset_alloc(E, E), *c = orc_orset_alloc(E, E);
+    orc_orset *m = orc_orset_alloc(2 * E, 2 * E), *f = orc_orset_alloc(2 * E, 2 * E);
+    if (!a || !b || !c || !m || !f) return -1;
+    u64 s = 0x4C415350ull;
+    for (uint32_t e = 0; e < n; ++e) {
+        orc_elem* ea = &a->elems[a->nelem++];
+        orc_elem* eb = &b->elems[b->nelem++];
+        ea->key = eb->key = e;
+        ea->off = a->ntok;
+        eb->off = b->ntok;
+        ea->n = eb->n = 1;
+        orc_tok* ta = &a->toks[a->ntok++];
+        orc_tok* tb = &b->toks[b->ntok++];
+        for (int k = 0; k < 20; k += 8) {
+            s = sm64(s);
+            memcpy(ta->tok + k, &s, k + 8 <= 20 ? 8 : 20 - k);
+            s = sm64(s);
+            memcpy(tb->tok + k, &s, k + 8 <= 20 ? 8 : 20 - k);
+        }
+        ta->removed = 0;
+        tb->removed = (uint8_t)(sm64(e ^ 1ull) % 10 == 0);
+        /* the union's right operand: elements n/2 .. 3n/2 (5k overlap at n = 10k) */
+        orc_elem* ec = &c->elems[c->nelem++];
+        ec->key = e + n / 2;
+        ec->off = c->ntok;
+        ec->n = 1;
+        c->toks[c->ntok++] = *tb;
+    }
+    double t0 = now_s();
+    for (int i = 0; i < iters; ++i) orc_orset_merge(a, b, m);
+    double t1 = now_s();
+    for (int i = 0; i < iters; ++i) orc_orset_union(m, c, f);
+    double t2 = now_s();
+    for (int i = 0; i < iters; ++i) orc_orset_filter_even(f, m);
+    double t3 = now_s();
+    *us_merge = (t1 - t0) * 1e6 / iters;
+    *us_union = (t2 - t1) * 1e6 / iters;
+    *us_filter = (t3 - t2) * 1e6 / iters;
+    orc_orset_free(a), orc_orset_free(b), orc_orset_free(c), orc_orset_free(m), orc_orset_free(f);
+    return 0;
 }
 
 /* ------------------------------------------------------------------ G-Set (ordsets) */
