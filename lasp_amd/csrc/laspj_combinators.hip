@@ -33,25 +33,43 @@ static int grid_for(const laspj_ctx* ctx, uint64_t items, int per_cu = 64) {
 
 // ------------------------------------------------------------------ intersection
 
-// One lane per 16-byte output half: lanes 2i and 2i+1 write cell i's L and R halves, so
-// every store instruction covers 1 KiB of consecutive bytes; the pair reads the same two
-// input cells (one cache line fetch serves both lanes).
+// A wave takes 64 consecutive cells: one coalesced 1 KiB load each of L and R, then a
+// lane shuffle (ds_bpermute) transposes them so each of the two 1 KiB stores writes
+// consecutive 16-byte halves: lanes 2k / 2k+1 store cell k's L / R half.
 __global__ __launch_bounds__(kB) void k_orset_intersection(u64x2* out, const u64x2* l,
                                                            const u64x2* r, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * kB;
-    for (uint64_t u = (uint64_t)blockIdx.x * kB + threadIdx.x; u < 2 * n; u += stride) {
-        uint64_t i = u >> 1;
-        u64x2 a = ldnt(l + i), b = ldnt(r + i);
-        bool keep = (a.x != 0) & (b.x != 0);   // X in L and lists:keyfind(X, R) found
-        u64x2 z = {0, 0};
-        stnt(out + u, keep ? ((u & 1) ? b : a) : z);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kB / 64);
+    for (uint64_t base = (((uint64_t)blockIdx.x * kB + threadIdx.x) >> 6) * 64; base < n;
+         base += nwaves * 64) {
+        uint64_t i = base + lane;
+        u64x2 a = {0, 0}, b = {0, 0};
+        if (i < n) {
+            a = ldnt(l + i);
+            b = ldnt(r + i);
+        }
+        if (!((a.x != 0) & (b.x != 0))) {      // keep X iff in L and keyfind(X, R) found
+            a = u64x2{0, 0};
+            b = a;
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            int src = half * 32 + (int)(lane >> 1);
+            u64 ax = __shfl(a.x, src, 64), ay = __shfl(a.y, src, 64);
+            u64 bx = __shfl(b.x, src, 64), by = __shfl(b.y, src, 64);
+            u64x2 v;
+            v.x = (lane & 1) ? bx : ax;
+            v.y = (lane & 1) ? by : ay;
+            uint64_t u = 2 * base + half * 64 + lane;
+            if (u < 2 * n) stnt(out + u, v);
+        }
     }
 }
 
 hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                      const laspj_batch* r) {
     uint64_t n = l->replicas * l->elements;
-    hipLaunchKernelGGL(k_orset_intersection, dim3(grid_for(ctx, 2 * n)), dim3(kB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_orset_intersection, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
                        reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
                        reinterpret_cast<const u64x2*>(r->dev), n);
     return hipGetLastError();
