@@ -1,0 +1,112 @@
+"""Randomised parity (hypothesis) of the device combinator bodies and the device
+lasp_core store against the oracle, beyond the fixed golden vectors."""
+
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from oracle import core as ocore
+from oracle import orset as oorset
+from oracle.terms import exact_eq
+
+pytestmark = pytest.mark.gpu
+
+ELEM = st.integers(min_value=-4, max_value=12)
+OP = st.one_of(st.tuples(st.just("add"), ELEM), st.tuples(st.just("remove"), ELEM))
+SET = st.lists(OP, max_size=14)
+
+
+def build(ops, seed):
+    s = oorset.new()
+    toks = oorset.TokenSource(seed)
+    for op in ops:
+        r = oorset.update(op, None, s, toks)
+        if r[0] == "ok":
+            s = r[1]
+    return s
+
+
+SETTINGS = settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+
+
+@SETTINGS
+@given(SET, SET)
+def test_bodies_random(lops, rops):
+    from lasp_amd import orset as do
+    from lasp_amd.codec import Domain, SeqOutput, decode_concat, decode_product
+    l, r = build(lops, 1), build(rops, 2)
+    ctx = do.context()
+    dom = Domain()
+    dom.register_orset(l)
+    dom.register_orset(r)
+    E = max(1, dom.size)
+    L, R = ctx.orset_batch(1, E), ctx.orset_batch(1, E)
+    L.upload(dom.encode_orset([l], E))
+    R.upload(dom.encode_orset([r], E))
+    U = ctx.orset_batch(1, E).union(L, R)
+    assert exact_eq(dom.decode_orset(U.download()[0]), ocore.union_body("lasp_orset", l, r))
+    X = L.intersection(R)
+    assert exact_eq(decode_concat(dom, X.download()[0]), ocore.intersection_body("lasp_orset", l, r))
+    odd = lambda x: x % 2 == 1          # noqa: E731
+    F = ctx.orset_batch(1, E).filter(L, dom.keep_bits(odd, E))
+    assert exact_eq(dom.decode_orset(F.download()[0]), ocore.filter_body("lasp_orset", odd, l))
+    for fun, kind in ((lambda x: -x, "map"), (lambda x: x // 3, "map"),
+                      (lambda x: [x, x + 100], "fold"), (lambda x: [] if x % 2 else [x], "fold")):
+        so = SeqOutput.map(dom, fun) if kind == "map" else SeqOutput.fold(dom, fun)
+        G = ctx.orset_batch(1, max(1, so.size)).gather(L, so.index())
+        want = (ocore.map_body if kind == "map" else ocore.fold_body)("lasp_orset", fun, l)
+        assert exact_eq(so.decode_orset(G.download()[0]), want)
+    # product over per-side dictionaries (token slots < 8 always hold here: <= 14 adds)
+    dl, dr = Domain(), Domain()
+    dl.register_orset(l)
+    dr.register_orset(r)
+    PL, PR = ctx.orset_batch(1, max(1, dl.size)), ctx.orset_batch(1, max(1, dr.size))
+    PL.upload(dl.encode_orset([l], PL.elements))
+    PR.upload(dr.encode_orset([r], PR.elements))
+    if all(len(t) <= 8 for _, t in l) and all(len(t) <= 8 for _, t in r):
+        P = PL.product(PR)
+        assert exact_eq(decode_product(dl, dr, P.download()[0]), ocore.product_body("lasp_orset", l, r))
+
+
+STEP = st.one_of(
+    st.tuples(st.just("update"), st.integers(0, 1), OP),
+    st.tuples(st.just("bind"), st.integers(0, 1), SET))
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(STEP, max_size=10))
+def test_store_random(steps):
+    """Two inputs feeding union / filter / map (monotone) / fold (non-decreasing keys):
+    after every step each variable decodes to the oracle store's value."""
+    from lasp_amd import core as dcore
+    ds, os_ = dcore.Store(capacity=128), ocore.Store(tokens=oorset.TokenSource(9))
+    toks = oorset.TokenSource(5)
+
+    def setup(store):
+        ids = [store.declare("lasp_orset")[1] for _ in range(6)]
+        a, b, u, f, m, fo = ids
+        store.union(a, b, u)
+        store.filter(a, lambda x: x % 2 == 0, f)
+        store.map(b, lambda x: 3 * x, m)
+        store.fold(a, lambda x: [x, x], fo)
+        return ids
+    idd, ido = setup(ds), setup(os_)
+    for step in steps:
+        kind, var = step[0], step[1]
+        if kind == "update":
+            op = step[2]
+            # deterministic tokens: the same token reaches both stores
+            if op[0] == "add":
+                op = ("add_by_token", toks(), op[1])
+            try:
+                os_.update(ido[var], op, None)
+            except RuntimeError:
+                with pytest.raises(RuntimeError):
+                    ds.update(idd[var], op, None)
+                continue
+            ds.update(idd[var], op, None)
+        else:
+            term = build(step[2], 100 + len(steps))
+            os_.bind(ido[var], term)
+            ds.bind(idd[var], term)
+        for i_d, i_o in zip(idd, ido):
+            assert exact_eq(ds.value(i_d), os_.value(i_o)), (step, ds.value(i_d), os_.value(i_o))
