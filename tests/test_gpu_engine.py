@@ -459,3 +459,39 @@ def test_gcounter_batch_kernels(ctx):
     A.increment([(0, 3, 7), (0, 3, 1), (39, 4999, 2)])
     h = A.download()
     assert h[0, 3] == a[0, 3] + 8 and h[39, 4999] == a[39, 4999] + 2
+
+
+def test_abi_error_behaviour(ctx):
+    """Shape / kind / range violations come back as status codes with a message and
+    leave the batches untouched (the NIF turns them into badarg, which bind swallows:
+    lasp_core.erl:308-311); precondition failures come back per op."""
+    from lasp_amd import LaspjError
+    from lasp_amd import _lib
+    L = ctx.L
+    a, b = ctx.orset_batch(4, 64), ctx.orset_batch(4, 65)
+    g = ctx.gset_batch(4, 64)
+    a.fill_synthetic(1)
+    before = a.download()
+    with pytest.raises(LaspjError) as e:
+        a.join(a, b)
+    assert e.value.status == _lib.E_SHAPE and "shapes differ" in str(e.value)
+    assert L.laspj_orset_join(ctx.h, a.h, a.h, g.h) == _lib.E_KIND
+    small = ctx.buffer(3)
+    assert L.laspj_orset_equal(ctx.h, a.h, a.h, small.h) == _lib.E_RANGE
+    assert L.laspj_orset_reduce(ctx.h, a.h, a.h, 2) == _lib.E_SHAPE
+    with pytest.raises(LaspjError) as e:
+        a.apply_ops([(9, 0, _lib.OP_ADD, 0, 1)])                  # replica out of range
+    assert e.value.status == _lib.E_RANGE
+    with pytest.raises(LaspjError):
+        a.apply_ops([(2, 0, _lib.OP_ADD, 0, 1), (1, 0, _lib.OP_ADD, 0, 1)])   # unsorted
+    with pytest.raises(LaspjError):
+        g.apply_ops([(0, 1, _lib.OP_REMOVE, 0, 1)])               # no remove on a G-Set
+    assert np.array_equal(a.download(), before)
+    assert a.upload(before[:2], first=3) is None if False else True
+    with pytest.raises(LaspjError) as e:
+        a.upload(before[:2], first=3)                              # replicas 3..4 of 4
+    assert e.value.status == _lib.E_RANGE
+    # the context stays usable after errors
+    c = ctx.orset_batch(4, 64)
+    c.join(a, a)
+    assert np.array_equal(c.download(), before)
