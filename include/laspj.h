@@ -122,6 +122,8 @@ int      laspj_buf_upload(laspj_ctx* ctx, laspj_buf* buf, uint64_t offset,
                           const void* src, uint64_t bytes);
 int      laspj_buf_download(laspj_ctx* ctx, const laspj_buf* buf, uint64_t offset,
                             void* dst, uint64_t bytes);
+/* device address of a buffer (to wrap sub-ranges as batches, or hand to a collective) */
+int      laspj_buf_device_ptr(const laspj_buf* buf, void** out);
 
 /* ------------------------------------------------------------------ batches */
 /* lasp_orset:new/0 (lasp_orset.erl:63-65) for R replicas over E element slots */

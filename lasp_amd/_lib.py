@@ -72,6 +72,7 @@ SIGNATURES = {
     "laspj_buf_bytes": (u64, [vp]),
     "laspj_buf_upload": (i, [vp, vp, u64, vp, u64]),
     "laspj_buf_download": (i, [vp, vp, u64, vp, u64]),
+    "laspj_buf_device_ptr": (i, [vp, vpp]),
     "laspj_orset_batch_create": (i, [vp, u64, u32, vpp]),
     "laspj_gset_batch_create": (i, [vp, u64, u32, vpp]),
     "laspj_batch_destroy": (i, [vp]),

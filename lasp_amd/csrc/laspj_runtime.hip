@@ -266,6 +266,12 @@ int laspj_buf_destroy(laspj_buf* b) {
 
 uint64_t laspj_buf_bytes(const laspj_buf* b) { return b ? b->bytes : 0; }
 
+int laspj_buf_device_ptr(const laspj_buf* b, void** out) {
+    if (!b || !out) return LASPJ_E_INVAL;
+    *out = b->dev;
+    return LASPJ_OK;
+}
+
 int laspj_buf_upload(laspj_ctx* ctx, laspj_buf* b, uint64_t off, const void* src,
                      uint64_t bytes) {
     if (!ctx || !b || b->ctx != ctx || (!src && bytes))
