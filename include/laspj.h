@@ -60,6 +60,8 @@ extern "C" {
 #define LASPJ_KIND_ORSET_PRODUCT 4  /* product: EL x ER cells of uint32
                                        {pX:8, rX:8, pY:8, rY:8}, cell (x,y) at x*ER+y  */
 #define LASPJ_KIND_GSET_PRODUCT  5  /* product: EL rows x ceil(ER/64) words           */
+#define LASPJ_KIND_ORSET_PRODUCT_WIDE 7  /* product with any token slots: EL x ER cells
+                                            of 32 B {pX, rX, pY, rY}                  */
 #define LASPJ_KIND_GCOUNTER      6  /* riak_dt_gcounter: R x E actor slots, uint64 count
                                        per slot (0 = actor absent from the orddict)   */
 
@@ -216,9 +218,13 @@ int laspj_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch
 /* product body for lasp_orset — lasp_core.erl:499-533 with
  * lasp_lattice:orset_causal_product/2 (:303-308): cell (x, y) holds the 8-bit token
  * masks of x and y (the token set is Tx x Ty, flag = Dx orelse Dy).  Token slots must
- * be < 8 (else LASPJ_E_RANGE, checked on the device).  l has EL slots, r ER slots. */
+ * be < 8 for a PRODUCT dst (else LASPJ_E_RANGE, checked on the device); a
+ * PRODUCT_WIDE dst takes any slots.  l has EL slots, r ER slots. */
 int laspj_orset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
                                      uint32_t er, laspj_batch** out);
+/* the same with 32-byte cells, for inputs that use token slots >= 8 */
+int laspj_orset_product_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                          uint32_t er, laspj_batch** out);
 int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                         const laspj_batch* r);
 /* map / fold bodies — lasp_core.erl:641-667, :460-486: output slot o takes the cell of

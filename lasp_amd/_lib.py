@@ -19,6 +19,7 @@ E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
     -1, -2, -3, -4, -5, -6, -7, -8)
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 KIND_GCOUNTER = 6
+KIND_ORSET_PRODUCT_WIDE = 7
 OP_ADD, OP_REMOVE = 1, 2
 OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK = 0, 1, 2
@@ -98,6 +99,7 @@ SIGNATURES = {
     "laspj_orset_intersection": (i, [vp, vp, vp, vp]),
     "laspj_orset_product_batch_create": (i, [vp, u64, u32, u32, vpp]),
     "laspj_orset_product": (i, [vp, vp, vp, vp]),
+    "laspj_orset_product_wide_batch_create": (i, [vp, u64, u32, u32, vpp]),
     "laspj_orset_gather": (i, [vp, vp, vp, vp]),
     "laspj_gset_union": (i, [vp, vp, vp, vp]),
     "laspj_gset_intersection": (i, [vp, vp, vp, vp]),

@@ -221,18 +221,25 @@ def decode_concat(dom: Domain, cells: np.ndarray) -> list:
 
 
 def decode_product(dl: Domain, dr: Domain, cells: np.ndarray) -> list:
-    """PRODUCT cells (EL, ER) uint32 -> the product body's list, X-major, each with
-    orset_causal_product's fully reversed token order (lasp_lattice.erl:303-308)."""
+    """PRODUCT cells (EL, ER) uint32, or PRODUCT_WIDE cells (EL, ER, 4) uint64 -> the
+    product body's list, X-major, each with orset_causal_product's fully reversed token
+    order (lasp_lattice.erl:303-308)."""
     out = []
+    wide = cells.ndim == 3
     xs = [int(x) for x in dl.elements.order() if x < cells.shape[0]]
     ys = [int(y) for y in dr.elements.order() if y < cells.shape[1]]
     for x in xs:
         row = cells[x]
         for y in ys:
-            c = int(row[y])
-            if not c:
-                continue
-            px, rx, py, ry = c & 0xFF, (c >> 8) & 0xFF, (c >> 16) & 0xFF, (c >> 24) & 0xFF
+            if wide:
+                px, rx, py, ry = (int(v) for v in row[y])
+                if not (px and py):
+                    continue
+            else:
+                c = int(row[y])
+                if not c:
+                    continue
+                px, rx, py, ry = c & 0xFF, (c >> 8) & 0xFF, (c >> 16) & 0xFF, (c >> 24) & 0xFF
             tdx, tdy = dl.tokens[x], dr.tokens[y]
             tx = [(tdx.terms[k], bool((rx >> int(k)) & 1)) for k in tdx.order() if (px >> int(k)) & 1]
             ty = [(tdy.terms[k], bool((ry >> int(k)) & 1)) for k in tdy.order() if (py >> int(k)) & 1]

@@ -96,6 +96,7 @@ class Store:
         out = type(b).__new__(type(b))
         if isinstance(b, engine._ProductBatch):
             engine._ProductBatch.__init__(out, self.ctx, b.replicas, b.elements, b.elements_r)
+            out.kind = b.kind
         else:
             engine._Batch.__init__(out, self.ctx, b.replicas, b.elements)
         _or_into(self.ctx, out, b, b)

@@ -133,8 +133,35 @@ __global__ __launch_bounds__(kB) void k_orset_product(uint32_t* out, const u64x2
     }
 }
 
+// wide form: cell (x, y) = {pX, rX, pY, rY} (32 B) for any token slots; a lane writes
+// one 16-byte half, lanes 2k / 2k+1 = cell k's X / Y half (contiguous 1 KiB stores)
+__global__ __launch_bounds__(kB) void k_orset_product_wide(u64x2* out, const u64x2* L,
+                                                           const u64x2* R, uint64_t reps,
+                                                           uint32_t EL, uint32_t ER) {
+    const uint64_t cells = (uint64_t)EL * ER;
+    const uint64_t n = reps * cells * 2;
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    for (uint64_t u = (uint64_t)blockIdx.x * kB + threadIdx.x; u < n; u += stride) {
+        uint64_t c = u >> 1;
+        uint64_t rep = c / cells, xy = c - rep * cells;
+        uint32_t x = (uint32_t)(xy / ER), y = (uint32_t)(xy - (uint64_t)x * ER);
+        u64x2 a = L[rep * EL + x], b = R[rep * ER + y];
+        u64x2 z = {0, 0};
+        bool keep = (a.x != 0) & (b.x != 0);
+        stnt(out + u, keep ? ((u & 1) ? b : a) : z);
+    }
+}
+
 hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                 const laspj_batch* r, uint32_t* flag) {
+    if (dst->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE) {
+        uint64_t n = l->replicas * (uint64_t)l->elements * r->elements * 2;
+        hipLaunchKernelGGL(k_orset_product_wide, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+                           reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
+                           reinterpret_cast<const u64x2*>(r->dev), l->replicas, l->elements,
+                           r->elements);
+        return hipGetLastError();
+    }
     uint64_t tiles = l->replicas * ((l->elements + kPX - 1) / kPX) *
                      ((r->elements + kPY - 1) / kPY);
     uint64_t g = tiles < (uint64_t)ctx->cus * 32 ? tiles : (uint64_t)ctx->cus * 32;
@@ -330,7 +357,34 @@ __global__ __launch_bounds__(kB) void k_product_value(const uint32_t* cells, u64
     }
 }
 
+// PRODUCT_WIDE: visible iff x and y both hold a live token
+__global__ __launch_bounds__(kB) void k_product_wide_value(const u64x2* cells, u64* out,
+                                                           uint64_t reps, uint64_t C) {
+    const uint64_t W = (C + 63u) / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kB / 64);
+    for (uint64_t w = ((uint64_t)blockIdx.x * kB + threadIdx.x) >> 6; w < reps * W;
+         w += nwaves) {
+        uint64_t rep = w / W;
+        uint64_t c = (w - rep * W) * 64u + lane;
+        bool vis = false;
+        if (c < C) {
+            u64x2 a = ldnt(cells + 2 * (rep * C + c)), b = ldnt(cells + 2 * (rep * C + c) + 1);
+            vis = ((a.x & ~a.y) != 0) && ((b.x & ~b.y) != 0);
+        }
+        u64 m = __ballot(vis);
+        if (lane == 0) out[w] = m;
+    }
+}
+
 hipError_t launch_combinator_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
+    if (b->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE) {
+        uint64_t words = b->replicas * ((b->cells + 63ull) / 64ull);
+        hipLaunchKernelGGL(k_product_wide_value, dim3(grid_for(ctx, words * 64, 8)), dim3(kB), 0,
+                           ctx->stream, reinterpret_cast<const u64x2*>(b->dev), (u64*)out,
+                           b->replicas, b->cells);
+        return hipGetLastError();
+    }
     uint64_t words = b->replicas * ((b->cells + 63ull) / 64ull);
     int grid = grid_for(ctx, words * 64, 8);
     if (b->kind == LASPJ_KIND_ORSET_CONCAT)

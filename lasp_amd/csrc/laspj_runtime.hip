@@ -73,12 +73,14 @@ uint64_t words_per(int32_t kind, uint32_t elements, uint32_t er) {
         case LASPJ_KIND_ORSET_PRODUCT: return ((uint64_t)elements * er + 1ull) / 2ull;
         case LASPJ_KIND_GSET_PRODUCT: return (uint64_t)elements * ((er + 63ull) / 64ull);
         case LASPJ_KIND_GCOUNTER: return elements;
+        case LASPJ_KIND_ORSET_PRODUCT_WIDE: return 4ull * elements * er;
     }
     return 0;
 }
 
 bool is_product(int32_t kind) {
-    return kind == LASPJ_KIND_ORSET_PRODUCT || kind == LASPJ_KIND_GSET_PRODUCT;
+    return kind == LASPJ_KIND_ORSET_PRODUCT || kind == LASPJ_KIND_GSET_PRODUCT ||
+           kind == LASPJ_KIND_ORSET_PRODUCT_WIDE;
 }
 
 int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t elements,
@@ -498,7 +500,8 @@ static int value_impl(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out, bool
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
     bool ok_kind = b->kind == LASPJ_KIND_ORSET ||
                    (!removed && (b->kind == LASPJ_KIND_ORSET_CONCAT ||
-                                 b->kind == LASPJ_KIND_ORSET_PRODUCT));
+                                 b->kind == LASPJ_KIND_ORSET_PRODUCT ||
+                                 b->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE));
     if (!ok_kind) return fail(ctx, LASPJ_E_KIND, "%s: not an OR-Set batch", what);
     uint64_t need = b->replicas * ((b->cells + 63ull) / 64ull) * 8ull;
     if (int s = check_buf(ctx, out, need, what)) return s;
@@ -676,6 +679,11 @@ int laspj_orset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t
     return batch_create(ctx, LASPJ_KIND_ORSET_PRODUCT, replicas, el, out, er);
 }
 
+int laspj_orset_product_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
+                                          uint32_t er, laspj_batch** out) {
+    return batch_create(ctx, LASPJ_KIND_ORSET_PRODUCT_WIDE, replicas, el, out, er);
+}
+
 int laspj_gset_product_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el,
                                     uint32_t er, laspj_batch** out) {
     return batch_create(ctx, LASPJ_KIND_GSET_PRODUCT, replicas, el, out, er);
@@ -699,7 +707,9 @@ static int product_check(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                          const char* what) {
     if (!same_ctx(ctx, dst) || !same_ctx(ctx, l) || !same_ctx(ctx, r))
         return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
-    if (l->kind != in_kind || r->kind != in_kind || dst->kind != out_kind)
+    bool out_ok = dst->kind == out_kind ||
+                  (out_kind == LASPJ_KIND_ORSET_PRODUCT && dst->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE);
+    if (l->kind != in_kind || r->kind != in_kind || !out_ok)
         return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kinds", what);
     if (l->replicas != r->replicas || dst->replicas != l->replicas ||
         dst->elements != l->elements || dst->elements_r != r->elements)
@@ -713,6 +723,10 @@ int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                               "orset_product"))
         return s;
     Guard g(ctx);
+    if (dst->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE) {
+        LJ_HIP(ctx, laspj::launch_orset_product(ctx, dst, l, r, ctx->flag));
+        return LASPJ_OK;
+    }
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
     LJ_HIP(ctx, laspj::launch_orset_product(ctx, dst, l, r, ctx->flag));
     uint32_t flag = 0;

@@ -250,10 +250,18 @@ class ORSetBatch(_Batch):
         check(self.ctx.L.laspj_orset_intersection(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
         return out
 
-    # product body (lasp_core.erl:499-533): returns a PRODUCT batch (EL x ER cells)
-    def product(self, r: "ORSetBatch", out: Optional["ORSetProductBatch"] = None):
-        if out is None:
+    # product body (lasp_core.erl:499-533): returns a PRODUCT batch (EL x ER cells):
+    # 4-byte cells when every token slot is < 8 (detected on the device), else 32-byte
+    def product(self, r: "ORSetBatch", out=None, wide: Optional[bool] = None):
+        if out is None and not wide:
             out = ORSetProductBatch(self.ctx, self.replicas, self.elements, r.elements)
+        if out is not None:
+            st = self.ctx.L.laspj_orset_product(self.ctx.h, out.h, self.h, r.h)
+            if st == _lib.OK:
+                return out
+            if st != _lib.E_RANGE or wide is False or not isinstance(out, ORSetProductBatch):
+                check(st, self.ctx.h)
+        out = ORSetProductWideBatch(self.ctx, self.replicas, self.elements, r.elements)
         check(self.ctx.L.laspj_orset_product(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
         return out
 
@@ -324,6 +332,23 @@ class ORSetProductBatch(_ProductBatch):
         w = self.download_words(first, count)
         return w.view(np.uint32)[:, : self.cells].reshape(w.shape[0], self.elements,
                                                            self.elements_r)
+
+    def value_bits(self) -> np.ndarray:
+        W = (self.cells + 63) // 64
+        buf = self.ctx.buffer(self.replicas * W * 8)
+        check(self.ctx.L.laspj_orset_value(self.ctx.h, self.h, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, W)
+
+
+class ORSetProductWideBatch(_ProductBatch):
+    """Product output for any token slots: EL x ER cells of {pX, rX, pY, rY} u64."""
+
+    kind = _lib.KIND_ORSET_PRODUCT_WIDE
+    _create = "laspj_orset_product_wide_batch_create"
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        w = self.download_words(first, count)
+        return w.reshape(w.shape[0], self.elements, self.elements_r, 4)
 
     def value_bits(self) -> np.ndarray:
         W = (self.cells + 63) // 64

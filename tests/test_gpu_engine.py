@@ -495,3 +495,39 @@ def test_abi_error_behaviour(ctx):
     c = ctx.orset_batch(4, 64)
     c.join(a, a)
     assert np.array_equal(c.download(), before)
+
+
+def test_orset_product_wide_any_token_slots(ctx, tokens):
+    """Elements with token slots >= 8 take the 32-byte product form automatically; the
+    decoded list equals the oracle's product body (descending [Tx, Ty] pairs)."""
+    from oracle import core
+    from lasp_amd.codec import Domain, decode_product
+    toks = [bytes([k]) * 20 for k in range(64)]
+    l = [(1, [(toks[k], k % 3 == 0) for k in (0, 9, 40)]), (2, [(toks[5], False)])]
+    r = [(7, [(toks[k], False) for k in (2, 63)]), (8, [(toks[11], True)])]
+    dl, dr = Domain(), Domain()
+    dl.register_orset(l)
+    dr.register_orset(r)
+    L, Rb = ctx.orset_batch(1, 2), ctx.orset_batch(1, 2)
+    L.upload(dl.encode_orset([l], 2))
+    Rb.upload(dr.encode_orset([r], 2))
+    P = L.product(Rb)
+    assert type(P).__name__ == "ORSetProductBatch"          # slots here are < 8
+    got = decode_product(dl, dr, P.download()[0])
+    assert got == core.product_body("lasp_orset", l, r)
+    # now slots beyond 8: cells spread over 64 token slots
+    h = np.zeros((1, 2, 2), np.uint64)
+    h[0, 0, 0] = np.uint64((1 << 9) | (1 << 40) | 1)
+    h[0, 0, 1] = np.uint64(1)
+    h[0, 1, 0] = np.uint64(1 << 63)
+    L.upload(h)
+    P = L.product(Rb)
+    assert type(P).__name__ == "ORSetProductWideBatch"
+    cells = P.download()[0]
+    rr = Rb.download()[0]
+    for x in range(2):
+        for y in range(2):
+            assert list(cells[x, y]) == [int(h[0, x, 0]), int(h[0, x, 1]), int(rr[y, 0]), int(rr[y, 1])]
+    vis = P.value_bits()[0]
+    # visible: x live in both rows; y = 0 live, y = 1 all tombstoned -> cells 0 and 2
+    assert int(vis[0]) & 0xF == 0b0101
