@@ -339,8 +339,9 @@ def test_orset_product_rejects_wide_token_slots(ctx):
     L.upload(h)
     Rb.upload(h)
     with pytest.raises(LaspjError) as ei:
-        L.product(Rb)
+        L.product(Rb, wide=False)              # 4-byte cells requested explicitly
     assert ei.value.status == E_RANGE
+    assert type(L.product(Rb)).__name__ == "ORSetProductWideBatch"   # automatic choice
 
 
 def test_orset_intersection_concat(ctx):
