@@ -87,6 +87,9 @@ typedef struct laspj_batch_info {
 #define LASPJ_OP_ADD     1  /* add / add_by_token: token slot `slot` of `element` := false */
 #define LASPJ_OP_REMOVE  2  /* remove: every token of `element` := true, or
                                {error,{precondition,{not_present,E}}} if absent       */
+#define LASPJ_OP_INSERT  3  /* lasp_orset_gbtree add (lasp_orset_gbtree.erl:232-240): like ADD,
+                               but gb_trees:insert of a token already present raises
+                               {key_exists, Token}: status KEY_EXISTS, call not applied */
 #define LASPJ_OP_FLAG_NEW_CALL 1  /* this op starts a new update/3 call; ops of one call
                                      are all-or-nothing ({update, Ops}, remove_all)   */
 typedef struct laspj_op {
@@ -101,6 +104,7 @@ typedef struct laspj_op {
 #define LASPJ_OPST_APPLIED   0
 #define LASPJ_OPST_NOT_PRESENT 1   /* this op's precondition failed; call rolled back */
 #define LASPJ_OPST_ROLLED_BACK 2   /* another op of the same call failed              */
+#define LASPJ_OPST_KEY_EXISTS  3   /* INSERT of a present token; call not applied      */
 
 /* ------------------------------------------------------------------ library / context */
 int         laspj_abi_version(void);

@@ -20,9 +20,9 @@ E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 KIND_GCOUNTER = 6
 KIND_ORSET_PRODUCT_WIDE = 7
-OP_ADD, OP_REMOVE = 1, 2
+OP_ADD, OP_REMOVE, OP_INSERT = 1, 2, 3
 OP_FLAG_NEW_CALL = 1
-OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK = 0, 1, 2
+OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK, OPST_KEY_EXISTS = 0, 1, 2, 3
 TUNE_STREAM_GRID, TUNE_STREAM_UNROLL, TUNE_STREAM_NT = 1, 2, 3
 
 

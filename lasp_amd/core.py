@@ -70,7 +70,7 @@ class Store:
 
     # ---------------------------------------------------------------- helpers
     def _new_batch(self, type_):
-        if type_ == "lasp_orset":
+        if type_ in ("lasp_orset", "lasp_orset_gbtree"):
             return self.ctx.orset_batch(1, self.cap)
         if type_ == "lasp_gset":
             return self.ctx.gset_batch(1, self.cap)
@@ -80,7 +80,10 @@ class Store:
 
     def _encode(self, type_, term):
         b = self._new_batch(type_)
-        if type_ == "lasp_orset":
+        if type_ == "lasp_orset_gbtree":
+            from .orset_gbtree import to_orddict
+            b.upload(self.odom.encode_orset([to_orddict(term)], self.cap))
+        elif type_ == "lasp_orset":
             b.upload(self.odom.encode_orset([term], self.cap))
         elif type_ == "lasp_gset":
             b.upload(self.gdom.encode_gset([term], self.cap))
@@ -207,10 +210,18 @@ class Store:
         if v.type == "riak_dt_gcounter":
             n = 1 if op == "increment" else op[1]
             cur.increment([(0, self.cdom.element_slot(actor), n)])
-        elif v.type == "lasp_orset":
+        elif v.type in ("lasp_orset", "lasp_orset_gbtree"):
             ops = []
-            _o._compile(op, self.odom, ops, new_call=True)
+            if v.type == "lasp_orset":
+                _o._compile(op, self.odom, ops, new_call=True)
+            else:
+                from . import orset_gbtree as _og
+                _og._compile(op, self.odom, ops, new_call=True)
             st = cur.apply_ops(ops)
+            if (st == _lib.OPST_KEY_EXISTS).any():
+                j = int(np.nonzero(st == _lib.OPST_KEY_EXISTS)[0][0])
+                from .orset_gbtree import KeyExists
+                raise KeyExists(self.odom.tokens[ops[j][1]].terms[ops[j][3]])
             if (st == _lib.OPST_NOT_PRESENT).any():
                 bad = ops[int(np.nonzero(st == _lib.OPST_NOT_PRESENT)[0][0])][1]
                 raise RuntimeError(f"badmatch: {{error,{{precondition,{{not_present,"
@@ -224,10 +235,11 @@ class Store:
     def read(self, id_, threshold=("strict", None)):
         """read/6 — lasp_core.erl:331-364 (non-blocking: None and a recorded waiter)."""
         v = self.vars[id_]
+        bottom = _type_new(v.type)
         if threshold is None:
-            threshold = []                                # Type:new()
+            threshold = bottom                            # Type:new()
         elif isinstance(threshold, tuple) and threshold[0] == "strict" and threshold[1] is None:
-            threshold = ("strict", [])
+            threshold = ("strict", bottom)
         if self._threshold_met(v, threshold):
             return ("ok", (id_, v.type, self.value(id_)))
         if threshold not in v.waiting:       # one pending entry per distinct threshold
@@ -260,6 +272,9 @@ class Store:
             return [(self.cdom.elements.terms[int(a)], int(cells[int(a)]))
                     for a in self.cdom.elements.order() if int(cells[int(a)])]
         if v.rep == "canonical":
+            if v.type == "lasp_orset_gbtree":
+                from .orset_gbtree import from_orddict
+                return from_orddict(self.odom.decode_orset(cells))
             return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
                 self.gdom.decode_gset(cells)
         if v.rep == "concat":
@@ -290,6 +305,12 @@ class Store:
 
     # ---------------------------------------------------------------- processes
     def _start(self, inputs, body):
+        for i in inputs:
+            if self.vars[i].type == "lasp_orset_gbtree":
+                # lasp_core's combinator bodies match the orddict shape and the
+                # lasp_orset / lasp_gset atoms only (lasp_core.erl:460-712): a gbtree
+                # input crashes the process in the reference
+                raise Unsupported("combinators take lasp_orset / lasp_gset inputs")
         proc = {"inputs": list(inputs), "seen": {i: None for i in inputs}, "body": body}
         self.procs.append(proc)
         self._propagate()
@@ -386,6 +407,14 @@ class Store:
             res = self._batch_like(t, so.size).gather(seen[i], so.index())
             self._bind_out(out, _DeviceValue("seq", res, so))
         return self._start([i], body)
+
+
+def _type_new(type_):
+    """Type:new() (lasp_core.erl:339-346 substitutes it for an undefined threshold)."""
+    if type_ == "lasp_orset_gbtree":
+        from .gbtrees import empty
+        return empty()
+    return []
 
 
 class _DeviceValue:

@@ -901,25 +901,37 @@ __global__ __launch_bounds__(kBlock) void k_apply_ops(u64* state, uint64_t wr, i
         uint64_t c1 = c0 + 1;
         while (c1 < end && !(ops[c1].flags & LASPJ_OP_FLAG_NEW_CALL)) ++c1;
         uint64_t bad = ~0ull;
+        int32_t why = LASPJ_OPST_NOT_PRESENT;
         if (kind == LASPJ_KIND_ORSET) {
             for (uint64_t k = c0; k < c1 && bad == ~0ull; ++k) {
-                if (ops[k].kind != LASPJ_OP_REMOVE) continue;
-                uint32_t e = ops[k].element;
-                bool present = s[2ull * e] != 0;
-                for (uint64_t j = c0; j < k && !present; ++j)
-                    present = ops[j].kind == LASPJ_OP_ADD && ops[j].element == e;
-                if (!present) bad = k;
+                const uint32_t e = ops[k].element;
+                if (ops[k].kind == LASPJ_OP_REMOVE) {
+                    bool present = s[2ull * e] != 0;
+                    for (uint64_t j = c0; j < k && !present; ++j)
+                        present = ops[j].kind != LASPJ_OP_REMOVE && ops[j].element == e;
+                    if (!present) bad = k;
+                } else if (ops[k].kind == LASPJ_OP_INSERT) {
+                    const uint8_t t = ops[k].slot;
+                    bool exists = (s[2ull * e] >> t) & 1ull;
+                    for (uint64_t j = c0; j < k && !exists; ++j)
+                        exists = ops[j].kind != LASPJ_OP_REMOVE && ops[j].element == e &&
+                                 ops[j].slot == t;
+                    if (exists) {
+                        bad = k;
+                        why = LASPJ_OPST_KEY_EXISTS;
+                    }
+                }
             }
         }
         if (bad != ~0ull) {
             for (uint64_t k = c0; k < c1; ++k)
-                status[k] = k == bad ? LASPJ_OPST_NOT_PRESENT : LASPJ_OPST_ROLLED_BACK;
+                status[k] = k == bad ? why : LASPJ_OPST_ROLLED_BACK;
         } else {
             for (uint64_t k = c0; k < c1; ++k) {
                 const laspj_op& o = ops[k];
                 if (kind == LASPJ_KIND_ORSET) {
                     u64* cell = s + 2ull * o.element;
-                    if (o.kind == LASPJ_OP_ADD) {
+                    if (o.kind != LASPJ_OP_REMOVE) {
                         // orddict:store(Token, false, Tokens) — present, flag false
                         cell[0] |= 1ull << o.slot;
                         cell[1] &= ~(1ull << o.slot);

@@ -603,7 +603,8 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
         if (o.slot >= 64) return fail(ctx, LASPJ_E_RANGE, "%s: op %llu token slot >= 64", what,
                                       (unsigned long long)i);
         bool ok_kind = kind == LASPJ_KIND_ORSET
-                           ? (o.kind == LASPJ_OP_ADD || o.kind == LASPJ_OP_REMOVE)
+                           ? (o.kind == LASPJ_OP_ADD || o.kind == LASPJ_OP_REMOVE ||
+                              o.kind == LASPJ_OP_INSERT)
                            : o.kind == LASPJ_OP_ADD;
         if (!ok_kind) return fail(ctx, LASPJ_E_INVAL, "%s: op %llu has kind %u", what,
                                   (unsigned long long)i, o.kind);

@@ -1,6 +1,11 @@
 """lasp_lattice mirror: threshold_met / is_inflation / is_strict_inflation for the
-lasp_orset and lasp_gset clauses (src/lasp_lattice.erl:62-75, 137-161, 212-253),
-computed by the wave64 ballot kernels on the device."""
+lasp_orset, lasp_orset_gbtree and lasp_gset clauses (src/lasp_lattice.erl:62-75,
+137-161, 212-253, 287-295), computed by the wave64 ballot kernels on the device.
+
+The lasp_orset_gbtree clauses run the lasp_orset kernels on the same cells: inflation
+is the same containment test; strict inflation has no `Prev == []` clause
+(:217-233), but there an empty Prev makes `NewElements` (size 0 < size Cur) carry the
+same answer, so the kernel's special case is immaterial."""
 
 from __future__ import annotations
 
@@ -12,6 +17,9 @@ from . import gset as _gset
 def _pair(type_, prev, cur):
     dom = Domain()
     ctx = context()
+    if type_ == "lasp_orset_gbtree":
+        from .orset_gbtree import to_orddict
+        prev, cur, type_ = to_orddict(prev), to_orddict(cur), "lasp_orset"
     if type_ == "lasp_orset":
         dom.register_orset(prev)
         dom.register_orset(cur)

@@ -1,0 +1,220 @@
+"""lasp_orset_gbtree mirror over the MI355X engine (src/lasp_orset_gbtree.erl).
+
+`lasp_orset_gbtree` is Lasp's default set for internal state (`?SET`,
+include/lasp.hrl:30): the same observed-remove set as lasp_orset with the two
+orddict levels replaced by gb_trees (Elem -> gb_tree Token -> Removed).  Its contents
+map onto the same columnar cells ({p, r} per element slot), so every call runs on the
+same HIP kernels as lasp_orset; only the host-side term walk differs:
+
+* operands are walked in order (gb_trees:to_list/1) into the shared Domain;
+* results are built as the trees OTP builds for them — `gb_trees_ext:merge/3`
+  inserts keys in ascending order into `empty()` at both levels, and so does
+  remove_elem's rebuild, which `lasp_amd.gbtrees.build_sorted` reproduces.
+
+Semantics kept from the reference:
+* add / add_by_token insert the token with gb_trees:insert/3 (:232-240): a token that
+  is already present raises {key_exists, Token} (`KeyExists`), detected on the device
+  (LASPJ_OP_INSERT / LASPJ_OPST_KEY_EXISTS) with the call left unapplied;
+* remove of an absent element -> {error, {precondition, {not_present, E}}};
+* value/1 and value(removed) are in-order folds (:67-76, :93-101).
+Divergence: equal/2 is gb_trees_ext:equal, which also compares the
+SHAPE of inner token trees; the device compares contents.  The two agree whenever both
+trees were built the way merge builds them (every value a lasp_core store holds).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib, gbtrees as gbt
+from .codec import Domain
+from .orset import _batch, _waste_pct, context
+from .terms import Atom
+
+
+class KeyExists(Exception):
+    """erlang:error({key_exists, Token}) raised by gb_trees:insert/3 in add_elem."""
+
+    def __init__(self, token):
+        super().__init__(("key_exists", token))
+        self.token = token
+
+
+def to_orddict(s) -> list:
+    """Both levels walked in order: the orddict-shaped contents of the set."""
+    out = []
+    for elem, toks in gbt.walk(s):
+        pairs = gbt.walk(toks)
+        for _t, rm in pairs:
+            if not isinstance(rm, bool):
+                raise ValueError(f"badarg: token flag {rm!r}")
+        out.append((elem, pairs))
+    return out
+
+
+def from_orddict(od) -> tuple:
+    """The tree gb_trees_ext:merge builds for these contents."""
+    return gbt.build_sorted([(e, gbt.build_sorted(toks)) for e, toks in od])
+
+
+# --------------------------------------------------------------------------- API
+
+def new():
+    """new/0 — src/lasp_orset_gbtree.erl:63-65."""
+    return gbt.empty()
+
+
+def merge(a, b):
+    """merge/2 — :134-140 (device join)."""
+    return merge_many([(a, b)])[0]
+
+
+def merge_many(pairs: Sequence[Tuple[tuple, tuple]]) -> List[tuple]:
+    """merge/2 over many independent pairs in one launch."""
+    if not pairs:
+        return []
+    dom = Domain()
+    ods = [(to_orddict(a), to_orddict(b)) for a, b in pairs]
+    A, E = _batch(dom, [p[0] for p in ods])
+    B, _ = _batch(dom, [p[1] for p in ods])
+    if B.elements != E:
+        A, E = _batch(dom, [p[0] for p in ods])
+    C = context().orset_batch(len(pairs), E)
+    C.join(A, B)
+    out = C.download()
+    return [from_orddict(dom.decode_orset(out[i])) for i in range(len(pairs))]
+
+
+def value(s):
+    """value/1 — :67-76 (device value bitmap, in-order)."""
+    dom = Domain()
+    b, _ = _batch(dom, [to_orddict(s)])
+    return dom.decode_value_bits(b.value_bits()[0])
+
+
+def value2(query, s):
+    """value/2 — :78-104.  `{tokens, E}` is E's token tree (or empty()); since that is
+    never the list `[]`, `{fragment, E}` is always the one-entry tree {E, Tokens}."""
+    if isinstance(query, tuple) and len(query) == 2 and query[0] == "fragment":
+        toks = value2(("tokens", query[1]), s)
+        return gbt.build_sorted([(query[1], toks)])
+    if isinstance(query, tuple) and len(query) == 2 and query[0] == "tokens":
+        dom = Domain()
+        b, _ = _batch(dom, [to_orddict(s)])
+        es = dom.element_slot(query[1], create=False)
+        if es < 0:
+            return gbt.empty()
+        for elem, toks in dom.decode_orset(b.download()[0]):
+            if dom.element_slot(elem, create=False) == es:
+                return gbt.build_sorted(toks)
+        return gbt.empty()
+    if query == "removed":
+        dom = Domain()
+        b, _ = _batch(dom, [to_orddict(s)])
+        return dom.decode_value_bits(b.value_bits(removed=True)[0])
+    return value(s)
+
+
+def _unique(_actor) -> bytes:
+    """unique/1 — :276-277: 20 random bytes."""
+    return os.urandom(20)
+
+
+def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
+    kind = op[0]
+    flag = _lib.OP_FLAG_NEW_CALL if new_call else 0
+    if kind in ("add", "add_by_token"):
+        elem = op[1] if kind == "add" else op[2]
+        tok = _unique(None) if kind == "add" else op[1]
+        es = dom.element_slot(elem)
+        ops.append((0, es, _lib.OP_INSERT, dom.token_slot(es, tok), flag))
+    elif kind == "add_all":
+        # foldl of `{ok, _} = update({add, E})` (:112-117): one call, fresh tokens
+        for k, e in enumerate(op[1]):
+            es = dom.element_slot(e)
+            ops.append((0, es, _lib.OP_INSERT, dom.token_slot(es, _unique(None)),
+                        flag if k == 0 else 0))
+    elif kind == "remove":
+        ops.append((0, dom.element_slot(op[1]), _lib.OP_REMOVE, 0, flag))
+    elif kind == "remove_all":
+        for k, e in enumerate(op[1]):           # remove_elems/2 (:255-263)
+            ops.append((0, dom.element_slot(e), _lib.OP_REMOVE, 0, flag if k == 0 else 0))
+    elif kind == "update":
+        first = len(ops)                        # apply_ops/3 (:266-274)
+        for sub in op[1]:
+            _compile(sub, dom, ops, new_call=False)
+        for j in range(first, len(ops)):
+            r, e, k, sl, _f = ops[j]
+            ops[j] = (r, e, k, sl, flag if j == first else 0)
+    else:
+        raise ValueError(f"function_clause: {op!r}")
+
+
+def update(op, actor, s):
+    """update/3 — :106-124.  ("ok", S1) | ("error", ("precondition", ("not_present",
+    E))); raises KeyExists where the reference's gb_trees:insert/3 crashes."""
+    od = to_orddict(s)
+    dom = Domain()
+    dom.register_orset(od)
+    ops = []
+    _compile(op, dom, ops, new_call=True)
+    E = max(1, dom.size)
+    b = context().orset_batch(1, E)
+    b.upload(dom.encode_orset([od], E))
+    st = b.apply_ops(ops)
+    bad = np.nonzero((st == _lib.OPST_NOT_PRESENT) | (st == _lib.OPST_KEY_EXISTS))[0]
+    if len(bad):
+        r, es, _k, slot, _f = ops[int(bad[0])]
+        if st[bad[0]] == _lib.OPST_KEY_EXISTS:
+            raise KeyExists(dom.tokens[es].terms[slot])
+        return ("error", ("precondition", ("not_present", dom.elements.terms[es])))
+    return ("ok", from_orddict(dom.decode_orset(b.download()[0])))
+
+
+def update4(op, actor, s, _ctx=None):
+    """update/4 — :126-128 (context ignored)."""
+    return update(op, actor, s)
+
+
+def equal(a, b) -> bool:
+    """equal/2 — :142-144, on contents (see the module note on shapes)."""
+    dom = Domain()
+    oa, ob = to_orddict(a), to_orddict(b)
+    dom.register_orset(oa)
+    dom.register_orset(ob)
+    E = max(1, dom.size)
+    A = context().orset_batch(1, E)
+    B = context().orset_batch(1, E)
+    A.upload(dom.encode_orset([oa], E))
+    B.upload(dom.encode_orset([ob], E))
+    return bool(A.equal(B)[0])
+
+
+def stats(s):
+    """stats/1 — :164-169 (element_count = gb_trees:size = elements with a token)."""
+    dom = Domain()
+    b, _ = _batch(dom, [to_orddict(s)])
+    elems, adds, rems = (int(x) for x in b.stats()[0])
+    return [("element_count", elems), ("adds_count", adds), ("removes_count", rems),
+            ("waste_pct", _waste_pct(adds, rems))]
+
+
+def stat(name, s):
+    """stat/2 — :171-200 (unknown stat -> undefined)."""
+    for k, v in stats(s):
+        if k == name:
+            return v
+    return Atom("undefined")
+
+
+def parent_clock(_clock, s):
+    """parent_clock/2 — :130-132."""
+    return s
+
+
+def to_version(_version, s):
+    """to_version/2 — :226-228."""
+    return s

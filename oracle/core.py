@@ -14,7 +14,7 @@ and re-runs its body.
 
 from __future__ import annotations
 
-from . import otp, orset, gset, lattice
+from . import otp, orset, orset_gbtree, gset, lattice
 from .terms import exact_eq
 
 # ----------------------------------------------------------------------------- types
@@ -76,7 +76,18 @@ class _GSet:
         return gset.update(op, actor, s)
 
 
+class _ORSetGBTree:
+    new = staticmethod(orset_gbtree.new)
+    value = staticmethod(orset_gbtree.value)
+    merge = staticmethod(orset_gbtree.merge)
+
+    @staticmethod
+    def update(op, actor, s, tokens=None):
+        return orset_gbtree.update(op, actor, s, tokens)
+
+
 _TYPES["lasp_orset"] = _ORSet
+_TYPES["lasp_orset_gbtree"] = _ORSetGBTree
 _TYPES["lasp_gset"] = _GSet
 _TYPES["riak_dt_gcounter"] = _GCounter
 

@@ -1,11 +1,11 @@
-"""lasp_lattice restatement (orset / gset / gcounter clauses) — oracle (TEST INFRASTRUCTURE).
+"""lasp_lattice restatement (orset / orset_gbtree / gset / gcounter clauses) — oracle (TEST INFRASTRUCTURE).
 
 Follows src/lasp_lattice.erl.  `prev` / `cur` are full lattice states (not values).
 """
 
 from __future__ import annotations
 
-from . import otp, gset as _gset
+from . import gbtrees as gb, otp, gset as _gset
 
 
 def threshold_met(type_, value, threshold) -> bool:
@@ -36,6 +36,18 @@ def is_inflation(type_, prev, cur) -> bool:
             else:
                 acc = acc and _ids_inflated(ids, found[1])
         return acc
+    if type_ == "lasp_orset_gbtree":
+        # :142-150 — in-order fold over Prev; gb_trees:lookup (==) in Cur; ids
+        # inflated per ids_inflated(lasp_orset_gbtree, ...) :287-295
+        acc = True
+        for elem, ids in gb.to_list(prev):
+            found = gb.lookup(elem, cur)
+            if found is None:
+                acc = acc and False
+            else:
+                acc = acc and all(gb.lookup(t, found[1]) is not None
+                                  for t, _ in gb.to_list(ids))
+        return acc
     if type_ == "riak_dt_gcounter":
         # :169-179
         acc = True
@@ -61,6 +73,16 @@ def is_strict_inflation(type_, prev, cur) -> bool:
         # :212-215
         return is_inflation(type_, prev, cur) and not _term_eq(
             otp.lists_usort(_gset.value(prev)), otp.lists_usort(_gset.value(cur)))
+    if type_ == "lasp_orset_gbtree":
+        # :217-233 — no `[]` special case; `Ids =/= Ids1` compares the token TREES
+        # (shape included); new elements by gb_trees:size
+        infl = is_inflation(type_, prev, cur)
+        deleted = False
+        for elem, ids in gb.to_list(prev):
+            found = gb.lookup(elem, cur)
+            if found is not None:
+                deleted = deleted or not gb.structurally_equal(ids, found[1])
+        return infl and (deleted or gb.size(prev) < gb.size(cur))
     if type_ == "lasp_orset":
         # :235-253
         if prev == [] and cur != []:
