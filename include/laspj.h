@@ -309,6 +309,44 @@ int laspj_gcounter_apply_increments(laspj_ctx* ctx, laspj_batch* batch,
 int laspj_gcounter_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                           uint32_t group);
 
+/* ------------------------------------------------------------------ wire codec */
+/* to_binary/1 — lasp_orset.erl:198-200, lasp_gset.erl:111-113:
+ *   <<?TAG:8, ?V1_VERS:8, (riak_dt:to_binary(S))/binary>>, riak_dt:to_binary = term_to_binary
+ * written on the device for every replica of a batch.  The
+ * payload of replica i is the external term format image (version byte 131, then the
+ * orddict [{Elem, [{Token, Bool}]}] as LIST_EXT / SMALL_TUPLE_EXT / ATOM_EXT, or the
+ * G-Set ordset as LIST_EXT or, for all-byte integers, STRING_EXT), prefixed by the two
+ * bytes (tag, vers) when tag >= 0 (tag < 0: the bare term_to_binary/1 image).  The
+ * compressed form ({compressed, N}) is not produced here.
+ *
+ * The dictionary holds each dictionary term's own external image (no version byte),
+ * which the host encodes once per distinct term:
+ *   elem_blob[elem_off[e] .. elem_off[e+1])         element slot e   (empty: unused)
+ *   elem_order[0 .. E)                              element slots in Erlang term order
+ *   tok_blob[tok_off[64e+k] .. tok_off[64e+k+1])    token slot k of element e (empty: unused)
+ *   tok_order[64e + j], j < 64                      token slots of e in term order,
+ *                                                   0xFF after the last used one
+ * tok_* may be NULL for a G-Set-only dictionary.  Encoding a cell whose slots are not
+ * in the dictionary fails with LASPJ_E_RANGE and writes nothing meaningful. */
+typedef struct laspj_etf_dict laspj_etf_dict;
+int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t elements, const uint8_t* elem_blob,
+                          const uint32_t* elem_off, const uint32_t* elem_order,
+                          const uint8_t* tok_blob, const uint32_t* tok_off,
+                          const uint8_t* tok_order, laspj_etf_dict** out);
+int laspj_etf_dict_destroy(laspj_etf_dict* d);
+/* sizes: offsets (a buffer of R+1 uint64) receives the exclusive prefix sum of the
+ * per-replica payload sizes; *total = offsets[R] (synchronous). */
+int laspj_orset_etf_size(laspj_ctx* ctx, const laspj_batch* batch, const laspj_etf_dict* d,
+                         int tag, laspj_buf* offsets, uint64_t* total);
+/* payloads: replica i at out[offsets[i] .. offsets[i+1]); offsets from *_etf_size
+ * with the same batch, dictionary and tag presence; out holds >= total bytes */
+int laspj_orset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_etf_dict* d,
+                          int tag, int vers, const laspj_buf* offsets, laspj_buf* out);
+int laspj_gset_etf_size(laspj_ctx* ctx, const laspj_batch* batch, const laspj_etf_dict* d,
+                        int tag, laspj_buf* offsets, uint64_t* total);
+int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_etf_dict* d,
+                         int tag, int vers, const laspj_buf* offsets, laspj_buf* out);
+
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);
 int laspj_event_destroy(laspj_event* ev);

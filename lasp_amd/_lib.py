@@ -121,6 +121,12 @@ SIGNATURES = {
     "laspj_gcounter_equal": (i, [vp, vp, vp, vp]),
     "laspj_gcounter_apply_increments": (i, [vp, vp, C.POINTER(Incr), u64]),
     "laspj_gcounter_reduce": (i, [vp, vp, vp, u32]),
+    "laspj_etf_dict_create": (i, [vp, u32, vp, vp, vp, vp, vp, vp, vpp]),
+    "laspj_etf_dict_destroy": (i, [vp]),
+    "laspj_orset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
+    "laspj_orset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
+    "laspj_gset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
+    "laspj_gset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

@@ -144,6 +144,41 @@ class Domain:
                 out.append(self.elements.terms[es])
         return out
 
+    # ------------------------------------------------------------------ wire codec
+    def etf_arrays(self, E: int, tokens: bool = True):
+        """The laspj_etf_dict_create arrays for E element slots: every registered term's
+        external image (lasp_amd.etf.encode, once per term), element slots in term
+        order (unregistered slots last) and, with `tokens`, per-element token images and
+        token slots in term order."""
+        from . import etf
+        if self.size > E:
+            raise CapacityError(f"{self.size} elements do not fit {E} slots")
+        eoff = np.zeros((E + 1,), dtype=np.uint32)
+        eparts = []
+        for es, term in enumerate(self.elements.terms):
+            img = etf.encode(term)
+            eparts.append(img)
+            eoff[es + 1] = len(img)
+        eoff = np.cumsum(eoff, dtype=np.uint64).astype(np.uint32)
+        order = np.concatenate([self.elements.order(),
+                                np.arange(self.size, E, dtype=np.int64)]).astype(np.uint32)
+        if not tokens:
+            return b"".join(eparts), eoff, order, None, None, None
+        tlen = np.zeros((64 * E + 1,), dtype=np.uint64)
+        tparts = []
+        tord = np.full((E, 64), 0xFF, dtype=np.uint8)
+        for es, td in enumerate(self.tokens[:self.size]):
+            for k, term in enumerate(td.terms):
+                img = etf.encode(term)
+                tparts.append((64 * es + k, img))
+                tlen[64 * es + k + 1] = len(img)
+            o = td.order()
+            tord[es, :len(o)] = o
+        toff = np.cumsum(tlen).astype(np.uint32)
+        tparts.sort(key=lambda x: x[0])
+        return (b"".join(eparts), eoff, order, b"".join(img for _k, img in tparts), toff,
+                tord.reshape(-1))
+
     # ------------------------------------------------------------------ G-Set
     def encode_gset(self, states: Sequence, E: int) -> np.ndarray:
         for s in states:

@@ -55,14 +55,6 @@ StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16) {
     return t;
 }
 
-static int wave_grid(const laspj_ctx* ctx, uint64_t items) {
-    // one wave per item, 4 waves per 256-thread block
-    uint64_t blocks = (items + 3) / 4;
-    uint64_t cap = (uint64_t)ctx->cus * 8;
-    if (blocks > cap) blocks = cap;
-    return blocks ? (int)blocks : 1;
-}
-
 // ------------------------------------------------------------------ join: d = a | b
 
 template <int U, bool NT>

@@ -120,6 +120,36 @@ class Event:
         return ms.value
 
 
+class ETFDict:
+    """Device copy of a dictionary's external term images (laspj_etf_dict_create):
+    element slot images in term order and, for OR-Sets, per-element token images."""
+
+    def __init__(self, ctx: Context, elements: int, elem_blob: bytes, elem_off: np.ndarray,
+                 elem_order: np.ndarray, tok_blob: Optional[bytes] = None,
+                 tok_off: Optional[np.ndarray] = None, tok_order: Optional[np.ndarray] = None):
+        self.ctx = ctx
+        eb = np.frombuffer(elem_blob or b"\0", dtype=np.uint8)
+        eo = np.ascontiguousarray(elem_off, dtype=np.uint32)
+        eord = np.ascontiguousarray(elem_order, dtype=np.uint32)
+        if tok_off is not None:
+            tb = np.frombuffer(tok_blob or b"\0", dtype=np.uint8)
+            to = np.ascontiguousarray(tok_off, dtype=np.uint32)
+            tord = np.ascontiguousarray(tok_order, dtype=np.uint8)
+            tptrs = (tb.ctypes.data, to.ctypes.data, tord.ctypes.data)
+        else:
+            tptrs = (None, None, None)
+        h = C.c_void_p()
+        check(ctx.L.laspj_etf_dict_create(ctx.h, elements, eb.ctypes.data, eo.ctypes.data,
+                                          eord.ctypes.data, *tptrs, C.byref(h)), ctx.h)
+        self.h = h
+        self.elements = elements
+
+    def __del__(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_etf_dict_destroy(self.h)
+            self.h = None
+
+
 class _Batch:
     kind = 0
     _create = ""
@@ -174,6 +204,26 @@ class _Batch:
               self.ctx.h)
         return self
 
+    def etf_encode(self, d: ETFDict, tag: int = -1, vers: int = 1):
+        """to_binary/1 payloads of every replica, on the device: (offsets Buffer of
+        R + 1 uint64, payload Buffer, total bytes).  tag < 0: bare term_to_binary/1."""
+        size_fn, write_fn = self._etf
+        offs = Buffer(self.ctx, 8 * (self.replicas + 1))
+        total = C.c_uint64()
+        check(getattr(self.ctx.L, size_fn)(self.ctx.h, self.h, d.h, tag, offs.h,
+                                           C.byref(total)), self.ctx.h)
+        out = Buffer(self.ctx, max(1, total.value))
+        check(getattr(self.ctx.L, write_fn)(self.ctx.h, self.h, d.h, tag, vers, offs.h, out.h),
+              self.ctx.h)
+        return offs, out, total.value
+
+    def to_binaries(self, d: ETFDict, tag: int = -1, vers: int = 1) -> list:
+        """etf_encode + download, split per replica."""
+        offs, out, total = self.etf_encode(d, tag, vers)
+        o = offs.download(np.uint64)
+        blob = out.download(np.uint8, count=total).tobytes() if total else b""
+        return [blob[int(o[i]):int(o[i + 1])] for i in range(self.replicas)]
+
     def _bool_out(self, fn, *args) -> np.ndarray:
         buf = self.ctx.buffer(self.replicas)
         check(fn(self.ctx.h, *args, buf.h), self.ctx.h)
@@ -196,6 +246,7 @@ class ORSetBatch(_Batch):
 
     kind = _lib.KIND_ORSET
     _create = "laspj_orset_batch_create"
+    _etf = ("laspj_orset_etf_size", "laspj_orset_etf_write")
 
     def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         """(count, E, 2) uint64 array of {p, r} cells."""
@@ -373,6 +424,7 @@ class GSetBatch(_Batch):
 
     kind = _lib.KIND_GSET
     _create = "laspj_gset_batch_create"
+    _etf = ("laspj_gset_etf_size", "laspj_gset_etf_write")
 
     def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         return self.download_words(first, count)

@@ -115,3 +115,39 @@ def _ext(t) -> int:
     if isinstance(t, list):
         return 1 if not t else 5 + sum(_ext(x) for x in t) + 1
     raise TypeError(t)
+
+
+# --------------------------------------------------------------------------- wire codec
+
+def to_binary(s, tag: int = None) -> bytes:
+    """to_binary/1 — lasp_gset.erl:111: <<?TAG, ?V1_VERS, term_to_binary(S)>>,
+    assembled on the device from the cells (laspj_gset_etf_write)."""
+    from . import etf
+    from .engine import ETFDict
+    dom = Domain()
+    b = _batch(dom, [s])
+    E = b.elements
+    d = ETFDict(context(), E, *dom.etf_arrays(E, tokens=False))
+    return b.to_binaries(d, etf.DT_GSET_TAG if tag is None else tag, etf.V1_VERS)[0]
+
+
+def to_binary2(vers, s):
+    """to_binary/2: version 1 -> {ok, Bin}; else {error, unsupported_version, Vers}."""
+    if vers == 1:
+        return ("ok", to_binary(s))
+    return ("error", "unsupported_version", vers)
+
+
+def from_binary(b: bytes, tag: int = None):
+    """from_binary/1 — lasp_gset.erl:111-128: binary_to_term of the payload after
+    <<?TAG, 1>> wrapped in {ok, S};
+    {error, unsupported_version, V} or {error, invalid_binary} otherwise."""
+    from . import etf
+    tag = etf.DT_GSET_TAG if tag is None else tag
+    b = bytes(b)
+    if len(b) >= 2 and b[0] == tag:
+        if b[1] != etf.V1_VERS:
+            return ("error", "unsupported_version", b[1])
+        state = etf.binary_to_term(b[2:])
+        return ("ok", state)
+    return ("error", "invalid_binary")

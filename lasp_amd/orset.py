@@ -190,3 +190,39 @@ def _waste_pct(adds: int, rems: int) -> int:
         return 0
     import math
     return int(math.floor(rems / (adds + rems) * 100 + 0.5))
+
+
+# --------------------------------------------------------------------------- wire codec
+
+def to_binary(s, tag: int = None) -> bytes:
+    """to_binary/1 — lasp_orset.erl:198: <<?TAG, ?V1_VERS, term_to_binary(S)>>,
+    assembled on the device from the cells (laspj_orset_etf_write)."""
+    from . import etf
+    from .engine import ETFDict
+    dom = Domain()
+    b, _ = _batch(dom, [s])
+    E = b.elements
+    d = ETFDict(context(), E, *dom.etf_arrays(E, tokens=True))
+    return b.to_binaries(d, etf.DT_ORSET_TAG if tag is None else tag, etf.V1_VERS)[0]
+
+
+def to_binary2(vers, s):
+    """to_binary/2: version 1 -> {ok, Bin}; else {error, unsupported_version, Vers}."""
+    if vers == 1:
+        return ("ok", to_binary(s))
+    return ("error", "unsupported_version", vers)
+
+
+def from_binary(b: bytes, tag: int = None):
+    """from_binary/1 — lasp_orset.erl:198-214: binary_to_term of the payload after
+    <<?TAG, 1>> (returned bare, as riak_dt:from_binary/1 returns it);
+    {error, unsupported_version, V} or {error, invalid_binary} otherwise."""
+    from . import etf
+    tag = etf.DT_ORSET_TAG if tag is None else tag
+    b = bytes(b)
+    if len(b) >= 2 and b[0] == tag:
+        if b[1] != etf.V1_VERS:
+            return ("error", "unsupported_version", b[1])
+        state = etf.binary_to_term(b[2:])
+        return state
+    return ("error", "invalid_binary")

@@ -1,0 +1,248 @@
+"""Wire codec: to_binary / from_binary (src/lasp_orset.erl:198-214, src/lasp_gset.erl:
+111-128; riak_dt:to_binary/1 = term_to_binary).
+
+CPU: the oracle's external-term-format restatement against the format's published
+examples; the host fragment encoder / decoder against the oracle.  GPU: payloads the
+device assembles from cells, byte for byte against the oracle, on the golden-vector
+states, random states with mixed terms, and a large synthetic batch; and the
+reference's round-trip property from_binary(to_binary(S)) == S
+(test/crdt_statem_eqc.erl:108-121).
+"""
+
+import json
+import os
+import random
+
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from oracle import etf as oetf
+from lasp_amd.terms import Atom as PAtom
+from oracle.terms import Atom, exact_eq
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# (term, term_to_binary(term)) from the external term format specification
+PUBLISHED = [
+    (1, bytes([131, 97, 1])),
+    (255, bytes([131, 97, 255])),
+    (256, bytes([131, 98, 0, 0, 1, 0])),
+    (-1, bytes([131, 98, 255, 255, 255, 255])),
+    (1 << 40, bytes([131, 110, 6, 0, 0, 0, 0, 0, 0, 1])),
+    (-(1 << 40), bytes([131, 110, 6, 1, 0, 0, 0, 0, 0, 1])),
+    (1.5, bytes([131, 70, 63, 248, 0, 0, 0, 0, 0, 0])),
+    (True, bytes([131, 100, 0, 4]) + b"true"),
+    (False, bytes([131, 100, 0, 5]) + b"false"),
+    (Atom("a"), bytes([131, 100, 0, 1, 97])),
+    (b"a", bytes([131, 109, 0, 0, 0, 1, 97])),
+    ((Atom("a"), 1), bytes([131, 104, 2, 100, 0, 1, 97, 97, 1])),
+    ([], bytes([131, 106])),
+    ([1, 2], bytes([131, 107, 0, 2, 1, 2])),
+    ([256], bytes([131, 108, 0, 0, 0, 1, 98, 0, 0, 1, 0, 106])),
+    ([(1, [(b"t", False)])], bytes([131, 108, 0, 0, 0, 1, 104, 2, 97, 1, 108, 0, 0, 0, 1,
+                                    104, 2, 109, 0, 0, 0, 1, 116, 100, 0, 5]) + b"false"
+     + bytes([106, 106])),
+]
+
+
+@pytest.mark.parametrize("term,image", PUBLISHED)
+def test_oracle_published_examples(term, image):
+    assert oetf.term_to_binary(term) == image
+    assert exact_eq(oetf.binary_to_term(image), term)
+
+
+def test_oracle_compressed_roundtrip_and_errors():
+    big = [(k, [(bytes([k % 251]) * 20, False)]) for k in range(300)]
+    z = oetf.term_to_binary(big, compressed=1)
+    assert z[:2] == bytes([131, 80]) and len(z) < len(oetf.term_to_binary(big))
+    assert exact_eq(oetf.binary_to_term(z), big)
+    for bad in (b"", b"\x83", b"\x84\x61\x01", b"\x83\x61\x01\x00", b"\x83\x6c\x00\x00\x00\x01"):
+        with pytest.raises(ValueError):
+            oetf.binary_to_term(bad)
+
+
+_atoms = st.sampled_from([Atom("a"), Atom("undefined"), Atom("ok"), True, False,
+                          Atom("été")])
+_leaf = st.one_of(st.integers(-(1 << 70), 1 << 70), st.integers(0, 300), _atoms,
+                  st.binary(max_size=40), st.floats(allow_nan=False, allow_infinity=False))
+_terms = st.recursive(_leaf, lambda ch: st.one_of(st.lists(ch, max_size=5),
+                                                  st.tuples(ch, ch), st.tuples(ch)),
+                      max_leaves=12)
+
+
+@settings(max_examples=400, deadline=None)
+@given(_terms)
+def test_host_encoder_matches_oracle(t):
+    from lasp_amd import etf
+    img = etf.encode(t)
+    assert bytes([131]) + img == oetf.term_to_binary(t)
+    assert exact_eq(etf.binary_to_term(bytes([131]) + img), oetf.binary_to_term(bytes([131]) + img))
+
+
+def test_host_decoder_rejects_malformed():
+    from lasp_amd import etf
+    for bad in (b"", b"\x83", b"\x83\x62\x00", b"\x83\x6c\x00\x00\x00\x01\x61\x01\x61",
+                b"\x83\x61\x01\x00", b"\x83\xff"):
+        with pytest.raises(ValueError):
+            etf.binary_to_term(bad)
+
+
+def test_domain_etf_arrays_slice_the_images():
+    from lasp_amd import etf
+    from lasp_amd.codec import Domain
+    s = [(1, [(b"x" * 20, False), (b"a" * 20, True)]), (PAtom("b"), [(b"q" * 3, False)]),
+         ((1, 2), [(b"z" * 20, True)])]
+    dom = Domain()
+    dom.register_orset(s)
+    eb, eo, order, tb, to, tord = dom.etf_arrays(5)
+    assert [dom.elements.terms[i] for i in order[:3]] == [1, PAtom("b"), (1, 2)]
+    assert list(order[3:]) == [3, 4]
+    for es, term in enumerate(dom.elements.terms):
+        assert eb[eo[es]:eo[es + 1]] == etf.encode(term)
+    assert eo[4] == eo[5] == eo[3]                       # unused slots: empty images
+    e0 = dom.element_slot(1, create=False)
+    assert list(tord[64 * e0:64 * e0 + 3]) == [1, 0, 0xFF]   # b"aaa.." < b"xxx.."
+    for k in (0, 1):
+        t = dom.tokens[e0].terms[k]
+        assert tb[to[64 * e0 + k]:to[64 * e0 + k + 1]] == etf.encode(t)
+
+
+def test_from_binary_errors_and_tags():
+    from lasp_amd import etf, gset, orset
+    s = [(1, [(b"t" * 20, False)])]
+    payload = oetf.to_binary(etf.DT_ORSET_TAG, 1, s)
+    assert exact_eq(orset.from_binary(payload), s)
+    assert orset.from_binary(bytes([etf.DT_ORSET_TAG, 2]) + payload[2:]) == \
+        ("error", "unsupported_version", 2)
+    assert orset.from_binary(b"\x00\x01\x83\x6a") == ("error", "invalid_binary")
+    assert orset.to_binary2(2, s) == ("error", "unsupported_version", 2)
+    g = oetf.to_binary(etf.DT_GSET_TAG, 1, [1, 2, 3])
+    assert gset.from_binary(g) == ("ok", [1, 2, 3])
+    assert orset.from_binary(oetf.to_binary(etf.DT_ORSET_TAG, 1, s, compressed=1)) == s
+
+
+# ------------------------------------------------------------------ GPU
+
+def _golden(name):
+    from tests.golden.termjson import dec
+    with open(os.path.join(HERE, name)) as f:
+        cases = json.load(f)["cases"]
+    return [dec(c[k], PAtom) for c in cases for k in ("a", "b")]
+
+
+@pytest.mark.gpu
+def test_gpu_orset_to_binary_golden():
+    from lasp_amd import etf, orset
+    for s in _golden("orset_cases.json"):
+        got = orset.to_binary(s)
+        assert got == oetf.to_binary(etf.DT_ORSET_TAG, 1, s), s
+        assert exact_eq(orset.from_binary(got), s)
+
+
+@pytest.mark.gpu
+def test_gpu_gset_to_binary_golden():
+    from lasp_amd import etf, gset
+    states = _golden("gset_cases.json") + [[], [0, 1, 255], [1, 256], list(range(300)),
+                                           [PAtom("a"), (1, 2), b"x"]]
+    for s in states:
+        got = gset.to_binary(s)
+        assert got == oetf.to_binary(etf.DT_GSET_TAG, 1, s), s
+        back = gset.from_binary(got)
+        assert back[0] == "ok" and exact_eq(back[1], s)
+
+
+def _random_orsets(rng, n, mixed):
+    elems = list(range(0, 600, 7)) + ([PAtom("x"), (1, PAtom("y")), b"bin", 1 << 40, -5, 2.5]
+                                      if mixed else [])
+    # each element draws its tokens from a pool of 40 (a dictionary holds <= 64 per element)
+    pool = {hk: [bytes(rng.randrange(256) for _ in range(20 if not mixed else rng.choice([1, 20, 33])))
+                 for _ in range(40)] for hk in range(len(elems))}
+    out = []
+    for _ in range(n):
+        d = {}
+        for i in rng.sample(range(len(elems)), rng.randint(0, min(40, len(elems)))):
+            d[elems[i]] = {t: rng.random() < 0.3 for t in rng.sample(pool[i], rng.randint(1, 6))}
+        out.append(d)
+    from oracle.otp import lists_sort
+    res = []
+    for d in out:
+        keys = lists_sort(list(d.keys()))
+        res.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in keys])
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mixed", [False, True])
+def test_gpu_orset_batch_payloads_random(mixed):
+    """One batch of 300 replicas over one dictionary; uniform (20-byte tokens) and
+    mixed token / element images; bare term_to_binary images and tagged payloads."""
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    rng = random.Random(7 + mixed)
+    states = _random_orsets(rng, 300, mixed)
+    dom = Domain()
+    for s in states:
+        dom.register_orset(s)
+    E = dom.size + 3                                     # unused trailing slots
+    b = context().orset_batch(len(states), E)
+    b.upload(dom.encode_orset(states, E))
+    d = engine.ETFDict(context(), E, *dom.etf_arrays(E))
+    bare = b.to_binaries(d)
+    tagged = b.to_binaries(d, tag=etf.DT_ORSET_TAG, vers=1)
+    for s, x, y in zip(states, bare, tagged):
+        assert x == oetf.term_to_binary(s)
+        assert y == bytes([etf.DT_ORSET_TAG, 1]) + x
+
+
+@pytest.mark.gpu
+def test_gpu_etf_rejects_unregistered_slots():
+    from lasp_amd import _lib, engine
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    s = [(1, [(b"t" * 20, False)])]
+    dom = Domain()
+    dom.register_orset(s)
+    b = context().orset_batch(2, 4)
+    cells = dom.encode_orset([s, s], 4)
+    cells[1, 2, 0] = 1                                   # element slot 2 has no image
+    b.upload(cells)
+    d = engine.ETFDict(context(), 4, *dom.etf_arrays(4))
+    with pytest.raises(_lib.LaspjError):
+        b.etf_encode(d)
+    cells[1, 2, 0] = 0
+    cells[1, 0, 0] = 0b10                                # token slot 1 of element 0
+    b.upload(cells)
+    with pytest.raises(_lib.LaspjError):
+        b.etf_encode(d)
+
+
+@pytest.mark.gpu
+def test_gpu_orset_large_synthetic_batch():
+    """4096 replicas x 512 slots x 64 token slots (seeded synthetic cells, the bench
+    dictionary of 20-byte tokens): sampled replicas match the oracle byte for byte and
+    the offsets are the prefix sums of the oracle's payload sizes."""
+    import numpy as np
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle import columnar as orc
+    R, E = 4096, 512
+    b = context().orset_batch(R, E)
+    b.fill_synthetic(5)
+    toks = orc.synth_tokens(E)
+    dom = Domain()
+    for e in range(E):
+        es = dom.element_slot(e)
+        for k in range(64):
+            dom.token_slot(es, bytes(toks[e][k]))
+    d = engine.ETFDict(context(), E, *dom.etf_arrays(E))
+    offs, out, total = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
+    o = offs.download(np.uint64)
+    cells = b.download()
+    assert o[0] == 0 and int(o[-1]) == total
+    for i in list(range(0, R, 257)) + [R - 1]:
+        s = dom.decode_orset(cells[i])
+        want = oetf.to_binary(etf.DT_ORSET_TAG, 1, s)
+        got = out.download(np.uint8, count=int(o[i + 1] - o[i]), offset=int(o[i])).tobytes()
+        assert got == want, i

@@ -190,12 +190,55 @@ def config5(ctx, steps):
     report("config5_product", ms, 4 * n * n + 32 * n, n * n, "cells_per_s", el=n, er=n)
 
 
+def etf(ctx, steps):
+    """to_binary/1 payloads of whole batches: the size pass
+    (cells read + a device scan) and the write pass (cells read, payload written).
+    Shapes: (a) 4096 replicas x 1024 slots x 64 token slots (synthetic cells, ~32
+    tokens per element); (b) 65536 replicas x 256 slots x <= 3 tokens.  Tokens are
+    20-byte binaries, elements integers (SMALL_INTEGER_EXT / INTEGER_EXT images)."""
+    import hashlib
+    from lasp_amd.codec import Domain
+    L = ctx.L
+    for tag, R, E, T in (("t64", 4096, 1024, 64), ("t3", 65536, 256, 3)):
+        b = ctx.orset_batch(R, E)
+        if T == 64:
+            b.fill_synthetic(9)
+        else:
+            rng = np.random.default_rng(3)
+            h = np.zeros((R, E, 2), np.uint64)
+            present = rng.random((R, E)) < 0.9
+            h[:, :, 0] = np.where(present, rng.integers(1, 8, (R, E), dtype=np.uint64), 0)
+            h[:, :, 1] = h[:, :, 0] & rng.integers(0, 8, (R, E), dtype=np.uint64) & \
+                rng.integers(0, 8, (R, E), dtype=np.uint64)
+            b.upload(h)
+        dom = Domain()
+        for e in range(E):
+            es = dom.element_slot(e * 1000)
+            for k in range(T):
+                dom.token_slot(es, hashlib.blake2b(b"%d:%d" % (e, k), digest_size=20).digest())
+        d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+        offs = ctx.buffer(8 * (R + 1))
+        total = _lib.C.c_uint64()
+        size_ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_size(
+            ctx.h, b.h, d.h, 76, offs.h, _lib.C.byref(total)), ctx.h), steps)
+        out = ctx.buffer(total.value)
+        ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
+            ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h), steps)
+        cells = R * E
+        report(f"orset_etf_size_{tag}", size_ms, 16 * cells + 16 * R, cells, "cells_per_s",
+               replicas=R, elements=E)
+        report(f"orset_etf_write_{tag}", ms, 16 * cells + total.value, cells, "cells_per_s",
+               replicas=R, elements=E, payload_bytes=total.value,
+               payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        del out, offs, d, b
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--replicas", type=int, default=1 << 20)
     ap.add_argument("--elements", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--only", default="kernels,ops,config4,config5")
+    ap.add_argument("--only", default="kernels,ops,config4,config5,etf")
     a = ap.parse_args()
     ctx = engine.Context(0)
     todo = a.only.split(",")
@@ -207,6 +250,8 @@ def main():
         config4(ctx, 1024, 1 << 20, a.steps)
     if "config5" in todo:
         config5(ctx, a.steps)
+    if "etf" in todo:
+        etf(ctx, a.steps)
 
 
 if __name__ == "__main__":
