@@ -20,6 +20,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -30,6 +31,7 @@ struct laspj_etf_dict {
     uint32_t elements = 0;
     bool has_tokens = false;
     uint32_t tok_uniform = 0;     // every used token image has this length (0: mixed)
+    uint32_t tok_max = 0;         // most token slots any element uses
     void* block = nullptr;        // one device allocation holding the arrays below
     const uint8_t* elem_blob = nullptr;
     const uint32_t* elem_off = nullptr;    // E + 1
@@ -39,6 +41,14 @@ struct laspj_etf_dict {
     const uint32_t* tok_off = nullptr;     // 64E + 1
     const uint8_t* tok_order = nullptr;    // 64E
     const uint64_t* tok_mask = nullptr;    // E: token slots with an image
+    // the same images again, each starting on a 16-byte boundary (wide loads)
+    const uint8_t* elem_pad = nullptr;
+    const uint32_t* elem_poff = nullptr;   // E
+    const uint8_t* tok_pad = nullptr;
+    const uint32_t* tok_poff = nullptr;    // 64E
+    // per element, tokens in term order: k | image length << 8 | padded offset << 32
+    // (k = 0xFF after the last one) — one load per (element, rank)
+    const uint64_t* tok_desc = nullptr;    // 64E
 };
 
 namespace laspj {
@@ -59,11 +69,17 @@ struct DictView {
     const uint8_t* tok_order;
     const uint64_t* tok_mask;
     uint32_t tok_uniform;
+    const uint8_t* elem_pad;
+    const uint32_t* elem_poff;
+    const uint8_t* tok_pad;
+    const uint32_t* tok_poff;
+    const uint64_t* tok_desc;
 };
 
 DictView view(const laspj_etf_dict* d) {
-    return {d->elem_blob, d->elem_off, d->elem_order, d->elem_byte, d->tok_blob,
-            d->tok_off, d->tok_order, d->tok_mask, d->tok_uniform};
+    return {d->elem_blob, d->elem_off,  d->elem_order, d->elem_byte, d->tok_blob,
+            d->tok_off,   d->tok_order, d->tok_mask,   d->tok_uniform, d->elem_pad,
+            d->elem_poff, d->tok_pad,   d->tok_poff,   d->tok_desc};
 }
 
 __device__ __forceinline__ u64 wave_sum(u64 v) {
@@ -141,11 +157,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds4,
     return before + x - v;
 }
 
-__device__ __forceinline__ uint8_t* put_bytes(uint8_t* o, const uint8_t* src, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i) o[i] = src[i];
-    return o + n;
-}
-
 __device__ __forceinline__ uint8_t* put_be32(uint8_t* o, uint32_t v) {
     o[0] = (uint8_t)(v >> 24);
     o[1] = (uint8_t)(v >> 16);
@@ -154,74 +165,366 @@ __device__ __forceinline__ uint8_t* put_be32(uint8_t* o, uint32_t v) {
     return o + 4;
 }
 
-__device__ __forceinline__ uint8_t* put_atom_bool(uint8_t* o, bool t) {
-    o[0] = 100;
-    o[1] = 0;
-    if (t) {
-        o[2] = 4; o[3] = 't'; o[4] = 'r'; o[5] = 'u'; o[6] = 'e';
-        return o + 7;
+__constant__ uint8_t kAtomTrue[7] = {100, 0, 4, 't', 'r', 'u', 'e'};
+__constant__ uint8_t kAtomFalse[8] = {100, 0, 5, 'f', 'a', 'l', 's', 'e'};
+
+// ---------------------------------------------------------------- staging windows
+// The write kernels assemble a replica chunk by chunk (256 elements in term order) and
+// each chunk window by window: the bytes of [w0, w0 + wl) (chunk-relative) are staged
+// in LDS by whichever threads own them, then the block copies the window out with
+// 16-byte non-temporal stores (LDS and HBM alignment made equal mod 16).  Byte-level
+// work stays in LDS; HBM sees whole 1 KiB wave stores.
+constexpr uint32_t kWin = 16384;
+
+struct Win {
+    uint8_t* buf;      // window byte x at buf[x]
+    uint32_t w0, wl;   // chunk-relative window [w0, w0 + wl)
+    __device__ __forceinline__ bool hits(uint32_t q, uint32_t n) const {
+        return q < w0 + wl && q + n > w0;
     }
-    o[2] = 5; o[3] = 'f'; o[4] = 'a'; o[5] = 'l'; o[6] = 's'; o[7] = 'e';
-    return o + 8;
+    __device__ __forceinline__ void put(uint32_t q, uint8_t b) const {
+        uint32_t x = q - w0;
+        if (x < wl) buf[x] = b;
+    }
+    __device__ __forceinline__ void span(uint32_t q, const uint8_t* src, uint32_t n) const {
+        uint32_t lo = q > w0 ? q : w0, hi = min(q + n, w0 + wl);
+        for (uint32_t y = lo; y < hi; ++y) buf[y - w0] = src[y - q];
+    }
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// n <= 48 bytes of a 16-byte-aligned padded image into LDS bytes dst[0 .. n): up to three
+// 16-byte loads issued together, then byte stores from registers
+__device__ __forceinline__ void lds_put48(uint8_t* dst, const uint8_t* src16, uint32_t n) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(src16);
+    const u32x4 z = {0, 0, 0, 0};
+    const u32x4 a = s[0], b = n > 16 ? s[1] : z, c = n > 32 ? s[2] : z;
+    const uint32_t wd[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (uint32_t i = 0; i < 48; ++i)
+        if (i < n) dst[i] = (uint8_t)(wd[i >> 2] >> ((i & 3u) * 8u));
 }
 
-__device__ void orset_elem_write(const DictView& d, uint32_t e, u64 p, u64 r, uint8_t* o) {
-    o[0] = 104;
-    o[1] = 2;
-    o = put_bytes(o + 2, d.elem_blob + d.elem_off[e], d.elem_off[e + 1] - d.elem_off[e]);
-    o[0] = 108;
-    o = put_be32(o + 1, (uint32_t)__popcll(p));
-    const uint8_t* ord = d.tok_order + 64u * e;
-    for (int j = 0; j < 64; ++j) {
-        uint32_t k = ord[j];
-        if (k >= 64) break;
-        if (!((p >> k) & 1ull)) continue;
+__device__ __forceinline__ bool inside(const Win& w, uint32_t q, uint32_t n) {
+    return q >= w.w0 && q + n <= w.w0 + w.wl;
+}
+
+// 104 2 <elem image> 108 <n:32>: 7 + el bytes at q
+__device__ __forceinline__ void stage_elem_header(const Win& w, const DictView& d, uint32_t e,
+                                                  uint32_t n, uint32_t q) {
+    const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
+    if (!w.hits(q, 7u + el)) return;
+    if (el <= 48 && inside(w, q, 7u + el)) {
+        uint8_t* o = w.buf + (q - w.w0);
         o[0] = 104;
         o[1] = 2;
-        uint32_t t = 64u * e + k;
-        o = put_bytes(o + 2, d.tok_blob + d.tok_off[t], d.tok_off[t + 1] - d.tok_off[t]);
-        o = put_atom_bool(o, (r >> k) & 1ull);
+        lds_put48(o + 2, d.elem_pad + d.elem_poff[e], el);
+        o += 2 + el;
+        o[0] = 108;
+        o[1] = (uint8_t)(n >> 24);
+        o[2] = (uint8_t)(n >> 16);
+        o[3] = (uint8_t)(n >> 8);
+        o[4] = (uint8_t)n;
+        return;
     }
-    o[0] = 106;
+    w.put(q, 104);
+    w.put(q + 1, 2);
+    w.span(q + 2, d.elem_blob + d.elem_off[e], el);
+    q += 2u + el;
+    w.put(q, 108);
+    w.put(q + 1, (uint8_t)(n >> 24));
+    w.put(q + 2, (uint8_t)(n >> 16));
+    w.put(q + 3, (uint8_t)(n >> 8));
+    w.put(q + 4, (uint8_t)n);
 }
 
+// 104 2 <token image> <true | false>; returns the record length
+__device__ __forceinline__ uint32_t record_len(const DictView& d, uint32_t t, bool removed) {
+    return 2u + (d.tok_off[t + 1] - d.tok_off[t]) + (removed ? 7u : 8u);
+}
+
+__device__ __forceinline__ void stage_record(const Win& w, const DictView& d, uint32_t t,
+                                             bool removed, uint32_t q, uint32_t rl) {
+    if (!w.hits(q, rl)) return;
+    const uint32_t L = d.tok_off[t + 1] - d.tok_off[t];
+    if (L <= 48 && inside(w, q, rl)) {
+        uint8_t* o = w.buf + (q - w.w0);
+        o[0] = 104;
+        o[1] = 2;
+        lds_put48(o + 2, d.tok_pad + d.tok_poff[t], L);
+        o += 2 + L;
+        o[0] = 100;
+        o[1] = 0;
+        o[2] = removed ? 4 : 5;
+        o[3] = removed ? 't' : 'f';
+        o[4] = removed ? 'r' : 'a';
+        o[5] = removed ? 'u' : 'l';
+        o[6] = removed ? 'e' : 's';
+        if (!removed) o[7] = 'e';
+        return;
+    }
+    w.put(q, 104);
+    w.put(q + 1, 2);
+    w.span(q + 2, d.tok_blob + d.tok_off[t], L);
+    if (removed) w.span(q + 2 + L, kAtomTrue, 7);
+    else w.span(q + 2 + L, kAtomFalse, 8);
+}
+
+// record from a term-order descriptor: image of L bytes at tok_pad + poff
+__device__ __forceinline__ void stage_record_desc(const Win& w, const DictView& d, uint32_t L,
+                                                  uint32_t poff, bool removed, uint32_t q,
+                                                  uint32_t rl) {
+    if (!w.hits(q, rl)) return;
+    const uint8_t* img = d.tok_pad + poff;
+    if (L <= 48 && inside(w, q, rl)) {
+        uint8_t* o = w.buf + (q - w.w0);
+        o[0] = 104;
+        o[1] = 2;
+        lds_put48(o + 2, img, L);
+        o += 2 + L;
+        o[0] = 100;
+        o[1] = 0;
+        o[2] = removed ? 4 : 5;
+        o[3] = removed ? 't' : 'f';
+        o[4] = removed ? 'r' : 'a';
+        o[5] = removed ? 'u' : 'l';
+        o[6] = removed ? 'e' : 's';
+        if (!removed) o[7] = 'e';
+        return;
+    }
+    w.put(q, 104);
+    w.put(q + 1, 2);
+    w.span(q + 2, img, L);
+    if (removed) w.span(q + 2 + L, kAtomTrue, 7);
+    else w.span(q + 2 + L, kAtomFalse, 8);
+}
+
+// one thread stages its whole element (few tokens per element)
+__device__ void stage_elem_thread(const Win& w, const DictView& d, uint32_t e, u64 p, u64 r,
+                                  uint32_t pos, uint32_t sz) {
+    if (!w.hits(pos, sz)) return;
+    stage_elem_header(w, d, e, (uint32_t)__popcll(p), pos);
+    uint32_t q = pos + 7u + (d.elem_off[e + 1] - d.elem_off[e]);
+    const uint64_t* desc = d.tok_desc + 64u * e;
+    for (int j = 0; j < 64; ++j) {
+        const uint64_t ds = desc[j];
+        const uint32_t k = (uint32_t)(ds & 0xFFu);
+        if (k >= 64) break;
+        if (!((p >> k) & 1ull)) continue;
+        const bool rm = (r >> k) & 1ull;
+        const uint32_t L = (uint32_t)(ds >> 8) & 0xFFFFFFu, rl = 2u + L + (rm ? 7u : 8u);
+        stage_record_desc(w, d, L, (uint32_t)(ds >> 32), rm, q, rl);
+        q += rl;
+    }
+    w.put(q, 106);
+}
+
+// a wave stages one element: lane j owns the j-th token of the element in term order
+__device__ void stage_elem_wave(const Win& w, const DictView& d, uint32_t e, u64 p, u64 r,
+                                uint32_t pos, uint32_t sz) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
+    if (lane == 0) {
+        stage_elem_header(w, d, e, (uint32_t)__popcll(p), pos);
+        w.put(pos + sz - 1u, 106);
+    }
+    const uint32_t k = d.tok_order[64u * e + lane];
+    const bool here = k < 64 && ((p >> k) & 1ull);
+    const bool rm = here && ((r >> k) & 1ull);
+    const uint32_t t = 64u * e + (k & 63u);
+    const uint32_t rl = here ? record_len(d, t, rm) : 0u;
+    uint32_t x = rl;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (here) stage_record(w, d, t, rm, pos + 7u + el + (x - rl), rl);
+}
+
+// copy window bytes buf[sh .. sh + wl) to out[g .. g + wl), (g - sh) % 16 == 0
+__device__ __forceinline__ void copy_out(const uint8_t* buf, uint32_t sh, uint32_t wl,
+                                         uint8_t* out, u64 g) {
+    uint32_t a = (16u - sh) & 15u;
+    if (a > wl) a = wl;
+    for (uint32_t x = threadIdx.x; x < a; x += kBlock) out[g + x] = buf[sh + x];
+    const uint32_t nv = (wl - a) >> 4;
+    const u32x4* src = reinterpret_cast<const u32x4*>(buf + sh + a);
+    u32x4* dst = reinterpret_cast<u32x4*>(out + g + a);
+    for (uint32_t v = threadIdx.x; v < nv; v += kBlock) __builtin_nontemporal_store(src[v], dst + v);
+    for (uint32_t x = a + 16u * nv + threadIdx.x; x < wl; x += kBlock) out[g + x] = buf[sh + x];
+}
+
+__device__ __forceinline__ void write_list_header(uint8_t* out, u64 base, uint32_t hdr, int tag,
+                                                  int vers, uint8_t list_tag, uint32_t n) {
+    uint8_t* o = out + base;
+    if (hdr) {
+        o[0] = (uint8_t)tag;
+        o[1] = (uint8_t)vers;
+    }
+    o[hdr] = 131;
+    o[hdr + 1] = list_tag;
+    if (list_tag == 108) put_be32(o + hdr + 2, n);
+    else if (list_tag == 107) {
+        o[hdr + 2] = (uint8_t)(n >> 8);
+        o[hdr + 3] = (uint8_t)n;
+    }
+}
+
+template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write(const u64x2* cells, uint64_t R,
                                                             uint32_t E, DictView d, int tag,
                                                             int vers, const u64* offs,
                                                             uint8_t* out) {
     __shared__ uint32_t lds4[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
+    __shared__ uint32_t s_e[WAVE ? kBlock : 1], s_pos[WAVE ? kBlock : 1], s_sz[WAVE ? kBlock : 1];
+    __shared__ u64 s_p[WAVE ? kBlock : 1], s_r[WAVE ? kBlock : 1];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    const int wave = threadIdx.x >> 6;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64x2* c = cells + rep * E;
         const u64 base = offs[rep], end = offs[rep + 1];
         u64 cursor = base + hdr + 6u;
         uint32_t n = 0;
         for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
-            uint32_t i = c0 + threadIdx.x;
-            uint32_t e = i < E ? d.elem_order[i] : 0u;
-            u64x2 v = i < E ? c[e] : u64x2{0, 0};
-            uint32_t sz = v.x ? orset_elem_size(d, e, v.x, v.y) : 0u;
+            const uint32_t i = c0 + threadIdx.x;
+            const uint32_t e = i < E ? d.elem_order[i] : 0u;
+            const u64x2 v = i < E ? c[e] : u64x2{0, 0};
+            const uint32_t sz = v.x ? orset_elem_size(d, e, v.x, v.y) : 0u;
             uint32_t tot, cnt;
-            uint32_t pos = block_excl_scan(sz, lds4, &tot);
+            const uint32_t pos = block_excl_scan(sz, lds4, &tot);
             block_excl_scan(v.x ? 1u : 0u, lds4, &cnt);
-            if (v.x && cursor + pos + sz <= end) orset_elem_write(d, e, v.x, v.y, out + cursor + pos);
+            if (cursor + tot + 1u > end) break;          // sizes disagree: never overrun
+            if (WAVE) {
+                s_e[threadIdx.x] = e;
+                s_p[threadIdx.x] = v.x;
+                s_r[threadIdx.x] = v.y;
+                s_pos[threadIdx.x] = pos;
+                s_sz[threadIdx.x] = sz;
+                __syncthreads();
+            }
+            for (uint32_t w0 = 0; w0 < tot; w0 += kWin) {
+                const uint32_t wl = min(kWin, tot - w0);
+                const u64 g = cursor + w0;
+                const uint32_t sh = (uint32_t)(g & 15u);
+                const Win win{buf + sh, w0, wl};
+                if (WAVE) {
+                    for (int j = wave; j < kBlock; j += kBlock / 64) {
+                        const uint32_t jp = s_pos[j], js = s_sz[j];
+                        if (js && win.hits(jp, js))
+                            stage_elem_wave(win, d, s_e[j], s_p[j], s_r[j], jp, js);
+                    }
+                } else if (v.x) {
+                    stage_elem_thread(win, d, e, v.x, v.y, pos, sz);
+                }
+                __syncthreads();
+                copy_out(buf, sh, wl, out, g);
+                __syncthreads();
+            }
             cursor += tot;
             n += cnt;
         }
         if (threadIdx.x == 0) {
-            uint8_t* o = out + base;
-            if (hdr) {
-                o[0] = (uint8_t)tag;
-                o[1] = (uint8_t)vers;
+            write_list_header(out, base, hdr, tag, vers, n ? 108 : 106, n);
+            if (n && cursor < end) out[cursor] = 106;
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Many tokens per element: each wave assembles whole elements on its own (lane j owns
+// the element's j-th token in term order) in a private LDS buffer and stores them with
+// 16-byte stores; only the chunk scan that places elements is block-wide.
+constexpr uint32_t kWB = 4096;
+
+__global__ __launch_bounds__(kBlock) void k_orset_etf_write_wave(const u64x2* cells, uint64_t R,
+                                                                 uint32_t E, DictView d, int tag,
+                                                                 int vers, const u64* offs,
+                                                                 uint8_t* out) {
+    __shared__ uint32_t lds4[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t wbuf[kBlock / 64][kWB + 16];
+    __shared__ uint32_t s_e[kBlock], s_pos[kBlock], s_sz[kBlock];
+    __shared__ u64 s_p[kBlock], s_r[kBlock];
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* mine = wbuf[wave];
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64x2* c = cells + rep * E;
+        const u64 base = offs[rep], end = offs[rep + 1];
+        u64 cursor = base + hdr + 6u;
+        uint32_t n = 0;
+        for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
+            const uint32_t i = c0 + threadIdx.x;
+            const uint32_t e = i < E ? d.elem_order[i] : 0u;
+            const u64x2 v = i < E ? c[e] : u64x2{0, 0};
+            const uint32_t sz = v.x ? orset_elem_size(d, e, v.x, v.y) : 0u;
+            uint32_t tot, cnt;
+            const uint32_t pos = block_excl_scan(sz, lds4, &tot);
+            block_excl_scan(v.x ? 1u : 0u, lds4, &cnt);
+            if (cursor + tot + 1u > end) break;          // sizes disagree: never overrun
+            s_e[threadIdx.x] = e;
+            s_p[threadIdx.x] = v.x;
+            s_r[threadIdx.x] = v.y;
+            s_pos[threadIdx.x] = pos;
+            s_sz[threadIdx.x] = sz;
+            __syncthreads();
+            for (int j = wave; j < kBlock; j += kBlock / 64) {
+                const uint32_t js = s_sz[j];
+                if (!js) continue;
+                const uint32_t je = s_e[j];
+                const u64 jp = s_p[j], jr = s_r[j];
+                const u64 g0 = cursor + s_pos[j];
+                const uint64_t ds = d.tok_desc[64u * je + lane];
+                const uint32_t k = (uint32_t)(ds & 0xFFu);
+                const bool here = k < 64 && ((jp >> k) & 1ull);
+                const bool rm = here && ((jr >> k) & 1ull);
+                const uint32_t L = (uint32_t)(ds >> 8) & 0xFFFFFFu;
+                const uint32_t rl = here ? 2u + L + (rm ? 7u : 8u) : 0u;
+                uint32_t x = rl;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    uint32_t y = __shfl_up(x, off, 64);
+                    if (lane >= off) x += y;
+                }
+                const uint32_t q = 7u + (d.elem_off[je + 1] - d.elem_off[je]) + (x - rl);
+                for (uint32_t w0 = 0; w0 < js; w0 += kWB) {
+                    const uint32_t wl = min(kWB, js - w0);
+                    const u64 g = g0 + w0;
+                    const uint32_t sh = (uint32_t)(g & 15u);
+                    const Win win{mine + sh, w0, wl};
+                    if (lane == 0) {
+                        stage_elem_header(win, d, je, (uint32_t)__popcll(jp), 0u);
+                        win.put(js - 1u, 106);
+                    }
+                    if (here) stage_record_desc(win, d, L, (uint32_t)(ds >> 32), rm, q, rl);
+                    wave_sync();
+                    uint32_t a = (16u - sh) & 15u;
+                    if (a > wl) a = wl;
+                    if ((uint32_t)lane < a) out[g + lane] = mine[sh + lane];
+                    const uint32_t nv = (wl - a) >> 4;
+                    const u32x4* src = reinterpret_cast<const u32x4*>(mine + sh + a);
+                    u32x4* dst = reinterpret_cast<u32x4*>(out + g + a);
+                    for (uint32_t vi = lane; vi < nv; vi += 64)
+                        __builtin_nontemporal_store(src[vi], dst + vi);
+                    for (uint32_t xx = a + 16u * nv + lane; xx < wl; xx += 64) out[g + xx] = mine[sh + xx];
+                    wave_sync();
+                }
             }
-            o[hdr] = 131;
-            if (n) {
-                o[hdr + 1] = 108;
-                put_be32(o + hdr + 2, n);
-                if (cursor < end) out[cursor] = 106;
-            } else {
-                o[hdr + 1] = 106;
-            }
+            __syncthreads();
+            cursor += tot;
+            n += cnt;
+        }
+        if (threadIdx.x == 0) {
+            write_list_header(out, base, hdr, tag, vers, n ? 108 : 106, n);
+            if (n && cursor < end) out[cursor] = 106;
         }
         __syncthreads();
     }
@@ -265,6 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uin
                                                            int tag, int vers, const u64* offs,
                                                            uint8_t* out) {
     __shared__ uint32_t lds4[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64* w = words + rep * W;
@@ -284,38 +588,35 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uin
         const bool str = n > 0 && nonbyte == 0 && n < 65536u;
         u64 cursor = base + hdr + 1u + (str ? 3u : 5u);
         for (uint32_t c0 = 0; c0 < E && n; c0 += kBlock) {
-            uint32_t i = c0 + threadIdx.x;
-            uint32_t e = i < E ? d.elem_order[i] : 0u;
-            bool here = i < E && ((w[e >> 6] >> (e & 63u)) & 1ull);
-            uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
-            uint32_t sz = here ? (str ? 1u : el) : 0u;
+            const uint32_t i = c0 + threadIdx.x;
+            const uint32_t e = i < E ? d.elem_order[i] : 0u;
+            const bool here = i < E && ((w[e >> 6] >> (e & 63u)) & 1ull);
+            const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
+            const uint32_t sz = here ? (str ? 1u : el) : 0u;
             uint32_t tot;
-            uint32_t pos = block_excl_scan(sz, lds4, &tot);
-            if (here && cursor + pos + sz <= end) {
-                const uint8_t* src = d.elem_blob + d.elem_off[e];
-                if (str) out[cursor + pos] = src[1];
-                else put_bytes(out + cursor + pos, src, el);
+            const uint32_t pos = block_excl_scan(sz, lds4, &tot);
+            if (cursor + tot + (str ? 0u : 1u) > end) break;
+            for (uint32_t w0 = 0; w0 < tot; w0 += kWin) {
+                const uint32_t wl = min(kWin, tot - w0);
+                const u64 g = cursor + w0;
+                const uint32_t sh = (uint32_t)(g & 15u);
+                const Win win{buf + sh, w0, wl};
+                if (here) {
+                    const uint8_t* src = d.elem_blob + d.elem_off[e];
+                    if (str) win.put(pos, src[1]);
+                    else if (el <= 48 && inside(win, pos, el))
+                        lds_put48(win.buf + (pos - w0), d.elem_pad + d.elem_poff[e], el);
+                    else win.span(pos, src, el);
+                }
+                __syncthreads();
+                copy_out(buf, sh, wl, out, g);
+                __syncthreads();
             }
             cursor += tot;
         }
         if (threadIdx.x == 0) {
-            uint8_t* o = out + base;
-            if (hdr) {
-                o[0] = (uint8_t)tag;
-                o[1] = (uint8_t)vers;
-            }
-            o[hdr] = 131;
-            if (n == 0) {
-                o[hdr + 1] = 106;
-            } else if (str) {
-                o[hdr + 1] = 107;
-                o[hdr + 2] = (uint8_t)(n >> 8);
-                o[hdr + 3] = (uint8_t)n;
-            } else {
-                o[hdr + 1] = 108;
-                put_be32(o + hdr + 2, n);
-                if (cursor < end) out[cursor] = 106;
-            }
+            write_list_header(out, base, hdr, tag, vers, n == 0 ? 106 : str ? 107 : 108, n);
+            if (n && !str && cursor < end) out[cursor] = 106;
         }
         __syncthreads();
     }
@@ -416,8 +717,13 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                     (unsigned long long)out->bytes, (unsigned long long)total);
     uint64_t cap = (uint64_t)ctx->cus * 8;
     int grid = (int)(R < cap ? R : cap);
-    if (kind == LASPJ_KIND_ORSET)
-        hipLaunchKernelGGL(k_orset_etf_write, dim3(grid), dim3(kBlock), 0, ctx->stream,
+    if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
+        hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
+                           vers, static_cast<const u64*>(offsets->dev),
+                           static_cast<uint8_t*>(out->dev));
+    else if (kind == LASPJ_KIND_ORSET)
+        hipLaunchKernelGGL(k_orset_etf_write<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
@@ -485,12 +791,42 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         }
     }
     const uint64_t eblob = elem_off[E], tblob = toks ? tok_off[64ull * E] : 0;
+    // 16-byte-aligned copies of every image (the write kernels load them 16 B at a time)
+    auto pad16 = [](uint64_t x) { return (x + 15ull) & ~15ull; };
+    std::vector<uint32_t> epoff(E), tpoff(toks ? 64ull * E : 0);
+    uint64_t epad_n = 0, tpad_n = 0;
+    for (uint32_t e = 0; e < E; ++e) {
+        epoff[e] = (uint32_t)epad_n;
+        epad_n += pad16(elem_off[e + 1] - elem_off[e]);
+    }
+    for (uint64_t t = 0; t < tpoff.size(); ++t) {
+        tpoff[t] = (uint32_t)tpad_n;
+        tpad_n += pad16(tok_off[t + 1] - tok_off[t]);
+    }
+    epad_n += 48;                 // a 48-byte load past the last image stays inside
+    tpad_n += 48;
+    if (epad_n >= (1ull << 32) || tpad_n >= (1ull << 32))
+        return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: images exceed 4 GiB");
+    std::vector<uint8_t> epad(epad_n, 0), tpad(tpad_n, 0);
+    std::vector<uint64_t> tdesc(toks ? 64ull * E : 0, 0xFFull);
+    for (uint64_t x = 0; x < tdesc.size(); ++x) {
+        const uint64_t k = tok_order[x];
+        if (k >= 64) continue;
+        const uint64_t t = (x / 64) * 64 + k, L = tok_off[t + 1] - tok_off[t];
+        tdesc[x] = k | (std::min<uint64_t>(L, 0xFFFFFFull) << 8) | ((uint64_t)tpoff[t] << 32);
+    }
+    for (uint32_t e = 0; e < E; ++e)
+        std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], epad.begin() + epoff[e]);
+    for (uint64_t t = 0; t < tpoff.size(); ++t)
+        std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
     const uint64_t o_eoff = 0, o_eord = o_eoff + al(4ull * (E + 1)), o_eb = o_eord + al(4ull * E),
                    o_mask = o_eb + al(E), o_toff = o_mask + al(8ull * E),
                    o_tord = o_toff + (toks ? al(4ull * (64ull * E + 1)) : 0),
                    o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
-                   bytes = o_tblob + al(tblob + 1);
+                   o_epoff = o_tblob + al(tblob + 1), o_tpoff = o_epoff + al(4ull * E),
+                   o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
+                   o_tdesc = o_tpad + al(tpad_n), bytes = o_tdesc + al(8ull * tdesc.size() + 8);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -513,6 +849,11 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess && toks) e = up(o_tord, tok_order, 64ull * E);
     if (e == hipSuccess) e = up(o_eblob, elem_blob, eblob);
     if (e == hipSuccess && toks) e = up(o_tblob, tok_blob, tblob);
+    if (e == hipSuccess) e = up(o_epoff, epoff.data(), 4ull * E);
+    if (e == hipSuccess && toks) e = up(o_tpoff, tpoff.data(), 4ull * tpoff.size());
+    if (e == hipSuccess) e = up(o_epad, epad.data(), epad_n);
+    if (e == hipSuccess && toks) e = up(o_tpad, tpad.data(), tpad_n);
+    if (e == hipSuccess && toks) e = up(o_tdesc, tdesc.data(), 8ull * tdesc.size());
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -522,6 +863,8 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->elements = E;
     d->has_tokens = toks;
     d->tok_uniform = mixed ? 0u : uniform;
+    for (uint32_t x = 0; x < E; ++x)
+        d->tok_max = std::max(d->tok_max, (uint32_t)__builtin_popcountll(tmask[x]));
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);
@@ -530,6 +873,11 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->tok_order = toks ? reinterpret_cast<const uint8_t*>(base + o_tord) : nullptr;
     d->elem_blob = reinterpret_cast<const uint8_t*>(base + o_eblob);
     d->tok_blob = toks ? reinterpret_cast<const uint8_t*>(base + o_tblob) : nullptr;
+    d->elem_poff = reinterpret_cast<const uint32_t*>(base + o_epoff);
+    d->tok_poff = toks ? reinterpret_cast<const uint32_t*>(base + o_tpoff) : nullptr;
+    d->elem_pad = reinterpret_cast<const uint8_t*>(base + o_epad);
+    d->tok_pad = toks ? reinterpret_cast<const uint8_t*>(base + o_tpad) : nullptr;
+    d->tok_desc = toks ? reinterpret_cast<const uint64_t*>(base + o_tdesc) : nullptr;
     *out = d;
     return LASPJ_OK;
 }
