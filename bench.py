@@ -22,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -52,6 +53,9 @@ def parse():
     ap.add_argument("--ae-objects", type=int, default=1 << 18,
                     help="objects per GPU for the anti-entropy leg (2^18 x 4096 = 16 GiB)")
     ap.add_argument("--ae-rounds", type=int, default=3)
+    ap.add_argument("--ae-timeout", type=float, default=240.0,
+                    help="seconds before a stuck anti-entropy leg is abandoned (the "
+                         "headline line is still printed)")
     return ap.parse_args()
 
 
@@ -212,58 +216,77 @@ def main():
 
     cfg1 = config1_gpu(ctx) if rank == 0 else None
 
-    ae = None
+    out = None
+    if rank == 0:
+        cells = R * E
+        achieved = BYTES_PER_JOIN * cells / (kern_ms / 1000.0) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": cells * world / (wall / args.steps),
+            "unit": "merged elements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall * 1000.0 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded splitmix64 replicas, DESIGN.md §5)",
+            "config": {
+                "workload": "batched OR-Set join lasp_orset:merge/2 (BASELINE configs[1])",
+                "replicas_per_gpu": R, "elements": E, "token_slots": 64,
+                "global_replicas": R * world, "parallelism": f"replica shards x{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.pmc, R, E),
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": BYTES_PER_JOIN * cells,
+            },
+            "cpu_baseline": None,
+        }
+        if cfg1 is not None:
+            out["config1_gpu"] = cfg1
+
     if ae_on:
         del a, b, c                      # free the 192 GiB of join operands first
         ctx.synchronize()
+
+        def abandon():
+            # a collective that never completes must not cost the headline line: rank 0
+            # prints it with the leg marked failed, and every rank leaves with status 0
+            if out is not None:
+                out["antientropy"] = {"error": f"timed out after {args.ae_timeout:.0f} s"}
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+
+        guard = threading.Timer(args.ae_timeout, abandon)
+        guard.daemon = True
+        guard.start()
         try:
             ae = antientropy_leg(ctx, args, rank, world, barrier)
         except Exception as e:           # reported, never fatal to the headline line
             ae = {"error": f"{type(e).__name__}: {e}"}
+        guard.cancel()
+        if out is not None:
+            out["antientropy"] = ae
 
     if rank != 0:
-        dist.barrier()
+        _final_barrier(dist)
         return
 
-    cells = R * E
-    ms_per_step = wall * 1000.0 / args.steps
-    value = cells * world / (wall / args.steps)
-    achieved = BYTES_PER_JOIN * cells / (kern_ms / 1000.0) / 1e9
-    traffic = load_traffic(args.pmc, R, E)
-    out = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "merged elements/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (seeded splitmix64 replicas, DESIGN.md §5)",
-        "config": {
-            "workload": "batched OR-Set join lasp_orset:merge/2 (BASELINE configs[1])",
-            "replicas_per_gpu": R, "elements": E, "token_slots": 64,
-            "global_replicas": R * world, "parallelism": f"replica shards x{world}",
-        },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": BYTES_PER_JOIN * cells,
-        },
-        "cpu_baseline": None,
-    }
-    if ae is not None:
-        out["antientropy"] = ae
-    if cfg1 is not None:
-        out["config1_gpu"] = cfg1
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
     print(json.dumps(out), flush=True)
     if dist is not None:
+        _final_barrier(dist)
+
+
+def _final_barrier(dist):
+    try:
         dist.barrier()
+    except Exception as e:               # the line is printed; a lost peer is not fatal
+        print(f"final barrier: {type(e).__name__}: {e}", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -303,6 +303,36 @@ def test_large_join_property(ctx):
     assert d.equal(c).all()
 
 
+def test_full_size_join_properties(ctx):
+    """BASELINE config 2 at its full size (2^20 replicas x 4096 elements x 64 token
+    slots, 3 x 64 GiB resident): sampled replicas on both sides of every 4 GiB / 32-bit
+    boundary equal lasp_orset:merge/2 of the oracle's orddicts token for token (value,
+    stats and inflation too); over the whole batch the join is commutative (B ⊔ A in
+    place equals A ⊔ B), idempotent and an inflation of both inputs."""
+    n, e_n = 1 << 20, 4096
+    toks = orc.synth_tokens(e_n)
+    a, b, c = (ctx.orset_batch(n, e_n) for _ in range(3))
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    c.join(a, b)
+    assert c.is_inflation_of(a).all() and c.is_inflation_of(b).all()
+    vis = c.value_bits()
+    st = c.stats()
+    for i in (0, 1, (1 << 16) - 1, 1 << 16, 699_051, n - 1):
+        A = orc.ORDict.from_cells(orc.synth_orset(2, i, e_n), toks)
+        B = orc.ORDict.from_cells(orc.synth_orset(3, i, e_n), toks)
+        M = A.merge(B)
+        assert orc.ORDict.from_cells(c.download(i, 1)[0], toks).equal(M), f"replica {i}"
+        bits = np.unpackbits(vis[i].view(np.uint8), bitorder="little")[:e_n]
+        assert np.array_equal(np.nonzero(bits)[0], M.value()), f"value/1 of replica {i}"
+        assert tuple(int(x) for x in st[i]) == M.stats(), f"stats/1 of replica {i}"
+    b.join(b, a)                                     # in place, operands swapped
+    assert b.equal(c).all()
+    b.join(b, b)
+    assert b.equal(c).all()
+    assert not c.is_inflation_of(b, strict=True).any()
+
+
 def test_orset_product_tiles_and_tails(ctx):
     """Outer-product tiling: EL and ER off the 64 x 1024 tile, several replicas; every
     cell equals {pX8, rX8, pY8, rY8} of its row / column (0 where either is absent)."""
