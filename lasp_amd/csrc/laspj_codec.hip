@@ -49,6 +49,14 @@ struct laspj_etf_dict {
     // per element, tokens in term order: k | image length << 8 | padded offset << 32
     // (k = 0xFF after the last one) — one load per (element, rank)
     const uint64_t* tok_desc = nullptr;    // 64E
+    // record templates for the uniform-token kernel (every token image rec_len - 2 bytes):
+    // element e, term rank j at rec_pad + (e * tok_max + j) * rec_stride holds
+    // 104 2 <token image>;  element e's header prefix 104 2 <elem image> 108 at
+    // ehdr_pad + ehdr_poff[e]
+    uint32_t rec_len = 0, rec_stride = 0;  // rec_len 0: no templates (mixed token lengths)
+    const uint8_t* rec_pad = nullptr;
+    const uint8_t* ehdr_pad = nullptr;
+    const uint32_t* ehdr_poff = nullptr;   // E
 };
 
 namespace laspj {
@@ -74,12 +82,17 @@ struct DictView {
     const uint8_t* tok_pad;
     const uint32_t* tok_poff;
     const uint64_t* tok_desc;
+    uint32_t tok_max, rec_len, rec_stride;
+    const uint8_t* rec_pad;
+    const uint8_t* ehdr_pad;
+    const uint32_t* ehdr_poff;
 };
 
 DictView view(const laspj_etf_dict* d) {
-    return {d->elem_blob, d->elem_off,  d->elem_order, d->elem_byte, d->tok_blob,
+    return {d->elem_blob, d->elem_off,  d->elem_order, d->elem_byte,  d->tok_blob,
             d->tok_off,   d->tok_order, d->tok_mask,   d->tok_uniform, d->elem_pad,
-            d->elem_poff, d->tok_pad,   d->tok_poff,   d->tok_desc};
+            d->elem_poff, d->tok_pad,   d->tok_poff,   d->tok_desc,    d->tok_max,
+            d->rec_len,   d->rec_stride, d->rec_pad,   d->ehdr_pad,    d->ehdr_poff};
 }
 
 __device__ __forceinline__ u64 wave_sum(u64 v) {
@@ -530,6 +543,295 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_wave(const u64x2* ce
     }
 }
 
+
+// ------------------------------------------------------- uniform-token record kernel
+// Every token image of the dictionary has the same length (Lasp's tokens are the
+// 20-byte binaries of unique/1 or add_by_token), so a record's position follows from
+// its element's position and its rank among the element's present tokens alone.  A
+// block assembles a replica 256 elements (one chunk) at a time:
+//   A  thread per element: the cell's token bits permuted into term order, its byte
+//      size and record count; one block scan places elements and numbers records.
+//   B  per 16 KiB LDS window (16-byte aligned in the output): threads stage element
+//      headers and, spread over all lanes, the chunk's records (record -> element by a
+//      binary search of the record prefix, -> token by rank select), each piece as
+//      byte-shifted dwords OR-ed into the zeroed window (ds_or_b32; neighbours share
+//      edge dwords); then whole 16-byte chunks go out with non-temporal stores and the
+//      trailing partial chunk is carried to the next window.
+// Lanes are busy on records whatever the tokens per element; no byte-wise LDS work.
+constexpr uint32_t kFWin = 16384;
+
+__device__ __forceinline__ uint32_t select64(u64 m, uint32_t k) {
+    uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)m);
+    if (k >= c) { k -= c; m >>= 32; pos = 32; }
+    uint32_t lo = (uint32_t)m;
+    c = (uint32_t)__popc(lo & 0xFFFFu);
+    if (k >= c) { k -= c; lo >>= 16; pos += 16; }
+    c = (uint32_t)__popc(lo & 0xFFu);
+    if (k >= c) { k -= c; lo >>= 8; pos += 8; }
+    c = (uint32_t)__popc(lo & 0xFu);
+    if (k >= c) { k -= c; lo >>= 4; pos += 4; }
+    c = (uint32_t)__popc(lo & 0x3u);
+    if (k >= c) { k -= c; lo >>= 2; pos += 2; }
+    if (k >= (lo & 1u)) pos += 1;
+    return pos;
+}
+
+__device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// OR n <= 4 * NW bytes, little-endian in w[], into the window at byte rel (window-
+// relative; may start before it or run past its end: dwords outside are dropped)
+template <int NW>
+__device__ __forceinline__ void or_piece(uint32_t* win, int64_t rel, const uint32_t (&w)[NW],
+                                         uint32_t n) {
+    const int64_t d0 = rel >> 2;
+    const uint32_t sh = 8u * ((uint32_t)rel & 3u);
+    const uint32_t nd = ((uint32_t)(rel & 3) + n + 3u) >> 2;
+#pragma unroll
+    for (int i = 0; i <= NW; ++i) {
+        if ((uint32_t)i < nd) {
+            const uint32_t hi = i < NW ? w[i] : 0u, lo = i > 0 ? w[i - 1] : 0u;
+            const uint32_t v = (uint32_t)((((u64)hi << 32) | lo) >> (32u - sh));
+            const int64_t dw = d0 + i;
+            if (v && dw >= 0 && dw < (int64_t)(kFWin / 4)) lds_or(win + dw, v);
+        }
+    }
+}
+
+// n bytes of a 16-byte-aligned zero-padded image (n <= 48) as a piece
+__device__ __forceinline__ void load_piece48(uint32_t (&w)[12], const uint8_t* src16, uint32_t n) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(src16);
+    const u32x4 z = {0, 0, 0, 0};
+    const u32x4 a = s[0], b = n > 16 ? s[1] : z, c = n > 32 ? s[2] : z;
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w;
+}
+
+__device__ __forceinline__ void or_bytes_slow(uint32_t* win, int64_t rel, const uint8_t* src,
+                                              uint32_t n) {
+    for (uint32_t x = 0; x < n; ++x) {
+        const int64_t b = rel + x;
+        if (b >= 0 && b < (int64_t)kFWin) lds_or(win + (b >> 2), (uint32_t)src[x] << (8u * (b & 3)));
+    }
+}
+
+__device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* lds4, u64* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u64 x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        u64 y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) lds4[w] = x;
+    __syncthreads();
+    u64 before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; ++i) {
+        u64 s = lds4[i];
+        if (i < w) before += s;
+        all += s;
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cells, uint64_t R,
+                                                                uint32_t E, DictView d, int tag,
+                                                                int vers, const u64* offs,
+                                                                uint8_t* out) {
+    __shared__ __attribute__((aligned(16))) uint32_t win[kFWin / 4];
+    __shared__ uint32_t s_e[kBlock], s_pos[kBlock + 1], s_rec[kBlock + 1], s_hl[kBlock];
+    __shared__ u64 s_p[kBlock], s_r[kBlock], lds4[kBlock / 64];
+    u32x4* win4 = reinterpret_cast<u32x4*>(win);
+    const uint32_t tid = threadIdx.x, hdr = tag >= 0 ? 2u : 0u;
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    for (uint32_t x = tid; x < kFWin / 16; x += kBlock) win4[x] = u32x4{0, 0, 0, 0};
+    __syncthreads();
+    const u64* cw = reinterpret_cast<const u64*>(cells);
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64x2* c = cells + rep * E;
+        const u64 base = offs[rep], end = offs[rep + 1];
+        // present elements: the list header's length field
+        u64 cnt = 0;
+        for (uint32_t e = tid; e < E; e += kBlock) cnt += cw[2ull * (rep * E + e)] != 0;
+        u64 n64;
+        block_excl_scan64(cnt, lds4, &n64);
+        const uint32_t n = (uint32_t)n64;
+        u64 cursor = base + hdr + (n ? 6u : 2u);   // next element byte
+        u64 seg_lo = base;      // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
+        for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
+            const bool last = c0 + kBlock >= E;
+            // ---- A: element sizes, term-order token masks, record numbering
+            const uint32_t i = c0 + tid;
+            uint32_t e = 0, sz = 0, nt = 0, hl = 0;
+            u64 pt = 0, rt = 0;
+            if (i < E) {
+                e = d.elem_order[i];
+                const u64x2 v = c[e];
+                if (v.x) {
+                    const u32x4* ord = reinterpret_cast<const u32x4*>(d.tok_order + 64ull * e);
+                    for (uint32_t j16 = 0; j16 < RK; j16 += 16) {
+                        const u32x4 o = ord[j16 >> 4];
+                        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                        for (int b = 0; b < 16; ++b) {
+                            const uint32_t k = (ow[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+                            if (k < 64) {
+                                pt |= ((v.x >> k) & 1ull) << (j16 + b);
+                                rt |= ((v.y >> k) & 1ull) << (j16 + b);
+                            }
+                        }
+                    }
+                    rt &= pt;
+                    nt = (uint32_t)__popcll(pt);
+                    hl = d.elem_off[e + 1] - d.elem_off[e] + 3u;
+                    sz = hl + 4u + nt * (RL + 8u) - (uint32_t)__popcll(rt) + 1u;
+                }
+            }
+            u64 tot2;
+            const u64 pr = block_excl_scan64((u64)sz | ((u64)nt << 32), lds4, &tot2);
+            const uint32_t pos = (uint32_t)pr, tot = (uint32_t)tot2;
+            s_e[tid] = e;
+            s_p[tid] = pt;
+            s_r[tid] = rt;
+            s_hl[tid] = hl;
+            s_pos[tid] = pos;
+            s_rec[tid] = (uint32_t)(pr >> 32);
+            if (tid == kBlock - 1) {
+                s_pos[kBlock] = tot;
+                s_rec[kBlock] = (uint32_t)(tot2 >> 32);
+            }
+            const u64 seg_hi = cursor + tot + (last && n ? 1u : 0u);
+            if (seg_hi > end) break;                      // sizes disagree: never overrun
+            __syncthreads();
+            const uint32_t nrec = s_rec[kBlock];
+            // ---- B: windows over [floor16(seg_lo), seg_hi)
+            for (u64 A = seg_lo & ~15ull; seg_lo < seg_hi && A < seg_hi; A += kFWin) {
+                const int64_t cur_rel = (int64_t)(cursor - A);   // chunk byte 0, window-relative
+                if (c0 == 0 && tid == 0) {                        // 131 108 <n:32> | 131 106
+                    uint32_t w[3] = {0, 0, 0};
+                    uint32_t nb = 0;
+                    auto put = [&](uint32_t byte) { w[nb >> 2] |= byte << (8 * (nb & 3)); ++nb; };
+                    if (hdr) { put((uint32_t)tag & 0xFFu); put((uint32_t)vers & 0xFFu); }
+                    put(131);
+                    if (n) {
+                        put(108); put(n >> 24); put((n >> 16) & 0xFFu); put((n >> 8) & 0xFFu);
+                        put(n & 0xFFu);
+                    } else {
+                        put(106);
+                    }
+                    or_piece<3>(win, (int64_t)(base - A), w, nb);
+                }
+                if (last && n && tid == 0) {
+                    const uint32_t w[1] = {106u};
+                    or_piece<1>(win, cur_rel + tot, w, 1);
+                }
+                // element headers 104 2 <elem> 108 <n:32> and closing 106
+                if (sz) {
+                    const int64_t r0 = cur_rel + pos;
+                    if (r0 < (int64_t)kFWin && r0 + sz > 0) {
+                        if (hl <= 48) {
+                            uint32_t w[12];
+                            load_piece48(w, d.ehdr_pad + d.ehdr_poff[e], hl);
+                            or_piece<12>(win, r0, w, hl);
+                        } else {
+                            uint8_t pre[2] = {104, 2};
+                            or_bytes_slow(win, r0, pre, 2);
+                            or_bytes_slow(win, r0 + 2, d.elem_blob + d.elem_off[e], hl - 3u);
+                            uint8_t post[1] = {108};
+                            or_bytes_slow(win, r0 + hl - 1, post, 1);
+                        }
+                        const uint32_t wn[1] = {__builtin_bswap32(nt)};
+                        or_piece<1>(win, r0 + hl, wn, 4);
+                        const uint32_t wc[1] = {106u};
+                        or_piece<1>(win, r0 + sz - 1, wc, 1);
+                    }
+                }
+                // records whose element intersects the window
+                uint32_t jlo, jhi;
+                {
+                    // first element ending after the window start
+                    uint32_t lo = 0, hi = kBlock;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (cur_rel + (int64_t)s_pos[m + 1] <= 0) lo = m + 1;
+                        else hi = m;
+                    }
+                    jlo = lo;
+                    // first element starting at or after the window end
+                    hi = kBlock;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (cur_rel + (int64_t)s_pos[m] < (int64_t)kFWin) lo = m + 1;
+                        else hi = m;
+                    }
+                    jhi = lo;
+                }
+                const uint32_t r_lo = jlo < kBlock ? s_rec[jlo] : nrec;
+                const uint32_t r_hi = s_rec[jhi];
+                for (uint32_t ri = r_lo + tid; ri < r_hi; ri += kBlock) {
+                    uint32_t lo = jlo, hi = jhi;            // last j with s_rec[j] <= ri
+                    while (hi - lo > 1) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (s_rec[m] <= ri) lo = m;
+                        else hi = m;
+                    }
+                    const uint32_t j = lo, rho = ri - s_rec[j];
+                    const u64 pj = s_p[j], rj = s_r[j];
+                    const uint32_t rank = select64(pj, rho);
+                    const bool rm = (rj >> rank) & 1ull;
+                    const u64 below = rank ? (~0ull >> (64u - rank)) : 0ull;
+                    const int64_t rel = cur_rel + s_pos[j] + s_hl[j] + 4u + rho * (RL + 8u) -
+                                        (uint32_t)__popcll(rj & below);
+                    uint32_t w[12];
+                    load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
+                    or_piece<12>(win, rel, w, RL);
+                    // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
+                    const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
+                                            rm ? 0x00657572u : 0x65736c61u};
+                    or_piece<2>(win, rel + RL, wa, rm ? 7u : 8u);
+                }
+                __syncthreads();
+                // whole 16-byte chunks out; the partial one below seg_hi stays as the carry
+                const u64 wend = A + kFWin < seg_hi ? A + kFWin : seg_hi;
+                const uint32_t full = (uint32_t)((wend - A) >> 4);
+                for (uint32_t m = tid; m < full; m += kBlock) {
+                    const u64 g = A + 16ull * m;
+                    const u32x4 v = win4[m];
+                    if (g >= base) {
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + g));
+                    } else {
+                        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+                        for (uint32_t b = (uint32_t)(base - g); b < 16; ++b)
+                            out[g + b] = (uint8_t)(vw[b >> 2] >> (8 * (b & 3)));
+                    }
+                    win4[m] = u32x4{0, 0, 0, 0};
+                }
+                if (tid == 0 && full > 0 && wend == seg_hi && (seg_hi & 15u)) {
+                    win4[0] = win4[full];
+                    win4[full] = u32x4{0, 0, 0, 0};
+                }
+                __syncthreads();
+            }
+            seg_lo = seg_hi;
+            cursor += tot;
+        }
+        // flush the carry: bytes [floor16(seg_lo), seg_lo) that belong to this payload
+        if (tid < 16) {
+            const u64 g = (seg_lo & ~15ull) + tid;
+            if (g >= base && g < seg_lo)
+                out[g] = (uint8_t)(win[tid >> 2] >> (8 * (tid & 3)));
+        }
+        __syncthreads();
+        if (tid == 0) win4[0] = u32x4{0, 0, 0, 0};
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_gset_etf_size(const u64* words, uint64_t R,
                                                           uint32_t E, uint32_t W, DictView d,
                                                           uint32_t hdr, u64* sizes,
@@ -717,7 +1019,12 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                     (unsigned long long)out->bytes, (unsigned long long)total);
     uint64_t cap = (uint64_t)ctx->cus * 8;
     int grid = (int)(R < cap ? R : cap);
-    if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
+    if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf == 0)
+        hipLaunchKernelGGL(k_orset_etf_write_rec, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
+                           vers, static_cast<const u64*>(offsets->dev),
+                           static_cast<uint8_t*>(out->dev));
+    else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
         hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),
@@ -817,6 +1124,44 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     }
     for (uint32_t e = 0; e < E; ++e)
         std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], epad.begin() + epoff[e]);
+    uint32_t tok_max = 0;
+    for (uint32_t x = 0; x < E; ++x)
+        tok_max = std::max(tok_max, (uint32_t)__builtin_popcountll(tmask[x]));
+    // record templates (uniform token images only): 104 2 <image> per (element, term rank),
+    // and 104 2 <elem image> 108 per element
+    const uint32_t rec_len = (toks && !mixed && uniform && uniform + 2u <= 48u) ? uniform + 2u : 0u;
+    const uint64_t rec_stride = pad16(rec_len);
+    std::vector<uint8_t> rpad, hpad;
+    std::vector<uint32_t> hpoff;
+    if (rec_len) {
+        rpad.assign((uint64_t)E * tok_max * rec_stride + 48, 0);
+        for (uint64_t e = 0; e < E; ++e)
+            for (uint32_t j = 0; j < tok_max; ++j) {
+                const uint8_t k = tok_order[64ull * e + j];
+                if (k >= 64) break;
+                const uint64_t t = 64ull * e + k;
+                uint8_t* r = rpad.data() + (e * tok_max + j) * rec_stride;
+                r[0] = 104;
+                r[1] = 2;
+                std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], r + 2);
+            }
+        hpoff.resize(E);
+        uint64_t hn = 0;
+        for (uint32_t e = 0; e < E; ++e) {
+            hpoff[e] = (uint32_t)hn;
+            hn += pad16(elem_off[e + 1] - elem_off[e] + 3ull);
+        }
+        if (hn + 48 >= (1ull << 32) || rpad.size() >= (1ull << 40))
+            return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: record templates too large");
+        hpad.assign(hn + 48, 0);
+        for (uint32_t e = 0; e < E; ++e) {
+            uint8_t* h = hpad.data() + hpoff[e];
+            h[0] = 104;
+            h[1] = 2;
+            std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], h + 2);
+            h[2 + elem_off[e + 1] - elem_off[e]] = 108;
+        }
+    }
     for (uint64_t t = 0; t < tpoff.size(); ++t)
         std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
@@ -826,7 +1171,9 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
                    o_epoff = o_tblob + al(tblob + 1), o_tpoff = o_epoff + al(4ull * E),
                    o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
-                   o_tdesc = o_tpad + al(tpad_n), bytes = o_tdesc + al(8ull * tdesc.size() + 8);
+                   o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
+                   o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
+                   bytes = o_hpoff + al(4ull * hpoff.size() + 4);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -854,6 +1201,9 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess) e = up(o_epad, epad.data(), epad_n);
     if (e == hipSuccess && toks) e = up(o_tpad, tpad.data(), tpad_n);
     if (e == hipSuccess && toks) e = up(o_tdesc, tdesc.data(), 8ull * tdesc.size());
+    if (e == hipSuccess && rec_len) e = up(o_rpad, rpad.data(), rpad.size());
+    if (e == hipSuccess && rec_len) e = up(o_hpad, hpad.data(), hpad.size());
+    if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -863,8 +1213,12 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->elements = E;
     d->has_tokens = toks;
     d->tok_uniform = mixed ? 0u : uniform;
-    for (uint32_t x = 0; x < E; ++x)
-        d->tok_max = std::max(d->tok_max, (uint32_t)__builtin_popcountll(tmask[x]));
+    d->tok_max = tok_max;
+    d->rec_len = rec_len;
+    d->rec_stride = (uint32_t)rec_stride;
+    d->rec_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_rpad) : nullptr;
+    d->ehdr_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_hpad) : nullptr;
+    d->ehdr_poff = rec_len ? reinterpret_cast<const uint32_t*>(base + o_hpoff) : nullptr;
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);

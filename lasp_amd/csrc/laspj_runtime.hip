@@ -221,6 +221,11 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
         case LASPJ_TUNE_STREAM_NT:
             ctx->tune_nt = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_ETF_KERNEL:
+            if (value != 0 && value != 1)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0 or 1");
+            ctx->tune_etf = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

@@ -246,3 +246,93 @@ def test_gpu_orset_large_synthetic_batch():
         want = oetf.to_binary(etf.DT_ORSET_TAG, 1, s)
         got = out.download(np.uint8, count=int(o[i + 1] - o[i]), offset=int(o[i])).tobytes()
         assert got == want, i
+
+
+def _both_kernels(ctx, fn):
+    """fn() under the record kernel (LASPJ_TUNE_ETF_KERNEL 0, chosen for uniform token
+    images) and the element-staging kernels (1)."""
+    from lasp_amd._lib import TUNE_ETF_KERNEL
+    out = []
+    try:
+        for k in (0, 1):
+            ctx.set_tuning(TUNE_ETF_KERNEL, k)
+            out.append(fn())
+    finally:
+        ctx.set_tuning(TUNE_ETF_KERNEL, 0)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tok_len,long_elems", [(20, False), (20, True), (41, True),
+                                                (42, False), (1, True)])
+def test_gpu_orset_record_kernel_edges(tok_len, long_elems):
+    """Payloads crossing many 16 KiB windows (up to 300 elements x 64 tokens), empty and
+    one-token replicas, element images longer than the 48-byte fast header (binaries,
+    tuples, long atoms), token images at the record kernel's 48-byte limit (41-byte
+    binaries) and just past it (42: the staging kernels), E not a multiple of 256:
+    both kernels match the oracle byte for byte, bare and tagged."""
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle.otp import lists_sort
+    rng = random.Random(tok_len * 7 + long_elems)
+    elems = list(range(0, 900, 3))
+    if long_elems:
+        elems += [b"L" * 60, (PAtom("k"), b"v" * 50), PAtom("a" * 47), b"s" * 40, 1 << 70]
+    pool = {i: [bytes(rng.randrange(256) for _ in range(tok_len)) for _ in range(64)]
+            for i in range(len(elems))}
+    if tok_len == 1:                                  # 64 distinct one-byte tokens
+        pool = {i: [bytes([x]) for x in rng.sample(range(256), 64)] for i in range(len(elems))}
+    raw = [{}, {elems[5]: {pool[5][0]: False}},
+           {elems[i]: {t: rng.random() < 0.25 for t in pool[i]} for i in range(len(elems))}]
+    for _ in range(37):
+        d = {}
+        k = rng.choice([1, 3, 40, 150, len(elems)])
+        for i in rng.sample(range(len(elems)), k):
+            d[elems[i]] = {t: rng.random() < 0.3 for t in rng.sample(pool[i], rng.randint(1, 64))}
+        raw.append(d)
+    states = []
+    for d in raw:
+        states.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in lists_sort(list(d))])
+    dom = Domain()
+    for s in states:
+        dom.register_orset(s)
+    E = dom.size + 11
+    ctx = context()
+    b = ctx.orset_batch(len(states), E)
+    b.upload(dom.encode_orset(states, E))
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    for bare, tagged in _both_kernels(ctx, lambda: (b.to_binaries(d),
+                                                    b.to_binaries(d, tag=etf.DT_ORSET_TAG))):
+        for s, x, y in zip(states, bare, tagged):
+            assert x == oetf.term_to_binary(s)
+            assert y == bytes([etf.DT_ORSET_TAG, 1]) + x
+
+
+@pytest.mark.gpu
+def test_gpu_record_kernel_whole_buffer_equals_staging():
+    """2048 replicas x 512 slots x 64 token slots (~1.1 GB of payloads): the record and
+    the staging kernels write identical buffers, every byte of every replica."""
+    import numpy as np
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle import columnar as orc
+    R, E = 2048, 512
+    ctx = context()
+    b = ctx.orset_batch(R, E)
+    b.fill_synthetic(11)
+    toks = orc.synth_tokens(E)
+    dom = Domain()
+    for e in range(E):
+        es = dom.element_slot(e * 1000)
+        for k in range(64):
+            dom.token_slot(es, bytes(toks[e][k]))
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+
+    def run():
+        offs, out, total = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
+        return offs.download(np.uint64), out.download(np.uint8, count=total)
+    (o1, p1), (o2, p2) = _both_kernels(ctx, run)
+    assert np.array_equal(o1, o2)
+    assert np.array_equal(p1, p2)

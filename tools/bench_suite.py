@@ -222,14 +222,18 @@ def etf(ctx, steps):
         size_ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_size(
             ctx.h, b.h, d.h, 76, offs.h, _lib.C.byref(total)), ctx.h), steps)
         out = ctx.buffer(total.value)
-        ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
-            ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h), steps)
         cells = R * E
         report(f"orset_etf_size_{tag}", size_ms, 16 * cells + 16 * R, cells, "cells_per_s",
                replicas=R, elements=E)
-        report(f"orset_etf_write_{tag}", ms, 16 * cells + total.value, cells, "cells_per_s",
-               replicas=R, elements=E, payload_bytes=total.value,
-               payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        # record kernel (default for uniform token images), then the staging kernels
+        for knob, name in ((0, "write"), (1, "write_staging")):
+            ctx.set_tuning(_lib.TUNE_ETF_KERNEL, knob)
+            ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
+                ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h), steps)
+            report(f"orset_etf_{name}_{tag}", ms, 16 * cells + total.value, cells,
+                   "cells_per_s", replicas=R, elements=E, payload_bytes=total.value,
+                   payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        ctx.set_tuning(_lib.TUNE_ETF_KERNEL, 0)
         del out, offs, d, b
 
 
