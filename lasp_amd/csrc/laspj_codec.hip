@@ -551,14 +551,13 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_wave(const u64x2* ce
 // block assembles a replica 256 elements (one chunk) at a time:
 //   A  thread per element: the cell's token bits permuted into term order, its byte
 //      size and record count; one block scan places elements and numbers records.
-//   B  per 16 KiB LDS window (16-byte aligned in the output): threads stage element
+//   B  per LDS window (16 KiB (16-byte aligned in the output): threads stage element
 //      headers and, spread over all lanes, the chunk's records (record -> element by a
 //      binary search of the record prefix, -> token by rank select), each piece as
 //      byte-shifted dwords OR-ed into the zeroed window (ds_or_b32; neighbours share
 //      edge dwords); then whole 16-byte chunks go out with non-temporal stores and the
 //      trailing partial chunk is carried to the next window.
 // Lanes are busy on records whatever the tokens per element; no byte-wise LDS work.
-constexpr uint32_t kFWin = 16384;
 
 __device__ __forceinline__ uint32_t select64(u64 m, uint32_t k) {
     uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)m);
@@ -580,21 +579,31 @@ __device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) {
     __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// OR n <= 4 * NW bytes, little-endian in w[], into the window at byte rel (window-
-// relative; may start before it or run past its end: dwords outside are dropped)
+// The window has kGuard bytes of slack on both sides, so a piece that overlaps it can be
+// written whole: bytes that land in the guards are dropped when the window goes out.
+constexpr int32_t kGuard = 64;
+
+template <uint32_t WIN>
+__device__ __forceinline__ bool overlaps(int32_t rel, uint32_t n) {
+    return rel < (int32_t)WIN && rel + (int32_t)n > 0;
+}
+
+// OR a piece of n <= min(nmax, 4 * NW) bytes, little-endian in w[] (zero past n), into
+// the window at window-relative byte rel (the piece must overlap the window).  With
+// d0 = floor((rel - 1) / 4) and sh = rel - 4 d0 in [1, 4], window dword d0 + i receives
+// bytes 4i - sh .. 4i - sh + 3 of the piece = alignbyte(w[i], w[i - 1], 4 - sh): one
+// VALU op and one ds_or_b32 per dword, dwords past nmax skipped on a uniform branch.
 template <int NW>
-__device__ __forceinline__ void or_piece(uint32_t* win, int64_t rel, const uint32_t (&w)[NW],
-                                         uint32_t n) {
-    const int64_t d0 = rel >> 2;
-    const uint32_t sh = 8u * ((uint32_t)rel & 3u);
-    const uint32_t nd = ((uint32_t)(rel & 3) + n + 3u) >> 2;
+__device__ __forceinline__ void or_piece(uint32_t* win, int32_t rel, const uint32_t (&w)[NW],
+                                         uint32_t nmax) {
+    const int32_t rm1 = rel - 1;
+    const uint32_t a = 3u - ((uint32_t)rm1 & 3u);
+    uint32_t* q = win + (rm1 >> 2);
 #pragma unroll
     for (int i = 0; i <= NW; ++i) {
-        if ((uint32_t)i < nd) {
+        if (4u * (uint32_t)i <= nmax + 3u) {
             const uint32_t hi = i < NW ? w[i] : 0u, lo = i > 0 ? w[i - 1] : 0u;
-            const uint32_t v = (uint32_t)((((u64)hi << 32) | lo) >> (32u - sh));
-            const int64_t dw = d0 + i;
-            if (v && dw >= 0 && dw < (int64_t)(kFWin / 4)) lds_or(win + dw, v);
+            lds_or(q + i, __builtin_amdgcn_alignbyte(hi, lo, a));
         }
     }
 }
@@ -609,11 +618,12 @@ __device__ __forceinline__ void load_piece48(uint32_t (&w)[12], const uint8_t* s
     w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w;
 }
 
-__device__ __forceinline__ void or_bytes_slow(uint32_t* win, int64_t rel, const uint8_t* src,
+template <uint32_t WIN>
+__device__ __forceinline__ void or_bytes_slow(uint32_t* win, int32_t rel, const uint8_t* src,
                                               uint32_t n) {
     for (uint32_t x = 0; x < n; ++x) {
-        const int64_t b = rel + x;
-        if (b >= 0 && b < (int64_t)kFWin) lds_or(win + (b >> 2), (uint32_t)src[x] << (8u * (b & 3)));
+        const int32_t b = rel + (int32_t)x;
+        if (b >= 0 && b < (int32_t)WIN) lds_or(win + (b >> 2), (uint32_t)src[x] << (8 * (b & 3)));
     }
 }
 
@@ -639,29 +649,36 @@ __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* lds4, u64* total) {
     return before + x - v;
 }
 
+template <uint32_t WIN>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cells, uint64_t R,
                                                                 uint32_t E, DictView d, int tag,
                                                                 int vers, const u64* offs,
                                                                 uint8_t* out) {
-    __shared__ __attribute__((aligned(16))) uint32_t win[kFWin / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t winbuf[(WIN + 2 * kGuard) / 4];
     __shared__ uint32_t s_e[kBlock], s_pos[kBlock + 1], s_rec[kBlock + 1], s_hl[kBlock];
     __shared__ u64 s_p[kBlock], s_r[kBlock], lds4[kBlock / 64];
+    uint32_t* win = winbuf + kGuard / 4;
     u32x4* win4 = reinterpret_cast<u32x4*>(win);
     const uint32_t tid = threadIdx.x, hdr = tag >= 0 ? 2u : 0u;
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
-    for (uint32_t x = tid; x < kFWin / 16; x += kBlock) win4[x] = u32x4{0, 0, 0, 0};
+    for (uint32_t x = tid; x < (WIN + 2 * kGuard) / 16; x += kBlock)
+        reinterpret_cast<u32x4*>(winbuf)[x] = u32x4{0, 0, 0, 0};
     __syncthreads();
     const u64* cw = reinterpret_cast<const u64*>(cells);
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64x2* c = cells + rep * E;
         const u64 base = offs[rep], end = offs[rep + 1];
-        // present elements: the list header's length field
-        u64 cnt = 0;
-        for (uint32_t e = tid; e < E; e += kBlock) cnt += cw[2ull * (rep * E + e)] != 0;
-        u64 n64;
-        block_excl_scan64(cnt, lds4, &n64);
-        const uint32_t n = (uint32_t)n64;
-        u64 cursor = base + hdr + (n ? 6u : 2u);   // next element byte
+        // present elements (the list header's length field): counted up front when the
+        // replica spans several chunks, else taken from the one chunk's scan
+        uint32_t n = 0;
+        if (E > kBlock) {
+            u64 cnt = 0;
+            for (uint32_t e = tid; e < E; e += kBlock) cnt += cw[2ull * (rep * E + e)] != 0;
+            u64 n64;
+            block_excl_scan64(cnt, lds4, &n64);
+            n = (uint32_t)n64;
+        }
+        u64 cursor = 0;                             // next element byte
         u64 seg_lo = base;      // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
         for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
             const bool last = c0 + kBlock >= E;
@@ -692,26 +709,32 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     sz = hl + 4u + nt * (RL + 8u) - (uint32_t)__popcll(rt) + 1u;
                 }
             }
+            // one scan: byte size (32 bits) | records (20) | present elements (12)
             u64 tot2;
-            const u64 pr = block_excl_scan64((u64)sz | ((u64)nt << 32), lds4, &tot2);
+            const u64 pr = block_excl_scan64((u64)sz | ((u64)nt << 32) | ((u64)(sz != 0) << 52),
+                                             lds4, &tot2);
             const uint32_t pos = (uint32_t)pr, tot = (uint32_t)tot2;
+            if (c0 == 0) {
+                if (E <= kBlock) n = (uint32_t)(tot2 >> 52);
+                cursor = base + hdr + (n ? 6u : 2u);
+            }
             s_e[tid] = e;
             s_p[tid] = pt;
             s_r[tid] = rt;
             s_hl[tid] = hl;
             s_pos[tid] = pos;
-            s_rec[tid] = (uint32_t)(pr >> 32);
+            s_rec[tid] = (uint32_t)(pr >> 32) & 0xFFFFFu;
             if (tid == kBlock - 1) {
                 s_pos[kBlock] = tot;
-                s_rec[kBlock] = (uint32_t)(tot2 >> 32);
+                s_rec[kBlock] = (uint32_t)(tot2 >> 32) & 0xFFFFFu;
             }
             const u64 seg_hi = cursor + tot + (last && n ? 1u : 0u);
             if (seg_hi > end) break;                      // sizes disagree: never overrun
             __syncthreads();
             const uint32_t nrec = s_rec[kBlock];
             // ---- B: windows over [floor16(seg_lo), seg_hi)
-            for (u64 A = seg_lo & ~15ull; seg_lo < seg_hi && A < seg_hi; A += kFWin) {
-                const int64_t cur_rel = (int64_t)(cursor - A);   // chunk byte 0, window-relative
+            for (u64 A = seg_lo & ~15ull; seg_lo < seg_hi && A < seg_hi; A += WIN) {
+                const int32_t cur_rel = (int32_t)(int64_t)(cursor - A);  // chunk byte 0, window-relative
                 if (c0 == 0 && tid == 0) {                        // 131 108 <n:32> | 131 106
                     uint32_t w[3] = {0, 0, 0};
                     uint32_t nb = 0;
@@ -724,52 +747,58 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     } else {
                         put(106);
                     }
-                    or_piece<3>(win, (int64_t)(base - A), w, nb);
+                    const int32_t rel = (int32_t)(int64_t)(base - A);
+                    if (overlaps<WIN>(rel, nb)) or_piece<3>(win, rel, w, 8);
                 }
                 if (last && n && tid == 0) {
                     const uint32_t w[1] = {106u};
-                    or_piece<1>(win, cur_rel + tot, w, 1);
+                    const int32_t rel = cur_rel + (int32_t)tot;
+                    if (overlaps<WIN>(rel, 1)) or_piece<1>(win, rel, w, 1);
                 }
                 // element headers 104 2 <elem> 108 <n:32> and closing 106
                 if (sz) {
-                    const int64_t r0 = cur_rel + pos;
-                    if (r0 < (int64_t)kFWin && r0 + sz > 0) {
-                        if (hl <= 48) {
-                            uint32_t w[12];
-                            load_piece48(w, d.ehdr_pad + d.ehdr_poff[e], hl);
-                            or_piece<12>(win, r0, w, hl);
+                    const int32_t r0 = cur_rel + (int32_t)pos;
+                    if (overlaps<WIN>(r0, sz)) {
+                        if (hl <= 16) {
+                            if (overlaps<WIN>(r0, hl)) {
+                                const u32x4 h = *reinterpret_cast<const u32x4*>(
+                                    d.ehdr_pad + d.ehdr_poff[e]);
+                                const uint32_t w[4] = {h.x, h.y, h.z, h.w};
+                                or_piece<4>(win, r0, w, 16);
+                            }
+                        } else if (hl <= 48) {
+                            if (overlaps<WIN>(r0, hl)) {
+                                uint32_t w[12];
+                                load_piece48(w, d.ehdr_pad + d.ehdr_poff[e], hl);
+                                or_piece<12>(win, r0, w, 48);
+                            }
                         } else {
                             uint8_t pre[2] = {104, 2};
-                            or_bytes_slow(win, r0, pre, 2);
-                            or_bytes_slow(win, r0 + 2, d.elem_blob + d.elem_off[e], hl - 3u);
+                            or_bytes_slow<WIN>(win, r0, pre, 2);
+                            or_bytes_slow<WIN>(win, r0 + 2, d.elem_blob + d.elem_off[e], hl - 3u);
                             uint8_t post[1] = {108};
-                            or_bytes_slow(win, r0 + hl - 1, post, 1);
+                            or_bytes_slow<WIN>(win, r0 + hl - 1, post, 1);
                         }
                         const uint32_t wn[1] = {__builtin_bswap32(nt)};
-                        or_piece<1>(win, r0 + hl, wn, 4);
+                        if (overlaps<WIN>(r0 + (int32_t)hl, 4)) or_piece<1>(win, r0 + (int32_t)hl, wn, 4);
                         const uint32_t wc[1] = {106u};
-                        or_piece<1>(win, r0 + sz - 1, wc, 1);
+                        if (overlaps<WIN>(r0 + (int32_t)sz - 1, 1)) or_piece<1>(win, r0 + (int32_t)sz - 1, wc, 1);
                     }
                 }
                 // records whose element intersects the window
-                uint32_t jlo, jhi;
+                // jlo = first element ending after the window start, jhi = first one
+                // starting at or past its end (both monotone: one ballot per 64 elements)
+                uint32_t jlo = kBlock, jhi = kBlock;
                 {
-                    // first element ending after the window start
-                    uint32_t lo = 0, hi = kBlock;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (cur_rel + (int64_t)s_pos[m + 1] <= 0) lo = m + 1;
-                        else hi = m;
+                    const uint32_t lane = tid & 63u;
+#pragma unroll
+                    for (uint32_t k = 0; k < kBlock / 64; ++k) {
+                        const uint32_t m = 64u * k + lane;
+                        const u64 b1 = __ballot(cur_rel + (int32_t)s_pos[m + 1] > 0);
+                        const u64 b2 = __ballot(cur_rel + (int32_t)s_pos[m] >= (int32_t)WIN);
+                        if (jlo == kBlock && b1) jlo = 64u * k + (uint32_t)__ffsll((long long)b1) - 1u;
+                        if (jhi == kBlock && b2) jhi = 64u * k + (uint32_t)__ffsll((long long)b2) - 1u;
                     }
-                    jlo = lo;
-                    // first element starting at or after the window end
-                    hi = kBlock;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (cur_rel + (int64_t)s_pos[m] < (int64_t)kFWin) lo = m + 1;
-                        else hi = m;
-                    }
-                    jhi = lo;
                 }
                 const uint32_t r_lo = jlo < kBlock ? s_rec[jlo] : nrec;
                 const uint32_t r_hi = s_rec[jhi];
@@ -785,19 +814,22 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     const uint32_t rank = select64(pj, rho);
                     const bool rm = (rj >> rank) & 1ull;
                     const u64 below = rank ? (~0ull >> (64u - rank)) : 0ull;
-                    const int64_t rel = cur_rel + s_pos[j] + s_hl[j] + 4u + rho * (RL + 8u) -
-                                        (uint32_t)__popcll(rj & below);
-                    uint32_t w[12];
-                    load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
-                    or_piece<12>(win, rel, w, RL);
+                    const int32_t rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u +
+                                                            rho * (RL + 8u) -
+                                                            (uint32_t)__popcll(rj & below));
+                    if (overlaps<WIN>(rel, RL)) {
+                        uint32_t w[12];
+                        load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
+                        or_piece<12>(win, rel, w, RL);
+                    }
                     // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
                     const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
                                             rm ? 0x00657572u : 0x65736c61u};
-                    or_piece<2>(win, rel + RL, wa, rm ? 7u : 8u);
+                    if (overlaps<WIN>(rel + (int32_t)RL, 8)) or_piece<2>(win, rel + (int32_t)RL, wa, 8);
                 }
                 __syncthreads();
                 // whole 16-byte chunks out; the partial one below seg_hi stays as the carry
-                const u64 wend = A + kFWin < seg_hi ? A + kFWin : seg_hi;
+                const u64 wend = A + WIN < seg_hi ? A + WIN : seg_hi;
                 const uint32_t full = (uint32_t)((wend - A) >> 4);
                 for (uint32_t m = tid; m < full; m += kBlock) {
                     const u64 g = A + 16ull * m;
@@ -814,6 +846,11 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                 if (tid == 0 && full > 0 && wend == seg_hi && (seg_hi & 15u)) {
                     win4[0] = win4[full];
                     win4[full] = u32x4{0, 0, 0, 0};
+                }
+                if (tid >= kBlock - 2 * kGuard / 16) {          // clear both guards
+                    const uint32_t gi = tid - (kBlock - 2 * kGuard / 16);
+                    const uint32_t x = gi < kGuard / 16 ? gi : (kGuard + WIN) / 16 + gi - kGuard / 16;
+                    reinterpret_cast<u32x4*>(winbuf)[x] = u32x4{0, 0, 0, 0};
                 }
                 __syncthreads();
             }
@@ -1019,12 +1056,16 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                     (unsigned long long)out->bytes, (unsigned long long)total);
     uint64_t cap = (uint64_t)ctx->cus * 8;
     int grid = (int)(R < cap ? R : cap);
-    if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf == 0)
-        hipLaunchKernelGGL(k_orset_etf_write_rec, dim3(grid), dim3(kBlock), 0, ctx->stream,
+    if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf != 1) {
+        // window size (profiles/r01_suite_etf_windows.log): 0 = 20 KiB; 2, 3 = 16, 24 KiB
+        auto k = k_orset_etf_write_rec<20480>;
+        if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384>;
+        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<24576>;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
-    else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
+    } else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
         hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),

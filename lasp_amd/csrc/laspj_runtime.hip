@@ -222,8 +222,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_nt = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_KERNEL:
-            if (value != 0 && value != 1)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0 or 1");
+            if (value < 0 || value > 3)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..3");
             ctx->tune_etf = value;
             return LASPJ_OK;
         default:

@@ -248,13 +248,14 @@ def test_gpu_orset_large_synthetic_batch():
         assert got == want, i
 
 
-def _both_kernels(ctx, fn):
+def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3)):
     """fn() under the record kernel (LASPJ_TUNE_ETF_KERNEL 0, chosen for uniform token
-    images) and the element-staging kernels (1)."""
+    images), the element-staging kernels (1) and the record kernel's other window
+    sizes (2, 3: 16 and 24 KiB)."""
     from lasp_amd._lib import TUNE_ETF_KERNEL
     out = []
     try:
-        for k in (0, 1):
+        for k in knobs:
             ctx.set_tuning(TUNE_ETF_KERNEL, k)
             out.append(fn())
     finally:
@@ -333,6 +334,7 @@ def test_gpu_record_kernel_whole_buffer_equals_staging():
     def run():
         offs, out, total = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
         return offs.download(np.uint64), out.download(np.uint8, count=total)
-    (o1, p1), (o2, p2) = _both_kernels(ctx, run)
-    assert np.array_equal(o1, o2)
-    assert np.array_equal(p1, p2)
+    (o1, p1), *rest = _both_kernels(ctx, run)
+    for o2, p2 in rest:
+        assert np.array_equal(o1, o2)
+        assert np.array_equal(p1, p2)

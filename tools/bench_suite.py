@@ -199,6 +199,7 @@ def etf(ctx, steps):
     import hashlib
     from lasp_amd.codec import Domain
     L = ctx.L
+    steps = max(steps, 20)                    # ~1 ms kernels: average over more launches
     for tag, R, E, T in (("t64", 4096, 1024, 64), ("t3", 65536, 256, 3)):
         b = ctx.orset_batch(R, E)
         if T == 64:
@@ -226,7 +227,10 @@ def etf(ctx, steps):
         report(f"orset_etf_size_{tag}", size_ms, 16 * cells + 16 * R, cells, "cells_per_s",
                replicas=R, elements=E)
         # record kernel (default for uniform token images), then the staging kernels
-        for knob, name in ((0, "write"), (1, "write_staging")):
+        variants = ((0, "write"), (1, "write_staging"))
+        if os.environ.get("ETF_WINDOWS"):
+            variants += ((2, "write_w16k"), (3, "write_w24k"))
+        for knob, name in variants:
             ctx.set_tuning(_lib.TUNE_ETF_KERNEL, knob)
             ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
                 ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h), steps)
