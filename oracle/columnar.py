@@ -60,6 +60,9 @@ def lib():
         L.orc_bench_orset_merge.argtypes = [C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
                                             C.c_double, C.POINTER(C.c_double), u64p,
                                             C.POINTER(C.c_double)]
+        L.orc_bench_orset_op.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
+                                          C.c_double, C.POINTER(C.c_double), u64p,
+                                          C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -174,6 +177,22 @@ def bench_orset_merge(E: int, seed: int, threads: int, pairs: int, budget_s: flo
     if rc != 0:
         raise RuntimeError("orc_bench_orset_merge failed")
     return eps.value, merges.value, secs.value
+
+
+BENCH_OPS = {"merge": 0, "value": 1, "stats": 2, "inflation": 3, "strict_inflation": 4}
+
+
+def bench_orset_op(op: str, E: int, seed: int, threads: int, pairs: int, budget_s: float):
+    """Time one operation of the C restatement (BENCH_OPS) on synthetic replicas;
+    returns (element slots/s, calls, s).  Inflation ops test merge(A, B) against A."""
+    eps = C.c_double()
+    calls = C.c_uint64()
+    secs = C.c_double()
+    rc = lib().orc_bench_orset_op(BENCH_OPS[op], E, seed, threads, pairs, budget_s,
+                                  C.byref(eps), C.byref(calls), C.byref(secs))
+    if rc != 0:
+        raise RuntimeError("orc_bench_orset_op failed")
+    return eps.value, calls.value, secs.value
 
 
 def bench_config1(n: int = 10_000, iters: int = 200):

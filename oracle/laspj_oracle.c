@@ -20,6 +20,9 @@
  *   orc_orset_is_strict    lasp_lattice clause        src/lasp_lattice.erl:235-253
  *   orc_gset_merge         lasp_gset:merge/2          src/lasp_gset.erl:99-101
  *                          (ordsets:union on integer ordsets)
+ *   orc_bench_orset_op     timing of merge / value / stats / inflation / strict
+ *                          inflation on host threads (bench.py cpu_baseline,
+ *                          tools/cpu_beside.py)
  *
  * Synthetic inputs are restated here independently of the HIP
  * generator so that a GPU test can check the device-generated batch against them.
@@ -451,6 +454,10 @@ uint32_t orc_gset_merge(const int64_t* a, uint32_t na, const int64_t* b, uint32_
 
 /* ------------------------------------------------------------------ timed baseline */
 
+/* timed operations: lasp_orset:merge/2, value/1, stat/2 (all three counters),
+ * is_inflation / is_strict_inflation of merge(A, B) over A (lasp_lattice clauses) */
+enum { ORC_OP_MERGE = 0, ORC_OP_VALUE, ORC_OP_STATS, ORC_OP_INFLATION, ORC_OP_STRICT };
+
 typedef struct {
     uint32_t E, T;
     const uint8_t* tokens;
@@ -461,6 +468,8 @@ typedef struct {
     u64 merges;
     double seconds;
     int err;
+    int op;
+    u64 sink;
 } bench_arg;
 
 static double now_s(void) {
@@ -476,7 +485,9 @@ static void* bench_thread(void* p) {
     orc_orset** B = (orc_orset**)calloc(a->pairs, sizeof(void*));
     orc_orset* out = orc_orset_alloc(2 * a->E, 2 * cap_t);
     u64* cells = (u64*)malloc((size_t)a->E * 16);
-    if (!A || !B || !out || !cells) {
+    int64_t* keys = (int64_t*)malloc((size_t)a->E * 8);
+    u64 st[3];
+    if (!A || !B || !out || !cells || !keys) {
         a->err = 1;
         return NULL;
     }
@@ -489,16 +500,31 @@ static void* bench_thread(void* p) {
         orc_orset_from_cells(a->E, cells, a->tokens, a->T, A[k]);
         orc_synth_orset(a->seed + 1, a->first_pair + k, a->E, cells);
         orc_orset_from_cells(a->E, cells, a->tokens, a->T, B[k]);
+        if (a->op == ORC_OP_INFLATION || a->op == ORC_OP_STRICT) {
+            /* B[k] := merge(A, B): the value a bind would test against A */
+            orc_orset_merge(A[k], B[k], out);
+            orc_orset* m = orc_orset_alloc(2 * a->E, 2 * cap_t);
+            orc_orset_merge(A[k], B[k], m);
+            orc_orset_free(B[k]);
+            B[k] = m;
+        }
     }
     double t0 = now_s(), t = t0;
-    u64 n = 0;
+    u64 n = 0, sink = 0;
     while (t - t0 < a->budget_s) {
         for (uint32_t k = 0; k < a->pairs; ++k) {
-            orc_orset_merge(A[k], B[k], out);
+            switch (a->op) {
+                case ORC_OP_MERGE: orc_orset_merge(A[k], B[k], out); break;
+                case ORC_OP_VALUE: sink += orc_orset_value(A[k], keys); break;
+                case ORC_OP_STATS: orc_orset_stats(A[k], st); sink += st[0] + st[1] + st[2]; break;
+                case ORC_OP_INFLATION: sink += orc_orset_is_inflation(A[k], B[k]); break;
+                default: sink += orc_orset_is_strict(A[k], B[k]); break;
+            }
             ++n;
         }
         t = now_s();
     }
+    a->sink = sink;
     a->merges = n;
     a->seconds = t - t0;
     for (uint32_t k = 0; k < a->pairs; ++k) {
@@ -508,15 +534,17 @@ static void* bench_thread(void* p) {
     free(A);
     free(B);
     free(cells);
+    free(keys);
     orc_orset_free(out);
     return NULL;
 }
 
-/* Time lasp_orset:merge/2 (this restatement) on `threads` host threads, each merging
- * `pairs` synthetic replica pairs of E elements round-robin for ~budget_s seconds.
- * Returns merged elements per second (E per merge) via *elem_per_s. */
-int orc_bench_orset_merge(uint32_t E, u64 seed, int threads, uint32_t pairs, double budget_s,
-                          double* elem_per_s, u64* merges_out, double* seconds_out) {
+/* Time operation `op` of this restatement on `threads` host threads, each running it on
+ * `pairs` synthetic replicas (pairs) of E elements round-robin for ~budget_s seconds.
+ * Returns elements per second (E element slots per call) via *elem_per_s. */
+int orc_bench_orset_op(int op, uint32_t E, u64 seed, int threads, uint32_t pairs,
+                       double budget_s, double* elem_per_s, u64* merges_out,
+                       double* seconds_out) {
     uint32_t T = 64;
     uint8_t* tokens = (uint8_t*)malloc((size_t)E * T * 20);
     if (!tokens) return -1;
@@ -524,7 +552,7 @@ int orc_bench_orset_merge(uint32_t E, u64 seed, int threads, uint32_t pairs, dou
     pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     bench_arg* args = (bench_arg*)calloc((size_t)threads, sizeof(bench_arg));
     for (int i = 0; i < threads; ++i) {
-        args[i] = (bench_arg){E, T, tokens, seed, (u64)i * pairs, pairs, budget_s, 0, 0, 0};
+        args[i] = (bench_arg){E, T, tokens, seed, (u64)i * pairs, pairs, budget_s, 0, 0, 0, op, 0};
         pthread_create(&th[i], NULL, bench_thread, &args[i]);
     }
     u64 merges = 0;
@@ -544,4 +572,11 @@ int orc_bench_orset_merge(uint32_t E, u64 seed, int threads, uint32_t pairs, dou
     *merges_out = merges;
     *seconds_out = secs;
     return 0;
+}
+
+/* lasp_orset:merge/2 timing (the headline cpu_baseline) */
+int orc_bench_orset_merge(uint32_t E, u64 seed, int threads, uint32_t pairs, double budget_s,
+                          double* elem_per_s, u64* merges_out, double* seconds_out) {
+    return orc_bench_orset_op(ORC_OP_MERGE, E, seed, threads, pairs, budget_s, elem_per_s,
+                              merges_out, seconds_out);
 }
