@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--ae-objects", type=int, default=1 << 18,
                     help="objects per GPU for the anti-entropy leg (2^18 x 4096 = 16 GiB)")
     ap.add_argument("--ae-rounds", type=int, default=3)
+    ap.add_argument("--gc-objects", type=int, default=1 << 22,
+                    help="G-Counters per GPU for the all_reduce(MAX) leg (x 64 actors x 8 B)")
     ap.add_argument("--ae-timeout", type=float, default=240.0,
                     help="seconds before a stuck anti-entropy leg is abandoned (the "
                          "headline line is still printed)")
@@ -87,13 +89,54 @@ def antientropy_leg(ctx, args, rank, world, barrier):
     per_round = float(t.item()) / args.ae_rounds
     S = ae.bytes
     xgmi = 2.0 * (world - 1) / world * S / per_round / 1e9 if world > 1 else 0.0
-    return {
+    out = {
         "workload": "gossip anti-entropy (BASELINE configs[2]): all_to_all + HIP OR + all_gather",
         "objects_per_gpu": O, "elements": E, "state_bytes_per_gpu": S,
         "rounds": args.ae_rounds, "ms_per_round": per_round * 1e3,
         "merged_elements_per_s": (world - 1) * O * E / per_round,
         "xgmi_GBps_per_gpu": xgmi,
         "frac_mesh": xgmi / (XGMI_LINK_GBS * 7), "frac_ring": xgmi / XGMI_LINK_GBS,
+    }
+    del ae
+    out["gcounter"] = gcounter_leg(ctx, args, rank, world, barrier, g)
+    return out
+
+
+def gcounter_leg(ctx, args, rank, world, barrier, g):
+    """G-Counter anti-entropy: one RCCL all_reduce(MAX) per round (riak_dt_gcounter's
+    join is the per-actor max); afterwards every rank must hold the owners' totals."""
+    import torch
+    import torch.distributed as dist
+    from lasp_amd.gossip import DeviceGCounterAntiEntropy
+    O, A = args.gc_objects, 64
+    gc = DeviceGCounterAntiEntropy(ctx, O, A, group=g)
+    gc.fill(rank, world)
+    gc.round()
+    gc.fill(rank, world)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.ae_rounds):
+        gc.round()
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    o = torch.arange(O, device=gc.state.device, dtype=torch.int64)
+    a = torch.arange(A, device=gc.state.device, dtype=torch.int64)
+    total = (o[:, None] * 7919 + a[None, :] * 104729) % 100003 + 8
+    ok = bool(torch.equal(gc.state.view(O, A), total))
+    reached = int(gc.batch.threshold_met(64 * 8).sum())     # threshold reads after gossip
+    t = torch.tensor([wall, 0.0 if ok else 1.0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per_round = float(t[0].item()) / args.ae_rounds
+    busbw = 2.0 * (world - 1) / world * gc.bytes / per_round / 1e9 if world > 1 else 0.0
+    return {
+        "workload": "G-Counter anti-entropy: RCCL all_reduce(MAX) on int64 counts",
+        "objects_per_gpu": O, "actors": A, "state_bytes_per_gpu": gc.bytes,
+        "ms_per_round": per_round * 1e3, "converged": t[1].item() == 0.0,
+        "threshold_objects": reached,
+        "merged_counts_per_s": (world - 1) * O * A / per_round,
+        "xgmi_GBps_per_gpu": busbw,
     }
 
 

@@ -143,9 +143,10 @@ int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t element
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out);
 int laspj_batch_destroy(laspj_batch* batch);
-/* A non-owning OR-Set / G-Set batch over caller device memory (e.g. a buffer another
- * allocator or a collective library owns; the bytes must stay valid until destroy).
- * `kind` is LASPJ_KIND_ORSET or LASPJ_KIND_GSET; `bytes` must equal the batch size. */
+/* A non-owning OR-Set / G-Set / G-Counter batch over caller device memory (e.g. a
+ * buffer another allocator or a collective library owns; the bytes must stay valid
+ * until destroy).  `kind` is LASPJ_KIND_ORSET, LASPJ_KIND_GSET or LASPJ_KIND_GCOUNTER;
+ * `bytes` must equal the batch size. */
 int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* device_ptr, uint64_t bytes,
                      uint64_t replicas, uint32_t elements, laspj_batch** out);
 int laspj_batch_info_get(const laspj_batch* batch, laspj_batch_info* out);

@@ -334,8 +334,8 @@ int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* dev, uint64_t bytes,
                      uint64_t replicas, uint32_t elements, laspj_batch** out) {
     if (!ctx || !out || !dev) return fail(ctx, LASPJ_E_INVAL, "batch_wrap: null argument");
     *out = nullptr;
-    if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET)
-        return fail(ctx, LASPJ_E_KIND, "batch_wrap: OR-Set or G-Set only");
+    if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET && kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "batch_wrap: OR-Set, G-Set or G-Counter only");
     if (replicas == 0 || elements == 0)
         return fail(ctx, LASPJ_E_SHAPE, "batch_wrap: empty shape");
     uint64_t wpr = words_per(kind, elements, 0);

@@ -325,21 +325,25 @@ class ORSetBatch(_Batch):
         return self
 
 
+def _wrap(self, ctx: Context, tensor, replicas: int, elements: int, bytes_per_replica: int):
+    self.ctx = ctx
+    self._keep = tensor
+    nbytes = tensor.numel() * tensor.element_size()
+    h = C.c_void_p()
+    check(ctx.L.laspj_batch_wrap(ctx.h, self.kind, C.c_void_p(tensor.data_ptr()),
+                                 nbytes, replicas, elements, C.byref(h)), ctx.h)
+    self.h = h
+    self.replicas, self.elements = replicas, elements
+    self.bytes_per_replica = bytes_per_replica
+    self.nbytes = nbytes
+
+
 class WrappedORSetBatch(ORSetBatch):
     """An OR-Set batch over device memory owned by someone else (e.g. a torch tensor
     that RCCL collectives write into); laspj_batch_wrap, non-owning."""
 
     def __init__(self, ctx: Context, tensor, replicas: int, elements: int):
-        self.ctx = ctx
-        self._keep = tensor
-        nbytes = tensor.numel() * tensor.element_size()
-        h = C.c_void_p()
-        check(ctx.L.laspj_batch_wrap(ctx.h, _lib.KIND_ORSET, C.c_void_p(tensor.data_ptr()),
-                                     nbytes, replicas, elements, C.byref(h)), ctx.h)
-        self.h = h
-        self.replicas, self.elements = replicas, elements
-        self.bytes_per_replica = 16 * elements
-        self.nbytes = nbytes
+        _wrap(self, ctx, tensor, replicas, elements, 16 * elements)
 
 
 class ConcatBatch(_Batch):
@@ -519,3 +523,11 @@ class GCounterBatch(_Batch):
             arr[k].replica, arr[k].actor, arr[k].amount = rep, actor, amount
         check(self.ctx.L.laspj_gcounter_apply_increments(self.ctx.h, self.h, arr, n), self.ctx.h)
         return self
+
+
+class WrappedGCounterBatch(GCounterBatch):
+    """A G-Counter batch over someone else's device memory (the int64 tensor an RCCL
+    all_reduce(MAX) writes into); laspj_batch_wrap, non-owning."""
+
+    def __init__(self, ctx: Context, tensor, replicas: int, actors: int):
+        _wrap(self, ctx, tensor, replicas, actors, 8 * actors)

@@ -17,6 +17,11 @@ phase drives all n-1 peer links at once instead of one ring neighbour.
 `anti_entropy_round` is the whole orchestration; it runs over torch.distributed with
 the nccl (= RCCL) backend on GPUs, and over gloo on CPU tensors in the tests, where the
 caller supplies the reduce.
+
+G-Counters are the one lattice here whose join IS a numeric max: riak_dt_gcounter
+merges per actor with max (the counter behind the ad counter's threshold reads,
+lasp_lattice.erl:87-90), so their anti-entropy is a single RCCL all_reduce(MAX) over
+the count words (`gcounter_anti_entropy_round`), with no custom reduce.
 """
 
 from __future__ import annotations
@@ -82,3 +87,39 @@ class DeviceAntiEntropy:
     def round(self):
         anti_entropy_round(self.state, self.recv, self.chunk, self._reduce, self.group,
                            self._sync)
+
+
+def gcounter_anti_entropy_round(counts: torch.Tensor, group=None) -> None:
+    """One G-Counter anti-entropy round: counts (int64, objects x actors, this rank's
+    replica of every object) become the per-actor max over all ranks = the
+    riak_dt_gcounter join.  Counts must stay below 2^63 (int64 max is the unsigned
+    max there)."""
+    dist.all_reduce(counts, op=dist.ReduceOp.MAX, group=group)
+
+
+class DeviceGCounterAntiEntropy:
+    """Device-resident G-Counter anti-entropy over `objects` counters of `actors` actor
+    slots; `batch` exposes the state to the engine (values, threshold reads)."""
+
+    def __init__(self, ctx, objects: int, actors: int, group=None):
+        from . import engine
+        self.ctx, self.group = ctx, group
+        self.objects, self.actors = objects, actors
+        dev = torch.device("cuda", ctx.device)
+        self.state = torch.empty(objects * actors, dtype=torch.int64, device=dev)
+        self.batch = engine.WrappedGCounterBatch(ctx, self.state, objects, actors)
+        self.bytes = objects * actors * 8
+
+    def fill(self, rank: int, world: int):
+        """Synthetic replicas: rank r has counted its own actors (a % world == r) up to
+        their current totals and holds stale views (up to 3 behind) of the others."""
+        o = torch.arange(self.objects, device=self.state.device, dtype=torch.int64)
+        a = torch.arange(self.actors, device=self.state.device, dtype=torch.int64)
+        total = (o[:, None] * 7919 + a[None, :] * 104729) % 100003 + 8
+        lag = (o[:, None] * 31 + a[None, :] * 17 + rank * 13) % 4
+        own = (a[None, :] % world) == rank
+        self.state.view(self.objects, self.actors).copy_(torch.where(own, total, total - 1 - lag))
+        torch.cuda.current_stream(self.state.device).synchronize()
+
+    def round(self):
+        gcounter_anti_entropy_round(self.state, self.group)

@@ -49,6 +49,17 @@ WORKER = textwrap.dedent("""
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)        # bench takes the max wall time
     assert t.item() == float(world)
+    # G-Counter anti-entropy: one all_reduce(MAX) = riak_dt_gcounter's per-actor max
+    from lasp_amd.gossip import gcounter_anti_entropy_round
+    objs, actors = 5, 7
+    rng = [np.random.default_rng(40 + r) for r in range(world)]
+    views = [g.integers(0, 1 << 40, (objs, actors)).astype(np.int64) for g in rng]
+    counts = torch.from_numpy(views[rank].copy())
+    gcounter_anti_entropy_round(counts)
+    want = np.maximum.reduce(views)
+    assert np.array_equal(counts.numpy(), want)
+    gcounter_anti_entropy_round(counts)             # idempotent
+    assert np.array_equal(counts.numpy(), want)
     print("ok", rank)
 """)
 
