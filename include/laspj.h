@@ -122,6 +122,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         token images are uniform (20 KiB window),
                                         1 = element staging, 2 / 3 = record kernel with a
                                         16 / 24 KiB window                               */
+#define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = flat sweep when
+                                        the replica length is a power of two and
+                                        2 <= group <= 4, 1 = per-replica segments with a
+                                        compile-time group, 2 = generic segments        */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -181,25 +181,38 @@ hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_ba
 
 // ------------------------------------------------------------------ gather (map / fold)
 
-// one block per (replica, 4096-slot segment of the output)
-constexpr uint32_t kGSeg = 4096;
+// A block owns one 4096-slot segment of the output and a run of replicas: its 16
+// index entries per lane are loaded once into registers, then every replica of the
+// run is 16 independent gathers + 16 coalesced 16-byte stores per lane.
+constexpr uint32_t kGSeg = 4096, kGPer = kGSeg / kB, kGRun = 8;
 
 __global__ __launch_bounds__(kB) void k_orset_gather(u64x2* out, const u64x2* src,
                                                      const uint32_t* index, uint64_t reps,
                                                      uint32_t E_out, uint32_t E_in,
                                                      uint32_t nseg) {
-    for (uint64_t it = blockIdx.x; it < reps * nseg; it += gridDim.x) {
-        uint64_t rep = it / nseg;
-        uint32_t o0 = (uint32_t)(it - rep * nseg) * kGSeg;
-        uint32_t o1 = min(E_out, o0 + kGSeg);
-        const u64x2* s = src + rep * E_in;
-        u64x2* d = out + rep * E_out;
-#pragma unroll 4
-        for (uint32_t o = o0 + threadIdx.x; o < o1; o += kB) {
-            uint32_t si = index[o];
-            u64x2 v = {0, 0};
-            if (si < E_in) v = s[si];
-            stnt(d + o, v);
+    const uint64_t runs = (reps + kGRun - 1) / kGRun;
+    for (uint64_t it = blockIdx.x; it < runs * nseg; it += gridDim.x) {
+        const uint64_t run = it / nseg;
+        const uint32_t o0 = (uint32_t)(it - run * nseg) * kGSeg;
+        uint32_t si[kGPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kGPer; ++k) {
+            const uint32_t o = o0 + k * kB + threadIdx.x;
+            si[k] = o < E_out ? index[o] : 0xFFFFFFFFu;
+        }
+        const uint64_t r1 = min(reps, (run + 1) * kGRun);
+        for (uint64_t rep = run * kGRun; rep < r1; ++rep) {
+            const u64x2* s = src + rep * E_in;
+            u64x2* d = out + rep * E_out;
+            u64x2 v[kGPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kGPer; ++k)
+                v[k] = si[k] < E_in ? s[si[k]] : u64x2{0, 0};
+#pragma unroll
+            for (uint32_t k = 0; k < kGPer; ++k) {
+                const uint32_t o = o0 + k * kB + threadIdx.x;
+                if (o < E_out) stnt(d + o, v[k]);
+            }
         }
     }
 }
@@ -207,7 +220,7 @@ __global__ __launch_bounds__(kB) void k_orset_gather(u64x2* out, const u64x2* sr
 hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                const uint32_t* index) {
     uint32_t ns = (dst->elements + kGSeg - 1) / kGSeg;
-    uint64_t items = dst->replicas * ns;
+    uint64_t items = (dst->replicas + kGRun - 1) / kGRun * ns;
     uint64_t cap = (uint64_t)ctx->cus * 32;
     uint64_t g = items < cap ? items : cap;
     hipLaunchKernelGGL(k_orset_gather, dim3((unsigned)(g ? g : 1)), dim3(kB), 0, ctx->stream,

@@ -147,14 +147,117 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or(u64* dst, const u64* src, 
     }
 }
 
+// group known at compile time (the FSMs' N = 2..4): all G loads of a step are issued
+// before the first OR, two steps per lane in flight
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_reduce_or_g(u64x2* dst, const u64x2* src,
+                                                        uint64_t groups, uint64_t per,
+                                                        uint32_t nseg) {
+    for (uint64_t it = blockIdx.x; it < groups * nseg; it += gridDim.x) {
+        const uint64_t g = it / nseg;
+        const uint64_t lo = (it - g * nseg) * kRSeg, hi = min(per, lo + kRSeg);
+        const u64x2* s = src + g * G * per;
+        u64x2* d = dst + g * per;
+        uint64_t i = lo + threadIdx.x;
+        for (; i + kBlock < hi; i += 2 * kBlock) {
+            u64x2 x[G], y[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) x[j] = ld2<true>(s + j * per + i);
+#pragma unroll
+            for (int j = 0; j < G; ++j) y[j] = ld2<true>(s + j * per + i + kBlock);
+#pragma unroll
+            for (int j = 1; j < G; ++j) {
+                x[0] |= x[j];
+                y[0] |= y[j];
+            }
+            st2<true>(d + i, x[0]);
+            st2<true>(d + i + kBlock, y[0]);
+        }
+        if (i < hi) {
+            u64x2 x[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) x[j] = ld2<true>(s + j * per + i);
+#pragma unroll
+            for (int j = 1; j < G; ++j) x[0] |= x[j];
+            st2<true>(d + i, x[0]);
+        }
+    }
+}
+
+// power-of-two replica length: one flat grid-stride sweep over the destination (all
+// blocks move through HBM together, as the join does), 2 cells x G loads per lane
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64x2* src,
+                                                           uint64_t n, uint32_t lg) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock, mask = (1ull << lg) - 1ull;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + stride < n; i += 2 * stride) {
+        const uint64_t i2 = i + stride;
+        const u64x2* s = src + (((i >> lg) * G) << lg) + (i & mask);
+        const u64x2* t = src + (((i2 >> lg) * G) << lg) + (i2 & mask);
+        u64x2 x[G], y[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) x[j] = ld2<true>(s + ((uint64_t)j << lg));
+#pragma unroll
+        for (int j = 0; j < G; ++j) y[j] = ld2<true>(t + ((uint64_t)j << lg));
+#pragma unroll
+        for (int j = 1; j < G; ++j) {
+            x[0] |= x[j];
+            y[0] |= y[j];
+        }
+        st2<true>(dst + i, x[0]);
+        st2<true>(dst + i2, y[0]);
+    }
+    if (i < n) {
+        const u64x2* s = src + (((i >> lg) * G) << lg) + (i & mask);
+        u64x2 x[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) x[j] = ld2<true>(s + ((uint64_t)j << lg));
+#pragma unroll
+        for (int j = 1; j < G; ++j) x[0] |= x[j];
+        st2<true>(dst + i, x[0]);
+    }
+}
+
+template <int G>
+static void launch_reduce_flat(laspj_ctx* ctx, u64x2* d, const u64x2* s, uint64_t n,
+                               uint32_t lg) {
+    StreamTune t = stream_tune(ctx, n);
+    hipLaunchKernelGGL((k_reduce_or_flat<G>), dim3(t.grid), dim3(kBlock), 0, ctx->stream, d, s,
+                       n, lg);
+}
+
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t wr) {
+    if ((wr % 2) == 0 && ctx->tune_reduce == 0) {
+        const uint64_t per = wr / 2;
+        if ((per & (per - 1)) == 0 && group >= 2 && group <= 4) {
+            const uint32_t lg = (uint32_t)__builtin_ctzll(per);
+            auto* d2 = reinterpret_cast<u64x2*>(dst);
+            auto* s2 = reinterpret_cast<const u64x2*>(src);
+            if (group == 2) launch_reduce_flat<2>(ctx, d2, s2, groups * per, lg);
+            else if (group == 3) launch_reduce_flat<3>(ctx, d2, s2, groups * per, lg);
+            else launch_reduce_flat<4>(ctx, d2, s2, groups * per, lg);
+            return hipGetLastError();
+        }
+    }
     bool vec2 = (wr % 2) == 0;
     uint64_t per = vec2 ? wr / 2 : wr;
     uint32_t ns = (uint32_t)((per + kRSeg - 1) / kRSeg);
     uint64_t items = groups * ns, cap = (uint64_t)ctx->cus * 32;
     unsigned g = (unsigned)(items < cap ? (items ? items : 1) : cap);
-    if (vec2)
+    auto* d2 = reinterpret_cast<u64x2*>(dst);
+    auto* s2 = reinterpret_cast<const u64x2*>(src);
+    if (vec2 && group == 2 && ctx->tune_reduce != 2)
+        hipLaunchKernelGGL((k_reduce_or_g<2>), dim3(g), dim3(kBlock), 0, ctx->stream, d2, s2,
+                           groups, per, ns);
+    else if (vec2 && group == 3 && ctx->tune_reduce != 2)
+        hipLaunchKernelGGL((k_reduce_or_g<3>), dim3(g), dim3(kBlock), 0, ctx->stream, d2, s2,
+                           groups, per, ns);
+    else if (vec2 && group == 4 && ctx->tune_reduce != 2)
+        hipLaunchKernelGGL((k_reduce_or_g<4>), dim3(g), dim3(kBlock), 0, ctx->stream, d2, s2,
+                           groups, per, ns);
+    else if (vec2)
         hipLaunchKernelGGL((k_reduce_or<true>), dim3(g), dim3(kBlock), 0, ctx->stream,
                            (u64*)dst, (const u64*)src, groups, group, wr, ns);
     else

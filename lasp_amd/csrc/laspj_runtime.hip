@@ -221,6 +221,11 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
         case LASPJ_TUNE_STREAM_NT:
             ctx->tune_nt = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_REDUCE_KERNEL:
+            if (value < 0 || value > 2)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: reduce kernel must be 0..2");
+            ctx->tune_reduce = value;
+            return LASPJ_OK;
         case LASPJ_TUNE_ETF_KERNEL:
             if (value < 0 || value > 3)
                 return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..3");

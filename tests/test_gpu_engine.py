@@ -170,6 +170,28 @@ def test_orset_threshold_broadcast(ctx, tokens):
         assert got[i] == orc.ORDict.from_cells(cur[i], tokens).is_inflation_of(Dt)
 
 
+@pytest.mark.parametrize("e_n", [256, 100, 4096])
+def test_orset_reduce_all_kernels(ctx, e_n):
+    """Every reduce kernel (LASPJ_TUNE_REDUCE_KERNEL 0 flat sweep for power-of-two
+    replica lengths, 1 per-replica segments with a compile-time group, 2 generic) for
+    groups 2..5 equals the OR over each group of replicas."""
+    from lasp_amd._lib import TUNE_REDUCE_KERNEL
+    for group in (2, 3, 4, 5):
+        ng = 37
+        src = ctx.orset_batch(group * ng, e_n)
+        src.fill_synthetic(60 + group)
+        hs = src.download()
+        want = np.bitwise_or.reduce(hs.reshape(ng, group, e_n, 2), axis=1)
+        try:
+            for knob in (0, 1, 2):
+                ctx.set_tuning(TUNE_REDUCE_KERNEL, knob)
+                dst = ctx.orset_batch(ng, e_n)
+                dst.reduce_from(src, group)
+                assert np.array_equal(dst.download(), want), (group, knob)
+        finally:
+            ctx.set_tuning(TUNE_REDUCE_KERNEL, 0)
+
+
 def test_orset_equal(ctx):
     a, b = ctx.orset_batch(8, E), ctx.orset_batch(8, E)
     a.fill_synthetic(5)

@@ -85,7 +85,21 @@ def kernels(ctx, R, E, steps):
     src = ctx.orset_batch(3 * g, E)
     dst = ctx.orset_batch(g, E)
     src.fill_synthetic(4)
-    report("orset_reduce_n3", timed(ctx, lambda: dst.reduce_from(src, 3), steps),
+    for knob, name in ((0, "orset_reduce_n3"), (1, "orset_reduce_n3_segments"),
+                       (2, "orset_reduce_n3_generic")):
+        ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, knob)
+        report(name, timed(ctx, lambda: dst.reduce_from(src, 3), steps),
+               64 * g * E, g * E, "dst_cells_per_s")
+    ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, 0)
+    for grp in (2, 4):
+        src2 = ctx.orset_batch(grp * (g // 2), E)
+        dst2 = ctx.orset_batch(g // 2, E)
+        report(f"orset_reduce_n{grp}_half", timed(ctx, lambda: dst2.reduce_from(src2, grp), steps),
+               16 * (grp + 1) * (g // 2) * E, (g // 2) * E, "dst_cells_per_s")
+        del src2, dst2
+    # the same N = 3 fold with the replies laid out chunk-major (reply j of every group
+    # contiguous, as the anti-entropy receive buffer is): laspj_batch_reduce_chunks
+    report("orset_reduce_chunks_n3", timed(ctx, lambda: dst.reduce_chunks(src, 3), steps),
            64 * g * E, g * E, "dst_cells_per_s")
     del src, dst, a, b
     h = R // 2                      # CONCAT output is 32 B per cell: half the replicas
