@@ -211,6 +211,10 @@ def main():
         # torch first: its bundled HIP runtime is then the one liblaspj binds to
         import torch
         import torch.distributed as dist
+        # one GPU per local rank; more ranks than GPUs (a rehearsal on a smaller box)
+        # share them round-robin
+        ndev = torch.cuda.device_count()
+        local = local % ndev if ndev else local
         torch.cuda.set_device(local)
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 

@@ -584,3 +584,44 @@ def test_orset_product_wide_any_token_slots(ctx, tokens):
     vis = P.value_bits()[0]
     # visible: x live in both rows; y = 0 live, y = 1 all tombstoned -> cells 0 and 2
     assert int(vis[0]) & 0xF == 0b0101
+
+
+def test_concurrent_callers_one_context(ctx):
+    """Re-entrancy (vnodes call merge concurrently from many BEAM
+    schedulers): 8 host threads share one context, each joining / counting / checking
+    inflation on its own batches in a loop (ctypes drops the GIL in every call); every
+    result equals the single-threaded one."""
+    import threading
+    n, e_n, T, iters = 64, 512, 8, 25
+    jobs = []
+    for t in range(T):
+        a, b, c = (ctx.orset_batch(n, e_n) for _ in range(3))
+        a.fill_synthetic(200 + t)
+        b.fill_synthetic(300 + t)
+        c.join(a, b)
+        jobs.append((a, b, c, c.download(), c.stats(), c.value_bits()))
+    errors = []
+
+    def work(t):
+        a, b, c, want, st, vis = jobs[t]
+        try:
+            for _ in range(iters):
+                c.join(a, b)
+                if not np.array_equal(c.stats(), st):
+                    errors.append((t, "stats"))
+                if not c.is_inflation_of(a).all() or not c.is_inflation_of(b).all():
+                    errors.append((t, "inflation"))
+                if not np.array_equal(c.value_bits(), vis):
+                    errors.append((t, "value"))
+            if not np.array_equal(c.download(), want):
+                errors.append((t, "join"))
+        except Exception as e:                      # surfaced below
+            errors.append((t, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors[:5]
