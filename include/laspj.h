@@ -126,6 +126,8 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         the replica length is a power of two and
                                         2 <= group <= 4, 1 = per-replica segments with a
                                         compile-time group, 2 = generic segments        */
+#define LASPJ_TUNE_PRODUCT_ROWS  6   /* rows per outer-product tile: 0 = default (256),
+                                        32, 64, 128, 256                                */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

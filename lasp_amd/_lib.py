@@ -25,6 +25,7 @@ OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK, OPST_KEY_EXISTS = 0, 1, 2, 3
 TUNE_STREAM_GRID, TUNE_STREAM_UNROLL, TUNE_STREAM_NT, TUNE_ETF_KERNEL = 1, 2, 3, 4
 TUNE_REDUCE_KERNEL = 5
+TUNE_PRODUCT_ROWS = 6
 
 
 class LaspjUnavailable(RuntimeError):

@@ -4,7 +4,7 @@
 //   intersection  per-slot select into 32-byte CONCAT cells {pL, rL, pR, rR}: the
 //                 reference's token list for a kept element is Cx ++ Cy
 //                 (lasp_lattice:orset_causal_union/2), so both halves are kept as is.
-//   product       LDS-tiled outer product: a 64-row x 1024-column tile stages the two
+//   product       LDS-tiled outer product: a 256-row x 1024-column tile stages the two
 //                 input strips once as packed 16-bit {p8, r8} words, then every lane
 //                 writes 4 cells (16 B, dwordx4, non-temporal) per row; output is 4 B
 //                 per (x, y) cell, i.e. the product is write-bound at |L|*|R|*4 B.
@@ -77,7 +77,7 @@ hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const las
 
 // ------------------------------------------------------------------ product (OR-Set)
 
-constexpr int kPX = 64;     // rows per tile
+constexpr int kPX = 256;    // rows per tile (profiles/r01_suite_product_rows.log: 256 > 128 > 64)
 constexpr int kPY = 1024;   // columns per tile = 4 per lane
 
 __device__ __forceinline__ uint32_t pack8(u64x2 c, uint32_t* flag) {
@@ -85,32 +85,32 @@ __device__ __forceinline__ uint32_t pack8(u64x2 c, uint32_t* flag) {
     return c.x ? (uint32_t)((c.x & 0xFFull) | ((c.y & 0xFFull) << 8)) : 0u;
 }
 
-template <bool ALIGNED>
+template <bool ALIGNED, int PX>
 __global__ __launch_bounds__(kB) void k_orset_product(uint32_t* out, const u64x2* L,
                                                       const u64x2* R, uint64_t reps,
                                                       uint32_t EL, uint32_t ER,
                                                       uint64_t cstride, uint32_t* flag) {
     __shared__ __attribute__((aligned(16))) uint32_t ry[kPY];
-    __shared__ uint32_t lx[kPX];
-    const uint64_t tx_n = (EL + kPX - 1) / kPX, ty_n = (ER + kPY - 1) / kPY;
+    __shared__ uint32_t lx[PX];
+    const uint64_t tx_n = (EL + PX - 1) / PX, ty_n = (ER + kPY - 1) / kPY;
     const uint64_t tiles = reps * tx_n * ty_n;
     for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
         uint64_t rep = t / (tx_n * ty_n);
         uint64_t rem = t - rep * tx_n * ty_n;
         uint32_t tx = (uint32_t)(rem / ty_n), ty = (uint32_t)(rem - (uint64_t)tx * ty_n);
-        uint32_t x0 = tx * kPX, y0 = ty * kPY;
+        uint32_t x0 = tx * PX, y0 = ty * kPY;
         for (int i = threadIdx.x; i < kPY; i += kB) {
             uint32_t y = y0 + i;
             ry[i] = y < ER ? pack8(ldnt(R + rep * ER + y), flag) << 16 : 0u;
         }
-        for (int i = threadIdx.x; i < kPX; i += kB) {
+        for (int i = threadIdx.x; i < PX; i += kB) {
             uint32_t x = x0 + i;
             lx[i] = x < EL ? pack8(ldnt(L + rep * EL + x), flag) : 0u;
         }
         __syncthreads();
         const uint32_t yl = threadIdx.x * 4;
         u32x4 ryv = *reinterpret_cast<const u32x4*>(&ry[yl]);
-        const uint32_t rows = min((uint32_t)kPX, EL - x0);
+        const uint32_t rows = min((uint32_t)PX, EL - x0);
         for (uint32_t rr = 0; rr < rows; ++rr) {
             uint32_t lv = lx[rr];
             u32x4 v;
@@ -162,20 +162,20 @@ hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_ba
                            r->elements);
         return hipGetLastError();
     }
-    uint64_t tiles = l->replicas * ((l->elements + kPX - 1) / kPX) *
+    const int px = ctx->tune_product_rows > 0 ? (int)ctx->tune_product_rows : kPX;
+    uint64_t tiles = l->replicas * ((l->elements + px - 1) / px) *
                      ((r->elements + kPY - 1) / kPY);
     uint64_t g = tiles < (uint64_t)ctx->cus * 32 ? tiles : (uint64_t)ctx->cus * 32;
     auto* o = reinterpret_cast<uint32_t*>(dst->dev);
     auto* L = reinterpret_cast<const u64x2*>(l->dev);
     auto* R = reinterpret_cast<const u64x2*>(r->dev);
-    if (r->elements % 4 == 0)
-        hipLaunchKernelGGL(k_orset_product<true>, dim3((unsigned)g), dim3(kB), 0, ctx->stream, o,
-                           L, R, l->replicas, l->elements, r->elements,
-                           2 * dst->words_per_replica, flag);
-    else
-        hipLaunchKernelGGL(k_orset_product<false>, dim3((unsigned)g), dim3(kB), 0, ctx->stream,
-                           o, L, R, l->replicas, l->elements, r->elements,
-                           2 * dst->words_per_replica, flag);
+    const bool al = r->elements % 4 == 0;
+    auto k = al ? k_orset_product<true, kPX> : k_orset_product<false, kPX>;
+    if (px == 128) k = al ? k_orset_product<true, 128> : k_orset_product<false, 128>;
+    if (px == 64) k = al ? k_orset_product<true, 64> : k_orset_product<false, 64>;
+    if (px == 32) k = al ? k_orset_product<true, 32> : k_orset_product<false, 32>;
+    hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(kB), 0, ctx->stream, o, L, R, l->replicas,
+                       l->elements, r->elements, 2 * dst->words_per_replica, flag);
     return hipGetLastError();
 }
 

@@ -221,6 +221,11 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
         case LASPJ_TUNE_STREAM_NT:
             ctx->tune_nt = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_PRODUCT_ROWS:
+            if (!(value == 0 || value == 32 || value == 64 || value == 128 || value == 256))
+                return fail(ctx, LASPJ_E_INVAL, "tuning: product rows must be 0,32,64,128,256");
+            ctx->tune_product_rows = value;
+            return LASPJ_OK;
         case LASPJ_TUNE_REDUCE_KERNEL:
             if (value < 0 || value > 2)
                 return fail(ctx, LASPJ_E_INVAL, "tuning: reduce kernel must be 0..2");

@@ -356,7 +356,7 @@ def test_full_size_join_properties(ctx):
 
 
 def test_orset_product_tiles_and_tails(ctx):
-    """Outer-product tiling: EL and ER off the 64 x 1024 tile, several replicas; every
+    """Outer-product tiling: EL and ER off the 32..256 x 1024 tiles, several replicas; every
     cell equals {pX8, rX8, pY8, rY8} of its row / column (0 where either is absent)."""
     n, el, er = 3, 130, 1027
     l = _synth(71, n, el)
@@ -366,8 +366,18 @@ def test_orset_product_tiles_and_tails(ctx):
     L, Rb = ctx.orset_batch(n, el), ctx.orset_batch(n, er)
     L.upload(l)
     Rb.upload(r)
-    P = L.product(Rb)
-    got = P.download()
+    from lasp_amd._lib import TUNE_PRODUCT_ROWS
+    outs = []
+    try:
+        for rows in (32, 64, 128, 0):                # every tile height; default last
+            ctx.set_tuning(TUNE_PRODUCT_ROWS, rows)
+            P = L.product(Rb)
+            outs.append(P.download())
+    finally:
+        ctx.set_tuning(TUNE_PRODUCT_ROWS, 0)
+    got = outs[-1]
+    for o in outs[:-1]:
+        assert np.array_equal(o, got)
     lx = np.where(l[:, :, 0] != 0, l[:, :, 0] | (l[:, :, 1] << np.uint64(8)), 0).astype(np.uint32)
     ry = np.where(r[:, :, 0] != 0, (r[:, :, 0] << np.uint64(16)) | (r[:, :, 1] << np.uint64(24)), 0
                   ).astype(np.uint32)

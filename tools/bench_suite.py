@@ -200,8 +200,12 @@ def config5(ctx, steps):
     pl.upload(h)
     pr.upload(h)
     out = engine.ORSetProductBatch(ctx, 1, n, n)
-    ms = timed(ctx, lambda: pl.product(pr, out), steps)
-    report("config5_product", ms, 4 * n * n + 32 * n, n * n, "cells_per_s", el=n, er=n)
+    for rows in (0, 64, 128):                      # 0 = default tile (256 rows)
+        ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, rows)
+        ms = timed(ctx, lambda: pl.product(pr, out), steps)
+        report("config5_product" + (f"_rows{rows}" if rows else ""), ms, 4 * n * n + 32 * n,
+               n * n, "cells_per_s", el=n, er=n)
+    ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, 0)
 
 
 def etf(ctx, steps):
