@@ -119,9 +119,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_STREAM_UNROLL 2   /* 16-B cells per lane per iteration: 1,2,4,8      */
 #define LASPJ_TUNE_STREAM_NT     3   /* 1 = non-temporal loads/stores, 0 = default      */
 #define LASPJ_TUNE_ETF_KERNEL    4   /* OR-Set payload writer: 0 = record kernel when the
-                                        token images are uniform (20 KiB window),
+                                        token images are uniform (24 KiB window),
                                         1 = element staging, 2 / 3 = record kernel with a
-                                        16 / 24 KiB window                               */
+                                        16 / 20 KiB window                               */
 #define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = flat sweep when
                                         the replica length is a power of two and
                                         2 <= group <= 4, 1 = per-replica segments with a

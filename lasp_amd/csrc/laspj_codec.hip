@@ -661,13 +661,47 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
     u32x4* win4 = reinterpret_cast<u32x4*>(win);
     const uint32_t tid = threadIdx.x, hdr = tag >= 0 ? 2u : 0u;
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    // a block owns a contiguous run of replicas, whose payloads are contiguous too: the
+    // carry flows from one payload into the next and only the run's two ends need
+    // byte stores
+    const uint64_t per_blk = (R + gridDim.x - 1) / gridDim.x;
+    const uint64_t r_begin = (uint64_t)blockIdx.x * per_blk;
+    const uint64_t r_end = r_begin + per_blk < R ? r_begin + per_blk : R;
+    if (r_begin >= R) return;
     for (uint32_t x = tid; x < (WIN + 2 * kGuard) / 16; x += kBlock)
         reinterpret_cast<u32x4*>(winbuf)[x] = u32x4{0, 0, 0, 0};
     __syncthreads();
     const u64* cw = reinterpret_cast<const u64*>(cells);
-    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+    // one chunk per replica: the element, its term-order token slots, header template
+    // and the next replica's cell stay in registers across the run
+    const bool single = E <= kBlock;
+    uint32_t e_c = 0, hl_c = 0;
+    u32x4 o_c = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, h_c = {0, 0, 0, 0};
+    u64x2 v_next = {0, 0};
+    if (single && tid < E) {
+        e_c = d.elem_order[tid];
+        hl_c = d.elem_off[e_c + 1] - d.elem_off[e_c] + 3u;
+        o_c = *reinterpret_cast<const u32x4*>(d.tok_order + 64ull * e_c);
+        if (hl_c <= 16) h_c = *reinterpret_cast<const u32x4*>(d.ehdr_pad + d.ehdr_poff[e_c]);
+        v_next = cells[r_begin * E + e_c];
+    }
+    u64 mask_lo = offs[r_begin];    // output bytes below this belong to another block
+    u64 seg_lo = mask_lo;           // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
+    for (uint64_t rep = r_begin; rep < r_end; ++rep) {
         const u64x2* c = cells + rep * E;
         const u64 base = offs[rep], end = offs[rep + 1];
+        if (seg_lo != base) {
+            // the previous payload broke off (sizes disagreed): flush, restart at base
+            if (tid < 16) {
+                const u64 g = (seg_lo & ~15ull) + tid;
+                if (g >= mask_lo && g < seg_lo)
+                    out[g] = (uint8_t)(win[tid >> 2] >> (8 * (tid & 3)));
+            }
+            __syncthreads();
+            if (tid == 0) win4[0] = u32x4{0, 0, 0, 0};
+            __syncthreads();
+            seg_lo = mask_lo = base;
+        }
         // present elements (the list header's length field): counted up front when the
         // replica spans several chunks, else taken from the one chunk's scan
         uint32_t n = 0;
@@ -679,7 +713,6 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             n = (uint32_t)n64;
         }
         u64 cursor = 0;                             // next element byte
-        u64 seg_lo = base;      // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
         for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
             const bool last = c0 + kBlock >= E;
             // ---- A: element sizes, term-order token masks, record numbering
@@ -687,12 +720,13 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             uint32_t e = 0, sz = 0, nt = 0, hl = 0;
             u64 pt = 0, rt = 0;
             if (i < E) {
-                e = d.elem_order[i];
-                const u64x2 v = c[e];
+                e = single ? e_c : d.elem_order[i];
+                const u64x2 v = single ? v_next : c[e];
+                if (single && rep + 1 < r_end) v_next = c[E + e];       // next replica
                 if (v.x) {
                     const u32x4* ord = reinterpret_cast<const u32x4*>(d.tok_order + 64ull * e);
                     for (uint32_t j16 = 0; j16 < RK; j16 += 16) {
-                        const u32x4 o = ord[j16 >> 4];
+                        const u32x4 o = (single && j16 == 0) ? o_c : ord[j16 >> 4];
                         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
                         for (int b = 0; b < 16; ++b) {
@@ -705,7 +739,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     }
                     rt &= pt;
                     nt = (uint32_t)__popcll(pt);
-                    hl = d.elem_off[e + 1] - d.elem_off[e] + 3u;
+                    hl = single ? hl_c : d.elem_off[e + 1] - d.elem_off[e] + 3u;
                     sz = hl + 4u + nt * (RL + 8u) - (uint32_t)__popcll(rt) + 1u;
                 }
             }
@@ -761,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     if (overlaps<WIN>(r0, sz)) {
                         if (hl <= 16) {
                             if (overlaps<WIN>(r0, hl)) {
-                                const u32x4 h = *reinterpret_cast<const u32x4*>(
+                                const u32x4 h = single ? h_c : *reinterpret_cast<const u32x4*>(
                                     d.ehdr_pad + d.ehdr_poff[e]);
                                 const uint32_t w[4] = {h.x, h.y, h.z, h.w};
                                 or_piece<4>(win, r0, w, 16);
@@ -834,11 +868,11 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                 for (uint32_t m = tid; m < full; m += kBlock) {
                     const u64 g = A + 16ull * m;
                     const u32x4 v = win4[m];
-                    if (g >= base) {
+                    if (g >= mask_lo) {
                         __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + g));
                     } else {
                         const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-                        for (uint32_t b = (uint32_t)(base - g); b < 16; ++b)
+                        for (uint32_t b = (uint32_t)(mask_lo - g); b < 16; ++b)
                             out[g + b] = (uint8_t)(vw[b >> 2] >> (8 * (b & 3)));
                     }
                     win4[m] = u32x4{0, 0, 0, 0};
@@ -857,15 +891,11 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             seg_lo = seg_hi;
             cursor += tot;
         }
-        // flush the carry: bytes [floor16(seg_lo), seg_lo) that belong to this payload
-        if (tid < 16) {
-            const u64 g = (seg_lo & ~15ull) + tid;
-            if (g >= base && g < seg_lo)
-                out[g] = (uint8_t)(win[tid >> 2] >> (8 * (tid & 3)));
-        }
-        __syncthreads();
-        if (tid == 0) win4[0] = u32x4{0, 0, 0, 0};
-        __syncthreads();
+    }
+    // flush the carry at the end of the run: bytes [floor16(seg_lo), seg_lo)
+    if (tid < 16) {
+        const u64 g = (seg_lo & ~15ull) + tid;
+        if (g >= mask_lo && g < seg_lo) out[g] = (uint8_t)(win[tid >> 2] >> (8 * (tid & 3)));
     }
 }
 
@@ -1057,10 +1087,19 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
     uint64_t cap = (uint64_t)ctx->cus * 8;
     int grid = (int)(R < cap ? R : cap);
     if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf != 1) {
-        // window size (profiles/r01_suite_etf_windows.log): 0 = 20 KiB; 2, 3 = 16, 24 KiB
-        auto k = k_orset_etf_write_rec<20480>;
+        // window size (profiles/r01_suite_etf_windows.log): 0 = 24 KiB; 2, 3 = 16, 20 KiB
+        auto k = k_orset_etf_write_rec<24576>;
         if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384>;
-        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<24576>;
+        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480>;
+        // one resident wave of blocks, each with a contiguous run of replicas
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||
+            occ < 1) {
+            hipGetLastError();
+            occ = 4;
+        }
+        const uint64_t resident = (uint64_t)ctx->cus * (uint64_t)occ;
+        grid = (int)(R < resident ? R : resident);
         hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),

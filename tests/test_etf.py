@@ -251,7 +251,7 @@ def test_gpu_orset_large_synthetic_batch():
 def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3)):
     """fn() under the record kernel (LASPJ_TUNE_ETF_KERNEL 0, chosen for uniform token
     images), the element-staging kernels (1) and the record kernel's other window
-    sizes (2, 3: 16 and 24 KiB)."""
+    sizes (2, 3: 16 and 20 KiB)."""
     from lasp_amd._lib import TUNE_ETF_KERNEL
     out = []
     try:

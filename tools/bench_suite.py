@@ -247,7 +247,7 @@ def etf(ctx, steps):
         # record kernel (default for uniform token images), then the staging kernels
         variants = ((0, "write"), (1, "write_staging"))
         if os.environ.get("ETF_WINDOWS"):
-            variants += ((2, "write_w16k"), (3, "write_w24k"))
+            variants += ((2, "write_w16k"), (3, "write_w20k"))
         for knob, name in variants:
             ctx.set_tuning(_lib.TUNE_ETF_KERNEL, knob)
             ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
