@@ -50,8 +50,9 @@ def parse():
                     help="PMC summary giving HBM traffic per join launch")
     ap.add_argument("--antientropy", choices=["auto", "on", "off"], default="auto",
                     help="config-3 gossip anti-entropy leg (auto: when N > 1)")
-    ap.add_argument("--ae-objects", type=int, default=1 << 18,
-                    help="objects per GPU for the anti-entropy leg (2^18 x 4096 = 16 GiB)")
+    ap.add_argument("--ae-objects", type=int, default=1 << 20,
+                    help="objects per GPU for the anti-entropy leg: BASELINE config 3, "
+                         "2^20 x 4096 = 64 GiB of state (+ 64 GiB receive buffer)")
     ap.add_argument("--ae-rounds", type=int, default=3)
     ap.add_argument("--gc-objects", type=int, default=1 << 22,
                     help="G-Counters per GPU for the all_reduce(MAX) leg (x 64 actors x 8 B)")
