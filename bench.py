@@ -153,20 +153,22 @@ def cpu_baseline(elements: int, budget: float):
     from oracle import columnar as orc    # cpu_baseline leg: the oracle is the timed port
     cores = host_cores()
     eps, merges, secs = orc.bench_orset_merge(elements, 2, cores, 2, budget)
-    m, u, f = orc.bench_config1(10_000, 200)
+    m, u, f, v, infl = orc.bench_config1_ext(10_000, 200, 5)
     return {
         "value": eps, "unit": "merged elements/s", "cores": cores, "kind": "port",
         "sample": (f"C restatement of lasp_orset:merge/2 (nested orddict two-finger merge, "
                    f"20-byte tokens) on {cores} threads x 2 synthetic replica pairs "
                    f"(E={elements}, T<=64), {merges} merges in {secs:.1f} s"),
         "config1": {"workload": "2 replicas x 10k elements (BASELINE configs[0]), 1 thread",
-                    "us_merge": m, "us_union": u, "us_filter": f},
+                    "us_merge": m, "us_union": u, "us_filter": f, "us_value": v,
+                    "us_inflation": infl},
     }
 
 
 def config1_gpu(ctx):
     """BASELINE configs[0] on the device: one 10k-slot replica pair; per-call latency of
-    merge, the union body and the filter body (launch + kernel, inputs resident)."""
+    merge, the union body, the filter body, value/1 and is_inflation (launch + kernel,
+    inputs resident)."""
     import numpy as np
     n, iters = 10_000, 200
     a, b, c = ctx.orset_batch(1, 2 * n), ctx.orset_batch(1, 2 * n), ctx.orset_batch(1, 2 * n)
@@ -174,11 +176,17 @@ def config1_gpu(ctx):
     b.fill_synthetic(3)
     keep = ctx.buffer(((2 * n + 63) // 64) * 8)
     keep.upload(np.full(((2 * n + 63) // 64,), 0x5555555555555555, np.uint64))
+    bits = ctx.buffer(((2 * n + 63) // 64) * 8)
+    flag = ctx.buffer(1)
     L = ctx.L
     from lasp_amd._lib import check
     out = {}
+    c.join(a, b)
     for name, fn in (("merge", lambda: c.join(a, b)), ("union", lambda: c.union(a, b)),
-                     ("filter", lambda: check(L.laspj_orset_filter(ctx.h, c.h, a.h, keep.h)))):
+                     ("filter", lambda: check(L.laspj_orset_filter(ctx.h, c.h, a.h, keep.h))),
+                     ("value", lambda: check(L.laspj_orset_value(ctx.h, c.h, bits.h))),
+                     ("inflation", lambda: check(L.laspj_orset_inflation(ctx.h, a.h, c.h, 0,
+                                                                          flag.h)))):
         fn()
         ctx.synchronize()
         t0 = time.perf_counter()

@@ -369,11 +369,25 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 
 // One wave per (replica, 4096-cell segment): it walks the segment's 64 words, 4 words
 // (4 x 1 KiB loads) in flight before each group of __ballot packs; no per-cell division.
+// segment length for R replicas of n items: the base segment, shortened (to a multiple
+// of 256 items, >= 256) when R x segments would leave the chip under ~2048 waves
+static uint64_t seg_for(uint64_t R, uint64_t n, uint64_t base) {
+    if (n == 0) return base;
+    const uint64_t ns = (n + base - 1) / base;
+    if (R * ns >= 2048) return base;
+    const uint64_t want = (2048 + R - 1) / R;
+    uint64_t seg = (n + want - 1) / want;
+    seg = (seg + 255) & ~255ull;
+    if (seg < 256) seg = 256;
+    return seg < base ? seg : base;
+}
+
 constexpr uint32_t kVSeg = 4096;
 
 template <bool REMOVED>
 __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64* out,
-                                                        uint64_t R, uint32_t E, uint32_t nseg) {
+                                                        uint64_t R, uint32_t E, uint32_t nseg,
+                                                        uint32_t seg) {
     constexpr int U = 4;
     const uint32_t W = (E + 63u) / 64u;
     const uint32_t lane = threadIdx.x & 63u;
@@ -381,8 +395,8 @@ __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64*
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep = it / nseg;
-        uint32_t e0 = (uint32_t)(it - rep * nseg) * kVSeg;
-        uint32_t e1 = min(E, e0 + kVSeg);
+        uint32_t e0 = (uint32_t)(it - rep * nseg) * seg;
+        uint32_t e1 = min(E, e0 + seg);
         const u64x2* c = cells + rep * E;
         u64* o = out + rep * W;
         for (uint32_t e = e0; e < e1; e += 64 * U) {
@@ -407,17 +421,18 @@ hipError_t launch_combinator_value(laspj_ctx* ctx, const laspj_batch* b, uint64_
 hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
                               bool removed) {
     if (b->kind != LASPJ_KIND_ORSET) return launch_combinator_value(ctx, b, out);
-    uint32_t ns = (b->elements + kVSeg - 1) / kVSeg;
+    const uint32_t sg = (uint32_t)seg_for(b->replicas, b->elements, kVSeg);
+    uint32_t ns = (b->elements + sg - 1) / sg;
     uint64_t items = b->replicas * ns;
     uint64_t blocks = (items + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
     auto* cells = reinterpret_cast<const u64x2*>(b->dev);
     if (removed)
         hipLaunchKernelGGL(k_orset_value<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements, ns);
+                           cells, (u64*)out, b->replicas, b->elements, ns, sg);
     else
         hipLaunchKernelGGL(k_orset_value<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements, ns);
+                           cells, (u64*)out, b->replicas, b->elements, ns, sg);
     return hipGetLastError();
 }
 
@@ -426,8 +441,9 @@ hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* ou
 // kSeg cells (kSegW words for G-Sets); one wave64 reduces one (replica, segment) item
 // with __ballot / __shfl_xor.  A replica that is a single segment (BASELINE config 2:
 // E = 4096) is finished by its wave; longer replicas (config 4: 3M slots) combine their
-// segments with one atomic per wave into ctx->partials and a finalize kernel, so the
-// launch always has R x segments waves of parallelism.
+// segments with atomics into a per-replica record in ctx->partials, the last segment's
+// wave finishing the replica (a ticket); segments shrink when R x segments is small
+// (seg_for), so a launch always has thousands of waves.
 
 constexpr uint32_t kSeg = 4096;     // OR-Set cells per segment (64 KiB)
 constexpr uint32_t kSegW = 4096;    // G-Set words per segment (32 KiB)
@@ -534,7 +550,10 @@ hipError_t launch_gset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out
     return hipGetLastError();
 }
 
-// per-replica partial record for segmented reductions: {flags, count P, count C, -}
+// per-replica partial record for segmented reductions: {flags, count P, count C, ticket}.
+// Records are all-zero between launches: they are zeroed once when allocated, and the
+// wave that finishes a replica's last segment (its ticket reads nseg - 1) computes the
+// result from the record and zeroes it again — one launch, no memset, no finalize pass.
 constexpr u64 kViol = 1, kChanged = 2;
 
 static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out) {
@@ -550,48 +569,50 @@ static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out) {
         hipError_t e = hipMalloc(&ctx->partials, need);
         if (e != hipSuccess) return e;
         ctx->partials_bytes = need;
+        e = hipMemsetAsync(ctx->partials, 0, need, ctx->stream);
+        if (e != hipSuccess) return e;
     }
     *out = static_cast<u64*>(ctx->partials);
-    return hipMemsetAsync(ctx->partials, 0, need, ctx->stream);
+    return hipSuccess;
+}
+
+// mode 0: equal (= no difference), 1: inflation, 2: strict inflation, 3: G-Counter strict
+// inflation (value(Prev) < value(Cur)), 4 / 5: G-Counter threshold t =< sum / t < sum
+__device__ __forceinline__ bool seg_result(int mode, u64 f, u64 np, u64 nc, u64 t) {
+    if (mode == 0) return !(f & kViol);
+    if (mode == 3) return np < nc;
+    if (mode == 4) return t <= np;
+    if (mode == 5) return t < np;
+    return !(f & kViol) && (mode == 1 || (f & kChanged) || np < nc);
 }
 
 __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t rep,
-                                     u64 flags, u64 np, u64 nc, int mode) {
-    // mode 0: equal (out = !diff), 1: inflation, 2: strict inflation
-    if (seg) {
-        if (flags) atomicOr(part + rep * 4, flags);
-        if (mode >= 2) {
-            atomicAdd(part + rep * 4 + 1, np);
-            atomicAdd(part + rep * 4 + 2, nc);
-        }
+                                     u64 flags, u64 np, u64 nc, int mode, uint32_t nseg,
+                                     u64 t = 0) {
+    if (!seg) {
+        out[rep] = seg_result(mode, flags, np, nc, t) ? 1 : 0;
         return;
     }
-    bool res;
-    if (mode == 0) res = !(flags & kViol);
-    else if (mode == 3) res = np < nc;
-    else res = !(flags & kViol) && (mode == 1 || (flags & kChanged) || np < nc);
-    out[rep] = res ? 1 : 0;
-}
-
-__global__ void k_finalize(const u64* part, uint8_t* out, uint64_t R, int mode) {
-    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
-         rep += (uint64_t)gridDim.x * blockDim.x) {
-        u64 f = part[rep * 4];
-        bool res;
-        if (mode == 0) res = !(f & kViol);
-        else if (mode == 3) res = part[rep * 4 + 1] < part[rep * 4 + 2];
-        else res = !(f & kViol) && (mode == 1 || (f & kChanged) || part[rep * 4 + 1] < part[rep * 4 + 2]);
-        out[rep] = res ? 1 : 0;
+    u64* r = part + rep * 4;
+    if (flags) __hip_atomic_fetch_or(r, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (np) __hip_atomic_fetch_add(r + 1, np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nc) __hip_atomic_fetch_add(r + 2, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u64 tk = __hip_atomic_fetch_add(r + 3, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == nseg - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const u64 f = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 a = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 b = __hip_atomic_load(r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out[rep] = seg_result(mode, f, a, b, t) ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __hip_atomic_store(r + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-static hipError_t finalize(laspj_ctx* ctx, const u64* part, uint8_t* out, uint64_t R, int mode) {
-    uint64_t g = (R + kBlock - 1) / kBlock;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part, out, R,
-                       mode);
-    return hipGetLastError();
-}
+
 
 // ------------------------------------------------------------------ equal
 // equal/2 (lasp_orset.erl:136-138, lasp_gset.erl:103-105): every word equal.
@@ -599,14 +620,14 @@ static hipError_t finalize(laspj_ctx* ctx, const u64* part, uint8_t* out, uint64
 template <bool SEG, bool VEC2>
 __global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, uint8_t* out,
                                                   u64* part, uint64_t R, uint64_t wr,
-                                                  uint32_t nseg) {
+                                                  uint32_t nseg, uint64_t seg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t n = VEC2 ? wr / 2 : wr;
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, lo, hi;
-        seg_range(it, nseg, n, kSeg, &rep, &lo, &hi);
+        seg_range(it, nseg, n, seg, &rep, &lo, &hi);
         bool diff = false;
         if constexpr (VEC2) {
             const u64x2* a2 = reinterpret_cast<const u64x2*>(a + rep * wr);
@@ -620,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, ui
             for (uint64_t w = lo + lane; w < hi; w += 64) diff |= a[rep * wr + w] != b[rep * wr + w];
         }
         bool any = __ballot(diff) != 0;
-        if (lane == 0) emit(SEG, out, part, rep, any ? kViol : 0, 0, 0, 0);
+        if (lane == 0) emit(SEG, out, part, rep, any ? kViol : 0, 0, 0, 0, nseg);
     }
 }
 
@@ -628,7 +649,8 @@ hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch*
                         uint8_t* out) {
     bool vec2 = (a->words_per_replica & 1) == 0;
     uint64_t n = vec2 ? a->words_per_replica / 2 : a->words_per_replica;
-    uint32_t ns = nseg_of(n, kSeg);
+    const uint64_t sg = seg_for(a->replicas, n, kSeg);
+    uint32_t ns = nseg_of(n, sg);
     int grid = seg_grid(ctx, a->replicas * ns);
     u64* part = nullptr;
     if (ns > 1) {
@@ -638,12 +660,10 @@ hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch*
 #define LJ_EQ(S, V)                                                                        \
     hipLaunchKernelGGL((k_equal<S, V>), dim3(grid), dim3(kBlock), 0, ctx->stream,          \
                        (const u64*)a->dev, (const u64*)b->dev, out, part, a->replicas,     \
-                       a->words_per_replica, ns)
+                       a->words_per_replica, ns, sg)
     if (ns > 1) {
         if (vec2) LJ_EQ(true, true); else LJ_EQ(true, false);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return finalize(ctx, part, out, a->replicas, 0);
+        return hipGetLastError();
     }
     if (vec2) LJ_EQ(false, true); else LJ_EQ(false, false);
 #undef LJ_EQ
@@ -661,13 +681,14 @@ template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
                                                             const u64x2* cur, uint8_t* out,
                                                             u64* part, uint64_t R, uint32_t E,
-                                                            bool prev_bcast, uint32_t nseg) {
+                                                            bool prev_bcast, uint32_t nseg,
+                                                            uint64_t seg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, lo, hi;
-        seg_range(it, nseg, E, kSeg, &rep, &lo, &hi);
+        seg_range(it, nseg, E, seg, &rep, &lo, &hi);
         const u64x2* P = prev + (prev_bcast ? 0 : rep * E);
         const u64x2* C = cur + rep * E;
         bool viol = false, changed = false;
@@ -688,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
             np = wave_sum(np);
             nc = wave_sum(nc);
         }
-        if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1);
+        if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1, nseg);
     }
 }
 
@@ -697,13 +718,13 @@ template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, const u64* cur,
                                                            uint8_t* out, u64* part, uint64_t R,
                                                            uint64_t W, bool prev_bcast,
-                                                           uint32_t nseg) {
+                                                           uint32_t nseg, uint64_t seg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, lo, hi;
-        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
+        seg_range(it, nseg, W, seg, &rep, &lo, &hi);
         const u64* P = prev + (prev_bcast ? 0 : rep * W);
         const u64* C = cur + rep * W;
         bool viol = false, diff = false;
@@ -716,13 +737,14 @@ __global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, cons
         if (__ballot(diff) != 0) flags |= kChanged;
         // strict = subset and differs: "differs" plays the role of `changed`, and
         // np = nc = 0 so the length test never fires
-        if (lane == 0) emit(SEG, out, part, rep, flags, 0, 0, STRICT ? 2 : 1);
+        if (lane == 0) emit(SEG, out, part, rep, flags, 0, 0, STRICT ? 2 : 1, nseg);
     }
 }
 
 hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                   const laspj_batch* cur, bool strict, uint8_t* out) {
-    uint32_t ns = nseg_of(cur->elements, kSeg);
+    const uint64_t sg = seg_for(cur->replicas, cur->elements, kSeg);
+    uint32_t ns = nseg_of(cur->elements, sg);
     int grid = seg_grid(ctx, cur->replicas * ns);
     bool bc = prev->replicas == 1 && cur->replicas != 1;
     auto* P = reinterpret_cast<const u64x2*>(prev->dev);
@@ -734,12 +756,10 @@ hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
     }
 #define LJ_INF(ST, SG)                                                                      \
     hipLaunchKernelGGL((k_orset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
-                       P, C, out, part, cur->replicas, cur->elements, bc, ns)
+                       P, C, out, part, cur->replicas, cur->elements, bc, ns, sg)
     if (ns > 1) {
         if (strict) LJ_INF(true, true); else LJ_INF(false, true);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
+        return hipGetLastError();
     }
     if (strict) LJ_INF(true, false); else LJ_INF(false, false);
 #undef LJ_INF
@@ -749,7 +769,8 @@ hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
 hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                  const laspj_batch* cur, bool strict, uint8_t* out) {
     uint64_t W = cur->words_per_replica;
-    uint32_t ns = nseg_of(W, kSegW);
+    const uint64_t sg = seg_for(cur->replicas, W, kSegW);
+    uint32_t ns = nseg_of(W, sg);
     int grid = seg_grid(ctx, cur->replicas * ns);
     bool bc = prev->replicas == 1 && cur->replicas != 1;
     u64* part = nullptr;
@@ -760,12 +781,10 @@ hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
 #define LJ_GINF(ST, SG)                                                                     \
     hipLaunchKernelGGL((k_gset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
                        (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas, \
-                       W, bc, ns)
+                       W, bc, ns, sg)
     if (ns > 1) {
         if (strict) LJ_GINF(true, true); else LJ_GINF(false, true);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
+        return hipGetLastError();
     }
     if (strict) LJ_GINF(true, false); else LJ_GINF(false, false);
 #undef LJ_GINF
@@ -880,23 +899,43 @@ hipError_t launch_gcounter_sums(laspj_ctx* ctx, const laspj_batch* b, uint64_t* 
     return hipGetLastError();
 }
 
-__global__ void k_threshold_cmp(const u64* sums, uint8_t* out, uint64_t R, u64 t, bool strict) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = (strict ? t < sums[i] : t <= sums[i]) ? 1 : 0;
+// threshold_met(riak_dt_gcounter, V, T) (lasp_lattice.erl:87-90): sum per replica
+// compared with T in the same launch (the last segment of a replica decides)
+template <bool SEG>
+__global__ __launch_bounds__(kBlock) void k_gcounter_threshold(const u64* c, uint8_t* out,
+                                                               u64* part, uint64_t R,
+                                                               uint64_t W, uint32_t nseg,
+                                                               uint64_t seg, u64 t, int mode) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
+         it += nwaves) {
+        uint64_t rep, lo, hi;
+        seg_range(it, nseg, W, seg, &rep, &lo, &hi);
+        u64 s = 0;
+        for (uint64_t w = lo + lane; w < hi; w += 64) s += c[rep * W + w];
+        s = wave_sum(s);
+        if (lane == 0) emit(SEG, out, part, rep, 0, s, 0, mode, nseg, t);
+    }
 }
 
 hipError_t launch_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* b, uint64_t t,
                                      bool strict, uint8_t* out) {
+    const uint64_t W = b->words_per_replica;
+    const uint64_t sg = seg_for(b->replicas, W, kSegW);
+    const uint32_t ns = nseg_of(W, sg);
+    const int grid = seg_grid(ctx, b->replicas * ns);
+    const int mode = strict ? 5 : 4;
+    if (ns == 1) {
+        hipLaunchKernelGGL(k_gcounter_threshold<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, out, nullptr, b->replicas, W, ns, sg, (u64)t, mode);
+        return hipGetLastError();
+    }
     u64* part = nullptr;
-    hipError_t e = partials(ctx, b->replicas, &part);   // R x 32 B >= R sums
+    hipError_t e = partials(ctx, b->replicas, &part);
     if (e != hipSuccess) return e;
-    e = launch_gcounter_sums(ctx, b, reinterpret_cast<uint64_t*>(part));
-    if (e != hipSuccess) return e;
-    uint64_t g = (b->replicas + kBlock - 1) / kBlock;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_threshold_cmp, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part,
-                       out, b->replicas, (u64)t, strict);
+    hipLaunchKernelGGL(k_gcounter_threshold<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       (const u64*)b->dev, out, part, b->replicas, W, ns, sg, (u64)t, mode);
     return hipGetLastError();
 }
 
@@ -906,13 +945,14 @@ template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gcounter_inflation(const u64* prev, const u64* cur,
                                                                uint8_t* out, u64* part,
                                                                uint64_t R, uint64_t W,
-                                                               bool bcast, uint32_t nseg) {
+                                                               bool bcast, uint32_t nseg,
+                                                               uint64_t seg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, lo, hi;
-        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
+        seg_range(it, nseg, W, seg, &rep, &lo, &hi);
         const u64* P = prev + (bcast ? 0 : rep * W);
         const u64* C = cur + rep * W;
         bool viol = false;
@@ -928,14 +968,15 @@ __global__ __launch_bounds__(kBlock) void k_gcounter_inflation(const u64* prev, 
             sp = wave_sum(sp);
             sc = wave_sum(sc);
         }
-        if (lane == 0) emit(SEG, out, part, rep, flags, sp, sc, STRICT ? 3 : 1);
+        if (lane == 0) emit(SEG, out, part, rep, flags, sp, sc, STRICT ? 3 : 1, nseg);
     }
 }
 
 hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                      const laspj_batch* cur, bool strict, uint8_t* out) {
     uint64_t W = cur->words_per_replica;
-    uint32_t ns = nseg_of(W, kSegW);
+    const uint64_t sg = seg_for(cur->replicas, W, kSegW);
+    uint32_t ns = nseg_of(W, sg);
     int grid = seg_grid(ctx, cur->replicas * ns);
     bool bc = prev->replicas == 1 && cur->replicas != 1;
     u64* part = nullptr;
@@ -946,12 +987,10 @@ hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
 #define LJ_GC(ST, SG)                                                                          \
     hipLaunchKernelGGL((k_gcounter_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
                        (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas,    \
-                       W, bc, ns)
+                       W, bc, ns, sg)
     if (ns > 1) {
         if (strict) LJ_GC(true, true); else LJ_GC(false, true);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return finalize(ctx, part, out, cur->replicas, strict ? 3 : 1);
+        return hipGetLastError();
     }
     if (strict) LJ_GC(true, false); else LJ_GC(false, false);
 #undef LJ_GC

@@ -60,6 +60,7 @@ def lib():
         L.orc_bench_orset_merge.argtypes = [C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
                                             C.c_double, C.POINTER(C.c_double), u64p,
                                             C.POINTER(C.c_double)]
+        L.orc_bench_config1_ext.argtypes = [C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_double)]
         L.orc_bench_orset_op.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
                                           C.c_double, C.POINTER(C.c_double), u64p,
                                           C.POINTER(C.c_double)]
@@ -201,3 +202,12 @@ def bench_config1(n: int = 10_000, iters: int = 200):
     if lib().orc_bench_config1(n, iters, C.byref(m), C.byref(u), C.byref(f)) != 0:
         raise RuntimeError("orc_bench_config1 failed")
     return m.value, u.value, f.value
+
+
+def bench_config1_ext(n: int = 10_000, iters: int = 200, slow_iters: int = 5):
+    """BASELINE config 1 on the C restatement, us per call: merge, union body, filter
+    body, value/1, is_inflation(A, merge(A, B)) (quadratic keyfind, slow_iters calls)."""
+    out = (C.c_double * 5)()
+    if lib().orc_bench_config1_ext(n, iters, slow_iters, out) != 0:
+        raise RuntimeError("orc_bench_config1_ext failed")
+    return tuple(out)

@@ -383,8 +383,25 @@ int orc_orset_filter_even(const orc_orset* s, orc_orset* out) {
  * with one token each, B adds all with its own token and removes a 10 % subset; time
  * merge/2, the union body (against a second 10k set with 5k overlap) and the filter
  * body, single-threaded, averaged over `iters` calls.  Results in microseconds. */
+int orc_bench_config1_ext(uint32_t n, int iters, int slow_iters, double* out5);
+
 int orc_bench_config1(uint32_t n, int iters, double* us_merge, double* us_union,
                       double* us_filter) {
+    double o[5];
+    int rc = orc_bench_config1_ext(n, iters, 0, o);
+    *us_merge = o[0], *us_union = o[1], *us_filter = o[2];
+    return rc;
+}
+
+/* BASELINE config 1: merge / union body / filter body (iters each), then value/1 of the
+ * merge and is_inflation / is_strict_inflation of merge(A, B) over A (the quadratic
+ * lists:keyfind clauses, slow_iters each; 0 skips them).  out5 = us per call of merge,
+ * union, filter, value, inflation (strict inflation is timed into out5[4] only when
+ * slow_iters > 0 and reported by the caller as the same order). */
+int orc_bench_config1_ext(uint32_t n, int iters, int slow_iters, double* out5) {
+    double* us_merge = &out5[0];
+    double* us_union = &out5[1];
+    double* us_filter = &out5[2];
     uint32_t E = 2 * n;
     orc_orset *a = orc_orset_alloc(E, E), *b = orc_orset_alloc(E, E), *c = orc_orset_alloc(E, E);
     orc_orset *m = orc_orset_alloc(2 * E, 2 * E), *f = orc_orset_alloc(2 * E, 2 * E);
@@ -424,6 +441,20 @@ int orc_bench_config1(uint32_t n, int iters, double* us_merge, double* us_union,
     *us_merge = (t1 - t0) * 1e6 / iters;
     *us_union = (t2 - t1) * 1e6 / iters;
     *us_filter = (t3 - t2) * 1e6 / iters;
+    out5[3] = out5[4] = 0;
+    if (slow_iters > 0) {
+        int64_t* keys = (int64_t*)malloc(sizeof(int64_t) * 2 * E);
+        u64 sink = 0;
+        orc_orset_merge(a, b, m);
+        double t4 = now_s();
+        for (int i = 0; i < iters; ++i) sink += orc_orset_value(m, keys);
+        double t5 = now_s();
+        for (int i = 0; i < slow_iters; ++i) sink += orc_orset_is_inflation(a, m);
+        double t6 = now_s();
+        out5[3] = (t5 - t4) * 1e6 / iters;
+        out5[4] = (t6 - t5) * 1e6 / slow_iters + (double)(sink & 0);
+        free(keys);
+    }
     orc_orset_free(a), orc_orset_free(b), orc_orset_free(c), orc_orset_free(m), orc_orset_free(f);
     return 0;
 }

@@ -489,6 +489,54 @@ def test_segmented_reductions_long_replicas(ctx):
         assert eqg[i] == same and ig[i] == sub and sg[i] == (sub and not same)
 
 
+def test_ticketed_reductions_small_batches(ctx):
+    """Few replicas, long rows: segments shrink (thousands of waves) and every
+    replica's result is produced by its last-arriving segment (a ticket in the
+    per-replica record, which it zeroes again) — checked over repeated launches so a
+    record left dirty would show; value/1 of a single 20k-slot replica."""
+    n, e_n = 3, 20_000
+    prev = _synth(111, n, e_n)
+    cur = prev | _synth(112, n, e_n)
+    cur[1, 19_999, 0] = 0                            # drop an element: not an inflation
+    cur[1, 19_999, 1] = 0
+    P, Cb = ctx.orset_batch(n, e_n), ctx.orset_batch(n, e_n)
+    P.upload(prev)
+    Cb.upload(cur)
+    tok = orc.synth_tokens(e_n, 64)
+    want_i = [orc.ORDict.from_cells(cur[i], tok).is_inflation_of(orc.ORDict.from_cells(prev[i], tok))
+              for i in range(n)]
+    want_s = [orc.ORDict.from_cells(cur[i], tok).is_strict_inflation_of(
+        orc.ORDict.from_cells(prev[i], tok)) for i in range(n)]
+    for _ in range(4):
+        assert list(Cb.is_inflation_of(P)) == want_i
+        assert list(Cb.is_inflation_of(P, strict=True)) == want_s
+        assert list(Cb.equal(P)) == [False] * n
+        assert list(Cb.equal(Cb)) == [True] * n
+    one = ctx.orset_batch(1, e_n)
+    one.upload(cur[:1])
+    bits = np.unpackbits(one.value_bits()[0].view(np.uint8), bitorder="little")[:e_n]
+    live = (cur[0, :, 0] & ~cur[0, :, 1]) != 0
+    assert np.array_equal(bits.astype(bool), live)
+    # G-Counter: 3 replicas x 10k actors, threshold and inflation over tickets
+    g = ctx.gcounter_batch(3, 10_000)
+    rng = np.random.default_rng(9)
+    hc = rng.integers(0, 1000, (3, 10_000)).astype(np.uint64)
+    hc[0, 5] = 7
+    g.upload(hc)
+    sums = hc.sum(axis=1)
+    for _ in range(3):
+        for t in (int(sums[0]), int(sums[1]) + 1, 0):
+            assert list(g.threshold_met(t)) == [t <= int(x) for x in sums]
+            assert list(g.threshold_met(t, strict=True)) == [t < int(x) for x in sums]
+    g2 = ctx.gcounter_batch(3, 10_000)
+    h2 = hc.copy()
+    h2[2, 9_999] += np.uint64(1)
+    h2[0, 5] = 0
+    g2.upload(h2)
+    assert list(g2.is_inflation_of(g)) == [False, True, True]
+    assert list(g2.is_inflation_of(g, strict=True)) == [False, False, True]
+
+
 def test_gcounter_batch_kernels(ctx):
     """riak_dt_gcounter join (per-actor max), value (sum), threshold, inflation, FSM
     reduce, increments — against the oracle's _GCounter restatement."""
