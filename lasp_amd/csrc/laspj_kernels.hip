@@ -369,6 +369,9 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 
 // One wave per (replica, 4096-cell segment): it walks the segment's 64 words, 4 words
 // (4 x 1 KiB loads) in flight before each group of __ballot packs; no per-cell division.
+constexpr uint64_t kTicketItems = 8192;     // see the partial-record note below
+static uint32_t fin_for(uint64_t items, uint32_t ns) { return items <= kTicketItems ? ns : 0u; }
+
 // segment length for R replicas of n items: the base segment, shortened (to a multiple
 // of 256 items, >= 256) when R x segments would leave the chip under ~2048 waves
 static uint64_t seg_for(uint64_t R, uint64_t n, uint64_t base) {
@@ -456,15 +459,69 @@ __device__ __forceinline__ void seg_range(uint64_t item, uint32_t nseg, uint64_t
     *e = min(n, *b + seg);
 }
 
+// K per-replica sums: written directly when a replica is one segment, else accumulated
+// in its record of ctx->partials and finished either by the last segment's wave
+// (fin = segments: a ticket in word 3, see `emit` below) or, for large launches
+// (fin = 0), by a finalize kernel; both re-zero the record
+template <int K>
+__device__ __forceinline__ void emit_sums(bool seg, u64* out, u64* part, uint64_t rep,
+                                          const u64 (&v)[K], uint32_t fin) {
+    if (!seg) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) out[rep * K + k] = v[k];
+        return;
+    }
+    u64* r = part + rep * 4;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (v[k]) __hip_atomic_fetch_add(r + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fin == 0) return;                 // a finalize kernel reads and re-zeroes the record
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u64 tk = __hip_atomic_fetch_add(r + 3, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == fin - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            out[rep * K + k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __hip_atomic_store(r + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int K>
+__global__ void k_finalize_sums(u64* part, u64* out, uint64_t R) {
+    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
+         rep += (uint64_t)gridDim.x * blockDim.x) {
+        u64* r = part + rep * 4;
+#pragma unroll
+        for (int k = 0; k < K; ++k) out[rep * K + k] = r[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = 0;
+    }
+}
+
+template <int K>
+static hipError_t finalize_sums(laspj_ctx* ctx, u64* part, uint64_t* out, uint64_t R) {
+    uint64_t g = (R + kBlock - 1) / kBlock;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_finalize_sums<K>, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part,
+                       (u64*)out, R);
+    return hipGetLastError();
+}
+
 template <bool SEG>
 __global__ __launch_bounds__(kBlock) void k_orset_stats(const u64x2* cells, u64* out,
-                                                        uint64_t R, uint32_t E, uint32_t nseg) {
+                                                        u64* part, uint64_t R, uint32_t E,
+                                                        uint32_t nseg, uint64_t sg,
+                                                        uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, b, e;
-        seg_range(it, nseg, E, kSeg, &rep, &b, &e);
+        seg_range(it, nseg, E, sg, &rep, &b, &e);
         const u64x2* c = cells + rep * E;
         u64 elems = 0, adds = 0, rems = 0;
 #pragma unroll 8
@@ -478,34 +535,28 @@ __global__ __launch_bounds__(kBlock) void k_orset_stats(const u64x2* cells, u64*
         adds = wave_sum(adds);
         rems = wave_sum(rems);
         if (lane == 0) {
-            if constexpr (SEG) {
-                atomicAdd(out + rep * 3 + 0, elems);
-                atomicAdd(out + rep * 3 + 1, adds);
-                atomicAdd(out + rep * 3 + 2, rems);
-            } else {
-                out[rep * 3 + 0] = elems;
-                out[rep * 3 + 1] = adds;
-                out[rep * 3 + 2] = rems;
-            }
+            const u64 v[3] = {elems, adds, rems};
+            emit_sums<3>(SEG, out, part, rep, v, fin);
         }
     }
 }
 
 template <bool SEG>
-__global__ __launch_bounds__(kBlock) void k_gset_stats(const u64* words, u64* out, uint64_t R,
-                                                       uint64_t W, uint32_t nseg) {
+__global__ __launch_bounds__(kBlock) void k_gset_stats(const u64* words, u64* out, u64* part,
+                                                       uint64_t R, uint64_t W, uint32_t nseg,
+                                                       uint64_t sg, uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, b, e;
-        seg_range(it, nseg, W, kSegW, &rep, &b, &e);
+        seg_range(it, nseg, W, sg, &rep, &b, &e);
         u64 n = 0;
         for (uint64_t w = b + lane; w < e; w += 64) n += __popcll(words[rep * W + w]);
         n = wave_sum(n);
         if (lane == 0) {
-            if constexpr (SEG) atomicAdd(out + rep, n);
-            else out[rep] = n;
+            const u64 v[1] = {n};
+            emit_sums<1>(SEG, out, part, rep, v, fin);
         }
     }
 }
@@ -519,41 +570,57 @@ static int seg_grid(const laspj_ctx* ctx, uint64_t items) {
     return blocks ? (int)blocks : 1;
 }
 
+static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out);
+
 hipError_t launch_orset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
-    uint32_t ns = nseg_of(b->elements, kSeg);
+    const uint64_t sg = seg_for(b->replicas, b->elements, kSeg);
+    uint32_t ns = nseg_of(b->elements, sg);
     int grid = seg_grid(ctx, b->replicas * ns);
     auto* cells = reinterpret_cast<const u64x2*>(b->dev);
     if (ns == 1) {
         hipLaunchKernelGGL(k_orset_stats<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, cells,
-                           (u64*)out, b->replicas, b->elements, ns);
+                           (u64*)out, nullptr, b->replicas, b->elements, ns, sg, 0u);
     } else {
-        hipError_t e = hipMemsetAsync(out, 0, b->replicas * 24, ctx->stream);
+        u64* part = nullptr;
+        hipError_t e = partials(ctx, b->replicas, &part);
         if (e != hipSuccess) return e;
+        const uint32_t fin = fin_for(b->replicas * ns, ns);
         hipLaunchKernelGGL(k_orset_stats<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, cells,
-                           (u64*)out, b->replicas, b->elements, ns);
+                           (u64*)out, part, b->replicas, b->elements, ns, sg, fin);
+        if (!fin) return finalize_sums<3>(ctx, part, out, b->replicas);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_gset_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out) {
-    uint32_t ns = nseg_of(b->words_per_replica, kSegW);
+    const uint64_t W = b->words_per_replica;
+    const uint64_t sg = seg_for(b->replicas, W, kSegW);
+    uint32_t ns = nseg_of(W, sg);
     int grid = seg_grid(ctx, b->replicas * ns);
     if (ns == 1) {
         hipLaunchKernelGGL(k_gset_stats<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, (u64*)out, b->replicas, b->words_per_replica, ns);
+                           (const u64*)b->dev, (u64*)out, nullptr, b->replicas, W, ns, sg, 0u);
     } else {
-        hipError_t e = hipMemsetAsync(out, 0, b->replicas * 8, ctx->stream);
+        u64* part = nullptr;
+        hipError_t e = partials(ctx, b->replicas, &part);
         if (e != hipSuccess) return e;
+        const uint32_t fin = fin_for(b->replicas * ns, ns);
         hipLaunchKernelGGL(k_gset_stats<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, (u64*)out, b->replicas, b->words_per_replica, ns);
+                           (const u64*)b->dev, (u64*)out, part, b->replicas, W, ns, sg, fin);
+        if (!fin) return finalize_sums<1>(ctx, part, out, b->replicas);
     }
     return hipGetLastError();
 }
 
 // per-replica partial record for segmented reductions: {flags, count P, count C, ticket}.
-// Records are all-zero between launches: they are zeroed once when allocated, and the
-// wave that finishes a replica's last segment (its ticket reads nseg - 1) computes the
-// result from the record and zeroes it again — one launch, no memset, no finalize pass.
+// Records are all-zero between launches: zeroed once when allocated, and re-zeroed by
+// whoever finishes them.  Small launches (<= kTicketItems segment items, e.g. one long
+// replica on the bind path) finish in the same launch: the wave whose ticket reads
+// fin - 1 computes the result.  Its agent-scope release / acquire fences write back and
+// invalidate the XCD's L2, which is cheap for a few hundred waves but not for 750k
+// (config 4), so large launches accumulate with plain atomics and a finalize kernel
+// reads and re-zeroes the records.
+
 constexpr u64 kViol = 1, kChanged = 2;
 
 static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out) {
@@ -587,7 +654,7 @@ __device__ __forceinline__ bool seg_result(int mode, u64 f, u64 np, u64 nc, u64 
 }
 
 __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t rep,
-                                     u64 flags, u64 np, u64 nc, int mode, uint32_t nseg,
+                                     u64 flags, u64 np, u64 nc, int mode, uint32_t fin,
                                      u64 t = 0) {
     if (!seg) {
         out[rep] = seg_result(mode, flags, np, nc, t) ? 1 : 0;
@@ -597,10 +664,11 @@ __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t
     if (flags) __hip_atomic_fetch_or(r, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (np) __hip_atomic_fetch_add(r + 1, np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (nc) __hip_atomic_fetch_add(r + 2, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fin == 0) return;                 // a finalize kernel reads and re-zeroes the record
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const u64 tk = __hip_atomic_fetch_add(r + 3, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == nseg - 1) {
+    if (tk == fin - 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const u64 f = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const u64 a = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -612,6 +680,25 @@ __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t
     }
 }
 
+__global__ void k_finalize(u64* part, uint8_t* out, uint64_t R, int mode, u64 t) {
+    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
+         rep += (uint64_t)gridDim.x * blockDim.x) {
+        u64* r = part + rep * 4;
+        out[rep] = seg_result(mode, r[0], r[1], r[2], t) ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = 0;
+    }
+}
+
+static hipError_t finalize(laspj_ctx* ctx, u64* part, uint8_t* out, uint64_t R, int mode,
+                           u64 t = 0) {
+    uint64_t g = (R + kBlock - 1) / kBlock;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream, part, out, R,
+                       mode, t);
+    return hipGetLastError();
+}
+
 
 
 // ------------------------------------------------------------------ equal
@@ -620,7 +707,7 @@ __device__ __forceinline__ void emit(bool seg, uint8_t* out, u64* part, uint64_t
 template <bool SEG, bool VEC2>
 __global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, uint8_t* out,
                                                   u64* part, uint64_t R, uint64_t wr,
-                                                  uint32_t nseg, uint64_t seg) {
+                                                  uint32_t nseg, uint64_t seg, uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t n = VEC2 ? wr / 2 : wr;
@@ -641,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void k_equal(const u64* a, const u64* b, ui
             for (uint64_t w = lo + lane; w < hi; w += 64) diff |= a[rep * wr + w] != b[rep * wr + w];
         }
         bool any = __ballot(diff) != 0;
-        if (lane == 0) emit(SEG, out, part, rep, any ? kViol : 0, 0, 0, 0, nseg);
+        if (lane == 0) emit(SEG, out, part, rep, any ? kViol : 0, 0, 0, 0, fin);
     }
 }
 
@@ -660,9 +747,11 @@ hipError_t launch_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch*
 #define LJ_EQ(S, V)                                                                        \
     hipLaunchKernelGGL((k_equal<S, V>), dim3(grid), dim3(kBlock), 0, ctx->stream,          \
                        (const u64*)a->dev, (const u64*)b->dev, out, part, a->replicas,     \
-                       a->words_per_replica, ns, sg)
+                       a->words_per_replica, ns, sg, fin)
+    const uint32_t fin = ns > 1 ? fin_for(a->replicas * ns, ns) : 0u;
     if (ns > 1) {
         if (vec2) LJ_EQ(true, true); else LJ_EQ(true, false);
+        if (!fin) return finalize(ctx, part, out, a->replicas, 0);
         return hipGetLastError();
     }
     if (vec2) LJ_EQ(false, true); else LJ_EQ(false, false);
@@ -682,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
                                                             const u64x2* cur, uint8_t* out,
                                                             u64* part, uint64_t R, uint32_t E,
                                                             bool prev_bcast, uint32_t nseg,
-                                                            uint64_t seg) {
+                                                            uint64_t seg, uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
@@ -709,7 +798,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
             np = wave_sum(np);
             nc = wave_sum(nc);
         }
-        if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1, nseg);
+        if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1, fin);
     }
 }
 
@@ -718,7 +807,8 @@ template <bool STRICT, bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, const u64* cur,
                                                            uint8_t* out, u64* part, uint64_t R,
                                                            uint64_t W, bool prev_bcast,
-                                                           uint32_t nseg, uint64_t seg) {
+                                                           uint32_t nseg, uint64_t seg,
+                                                           uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
@@ -737,7 +827,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_inflation(const u64* prev, cons
         if (__ballot(diff) != 0) flags |= kChanged;
         // strict = subset and differs: "differs" plays the role of `changed`, and
         // np = nc = 0 so the length test never fires
-        if (lane == 0) emit(SEG, out, part, rep, flags, 0, 0, STRICT ? 2 : 1, nseg);
+        if (lane == 0) emit(SEG, out, part, rep, flags, 0, 0, STRICT ? 2 : 1, fin);
     }
 }
 
@@ -756,9 +846,11 @@ hipError_t launch_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
     }
 #define LJ_INF(ST, SG)                                                                      \
     hipLaunchKernelGGL((k_orset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
-                       P, C, out, part, cur->replicas, cur->elements, bc, ns, sg)
+                       P, C, out, part, cur->replicas, cur->elements, bc, ns, sg, fin)
+    const uint32_t fin = ns > 1 ? fin_for(cur->replicas * ns, ns) : 0u;
     if (ns > 1) {
         if (strict) LJ_INF(true, true); else LJ_INF(false, true);
+        if (!fin) return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
         return hipGetLastError();
     }
     if (strict) LJ_INF(true, false); else LJ_INF(false, false);
@@ -781,9 +873,11 @@ hipError_t launch_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev,
 #define LJ_GINF(ST, SG)                                                                     \
     hipLaunchKernelGGL((k_gset_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
                        (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas, \
-                       W, bc, ns, sg)
+                       W, bc, ns, sg, fin)
+    const uint32_t fin = ns > 1 ? fin_for(cur->replicas * ns, ns) : 0u;
     if (ns > 1) {
         if (strict) LJ_GINF(true, true); else LJ_GINF(false, true);
+        if (!fin) return finalize(ctx, part, out, cur->replicas, strict ? 2 : 1);
         return hipGetLastError();
     }
     if (strict) LJ_GINF(true, false); else LJ_GINF(false, false);
@@ -866,35 +960,41 @@ hipError_t launch_reduce_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
 
 // per replica: sum of counts (mode 3 partial np/nc or plain sums)
 template <bool SEG>
-__global__ __launch_bounds__(kBlock) void k_gcounter_sums(const u64* c, u64* sums, uint64_t R,
-                                                          uint64_t W, uint32_t nseg) {
+__global__ __launch_bounds__(kBlock) void k_gcounter_sums(const u64* c, u64* sums, u64* part,
+                                                          uint64_t R, uint64_t W, uint32_t nseg,
+                                                          uint64_t sg, uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
          it += nwaves) {
         uint64_t rep, lo, hi;
-        seg_range(it, nseg, W, kSegW, &rep, &lo, &hi);
+        seg_range(it, nseg, W, sg, &rep, &lo, &hi);
         u64 s = 0;
         for (uint64_t w = lo + lane; w < hi; w += 64) s += c[rep * W + w];
         s = wave_sum(s);
         if (lane == 0) {
-            if constexpr (SEG) atomicAdd(sums + rep, s);
-            else sums[rep] = s;
+            const u64 v[1] = {s};
+            emit_sums<1>(SEG, sums, part, rep, v, fin);
         }
     }
 }
 
 hipError_t launch_gcounter_sums(laspj_ctx* ctx, const laspj_batch* b, uint64_t* sums) {
-    uint32_t ns = nseg_of(b->words_per_replica, kSegW);
+    const uint64_t W = b->words_per_replica;
+    const uint64_t sg = seg_for(b->replicas, W, kSegW);
+    uint32_t ns = nseg_of(W, sg);
     int grid = seg_grid(ctx, b->replicas * ns);
     if (ns == 1) {
         hipLaunchKernelGGL(k_gcounter_sums<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, (u64*)sums, b->replicas, b->words_per_replica, ns);
+                           (const u64*)b->dev, (u64*)sums, nullptr, b->replicas, W, ns, sg, 0u);
     } else {
-        hipError_t e = hipMemsetAsync(sums, 0, b->replicas * 8, ctx->stream);
+        u64* part = nullptr;
+        hipError_t e = partials(ctx, b->replicas, &part);
         if (e != hipSuccess) return e;
+        const uint32_t fin = fin_for(b->replicas * ns, ns);
         hipLaunchKernelGGL(k_gcounter_sums<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, (u64*)sums, b->replicas, b->words_per_replica, ns);
+                           (const u64*)b->dev, (u64*)sums, part, b->replicas, W, ns, sg, fin);
+        if (!fin) return finalize_sums<1>(ctx, part, sums, b->replicas);
     }
     return hipGetLastError();
 }
@@ -905,7 +1005,8 @@ template <bool SEG>
 __global__ __launch_bounds__(kBlock) void k_gcounter_threshold(const u64* c, uint8_t* out,
                                                                u64* part, uint64_t R,
                                                                uint64_t W, uint32_t nseg,
-                                                               uint64_t seg, u64 t, int mode) {
+                                                               uint64_t seg, u64 t, int mode,
+                                                               uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
@@ -915,7 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_gcounter_threshold(const u64* c, uin
         u64 s = 0;
         for (uint64_t w = lo + lane; w < hi; w += 64) s += c[rep * W + w];
         s = wave_sum(s);
-        if (lane == 0) emit(SEG, out, part, rep, 0, s, 0, mode, nseg, t);
+        if (lane == 0) emit(SEG, out, part, rep, 0, s, 0, mode, fin, t);
     }
 }
 
@@ -928,14 +1029,17 @@ hipError_t launch_gcounter_threshold(laspj_ctx* ctx, const laspj_batch* b, uint6
     const int mode = strict ? 5 : 4;
     if (ns == 1) {
         hipLaunchKernelGGL(k_gcounter_threshold<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, out, nullptr, b->replicas, W, ns, sg, (u64)t, mode);
+                           (const u64*)b->dev, out, nullptr, b->replicas, W, ns, sg, (u64)t, mode,
+                           0u);
         return hipGetLastError();
     }
     u64* part = nullptr;
     hipError_t e = partials(ctx, b->replicas, &part);
     if (e != hipSuccess) return e;
+    const uint32_t fin = fin_for(b->replicas * ns, ns);
     hipLaunchKernelGGL(k_gcounter_threshold<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       (const u64*)b->dev, out, part, b->replicas, W, ns, sg, (u64)t, mode);
+                       (const u64*)b->dev, out, part, b->replicas, W, ns, sg, (u64)t, mode, fin);
+    if (!fin) return finalize(ctx, part, out, b->replicas, mode, (u64)t);
     return hipGetLastError();
 }
 
@@ -946,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) void k_gcounter_inflation(const u64* prev, 
                                                                uint8_t* out, u64* part,
                                                                uint64_t R, uint64_t W,
                                                                bool bcast, uint32_t nseg,
-                                                               uint64_t seg) {
+                                                               uint64_t seg, uint32_t fin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t it = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; it < R * nseg;
@@ -968,7 +1072,7 @@ __global__ __launch_bounds__(kBlock) void k_gcounter_inflation(const u64* prev, 
             sp = wave_sum(sp);
             sc = wave_sum(sc);
         }
-        if (lane == 0) emit(SEG, out, part, rep, flags, sp, sc, STRICT ? 3 : 1, nseg);
+        if (lane == 0) emit(SEG, out, part, rep, flags, sp, sc, STRICT ? 3 : 1, fin);
     }
 }
 
@@ -987,9 +1091,11 @@ hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
 #define LJ_GC(ST, SG)                                                                          \
     hipLaunchKernelGGL((k_gcounter_inflation<ST, SG>), dim3(grid), dim3(kBlock), 0, ctx->stream, \
                        (const u64*)prev->dev, (const u64*)cur->dev, out, part, cur->replicas,    \
-                       W, bc, ns, sg)
+                       W, bc, ns, sg, fin)
+    const uint32_t fin = ns > 1 ? fin_for(cur->replicas * ns, ns) : 0u;
     if (ns > 1) {
         if (strict) LJ_GC(true, true); else LJ_GC(false, true);
+        if (!fin) return finalize(ctx, part, out, cur->replicas, strict ? 3 : 1);
         return hipGetLastError();
     }
     if (strict) LJ_GC(true, false); else LJ_GC(false, false);

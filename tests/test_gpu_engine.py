@@ -507,7 +507,9 @@ def test_ticketed_reductions_small_batches(ctx):
               for i in range(n)]
     want_s = [orc.ORDict.from_cells(cur[i], tok).is_strict_inflation_of(
         orc.ORDict.from_cells(prev[i], tok)) for i in range(n)]
+    want_st = [orc.ORDict.from_cells(cur[i], tok).stats() for i in range(n)]
     for _ in range(4):
+        assert [tuple(int(x) for x in r) for r in Cb.stats()] == want_st
         assert list(Cb.is_inflation_of(P)) == want_i
         assert list(Cb.is_inflation_of(P, strict=True)) == want_s
         assert list(Cb.equal(P)) == [False] * n
@@ -525,6 +527,11 @@ def test_ticketed_reductions_small_batches(ctx):
     g.upload(hc)
     sums = hc.sum(axis=1)
     for _ in range(3):
+        assert np.array_equal(g.values(), sums)
+        gs = ctx.gset_batch(2, 640_000)
+        gs.fill_synthetic(13)
+        assert list(gs.stats()) == [sum(bin(int(w)).count("1") for w in row)
+                                    for row in gs.download()]
         for t in (int(sums[0]), int(sums[1]) + 1, 0):
             assert list(g.threshold_met(t)) == [t <= int(x) for x in sums]
             assert list(g.threshold_met(t, strict=True)) == [t < int(x) for x in sums]
@@ -535,6 +542,42 @@ def test_ticketed_reductions_small_batches(ctx):
     g2.upload(h2)
     assert list(g2.is_inflation_of(g)) == [False, True, True]
     assert list(g2.is_inflation_of(g, strict=True)) == [False, False, True]
+
+
+def test_segmented_reductions_large_launch(ctx):
+    """More segment items than the ticket limit (5000 replicas x 2 segments): partial
+    records are finished by the finalize kernel, which also re-zeroes them — repeated,
+    interleaved with ticketed small launches, against numpy restatements of the
+    columnar predicates (lasp_lattice.erl:153-161, 235-253; stat/2)."""
+    n, e_n = 5000, 5000
+    P, Cb = ctx.orset_batch(n, e_n), ctx.orset_batch(n, e_n)
+    P.fill_synthetic(121)
+    prev = P.download()
+    cur = prev.copy()
+    cur[::3] |= _synth(122, 1, e_n)[0]                       # growth
+    cur[1::7, 4_999, 0] = 0                                  # drop the last element
+    cur[1::7, 4_999, 1] = 0
+    cur[2::11, 10, 1] = cur[2::11, 10, 0]                    # tombstone
+    Cb.upload(cur)
+    pp, rp, pc, rc = prev[..., 0], prev[..., 1], cur[..., 0], cur[..., 1]
+    viol = ((pp & ~pc) != 0).any(axis=1)
+    changed = ((pp != 0) & (pc != 0) & ((pp != pc) | (rp != rc))).any(axis=1)
+    npres, ncres = (pp != 0).sum(axis=1), (pc != 0).sum(axis=1)
+    want_i = ~viol
+    want_s = ~viol & (changed | (npres < ncres))
+    want_s |= (npres == 0) & (ncres != 0)
+    want_st = np.stack([(pc != 0).sum(axis=1),
+                        np.bitwise_count(pc & ~rc).sum(axis=1, dtype=np.int64),
+                        np.bitwise_count(rc).sum(axis=1, dtype=np.int64)], axis=1)
+    want_eq = (prev == cur).all(axis=(1, 2))
+    small = ctx.orset_batch(1, 20_000)
+    small.fill_synthetic(5)
+    for _ in range(3):
+        assert np.array_equal(Cb.is_inflation_of(P), want_i)
+        assert np.array_equal(Cb.is_inflation_of(P, strict=True), want_s)
+        assert np.array_equal(Cb.equal(P), want_eq)
+        assert np.array_equal(Cb.stats().astype(np.int64), want_st)
+        assert small.is_inflation_of(small).all() and small.equal(small).all()
 
 
 def test_gcounter_batch_kernels(ctx):
