@@ -119,9 +119,12 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_STREAM_UNROLL 2   /* 16-B cells per lane per iteration: 1,2,4,8      */
 #define LASPJ_TUNE_STREAM_NT     3   /* 1 = non-temporal loads/stores, 0 = default      */
 #define LASPJ_TUNE_ETF_KERNEL    4   /* OR-Set payload writer: 0 = record kernel when the
-                                        token images are uniform (24 KiB window),
-                                        1 = element staging, 2 / 3 = record kernel with a
-                                        16 / 20 KiB window                               */
+                                        token images are uniform (24 KiB window; records
+                                        staged per element when elements hold <= 8 token
+                                        slots, spread over lanes otherwise), 1 = element
+                                        staging, 2 / 3 = record kernel, lanes, 16 / 20 KiB,
+                                        4 = record kernel, lanes, 24 KiB, 5 = record
+                                        kernel, per element thread, 24 KiB               */
 #define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = flat sweep when
                                         the replica length is a power of two and
                                         2 <= group <= 4, 1 = per-replica segments with a

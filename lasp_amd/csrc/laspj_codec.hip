@@ -649,7 +649,9 @@ __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* lds4, u64* total) {
     return before + x - v;
 }
 
-template <uint32_t WIN>
+// EPAR (few token slots per element): each element's thread also stages its own records
+// (no record -> element search, no rank select); otherwise records are spread over lanes
+template <uint32_t WIN, bool EPAR>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cells, uint64_t R,
                                                                 uint32_t E, DictView d, int tag,
                                                                 int vers, const u64* offs,
@@ -819,47 +821,68 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                         if (overlaps<WIN>(r0 + (int32_t)sz - 1, 1)) or_piece<1>(win, r0 + (int32_t)sz - 1, wc, 1);
                     }
                 }
-                // records whose element intersects the window
-                // jlo = first element ending after the window start, jhi = first one
-                // starting at or past its end (both monotone: one ballot per 64 elements)
-                uint32_t jlo = kBlock, jhi = kBlock;
-                {
-                    const uint32_t lane = tid & 63u;
-#pragma unroll
-                    for (uint32_t k = 0; k < kBlock / 64; ++k) {
-                        const uint32_t m = 64u * k + lane;
-                        const u64 b1 = __ballot(cur_rel + (int32_t)s_pos[m + 1] > 0);
-                        const u64 b2 = __ballot(cur_rel + (int32_t)s_pos[m] >= (int32_t)WIN);
-                        if (jlo == kBlock && b1) jlo = 64u * k + (uint32_t)__ffsll((long long)b1) - 1u;
-                        if (jhi == kBlock && b2) jhi = 64u * k + (uint32_t)__ffsll((long long)b2) - 1u;
+                if (EPAR) {
+                    // this thread's element: its records in term order, one after another
+                    if (sz && overlaps<WIN>(cur_rel + (int32_t)pos, sz)) {
+                        int32_t rel = cur_rel + (int32_t)(pos + hl + 4u);
+                        for (u64 m = pt; m; m &= m - 1) {
+                            const uint32_t rank = (uint32_t)__ffsll((long long)m) - 1u;
+                            const bool rm = (rt >> rank) & 1ull;
+                            if (overlaps<WIN>(rel, RL)) {
+                                uint32_t w[12];
+                                load_piece48(w, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
+                                or_piece<12>(win, rel, w, RL);
+                            }
+                            const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
+                                                    rm ? 0x00657572u : 0x65736c61u};
+                            if (overlaps<WIN>(rel + (int32_t)RL, 8))
+                                or_piece<2>(win, rel + (int32_t)RL, wa, 8);
+                            rel += (int32_t)(RL + (rm ? 7u : 8u));
+                        }
                     }
-                }
-                const uint32_t r_lo = jlo < kBlock ? s_rec[jlo] : nrec;
-                const uint32_t r_hi = s_rec[jhi];
-                for (uint32_t ri = r_lo + tid; ri < r_hi; ri += kBlock) {
-                    uint32_t lo = jlo, hi = jhi;            // last j with s_rec[j] <= ri
-                    while (hi - lo > 1) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (s_rec[m] <= ri) lo = m;
-                        else hi = m;
+                } else {
+                    // records whose element intersects the window
+                    // jlo = first element ending after the window start, jhi = first one
+                    // starting at or past its end (both monotone: one ballot per 64 elements)
+                    uint32_t jlo = kBlock, jhi = kBlock;
+                    {
+                        const uint32_t lane = tid & 63u;
+    #pragma unroll
+                        for (uint32_t k = 0; k < kBlock / 64; ++k) {
+                            const uint32_t m = 64u * k + lane;
+                            const u64 b1 = __ballot(cur_rel + (int32_t)s_pos[m + 1] > 0);
+                            const u64 b2 = __ballot(cur_rel + (int32_t)s_pos[m] >= (int32_t)WIN);
+                            if (jlo == kBlock && b1) jlo = 64u * k + (uint32_t)__ffsll((long long)b1) - 1u;
+                            if (jhi == kBlock && b2) jhi = 64u * k + (uint32_t)__ffsll((long long)b2) - 1u;
+                        }
                     }
-                    const uint32_t j = lo, rho = ri - s_rec[j];
-                    const u64 pj = s_p[j], rj = s_r[j];
-                    const uint32_t rank = select64(pj, rho);
-                    const bool rm = (rj >> rank) & 1ull;
-                    const u64 below = rank ? (~0ull >> (64u - rank)) : 0ull;
-                    const int32_t rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u +
-                                                            rho * (RL + 8u) -
-                                                            (uint32_t)__popcll(rj & below));
-                    if (overlaps<WIN>(rel, RL)) {
-                        uint32_t w[12];
-                        load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
-                        or_piece<12>(win, rel, w, RL);
+                    const uint32_t r_lo = jlo < kBlock ? s_rec[jlo] : nrec;
+                    const uint32_t r_hi = s_rec[jhi];
+                    for (uint32_t ri = r_lo + tid; ri < r_hi; ri += kBlock) {
+                        uint32_t lo = jlo, hi = jhi;            // last j with s_rec[j] <= ri
+                        while (hi - lo > 1) {
+                            const uint32_t m = (lo + hi) >> 1;
+                            if (s_rec[m] <= ri) lo = m;
+                            else hi = m;
+                        }
+                        const uint32_t j = lo, rho = ri - s_rec[j];
+                        const u64 pj = s_p[j], rj = s_r[j];
+                        const uint32_t rank = select64(pj, rho);
+                        const bool rm = (rj >> rank) & 1ull;
+                        const u64 below = rank ? (~0ull >> (64u - rank)) : 0ull;
+                        const int32_t rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u +
+                                                                rho * (RL + 8u) -
+                                                                (uint32_t)__popcll(rj & below));
+                        if (overlaps<WIN>(rel, RL)) {
+                            uint32_t w[12];
+                            load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
+                            or_piece<12>(win, rel, w, RL);
+                        }
+                        // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
+                        const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
+                                                rm ? 0x00657572u : 0x65736c61u};
+                        if (overlaps<WIN>(rel + (int32_t)RL, 8)) or_piece<2>(win, rel + (int32_t)RL, wa, 8);
                     }
-                    // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
-                    const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
-                                            rm ? 0x00657572u : 0x65736c61u};
-                    if (overlaps<WIN>(rel + (int32_t)RL, 8)) or_piece<2>(win, rel + (int32_t)RL, wa, 8);
                 }
                 __syncthreads();
                 // whole 16-byte chunks out; the partial one below seg_hi stays as the carry
@@ -1087,10 +1110,15 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
     uint64_t cap = (uint64_t)ctx->cus * 8;
     int grid = (int)(R < cap ? R : cap);
     if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf != 1) {
-        // window size (profiles/r01_suite_etf_windows.log): 0 = 24 KiB; 2, 3 = 16, 20 KiB
-        auto k = k_orset_etf_write_rec<24576>;
-        if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384>;
-        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480>;
+        // 0: 24 KiB window (profiles/r01_suite_etf_windows.log), records staged by their
+        // element's thread when elements hold <= 8 token slots, spread over lanes otherwise;
+        // 2, 3: 16 / 20 KiB windows, 4: 24 KiB, always spread over lanes
+        auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true>
+                                 : k_orset_etf_write_rec<24576, false>;
+        if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384, false>;
+        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480, false>;
+        if (ctx->tune_etf == 4) k = k_orset_etf_write_rec<24576, false>;
+        if (ctx->tune_etf == 5) k = k_orset_etf_write_rec<24576, true>;
         // one resident wave of blocks, each with a contiguous run of replicas
         int occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||

@@ -232,8 +232,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_reduce = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_KERNEL:
-            if (value < 0 || value > 3)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..3");
+            if (value < 0 || value > 5)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..5");
             ctx->tune_etf = value;
             return LASPJ_OK;
         default:

@@ -248,10 +248,12 @@ def test_gpu_orset_large_synthetic_batch():
         assert got == want, i
 
 
-def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3)):
+def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3, 4, 5)):
     """fn() under the record kernel (LASPJ_TUNE_ETF_KERNEL 0, chosen for uniform token
-    images), the element-staging kernels (1) and the record kernel's other window
-    sizes (2, 3: 16 and 20 KiB)."""
+    images: records per element thread when <= 8 token slots, else spread over lanes),
+    the element-staging kernels (1) and the lane-spread record kernel at other window
+    sizes (2, 3: 16 and 20 KiB) and at 24 KiB (4), and the per-element-thread record
+    kernel for any token count (5)."""
     from lasp_amd._lib import TUNE_ETF_KERNEL
     out = []
     try:
@@ -264,14 +266,17 @@ def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3)):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tok_len,long_elems", [(20, False), (20, True), (41, True),
-                                                (42, False), (1, True)])
-def test_gpu_orset_record_kernel_edges(tok_len, long_elems):
+@pytest.mark.parametrize("tok_len,long_elems,pool_n", [
+    (20, False, 64), (20, True, 64), (41, True, 64), (42, False, 64), (1, True, 64),
+    (20, True, 6), (41, False, 8), (1, False, 3)])
+def test_gpu_orset_record_kernel_edges(tok_len, long_elems, pool_n):
     """Payloads crossing many 16 KiB windows (up to 300 elements x 64 tokens), empty and
     one-token replicas, element images longer than the 48-byte fast header (binaries,
     tuples, long atoms), token images at the record kernel's 48-byte limit (41-byte
-    binaries) and just past it (42: the staging kernels), E not a multiple of 256:
-    both kernels match the oracle byte for byte, bare and tagged."""
+    binaries) and just past it (42: the staging kernels), E not a multiple of 256,
+    elements with up to 64 token slots (records spread over lanes) and with <= 8 (records
+    staged by their element's thread): every kernel matches the oracle byte for byte,
+    bare and tagged."""
     from lasp_amd import engine, etf
     from lasp_amd.codec import Domain
     from lasp_amd.orset import context
@@ -280,17 +285,19 @@ def test_gpu_orset_record_kernel_edges(tok_len, long_elems):
     elems = list(range(0, 900, 3))
     if long_elems:
         elems += [b"L" * 60, (PAtom("k"), b"v" * 50), PAtom("a" * 47), b"s" * 40, 1 << 70]
-    pool = {i: [bytes(rng.randrange(256) for _ in range(tok_len)) for _ in range(64)]
+    pool = {i: [bytes(rng.randrange(256) for _ in range(tok_len)) for _ in range(pool_n)]
             for i in range(len(elems))}
-    if tok_len == 1:                                  # 64 distinct one-byte tokens
-        pool = {i: [bytes([x]) for x in rng.sample(range(256), 64)] for i in range(len(elems))}
+    if tok_len == 1:                                  # distinct one-byte tokens
+        pool = {i: [bytes([x]) for x in rng.sample(range(256), pool_n)]
+                for i in range(len(elems))}
     raw = [{}, {elems[5]: {pool[5][0]: False}},
            {elems[i]: {t: rng.random() < 0.25 for t in pool[i]} for i in range(len(elems))}]
     for _ in range(37):
         d = {}
         k = rng.choice([1, 3, 40, 150, len(elems)])
         for i in rng.sample(range(len(elems)), k):
-            d[elems[i]] = {t: rng.random() < 0.3 for t in rng.sample(pool[i], rng.randint(1, 64))}
+            d[elems[i]] = {t: rng.random() < 0.3
+                           for t in rng.sample(pool[i], rng.randint(1, pool_n))}
         raw.append(d)
     states = []
     for d in raw:

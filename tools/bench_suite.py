@@ -27,7 +27,7 @@ from lasp_amd import _lib  # noqa: E402
 PEAK = 8000.0
 
 
-def timed(ctx, fn, steps, warmup=1):
+def timed(ctx, fn, steps, warmup=3):
     for _ in range(warmup):
         fn()
     ctx.synchronize()
@@ -247,7 +247,8 @@ def etf(ctx, steps):
         # record kernel (default for uniform token images), then the staging kernels
         variants = ((0, "write"), (1, "write_staging"))
         if os.environ.get("ETF_WINDOWS"):
-            variants += ((2, "write_w16k"), (3, "write_w20k"))
+            variants += ((2, "write_w16k"), (3, "write_w20k"), (4, "write_lanes"),
+                         (5, "write_elem"))
         for knob, name in variants:
             ctx.set_tuning(_lib.TUNE_ETF_KERNEL, knob)
             ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_write(
