@@ -248,7 +248,7 @@ def test_gpu_orset_large_synthetic_batch():
         assert got == want, i
 
 
-def _both_kernels(ctx, fn, knobs=(0, 1, 2, 3, 4, 5)):
+def _etf_variants(ctx, fn, knobs=(0, 1, 2, 3, 4, 5)):
     """fn() under the record kernel (LASPJ_TUNE_ETF_KERNEL 0, chosen for uniform token
     images: records per element thread when <= 8 token slots, else spread over lanes),
     the element-staging kernels (1) and the lane-spread record kernel at other window
@@ -310,7 +310,7 @@ def test_gpu_orset_record_kernel_edges(tok_len, long_elems, pool_n):
     b = ctx.orset_batch(len(states), E)
     b.upload(dom.encode_orset(states, E))
     d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
-    for bare, tagged in _both_kernels(ctx, lambda: (b.to_binaries(d),
+    for bare, tagged in _etf_variants(ctx, lambda: (b.to_binaries(d),
                                                     b.to_binaries(d, tag=etf.DT_ORSET_TAG))):
         for s, x, y in zip(states, bare, tagged):
             assert x == oetf.term_to_binary(s)
@@ -341,7 +341,7 @@ def test_gpu_record_kernel_whole_buffer_equals_staging():
     def run():
         offs, out, total = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
         return offs.download(np.uint64), out.download(np.uint8, count=total)
-    (o1, p1), *rest = _both_kernels(ctx, run)
+    (o1, p1), *rest = _etf_variants(ctx, run)
     for o2, p2 in rest:
         assert np.array_equal(o1, o2)
         assert np.array_equal(p1, p2)
