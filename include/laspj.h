@@ -131,6 +131,8 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         compile-time group, 2 = generic segments        */
 #define LASPJ_TUNE_PRODUCT_ROWS  6   /* rows per outer-product tile: 0 = default (256),
                                         32, 64, 128, 256                                */
+#define LASPJ_TUNE_PRODUCT_COLS  7   /* columns per outer-product tile: 0 = default
+                                        (1024), 2048, 4096                              */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -26,6 +26,7 @@ OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK, OPST_KEY_EXISTS = 0, 1, 2, 3
 TUNE_STREAM_GRID, TUNE_STREAM_UNROLL, TUNE_STREAM_NT, TUNE_ETF_KERNEL = 1, 2, 3, 4
 TUNE_REDUCE_KERNEL = 5
 TUNE_PRODUCT_ROWS = 6
+TUNE_PRODUCT_COLS = 7
 
 
 class LaspjUnavailable(RuntimeError):

@@ -78,6 +78,7 @@ hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const las
 // ------------------------------------------------------------------ product (OR-Set)
 
 constexpr int kPX = 256;    // rows per tile (profiles/r01_suite_product_rows.log: 256 > 128 > 64)
+constexpr int kPG = 1;      // 1024-column groups per tile (default)
 constexpr int kPY = 1024;   // columns per tile = 4 per lane
 
 __device__ __forceinline__ uint32_t pack8(u64x2 c, uint32_t* flag) {
@@ -85,21 +86,24 @@ __device__ __forceinline__ uint32_t pack8(u64x2 c, uint32_t* flag) {
     return c.x ? (uint32_t)((c.x & 0xFFull) | ((c.y & 0xFFull) << 8)) : 0u;
 }
 
-template <bool ALIGNED, int PX>
+// G column groups of 1024 per tile: a lane keeps G x 4 packed column cells in registers
+// and every row is G 16-byte stores per lane (G x 4 KiB contiguous per row and block)
+template <bool ALIGNED, int PX, int G>
 __global__ __launch_bounds__(kB) void k_orset_product(uint32_t* out, const u64x2* L,
                                                       const u64x2* R, uint64_t reps,
                                                       uint32_t EL, uint32_t ER,
                                                       uint64_t cstride, uint32_t* flag) {
-    __shared__ __attribute__((aligned(16))) uint32_t ry[kPY];
+    constexpr uint32_t PY = G * kPY;
+    __shared__ __attribute__((aligned(16))) uint32_t ry[PY];
     __shared__ uint32_t lx[PX];
-    const uint64_t tx_n = (EL + PX - 1) / PX, ty_n = (ER + kPY - 1) / kPY;
+    const uint64_t tx_n = (EL + PX - 1) / PX, ty_n = (ER + PY - 1) / PY;
     const uint64_t tiles = reps * tx_n * ty_n;
     for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
         uint64_t rep = t / (tx_n * ty_n);
         uint64_t rem = t - rep * tx_n * ty_n;
         uint32_t tx = (uint32_t)(rem / ty_n), ty = (uint32_t)(rem - (uint64_t)tx * ty_n);
-        uint32_t x0 = tx * PX, y0 = ty * kPY;
-        for (int i = threadIdx.x; i < kPY; i += kB) {
+        uint32_t x0 = tx * PX, y0 = ty * PY;
+        for (int i = threadIdx.x; i < (int)PY; i += kB) {
             uint32_t y = y0 + i;
             ry[i] = y < ER ? pack8(ldnt(R + rep * ER + y), flag) << 16 : 0u;
         }
@@ -108,72 +112,107 @@ __global__ __launch_bounds__(kB) void k_orset_product(uint32_t* out, const u64x2
             lx[i] = x < EL ? pack8(ldnt(L + rep * EL + x), flag) : 0u;
         }
         __syncthreads();
-        const uint32_t yl = threadIdx.x * 4;
-        u32x4 ryv = *reinterpret_cast<const u32x4*>(&ry[yl]);
+        u32x4 ryv[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            ryv[g] = *reinterpret_cast<const u32x4*>(&ry[g * kPY + threadIdx.x * 4]);
         const uint32_t rows = min((uint32_t)PX, EL - x0);
         for (uint32_t rr = 0; rr < rows; ++rr) {
-            uint32_t lv = lx[rr];
-            u32x4 v;
-            v.x = (lv && ryv.x) ? lv | ryv.x : 0u;
-            v.y = (lv && ryv.y) ? lv | ryv.y : 0u;
-            v.z = (lv && ryv.z) ? lv | ryv.z : 0u;
-            v.w = (lv && ryv.w) ? lv | ryv.w : 0u;
-            uint64_t base = rep * cstride + (uint64_t)(x0 + rr) * ER + y0 + yl;
-            if (ALIGNED && y0 + yl + 3 < ER) {
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + base));
-            } else {
-                uint32_t y = y0 + yl;
-                if (y < ER) out[base] = v.x;
-                if (y + 1 < ER) out[base + 1] = v.y;
-                if (y + 2 < ER) out[base + 2] = v.z;
-                if (y + 3 < ER) out[base + 3] = v.w;
+            const uint32_t lv = lx[rr];
+            const uint64_t rowb = rep * cstride + (uint64_t)(x0 + rr) * ER + y0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const u32x4 c = ryv[g];
+                u32x4 v;
+                v.x = (lv && c.x) ? lv | c.x : 0u;
+                v.y = (lv && c.y) ? lv | c.y : 0u;
+                v.z = (lv && c.z) ? lv | c.z : 0u;
+                v.w = (lv && c.w) ? lv | c.w : 0u;
+                const uint32_t yl = g * kPY + threadIdx.x * 4;
+                const uint64_t base = rowb + yl;
+                if (ALIGNED && y0 + yl + 3 < ER) {
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + base));
+                } else {
+                    uint32_t y = y0 + yl;
+                    if (y < ER) out[base] = v.x;
+                    if (y + 1 < ER) out[base + 1] = v.y;
+                    if (y + 2 < ER) out[base + 2] = v.z;
+                    if (y + 3 < ER) out[base + 3] = v.w;
+                }
             }
         }
         __syncthreads();
     }
 }
 
-// wide form: cell (x, y) = {pX, rX, pY, rY} (32 B) for any token slots; a lane writes
-// one 16-byte half, lanes 2k / 2k+1 = cell k's X / Y half (contiguous 1 KiB stores)
+// wide form: cell (x, y) = {pX, rX, pY, rY} (32 B) for any token slots.  A block takes a
+// (replica, row x, 1024-column tile): row x's cell is one broadcast load, lanes 2k /
+// 2k+1 write cell k's X / Y half, so each wave store covers 1 KiB contiguously; the
+// only divisions are per tile.
+constexpr uint32_t kWTile = 1024;
+
 __global__ __launch_bounds__(kB) void k_orset_product_wide(u64x2* out, const u64x2* L,
                                                            const u64x2* R, uint64_t reps,
                                                            uint32_t EL, uint32_t ER) {
-    const uint64_t cells = (uint64_t)EL * ER;
-    const uint64_t n = reps * cells * 2;
-    const uint64_t stride = (uint64_t)gridDim.x * kB;
-    for (uint64_t u = (uint64_t)blockIdx.x * kB + threadIdx.x; u < n; u += stride) {
-        uint64_t c = u >> 1;
-        uint64_t rep = c / cells, xy = c - rep * cells;
-        uint32_t x = (uint32_t)(xy / ER), y = (uint32_t)(xy - (uint64_t)x * ER);
-        u64x2 a = L[rep * EL + x], b = R[rep * ER + y];
-        u64x2 z = {0, 0};
-        bool keep = (a.x != 0) & (b.x != 0);
-        stnt(out + u, keep ? ((u & 1) ? b : a) : z);
+    const uint64_t ty_n = (ER + kWTile - 1) / kWTile;
+    const uint64_t tiles = reps * EL * ty_n;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const uint64_t row = t / ty_n;                  // rep * EL + x
+        const uint32_t y0 = (uint32_t)(t - row * ty_n) * kWTile;
+        const uint64_t rep = row / EL;
+        const u64x2 a = L[row];
+        const u64x2* Rr = R + rep * ER;
+        u64x2* o = out + (row * ER + y0) * 2;
+        const uint32_t units = 2u * min(kWTile, ER - y0);
+#pragma unroll 4
+        for (uint32_t u = threadIdx.x; u < units; u += kB) {
+            const u64x2 b = Rr[y0 + (u >> 1)];
+            const bool keep = (a.x != 0) & (b.x != 0);
+            stnt(o + u, keep ? ((u & 1) ? b : a) : u64x2{0, 0});
+        }
     }
 }
 
 hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                 const laspj_batch* r, uint32_t* flag) {
     if (dst->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE) {
-        uint64_t n = l->replicas * (uint64_t)l->elements * r->elements * 2;
-        hipLaunchKernelGGL(k_orset_product_wide, dim3(grid_for(ctx, n)), dim3(kB), 0, ctx->stream,
+        uint64_t tiles = l->replicas * (uint64_t)l->elements *
+                         ((r->elements + kWTile - 1) / kWTile);
+        uint64_t g = tiles < (uint64_t)ctx->cus * 32 ? tiles : (uint64_t)ctx->cus * 32;
+        hipLaunchKernelGGL(k_orset_product_wide, dim3((unsigned)(g ? g : 1)), dim3(kB), 0, ctx->stream,
                            reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(l->dev),
                            reinterpret_cast<const u64x2*>(r->dev), l->replicas, l->elements,
                            r->elements);
         return hipGetLastError();
     }
     const int px = ctx->tune_product_rows > 0 ? (int)ctx->tune_product_rows : kPX;
+    const int gy = ctx->tune_product_cols > 0 ? (int)(ctx->tune_product_cols / kPY) : kPG;
     uint64_t tiles = l->replicas * ((l->elements + px - 1) / px) *
-                     ((r->elements + kPY - 1) / kPY);
+                     ((r->elements + (uint64_t)gy * kPY - 1) / ((uint64_t)gy * kPY));
     uint64_t g = tiles < (uint64_t)ctx->cus * 32 ? tiles : (uint64_t)ctx->cus * 32;
     auto* o = reinterpret_cast<uint32_t*>(dst->dev);
     auto* L = reinterpret_cast<const u64x2*>(l->dev);
     auto* R = reinterpret_cast<const u64x2*>(r->dev);
     const bool al = r->elements % 4 == 0;
-    auto k = al ? k_orset_product<true, kPX> : k_orset_product<false, kPX>;
-    if (px == 128) k = al ? k_orset_product<true, 128> : k_orset_product<false, 128>;
-    if (px == 64) k = al ? k_orset_product<true, 64> : k_orset_product<false, 64>;
-    if (px == 32) k = al ? k_orset_product<true, 32> : k_orset_product<false, 32>;
+#define LJ_PK(PXV, GV) (al ? k_orset_product<true, PXV, GV> : k_orset_product<false, PXV, GV>)
+    auto k = LJ_PK(kPX, kPG);
+    if (gy == 1) {
+        if (px == 256) k = LJ_PK(256, 1);
+        if (px == 128) k = LJ_PK(128, 1);
+        if (px == 64) k = LJ_PK(64, 1);
+        if (px == 32) k = LJ_PK(32, 1);
+    } else if (gy == 2) {
+        if (px == 256) k = LJ_PK(256, 2);
+        if (px == 128) k = LJ_PK(128, 2);
+        if (px == 64) k = LJ_PK(64, 2);
+        if (px == 32) k = LJ_PK(32, 2);
+    } else {
+        if (px == 256) k = LJ_PK(256, 4);
+        if (px == 128) k = LJ_PK(128, 4);
+        if (px == 64) k = LJ_PK(64, 4);
+        if (px == 32) k = LJ_PK(32, 4);
+    }
+#undef LJ_PK
     hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(kB), 0, ctx->stream, o, L, R, l->replicas,
                        l->elements, r->elements, 2 * dst->words_per_replica, flag);
     return hipGetLastError();

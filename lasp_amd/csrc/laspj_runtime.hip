@@ -226,6 +226,11 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
                 return fail(ctx, LASPJ_E_INVAL, "tuning: product rows must be 0,32,64,128,256");
             ctx->tune_product_rows = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_PRODUCT_COLS:
+            if (!(value == 0 || value == 1024 || value == 2048 || value == 4096))
+                return fail(ctx, LASPJ_E_INVAL, "tuning: product cols must be 0,1024,2048,4096");
+            ctx->tune_product_cols = value;
+            return LASPJ_OK;
         case LASPJ_TUNE_REDUCE_KERNEL:
             if (value < 0 || value > 2)
                 return fail(ctx, LASPJ_E_INVAL, "tuning: reduce kernel must be 0..2");

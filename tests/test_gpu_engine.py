@@ -366,15 +366,17 @@ def test_orset_product_tiles_and_tails(ctx):
     L, Rb = ctx.orset_batch(n, el), ctx.orset_batch(n, er)
     L.upload(l)
     Rb.upload(r)
-    from lasp_amd._lib import TUNE_PRODUCT_ROWS
+    from lasp_amd._lib import TUNE_PRODUCT_COLS, TUNE_PRODUCT_ROWS
     outs = []
     try:
-        for rows in (32, 64, 128, 0):                # every tile height; default last
-            ctx.set_tuning(TUNE_PRODUCT_ROWS, rows)
+        for rows, cols in ((32, 0), (64, 2048), (128, 4096), (256, 2048), (0, 0)):
+            ctx.set_tuning(TUNE_PRODUCT_ROWS, rows)  # every tile shape; default last
+            ctx.set_tuning(TUNE_PRODUCT_COLS, cols)
             P = L.product(Rb)
             outs.append(P.download())
     finally:
         ctx.set_tuning(TUNE_PRODUCT_ROWS, 0)
+        ctx.set_tuning(TUNE_PRODUCT_COLS, 0)
     got = outs[-1]
     for o in outs[:-1]:
         assert np.array_equal(o, got)
@@ -685,6 +687,24 @@ def test_orset_product_wide_any_token_slots(ctx, tokens):
     vis = P.value_bits()[0]
     # visible: x live in both rows; y = 0 live, y = 1 all tombstoned -> cells 0 and 2
     assert int(vis[0]) & 0xF == 0b0101
+
+
+def test_orset_product_wide_tiles(ctx):
+    """32-byte product over 1024-column tiles: 3 replicas x 37 rows x 2500 columns
+    (a tail tile, absent rows and columns): every cell is {pX, rX, pY, rY} or 0."""
+    n, el, er = 3, 37, 2500
+    l, r = _synth(131, n, el), _synth(132, n, er)
+    L, Rb = ctx.orset_batch(n, el), ctx.orset_batch(n, er)
+    L.upload(l)
+    Rb.upload(r)
+    P = L.product(Rb)
+    assert type(P).__name__ == "ORSetProductWideBatch"
+    got = P.download()
+    keep = (l[:, :, None, 0] != 0) & (r[:, None, :, 0] != 0)
+    want = np.concatenate([np.broadcast_to(l[:, :, None, :], (n, el, er, 2)),
+                           np.broadcast_to(r[:, None, :, :], (n, el, er, 2))], axis=3)
+    want = np.where(keep[..., None], want, np.uint64(0))
+    assert np.array_equal(got.reshape(n, el, er, 4), want)
 
 
 def test_concurrent_callers_one_context(ctx):

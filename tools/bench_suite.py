@@ -200,12 +200,24 @@ def config5(ctx, steps):
     pl.upload(h)
     pr.upload(h)
     out = engine.ORSetProductBatch(ctx, 1, n, n)
-    for rows in (0, 64, 128):                      # 0 = default tile (256 rows)
-        ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, rows)
+    for rows, cols in ((0, 0), (64, 0), (128, 0), (0, 2048), (0, 4096), (128, 4096)):
+        ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, rows)     # 0 = default tile (256 x 1024)
+        ctx.set_tuning(_lib.TUNE_PRODUCT_COLS, cols)
         ms = timed(ctx, lambda: pl.product(pr, out), steps)
-        report("config5_product" + (f"_rows{rows}" if rows else ""), ms, 4 * n * n + 32 * n,
-               n * n, "cells_per_s", el=n, er=n)
+        tag = (f"_rows{rows}" if rows else "") + (f"_cols{cols}" if cols else "")
+        report("config5_product" + tag, ms, 4 * n * n + 32 * n, n * n, "cells_per_s",
+               el=n, er=n)
     ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, 0)
+    ctx.set_tuning(_lib.TUNE_PRODUCT_COLS, 0)
+    del out, pl, pr
+    # wide form (token slots >= 8: 32-byte cells {pX, rX, pY, rY}), 30k x 30k x 64 slots
+    m = 30_000
+    wl, wr = ctx.orset_batch(1, m), ctx.orset_batch(1, m)
+    wl.fill_synthetic(7)
+    wr.fill_synthetic(8)
+    wout = engine.ORSetProductWideBatch(ctx, 1, m, m)
+    ms = timed(ctx, lambda: wl.product(wr, wout), steps)
+    report("config5_product_wide_30k", ms, 32 * m * m + 32 * m, m * m, "cells_per_s", el=m, er=m)
 
 
 def etf(ctx, steps):
