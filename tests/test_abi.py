@@ -71,3 +71,36 @@ def test_engine_fails_loudly_without_library(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/liblaspj.so")
     with pytest.raises(_lib.LaspjUnavailable):
         _lib.load()
+
+
+def _build_c_client(tmp_path):
+    """Compile tests/c/laspj_c_client.c against include/laspj.h and liblaspj.so alone
+    (the NIF's view of the boundary)."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    exe = str(tmp_path / "laspj_c_client")
+    libdir = os.path.join(root, "lasp_amd")
+    cmd = [cc, "-std=c11", "-O2", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+           os.path.join(root, "tests", "c", "laspj_c_client.c"), "-L", libdir, "-llaspj",
+           f"-Wl,-rpath,{libdir}", "-o", exe]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr
+    return exe
+
+
+def test_c_client_compiles_against_header(tmp_path):
+    _build_c_client(tmp_path)
+
+
+@pytest.mark.gpu
+def test_c_client_runs(tmp_path):
+    """merge / value / stats / inflation / update / error status from plain C."""
+    import subprocess
+    exe = _build_c_client(tmp_path)
+    res = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "laspj C client OK" in res.stdout
