@@ -49,6 +49,10 @@ StreamTune stream_tune(const laspj_ctx* ctx, uint64_t n16) {
     // stayed at 5.6-5.8 TB/s.
     t.grid = ctx->tune_grid > 0 ? (int)ctx->tune_grid : ctx->cus * 64;
     t.unroll = ctx->tune_unroll > 0 ? (int)ctx->tune_unroll : 2;
+    // a launch smaller than 8 cells per lane of one full wave of blocks has nothing to
+    // unroll over (the bind path's single replica); it also keeps those launches apart
+    // from the batched ones in kernel-trace statistics (k_or16<1, ...>)
+    if (ctx->tune_unroll <= 0 && n16 < (uint64_t)ctx->cus * kBlock * 8) t.unroll = 1;
     t.nt = ctx->tune_nt < 0 ? true : ctx->tune_nt != 0;
     uint64_t need = (n16 + kBlock - 1) / kBlock;
     if (need < (uint64_t)t.grid) t.grid = need > 0 ? (int)need : 1;
