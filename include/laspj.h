@@ -168,8 +168,9 @@ int laspj_batch_download(laspj_ctx* ctx, const laspj_batch* batch, uint64_t firs
                          uint64_t count, void* host);
 /* every replica := new() */
 int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* batch);
-/* deterministic synthetic replicas (oracle/laspj_oracle.c restates it):
- * replica i of the batch is synthetic replica (replica_base + i) of stream `seed` */
+/* deterministic synthetic replicas (oracle/laspj_oracle.c restates the
+ * OR-Set and G-Set streams): replica i of the batch is synthetic replica
+ * (replica_base + i) of stream `seed`; G-Counter batches get 20-bit counts (bench data) */
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed,
                                uint64_t replica_base);
 

@@ -355,8 +355,27 @@ __global__ __launch_bounds__(kBlock) void k_fill_gset(u64* words, uint64_t R, ui
     }
 }
 
+// G-Counter replicas: count of actor slot a = 20 low bits of the stream word (bench data)
+__global__ __launch_bounds__(kBlock) void k_fill_gcounter(u64* words, uint64_t R, uint64_t W,
+                                                          u64 seed, u64 base) {
+    const uint64_t n = R * W;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint64_t rep = i / W;
+        uint64_t a = i - rep * W;
+        u64 h = synth_replica_key(seed, base + rep);
+        words[i] = sm64(h + a * 0xD1B54A32D192ED03ull) & 0xFFFFFull;
+    }
+}
+
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                  uint64_t base) {
+    if (b->kind == LASPJ_KIND_GCOUNTER) {
+        StreamTune t = stream_tune(ctx, b->replicas * b->words_per_replica / 2 + 1);
+        hipLaunchKernelGGL(k_fill_gcounter, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                           (u64*)b->dev, b->replicas, b->words_per_replica, (u64)seed, (u64)base);
+        return hipGetLastError();
+    }
     StreamTune t = stream_tune(ctx, b->replicas * b->words_per_replica / 2 + 1);
     if (b->kind == LASPJ_KIND_ORSET)
         hipLaunchKernelGGL(k_fill_orset, dim3(t.grid), dim3(kBlock), 0, ctx->stream,

@@ -441,8 +441,9 @@ int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* b) {
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                uint64_t replica_base) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
-    if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_GSET)
-        return fail(ctx, LASPJ_E_KIND, "fill_synthetic: OR-Set or G-Set batches only");
+    if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_GSET &&
+        b->kind != LASPJ_KIND_GCOUNTER)
+        return fail(ctx, LASPJ_E_KIND, "fill_synthetic: OR-Set, G-Set or G-Counter batches only");
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base));
     return LASPJ_OK;

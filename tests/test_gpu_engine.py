@@ -582,6 +582,21 @@ def test_segmented_reductions_large_launch(ctx):
         assert small.is_inflation_of(small).all() and small.equal(small).all()
 
 
+def test_gcounter_synthetic_join_value(ctx):
+    """Synthetic G-Counter batches (bench data): deterministic, 20-bit counts; the
+    join is the per-actor max and value/1 the sum (riak_dt_gcounter merge / value)."""
+    a, b, c = (ctx.gcounter_batch(300, 1000) for _ in range(3))
+    a.fill_synthetic(5)
+    b.fill_synthetic(6)
+    ha, hb = a.download(), b.download()
+    a.fill_synthetic(5)
+    assert np.array_equal(a.download(), ha)
+    assert ha.max() < (1 << 20) and not np.array_equal(ha, hb)
+    c.join(a, b)
+    assert np.array_equal(c.download(), np.maximum(ha, hb))
+    assert np.array_equal(c.values(), np.maximum(ha, hb).sum(axis=1))
+
+
 def test_gcounter_batch_kernels(ctx):
     """riak_dt_gcounter join (per-actor max), value (sum), threshold, inflation, FSM
     reduce, increments — against the oracle's _GCounter restatement."""

@@ -115,6 +115,27 @@ def kernels(ctx, R, E, steps):
     ga.fill_synthetic(5)
     gb.fill_synthetic(6)
     report("gset_join", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * R * W, R * E, "elements_per_s")
+    del ga, gb, gc
+    # riak_dt_gcounter (the ad counter's threshold counter): 2^20 replicas x 1024 actors
+    RG, A = 1 << 20, 1024
+    ka, kb, kc = (ctx.gcounter_batch(RG, A) for _ in range(3))
+    ka.fill_synthetic(7)
+    kb.fill_synthetic(8)
+    n8 = RG * A * 8
+    report("gcounter_join_max", timed(ctx, lambda: kc.join(ka, kb), steps), 3 * n8, RG * A,
+           "actor_slots_per_s")
+    sums = ctx.buffer(RG * 8)
+    report("gcounter_value", timed(ctx, lambda: _lib.check(
+        L.laspj_gcounter_value(ctx.h, kc.h, sums.h), ctx.h), steps), n8 + RG * 8, RG * A,
+        "actor_slots_per_s")
+    og = ctx.buffer(RG)
+    report("gcounter_threshold", timed(ctx, lambda: _lib.check(
+        L.laspj_gcounter_threshold(ctx.h, kc.h, 1 << 29, 0, og.h), ctx.h), steps), n8 + RG,
+        RG * A, "actor_slots_per_s")
+    report("gcounter_inflation", timed(ctx, lambda: _lib.check(
+        L.laspj_gcounter_inflation(ctx.h, ka.h, kc.h, 0, og.h), ctx.h), steps), 2 * n8 + RG,
+        RG * A, "actor_slots_per_s")
+    del ka, kb, kc
 
 
 def ops(ctx, steps):
