@@ -1,6 +1,8 @@
 """Randomised parity (hypothesis) of the device combinator bodies and the device
 lasp_core store against the oracle, beyond the fixed golden vectors."""
 
+import os
+
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
 
@@ -25,7 +27,8 @@ def build(ops, seed):
     return s
 
 
-SETTINGS = settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+SOAK = int(os.environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+SETTINGS = settings(max_examples=40 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 
 
 @SETTINGS
@@ -72,7 +75,7 @@ STEP = st.one_of(
     st.tuples(st.just("bind"), st.integers(0, 1), SET))
 
 
-@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=25 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(STEP, max_size=10))
 def test_store_random(steps):
     """Two inputs feeding union / filter / map (monotone) / fold (non-decreasing keys):

@@ -10,6 +10,8 @@ lasp_orset.erl:294-303 / lasp_gset.erl:167-169.
 CPU: the oracle restatement.  GPU: the device mirrors (lasp_amd.orset / lasp_amd.gset).
 """
 
+import os
+
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
 
@@ -186,7 +188,7 @@ def test_gset_converges(cmds):
 
 
 @pytest.mark.gpu
-@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=60 * int(os.environ.get("LASPJ_SOAK", "1")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(commands(GEN_OP))
 def test_gpu_orset_converges(cmds):
     from lasp_amd import orset as do
@@ -195,7 +197,7 @@ def test_gpu_orset_converges(cmds):
 
 
 @pytest.mark.gpu
-@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=40 * int(os.environ.get("LASPJ_SOAK", "1")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(commands(GSET_OP))
 def test_gpu_gset_converges(cmds):
     from lasp_amd import gset as dg
