@@ -390,8 +390,9 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 // ------------------------------------------------------------------ value / removed
 // One wave per 64-element word: lane l tests element 64*w + l, __ballot packs the bits.
 
-// One wave per (replica, 4096-cell segment): it walks the segment's 64 words, 4 words
-// (4 x 1 KiB loads) in flight before each group of __ballot packs; no per-cell division.
+// One wave per (replica, <= 4096-cell segment): it walks the segment's <= 64 words, 4
+// words (4 x 1 KiB loads) in flight before each group of __ballot packs, lane g keeping
+// word g for one coalesced store at the end; no per-cell division.
 constexpr uint64_t kTicketItems = 8192;     // see the partial-record note below
 static uint32_t fin_for(uint64_t items, uint32_t ns) { return items <= kTicketItems ? ns : 0u; }
 
@@ -410,11 +411,10 @@ static uint64_t seg_for(uint64_t R, uint64_t n, uint64_t base) {
 
 constexpr uint32_t kVSeg = 4096;
 
-template <bool REMOVED>
+template <bool REMOVED, int U>
 __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64* out,
                                                         uint64_t R, uint32_t E, uint32_t nseg,
                                                         uint32_t seg) {
-    constexpr int U = 4;
     const uint32_t W = (E + 63u) / 64u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
@@ -425,6 +425,10 @@ __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64*
         uint32_t e1 = min(E, e0 + seg);
         const u64x2* c = cells + rep * E;
         u64* o = out + rep * W;
+        // lane g keeps the segment's g-th word (segments are <= 64 words), so the words
+        // leave as one coalesced store instead of one single-lane store each
+        const uint32_t g0 = e0 >> 6;
+        u64 mine = 0;
         for (uint32_t e = e0; e < e1; e += 64 * U) {
             u64x2 v[U];
 #pragma unroll
@@ -436,9 +440,10 @@ __global__ __launch_bounds__(kBlock) void k_orset_value(const u64x2* cells, u64*
             for (int u = 0; u < U; ++u) {
                 bool pred = REMOVED ? (v[u].y != 0) : ((v[u].x & ~v[u].y) != 0);
                 u64 m = __ballot(pred);
-                if (lane == 0 && e + u * 64 < e1) o[(e + u * 64) >> 6] = m;
+                if (lane == ((e + u * 64) >> 6) - g0) mine = m;
             }
         }
+        if (lane < ((e1 - e0 + 63u) >> 6)) o[g0 + lane] = mine;
     }
 }
 
@@ -453,12 +458,12 @@ hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* ou
     uint64_t blocks = (items + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
     auto* cells = reinterpret_cast<const u64x2*>(b->dev);
-    if (removed)
-        hipLaunchKernelGGL(k_orset_value<true>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements, ns, sg);
-    else
-        hipLaunchKernelGGL(k_orset_value<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           cells, (u64*)out, b->replicas, b->elements, ns, sg);
+    // words in flight per lane: 4 (default) or the stream unroll knob when it is 8
+    const bool u8 = ctx->tune_unroll == 8;
+    auto k = removed ? (u8 ? k_orset_value<true, 8> : k_orset_value<true, 4>)
+                     : (u8 ? k_orset_value<false, 8> : k_orset_value<false, 4>);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, cells, (u64*)out,
+                       b->replicas, b->elements, ns, sg);
     return hipGetLastError();
 }
 

@@ -59,6 +59,10 @@ def kernels(ctx, R, E, steps):
     L = ctx.L
     report("orset_value", timed(ctx, lambda: _lib.check(L.laspj_orset_value(ctx.h, a.h, bits.h)), steps),
            16 * cells + R * W * 8, cells, "cells_per_s")
+    ctx.set_tuning(_lib.TUNE_STREAM_UNROLL, 8)      # value with 8 words in flight per lane
+    report("orset_value_u8", timed(ctx, lambda: _lib.check(L.laspj_orset_value(ctx.h, a.h, bits.h)), steps),
+           16 * cells + R * W * 8, cells, "cells_per_s")
+    ctx.set_tuning(_lib.TUNE_STREAM_UNROLL, 0)
     st = ctx.buffer(R * 24)
     report("orset_stats", timed(ctx, lambda: _lib.check(L.laspj_orset_stats(ctx.h, a.h, st.h)), steps),
            16 * cells + R * 24, cells, "cells_per_s")
