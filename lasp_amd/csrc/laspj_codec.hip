@@ -13,9 +13,15 @@
 //             131 108 <n:32> <elem image>* 106  |  131 106 when empty
 //
 // Two launches: k_*_etf_size (one wave per replica: payload size, dictionary check)
-// feeding a device exclusive scan (hipcub) into the caller's offsets, then
-// k_*_etf_write (one 256-thread block per replica: elements in term order, a block
-// scan of their sizes gives every thread its output position).  The path is
+// feeding a device exclusive scan (hipcub) into the caller's offsets, then a writer:
+//   k_orset_etf_write_rec   every token image the same length (Lasp's 20-byte tokens):
+//                           host-built record templates, records OR-ed into 16-byte
+//                           aligned LDS windows as byte-shifted dwords (below);
+//   k_orset_etf_write       mixed image lengths, few tokens per element: one thread
+//                           stages its element byte by byte;
+//   k_orset_etf_write_wave  mixed image lengths, many tokens: a wave per element;
+//   k_gset_etf_write        G-Set lists.
+// Elements go in term order; a block scan of their sizes places them.  The path is
 // write-bound: a payload is ~15-70x the bytes of its cells.
 
 #include <hipcub/hipcub.hpp>
@@ -252,38 +258,6 @@ __device__ __forceinline__ void stage_elem_header(const Win& w, const DictView& 
     w.put(q + 4, (uint8_t)n);
 }
 
-// 104 2 <token image> <true | false>; returns the record length
-__device__ __forceinline__ uint32_t record_len(const DictView& d, uint32_t t, bool removed) {
-    return 2u + (d.tok_off[t + 1] - d.tok_off[t]) + (removed ? 7u : 8u);
-}
-
-__device__ __forceinline__ void stage_record(const Win& w, const DictView& d, uint32_t t,
-                                             bool removed, uint32_t q, uint32_t rl) {
-    if (!w.hits(q, rl)) return;
-    const uint32_t L = d.tok_off[t + 1] - d.tok_off[t];
-    if (L <= 48 && inside(w, q, rl)) {
-        uint8_t* o = w.buf + (q - w.w0);
-        o[0] = 104;
-        o[1] = 2;
-        lds_put48(o + 2, d.tok_pad + d.tok_poff[t], L);
-        o += 2 + L;
-        o[0] = 100;
-        o[1] = 0;
-        o[2] = removed ? 4 : 5;
-        o[3] = removed ? 't' : 'f';
-        o[4] = removed ? 'r' : 'a';
-        o[5] = removed ? 'u' : 'l';
-        o[6] = removed ? 'e' : 's';
-        if (!removed) o[7] = 'e';
-        return;
-    }
-    w.put(q, 104);
-    w.put(q + 1, 2);
-    w.span(q + 2, d.tok_blob + d.tok_off[t], L);
-    if (removed) w.span(q + 2 + L, kAtomTrue, 7);
-    else w.span(q + 2 + L, kAtomFalse, 8);
-}
-
 // record from a term-order descriptor: image of L bytes at tok_pad + poff
 __device__ __forceinline__ void stage_record_desc(const Win& w, const DictView& d, uint32_t L,
                                                   uint32_t poff, bool removed, uint32_t q,
@@ -333,29 +307,6 @@ __device__ void stage_elem_thread(const Win& w, const DictView& d, uint32_t e, u
     w.put(q, 106);
 }
 
-// a wave stages one element: lane j owns the j-th token of the element in term order
-__device__ void stage_elem_wave(const Win& w, const DictView& d, uint32_t e, u64 p, u64 r,
-                                uint32_t pos, uint32_t sz) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
-    if (lane == 0) {
-        stage_elem_header(w, d, e, (uint32_t)__popcll(p), pos);
-        w.put(pos + sz - 1u, 106);
-    }
-    const uint32_t k = d.tok_order[64u * e + lane];
-    const bool here = k < 64 && ((p >> k) & 1ull);
-    const bool rm = here && ((r >> k) & 1ull);
-    const uint32_t t = 64u * e + (k & 63u);
-    const uint32_t rl = here ? record_len(d, t, rm) : 0u;
-    uint32_t x = rl;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    if (here) stage_record(w, d, t, rm, pos + 7u + el + (x - rl), rl);
-}
-
 // copy window bytes buf[sh .. sh + wl) to out[g .. g + wl), (g - sh) % 16 == 0
 __device__ __forceinline__ void copy_out(const uint8_t* buf, uint32_t sh, uint32_t wl,
                                          uint8_t* out, u64 g) {
@@ -385,17 +336,15 @@ __device__ __forceinline__ void write_list_header(uint8_t* out, u64 base, uint32
     }
 }
 
-template <bool WAVE>
+// few tokens per element and mixed token image lengths: one thread stages its whole
+// element into the block's window
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write(const u64x2* cells, uint64_t R,
                                                             uint32_t E, DictView d, int tag,
                                                             int vers, const u64* offs,
                                                             uint8_t* out) {
     __shared__ uint32_t lds4[kBlock / 64];
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
-    __shared__ uint32_t s_e[WAVE ? kBlock : 1], s_pos[WAVE ? kBlock : 1], s_sz[WAVE ? kBlock : 1];
-    __shared__ u64 s_p[WAVE ? kBlock : 1], s_r[WAVE ? kBlock : 1];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
-    const int wave = threadIdx.x >> 6;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64x2* c = cells + rep * E;
         const u64 base = offs[rep], end = offs[rep + 1];
@@ -410,28 +359,12 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write(const u64x2* cells, 
             const uint32_t pos = block_excl_scan(sz, lds4, &tot);
             block_excl_scan(v.x ? 1u : 0u, lds4, &cnt);
             if (cursor + tot + 1u > end) break;          // sizes disagree: never overrun
-            if (WAVE) {
-                s_e[threadIdx.x] = e;
-                s_p[threadIdx.x] = v.x;
-                s_r[threadIdx.x] = v.y;
-                s_pos[threadIdx.x] = pos;
-                s_sz[threadIdx.x] = sz;
-                __syncthreads();
-            }
             for (uint32_t w0 = 0; w0 < tot; w0 += kWin) {
                 const uint32_t wl = min(kWin, tot - w0);
                 const u64 g = cursor + w0;
                 const uint32_t sh = (uint32_t)(g & 15u);
                 const Win win{buf + sh, w0, wl};
-                if (WAVE) {
-                    for (int j = wave; j < kBlock; j += kBlock / 64) {
-                        const uint32_t jp = s_pos[j], js = s_sz[j];
-                        if (js && win.hits(jp, js))
-                            stage_elem_wave(win, d, s_e[j], s_p[j], s_r[j], jp, js);
-                    }
-                } else if (v.x) {
-                    stage_elem_thread(win, d, e, v.x, v.y, pos, sz);
-                }
+                if (v.x) stage_elem_thread(win, d, e, v.x, v.y, pos, sz);
                 __syncthreads();
                 copy_out(buf, sh, wl, out, g);
                 __syncthreads();
@@ -1138,7 +1071,7 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                            vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
     else if (kind == LASPJ_KIND_ORSET)
-        hipLaunchKernelGGL(k_orset_etf_write<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+        hipLaunchKernelGGL(k_orset_etf_write, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
