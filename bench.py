@@ -341,6 +341,7 @@ def main():
 def _final_barrier(dist):
     try:
         dist.barrier()
+        dist.destroy_process_group()
     except Exception as e:               # the line is printed; a lost peer is not fatal
         print(f"final barrier: {type(e).__name__}: {e}", file=sys.stderr)
 
