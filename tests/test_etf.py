@@ -345,3 +345,42 @@ def test_gpu_record_kernel_whole_buffer_equals_staging():
     for o2, p2 in rest:
         assert np.array_equal(o1, o2)
         assert np.array_equal(p1, p2)
+
+
+@pytest.mark.gpu
+def test_gpu_record_kernel_runs_with_tiny_payloads():
+    """6000 replicas (several per block run): empty payloads (2 / 4 bytes), one-token
+    payloads shorter than 16 bytes of element data, and larger ones, interleaved — the
+    carry flows through payloads smaller than a 16-byte chunk; every payload equals the
+    oracle's, bare and tagged, under every writer variant."""
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle.otp import lists_sort
+    rng = random.Random(99)
+    toks = [bytes(rng.randrange(256) for _ in range(20)) for _ in range(12)]
+    states = []
+    for i in range(6000):
+        kind = rng.random()
+        d = {}
+        if kind < 0.4:
+            pass                                              # empty
+        elif kind < 0.8:
+            d[rng.randrange(5)] = {toks[rng.randrange(12)]: rng.random() < 0.5}
+        else:
+            for e in rng.sample(range(40), rng.randint(2, 30)):
+                d[e] = {t: rng.random() < 0.3 for t in rng.sample(toks, rng.randint(1, 12))}
+        states.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in lists_sort(list(d))])
+    dom = Domain()
+    for s in states:
+        dom.register_orset(s)
+    E = dom.size
+    ctx = context()
+    b = ctx.orset_batch(len(states), E)
+    b.upload(dom.encode_orset(states, E))
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    want = [oetf.term_to_binary(s) for s in states]
+    for bare, tagged in _etf_variants(ctx, lambda: (b.to_binaries(d),
+                                                    b.to_binaries(d, tag=etf.DT_ORSET_TAG))):
+        assert bare == want
+        assert tagged == [bytes([etf.DT_ORSET_TAG, 1]) + w for w in want]
