@@ -363,6 +363,26 @@ int laspj_gset_etf_size(laspj_ctx* ctx, const laspj_batch* batch, const laspj_et
                         int tag, laspj_buf* offsets, uint64_t* total);
 int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_etf_dict* d,
                          int tag, int vers, const laspj_buf* offsets, laspj_buf* out);
+/* from_binary/1 — lasp_orset.erl:202-214 (riak_dt:from_binary/1 = binary_to_term/1) for
+ * a batch: payload bytes [offsets[i], offsets[i+1]) are decoded into replica i of
+ * `batch` (cleared first; replicas with a non-zero status are undefined).  A payload
+ * is <<Tag, Vers>> (when tag >= 0) ++ the external term format image of an orddict
+ * whose element and token terms are in the dictionary, in term order, with flags
+ * `true` / `false` (ATOM_EXT, ATOM_UTF8_EXT or SMALL_ATOM_UTF8_EXT).  Needs a dictionary
+ * whose token images all have one length (else LASPJ_E_UNSUPPORTED); element images up
+ * to ~2 KiB.  status: R int32 of LASPJ_DEC_*. */
+#define LASPJ_DEC_OK                  0
+#define LASPJ_DEC_INVALID_BINARY      1  /* not <<Tag, _, ...>>: ?INVALID_BINARY            */
+#define LASPJ_DEC_UNSUPPORTED_VERSION 2  /* tag matches, version does not: ?UNSUPPORTED_VERSION(V) */
+#define LASPJ_DEC_MALFORMED           3  /* binary_to_term would fail (no 131, truncated,
+                                            trailing bytes) or the term is not an orddict
+                                            of {Elem, [{Token, Flag}]}                    */
+#define LASPJ_DEC_UNKNOWN_TERM        4  /* an element or token outside the dictionary, or
+                                            out of term order (not an orddict)           */
+#define LASPJ_DEC_UNREPRESENTABLE     5  /* an element with no tokens or more than 64     */
+int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict* d,
+                         int tag, int vers, const laspj_buf* payload,
+                         const laspj_buf* offsets, laspj_buf* status);
 
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);

@@ -20,6 +20,9 @@ E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 KIND_GCOUNTER = 6
 KIND_ORSET_PRODUCT_WIDE = 7
+# from_binary statuses (laspj_orset_etf_read)
+DEC_OK, DEC_INVALID_BINARY, DEC_UNSUPPORTED_VERSION, DEC_MALFORMED, DEC_UNKNOWN_TERM, \
+    DEC_UNREPRESENTABLE = 0, 1, 2, 3, 4, 5
 OP_ADD, OP_REMOVE, OP_INSERT = 1, 2, 3
 OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK, OPST_KEY_EXISTS = 0, 1, 2, 3
@@ -130,6 +133,7 @@ SIGNATURES = {
     "laspj_orset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
     "laspj_gset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
     "laspj_gset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
+    "laspj_orset_etf_read": (i, [vp, vp, vp, i, i, vp, vp, vp]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

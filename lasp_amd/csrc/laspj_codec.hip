@@ -947,6 +947,213 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uin
     }
 }
 
+// ------------------------------------------------------------------ from_binary/1
+// binary_to_term of OR-Set payloads into cells (lasp_orset.erl:202-214 decodes with
+// riak_dt:from_binary/1 = binary_to_term/1), for dictionaries with uniform token images.
+// One wave parses one replica: the payload streams through a 2 KiB LDS window; the
+// element at the cursor is found by 64 lanes comparing the header templates
+// `104 2 <elem image> 108` of the next 64 elements in term order, each record likewise
+// by 64 lanes comparing `104 2 <token image>` of the element's next 64 token ranks,
+// then the flag atom (ATOM_EXT, ATOM_UTF8_EXT or SMALL_ATOM_UTF8_EXT).  Elements and
+// tokens must come in term order (an orddict), so every comparison is a forward scan.
+constexpr uint32_t kDWin = 2048;
+
+struct Stage {
+    uint8_t* buf;          // wave-private LDS window
+    const uint8_t* src;    // the payload buffer
+    u64 total;             // bytes in the payload buffer
+    u64 lo, hi;            // staged [lo, hi)
+};
+
+// make [p, p + n) resident (n <= kDWin - 16; wave-uniform); false past `lim`
+__device__ bool stage_span(Stage& s, u64 p, uint32_t n, u64 lim) {
+    if (p + n > lim) return false;
+    if (p >= s.lo && p + n <= s.hi) return true;
+    const u64 lo = p & ~15ull;
+    const u64 hi = min(s.total, lo + kDWin);
+    const uint32_t lane = threadIdx.x & 63u;
+    wave_sync();
+    const u64 nfull = (hi - lo) >> 4;
+    for (u64 v = lane; v < nfull; v += 64)
+        reinterpret_cast<u32x4*>(s.buf)[v] = *reinterpret_cast<const u32x4*>(s.src + lo + 16 * v);
+    for (u64 b = lo + 16 * nfull + lane; b < hi; b += 64) s.buf[b - lo] = s.src[b];
+    wave_sync();
+    s.lo = lo;
+    s.hi = hi;
+    return true;
+}
+
+__device__ __forceinline__ uint32_t at(const Stage& s, u64 p) { return s.buf[p - s.lo]; }
+
+// staged bytes [p, p + L) equal the 16-byte-aligned, zero-padded template (L <= 48)
+__device__ __forceinline__ bool same48(const Stage& s, u64 p, const uint8_t* t16, uint32_t L) {
+    const u32x4* t = reinterpret_cast<const u32x4*>(t16);
+    const u32x4 z = {0, 0, 0, 0};
+    const u32x4 a = t[0], b = L > 16 ? t[1] : z, c = L > 32 ? t[2] : z;
+    const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    const uint8_t* q = s.buf + (p - s.lo);
+    bool eq = true;
+#pragma unroll
+    for (uint32_t i = 0; i < 48; ++i)
+        if (i < L) eq &= q[i] == ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+    return eq;
+}
+
+// longer templates (element images past 45 bytes), already staged
+__device__ bool same_long(const Stage& s, u64 p, const uint8_t* t, uint32_t L) {
+    const uint8_t* q = s.buf + (p - s.lo);
+    for (uint32_t i = 0; i < L; ++i)
+        if (q[i] != t[i]) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
+                                                           const u64* offs, uint64_t R,
+                                                           uint32_t E, DictView d, int tag,
+                                                           int vers, u64x2* cells,
+                                                           int32_t* status) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
+        Stage s{stage[wave], payload, total, 0, 0};
+        const u64 base = offs[rep], end = offs[rep + 1];
+        u64 p = base;
+        int32_t st = LASPJ_DEC_OK;
+        u64x2* c = cells + rep * E;
+        do {
+            if (tag >= 0) {
+                if (!stage_span(s, p, 2, end) || at(s, p) != (uint32_t)(tag & 0xFF)) {
+                    st = LASPJ_DEC_INVALID_BINARY;
+                    break;
+                }
+                if (at(s, p + 1) != (uint32_t)(vers & 0xFF)) {
+                    st = LASPJ_DEC_UNSUPPORTED_VERSION;
+                    break;
+                }
+                p += 2;
+            }
+            if (!stage_span(s, p, 2, end) || at(s, p) != 131) {
+                st = LASPJ_DEC_MALFORMED;                 // binary_to_term: badarg
+                break;
+            }
+            uint32_t n = 0;
+            if (at(s, p + 1) == 106) {
+                p += 2;
+            } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
+                n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
+                p += 6;
+            } else {
+                st = LASPJ_DEC_MALFORMED;
+                break;
+            }
+            int64_t prev = -1;                    // term rank of the previous element
+            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
+                // 104 2 <elem image> 108 of the next elements in term order
+                const uint32_t span = (uint32_t)min((u64)(kDWin - 16), end - p);
+                if (!stage_span(s, p, span, end)) { st = LASPJ_DEC_MALFORMED; break; }
+                int64_t found = -1;
+                uint32_t e = 0, hl = 0;
+                for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
+                    const int64_t r = c0 + lane;
+                    bool hit = false;
+                    uint32_t ec = 0, hlc = 0;
+                    if (r < (int64_t)E) {
+                        ec = d.elem_order[r];
+                        hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                        // 104 2 <elem image> (the template's closing 108 is checked below)
+                        if (hlc > 3u && hlc <= span) {
+                            const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
+                            hit = hlc - 1u <= 48 ? same48(s, p, t, hlc - 1u)
+                                                 : same_long(s, p, t, hlc - 1u);
+                        }
+                    }
+                    const u64 m = __ballot(hit);
+                    if (m) {
+                        const uint32_t w = (uint32_t)__ffsll((long long)m) - 1u;
+                        found = c0 + w;
+                        e = __shfl(ec, w, 64);
+                        hl = __shfl(hlc, w, 64);
+                    }
+                }
+                if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                prev = found;
+                p += hl;
+                if (at(s, p - 1) != 108) {                 // [] tokens: no columnar form
+                    st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
+                    break;
+                }
+                if (p + 4 > s.hi) { st = LASPJ_DEC_MALFORMED; break; }   // truncated count
+                const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
+                                       at(s, p + 3);
+                p += 4;
+                if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+                u64 pb = 0, rb = 0;
+                int32_t tprev = -1;
+                for (uint32_t j = 0; j < m_tok; ++j) {
+                    if (!stage_span(s, p, RL + 8u, end) && !stage_span(s, p, RL + 6u, end)) {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    const int32_t q = tprev + 1 + (int32_t)lane;
+                    bool hit = false;
+                    if (q < (int32_t)RK && p + RL <= s.hi)
+                        hit = same48(s, p, d.rec_pad + ((u64)e * RK + (uint32_t)q) * RS, RL);
+                    const u64 m = __ballot(hit);
+                    if (!m) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                    const int32_t rank = tprev + (int32_t)__ffsll((long long)m);
+                    tprev = rank;
+                    p += RL;
+                    // the flag: ATOM_EXT / ATOM_UTF8_EXT (100 / 118, 2-byte length) or
+                    // SMALL_ATOM_UTF8_EXT (119, 1-byte length), "true" or "false"
+                    const uint32_t t0 = p < s.hi ? at(s, p) : 0u;
+                    uint32_t len, h;
+                    if ((t0 == 100 || t0 == 118) && p + 3 <= s.hi && at(s, p + 1) == 0) {
+                        len = at(s, p + 2);
+                        h = 3;
+                    } else if (t0 == 119 && p + 2 <= s.hi) {
+                        len = at(s, p + 1);
+                        h = 2;
+                    } else {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    bool flag;
+                    if (len == 4 && p + h + 4 <= end && stage_span(s, p, h + 4, end) &&
+                        at(s, p + h) == 't' && at(s, p + h + 1) == 'r' && at(s, p + h + 2) == 'u' &&
+                        at(s, p + h + 3) == 'e') {
+                        flag = true;
+                    } else if (len == 5 && p + h + 5 <= end && stage_span(s, p, h + 5, end) &&
+                               at(s, p + h) == 'f' && at(s, p + h + 1) == 'a' &&
+                               at(s, p + h + 2) == 'l' && at(s, p + h + 3) == 's' &&
+                               at(s, p + h + 4) == 'e') {
+                        flag = false;
+                    } else {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    p += h + len;
+                    const uint32_t slot = d.tok_order[64ull * e + (uint32_t)rank];
+                    pb |= 1ull << slot;
+                    if (flag) rb |= 1ull << slot;
+                }
+                if (st != LASPJ_DEC_OK) break;
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+                if (lane == 0) c[e] = u64x2{pb, rb};
+            }
+            if (st != LASPJ_DEC_OK) break;
+            if (n) {
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+            }
+            if (p != end) st = LASPJ_DEC_MALFORMED;      // trailing bytes
+        } while (false);
+        if (lane == 0) status[rep] = st;
+    }
+}
+
 struct Guard {
     std::lock_guard<std::mutex> lk;
     explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
@@ -1080,6 +1287,44 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                            (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
                            view(d), tag, vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+
+int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+             const laspj_buf* payload, const laspj_buf* offsets, laspj_buf* status) {
+    const char* what = "orset_etf_read";
+    if (int s = check_args(ctx, b, d, LASPJ_KIND_ORSET, what)) return s;
+    if (!d->rec_len)
+        return fail(ctx, LASPJ_E_UNSUPPORTED, "%s: token images of different lengths", what);
+    if (!payload || payload->ctx != ctx || !offsets || offsets->ctx != ctx || !status ||
+        status->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad buffer", what);
+    if (offsets->bytes < 8ull * (b->replicas + 1) || status->bytes < 4ull * b->replicas)
+        return fail(ctx, LASPJ_E_RANGE, "%s: offsets must hold R + 1 uint64, status R int32",
+                    what);
+    if (tag > 255 || vers < 0 || vers > 255)
+        return fail(ctx, LASPJ_E_INVAL, "%s: tag and version are bytes", what);
+    Guard g(ctx);
+    const uint64_t R = b->replicas;
+    std::vector<u64> off(R + 1);
+    LJ_HIP(ctx, hipMemcpyAsync(off.data(), offsets->dev, 8ull * (R + 1), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint64_t i = 0; i < R; ++i)
+        if (off[i] > off[i + 1])
+            return fail(ctx, LASPJ_E_RANGE, "%s: offsets decrease at replica %llu", what,
+                        (unsigned long long)i);
+    if (off[R] > payload->bytes)
+        return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
+    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
+    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
+    const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
+    hipLaunchKernelGGL(k_orset_etf_read, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
+                       static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tag, vers,
+                       reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev));
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }
@@ -1309,6 +1554,12 @@ int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_d
                          int vers, const laspj_buf* offsets, laspj_buf* out) {
     return laspj::etf_write(ctx, b, d, tag, vers, offsets, out, LASPJ_KIND_GSET,
                             "gset_etf_write");
+}
+
+int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag,
+                         int vers, const laspj_buf* payload, const laspj_buf* offsets,
+                         laspj_buf* status) {
+    return laspj::etf_read(ctx, b, d, tag, vers, payload, offsets, status);
 }
 
 }  // extern "C"

@@ -384,3 +384,164 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
                                                     b.to_binaries(d, tag=etf.DT_ORSET_TAG))):
         assert bare == want
         assert tagged == [bytes([etf.DT_ORSET_TAG, 1]) + w for w in want]
+
+
+def _decode_setup(states, rng_seed=0):
+    from lasp_amd import engine
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    dom = Domain()
+    for s in states:
+        dom.register_orset(s)
+    E = dom.size + 5
+    ctx = context()
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    return ctx, dom, E, d
+
+
+def _upload_payloads(ctx, blobs):
+    import numpy as np
+    off = np.zeros(len(blobs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in blobs])
+    flat = b"".join(blobs) or b"\0"
+    pay = ctx.buffer(len(flat))
+    pay.upload(np.frombuffer(flat, np.uint8))
+    offs = ctx.buffer(8 * len(off))
+    offs.upload(off)
+    return pay, offs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tagged", [False, True])
+def test_gpu_from_binary_round_trip(tagged):
+    """Device from_binary/1 of oracle payloads (term_to_binary of random orddicts with
+    20-byte tokens, long and short element terms) yields the same cells the host
+    encoder gives, and device to_binary -> from_binary is the identity on cells."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    rng = random.Random(31 + tagged)
+    states = _random_orsets(rng, 200, mixed=False)
+    states += [[], [((PAtom("k"), b"v" * 50), [(b"t" * 20, True)])],
+               [(1 << 70, [(b"u" * 20, False), (b"w" * 20, True)])]]
+    ctx, dom, E, d = _decode_setup(states)
+    tag = etf.DT_ORSET_TAG if tagged else -1
+    blobs = [oetf.to_binary(tag, 1, s) if tagged else oetf.term_to_binary(s) for s in states]
+    pay, offs = _upload_payloads(ctx, blobs)
+    b = ctx.orset_batch(len(states), E)
+    st = b.etf_decode(d, pay, offs, tag=tag, vers=1)
+    assert (st == _lib.DEC_OK).all(), np.nonzero(st)[0][:10]
+    want = dom.encode_orset(states, E)
+    assert np.array_equal(b.download(), want)
+    # device to_binary -> from_binary
+    offs2, out2, _ = b.etf_encode(d, tag=tag, vers=1)
+    b2 = ctx.orset_batch(len(states), E)
+    assert (b2.etf_decode(d, out2, offs2, tag=tag, vers=1) == 0).all()
+    assert np.array_equal(b2.download(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_errors_and_atom_forms():
+    """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
+    malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
+    outside the dictionary or out of term order; SMALL_ATOM_UTF8_EXT / ATOM_UTF8_EXT
+    flags (what newer OTP releases emit) decode like ATOM_EXT.  No payload faults."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    tok = [bytes([k]) * 20 for k in range(1, 6)]
+    s0 = [(1, [(tok[0], False), (tok[1], True)]), (2, [(tok[2], False)])]
+    ctx, dom, E, d = _decode_setup([s0, [(3, [(tok[3], True)])]])
+    T = etf.DT_ORSET_TAG
+    good = oetf.to_binary(T, 1, s0)
+    small_atoms = good.replace(bytes([100, 0, 4]) + b"true", bytes([119, 4]) + b"true") \
+                      .replace(bytes([100, 0, 5]) + b"false", bytes([119, 5]) + b"false")
+    utf8_atoms = good.replace(bytes([100, 0, 4]) + b"true", bytes([118, 0, 4]) + b"true")
+    unknown = oetf.to_binary(T, 1, [(1, [(b"z" * 20, False)])])
+    out_of_order = oetf.to_binary(T, 1, [(2, [(tok[2], False)]), (1, [(tok[0], False)])])
+    no_tokens = oetf.to_binary(T, 1, [(1, [])])
+    bad_flag = good.replace(b"false", b"fals\x65"[:4] + b"x", 1)
+    cases = [
+        (good, _lib.DEC_OK), (small_atoms, _lib.DEC_OK), (utf8_atoms, _lib.DEC_OK),
+        (bytes([T + 1]) + good[1:], _lib.DEC_INVALID_BINARY),
+        (bytes([T, 2]) + good[2:], _lib.DEC_UNSUPPORTED_VERSION),
+        (b"", _lib.DEC_INVALID_BINARY), (bytes([T, 1, 130]) + good[3:], _lib.DEC_MALFORMED),
+        (good[:-1], _lib.DEC_MALFORMED), (good + b"\0", _lib.DEC_MALFORMED),
+        (good[:len(good) // 2], _lib.DEC_MALFORMED), (bad_flag, _lib.DEC_MALFORMED),
+        (unknown, _lib.DEC_UNKNOWN_TERM), (out_of_order, _lib.DEC_UNKNOWN_TERM),
+        (no_tokens, _lib.DEC_UNREPRESENTABLE),
+        (oetf.to_binary(T, 1, []), _lib.DEC_OK),
+    ]
+    pay, offs = _upload_payloads(ctx, [c[0] for c in cases])
+    b = ctx.orset_batch(len(cases), E)
+    st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert list(st) == [c[1] for c in cases]
+    cells = b.download()
+    want = dom.encode_orset([s0], E)[0]
+    for i in (0, 1, 2):
+        assert np.array_equal(cells[i], want)
+    assert not cells[len(cases) - 1].any()
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_large_round_trip():
+    """4096 replicas x 512 slots x 64 token slots: device to_binary then from_binary
+    restores every cell."""
+    import numpy as np
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle import columnar as orc
+    R, E = 4096, 512
+    ctx = context()
+    b = ctx.orset_batch(R, E)
+    b.fill_synthetic(17)
+    toks = orc.synth_tokens(E)
+    dom = Domain()
+    for e in range(E):
+        es = dom.element_slot(e)
+        for k in range(64):
+            dom.token_slot(es, bytes(toks[e][k]))
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    offs, out, _ = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
+    b2 = ctx.orset_batch(R, E)
+    st = b2.etf_decode(d, out, offs, tag=etf.DT_ORSET_TAG, vers=1)
+    assert (st == 0).all()
+    assert np.array_equal(b2.download(), b.download())
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_fuzz():
+    """2000 corrupted payloads (byte flips, truncations, insertions, splices of two
+    payloads): every status is a LASPJ_DEC_* code, a payload that decodes OK re-encodes
+    to itself, and nothing faults."""
+    import numpy as np
+    from lasp_amd import etf
+    rng = random.Random(77)
+    states = _random_orsets(rng, 60, mixed=False)
+    ctx, dom, E, d = _decode_setup(states)
+    T = etf.DT_ORSET_TAG
+    base = [oetf.to_binary(T, 1, s) for s in states]
+    blobs = []
+    for _ in range(2000):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(4)
+        if kind == 0 and b:
+            for _ in range(rng.randint(1, 3)):
+                b[rng.randrange(len(b))] = rng.randrange(256)
+        elif kind == 1 and b:
+            del b[rng.randrange(len(b)):]
+        elif kind == 2:
+            pos = rng.randrange(len(b) + 1)
+            b[pos:pos] = bytes(rng.randrange(256) for _ in range(rng.randint(1, 9)))
+        else:
+            other = rng.choice(base)
+            b = b[:rng.randrange(len(b) + 1)] + other[rng.randrange(len(other) + 1):]
+        blobs.append(bytes(b))
+    pay, offs = _upload_payloads(ctx, blobs)
+    bt = ctx.orset_batch(len(blobs), E)
+    st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert set(np.unique(st)) <= {0, 1, 2, 3, 4, 5}
+    ok = np.nonzero(st == 0)[0]
+    if len(ok):
+        again = bt.to_binaries(d, tag=T, vers=1)
+        for i in ok:
+            assert again[i] == blobs[i], i

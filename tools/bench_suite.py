@@ -294,6 +294,16 @@ def etf(ctx, steps):
                    "cells_per_s", replicas=R, elements=E, payload_bytes=total.value,
                    payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
         ctx.set_tuning(_lib.TUNE_ETF_KERNEL, 0)
+        # from_binary: the payloads just written, decoded back into a batch
+        _lib.check(L.laspj_orset_etf_write(ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h)
+        back = ctx.orset_batch(R, E)
+        stb = ctx.buffer(4 * R)
+        ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_read(
+            ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h), ctx.h), steps)
+        report(f"orset_etf_read_{tag}", ms, 16 * cells + total.value, cells, "cells_per_s",
+               replicas=R, elements=E, payload_bytes=total.value,
+               payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        del back, stb
         del out, offs, d, b
 
 
