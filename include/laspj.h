@@ -133,6 +133,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         32, 64, 128, 256                                */
 #define LASPJ_TUNE_PRODUCT_COLS  7   /* columns per outer-product tile: 0 = default
                                         (1024), 2048, 4096                              */
+#define LASPJ_TUNE_ETF_READ      8   /* OR-Set from_binary: 0 = batched records when the
+                                        dictionary's record templates hash apart within
+                                        every element, 1 = serial record scan            */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -30,6 +30,7 @@ TUNE_STREAM_GRID, TUNE_STREAM_UNROLL, TUNE_STREAM_NT, TUNE_ETF_KERNEL = 1, 2, 3,
 TUNE_REDUCE_KERNEL = 5
 TUNE_PRODUCT_ROWS = 6
 TUNE_PRODUCT_COLS = 7
+TUNE_ETF_READ = 8
 
 
 class LaspjUnavailable(RuntimeError):

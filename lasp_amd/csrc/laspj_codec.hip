@@ -27,6 +27,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <new>
 #include <vector>
 
@@ -63,6 +64,10 @@ struct laspj_etf_dict {
     const uint8_t* rec_pad = nullptr;
     const uint8_t* ehdr_pad = nullptr;
     const uint32_t* ehdr_poff = nullptr;   // E
+    uint32_t ehdr_max = 0;                 // longest element header template
+    // per (element, term rank < tok_max): laspj::rec_hash of the record template; null
+    // when two templates of one element hash alike (from_binary then scans serially)
+    const uint64_t* rec_hash = nullptr;
 };
 
 namespace laspj {
@@ -92,13 +97,32 @@ struct DictView {
     const uint8_t* rec_pad;
     const uint8_t* ehdr_pad;
     const uint32_t* ehdr_poff;
+    uint32_t ehdr_max;
 };
 
 DictView view(const laspj_etf_dict* d) {
     return {d->elem_blob, d->elem_off,  d->elem_order, d->elem_byte,  d->tok_blob,
             d->tok_off,   d->tok_order, d->tok_mask,   d->tok_uniform, d->elem_pad,
             d->elem_poff, d->tok_pad,   d->tok_poff,   d->tok_desc,    d->tok_max,
-            d->rec_len,   d->rec_stride, d->rec_pad,   d->ehdr_pad,    d->ehdr_poff};
+            d->rec_len,   d->rec_stride, d->rec_pad,   d->ehdr_pad,    d->ehdr_poff,
+            d->ehdr_max};
+}
+
+// 64-bit hash of a record template held as 12 little-endian words, zero past its length
+// (the host hashes rec_pad, the from_binary kernel the payload's record)
+__host__ __device__ __forceinline__ u64 rec_hash(const uint32_t (&w)[12]) {
+    uint32_t a = 0x9E3779B9u, b = 0x7F4A7C15u;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        a = (a ^ w[i]) * 0xCC9E2D51u;
+        a = (a << 15) | (a >> 17);
+        b = (b + w[i]) * 0x1B873593u;
+        b ^= b >> 13;
+    }
+    a ^= a >> 16;
+    a *= 0x85EBCA6Bu;
+    a ^= a >> 13;
+    return ((u64)a << 32) | b;
 }
 
 __device__ __forceinline__ u64 wave_sum(u64 v) {
@@ -985,6 +1009,16 @@ __device__ bool stage_span(Stage& s, u64 p, uint32_t n, u64 lim) {
 
 __device__ __forceinline__ uint32_t at(const Stage& s, u64 p) { return s.buf[p - s.lo]; }
 
+// 48-byte template in registers: words of a 16-byte-aligned zero-padded image
+__device__ __forceinline__ void load48(uint32_t (&w)[12], const uint8_t* t16, uint32_t L) {
+    const u32x4* t = reinterpret_cast<const u32x4*>(t16);
+    const u32x4 z = {0, 0, 0, 0};
+    const u32x4 a = t[0], b = L > 16 ? t[1] : z, c = L > 32 ? t[2] : z;
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w;
+}
+
 // staged bytes [p, p + L) equal the 16-byte-aligned, zero-padded template (L <= 48)
 __device__ __forceinline__ bool same48(const Stage& s, u64 p, const uint8_t* t16, uint32_t L) {
     const u32x4* t = reinterpret_cast<const u32x4*>(t16);
@@ -1007,11 +1041,11 @@ __device__ bool same_long(const Stage& s, u64 p, const uint8_t* t, uint32_t L) {
     return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
-                                                           const u64* offs, uint64_t R,
-                                                           uint32_t E, DictView d, int tag,
-                                                           int vers, u64x2* cells,
-                                                           int32_t* status) {
+__global__ __launch_bounds__(kBlock) void k_orset_etf_read_serial(const uint8_t* payload, u64 total,
+                                                                  const u64* offs, uint64_t R,
+                                                                  uint32_t E, DictView d, int tag,
+                                                                  int vers, u64x2* cells,
+                                                                  int32_t* status) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
@@ -1084,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payloa
                     st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
                     break;
                 }
-                if (p + 4 > s.hi) { st = LASPJ_DEC_MALFORMED; break; }   // truncated count
+                if (!stage_span(s, p, 4, end)) { st = LASPJ_DEC_MALFORMED; break; }  // truncated count
                 const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
                                        at(s, p + 3);
                 p += 4;
@@ -1137,6 +1171,240 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payloa
                     const uint32_t slot = d.tok_order[64ull * e + (uint32_t)rank];
                     pb |= 1ull << slot;
                     if (flag) rb |= 1ull << slot;
+                }
+                if (st != LASPJ_DEC_OK) break;
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+                if (lane == 0) c[e] = u64x2{pb, rb};
+            }
+            if (st != LASPJ_DEC_OK) break;
+            if (n) {
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+            }
+            if (p != end) st = LASPJ_DEC_MALFORMED;      // trailing bytes
+        } while (false);
+        if (lane == 0) status[rep] = st;
+    }
+}
+
+// Batched record decode (the default when every element's record templates hash apart,
+// see rec_hash below).  Element headers as in the serial scan, with the next rank in
+// term order tried first one byte per lane.  Records go in batches of up to 64: the wave
+// walks the record chain reading only each flag's header bytes (three LDS reads per
+// record, one address for every lane), then lane j takes record j: its token template
+// from LDS as aligned dwords, a 64-bit hash matched against the element's per-rank
+// template hashes (one ballot per record), an exact compare against the matched
+// template, the term-order check and the flag bytes.  The first failing record in stream
+// order gives the status the serial scan gives: templates are distinct within an
+// element, so "the first rank after the previous one whose template matches" is "the
+// one rank whose template matches, if it comes after the previous one".
+
+// words of staged bytes [o, o + L) (L <= 48), zero past L; reads 52 bytes from o & ~3
+__device__ __forceinline__ void rec_words(const uint8_t* buf, uint32_t o, uint32_t L,
+                                          uint32_t (&w)[12]) {
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf + (o & ~3u));
+    uint32_t q[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) q[i] = b32[i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(q[i + 1], q[i], o & 3u);
+        const int rem = (int)L - 4 * i;
+        w[i] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+    }
+}
+
+__device__ __forceinline__ u64 wave_or(u64 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
+                                                           const u64* offs, uint64_t R,
+                                                           uint32_t E, DictView d,
+                                                           const u64* rhash, int tag, int vers,
+                                                           u64x2* cells, int32_t* status) {
+    // 64 bytes of slack per window: rec_words reads up to 52 bytes from a record's start
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin + 64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint32_t hmax = min(d.ehdr_max + 4u, kDWin - 16u);
+    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
+        Stage s{stage[wave], payload, total, 0, 0};
+        const u64 base = offs[rep], end = offs[rep + 1];
+        u64 p = base;
+        int32_t st = LASPJ_DEC_OK;
+        u64x2* c = cells + rep * E;
+        do {
+            if (tag >= 0) {
+                if (!stage_span(s, p, 2, end) || at(s, p) != (uint32_t)(tag & 0xFF)) {
+                    st = LASPJ_DEC_INVALID_BINARY;
+                    break;
+                }
+                if (at(s, p + 1) != (uint32_t)(vers & 0xFF)) {
+                    st = LASPJ_DEC_UNSUPPORTED_VERSION;
+                    break;
+                }
+                p += 2;
+            }
+            if (!stage_span(s, p, 2, end) || at(s, p) != 131) {
+                st = LASPJ_DEC_MALFORMED;                 // binary_to_term: badarg
+                break;
+            }
+            uint32_t n = 0;
+            if (at(s, p + 1) == 106) {
+                p += 2;
+            } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
+                n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
+                p += 6;
+            } else {
+                st = LASPJ_DEC_MALFORMED;
+                break;
+            }
+            int64_t prev = -1;                    // term rank of the previous element
+            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
+                // 104 2 <elem image> 108 of the next elements in term order
+                const uint32_t span = (uint32_t)min((u64)hmax, end - p);
+                stage_span(s, p, span, end);
+                int64_t found = -1;
+                uint32_t e = 0, hl = 0;
+                if (prev + 1 < (int64_t)E) {      // the next rank, one byte per lane
+                    const uint32_t ec = d.elem_order[prev + 1];
+                    const uint32_t hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                    if (hlc > 3u && hlc <= span && hlc - 1u <= 64u) {
+                        const bool ok = lane >= hlc - 1u ||
+                                        at(s, p + lane) == d.ehdr_pad[d.ehdr_poff[ec] + lane];
+                        if (!__ballot(!ok)) {
+                            found = prev + 1;
+                            e = ec;
+                            hl = hlc;
+                        }
+                    }
+                }
+                for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
+                    const int64_t r = c0 + lane;
+                    bool hit = false;
+                    uint32_t ec = 0, hlc = 0;
+                    if (r < (int64_t)E) {
+                        ec = d.elem_order[r];
+                        hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                        // 104 2 <elem image> (the template's closing 108 is checked below)
+                        if (hlc > 3u && hlc <= span) {
+                            const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
+                            hit = hlc - 1u <= 48 ? same48(s, p, t, hlc - 1u)
+                                                 : same_long(s, p, t, hlc - 1u);
+                        }
+                    }
+                    const u64 m = __ballot(hit);
+                    if (m) {
+                        const uint32_t w = (uint32_t)__ffsll((long long)m) - 1u;
+                        found = c0 + w;
+                        e = __shfl(ec, w, 64);
+                        hl = __shfl(hlc, w, 64);
+                    }
+                }
+                if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                prev = found;
+                p += hl;
+                if (at(s, p - 1) != 108) {                 // [] tokens: no columnar form
+                    st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
+                    break;
+                }
+                if (!stage_span(s, p, 4, end)) { st = LASPJ_DEC_MALFORMED; break; }  // truncated count
+                const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
+                                       at(s, p + 3);
+                p += 4;
+                if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+                // lane k: hash of the template of token rank k (ranks < cnt exist)
+                const uint32_t cnt = (uint32_t)__popcll(d.tok_mask[e]);
+                const u64 th = lane < cnt ? rhash[(u64)e * RK + lane] : 0ull;
+                u64 pb = 0, rb = 0;
+                int32_t tprev = -1;
+                for (uint32_t done = 0; done < m_tok;) {
+                    // the chain: record starts from the flags' header bytes
+                    uint32_t nb = 0;
+                    bool trunc = false;
+                    u64 x = p, myx = 0;
+                    while (nb < 64 && done + nb < m_tok) {
+                        if (x + RL + 6 > end) { trunc = true; break; }
+                        if (x + RL + 8 > s.hi && s.hi < end) {   // record past the window
+                            if (nb) break;
+                            stage_span(s, x, (uint32_t)min((u64)RL + 8, end - x), end);
+                        }
+                        if (lane == nb) myx = x;
+                        const uint32_t t0 = at(s, x + RL), b1 = at(s, x + RL + 1),
+                                       b2 = at(s, x + RL + 2);
+                        uint32_t h = 0, len = 0;
+                        if ((t0 == 100 || t0 == 118) && b1 == 0) { h = 3; len = b2; }
+                        else if (t0 == 119) { h = 2; len = b1; }
+                        ++nb;
+                        // a bad flag header ends the chain; lane nb - 1 reports it
+                        if ((len != 4 && len != 5) || x + RL + h + len > end) break;
+                        x += RL + h + len;
+                    }
+                    // lane j < nb: record j
+                    const bool mine = lane < nb;
+                    uint32_t w[12];
+                    u64 hh = 0;
+                    if (mine) {
+                        rec_words(s.buf, (uint32_t)(myx - s.lo), RL, w);
+                        hh = rec_hash(w);
+                    }
+                    int32_t rank = -1;
+                    for (uint32_t j = 0; j < nb; ++j) {
+                        const u64 hj = __shfl(hh, j, 64);
+                        const u64 m = __ballot(lane < cnt && th == hj);
+                        if (lane == j && m) rank = (int32_t)__ffsll((long long)m) - 1;
+                    }
+                    int32_t lst = LASPJ_DEC_OK;
+                    bool flag = false;
+                    const int32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+                    if (mine) {
+                        if (rank >= 0) {                    // exact compare
+                            uint32_t t[12];
+                            load48(t, d.rec_pad + ((u64)e * RK + (uint32_t)rank) * RS, RL);
+                            bool eq = true;
+#pragma unroll
+                            for (int i = 0; i < 12; ++i) eq &= t[i] == w[i];
+                            if (!eq) rank = -1;
+                        }
+                        if (rank < 0 || rank <= (lane ? pr : tprev)) {
+                            lst = LASPJ_DEC_UNKNOWN_TERM;
+                        } else {
+                            // ATOM_EXT / ATOM_UTF8_EXT (2-byte length) or SMALL_ATOM_UTF8_EXT
+                            const u64 q = myx + RL;
+                            const uint32_t t0 = at(s, q), b1 = at(s, q + 1);
+                            uint32_t h = 0, len = 0;
+                            if ((t0 == 100 || t0 == 118) && b1 == 0) { h = 3; len = at(s, q + 2); }
+                            else if (t0 == 119) { h = 2; len = b1; }
+                            const u64 f = q + h;
+                            if (h && len == 4 && f + 4 <= end && at(s, f) == 't' &&
+                                at(s, f + 1) == 'r' && at(s, f + 2) == 'u' && at(s, f + 3) == 'e')
+                                flag = true;
+                            else if (h && len == 5 && f + 5 <= end && at(s, f) == 'f' &&
+                                     at(s, f + 1) == 'a' && at(s, f + 2) == 'l' &&
+                                     at(s, f + 3) == 's' && at(s, f + 4) == 'e')
+                                flag = false;
+                            else
+                                lst = LASPJ_DEC_MALFORMED;
+                        }
+                    }
+                    const u64 bad = __ballot(lst != LASPJ_DEC_OK);
+                    if (bad) {
+                        st = __shfl(lst, (uint32_t)__ffsll((long long)bad) - 1u, 64);
+                        break;
+                    }
+                    if (trunc) { st = LASPJ_DEC_MALFORMED; break; }
+                    u64 pbit = 0;
+                    if (mine) pbit = 1ull << d.tok_order[64ull * e + (uint32_t)rank];
+                    pb |= wave_or(pbit);
+                    rb |= wave_or(flag ? pbit : 0ull);
+                    tprev = __shfl(rank, nb - 1u, 64);
+                    done += nb;
+                    p = x;
                 }
                 if (st != LASPJ_DEC_OK) break;
                 if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
@@ -1321,10 +1589,18 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    hipLaunchKernelGGL(k_orset_etf_read, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
-                       static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tag, vers,
-                       reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev));
+    if (d->rec_hash && ctx->tune_etf_read == 0)
+        hipLaunchKernelGGL(k_orset_etf_read, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
+                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d),
+                           reinterpret_cast<const u64*>(d->rec_hash), tag, vers,
+                           reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev));
+    else
+        hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
+                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tag,
+                           vers, reinterpret_cast<u64x2*>(b->dev),
+                           static_cast<int32_t*>(status->dev));
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }
@@ -1417,8 +1693,11 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     // and 104 2 <elem image> 108 per element
     const uint32_t rec_len = (toks && !mixed && uniform && uniform + 2u <= 48u) ? uniform + 2u : 0u;
     const uint64_t rec_stride = pad16(rec_len);
+    uint64_t ehdr_max = 0;
     std::vector<uint8_t> rpad, hpad;
     std::vector<uint32_t> hpoff;
+    std::vector<uint64_t> rhash;
+    bool hashed = rec_len != 0;
     if (rec_len) {
         rpad.assign((uint64_t)E * tok_max * rec_stride + 48, 0);
         for (uint64_t e = 0; e < E; ++e)
@@ -1436,6 +1715,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         for (uint32_t e = 0; e < E; ++e) {
             hpoff[e] = (uint32_t)hn;
             hn += pad16(elem_off[e + 1] - elem_off[e] + 3ull);
+            ehdr_max = std::max<uint64_t>(ehdr_max, elem_off[e + 1] - elem_off[e] + 3ull);
         }
         if (hn + 48 >= (1ull << 32) || rpad.size() >= (1ull << 40))
             return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: record templates too large");
@@ -1446,6 +1726,21 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
             h[1] = 2;
             std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], h + 2);
             h[2 + elem_off[e + 1] - elem_off[e]] = 108;
+        }
+        // template hashes; any two alike within one element turn the batched decode off
+        rhash.assign((uint64_t)E * tok_max, 0);
+        std::vector<uint64_t> hs;
+        for (uint64_t e = 0; e < E && hashed; ++e) {
+            hs.clear();
+            for (uint32_t j = 0; j < tok_max && tok_order[64ull * e + j] < 64; ++j) {
+                const uint8_t* r = rpad.data() + (e * tok_max + j) * rec_stride;
+                uint32_t w[12] = {};
+                std::memcpy(w, r, rec_len);     // little-endian words, zero past rec_len
+                rhash[e * tok_max + j] = laspj::rec_hash(w);
+                hs.push_back(rhash[e * tok_max + j]);
+            }
+            std::sort(hs.begin(), hs.end());
+            hashed = std::adjacent_find(hs.begin(), hs.end()) == hs.end();
         }
     }
     for (uint64_t t = 0; t < tpoff.size(); ++t)
@@ -1459,7 +1754,8 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
                    o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
-                   bytes = o_hpoff + al(4ull * hpoff.size() + 4);
+                   o_rhash = o_hpoff + al(4ull * hpoff.size() + 4),
+                   bytes = o_rhash + al(8ull * rhash.size() + 8);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1490,6 +1786,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess && rec_len) e = up(o_rpad, rpad.data(), rpad.size());
     if (e == hipSuccess && rec_len) e = up(o_hpad, hpad.data(), hpad.size());
     if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
+    if (e == hipSuccess && hashed) e = up(o_rhash, rhash.data(), 8ull * rhash.size());
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -1501,10 +1798,12 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->tok_uniform = mixed ? 0u : uniform;
     d->tok_max = tok_max;
     d->rec_len = rec_len;
+    d->ehdr_max = (uint32_t)std::min<uint64_t>(ehdr_max, 0xFFFFFFFFull);
     d->rec_stride = (uint32_t)rec_stride;
     d->rec_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_rpad) : nullptr;
     d->ehdr_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_hpad) : nullptr;
     d->ehdr_poff = rec_len ? reinterpret_cast<const uint32_t*>(base + o_hpoff) : nullptr;
+    d->rec_hash = hashed ? reinterpret_cast<const uint64_t*>(base + o_rhash) : nullptr;
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);

@@ -241,6 +241,11 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
                 return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..5");
             ctx->tune_etf = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_ETF_READ:
+            if (value < 0 || value > 1)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0 or 1");
+            ctx->tune_etf_read = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

@@ -9,6 +9,7 @@ reference's round-trip property from_binary(to_binary(S)) == S
 (test/crdt_statem_eqc.erl:108-121).
 """
 
+import contextlib
 import json
 import os
 import random
@@ -386,6 +387,17 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
         assert tagged == [bytes([etf.DT_ORSET_TAG, 1]) + w for w in want]
 
 
+@contextlib.contextmanager
+def _read_kernel(ctx, knob):
+    """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records, 1 = serial scan."""
+    from lasp_amd import _lib
+    ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
+    try:
+        yield
+    finally:
+        ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
+
+
 def _decode_setup(states, rng_seed=0):
     from lasp_amd import engine
     from lasp_amd.codec import Domain
@@ -412,8 +424,9 @@ def _upload_payloads(ctx, blobs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("knob", [0, 1])
 @pytest.mark.parametrize("tagged", [False, True])
-def test_gpu_from_binary_round_trip(tagged):
+def test_gpu_from_binary_round_trip(tagged, knob):
     """Device from_binary/1 of oracle payloads (term_to_binary of random orddicts with
     20-byte tokens, long and short element terms) yields the same cells the host
     encoder gives, and device to_binary -> from_binary is the identity on cells."""
@@ -428,19 +441,21 @@ def test_gpu_from_binary_round_trip(tagged):
     blobs = [oetf.to_binary(tag, 1, s) if tagged else oetf.term_to_binary(s) for s in states]
     pay, offs = _upload_payloads(ctx, blobs)
     b = ctx.orset_batch(len(states), E)
-    st = b.etf_decode(d, pay, offs, tag=tag, vers=1)
-    assert (st == _lib.DEC_OK).all(), np.nonzero(st)[0][:10]
-    want = dom.encode_orset(states, E)
-    assert np.array_equal(b.download(), want)
-    # device to_binary -> from_binary
-    offs2, out2, _ = b.etf_encode(d, tag=tag, vers=1)
-    b2 = ctx.orset_batch(len(states), E)
-    assert (b2.etf_decode(d, out2, offs2, tag=tag, vers=1) == 0).all()
-    assert np.array_equal(b2.download(), want)
+    with _read_kernel(ctx, knob):
+        st = b.etf_decode(d, pay, offs, tag=tag, vers=1)
+        assert (st == _lib.DEC_OK).all(), np.nonzero(st)[0][:10]
+        want = dom.encode_orset(states, E)
+        assert np.array_equal(b.download(), want)
+        # device to_binary -> from_binary
+        offs2, out2, _ = b.etf_encode(d, tag=tag, vers=1)
+        b2 = ctx.orset_batch(len(states), E)
+        assert (b2.etf_decode(d, out2, offs2, tag=tag, vers=1) == 0).all()
+        assert np.array_equal(b2.download(), want)
 
 
 @pytest.mark.gpu
-def test_gpu_from_binary_errors_and_atom_forms():
+@pytest.mark.parametrize("knob", [0, 1])
+def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
     outside the dictionary or out of term order; SMALL_ATOM_UTF8_EXT / ATOM_UTF8_EXT
@@ -469,20 +484,34 @@ def test_gpu_from_binary_errors_and_atom_forms():
         (unknown, _lib.DEC_UNKNOWN_TERM), (out_of_order, _lib.DEC_UNKNOWN_TERM),
         (no_tokens, _lib.DEC_UNREPRESENTABLE),
         (oetf.to_binary(T, 1, []), _lib.DEC_OK),
+        # token count larger / smaller than the records present, count cut short
+        (good.replace(bytes([108, 0, 0, 0, 2]), bytes([108, 0, 0, 0, 3]), 1),
+         _lib.DEC_UNKNOWN_TERM),
+        (good.replace(bytes([108, 0, 0, 0, 2]), bytes([108, 0, 0, 0, 1]), 1),
+         _lib.DEC_MALFORMED),
+        (good[:good.index(bytes([108, 0, 0, 0, 2])) + 3], _lib.DEC_MALFORMED),
+        # a duplicated record (same token twice) is out of term order
+        (oetf.to_binary(T, 1, [(1, [(tok[0], False), (tok[0], True)])]),
+         _lib.DEC_UNKNOWN_TERM),
+        # an unknown token after a bad flag: the flag comes first in stream order
+        (oetf.to_binary(T, 1, [(1, [(tok[0], False), (b"z" * 20, True)])])
+         .replace(b"false", b"falsx", 1), _lib.DEC_MALFORMED),
     ]
     pay, offs = _upload_payloads(ctx, [c[0] for c in cases])
     b = ctx.orset_batch(len(cases), E)
-    st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    with _read_kernel(ctx, knob):
+        st = b.etf_decode(d, pay, offs, tag=T, vers=1)
     assert list(st) == [c[1] for c in cases]
     cells = b.download()
     want = dom.encode_orset([s0], E)[0]
     for i in (0, 1, 2):
         assert np.array_equal(cells[i], want)
-    assert not cells[len(cases) - 1].any()
+    assert not cells[14].any()
 
 
 @pytest.mark.gpu
-def test_gpu_from_binary_large_round_trip():
+@pytest.mark.parametrize("knob", [0, 1])
+def test_gpu_from_binary_large_round_trip(knob):
     """4096 replicas x 512 slots x 64 token slots: device to_binary then from_binary
     restores every cell."""
     import numpy as np
@@ -503,7 +532,8 @@ def test_gpu_from_binary_large_round_trip():
     d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
     offs, out, _ = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
     b2 = ctx.orset_batch(R, E)
-    st = b2.etf_decode(d, out, offs, tag=etf.DT_ORSET_TAG, vers=1)
+    with _read_kernel(ctx, knob):
+        st = b2.etf_decode(d, out, offs, tag=etf.DT_ORSET_TAG, vers=1)
     assert (st == 0).all()
     assert np.array_equal(b2.download(), b.download())
 
@@ -512,7 +542,8 @@ def test_gpu_from_binary_large_round_trip():
 def test_gpu_from_binary_fuzz():
     """2000 corrupted payloads (byte flips, truncations, insertions, splices of two
     payloads): every status is a LASPJ_DEC_* code, a payload that decodes OK re-encodes
-    to itself, and nothing faults."""
+    to itself, the batched and the serial decode agree on every status and cell, and
+    nothing faults."""
     import numpy as np
     from lasp_amd import etf
     rng = random.Random(77)
@@ -540,6 +571,12 @@ def test_gpu_from_binary_fuzz():
     bt = ctx.orset_batch(len(blobs), E)
     st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
     assert set(np.unique(st)) <= {0, 1, 2, 3, 4, 5}
+    bs = ctx.orset_batch(len(blobs), E)
+    with _read_kernel(ctx, 1):
+        st_serial = bs.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert np.array_equal(st, st_serial), np.nonzero(st != st_serial)[0][:10]
+    ok0 = st == 0
+    assert np.array_equal(bt.download()[ok0], bs.download()[ok0])
     ok = np.nonzero(st == 0)[0]
     if len(ok):
         again = bt.to_binaries(d, tag=T, vers=1)
