@@ -65,9 +65,12 @@ struct laspj_etf_dict {
     const uint8_t* ehdr_pad = nullptr;
     const uint32_t* ehdr_poff = nullptr;   // E
     uint32_t ehdr_max = 0;                 // longest element header template
-    // per (element, term rank < tok_max): laspj::rec_hash of the record template; null
-    // when two templates of one element hash alike (from_binary then scans serially)
-    const uint64_t* rec_hash = nullptr;
+    // from_binary tables by element rank (term order), see ReadTabs; null when some
+    // element's tokens share every bucket choice (from_binary then scans serially)
+    const void* rd_desc = nullptr;         // E x {slot, header length, 0, token ranks}
+    const uint8_t* rd_hdr = nullptr;       // E x 64 header template bytes
+    const uint16_t* rd_tb = nullptr;       // E x tok_max token buckets (see ReadTabs)
+    const uint8_t* rd_ros = nullptr;       // E x 64: token slot -> token rank (0xFF: none)
 };
 
 namespace laspj {
@@ -106,23 +109,6 @@ DictView view(const laspj_etf_dict* d) {
             d->elem_poff, d->tok_pad,   d->tok_poff,   d->tok_desc,    d->tok_max,
             d->rec_len,   d->rec_stride, d->rec_pad,   d->ehdr_pad,    d->ehdr_poff,
             d->ehdr_max};
-}
-
-// 64-bit hash of a record template held as 12 little-endian words, zero past its length
-// (the host hashes rec_pad, the from_binary kernel the payload's record)
-__host__ __device__ __forceinline__ u64 rec_hash(const uint32_t (&w)[12]) {
-    uint32_t a = 0x9E3779B9u, b = 0x7F4A7C15u;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        a = (a ^ w[i]) * 0xCC9E2D51u;
-        a = (a << 15) | (a >> 17);
-        b = (b + w[i]) * 0x1B873593u;
-        b ^= b >> 13;
-    }
-    a ^= a >> 16;
-    a *= 0x85EBCA6Bu;
-    a ^= a >> 13;
-    return ((u64)a << 32) | b;
 }
 
 __device__ __forceinline__ u64 wave_sum(u64 v) {
@@ -987,14 +973,15 @@ struct Stage {
     const uint8_t* src;    // the payload buffer
     u64 total;             // bytes in the payload buffer
     u64 lo, hi;            // staged [lo, hi)
+    uint32_t win = kDWin;  // window bytes
 };
 
-// make [p, p + n) resident (n <= kDWin - 16; wave-uniform); false past `lim`
+// make [p, p + n) resident (n <= s.win - 16; wave-uniform); false past `lim`
 __device__ bool stage_span(Stage& s, u64 p, uint32_t n, u64 lim) {
     if (p + n > lim) return false;
     if (p >= s.lo && p + n <= s.hi) return true;
     const u64 lo = p & ~15ull;
-    const u64 hi = min(s.total, lo + kDWin);
+    const u64 hi = min(s.total, lo + s.win);
     const uint32_t lane = threadIdx.x & 63u;
     wave_sync();
     const u64 nfull = (hi - lo) >> 4;
@@ -1188,17 +1175,40 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_serial(const uint8_t*
     }
 }
 
-// Batched record decode (the default when every element's record templates hash apart,
-// see rec_hash below).  Element headers as in the serial scan, with the next rank in
-// term order tried first one byte per lane.  Records go in batches of up to 64: the wave
-// walks the record chain reading only each flag's header bytes (three LDS reads per
-// record, one address for every lane), then lane j takes record j: its token template
-// from LDS as aligned dwords, a 64-bit hash matched against the element's per-rank
-// template hashes (one ballot per record), an exact compare against the matched
-// template, the term-order check and the flag bytes.  The first failing record in stream
-// order gives the status the serial scan gives: templates are distinct within an
-// element, so "the first rank after the previous one whose template matches" is "the
-// one rank whose template matches, if it comes after the previous one".
+// Batched record decode (the default when the dictionary admits it, see ReadTabs).
+// Elements: the next rank in term order is predicted, and what the wave needs about it
+// (descriptor, the first 64 bytes of its header template, its token buckets and slot ->
+// rank map, all stored by rank) is loaded while the element before it decodes; one LDS
+// byte per lane then checks the header and carries the token count.  Any other element
+// is found by the serial scan over 64 candidates per step.
+// Records go in batches of up to 64 through a 4 KiB window.  The record chain (where
+// each record starts: a record is 104 2 <token image> <flag atom> and only the flag's
+// length varies) is walked ten records per step: lane (j, f) reads the flag header that
+// record j would have if f of the records before it said `false` (one LDS round trip for
+// all 55 cases), and the scalar walk reads the ten cases it needs with readlane.  A
+// record whose flag uses another atom encoding than the batch's first takes one general
+// step.  Then lane j takes record j on its own: a 32-bit word of its token image (word
+// and shift chosen per element by the host so that every token of the element lands in
+// its own bucket of a 1024-entry LDS table) gives the token rank, the exact compare
+// against that rank's template decides, term order is the previous lane's rank, and the
+// flag letters are checked.  Present and `true` ranks go to a 64-byte LDS presence table
+// that the element's slot lanes read back with one ballot each.  The first failing
+// record in stream order gives the status the serial scan gives (templates are distinct
+// within an element, so "the first rank after the previous one whose template matches"
+// is "the one rank whose template matches, if it comes after the previous one").
+
+constexpr uint32_t kBWin = 4096;         // batched decode window
+constexpr uint32_t kBuckets = 1024;      // token buckets per element
+
+struct ReadTabs {
+    const uint4* desc;      // by rank: slot, header length, word | shift << 8, token ranks
+    const uint8_t* hdr;     // by rank: 64 bytes of 104 2 <elem image> 108, zero padded
+    const uint16_t* tb;     // by rank r, token rank k: bucket at r * tok_max + k
+    const uint8_t* ros;     // by rank r, token slot s: its token rank at 64 r + s (0xFF: none)
+};
+
+// bytes of the ReadTabs tables: desc, hdr, tb, ros
+inline uint64_t rd_bytes(uint64_t E, uint64_t RK) { return E * (16 + 64 + 2 * RK + 64) + 64; }
 
 // words of staged bytes [o, o + L) (L <= 48), zero past L; reads 52 bytes from o & ~3
 __device__ __forceinline__ void rec_words(const uint8_t* buf, uint32_t o, uint32_t L,
@@ -1215,208 +1225,369 @@ __device__ __forceinline__ void rec_words(const uint8_t* buf, uint32_t o, uint32
     }
 }
 
-__device__ __forceinline__ u64 wave_or(u64 v) {
+// the 32-bit word of staged bytes at o (any alignment)
+__device__ __forceinline__ uint32_t word_at(const uint8_t* buf, uint32_t o) {
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf + (o & ~3u));
+    return __builtin_amdgcn_alignbyte(b32[1], b32[0], o & 3u);
+}
+
+// what the wave holds about one element rank (lane-distributed where per lane)
+struct RankPre {
+    uint32_t e, hl, key, cnt;   // slot, header length with the 108, word | shift << 8, tokens
+    uint32_t hb;                // lane i: header template byte i
+    uint32_t tb;                // lane k < cnt: bucket of token rank k
+    uint32_t ros;               // lane s: token rank of slot s (0xFF: none)
+};
+
+__device__ __forceinline__ RankPre load_rank(const ReadTabs& t, uint32_t RK, int64_t r,
+                                             uint32_t E, uint32_t lane) {
+    RankPre x{0, 0, 0, 0, 0, 0, 0xFF};
+    if (r >= (int64_t)E) return x;
+    const uint4 d = t.desc[r];
+    x.e = (uint32_t)__builtin_amdgcn_readfirstlane(d.x);
+    x.hl = (uint32_t)__builtin_amdgcn_readfirstlane(d.y);
+    x.key = (uint32_t)__builtin_amdgcn_readfirstlane(d.z);
+    x.cnt = (uint32_t)__builtin_amdgcn_readfirstlane(d.w);
+    x.hb = t.hdr[64ull * r + lane];
+    x.tb = lane < RK ? t.tb[(u64)r * RK + lane] : 0u;
+    x.ros = t.ros[64ull * r + lane];
+    return x;
+}
+
+// a 64-bit wave-uniform value kept in scalar registers
+__device__ __forceinline__ u64 ufl(u64 v) {
+    // readfirstlane returns int: through uint32_t, or the low word would sign-extend
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t i) {
+    return (uint32_t)__builtin_amdgcn_readlane(v, i);
+}
+
+// flag header at o (atom tag, then length): 1 | false << 1 when it is the encoding with
+// atom header length h (3: ATOM_EXT / ATOM_UTF8_EXT, 2: SMALL_ATOM_UTF8_EXT) and a
+// length of 4 or 5; 0 otherwise
+__device__ __forceinline__ uint32_t flag_code(uint32_t v, uint32_t h) {
+    const uint32_t t0 = v & 0xFFu, b1 = (v >> 8) & 0xFFu, b2 = (v >> 16) & 0xFFu;
+    const uint32_t len = h == 3 ? b2 : b1;
+    const bool ok = (h == 3 ? (t0 == 100 || t0 == 118) && b1 == 0 : t0 == 119) &&
+                    (len == 4 || len == 5);
+    return ok ? 1u | ((len == 5) << 1) : 0u;
+}
+
+struct ReadLds {
+    uint8_t win[kBWin + 64];     // 64 bytes of slack: rec_words reads 52 past a start
+    uint8_t tab[kBuckets];       // bucket -> token rank of the current element
+    uint8_t pres[64];            // token rank -> 1 present | 2 true
+};
+
+// The batched decode's view of one payload: a 4 KiB LDS window over it, with every
+// position inside the window a 32-bit offset (scalar arithmetic stays 32-bit)
+struct PWin {
+    uint8_t* buf;          // wave-private LDS window
+    const uint8_t* src;    // the payload buffer
+    u64 total;             // bytes in the payload buffer
+    u64 aend;              // this payload's end (absolute)
+    u64 lo;                // absolute position of buf[0]
+    uint32_t hi;           // staged bytes [0, hi)
+    uint32_t end;          // payload end relative to lo (clamped to 2^31)
+};
+
+// restage the window at the cursor; returns the cursor's offset in the new window
+__device__ uint32_t refill(PWin& w, uint32_t pc) {
+    const u64 a = w.lo + pc;
+    const u64 lo = a & ~15ull;
+    const u64 hi = min(w.total, lo + kBWin);
+    const uint32_t lane = threadIdx.x & 63u;
+    wave_sync();
+    const uint32_t nfull = (uint32_t)((hi - lo) >> 4);
+    for (uint32_t v = lane; v < nfull; v += 64)
+        reinterpret_cast<u32x4*>(w.buf)[v] = *reinterpret_cast<const u32x4*>(w.src + lo + 16ull * v);
+    for (u64 b = lo + 16ull * nfull + lane; b < hi; b += 64) w.buf[b - lo] = w.src[b];
+    wave_sync();
+    w.lo = lo;
+    w.hi = (uint32_t)(hi - lo);
+    w.end = (uint32_t)min(w.aend - lo, (u64)0x7FFFFFFF);
+    return (uint32_t)(a - lo);
+}
+
+// [pc, pc + n) resident (the caller checked pc + n <= w.end; n <= kBWin - 16)
+__device__ __forceinline__ uint32_t need(PWin& w, uint32_t pc, uint32_t n) {
+    return pc + n <= w.hi ? pc : refill(w, pc);
+}
+
+// a window byte every lane reads at the same offset, as a wave-uniform value
+__device__ __forceinline__ uint32_t ub(const PWin& w, uint32_t o) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(w.buf[o]);
+}
+
+// bytes at q equal the 16-byte-aligned, zero-padded template (L <= 48)
+__device__ __forceinline__ bool eq48(const uint8_t* q, const uint8_t* t16, uint32_t L) {
+    const u32x4* t = reinterpret_cast<const u32x4*>(t16);
+    const u32x4 z = {0, 0, 0, 0};
+    const u32x4 a = t[0], b = L > 16 ? t[1] : z, c = L > 32 ? t[2] : z;
+    const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    bool eq = true;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
-    return v;
+    for (uint32_t i = 0; i < 48; ++i)
+        if (i < L) eq &= q[i] == ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+    return eq;
 }
 
 __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
-                                                           const u64* rhash, int tag, int vers,
+                                                           ReadTabs tabs, int tag, int vers,
                                                            u64x2* cells, int32_t* status) {
-    // 64 bytes of slack per window: rec_words reads up to 52 bytes from a record's start
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin + 64];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    // the wave index as a scalar: everything per replica then stays wave-uniform
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    const uint32_t hmax = min(d.ehdr_max + 4u, kDWin - 16u);
+    const uint32_t hmax = min(d.ehdr_max + 4u, kBWin - 16u);
+    // lane (lj, lf), lj < 10, lf <= lj: case index lj (lj + 1) / 2 + lf of a chain step
+    uint32_t lj = 0;
+    while ((lj + 1) * (lj + 2) / 2 <= lane) ++lj;
+    const uint32_t lf = lane - lj * (lj + 1) / 2;
+    const bool lcase = lane < 55;
+    ReadLds& L = lds[wave];
     for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
-        Stage s{stage[wave], payload, total, 0, 0};
-        const u64 base = offs[rep], end = offs[rep + 1];
-        u64 p = base;
+        const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
+        PWin w{L.win, payload, total, aend, base, 0,
+              (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
+        uint32_t pc = 0;
         int32_t st = LASPJ_DEC_OK;
         u64x2* c = cells + rep * E;
         do {
             if (tag >= 0) {
-                if (!stage_span(s, p, 2, end) || at(s, p) != (uint32_t)(tag & 0xFF)) {
-                    st = LASPJ_DEC_INVALID_BINARY;
-                    break;
-                }
-                if (at(s, p + 1) != (uint32_t)(vers & 0xFF)) {
+                if (pc + 2 > w.end) { st = LASPJ_DEC_INVALID_BINARY; break; }
+                pc = need(w, pc, 2);
+                if (ub(w, pc) != (uint32_t)(tag & 0xFF)) { st = LASPJ_DEC_INVALID_BINARY; break; }
+                if (ub(w, pc + 1) != (uint32_t)(vers & 0xFF)) {
                     st = LASPJ_DEC_UNSUPPORTED_VERSION;
                     break;
                 }
-                p += 2;
+                pc += 2;
             }
-            if (!stage_span(s, p, 2, end) || at(s, p) != 131) {
-                st = LASPJ_DEC_MALFORMED;                 // binary_to_term: badarg
-                break;
-            }
+            if (pc + 2 > w.end) { st = LASPJ_DEC_MALFORMED; break; }   // binary_to_term: badarg
+            pc = need(w, pc, 2);
+            if (ub(w, pc) != 131) { st = LASPJ_DEC_MALFORMED; break; }
             uint32_t n = 0;
-            if (at(s, p + 1) == 106) {
-                p += 2;
-            } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
-                n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
-                p += 6;
+            if (ub(w, pc + 1) == 106) {
+                pc += 2;
+            } else if (ub(w, pc + 1) == 108 && pc + 6 <= w.end) {
+                pc = need(w, pc, 6);
+                n = (ub(w, pc + 2) << 24) | (ub(w, pc + 3) << 16) | (ub(w, pc + 4) << 8) |
+                    ub(w, pc + 5);
+                pc += 6;
             } else {
                 st = LASPJ_DEC_MALFORMED;
                 break;
             }
             int64_t prev = -1;                    // term rank of the previous element
+            RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
             for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
-                // 104 2 <elem image> 108 of the next elements in term order
-                const uint32_t span = (uint32_t)min((u64)hmax, end - p);
-                stage_span(s, p, span, end);
+                // 104 2 <elem image> 108 <count:32> of the next element in term order
+                const uint32_t span = min(hmax, w.end - pc);
+                pc = need(w, pc, span);
+                const uint32_t byte = pc + lane < min(w.hi, w.end) ? w.buf[pc + lane] : 0x100u;
                 int64_t found = -1;
-                uint32_t e = 0, hl = 0;
-                if (prev + 1 < (int64_t)E) {      // the next rank, one byte per lane
-                    const uint32_t ec = d.elem_order[prev + 1];
-                    const uint32_t hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
-                    if (hlc > 3u && hlc <= span && hlc - 1u <= 64u) {
-                        const bool ok = lane >= hlc - 1u ||
-                                        at(s, p + lane) == d.ehdr_pad[d.ehdr_poff[ec] + lane];
-                        if (!__ballot(!ok)) {
-                            found = prev + 1;
-                            e = ec;
-                            hl = hlc;
-                        }
-                    }
+                RankPre cur = nx;
+                if (prev + 1 < (int64_t)E && cur.hl > 3u && cur.hl <= span && cur.hl <= 64u) {
+                    const bool ok = lane >= cur.hl - 1u || byte == cur.hb;
+                    if (!__ballot(!ok)) found = prev + 1;
                 }
-                for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
-                    const int64_t r = c0 + lane;
-                    bool hit = false;
-                    uint32_t ec = 0, hlc = 0;
-                    if (r < (int64_t)E) {
-                        ec = d.elem_order[r];
-                        hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
-                        // 104 2 <elem image> (the template's closing 108 is checked below)
-                        if (hlc > 3u && hlc <= span) {
-                            const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
-                            hit = hlc - 1u <= 48 ? same48(s, p, t, hlc - 1u)
-                                                 : same_long(s, p, t, hlc - 1u);
+                if (found < 0) {
+                    for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
+                        const int64_t r = c0 + lane;
+                        bool hit = false;
+                        if (r < (int64_t)E) {
+                            const uint32_t ec = d.elem_order[r];
+                            const uint32_t hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                            // 104 2 <elem image> (the closing 108 is checked below)
+                            if (hlc > 3u && hlc <= span) {
+                                const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
+                                const uint8_t* q = w.buf + pc;
+                                if (hlc - 1u <= 48) {
+                                    hit = eq48(q, t, hlc - 1u);
+                                } else {
+                                    hit = true;
+                                    for (uint32_t i = 0; i < hlc - 1u && hit; ++i) hit = q[i] == t[i];
+                                }
+                            }
                         }
+                        const u64 m = __ballot(hit);
+                        if (m) found = c0 + __ffsll((long long)m) - 1;
                     }
-                    const u64 m = __ballot(hit);
-                    if (m) {
-                        const uint32_t w = (uint32_t)__ffsll((long long)m) - 1u;
-                        found = c0 + w;
-                        e = __shfl(ec, w, 64);
-                        hl = __shfl(hlc, w, 64);
-                    }
+                    if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                    cur = load_rank(tabs, RK, found, E, lane);
                 }
-                if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
                 prev = found;
-                p += hl;
-                if (at(s, p - 1) != 108) {                 // [] tokens: no columnar form
-                    st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
+                nx = load_rank(tabs, RK, found + 1, E, lane);
+                const uint32_t e = cur.e, hl = cur.hl;
+                pc += hl;
+                const uint32_t close = hl <= 64u ? rdlane(byte, hl - 1u) : ub(w, pc - 1);
+                if (close != 108) {                        // [] tokens: no columnar form
+                    st = close == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
                     break;
                 }
-                if (!stage_span(s, p, 4, end)) { st = LASPJ_DEC_MALFORMED; break; }  // truncated count
-                const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
-                                       at(s, p + 3);
-                p += 4;
+                if (pc + 4 > w.end) { st = LASPJ_DEC_MALFORMED; break; }    // truncated count
+                uint32_t m_tok;
+                if (hl + 4u <= 64u) {
+                    m_tok = (rdlane(byte, hl) << 24) | (rdlane(byte, hl + 1u) << 16) |
+                            (rdlane(byte, hl + 2u) << 8) | rdlane(byte, hl + 3u);
+                } else {
+                    pc = need(w, pc, 4);
+                    m_tok = (ub(w, pc) << 24) | (ub(w, pc + 1) << 16) | (ub(w, pc + 2) << 8) |
+                            ub(w, pc + 3);
+                }
+                pc += 4;
                 if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
-                // lane k: hash of the template of token rank k (ranks < cnt exist)
-                const uint32_t cnt = (uint32_t)__popcll(d.tok_mask[e]);
-                const u64 th = lane < cnt ? rhash[(u64)e * RK + lane] : 0ull;
-                u64 pb = 0, rb = 0;
+                // the element's bucket table and an empty presence table
+                const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = cur.key >> 8;
+                wave_sync();
+                if (lane < cur.cnt) L.tab[cur.tb] = (uint8_t)lane;
+                L.pres[lane] = 0;
+                wave_sync();
                 int32_t tprev = -1;
                 for (uint32_t done = 0; done < m_tok;) {
-                    // the chain: record starts from the flags' header bytes
-                    uint32_t nb = 0;
+                    // room for the batch in the window
+                    {
+                        const uint32_t want = min((m_tok - done) * (RL + 8u) + 8u, w.end - pc);
+                        if (pc + want > w.hi && w.hi < w.end) pc = refill(w, pc);
+                    }
+                    // the chain, in window offsets: a record at x is complete before the
+                    // payload end when x <= tlim, inside the window when x <= wlim
+                    const int32_t tlim = (int32_t)w.end - (int32_t)RL - 6;
+                    const int32_t wlim = w.hi >= w.end ? 0x7FFFFFFF : (int32_t)w.hi - (int32_t)RL - 8;
+                    const int32_t lim = min(tlim, wlim);
+                    const uint32_t t0 = pc + RL < w.hi ? ub(w, pc + RL) : 0u;
+                    const uint32_t h = t0 == 119 ? 2u : 3u;     // the batch's atom header
+                    const uint32_t L0 = RL + h + 4u;              // a `true` record
+                    uint32_t nb = 0, x = pc, myx = 0;
                     bool trunc = false;
-                    u64 x = p, myx = 0;
                     while (nb < 64 && done + nb < m_tok) {
-                        if (x + RL + 6 > end) { trunc = true; break; }
-                        if (x + RL + 8 > s.hi && s.hi < end) {   // record past the window
-                            if (nb) break;
-                            stage_span(s, x, (uint32_t)min((u64)RL + 8, end - x), end);
+                        const uint32_t J = min(10u, min(64u - nb, m_tok - done - nb));
+                        // lane (lj, lf): the flag header of record lj after lf falses
+                        uint32_t code = 0;
+                        if (lcase && lj < J) {
+                            const uint32_t q = x + lj * L0 + lf + RL;
+                            if (q + 3 <= w.hi) {
+                                code = flag_code(word_at(w.buf, q), h);
+                                if (q + h + 4 + (code >> 1) > w.end) code = 0;
+                            }
                         }
+                        uint32_t f = 0, jr = 0, idx = 0;
+                        u64 fz = 0;
+                        bool stop = false;
+                        for (; jr < J; ++jr) {
+                            const int32_t xj = (int32_t)(x + jr * L0 + f);
+                            if (xj > lim) { trunc = xj > tlim; stop = true; break; }
+                            const uint32_t cj = rdlane(code, idx + f);
+                            if (!(cj & 1u)) break;
+                            fz |= (u64)(cj >> 1) << jr;
+                            f += cj >> 1;
+                            idx += jr + 1;
+                        }
+                        // lanes nb .. nb + jr - 1: starts of the walked records
+                        if (lane >= nb && lane < nb + jr) {
+                            const uint32_t i = lane - nb;
+                            myx = x + i * L0 + __popcll(fz & ((1ull << i) - 1ull));
+                        }
+                        x += jr * L0 + f;
+                        nb += jr;
+                        if (stop || nb >= 64 || done + nb >= m_tok) break;
+                        if (jr == J) continue;
+                        // a record the walk did not take: one general step
                         if (lane == nb) myx = x;
-                        const uint32_t t0 = at(s, x + RL), b1 = at(s, x + RL + 1),
-                                       b2 = at(s, x + RL + 2);
-                        uint32_t h = 0, len = 0;
-                        if ((t0 == 100 || t0 == 118) && b1 == 0) { h = 3; len = b2; }
-                        else if (t0 == 119) { h = 2; len = b1; }
+                        const uint32_t a0 = ub(w, x + RL), a1 = ub(w, x + RL + 1),
+                                       a2 = ub(w, x + RL + 2);
+                        uint32_t gh = 0, len = 0;
+                        if ((a0 == 100 || a0 == 118) && a1 == 0) { gh = 3; len = a2; }
+                        else if (a0 == 119) { gh = 2; len = a1; }
                         ++nb;
                         // a bad flag header ends the chain; lane nb - 1 reports it
-                        if ((len != 4 && len != 5) || x + RL + h + len > end) break;
-                        x += RL + h + len;
+                        if ((len != 4 && len != 5) || x + RL + gh + len > w.end) break;
+                        x += RL + gh + len;
                     }
+                    if (nb == 0 && !trunc) { st = LASPJ_DEC_MALFORMED; break; }   // no progress
                     // lane j < nb: record j
                     const bool mine = lane < nb;
-                    uint32_t w[12];
-                    u64 hh = 0;
-                    if (mine) {
-                        rec_words(s.buf, (uint32_t)(myx - s.lo), RL, w);
-                        hh = rec_hash(w);
-                    }
-                    int32_t rank = -1;
-                    for (uint32_t j = 0; j < nb; ++j) {
-                        const u64 hj = __shfl(hh, j, 64);
-                        const u64 m = __ballot(lane < cnt && th == hj);
-                        if (lane == j && m) rank = (int32_t)__ffsll((long long)m) - 1;
-                    }
                     int32_t lst = LASPJ_DEC_OK;
-                    bool flag = false;
-                    const int32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+                    uint32_t rank = 0xFFu, fl = 0;
                     if (mine) {
-                        if (rank >= 0) {                    // exact compare
-                            uint32_t t[12];
-                            load48(t, d.rec_pad + ((u64)e * RK + (uint32_t)rank) * RS, RL);
-                            bool eq = true;
+                        rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
+                        bool eq = rank < cur.cnt;
+                        if (eq) {                           // exact compare
+                            uint32_t rw[12], t[12];
+                            rec_words(w.buf, myx, RL, rw);
+                            load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
 #pragma unroll
-                            for (int i = 0; i < 12; ++i) eq &= t[i] == w[i];
-                            if (!eq) rank = -1;
+                            for (int i = 0; i < 12; ++i) eq &= t[i] == rw[i];
                         }
-                        if (rank < 0 || rank <= (lane ? pr : tprev)) {
-                            lst = LASPJ_DEC_UNKNOWN_TERM;
-                        } else {
-                            // ATOM_EXT / ATOM_UTF8_EXT (2-byte length) or SMALL_ATOM_UTF8_EXT
-                            const u64 q = myx + RL;
-                            const uint32_t t0 = at(s, q), b1 = at(s, q + 1);
-                            uint32_t h = 0, len = 0;
-                            if ((t0 == 100 || t0 == 118) && b1 == 0) { h = 3; len = at(s, q + 2); }
-                            else if (t0 == 119) { h = 2; len = b1; }
-                            const u64 f = q + h;
-                            if (h && len == 4 && f + 4 <= end && at(s, f) == 't' &&
-                                at(s, f + 1) == 'r' && at(s, f + 2) == 'u' && at(s, f + 3) == 'e')
-                                flag = true;
-                            else if (h && len == 5 && f + 5 <= end && at(s, f) == 'f' &&
-                                     at(s, f + 1) == 'a' && at(s, f + 2) == 'l' &&
-                                     at(s, f + 3) == 's' && at(s, f + 4) == 'e')
-                                flag = false;
-                            else
-                                lst = LASPJ_DEC_MALFORMED;
+                        // ATOM_EXT / ATOM_UTF8_EXT (2-byte length), SMALL_ATOM_UTF8_EXT
+                        // (1-byte length), then "true" / "false"
+                        const uint32_t fo = myx + RL;
+                        const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
+                        const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
+                        const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
+                        const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
+                        uint32_t gh = 0, len = 0, word = 0, c4 = 0;
+                        if ((a0 == 100 || a0 == 118) && a1 == 0) {
+                            gh = 3;
+                            len = (v0 >> 16) & 0xFFu;
+                            word = __builtin_amdgcn_alignbyte(v1, v0, 3);
+                            c4 = v1 >> 24;
+                        } else if (a0 == 119) {
+                            gh = 2;
+                            len = a1;
+                            word = __builtin_amdgcn_alignbyte(v1, v0, 2);
+                            c4 = (v1 >> 16) & 0xFFu;
                         }
+                        const uint32_t fend = fo + gh + len;      // one past the flag
+                        const bool tr = gh && len == 4 && fend <= w.end && word == 0x65757274u;
+                        const bool fa = gh && len == 5 && fend <= w.end &&
+                                        word == 0x736C6166u && c4 == 'e';
+                        fl = tr;
+                        // term order: after the previous record's rank
+                        const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+                        const int32_t before = lane ? (int32_t)pr : tprev;
+                        lst = !eq || (int32_t)rank <= before ? LASPJ_DEC_UNKNOWN_TERM
+                              : !(tr || fa)                  ? LASPJ_DEC_MALFORMED
+                                                             : LASPJ_DEC_OK;
                     }
                     const u64 bad = __ballot(lst != LASPJ_DEC_OK);
                     if (bad) {
-                        st = __shfl(lst, (uint32_t)__ffsll((long long)bad) - 1u, 64);
+                        st = (int32_t)rdlane((uint32_t)lst, (uint32_t)__ffsll((long long)bad) - 1u);
                         break;
                     }
                     if (trunc) { st = LASPJ_DEC_MALFORMED; break; }
-                    u64 pbit = 0;
-                    if (mine) pbit = 1ull << d.tok_order[64ull * e + (uint32_t)rank];
-                    pb |= wave_or(pbit);
-                    rb |= wave_or(flag ? pbit : 0ull);
-                    tprev = __shfl(rank, nb - 1u, 64);
+                    if (mine) L.pres[rank] = (uint8_t)(1u | (fl << 1));
+                    tprev = (int32_t)rdlane(rank, nb - 1u);
                     done += nb;
-                    p = x;
+                    pc = x;
                 }
                 if (st != LASPJ_DEC_OK) break;
-                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
-                p += 1;
+                if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
+                pc = need(w, pc, 1);
+                if (ub(w, pc) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                pc += 1;
+                // presence by rank -> slot bits: lane s reads its slot's rank
+                wave_sync();
+                const uint32_t v = cur.ros < 64u ? L.pres[cur.ros] : 0u;
+                const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
                 if (lane == 0) c[e] = u64x2{pb, rb};
             }
             if (st != LASPJ_DEC_OK) break;
             if (n) {
-                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
-                p += 1;
+                if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
+                pc = need(w, pc, 1);
+                if (ub(w, pc) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                pc += 1;
             }
-            if (p != end) st = LASPJ_DEC_MALFORMED;      // trailing bytes
+            if (w.lo + pc != aend) st = LASPJ_DEC_MALFORMED;      // trailing bytes
         } while (false);
         if (lane == 0) status[rep] = st;
     }
@@ -1589,11 +1760,13 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    if (d->rec_hash && ctx->tune_etf_read == 0)
+    if (d->rd_desc && ctx->tune_etf_read == 0)
         hipLaunchKernelGGL(k_orset_etf_read, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
                            static_cast<const u64*>(offsets->dev), R, b->elements, view(d),
-                           reinterpret_cast<const u64*>(d->rec_hash), tag, vers,
+                           ReadTabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb,
+                                    d->rd_ros},
+                           tag, vers,
                            reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev));
     else
         hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,
@@ -1696,7 +1869,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     uint64_t ehdr_max = 0;
     std::vector<uint8_t> rpad, hpad;
     std::vector<uint32_t> hpoff;
-    std::vector<uint64_t> rhash;
+    std::vector<uint8_t> rd;
     bool hashed = rec_len != 0;
     if (rec_len) {
         rpad.assign((uint64_t)E * tok_max * rec_stride + 48, 0);
@@ -1727,21 +1900,52 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
             std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], h + 2);
             h[2 + elem_off[e + 1] - elem_off[e]] = 108;
         }
-        // template hashes; any two alike within one element turn the batched decode off
-        rhash.assign((uint64_t)E * tok_max, 0);
-        std::vector<uint64_t> hs;
-        for (uint64_t e = 0; e < E && hashed; ++e) {
-            hs.clear();
-            for (uint32_t j = 0; j < tok_max && tok_order[64ull * e + j] < 64; ++j) {
-                const uint8_t* r = rpad.data() + (e * tok_max + j) * rec_stride;
-                uint32_t w[12] = {};
-                std::memcpy(w, r, rec_len);     // little-endian words, zero past rec_len
-                rhash[e * tok_max + j] = laspj::rec_hash(w);
-                hs.push_back(rhash[e * tok_max + j]);
+        // from_binary tables by element rank: per element a template word and shift
+        // that put its tokens in distinct buckets (none found: serial decode)
+        rd.assign(laspj::rd_bytes(E, tok_max), 0);
+        uint32_t* desc = reinterpret_cast<uint32_t*>(rd.data());
+        uint8_t* hdr = rd.data() + 16ull * E;
+        uint16_t* tbk = reinterpret_cast<uint16_t*>(hdr + 64ull * E);
+        uint8_t* ros = reinterpret_cast<uint8_t*>(tbk + (uint64_t)E * tok_max);
+        std::memset(ros, 0xFF, 64ull * E);
+        const uint32_t nwords = rec_len / 4;     // whole words of the template
+        std::vector<uint32_t> keys;
+        for (uint64_t r = 0; r < E && hashed; ++r) {
+            const uint32_t e = elem_order[r];
+            const uint32_t hl = elem_off[e + 1] - elem_off[e] + 3u;
+            uint32_t cnt = 0;
+            while (cnt < tok_max && tok_order[64ull * e + cnt] < 64) ++cnt;
+            desc[4 * r] = e;
+            desc[4 * r + 1] = hl;
+            desc[4 * r + 3] = cnt;
+            std::copy(hpad.data() + hpoff[e], hpad.data() + hpoff[e] + std::min(hl, 64u),
+                      hdr + 64 * r);
+            for (uint32_t j = 0; j < cnt; ++j) ros[64 * r + tok_order[64ull * e + j]] = (uint8_t)j;
+            if (cnt == 0) continue;
+            bool placed = false;
+            for (uint32_t wi = nwords; wi-- > 0 && !placed;) {
+                keys.resize(cnt);
+                for (uint32_t j = 0; j < cnt; ++j)
+                    std::memcpy(&keys[j], rpad.data() + ((uint64_t)e * tok_max + j) * rec_stride +
+                                               4 * wi, 4);
+                for (uint32_t sh = 0; sh + 10 <= 32 && !placed; ++sh) {
+                    uint64_t seen[laspj::kBuckets / 64] = {};
+                    bool ok = true;
+                    for (uint32_t j = 0; j < cnt && ok; ++j) {
+                        const uint32_t bk = (keys[j] >> sh) & (laspj::kBuckets - 1u);
+                        ok = !((seen[bk / 64] >> (bk % 64)) & 1ull);
+                        seen[bk / 64] |= 1ull << (bk % 64);
+                    }
+                    if (!ok) continue;
+                    placed = true;
+                    desc[4 * r + 2] = wi | (sh << 8);
+                    for (uint32_t j = 0; j < cnt; ++j)
+                        tbk[r * tok_max + j] = (uint16_t)((keys[j] >> sh) & (laspj::kBuckets - 1u));
+                }
             }
-            std::sort(hs.begin(), hs.end());
-            hashed = std::adjacent_find(hs.begin(), hs.end()) == hs.end();
+            hashed = placed;
         }
+        if (!hashed) rd.clear();
     }
     for (uint64_t t = 0; t < tpoff.size(); ++t)
         std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
@@ -1754,8 +1958,8 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
                    o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
-                   o_rhash = o_hpoff + al(4ull * hpoff.size() + 4),
-                   bytes = o_rhash + al(8ull * rhash.size() + 8);
+                   o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
+                   bytes = o_rd + al(rd.size() + 8);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1786,7 +1990,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess && rec_len) e = up(o_rpad, rpad.data(), rpad.size());
     if (e == hipSuccess && rec_len) e = up(o_hpad, hpad.data(), hpad.size());
     if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
-    if (e == hipSuccess && hashed) e = up(o_rhash, rhash.data(), 8ull * rhash.size());
+    if (e == hipSuccess && hashed) e = up(o_rd, rd.data(), rd.size());
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -1803,7 +2007,13 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->rec_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_rpad) : nullptr;
     d->ehdr_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_hpad) : nullptr;
     d->ehdr_poff = rec_len ? reinterpret_cast<const uint32_t*>(base + o_hpoff) : nullptr;
-    d->rec_hash = hashed ? reinterpret_cast<const uint64_t*>(base + o_rhash) : nullptr;
+    if (hashed) {
+        const uint8_t* t = reinterpret_cast<const uint8_t*>(base + o_rd);
+        d->rd_desc = t;
+        d->rd_hdr = t + 16ull * E;
+        d->rd_tb = reinterpret_cast<const uint16_t*>(t + 16ull * E + 64ull * E);
+        d->rd_ros = reinterpret_cast<const uint8_t*>(d->rd_tb + (uint64_t)E * tok_max);
+    }
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);
