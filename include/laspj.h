@@ -135,7 +135,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         (1024), 2048, 4096                              */
 #define LASPJ_TUNE_ETF_READ      8   /* OR-Set from_binary: 0 = batched records when the
                                         dictionary's record templates hash apart within
-                                        every element, 1 = serial record scan            */
+                                        every element, plus element batches when elements
+                                        hold <= 8 token slots, 1 = serial record scan,
+                                        2 = batched records without element batches      */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -1336,6 +1336,152 @@ __device__ __forceinline__ bool eq48(const uint8_t* q, const uint8_t* t16, uint3
     return eq;
 }
 
+// Element batches, for dictionaries with few token slots per element (tok_max <= 8,
+// e.g. the ad counter's 3-replica tokens): one element at a time leaves 60 of 64 lanes
+// idle, so the wave walks up to 64 whole elements before checking any record.  Lane i
+// holds the 64-byte header template and descriptor of rank prev + 1 + i; per element the
+// scalar walk compares the bytes at the cursor with every held header at once (ballot:
+// the element's rank, absent elements need no scan), reads its token count and each
+// record's flag length, and checks the closing 106.  Then lane j takes record j of the
+// batch: bucket -> token rank among its element's <= 8 buckets, exact template compare,
+// term order against the previous record of the same element, flag letters; token bits
+// are ORed into per-element LDS cells.  Only elements before the first failing record
+// (or the first walk step that is not a well-formed element) are committed: the caller's
+// element-at-a-time path decodes from there and gives the status.  What a batch commits
+// is what that path would accept, with the same cells (element images are
+// self-delimiting and distinct, so the header match is the scan's first match).
+constexpr uint32_t kSmallTok = 8;
+
+__device__ __forceinline__ uint32_t ufl32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t left,
+                               const ReadTabs& t, const DictView& d, uint32_t E, uint32_t RL,
+                               uint32_t RS, ReadLds& L, u64x2* c, uint32_t lane) {
+    const uint32_t RK = d.tok_max;
+    if (w.hi < w.end && pc + kBWin / 2 > w.hi) pc = refill(w, pc);
+    // lane i: rank prev + 1 + i (descriptor, header template words)
+    const int64_t cr = prev + 1 + (int64_t)lane;
+    uint32_t ce = 0, chl = 0, ckey = 0, ccnt = 0, ch[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ch[i] = 0;
+    if (cr < (int64_t)E) {
+        const uint4 ds = t.desc[cr];
+        ce = ds.x; chl = ds.y; ckey = ds.z; ccnt = ds.w;
+        const u32x4* h = reinterpret_cast<const u32x4*>(t.hdr + 64ull * (u64)cr);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = h[i];
+            ch[4 * i] = v.x; ch[4 * i + 1] = v.y; ch[4 * i + 2] = v.z; ch[4 * i + 3] = v.w;
+        }
+    }
+    const bool cval = chl > 3u && chl <= 64u;
+    const uint32_t lim = min(w.hi, w.end);
+    // the walk: element lanes (start, candidate lane), record lanes (start, element,
+    // atom header length, atom length)
+    uint32_t x = pc, ne = 0, nr = 0, ex = 0, ec = 0, ry = 0, rel = 0, rh = 0, rlen = 0;
+    int32_t fmin = -1;
+    while (ne < 64u && ne < left && x < lim) {
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(w.buf + (x & ~3u));
+        const uint32_t sh = x & 3u;
+        bool hit = cval && (int32_t)lane > fmin && x + chl <= lim;
+        uint32_t q0 = b32[0];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t q1 = b32[i + 1];
+            const uint32_t v = __builtin_amdgcn_alignbyte(q1, q0, sh);
+            q0 = q1;
+            const int rem = (int)chl - 4 * i;
+            const uint32_t msk = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+            hit &= (v & msk) == ch[i];
+        }
+        // read beside the compare, as if this lane's rank matched: the token count and
+        // the first record's flag header (clamped inside the window; used only in bounds)
+        const uint32_t cws = word_at(w.buf, min(x + chl, kBWin));
+        const uint32_t fws = word_at(w.buf, min(x + chl + 4u + RL, kBWin));
+        const u64 m = __ballot(hit);
+        if (!m) break;
+        const uint32_t f = (uint32_t)__ffsll((long long)m) - 1u;
+        const uint32_t hl = rdlane(chl, f), cnt = rdlane(ccnt, f);
+        if (x + hl + 4u > lim) break;
+        const uint32_t m_tok = __builtin_bswap32(rdlane(cws, f));
+        if (m_tok == 0 || m_tok > cnt || nr + m_tok > 64u) break;
+        uint32_t y = x + hl + 4u;
+        bool okr = true;
+        for (uint32_t j = 0; j < m_tok; ++j) {
+            const uint32_t v = j ? ufl32(word_at(w.buf, y + RL)) : rdlane(fws, f);
+            const uint32_t a0 = v & 0xFFu, a1 = (v >> 8) & 0xFFu, a2 = (v >> 16) & 0xFFu;
+            uint32_t gh = 0, len = 0;
+            if ((a0 == 100 || a0 == 118) && a1 == 0) { gh = 3; len = a2; }
+            else if (a0 == 119) { gh = 2; len = a1; }
+            if (!gh || (len != 4 && len != 5) || y + RL + gh + len > lim) { okr = false; break; }
+            if (lane == nr + j) { ry = y; rel = ne; rh = gh; rlen = len; }
+            y += RL + gh + len;
+        }
+        if (!okr || y + 1u > lim || ufl32(w.buf[y]) != 106) break;
+        if (lane == ne) { ex = x; ec = f; }
+        nr += m_tok;
+        ++ne;
+        fmin = (int32_t)f;
+        x = y + 1u;
+    }
+    if (ne == 0) return 0;
+    // lane j < nr: record j
+    const bool mine = lane < nr;
+    const uint32_t myc = __shfl(ec, rel, 64);
+    const uint32_t re = __shfl(ce, myc, 64), rkey = __shfl(ckey, myc, 64),
+                   rcnt = __shfl(ccnt, myc, 64);
+    uint32_t k = 0xFFu, fl = 0;
+    bool ok = false;
+    if (mine) {
+        const u64 r = (u64)(prev + 1) + myc;
+        const uint32_t kw = 4u * (rkey & 0xFFu), ksh = rkey >> 8;
+        const uint32_t bk = (word_at(w.buf, ry + kw) >> ksh) & (kBuckets - 1u);
+        for (uint32_t j = 0; j < rcnt && j < RK; ++j)
+            if (t.tb[r * RK + j] == bk) k = j;
+        ok = k < rcnt;
+        if (ok) {                                   // exact compare
+            uint32_t rw[12], tw[12];
+            rec_words(w.buf, ry, RL, rw);
+            load48(tw, d.rec_pad + ((u64)re * RK + k) * RS, RL);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) ok &= tw[i] == rw[i];
+        }
+        // "true" / "false" after the atom header the walk read
+        const uint32_t fo = ry + RL + rh;
+        const uint32_t word = word_at(w.buf, fo), c4 = w.buf[fo + 4];
+        const bool tr = rlen == 4 && word == 0x65757274u;
+        const bool fa = rlen == 5 && word == 0x736C6166u && c4 == 'e';
+        ok &= tr || fa;
+        fl = tr;
+    }
+    // term order within the element
+    const uint32_t pk = __shfl(k, (lane + 63u) & 63u, 64), pel = __shfl(rel, (lane + 63u) & 63u, 64);
+    if (mine && lane > 0 && pel == rel && k <= pk) ok = false;
+    const u64 bad = __ballot(mine && !ok);
+    const uint32_t commit = bad ? rdlane(rel, (uint32_t)__ffsll((long long)bad) - 1u) : ne;
+    if (commit == 0) return 0;
+    // cells: token bits by slot, ORed per element in LDS
+    unsigned long long* pc64 = reinterpret_cast<unsigned long long*>(L.tab);
+    wave_sync();
+    pc64[2 * lane] = 0;
+    pc64[2 * lane + 1] = 0;
+    wave_sync();
+    if (mine && rel < commit) {
+        const uint32_t slot = d.tok_order[64ull * re + k];
+        atomicOr(pc64 + 2 * rel, 1ull << slot);
+        if (fl) atomicOr(pc64 + 2 * rel + 1, 1ull << slot);
+    }
+    wave_sync();
+    const uint32_t me = __shfl(ce, ec, 64);
+    if (lane < commit) c[me] = u64x2{pc64[2 * lane], pc64[2 * lane + 1]};
+    prev += 1 + (int64_t)rdlane(ec, commit - 1u);
+    pc = commit == ne ? x : rdlane(ex, commit);
+    return commit;
+}
+
+template <bool SMALL>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
@@ -1388,7 +1534,16 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payloa
             }
             int64_t prev = -1;                    // term rank of the previous element
             RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
-            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
+            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK;) {
+                if (SMALL) {
+                    const uint32_t got = read_batch(w, pc, prev, n - k, tabs, d, E, RL, RS, L, c,
+                                                    lane);
+                    if (got) {
+                        k += got;
+                        if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
+                        continue;
+                    }
+                }
                 // 104 2 <elem image> 108 <count:32> of the next element in term order
                 const uint32_t span = min(hmax, w.end - pc);
                 pc = need(w, pc, span);
@@ -1579,6 +1734,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payloa
                 const uint32_t v = cur.ros < 64u ? L.pres[cur.ros] : 0u;
                 const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
                 if (lane == 0) c[e] = u64x2{pb, rb};
+                ++k;
             }
             if (st != LASPJ_DEC_OK) break;
             if (n) {
@@ -1760,8 +1916,10 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    if (d->rd_desc && ctx->tune_etf_read == 0)
-        hipLaunchKernelGGL(k_orset_etf_read, dim3(grid), dim3(kBlock), 0, ctx->stream,
+    if (d->rd_desc && ctx->tune_etf_read != 1)
+        // 0: element batches when elements hold <= 8 token slots; 2: records batched only
+        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read == 0
+                               ? k_orset_etf_read<true> : k_orset_etf_read<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
                            static_cast<const u64*>(offsets->dev), R, b->elements, view(d),
                            ReadTabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb,

@@ -389,7 +389,8 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 
 @contextlib.contextmanager
 def _read_kernel(ctx, knob):
-    """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records, 1 = serial scan."""
+    """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
+    <= 8 token slots), 1 = serial scan, 2 = batched records only."""
     from lasp_amd import _lib
     ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
     try:
@@ -454,7 +455,7 @@ def test_gpu_from_binary_round_trip(tagged, knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1])
+@pytest.mark.parametrize("knob", [0, 1, 2])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
@@ -582,3 +583,138 @@ def test_gpu_from_binary_fuzz():
         again = bt.to_binaries(d, tag=T, vers=1)
         for i in ok:
             assert again[i] == blobs[i], i
+
+
+def _small_orsets(rng, n):
+    """Random orddicts whose elements hold <= 3 of their own 20-byte tokens (the
+    dictionary's tok_max <= 8: the decoder's element batches); small and large integer
+    elements, an atom, and binaries whose element header is longer than 64 bytes."""
+    elems = list(range(0, 300, 3)) + [1 << 40, -7, PAtom("ad"), b"b" * 70, b"c" * 61]
+    pool = {i: [bytes(rng.randrange(256) for _ in range(20)) for _ in range(3)]
+            for i in range(len(elems))}
+    from oracle.otp import lists_sort
+    res = []
+    for _ in range(n):
+        d = {}
+        for i in rng.sample(range(len(elems)), rng.randint(0, len(elems))):
+            d[elems[i]] = {t: rng.random() < 0.4 for t in rng.sample(pool[i], rng.randint(1, 3))}
+        keys = lists_sort(list(d.keys()))
+        res.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in keys])
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", [0, 1, 2])
+def test_gpu_from_binary_small_tokens_round_trip(knob):
+    """Elements with <= 3 token slots (element batches under knob 0): oracle payloads
+    with every flag atom form decode to the host encoder's cells, and device to_binary ->
+    from_binary is the identity, under every read kernel."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    rng = random.Random(5)
+    states = _small_orsets(rng, 300) + [[]]
+    ctx, dom, E, d = _decode_setup(states)
+    T = etf.DT_ORSET_TAG
+    blobs = []
+    for i, s in enumerate(states):
+        p = oetf.to_binary(T, 1, s)
+        if i % 3 == 1:       # SMALL_ATOM_UTF8_EXT flags
+            p = p.replace(bytes([100, 0, 4]) + b"true", bytes([119, 4]) + b"true") \
+                 .replace(bytes([100, 0, 5]) + b"false", bytes([119, 5]) + b"false")
+        elif i % 3 == 2:     # ATOM_UTF8_EXT `true` beside ATOM_EXT `false`
+            p = p.replace(bytes([100, 0, 4]) + b"true", bytes([118, 0, 4]) + b"true")
+        blobs.append(p)
+    pay, offs = _upload_payloads(ctx, blobs)
+    b = ctx.orset_batch(len(states), E)
+    want = dom.encode_orset(states, E)
+    with _read_kernel(ctx, knob):
+        st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+        assert (st == _lib.DEC_OK).all(), np.nonzero(st)[0][:10]
+        assert np.array_equal(b.download(), want)
+        offs2, out2, _ = b.etf_encode(d, tag=T, vers=1)
+        b2 = ctx.orset_batch(len(states), E)
+        assert (b2.etf_decode(d, out2, offs2, tag=T, vers=1) == 0).all()
+        assert np.array_equal(b2.download(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_small_tokens_fuzz():
+    """3000 corrupted small-token payloads and the 80 intact ones: the element-batch
+    decode (knob 0), the record-batch decode (2) and the serial scan (1) give the same
+    status and cells for every payload."""
+    import numpy as np
+    from lasp_amd import etf
+    rng = random.Random(91)
+    states = _small_orsets(rng, 80)
+    ctx, dom, E, d = _decode_setup(states)
+    T = etf.DT_ORSET_TAG
+    base = [oetf.to_binary(T, 1, s) for s in states]
+    blobs = []
+    for _ in range(3000):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(5)
+        if kind == 0 and b:
+            for _ in range(rng.randint(1, 3)):
+                b[rng.randrange(len(b))] = rng.randrange(256)
+        elif kind == 1 and b:
+            del b[rng.randrange(len(b)):]
+        elif kind == 2:
+            pos = rng.randrange(len(b) + 1)
+            b[pos:pos] = bytes(rng.randrange(256) for _ in range(rng.randint(1, 9)))
+        elif kind == 3 and len(b) > 8:      # a flag / count / tail byte nudged by one
+            pos = rng.randrange(2, len(b))
+            b[pos] = (b[pos] + rng.choice([1, 255])) & 0xFF
+        else:
+            other = rng.choice(base)
+            b = b[:rng.randrange(len(b) + 1)] + other[rng.randrange(len(other) + 1):]
+        blobs.append(bytes(b))
+    blobs += base                             # and the payloads themselves
+    pay, offs = _upload_payloads(ctx, blobs)
+    res = {}
+    for knob in (0, 2, 1):
+        bt = ctx.orset_batch(len(blobs), E)
+        with _read_kernel(ctx, knob):
+            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+        res[knob] = (st, bt.download())
+    st0, c0 = res[0]
+    assert set(np.unique(st0)) <= {0, 1, 2, 3, 4, 5}
+    assert (st0 == 0).sum() >= len(base)
+    for knob in (1, 2):
+        st, c = res[knob]
+        assert np.array_equal(st0, st), (knob, np.nonzero(st0 != st)[0][:10])
+        ok = st0 == 0
+        assert np.array_equal(c0[ok], c[ok]), knob
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_small_tokens_large():
+    """8192 replicas x 256 slots x <= 3 tokens (the suite's t3 shape, 10 % of elements
+    absent): device to_binary -> from_binary restores every cell; the element-batch and
+    record-batch kernels agree."""
+    import hashlib
+    import numpy as np
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    R, E = 8192, 256
+    ctx = context()
+    rng = np.random.default_rng(3)
+    h = np.zeros((R, E, 2), np.uint64)
+    present = rng.random((R, E)) < 0.9
+    h[:, :, 0] = np.where(present, rng.integers(1, 8, (R, E), dtype=np.uint64), 0)
+    h[:, :, 1] = h[:, :, 0] & rng.integers(0, 8, (R, E), dtype=np.uint64)
+    b = ctx.orset_batch(R, E)
+    b.upload(h)
+    dom = Domain()
+    for e in range(E):
+        es = dom.element_slot(e * 1000)
+        for k in range(3):
+            dom.token_slot(es, hashlib.blake2b(b"%d:%d" % (e, k), digest_size=20).digest())
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    offs, out, _ = b.etf_encode(d, tag=etf.DT_ORSET_TAG, vers=1)
+    for knob in (0, 2):
+        b2 = ctx.orset_batch(R, E)
+        with _read_kernel(ctx, knob):
+            st = b2.etf_decode(d, out, offs, tag=etf.DT_ORSET_TAG, vers=1)
+        assert (st == 0).all(), knob
+        assert np.array_equal(b2.download(), h), knob

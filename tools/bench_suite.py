@@ -298,11 +298,15 @@ def etf(ctx, steps):
         _lib.check(L.laspj_orset_etf_write(ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h)
         back = ctx.orset_batch(R, E)
         stb = ctx.buffer(4 * R)
-        ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_read(
-            ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h), ctx.h), steps)
-        report(f"orset_etf_read_{tag}", ms, 16 * cells + total.value, cells, "cells_per_s",
-               replicas=R, elements=E, payload_bytes=total.value,
-               payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        # 0: default (element batches at <= 8 token slots), 2: record batches only
+        for knob, name in ((0, "read"), (2, "read_records")) if T <= 8 else ((0, "read"),):
+            ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
+            ms = timed(ctx, lambda: _lib.check(L.laspj_orset_etf_read(
+                ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h), ctx.h), steps)
+            report(f"orset_etf_{name}_{tag}", ms, 16 * cells + total.value, cells,
+                   "cells_per_s", replicas=R, elements=E, payload_bytes=total.value,
+                   payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+        ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
         del back, stb
         del out, offs, d, b
 
