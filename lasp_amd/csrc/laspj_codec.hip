@@ -1377,24 +1377,30 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
         }
     }
     const bool cval = chl > 3u && chl <= 64u;
+    // the walk tells elements apart by their first 16 header bytes (masks per lane);
+    // every header is compared whole below, before anything is committed
+    uint32_t mk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rem = (int)chl - 4 * i;
+        mk[i] = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+    }
     const uint32_t lim = min(w.hi, w.end);
     // the walk: element lanes (start, candidate lane), record lanes (start, element,
     // atom header length, atom length)
     uint32_t x = pc, ne = 0, nr = 0, ex = 0, ec = 0, ry = 0, rel = 0, rh = 0, rlen = 0;
     int32_t fmin = -1;
+    u64 cm = 0;                          // candidate lanes the walk matched
     while (ne < 64u && ne < left && x < lim) {
         const uint32_t* b32 = reinterpret_cast<const uint32_t*>(w.buf + (x & ~3u));
         const uint32_t sh = x & 3u;
         bool hit = cval && (int32_t)lane > fmin && x + chl <= lim;
         uint32_t q0 = b32[0];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < 4; ++i) {
             const uint32_t q1 = b32[i + 1];
-            const uint32_t v = __builtin_amdgcn_alignbyte(q1, q0, sh);
+            hit &= (__builtin_amdgcn_alignbyte(q1, q0, sh) & mk[i]) == ch[i];
             q0 = q1;
-            const int rem = (int)chl - 4 * i;
-            const uint32_t msk = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
-            hit &= (v & msk) == ch[i];
         }
         // read beside the compare, as if this lane's rank matched: the token count and
         // the first record's flag header (clamped inside the window; used only in bounds)
@@ -1424,6 +1430,7 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
         nr += m_tok;
         ++ne;
         fmin = (int32_t)f;
+        cm |= 1ull << f;
         x = y + 1u;
     }
     if (ne == 0) return 0;
@@ -1460,7 +1467,28 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
     const uint32_t pk = __shfl(k, (lane + 63u) & 63u, 64), pel = __shfl(rel, (lane + 63u) & 63u, 64);
     if (mine && lane > 0 && pel == rel && k <= pk) ok = false;
     const u64 bad = __ballot(mine && !ok);
-    const uint32_t commit = bad ? rdlane(rel, (uint32_t)__ffsll((long long)bad) - 1u) : ne;
+    uint32_t commit = bad ? rdlane(rel, (uint32_t)__ffsll((long long)bad) - 1u) : ne;
+    // whole headers: matched candidate lane c checks element popcount(cm below c)
+    const bool cme = (cm >> lane) & 1ull;
+    const uint32_t ei = (uint32_t)__popcll(cm & ((1ull << lane) - 1ull));
+    const uint32_t xi = __shfl(ex, ei & 63u, 64);
+    bool hok = true;
+    if (cme) {
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(w.buf + (xi & ~3u));
+        const uint32_t sh = xi & 3u;
+        uint32_t q0 = b32[0];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t q1 = b32[i + 1];
+            const uint32_t v = __builtin_amdgcn_alignbyte(q1, q0, sh);
+            q0 = q1;
+            const int rem = (int)chl - 4 * i;
+            const uint32_t msk = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+            hok &= (v & msk) == ch[i];
+        }
+    }
+    const u64 hbad = __ballot(cme && !hok);
+    if (hbad) commit = min(commit, rdlane(ei, (uint32_t)__ffsll((long long)hbad) - 1u));
     if (commit == 0) return 0;
     // cells: token bits by slot, ORed per element in LDS
     unsigned long long* pc64 = reinterpret_cast<unsigned long long*>(L.tab);
