@@ -1942,7 +1942,9 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     if (off[R] > payload->bytes)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
-    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
+    // one replica per wave up to 64 blocks per CU: short blocks keep every CU busy to the
+    // end (a grid-stride over a few resident waves left a 20 % tail at 65536 replicas)
+    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
     const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
     if (d->rd_desc && ctx->tune_etf_read != 1)
         // 0: element batches when elements hold <= 8 token slots; 2: records batched only
