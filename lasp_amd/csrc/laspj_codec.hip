@@ -1363,18 +1363,14 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
     if (w.hi < w.end && pc + kBWin / 2 > w.hi) pc = refill(w, pc);
     // lane i: rank prev + 1 + i (descriptor, header template words)
     const int64_t cr = prev + 1 + (int64_t)lane;
-    uint32_t ce = 0, chl = 0, ckey = 0, ccnt = 0, ch[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ch[i] = 0;
+    // (the template's other 48 bytes are loaded again for the whole-header check)
+    uint32_t ce = 0, chl = 0, ckey = 0, ccnt = 0, ch[4] = {0, 0, 0, 0};
+    const u32x4* hsrc = reinterpret_cast<const u32x4*>(t.hdr + 64ull * (u64)max(cr, (int64_t)0));
     if (cr < (int64_t)E) {
         const uint4 ds = t.desc[cr];
         ce = ds.x; chl = ds.y; ckey = ds.z; ccnt = ds.w;
-        const u32x4* h = reinterpret_cast<const u32x4*>(t.hdr + 64ull * (u64)cr);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 v = h[i];
-            ch[4 * i] = v.x; ch[4 * i + 1] = v.y; ch[4 * i + 2] = v.z; ch[4 * i + 3] = v.w;
-        }
+        const u32x4 v = hsrc[0];
+        ch[0] = v.x; ch[1] = v.y; ch[2] = v.z; ch[3] = v.w;
     }
     const bool cval = chl > 3u && chl <= 64u;
     // the walk tells elements apart by their first 16 header bytes (masks per lane);
@@ -1474,6 +1470,13 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
     const uint32_t xi = __shfl(ex, ei & 63u, 64);
     bool hok = true;
     if (cme) {
+        uint32_t tw[16];
+        tw[0] = ch[0]; tw[1] = ch[1]; tw[2] = ch[2]; tw[3] = ch[3];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+            const u32x4 v = hsrc[i];
+            tw[4 * i] = v.x; tw[4 * i + 1] = v.y; tw[4 * i + 2] = v.z; tw[4 * i + 3] = v.w;
+        }
         const uint32_t* b32 = reinterpret_cast<const uint32_t*>(w.buf + (xi & ~3u));
         const uint32_t sh = xi & 3u;
         uint32_t q0 = b32[0];
@@ -1484,7 +1487,7 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
             q0 = q1;
             const int rem = (int)chl - 4 * i;
             const uint32_t msk = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
-            hok &= (v & msk) == ch[i];
+            hok &= (v & msk) == tw[i];
         }
     }
     const u64 hbad = __ballot(cme && !hok);
@@ -1510,7 +1513,7 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
 }
 
 template <bool SMALL>
-__global__ __launch_bounds__(kBlock) void k_orset_etf_read(const uint8_t* payload, u64 total,
+__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
                                                            ReadTabs tabs, int tag, int vers,
