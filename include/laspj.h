@@ -128,7 +128,8 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = flat sweep when
                                         the replica length is a power of two and
                                         2 <= group <= 4, 1 = per-replica segments with a
-                                        compile-time group, 2 = generic segments        */
+                                        compile-time group, 2 = generic segments (also
+                                        the runtime-count loop of reduce_chunks)       */
 #define LASPJ_TUNE_PRODUCT_ROWS  6   /* rows per outer-product tile: 0 = default (256),
                                         32, 64, 128, 256                                */
 #define LASPJ_TUNE_PRODUCT_COLS  7   /* columns per outer-product tile: 0 = default
@@ -181,13 +182,16 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed
 
 /* Slot-wise join of two batches of the same kind and shape (any kind): dst = a | b
  * word by word.  For OR-Set / G-Set batches this is merge/2; for combinator outputs
- * it ORs both halves of CONCAT cells and the packed masks of PRODUCT cells. */
+ * it ORs both halves of CONCAT cells and the packed masks of PRODUCT cells; for
+ * G-Counter batches it is the per-actor max (riak_dt_gcounter merge, as
+ * laspj_gcounter_join). */
 int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b);
 
 /* Anti-entropy reduce step: src holds nchunks copies of dst's replica
  * range laid out chunk-major (what an all-to-all delivers); dst[i] = ⊔_j src[j*R + i].
- * Any kind; src.replicas = nchunks * dst.replicas. */
+ * Any kind; src.replicas = nchunks * dst.replicas.  ⊔ is the kind's join: OR of the
+ * words for bitmap kinds, per-actor max for G-Counters. */
 int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                               uint32_t nchunks);
 

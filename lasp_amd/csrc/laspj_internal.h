@@ -101,8 +101,9 @@ hipError_t launch_gcounter_inflation(laspj_ctx* ctx, const laspj_batch* prev,
                                      const laspj_batch* cur, bool strict, uint8_t* out);
 hipError_t launch_gcounter_incr(laspj_ctx* ctx, laspj_batch* b, const laspj_incr* incs,
                                 uint64_t n);
+// max_join: per-word unsigned max (G-Counter counts) instead of OR (set bitmaps)
 hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
-                                uint64_t words, uint32_t nchunks);
+                                uint64_t words, uint32_t nchunks, bool max_join);
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t words_per_replica);
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,

@@ -270,39 +270,91 @@ hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
     return hipGetLastError();
 }
 
-// dst[w] = OR_j src[j*n + w]: the reduce of an all-to-all receive buffer
+// dst[w] = join_j src[j*n + w]: the reduce of an all-to-all receive buffer.  The join
+// is the word-wise OR for set bitmaps and the per-actor (unsigned) max for G-Counter
+// counts (riak_dt_gcounter merge); MAX selects the latter.
+template <bool MAX>
+__device__ __forceinline__ u64 join_word(u64 x, u64 y) {
+    if constexpr (MAX) return x > y ? x : y;
+    else return x | y;
+}
+
+template <bool MAX>
 __global__ __launch_bounds__(kBlock) void k_reduce_chunks(u64x2* dst, const u64x2* src,
                                                           uint64_t n, uint32_t nchunks) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         u64x2 acc = ld2<true>(src + i);
-        for (uint32_t j = 1; j < nchunks; ++j) acc |= ld2<true>(src + (uint64_t)j * n + i);
+        for (uint32_t j = 1; j < nchunks; ++j) {
+            const u64x2 v = ld2<true>(src + (uint64_t)j * n + i);
+            acc.x = join_word<MAX>(acc.x, v.x);
+            acc.y = join_word<MAX>(acc.y, v.y);
+        }
         st2<true>(dst + i, acc);
     }
 }
 
+// chunk count known at compile time (world sizes 2..8): all NC loads of a cell are
+// issued before the first join, so a lane keeps NC x 16 B in flight
+template <bool MAX, int NC>
+__global__ __launch_bounds__(kBlock) void k_reduce_chunks_n(u64x2* dst, const u64x2* src,
+                                                            uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        u64x2 v[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) v[j] = ld2<true>(src + (uint64_t)j * n + i);
+#pragma unroll
+        for (int j = 1; j < NC; ++j) {
+            v[0].x = join_word<MAX>(v[0].x, v[j].x);
+            v[0].y = join_word<MAX>(v[0].y, v[j].y);
+        }
+        st2<true>(dst + i, v[0]);
+    }
+}
+
+template <bool MAX>
 __global__ __launch_bounds__(kBlock) void k_reduce_chunks_scalar(u64* dst, const u64* src,
                                                                  uint64_t n, uint32_t nchunks) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         u64 acc = src[i];
-        for (uint32_t j = 1; j < nchunks; ++j) acc |= src[(uint64_t)j * n + i];
+        for (uint32_t j = 1; j < nchunks; ++j) acc = join_word<MAX>(acc, src[(uint64_t)j * n + i]);
         dst[i] = acc;
     }
 }
 
-hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
-                                uint64_t words, uint32_t nchunks) {
+template <bool MAX>
+static void launch_reduce_chunks_t(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                                   uint64_t words, uint32_t nchunks) {
     if ((words & 1) == 0) {
         StreamTune t = stream_tune(ctx, words / 2);
-        hipLaunchKernelGGL(k_reduce_chunks, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<u64x2*>(dst), reinterpret_cast<const u64x2*>(src),
-                           words / 2, nchunks);
+        auto* d2 = reinterpret_cast<u64x2*>(dst);
+        auto* s2 = reinterpret_cast<const u64x2*>(src);
+        const uint64_t n = words / 2;
+#define LJ_RCN(NC)                                                                          \
+    case NC:                                                                                \
+        hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC>), dim3(t.grid), dim3(kBlock), 0,    \
+                           ctx->stream, d2, s2, n);                                         \
+        break
+        switch (ctx->tune_reduce == 2 ? 0u : nchunks) {
+            LJ_RCN(2); LJ_RCN(3); LJ_RCN(4); LJ_RCN(5); LJ_RCN(6); LJ_RCN(7); LJ_RCN(8);
+            default:
+                hipLaunchKernelGGL(k_reduce_chunks<MAX>, dim3(t.grid), dim3(kBlock), 0,
+                                   ctx->stream, d2, s2, n, nchunks);
+        }
+#undef LJ_RCN
     } else {    // odd word count: chunk starts are only 8-byte aligned
         StreamTune t = stream_tune(ctx, words);
-        hipLaunchKernelGGL(k_reduce_chunks_scalar, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
-                           (u64*)dst, (const u64*)src, words, nchunks);
+        hipLaunchKernelGGL(k_reduce_chunks_scalar<MAX>, dim3(t.grid), dim3(kBlock), 0,
+                           ctx->stream, (u64*)dst, (const u64*)src, words, nchunks);
     }
+}
+
+hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
+                                uint64_t words, uint32_t nchunks, bool max_join) {
+    if (max_join) launch_reduce_chunks_t<true>(ctx, dst, src, words, nchunks);
+    else launch_reduce_chunks_t<false>(ctx, dst, src, words, nchunks);
     return hipGetLastError();
 }
 

@@ -388,8 +388,10 @@ int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batc
         return fail(ctx, LASPJ_E_SHAPE, "reduce_chunks: need src replicas = nchunks x dst");
     if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "reduce_chunks: dst aliases src");
     Guard g(ctx);
+    // the join of the batch's lattice: OR for bitmaps, per-actor max for G-Counters
     LJ_HIP(ctx, laspj::launch_reduce_chunks(ctx, dst->dev, src->dev,
-                                            dst->replicas * dst->words_per_replica, nchunks));
+                                            dst->replicas * dst->words_per_replica, nchunks,
+                                            dst->kind == LASPJ_KIND_GCOUNTER));
     return LASPJ_OK;
 }
 
@@ -478,8 +480,11 @@ int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         a->elements_r != b->elements_r)
         return fail(ctx, LASPJ_E_SHAPE, "batch_join: shapes differ");
     Guard g(ctx);
-    LJ_HIP(ctx, laspj::launch_or(ctx, dst->dev, a->dev, b->dev,
-                                 a->replicas * a->words_per_replica));
+    const uint64_t words = a->replicas * a->words_per_replica;
+    if (a->kind == LASPJ_KIND_GCOUNTER)     // riak_dt_gcounter merge: per-actor max
+        LJ_HIP(ctx, laspj::launch_max(ctx, dst->dev, a->dev, b->dev, words));
+    else
+        LJ_HIP(ctx, laspj::launch_or(ctx, dst->dev, a->dev, b->dev, words));
     return LASPJ_OK;
 }
 

@@ -192,6 +192,58 @@ def test_orset_reduce_all_kernels(ctx, e_n):
             ctx.set_tuning(TUNE_REDUCE_KERNEL, 0)
 
 
+@pytest.mark.parametrize("nchunks", [1, 2, 3, 5, 8])
+def test_reduce_chunks_every_kind(ctx, nchunks):
+    """laspj_batch_reduce_chunks (the anti-entropy reduce of an all-to-all receive
+    buffer, gossip.DeviceAntiEntropy) is the kind's join over the chunk-major copies:
+    OR for OR-Set cells and G-Set words (odd word counts take the 8-byte kernel), the
+    per-actor max for riak_dt_gcounter counts."""
+    from lasp_amd._lib import TUNE_REDUCE_KERNEL
+    rng = np.random.default_rng(100 + nchunks)
+    n = 29
+    cases = ((ctx.orset_batch, 100, "or"), (ctx.gset_batch, 100, "or"),     # G-Set: 2 words
+             (ctx.gset_batch, 64, "or"),                                   # 29 words: odd
+             (ctx.gcounter_batch, 7, "max"), (ctx.gcounter_batch, 8, "max"))
+    for make, e_n, op in cases:
+        src, dst = make(nchunks * n, e_n), make(n, e_n)
+        w = src.words_per_replica
+        if op == "max":       # small counts so chunks collide, some equal
+            hs = rng.integers(0, 5, size=(nchunks * n, w), dtype=np.uint64)
+        else:
+            hs = rng.integers(0, 2**63, size=(nchunks * n, w), dtype=np.uint64) * np.uint64(2) \
+                + rng.integers(0, 2, size=(nchunks * n, w), dtype=np.uint64)
+            if make is ctx.gset_batch and e_n % 64:   # padding bits beyond E stay zero
+                hs[:, -1] &= np.uint64((1 << (e_n % 64)) - 1)
+        src.upload(hs)
+        red = np.maximum.reduce if op == "max" else np.bitwise_or.reduce
+        want = red(hs.reshape(nchunks, n, w), axis=0)
+        try:
+            for knob in (0, 2):    # compile-time chunk count / runtime-count loop
+                ctx.set_tuning(TUNE_REDUCE_KERNEL, knob)
+                dst.clear()
+                dst.reduce_chunks(src, nchunks)
+                assert np.array_equal(dst.download_words(), want), (make.__name__, e_n, knob)
+        finally:
+            ctx.set_tuning(TUNE_REDUCE_KERNEL, 0)
+
+
+def test_batch_join_gcounter_is_max(ctx):
+    """laspj_batch_join on G-Counter batches is riak_dt_gcounter's merge (per-actor max,
+    the same as laspj_gcounter_join), not a bitwise OR of the counts."""
+    rng = np.random.default_rng(7)
+    a, b, c, d = (ctx.gcounter_batch(33, 9) for _ in range(4))
+    ha = rng.integers(0, 6, size=(33, 9), dtype=np.uint64)
+    hb = rng.integers(0, 6, size=(33, 9), dtype=np.uint64)
+    a.upload(ha)
+    b.upload(hb)
+    L = ctx.L
+    from lasp_amd._lib import check
+    check(L.laspj_batch_join(ctx.h, c.h, a.h, b.h), ctx.h)
+    d.join(a, b)
+    assert np.array_equal(c.download(), np.maximum(ha, hb))
+    assert np.array_equal(d.download(), c.download())
+
+
 def test_orset_equal(ctx):
     a, b = ctx.orset_batch(8, E), ctx.orset_batch(8, E)
     a.fill_synthetic(5)

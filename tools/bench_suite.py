@@ -106,6 +106,15 @@ def kernels(ctx, R, E, steps):
     report("orset_reduce_chunks_n3", timed(ctx, lambda: dst.reduce_chunks(src, 3), steps),
            64 * g * E, g * E, "dst_cells_per_s")
     del src, dst, a, b
+    # the anti-entropy reduce at N = 8 (gossip round on 8 GPUs: 8 chunk-major copies)
+    q = (3 * g) // 8
+    src8, dst8 = ctx.orset_batch(8 * q, E), ctx.orset_batch(q, E)
+    for knob, name in ((0, "orset_reduce_chunks_n8"), (2, "orset_reduce_chunks_n8_loop")):
+        ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, knob)
+        report(name, timed(ctx, lambda: dst8.reduce_chunks(src8, 8), steps),
+               16 * 9 * q * E, q * E, "dst_cells_per_s")
+    ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, 0)
+    del src8, dst8
     h = R // 2                      # CONCAT output is 32 B per cell: half the replicas
     a2, b2 = ctx.orset_batch(h, E), ctx.orset_batch(h, E)
     a2.fill_synthetic(2)
