@@ -188,9 +188,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or_g(u64x2* dst, const u64x2*
     }
 }
 
+// the join of one 64-bit word: OR for set bitmaps, unsigned max for G-Counter counts
+// (riak_dt_gcounter merge)
+template <bool MAX>
+__device__ __forceinline__ u64 join_word(u64 x, u64 y) {
+    if constexpr (MAX) return x > y ? x : y;
+    else return x | y;
+}
+
 // power-of-two replica length: one flat grid-stride sweep over the destination (all
-// blocks move through HBM together, as the join does), 2 cells x G loads per lane
-template <int G>
+// blocks move through HBM together, as the join does), 2 cells x G loads per lane;
+// MAX: the same sweep for the G-Counter reduce (per-actor max)
+template <int G, bool MAX = false>
 __global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64x2* src,
                                                            uint64_t n, uint32_t lg) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock, mask = (1ull << lg) - 1ull;
@@ -206,8 +215,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64
         for (int j = 0; j < G; ++j) y[j] = ld2<true>(t + ((uint64_t)j << lg));
 #pragma unroll
         for (int j = 1; j < G; ++j) {
-            x[0] |= x[j];
-            y[0] |= y[j];
+            x[0].x = join_word<MAX>(x[0].x, x[j].x);
+            x[0].y = join_word<MAX>(x[0].y, x[j].y);
+            y[0].x = join_word<MAX>(y[0].x, y[j].x);
+            y[0].y = join_word<MAX>(y[0].y, y[j].y);
         }
         st2<true>(dst + i, x[0]);
         st2<true>(dst + i2, y[0]);
@@ -218,17 +229,20 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64
 #pragma unroll
         for (int j = 0; j < G; ++j) x[j] = ld2<true>(s + ((uint64_t)j << lg));
 #pragma unroll
-        for (int j = 1; j < G; ++j) x[0] |= x[j];
+        for (int j = 1; j < G; ++j) {
+            x[0].x = join_word<MAX>(x[0].x, x[j].x);
+            x[0].y = join_word<MAX>(x[0].y, x[j].y);
+        }
         st2<true>(dst + i, x[0]);
     }
 }
 
-template <int G>
+template <int G, bool MAX = false>
 static void launch_reduce_flat(laspj_ctx* ctx, u64x2* d, const u64x2* s, uint64_t n,
                                uint32_t lg) {
     StreamTune t = stream_tune(ctx, n);
-    hipLaunchKernelGGL((k_reduce_or_flat<G>), dim3(t.grid), dim3(kBlock), 0, ctx->stream, d, s,
-                       n, lg);
+    hipLaunchKernelGGL((k_reduce_or_flat<G, MAX>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
+                       d, s, n, lg);
 }
 
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
@@ -273,12 +287,6 @@ hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
 // dst[w] = join_j src[j*n + w]: the reduce of an all-to-all receive buffer.  The join
 // is the word-wise OR for set bitmaps and the per-actor (unsigned) max for G-Counter
 // counts (riak_dt_gcounter merge); MAX selects the latter.
-template <bool MAX>
-__device__ __forceinline__ u64 join_word(u64 x, u64 y) {
-    if constexpr (MAX) return x > y ? x : y;
-    else return x | y;
-}
-
 template <bool MAX>
 __global__ __launch_bounds__(kBlock) void k_reduce_chunks(u64x2* dst, const u64x2* src,
                                                           uint64_t n, uint32_t nchunks) {
@@ -1032,6 +1040,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_max(u64* dst, const u64* src,
 
 hipError_t launch_reduce_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                              uint64_t groups, uint32_t group, uint64_t wr) {
+    if ((wr % 2) == 0 && ctx->tune_reduce == 0) {     // the flat sweep, as the OR reduce
+        const uint64_t per = wr / 2;
+        if ((per & (per - 1)) == 0 && group >= 2 && group <= 4) {
+            const uint32_t lg = (uint32_t)__builtin_ctzll(per);
+            auto* d2 = reinterpret_cast<u64x2*>(dst);
+            auto* s2 = reinterpret_cast<const u64x2*>(src);
+            if (group == 2) launch_reduce_flat<2, true>(ctx, d2, s2, groups * per, lg);
+            else if (group == 3) launch_reduce_flat<3, true>(ctx, d2, s2, groups * per, lg);
+            else launch_reduce_flat<4, true>(ctx, d2, s2, groups * per, lg);
+            return hipGetLastError();
+        }
+    }
     StreamTune t = stream_tune(ctx, groups * wr);
     hipLaunchKernelGGL(k_reduce_max, dim3(t.grid), dim3(kBlock), 0, ctx->stream, (u64*)dst,
                        (const u64*)src, groups, group, wr);

@@ -684,6 +684,29 @@ def test_gcounter_batch_kernels(ctx):
     assert h[0, 3] == a[0, 3] + 8 and h[39, 4999] == a[39, 4999] + 2
 
 
+@pytest.mark.parametrize("actors", [2, 64, 1024, 5000, 7])
+def test_gcounter_reduce_all_kernels(ctx, actors):
+    """The G-Counter FSM reduce (per-actor max over each group) for groups 2..5: the
+    flat sweep (power-of-two actor pairs, group <= 4) and the generic kernel
+    (LASPJ_TUNE_REDUCE_KERNEL 2, odd actor counts, group 5) agree with numpy."""
+    from lasp_amd._lib import TUNE_REDUCE_KERNEL
+    rng = np.random.default_rng(actors)
+    ng = 37
+    for group in (2, 3, 4, 5):
+        a = rng.integers(0, 6, (group * ng, actors), dtype=np.uint64)
+        a[::7] = np.uint64(2**64 - 1) - a[::7]        # counts above 2^63: unsigned max
+        src = ctx.gcounter_batch(group * ng, actors)
+        src.upload(a)
+        want = a.reshape(ng, group, actors).max(axis=1)
+        try:
+            for knob in (0, 2):
+                ctx.set_tuning(TUNE_REDUCE_KERNEL, knob)
+                got = ctx.gcounter_batch(ng, actors).reduce_from(src, group).download()
+                assert np.array_equal(got, want), (group, knob)
+        finally:
+            ctx.set_tuning(TUNE_REDUCE_KERNEL, 0)
+
+
 def test_abi_error_behaviour(ctx):
     """Shape / kind / range violations come back as status codes with a message and
     leave the batches untouched (the NIF turns them into badarg, which bind swallows:

@@ -148,6 +148,14 @@ def kernels(ctx, R, E, steps):
     report("gcounter_inflation", timed(ctx, lambda: _lib.check(
         L.laspj_gcounter_inflation(ctx.h, ka.h, kc.h, 0, og.h), ctx.h), steps), 2 * n8 + RG,
         RG * A, "actor_slots_per_s")
+    # FSM N = 4 reduce of counters (per-actor max): flat sweep vs the generic kernel
+    kr = ctx.gcounter_batch(RG // 4, A)
+    for knob, name in ((0, "gcounter_reduce_n4"), (2, "gcounter_reduce_n4_generic")):
+        ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, knob)
+        report(name, timed(ctx, lambda: kr.reduce_from(ka, 4), steps), n8 + n8 // 4,
+               (RG // 4) * A, "dst_slots_per_s")
+    ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, 0)
+    del kr
     del ka, kb, kc
 
 
