@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="check the launch (ranks, world size) and exit before any GPU work")
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--nt", type=int, default=-1)
@@ -209,9 +211,39 @@ def load_traffic(path: str, replicas: int, elements: int):
     return d.get("hbm_bytes_per_launch")
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run N rank processes under
+    torch.distributed.run as a CHILD (nothing here has touched the GPU yet, and no
+    process is replaced) and exit with its status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        print(f"bench dry-run rank {os.environ.get('RANK', '0')} of {world}", flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -310,30 +342,40 @@ def main():
 
         def abandon():
             # a collective that never completes must not cost the headline line: rank 0
-            # prints it with the leg marked failed, and every rank leaves with status 0
+            # prints it with the leg marked failed; every rank then exits with status 3
             if out is not None:
                 out["antientropy"] = {"error": f"timed out after {args.ae_timeout:.0f} s"}
                 print(json.dumps(out), flush=True)
-            os._exit(0)
+            sys.stdout.flush()
+            os._exit(3)
 
         guard = threading.Timer(args.ae_timeout, abandon)
         guard.daemon = True
         guard.start()
         try:
             ae = antientropy_leg(ctx, args, rank, world, barrier)
-        except Exception as e:           # reported, never fatal to the headline line
+        except Exception as e:           # reported with the headline line, then rc 3
             ae = {"error": f"{type(e).__name__}: {e}"}
         guard.cancel()
         if out is not None:
             out["antientropy"] = ae
+    else:
+        ae = {}
+    ae_failed = "error" in ae or not ae.get("gcounter", {}).get("converged", True)
 
     if rank != 0:
+        if ae_failed:                    # a peer may be gone: no final barrier
+            os._exit(3)
         _final_barrier(dist)
         return
 
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
     print(json.dumps(out), flush=True)
+    if ae_failed:
+        print("bench: anti-entropy leg failed (see antientropy.error)", file=sys.stderr)
+        sys.stdout.flush()
+        os._exit(3)
     if dist is not None:
         _final_barrier(dist)
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LASPJ_ABI_VERSION 1
+#define LASPJ_ABI_VERSION 2
 
 /* status codes */
 #define LASPJ_OK               0
@@ -309,7 +309,11 @@ int laspj_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
 typedef struct laspj_incr {
     uint64_t replica;
     uint32_t actor;              /* actor slot */
-    uint32_t amount;             /* increment / {increment, N} */
+    uint32_t reserved;
+    uint64_t amount;             /* increment = 1 / {increment, N}: N > 0 (riak_dt_gcounter
+                                    rejects other N with function_clause; the NIF checks
+                                    it before the call).  Counts are uint64: riak_dt's are
+                                    bignums, so counts and sums wrap at 2^64 here.       */
 } laspj_incr;
 int laspj_gcounter_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t actors,
                                 laspj_batch** out);

@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblaspj.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "laspj.h")
 
+ABI_VERSION = 2
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
     -1, -2, -3, -4, -5, -6, -7, -8)
@@ -56,7 +57,8 @@ class Op(C.Structure):
 
 
 class Incr(C.Structure):
-    _fields_ = [("replica", C.c_uint64), ("actor", C.c_uint32), ("amount", C.c_uint32)]
+    _fields_ = [("replica", C.c_uint64), ("actor", C.c_uint32), ("reserved", C.c_uint32),
+                ("amount", C.c_uint64)]
 
 
 vp = C.c_void_p
@@ -160,7 +162,7 @@ def load():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.laspj_abi_version() != 1:
+    if L.laspj_abi_version() != ABI_VERSION:
         raise LaspjUnavailable("ABI version mismatch")
     _lib = L
     return L

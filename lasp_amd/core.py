@@ -208,7 +208,8 @@ class Store:
         from . import orset as _o
         cur = self._copy(v.val)
         if v.type == "riak_dt_gcounter":
-            n = 1 if op == "increment" else op[1]
+            from .gcounter import increment_amount
+            n = increment_amount(op)
             cur.increment([(0, self.cdom.element_slot(actor), n)])
         elif v.type in ("lasp_orset", "lasp_orset_gbtree"):
             ops = []
@@ -251,11 +252,13 @@ class Store:
         strict = isinstance(threshold, tuple) and threshold[0] == "strict"
         term = threshold[1] if strict else threshold
         if v.type == "riak_dt_gcounter":
-            # Threshold =< value(V) (lasp_lattice.erl:87-90); an integer threshold is
-            # compared on the device; new() = [] is never below a number in term order
-            if not isinstance(term, int) or isinstance(term, bool):
-                return False
-            return bool(v.val.threshold_met(term, strict)[0])
+            # Threshold =< value(V) (lasp_lattice.erl:87-90): term-order cases on the
+            # host (gcounter.threshold_plan), the sum compared on the device
+            from .gcounter import threshold_plan
+            const, t = threshold_plan(term, strict)
+            if const is not None:
+                return const
+            return bool(v.val.threshold_met(t, False)[0])
         if v.rep != "canonical":
             # combinator outputs are only read with the bottom threshold
             if term not in ([],):

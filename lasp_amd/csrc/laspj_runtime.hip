@@ -895,10 +895,15 @@ int laspj_gcounter_apply_increments(laspj_ctx* ctx, laspj_batch* b, const laspj_
         return fail(ctx, LASPJ_E_INVAL, "gcounter_apply_increments: bad argument");
     if (b->kind != LASPJ_KIND_GCOUNTER)
         return fail(ctx, LASPJ_E_KIND, "gcounter_apply_increments: kind");
-    for (uint64_t i = 0; i < n; ++i)
+    for (uint64_t i = 0; i < n; ++i) {
         if (incs[i].replica >= b->replicas || incs[i].actor >= b->elements)
             return fail(ctx, LASPJ_E_RANGE, "gcounter_apply_increments: op %llu out of range",
                         (unsigned long long)i);
+        // riak_dt_gcounter:update({increment, N}, ...) takes N > 0 only (function_clause)
+        if (incs[i].amount == 0)
+            return fail(ctx, LASPJ_E_INVAL, "gcounter_apply_increments: op %llu amount 0",
+                        (unsigned long long)i);
+    }
     if (!n) return LASPJ_OK;
     Guard g(ctx);
     uint64_t need = n * sizeof(laspj_incr);

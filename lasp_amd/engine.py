@@ -530,6 +530,8 @@ class GCounterBatch(_Batch):
         n = len(incs)
         arr = (_lib.Incr * max(n, 1))()
         for k, (rep, actor, amount) in enumerate(incs):
+            if not 0 < amount < (1 << 64):
+                raise ValueError(f"increment amount {amount} is not in 1 .. 2^64-1")
             arr[k].replica, arr[k].actor, arr[k].amount = rep, actor, amount
         check(self.ctx.L.laspj_gcounter_apply_increments(self.ctx.h, self.h, arr, n), self.ctx.h)
         return self

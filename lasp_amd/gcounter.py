@@ -13,6 +13,52 @@ from .codec import Domain
 from .orset import context
 
 
+class FunctionClause(ValueError):
+    """riak_dt_gcounter:update/3 has no clause for the operation (function_clause)."""
+
+
+def increment_amount(op) -> int:
+    """The N of `increment` / `{increment, N}`: riak_dt_gcounter takes an integer N > 0
+    only; counts live in uint64 slots, so N >= 2^64 is refused (OverflowError) rather
+    than truncated."""
+    if op == "increment":
+        return 1
+    if isinstance(op, tuple) and len(op) == 2 and op[0] == "increment" and \
+            isinstance(op[1], int) and not isinstance(op[1], bool) and op[1] > 0:
+        if op[1] >= 1 << 64:
+            raise OverflowError(f"increment {op[1]} does not fit a uint64 count")
+        return op[1]
+    raise FunctionClause(f"riak_dt_gcounter:update({op!r}, ...)")
+
+
+def threshold_plan(threshold, strict: bool):
+    """threshold_met(riak_dt_gcounter, V, T) (lasp_lattice.erl:87-90) is `T =< value(V)`
+    (strict: `T < value(V)`) in Erlang term order, value(V) a non-negative integer.
+    Returns (const, None) when T alone decides it, else (None, t) with `t =< value(V)`
+    to run on the device (t a uint64):
+      * a non-number T (atom, list -- new() = [] included --, tuple, binary ...) is
+        above every number in term order: never met;
+      * integers and floats compare numerically: T =< V iff ceil(T) =< V, and
+        T < V iff floor(T) + 1 =< V;
+      * t =< 0 is always met; t >= 2^64 is never met by a uint64 sum."""
+    import math
+    if isinstance(threshold, bool) or not isinstance(threshold, (int, float)):
+        return False, None
+    if isinstance(threshold, float):
+        if math.isnan(threshold):
+            return False, None
+        if math.isinf(threshold):
+            return threshold < 0, None
+        t = math.floor(threshold) + 1 if strict else math.ceil(threshold)
+    else:
+        t = threshold + 1 if strict else threshold
+    if t <= 0:
+        return True, None
+    if t >= 1 << 64:
+        return False, None
+    return None, t
+
+
 def _batch(dom: Domain, states):
     for s in states:
         for actor, _n in s:
@@ -44,7 +90,7 @@ def value(c) -> int:
 
 def update(op, actor, c):
     """increment | {increment, N}"""
-    n = 1 if op == "increment" else op[1]
+    n = increment_amount(op)
     dom = Domain()
     dom.element_slot(actor)
     b = _batch(dom, [c])

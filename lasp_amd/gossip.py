@@ -8,7 +8,8 @@ and `max` on packed masks is not a join, so a round is
 
   1. all_to_all_single  — rank j receives every rank's copy of object chunk j
                           (the reduce-scatter layout), (n-1)/n * S bytes per GPU;
-  2. reduce_chunks      — one HIP kernel ORs the n copies in HBM (laspj_batch_reduce_chunks);
+  2. reduce_chunks      — one HIP kernel joins the n copies in HBM (laspj_batch_reduce_chunks;
+                          the kind's join: OR for set bitmaps, per-actor max for G-Counters);
   3. all_gather         — the joined chunks are redistributed, (n-1)/n * S bytes per GPU.
 
 Per-GPU xGMI traffic 2(n-1)/n * S, the same as a ring all-reduce, but the all-to-all
@@ -37,7 +38,7 @@ def anti_entropy_round(state: torch.Tensor, recv: torch.Tensor, chunk: torch.Ten
                        sync: Optional[Callable[[], None]] = None) -> None:
     """One anti-entropy round over flat int64 tensors: `state` (S bytes, objects laid
     out chunk-major: rank j owns chunk j), `recv` (S bytes) and `chunk` (S/n bytes).
-    `reduce_fn()` must leave chunk[i] = OR_j recv[j*|chunk| + i]."""
+    `reduce_fn()` must leave chunk[i] = ⊔_j recv[j*|chunk| + i] (the kind's join)."""
     world = dist.get_world_size(group)
     if state.numel() % world or chunk.numel() * world != state.numel() or \
             recv.numel() != state.numel():
@@ -53,7 +54,8 @@ def anti_entropy_round(state: torch.Tensor, recv: torch.Tensor, chunk: torch.Ten
 
 class DeviceAntiEntropy:
     """Device-resident anti-entropy over `objects` OR-Set objects of E element slots:
-    this rank's replicas live in `state`; the reduce is the HIP kernel."""
+    this rank's replicas live in `state`; the reduce is the HIP kernel (OR-Sets only:
+    G-Counters go through DeviceGCounterAntiEntropy)."""
 
     def __init__(self, ctx, objects: int, elements: int, group=None):
         from . import engine
@@ -89,12 +91,19 @@ class DeviceAntiEntropy:
                            self._sync)
 
 
+_SIGN = -(1 << 63)
+
+
 def gcounter_anti_entropy_round(counts: torch.Tensor, group=None) -> None:
-    """One G-Counter anti-entropy round: counts (int64, objects x actors, this rank's
-    replica of every object) become the per-actor max over all ranks = the
-    riak_dt_gcounter join.  Counts must stay below 2^63 (int64 max is the unsigned
-    max there)."""
+    """One G-Counter anti-entropy round: counts (int64 words holding uint64 counts,
+    objects x actors, this rank's replica of every object) become the per-actor max
+    over all ranks = the riak_dt_gcounter join.  torch.distributed's MAX on int64 is a
+    signed max; flipping the sign bit before and after makes it the unsigned max the
+    device join and reduces use (u ≤ v  ⇔  (u ^ 2^63) ≤ (v ^ 2^63) as signed), so
+    counts at or above 2^63 join the same way on both paths."""
+    counts.bitwise_xor_(_SIGN)
     dist.all_reduce(counts, op=dist.ReduceOp.MAX, group=group)
+    counts.bitwise_xor_(_SIGN)
 
 
 class DeviceGCounterAntiEntropy:

@@ -60,10 +60,13 @@ def threshold_met(type_, value, threshold) -> bool:
     riak_dt_gcounter (:87-90): T =< value(V), strict T < value(V)."""
     if type_ == "riak_dt_gcounter":
         from . import gcounter as _gc
-        strict = isinstance(threshold, tuple) and threshold[0] == "strict"
-        t = threshold[1] if strict else threshold
+        strict = isinstance(threshold, tuple) and len(threshold) == 2 and \
+            threshold[0] == "strict"
+        const, t = _gc.threshold_plan(threshold[1] if strict else threshold, strict)
+        if const is not None:
+            return const
         b = _gc._batch(Domain(), [value])
-        return bool(b.threshold_met(t, strict)[0])
+        return bool(b.threshold_met(t, False)[0])
     if isinstance(threshold, tuple) and len(threshold) == 2 and threshold[0] == "strict":
         return is_strict_inflation(type_, threshold[1], value)
     return is_inflation(type_, threshold, value)

@@ -40,7 +40,8 @@ class _GCounter:
         # update_counter(Actor, N, C)
         if op == "increment":
             op = ("increment", 1)
-        if isinstance(op, tuple) and op[0] == "increment" and op[1] > 0:
+        if isinstance(op, tuple) and len(op) == 2 and op[0] == "increment" and \
+                isinstance(op[1], int) and not isinstance(op[1], bool) and op[1] > 0:
             found = otp.orddict_find(actor, c)
             n = 0 if found is None else found[1]
             return ("ok", otp.orddict_store(actor, n + op[1], c))

@@ -12,8 +12,10 @@ def threshold_met(type_, value, threshold) -> bool:
     """threshold_met/3 — lasp_lattice.erl:62-75 (gset / orset) and :87-90 (gcounter)."""
     strict = isinstance(threshold, tuple) and len(threshold) == 2 and threshold[0] == "strict"
     if type_ == "riak_dt_gcounter":
+        # Erlang term order: numbers compare numerically, anything else is above them
+        from .terms import compare
         v = gcounter_value(value)
-        return threshold[1] < v if strict else threshold <= v
+        return compare(threshold[1], v) < 0 if strict else compare(threshold, v) <= 0
     if strict:
         return is_strict_inflation(type_, threshold[1], value)
     return is_inflation(type_, threshold, value)

@@ -47,7 +47,7 @@ def test_binding_covers_header():
 
 
 def test_abi_calls_without_gpu(lib):
-    assert lib.laspj_abi_version() == 1
+    assert lib.laspj_abi_version() == 2
     assert lib.laspj_strerror(_lib.E_SHAPE) == b"shape mismatch"
     n = ctypes.c_int(-1)
     assert lib.laspj_device_count(ctypes.byref(n)) == 0

@@ -60,6 +60,14 @@ WORKER = textwrap.dedent("""
     assert np.array_equal(counts.numpy(), want)
     gcounter_anti_entropy_round(counts)             # idempotent
     assert np.array_equal(counts.numpy(), want)
+    # counts at and above 2^63 (uint64 in int64 words): the join is the UNSIGNED max,
+    # as the device join / reduces compute it
+    big = [g.integers(0, 1 << 64, (objs, actors), dtype=np.uint64) for g in
+           [np.random.default_rng(70 + r) for r in range(world)]]
+    big[0][0, 0], big[1][0, 0] = np.uint64(1 << 63), np.uint64(5)
+    counts = torch.from_numpy(big[rank].view(np.int64).copy())
+    gcounter_anti_entropy_round(counts)
+    assert np.array_equal(counts.numpy().view(np.uint64), np.maximum.reduce(big))
     print("ok", rank)
 """)
 
@@ -83,3 +91,20 @@ def test_anti_entropy_gloo_world2(tmp_path):
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     assert res.stdout.count("ok") == 2
+
+
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (torch.distributed.run
+    as a child process) and each sees WORLD_SIZE=2; a launcher world that disagrees
+    with --gpus is refused with a non-zero status."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert sorted(l for l in res.stdout.splitlines() if "dry-run" in l) == \
+        ["bench dry-run rank 0 of 2", "bench dry-run rank 1 of 2"]
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--dry-run"], capture_output=True, text=True, timeout=60,
+                         env=dict(env, WORLD_SIZE="1", RANK="0"))
+    assert bad.returncode == 2 and "WORLD_SIZE=1 but --gpus 2" in bad.stderr

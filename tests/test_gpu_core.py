@@ -169,3 +169,24 @@ def test_adcounter_orset_kat_on_device():
                 removed.add(x)
     assert st.type_value(ads) == []
     assert [st.type_value(x) for x in ad_ids] == [5] * 5
+
+
+def test_gcounter_increment_amounts_on_device():
+    """{increment, N} reaches the device whole (uint64 amounts: 2^32 + 5 adds 2^32 + 5,
+    not 5) and bad N raise like riak_dt_gcounter's function_clause; thresholds follow
+    term order (lasp_lattice.erl:87-90)."""
+    from lasp_amd import core as dcore
+    from lasp_amd.terms import Atom
+    st = dcore.Store(capacity=16)
+    _, c = st.declare("riak_dt_gcounter")
+    st.update(c, ("increment", (1 << 32) + 5), Atom("a"))
+    st.update(c, "increment", Atom("b"))
+    assert st.type_value(c) == (1 << 32) + 6
+    for bad in (("increment", 0), ("increment", -1), ("increment", 2.0)):
+        with pytest.raises(ValueError):
+            st.update(c, bad, Atom("a"))
+    assert st.type_value(c) == (1 << 32) + 6
+    assert st.read(c, -1) is not None
+    assert st.read(c, (1 << 32) + 6) is not None
+    assert st.read(c, ("strict", (1 << 32) + 6)) is None
+    assert st.read(c, ("strict", (1 << 32) + 5.5)) is not None
