@@ -242,7 +242,8 @@ def main():
         print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
     if args.dry_run:
-        print(f"bench dry-run rank {os.environ.get('RANK', '0')} of {world}", flush=True)
+        sys.stdout.write(f"bench dry-run rank {os.environ.get('RANK', '0')} of {world}\n")
+        sys.stdout.flush()
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

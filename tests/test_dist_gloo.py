@@ -102,8 +102,9 @@ def test_bench_self_launches_ranks():
     res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                           "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
     assert res.returncode == 0, res.stderr[-3000:]
-    assert sorted(l for l in res.stdout.splitlines() if "dry-run" in l) == \
-        ["bench dry-run rank 0 of 2", "bench dry-run rank 1 of 2"]
+    import re
+    assert sorted(re.findall(r"bench dry-run rank \d+ of \d+", res.stdout)) == \
+        ["bench dry-run rank 0 of 2", "bench dry-run rank 1 of 2"], res.stdout
     bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                           "--dry-run"], capture_output=True, text=True, timeout=60,
                          env=dict(env, WORLD_SIZE="1", RANK="0"))
