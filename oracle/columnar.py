@@ -13,7 +13,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "build", "liblaspj_oracle.so")
+# LASPJ_ORACLE_SO selects another build of the same source (the sanitized one, run by
+# tests/test_oracle_pin.py in a child process with libasan preloaded)
+_SO = os.environ.get("LASPJ_ORACLE_SO") or os.path.join(_HERE, "build", "liblaspj_oracle.so")
 _lib = None
 
 u64p = C.POINTER(C.c_uint64)
@@ -51,6 +53,8 @@ def lib():
         L.orc_orset_stats.argtypes = [C.c_void_p, u64p]
         L.orc_orset_is_inflation.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_orset_is_strict.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_orset_union.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_orset_filter_even.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_gset_from_words.argtypes = [C.c_uint32, u64p, i64p]
         L.orc_gset_from_words.restype = C.c_uint32
         L.orc_gset_merge.argtypes = [i64p, C.c_uint32, i64p, C.c_uint32, i64p]
@@ -125,6 +129,23 @@ class ORDict:
         out = ORDict(L.orc_orset_nelem(self.h) + L.orc_orset_nelem(other.h),
                      L.orc_orset_ntok(self.h) + L.orc_orset_ntok(other.h))
         if L.orc_orset_merge(self.h, other.h, out.h) != 0:
+            raise ValueError("capacity")
+        return out
+
+    def union(self, other: "ORDict") -> "ORDict":
+        """the lasp_orset union body (keep-left orddict:merge)"""
+        L = lib()
+        out = ORDict(L.orc_orset_nelem(self.h) + L.orc_orset_nelem(other.h),
+                     L.orc_orset_ntok(self.h) + L.orc_orset_ntok(other.h))
+        if L.orc_orset_union(self.h, other.h, out.h) != 0:
+            raise ValueError("capacity")
+        return out
+
+    def filter_even(self) -> "ORDict":
+        """the filter body with fun(X) -> X rem 2 == 0 end"""
+        L = lib()
+        out = ORDict(max(1, L.orc_orset_nelem(self.h)), max(1, L.orc_orset_ntok(self.h)))
+        if L.orc_orset_filter_even(self.h, out.h) != 0:
             raise ValueError("capacity")
         return out
 
