@@ -51,6 +51,8 @@ extern "C" {
 #define LASPJ_E_RANGE         -6   /* replica / offset / byte range out of bounds        */
 #define LASPJ_E_COMM          -7   /* RCCL communicator error                            */
 #define LASPJ_E_UNSUPPORTED   -8   /* built without the feature                          */
+#define LASPJ_E_FUN           -9   /* a host-evaluated fun failed on a key that is in the
+                                      list (the reference's combinator body crashes)     */
 
 #define LASPJ_KIND_ORSET         1
 #define LASPJ_KIND_GSET          2
@@ -396,6 +398,115 @@ int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_e
 int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict* d,
                          int tag, int vers, const laspj_buf* payload,
                          const laspj_buf* offsets, laspj_buf* status);
+
+/* ------------------------------------------------------------------ list values */
+/* List-faithful values.  The combinator bodies of lasp_core bind lists that are not
+ * orddicts: intersection entries carry `Cx ++ Cy` (lasp_core.erl:546-589,
+ * lasp_lattice.erl:311-312), product entries the fully reversed token pairs of
+ * orset_causal_product (lasp_core.erl:499-533, lasp_lattice.erl:303-308), a map or fold
+ * may reorder or repeat keys (:641-667, :460-486), and the G-Set union binds `L ++ R`
+ * (:620).  Every later re-run binds its new output with Type:merge (lasp_core.erl:300),
+ * i.e. orddict:merge / ordsets:union run as written over those lists: a two-finger
+ * merge that can interleave and duplicate keys and tokens.  A LIST batch holds such
+ * values exactly, in list order, and the entry points below restate every list
+ * operation of the path over them on the device.
+ *
+ * Layout: R replicas, each a list of up to cap_entries entries and cap_tokens tokens:
+ *   entry i of replica r: key item key[r][i]; its token run tok[r][toff[r][i] ..
+ *   toff[r][i+1]) (OR-Set lists; a G-Set list has keys only).
+ * Key item (uint64):  bit 62 clear: element slot e (bits 0-30);
+ *                     bit 62 set:   the pair {X, Y} of element slots x (bits 31-61), y
+ *                                   (bits 0-30) — product keys.
+ * Token item (uint64): bit 63: the {Token, Bool} flag (1 = true);
+ *                     bit 62 clear: token g = 64*e + k, token slot k of element slot e;
+ *                     bit 62 set:   the 2-list [Tx, Ty] of tokens gx (bits 31-61) and
+ *                                   gy (bits 0-30) — product tokens.
+ * Order: term order is given by rank tables the host derives from its dictionaries
+ * (laspj_list_order): krank[e] = rank of element slot e's term, grank[g] = rank of
+ * token g's term (equal terms share a rank); pairs and 2-lists compare element-wise;
+ * a 2-list token sorts below every simple token (lists < binaries).  Comparisons and
+ * equality are by rank, so `==`-equal terms held in different slots are equal.
+ * Entry points that produce a list size their dst themselves: dst (a LIST batch of the
+ * right kind and replica count) is re-allocated when its capacity is too small.  They
+ * synchronise (they read back sizes and argument checks).  LASPJ_E_UNSUPPORTED: a
+ * product of product outputs (nested pairs), which this layout does not express. */
+#define LASPJ_KIND_ORSET_LIST 8
+#define LASPJ_KIND_GSET_LIST  9
+#define LASPJ_LIST_PAIR      (1ull << 62)
+#define LASPJ_LIST_COMPOUND  (1ull << 62)
+#define LASPJ_LIST_REMOVED   (1ull << 63)
+typedef struct laspj_list_order {
+    const laspj_buf* krank;      /* uint32 per element slot                          */
+    uint32_t         nkeys;      /* element slots covered by krank                   */
+    uint32_t         ntokens;    /* tokens covered by grank (64 * element slots)     */
+    const laspj_buf* grank;      /* uint32 per token g; may be NULL for G-Set lists  */
+} laspj_list_order;
+int laspj_list_batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas,
+                            uint32_t cap_entries, uint32_t cap_tokens, laspj_batch** out);
+/* per replica {entries, tokens} as 2 uint32 (synchronous) */
+int laspj_list_counts(laspj_ctx* ctx, const laspj_batch* list, uint32_t* out);
+/* replica `replica` := the list (keys[n], toff[n+1] with toff[0] = 0, toks[toff[n]]) */
+int laspj_list_upload(laspj_ctx* ctx, laspj_batch* list, uint64_t replica, uint32_t n,
+                      const uint64_t* keys, const uint32_t* toff, const uint64_t* toks);
+/* the list of replica `replica` (sizes from laspj_list_counts; toff gets n+1 words) */
+int laspj_list_download(laspj_ctx* ctx, const laspj_batch* list, uint64_t replica,
+                        uint64_t* keys, uint32_t* toff, uint64_t* toks);
+/* a canonical OR-Set / G-Set batch as lists: elements in term order (elem_order: the
+ * nslots element slots in term order, uint32), tokens of element e in term order
+ * (tok_order: 64 uint8 per element slot, token slots ascending in term order, 0xFF
+ * after the last; NULL for G-Sets) */
+int laspj_list_from_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                        const laspj_buf* elem_order, uint32_t nslots,
+                        const laspj_buf* tok_order);
+/* dst := Type:merge(a, b) — lasp_orset:merge/2 (lasp_orset.erl:128-134: nested
+ * orddict:merge, inner BoolA or BoolB) on OR-Set lists, lasp_gset:merge/2
+ * (lasp_gset.erl:99-101: ordsets:union, OTP 17 clauses incl. the argument switch) on
+ * G-Set lists; run as written on any list */
+int laspj_list_merge(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b, const laspj_list_order* ord);
+/* out[i] = (a[i] =:= b[i]) as one byte — the `case Value0 of Value` match of bind/3
+ * (lasp_core.erl:294-296) */
+int laspj_list_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                     const laspj_list_order* ord, laspj_buf* out);
+/* is_inflation / is_strict_inflation of prev -> cur (lasp_lattice.erl:137-161, 212-253,
+ * 277-285: lists:keyfind first match, ids_inflated, order-sensitive =/=, length/1;
+ * G-Sets: sets:is_subset, usort =/=); prev has R replicas or 1 (broadcast) */
+int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                         int strict, const laspj_list_order* ord, laspj_buf* out);
+/* value/1 of OR-Set lists (lasp_orset.erl:67-73): the keys of entries with a {_, false}
+ * token, in list order, as a G-Set list dst */
+int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
+/* union body (lasp_core.erl:616-620): OR-Set lists orddict:merge keeping the left
+ * tokens; G-Set lists `L ++ R` */
+int laspj_list_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                     const laspj_batch* r, const laspj_list_order* ord);
+/* intersection body (lasp_core.erl:546-589): per entry of l in order, lists:keyfind in r
+ * (first match) -> {X, Cx ++ Cy}; G-Set lists: lists:member -> X */
+int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                            const laspj_batch* r, const laspj_list_order* ord);
+/* product body (lasp_core.erl:499-533): l-major pairs {X, Y}; OR-Set tokens
+ * orset_causal_product(Cx, Cy) (both runs reversed, [Tx, Ty], Dx orelse Dy) */
+int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                       const laspj_batch* r);
+/* map / filter / fold bodies (lasp_core.erl:641-667, 681-712, 460-486) over a list in
+ * list order.  The fun runs on the host once per key (an Erlang fun); its results come
+ * as tables indexed by the entry's element slot (per_entry = 0; simple keys only) or by
+ * entry position (per_entry = 1):
+ *   map:    keys[idx] = the output key item;
+ *   filter: keep[idx] = 1 to keep the entry (tombstoned entries are kept like others);
+ *   fold:   the output key items of entry idx are keys[off[idx] .. off[idx+1]), each
+ *           with a copy of the entry's tokens.
+ * A fun that raised on a key is marked in its table entry (map / fold key item
+ * ~0; filter keep = 2): if that key is in the list, the call fails with LASPJ_E_FUN
+ * (the reference's body would crash there); entries for keys not in the list are never
+ * looked at. */
+int laspj_list_map(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                   const laspj_buf* keys, uint32_t nidx, int per_entry);
+int laspj_list_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* keep, uint32_t nidx, int per_entry);
+int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                    const laspj_buf* off, const laspj_buf* keys, uint32_t nidx,
+                    int per_entry);
 
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);

@@ -16,11 +16,15 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "laspj.h")
 
 ABI_VERSION = 2
 OK = 0
-E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED = (
-    -1, -2, -3, -4, -5, -6, -7, -8)
+E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED, E_FUN = (
+    -1, -2, -3, -4, -5, -6, -7, -8, -9)
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 KIND_GCOUNTER = 6
 KIND_ORSET_PRODUCT_WIDE = 7
+KIND_ORSET_LIST, KIND_GSET_LIST = 8, 9
+LIST_PAIR = 1 << 62          # key item: {X, Y} of element slots (bits 31-61, 0-30)
+LIST_COMPOUND = 1 << 62      # token item: [Tx, Ty] of tokens (bits 31-61, 0-30)
+LIST_REMOVED = 1 << 63       # token item: the {Token, true} flag
 # from_binary statuses (laspj_orset_etf_read)
 DEC_OK, DEC_INVALID_BINARY, DEC_UNSUPPORTED_VERSION, DEC_MALFORMED, DEC_UNKNOWN_TERM, \
     DEC_UNREPRESENTABLE = 0, 1, 2, 3, 4, 5
@@ -54,6 +58,11 @@ class BatchInfo(C.Structure):
 class Op(C.Structure):
     _fields_ = [("replica", C.c_uint64), ("element", C.c_uint32), ("kind", C.c_uint8),
                 ("slot", C.c_uint8), ("flags", C.c_uint8), ("pad", C.c_uint8)]
+
+
+class ListOrder(C.Structure):
+    _fields_ = [("krank", C.c_void_p), ("nkeys", C.c_uint32), ("ntokens", C.c_uint32),
+                ("grank", C.c_void_p)]
 
 
 class Incr(C.Structure):
@@ -137,6 +146,21 @@ SIGNATURES = {
     "laspj_gset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
     "laspj_gset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
     "laspj_orset_etf_read": (i, [vp, vp, vp, i, i, vp, vp, vp]),
+    "laspj_list_batch_create": (i, [vp, C.c_int32, u64, u32, u32, vpp]),
+    "laspj_list_counts": (i, [vp, vp, vp]),
+    "laspj_list_upload": (i, [vp, vp, u64, u32, vp, vp, vp]),
+    "laspj_list_download": (i, [vp, vp, u64, vp, vp, vp]),
+    "laspj_list_from_set": (i, [vp, vp, vp, vp, u32, vp]),
+    "laspj_list_merge": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
+    "laspj_list_equal": (i, [vp, vp, vp, C.POINTER(ListOrder), vp]),
+    "laspj_list_inflation": (i, [vp, vp, vp, i, C.POINTER(ListOrder), vp]),
+    "laspj_list_value": (i, [vp, vp, vp]),
+    "laspj_list_union": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
+    "laspj_list_intersection": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
+    "laspj_list_product": (i, [vp, vp, vp, vp]),
+    "laspj_list_map": (i, [vp, vp, vp, vp, u32, i]),
+    "laspj_list_filter": (i, [vp, vp, vp, vp, u32, i]),
+    "laspj_list_fold": (i, [vp, vp, vp, vp, vp, u32, i]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

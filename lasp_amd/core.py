@@ -7,23 +7,25 @@ Mirrors src/lasp_core.erl:
   map/6 :641-667   filter/6 :681-712   fold/6 :460-486
   lasp_process:process/3 (src/lasp_process.erl:61-95) — the re-run-on-every-change loop,
   run synchronously: after each write, every process whose input is now a strict
-  inflation of the value it last read (a device inflation kernel) re-runs its body on
-  the device and binds the result.
+  inflation of the value it last read re-runs its body on the device and binds the
+  result.
 
 All OR-Set variables of a Store share one element/token dictionary (codec.Domain), as
 do all G-Set variables, so joins, predicates and combinators never re-map slots.
-A variable holds one of
-  canonical   ORSetBatch / GSetBatch over the store dictionary,
-  concat      the intersection body's {X, Cx ++ Cy} list (ConcatBatch),
-  product     the product body's list (ORSetProductBatch / GSetProductBatch),
-  seq         the map / fold body's list (a batch over SeqOutput slots, list order).
-bind(Var, V): if Var still holds new(), the reference's merge(new(), V) is V itself
-(orddict:merge([], D) = D, ordsets:union([], S) = S), so V is stored as is; otherwise
-Var and V must have the same representation and are joined slot-wise on the device.
-For canonical values that is exactly lasp_orset:merge/2; for seq values with
-non-decreasing keys (map X -> 2X, fold X -> [X,X,X]) it equals orddict:merge's
-positional pairing; for concat / product values the reference's two-finger merge of
-unsorted token lists is not reproduced (parity unpinned there).
+A variable holds one of two representations:
+  canonical   an OR-Set / G-Set batch (16-byte {p, r} cells / bit words): the value is
+              an orddict / ordset, and merge, equal and inflation are bit operations;
+  list        a LIST batch (engine.ListBatch): the value exactly as a list — entries in
+              list order, token runs in list order — for the non-canonical values the
+              combinator bodies bind (intersection `Cx ++ Cy`, reversed product token
+              pairs, reordered / repeated map and fold keys, the G-Set `L ++ R`).
+A bind whose sides are both canonical uses the cell kernels; otherwise both sides are
+lists (a canonical side converted on the device, laspj_list_from_set) and the bind is
+the reference's own sequence — `Value0 =:= Value` (laspj_list_equal), Type:merge
+(laspj_list_merge: orddict:merge / ordsets:union as written), is_inflation
+(laspj_list_inflation) — so every re-run's output is merged exactly as lasp_core
+merges it, duplicates and interleavings included.  Values are never updated in place
+(every merge writes a new batch), so processes keep references to what they read.
 """
 
 from __future__ import annotations
@@ -33,26 +35,40 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 from . import _lib, engine
-from .codec import Domain, NonCanonical, SeqOutput, decode_concat, decode_gset_product, \
-    decode_product
+from . import lists as L
+from .codec import CapacityError, Domain, NonCanonical, _check_canonical_gset, \
+    _check_canonical_orset
 from .orset import context
-from .terms import hkey
 
 
 class Unsupported(Exception):
-    """A type that is not on the device path (the store holds lasp_orset / lasp_gset)."""
+    """A value or type this device store does not represent (documented in DESIGN.md)."""
+
+
+class BodyCrash(Exception):
+    """A combinator body raised (its fun failed on a key of the input): the reference's
+    process crashes and binds nothing."""
 
 
 class _Var:
-    __slots__ = ("type", "rep", "val", "seq", "empty", "waiting")
+    __slots__ = ("type", "rep", "val", "empty", "waiting", "pairs", "as_list")
 
     def __init__(self, type_, val):
         self.type = type_
         self.rep = "canonical"
-        self.val = val            # device batch
-        self.seq: Optional[SeqOutput] = None
-        self.empty = True         # still new()
+        self.val = val            # device batch (canonical) or engine.ListBatch (list)
+        self.empty = True         # still new() = []
         self.waiting: List = []
+        self.pairs = False        # list keys are product pairs {X, Y}
+        self.as_list = None       # (value object, its list form) cache
+
+
+class _Value:
+    """A device value about to be bound, or last read by a process."""
+    __slots__ = ("rep", "batch", "pairs", "empty")
+
+    def __init__(self, rep, batch, pairs=False, empty=None):
+        self.rep, self.batch, self.pairs, self.empty = rep, batch, pairs, empty
 
 
 class Store:
@@ -62,6 +78,8 @@ class Store:
         self.odom = Domain(element_capacity=capacity)
         self.gdom = Domain(element_capacity=capacity)
         self.cdom = Domain(element_capacity=capacity)      # G-Counter actors
+        self.ospace = L.ListSpace(self.ctx, self.odom, tokens=True)
+        self.gspace = L.ListSpace(self.ctx, self.gdom, tokens=False)
         self.vars: Dict = {}
         self.procs: List[dict] = []
         self._n = 0
@@ -78,32 +96,80 @@ class Store:
             return self.ctx.gcounter_batch(1, self.cap)
         raise Unsupported(type_)
 
-    def _encode(self, type_, term):
-        b = self._new_batch(type_)
-        if type_ == "lasp_orset_gbtree":
-            from .orset_gbtree import to_orddict
-            b.upload(self.odom.encode_orset([to_orddict(term)], self.cap))
-        elif type_ == "lasp_orset":
-            b.upload(self.odom.encode_orset([term], self.cap))
-        elif type_ == "lasp_gset":
-            b.upload(self.gdom.encode_gset([term], self.cap))
-        else:
+    def _dom(self, type_) -> Domain:
+        return self.gdom if type_ == "lasp_gset" else self.odom
+
+    def _space(self, type_) -> L.ListSpace:
+        return self.gspace if type_ == "lasp_gset" else self.ospace
+
+    def _encode(self, type_, term, pairs: bool = False) -> _Value:
+        """A host term as a device value: canonical when it is an orddict / ordset (and
+        the variable holds no product pairs), else a list."""
+        if type_ == "riak_dt_gcounter":
+            b = self._new_batch(type_)
             host = np.zeros((1, self.cap), dtype=np.uint64)
             for actor, n in term:
                 host[0, self.cdom.element_slot(actor)] = n
             b.upload(host)
-        return b
+            return _Value("canonical", b, empty=not term)
+        if type_ == "lasp_orset_gbtree":
+            from .orset_gbtree import to_orddict
+            b = self._new_batch(type_)
+            b.upload(self.odom.encode_orset([to_orddict(term)], self.cap))
+            return _Value("canonical", b)
+        if not pairs:
+            try:
+                if type_ == "lasp_orset":
+                    _check_canonical_orset(term)
+                    ok = all(isinstance(f, bool) for _e, ts in term for _t, f in ts)
+                else:
+                    _check_canonical_gset(term)
+                    ok = True
+            except (NonCanonical, TypeError, ValueError):
+                ok = False
+            if ok:
+                b = self._new_batch(type_)
+                if type_ == "lasp_orset":
+                    b.upload(self.odom.encode_orset([term], self.cap))
+                else:
+                    b.upload(self.gdom.encode_gset([term], self.cap))
+                return _Value("canonical", b, empty=not term)
+        keys, toff, toks = L.encode(self._dom(type_), term, type_ == "lasp_gset", pairs)
+        kind = _lib.KIND_GSET_LIST if type_ == "lasp_gset" else _lib.KIND_ORSET_LIST
+        lb = engine.ListBatch(self.ctx, kind).upload(keys, toff, toks)
+        return _Value("list", lb, pairs, empty=not term)
 
-    def _copy(self, b):
-        """Device copy of a batch (x ⊔ x = x for canonical kinds, OR otherwise)."""
-        out = type(b).__new__(type(b))
-        if isinstance(b, engine._ProductBatch):
-            engine._ProductBatch.__init__(out, self.ctx, b.replicas, b.elements, b.elements_r)
-            out.kind = b.kind
-        else:
-            engine._Batch.__init__(out, self.ctx, b.replicas, b.elements)
-        _or_into(self.ctx, out, b, b)
-        return out
+    def _to_list(self, type_, batch):
+        """A canonical batch as a list (laspj_list_from_set)."""
+        eb, n, tb = self._space(type_).set_orders(batch.elements)
+        return engine.ListBatch.from_set(batch, eb, n, tb)
+
+    def _var_list(self, v: _Var):
+        if v.rep == "list":
+            return v.val
+        c = v.as_list
+        if c is None or c[0] is not v.val:
+            c = v.as_list = (v.val, self._to_list(v.type, v.val))
+        return c[1]
+
+    def _value_list(self, type_, dv: _Value):
+        return dv.batch if dv.rep == "list" else self._to_list(type_, dv.batch)
+
+    def _order(self, type_):
+        return self._space(type_).order()
+
+    def _is_empty(self, dv: _Value, type_) -> bool:
+        if dv.empty is not None:
+            return dv.empty
+        if dv.rep == "list":
+            return int(dv.batch.counts()[0][0]) == 0
+        return bool(dv.batch.equal(self._bottom(type_))[0])
+
+    def _bottom(self, type_):
+        b = self._bottoms.get(type_)
+        if b is None:
+            b = self._bottoms[type_] = self._new_batch(type_)
+        return b
 
     # ---------------------------------------------------------------- declare / bind
     def declare(self, type_, id_=None):
@@ -117,96 +183,69 @@ class Store:
 
     def bind(self, id_, value):
         """bind/3 — lasp_core.erl:291-312.  `value` is a host term or a device value
-        produced by a combinator body (`_DeviceValue`)."""
+        produced by a combinator body (`_Value`)."""
         v = self.vars[id_]
         try:
-            dv = value if isinstance(value, _DeviceValue) else \
-                _DeviceValue("canonical", self._encode(v.type, value))
+            dv = value if isinstance(value, _Value) else self._encode(v.type, value, v.pairs)
             self._bind_device(id_, v, dv)
-        except (NonCanonical, _lib.LaspjError, ValueError):
+        except (NonCanonical, CapacityError, ValueError, TypeError):
             pass        # merge may throw for invalid values; bind swallows it (:308-311)
+        except _lib.LaspjError as e:
+            if e.status in (_lib.E_UNSUPPORTED, _lib.E_NOMEM, _lib.E_DEVICE):
+                raise Unsupported(str(e)) if e.status == _lib.E_UNSUPPORTED else e
         return ("ok", (id_, v.type, value))
 
-    def _is_bottom(self, v: _Var, dv: "_DeviceValue") -> bool:
-        if dv.rep != "canonical":
-            return False
-        return bool(dv.batch.equal(self._bottom(v.type))[0])
-
-    def _bottom(self, type_):
-        b = self._bottoms.get(type_)
-        if b is None:
-            b = self._bottoms[type_] = self._new_batch(type_)
-        return b
-
-    def _bind_device(self, id_, v: _Var, dv: "_DeviceValue"):
+    def _bind_device(self, id_, v: _Var, dv: _Value):
+        t = v.type
         if v.empty:
-            if self._is_bottom(v, dv):       # Value0 =:= Value = new(): no-op
+            # Value0 = new() = []: `[] =:= Value` is a no-op; otherwise merge([], V) = V
+            # (orddict:merge([], D) = D, ordsets:union([], S) = S) and it inflates []
+            if self._is_empty(dv, t):
                 return
-            # merge(new(), V) = V; is_inflation(new(), V) holds
-            v.rep, v.seq, v.val = dv.rep, dv.seq, self._copy(dv.batch)
+            v.rep, v.val, v.pairs = dv.rep, dv.batch, dv.pairs
             v.empty = False
             self._written(id_, v)
             return
-        if v.rep != dv.rep:
-            raise ValueError("representation mismatch (merge would throw)")
-        new = dv.batch
-        if v.rep == "seq" and v.seq.keys != dv.seq.keys:
-            new = self._align_seq(v, dv)
-        # Value0 =:= Value: no-op (lasp_core.erl:294-296)
-        if v.rep == "canonical" and bool(v.val.equal(new)[0]):
-            return
-        merged = self._copy(v.val)
-        _or_into(self.ctx, merged, merged, new)
-        if v.rep == "canonical":
-            if not bool(merged.is_inflation_of(v.val)[0]):     # lasp_core.erl:301
+        if v.rep == "canonical" and dv.rep == "canonical":
+            new = dv.batch
+            if bool(v.val.equal(new)[0]):                        # lasp_core.erl:294-296
                 return
-        v.val = merged
+            merged = _new_like(self.ctx, v.val)
+            _or_into(self.ctx, merged, v.val, new)
+            if not bool(merged.is_inflation_of(v.val)[0]):       # lasp_core.erl:301
+                return
+            v.val = merged
+            self._written(id_, v)
+            return
+        if t not in ("lasp_orset", "lasp_gset"):
+            raise Unsupported(f"list values of {t}")
+        if dv.pairs != v.pairs and not self._is_empty(dv, t):
+            # product pairs meet plain keys: the rank tables do not order the two
+            raise Unsupported("a product output and plain keys in one variable")
+        old, new = self._var_list(v), self._value_list(t, dv)
+        order = self._order(t)
+        if bool(old.equal(new, order)[0]):                       # Value0 =:= Value
+            return
+        merged = old.merge(new, order)                           # Type:merge(Value0, Value)
+        if not bool(merged.is_inflation_of(old, order)[0]):      # is_inflation(Value0, Merged)
+            return
+        v.rep, v.val = "list", merged
         self._written(id_, v)
-
-    def _align_seq(self, v: _Var, dv: "_DeviceValue"):
-        """Re-run outputs grow with the input dictionary: lay the new list out on the
-        variable's slots extended by the new slots (keys and causality source match)."""
-        old_keys = [(hkey(k) if s != 0xFFFFFFFF else None, s) for k, s in zip(v.seq.keys, v.seq.src)]
-        new_keys = [(hkey(k) if s != 0xFFFFFFFF else None, s) for k, s in zip(dv.seq.keys, dv.seq.src)]
-        # the k-th occurrence of (key, source slot) in the old layout moves to the k-th
-        # occurrence in the new one; slots only the new layout has start empty
-        pos = {}
-        for o, k in enumerate(new_keys):
-            pos.setdefault(k, []).append(o)
-        idx = np.full((len(new_keys),), 0xFFFFFFFF, np.uint32)
-        seen = {}
-        for o, k in enumerate(old_keys):
-            j = seen.get(k, 0)
-            if j >= len(pos.get(k, [])):
-                raise ValueError("map/fold layout changed incompatibly")
-            idx[pos[k][j]] = o
-            seen[k] = j + 1
-        widened = self._batch_like(v.type, len(new_keys))
-        widened.gather(v.val, idx)
-        v.val, v.seq = widened, dv.seq
-        return dv.batch
-
-    def _batch_like(self, type_, n):
-        return self.ctx.orset_batch(1, max(1, n)) if type_ == "lasp_orset" else \
-            self.ctx.gset_batch(1, max(1, n))
 
     def _written(self, id_, v: _Var):
         # write/4 + reply_to_all/3 (lasp_core.erl:839-844, 765-825)
-        still = []
-        for th in v.waiting:
-            if not self._threshold_met(v, th):
-                still.append(th)
-        v.waiting = still
+        v.waiting = [th for th in v.waiting if not self._threshold_met(v, th)]
         self._propagate()
 
     # ---------------------------------------------------------------- update / read
     def update(self, id_, op, actor):
-        """update/4 — lasp_core.erl:283-287: Type:update on a copy, then bind."""
+        """update/4 — lasp_core.erl:283-287: Type:update on the value, then bind."""
         v = self.vars[id_]
         if v.rep != "canonical":
-            raise ValueError("badmatch: update on a combinator output")
+            raise Unsupported("update/3 on a combinator output (a list value)")
         from . import orset as _o
-        cur = self._copy(v.val)
+        cur = _new_like(self.ctx, v.val)
+        _or_into(self.ctx, cur, v.val, v.val)
         if v.type == "riak_dt_gcounter":
             from .gcounter import increment_amount
             n = increment_amount(op)
@@ -230,7 +269,7 @@ class Store:
         else:
             elems = [op[1]] if op[0] == "add" else list(op[1])
             cur.apply_ops([(0, self.gdom.element_slot(e), _lib.OP_ADD, 0, 1) for e in elems])
-        self._bind_device(id_, v, _DeviceValue("canonical", cur))
+        self._bind_device(id_, v, _Value("canonical", cur, empty=False))
         return ("ok", (id_, v.type, None))
 
     def read(self, id_, threshold=("strict", None)):
@@ -249,7 +288,8 @@ class Store:
 
     def _threshold_met(self, v: _Var, threshold) -> bool:
         """lasp_lattice:threshold_met/3 on the device (lasp_lattice.erl:62-75)."""
-        strict = isinstance(threshold, tuple) and threshold[0] == "strict"
+        strict = isinstance(threshold, tuple) and len(threshold) == 2 and \
+            threshold[0] == "strict"
         term = threshold[1] if strict else threshold
         if v.type == "riak_dt_gcounter":
             # Threshold =< value(V) (lasp_lattice.erl:87-90): term-order cases on the
@@ -259,33 +299,33 @@ class Store:
             if const is not None:
                 return const
             return bool(v.val.threshold_met(t, False)[0])
-        if v.rep != "canonical":
-            # combinator outputs are only read with the bottom threshold
-            if term not in ([],):
-                raise ValueError("threshold reads on combinator outputs take new()")
-            return (not strict) or not v.empty
-        t = self._encode(v.type, term)
-        return bool(v.val.is_inflation_of(t, strict=strict)[0])
+        return self._inflates(v, self._encode(v.type, term, v.pairs), strict)
+
+    def _inflates(self, v: _Var, prev: _Value, strict: bool) -> bool:
+        """is_inflation(prev, V) / is_strict_inflation(prev, V) for V = v's value."""
+        if v.rep == "canonical" and prev.rep == "canonical":
+            return bool(v.val.is_inflation_of(prev.batch, strict=strict)[0])
+        if v.type not in ("lasp_orset", "lasp_gset"):
+            raise Unsupported(f"list values of {v.type}")
+        cur = self._var_list(v)
+        return bool(cur.is_inflation_of(self._value_list(v.type, prev), self._order(v.type),
+                                        strict=strict)[0])
 
     def value(self, id_):
         """The variable's value as the reference would hold it (decoded from HBM)."""
         v = self.vars[id_]
+        if v.rep == "list":
+            keys, toff, toks = v.val.download()
+            return L.decode(self._dom(v.type), keys, toff, toks, v.type == "lasp_gset")
         cells = v.val.download()[0]
         if v.type == "riak_dt_gcounter":
             return [(self.cdom.elements.terms[int(a)], int(cells[int(a)]))
                     for a in self.cdom.elements.order() if int(cells[int(a)])]
-        if v.rep == "canonical":
-            if v.type == "lasp_orset_gbtree":
-                from .orset_gbtree import from_orddict
-                return from_orddict(self.odom.decode_orset(cells))
-            return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
-                self.gdom.decode_gset(cells)
-        if v.rep == "concat":
-            return decode_concat(self.odom, cells)
-        if v.rep == "product":
-            return decode_product(self.odom, self.odom, cells) if v.type == "lasp_orset" \
-                else decode_gset_product(self.gdom, self.gdom, cells)
-        return v.seq.decode_orset(cells) if v.type == "lasp_orset" else v.seq.decode_bits(cells)
+        if v.type == "lasp_orset_gbtree":
+            from .orset_gbtree import from_orddict
+            return from_orddict(self.odom.decode_orset(cells))
+        return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
+            self.gdom.decode_gset(cells)
 
     def type_value(self, id_):
         """Type:value(Value) of the variable (value/1 kernel + decode)."""
@@ -294,25 +334,17 @@ class Store:
             return int(v.val.values()[0])
         if v.type == "lasp_gset":
             return self.value(id_)
-        bits = v.val.value_bits()[0]
-        if v.rep == "canonical":
-            return self.odom.decode_value_bits(bits)
-        if v.rep == "concat":
-            return _concat_visible(self.odom, bits)
-        if v.rep == "product":
-            ER = v.val.elements_r
-            return [(self.odom.elements.terms[x], self.odom.elements.terms[y])
-                    for x in self.odom.elements.order() for y in self.odom.elements.order()
-                    if (int(bits[(int(x) * ER + int(y)) >> 6]) >> ((int(x) * ER + int(y)) & 63)) & 1]
-        return v.seq.decode_bits(bits)
+        if v.rep == "list":
+            keys, _o, _t = v.val.value().download()
+            return [L._key_term(self.odom, int(k)) for k in keys]
+        return self.odom.decode_value_bits(v.val.value_bits()[0])
 
     # ---------------------------------------------------------------- processes
     def _start(self, inputs, body):
         for i in inputs:
-            if self.vars[i].type == "lasp_orset_gbtree":
+            if self.vars[i].type not in ("lasp_orset", "lasp_gset"):
                 # lasp_core's combinator bodies match the orddict shape and the
-                # lasp_orset / lasp_gset atoms only (lasp_core.erl:460-712): a gbtree
-                # input crashes the process in the reference
+                # lasp_orset / lasp_gset atoms only (lasp_core.erl:460-712)
                 raise Unsupported("combinators take lasp_orset / lasp_gset inputs")
         proc = {"inputs": list(inputs), "seen": {i: None for i in inputs}, "body": body}
         self.procs.append(proc)
@@ -328,23 +360,28 @@ class Store:
             changed = True
             while changed:
                 changed = False
-                for proc in self.procs:
+                for proc in list(self.procs):
                     for i in proc["inputs"]:
+                        if proc not in self.procs:
+                            break
                         v = self.vars[i]
                         last = proc["seen"][i]
                         if v.empty:
                             continue
-                        if last is None:
-                            # {strict, new()}: a non-empty value is a strict inflation
-                            fire = True
-                        elif v.rep == "canonical":
-                            fire = bool(v.val.is_inflation_of(last, strict=True)[0])
-                        else:
-                            fire = False
-                        if fire:
-                            proc["seen"][i] = self._copy(v.val)
+                        # {strict, new()}: a non-empty value is a strict inflation of []
+                        if last is not None and (last.batch is v.val or
+                                                 not self._inflates(v, last, strict=True)):
+                            # unchanged since read: one re-run per write (a list with
+                            # repeated keys can strictly inflate itself, on which the
+                            # reference's reader re-fires forever)
+                            continue
+                        proc["seen"][i] = _Value(v.rep, v.val, v.pairs, empty=False)
+                        try:
                             proc["body"](proc["seen"])
-                            changed = True
+                        except BodyCrash:
+                            # the process dies: nothing bound, no more re-runs
+                            self.procs.remove(proc)
+                        changed = True
         finally:
             self._depth -= 1
 
@@ -352,64 +389,122 @@ class Store:
         if dv is not None:
             self.bind(out_id, dv)
 
+    def _lists(self, t, *vals):
+        return [self._value_list(t, x) for x in vals]
+
+    @staticmethod
+    def _run(fn, *args):
+        try:
+            return fn(*args)
+        except _lib.LaspjError as e:
+            if e.status == _lib.E_FUN:
+                raise BodyCrash(str(e)) from e
+            raise
+
     def union(self, l, r, out):
         t = self.vars[l].type
 
         def body(seen):
-            if seen[l] is None or seen[r] is None:
+            a, b = seen[l], seen[r]
+            if a is None or b is None:
                 return
-            res = self._new_batch(t)
-            if t == "lasp_orset":
-                res.union(seen[l], seen[r])
-            else:
-                res.union(seen[l], seen[r])
-            self._bind_out(out, _DeviceValue("canonical", res))
+            if t == "lasp_orset" and a.rep == b.rep == "canonical":
+                res = self._new_batch(t).union(a.batch, b.batch)       # keep-left merge
+                return self._bind_out(out, _Value("canonical", res))
+            _pairs_guard(a, b)
+            la, lb = self._lists(t, a, b)
+            # OR-Set: orddict:merge keep-left; G-Set: LValue ++ RValue
+            self._bind_out(out, _Value("list", la.union(lb, self._order(t)), a.pairs))
         return self._start([l, r], body)
 
     def intersection(self, l, r, out):
         t = self.vars[l].type
 
         def body(seen):
-            if seen[l] is None or seen[r] is None:
+            a, b = seen[l], seen[r]
+            if a is None or b is None:
                 return
-            if t == "lasp_orset":
-                self._bind_out(out, _DeviceValue("concat", seen[l].intersection(seen[r])))
-            else:
-                res = self._new_batch(t).intersection(seen[l], seen[r])
-                self._bind_out(out, _DeviceValue("canonical", res))
+            self._gset_tuples_guard(t, a, b)
+            if t == "lasp_gset" and a.rep == b.rep == "canonical":
+                res = self._new_batch(t).intersection(a.batch, b.batch)
+                return self._bind_out(out, _Value("canonical", res))
+            _pairs_guard(a, b)
+            la, lb = self._lists(t, a, b)
+            self._bind_out(out, _Value("list", la.intersection(lb, self._order(t)), a.pairs))
         return self._start([l, r], body)
 
     def product(self, l, r, out):
+        t = self.vars[l].type
+
         def body(seen):
-            if seen[l] is None or seen[r] is None:
+            a, b = seen[l], seen[r]
+            if a is None or b is None:
                 return
-            self._bind_out(out, _DeviceValue("product", seen[l].product(seen[r])))
+            self._gset_tuples_guard(t, a, b)
+            la, lb = self._lists(t, a, b)
+            self._bind_out(out, _Value("list", la.product(lb), True))
         return self._start([l, r], body)
 
     def filter(self, i, fun: Callable, out):
         t = self.vars[i].type
+        fc = L.FunCache(fun)
+        dom = self._dom(t)
 
         def body(seen):
-            dom = self.odom if t == "lasp_orset" else self.gdom
-            res = self._new_batch(t).filter(seen[i], dom.keep_bits(fun, self.cap))
-            self._bind_out(out, _DeviceValue("canonical", res))
+            a = seen[i]
+            if a.rep == "canonical":
+                keep = L.filter_table(fc, dom.elements.terms, t == "lasp_gset")
+                if not (keep == 2).any():
+                    bits = np.zeros(((self.cap + 63) // 64,), dtype=np.uint64)
+                    for e in np.nonzero(keep == 1)[0]:
+                        bits[e >> 6] |= np.uint64(1) << np.uint64(e & 63)
+                    res = self._new_batch(t).filter(a.batch, bits)
+                    return self._bind_out(out, _Value("canonical", res))
+            la = self._value_list(t, a)
+            terms, per_entry = L.table_terms(dom, la, a.pairs)
+            keep = L.filter_table(fc, terms, t == "lasp_gset")
+            self._bind_out(out, _Value("list", self._run(la.filter, keep, per_entry), a.pairs))
         return self._start([i], body)
 
     def map(self, i, fun: Callable, out):
-        return self._seq_proc(i, out, lambda dom: SeqOutput.map(dom, fun))
-
-    def fold(self, i, fun: Callable, out):
-        return self._seq_proc(i, out, lambda dom: SeqOutput.fold(dom, fun))
-
-    def _seq_proc(self, i, out, layout):
         t = self.vars[i].type
+        fc = L.FunCache(fun)
+        dom = self._dom(t)
 
         def body(seen):
-            dom = self.odom if t == "lasp_orset" else self.gdom
-            so = layout(dom)
-            res = self._batch_like(t, so.size).gather(seen[i], so.index())
-            self._bind_out(out, _DeviceValue("seq", res, so))
+            la = self._value_list(t, seen[i])
+            terms, per_entry = L.table_terms(dom, la, seen[i].pairs)
+            keys = L.map_table(dom, fc, terms, t == "lasp_gset")
+            self._bind_out(out, _Value("list", self._run(la.map, keys, per_entry)))
         return self._start([i], body)
+
+    def fold(self, i, fun: Callable, out):
+        t = self.vars[i].type
+        fc = L.FunCache(fun)
+        dom = self._dom(t)
+
+        def body(seen):
+            la = self._value_list(t, seen[i])
+            terms, per_entry = L.table_terms(dom, la, seen[i].pairs)
+            off, keys = L.fold_table(dom, fc, terms, t == "lasp_gset")
+            self._bind_out(out, _Value("list", self._run(la.fold, off, keys, per_entry)))
+        return self._start([i], body)
+
+    def _gset_tuples_guard(self, t, a: _Value, b: _Value):
+        """lasp_core's intersection / product bodies match `{X, Causality}` first
+        (lasp_core.erl:513-521, 560-576): a G-Set holding 2-tuples goes down the OR-Set
+        branch (keyfind and `++` on the tuples' second elements), which this store does
+        not reproduce."""
+        if t != "lasp_gset":
+            return
+        if a.pairs or b.pairs or any(isinstance(x, tuple) and len(x) == 2
+                                     for x in self.gdom.elements.terms):
+            raise Unsupported("G-Set intersection / product over 2-tuple elements")
+
+
+def _pairs_guard(a: _Value, b: _Value):
+    if a.pairs != b.pairs:
+        raise Unsupported("a product output and plain keys in one combinator")
 
 
 def _type_new(type_):
@@ -420,23 +515,16 @@ def _type_new(type_):
     return []
 
 
-class _DeviceValue:
-    __slots__ = ("rep", "batch", "seq")
-
-    def __init__(self, rep, batch, seq=None):
-        self.rep, self.batch, self.seq = rep, batch, seq
+def _new_like(ctx, b):
+    """An empty batch of b's kind and shape."""
+    out = type(b).__new__(type(b))
+    engine._Batch.__init__(out, ctx, b.replicas, b.elements)
+    return out
 
 
 def _or_into(ctx, dst, a, b):
-    """dst := a ⊔ b slot-wise for any representation: one k_or16 launch, or the
-    per-actor max for G-Counters."""
+    """dst := a ⊔ b slot-wise: one k_or16 launch, or the per-actor max for G-Counters."""
     if isinstance(dst, engine.GCounterBatch):
         _lib.check(ctx.L.laspj_gcounter_join(ctx.h, dst.h, a.h, b.h), ctx.h)
     else:
         _lib.check(ctx.L.laspj_batch_join(ctx.h, dst.h, a.h, b.h), ctx.h)
-
-
-def _concat_visible(dom: Domain, bits) -> list:
-    return [dom.elements.terms[int(e)] for e in dom.elements.order()
-            if (int(bits[int(e) >> 6]) >> (int(e) & 63)) & 1]
-

@@ -33,6 +33,9 @@ struct laspj_ctx {
     // per-replica partial records of segmented reductions (grown on demand)
     void* partials = nullptr;
     uint64_t partials_bytes = 0;
+    // list kernels' scratch (merge plans, key-order arrays, hash tables, sizes)
+    void* lscratch = nullptr;
+    uint64_t lscratch_bytes = 0;
 };
 
 struct laspj_buf {
@@ -51,7 +54,14 @@ struct laspj_batch {
     uint64_t cells = 0;         // cells per replica: E, or EL*ER for products
     uint64_t* dev = nullptr;
     bool owns = true;           // false for laspj_batch_wrap
+    // LASPJ_KIND_*_LIST: entry / token capacity per replica (laspj_lists.hip)
+    uint32_t cap_e = 0;
+    uint32_t cap_t = 0;
 };
+
+inline bool laspj_is_list(int32_t kind) {
+    return kind == LASPJ_KIND_ORSET_LIST || kind == LASPJ_KIND_GSET_LIST;
+}
 
 struct laspj_event {
     laspj_ctx* ctx = nullptr;

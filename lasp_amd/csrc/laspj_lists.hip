@@ -1,0 +1,1357 @@
+// List-faithful values on the device (include/laspj.h "list values").
+//
+// lasp_core's combinator bodies bind lists that are not orddicts (intersection
+// `Cx ++ Cy`, reversed product token pairs, reordered / repeated map and fold keys, the
+// G-Set `L ++ R`), and every re-run merges its new output into the old one with
+// orddict:merge / ordsets:union run as written — a two-finger merge over unsorted
+// lists.  A LIST batch keeps such a value exactly; the kernels below restate the list
+// operations of the path over it.
+//
+// Execution shape: one wave64 workgroup per replica (the bind path holds one replica
+// per variable; batched callers get one wave per replica).  Work that is a sequential
+// chain in the reference — the two-finger walk of orddict:merge / ordsets:union over
+// keys that need not ascend — runs on lane 0 over key ranks precomputed lane-parallel
+// into scratch (L1-resident, read in order); everything else (token merges per merged
+// entry, prefix sums for output positions, keyfind through a per-replica hash table,
+// ballots for the predicates) is lane-parallel.  Output positions come from wave
+// prefix sums, so each kernel runs twice: a size pass (WRITE = false) whose per-replica
+// {entries, tokens} the runtime reads back to size dst, then the write pass.
+//
+// Term order comes from host-built rank tables (krank per element slot, grank per token
+// slot), so a comparison is one integer compare and `==` is rank equality.
+
+#include <new>
+#include <vector>
+
+#include "laspj_internal.h"
+
+namespace laspj {
+
+namespace {
+
+typedef unsigned long long u64;
+
+constexpr u64 kPair = 1ull << 62;
+constexpr u64 kCompound = 1ull << 62;
+constexpr u64 kRemoved = 1ull << 63;
+constexpr u64 kIdMask = 0x7FFFFFFFull;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr u64 kEmpty = ~0ull;
+
+// flag bits (ctx->flag[1])
+constexpr uint32_t kErrRange = 1;    // an output ran past dst's capacity
+constexpr uint32_t kErrId = 2;       // an item's slot is outside the rank tables
+constexpr uint32_t kErrNested = 4;   // product of product outputs (nested pairs)
+constexpr uint32_t kErrTable = 8;    // a map / filter / fold table index out of range
+constexpr uint32_t kErrFun = 16;     // the fun failed on a key present in the list
+
+struct LV {
+    uint32_t* hdr;     // [R][2] {entries, tokens}
+    u64* key;          // [R][ce]
+    u64* tok;          // [R][ct]
+    uint32_t* toff;    // [R][ce + 1]
+    uint32_t ce, ct;
+    __device__ uint32_t n(u64 r) const { return hdr[2 * r]; }
+    __device__ uint32_t nt(u64 r) const { return hdr[2 * r + 1]; }
+    __device__ u64* K(u64 r) const { return key + r * ce; }
+    __device__ u64* T(u64 r) const { return tok + r * (u64)ct; }
+    __device__ uint32_t* O(u64 r) const { return toff + r * ((u64)ce + 1); }
+};
+
+struct RK {
+    const uint32_t* krank;
+    const uint32_t* grank;
+    uint32_t nk, ng;
+    uint32_t* flag;
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// exclusive prefix sum over the wave; *total = the wave's sum
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t* total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane_id() >= off) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ void lraise(uint32_t* flag, uint32_t bit) { atomicOr(flag, bit); }
+
+// term order of a key item: slots by krank, {X, Y} pairs element-wise after them
+__device__ __forceinline__ u64 key_ord(u64 it, const RK& rk) {
+    if (it & kPair) {
+        const uint32_t x = (uint32_t)((it >> 31) & kIdMask), y = (uint32_t)(it & kIdMask);
+        if (x >= rk.nk || y >= rk.nk) {
+            lraise(rk.flag, kErrId);
+            return 0;
+        }
+        return (1ull << 63) | ((u64)rk.krank[x] << 31) | rk.krank[y];
+    }
+    const uint32_t e = (uint32_t)(it & kIdMask);
+    if (e >= rk.nk) {
+        lraise(rk.flag, kErrId);
+        return 0;
+    }
+    return rk.krank[e];
+}
+
+// term order of a token item (flag ignored): [Tx, Ty] element-wise, below binaries
+__device__ __forceinline__ u64 tok_ord(u64 it, const RK& rk) {
+    if (it & kCompound) {
+        const uint32_t x = (uint32_t)((it >> 31) & kIdMask), y = (uint32_t)(it & kIdMask);
+        if (x >= rk.ng || y >= rk.ng) {
+            lraise(rk.flag, kErrId);
+            return 0;
+        }
+        return ((u64)rk.grank[x] << 31) | rk.grank[y];
+    }
+    const uint32_t g = (uint32_t)(it & kIdMask);
+    if (g >= rk.ng) {
+        lraise(rk.flag, kErrId);
+        return 0;
+    }
+    return (1ull << 62) | rk.grank[g];
+}
+
+// ---------------------------------------------------------------- per-replica hash
+// keyfind / member through an open-addressing table of key ranks -> first index
+// (size a power of two >= 2 x entries, so probes always end)
+
+__device__ __forceinline__ uint32_t hmix(u64 k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
+
+__device__ __forceinline__ void h_clear(u64* hk, uint32_t* hi, uint32_t hsize) {
+    for (uint32_t h = lane_id(); h < hsize; h += 64) {
+        hk[h] = kEmpty;
+        hi[h] = kNone;
+    }
+}
+
+__device__ __forceinline__ void h_insert(u64* hk, uint32_t* hi, uint32_t mask, u64 key,
+                                         uint32_t idx) {
+    uint32_t h = hmix(key) & mask;
+    for (;;) {
+        const u64 prev = atomicCAS(hk + h, kEmpty, key);
+        if (prev == kEmpty || prev == key) {
+            atomicMin(hi + h, idx);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ uint32_t h_find(const u64* hk, const uint32_t* hi, uint32_t mask,
+                                           u64 key) {
+    uint32_t h = hmix(key) & mask;
+    for (;;) {
+        const u64 k = __hip_atomic_load(const_cast<u64*>(hk + h), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key)
+            return __hip_atomic_load(const_cast<uint32_t*>(hi + h), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (k == kEmpty) return kNone;
+        h = (h + 1) & mask;
+    }
+}
+
+// orddict:merge over two token runs (inner clause of lasp_orset:merge/2): count or write
+template <bool W>
+__device__ uint32_t inner_merge(const u64* ta, uint32_t la, const u64* tb, uint32_t lb,
+                                u64* to, const RK& rk) {
+    uint32_t x = 0, y = 0, n = 0;
+    while (x < la && y < lb) {
+        const u64 A = ta[x], B = tb[y];
+        const u64 oa = tok_ord(A, rk), ob = tok_ord(B, rk);
+        if (oa < ob) {
+            if (W) to[n] = A;
+            ++x;
+        } else if (oa > ob) {
+            if (W) to[n] = B;
+            ++y;
+        } else {                       // {Token, BoolA or BoolB}, key of the first
+            if (W) to[n] = A | (B & kRemoved);
+            ++x, ++y;
+        }
+        ++n;
+    }
+    for (; x < la; ++x, ++n)
+        if (W) to[n] = ta[x];
+    for (; y < lb; ++y, ++n)
+        if (W) to[n] = tb[y];
+    return n;
+}
+
+__device__ __forceinline__ void finish(LV out, u64 r, uint32_t n, uint32_t nt, bool write,
+                                       uint32_t* need, uint32_t* flag) {
+    if (lane_id() != 0) return;
+    if (!write) {
+        need[2 * r] = n;
+        need[2 * r + 1] = nt;
+        return;
+    }
+    if (n > out.ce || nt > out.ct) {
+        lraise(flag, kErrRange);
+        return;
+    }
+    out.hdr[2 * r] = n;
+    out.hdr[2 * r + 1] = nt;
+    out.O(r)[n] = nt;
+}
+
+// ================================================================ kernels
+
+// canonical dense batch -> list: elements ascending in term order, tokens likewise
+template <bool GSET, bool WRITE>
+__global__ __launch_bounds__(64) void k_list_from_set(const u64* src, uint64_t wpr,
+                                                      const uint32_t* order, uint32_t nord,
+                                                      const uint8_t* tord, LV out,
+                                                      uint32_t* need, uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const u64* s = src + r * wpr;
+    uint32_t n = 0, nt = 0;
+    for (uint32_t c = 0; c < nord; c += 64) {
+        const uint32_t idx = c + lane_id();
+        uint32_t e = 0;
+        u64 p = 0, rm = 0;
+        if (idx < nord) {
+            e = order[idx];
+            if (GSET) {
+                p = (s[e >> 6] >> (e & 63)) & 1ull;
+            } else {
+                p = s[2ull * e];
+                rm = s[2ull * e + 1];
+            }
+        }
+        const uint32_t pres = p != 0, cnt = GSET ? 0u : (uint32_t)__popcll(p);
+        uint32_t tp, tt;
+        const uint32_t pos = n + wave_excl(pres, &tp);
+        uint32_t tpos = nt + wave_excl(pres ? cnt : 0u, &tt);
+        if (WRITE && pres) {
+            if (pos >= out.ce || tpos + cnt > out.ct) {
+                lraise(flag, kErrRange);
+            } else {
+                out.K(r)[pos] = e;
+                if (!GSET) {
+                    out.O(r)[pos] = tpos;
+                    u64* T = out.T(r);
+                    const uint8_t* to = tord + 64ull * e;
+                    for (int j = 0; j < 64; ++j) {
+                        const uint32_t k = to[j];
+                        if (k >= 64) break;
+                        if ((p >> k) & 1ull)
+                            T[tpos++] = (64ull * e + k) | (((rm >> k) & 1ull) << 63);
+                    }
+                }
+            }
+        }
+        n += tp;
+        nt += tt;
+    }
+    finish(out, r, n, nt, WRITE, need, flag);
+}
+
+// lasp_orset:merge/2 (MODE 0), the OR-Set union body = orddict:merge keeping the left
+// value (MODE 1), lasp_gset:merge/2 = OTP 17 ordsets:union (MODE 2)
+template <int MODE, bool WRITE>
+__global__ __launch_bounds__(64) void k_list_merge(LV a, LV b, LV out, RK rk, u64* sa, u64* sb,
+                                                   u64* plan, uint32_t* need) {
+    __shared__ uint32_t s_nout;
+    const u64 r = blockIdx.x;
+    const uint32_t na = a.n(r), nb = b.n(r);
+    sa += r * a.ce;
+    sb += r * b.ce;
+    plan += r * ((u64)a.ce + b.ce);
+    const u64* KA = a.K(r);
+    const u64* KB = b.K(r);
+    for (uint32_t i = lane_id(); i < na; i += 64) sa[i] = key_ord(KA[i], rk);
+    for (uint32_t j = lane_id(); j < nb; j += 64) sb[j] = key_ord(KB[j], rk);
+    __syncthreads();
+    if (lane_id() == 0) {
+        uint32_t o = 0, i = 0, j = 0;
+        if (MODE != 2) {
+            // merge(F,[{K1,_}=E1|D1],[{K2,_}=E2|D2]) when K1 < K2 -> [E1|merge(F,D1,[E2|D2])];
+            //   ... when K1 > K2 -> [E2|merge(F,[E1|D1],D2)];  equal -> F on both;
+            // merge(F,[],D2) -> D2;  merge(F,D1,[]) -> D1.
+            while (i < na && j < nb) {
+                const u64 x = sa[i], y = sb[j];
+                if (x < y) plan[o++] = (u64)i++ | ((u64)kNone << 32);
+                else if (x > y) plan[o++] = (u64)kNone | ((u64)j++ << 32);
+                else plan[o++] = (u64)i++ | ((u64)j++ << 32);
+            }
+            for (; i < na; ++i) plan[o++] = (u64)i | ((u64)kNone << 32);
+            for (; j < nb; ++j) plan[o++] = (u64)kNone | ((u64)j << 32);
+        } else {
+            // union([E1|Es1],[E2|_]=S2) when E1 < E2 -> [E1|union(Es1,S2)];
+            // union([E1|_]=S1,[E2|Es2]) when E1 > E2 -> [E2|union(Es2,S1)];  (switch)
+            // union([E1|Es1],[_|Es2]) -> [E1|union(Es1,Es2)];  tails as they are.
+            const u64* X = sa;
+            const u64* Y = sb;
+            uint32_t nx = na, ny = nb, sx = 0, sy = 1;
+            while (i < nx && j < ny) {
+                const u64 x = X[i], y = Y[j];
+                if (x < y) {
+                    plan[o++] = (u64)i++ | ((u64)sx << 32);
+                } else if (x > y) {
+                    plan[o++] = (u64)j | ((u64)sy << 32);
+                    const u64* T = X;
+                    X = Y, Y = T;
+                    uint32_t t = nx;
+                    nx = ny, ny = t;
+                    t = sx, sx = sy, sy = t;
+                    const uint32_t ni = j + 1;
+                    j = i, i = ni;
+                } else {
+                    plan[o++] = (u64)i++ | ((u64)sx << 32);
+                    ++j;
+                }
+            }
+            for (; i < nx; ++i) plan[o++] = (u64)i | ((u64)sx << 32);
+            for (; j < ny; ++j) plan[o++] = (u64)j | ((u64)sy << 32);
+        }
+        s_nout = o;
+    }
+    __syncthreads();
+    const uint32_t nout = s_nout;
+    const u64* TA = a.T(r);
+    const u64* TB = b.T(r);
+    const uint32_t* OA = a.O(r);
+    const uint32_t* OB = b.O(r);
+    uint32_t nt = 0;
+    for (uint32_t c = 0; c < nout; c += 64) {
+        const uint32_t o = c + lane_id();
+        uint32_t ia = kNone, jb = kNone, cnt = 0;
+        if (o < nout) {
+            const u64 p = plan[o];
+            if (MODE == 2) {
+                if (p >> 32) jb = (uint32_t)p;
+                else ia = (uint32_t)p;
+            } else {
+                ia = (uint32_t)p;
+                jb = (uint32_t)(p >> 32);
+                if (ia != kNone && jb != kNone) {
+                    cnt = MODE == 0 ? inner_merge<false>(TA + OA[ia], OA[ia + 1] - OA[ia],
+                                                         TB + OB[jb], OB[jb + 1] - OB[jb],
+                                                         nullptr, rk)
+                                    : OA[ia + 1] - OA[ia];
+                } else if (ia != kNone) {
+                    cnt = OA[ia + 1] - OA[ia];
+                } else {
+                    cnt = OB[jb + 1] - OB[jb];
+                }
+            }
+        }
+        uint32_t tt;
+        const uint32_t tpos = nt + wave_excl(cnt, &tt);
+        if (WRITE && o < nout) {
+            if (o >= out.ce || tpos + cnt > out.ct) {
+                lraise(rk.flag, kErrRange);
+            } else {
+                out.K(r)[o] = ia != kNone ? KA[ia] : KB[jb];
+                if (MODE != 2) {
+                    out.O(r)[o] = tpos;
+                    u64* to = out.T(r) + tpos;
+                    if (MODE == 0 && ia != kNone && jb != kNone) {
+                        inner_merge<true>(TA + OA[ia], OA[ia + 1] - OA[ia], TB + OB[jb],
+                                          OB[jb + 1] - OB[jb], to, rk);
+                    } else {
+                        const u64* from = ia != kNone ? TA + OA[ia] : TB + OB[jb];
+                        for (uint32_t k = 0; k < cnt; ++k) to[k] = from[k];
+                    }
+                }
+            }
+        }
+        nt += tt;
+    }
+    finish(out, r, nout, nt, WRITE, need, rk.flag);
+}
+
+// `case Value0 of Value` (=:=): same entries, keys, token runs and flags
+__global__ __launch_bounds__(64) void k_list_equal(LV a, LV b, RK rk, uint8_t* out) {
+    const u64 r = blockIdx.x;
+    const uint32_t n = a.n(r), nt = a.nt(r);
+    bool diff = n != b.n(r) || nt != b.nt(r);
+    if (!diff) {
+        const u64 *KA = a.K(r), *KB = b.K(r), *TA = a.T(r), *TB = b.T(r);
+        const uint32_t *OA = a.O(r), *OB = b.O(r);
+        for (uint32_t i = lane_id(); i < n && !diff; i += 64)
+            diff = key_ord(KA[i], rk) != key_ord(KB[i], rk) || OA[i] != OB[i];
+        for (uint32_t t = lane_id(); t < nt && !diff; t += 64)
+            diff = tok_ord(TA[t], rk) != tok_ord(TB[t], rk) ||
+                   ((TA[t] ^ TB[t]) & kRemoved) != 0;
+        diff = __ballot(diff) != 0;
+    }
+    if (lane_id() == 0) out[r] = diff ? 0 : 1;
+}
+
+// is_lattice_inflation / is_lattice_strict_inflation (lasp_lattice.erl:137-161,
+// 212-215, 235-253, 277-285)
+template <bool GSET, bool STRICT>
+__global__ __launch_bounds__(64) void k_list_inflation(LV prev, LV cur, RK rk, u64* hk,
+                                                       uint32_t* hi, uint32_t hsize,
+                                                       bool bcast, uint8_t* out) {
+    const u64 r = blockIdx.x, pr = bcast ? 0 : r;
+    const uint32_t np = prev.n(pr), nc = cur.n(r);
+    const uint32_t mask = hsize - 1;
+    u64* hk0 = hk + r * 2ull * hsize;
+    uint32_t* hi0 = hi + r * 2ull * hsize;
+    u64* hk1 = hk0 + hsize;      // G-Set strict: the set of Prev keys
+    uint32_t* hi1 = hi0 + hsize;
+    h_clear(hk0, hi0, hsize);
+    if (GSET && STRICT) h_clear(hk1, hi1, hsize);
+    __syncthreads();
+    const u64* KP = prev.K(pr);
+    const u64* KC = cur.K(r);
+    for (uint32_t j = lane_id(); j < nc; j += 64) h_insert(hk0, hi0, mask, key_ord(KC[j], rk), j);
+    if (GSET && STRICT)
+        for (uint32_t i = lane_id(); i < np; i += 64)
+            h_insert(hk1, hi1, mask, key_ord(KP[i], rk), i);
+    __syncthreads();
+    bool viol = false, changed = false;
+    if (GSET) {
+        // sets:is_subset(from_list(Prev), from_list(Cur))
+        for (uint32_t i = lane_id(); i < np; i += 64)
+            viol |= h_find(hk0, hi0, mask, key_ord(KP[i], rk)) == kNone;
+        // usort(Prev) =/= usort(Cur): with Prev ⊆ Cur, some Cur key is not in Prev
+        if (STRICT)
+            for (uint32_t j = lane_id(); j < nc; j += 64)
+                changed |= h_find(hk1, hi1, mask, key_ord(KC[j], rk)) == kNone;
+    } else {
+        const u64* TP = prev.T(pr);
+        const u64* TC = cur.T(r);
+        const uint32_t* OP = prev.O(pr);
+        const uint32_t* OC = cur.O(r);
+        for (uint32_t i = lane_id(); i < np; i += 64) {
+            // lists:keyfind(Element, 1, Current): the first entry with an equal key
+            const uint32_t j = h_find(hk0, hi0, mask, key_ord(KP[i], rk));
+            if (j == kNone) {
+                viol = true;
+                continue;
+            }
+            const u64* tp = TP + OP[i];
+            const u64* tc = TC + OC[j];
+            const uint32_t lp = OP[i + 1] - OP[i], lc = OC[j + 1] - OC[j];
+            // ids_inflated: every Prev token keyfind-s among Cur's (flags ignored)
+            for (uint32_t x = 0; x < lp && !viol; ++x) {
+                const u64 ox = tok_ord(tp[x], rk);
+                bool found = false;
+                for (uint32_t y = 0; y < lc && !found; ++y) found = tok_ord(tc[y], rk) == ox;
+                viol = !found;
+            }
+            // DeletedElements: Ids =/= Ids1 (order- and flag-sensitive)
+            if (STRICT && !changed) {
+                if (lp != lc) {
+                    changed = true;
+                } else {
+                    for (uint32_t x = 0; x < lp && !changed; ++x)
+                        changed = tok_ord(tp[x], rk) != tok_ord(tc[x], rk) ||
+                                  ((tp[x] ^ tc[x]) & kRemoved) != 0;
+                }
+            }
+        }
+    }
+    viol = __ballot(viol) != 0;
+    changed = __ballot(changed) != 0;
+    if (lane_id() == 0) {
+        bool res = !viol;
+        if (STRICT) {
+            if (GSET) res = res && changed;
+            else if (np == 0 && nc != 0) res = true;       // ([], Current) when Current =/= []
+            else res = res && (changed || np < nc);        // NewElements: length/1
+        }
+        out[r] = res ? 1 : 0;
+    }
+}
+
+// value/1: keys of entries with a {_, false} token, in list order
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_list_value(LV src, LV out, uint32_t* need,
+                                                   uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t n = src.n(r);
+    const u64* K = src.K(r);
+    const u64* T = src.T(r);
+    const uint32_t* O = src.O(r);
+    uint32_t m = 0;
+    for (uint32_t c = 0; c < n; c += 64) {
+        const uint32_t i = c + lane_id();
+        uint32_t live = 0;
+        if (i < n)
+            for (uint32_t t = O[i]; t < O[i + 1] && !live; ++t) live = (T[t] & kRemoved) == 0;
+        uint32_t tot;
+        const uint32_t pos = m + wave_excl(live, &tot);
+        if (WRITE && live) {
+            if (pos >= out.ce) lraise(flag, kErrRange);
+            else out.K(r)[pos] = K[i];
+        }
+        m += tot;
+    }
+    finish(out, r, m, 0, WRITE, need, flag);
+}
+
+// G-Set union body: L ++ R
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_list_concat(LV l, LV rr, LV out, uint32_t* need,
+                                                    uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t nl = l.n(r), nr = rr.n(r);
+    if (WRITE && nl + nr <= out.ce) {
+        for (uint32_t i = lane_id(); i < nl; i += 64) out.K(r)[i] = l.K(r)[i];
+        for (uint32_t j = lane_id(); j < nr; j += 64) out.K(r)[nl + j] = rr.K(r)[j];
+    }
+    finish(out, r, nl + nr, 0, WRITE, need, flag);
+}
+
+// intersection body: per entry of L in order, keyfind (OR-Set) / member (G-Set) in R
+template <bool GSET, bool WRITE>
+__global__ __launch_bounds__(64) void k_list_intersection(LV l, LV rr, LV out, RK rk, u64* hk,
+                                                          uint32_t* hi, uint32_t hsize,
+                                                          uint32_t* need) {
+    const u64 r = blockIdx.x;
+    const uint32_t nl = l.n(r), nr = rr.n(r), mask = hsize - 1;
+    hk += r * (u64)hsize;
+    hi += r * (u64)hsize;
+    h_clear(hk, hi, hsize);
+    __syncthreads();
+    const u64* KL = l.K(r);
+    const u64* KR = rr.K(r);
+    for (uint32_t j = lane_id(); j < nr; j += 64) h_insert(hk, hi, mask, key_ord(KR[j], rk), j);
+    __syncthreads();
+    const uint32_t* OL = l.O(r);
+    const uint32_t* OR = rr.O(r);
+    uint32_t m = 0, nt = 0;
+    for (uint32_t c = 0; c < nl; c += 64) {
+        const uint32_t i = c + lane_id();
+        uint32_t j = kNone, cnt = 0;
+        if (i < nl) {
+            j = h_find(hk, hi, mask, key_ord(KL[i], rk));
+            if (!GSET && j != kNone) cnt = (OL[i + 1] - OL[i]) + (OR[j + 1] - OR[j]);
+        }
+        const uint32_t hit = j != kNone;
+        uint32_t th, tt;
+        const uint32_t pos = m + wave_excl(hit, &th);
+        const uint32_t tpos = nt + wave_excl(cnt, &tt);
+        if (WRITE && hit) {
+            if (pos >= out.ce || tpos + cnt > out.ct) {
+                lraise(rk.flag, kErrRange);
+            } else {
+                out.K(r)[pos] = KL[i];
+                if (!GSET) {
+                    // orset_causal_union(Cx, Cy) = Cx ++ Cy
+                    out.O(r)[pos] = tpos;
+                    u64* to = out.T(r) + tpos;
+                    const u64* tl = l.T(r) + OL[i];
+                    const uint32_t ll = OL[i + 1] - OL[i];
+                    for (uint32_t k = 0; k < ll; ++k) to[k] = tl[k];
+                    const u64* tr = rr.T(r) + OR[j];
+                    for (uint32_t k = 0; k < cnt - ll; ++k) to[ll + k] = tr[k];
+                }
+            }
+        }
+        m += th;
+        nt += tt;
+    }
+    finish(out, r, m, nt, WRITE, need, rk.flag);
+}
+
+// product body: entry (x, y), x-major; tokens of (x, y): orset_causal_product(Cx, Cy)
+template <bool GSET, bool WRITE>
+__global__ __launch_bounds__(64) void k_list_product(LV l, LV rr, LV out, uint32_t* need,
+                                                     uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t nl = l.n(r), nr = rr.n(r);
+    const uint32_t ntl = GSET ? 0 : l.nt(r), ntr = GSET ? 0 : rr.nt(r);
+    const u64 n64 = (u64)nl * nr, nt64 = (u64)ntl * ntr;
+    if (n64 > 0xFFFFFFFFull || nt64 > 0xFFFFFFFFull) {
+        if (lane_id() == 0) lraise(flag, kErrRange);
+        return;
+    }
+    if (WRITE && n64 <= out.ce && nt64 <= out.ct) {
+        const u64* KL = l.K(r);
+        const u64* KR = rr.K(r);
+        const uint32_t* OL = l.O(r);
+        const uint32_t* OR = rr.O(r);
+        for (u64 o = lane_id(); o < n64; o += 64) {
+            const uint32_t xi = (uint32_t)(o / nr), yi = (uint32_t)(o % nr);
+            const u64 kx = KL[xi], ky = KR[yi];
+            if ((kx & kPair) || (ky & kPair)) {
+                lraise(flag, kErrNested);
+                continue;
+            }
+            out.K(r)[o] = kPair | ((kx & kIdMask) << 31) | (ky & kIdMask);
+            if (GSET) continue;
+            const uint32_t lx = OL[xi + 1] - OL[xi], ly = OR[yi + 1] - OR[yi];
+            // tokens before (xi, yi): all of rows < xi, then |Cx| x tokens of columns < yi
+            const uint32_t tpos = OL[xi] * ntr + lx * OR[yi];
+            out.O(r)[o] = tpos;
+            u64* to = out.T(r) + tpos;
+            const u64* tx = l.T(r) + OL[xi];
+            const u64* ty = rr.T(r) + OR[yi];
+            uint32_t k = 0;
+            for (uint32_t a = lx; a-- > 0;) {           // reversed foldl: Xs backwards
+                const u64 X = tx[a];
+                for (uint32_t b = ly; b-- > 0;) {       // ... and Ys backwards
+                    const u64 Y = ty[b];
+                    if ((X & kCompound) || (Y & kCompound)) {
+                        lraise(flag, kErrNested);
+                        continue;
+                    }
+                    to[k++] = kCompound | ((X & kIdMask) << 31) | (Y & kIdMask) |
+                              ((X | Y) & kRemoved);     // XDeleted orelse YDeleted
+                }
+            }
+        }
+    }
+    finish(out, r, (uint32_t)n64, (uint32_t)nt64, WRITE, need, flag);
+}
+
+__device__ __forceinline__ uint32_t tab_index(u64 key, uint32_t i, int per_entry, uint32_t ntab,
+                                              uint32_t* flag) {
+    if (!per_entry && (key & kPair)) {
+        lraise(flag, kErrTable);
+        return kNone;
+    }
+    const uint32_t idx = per_entry ? i : (uint32_t)(key & kIdMask);
+    if (idx >= ntab) {
+        lraise(flag, kErrTable);
+        return kNone;
+    }
+    return idx;
+}
+
+// map body: {F(X), C} / F(X) in list order — keys replaced, tokens kept
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_list_map(LV src, LV out, const u64* tab, uint32_t ntab,
+                                                 int per_entry, uint32_t* need,
+                                                 uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t n = src.n(r), nt = src.nt(r);
+    if (WRITE && n <= out.ce && nt <= out.ct) {
+        const u64* K = src.K(r);
+        for (uint32_t i = lane_id(); i < n; i += 64) {
+            const uint32_t idx = tab_index(K[i], i, per_entry, ntab, flag);
+            const u64 k = idx == kNone ? 0 : tab[idx];
+            if (k == kEmpty) lraise(flag, kErrFun);     // Function(X) raised
+            out.K(r)[i] = k;
+            out.O(r)[i] = src.O(r)[i];
+        }
+        for (uint32_t t = lane_id(); t < nt; t += 64) out.T(r)[t] = src.T(r)[t];
+    }
+    finish(out, r, n, nt, WRITE, need, flag);
+}
+
+// filter body: keep {X, C} / X when F(X) =:= true (tombstoned entries included)
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_list_filter(LV src, LV out, const uint8_t* keep,
+                                                    uint32_t ntab, int per_entry,
+                                                    uint32_t* need, uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t n = src.n(r);
+    const u64* K = src.K(r);
+    const uint32_t* O = src.O(r);
+    uint32_t m = 0, nt = 0;
+    for (uint32_t c = 0; c < n; c += 64) {
+        const uint32_t i = c + lane_id();
+        uint32_t k = 0, cnt = 0;
+        if (i < n) {
+            const uint32_t idx = tab_index(K[i], i, per_entry, ntab, flag);
+            if (idx != kNone && keep[idx] == 2) lraise(flag, kErrFun);   // Function(V) raised
+            k = idx != kNone && keep[idx] == 1;
+            cnt = k ? O[i + 1] - O[i] : 0;
+        }
+        uint32_t tk, tt;
+        const uint32_t pos = m + wave_excl(k, &tk);
+        const uint32_t tpos = nt + wave_excl(cnt, &tt);
+        if (WRITE && k) {
+            if (pos >= out.ce || tpos + cnt > out.ct) {
+                lraise(flag, kErrRange);
+            } else {
+                out.K(r)[pos] = K[i];
+                out.O(r)[pos] = tpos;
+                const u64* from = src.T(r) + O[i];
+                for (uint32_t t = 0; t < cnt; ++t) out.T(r)[tpos + t] = from[t];
+            }
+        }
+        m += tk;
+        nt += tt;
+    }
+    finish(out, r, m, nt, WRITE, need, flag);
+}
+
+// fold body: [{V, C} || V <- F(X)] / F(X), concatenated in list order
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_list_fold(LV src, LV out, const uint32_t* off,
+                                                  const u64* keys, uint32_t ntab,
+                                                  int per_entry, uint32_t* need,
+                                                  uint32_t* flag) {
+    const u64 r = blockIdx.x;
+    const uint32_t n = src.n(r);
+    const u64* K = src.K(r);
+    const uint32_t* O = src.O(r);
+    uint32_t m = 0, nt = 0;
+    for (uint32_t c = 0; c < n; c += 64) {
+        const uint32_t i = c + lane_id();
+        uint32_t idx = kNone, k = 0, len = 0;
+        if (i < n) {
+            idx = tab_index(K[i], i, per_entry, ntab, flag);
+            if (idx != kNone) {
+                k = off[idx + 1] - off[idx];
+                len = O[i + 1] - O[i];
+                for (uint32_t v = 0; v < k; ++v)
+                    if (keys[off[idx] + v] == kEmpty) lraise(flag, kErrFun);
+            }
+        }
+        uint32_t tk, tt;
+        const uint32_t pos = m + wave_excl(k, &tk);
+        const uint32_t tpos = nt + wave_excl(k * len, &tt);
+        if (WRITE && k) {
+            if (pos + k > out.ce || tpos + k * len > out.ct) {
+                lraise(flag, kErrRange);
+            } else {
+                const u64* from = src.T(r) + O[i];
+                for (uint32_t v = 0; v < k; ++v) {
+                    out.K(r)[pos + v] = keys[off[idx] + v];
+                    out.O(r)[pos + v] = tpos + v * len;
+                    for (uint32_t t = 0; t < len; ++t) out.T(r)[tpos + v * len + t] = from[t];
+                }
+            }
+        }
+        m += tk;
+        nt += tt;
+    }
+    finish(out, r, m, nt, WRITE, need, flag);
+}
+
+}  // namespace
+
+}  // namespace laspj
+
+// ================================================================ runtime + C ABI
+
+using laspj::fail;
+using namespace laspj;
+
+namespace {
+
+struct LGuard {
+    std::lock_guard<std::mutex> lk;
+    explicit LGuard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
+};
+
+uint64_t list_wpr(uint32_t ce, uint32_t ct) {
+    return (8ull + 8ull * ce + 8ull * ct + 4ull * ((uint64_t)ce + 1) + 7ull) / 8ull;
+}
+
+LV view(const laspj_batch* b) {
+    LV v;
+    char* base = reinterpret_cast<char*>(b->dev);
+    const uint64_t R = b->replicas;
+    v.hdr = reinterpret_cast<uint32_t*>(base);
+    base += R * 8ull;
+    v.key = reinterpret_cast<u64*>(base);
+    base += R * 8ull * b->cap_e;
+    v.tok = reinterpret_cast<u64*>(base);
+    base += R * 8ull * b->cap_t;
+    v.toff = reinterpret_cast<uint32_t*>(base);
+    v.ce = b->cap_e;
+    v.ct = b->cap_t;
+    return v;
+}
+
+// (re)allocate a list batch's device memory for caps (ce, ct); contents: empty lists
+int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
+    if (ce == 0) ce = 1;
+    if (ct == 0) ct = 1;
+    const uint64_t wpr = list_wpr(ce, ct);
+    if (b->replicas > (~0ull / 8ull) / wpr)
+        return fail(ctx, LASPJ_E_SHAPE, "list: size overflow");
+    const uint64_t bytes = b->replicas * wpr * 8ull;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        hipGetLastError();
+        return fail(ctx, LASPJ_E_NOMEM, "list: hipMalloc(%llu): %s", (unsigned long long)bytes,
+                    hipGetErrorString(e));
+    }
+    e = hipMemsetAsync(p, 0, bytes, ctx->stream);
+    if (e != hipSuccess) {
+        hipFree(p);
+        return fail(ctx, LASPJ_E_DEVICE, "list: memset: %s", hipGetErrorString(e));
+    }
+    if (b->dev) {
+        hipStreamSynchronize(ctx->stream);
+        hipFree(b->dev);
+    }
+    b->dev = static_cast<uint64_t*>(p);
+    b->cap_e = ce;
+    b->cap_t = ct;
+    b->words_per_replica = wpr;
+    b->elements = ce;
+    b->cells = ce;
+    return LASPJ_OK;
+}
+
+void* lscratch(laspj_ctx* ctx, uint64_t bytes) {
+    if (bytes == 0) bytes = 8;
+    if (ctx->lscratch_bytes < bytes) {
+        if (ctx->lscratch) {
+            hipStreamSynchronize(ctx->stream);
+            hipFree(ctx->lscratch);
+            ctx->lscratch = nullptr;
+            ctx->lscratch_bytes = 0;
+        }
+        if (hipMalloc(&ctx->lscratch, bytes) != hipSuccess) {
+            hipGetLastError();
+            return nullptr;
+        }
+        ctx->lscratch_bytes = bytes;
+    }
+    return ctx->lscratch;
+}
+
+int check_list(laspj_ctx* ctx, const laspj_batch* b, const char* what) {
+    if (!b || b->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "%s: null batch or other context", what);
+    if (!laspj_is_list(b->kind)) return fail(ctx, LASPJ_E_KIND, "%s: not a list batch", what);
+    return LASPJ_OK;
+}
+
+int ranks(laspj_ctx* ctx, const laspj_list_order* ord, bool need_tokens, RK* rk,
+          const char* what) {
+    if (!ord || !ord->krank || ord->krank->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: rank tables missing", what);
+    if ((uint64_t)ord->nkeys * 4ull > ord->krank->bytes)
+        return fail(ctx, LASPJ_E_RANGE, "%s: krank holds fewer than %u ranks", what, ord->nkeys);
+    rk->krank = static_cast<const uint32_t*>(ord->krank->dev);
+    rk->nk = ord->nkeys;
+    rk->grank = nullptr;
+    rk->ng = 0;
+    if (ord->grank) {
+        if (ord->grank->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "%s: grank context", what);
+        if ((uint64_t)ord->ntokens * 4ull > ord->grank->bytes)
+            return fail(ctx, LASPJ_E_RANGE, "%s: grank holds fewer than %u ranks", what,
+                        ord->ntokens);
+        rk->grank = static_cast<const uint32_t*>(ord->grank->dev);
+        rk->ng = ord->ntokens;
+    } else if (need_tokens) {
+        return fail(ctx, LASPJ_E_INVAL, "%s: OR-Set lists need token ranks", what);
+    }
+    rk->flag = ctx->flag + 1;
+    return LASPJ_OK;
+}
+
+uint32_t pow2_at_least(uint64_t n) {
+    uint64_t h = 64;
+    while (h < n) h <<= 1;
+    return (uint32_t)h;
+}
+
+int read_flag(laspj_ctx* ctx, const char* what) {
+    uint32_t f = 0;
+    LJ_HIP(ctx, hipMemcpyAsync(&f, ctx->flag + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (f & kErrFun)
+        return fail(ctx, LASPJ_E_FUN, "%s: the fun failed on a key of the list", what);
+    if (f & kErrNested)
+        return fail(ctx, LASPJ_E_UNSUPPORTED, "%s: product of product outputs (nested pairs)",
+                    what);
+    if (f & kErrId) return fail(ctx, LASPJ_E_RANGE, "%s: item outside the rank tables", what);
+    if (f & kErrTable) return fail(ctx, LASPJ_E_RANGE, "%s: table index out of range", what);
+    if (f & kErrRange) return fail(ctx, LASPJ_E_RANGE, "%s: output capacity exceeded", what);
+    return LASPJ_OK;
+}
+
+// run a size pass, size dst from the per-replica maxima, then the write pass
+template <class SizeFn, class WriteFn>
+int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, WriteFn write_pass,
+          const char* what) {
+    const uint64_t R = dst->replicas;
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    size_pass();
+    LJ_LAUNCHED(ctx);
+    std::vector<uint32_t> h(2 * R);
+    LJ_HIP(ctx, hipMemcpyAsync(h.data(), need, 8ull * R, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int s = read_flag(ctx, what)) return s;
+    uint32_t ce = 0, ct = 0;
+    for (uint64_t i = 0; i < R; ++i) {
+        ce = h[2 * i] > ce ? h[2 * i] : ce;
+        ct = h[2 * i + 1] > ct ? h[2 * i + 1] : ct;
+    }
+    if (ce > dst->cap_e || ct > dst->cap_t)
+        if (int s = list_alloc(ctx, dst, ce > dst->cap_e ? ce : dst->cap_e,
+                               ct > dst->cap_t ? ct : dst->cap_t))
+            return s;
+    write_pass(view(dst));
+    LJ_LAUNCHED(ctx);
+    return read_flag(ctx, what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int laspj_list_batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas,
+                            uint32_t cap_entries, uint32_t cap_tokens, laspj_batch** out) {
+    if (!ctx || !out) return fail(ctx, LASPJ_E_INVAL, "list_batch_create: null argument");
+    *out = nullptr;
+    if (!laspj_is_list(kind)) return fail(ctx, LASPJ_E_KIND, "list_batch_create: kind");
+    if (replicas == 0) return fail(ctx, LASPJ_E_SHAPE, "list_batch_create: no replicas");
+    if (replicas > 0x7FFFFFFFull)
+        return fail(ctx, LASPJ_E_SHAPE, "list_batch_create: at most 2^31-1 replicas");
+    LGuard g(ctx);
+    auto* b = new (std::nothrow) laspj_batch;
+    if (!b) return fail(ctx, LASPJ_E_NOMEM, "list_batch_create: host allocation");
+    b->ctx = ctx;
+    b->kind = kind;
+    b->replicas = replicas;
+    if (int s = list_alloc(ctx, b, cap_entries, kind == LASPJ_KIND_GSET_LIST ? 1 : cap_tokens)) {
+        delete b;
+        return s;
+    }
+    *out = b;
+    return LASPJ_OK;
+}
+
+int laspj_list_counts(laspj_ctx* ctx, const laspj_batch* b, uint32_t* out) {
+    if (int s = check_list(ctx, b, "list_counts")) return s;
+    if (!out) return fail(ctx, LASPJ_E_INVAL, "list_counts: null output");
+    LGuard g(ctx);
+    LJ_HIP(ctx, hipMemcpyAsync(out, b->dev, 8ull * b->replicas, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_list_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t replica, uint32_t n,
+                      const uint64_t* keys, const uint32_t* toff, const uint64_t* toks) {
+    if (int s = check_list(ctx, b, "list_upload")) return s;
+    const bool gs = b->kind == LASPJ_KIND_GSET_LIST;
+    if (replica >= b->replicas) return fail(ctx, LASPJ_E_RANGE, "list_upload: replica");
+    if ((n && !keys) || (!gs && !toff))
+        return fail(ctx, LASPJ_E_INVAL, "list_upload: null arrays");
+    uint32_t nt = 0;
+    if (!gs) {
+        if (toff[0] != 0) return fail(ctx, LASPJ_E_INVAL, "list_upload: toff[0] != 0");
+        for (uint32_t i = 0; i < n; ++i)
+            if (toff[i + 1] < toff[i])
+                return fail(ctx, LASPJ_E_INVAL, "list_upload: toff not ascending");
+        nt = toff[n];
+        if (nt && !toks) return fail(ctx, LASPJ_E_INVAL, "list_upload: null tokens");
+    }
+    LGuard g(ctx);
+    if (n > b->cap_e || nt > b->cap_t) {
+        // keep the other replicas: only a 1-replica batch grows here
+        if (b->replicas != 1)
+            return fail(ctx, LASPJ_E_RANGE, "list_upload: list exceeds the batch capacity");
+        if (int s = list_alloc(ctx, b, n > b->cap_e ? n : b->cap_e, nt > b->cap_t ? nt : b->cap_t))
+            return s;
+    }
+    LV v = view(b);
+    uint32_t hdr[2] = {n, nt};
+    LJ_HIP(ctx, hipMemcpyAsync(v.hdr + 2 * replica, hdr, 8, hipMemcpyHostToDevice, ctx->stream));
+    if (n)
+        LJ_HIP(ctx, hipMemcpyAsync(v.key + replica * v.ce, keys, 8ull * n, hipMemcpyHostToDevice,
+                                   ctx->stream));
+    if (!gs) {
+        LJ_HIP(ctx, hipMemcpyAsync(v.toff + replica * ((uint64_t)v.ce + 1), toff, 4ull * (n + 1),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        if (nt)
+            LJ_HIP(ctx, hipMemcpyAsync(v.tok + replica * (uint64_t)v.ct, toks, 8ull * nt,
+                                       hipMemcpyHostToDevice, ctx->stream));
+    }
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_list_download(laspj_ctx* ctx, const laspj_batch* b, uint64_t replica, uint64_t* keys,
+                        uint32_t* toff, uint64_t* toks) {
+    if (int s = check_list(ctx, b, "list_download")) return s;
+    if (replica >= b->replicas) return fail(ctx, LASPJ_E_RANGE, "list_download: replica");
+    const bool gs = b->kind == LASPJ_KIND_GSET_LIST;
+    LGuard g(ctx);
+    LV v = view(b);
+    uint32_t hdr[2];
+    LJ_HIP(ctx, hipMemcpyAsync(hdr, v.hdr + 2 * replica, 8, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if ((hdr[0] && !keys) || (!gs && (!toff || (hdr[1] && !toks))))
+        return fail(ctx, LASPJ_E_INVAL, "list_download: null arrays");
+    if (hdr[0])
+        LJ_HIP(ctx, hipMemcpyAsync(keys, v.key + replica * v.ce, 8ull * hdr[0],
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    if (!gs) {
+        LJ_HIP(ctx, hipMemcpyAsync(toff, v.toff + replica * ((uint64_t)v.ce + 1),
+                                   4ull * (hdr[0] + 1), hipMemcpyDeviceToHost, ctx->stream));
+        if (hdr[1])
+            LJ_HIP(ctx, hipMemcpyAsync(toks, v.tok + replica * (uint64_t)v.ct, 8ull * hdr[1],
+                                       hipMemcpyDeviceToHost, ctx->stream));
+    }
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
+int laspj_list_from_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                        const laspj_buf* elem_order, uint32_t nslots, const laspj_buf* tok_order) {
+    if (int s = check_list(ctx, dst, "list_from_set")) return s;
+    if (!src || src->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "list_from_set: src");
+    const bool gs = src->kind == LASPJ_KIND_GSET;
+    if (!(src->kind == LASPJ_KIND_ORSET || gs) ||
+        dst->kind != (gs ? LASPJ_KIND_GSET_LIST : LASPJ_KIND_ORSET_LIST))
+        return fail(ctx, LASPJ_E_KIND, "list_from_set: OR-Set -> OR-Set list, G-Set -> G-Set list");
+    if (dst->replicas != src->replicas) return fail(ctx, LASPJ_E_SHAPE, "list_from_set: replicas");
+    if (!elem_order || elem_order->ctx != ctx || (uint64_t)nslots * 4 > elem_order->bytes ||
+        nslots > src->elements)
+        return fail(ctx, LASPJ_E_RANGE, "list_from_set: element order");
+    if (!gs && (!tok_order || tok_order->ctx != ctx ||
+                tok_order->bytes < 64ull * src->elements))
+        return fail(ctx, LASPJ_E_RANGE, "list_from_set: token order (64 bytes per slot)");
+    if ((uint64_t)src->elements * 64ull > kIdMask)
+        return fail(ctx, LASPJ_E_RANGE, "list_from_set: too many element slots for token ids");
+    // element slots in elem_order must be < E: checked on the host copy would need a
+    // download; the kernel reads cells of slot order[i] — validate by bound instead
+    LGuard g(ctx);
+    {
+        std::vector<uint32_t> ord(nslots);
+        if (nslots) {
+            LJ_HIP(ctx, hipMemcpyAsync(ord.data(), elem_order->dev, 4ull * nslots,
+                                       hipMemcpyDeviceToHost, ctx->stream));
+            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        for (uint32_t v : ord)
+            if (v >= src->elements)
+                return fail(ctx, LASPJ_E_RANGE, "list_from_set: slot %u >= %u", v, src->elements);
+    }
+    const uint64_t R = src->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_from_set: scratch");
+    const auto* ordp = static_cast<const uint32_t*>(elem_order->dev);
+    const auto* tordp = gs ? nullptr : static_cast<const uint8_t*>(tok_order->dev);
+    uint32_t* flag = ctx->flag + 1;
+    LV nil = view(dst);
+    return sized(
+        ctx, dst, need,
+        [&] {
+            if (gs)
+                hipLaunchKernelGGL((k_list_from_set<true, false>), dim3(R), dim3(64), 0, ctx->stream,
+                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
+                                   tordp, nil, need, flag);
+            else
+                hipLaunchKernelGGL((k_list_from_set<false, false>), dim3(R), dim3(64), 0,
+                                   ctx->stream, (const u64*)src->dev, src->words_per_replica,
+                                   ordp, nslots, tordp, nil, need, flag);
+        },
+        [&](LV out) {
+            if (gs)
+                hipLaunchKernelGGL((k_list_from_set<true, true>), dim3(R), dim3(64), 0, ctx->stream,
+                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
+                                   tordp, out, need, flag);
+            else
+                hipLaunchKernelGGL((k_list_from_set<false, true>), dim3(R), dim3(64), 0, ctx->stream,
+                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
+                                   tordp, out, need, flag);
+        },
+        "list_from_set");
+}
+
+static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch* a,
+                       const laspj_batch* b, const char* what) {
+    if (int s = check_list(ctx, dst, what)) return s;
+    if (int s = check_list(ctx, a, what)) return s;
+    if (int s = check_list(ctx, b, what)) return s;
+    if (a->kind != b->kind || dst->kind != a->kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: list kinds differ", what);
+    if (a->replicas != b->replicas || dst->replicas != a->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: replica counts differ", what);
+    if (dst == a || dst == b) return fail(ctx, LASPJ_E_INVAL, "%s: dst aliases an input", what);
+    return LASPJ_OK;
+}
+
+static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                      const laspj_batch* b, const laspj_list_order* ord, bool keep_left,
+                      const char* what) {
+    if (int s = pair_checks(ctx, dst, a, b, what)) return s;
+    const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
+    RK rk;
+    if (int s = ranks(ctx, ord, !gs, &rk, what)) return s;
+    LGuard g(ctx);
+    const uint64_t R = a->replicas;
+    const uint64_t sa_b = R * 8ull * a->cap_e, sb_b = R * 8ull * b->cap_e;
+    const uint64_t pl_b = R * 8ull * ((uint64_t)a->cap_e + b->cap_e);
+    char* base = static_cast<char*>(lscratch(ctx, sa_b + sb_b + pl_b + 8ull * R));
+    if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
+    u64* sa = reinterpret_cast<u64*>(base);
+    u64* sb = reinterpret_cast<u64*>(base + sa_b);
+    u64* plan = reinterpret_cast<u64*>(base + sa_b + sb_b);
+    auto* need = reinterpret_cast<uint32_t*>(base + sa_b + sb_b + pl_b);
+    const LV A = view(a), B = view(b), nil = view(dst);
+#define LJ_MERGE(MODE, W, OUT)                                                              \
+    hipLaunchKernelGGL((k_list_merge<MODE, W>), dim3(R), dim3(64), 0, ctx->stream, A, B, OUT, \
+                       rk, sa, sb, plan, need)
+    if (gs)
+        return sized(ctx, dst, need, [&] { LJ_MERGE(2, false, nil); },
+                     [&](LV out) { LJ_MERGE(2, true, out); }, what);
+    if (keep_left)
+        return sized(ctx, dst, need, [&] { LJ_MERGE(1, false, nil); },
+                     [&](LV out) { LJ_MERGE(1, true, out); }, what);
+    return sized(ctx, dst, need, [&] { LJ_MERGE(0, false, nil); },
+                 [&](LV out) { LJ_MERGE(0, true, out); }, what);
+#undef LJ_MERGE
+}
+
+int laspj_list_merge(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b, const laspj_list_order* ord) {
+    return merge_impl(ctx, dst, a, b, ord, false, "list_merge");
+}
+
+int laspj_list_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                     const laspj_batch* r, const laspj_list_order* ord) {
+    if (l && l->kind == LASPJ_KIND_GSET_LIST) {
+        if (int s = pair_checks(ctx, dst, l, r, "list_union")) return s;
+        LGuard g(ctx);
+        const uint64_t R = l->replicas;
+        auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+        if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_union: scratch");
+        const LV L = view(l), Rr = view(r), nil = view(dst);
+        uint32_t* flag = ctx->flag + 1;
+        return sized(
+            ctx, dst, need,
+            [&] {
+                hipLaunchKernelGGL((k_list_concat<false>), dim3(R), dim3(64), 0, ctx->stream, L,
+                                   Rr, nil, need, flag);
+            },
+            [&](LV out) {
+                hipLaunchKernelGGL((k_list_concat<true>), dim3(R), dim3(64), 0, ctx->stream, L,
+                                   Rr, out, need, flag);
+            },
+            "list_union");
+    }
+    return merge_impl(ctx, dst, l, r, ord, true, "list_union");
+}
+
+int laspj_list_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
+                     const laspj_list_order* ord, laspj_buf* out) {
+    if (int s = check_list(ctx, a, "list_equal")) return s;
+    if (int s = check_list(ctx, b, "list_equal")) return s;
+    if (a->kind != b->kind) return fail(ctx, LASPJ_E_KIND, "list_equal: kinds differ");
+    if (a->replicas != b->replicas) return fail(ctx, LASPJ_E_SHAPE, "list_equal: replicas");
+    if (!out || out->ctx != ctx || out->bytes < a->replicas)
+        return fail(ctx, LASPJ_E_RANGE, "list_equal: output buffer");
+    RK rk;
+    if (int s = ranks(ctx, ord, a->kind == LASPJ_KIND_ORSET_LIST, &rk, "list_equal")) return s;
+    LGuard g(ctx);
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(k_list_equal, dim3(a->replicas), dim3(64), 0, ctx->stream, view(a),
+                       view(b), rk, static_cast<uint8_t*>(out->dev));
+    LJ_LAUNCHED(ctx);
+    return read_flag(ctx, "list_equal");
+}
+
+int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                         int strict, const laspj_list_order* ord, laspj_buf* out) {
+    if (int s = check_list(ctx, prev, "list_inflation")) return s;
+    if (int s = check_list(ctx, cur, "list_inflation")) return s;
+    if (prev->kind != cur->kind) return fail(ctx, LASPJ_E_KIND, "list_inflation: kinds differ");
+    const bool bcast = prev->replicas == 1 && cur->replicas != 1;
+    if (!bcast && prev->replicas != cur->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "list_inflation: replicas");
+    if (!out || out->ctx != ctx || out->bytes < cur->replicas)
+        return fail(ctx, LASPJ_E_RANGE, "list_inflation: output buffer");
+    const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
+    RK rk;
+    if (int s = ranks(ctx, ord, !gs, &rk, "list_inflation")) return s;
+    LGuard g(ctx);
+    const uint64_t R = cur->replicas;
+    const uint32_t hsize = pow2_at_least(2ull * (cur->cap_e > prev->cap_e ? cur->cap_e
+                                                                          : prev->cap_e));
+    char* base = static_cast<char*>(lscratch(ctx, R * 2ull * hsize * 12ull));
+    if (!base) return fail(ctx, LASPJ_E_NOMEM, "list_inflation: scratch");
+    u64* hk = reinterpret_cast<u64*>(base);
+    auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    auto* o = static_cast<uint8_t*>(out->dev);
+    const LV P = view(prev), C = view(cur);
+#define LJ_INFL(G, S)                                                                         \
+    hipLaunchKernelGGL((k_list_inflation<G, S>), dim3(R), dim3(64), 0, ctx->stream, P, C, rk, hk, \
+                       hi, hsize, bcast, o)
+    if (gs) {
+        if (strict) LJ_INFL(true, true); else LJ_INFL(true, false);
+    } else {
+        if (strict) LJ_INFL(false, true); else LJ_INFL(false, false);
+    }
+#undef LJ_INFL
+    LJ_LAUNCHED(ctx);
+    return read_flag(ctx, "list_inflation");
+}
+
+int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
+    if (int s = check_list(ctx, dst, "list_value")) return s;
+    if (int s = check_list(ctx, src, "list_value")) return s;
+    if (src->kind != LASPJ_KIND_ORSET_LIST || dst->kind != LASPJ_KIND_GSET_LIST)
+        return fail(ctx, LASPJ_E_KIND, "list_value: OR-Set list -> G-Set list");
+    if (dst->replicas != src->replicas) return fail(ctx, LASPJ_E_SHAPE, "list_value: replicas");
+    LGuard g(ctx);
+    const uint64_t R = src->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_value: scratch");
+    const LV S = view(src), nil = view(dst);
+    uint32_t* flag = ctx->flag + 1;
+    return sized(
+        ctx, dst, need,
+        [&] {
+            hipLaunchKernelGGL((k_list_value<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
+                               need, flag);
+        },
+        [&](LV out) {
+            hipLaunchKernelGGL((k_list_value<true>), dim3(R), dim3(64), 0, ctx->stream, S, out,
+                               need, flag);
+        },
+        "list_value");
+}
+
+int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                            const laspj_batch* r, const laspj_list_order* ord) {
+    if (int s = pair_checks(ctx, dst, l, r, "list_intersection")) return s;
+    const bool gs = l->kind == LASPJ_KIND_GSET_LIST;
+    RK rk;
+    if (int s = ranks(ctx, ord, !gs, &rk, "list_intersection")) return s;
+    LGuard g(ctx);
+    const uint64_t R = l->replicas;
+    const uint32_t hsize = pow2_at_least(2ull * r->cap_e);
+    char* base = static_cast<char*>(lscratch(ctx, R * hsize * 12ull + 8ull * R));
+    if (!base) return fail(ctx, LASPJ_E_NOMEM, "list_intersection: scratch");
+    u64* hk = reinterpret_cast<u64*>(base);
+    auto* hi = reinterpret_cast<uint32_t*>(base + R * hsize * 8ull);
+    auto* need = reinterpret_cast<uint32_t*>(base + R * hsize * 12ull);
+    const LV L = view(l), Rr = view(r), nil = view(dst);
+#define LJ_ISECT(G, W, OUT)                                                                    \
+    hipLaunchKernelGGL((k_list_intersection<G, W>), dim3(R), dim3(64), 0, ctx->stream, L, Rr, OUT, \
+                       rk, hk, hi, hsize, need)
+    if (gs)
+        return sized(ctx, dst, need, [&] { LJ_ISECT(true, false, nil); },
+                     [&](LV out) { LJ_ISECT(true, true, out); }, "list_intersection");
+    return sized(ctx, dst, need, [&] { LJ_ISECT(false, false, nil); },
+                 [&](LV out) { LJ_ISECT(false, true, out); }, "list_intersection");
+#undef LJ_ISECT
+}
+
+int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                       const laspj_batch* r) {
+    if (int s = pair_checks(ctx, dst, l, r, "list_product")) return s;
+    const bool gs = l->kind == LASPJ_KIND_GSET_LIST;
+    LGuard g(ctx);
+    const uint64_t R = l->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_product: scratch");
+    const LV L = view(l), Rr = view(r), nil = view(dst);
+    uint32_t* flag = ctx->flag + 1;
+#define LJ_PROD(G, W, OUT)                                                                     \
+    hipLaunchKernelGGL((k_list_product<G, W>), dim3(R), dim3(64), 0, ctx->stream, L, Rr, OUT,   \
+                       need, flag)
+    if (gs)
+        return sized(ctx, dst, need, [&] { LJ_PROD(true, false, nil); },
+                     [&](LV out) { LJ_PROD(true, true, out); }, "list_product");
+    return sized(ctx, dst, need, [&] { LJ_PROD(false, false, nil); },
+                 [&](LV out) { LJ_PROD(false, true, out); }, "list_product");
+#undef LJ_PROD
+}
+
+static int unary_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch* src,
+                        const laspj_buf* tab, uint64_t tab_bytes, const char* what) {
+    if (int s = check_list(ctx, dst, what)) return s;
+    if (int s = check_list(ctx, src, what)) return s;
+    if (dst->kind != src->kind) return fail(ctx, LASPJ_E_KIND, "%s: kinds differ", what);
+    if (dst->replicas != src->replicas) return fail(ctx, LASPJ_E_SHAPE, "%s: replicas", what);
+    if (dst == src) return fail(ctx, LASPJ_E_INVAL, "%s: dst aliases src", what);
+    if (!tab || tab->ctx != ctx || tab->bytes < tab_bytes)
+        return fail(ctx, LASPJ_E_RANGE, "%s: table buffer too small", what);
+    return LASPJ_OK;
+}
+
+int laspj_list_map(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                   const laspj_buf* keys, uint32_t nidx, int per_entry) {
+    if (int s = unary_checks(ctx, dst, src, keys, 8ull * nidx, "list_map")) return s;
+    LGuard g(ctx);
+    const uint64_t R = src->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_map: scratch");
+    const LV S = view(src), nil = view(dst);
+    const auto* tab = static_cast<const u64*>(keys->dev);
+    uint32_t* flag = ctx->flag + 1;
+    return sized(
+        ctx, dst, need,
+        [&] {
+            hipLaunchKernelGGL((k_list_map<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
+                               tab, nidx, per_entry, need, flag);
+        },
+        [&](LV out) {
+            hipLaunchKernelGGL((k_list_map<true>), dim3(R), dim3(64), 0, ctx->stream, S, out, tab,
+                               nidx, per_entry, need, flag);
+        },
+        "list_map");
+}
+
+int laspj_list_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                      const laspj_buf* keep, uint32_t nidx, int per_entry) {
+    if (int s = unary_checks(ctx, dst, src, keep, nidx, "list_filter")) return s;
+    LGuard g(ctx);
+    const uint64_t R = src->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_filter: scratch");
+    const LV S = view(src), nil = view(dst);
+    const auto* tab = static_cast<const uint8_t*>(keep->dev);
+    uint32_t* flag = ctx->flag + 1;
+    return sized(
+        ctx, dst, need,
+        [&] {
+            hipLaunchKernelGGL((k_list_filter<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
+                               tab, nidx, per_entry, need, flag);
+        },
+        [&](LV out) {
+            hipLaunchKernelGGL((k_list_filter<true>), dim3(R), dim3(64), 0, ctx->stream, S, out,
+                               tab, nidx, per_entry, need, flag);
+        },
+        "list_filter");
+}
+
+int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                    const laspj_buf* off, const laspj_buf* keys, uint32_t nidx, int per_entry) {
+    if (int s = unary_checks(ctx, dst, src, off, 4ull * ((uint64_t)nidx + 1), "list_fold"))
+        return s;
+    if (!keys || keys->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "list_fold: keys buffer");
+    LGuard g(ctx);
+    // the CSR offsets must stay inside the keys buffer
+    std::vector<uint32_t> h((uint64_t)nidx + 1);
+    LJ_HIP(ctx, hipMemcpyAsync(h.data(), off->dev, 4ull * h.size(), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t i = 0; i < nidx; ++i)
+        if (h[i + 1] < h[i]) return fail(ctx, LASPJ_E_INVAL, "list_fold: offsets not ascending");
+    if (8ull * h[nidx] > keys->bytes)
+        return fail(ctx, LASPJ_E_RANGE, "list_fold: keys buffer too small");
+    const uint64_t R = src->replicas;
+    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
+    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_fold: scratch");
+    const LV S = view(src), nil = view(dst);
+    const auto* po = static_cast<const uint32_t*>(off->dev);
+    const auto* pk = static_cast<const u64*>(keys->dev);
+    uint32_t* flag = ctx->flag + 1;
+    return sized(
+        ctx, dst, need,
+        [&] {
+            hipLaunchKernelGGL((k_list_fold<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
+                               po, pk, nidx, per_entry, need, flag);
+        },
+        [&](LV out) {
+            hipLaunchKernelGGL((k_list_fold<true>), dim3(R), dim3(64), 0, ctx->stream, S, out, po,
+                               pk, nidx, per_entry, need, flag);
+        },
+        "list_fold");
+}
+
+}  // extern "C"

@@ -138,6 +138,7 @@ const char* laspj_strerror(int s) {
         case LASPJ_E_RANGE: return "out of range";
         case LASPJ_E_COMM: return "communicator error";
         case LASPJ_E_UNSUPPORTED: return "unsupported";
+        case LASPJ_E_FUN: return "fun failed";
         default: return "unknown status";
     }
 }
@@ -189,6 +190,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->scratch) hipFree(ctx->scratch);
         if (ctx->flag) hipFree(ctx->flag);
         if (ctx->partials) hipFree(ctx->partials);
+        if (ctx->lscratch) hipFree(ctx->lscratch);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -382,7 +384,8 @@ int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batc
                               uint32_t nchunks) {
     if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
         return fail(ctx, LASPJ_E_INVAL, "reduce_chunks: bad batch");
-    if (dst->kind != src->kind) return fail(ctx, LASPJ_E_KIND, "reduce_chunks: kinds differ");
+    if (dst->kind != src->kind || laspj_is_list(dst->kind))
+        return fail(ctx, LASPJ_E_KIND, "reduce_chunks: kinds differ or list batch");
     if (nchunks == 0 || dst->words_per_replica != src->words_per_replica ||
         dst->elements != src->elements || dst->replicas * (uint64_t)nchunks != src->replicas)
         return fail(ctx, LASPJ_E_SHAPE, "reduce_chunks: need src replicas = nchunks x dst");
@@ -412,6 +415,8 @@ int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t first, uint64_t 
                        const void* host) {
     if (!same_ctx(ctx, b) || (!host && count))
         return fail(ctx, LASPJ_E_INVAL, "batch_upload: bad argument");
+    if (laspj_is_list(b->kind))
+        return fail(ctx, LASPJ_E_KIND, "batch_upload: list batches use laspj_list_upload");
     if (first > b->replicas || count > b->replicas - first)
         return fail(ctx, LASPJ_E_RANGE, "batch_upload: replicas [%llu, +%llu) out of %llu",
                     (unsigned long long)first, (unsigned long long)count,
@@ -428,6 +433,8 @@ int laspj_batch_download(laspj_ctx* ctx, const laspj_batch* b, uint64_t first,
                          uint64_t count, void* host) {
     if (!same_ctx(ctx, b) || (!host && count))
         return fail(ctx, LASPJ_E_INVAL, "batch_download: bad argument");
+    if (laspj_is_list(b->kind))
+        return fail(ctx, LASPJ_E_KIND, "batch_download: list batches use laspj_list_download");
     if (first > b->replicas || count > b->replicas - first)
         return fail(ctx, LASPJ_E_RANGE, "batch_download: replicas out of range");
     Guard g(ctx);
@@ -474,6 +481,8 @@ int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         return fail(ctx, LASPJ_E_INVAL, "batch_join: bad batch");
     if (a->kind != b->kind || dst->kind != a->kind)
         return fail(ctx, LASPJ_E_KIND, "batch_join: kinds differ");
+    if (laspj_is_list(a->kind))
+        return fail(ctx, LASPJ_E_KIND, "batch_join: list batches join with laspj_list_merge");
     if (a->replicas != b->replicas || dst->replicas != a->replicas ||
         a->words_per_replica != b->words_per_replica ||
         dst->words_per_replica != a->words_per_replica || a->elements != b->elements ||

@@ -543,3 +543,137 @@ class WrappedGCounterBatch(GCounterBatch):
 
     def __init__(self, ctx: Context, tensor, replicas: int, actors: int):
         _wrap(self, ctx, tensor, replicas, actors, 8 * actors)
+
+
+class ListBatch:
+    """R list-faithful values (LASPJ_KIND_ORSET_LIST / GSET_LIST, include/laspj.h "list
+    values"): entries in list order, key items and token runs.  Every method is one
+    C-ABI call; the list entry points size their outputs themselves."""
+
+    def __init__(self, ctx: Context, kind: int, replicas: int = 1, cap_entries: int = 1,
+                 cap_tokens: int = 1):
+        self.ctx, self.kind, self.replicas = ctx, kind, replicas
+        h = C.c_void_p()
+        check(ctx.L.laspj_list_batch_create(ctx.h, kind, replicas, cap_entries, cap_tokens,
+                                            C.byref(h)), ctx.h)
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_batch_destroy(self.h)
+            self.h = None
+
+    @property
+    def gset(self) -> bool:
+        return self.kind == _lib.KIND_GSET_LIST
+
+    def _like(self, kind: Optional[int] = None) -> "ListBatch":
+        return ListBatch(self.ctx, self.kind if kind is None else kind, self.replicas)
+
+    def counts(self) -> np.ndarray:
+        out = np.zeros((self.replicas, 2), dtype=np.uint32)
+        check(self.ctx.L.laspj_list_counts(self.ctx.h, self.h, out.ctypes.data), self.ctx.h)
+        return out
+
+    def upload(self, keys, toff=None, toks=None, replica: int = 0):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        n = len(keys)
+        if toff is None:
+            toff = np.zeros((n + 1,), dtype=np.uint32)
+        toff = np.ascontiguousarray(toff, dtype=np.uint32)
+        toks = np.ascontiguousarray(np.zeros((0,), np.uint64) if toks is None else toks,
+                                    dtype=np.uint64)
+        check(self.ctx.L.laspj_list_upload(self.ctx.h, self.h, replica, n,
+                                           keys.ctypes.data if n else None,
+                                           toff.ctypes.data,
+                                           toks.ctypes.data if len(toks) else None), self.ctx.h)
+        return self
+
+    def download(self, replica: int = 0):
+        """(keys u64[n], toff u32[n+1], toks u64[nt]) of one replica."""
+        n, nt = (int(x) for x in self.counts()[replica])
+        keys = np.zeros((max(n, 1),), dtype=np.uint64)
+        toff = np.zeros((n + 1,), dtype=np.uint32)
+        toks = np.zeros((max(nt, 1),), dtype=np.uint64)
+        check(self.ctx.L.laspj_list_download(self.ctx.h, self.h, replica, keys.ctypes.data,
+                                             toff.ctypes.data, toks.ctypes.data), self.ctx.h)
+        return keys[:n], toff, toks[:nt]
+
+    @classmethod
+    def from_set(cls, batch, elem_order: "Buffer", nslots: int,
+                 tok_order: Optional["Buffer"]) -> "ListBatch":
+        kind = _lib.KIND_GSET_LIST if batch.kind == _lib.KIND_GSET else _lib.KIND_ORSET_LIST
+        out = cls(batch.ctx, kind, batch.replicas)
+        check(batch.ctx.L.laspj_list_from_set(batch.ctx.h, out.h, batch.h, elem_order.h, nslots,
+                                              tok_order.h if tok_order is not None else None),
+              batch.ctx.h)
+        return out
+
+    def _binary(self, fn, other: "ListBatch", order) -> "ListBatch":
+        out = self._like()
+        args = (C.byref(order),) if order is not None else ()
+        check(fn(self.ctx.h, out.h, self.h, other.h, *args), self.ctx.h)
+        return out
+
+    # lasp_orset:merge/2, lasp_gset:merge/2 on lists
+    def merge(self, other: "ListBatch", order) -> "ListBatch":
+        return self._binary(self.ctx.L.laspj_list_merge, other, order)
+
+    def union(self, other: "ListBatch", order) -> "ListBatch":
+        return self._binary(self.ctx.L.laspj_list_union, other, order)
+
+    def intersection(self, other: "ListBatch", order) -> "ListBatch":
+        return self._binary(self.ctx.L.laspj_list_intersection, other, order)
+
+    def product(self, other: "ListBatch") -> "ListBatch":
+        return self._binary(self.ctx.L.laspj_list_product, other, None)
+
+    def equal(self, other: "ListBatch", order) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas)
+        check(self.ctx.L.laspj_list_equal(self.ctx.h, self.h, other.h, C.byref(order), buf.h),
+              self.ctx.h)
+        return buf.download(np.uint8).astype(bool)
+
+    def is_inflation_of(self, prev: "ListBatch", order, strict: bool = False) -> np.ndarray:
+        buf = self.ctx.buffer(self.replicas)
+        check(self.ctx.L.laspj_list_inflation(self.ctx.h, prev.h, self.h, int(strict),
+                                              C.byref(order), buf.h), self.ctx.h)
+        return buf.download(np.uint8).astype(bool)
+
+    def value(self) -> "ListBatch":
+        out = self._like(_lib.KIND_GSET_LIST)
+        check(self.ctx.L.laspj_list_value(self.ctx.h, out.h, self.h), self.ctx.h)
+        return out
+
+    def map(self, keys: np.ndarray, per_entry: bool) -> "ListBatch":
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        tab = self.ctx.buffer(max(8, keys.nbytes))
+        if len(keys):
+            tab.upload(keys)
+        out = self._like()
+        check(self.ctx.L.laspj_list_map(self.ctx.h, out.h, self.h, tab.h, len(keys),
+                                        int(per_entry)), self.ctx.h)
+        return out
+
+    def filter(self, keep: np.ndarray, per_entry: bool) -> "ListBatch":
+        keep = np.ascontiguousarray(keep, dtype=np.uint8)
+        tab = self.ctx.buffer(max(1, keep.nbytes))
+        if len(keep):
+            tab.upload(keep)
+        out = self._like()
+        check(self.ctx.L.laspj_list_filter(self.ctx.h, out.h, self.h, tab.h, len(keep),
+                                           int(per_entry)), self.ctx.h)
+        return out
+
+    def fold(self, off: np.ndarray, keys: np.ndarray, per_entry: bool) -> "ListBatch":
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        ob = self.ctx.buffer(off.nbytes)
+        ob.upload(off)
+        kb = self.ctx.buffer(max(8, keys.nbytes))
+        if len(keys):
+            kb.upload(keys)
+        out = self._like()
+        check(self.ctx.L.laspj_list_fold(self.ctx.h, out.h, self.h, ob.h, kb.h, len(off) - 1,
+                                         int(per_entry)), self.ctx.h)
+        return out

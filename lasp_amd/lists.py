@@ -1,0 +1,255 @@
+"""Host side of the list-faithful values (include/laspj.h "list values").
+
+A `ListSpace` keeps the device rank tables of one dictionary (codec.Domain): the term
+order of every element slot (krank) and of every token slot (grank, 64 per element
+slot), re-uploaded when the dictionary has grown.  `encode` / `decode` move a Lasp
+value written as a Python term to and from the list items; `map_table`,
+`filter_table` and `fold_table` evaluate a combinator's fun once per key (the NIF
+would call the Erlang fun the same way) and hand the device its results.
+
+Items (laspj.h): key = element slot, or LIST_PAIR | x << 31 | y for a product key
+{X, Y}; token = 64*e + k (token slot k of element slot e), or LIST_COMPOUND | gx << 31
+| gy for a product token [Tx, Ty]; bit 63 of a token = its flag.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _lib
+from .codec import Domain, NonCanonical
+from .terms import term_cmp, term_key
+
+PAIR = _lib.LIST_PAIR
+COMPOUND = _lib.LIST_COMPOUND
+REMOVED = _lib.LIST_REMOVED
+ID = (1 << 31) - 1
+FAILED = (1 << 64) - 1          # table entry of a key on which the fun raised
+
+
+class FunFailed(RuntimeError):
+    """The combinator's fun raised on a key of its input (the reference body crashes)."""
+
+
+class ListSpace:
+    """Rank tables of one Domain on one device context."""
+
+    def __init__(self, ctx, dom: Domain, tokens: bool = True):
+        self.ctx, self.dom, self.tokens = ctx, dom, tokens
+        self._sig = None
+        self._order = _lib.ListOrder()
+        self._bufs = ()
+        self._eorder = None
+        self._torder = None
+
+    def _signature(self):
+        d = self.dom
+        return (d.size, sum(len(t) for t in d.tokens[:d.size]) if self.tokens else 0)
+
+    def order(self) -> _lib.ListOrder:
+        """laspj_list_order over the current dictionary (refreshed when it grew)."""
+        sig = self._signature()
+        if sig != self._sig:
+            self._refresh()
+            self._sig = sig
+        return self._order
+
+    def _refresh(self):
+        d = self.dom
+        K = max(1, d.size)
+        krank = np.zeros((K,), dtype=np.uint32)
+        order = d.elements.order()
+        krank[order] = np.arange(len(order), dtype=np.uint32)
+        kb = self.ctx.buffer(krank.nbytes)
+        kb.upload(krank)
+        self._order.krank = kb.h.value
+        self._order.nkeys = K
+        bufs = [kb]
+        if self.tokens:
+            grank = np.zeros((64 * K,), dtype=np.uint32)
+            toks = [(t, 64 * e + k) for e, td in enumerate(d.tokens[:d.size])
+                    for k, t in enumerate(td.terms)]
+            toks.sort(key=lambda x: term_key(x[0]))
+            rank, prev = -1, None
+            for t, g in toks:
+                if prev is None or term_cmp(prev[0], t) != 0:
+                    rank += 1
+                    prev = (t,)
+                grank[g] = rank
+            gb = self.ctx.buffer(grank.nbytes)
+            gb.upload(grank)
+            self._order.grank = gb.h.value
+            self._order.ntokens = 64 * K
+            bufs.append(gb)
+        else:
+            self._order.grank = None
+            self._order.ntokens = 0
+        self._bufs = tuple(bufs)         # keep the buffers alive with the order
+
+    def set_orders(self, E: int):
+        """(elem_order buffer, nslots, tok_order buffer) for laspj_list_from_set over a
+        dense batch of E element slots."""
+        d = self.dom
+        order = d.elements.order().astype(np.uint32)
+        eb = self.ctx.buffer(max(4, order.nbytes))
+        if len(order):
+            eb.upload(order)
+        tb = None
+        if self.tokens:
+            tord = np.full((E, 64), 0xFF, dtype=np.uint8)
+            for e, td in enumerate(d.tokens[:min(d.size, E)]):
+                o = td.order()
+                tord[e, :len(o)] = o
+            tb = self.ctx.buffer(tord.nbytes)
+            tb.upload(tord.reshape(-1))
+        return eb, len(order), tb
+
+
+# ------------------------------------------------------------------- items <-> terms
+
+def _key_item(dom: Domain, key, pairs: bool) -> int:
+    if pairs and isinstance(key, tuple) and len(key) == 2:
+        return PAIR | (dom.element_slot(key[0]) << 31) | dom.element_slot(key[1])
+    return dom.element_slot(key)
+
+
+def _key_term(dom: Domain, item: int):
+    if item & PAIR:
+        return (dom.elements.terms[(item >> 31) & ID], dom.elements.terms[item & ID])
+    return dom.elements.terms[item & ID]
+
+
+def _tok_term(dom: Domain, item: int):
+    if item & COMPOUND:
+        gx, gy = (item >> 31) & ID, item & ID
+        return [dom.tokens[gx >> 6].terms[gx & 63], dom.tokens[gy >> 6].terms[gy & 63]]
+    g = item & ID
+    return dom.tokens[g >> 6].terms[g & 63]
+
+
+def encode(dom: Domain, term, gset: bool, pairs: bool = False):
+    """A Lasp value (any list: orddict-shaped or not) -> (keys, toff, toks) items.
+    With `pairs`, 2-tuple keys become product key items and, under them, 2-list tokens
+    product token items (the shape product outputs have)."""
+    if not isinstance(term, list):
+        raise NonCanonical("a set value is a list")
+    keys = np.zeros((len(term),), dtype=np.uint64)
+    if gset:
+        for i, e in enumerate(term):
+            keys[i] = _key_item(dom, e, pairs)
+        return keys, None, None
+    toff = np.zeros((len(term) + 1,), dtype=np.uint32)
+    toks = []
+    for i, entry in enumerate(term):
+        if not (isinstance(entry, tuple) and len(entry) == 2 and isinstance(entry[1], list)):
+            raise NonCanonical(f"entry {entry!r} is not {{Key, [{{Token, Bool}}]}}")
+        k, ts = entry
+        item = _key_item(dom, k, pairs)
+        keys[i] = item
+        for t in ts:
+            if not (isinstance(t, tuple) and len(t) == 2 and isinstance(t[1], bool)):
+                raise NonCanonical(f"token entry {t!r} is not {{Token, Bool}}")
+            tok, flag = t
+            if item & PAIR and isinstance(tok, list) and len(tok) == 2:
+                x, y = (item >> 31) & ID, item & ID
+                g = COMPOUND | ((64 * x + dom.token_slot(x, tok[0])) << 31) | \
+                    (64 * y + dom.token_slot(y, tok[1]))
+            else:
+                e = item & ID if not item & PAIR else None
+                if e is None:
+                    raise NonCanonical("a product key's tokens are [Tx, Ty] pairs")
+                g = 64 * e + dom.token_slot(e, tok)
+            toks.append(g | (REMOVED if flag else 0))
+        toff[i + 1] = len(toks)
+    return keys, toff, np.asarray(toks, dtype=np.uint64)
+
+
+def decode(dom: Domain, keys, toff, toks, gset: bool) -> list:
+    if gset:
+        return [_key_term(dom, int(k)) for k in keys]
+    out = []
+    for i, k in enumerate(keys):
+        run = toks[int(toff[i]):int(toff[i + 1])]
+        out.append((_key_term(dom, int(k)),
+                    [(_tok_term(dom, int(t)), bool(int(t) & REMOVED)) for t in run]))
+    return out
+
+
+# ------------------------------------------------------------------- fun tables
+
+class FunCache:
+    """Results of one combinator fun per key term (the fun is fixed for a process, so
+    each key is evaluated once over the process's life)."""
+
+    def __init__(self, fun: Callable):
+        self.fun = fun
+        self.cache = {}
+
+    def __call__(self, x):
+        from .terms import hkey
+        k = hkey(x)
+        if k not in self.cache:
+            try:
+                self.cache[k] = (True, self.fun(x))
+            except Exception as e:           # the reference body would crash on x
+                self.cache[k] = (False, e)
+        return self.cache[k]
+
+
+def _arg(term, gset: bool):
+    """What the body passes to the fun, and the tail it re-attaches: lasp_core matches
+    `{X, Causality}` before `X` (lasp_core.erl:467-474, 648-655, 688-695), so a G-Set
+    element that is a 2-tuple goes through the OR-Set branch."""
+    if gset and isinstance(term, tuple) and len(term) == 2:
+        return term[0], (term[1],)
+    return term, None
+
+
+def map_table(dom: Domain, fun: FunCache, terms, gset: bool) -> np.ndarray:
+    out = np.zeros((len(terms),), dtype=np.uint64)
+    for i, t in enumerate(terms):
+        x, tail = _arg(t, gset)
+        ok, v = fun(x)
+        if not ok:
+            out[i] = FAILED
+            continue
+        out[i] = dom.element_slot(v if tail is None else (v,) + tail)
+    return out
+
+
+def filter_table(fun: FunCache, terms, gset: bool) -> np.ndarray:
+    """keep = 1 when F(V) =:= true, V = the key (OR-Set) or the element (G-Set; its
+    first component when it is a 2-tuple, lasp_core.erl:688-695); 2 when F raised."""
+    out = np.zeros((len(terms),), dtype=np.uint8)
+    for i, t in enumerate(terms):
+        x = _arg(t, gset)[0]
+        ok, v = fun(x)
+        out[i] = 2 if not ok else (1 if v is True else 0)
+    return out
+
+
+def fold_table(dom: Domain, fun: FunCache, terms, gset: bool):
+    off = np.zeros((len(terms) + 1,), dtype=np.uint32)
+    keys = []
+    for i, t in enumerate(terms):
+        x, tail = _arg(t, gset)
+        ok, v = fun(x)
+        if ok and not isinstance(v, list):
+            ok = False                       # a generator over a non-list crashes
+        if not ok:
+            keys.append(FAILED)
+        else:
+            keys.extend(dom.element_slot(y if tail is None else (y,) + tail) for y in v)
+        off[i + 1] = len(keys)
+    return off, np.asarray(keys, dtype=np.uint64)
+
+
+def table_terms(dom: Domain, lst, pairs: bool):
+    """(terms, per_entry): a table per element slot of the dictionary (no download);
+    product outputs (pair keys) get one per entry of the list (its keys downloaded)."""
+    if pairs:
+        keys, _o, _t = lst.download()
+        return [_key_term(dom, int(k)) for k in keys], True
+    return list(dom.elements.terms), False

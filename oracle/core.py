@@ -111,16 +111,39 @@ def union_body(type_, lvalue, rvalue):
     raise ValueError(type_)
 
 
+def _entry(element):
+    """The bodies' `case Element of {X, Causality} -> ...; X -> ... end`: any 2-tuple
+    takes the first (OR-Set) branch, whatever the type (lasp_core.erl:467-474,
+    513-521, 560-576, 648-655, 688-695)."""
+    if isinstance(element, tuple) and len(element) == 2:
+        return element
+    return None
+
+
+def _append(acc, values):
+    """`Acc ++ Values`: Values must be a proper list here (an improper result is not a
+    Lasp value; the oracle treats it as the crash it becomes at the next merge)."""
+    if not isinstance(values, list):
+        raise TypeError("badarg: ++ with a non-list")
+    return acc + values
+
+
 def intersection_body(type_, lvalue, rvalue):
     """intersection/7 body — lasp_core.erl:546-589."""
     if lvalue is None or rvalue is None:
         return None
     acc = []
     for element in lvalue:
-        if type_ == "lasp_orset":
-            x, xc = element
+        e = _entry(element)
+        if e is not None:
+            x, xc = e
             found = otp.lists_keyfind(x, rvalue)
-            vals = [] if found is False else [(x, lattice.orset_causal_union(xc, found[1]))]
+            if found is False:
+                vals = []
+            else:
+                if not isinstance(xc, list):
+                    raise TypeError("badarg: ++ on a non-list")
+                vals = [(x, lattice.orset_causal_union(xc, _append([], found[1])))]
         else:
             vals = [element] if otp.lists_member(element, rvalue) else []
         acc = acc + vals
@@ -128,14 +151,19 @@ def intersection_body(type_, lvalue, rvalue):
 
 
 def product_body(type_, lvalue, rvalue):
-    """product/7 body — lasp_core.erl:499-533 (X-major)."""
+    """product/7 body — lasp_core.erl:499-533 (X-major).  The OR-Set branch's generator
+    `{Y, YCausality} <- RValue` skips elements of R that are not 2-tuples."""
     if lvalue is None or rvalue is None:
         return None
     acc = []
     for element in lvalue:
-        if type_ == "lasp_orset":
-            x, xc = element
-            vals = [((x, y), lattice.orset_causal_product(xc, yc)) for y, yc in rvalue]
+        e = _entry(element)
+        if e is not None:
+            x, xc = e
+            if not isinstance(xc, list):
+                raise TypeError("function_clause: lists:foldl on a non-list")
+            vals = [((x, y), lattice.orset_causal_product(xc, yc))
+                    for y, yc in (t for t in rvalue if _entry(t) is not None)]
         else:
             vals = [(element, y) for y in rvalue]
         acc = acc + vals
@@ -146,11 +174,8 @@ def map_body(type_, fun, value):
     """map/6 body — lasp_core.erl:641-667."""
     acc = []
     for element in value:
-        if type_ == "lasp_orset":
-            x, c = element
-            acc = acc + [(fun(x), c)]
-        else:
-            acc = acc + [fun(element)]
+        e = _entry(element)
+        acc = acc + [(fun(e[0]), e[1]) if e is not None else fun(element)]
     return acc
 
 
@@ -158,7 +183,8 @@ def filter_body(type_, fun, value):
     """filter/6 body — lasp_core.erl:681-712 (keeps tombstoned OR-Set elements)."""
     acc = []
     for element in value:
-        v = element[0] if type_ == "lasp_orset" else element
+        e = _entry(element)
+        v = e[0] if e is not None else element
         if fun(v) is True:
             acc = acc + [element]
     return acc
@@ -168,12 +194,16 @@ def fold_body(type_, fun, value):
     """fold/6 body — lasp_core.erl:460-486."""
     acc = []
     for element in value:
-        if type_ == "lasp_orset":
-            x, c = element
-            vals = [(v, c) for v in fun(x)]
+        e = _entry(element)
+        if e is not None:
+            x, c = e
+            vals = fun(x)
+            if not isinstance(vals, list):
+                raise TypeError("bad generator: a list comprehension over a non-list")
+            vals = [(v, c) for v in vals]
         else:
-            vals = list(fun(element))
-        acc = acc + vals
+            vals = fun(element)
+        acc = _append(acc, vals)
     return acc
 
 
@@ -260,14 +290,29 @@ class Store:
             changed = True
             while changed:
                 changed = False
-                for proc in self.procs:
+                for proc in list(self.procs):
                     for i in proc["inputs"]:
                         dv = self.vars[i]
                         last = proc["seen"][i]
                         th = ("strict", type_mod(dv["type"]).new() if last is None else last)
+                        if proc not in self.procs:
+                            break
+                        if last is dv["value"]:
+                            # nothing was written since the process read it.  (A list
+                            # with repeated keys can be a strict inflation of itself —
+                            # keyfind pairs a later entry with the first one, whose ids
+                            # differ — and the reference's reader then re-fires forever;
+                            # this synchronous model re-runs once per write instead.)
+                            continue
                         if lattice.threshold_met(dv["type"], dv["value"], th):
                             proc["seen"][i] = dv["value"]
-                            proc["body"](proc["seen"])
+                            try:
+                                proc["body"](proc["seen"])
+                            except Exception:
+                                # Function(Scope) raised: the lasp_process dies and binds
+                                # nothing (its supervisor's restarts re-read from scratch
+                                # and crash the same way; lasp_process_sup.erl:57-60)
+                                self.procs.remove(proc)
                             changed = True
         finally:
             self._depth -= 1

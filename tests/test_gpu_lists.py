@@ -1,0 +1,174 @@
+"""List-faithful values on the device (laspj_list_*) against the oracle, on lists that
+are NOT orddicts: unsorted and repeated keys, unsorted and repeated tokens, product
+pairs — the values lasp_core's combinator bodies bind and then merge on every re-run
+(lasp_core.erl:292-303, 460-712; lasp_orset.erl:128-134; lasp_gset.erl:99-101;
+lasp_lattice.erl:137-161, 212-253, 277-312).  Each case encodes the oracle's list,
+runs one entry point, decodes and compares as terms (exact_eq)."""
+
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from oracle import core as ocore, gset as ogset, lattice as olat, orset as oorset
+from oracle.terms import exact_eq
+
+pytestmark = pytest.mark.gpu
+
+TOK = st.sampled_from([b"t%02d" % i + b"\x00" * 17 for i in range(7)])
+KEY = st.integers(min_value=-3, max_value=9)
+ENTRY = st.tuples(KEY, st.lists(st.tuples(TOK, st.booleans()), max_size=5))
+OLIST = st.lists(ENTRY, max_size=10)
+GLIST = st.lists(KEY, max_size=12)
+SETTINGS = settings(max_examples=60, deadline=None,
+                    suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+
+
+class Space:
+    def __init__(self, gset=False):
+        from lasp_amd import engine, lists as L
+        from lasp_amd.codec import Domain
+        from lasp_amd.orset import context
+        self.ctx, self.L, self.engine, self.gset = context(), L, engine, gset
+        self.dom = Domain()
+        self.space = L.ListSpace(self.ctx, self.dom, tokens=not gset)
+
+    def enc(self, term, pairs=False):
+        from lasp_amd import _lib
+        kind = _lib.KIND_GSET_LIST if self.gset else _lib.KIND_ORSET_LIST
+        keys, toff, toks = self.L.encode(self.dom, term, self.gset, pairs)
+        return self.engine.ListBatch(self.ctx, kind).upload(keys, toff, toks)
+
+    def dec(self, lb, gset=None):
+        keys, toff, toks = lb.download()
+        return self.L.decode(self.dom, keys, toff, toks, self.gset if gset is None else gset)
+
+    @property
+    def order(self):
+        return self.space.order()
+
+
+@SETTINGS
+@given(OLIST, OLIST)
+def test_orset_list_merge_equal_inflation(a, b):
+    """merge/2 as written on unsorted lists, =:=, is_inflation / is_strict_inflation."""
+    s = Space()
+    A, B = s.enc(a), s.enc(b)
+    m = oorset.merge(a, b)
+    M = A.merge(B, s.order)
+    assert exact_eq(s.dec(M), m), (a, b)
+    for p, c, P, C in ((a, m, A, M), (b, m, B, M), (a, b, A, B), (m, a, M, A), (a, a, A, A)):
+        assert bool(C.is_inflation_of(P, s.order)[0]) == olat.is_inflation("lasp_orset", p, c)
+        assert bool(C.is_inflation_of(P, s.order, strict=True)[0]) == \
+            olat.is_strict_inflation("lasp_orset", p, c), (p, c)
+        assert bool(P.equal(C, s.order)[0]) == exact_eq(p, c)
+    assert [x for x in s.dec(M.value(), gset=True)] == oorset.value(m)
+
+
+@SETTINGS
+@given(GLIST, GLIST)
+def test_gset_list_merge_equal_inflation(a, b):
+    """ordsets:union with OTP 17's argument switch on unsorted / repeated lists."""
+    s = Space(gset=True)
+    A, B = s.enc(a), s.enc(b)
+    m = ogset.merge(a, b)
+    M = A.merge(B, s.order)
+    assert exact_eq(s.dec(M), m), (a, b)
+    for p, c, P, C in ((a, m, A, M), (b, m, B, M), (a, b, A, B), (m, a, M, A)):
+        assert bool(C.is_inflation_of(P, s.order)[0]) == olat.is_inflation("lasp_gset", p, c)
+        assert bool(C.is_inflation_of(P, s.order, strict=True)[0]) == \
+            olat.is_strict_inflation("lasp_gset", p, c)
+        assert bool(P.equal(C, s.order)[0]) == exact_eq(p, c)
+
+
+@SETTINGS
+@given(OLIST, OLIST)
+def test_orset_list_bodies(a, b):
+    """union (keep-left orddict:merge), intersection (keyfind, Cx ++ Cy), product
+    (reversed token pairs), map / filter / fold over unsorted lists."""
+    s = Space()
+    A, B = s.enc(a), s.enc(b)
+    assert exact_eq(s.dec(A.union(B, s.order)), ocore.union_body("lasp_orset", a, b))
+    assert exact_eq(s.dec(A.intersection(B, s.order)),
+                    ocore.intersection_body("lasp_orset", a, b))
+    P = A.product(B)
+    assert exact_eq(s.dec(P), ocore.product_body("lasp_orset", a, b))
+    L = s.L
+    for fun in (lambda x: -x, lambda x: x // 3, lambda x: x * 2):
+        fc = L.FunCache(fun)
+        terms, per_entry = L.table_terms(s.dom, A, False)
+        got = A.map(L.map_table(s.dom, fc, terms, False), per_entry)
+        assert exact_eq(s.dec(got), ocore.map_body("lasp_orset", fun, a))
+    even = lambda x: x % 2 == 0          # noqa: E731
+    terms, per_entry = L.table_terms(s.dom, A, False)
+    got = A.filter(L.filter_table(L.FunCache(even), terms, False), per_entry)
+    assert exact_eq(s.dec(got), ocore.filter_body("lasp_orset", even, a))
+    for fun in (lambda x: [x, x, x], lambda x: [] if x % 2 else [x, -x]):
+        terms, per_entry = L.table_terms(s.dom, A, False)
+        off, keys = L.fold_table(s.dom, L.FunCache(fun), terms, False)
+        assert exact_eq(s.dec(A.fold(off, keys, per_entry)), ocore.fold_body("lasp_orset", fun, a))
+    # over the product output: pair keys, tables per entry
+    terms, per_entry = L.table_terms(s.dom, P, True)
+    assert per_entry
+    swap = lambda k: (k[1], k[0])         # noqa: E731
+    got = P.map(L.map_table(s.dom, L.FunCache(swap), terms, False), per_entry)
+    assert exact_eq(s.dec(got), ocore.map_body("lasp_orset", swap, ocore.product_body(
+        "lasp_orset", a, b)))
+
+
+@SETTINGS
+@given(GLIST, GLIST)
+def test_gset_list_bodies(a, b):
+    s = Space(gset=True)
+    A, B = s.enc(a), s.enc(b)
+    assert exact_eq(s.dec(A.union(B, s.order)), ocore.union_body("lasp_gset", a, b))
+    assert exact_eq(s.dec(A.intersection(B, s.order)),
+                    ocore.intersection_body("lasp_gset", a, b))
+    P = A.product(B)
+    assert exact_eq(s.dec(P), ocore.product_body("lasp_gset", a, b))
+    L = s.L
+    # a G-Set of pairs goes down the {X, Causality} branch of map / filter / fold
+    prod = ocore.product_body("lasp_gset", a, b)
+    terms, per_entry = L.table_terms(s.dom, P, True)
+    inc = lambda x: x + 1                 # noqa: E731
+    got = P.map(L.map_table(s.dom, L.FunCache(inc), terms, True), per_entry)
+    assert exact_eq(s.dec(got), ocore.map_body("lasp_gset", inc, prod))
+    pos = lambda x: x > 0                 # noqa: E731
+    got = P.filter(L.filter_table(L.FunCache(pos), terms, True), per_entry)
+    assert exact_eq(s.dec(got), ocore.filter_body("lasp_gset", pos, prod))
+    dup = lambda x: [x, x]                # noqa: E731
+    off, keys = L.fold_table(s.dom, L.FunCache(dup), terms, True)
+    assert exact_eq(s.dec(P.fold(off, keys, per_entry)), ocore.fold_body("lasp_gset", dup, prod))
+
+
+def test_list_from_set_and_edges():
+    """canonical batches convert to their lists; empty lists; a fun that fails on a key
+    in the list reports E_FUN, one that fails on a key not in the list does not."""
+    from lasp_amd import _lib
+    s = Space()
+    t = oorset.TokenSource(3)
+    v = oorset.new()
+    for op in (("add", 5), ("add", 1), ("add", 5), ("remove", 1), ("add", 3)):
+        v = oorset.update(op, None, v, t)[1]
+    b = s.ctx.orset_batch(1, 16)
+    b.upload(s.dom.encode_orset([v], 16))
+    eb, n, tb = s.space.set_orders(16)
+    lb = s.engine.ListBatch.from_set(b, eb, n, tb)
+    assert exact_eq(s.dec(lb), v)
+    E = s.enc([])
+    assert s.dec(E.merge(lb, s.order)) == s.dec(lb)
+    assert bool(lb.is_inflation_of(E, s.order, strict=True)[0])
+    assert not bool(E.is_inflation_of(E, s.order, strict=True)[0])
+    L = s.L
+    boom = lambda x: 1 // (x - 3)         # noqa: E731   raises on 3 only
+    terms, per_entry = L.table_terms(s.dom, lb, False)
+    with pytest.raises(_lib.LaspjError) as ei:
+        lb.map(L.map_table(s.dom, L.FunCache(boom), terms, False), per_entry)
+    assert ei.value.status == _lib.E_FUN
+    lb2 = s.enc([(5, [(b"x" * 20, False)])])
+    terms, per_entry = L.table_terms(s.dom, lb2, False)
+    got = lb2.map(L.map_table(s.dom, L.FunCache(boom), terms, False), per_entry)
+    assert exact_eq(s.dec(got), [(0, [(b"x" * 20, False)])])
+    # product of a product output: nested pairs are refused, not mis-encoded
+    P = lb.product(lb)
+    with pytest.raises(_lib.LaspjError) as ei:
+        P.product(lb)
+    assert ei.value.status == _lib.E_UNSUPPORTED

@@ -72,28 +72,46 @@ def test_bodies_random(lops, rops):
 
 STEP = st.one_of(
     st.tuples(st.just("update"), st.integers(0, 1), OP),
-    st.tuples(st.just("bind"), st.integers(0, 1), SET))
+    st.tuples(st.just("bind"), st.integers(0, 1), SET),
+    st.tuples(st.just("gadd"), st.integers(0, 1), st.lists(ELEM, min_size=1, max_size=4)),
+    st.tuples(st.just("gbind"), st.integers(0, 1), st.lists(ELEM, max_size=6)))
+
+
+def _setup(store):
+    """Two OR-Set inputs and two G-Set inputs feeding every combinator, including the
+    ones whose outputs are not orddicts (intersection, product, a non-monotone map, the
+    G-Set `L ++ R` union) and processes chained onto those outputs; every input change
+    re-runs them, so each output is re-bound (merged into its previous value) again
+    and again."""
+    ids = [store.declare("lasp_orset")[1] for _ in range(10)]
+    a, b, u, x, p, f, m, fo, mx, ux = ids
+    store.union(a, b, u)
+    store.intersection(a, b, x)
+    store.product(a, b, p)
+    store.filter(a, lambda v: v % 2 == 0, f)
+    store.map(b, lambda v: v % 3, m)                      # non-monotone, collapsing
+    store.fold(a, lambda v: [v, -v], fo)                  # unsorted output keys
+    store.map(x, lambda v: -v, mx)                        # chained on a list value
+    store.union(m, fo, ux)                                # keep-left merge of lists
+    gids = [store.declare("lasp_gset")[1] for _ in range(6)]
+    ga, gb, gu, gx, gm, gf = gids
+    store.union(ga, gb, gu)                               # L ++ R
+    store.intersection(ga, gb, gx)
+    store.map(gu, lambda v: v // 2, gm)
+    store.filter(gu, lambda v: v > 0, gf)
+    return ids, gids
 
 
 @settings(max_examples=25 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(STEP, max_size=10))
 def test_store_random(steps):
-    """Two inputs feeding union / filter / map (monotone) / fold (non-decreasing keys):
-    after every step each variable decodes to the oracle store's value."""
+    """After every step each variable — inputs and every combinator output, list values
+    included — decodes to the oracle store's value, term for term."""
     from lasp_amd import core as dcore
-    ds, os_ = dcore.Store(capacity=128), ocore.Store(tokens=oorset.TokenSource(9))
+    ds, os_ = dcore.Store(capacity=256), ocore.Store(tokens=oorset.TokenSource(9))
     toks = oorset.TokenSource(5)
-
-    def setup(store):
-        ids = [store.declare("lasp_orset")[1] for _ in range(6)]
-        a, b, u, f, m, fo = ids
-        store.union(a, b, u)
-        store.filter(a, lambda x: x % 2 == 0, f)
-        store.map(b, lambda x: 3 * x, m)
-        store.fold(a, lambda x: [x, x], fo)
-        return ids
-    idd, ido = setup(ds), setup(os_)
-    for step in steps:
+    (idd, gdd), (ido, gdo) = _setup(ds), _setup(os_)
+    for n, step in enumerate(steps):
         kind, var = step[0], step[1]
         if kind == "update":
             op = step[2]
@@ -107,9 +125,36 @@ def test_store_random(steps):
                     ds.update(idd[var], op, None)
                 continue
             ds.update(idd[var], op, None)
-        else:
-            term = build(step[2], 100 + len(steps))
+        elif kind == "bind":
+            term = build(step[2], 100 + n)
             os_.bind(ido[var], term)
             ds.bind(idd[var], term)
-        for i_d, i_o in zip(idd, ido):
+        elif kind == "gadd":
+            os_.update(gdo[var], ("add_all", step[2]), None)
+            ds.update(gdd[var], ("add_all", step[2]), None)
+        else:
+            term = sorted(set(step[2]))
+            os_.bind(gdo[var], term)
+            ds.bind(gdd[var], term)
+        for i_d, i_o in list(zip(idd, ido)) + list(zip(gdd, gdo)):
             assert exact_eq(ds.value(i_d), os_.value(i_o)), (step, ds.value(i_d), os_.value(i_o))
+        assert len(ds.procs) == len(os_.procs)
+
+
+def test_store_rebinds_intersection_twice():
+    """The VERDICT's example: re-binding an intersection output merges `Cx ++ Cy` lists
+    with orddict:merge's two-finger walk and keeps the duplicated token."""
+    from lasp_amd import core as dcore
+    from oracle.terms import Atom
+    ds, os_ = dcore.Store(capacity=64), ocore.Store()
+    t = [bytes([i]) * 20 for i in range(8)]
+    for st_ in (ds, os_):
+        a, b, x = (st_.declare("lasp_orset")[1] for _ in range(3))
+        st_.intersection(a, b, x)
+        st_.update(a, ("add_by_token", t[3], 1), Atom("a"))
+        st_.update(b, ("add_by_token", t[1], 1), Atom("a"))     # x = [{1, [t3, t1]}]
+        st_.update(a, ("add_by_token", t[5], 1), Atom("a"))     # new output [t3, t5, t1]
+        st_.result = st_.value(x)                               # merged: [t3, t1, t5, t1]
+    assert exact_eq(ds.result, os_.result)
+    toks = [tok for tok, _f in os_.result[0][1]]
+    assert len(toks) != len(set(toks)), "the reference's merge duplicates a token here"
