@@ -67,75 +67,105 @@ def parse():
 XGMI_LINK_GBS = 153.0        # per link per direction
 
 
+def _uid(rank):
+    """A communicator id made on rank 0 and handed to every rank over the gloo group
+    (the NIF would send it over Erlang distribution)."""
+    import torch.distributed as dist
+    from lasp_amd.engine import Comm
+    box = [Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def _sampled_join_ok(ctx, state, make, join, seed0, world, objects):
+    """Objects spread over every chunk: the state after a round must equal the join of
+    all ranks' synthetic replicas of that object (computed here from the streams)."""
+    import numpy as np
+    picks = sorted({int(x) for x in np.linspace(0, objects - 1, 16)})
+    exp, tmp = make(), make()
+    for o in picks:
+        exp.clear()
+        for r in range(world):
+            tmp.fill_synthetic(seed0 + r, replica_base=o)
+            join(exp, exp, tmp)
+        if not np.array_equal(state.download(o, 1), exp.download()):
+            return False
+    return True
+
+
 def antientropy_leg(ctx, args, rank, world, barrier):
-    """BASELINE config 3: every rank holds one replica of `objects` OR-Sets; a round
-    leaves every rank with the join of all ranks' replicas (lasp_amd.gossip)."""
-    import datetime
+    """BASELINE config 3 through the C ABI (laspj_antientropy, RCCL over xGMI): every
+    rank holds one replica of `objects` OR-Sets; a round (all-to-all -> HIP OR of the
+    copies -> all-gather, all on the engine stream) leaves every rank with the join of
+    all ranks' replicas."""
     import torch
     import torch.distributed as dist
-    from lasp_amd.gossip import DeviceAntiEntropy
-    g = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+    from lasp_amd.engine import Comm
+    comm = Comm(ctx, world, _uid(rank), rank)
     O, E = args.ae_objects, args.elements
-    ae = DeviceAntiEntropy(ctx, O, E, group=g)
-    ae.fill(10 + rank)
-    ae.round()                                   # warm-up (RCCL connection setup)
+    st, rv, ch = ctx.orset_batch(O, E), ctx.orset_batch(O, E), ctx.orset_batch(O // world, E)
+    st.fill_synthetic(10 + rank)
+    ctx.synchronize()
+    comm.antientropy(st, rv, ch)                 # warm-up round (RCCL connection setup)
+    ctx.synchronize()
+    ok = _sampled_join_ok(ctx, st, lambda: ctx.orset_batch(1, E),
+                          lambda d, a, b: d.join(a, b), 10, world, O)
     barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.ae_rounds):
-        ae.round()
-    torch.cuda.synchronize()
+        comm.antientropy(st, rv, ch)
+    ctx.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64)
+    t = torch.tensor([wall, 0.0 if ok else 1.0], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    per_round = float(t.item()) / args.ae_rounds
-    S = ae.bytes
+    per_round = float(t[0].item()) / args.ae_rounds
+    S = st.nbytes
     xgmi = 2.0 * (world - 1) / world * S / per_round / 1e9 if world > 1 else 0.0
     out = {
-        "workload": "gossip anti-entropy (BASELINE configs[2]): all_to_all + HIP OR + all_gather",
+        "workload": "gossip anti-entropy (BASELINE configs[2]) via laspj_antientropy: "
+                    "RCCL all-to-all + HIP OR + RCCL all-gather on the engine stream",
         "objects_per_gpu": O, "elements": E, "state_bytes_per_gpu": S,
         "rounds": args.ae_rounds, "ms_per_round": per_round * 1e3,
         "merged_elements_per_s": (world - 1) * O * E / per_round,
         "xgmi_GBps_per_gpu": xgmi,
         "frac_mesh": xgmi / (XGMI_LINK_GBS * 7), "frac_ring": xgmi / XGMI_LINK_GBS,
+        "converged": t[1].item() == 0.0,
     }
-    del ae
-    out["gcounter"] = gcounter_leg(ctx, args, rank, world, barrier, g)
+    del st, rv, ch
+    out["gcounter"] = gcounter_leg(ctx, args, rank, world, barrier, comm)
+    comm.close()
     return out
 
 
-def gcounter_leg(ctx, args, rank, world, barrier, g):
-    """G-Counter anti-entropy: one RCCL all_reduce(MAX) per round (riak_dt_gcounter's
-    join is the per-actor max); afterwards every rank must hold the owners' totals."""
+def gcounter_leg(ctx, args, rank, world, barrier, comm):
+    """G-Counter anti-entropy: one RCCL all_reduce(max) on uint64 counts per round
+    (riak_dt_gcounter's join is the per-actor max); afterwards sampled counters must be
+    the max over every rank's synthetic replica, and threshold reads run on the result."""
     import torch
     import torch.distributed as dist
-    from lasp_amd.gossip import DeviceGCounterAntiEntropy
     O, A = args.gc_objects, 64
-    gc = DeviceGCounterAntiEntropy(ctx, O, A, group=g)
-    gc.fill(rank, world)
-    gc.round()
-    gc.fill(rank, world)
+    gc = ctx.gcounter_batch(O, A)
+    gc.fill_synthetic(20 + rank)
+    comm.antientropy(gc)
+    ctx.synchronize()
+    ok = _sampled_join_ok(ctx, gc, lambda: ctx.gcounter_batch(1, A),
+                          lambda d, a, b: d.join(a, b), 20, world, O)
     barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.ae_rounds):
-        gc.round()
-    torch.cuda.synchronize()
+        comm.antientropy(gc)
+    ctx.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    o = torch.arange(O, device=gc.state.device, dtype=torch.int64)
-    a = torch.arange(A, device=gc.state.device, dtype=torch.int64)
-    total = (o[:, None] * 7919 + a[None, :] * 104729) % 100003 + 8
-    ok = bool(torch.equal(gc.state.view(O, A), total))
-    reached = int(gc.batch.threshold_met(64 * 8).sum())     # threshold reads after gossip
+    reached = int(gc.threshold_met(64 * (1 << 19)).sum())     # threshold reads after gossip
     t = torch.tensor([wall, 0.0 if ok else 1.0], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     per_round = float(t[0].item()) / args.ae_rounds
-    busbw = 2.0 * (world - 1) / world * gc.bytes / per_round / 1e9 if world > 1 else 0.0
+    busbw = 2.0 * (world - 1) / world * gc.nbytes / per_round / 1e9 if world > 1 else 0.0
     return {
-        "workload": "G-Counter anti-entropy: RCCL all_reduce(MAX) on int64 counts",
-        "objects_per_gpu": O, "actors": A, "state_bytes_per_gpu": gc.bytes,
+        "workload": "G-Counter anti-entropy: RCCL all_reduce(max) on uint64 counts",
+        "objects_per_gpu": O, "actors": A, "state_bytes_per_gpu": gc.nbytes,
         "ms_per_round": per_round * 1e3, "converged": t[1].item() == 0.0,
         "threshold_objects": reached,
         "merged_counts_per_s": (world - 1) * O * A / per_round,
@@ -362,7 +392,8 @@ def main():
             out["antientropy"] = ae
     else:
         ae = {}
-    ae_failed = "error" in ae or not ae.get("gcounter", {}).get("converged", True)
+    ae_failed = "error" in ae or not ae.get("converged", True) or \
+        not ae.get("gcounter", {}).get("converged", True)
 
     if rank != 0:
         if ae_failed:                    # a peer may be gone: no final barrier

@@ -399,6 +399,41 @@ int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dic
                          int tag, int vers, const laspj_buf* payload,
                          const laspj_buf* offsets, laspj_buf* status);
 
+/* ------------------------------------------------------------------ anti-entropy */
+/* Gossip anti-entropy across GPUs over RCCL (xGMI) — the reference's N-way merge and
+ * read-repair (lasp_update_fsm.erl:174-216, lasp_bind_fsm.erl:170-212) and coverage
+ * reduce (lasp_execute_coverage_fsm.erl:59-62) as one all-reduce with the lattice's
+ * join.  Every rank holds one replica of each of R objects (a batch with R replicas);
+ * after a round every rank holds the join of all ranks' replicas of every object.
+ *   OR-Set / G-Set: grouped ncclSend/ncclRecv all-to-all (rank j receives every rank's
+ *     copy of object chunk j, objects chunk-major: rank j owns objects
+ *     [j*R/n, (j+1)*R/n)), the reduce_chunks kernel (OR over the n copies), then
+ *     ncclAllGather of the joined chunks — RCCL has no bitwise-OR reduction;
+ *   G-Counter: one ncclAllReduce(ncclMax) over the uint64 counts (in place).
+ * Everything is enqueued on the contexts' streams (no host synchronisation); results
+ * are valid after the next synchronising call.  LASPJ_E_UNSUPPORTED when RCCL cannot be
+ * loaded, LASPJ_E_COMM for RCCL failures. */
+#define LASPJ_COMM_ID_BYTES 128
+/* a fresh communicator id (ncclGetUniqueId); rank 0 makes it, the caller hands it to
+ * every rank (the NIF: over Erlang distribution) */
+int laspj_comm_unique_id(uint8_t* id);
+/* one process per GPU: this context joins communicator `id` as `rank` of `nranks` */
+int laspj_comm_init_rank(laspj_ctx* ctx, int nranks, const uint8_t* id, int rank,
+                         laspj_comm** out);
+/* one process owning n GPUs (one BEAM node driving all 8): a communicator per context,
+ * out[i] for ctxs[i] (ncclCommInitAll over the contexts' devices) */
+int laspj_comm_init_all(laspj_ctx* const* ctxs, int n, laspj_comm** out);
+int laspj_comm_destroy(laspj_comm* comm);
+int laspj_comm_info(const laspj_comm* comm, int* rank, int* nranks);
+/* one round on this rank: state (R objects, R % nranks == 0), recv (R, scratch) and
+ * chunk (R / nranks, scratch) of state's kind; for G-Counters recv and chunk may be NULL */
+int laspj_antientropy(laspj_comm* comm, laspj_batch* state, laspj_batch* recv,
+                      laspj_batch* chunk);
+/* the same for n communicators of one process (laspj_comm_init_all), as one RCCL group
+ * per phase */
+int laspj_antientropy_group(laspj_comm* const* comms, laspj_batch* const* state,
+                            laspj_batch* const* recv, laspj_batch* const* chunk, int n);
+
 /* ------------------------------------------------------------------ list values */
 /* List-faithful values.  The combinator bodies of lasp_core bind lists that are not
  * orddicts: intersection entries carry `Cx ++ Cy` (lasp_core.erl:546-589,

@@ -146,6 +146,13 @@ SIGNATURES = {
     "laspj_gset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
     "laspj_gset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
     "laspj_orset_etf_read": (i, [vp, vp, vp, i, i, vp, vp, vp]),
+    "laspj_comm_unique_id": (i, [vp]),
+    "laspj_comm_init_rank": (i, [vp, i, vp, i, vpp]),
+    "laspj_comm_init_all": (i, [vp, i, vp]),
+    "laspj_comm_destroy": (i, [vp]),
+    "laspj_comm_info": (i, [vp, C.POINTER(i), C.POINTER(i)]),
+    "laspj_antientropy": (i, [vp, vp, vp, vp]),
+    "laspj_antientropy_group": (i, [vp, vp, vp, vp, i]),
     "laspj_list_batch_create": (i, [vp, C.c_int32, u64, u32, u32, vpp]),
     "laspj_list_counts": (i, [vp, vp, vp]),
     "laspj_list_upload": (i, [vp, vp, u64, u32, vp, vp, vp]),

@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblaspj.so")
 SOURCES = ["laspj_runtime.hip", "laspj_kernels.hip", "laspj_combinators.hip",
-           "laspj_codec.hip", "laspj_lists.hip"]
+           "laspj_codec.hip", "laspj_lists.hip", "laspj_comm.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-value", "-Wno-unused-result"]
@@ -23,7 +23,7 @@ def build(force: bool = False) -> str:
     if not force and os.path.exists(OUT) and \
             os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *srcs, "-lamdhip64"]
+    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *srcs, "-lamdhip64", "-ldl"]
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT

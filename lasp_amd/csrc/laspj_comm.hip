@@ -1,0 +1,331 @@
+// Anti-entropy across GPUs behind the C ABI (BASELINE config 3).
+//
+// The reference's fan-out -> N-way fold-merge -> read-repair (lasp_update_fsm.erl:174-216,
+// lasp_bind_fsm.erl:170-212, coverage reduce lasp_execute_coverage_fsm.erl:59-62) is an
+// all-reduce whose operator is the lattice join.  Every rank holds one replica of each
+// object; a round leaves every rank with the join of all ranks' replicas:
+//   * bitmap kinds (OR-Set, G-Set): RCCL has no bitwise-OR reduction and max on packed
+//     masks is not a join, so a round is a grouped ncclSend/ncclRecv all-to-all (rank j
+//     receives every rank's copy of object chunk j: the reduce-scatter layout, driving
+//     all n-1 xGMI links at once), the HIP reduce_chunks kernel (one OR over the n
+//     copies), and ncclAllGather of the joined chunks;
+//   * G-Counters: the join IS the per-actor max, so a round is one ncclAllReduce(ncclMax)
+//     on ncclUint64 counts (the unsigned max the device join uses).
+// All phases are enqueued on the engine context's stream: RCCL, the reduce kernel and the
+// next round are ordered by the stream, with no host synchronisation.
+//
+// RCCL is loaded at run time (dlopen): the copy already in the process (torch's bundled
+// librccl.so.1) if there is one, else ROCm's.  A library without RCCL still loads; the
+// comm entry points then return LASPJ_E_UNSUPPORTED.
+
+#include <dlfcn.h>
+
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "laspj_internal.h"
+
+struct laspj_comm {
+    laspj_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int rank = 0;
+    int nranks = 1;
+};
+
+namespace {
+
+using laspj::fail;
+
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t,
+                              ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+std::mutex g_rccl_mu;
+Rccl g_rccl;
+
+template <class F>
+bool sym(void* h, const char* name, F* out) {
+    *out = reinterpret_cast<F>(dlsym(h, name));
+    return *out != nullptr;
+}
+
+const Rccl* rccl() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    Rccl& r = g_rccl;
+    if (r.tried) return r.ok ? &r : nullptr;
+    r.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        const char* e = dlerror();
+        r.why = e ? e : "dlopen(librccl.so.1) failed";
+        return nullptr;
+    }
+    r.ok = sym(h, "ncclGetUniqueId", &r.GetUniqueId) && sym(h, "ncclCommInitRank", &r.CommInitRank) &&
+           sym(h, "ncclCommInitAll", &r.CommInitAll) && sym(h, "ncclCommDestroy", &r.CommDestroy) &&
+           sym(h, "ncclGroupStart", &r.GroupStart) && sym(h, "ncclGroupEnd", &r.GroupEnd) &&
+           sym(h, "ncclSend", &r.Send) && sym(h, "ncclRecv", &r.Recv) &&
+           sym(h, "ncclAllGather", &r.AllGather) && sym(h, "ncclAllReduce", &r.AllReduce) &&
+           sym(h, "ncclGetErrorString", &r.GetErrorString);
+    if (!r.ok) r.why = "librccl lacks a required symbol";
+    return r.ok ? &r : nullptr;
+}
+
+#define LJ_NCCL(ctx, R, call)                                                               \
+    do {                                                                                    \
+        ncclResult_t e_ = (call);                                                           \
+        if (e_ != ncclSuccess)                                                              \
+            return fail((ctx), LASPJ_E_COMM, "%s: %s", #call, (R)->GetErrorString(e_));     \
+    } while (0)
+
+struct CGuard {
+    std::lock_guard<std::mutex> lk;
+    explicit CGuard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
+};
+
+bool set_kind(int32_t k) {
+    return k == LASPJ_KIND_ORSET || k == LASPJ_KIND_GSET || k == LASPJ_KIND_GCOUNTER;
+}
+
+// shapes of one rank's round: state R objects (R % n == 0), recv R, chunk R / n
+int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batch* recv,
+                 const laspj_batch* chunk, const char* what) {
+    laspj_ctx* ctx = c->ctx;
+    if (!state || state->ctx != ctx || !set_kind(state->kind))
+        return fail(ctx, LASPJ_E_INVAL, "%s: state must be an OR-Set, G-Set or G-Counter batch of "
+                    "the communicator's context", what);
+    if (state->kind == LASPJ_KIND_GCOUNTER) return LASPJ_OK;   // in place, no scratch
+    if (!recv || !chunk || recv->ctx != ctx || chunk->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: recv / chunk batches missing", what);
+    if (recv->kind != state->kind || chunk->kind != state->kind)
+        return fail(ctx, LASPJ_E_KIND, "%s: kinds differ", what);
+    const uint64_t n = (uint64_t)c->nranks;
+    if (state->replicas % n || recv->replicas != state->replicas ||
+        chunk->replicas * n != state->replicas || recv->elements != state->elements ||
+        chunk->elements != state->elements)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: need objects %% ranks == 0, recv = state, "
+                    "chunk = objects / ranks", what);
+    if (recv->dev == state->dev || chunk->dev == state->dev || chunk->dev == recv->dev)
+        return fail(ctx, LASPJ_E_INVAL, "%s: state, recv and chunk must not alias", what);
+    return LASPJ_OK;
+}
+
+// the three phases of one bitmap round, enqueued on the context's stream (the caller
+// groups the RCCL calls)
+int phase_all_to_all(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
+    laspj_ctx* ctx = c->ctx;
+    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
+    for (int p = 0; p < c->nranks; ++p) {
+        LJ_NCCL(ctx, R, R->Send(state->dev + (uint64_t)p * cw, cw, ncclUint64, p, c->comm,
+                                ctx->stream));
+        LJ_NCCL(ctx, R, R->Recv(recv->dev + (uint64_t)p * cw, cw, ncclUint64, p, c->comm,
+                                ctx->stream));
+    }
+    return LASPJ_OK;
+}
+
+int phase_reduce(laspj_comm* c, laspj_batch* recv, laspj_batch* chunk) {
+    laspj_ctx* ctx = c->ctx;
+    LJ_HIP(ctx, laspj::launch_reduce_chunks(ctx, chunk->dev, recv->dev,
+                                            chunk->replicas * chunk->words_per_replica,
+                                            (uint32_t)c->nranks, false));
+    return LASPJ_OK;
+}
+
+int phase_all_gather(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* chunk) {
+    laspj_ctx* ctx = c->ctx;
+    LJ_NCCL(ctx, R, R->AllGather(chunk->dev, state->dev,
+                                 chunk->replicas * chunk->words_per_replica, ncclUint64,
+                                 c->comm, ctx->stream));
+    return LASPJ_OK;
+}
+
+int phase_max(const Rccl* R, laspj_comm* c, laspj_batch* state) {
+    laspj_ctx* ctx = c->ctx;
+    LJ_NCCL(ctx, R, R->AllReduce(state->dev, state->dev,
+                                 state->replicas * state->words_per_replica, ncclUint64,
+                                 ncclMax, c->comm, ctx->stream));
+    return LASPJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int laspj_comm_unique_id(uint8_t* id) {
+    if (!id) return LASPJ_E_INVAL;
+    const Rccl* R = rccl();
+    if (!R) return LASPJ_E_UNSUPPORTED;
+    ncclUniqueId u;
+    if (R->GetUniqueId(&u) != ncclSuccess) return LASPJ_E_COMM;
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return LASPJ_OK;
+}
+
+int laspj_comm_init_rank(laspj_ctx* ctx, int nranks, const uint8_t* id, int rank,
+                         laspj_comm** out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(ctx, LASPJ_E_INVAL, "comm_init_rank: bad argument");
+    *out = nullptr;
+    const Rccl* R = rccl();
+    if (!R) return fail(ctx, LASPJ_E_UNSUPPORTED, "comm_init_rank: RCCL not loadable: %s",
+                        g_rccl.why.c_str());
+    auto* c = new (std::nothrow) laspj_comm;
+    if (!c) return fail(ctx, LASPJ_E_NOMEM, "comm_init_rank: host allocation");
+    c->ctx = ctx;
+    c->rank = rank;
+    c->nranks = nranks;
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t e;
+    {
+        CGuard g(ctx);
+        e = R->CommInitRank(&c->comm, nranks, u, rank);
+    }
+    if (e != ncclSuccess) {
+        delete c;
+        return fail(ctx, LASPJ_E_COMM, "ncclCommInitRank: %s", R->GetErrorString(e));
+    }
+    *out = c;
+    return LASPJ_OK;
+}
+
+int laspj_comm_init_all(laspj_ctx* const* ctxs, int n, laspj_comm** out) {
+    if (!ctxs || !out || n < 1) return LASPJ_E_INVAL;
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return LASPJ_E_INVAL;
+        out[i] = nullptr;
+    }
+    const Rccl* R = rccl();
+    if (!R) return fail(ctxs[0], LASPJ_E_UNSUPPORTED, "comm_init_all: RCCL not loadable: %s",
+                        g_rccl.why.c_str());
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = ctxs[i]->device;
+    std::vector<ncclComm_t> comms(n);
+    ncclResult_t e = R->CommInitAll(comms.data(), n, devs.data());
+    if (e != ncclSuccess)
+        return fail(ctxs[0], LASPJ_E_COMM, "ncclCommInitAll: %s", R->GetErrorString(e));
+    for (int i = 0; i < n; ++i) {
+        auto* c = new (std::nothrow) laspj_comm;
+        if (!c) {
+            for (int j = 0; j < n; ++j) {
+                if (j < i) delete out[j];
+                R->CommDestroy(comms[j]);
+                out[j] = nullptr;
+            }
+            return fail(ctxs[0], LASPJ_E_NOMEM, "comm_init_all: host allocation");
+        }
+        c->ctx = ctxs[i];
+        c->comm = comms[i];
+        c->rank = i;
+        c->nranks = n;
+        out[i] = c;
+    }
+    return LASPJ_OK;
+}
+
+int laspj_comm_destroy(laspj_comm* c) {
+    if (!c) return LASPJ_E_INVAL;
+    const Rccl* R = rccl();
+    {
+        CGuard g(c->ctx);
+        hipStreamSynchronize(c->ctx->stream);
+        if (R && c->comm) R->CommDestroy(c->comm);
+    }
+    delete c;
+    return LASPJ_OK;
+}
+
+int laspj_comm_info(const laspj_comm* c, int* rank, int* nranks) {
+    if (!c) return LASPJ_E_INVAL;
+    if (rank) *rank = c->rank;
+    if (nranks) *nranks = c->nranks;
+    return LASPJ_OK;
+}
+
+int laspj_antientropy(laspj_comm* c, laspj_batch* state, laspj_batch* recv, laspj_batch* chunk) {
+    return laspj_antientropy_group(&c, &state, &recv, &chunk, 1);
+}
+
+int laspj_antientropy_group(laspj_comm* const* cs, laspj_batch* const* state,
+                            laspj_batch* const* recv, laspj_batch* const* chunk, int n) {
+    if (!cs || !state || n < 1) return LASPJ_E_INVAL;
+    for (int i = 0; i < n; ++i)
+        if (!cs[i] || !cs[i]->ctx) return LASPJ_E_INVAL;
+    const Rccl* R = rccl();
+    if (!R) return fail(cs[0]->ctx, LASPJ_E_UNSUPPORTED, "antientropy: RCCL not loadable");
+    for (int i = 0; i < n; ++i)
+        if (int s = round_checks(cs[i], state[i], recv ? recv[i] : nullptr,
+                                 chunk ? chunk[i] : nullptr, "antientropy"))
+            return s;
+    const bool max_join = state[0]->kind == LASPJ_KIND_GCOUNTER;
+    for (int i = 1; i < n; ++i)
+        if ((state[i]->kind == LASPJ_KIND_GCOUNTER) != max_join)
+            return fail(cs[0]->ctx, LASPJ_E_KIND, "antientropy: mixed kinds in one group");
+    // one process may drive several GPUs: every RCCL phase is one group over all of them
+    // (the device is set per call; the contexts' mutexes serialise other callers)
+    std::vector<std::unique_ptr<CGuard>> guards;
+    for (int i = 0; i < n; ++i) {
+        bool dup = false;
+        for (int j = 0; j < i; ++j) dup |= cs[j]->ctx == cs[i]->ctx;
+        if (dup) return fail(cs[0]->ctx, LASPJ_E_INVAL, "antientropy: one context twice");
+    }
+    for (int i = 0; i < n; ++i) guards.emplace_back(new CGuard(cs[i]->ctx));
+    if (max_join) {
+        LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
+        for (int i = 0; i < n; ++i) {
+            hipSetDevice(cs[i]->ctx->device);
+            if (int s = phase_max(R, cs[i], state[i])) {
+                R->GroupEnd();
+                return s;
+            }
+        }
+        LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
+        return LASPJ_OK;
+    }
+    LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
+    for (int i = 0; i < n; ++i) {
+        hipSetDevice(cs[i]->ctx->device);
+        if (int s = phase_all_to_all(R, cs[i], state[i], recv[i])) {
+            R->GroupEnd();
+            return s;
+        }
+    }
+    LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
+    for (int i = 0; i < n; ++i) {
+        hipSetDevice(cs[i]->ctx->device);
+        if (int s = phase_reduce(cs[i], recv[i], chunk[i])) return s;
+    }
+    LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
+    for (int i = 0; i < n; ++i) {
+        hipSetDevice(cs[i]->ctx->device);
+        if (int s = phase_all_gather(R, cs[i], state[i], chunk[i])) {
+            R->GroupEnd();
+            return s;
+        }
+    }
+    LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
+    return LASPJ_OK;
+}
+
+}  // extern "C"

@@ -677,3 +677,65 @@ class ListBatch:
         check(self.ctx.L.laspj_list_fold(self.ctx.h, out.h, self.h, ob.h, kb.h, len(off) - 1,
                                          int(per_entry)), self.ctx.h)
         return out
+
+
+class Comm:
+    """A communicator of the anti-entropy collective (laspj_comm_*, RCCL over xGMI)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, ctx: Context, nranks: int, uid: bytes, rank: int, _h=None):
+        self.ctx = ctx
+        if _h is not None:
+            self.h = _h
+        else:
+            buf = (C.c_uint8 * self.ID_BYTES).from_buffer_copy(uid)
+            h = C.c_void_p()
+            check(ctx.L.laspj_comm_init_rank(ctx.h, nranks, buf, rank, C.byref(h)), ctx.h)
+            self.h = h
+        r, n = C.c_int(), C.c_int()
+        check(ctx.L.laspj_comm_info(self.h, C.byref(r), C.byref(n)))
+        self.rank, self.nranks = r.value, n.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = load()
+        buf = (C.c_uint8 * Comm.ID_BYTES)()
+        check(L.laspj_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def init_all(cls, ctxs: Sequence[Context]) -> list:
+        """One communicator per context, one process driving every GPU."""
+        n = len(ctxs)
+        L = ctxs[0].L
+        harr = (C.c_void_p * n)(*[c.h.value for c in ctxs])
+        out = (C.c_void_p * n)()
+        check(L.laspj_comm_init_all(harr, n, out), ctxs[0].h)
+        return [cls(ctxs[i], n, b"", i, _h=C.c_void_p(out[i])) for i in range(n)]
+
+    def close(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.laspj_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def antientropy(self, state, recv=None, chunk=None):
+        """One round (laspj_antientropy): state becomes the join over all ranks."""
+        check(self.ctx.L.laspj_antientropy(self.h, state.h, recv.h if recv else None,
+                                           chunk.h if chunk else None), self.ctx.h)
+
+    @staticmethod
+    def antientropy_group(comms: Sequence["Comm"], states, recvs=None, chunks=None):
+        n = len(comms)
+        L = comms[0].ctx.L
+        arr = lambda xs: (C.c_void_p * n)(*[x.h.value if x is not None else None  # noqa: E731
+                                             for x in xs])
+        check(L.laspj_antientropy_group(arr(comms), arr(states),
+                                        arr(recvs) if recvs else None,
+                                        arr(chunks) if chunks else None, n), comms[0].ctx.h)
