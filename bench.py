@@ -288,6 +288,9 @@ def main():
         ndev = torch.cuda.device_count()
         local = local % ndev if ndev else local
         torch.cuda.set_device(local)
+        if world == 1:                   # a one-rank group (the anti-entropy rehearsal)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 
     from lasp_amd import engine

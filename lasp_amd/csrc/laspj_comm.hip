@@ -130,16 +130,42 @@ int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batc
     return LASPJ_OK;
 }
 
-// the three phases of one bitmap round, enqueued on the context's stream (the caller
-// groups the RCCL calls)
+// RCCL point-to-point calls move at most 4 GiB each (measured: a 64 GiB ncclSend/Recv
+// pair delivered only the first 2^32 bytes, tools/ae_probe.py), so every transfer goes
+// in pieces of 2^27 words (1 GiB), all inside the caller's group.
+constexpr uint64_t kPiece = 1ull << 27;
+
+int p2p(const Rccl* R, laspj_comm* c, const uint64_t* src, uint64_t* dst, uint64_t words,
+        int peer) {
+    laspj_ctx* ctx = c->ctx;
+    for (uint64_t off = 0; off < words; off += kPiece) {
+        const uint64_t len = words - off < kPiece ? words - off : kPiece;
+        LJ_NCCL(ctx, R, R->Send(src + off, len, ncclUint64, peer, c->comm, ctx->stream));
+        LJ_NCCL(ctx, R, R->Recv(dst + off, len, ncclUint64, peer, c->comm, ctx->stream));
+    }
+    return LASPJ_OK;
+}
+
+// the phases of one bitmap round, enqueued on the context's stream (the caller groups
+// the RCCL calls).  The rank's own chunk is a device copy, not a self-send.
 int phase_all_to_all(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
     laspj_ctx* ctx = c->ctx;
     const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
     for (int p = 0; p < c->nranks; ++p) {
-        LJ_NCCL(ctx, R, R->Send(state->dev + (uint64_t)p * cw, cw, ncclUint64, p, c->comm,
-                                ctx->stream));
-        LJ_NCCL(ctx, R, R->Recv(recv->dev + (uint64_t)p * cw, cw, ncclUint64, p, c->comm,
-                                ctx->stream));
+        // this rank's copy of chunk p goes to rank p, which stores it at slot `rank`;
+        // the copy of chunk `rank` held by rank p arrives at slot p
+        if (p == c->rank) {
+            LJ_HIP(ctx, hipMemcpyAsync(recv->dev + (uint64_t)p * cw, state->dev + (uint64_t)p * cw,
+                                       cw * 8ull, hipMemcpyDeviceToDevice, ctx->stream));
+            continue;
+        }
+        for (uint64_t off = 0; off < cw; off += kPiece) {
+            const uint64_t len = cw - off < kPiece ? cw - off : kPiece;
+            LJ_NCCL(ctx, R, R->Send(state->dev + (uint64_t)p * cw + off, len, ncclUint64, p,
+                                    c->comm, ctx->stream));
+            LJ_NCCL(ctx, R, R->Recv(recv->dev + (uint64_t)p * cw + off, len, ncclUint64, p,
+                                    c->comm, ctx->stream));
+        }
     }
     return LASPJ_OK;
 }
@@ -152,19 +178,29 @@ int phase_reduce(laspj_comm* c, laspj_batch* recv, laspj_batch* chunk) {
     return LASPJ_OK;
 }
 
+// all-gather as point-to-point pieces: the joined chunk goes to every peer's slot `rank`
 int phase_all_gather(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* chunk) {
     laspj_ctx* ctx = c->ctx;
-    LJ_NCCL(ctx, R, R->AllGather(chunk->dev, state->dev,
-                                 chunk->replicas * chunk->words_per_replica, ncclUint64,
-                                 c->comm, ctx->stream));
+    const uint64_t cw = chunk->replicas * chunk->words_per_replica;
+    for (int p = 0; p < c->nranks; ++p) {
+        if (p == c->rank) {
+            LJ_HIP(ctx, hipMemcpyAsync(state->dev + (uint64_t)p * cw, chunk->dev, cw * 8ull,
+                                       hipMemcpyDeviceToDevice, ctx->stream));
+            continue;
+        }
+        if (int s = p2p(R, c, chunk->dev, state->dev + (uint64_t)p * cw, cw, p)) return s;
+    }
     return LASPJ_OK;
 }
 
 int phase_max(const Rccl* R, laspj_comm* c, laspj_batch* state) {
     laspj_ctx* ctx = c->ctx;
-    LJ_NCCL(ctx, R, R->AllReduce(state->dev, state->dev,
-                                 state->replicas * state->words_per_replica, ncclUint64,
-                                 ncclMax, c->comm, ctx->stream));
+    const uint64_t words = state->replicas * state->words_per_replica;
+    for (uint64_t off = 0; off < words; off += kPiece) {
+        const uint64_t len = words - off < kPiece ? words - off : kPiece;
+        LJ_NCCL(ctx, R, R->AllReduce(state->dev + off, state->dev + off, len, ncclUint64,
+                                     ncclMax, c->comm, ctx->stream));
+    }
     return LASPJ_OK;
 }
 
