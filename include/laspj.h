@@ -169,6 +169,13 @@ int laspj_batch_destroy(laspj_batch* batch);
 int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* device_ptr, uint64_t bytes,
                      uint64_t replicas, uint32_t elements, laspj_batch** out);
 int laspj_batch_info_get(const laspj_batch* batch, laspj_batch_info* out);
+/* device address of a batch's first word (to wrap replica ranges with laspj_batch_wrap
+ * or hand them to a collective); list batches have no flat layout (LASPJ_E_KIND) */
+int laspj_batch_device_ptr(const laspj_batch* batch, void** out);
+/* bytes [offset, offset + bytes) of a batch's device image (synchronous), e.g. one row
+ * window of a product batch */
+int laspj_batch_download_range(laspj_ctx* ctx, const laspj_batch* batch, uint64_t offset,
+                               uint64_t bytes, void* host);
 /* host <-> device, replicas [first, first+count), host layout = device layout */
 int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* batch, uint64_t first, uint64_t count,
                        const void* host);
@@ -181,6 +188,11 @@ int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* batch);
  * (replica_base + i) of stream `seed`; G-Counter batches get 20-bit counts (bench data) */
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed,
                                uint64_t replica_base);
+/* the OR-Set stream restricted to token_slots token slots: p and r masked to the low
+ * token_slots bits, and every element present (p = 1 when the mask leaves none, and no
+ * 5 % of absent elements) — BASELINE configs 4 / 5: sets of exactly E elements, T = 3 */
+int laspj_batch_fill_synthetic_tokens(laspj_ctx* ctx, laspj_batch* batch, uint64_t seed,
+                                      uint64_t replica_base, uint32_t token_slots);
 
 /* Slot-wise join of two batches of the same kind and shape (any kind): dst = a | b
  * word by word.  For OR-Set / G-Set batches this is merge/2; for combinator outputs
@@ -265,6 +277,17 @@ int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
  * one slot per F(X) entry, in list order). */
 int laspj_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                        const laspj_buf* index);
+
+/* A combinator stage whose output is threshold-read in the same pass (BASELINE config 4:
+ * map -> filter -> fold -> read {strict, Prev}, lasp_core.erl:641-712, 460-486, and
+ * lasp_process.erl:61-95): dst = src gathered through index (as laspj_orset_gather; the
+ * host composes the stages' indexes: fold slot o <- filtered slot f[o] <- mapped slot
+ * <- src slot m[f[o]], or empty when the filter drops it) and out[i] = one byte,
+ * is_inflation (strict = 0) / is_strict_inflation (strict = 1) of prev[i] -> dst[i]
+ * (lasp_lattice.erl:153-161, 235-253).  prev has dst's shape or 1 replica. */
+int laspj_orset_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                 const laspj_buf* index, const laspj_batch* prev, int strict,
+                                 laspj_buf* out);
 
 /* ------------------------------------------------------------------ lasp_gset */
 /* merge/2 — lasp_gset.erl:99-101 (ordsets:union on canonical sets = OR) */

@@ -98,10 +98,14 @@ SIGNATURES = {
     "laspj_batch_wrap": (i, [vp, C.c_int32, vp, u64, u64, u32, vpp]),
     "laspj_batch_reduce_chunks": (i, [vp, vp, vp, u32]),
     "laspj_batch_info_get": (i, [vp, C.POINTER(BatchInfo)]),
+    "laspj_batch_device_ptr": (i, [vp, vpp]),
+    "laspj_batch_download_range": (i, [vp, vp, u64, u64, vp]),
     "laspj_batch_upload": (i, [vp, vp, u64, u64, vp]),
     "laspj_batch_download": (i, [vp, vp, u64, u64, vp]),
     "laspj_batch_clear": (i, [vp, vp]),
     "laspj_batch_fill_synthetic": (i, [vp, vp, u64, u64]),
+    "laspj_batch_fill_synthetic_tokens": (i, [vp, vp, u64, u64, u32]),
+    "laspj_orset_gather_inflation": (i, [vp, vp, vp, vp, vp, i, vp]),
     "laspj_batch_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_reduce": (i, [vp, vp, vp, u32]),

@@ -381,7 +381,7 @@ __device__ __forceinline__ u64 synth_replica_key(u64 seed, u64 grep) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_fill_orset(u64x2* cells, uint64_t R, uint32_t E,
-                                                       u64 seed, u64 base) {
+                                                       u64 seed, u64 base, u64 tmask) {
     const uint64_t n = R * E;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
@@ -392,7 +392,13 @@ __global__ __launch_bounds__(kBlock) void k_fill_orset(u64x2* cells, uint64_t R,
         u64 y = sm64(x ^ 0xA5A5A5A5A5A5A5A5ull);
         u64 z = sm64(y ^ 0x5A5A5A5A5A5A5A5Aull);
         u64 w = sm64(z);
+        // the full stream leaves ~5 % of elements absent; the T-token stream
+        // (laspj_batch_fill_synthetic_tokens) keeps every element with 1..T tokens
         u64 p = (z % 20ull) == 0 ? 0ull : x;
+        if (tmask != ~0ull) {
+            p = x & tmask;
+            if (p == 0) p = 1;
+        }
         u64x2 c;
         c.x = p;
         c.y = p & y & w;
@@ -429,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_gcounter(u64* words, uint64_t R
 }
 
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
-                                 uint64_t base) {
+                                 uint64_t base, uint64_t tmask) {
     if (b->kind == LASPJ_KIND_GCOUNTER) {
         StreamTune t = stream_tune(ctx, b->replicas * b->words_per_replica / 2 + 1);
         hipLaunchKernelGGL(k_fill_gcounter, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
@@ -440,7 +446,7 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
     if (b->kind == LASPJ_KIND_ORSET)
         hipLaunchKernelGGL(k_fill_orset, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<u64x2*>(b->dev), b->replicas, b->elements,
-                           (u64)seed, (u64)base);
+                           (u64)seed, (u64)base, (u64)tmask);
     else
         hipLaunchKernelGGL(k_fill_gset, dim3(t.grid), dim3(kBlock), 0, ctx->stream,
                            (u64*)b->dev, b->replicas, b->elements, (u64)seed, (u64)base);
@@ -888,6 +894,114 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
         }
         if (lane == 0) emit(SEG, out, part, rep, flags, np, nc, STRICT ? 2 : 1, fin);
     }
+}
+
+// A dataflow stage whose output is threshold-checked in the same pass (BASELINE config
+// 4's map -> filter -> fold -> {strict, Prev} read, fused): dst = src gathered through
+// index (map / filter / fold compose into one index on the host: the fold's slot o takes
+// filtered slot f[o], which is mapped slot f[o] when kept, which is src slot m[f[o]]),
+// and out[i] = is_(strict_)inflation(prev[i], dst[i]) — lasp_lattice.erl:153-161,
+// 235-253 — over the cells just written.  A block owns a 4096-slot segment of the output
+// and a run of 8 replicas (its 16 index entries per lane stay in registers); the block's
+// 4 waves combine their ballots in LDS and emit one partial per (replica, segment).
+constexpr uint32_t kFSeg = 4096, kFPer = kFSeg / kBlock, kFRun = 8;
+
+template <bool STRICT, bool SEG>
+__global__ __launch_bounds__(kBlock) void k_gather_inflation(u64x2* out, const u64x2* src,
+                                                             const u64x2* prev,
+                                                             const uint32_t* index,
+                                                             uint8_t* res, u64* part,
+                                                             uint64_t reps, uint32_t E_out,
+                                                             uint32_t E_in, uint32_t nseg,
+                                                             uint32_t fin, bool bcast) {
+    __shared__ u64 s_f[kBlock / 64], s_np[kBlock / 64], s_nc[kBlock / 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t runs = (reps + kFRun - 1) / kFRun;
+    for (uint64_t it = blockIdx.x; it < runs * nseg; it += gridDim.x) {
+        const uint64_t run = it / nseg;
+        const uint32_t o0 = (uint32_t)(it - run * nseg) * kFSeg;
+        uint32_t si[kFPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kFPer; ++k) {
+            const uint32_t o = o0 + k * kBlock + threadIdx.x;
+            si[k] = o < E_out ? index[o] : 0xFFFFFFFFu;
+        }
+        const uint64_t r1 = min(reps, (run + 1) * kFRun);
+        for (uint64_t rep = run * kFRun; rep < r1; ++rep) {
+            const u64x2* s = src + rep * E_in;
+            const u64x2* P = prev + (bcast ? 0 : rep * E_out);
+            u64x2* d = out + rep * E_out;
+            u64x2 v[kFPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kFPer; ++k)
+                v[k] = si[k] < E_in ? s[si[k]] : u64x2{0, 0};
+            bool viol = false, changed = false;
+            u64 np = 0, nc = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kFPer; ++k) {
+                const uint32_t o = o0 + k * kBlock + threadIdx.x;
+                if (o < E_out) {
+                    __builtin_nontemporal_store(v[k], d + o);
+                    const u64x2 p = __builtin_nontemporal_load(P + o);
+                    viol |= (p.x & ~v[k].x) != 0;
+                    if constexpr (STRICT) {
+                        changed |= (p.x != 0) & (v[k].x != 0) & ((p.x != v[k].x) | (p.y != v[k].y));
+                        np += p.x != 0;
+                        nc += v[k].x != 0;
+                    }
+                }
+            }
+            u64 f = (__ballot(viol) != 0) ? kViol : 0;
+            if constexpr (STRICT) {
+                if (__ballot(changed) != 0) f |= kChanged;
+                np = wave_sum(np);
+                nc = wave_sum(nc);
+            }
+            if (lane == 0) {
+                s_f[wv] = f;
+                s_np[wv] = np;
+                s_nc[wv] = nc;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                u64 F = 0, NP = 0, NC = 0;
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) F |= s_f[w], NP += s_np[w], NC += s_nc[w];
+                emit(SEG, res, part, rep, F, NP, NC, STRICT ? 2 : 1, fin);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                   const uint32_t* index, const laspj_batch* prev, bool strict,
+                                   uint8_t* res) {
+    const uint32_t ns = (dst->elements + kFSeg - 1) / kFSeg;
+    const uint64_t items = (dst->replicas + kFRun - 1) / kFRun * ns;
+    const uint64_t cap = (uint64_t)ctx->cus * 32;
+    const uint64_t g = items < cap ? items : cap;
+    const bool bc = prev->replicas == 1 && dst->replicas != 1;
+    u64* part = nullptr;
+    if (ns > 1) {
+        hipError_t e = partials(ctx, dst->replicas, &part);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t fin = ns > 1 ? fin_for(dst->replicas * ns, ns) : 0u;
+#define LJ_GI(ST, SG)                                                                        \
+    hipLaunchKernelGGL((k_gather_inflation<ST, SG>), dim3((unsigned)(g ? g : 1)), dim3(kBlock), \
+                       0, ctx->stream, reinterpret_cast<u64x2*>(dst->dev),                   \
+                       reinterpret_cast<const u64x2*>(src->dev),                             \
+                       reinterpret_cast<const u64x2*>(prev->dev), index, res, part,          \
+                       dst->replicas, dst->elements, src->elements, ns, fin, bc)
+    if (ns > 1) {
+        if (strict) LJ_GI(true, true); else LJ_GI(false, true);
+        if (!fin) return finalize(ctx, part, res, dst->replicas, strict ? 2 : 1);
+        return hipGetLastError();
+    }
+    if (strict) LJ_GI(true, false); else LJ_GI(false, false);
+#undef LJ_GI
+    return hipGetLastError();
 }
 
 // lasp_lattice.erl:137-140 / :212-215: subset, and strict adds "sets differ".

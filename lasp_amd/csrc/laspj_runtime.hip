@@ -411,6 +411,30 @@ int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
     return LASPJ_OK;
 }
 
+int laspj_batch_device_ptr(const laspj_batch* b, void** out) {
+    if (!b || !out) return LASPJ_E_INVAL;
+    if (laspj_is_list(b->kind)) return LASPJ_E_KIND;
+    *out = b->dev;
+    return LASPJ_OK;
+}
+
+int laspj_batch_download_range(laspj_ctx* ctx, const laspj_batch* b, uint64_t offset,
+                               uint64_t bytes, void* host) {
+    if (!same_ctx(ctx, b) || (!host && bytes))
+        return fail(ctx, LASPJ_E_INVAL, "batch_download_range: bad argument");
+    if (laspj_is_list(b->kind))
+        return fail(ctx, LASPJ_E_KIND, "batch_download_range: list batches use laspj_list_download");
+    const uint64_t total = laspj::bytes_of(b);
+    if (offset > total || bytes > total - offset)
+        return fail(ctx, LASPJ_E_RANGE, "batch_download_range: range out of bounds");
+    Guard g(ctx);
+    if (!bytes) return LASPJ_OK;
+    LJ_HIP(ctx, hipMemcpyAsync(host, reinterpret_cast<const char*>(b->dev) + offset, bytes,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LASPJ_OK;
+}
+
 int laspj_batch_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t first, uint64_t count,
                        const void* host) {
     if (!same_ctx(ctx, b) || (!host && count))
@@ -452,6 +476,19 @@ int laspj_batch_clear(laspj_ctx* ctx, laspj_batch* b) {
     return LASPJ_OK;
 }
 
+int laspj_batch_fill_synthetic_tokens(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
+                                      uint64_t replica_base, uint32_t token_slots) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
+    if (b->kind != LASPJ_KIND_ORSET)
+        return fail(ctx, LASPJ_E_KIND, "fill_synthetic_tokens: OR-Set batches only");
+    if (token_slots < 1 || token_slots > 64)
+        return fail(ctx, LASPJ_E_INVAL, "fill_synthetic_tokens: token slots must be 1..64");
+    Guard g(ctx);
+    const uint64_t mask = token_slots == 64 ? ~0ull : ((1ull << token_slots) - 1ull);
+    LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base, mask));
+    return LASPJ_OK;
+}
+
 int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                uint64_t replica_base) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
@@ -460,6 +497,28 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
         return fail(ctx, LASPJ_E_KIND, "fill_synthetic: OR-Set, G-Set or G-Counter batches only");
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base));
+    return LASPJ_OK;
+}
+
+int laspj_orset_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                 const laspj_buf* index, const laspj_batch* prev, int strict,
+                                 laspj_buf* out) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src) || !same_ctx(ctx, prev))
+        return fail(ctx, LASPJ_E_INVAL, "gather_inflation: bad batch");
+    if (dst->kind != LASPJ_KIND_ORSET || src->kind != LASPJ_KIND_ORSET ||
+        prev->kind != LASPJ_KIND_ORSET)
+        return fail(ctx, LASPJ_E_KIND, "gather_inflation: OR-Set batches only");
+    if (dst->replicas != src->replicas || prev->elements != dst->elements ||
+        (prev->replicas != dst->replicas && prev->replicas != 1))
+        return fail(ctx, LASPJ_E_SHAPE, "gather_inflation: shapes");
+    if (dst->dev == src->dev || dst->dev == prev->dev)
+        return fail(ctx, LASPJ_E_INVAL, "gather_inflation: dst aliases an input");
+    if (int s = check_buf(ctx, index, 4ull * dst->elements, "gather_inflation")) return s;
+    if (int s = check_buf(ctx, out, dst->replicas, "gather_inflation")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gather_inflation(ctx, dst, src,
+                                               static_cast<const uint32_t*>(index->dev), prev,
+                                               strict != 0, static_cast<uint8_t*>(out->dev)));
     return LASPJ_OK;
 }
 

@@ -194,7 +194,39 @@ class _Batch:
     def clear(self):
         check(self.ctx.L.laspj_batch_clear(self.ctx.h, self.h), self.ctx.h)
 
-    def fill_synthetic(self, seed: int, replica_base: int = 0):
+    def download_range(self, offset: int, nbytes: int) -> np.ndarray:
+        """Bytes [offset, offset + nbytes) of the batch's device image."""
+        out = np.zeros((nbytes,), dtype=np.uint8)
+        check(self.ctx.L.laspj_batch_download_range(self.ctx.h, self.h, offset, nbytes,
+                                                    out.ctypes.data), self.ctx.h)
+        return out
+
+    def view(self, first: int, count: int) -> "_Batch":
+        """A non-owning batch of the same kind over replicas [first, first + count)
+        (laspj_batch_device_ptr + laspj_batch_wrap); keeps this batch alive."""
+        if first < 0 or count < 1 or first + count > self.replicas:
+            raise ValueError("replica range out of bounds")
+        p = C.c_void_p()
+        check(self.ctx.L.laspj_batch_device_ptr(self.h, C.byref(p)))
+        out = type(self).__new__(type(self))
+        out.ctx, out._keep = self.ctx, self
+        h = C.c_void_p()
+        check(self.ctx.L.laspj_batch_wrap(self.ctx.h, self.kind,
+                                          C.c_void_p(p.value + first * self.bytes_per_replica),
+                                          count * self.bytes_per_replica, count, self.elements,
+                                          C.byref(h)), self.ctx.h)
+        out.h = h
+        out.replicas, out.elements = count, self.elements
+        out.bytes_per_replica = self.bytes_per_replica
+        out.nbytes = count * self.bytes_per_replica
+        return out
+
+    def fill_synthetic(self, seed: int, replica_base: int = 0, token_slots: int = 0):
+        if token_slots:
+            check(self.ctx.L.laspj_batch_fill_synthetic_tokens(self.ctx.h, self.h, seed,
+                                                               replica_base, token_slots),
+                  self.ctx.h)
+            return
         check(self.ctx.L.laspj_batch_fill_synthetic(self.ctx.h, self.h, seed, replica_base),
               self.ctx.h)
 
@@ -325,6 +357,20 @@ class ORSetBatch(_Batch):
         out = ORSetProductWideBatch(self.ctx, self.replicas, self.elements, r.elements)
         check(self.ctx.L.laspj_orset_product(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
         return out
+
+    # a gather whose output is threshold-checked in the same pass (config 4 fused)
+    def gather_inflation(self, src: "ORSetBatch", index, prev: "ORSetBatch",
+                         strict: bool = True) -> np.ndarray:
+        """self <- src through index; returns is_(strict_)inflation(prev, self) per
+        replica (laspj_orset_gather_inflation).  `index` is a uint32 array or Buffer."""
+        idx = index if isinstance(index, Buffer) else None
+        if idx is None:
+            idx = self.ctx.buffer(4 * self.elements)
+            idx.upload(np.ascontiguousarray(index, dtype=np.uint32))
+        out = self.ctx.buffer(self.replicas)
+        check(self.ctx.L.laspj_orset_gather_inflation(self.ctx.h, self.h, src.h, idx.h, prev.h,
+                                                      int(strict), out.h), self.ctx.h)
+        return out.download(np.uint8).astype(bool)
 
     # map / fold bodies: self <- src gathered through index (one u32 per slot of self)
     def gather(self, src: "ORSetBatch", index: np.ndarray):

@@ -35,6 +35,8 @@ def lib():
             build()
         L = C.CDLL(_SO)
         L.orc_synth_orset.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, u64p]
+        L.orc_synth_orset_t.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, u64p]
         L.orc_synth_gset.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, u64p]
         L.orc_synth_tokens.argtypes = [C.c_uint32, C.c_uint32, u8p]
         L.orc_orset_alloc.argtypes = [C.c_uint32, C.c_uint32]
@@ -80,6 +82,14 @@ def synth_orset(seed: int, grep: int, E: int) -> np.ndarray:
     """Synthetic OR-Set replica as an (E, 2) uint64 array of {p, r} cells."""
     out = np.empty((E, 2), dtype=np.uint64)
     lib().orc_synth_orset(seed, grep, E, _p(out))
+    return out
+
+
+def synth_orset_t(seed: int, grep: int, e0: int, n: int, T: int) -> np.ndarray:
+    """Elements [e0, e0+n) of the T-token stream replica (laspj_batch_fill_synthetic_tokens)
+    as an (n, 2) uint64 array."""
+    out = np.empty((n, 2), dtype=np.uint64)
+    lib().orc_synth_orset_t(seed, grep, e0, n, T, _p(out))
     return out
 
 

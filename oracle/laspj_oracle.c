@@ -65,6 +65,24 @@ void orc_synth_orset(u64 seed, u64 grep, uint32_t E, u64* cells) {
     }
 }
 
+/* the T-token stream (laspj_batch_fill_synthetic_tokens): p = x masked to T bits (1 if
+ * that leaves none; every element present), r = p & y & w; elements [e0, e0 + n) */
+void orc_synth_orset_t(u64 seed, u64 grep, uint32_t e0, uint32_t n, uint32_t T, u64* cells) {
+    u64 h = replica_key(seed, grep);
+    u64 m = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
+    for (uint32_t i = 0; i < n; ++i) {
+        u64 e = (u64)e0 + i;
+        u64 x = sm64(h + e * 0xD1B54A32D192ED03ull);
+        u64 y = sm64(x ^ 0xA5A5A5A5A5A5A5A5ull);
+        u64 z = sm64(y ^ 0x5A5A5A5A5A5A5A5Aull);
+        u64 w = sm64(z);
+        u64 p = x & m;
+        if (!p) p = 1;
+        cells[2ull * i] = p;
+        cells[2ull * i + 1] = p & y & w;
+    }
+}
+
 void orc_synth_gset(u64 seed, u64 grep, uint32_t E, u64* words) {
     u64 h = replica_key(seed, grep);
     u64 W = (E + 63ull) / 64ull;

@@ -185,19 +185,27 @@ def ops(ctx, steps):
 
 
 def config4(ctx, objects, elements, steps):
-    """map X->2X -> filter even -> fold X->[X,X,X] -> strict threshold vs previous fold.
-    Dictionary-level work (F evaluated once per element) is host-side and not timed;
-    the per-replica work is one gather / filter / gather / inflation launch each."""
-    E = elements
+    """BASELINE configs[3]: 1024 OR-Set objects x 2^20 int elements x T = 3 tokens
+    (laspj_batch_fill_synthetic_tokens) through map X -> 2X, filter even, fold
+    X -> [X, X, X] and the {strict, Prev} threshold read of the fold output.  The
+    dictionary-level work (each fun evaluated once per element, composing the indexes)
+    is host-side and not timed.
+      staged: gather (map) -> filter -> gather (fold) -> strict inflation, every stage's
+              output written: 16+16 + 16+16 + 16+48 + 48+48 = 224 B per input element
+              (+ index / keep reads);
+      fused:  laspj_orset_gather_inflation with the composed index o -> o // 3: src read
+              once (16 B; each cell feeds 3 fold slots from cache), fold written (48 B),
+              Prev read (48 B) = 112 B per input element.  The map / filter outputs are
+              the same gather of src with their own indexes; they are produced on demand,
+              not per step."""
+    E, T = elements, 3
     src = ctx.orset_batch(objects, E)
-    src.fill_synthetic(40)
-    # T = 3 tokens: keep token slots 0..2 (synthetic cells masked on device by a filter
-    # is not possible; tokens beyond slot 2 are simply present - the byte traffic is the
-    # same 16 B per cell either way)
+    src.fill_synthetic(40, token_slots=T)
     mapped = ctx.orset_batch(objects, E)
     filt = ctx.orset_batch(objects, E)
     fold = ctx.orset_batch(objects, 3 * E)
     prev = ctx.orset_batch(objects, 3 * E)
+    prev.fill_synthetic(41, token_slots=T)
     L = ctx.L
     ident = ctx.buffer(4 * E)
     ident.upload(np.arange(E, dtype=np.uint32))       # X -> 2X is monotone: slot order kept
@@ -207,25 +215,43 @@ def config4(ctx, objects, elements, steps):
     fidx.upload(np.repeat(np.arange(E, dtype=np.uint32), 3))
     out = ctx.buffer(objects)
 
-    def step():
+    def staged():
         _lib.check(L.laspj_orset_gather(ctx.h, mapped.h, src.h, ident.h), ctx.h)
         _lib.check(L.laspj_orset_filter(ctx.h, filt.h, mapped.h, keep.h), ctx.h)
         _lib.check(L.laspj_orset_gather(ctx.h, fold.h, filt.h, fidx.h), ctx.h)
         _lib.check(L.laspj_orset_inflation(ctx.h, prev.h, fold.h, 1, out.h), ctx.h)
-    ms = timed(ctx, step, steps)
     cells = objects * E
-    nbytes = 32 * cells + 32 * cells + (16 + 48) * cells + 2 * 48 * cells
-    report("config4_dataflow", ms, nbytes, cells, "input_elements_per_s",
-           objects=objects, elements=E,
+    ms = timed(ctx, staged, steps)
+    report("config4_dataflow", ms, 224 * cells, cells, "input_elements_per_s",
+           objects=objects, elements=E, token_slots=T,
            stages="gather 32B + filter 32B + fold-gather 64B + strict inflation 96B per input element")
+    del mapped, filt
+
+    def fused():
+        _lib.check(L.laspj_orset_gather_inflation(ctx.h, fold.h, src.h, fidx.h, prev.h, 1,
+                                                  out.h), ctx.h)
+    ms = timed(ctx, fused, steps)
+    report("config4_dataflow_fused", ms, 112 * cells, cells, "input_elements_per_s",
+           objects=objects, elements=E, token_slots=T,
+           stages="src 16B read once + fold 48B written + Prev 48B read per input element")
 
 
 def config5(ctx, steps):
     # intersection: 1024 pairs over a 150k-slot dictionary, each side 100k elements
-    P, E = 1024, 150_000
-    l, r = ctx.orset_batch(P, E), ctx.orset_batch(P, E)
-    l.fill_synthetic(5)
-    r.fill_synthetic(6)
+    # L = elements [0, 100k), R = [50k, 150k): 100k-element sets (every element present,
+    # T = 3 tokens) with 50 % id overlap, as tests/test_gpu_configs.py checks them
+    P, E, N = 1024, 150_000, 100_000
+    bl, br = ctx.orset_batch(P, E), ctx.orset_batch(P, E)
+    bl.fill_synthetic(5, token_slots=3)
+    br.fill_synthetic(6, token_slots=3)
+    ids = np.arange(E)
+
+    def bits(mask):
+        b = np.packbits(mask.astype(np.uint8), bitorder="little")
+        return np.concatenate([b, np.zeros((8 * ((E + 63) // 64) - len(b),), np.uint8)]).view(np.uint64)
+    l = ctx.orset_batch(P, E).filter(bl, bits(ids < N))
+    r = ctx.orset_batch(P, E).filter(br, bits(ids >= E - N))
+    del bl, br
     x = l.intersection(r)
     L = ctx.L
     report("config5_intersection", timed(ctx, lambda: _lib.check(
@@ -235,12 +261,8 @@ def config5(ctx, steps):
     # product: 100k x 100k, T = 3 token slots
     n = 100_000
     pl, pr = ctx.orset_batch(1, n), ctx.orset_batch(1, n)
-    h = np.zeros((1, n, 2), np.uint64)
-    rng = np.random.default_rng(5)
-    h[0, :, 0] = rng.integers(1, 8, n, dtype=np.uint64)
-    h[0, :, 1] = h[0, :, 0] & rng.integers(0, 8, n, dtype=np.uint64)
-    pl.upload(h)
-    pr.upload(h)
+    pl.fill_synthetic(7, token_slots=3)
+    pr.fill_synthetic(8, token_slots=3)
     out = engine.ORSetProductBatch(ctx, 1, n, n)
     for rows, cols in ((0, 0), (64, 0), (128, 0), (0, 2048), (0, 4096), (128, 4096)):
         ctx.set_tuning(_lib.TUNE_PRODUCT_ROWS, rows)     # 0 = default tile (256 x 1024)
