@@ -223,6 +223,15 @@ int laspj_orset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
  * Also accepts combinator outputs: a CONCAT cell is visible if Cx ++ Cy has a false
  * flag, a PRODUCT cell (x, y) iff both x and y have one. */
 int laspj_orset_value(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
+/* value({tokens, E}, S) / value({fragment, E}, S) — lasp_orset.erl:76-89: out receives
+ * the 16-byte cell of element slot `element` of every replica (R cells): its tokens are
+ * E's token orddict ([] when p = 0), the fragment is [{E, Tokens}] or [] */
+int laspj_orset_fragment(laspj_ctx* ctx, const laspj_batch* batch, uint32_t element,
+                         laspj_buf* out);
+/* precondition_context/1 — lasp_orset.erl:147-154 with minimum_tokens (:264-267): every
+ * element keeps the tokens flagged false (p & ~r, r = 0) and drops out when none is
+ * left; dst may alias src */
+int laspj_orset_precondition_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
 /* value(removed, S) — lasp_orset.erl:90-95: elements with a token flagged true */
 int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
 /* stats/1 — lasp_orset.erl:156-192: per replica {element_count, adds_count,

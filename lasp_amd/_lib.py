@@ -105,6 +105,8 @@ SIGNATURES = {
     "laspj_batch_clear": (i, [vp, vp]),
     "laspj_batch_fill_synthetic": (i, [vp, vp, u64, u64]),
     "laspj_batch_fill_synthetic_tokens": (i, [vp, vp, u64, u64, u32]),
+    "laspj_orset_fragment": (i, [vp, vp, u32, vp]),
+    "laspj_orset_precondition_context": (i, [vp, vp, vp]),
     "laspj_orset_gather_inflation": (i, [vp, vp, vp, vp, vp, i, vp]),
     "laspj_batch_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_join": (i, [vp, vp, vp, vp]),

@@ -118,6 +118,8 @@ hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t words_per_replica);
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                  uint64_t replica_base, uint64_t tmask = ~0ull);
+hipError_t launch_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t e, void* out);
+hipError_t launch_orset_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
 hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                    const uint32_t* index, const laspj_batch* prev, bool strict,
                                    uint8_t* res);

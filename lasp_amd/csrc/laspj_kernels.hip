@@ -453,6 +453,54 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ fragment / context
+// value({tokens, E}) / value({fragment, E}) (lasp_orset.erl:76-89): the cell of element
+// slot e of every replica; precondition_context/1 (:147-154, minimum_tokens :264-267):
+// every element keeps its tokens flagged false, and drops out when none is left.
+
+__global__ __launch_bounds__(kBlock) void k_orset_fragment(const u64x2* cells, u64x2* out,
+                                                           uint64_t R, uint32_t E, uint32_t e) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R;
+         i += (uint64_t)gridDim.x * kBlock)
+        out[i] = cells[i * E + e];
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_orset_context(u64x2* d, const u64x2* a, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        u64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld2<NT>(a + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st2<NT>(d + i + u * stride, u64x2{x[u].x & ~x[u].y, 0});
+    }
+    for (; i < n; i += stride) {
+        const u64x2 x = ld2<NT>(a + i);
+        st2<NT>(d + i, u64x2{x.x & ~x.y, 0});
+    }
+}
+
+hipError_t launch_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t e, void* out) {
+    uint64_t g = (b->replicas + kBlock - 1) / kBlock;
+    if (g > (uint64_t)ctx->cus * 16) g = (uint64_t)ctx->cus * 16;
+    hipLaunchKernelGGL(k_orset_fragment, dim3((unsigned)(g ? g : 1)), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const u64x2*>(b->dev), reinterpret_cast<u64x2*>(out),
+                       b->replicas, b->elements, e);
+    return hipGetLastError();
+}
+
+hipError_t launch_orset_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
+    const uint64_t n = src->replicas * (uint64_t)src->elements;
+    StreamTune t = stream_tune(ctx, n);
+    auto* d = reinterpret_cast<u64x2*>(dst->dev);
+    auto* a = reinterpret_cast<const u64x2*>(src->dev);
+    if (t.unroll == 1) hipLaunchKernelGGL((k_orset_context<1, true>), dim3(t.grid), dim3(kBlock), 0, ctx->stream, d, a, n);
+    else hipLaunchKernelGGL((k_orset_context<2, true>), dim3(t.grid), dim3(kBlock), 0, ctx->stream, d, a, n);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ value / removed
 // One wave per 64-element word: lane l tests element 64*w + l, __ballot packs the bits.
 

@@ -500,6 +500,24 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
     return LASPJ_OK;
 }
 
+int laspj_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t element,
+                         laspj_buf* out) {
+    if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "orset_fragment: bad batch");
+    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "orset_fragment: kind");
+    if (element >= b->elements) return fail(ctx, LASPJ_E_RANGE, "orset_fragment: element slot");
+    if (int s = check_buf(ctx, out, 16ull * b->replicas, "orset_fragment")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_fragment(ctx, b, element, out->dev));
+    return LASPJ_OK;
+}
+
+int laspj_orset_precondition_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
+    if (int s = check_pair(ctx, dst, src, LASPJ_KIND_ORSET, "orset_precondition_context")) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_orset_context(ctx, dst, src));
+    return LASPJ_OK;
+}
+
 int laspj_orset_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                  const laspj_buf* index, const laspj_batch* prev, int strict,
                                  laspj_buf* out) {

@@ -311,6 +311,18 @@ class ORSetBatch(_Batch):
         check(fn(self.ctx.h, self.h, buf.h), self.ctx.h)
         return buf.download(np.uint64).reshape(self.replicas, W)
 
+    def fragment(self, element: int) -> np.ndarray:
+        """(R, 2) cells of one element slot (value({tokens, E}) / {fragment, E})."""
+        buf = self.ctx.buffer(self.replicas * 16)
+        check(self.ctx.L.laspj_orset_fragment(self.ctx.h, self.h, element, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, 2)
+
+    def precondition_context(self, src: "ORSetBatch"):
+        """self := precondition_context(src) per replica."""
+        check(self.ctx.L.laspj_orset_precondition_context(self.ctx.h, self.h, src.h),
+              self.ctx.h)
+        return self
+
     def stats(self) -> np.ndarray:
         buf = self.ctx.buffer(self.replicas * 24)
         check(self.ctx.L.laspj_orset_stats(self.ctx.h, self.h, buf.h), self.ctx.h)

@@ -78,18 +78,30 @@ def value2(query, s):
         toks = value2(("tokens", query[1]), s)
         return [] if toks == [] else [(query[1], toks)]
     if isinstance(query, tuple) and len(query) == 2 and query[0] == "tokens":
+        # orddict:find(Elem, ORSet): the element's cell, read on the device
         dom = Domain()
         b, _ = _batch(dom, [s])
         es = dom.element_slot(query[1], create=False)
         if es < 0:
             return []
-        cells = b.download()[0]
-        return dict(dom.decode_orset(cells)).get(dom.elements.terms[es], [])
+        cell = b.fragment(es)[0]
+        p, r = int(cell[0]), int(cell[1])
+        td = dom.tokens[es]
+        return [(td.terms[k], bool((r >> int(k)) & 1)) for k in td.order() if (p >> int(k)) & 1]
     if query == "removed":
         dom = Domain()
         b, _ = _batch(dom, [s])
         return dom.decode_value_bits(b.value_bits(removed=True)[0])
     return value(s)
+
+
+def precondition_context(s):
+    """precondition_context/1 — lasp_orset.erl:147-154: the adds observed (tokens
+    flagged false), computed on the device."""
+    dom = Domain()
+    b, E = _batch(dom, [s])
+    out = context().orset_batch(1, E).precondition_context(b)
+    return dom.decode_orset(out.download()[0])
 
 
 def update(op, actor, s):

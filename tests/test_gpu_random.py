@@ -158,3 +158,15 @@ def test_store_rebinds_intersection_twice():
     assert exact_eq(ds.result, os_.result)
     toks = [tok for tok, _f in os_.result[0][1]]
     assert len(toks) != len(set(toks)), "the reference's merge duplicates a token here"
+
+
+@SETTINGS
+@given(SET, ELEM)
+def test_value2_and_precondition_context(ops, e):
+    """value/2 ({tokens, E}, {fragment, E}, removed) and precondition_context/1 on the
+    device against the oracle (lasp_orset.erl:75-97, 147-154, 264-267)."""
+    from lasp_amd import orset as do
+    s = build(ops, 3)
+    for q in (("tokens", e), ("fragment", e), "removed"):
+        assert exact_eq(do.value2(q, s), oorset.value2(q, s)), q
+    assert exact_eq(do.precondition_context(s), oorset.precondition_context(s))
