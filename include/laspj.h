@@ -202,6 +202,22 @@ int laspj_batch_fill_synthetic_tokens(laspj_ctx* ctx, laspj_batch* batch, uint64
 int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b);
 
+/* Many variables per launch (the bind path and the process loop over a store of
+ * one-replica batches, lasp_core.erl:291-312, lasp_process.erl:61-95): n triples /
+ * pairs of one-replica OR-Set, G-Set or G-Counter batches (a triple's batches share
+ * kind and shape; triples may differ), one kernel over all of them.
+ * bind_many: status[i] = 0 when cur[i] =:= val[i] (bind is a no-op, :294-296); else
+ *   dst[i] := merge(cur[i], val[i]) and status[i] = 1 (a canonical merge always
+ *   inflates cur, and the reference writes whenever it does, :301-303).  dst[i] may be
+ *   cur[i].  inflation_many: out[i] = is_inflation (strict = 0) / is_strict_inflation
+ *   (strict = 1) of prev[i] -> cur[i] per kind (lasp_lattice.erl:137-161, 169-179,
+ *   212-253, 273-275).  Both return after the work has completed. */
+int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
+                          const laspj_batch* const* cur, const laspj_batch* const* val,
+                          laspj_buf* status);
+int laspj_batch_inflation_many(laspj_ctx* ctx, uint32_t n, const laspj_batch* const* prev,
+                               const laspj_batch* const* cur, int strict, laspj_buf* out);
+
 /* Anti-entropy reduce step: src holds nchunks copies of dst's replica
  * range laid out chunk-major (what an all-to-all delivers); dst[i] = ⊔_j src[j*R + i].
  * Any kind; src.replicas = nchunks * dst.replicas.  ⊔ is the kind's join: OR of the

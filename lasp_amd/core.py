@@ -195,6 +195,45 @@ class Store:
                 raise Unsupported(str(e)) if e.status == _lib.E_UNSUPPORTED else e
         return ("ok", (id_, v.type, value))
 
+    def bind_many(self, pairs):
+        """Many binds as one device launch (laspj_batch_bind_many): every pair
+        (id, term) whose variable and value are canonical is encoded, then ONE kernel
+        does `Value0 =:= Value` + merge + write for all of them and ONE status download
+        says which variables were written (lasp_core.erl:291-312 for each); other pairs
+        bind one by one.  The writes land first and the dataflow then runs once over all
+        of them — one of the interleavings the reference's asynchronous processes allow
+        (its lasp_process readers race with binds), and the same result whenever the
+        outputs are canonical, where merges commute."""
+        pend, rest = [], []
+        for id_, term in pairs:
+            v = self.vars[id_]
+            if v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter") and \
+                    v.rep == "canonical" and not v.empty and id_ not in (p[0] for p in pend):
+                try:
+                    dv = self._encode(v.type, term, v.pairs)
+                except (NonCanonical, CapacityError, ValueError, TypeError):
+                    continue                     # merge would throw: bind swallows it
+                if dv.rep == "canonical":
+                    pend.append((id_, v, dv))
+                    continue
+            rest.append((id_, term))
+        if pend:
+            dsts = [_new_like(self.ctx, v.val) for _i, v, _d in pend]
+            st = self.ctx.bind_many(dsts, [v.val for _i, v, _d in pend],
+                                    [d.batch for _i, _v, d in pend])
+            self._depth += 1                      # one propagation after all writes
+            try:
+                for (id_, v, _d), dst, s_ in zip(pend, dsts, st):
+                    if s_:
+                        v.val = dst
+                        self._written(id_, v)
+            finally:
+                self._depth -= 1
+            self._propagate()
+        for id_, term in rest:
+            self.bind(id_, term)
+        return [("ok", (i, self.vars[i].type, t)) for i, t in pairs]
+
     def _bind_device(self, id_, v: _Var, dv: _Value):
         t = v.type
         if v.empty:
@@ -360,6 +399,7 @@ class Store:
             changed = True
             while changed:
                 changed = False
+                pre = self._strict_checks()
                 for proc in list(self.procs):
                     for i in proc["inputs"]:
                         if proc not in self.procs:
@@ -369,12 +409,18 @@ class Store:
                         if v.empty:
                             continue
                         # {strict, new()}: a non-empty value is a strict inflation of []
-                        if last is not None and (last.batch is v.val or
-                                                 not self._inflates(v, last, strict=True)):
-                            # unchanged since read: one re-run per write (a list with
-                            # repeated keys can strictly inflate itself, on which the
-                            # reference's reader re-fires forever)
-                            continue
+                        if last is not None:
+                            if last.batch is v.val:
+                                # unchanged since read: one re-run per write (a list
+                                # with repeated keys can strictly inflate itself, on
+                                # which the reference's reader re-fires forever;
+                                # DESIGN.md §2)
+                                continue
+                            hit = pre.get((id(proc), i))
+                            fire = hit[1] if hit is not None and hit[0] is v.val and \
+                                hit[2] is last.batch else self._inflates(v, last, strict=True)
+                            if not fire:
+                                continue
                         proc["seen"][i] = _Value(v.rep, v.val, v.pairs, empty=False)
                         try:
                             proc["body"](proc["seen"])
@@ -384,6 +430,25 @@ class Store:
                         changed = True
         finally:
             self._depth -= 1
+
+    def _strict_checks(self):
+        """Every pending {strict, Last} re-check between canonical values, in ONE
+        launch (laspj_batch_inflation_many): {(proc, input): (value, result, last)}."""
+        keys, prevs, curs = [], [], []
+        for proc in self.procs:
+            for i in proc["inputs"]:
+                v, last = self.vars[i], proc["seen"][i]
+                if v.empty or last is None or last.batch is v.val:
+                    continue
+                if v.rep == "canonical" and last.rep == "canonical" and \
+                        v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter"):
+                    keys.append(((id(proc), i), v.val, last.batch))
+                    prevs.append(last.batch)
+                    curs.append(v.val)
+        if len(keys) < 2:
+            return {}
+        res = self.ctx.inflation_many(prevs, curs, strict=True)
+        return {k: (val, bool(r), lb) for (k, val, lb), r in zip(keys, res)}
 
     def _bind_out(self, out_id, dv):
         if dv is not None:

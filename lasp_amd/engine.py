@@ -23,9 +23,38 @@ class Context:
         check(self.L.laspj_ctx_create(device, C.byref(h)))
         self.h = h
         self.device = device
+        # free lists of small batches (the bind path allocates one per call): a batch
+        # handle goes back here when its Python object dies and is cleared on reuse
+        self._pool = {}
+        self.pool_hits = 0
+
+    POOL_MAX_BYTES = 4 << 20
+    POOL_MAX_PER_SHAPE = 64
+
+    def _pool_take(self, key):
+        lst = self._pool.get(key)
+        if lst:
+            h = lst.pop()
+            check(self.L.laspj_batch_clear(self.h, h), self.h)      # new() again
+            self.pool_hits += 1
+            return h
+        return None
+
+    def _pool_give(self, key, h, nbytes) -> bool:
+        if nbytes > self.POOL_MAX_BYTES:
+            return False
+        lst = self._pool.setdefault(key, [])
+        if len(lst) >= self.POOL_MAX_PER_SHAPE:
+            return False
+        lst.append(h)
+        return True
 
     def close(self):
         if getattr(self, "h", None):
+            for lst in getattr(self, "_pool", {}).values():
+                for h in lst:
+                    self.L.laspj_batch_destroy(h)
+            self._pool = {}
             self.L.laspj_ctx_destroy(self.h)
             self.h = None
 
@@ -62,6 +91,29 @@ class Context:
 
     def event(self) -> "Event":
         return Event(self)
+
+    # -- many one-replica batches per launch
+    def bind_many(self, dsts, curs, vals) -> np.ndarray:
+        """laspj_batch_bind_many: status per item (0 = no-op, 1 = merged into dst)."""
+        n = len(curs)
+        if n == 0:
+            return np.zeros((0,), dtype=np.uint8)
+        arr = lambda xs: (C.c_void_p * n)(*[x.h.value for x in xs])  # noqa: E731
+        st = self.buffer(n)
+        check(self.L.laspj_batch_bind_many(self.h, n, arr(dsts), arr(curs), arr(vals), st.h),
+              self.h)
+        return st.download(np.uint8)
+
+    def inflation_many(self, prevs, curs, strict: bool) -> np.ndarray:
+        """laspj_batch_inflation_many: is_(strict_)inflation(prev[i], cur[i])."""
+        n = len(curs)
+        if n == 0:
+            return np.zeros((0,), dtype=bool)
+        arr = lambda xs: (C.c_void_p * n)(*[x.h.value for x in xs])  # noqa: E731
+        out = self.buffer(n)
+        check(self.L.laspj_batch_inflation_many(self.h, n, arr(prevs), arr(curs), int(strict),
+                                                out.h), self.h)
+        return out.download(np.uint8).astype(bool)
 
 
 def device_count() -> int:
@@ -156,9 +208,13 @@ class _Batch:
 
     def __init__(self, ctx: Context, replicas: int, elements: int):
         self.ctx = ctx
-        h = C.c_void_p()
-        check(getattr(ctx.L, self._create)(ctx.h, replicas, elements, C.byref(h)), ctx.h)
+        key = (self._create, replicas, elements)
+        h = ctx._pool_take(key)
+        if h is None:
+            h = C.c_void_p()
+            check(getattr(ctx.L, self._create)(ctx.h, replicas, elements, C.byref(h)), ctx.h)
         self.h = h
+        self._pool_key = key
         self.replicas = replicas
         self.elements = elements
         info = _lib.BatchInfo()
@@ -168,7 +224,9 @@ class _Batch:
 
     def __del__(self):
         if getattr(self, "h", None) and getattr(self.ctx, "h", None):
-            self.ctx.L.laspj_batch_destroy(self.h)
+            key = getattr(self, "_pool_key", None)
+            if key is None or not self.ctx._pool_give(key, self.h, self.nbytes):
+                self.ctx.L.laspj_batch_destroy(self.h)
             self.h = None
 
     @property

@@ -1,0 +1,113 @@
+"""Many variables per launch: laspj_batch_bind_many / laspj_batch_inflation_many against
+the one-variable kernels, and the Store's batched bind path (bind_many, the batched
+{strict, Last} re-checks of the process loop) against sequential binds on the oracle
+store (lasp_core.erl:291-312, lasp_process.erl:61-95)."""
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from oracle import core as ocore
+from oracle import orset as oorset
+from oracle.terms import exact_eq
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from lasp_amd.orset import context
+    return context()
+
+
+def _batches(ctx, kind, n, E, seed):
+    mk = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[kind]
+    out = []
+    for i in range(n):
+        b = mk(1, E)
+        b.fill_synthetic(seed, replica_base=i)
+        out.append(b)
+    return out
+
+
+def test_bind_many_matches_single_kernels(ctx):
+    """Mixed kinds and shapes in one call; equal pairs are no-ops (status 0), others are
+    merged (OR / per-actor max) into dst (status 1)."""
+    shapes = [("o", 4096), ("o", 100), ("g", 5000), ("c", 300), ("o", 12000), ("g", 64)]
+    curs, vals, dsts, want = [], [], [], []
+    for j, (k, E) in enumerate(shapes):
+        a = _batches(ctx, k, 1, E, 2 + j)[0]
+        b = _batches(ctx, k, 1, E, 30 + j)[0] if j % 3 else a     # every third: equal
+        d = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
+        curs.append(a)
+        vals.append(b)
+        dsts.append(d)
+        want.append(0 if b is a else 1)
+    st = ctx.bind_many(dsts, curs, vals)
+    assert list(st) == want
+    for (k, E), a, b, d, s in zip(shapes, curs, vals, dsts, st):
+        if s:
+            ref = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
+            ref.join(a, b)
+            assert np.array_equal(d.download_words(), ref.download_words())
+    # in place (dst = cur)
+    a, b = _batches(ctx, "o", 1, 777, 5)[0], _batches(ctx, "o", 1, 777, 6)[0]
+    ref = ctx.orset_batch(1, 777).join(a, b)
+    assert list(ctx.bind_many([a], [a], [b])) == [1]
+    assert np.array_equal(a.download_words(), ref.download_words())
+
+
+def test_inflation_many_matches_single_kernels(ctx):
+    pairs = []
+    for k, E in (("o", 4096), ("o", 50), ("g", 3000), ("c", 200), ("o", 9000)):
+        p = _batches(ctx, k, 1, E, 11)[0]
+        q = _batches(ctx, k, 1, E, 12)[0]
+        m = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
+        m.join(p, q)
+        empty = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
+        pairs += [(p, m), (m, p), (p, p), (q, m), (empty, p), (p, empty), (empty, empty)]
+    for strict in (False, True):
+        got = ctx.inflation_many([a for a, _ in pairs], [b for _, b in pairs], strict)
+        want = [bool(b.is_inflation_of(a, strict=strict)[0]) for a, b in pairs]
+        assert list(got) == want, strict
+
+
+SET = st.lists(st.tuples(st.sampled_from(["add", "remove"]), st.integers(0, 9)), max_size=10)
+
+
+@settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(st.tuples(st.integers(0, 3), SET), min_size=1, max_size=6))
+def test_store_bind_many_vs_sequential_oracle(batch):
+    """Store.bind_many over canonical variables feeding canonical outputs (union, filter)
+    ends where the oracle's sequential binds end."""
+    from lasp_amd import core as dcore
+    ds, os_ = dcore.Store(capacity=64), ocore.Store()
+
+    def setup(store):
+        ids = [store.declare("lasp_orset")[1] for _ in range(6)]
+        store.union(ids[0], ids[1], ids[4])
+        store.filter(ids[2], lambda x: x % 2 == 0, ids[5])
+        return ids
+    idd, ido = setup(ds), setup(os_)
+    seed = oorset.TokenSource(4)
+    terms = []
+    for var, ops in batch:
+        s = oorset.new()
+        for op in ops:
+            if op[0] == "add":
+                op = ("add_by_token", seed(), op[1])
+            r = oorset.update(op, None, s)
+            if r[0] == "ok":
+                s = r[1]
+        terms.append((var, s))
+    # every variable starts non-empty so the batched path is the one taken
+    for k in range(4):
+        first = [(("add_by_token", bytes([k + 1]) * 20, 100 + k))]
+        for store, ids in ((ds, idd), (os_, ido)):
+            store.update(ids[k], first[0], None)
+    ds.bind_many([(idd[v], s) for v, s in terms])
+    for v, s in terms:
+        os_.bind(ido[v], s)
+    for a, b in zip(idd, ido):
+        assert exact_eq(ds.value(a), os_.value(b))
+    assert ds.ctx.pool_hits > 0
