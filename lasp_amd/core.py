@@ -202,8 +202,9 @@ class Store:
         says which variables were written (lasp_core.erl:291-312 for each); other pairs
         bind one by one.  The writes land first and the dataflow then runs once over all
         of them — one of the interleavings the reference's asynchronous processes allow
-        (its lasp_process readers race with binds), and the same result whenever the
-        outputs are canonical, where merges commute."""
+        (its lasp_process readers race with binds).  Schedules are observable (the
+        union body keeps the left side's tokens, and re-runs merge into the output), so
+        this is that interleaving, not the one-bind-at-a-time one."""
         pend, rest = [], []
         for id_, term in pairs:
             v = self.vars[id_]

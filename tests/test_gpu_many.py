@@ -78,8 +78,9 @@ SET = st.lists(st.tuples(st.sampled_from(["add", "remove"]), st.integers(0, 9)),
 @settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(st.tuples(st.integers(0, 3), SET), min_size=1, max_size=6))
 def test_store_bind_many_vs_sequential_oracle(batch):
-    """Store.bind_many over canonical variables feeding canonical outputs (union, filter)
-    ends where the oracle's sequential binds end."""
+    """Store.bind_many ends where the oracle ends when it applies the same binds with the
+    dataflow deferred until all of them have landed (the interleaving bind_many runs;
+    the keep-left union makes the schedule observable, so the oracle runs the same one)."""
     from lasp_amd import core as dcore
     ds, os_ = dcore.Store(capacity=64), ocore.Store()
 
@@ -106,8 +107,13 @@ def test_store_bind_many_vs_sequential_oracle(batch):
         for store, ids in ((ds, idd), (os_, ido)):
             store.update(ids[k], first[0], None)
     ds.bind_many([(idd[v], s) for v, s in terms])
-    for v, s in terms:
-        os_.bind(ido[v], s)
+    os_._depth += 1                      # writes first, then one propagation
+    try:
+        for v, s in terms:
+            os_.bind(ido[v], s)
+    finally:
+        os_._depth -= 1
+    os_._propagate()
     for a, b in zip(idd, ido):
         assert exact_eq(ds.value(a), os_.value(b))
     assert ds.ctx.pool_hits > 0

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Latency of the drop-in's host paths (not the batched headline):
+  * config 1 end to end: lasp_orset:merge/2 of two 10k-element orddicts through the
+    mirror (lasp_amd.orset.merge: dictionary + encode, upload, k_or16, download, decode)
+    next to the kernel on resident inputs;
+  * the Store's bind path: 1000 OR-Set variables each bound to a new value, one bind/3
+    at a time vs Store.bind_many (one laspj_batch_bind_many launch);
+  * a list-value re-bind (an intersection output re-run after an input change)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from lasp_amd import core, orset  # noqa: E402
+from lasp_amd.terms import Atom  # noqa: E402
+
+
+def cfg1_terms(n=10_000):
+    ta = [(e, [(b"A" + e.to_bytes(19, "big"), False)]) for e in range(n)]
+    tb = [(e, [(b"B" + e.to_bytes(19, "big"), e % 10 == 0)]) for e in range(n)]
+    return ta, tb
+
+
+def main():
+    out = {}
+    a, b = cfg1_terms()
+    orset.merge(a, b)
+    t0 = time.perf_counter()
+    it = 5
+    for _ in range(it):
+        m = orset.merge(a, b)
+    out["config1_mirror_merge_us"] = (time.perf_counter() - t0) / it * 1e6
+    assert len(m) == 10_000
+    ctx = orset.context()
+    A, B, C = ctx.orset_batch(1, 20_000), ctx.orset_batch(1, 20_000), ctx.orset_batch(1, 20_000)
+    A.fill_synthetic(2)
+    B.fill_synthetic(3)
+    C.join(A, B)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        C.join(A, B)
+    ctx.synchronize()
+    out["config1_kernel_merge_us"] = (time.perf_counter() - t0) / 200 * 1e6
+
+    n = 1000
+    st = core.Store(capacity=256)
+    ids = [st.declare("lasp_orset")[1] for _ in range(n)]
+    for k, i in enumerate(ids):
+        st.update(i, ("add_by_token", b"x" * 19 + bytes([k % 251]), k % 200), Atom("a"))
+    vals = [[(k % 200, [(b"y" * 19 + bytes([k % 251]), False)])] for k in range(n)]
+    t0 = time.perf_counter()
+    for i, v in zip(ids, vals):
+        st.bind(i, v)
+    out["store_bind_sequential_us"] = (time.perf_counter() - t0) / n * 1e6
+    vals2 = [[(k % 200, [(b"z" * 19 + bytes([k % 251]), False)])] for k in range(n)]
+    t0 = time.perf_counter()
+    st.bind_many(list(zip(ids, vals2)))
+    out["store_bind_many_us_per_bind"] = (time.perf_counter() - t0) / n * 1e6
+    out["pool_hits"] = ctx.pool_hits
+
+    s2 = core.Store(capacity=256)
+    l, r, x = (s2.declare("lasp_orset")[1] for _ in range(3))
+    s2.intersection(l, r, x)
+    for e in range(100):
+        s2.update(l, ("add_by_token", b"l" + e.to_bytes(19, "big"), e), Atom("a"))
+        s2.update(r, ("add_by_token", b"r" + e.to_bytes(19, "big"), e), Atom("a"))
+    t0 = time.perf_counter()
+    k = 20
+    for e in range(k):
+        s2.update(l, ("add_by_token", b"m" + e.to_bytes(19, "big"), e), Atom("a"))
+    out["list_rebind_update_plus_rerun_ms"] = (time.perf_counter() - t0) / k * 1e3
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
