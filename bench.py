@@ -103,17 +103,17 @@ def antientropy_leg(ctx, args, rank, world, barrier):
     from lasp_amd.engine import Comm
     comm = Comm(ctx, world, _uid(rank), rank)
     O, E = args.ae_objects, args.elements
-    st, rv, ch = ctx.orset_batch(O, E), ctx.orset_batch(O, E), ctx.orset_batch(O // world, E)
+    st, rv = ctx.orset_batch(O, E), ctx.orset_batch(O, E)
     st.fill_synthetic(10 + rank)
     ctx.synchronize()
-    comm.antientropy(st, rv, ch)                 # warm-up round (RCCL connection setup)
+    comm.antientropy(st, rv)                     # warm-up round (RCCL connection setup)
     ctx.synchronize()
     ok = _sampled_join_ok(ctx, st, lambda: ctx.orset_batch(1, E),
                           lambda d, a, b: d.join(a, b), 10, world, O)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.ae_rounds):
-        comm.antientropy(st, rv, ch)
+        comm.antientropy(st, rv)
     ctx.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -124,7 +124,9 @@ def antientropy_leg(ctx, args, rank, world, barrier):
     xgmi = 2.0 * (world - 1) / world * S / per_round / 1e9 if world > 1 else 0.0
     out = {
         "workload": "gossip anti-entropy (BASELINE configs[2]) via laspj_antientropy: "
-                    "RCCL all-to-all + HIP OR + RCCL all-gather on the engine stream",
+                    "RCCL all-to-all + HIP OR (own chunk joined in place) + RCCL "
+                    "all-gather, all on the engine stream",
+        "hbm_bytes_per_round": S + S // world,
         "objects_per_gpu": O, "elements": E, "state_bytes_per_gpu": S,
         "rounds": args.ae_rounds, "ms_per_round": per_round * 1e3,
         "merged_elements_per_s": (world - 1) * O * E / per_round,
@@ -132,7 +134,7 @@ def antientropy_leg(ctx, args, rank, world, barrier):
         "frac_mesh": xgmi / (XGMI_LINK_GBS * 7), "frac_ring": xgmi / XGMI_LINK_GBS,
         "converged": t[1].item() == 0.0,
     }
-    del st, rv, ch
+    del st, rv
     out["gcounter"] = gcounter_leg(ctx, args, rank, world, barrier, comm)
     comm.close()
     return out

@@ -473,8 +473,11 @@ int laspj_comm_init_rank(laspj_ctx* ctx, int nranks, const uint8_t* id, int rank
 int laspj_comm_init_all(laspj_ctx* const* ctxs, int n, laspj_comm** out);
 int laspj_comm_destroy(laspj_comm* comm);
 int laspj_comm_info(const laspj_comm* comm, int* rank, int* nranks);
-/* one round on this rank: state (R objects, R % nranks == 0), recv (R, scratch) and
- * chunk (R / nranks, scratch) of state's kind; for G-Counters recv and chunk may be NULL */
+/* one round on this rank: state (R objects, R % nranks == 0, nranks <= 8) and recv (R
+ * objects of state's kind: the peers' copies land there).  The rank's own chunk is
+ * joined in place in state and sent from there; `chunk` is not needed (may be NULL; when
+ * given it must hold R / nranks objects and is left untouched).  For G-Counters recv
+ * may be NULL too. */
 int laspj_antientropy(laspj_comm* comm, laspj_batch* state, laspj_batch* recv,
                       laspj_batch* chunk);
 /* the same for n communicators of one process (laspj_comm_init_all), as one RCCL group

@@ -115,18 +115,22 @@ int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batc
         return fail(ctx, LASPJ_E_INVAL, "%s: state must be an OR-Set, G-Set or G-Counter batch of "
                     "the communicator's context", what);
     if (state->kind == LASPJ_KIND_GCOUNTER) return LASPJ_OK;   // in place, no scratch
-    if (!recv || !chunk || recv->ctx != ctx || chunk->ctx != ctx)
-        return fail(ctx, LASPJ_E_INVAL, "%s: recv / chunk batches missing", what);
-    if (recv->kind != state->kind || chunk->kind != state->kind)
+    if (!recv || recv->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: recv batch missing", what);
+    if (recv->kind != state->kind || (chunk && chunk->kind != state->kind))
         return fail(ctx, LASPJ_E_KIND, "%s: kinds differ", what);
     const uint64_t n = (uint64_t)c->nranks;
+    if (n > 8)
+        return fail(ctx, LASPJ_E_UNSUPPORTED, "%s: more than 8 ranks (one node's GPUs)", what);
     if (state->replicas % n || recv->replicas != state->replicas ||
-        chunk->replicas * n != state->replicas || recv->elements != state->elements ||
-        chunk->elements != state->elements)
-        return fail(ctx, LASPJ_E_SHAPE, "%s: need objects %% ranks == 0, recv = state, "
-                    "chunk = objects / ranks", what);
-    if (recv->dev == state->dev || chunk->dev == state->dev || chunk->dev == recv->dev)
-        return fail(ctx, LASPJ_E_INVAL, "%s: state, recv and chunk must not alias", what);
+        recv->elements != state->elements ||
+        (chunk && (chunk->replicas * n != state->replicas || chunk->elements != state->elements)))
+        return fail(ctx, LASPJ_E_SHAPE, "%s: need objects %% ranks == 0, recv = state "
+                    "(chunk, when given = objects / ranks)", what);
+    if (recv->dev == state->dev)
+        return fail(ctx, LASPJ_E_INVAL, "%s: state and recv must not alias", what);
+    if ((state->words_per_replica * (state->replicas / n)) & 1)
+        return fail(ctx, LASPJ_E_SHAPE, "%s: a chunk must hold an even word count", what);
     return LASPJ_OK;
 }
 
@@ -147,48 +151,41 @@ int p2p(const Rccl* R, laspj_comm* c, const uint64_t* src, uint64_t* dst, uint64
 }
 
 // the phases of one bitmap round, enqueued on the context's stream (the caller groups
-// the RCCL calls).  The rank's own chunk is a device copy, not a self-send.
+// the RCCL calls).  The rank's own chunk never moves: the reduce reads it in place in
+// the state, joins the peers' copies from the receive buffer into it, and the all-gather
+// sends it from there.  Per round this rank moves (n-1)/n S over xGMI each way and reads
+// S + writes S/n of HBM for the join.
 int phase_all_to_all(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
     laspj_ctx* ctx = c->ctx;
     const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
     for (int p = 0; p < c->nranks; ++p) {
-        // this rank's copy of chunk p goes to rank p, which stores it at slot `rank`;
-        // the copy of chunk `rank` held by rank p arrives at slot p
-        if (p == c->rank) {
-            LJ_HIP(ctx, hipMemcpyAsync(recv->dev + (uint64_t)p * cw, state->dev + (uint64_t)p * cw,
-                                       cw * 8ull, hipMemcpyDeviceToDevice, ctx->stream));
-            continue;
-        }
-        for (uint64_t off = 0; off < cw; off += kPiece) {
-            const uint64_t len = cw - off < kPiece ? cw - off : kPiece;
-            LJ_NCCL(ctx, R, R->Send(state->dev + (uint64_t)p * cw + off, len, ncclUint64, p,
-                                    c->comm, ctx->stream));
-            LJ_NCCL(ctx, R, R->Recv(recv->dev + (uint64_t)p * cw + off, len, ncclUint64, p,
-                                    c->comm, ctx->stream));
-        }
+        // this rank's copy of chunk p goes to rank p; rank p's copy of chunk `rank`
+        // arrives at slot p of recv
+        if (p == c->rank) continue;
+        if (int s = p2p(R, c, state->dev + (uint64_t)p * cw, recv->dev + (uint64_t)p * cw, cw, p))
+            return s;
     }
     return LASPJ_OK;
 }
 
-int phase_reduce(laspj_comm* c, laspj_batch* recv, laspj_batch* chunk) {
+int phase_reduce(laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
     laspj_ctx* ctx = c->ctx;
-    LJ_HIP(ctx, laspj::launch_reduce_chunks(ctx, chunk->dev, recv->dev,
-                                            chunk->replicas * chunk->words_per_replica,
-                                            (uint32_t)c->nranks, false));
+    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
+    uint64_t* own = state->dev + (uint64_t)c->rank * cw;
+    const uint64_t* srcs[8];
+    for (int p = 0; p < c->nranks; ++p)
+        srcs[p] = p == c->rank ? own : recv->dev + (uint64_t)p * cw;
+    LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, own, srcs, (uint32_t)c->nranks, cw, false));
     return LASPJ_OK;
 }
 
 // all-gather as point-to-point pieces: the joined chunk goes to every peer's slot `rank`
-int phase_all_gather(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* chunk) {
-    laspj_ctx* ctx = c->ctx;
-    const uint64_t cw = chunk->replicas * chunk->words_per_replica;
+int phase_all_gather(const Rccl* R, laspj_comm* c, laspj_batch* state) {
+    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
+    const uint64_t* own = state->dev + (uint64_t)c->rank * cw;
     for (int p = 0; p < c->nranks; ++p) {
-        if (p == c->rank) {
-            LJ_HIP(ctx, hipMemcpyAsync(state->dev + (uint64_t)p * cw, chunk->dev, cw * 8ull,
-                                       hipMemcpyDeviceToDevice, ctx->stream));
-            continue;
-        }
-        if (int s = p2p(R, c, chunk->dev, state->dev + (uint64_t)p * cw, cw, p)) return s;
+        if (p == c->rank) continue;
+        if (int s = p2p(R, c, own, state->dev + (uint64_t)p * cw, cw, p)) return s;
     }
     return LASPJ_OK;
 }
@@ -350,12 +347,12 @@ int laspj_antientropy_group(laspj_comm* const* cs, laspj_batch* const* state,
     LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
     for (int i = 0; i < n; ++i) {
         hipSetDevice(cs[i]->ctx->device);
-        if (int s = phase_reduce(cs[i], recv[i], chunk[i])) return s;
+        if (int s = phase_reduce(cs[i], state[i], recv[i])) return s;
     }
     LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
     for (int i = 0; i < n; ++i) {
         hipSetDevice(cs[i]->ctx->device);
-        if (int s = phase_all_gather(R, cs[i], state[i], chunk[i])) {
+        if (int s = phase_all_gather(R, cs[i], state[i])) {
             R->GroupEnd();
             return s;
         }

@@ -114,6 +114,8 @@ hipError_t launch_gcounter_incr(laspj_ctx* ctx, laspj_batch* b, const laspj_incr
 // max_join: per-word unsigned max (G-Counter counts) instead of OR (set bitmaps)
 hipError_t launch_reduce_chunks(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                                 uint64_t words, uint32_t nchunks, bool max_join);
+hipError_t launch_reduce_ptrs(laspj_ctx* ctx, uint64_t* dst, const uint64_t* const* srcs,
+                              uint32_t nsrc, uint64_t words, bool max_join);
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t words_per_replica);
 hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,

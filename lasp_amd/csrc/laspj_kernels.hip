@@ -303,15 +303,73 @@ __global__ __launch_bounds__(kBlock) void k_reduce_chunks(u64x2* dst, const u64x
 }
 
 // chunk count known at compile time (world sizes 2..8): all NC loads of a cell are
-// issued before the first join, so a lane keeps NC x 16 B in flight
-template <bool MAX, int NC>
+// issued before the first join, so a lane keeps U x NC x 16 B in flight (U cells per
+// lane per step, a stride apart, as the join's sweep does)
+template <bool MAX, int NC, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_reduce_chunks_n(u64x2* dst, const u64x2* src,
                                                             uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        u64x2 v[U][NC];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < NC; ++j) v[u][j] = ld2<NT>(src + (uint64_t)j * n + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int j = 1; j < NC; ++j) {
+                v[u][0].x = join_word<MAX>(v[u][0].x, v[u][j].x);
+                v[u][0].y = join_word<MAX>(v[u][0].y, v[u][j].y);
+            }
+            st2<NT>(dst + i + u * stride, v[u][0]);
+        }
+    }
+    for (; i < n; i += stride) {
         u64x2 v[NC];
 #pragma unroll
-        for (int j = 0; j < NC; ++j) v[j] = ld2<true>(src + (uint64_t)j * n + i);
+        for (int j = 0; j < NC; ++j) v[j] = ld2<NT>(src + (uint64_t)j * n + i);
+#pragma unroll
+        for (int j = 1; j < NC; ++j) {
+            v[0].x = join_word<MAX>(v[0].x, v[j].x);
+            v[0].y = join_word<MAX>(v[0].y, v[j].y);
+        }
+        st2<NT>(dst + i, v[0]);
+    }
+}
+
+// the same reduce over NC arbitrary source arrays (the anti-entropy round reads the
+// rank's own copy in place in its state and the peers' copies from the receive buffer,
+// and writes the join back into the state: no staging copies)
+struct Srcs {
+    const u64x2* p[8];
+};
+
+template <bool MAX, int NC>
+__global__ __launch_bounds__(kBlock) void k_reduce_ptrs(u64x2* dst, Srcs s, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + stride < n; i += 2 * stride) {
+        u64x2 v[2][NC];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int j = 0; j < NC; ++j) v[u][j] = ld2<true>(s.p[j] + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int j = 1; j < NC; ++j) {
+                v[u][0].x = join_word<MAX>(v[u][0].x, v[u][j].x);
+                v[u][0].y = join_word<MAX>(v[u][0].y, v[u][j].y);
+            }
+            st2<true>(dst + i + u * stride, v[u][0]);
+        }
+    }
+    for (; i < n; i += stride) {
+        u64x2 v[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) v[j] = ld2<true>(s.p[j] + i);
 #pragma unroll
         for (int j = 1; j < NC; ++j) {
             v[0].x = join_word<MAX>(v[0].x, v[j].x);
@@ -319,6 +377,31 @@ __global__ __launch_bounds__(kBlock) void k_reduce_chunks_n(u64x2* dst, const u6
         }
         st2<true>(dst + i, v[0]);
     }
+}
+
+hipError_t launch_reduce_ptrs(laspj_ctx* ctx, uint64_t* dst, const uint64_t* const* srcs,
+                              uint32_t nsrc, uint64_t words, bool max_join) {
+    if (nsrc < 1 || nsrc > 8 || (words & 1)) return hipErrorInvalidValue;
+    Srcs s;
+    for (uint32_t j = 0; j < 8; ++j)
+        s.p[j] = reinterpret_cast<const u64x2*>(srcs[j < nsrc ? j : 0]);
+    const uint64_t n = words / 2;
+    StreamTune t = stream_tune(ctx, n);
+    auto* d = reinterpret_cast<u64x2*>(dst);
+#define LJ_RP(NC)                                                                              \
+    case NC:                                                                                   \
+        if (max_join)                                                                          \
+            hipLaunchKernelGGL((k_reduce_ptrs<true, NC>), dim3(t.grid), dim3(kBlock), 0,      \
+                               ctx->stream, d, s, n);                                          \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_reduce_ptrs<false, NC>), dim3(t.grid), dim3(kBlock), 0,     \
+                               ctx->stream, d, s, n);                                          \
+        break
+    switch (nsrc) {
+        LJ_RP(1); LJ_RP(2); LJ_RP(3); LJ_RP(4); LJ_RP(5); LJ_RP(6); LJ_RP(7); LJ_RP(8);
+    }
+#undef LJ_RP
+    return hipGetLastError();
 }
 
 template <bool MAX>
@@ -340,10 +423,23 @@ static void launch_reduce_chunks_t(laspj_ctx* ctx, uint64_t* dst, const uint64_t
         auto* d2 = reinterpret_cast<u64x2*>(dst);
         auto* s2 = reinterpret_cast<const u64x2*>(src);
         const uint64_t n = words / 2;
+        // cells per lane per step: the unroll knob when set (1 or 2), else 1; the
+        // non-temporal knob as for the join
+        const int u = ctx->tune_unroll == 2 ? 2 : 1;
 #define LJ_RCN(NC)                                                                          \
     case NC:                                                                                \
-        hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC>), dim3(t.grid), dim3(kBlock), 0,    \
-                           ctx->stream, d2, s2, n);                                         \
+        if (u == 2 && t.nt)                                                                 \
+            hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC, 2, true>), dim3(t.grid),        \
+                               dim3(kBlock), 0, ctx->stream, d2, s2, n);                    \
+        else if (u == 2)                                                                    \
+            hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC, 2, false>), dim3(t.grid),       \
+                               dim3(kBlock), 0, ctx->stream, d2, s2, n);                    \
+        else if (t.nt)                                                                      \
+            hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC, 1, true>), dim3(t.grid),        \
+                               dim3(kBlock), 0, ctx->stream, d2, s2, n);                    \
+        else                                                                                \
+            hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC, 1, false>), dim3(t.grid),       \
+                               dim3(kBlock), 0, ctx->stream, d2, s2, n);                    \
         break
         switch (ctx->tune_reduce == 2 ? 0u : nchunks) {
             LJ_RCN(2); LJ_RCN(3); LJ_RCN(4); LJ_RCN(5); LJ_RCN(6); LJ_RCN(7); LJ_RCN(8);

@@ -211,9 +211,9 @@ def test_config3_round_full_size(ctx):
         assert got.equal(acc), o
     del recv, chunk
     comm = Comm(ctx, 1, Comm.unique_id(), 0)
-    st, rv, ch = (ctx.orset_batch(1 << 20, E) for _ in range(3))
+    st, rv = (ctx.orset_batch(1 << 20, E) for _ in range(2))
     st.fill_synthetic(10)
-    comm.antientropy(st, rv, ch)
+    comm.antientropy(st, rv)
     ctx.synchronize()
     for o in (0, 654_321, (1 << 20) - 1):
         assert np.array_equal(st.download(o, 1)[0], orc.synth_orset(10, o, E))

@@ -48,6 +48,10 @@ def report(name, ms, nbytes, units, unit_name, **extra):
     print(json.dumps(d), flush=True)
 
 
+def ctx_cus(ctx) -> int:
+    return 256          # MI355X: 256 CUs (the grid knob takes workgroups)
+
+
 def kernels(ctx, R, E, steps):
     a, b, c = ctx.orset_batch(R, E), ctx.orset_batch(R, E), ctx.orset_batch(R, E)
     a.fill_synthetic(2)
@@ -114,6 +118,20 @@ def kernels(ctx, R, E, steps):
         report(name, timed(ctx, lambda: dst8.reduce_chunks(src8, 8), steps),
                16 * 9 * q * E, q * E, "dst_cells_per_s")
     ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, 0)
+    if os.environ.get("REDUCE_SWEEP"):
+        # launch shape of the N = 8 reduce: grid (workgroups per CU) x cells per lane x NT
+        for grid_per_cu in (8, 16, 32, 64, 128):
+            for unroll in (1, 2):
+                for nt in (1, 0):
+                    ctx.set_tuning(_lib.TUNE_STREAM_GRID, ctx_cus(ctx) * grid_per_cu)
+                    ctx.set_tuning(_lib.TUNE_STREAM_UNROLL, unroll)
+                    ctx.set_tuning(_lib.TUNE_STREAM_NT, nt)
+                    report(f"orset_reduce_chunks_n8_g{grid_per_cu}_u{unroll}_nt{nt}",
+                           timed(ctx, lambda: dst8.reduce_chunks(src8, 8), steps),
+                           16 * 9 * q * E, q * E, "dst_cells_per_s")
+        ctx.set_tuning(_lib.TUNE_STREAM_GRID, 0)
+        ctx.set_tuning(_lib.TUNE_STREAM_UNROLL, 0)
+        ctx.set_tuning(_lib.TUNE_STREAM_NT, -1)
     del src8, dst8
     h = R // 2                      # CONCAT output is 32 B per cell: half the replicas
     a2, b2 = ctx.orset_batch(h, E), ctx.orset_batch(h, E)
