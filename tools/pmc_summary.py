@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--stats-dir", required=True)
     ap.add_argument("--fetch-dir", required=True)
     ap.add_argument("--write-dir", required=True)
-    ap.add_argument("--kernel", default="k_or16")
+    ap.add_argument("--kernel", default="k_or16<2")
     ap.add_argument("--replicas", type=int, default=1 << 20)
     ap.add_argument("--elements", type=int, default=4096)
     ap.add_argument("--out", required=True)
