@@ -594,6 +594,40 @@ int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                     const laspj_buf* off, const laspj_buf* keys, uint32_t nidx,
                     int per_entry);
 
+/* ------------------------------------------------------------------ host dictionary */
+/* The NIF side of the boundary, native (no GPU involved): element / token dictionaries
+ * over external-term-format images (term_to_binary/1 of each term, no version byte),
+ * ordered by Erlang term order, plus the encoder of whole values into cells.  Values
+ * arrive as payloads: optional <<Tag, Vers>> (tag >= 0) + 131 + the ETF of the orddict
+ * [{Elem, [{Token, true|false}]}] (OR-Set) or the ordset list (G-Set), back to back in
+ * `blob` with n + 1 offsets.  Per-payload statuses are the LASPJ_DEC_* codes above. */
+typedef struct laspj_dict laspj_dict;
+/* Erlang term order of two ETF images (-1, 0, 1 in *out); LASPJ_E_UNSUPPORTED for terms
+ * outside this path (pids, refs, funs, maps, bit strings, improper lists) */
+int laspj_term_compare(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, int* out);
+int laspj_dict_create(laspj_dict** out);
+int laspj_dict_destroy(laspj_dict* dict);
+/* register every element and token term the payloads hold (append-only slots; an
+ * element keeps at most 64 token slots: LASPJ_DEC_UNREPRESENTABLE past that) */
+int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const uint64_t* offsets,
+                   uint64_t n, int tag, int32_t* status);
+int laspj_dict_info(const laspj_dict* dict, uint32_t* elements, uint64_t* elem_bytes,
+                    uint64_t* tok_bytes);
+/* the arrays laspj_etf_dict_create takes, for E >= elements slots: elem_blob (elem_bytes)
+ * / elem_off (E + 1) / elem_order (E: slots in term order, unused slots last); tok_blob
+ * (tok_bytes) / tok_off (64 E + 1) / tok_order (64 E, 0xFF after the last) may be NULL */
+int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, uint32_t* elem_off,
+                      uint32_t* elem_order, uint8_t* tok_blob, uint32_t* tok_off,
+                      uint8_t* tok_order);
+/* payloads -> cells over the dictionary: out holds n replicas of the batch layout
+ * (OR-Set 2E words, G-Set ceil(E/64) words).  A value that is not an orddict / ordset
+ * (keys or tokens not strictly ascending in term order) or holds a term outside the
+ * dictionary gets LASPJ_DEC_UNKNOWN_TERM and an empty replica — such lists take the
+ * list path (laspj_list_upload) */
+int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
+                      const uint64_t* offsets, uint64_t n, int tag, uint32_t E, uint64_t* out,
+                      int32_t* status);
+
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);
 int laspj_event_destroy(laspj_event* ev);

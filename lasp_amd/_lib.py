@@ -176,6 +176,13 @@ SIGNATURES = {
     "laspj_list_map": (i, [vp, vp, vp, vp, u32, i]),
     "laspj_list_filter": (i, [vp, vp, vp, vp, u32, i]),
     "laspj_list_fold": (i, [vp, vp, vp, vp, vp, u32, i]),
+    "laspj_term_compare": (i, [vp, C.c_size_t, vp, C.c_size_t, C.POINTER(i)]),
+    "laspj_dict_create": (i, [vpp]),
+    "laspj_dict_destroy": (i, [vp]),
+    "laspj_dict_add": (i, [vp, C.c_int32, vp, vp, u64, i, vp]),
+    "laspj_dict_info": (i, [vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64)]),
+    "laspj_dict_export": (i, [vp, u32, vp, vp, vp, vp, vp, vp]),
+    "laspj_dict_encode": (i, [vp, C.c_int32, vp, vp, u64, i, u32, vp, vp]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

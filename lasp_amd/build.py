@@ -11,7 +11,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblaspj.so")
 SOURCES = ["laspj_runtime.hip", "laspj_kernels.hip", "laspj_combinators.hip",
            "laspj_codec.hip", "laspj_lists.hip", "laspj_comm.hip",
-           "laspj_many.hip"]
+           "laspj_many.hip", "laspj_host.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-value", "-Wno-unused-result"]

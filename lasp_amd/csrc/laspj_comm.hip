@@ -156,7 +156,6 @@ int p2p(const Rccl* R, laspj_comm* c, const uint64_t* src, uint64_t* dst, uint64
 // sends it from there.  Per round this rank moves (n-1)/n S over xGMI each way and reads
 // S + writes S/n of HBM for the join.
 int phase_all_to_all(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
-    laspj_ctx* ctx = c->ctx;
     const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
     for (int p = 0; p < c->nranks; ++p) {
         // this rank's copy of chunk p goes to rank p; rank p's copy of chunk `rank`

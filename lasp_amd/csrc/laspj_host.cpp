@@ -1,0 +1,772 @@
+// Host side of the drop-in, native (what the NIF links; include/laspj.h "host dictionary").
+//
+// The device never sees terms: element and token slots are positions in a dictionary the
+// host keeps, ordered by Erlang term order.  The NIF receives values as terms; the bulk
+// path hands them over as their external term format (term_to_binary/1 images, which
+// the device codec also reads and writes), so the dictionary works on ETF:
+//   * a walker over ETF images (the subset on this path: integers incl. bignums, floats,
+//     atoms in all four encodings, tuples, nil, STRING_EXT and LIST_EXT lists, binaries)
+//     that finds each term's extent without decoding it;
+//   * Erlang's term order over two images (number < atom < tuple < nil < list <
+//     bitstring; numbers compared by value across integer / bignum / float; atoms by
+//     name; tuples by arity then elements; lists element-wise with prefix smaller;
+//     binaries byte-wise), replacing enif_compare;
+//   * the dictionary: element images -> element slot, and per element slot token images
+//     -> token slot (<= 64), append-only, hashed by image bytes; term-order permutations
+//     are computed on export (laspj_dict_export: the arrays laspj_etf_dict_create takes);
+//   * encode: OR-Set / G-Set payloads -> {p, r} cells / bit words over the dictionary,
+//     rejecting a value that is not an orddict / ordset (keys must ascend strictly in
+//     term order), and decode for the reverse direction of small calls.
+// Pure host code: no GPU needed (the CPU test suite runs it).
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/laspj.h"
+
+namespace {
+
+// ------------------------------------------------------------------ ETF reading
+
+enum : int {
+    kSmallInt = 97, kInt = 98, kFloatOld = 99, kAtom = 100, kSmallTuple = 104,
+    kLargeTuple = 105, kNil = 106, kString = 107, kList = 108, kBinary = 109,
+    kSmallBig = 110, kLargeBig = 111, kNewFloat = 70, kSmallAtom = 115, kAtomUtf8 = 118,
+    kSmallAtomUtf8 = 119
+};
+
+inline uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+inline uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+// the extent of the term at p (no version byte); 0 if malformed / unsupported
+size_t term_len(const uint8_t* p, size_t n, int depth = 0) {
+    if (n < 1 || depth > 64) return 0;
+    switch (p[0]) {
+        case kSmallInt: return n >= 2 ? 2 : 0;
+        case kInt: return n >= 5 ? 5 : 0;
+        case kNewFloat: return n >= 9 ? 9 : 0;
+        case kFloatOld: return n >= 32 ? 32 : 0;
+        case kAtom:
+        case kAtomUtf8: {
+            if (n < 3) return 0;
+            size_t l = 3 + be16(p + 1);
+            return l <= n ? l : 0;
+        }
+        case kSmallAtom:
+        case kSmallAtomUtf8: {
+            if (n < 2) return 0;
+            size_t l = 2 + p[1];
+            return l <= n ? l : 0;
+        }
+        case kSmallBig: {
+            if (n < 3) return 0;
+            size_t l = 3 + p[1];
+            return l <= n ? l : 0;
+        }
+        case kLargeBig: {
+            if (n < 6) return 0;
+            size_t l = 6 + (size_t)be32(p + 1);
+            return l <= n ? l : 0;
+        }
+        case kNil: return 1;
+        case kString: {
+            if (n < 3) return 0;
+            size_t l = 3 + be16(p + 1);
+            return l <= n ? l : 0;
+        }
+        case kBinary: {
+            if (n < 5) return 0;
+            size_t l = 5 + (size_t)be32(p + 1);
+            return l <= n ? l : 0;
+        }
+        case kSmallTuple:
+        case kLargeTuple: {
+            const bool small = p[0] == kSmallTuple;
+            if (n < (small ? 2u : 5u)) return 0;
+            uint64_t ar = small ? p[1] : be32(p + 1);
+            size_t off = small ? 2 : 5;
+            for (uint64_t i = 0; i < ar; ++i) {
+                size_t l = term_len(p + off, n - off, depth + 1);
+                if (!l) return 0;
+                off += l;
+            }
+            return off;
+        }
+        case kList: {
+            if (n < 5) return 0;
+            uint64_t cnt = be32(p + 1);
+            size_t off = 5;
+            for (uint64_t i = 0; i <= cnt; ++i) {      // elements, then the tail
+                size_t l = term_len(p + off, n - off, depth + 1);
+                if (!l) return 0;
+                off += l;
+            }
+            return off;
+        }
+        default: return 0;
+    }
+}
+
+int term_class(uint8_t tag) {
+    switch (tag) {
+        case kSmallInt: case kInt: case kSmallBig: case kLargeBig: case kNewFloat: case kFloatOld:
+            return 0;
+        case kAtom: case kSmallAtom: case kAtomUtf8: case kSmallAtomUtf8: return 1;
+        case kSmallTuple: case kLargeTuple: return 6;
+        case kNil: return 8;
+        case kString: case kList: return 9;
+        case kBinary: return 10;
+        default: return -1;
+    }
+}
+
+// a number: an exact integer (sign + little-endian magnitude) or a double
+struct Num {
+    bool is_float = false;
+    double f = 0;
+    int sign = 0;                 // -1, 0, 1
+    std::vector<uint8_t> mag;     // little-endian, no high zero bytes
+};
+
+Num read_num(const uint8_t* p) {
+    Num x;
+    auto set_int = [&](int64_t v) {
+        x.sign = v < 0 ? -1 : (v > 0 ? 1 : 0);
+        uint64_t m = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+        while (m) {
+            x.mag.push_back((uint8_t)m);
+            m >>= 8;
+        }
+    };
+    switch (p[0]) {
+        case kSmallInt: set_int(p[1]); break;
+        case kInt: set_int((int32_t)be32(p + 1)); break;
+        case kSmallBig:
+        case kLargeBig: {
+            const bool small = p[0] == kSmallBig;
+            size_t len = small ? p[1] : be32(p + 1);
+            const uint8_t* s = p + (small ? 2 : 5);
+            x.mag.assign(s + 1, s + 1 + len);
+            while (!x.mag.empty() && x.mag.back() == 0) x.mag.pop_back();
+            x.sign = x.mag.empty() ? 0 : (s[0] ? -1 : 1);
+            break;
+        }
+        case kNewFloat: {
+            uint64_t b = 0;
+            for (int i = 0; i < 8; ++i) b = (b << 8) | p[1 + i];
+            memcpy(&x.f, &b, 8);
+            x.is_float = true;
+            break;
+        }
+        case kFloatOld: {
+            char buf[32];
+            memcpy(buf, p + 1, 31);
+            buf[31] = 0;
+            x.f = strtod(buf, nullptr);
+            x.is_float = true;
+            break;
+        }
+    }
+    return x;
+}
+
+int cmp_mag(const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
+    if (a.size() != b.size()) return a.size() < b.size() ? -1 : 1;
+    for (size_t i = a.size(); i-- > 0;)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return 0;
+}
+
+// integer vs double, exactly: through long double while the integer fits 64 bits (a
+// long double holds a uint64 exactly, and every double converts exactly); beyond that
+// by bit length, then the double's integral magnitude against the bignum's
+int cmp_int_float(const Num& i, double f) {
+    if (std::isnan(f)) return -1;
+    if (std::isinf(f)) return f > 0 ? -1 : 1;
+    long double fi;
+    if (i.mag.size() <= 8) {
+        uint64_t m = 0;
+        for (size_t k = i.mag.size(); k-- > 0;) m = (m << 8) | i.mag[k];
+        fi = (long double)m;
+    } else {
+        const int fs = f < 0 ? -1 : (f > 0 ? 1 : 0);
+        if (i.sign != fs) return i.sign < fs ? -1 : 1;
+        int bits = 8 * (int)(i.mag.size() - 1);
+        for (uint8_t top = i.mag.back(); top; top >>= 1) ++bits;
+        int ex = 0;
+        const double m = std::frexp(std::fabs(f), &ex);   // |f| = m 2^ex, m in [0.5, 1)
+        if (bits != ex) return ((bits < ex) == (i.sign > 0)) ? -1 : 1;
+        // same bit length (> 64, so |f| >= 2^64 is an integer): |f| = mant << (ex - 53)
+        const uint64_t mant = (uint64_t)std::ldexp(m, 53);
+        const int sh = ex - 53;
+        std::vector<uint8_t> fm(i.mag.size() + 1, 0);
+        for (int k = 0; k < 8; ++k) {
+            const unsigned v = (unsigned)((mant >> (8 * k)) & 0xFF) << (sh % 8);
+            const size_t at = (size_t)(k + sh / 8);
+            if (at < fm.size()) fm[at] |= (uint8_t)v;
+            if (at + 1 < fm.size()) fm[at + 1] |= (uint8_t)(v >> 8);
+        }
+        while (!fm.empty() && fm.back() == 0) fm.pop_back();
+        const int c = cmp_mag(i.mag, fm);
+        return i.sign > 0 ? c : -c;
+    }
+    if (i.sign < 0) fi = -fi;
+    const long double lf = f;
+    return fi < lf ? -1 : (fi > lf ? 1 : 0);
+}
+
+int cmp_num(const uint8_t* a, const uint8_t* b) {
+    // integers that fit 32 bits (SMALL_INTEGER_EXT / INTEGER_EXT): no decoding needed
+    if ((a[0] == kSmallInt || a[0] == kInt) && (b[0] == kSmallInt || b[0] == kInt)) {
+        const int64_t x = a[0] == kSmallInt ? a[1] : (int32_t)be32(a + 1);
+        const int64_t y = b[0] == kSmallInt ? b[1] : (int32_t)be32(b + 1);
+        return x < y ? -1 : (x > y ? 1 : 0);
+    }
+    Num x = read_num(a), y = read_num(b);
+    if (x.is_float && y.is_float) return x.f < y.f ? -1 : (x.f > y.f ? 1 : 0);
+    if (!x.is_float && !y.is_float) {
+        if (x.sign != y.sign) return x.sign < y.sign ? -1 : 1;
+        int c = cmp_mag(x.mag, y.mag);
+        return x.sign >= 0 ? c : -c;
+    }
+    if (!x.is_float) return cmp_int_float(x, y.f);
+    return -cmp_int_float(y, x.f);
+}
+
+// an atom's name as UTF-8 (ATOM_EXT / SMALL_ATOM_EXT are latin-1)
+std::string atom_name(const uint8_t* p) {
+    const bool small = p[0] == kSmallAtom || p[0] == kSmallAtomUtf8;
+    const bool utf8 = p[0] == kAtomUtf8 || p[0] == kSmallAtomUtf8;
+    size_t len = small ? p[1] : be16(p + 1);
+    const uint8_t* s = p + (small ? 2 : 3);
+    if (utf8) return std::string((const char*)s, len);
+    std::string out;
+    for (size_t i = 0; i < len; ++i) {
+        if (s[i] < 0x80) out.push_back((char)s[i]);
+        else {
+            out.push_back((char)(0xC0 | (s[i] >> 6)));
+            out.push_back((char)(0x80 | (s[i] & 0x3F)));
+        }
+    }
+    return out;
+}
+
+// 1 for the atom `true`, 0 for `false` (any of the four atom encodings), else -1
+int bool_atom(const uint8_t* p) {
+    const uint8_t* s;
+    size_t len;
+    if (p[0] == kAtom || p[0] == kAtomUtf8) {
+        len = be16(p + 1);
+        s = p + 3;
+    } else if (p[0] == kSmallAtom || p[0] == kSmallAtomUtf8) {
+        len = p[1];
+        s = p + 2;
+    } else {
+        return -1;
+    }
+    if (len == 4 && !memcmp(s, "true", 4)) return 1;
+    if (len == 5 && !memcmp(s, "false", 5)) return 0;
+    return -1;
+}
+
+// elements of a list image, STRING_EXT or LIST_EXT (each STRING_EXT byte stands for a
+// SMALL_INTEGER_EXT element)
+struct ListIt {
+    const uint8_t* p;
+    size_t n;
+    bool str;
+    uint64_t count, i = 0;
+    size_t off;
+    uint8_t tmp[2];
+    explicit ListIt(const uint8_t* img, size_t len) : p(img), n(len) {
+        str = img[0] == kString;
+        count = str ? be16(img + 1) : be32(img + 1);
+        off = str ? 3 : 5;
+    }
+    // the next element's image, or nullptr at the end
+    const uint8_t* next(size_t* len) {
+        if (i >= count) return nullptr;
+        ++i;
+        if (str) {
+            tmp[0] = kSmallInt;
+            tmp[1] = p[off++];
+            *len = 2;
+            return tmp;
+        }
+        const uint8_t* e = p + off;
+        *len = term_len(e, n - off);
+        off += *len;
+        return e;
+    }
+    const uint8_t* tail() const { return str ? nullptr : p + off; }
+};
+
+int term_cmp(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, bool* ok) {
+    const int ca = term_class(a[0]), cb = term_class(b[0]);
+    if (ca < 0 || cb < 0) {
+        *ok = false;
+        return 0;
+    }
+    if (ca != cb) return ca < cb ? -1 : 1;
+    switch (ca) {
+        case 0: return cmp_num(a, b);
+        case 1: {
+            std::string x = atom_name(a), y = atom_name(b);
+            int c = x.compare(y);
+            return c < 0 ? -1 : (c > 0 ? 1 : 0);
+        }
+        case 6: {
+            const bool sa = a[0] == kSmallTuple, sb = b[0] == kSmallTuple;
+            uint64_t ra = sa ? a[1] : be32(a + 1), rb = sb ? b[1] : be32(b + 1);
+            if (ra != rb) return ra < rb ? -1 : 1;
+            size_t oa = sa ? 2 : 5, ob = sb ? 2 : 5;
+            for (uint64_t k = 0; k < ra; ++k) {
+                size_t la = term_len(a + oa, na - oa), lb = term_len(b + ob, nb - ob);
+                int c = term_cmp(a + oa, la, b + ob, lb, ok);
+                if (c || !*ok) return c;
+                oa += la;
+                ob += lb;
+            }
+            return 0;
+        }
+        case 8: return 0;
+        case 9: {
+            ListIt x(a, na), y(b, nb);
+            for (;;) {
+                size_t la = 0, lb = 0;
+                const uint8_t* ea = x.next(&la);
+                const uint8_t* eb = y.next(&lb);
+                if (!ea || !eb) {
+                    // proper lists only: a non-nil tail is outside this path
+                    const uint8_t* ta = x.tail();
+                    const uint8_t* tb = y.tail();
+                    if ((!ea && ta && ta[0] != kNil) || (!eb && tb && tb[0] != kNil)) *ok = false;
+                    if (!ea && !eb) return 0;
+                    return !ea ? -1 : 1;     // a proper prefix is smaller
+                }
+                int c = term_cmp(ea, la, eb, lb, ok);
+                if (c || !*ok) return c;
+            }
+        }
+        case 10: {
+            uint32_t la = be32(a + 1), lb = be32(b + 1);
+            int c = memcmp(a + 5, b + 5, std::min(la, lb));
+            if (c) return c < 0 ? -1 : 1;
+            return la < lb ? -1 : (la > lb ? 1 : 0);
+        }
+    }
+    *ok = false;
+    return 0;
+}
+
+// ------------------------------------------------------------------ dictionary
+
+// images are stored once (a deque keeps their addresses); lookups hash the payload's
+// own bytes in an open-addressing table (linear probing, 64-bit hashes kept beside the
+// slots), so encoding allocates nothing and touches ~one cache line per lookup
+inline uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t seed) {
+    uint64_t h = seed ^ (n * 0x9E3779B97F4A7C15ull);
+    while (n >= 8) {
+        uint64_t v;
+        memcpy(&v, p, 8);
+        h = (h ^ v) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+        p += 8;
+        n -= 8;
+    }
+    uint64_t v = 0;
+    memcpy(&v, p, n);
+    h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 29);
+}
+
+struct Table {
+    struct Ent {
+        uint64_t h;
+        uint32_t owner;          // element slot for token keys, 0 for element keys
+        uint32_t val;
+        std::string_view key;
+    };
+    std::vector<Ent> ents;
+    std::vector<uint32_t> idx;   // entry index + 1, 0 = empty
+    uint64_t mask = 0;
+
+    const Ent* find(uint64_t h, uint32_t owner, std::string_view key) const {
+        if (idx.empty()) return nullptr;
+        for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+            const uint32_t k = idx[i];
+            if (!k) return nullptr;
+            const Ent& e = ents[k - 1];
+            if (e.h == h && e.owner == owner && e.key == key) return &e;
+        }
+    }
+    void grow() {
+        const uint64_t cap = idx.empty() ? 1024 : idx.size() * 2;
+        idx.assign(cap, 0);
+        mask = cap - 1;
+        for (uint32_t k = 0; k < ents.size(); ++k) {
+            uint64_t i = ents[k].h & mask;
+            while (idx[i]) i = (i + 1) & mask;
+            idx[i] = k + 1;
+        }
+    }
+    void insert(uint64_t h, uint32_t owner, std::string_view key, uint32_t val) {
+        if (2 * (ents.size() + 1) > idx.size()) grow();
+        ents.push_back(Ent{h, owner, val, key});
+        uint64_t i = h & mask;
+        while (idx[i]) i = (i + 1) & mask;
+        idx[i] = (uint32_t)ents.size();
+    }
+};
+
+constexpr uint64_t kElemSeed = 0x4C415350ull;
+
+inline uint64_t tok_hash(uint32_t slot, const uint8_t* p, size_t n) {
+    return hash_bytes(p, n, 0x9E3779B97F4A7C15ull * (slot + 1));
+}
+
+struct Dict {
+    std::deque<std::string> store;
+    std::vector<std::string_view> elems;
+    std::vector<std::vector<std::string_view>> toks;
+    Table elem_slot, tok_slot;
+
+    std::string_view keep(const uint8_t* p, size_t n) {
+        store.emplace_back((const char*)p, n);
+        return std::string_view(store.back());
+    }
+    // element slot of an image, or -1
+    int64_t elem(const uint8_t* k, size_t kl) const {
+        const Table::Ent* e = elem_slot.find(hash_bytes(k, kl, kElemSeed), 0,
+                                             std::string_view((const char*)k, kl));
+        return e ? (int64_t)e->val : -1;
+    }
+    int tok(uint32_t es, const uint8_t* t, size_t tl) const {
+        const Table::Ent* e = tok_slot.find(tok_hash(es, t, tl), es,
+                                            std::string_view((const char*)t, tl));
+        return e ? (int)e->val : -1;
+    }
+};
+
+// the payload's term: after an optional <<Tag, Vers>> prefix and the version byte 131
+int payload_term(const uint8_t* p, size_t n, int tag, int vers, const uint8_t** t, size_t* tn) {
+    if (tag >= 0) {
+        if (n < 2 || p[0] != (uint8_t)tag) return LASPJ_DEC_INVALID_BINARY;
+        if (vers >= 0 && p[1] != (uint8_t)vers) return LASPJ_DEC_UNSUPPORTED_VERSION;
+        p += 2;
+        n -= 2;
+    }
+    if (n < 2 || p[0] != 131) return LASPJ_DEC_MALFORMED;
+    size_t l = term_len(p + 1, n - 1);
+    if (!l || l != n - 1) return LASPJ_DEC_MALFORMED;
+    *t = p + 1;
+    *tn = l;
+    return LASPJ_DEC_OK;
+}
+
+// walk [{Elem, [{Tok, Bool}]}]; fn(elem image, tok image, flag) per token, and
+// on_elem(elem image, ntoks) per element; returns a LASPJ_DEC_* status
+template <class OnElem, class OnTok>
+int walk_orset(const uint8_t* t, size_t tn, OnElem on_elem, OnTok on_tok) {
+    if (t[0] == kNil) return LASPJ_DEC_OK;
+    if (t[0] != kList) return LASPJ_DEC_MALFORMED;
+    ListIt it(t, tn);
+    size_t el;
+    while (const uint8_t* e = it.next(&el)) {
+        if (e[0] != kSmallTuple || e[1] != 2) return LASPJ_DEC_MALFORMED;
+        const uint8_t* k = e + 2;
+        size_t kl = term_len(k, el - 2);
+        const uint8_t* v = k + kl;
+        size_t vl = el - 2 - kl;
+        if (v[0] == kNil) return LASPJ_DEC_UNREPRESENTABLE;     // an element without tokens
+        if (v[0] != kList) return LASPJ_DEC_MALFORMED;
+        ListIt ti(v, vl);
+        size_t tl;
+        int st = on_elem(k, kl);
+        if (st) return st;
+        while (const uint8_t* te = ti.next(&tl)) {
+            if (te[0] != kSmallTuple || te[1] != 2) return LASPJ_DEC_MALFORMED;
+            const uint8_t* tk = te + 2;
+            size_t tkl = term_len(tk, tl - 2);
+            const uint8_t* f = tk + tkl;
+            const int flag = bool_atom(f);
+            if (flag < 0) return LASPJ_DEC_MALFORMED;
+            if ((st = on_tok(k, kl, tk, tkl, flag == 1))) return st;
+        }
+        if (ti.tail() && ti.tail()[0] != kNil) return LASPJ_DEC_MALFORMED;
+    }
+    if (it.tail() && it.tail()[0] != kNil) return LASPJ_DEC_MALFORMED;
+    return LASPJ_DEC_OK;
+}
+
+template <class OnElem>
+int walk_gset(const uint8_t* t, size_t tn, OnElem on_elem) {
+    if (t[0] == kNil) return LASPJ_DEC_OK;
+    if (t[0] != kList && t[0] != kString) return LASPJ_DEC_MALFORMED;
+    ListIt it(t, tn);
+    size_t el;
+    while (const uint8_t* e = it.next(&el)) {
+        // STRING_EXT elements are synthesised SMALL_INTEGER_EXT images (2 bytes)
+        if (int st = on_elem(e, el)) return st;
+    }
+    if (it.tail() && it.tail()[0] != kNil) return LASPJ_DEC_MALFORMED;
+    return LASPJ_DEC_OK;
+}
+
+int reg_elem(Dict* d, const uint8_t* k, size_t kl, uint32_t* slot) {
+    const int64_t f = d->elem(k, kl);
+    if (f >= 0) {
+        *slot = (uint32_t)f;
+        return LASPJ_DEC_OK;
+    }
+    bool ok = true;
+    term_cmp(k, kl, k, kl, &ok);              // the comparator must handle the term
+    if (!ok) return LASPJ_DEC_MALFORMED;
+    if (d->elems.size() >= (1u << 24)) return LASPJ_DEC_UNREPRESENTABLE;
+    *slot = (uint32_t)d->elems.size();
+    std::string_view v = d->keep(k, kl);
+    d->elem_slot.insert(hash_bytes(k, kl, kElemSeed), 0, v, *slot);
+    d->elems.push_back(v);
+    d->toks.emplace_back();
+    return LASPJ_DEC_OK;
+}
+
+int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
+    const int f = d->tok(es, t, tl);
+    if (f >= 0) {
+        *slot = (uint8_t)f;
+        return LASPJ_DEC_OK;
+    }
+    bool ok = true;
+    term_cmp(t, tl, t, tl, &ok);
+    if (!ok) return LASPJ_DEC_MALFORMED;
+    if (d->toks[es].size() >= 64) return LASPJ_DEC_UNREPRESENTABLE;
+    *slot = (uint8_t)d->toks[es].size();
+    std::string_view v = d->keep(t, tl);
+    d->tok_slot.insert(tok_hash(es, t, tl), es, v, *slot);
+    d->toks[es].push_back(v);
+    return LASPJ_DEC_OK;
+}
+
+int cmp_view(std::string_view a, std::string_view b) {
+    bool ok = true;
+    return term_cmp((const uint8_t*)a.data(), a.size(), (const uint8_t*)b.data(), b.size(), &ok);
+}
+
+}  // namespace
+
+struct laspj_dict {
+    Dict d;
+};
+
+extern "C" {
+
+int laspj_term_compare(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, int* out) {
+    if (!a || !b || !out || !na || !nb) return LASPJ_E_INVAL;
+    // maps, pids, ports, references, funs, exports and bit strings: valid terms, but not
+    // ones this path holds
+    auto other = [](uint8_t t) {
+        return t == 116 || t == 88 || t == 103 || t == 89 || t == 102 || t == 120 ||
+               t == 90 || t == 114 || t == 101 || t == 112 || t == 117 || t == 113 || t == 77;
+    };
+    if (other(a[0]) || other(b[0])) return LASPJ_E_UNSUPPORTED;
+    if (term_len(a, na) != na || term_len(b, nb) != nb) return LASPJ_E_INVAL;
+    bool ok = true;
+    int c = term_cmp(a, na, b, nb, &ok);
+    if (!ok) return LASPJ_E_UNSUPPORTED;
+    *out = c;
+    return LASPJ_OK;
+}
+
+int laspj_dict_create(laspj_dict** out) {
+    if (!out) return LASPJ_E_INVAL;
+    *out = new (std::nothrow) laspj_dict;
+    return *out ? LASPJ_OK : LASPJ_E_NOMEM;
+}
+
+int laspj_dict_destroy(laspj_dict* d) {
+    if (!d) return LASPJ_E_INVAL;
+    delete d;
+    return LASPJ_OK;
+}
+
+int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const uint64_t* offsets,
+                   uint64_t n, int tag, int32_t* status) {
+    if (!dict || (n && (!blob || !offsets || !status))) return LASPJ_E_INVAL;
+    if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET) return LASPJ_E_KIND;
+    Dict* d = &dict->d;
+    try {
+        for (uint64_t i = 0; i < n; ++i) {
+            if (offsets[i + 1] < offsets[i]) return LASPJ_E_INVAL;
+            const uint8_t* t;
+            size_t tn;
+            int st = payload_term(blob + offsets[i], offsets[i + 1] - offsets[i], tag, -1, &t, &tn);
+            if (st == LASPJ_DEC_OK) {
+                if (kind == LASPJ_KIND_ORSET) {
+                    uint32_t cur = 0;
+                    st = walk_orset(
+                        t, tn, [&](const uint8_t* k, size_t kl) { return reg_elem(d, k, kl, &cur); },
+                        [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl, bool) {
+                            uint8_t s;
+                            return reg_tok(d, cur, tk, tkl, &s);
+                        });
+                } else {
+                    st = walk_gset(t, tn, [&](const uint8_t* e, size_t el) {
+                        uint32_t s;
+                        return reg_elem(d, e, el, &s);
+                    });
+                }
+            }
+            status[i] = st;
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
+int laspj_dict_info(const laspj_dict* dict, uint32_t* elements, uint64_t* elem_bytes,
+                    uint64_t* tok_bytes) {
+    if (!dict) return LASPJ_E_INVAL;
+    const Dict& d = dict->d;
+    uint64_t eb = 0, tb = 0;
+    for (const auto& e : d.elems) eb += e.size();
+    for (const auto& v : d.toks)
+        for (const auto& t : v) tb += t.size();
+    if (elements) *elements = (uint32_t)d.elems.size();
+    if (elem_bytes) *elem_bytes = eb;
+    if (tok_bytes) *tok_bytes = tb;
+    return LASPJ_OK;
+}
+
+int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, uint32_t* elem_off,
+                      uint32_t* elem_order, uint8_t* tok_blob, uint32_t* tok_off,
+                      uint8_t* tok_order) {
+    if (!dict || !elem_off || !elem_order) return LASPJ_E_INVAL;
+    const Dict& d = dict->d;
+    const uint32_t K = (uint32_t)d.elems.size();
+    if (E < K) return LASPJ_E_RANGE;
+    try {
+        // element images and offsets (E + 1), slots in term order, unused slots last
+        uint64_t off = 0;
+        elem_off[0] = 0;
+        for (uint32_t e = 0; e < E; ++e) {
+            if (e < K) {
+                if (elem_blob) memcpy(elem_blob + off, d.elems[e].data(), d.elems[e].size());
+                off += d.elems[e].size();
+            }
+            if (off > 0xFFFFFFFFull) return LASPJ_E_RANGE;
+            elem_off[e + 1] = (uint32_t)off;
+        }
+        std::vector<uint32_t> ord(K);
+        for (uint32_t e = 0; e < K; ++e) ord[e] = e;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            return cmp_view(d.elems[x], d.elems[y]) < 0;
+        });
+        for (uint32_t e = 0; e < E; ++e) elem_order[e] = e < K ? ord[e] : e;
+        if (tok_off) {
+            uint64_t to = 0;
+            tok_off[0] = 0;
+            for (uint32_t e = 0; e < E; ++e) {
+                for (uint32_t k = 0; k < 64; ++k) {
+                    if (e < K && k < d.toks[e].size()) {
+                        if (tok_blob) memcpy(tok_blob + to, d.toks[e][k].data(), d.toks[e][k].size());
+                        to += d.toks[e][k].size();
+                    }
+                    if (to > 0xFFFFFFFFull) return LASPJ_E_RANGE;
+                    tok_off[64ull * e + k + 1] = (uint32_t)to;
+                }
+                if (tok_order) {
+                    uint8_t* o = tok_order + 64ull * e;
+                    memset(o, 0xFF, 64);
+                    if (e < K) {
+                        std::vector<uint8_t> ts(d.toks[e].size());
+                        for (size_t k = 0; k < ts.size(); ++k) ts[k] = (uint8_t)k;
+                        std::stable_sort(ts.begin(), ts.end(), [&](uint8_t x, uint8_t y) {
+                            return cmp_view(d.toks[e][x], d.toks[e][y]) < 0;
+                        });
+                        memcpy(o, ts.data(), ts.size());
+                    }
+                }
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
+int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
+                      const uint64_t* offsets, uint64_t n, int tag, uint32_t E, uint64_t* out,
+                      int32_t* status) {
+    if (!dict || (n && (!blob || !offsets || !status || !out))) return LASPJ_E_INVAL;
+    if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET) return LASPJ_E_KIND;
+    const Dict& d = dict->d;
+    const uint64_t wpr = kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
+    try {
+        for (uint64_t i = 0; i < n; ++i) {
+            uint64_t* cells = out + i * wpr;
+            memset(cells, 0, wpr * 8);
+            const uint8_t* t;
+            size_t tn;
+            int st = payload_term(blob + offsets[i], offsets[i + 1] - offsets[i], tag, -1, &t, &tn);
+            if (st == LASPJ_DEC_OK) {
+                // keys must ascend strictly (an orddict / ordset), tokens likewise
+                std::string_view prev_e, prev_t;
+                std::string prev_buf;
+                bool have_e = false, have_t = false;
+                uint32_t cur = 0;
+                auto on_elem = [&](const uint8_t* k, size_t kl) -> int {
+                    std::string_view key((const char*)k, kl);
+                    const int64_t f = d.elem(k, kl);
+                    if (f < 0 || f >= (int64_t)E) return LASPJ_DEC_UNKNOWN_TERM;
+                    if (have_e && cmp_view(prev_e, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
+                    // a STRING_EXT element's image lives in the iterator's scratch: copy it
+                    // (the buffer keeps its capacity, so this does not allocate per element)
+                    prev_buf.assign(key.data(), key.size());
+                    prev_e = prev_buf;
+                    have_e = true;
+                    have_t = false;
+                    cur = (uint32_t)f;
+                    if (kind == LASPJ_KIND_GSET) cells[cur >> 6] |= 1ull << (cur & 63);
+                    return LASPJ_DEC_OK;
+                };
+                if (kind == LASPJ_KIND_ORSET) {
+                    st = walk_orset(t, tn, on_elem,
+                                    [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl,
+                                        bool flag) -> int {
+                                        std::string_view key((const char*)tk, tkl);
+                                        const int f = d.tok(cur, tk, tkl);
+                                        if (f < 0) return LASPJ_DEC_UNKNOWN_TERM;
+                                        if (have_t && cmp_view(prev_t, key) >= 0)
+                                            return LASPJ_DEC_UNKNOWN_TERM;
+                                        prev_t = key;
+                                        have_t = true;
+                                        cells[2ull * cur] |= 1ull << f;
+                                        if (flag) cells[2ull * cur + 1] |= 1ull << f;
+                                        return LASPJ_DEC_OK;
+                                    });
+                } else {
+                    st = walk_gset(t, tn, on_elem);
+                }
+            }
+            if (st != LASPJ_DEC_OK) memset(cells, 0, wpr * 8);
+            status[i] = st;
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,165 @@
+"""The native host side of the boundary (laspj_term_compare, laspj_dict_*), on the CPU:
+the term-order comparator against the Python restatement of Erlang term order
+(lasp_amd.terms.term_cmp, which the oracle's KATs rely on), and the dictionary + encoder
+against the Python codec (codec.Domain) on random orddicts / ordsets written as
+term_to_binary/1 payloads (lasp_amd.etf)."""
+
+import ctypes as C
+import struct
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from lasp_amd import _lib, etf
+from lasp_amd.codec import Domain
+from lasp_amd.terms import Atom, term_cmp
+
+ATOMS = st.sampled_from([Atom(a) for a in ("a", "b", "abc", "zz", "é", "ünïcode", "true", "false")])
+NUM = st.one_of(st.integers(-(1 << 70), 1 << 70), st.integers(-300, 300),
+                st.floats(allow_nan=False, allow_infinity=False, width=64),
+                st.sampled_from([0, 1, 1.0, -1, 255, 256, 2 ** 31, 2 ** 63, 0.5, -0.0]))
+LEAF = st.one_of(NUM, ATOMS, st.binary(max_size=6), st.just([]),
+                 st.lists(st.integers(0, 255), max_size=4))
+TERM = st.recursive(LEAF, lambda ch: st.one_of(st.tuples(ch, ch), st.tuples(ch),
+                                               st.lists(ch, max_size=3)), max_leaves=6)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from lasp_amd import build
+    build.build()
+    return _lib.load()
+
+
+def compare(lib, a, b):
+    x, y = etf.encode(a), etf.encode(b)
+    out = C.c_int()
+    st_ = lib.laspj_term_compare(x, len(x), y, len(y), C.byref(out))
+    assert st_ == 0, (a, b)
+    return out.value
+
+
+@settings(max_examples=600, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(TERM, TERM)
+def test_term_compare_matches_erlang_order(lib, a, b):
+    assert compare(lib, a, b) == term_cmp(a, b), (a, b)
+    assert compare(lib, a, a) == 0
+
+
+def test_term_compare_edges(lib):
+    assert compare(lib, 1, 1.0) == 0                  # numbers compare by value
+    assert compare(lib, 2 ** 64 + 1, 1.8446744073709552e19) == 1
+    assert compare(lib, -(2 ** 70), -1e21) == -1
+    assert compare(lib, [1, 2], [1, 2, 0]) == -1      # STRING_EXT vs STRING_EXT prefix
+    assert compare(lib, [1, 2], [1, Atom("a")]) == -1  # STRING_EXT vs LIST_EXT
+    assert compare(lib, (1,), [1]) == -1               # tuple < list
+    assert compare(lib, [], [0]) == -1                 # nil < list
+    assert compare(lib, b"", []) == 1                  # bitstring > everything
+    out = C.c_int()
+    bad = bytes([116, 0, 0, 0, 0])                     # a map: outside this path
+    assert lib.laspj_term_compare(bad, 5, bad, 5, C.byref(out)) == _lib.E_UNSUPPORTED
+
+
+class NDict:
+    """the test's view: lasp_amd.hostdict.NativeDict with the library fixture"""
+
+    def __init__(self, lib):
+        from lasp_amd.hostdict import NativeDict
+        self.n = NativeDict()
+        self.h = self.n.h
+
+    def add(self, kind, payloads, tag=-1):
+        return self.n.add(kind, payloads, tag)
+
+    def export(self, E, tokens=True):
+        return self.n.export(E, tokens)
+
+    def encode(self, kind, payloads, E, tag=-1):
+        return self.n.encode(kind, payloads, E, tag)
+
+
+def orsets(draw_ops, seed):
+    from oracle import orset
+    toks = orset.TokenSource(seed)
+    s = orset.new()
+    for kind, e in draw_ops:
+        op = ("add_by_token", toks(), e) if kind == "add" else ("remove", e)
+        r = orset.update(op, None, s)
+        if r[0] == "ok":
+            s = r[1]
+    return s
+
+
+ELEMS = st.one_of(st.integers(-5, 300), ATOMS, st.tuples(st.integers(0, 3), ATOMS),
+                  st.binary(min_size=1, max_size=3))
+OPS = st.lists(st.tuples(st.sampled_from(["add", "add", "remove"]), ELEMS), max_size=20)
+
+
+@settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(OPS, min_size=1, max_size=4))
+def test_dict_export_and_encode_match_python_codec(lib, opss):
+    values = [orsets(ops, 10 + i) for i, ops in enumerate(opss)]
+    payloads = [bytes([76, 1]) + etf.term_to_binary(v) for v in values]
+    d = NDict(lib)
+    assert list(d.add(_lib.KIND_ORSET, payloads, tag=76)) == [0] * len(values)
+    dom = Domain()
+    for v in values:
+        dom.register_orset(v)
+    E = max(1, dom.size) + 3
+    eb, eo, eord, tb, to, tord = d.export(E)
+    peb, peo, peord, ptb, pto, ptord = dom.etf_arrays(E)
+    # slots are assigned in first-seen order by both: images and orders must agree
+    assert eb == peb and np.array_equal(eo, peo) and np.array_equal(eord, peord)
+    assert tb == ptb and np.array_equal(to, pto) and np.array_equal(tord, ptord)
+    cells, st_ = d.encode(_lib.KIND_ORSET, payloads, E, tag=76)
+    assert list(st_) == [0] * len(values)
+    want = dom.encode_orset(values, E).reshape(len(values), 2 * E)
+    assert np.array_equal(cells, want)
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.lists(st.lists(ELEMS, max_size=12), min_size=1, max_size=4))
+def test_gset_dict_and_encode(lib, sets):
+    from oracle import otp
+    values = [otp.lists_usort(s) for s in sets]
+    payloads = [etf.term_to_binary(v) for v in values]
+    d = NDict(lib)
+    assert list(d.add(_lib.KIND_GSET, payloads)) == [0] * len(values)
+    dom = Domain()
+    E = 1
+    gw = dom.encode_gset(values, 4096)
+    E = max(1, dom.size)
+    eb, eo, eord, *_ = d.export(E, tokens=False)
+    peb, peo, peord, *_ = dom.etf_arrays(E, tokens=False)
+    assert eb == peb and np.array_equal(eord, peord)
+    words, st_ = d.encode(_lib.KIND_GSET, payloads, E)
+    assert list(st_) == [0] * len(values)
+    W = (E + 63) // 64
+    assert np.array_equal(words, gw[:, :W])
+
+
+def test_dict_statuses(lib):
+    d = NDict(lib)
+    tok = b"t" * 20
+    good = etf.term_to_binary([(1, [(tok, False)]), (2, [(tok, True)])])
+    unsorted = etf.term_to_binary([(2, [(tok, False)]), (1, [(tok, False)])])
+    dup_tok = etf.term_to_binary([(1, [(tok, False), (tok, True)])])
+    no_toks = etf.term_to_binary([(1, [])])
+    bad_flag = etf.term_to_binary([(1, [(tok, Atom("maybe"))])])
+    truncated = good[:-3]
+    st_ = d.add(_lib.KIND_ORSET, [good, unsorted, dup_tok, no_toks, bad_flag, truncated,
+                                  bytes([76, 2]) + good[0:0] + good])
+    assert list(st_) == [_lib.DEC_OK, _lib.DEC_OK, _lib.DEC_OK, _lib.DEC_UNREPRESENTABLE,
+                         _lib.DEC_MALFORMED, _lib.DEC_MALFORMED, _lib.DEC_MALFORMED]
+    assert list(d.add(_lib.KIND_ORSET, [bytes([76, 2]) + good, bytes([9, 1]) + good],
+                      tag=76)) == [_lib.DEC_OK, _lib.DEC_INVALID_BINARY]
+    cells, st_ = d.encode(_lib.KIND_ORSET, [good, unsorted, dup_tok], 4)
+    # not an orddict (keys / tokens not strictly ascending): the list path takes it
+    assert list(st_) == [_lib.DEC_OK, _lib.DEC_UNKNOWN_TERM, _lib.DEC_UNKNOWN_TERM]
+    assert not cells[1].any() and not cells[2].any()
+    many = etf.term_to_binary([(7, [(bytes([k]) * 20, False) for k in range(65)])])
+    assert list(d.add(_lib.KIND_ORSET, [many])) == [_lib.DEC_UNREPRESENTABLE]
+    st2 = np.zeros((1,), np.int32)
+    assert lib.laspj_dict_add(d.h, _lib.KIND_GCOUNTER, good, np.array([0, len(good)],
+                              np.uint64).ctypes.data, 1, -1, st2.ctypes.data) == _lib.E_KIND

@@ -3,6 +3,8 @@
   * config 1 end to end: lasp_orset:merge/2 of two 10k-element orddicts through the
     mirror (lasp_amd.orset.merge: dictionary + encode, upload, k_or16, download, decode)
     next to the kernel on resident inputs;
+  * the same merge on the NIF's native path: payload bytes -> laspj_dict_encode ->
+    upload -> k_or16 -> device to_binary -> download;
   * the Store's bind path: 1000 OR-Set variables each bound to a new value, one bind/3
     at a time vs Store.bind_many (one laspj_batch_bind_many launch);
   * a list-value re-bind (an intersection output re-run after an input change)."""
@@ -10,6 +12,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -44,6 +48,40 @@ def main():
         C.join(A, B)
     ctx.synchronize()
     out["config1_kernel_merge_us"] = (time.perf_counter() - t0) / 200 * 1e6
+
+    # the NIF's native path for the same call: payloads (what term_to_binary/1 hands the
+    # NIF; made here untimed) -> native dictionary encode -> upload -> k_or16 -> device
+    # to_binary -> download of the merged payload
+    from lasp_amd import _lib, etf
+    from lasp_amd.engine import ETFDict
+    from lasp_amd.hostdict import NativeDict
+    pa, pb = etf.term_to_binary(a), etf.term_to_binary(b)
+    nd = NativeDict()
+    t0 = time.perf_counter()
+    nd.add(_lib.KIND_ORSET, [pa, pb])
+    out["config1_native_dict_register_us"] = (time.perf_counter() - t0) * 1e6
+    E = nd.info()[0]
+    d = ETFDict(ctx, E, *nd.export(E))
+    NA, NB, NC = ctx.orset_batch(1, E), ctx.orset_batch(1, E), ctx.orset_batch(1, E)
+    host = np.zeros((2, 2 * E), np.uint64)
+
+    def native_merge():
+        cells, stt = nd.encode(_lib.KIND_ORSET, [pa, pb], E, out=host)
+        assert not stt.any()
+        NA.upload(cells[0])
+        NB.upload(cells[1])
+        NC.join(NA, NB)
+        return NC.to_binaries(d)[0]
+    got = native_merge()
+    assert got == etf.term_to_binary(m), "native path disagrees with the mirror"
+    t0 = time.perf_counter()
+    for _ in range(it):
+        native_merge()
+    out["config1_native_e2e_merge_us"] = (time.perf_counter() - t0) / it * 1e6
+    t0 = time.perf_counter()
+    for _ in range(it):
+        nd.encode(_lib.KIND_ORSET, [pa, pb], E, out=host)
+    out["config1_native_encode_2x10k_us"] = (time.perf_counter() - t0) / it * 1e6
 
     n = 1000
     st = core.Store(capacity=256)
