@@ -131,7 +131,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         the replica length is a power of two and
                                         2 <= group <= 4, 1 = per-replica segments with a
                                         compile-time group, 2 = generic segments (also
-                                        the runtime-count loop of reduce_chunks)       */
+                                        the runtime-count loop of reduce_chunks);
+                                        reduce_chunks at 2..8 chunks: tiles read one
+                                        source at a time (stream unroll 2/4/8 cells per
+                                        lane, default 4) unless 2, or 3 = grid-stride
+                                        sweep with every chunk's load in flight       */
 #define LASPJ_TUNE_PRODUCT_ROWS  6   /* rows per outer-product tile: 0 = default (256),
                                         32, 64, 128, 256                                */
 #define LASPJ_TUNE_PRODUCT_COLS  7   /* columns per outer-product tile: 0 = default
@@ -139,8 +143,12 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_ETF_READ      8   /* OR-Set from_binary: 0 = batched records when the
                                         dictionary's record templates hash apart within
                                         every element, plus element batches when elements
-                                        hold <= 8 token slots, 1 = serial record scan,
-                                        2 = batched records without element batches      */
+                                        hold <= 8 token slots, and long payloads split
+                                        between waves when there are few of them,
+                                        1 = serial record scan, 2 = batched records
+                                        without element batches, 3 = never split,
+                                        4 = always split (256-byte segments),
+                                        5 = always split (sized segments)                */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -71,6 +71,10 @@ struct laspj_etf_dict {
     const uint8_t* rd_hdr = nullptr;       // E x 64 header template bytes
     const uint16_t* rd_tb = nullptr;       // E x tok_max token buckets (see ReadTabs)
     const uint8_t* rd_ros = nullptr;       // E x 64: token slot -> token rank (0xFF: none)
+    // header template hash -> rank + 1 (segment mode's first element; with rd_*)
+    const uint32_t* rd_htab = nullptr;
+    uint32_t rd_hmask = 0;
+    uint64_t rd_hlens = 0;                 // bit hl - 1: a header template of hl <= 64 bytes
 };
 
 namespace laspj {
@@ -1060,11 +1064,13 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_serial(const uint8_t*
                 break;
             }
             uint32_t n = 0;
+            bool list = false;             // LIST_EXT (also of 0 elements): its tail follows
             if (at(s, p + 1) == 106) {
                 p += 2;
             } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
                 n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
                 p += 6;
+                list = true;
             } else {
                 st = LASPJ_DEC_MALFORMED;
                 break;
@@ -1165,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_serial(const uint8_t*
                 if (lane == 0) c[e] = u64x2{pb, rb};
             }
             if (st != LASPJ_DEC_OK) break;
-            if (n) {
+            if (list) {
                 if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
                 p += 1;
             }
@@ -1356,7 +1362,7 @@ __device__ __forceinline__ uint32_t ufl32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane(v);
 }
 
-__device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t left,
+__device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t left, u64 stop,
                                const ReadTabs& t, const DictView& d, uint32_t E, uint32_t RL,
                                uint32_t RS, ReadLds& L, u64x2* c, uint32_t lane) {
     const uint32_t RK = d.tok_max;
@@ -1382,12 +1388,14 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
         mk[i] = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
     }
     const uint32_t lim = min(w.hi, w.end);
+    // elements starting at or after `stop` belong to the next segment
+    const uint32_t srel = stop <= w.lo ? 0u : (uint32_t)min(stop - w.lo, (u64)0xFFFFFFFFu);
     // the walk: element lanes (start, candidate lane), record lanes (start, element,
     // atom header length, atom length)
     uint32_t x = pc, ne = 0, nr = 0, ex = 0, ec = 0, ry = 0, rel = 0, rh = 0, rlen = 0;
     int32_t fmin = -1;
     u64 cm = 0;                          // candidate lanes the walk matched
-    while (ne < 64u && ne < left && x < lim) {
+    while (ne < 64u && ne < left && x < lim && x < srel) {
         const uint32_t* b32 = reinterpret_cast<const uint32_t*>(w.buf + (x & ~3u));
         const uint32_t sh = x & 3u;
         bool hit = cval && (int32_t)lane > fmin && x + chl <= lim;
@@ -1512,271 +1520,526 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
     return commit;
 }
 
+// the list header after the optional <<Tag, Vers>>: 131 106 (n = 0) or 131 108 <n:32>
+// (a LIST_EXT of n elements ends in its tail: `list` says the caller checks the 106)
+__device__ __forceinline__ int32_t parse_head(PWin& w, uint32_t& pc, int tag, int vers,
+                                              uint32_t& n, bool& list) {
+    n = 0;
+    list = false;
+    if (tag >= 0) {
+        if (pc + 2 > w.end) return LASPJ_DEC_INVALID_BINARY;
+        pc = need(w, pc, 2);
+        if (ub(w, pc) != (uint32_t)(tag & 0xFF)) return LASPJ_DEC_INVALID_BINARY;
+        if (ub(w, pc + 1) != (uint32_t)(vers & 0xFF)) return LASPJ_DEC_UNSUPPORTED_VERSION;
+        pc += 2;
+    }
+    if (pc + 2 > w.end) return LASPJ_DEC_MALFORMED;                // binary_to_term: badarg
+    pc = need(w, pc, 2);
+    if (ub(w, pc) != 131) return LASPJ_DEC_MALFORMED;
+    if (ub(w, pc + 1) == 106) {
+        pc += 2;
+        return LASPJ_DEC_OK;
+    }
+    if (ub(w, pc + 1) == 108 && pc + 6 <= w.end) {
+        pc = need(w, pc, 6);
+        n = (ub(w, pc + 2) << 24) | (ub(w, pc + 3) << 16) | (ub(w, pc + 4) << 8) | ub(w, pc + 5);
+        pc += 6;
+        list = true;
+        return LASPJ_DEC_OK;
+    }
+    return LASPJ_DEC_MALFORMED;
+}
+
+// per-lane constants of the batched record walk: lane (lj, lf), lj < 10, lf <= lj, is
+// case lj (lj + 1) / 2 + lf of a chain step
+struct Cases {
+    uint32_t lj, lf;
+    bool on;
+};
+
+__device__ __forceinline__ Cases lane_cases(uint32_t lane) {
+    uint32_t lj = 0;
+    while ((lj + 1) * (lj + 2) / 2 <= lane) ++lj;
+    return Cases{lj, lane - lj * (lj + 1) / 2, lane < 55};
+}
+
+// Decode elements at the cursor into cells c: at most n of them (count mode), or with
+// n = ~0u every element that starts before the absolute payload position `stop`, up to
+// the list's closing 106 (segment mode: *tail is set when the cursor stops on it).
+// prev is the previous element's term rank, nx the rank predicted next.  Returns the
+// elements decoded; st receives the first failure's LASPJ_DEC_* status.
+template <bool SMALL>
+__device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t& prev,
+                                                 RankPre& nx, uint32_t n, u64 stop, bool& tail,
+                                                 int32_t& st, const ReadTabs& tabs,
+                                                 const DictView& d, uint32_t E, ReadLds& L,
+                                                 u64x2* c, uint32_t lane, Cases cs) {
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    const uint32_t hmax = min(d.ehdr_max + 4u, kBWin - 16u);
+    const bool seg = n == 0xFFFFFFFFu;
+    const uint32_t lj = cs.lj, lf = cs.lf;
+    const bool lcase = cs.on;
+    uint32_t k = 0;
+    while (k < n && st == LASPJ_DEC_OK) {
+        if (seg) {
+            if (w.lo + pc >= stop) break;
+            if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
+            pc = need(w, pc, 1);
+            if (ub(w, pc) == 106) { tail = true; break; }
+        }
+        if (SMALL) {
+            const uint32_t got = read_batch(w, pc, prev, n - k, stop, tabs, d, E, RL, RS, L, c,
+                                            lane);
+            if (got) {
+                k += got;
+                if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
+                continue;
+            }
+        }
+        // 104 2 <elem image> 108 <count:32> of the next element in term order
+        const uint32_t span = min(hmax, w.end - pc);
+        pc = need(w, pc, span);
+        const uint32_t byte = pc + lane < min(w.hi, w.end) ? w.buf[pc + lane] : 0x100u;
+        int64_t found = -1;
+        RankPre cur = nx;
+        if (prev + 1 < (int64_t)E && cur.hl > 3u && cur.hl <= span && cur.hl <= 64u) {
+            const bool ok = lane >= cur.hl - 1u || byte == cur.hb;
+            if (!__ballot(!ok)) found = prev + 1;
+        }
+        if (found < 0) {
+            for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
+                const int64_t r = c0 + lane;
+                bool hit = false;
+                if (r < (int64_t)E) {
+                    const uint32_t ec = d.elem_order[r];
+                    const uint32_t hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                    // 104 2 <elem image> (the closing 108 is checked below)
+                    if (hlc > 3u && hlc <= span) {
+                        const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
+                        const uint8_t* q = w.buf + pc;
+                        if (hlc - 1u <= 48) {
+                            hit = eq48(q, t, hlc - 1u);
+                        } else {
+                            hit = true;
+                            for (uint32_t i = 0; i < hlc - 1u && hit; ++i) hit = q[i] == t[i];
+                        }
+                    }
+                }
+                const u64 m = __ballot(hit);
+                if (m) found = c0 + __ffsll((long long)m) - 1;
+            }
+            if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+            cur = load_rank(tabs, RK, found, E, lane);
+        }
+        prev = found;
+        nx = load_rank(tabs, RK, found + 1, E, lane);
+        const uint32_t e = cur.e, hl = cur.hl;
+        pc += hl;
+        const uint32_t close = hl <= 64u ? rdlane(byte, hl - 1u) : ub(w, pc - 1);
+        if (close != 108) {                        // [] tokens: no columnar form
+            st = close == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
+            break;
+        }
+        if (pc + 4 > w.end) { st = LASPJ_DEC_MALFORMED; break; }    // truncated count
+        uint32_t m_tok;
+        if (hl + 4u <= 64u) {
+            m_tok = (rdlane(byte, hl) << 24) | (rdlane(byte, hl + 1u) << 16) |
+                    (rdlane(byte, hl + 2u) << 8) | rdlane(byte, hl + 3u);
+        } else {
+            pc = need(w, pc, 4);
+            m_tok = (ub(w, pc) << 24) | (ub(w, pc + 1) << 16) | (ub(w, pc + 2) << 8) |
+                    ub(w, pc + 3);
+        }
+        pc += 4;
+        if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+        // the element's bucket table and an empty presence table
+        const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = cur.key >> 8;
+        wave_sync();
+        if (lane < cur.cnt) L.tab[cur.tb] = (uint8_t)lane;
+        L.pres[lane] = 0;
+        wave_sync();
+        int32_t tprev = -1;
+        for (uint32_t done = 0; done < m_tok;) {
+            // room for the batch in the window
+            {
+                const uint32_t want = min((m_tok - done) * (RL + 8u) + 8u, w.end - pc);
+                if (pc + want > w.hi && w.hi < w.end) pc = refill(w, pc);
+            }
+            // the chain, in window offsets: a record at x is complete before the
+            // payload end when x <= tlim, inside the window when x <= wlim
+            const int32_t tlim = (int32_t)w.end - (int32_t)RL - 6;
+            const int32_t wlim = w.hi >= w.end ? 0x7FFFFFFF : (int32_t)w.hi - (int32_t)RL - 8;
+            const int32_t lim = min(tlim, wlim);
+            const uint32_t t0 = pc + RL < w.hi ? ub(w, pc + RL) : 0u;
+            const uint32_t h = t0 == 119 ? 2u : 3u;     // the batch's atom header
+            const uint32_t L0 = RL + h + 4u;              // a `true` record
+            uint32_t nb = 0, x = pc, myx = 0;
+            bool trunc = false;
+            while (nb < 64 && done + nb < m_tok) {
+                const uint32_t J = min(10u, min(64u - nb, m_tok - done - nb));
+                // lane (lj, lf): the flag header of record lj after lf falses
+                uint32_t code = 0;
+                if (lcase && lj < J) {
+                    const uint32_t q = x + lj * L0 + lf + RL;
+                    if (q + 3 <= w.hi) {
+                        code = flag_code(word_at(w.buf, q), h);
+                        if (q + h + 4 + (code >> 1) > w.end) code = 0;
+                    }
+                }
+                uint32_t f = 0, jr = 0, idx = 0;
+                u64 fz = 0;
+                bool stop_walk = false;
+                for (; jr < J; ++jr) {
+                    const int32_t xj = (int32_t)(x + jr * L0 + f);
+                    if (xj > lim) { trunc = xj > tlim; stop_walk = true; break; }
+                    const uint32_t cj = rdlane(code, idx + f);
+                    if (!(cj & 1u)) break;
+                    fz |= (u64)(cj >> 1) << jr;
+                    f += cj >> 1;
+                    idx += jr + 1;
+                }
+                // lanes nb .. nb + jr - 1: starts of the walked records
+                if (lane >= nb && lane < nb + jr) {
+                    const uint32_t i = lane - nb;
+                    myx = x + i * L0 + __popcll(fz & ((1ull << i) - 1ull));
+                }
+                x += jr * L0 + f;
+                nb += jr;
+                if (stop_walk || nb >= 64 || done + nb >= m_tok) break;
+                if (jr == J) continue;
+                // a record the walk did not take: one general step
+                if (lane == nb) myx = x;
+                const uint32_t a0 = ub(w, x + RL), a1 = ub(w, x + RL + 1), a2 = ub(w, x + RL + 2);
+                uint32_t gh = 0, len = 0;
+                if ((a0 == 100 || a0 == 118) && a1 == 0) { gh = 3; len = a2; }
+                else if (a0 == 119) { gh = 2; len = a1; }
+                ++nb;
+                // a bad flag header ends the chain; lane nb - 1 reports it
+                if ((len != 4 && len != 5) || x + RL + gh + len > w.end) break;
+                x += RL + gh + len;
+            }
+            if (nb == 0 && !trunc) { st = LASPJ_DEC_MALFORMED; break; }   // no progress
+            // lane j < nb: record j
+            const bool mine = lane < nb;
+            int32_t lst = LASPJ_DEC_OK;
+            uint32_t rank = 0xFFu, fl = 0;
+            if (mine) {
+                rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
+                bool eq = rank < cur.cnt;
+                if (eq) {                           // exact compare
+                    uint32_t rw[12], t[12];
+                    rec_words(w.buf, myx, RL, rw);
+                    load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) eq &= t[i] == rw[i];
+                }
+                // ATOM_EXT / ATOM_UTF8_EXT (2-byte length), SMALL_ATOM_UTF8_EXT
+                // (1-byte length), then "true" / "false"
+                const uint32_t fo = myx + RL;
+                const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
+                const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
+                const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
+                const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
+                uint32_t gh = 0, len = 0, word = 0, c4 = 0;
+                if ((a0 == 100 || a0 == 118) && a1 == 0) {
+                    gh = 3;
+                    len = (v0 >> 16) & 0xFFu;
+                    word = __builtin_amdgcn_alignbyte(v1, v0, 3);
+                    c4 = v1 >> 24;
+                } else if (a0 == 119) {
+                    gh = 2;
+                    len = a1;
+                    word = __builtin_amdgcn_alignbyte(v1, v0, 2);
+                    c4 = (v1 >> 16) & 0xFFu;
+                }
+                const uint32_t fend = fo + gh + len;      // one past the flag
+                const bool tr = gh && len == 4 && fend <= w.end && word == 0x65757274u;
+                const bool fa = gh && len == 5 && fend <= w.end && word == 0x736C6166u && c4 == 'e';
+                fl = tr;
+                // term order: after the previous record's rank
+                const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+                const int32_t before = lane ? (int32_t)pr : tprev;
+                lst = !eq || (int32_t)rank <= before ? LASPJ_DEC_UNKNOWN_TERM
+                      : !(tr || fa)                  ? LASPJ_DEC_MALFORMED
+                                                     : LASPJ_DEC_OK;
+            }
+            const u64 bad = __ballot(lst != LASPJ_DEC_OK);
+            if (bad) {
+                st = (int32_t)rdlane((uint32_t)lst, (uint32_t)__ffsll((long long)bad) - 1u);
+                break;
+            }
+            if (trunc) { st = LASPJ_DEC_MALFORMED; break; }
+            if (mine) L.pres[rank] = (uint8_t)(1u | (fl << 1));
+            tprev = (int32_t)rdlane(rank, nb - 1u);
+            done += nb;
+            pc = x;
+        }
+        if (st != LASPJ_DEC_OK) break;
+        if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
+        pc = need(w, pc, 1);
+        if (ub(w, pc) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+        pc += 1;
+        // presence by rank -> slot bits: lane s reads its slot's rank
+        wave_sync();
+        const uint32_t v = cur.ros < 64u ? L.pres[cur.ros] : 0u;
+        const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
+        if (lane == 0) c[e] = u64x2{pb, rb};
+        ++k;
+    }
+    return k;
+}
+
+// One wave per replica.  With `redo` (segment mode's fallback) the wave takes the
+// replicas listed there (redo[0] of them) and clears their cells first.
 template <bool SMALL>
 __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
                                                            ReadTabs tabs, int tag, int vers,
-                                                           u64x2* cells, int32_t* status) {
+                                                           u64x2* cells, int32_t* status,
+                                                           const uint32_t* redo) {
     __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
     // the wave index as a scalar: everything per replica then stays wave-uniform
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    const uint32_t RK = d.tok_max;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    const uint32_t hmax = min(d.ehdr_max + 4u, kBWin - 16u);
-    // lane (lj, lf), lj < 10, lf <= lj: case index lj (lj + 1) / 2 + lf of a chain step
-    uint32_t lj = 0;
-    while ((lj + 1) * (lj + 2) / 2 <= lane) ++lj;
-    const uint32_t lf = lane - lj * (lj + 1) / 2;
-    const bool lcase = lane < 55;
+    const Cases cs = lane_cases(lane);
     ReadLds& L = lds[wave];
-    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
+    const uint64_t count = redo ? (uint64_t)ufl32(redo[0]) : R;
+    for (uint64_t i = (uint64_t)blockIdx.x * (kBlock / 64) + wave; i < count; i += nwaves) {
+        const uint64_t rep = redo ? (uint64_t)ufl32(redo[1 + i]) : i;
         const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
-        PWin w{L.win, payload, total, aend, base, 0,
-              (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
-        uint32_t pc = 0;
-        int32_t st = LASPJ_DEC_OK;
         u64x2* c = cells + rep * E;
-        do {
-            if (tag >= 0) {
-                if (pc + 2 > w.end) { st = LASPJ_DEC_INVALID_BINARY; break; }
-                pc = need(w, pc, 2);
-                if (ub(w, pc) != (uint32_t)(tag & 0xFF)) { st = LASPJ_DEC_INVALID_BINARY; break; }
-                if (ub(w, pc + 1) != (uint32_t)(vers & 0xFF)) {
-                    st = LASPJ_DEC_UNSUPPORTED_VERSION;
-                    break;
-                }
-                pc += 2;
-            }
-            if (pc + 2 > w.end) { st = LASPJ_DEC_MALFORMED; break; }   // binary_to_term: badarg
-            pc = need(w, pc, 2);
-            if (ub(w, pc) != 131) { st = LASPJ_DEC_MALFORMED; break; }
-            uint32_t n = 0;
-            if (ub(w, pc + 1) == 106) {
-                pc += 2;
-            } else if (ub(w, pc + 1) == 108 && pc + 6 <= w.end) {
-                pc = need(w, pc, 6);
-                n = (ub(w, pc + 2) << 24) | (ub(w, pc + 3) << 16) | (ub(w, pc + 4) << 8) |
-                    ub(w, pc + 5);
-                pc += 6;
-            } else {
-                st = LASPJ_DEC_MALFORMED;
-                break;
-            }
+        if (redo)
+            for (uint32_t e = lane; e < E; e += 64) c[e] = u64x2{0, 0};
+        PWin w{L.win, payload, total, aend, base, 0, (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
+        uint32_t pc = 0, n = 0;
+        bool list = false;
+        int32_t st = parse_head(w, pc, tag, vers, n, list);
+        if (st == LASPJ_DEC_OK) {
             int64_t prev = -1;                    // term rank of the previous element
             RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
-            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK;) {
-                if (SMALL) {
-                    const uint32_t got = read_batch(w, pc, prev, n - k, tabs, d, E, RL, RS, L, c,
-                                                    lane);
-                    if (got) {
-                        k += got;
-                        if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
-                        continue;
-                    }
-                }
-                // 104 2 <elem image> 108 <count:32> of the next element in term order
-                const uint32_t span = min(hmax, w.end - pc);
-                pc = need(w, pc, span);
-                const uint32_t byte = pc + lane < min(w.hi, w.end) ? w.buf[pc + lane] : 0x100u;
-                int64_t found = -1;
-                RankPre cur = nx;
-                if (prev + 1 < (int64_t)E && cur.hl > 3u && cur.hl <= span && cur.hl <= 64u) {
-                    const bool ok = lane >= cur.hl - 1u || byte == cur.hb;
-                    if (!__ballot(!ok)) found = prev + 1;
-                }
-                if (found < 0) {
-                    for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
-                        const int64_t r = c0 + lane;
-                        bool hit = false;
-                        if (r < (int64_t)E) {
-                            const uint32_t ec = d.elem_order[r];
-                            const uint32_t hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
-                            // 104 2 <elem image> (the closing 108 is checked below)
-                            if (hlc > 3u && hlc <= span) {
-                                const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
-                                const uint8_t* q = w.buf + pc;
-                                if (hlc - 1u <= 48) {
-                                    hit = eq48(q, t, hlc - 1u);
-                                } else {
-                                    hit = true;
-                                    for (uint32_t i = 0; i < hlc - 1u && hit; ++i) hit = q[i] == t[i];
-                                }
-                            }
-                        }
-                        const u64 m = __ballot(hit);
-                        if (m) found = c0 + __ffsll((long long)m) - 1;
-                    }
-                    if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
-                    cur = load_rank(tabs, RK, found, E, lane);
-                }
-                prev = found;
-                nx = load_rank(tabs, RK, found + 1, E, lane);
-                const uint32_t e = cur.e, hl = cur.hl;
-                pc += hl;
-                const uint32_t close = hl <= 64u ? rdlane(byte, hl - 1u) : ub(w, pc - 1);
-                if (close != 108) {                        // [] tokens: no columnar form
-                    st = close == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
-                    break;
-                }
-                if (pc + 4 > w.end) { st = LASPJ_DEC_MALFORMED; break; }    // truncated count
-                uint32_t m_tok;
-                if (hl + 4u <= 64u) {
-                    m_tok = (rdlane(byte, hl) << 24) | (rdlane(byte, hl + 1u) << 16) |
-                            (rdlane(byte, hl + 2u) << 8) | rdlane(byte, hl + 3u);
-                } else {
-                    pc = need(w, pc, 4);
-                    m_tok = (ub(w, pc) << 24) | (ub(w, pc + 1) << 16) | (ub(w, pc + 2) << 8) |
-                            ub(w, pc + 3);
-                }
-                pc += 4;
-                if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
-                // the element's bucket table and an empty presence table
-                const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = cur.key >> 8;
-                wave_sync();
-                if (lane < cur.cnt) L.tab[cur.tb] = (uint8_t)lane;
-                L.pres[lane] = 0;
-                wave_sync();
-                int32_t tprev = -1;
-                for (uint32_t done = 0; done < m_tok;) {
-                    // room for the batch in the window
-                    {
-                        const uint32_t want = min((m_tok - done) * (RL + 8u) + 8u, w.end - pc);
-                        if (pc + want > w.hi && w.hi < w.end) pc = refill(w, pc);
-                    }
-                    // the chain, in window offsets: a record at x is complete before the
-                    // payload end when x <= tlim, inside the window when x <= wlim
-                    const int32_t tlim = (int32_t)w.end - (int32_t)RL - 6;
-                    const int32_t wlim = w.hi >= w.end ? 0x7FFFFFFF : (int32_t)w.hi - (int32_t)RL - 8;
-                    const int32_t lim = min(tlim, wlim);
-                    const uint32_t t0 = pc + RL < w.hi ? ub(w, pc + RL) : 0u;
-                    const uint32_t h = t0 == 119 ? 2u : 3u;     // the batch's atom header
-                    const uint32_t L0 = RL + h + 4u;              // a `true` record
-                    uint32_t nb = 0, x = pc, myx = 0;
-                    bool trunc = false;
-                    while (nb < 64 && done + nb < m_tok) {
-                        const uint32_t J = min(10u, min(64u - nb, m_tok - done - nb));
-                        // lane (lj, lf): the flag header of record lj after lf falses
-                        uint32_t code = 0;
-                        if (lcase && lj < J) {
-                            const uint32_t q = x + lj * L0 + lf + RL;
-                            if (q + 3 <= w.hi) {
-                                code = flag_code(word_at(w.buf, q), h);
-                                if (q + h + 4 + (code >> 1) > w.end) code = 0;
-                            }
-                        }
-                        uint32_t f = 0, jr = 0, idx = 0;
-                        u64 fz = 0;
-                        bool stop = false;
-                        for (; jr < J; ++jr) {
-                            const int32_t xj = (int32_t)(x + jr * L0 + f);
-                            if (xj > lim) { trunc = xj > tlim; stop = true; break; }
-                            const uint32_t cj = rdlane(code, idx + f);
-                            if (!(cj & 1u)) break;
-                            fz |= (u64)(cj >> 1) << jr;
-                            f += cj >> 1;
-                            idx += jr + 1;
-                        }
-                        // lanes nb .. nb + jr - 1: starts of the walked records
-                        if (lane >= nb && lane < nb + jr) {
-                            const uint32_t i = lane - nb;
-                            myx = x + i * L0 + __popcll(fz & ((1ull << i) - 1ull));
-                        }
-                        x += jr * L0 + f;
-                        nb += jr;
-                        if (stop || nb >= 64 || done + nb >= m_tok) break;
-                        if (jr == J) continue;
-                        // a record the walk did not take: one general step
-                        if (lane == nb) myx = x;
-                        const uint32_t a0 = ub(w, x + RL), a1 = ub(w, x + RL + 1),
-                                       a2 = ub(w, x + RL + 2);
-                        uint32_t gh = 0, len = 0;
-                        if ((a0 == 100 || a0 == 118) && a1 == 0) { gh = 3; len = a2; }
-                        else if (a0 == 119) { gh = 2; len = a1; }
-                        ++nb;
-                        // a bad flag header ends the chain; lane nb - 1 reports it
-                        if ((len != 4 && len != 5) || x + RL + gh + len > w.end) break;
-                        x += RL + gh + len;
-                    }
-                    if (nb == 0 && !trunc) { st = LASPJ_DEC_MALFORMED; break; }   // no progress
-                    // lane j < nb: record j
-                    const bool mine = lane < nb;
-                    int32_t lst = LASPJ_DEC_OK;
-                    uint32_t rank = 0xFFu, fl = 0;
-                    if (mine) {
-                        rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
-                        bool eq = rank < cur.cnt;
-                        if (eq) {                           // exact compare
-                            uint32_t rw[12], t[12];
-                            rec_words(w.buf, myx, RL, rw);
-                            load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
-#pragma unroll
-                            for (int i = 0; i < 12; ++i) eq &= t[i] == rw[i];
-                        }
-                        // ATOM_EXT / ATOM_UTF8_EXT (2-byte length), SMALL_ATOM_UTF8_EXT
-                        // (1-byte length), then "true" / "false"
-                        const uint32_t fo = myx + RL;
-                        const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
-                        const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
-                        const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
-                        const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
-                        uint32_t gh = 0, len = 0, word = 0, c4 = 0;
-                        if ((a0 == 100 || a0 == 118) && a1 == 0) {
-                            gh = 3;
-                            len = (v0 >> 16) & 0xFFu;
-                            word = __builtin_amdgcn_alignbyte(v1, v0, 3);
-                            c4 = v1 >> 24;
-                        } else if (a0 == 119) {
-                            gh = 2;
-                            len = a1;
-                            word = __builtin_amdgcn_alignbyte(v1, v0, 2);
-                            c4 = (v1 >> 16) & 0xFFu;
-                        }
-                        const uint32_t fend = fo + gh + len;      // one past the flag
-                        const bool tr = gh && len == 4 && fend <= w.end && word == 0x65757274u;
-                        const bool fa = gh && len == 5 && fend <= w.end &&
-                                        word == 0x736C6166u && c4 == 'e';
-                        fl = tr;
-                        // term order: after the previous record's rank
-                        const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
-                        const int32_t before = lane ? (int32_t)pr : tprev;
-                        lst = !eq || (int32_t)rank <= before ? LASPJ_DEC_UNKNOWN_TERM
-                              : !(tr || fa)                  ? LASPJ_DEC_MALFORMED
-                                                             : LASPJ_DEC_OK;
-                    }
-                    const u64 bad = __ballot(lst != LASPJ_DEC_OK);
-                    if (bad) {
-                        st = (int32_t)rdlane((uint32_t)lst, (uint32_t)__ffsll((long long)bad) - 1u);
-                        break;
-                    }
-                    if (trunc) { st = LASPJ_DEC_MALFORMED; break; }
-                    if (mine) L.pres[rank] = (uint8_t)(1u | (fl << 1));
-                    tprev = (int32_t)rdlane(rank, nb - 1u);
-                    done += nb;
-                    pc = x;
-                }
-                if (st != LASPJ_DEC_OK) break;
-                if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
+            bool tail = false;
+            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, E, L, c, lane, cs);
+        }
+        if (st == LASPJ_DEC_OK && list) {
+            if (pc + 1 > w.end) st = LASPJ_DEC_MALFORMED;
+            else {
                 pc = need(w, pc, 1);
-                if (ub(w, pc) != 106) { st = LASPJ_DEC_MALFORMED; break; }
-                pc += 1;
-                // presence by rank -> slot bits: lane s reads its slot's rank
-                wave_sync();
-                const uint32_t v = cur.ros < 64u ? L.pres[cur.ros] : 0u;
-                const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
-                if (lane == 0) c[e] = u64x2{pb, rb};
-                ++k;
-            }
-            if (st != LASPJ_DEC_OK) break;
-            if (n) {
-                if (pc + 1 > w.end) { st = LASPJ_DEC_MALFORMED; break; }
-                pc = need(w, pc, 1);
-                if (ub(w, pc) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                if (ub(w, pc) != 106) st = LASPJ_DEC_MALFORMED;
                 pc += 1;
             }
-            if (w.lo + pc != aend) st = LASPJ_DEC_MALFORMED;      // trailing bytes
-        } while (false);
+        }
+        if (st == LASPJ_DEC_OK && w.lo + pc != aend) st = LASPJ_DEC_MALFORMED;   // trailing bytes
         if (lane == 0) status[rep] = st;
+    }
+}
+
+// ---- long payloads split between waves (segment mode)
+//
+// A payload of len bytes is cut into segments of S bytes; segment s of a replica is
+// decoded by its own wave.  Segment 0 parses the list header; segment s > 0 first
+// looks for an element header 106 104 2 <elem image> 108 at or after s S (the byte
+// before an element is the previous element's closing 106) whose image is in the
+// dictionary (hash of the header bytes -> rank, then an exact compare), then decodes
+// every element that starts inside the segment.  A token image may contain such a
+// byte run, so nothing is trusted yet: k_etf_read_chain checks per replica that each
+// segment starts exactly where the previous one ended, ranks ascend across segments,
+// the element count matches the header and the list closes at the payload end.  A
+// replica that fails any of this (or any segment status) is decoded again from the
+// start by k_orset_etf_read over the redo list, which gives the reference's status.
+struct SegRes {
+    int32_t st;
+    uint32_t start, end, cnt;    // first element / cursor at the end (relative), elements
+    int32_t rfirst, rlast;       // rank of the first / last element decoded
+    uint32_t n, flags;           // segment 0: the header's count; kSeg* bits
+};
+constexpr uint32_t kSegNone = 0xFFFFFFFFu;
+constexpr uint32_t kSegEmptyList = 1u;
+
+struct HdrHash {
+    const uint32_t* tab;   // open addressing: rank + 1, 0 empty
+    uint32_t mask;
+    u64 lens;              // bit hl - 1: some header template is hl bytes (hl <= 64)
+};
+
+// the header-template hash (host and device agree): 16 words, bytes >= hl zero
+__host__ __device__ inline uint32_t hdr_mix(uint32_t h, uint32_t v) {
+    h ^= v;
+    h *= 0x9E3779B1u;
+    return h ^ (h >> 16);
+}
+
+// the rank of the element whose header template is at window offset x, or -1
+__device__ int64_t resolve_hdr(const PWin& w, uint32_t x, const HdrHash& hh,
+                               const ReadTabs& t, uint32_t E, uint32_t lane) {
+    const uint32_t hl = lane + 1u;
+    const uint32_t lim = min(w.hi, w.end);
+    const bool on = ((hh.lens >> lane) & 1ull) && x + hl <= lim;
+    uint32_t h = hl * 0x85EBCA6Bu;
+    uint32_t q[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int rem = (int)hl - 4 * i;
+        const uint32_t v = word_at(w.buf, min(x + 4u * i, kBWin + 56u));
+        q[i] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+        h = hdr_mix(h, q[i]);
+    }
+    int64_t rank = -1;
+    if (on) {
+        for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
+            const uint32_t v = hh.tab[i];
+            if (!v || v > E) break;
+            const uint32_t rk = v - 1u;
+            if (t.desc[rk].y != hl) continue;
+            const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * rk);
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 a = tp[j];
+                eq &= a.x == q[4 * j] && a.y == q[4 * j + 1] && a.z == q[4 * j + 2] &&
+                      a.w == q[4 * j + 3];
+            }
+            if (eq) { rank = rk; break; }
+        }
+    }
+    const u64 m = __ballot(rank >= 0);
+    // images are self-delimiting and distinct: at most one header length matches
+    return m ? (int64_t)rdlane((uint32_t)rank, (uint32_t)__ffsll((long long)m) - 1u) : -1;
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
+    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
+    ReadTabs tabs, int tag, int vers, u64x2* cells, const uint32_t* segbase, uint64_t nseg,
+    uint32_t S, HdrHash hh, SegRes* res) {
+    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t RK = d.tok_max;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const Cases cs = lane_cases(lane);
+    ReadLds& L = lds[wave];
+    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
+        // the replica: the last r with segbase[r] <= g
+        uint64_t lo = 0, hi = R;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (ufl32(segbase[mid]) <= g) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t rep = lo;
+        const uint32_t s = (uint32_t)(g - ufl32(segbase[rep]));
+        const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
+        const uint32_t len = (uint32_t)min(aend - base, (u64)0x7FFFFFFF);
+        u64x2* c = cells + rep * E;
+        PWin w{L.win, payload, total, aend, base, 0, len};
+        SegRes out{LASPJ_DEC_OK, kSegNone, kSegNone, 0, -1, -1, 0, 0};
+        const uint32_t send = (uint32_t)min((u64)(s + 1) * S, (u64)len);
+        const u64 stop = base + (u64)(s + 1) * S;
+        uint32_t pc = 0;
+        int64_t prev = -1;
+        RankPre nx;
+        bool go = true;
+        if (s == 0) {
+            uint32_t n = 0;
+            bool list = false;
+            out.st = parse_head(w, pc, tag, vers, n, list);
+            out.n = n;
+            if (out.st != LASPJ_DEC_OK || !list) {
+                if (out.st == LASPJ_DEC_OK) out.flags = kSegEmptyList;     // 131 106
+                out.end = (uint32_t)(w.lo + pc - base);
+                go = false;
+            } else {
+                out.start = (uint32_t)(w.lo + pc - base);
+                nx = load_rank(tabs, RK, 0, E, lane);
+            }
+        } else {
+            // the first element header at or after s S: 106 104 2 <elem image> 108
+            pc = s * S - 1u;
+            int64_t found = -1;
+            while (w.lo + pc + 1u < base + send) {
+                pc = need(w, pc, min(w.end - pc, 136u));
+                const uint32_t lim = min(w.hi, w.end);
+                const uint32_t x = pc + 1u + lane;
+                const bool hit = w.lo + x < base + send && x + 1u < lim &&
+                                 w.buf[min(x - 1u, kBWin + 63u)] == 106 &&
+                                 w.buf[min(x, kBWin + 63u)] == 104 &&
+                                 w.buf[min(x + 1u, kBWin + 63u)] == 2;
+                u64 m = __ballot(hit);
+                while (m && found < 0) {
+                    const uint32_t f = (uint32_t)__ffsll((long long)m) - 1u;
+                    m &= m - 1ull;
+                    found = resolve_hdr(w, pc + 1u + f, hh, tabs, E, lane);
+                    if (found >= 0) pc = pc + 1u + f;
+                }
+                if (found >= 0) break;
+                pc += 64u;
+            }
+            if (found < 0) {
+                go = false;                       // no element starts in this segment
+            } else {
+                out.start = (uint32_t)(w.lo + pc - base);
+                out.rfirst = (int32_t)found;
+                prev = found - 1;
+                nx = load_rank(tabs, RK, found, E, lane);
+            }
+        }
+        if (go) {
+            bool tail = false;
+            int32_t st = LASPJ_DEC_OK;
+            out.cnt = decode_elems<SMALL>(w, pc, prev, nx, 0xFFFFFFFFu, stop, tail, st, tabs, d, E,
+                                          L, c, lane, cs);
+            out.st = st;
+            out.end = (uint32_t)(w.lo + pc - base);
+            out.rlast = (int32_t)prev;
+        }
+        if (lane == 0) res[g] = out;
+    }
+}
+
+// per replica: is the segment chain one well-formed orddict?  Yes: status OK.  No:
+// onto the redo list (decoded again serially, which gives the reference's status).
+__global__ void k_etf_read_chain(const uint8_t* payload, const u64* offs, uint64_t R,
+                                 const uint32_t* segbase, uint32_t S, const SegRes* res,
+                                 int32_t* status, uint32_t* redo) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const u64 base = offs[r];
+    const u64 len = offs[r + 1] - base;
+    const uint32_t g0 = segbase[r], ns = segbase[r + 1] - g0;
+    const SegRes a = res[g0];
+    bool ok = a.st == LASPJ_DEC_OK;
+    if (ok && (a.flags & kSegEmptyList)) {
+        ok = a.end == len;
+    } else if (ok) {
+        u64 q = a.end;
+        uint32_t cnt = a.cnt;
+        int64_t rl = a.rlast;
+        for (uint32_t s = 1; s < ns && ok; ++s) {
+            const SegRes b = res[g0 + s];
+            const u64 send = (u64)(s + 1) * S;
+            if (b.start == kSegNone) {
+                // no header found: fine only if none starts here (q past the segment, or
+                // q on the list's closing 106)
+                if (q < send && q < len && payload[base + q] != 106) ok = false;
+                continue;
+            }
+            if (b.start != q || b.st != LASPJ_DEC_OK || b.rfirst <= rl) {
+                ok = false;
+                break;
+            }
+            q = b.end;
+            cnt += b.cnt;
+            rl = b.rlast;
+        }
+        ok = ok && cnt == a.n && q + 1 == len && payload[base + q] == 106;
+    }
+    if (ok) {
+        status[r] = LASPJ_DEC_OK;
+    } else {
+        status[r] = LASPJ_DEC_MALFORMED;       // rewritten by the redo pass
+        const uint32_t i = atomicAdd(redo, 1u);
+        redo[1 + i] = (uint32_t)r;
     }
 }
 
@@ -1945,20 +2208,85 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     if (off[R] > payload->bytes)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
+    const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
+    auto kread = d->tok_max <= kSmallTok && ctx->tune_etf_read == 0 ? k_orset_etf_read<true>
+                                                                    : k_orset_etf_read<false>;
+    const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+    // Segment mode when there are too few payloads to fill the chip with one wave each
+    // (fewer than 8 per CU) and they are long: segments of S bytes, S sized for ~48 waves
+    // per CU (6 resident per SIMD, the rest queued behind them for balance), at least
+    // 2 KiB.  Knob 4 splits every payload longer than 256 bytes into 256-byte segments
+    // (what the tests use to stress the chain), 5 always splits with the sized S.
+    const uint64_t bytes_in = off[R] - off[0];
+    uint64_t S = 0, nseg = 0;
+    if (batched && d->rd_htab && ctx->tune_etf_read != 3) {
+        const uint64_t want = (uint64_t)ctx->cus * 48;
+        uint64_t longest = 0;
+        for (uint64_t i = 0; i < R; ++i) longest = std::max<uint64_t>(longest, off[i + 1] - off[i]);
+        S = std::max<uint64_t>(2048, ((bytes_in / want) + 255) & ~255ull);
+        if (ctx->tune_etf_read == 4) S = 256;
+        const bool split = ctx->tune_etf_read >= 4 || R < (uint64_t)ctx->cus * 8;
+        if (longest < (1ull << 31) && split && longest > S) {
+            for (uint64_t i = 0; i < R; ++i)
+                nseg += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);
+            if (nseg >= (1ull << 32)) nseg = 0;
+        }
+    }
+    if (nseg) {
+        std::vector<uint32_t> segbase(R + 1);
+        uint64_t acc = 0;
+        for (uint64_t i = 0; i < R; ++i) {
+            segbase[i] = (uint32_t)acc;
+            acc += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);
+        }
+        segbase[R] = (uint32_t)acc;
+        auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
+        const uint64_t o_res = al(4ull * (R + 1)), o_redo = o_res + al(sizeof(SegRes) * nseg);
+        if (int s2 = reserve_scratch(ctx, o_redo + 4ull * (R + 1))) return s2;
+        char* sc = static_cast<char*>(ctx->scratch);
+        uint32_t* dsegbase = reinterpret_cast<uint32_t*>(sc);
+        SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
+        uint32_t* redo = reinterpret_cast<uint32_t*>(sc + o_redo);
+        LJ_HIP(ctx, hipMemcpyAsync(dsegbase, segbase.data(), 4ull * (R + 1), hipMemcpyHostToDevice,
+                                   ctx->stream));
+        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
+        const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
+        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
+                               ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
+                           dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
+                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
+                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tabs,
+                           tag, vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
+                           (uint32_t)S, hh, dres);
+        LJ_LAUNCHED(ctx);
+        hipLaunchKernelGGL(k_etf_read_chain, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,
+                           ctx->stream, static_cast<const uint8_t*>(payload->dev),
+                           static_cast<const u64*>(offsets->dev), R, dsegbase, (uint32_t)S, dres,
+                           static_cast<int32_t*>(status->dev), redo);
+        LJ_LAUNCHED(ctx);
+        // the redo pass: usually an empty list (the kernel exits at once)
+        const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
+        hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
+                           ctx->stream, static_cast<const uint8_t*>(payload->dev),
+                           (u64)payload->bytes, static_cast<const u64*>(offsets->dev), R,
+                           b->elements, view(d), tabs, tag, vers,
+                           reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev),
+                           (const uint32_t*)redo);
+        LJ_LAUNCHED(ctx);
+        return LASPJ_OK;
+    }
     // one replica per wave up to 64 blocks per CU: short blocks keep every CU busy to the
     // end (a grid-stride over a few resident waves left a 20 % tail at 65536 replicas)
     uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
     const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    if (d->rd_desc && ctx->tune_etf_read != 1)
+    if (batched)
         // 0: element batches when elements hold <= 8 token slots; 2: records batched only
-        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read == 0
-                               ? k_orset_etf_read<true> : k_orset_etf_read<false>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+        hipLaunchKernelGGL(kread, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
-                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d),
-                           ReadTabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb,
-                                    d->rd_ros},
-                           tag, vers,
-                           reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev));
+                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tabs,
+                           tag, vers, reinterpret_cast<u64x2*>(b->dev),
+                           static_cast<int32_t*>(status->dev), (const uint32_t*)nullptr);
     else
         hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
@@ -2138,6 +2466,30 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         }
         if (!hashed) rd.clear();
     }
+    // segment mode: header template (<= 64 bytes) -> rank, hashed as the device hashes
+    std::vector<uint32_t> htab;
+    uint64_t hlens = 0;
+    if (hashed) {
+        uint64_t cap = 64;
+        while (cap < 2ull * E) cap <<= 1;
+        htab.assign(cap, 0);
+        const uint8_t* hdr = rd.data() + 16ull * E;
+        const uint32_t* desc = reinterpret_cast<const uint32_t*>(rd.data());
+        for (uint64_t r = 0; r < E; ++r) {
+            const uint32_t hl = desc[4 * r + 1];
+            if (hl < 4 || hl > 64) continue;
+            uint32_t h = hl * 0x85EBCA6Bu;
+            for (int i = 0; i < 16; ++i) {
+                uint32_t v;
+                std::memcpy(&v, hdr + 64 * r + 4 * i, 4);   // zero past hl
+                h = laspj::hdr_mix(h, v);
+            }
+            uint64_t i = h & (cap - 1);
+            while (htab[i]) i = (i + 1) & (cap - 1);
+            htab[i] = (uint32_t)r + 1u;
+            hlens |= 1ull << (hl - 1);
+        }
+    }
     for (uint64_t t = 0; t < tpoff.size(); ++t)
         std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
@@ -2150,7 +2502,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
                    o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
-                   bytes = o_rd + al(rd.size() + 8);
+                   o_htab = o_rd + al(rd.size() + 8), bytes = o_htab + al(4ull * htab.size() + 4);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -2182,6 +2534,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess && rec_len) e = up(o_hpad, hpad.data(), hpad.size());
     if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
     if (e == hipSuccess && hashed) e = up(o_rd, rd.data(), rd.size());
+    if (e == hipSuccess && hashed) e = up(o_htab, htab.data(), 4ull * htab.size());
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -2204,6 +2557,9 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         d->rd_hdr = t + 16ull * E;
         d->rd_tb = reinterpret_cast<const uint16_t*>(t + 16ull * E + 64ull * E);
         d->rd_ros = reinterpret_cast<const uint8_t*>(d->rd_tb + (uint64_t)E * tok_max);
+        d->rd_htab = reinterpret_cast<const uint32_t*>(base + o_htab);
+        d->rd_hmask = (uint32_t)(htab.size() - 1);
+        d->rd_hlens = hlens;
     }
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);

@@ -14,6 +14,8 @@
 // Layout (include/laspj.h): OR-Set cell (i, e) = words [2(iE+e), 2(iE+e)+1] = {p, r};
 // G-Set replica i = words [iW, (i+1)W), W = ceil(E/64).
 
+#include <algorithm>
+
 #include "laspj_internal.h"
 
 namespace laspj {
@@ -339,6 +341,73 @@ __global__ __launch_bounds__(kBlock) void k_reduce_chunks_n(u64x2* dst, const u6
     }
 }
 
+// Tiled, one source at a time: a block owns T x 256 consecutive cells and reads them
+// from source 0, then 1, ... (T loads in flight per lane per source), one tile per
+// block and no grid stride, so the blocks in flight cover one contiguous run of every
+// source.  At N = 8 (98304 x 4096 cells, 51.5 GB read + 6.4 GB written) this runs
+// 10.2 ms against 11.4 ms for the grid-stride sweep with all 8 loads of a cell in
+// flight (profiles/r02_sweep_reduce_tiles.log); the two-stream join gains nothing from
+// the same shape (r02_sweep_join_tiles.log), so it keeps its sweep.
+template <bool MAX, int NC, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_chunks_tile(u64x2* dst, const u64x2* src,
+                                                               uint64_t n) {
+    const uint64_t tile = (uint64_t)T * kBlock;
+    const uint64_t tiles = n / tile;
+    for (uint64_t b = blockIdx.x; b < tiles; b += gridDim.x) {
+        const uint64_t i0 = b * tile + threadIdx.x;
+        u64x2 acc[T];
+#pragma unroll
+        for (int u = 0; u < T; ++u) acc[u] = ld2<true>(src + i0 + u * kBlock);
+#pragma unroll
+        for (int j = 1; j < NC; ++j) {
+            u64x2 v[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) v[u] = ld2<true>(src + (uint64_t)j * n + i0 + u * kBlock);
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                acc[u].x = join_word<MAX>(acc[u].x, v[u].x);
+                acc[u].y = join_word<MAX>(acc[u].y, v[u].y);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < T; ++u) st2<true>(dst + i0 + u * kBlock, acc[u]);
+    }
+    // the cells past the last whole tile
+    for (uint64_t i = tiles * tile + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        u64x2 a = ld2<true>(src + i);
+        for (int j = 1; j < NC; ++j) {
+            const u64x2 v = ld2<true>(src + (uint64_t)j * n + i);
+            a.x = join_word<MAX>(a.x, v.x);
+            a.y = join_word<MAX>(a.y, v.y);
+        }
+        st2<true>(dst + i, a);
+    }
+}
+
+template <bool MAX>
+static void launch_reduce_tiles(laspj_ctx* ctx, u64x2* d, const u64x2* s, uint64_t n,
+                                uint32_t nchunks) {
+    // T cells per lane: the unroll knob when 2, 4 or 8, else 4
+    const int T = ctx->tune_unroll == 8 ? 8 : ctx->tune_unroll == 2 ? 2 : 4;
+    const uint64_t tiles = n / ((uint64_t)T * kBlock);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1u << 30));
+#define LJ_RT(NC, TT)                                                                        \
+    hipLaunchKernelGGL((k_reduce_chunks_tile<MAX, NC, TT>), dim3(grid), dim3(kBlock), 0,     \
+                       ctx->stream, d, s, n)
+#define LJ_RTN(NC)                                                                           \
+    case NC:                                                                                 \
+        if (T == 8) LJ_RT(NC, 8);                                                            \
+        else if (T == 2) LJ_RT(NC, 2);                                                       \
+        else LJ_RT(NC, 4);                                                                   \
+        break
+    switch (nchunks) {
+        LJ_RTN(2); LJ_RTN(3); LJ_RTN(4); LJ_RTN(5); LJ_RTN(6); LJ_RTN(7); LJ_RTN(8);
+    }
+#undef LJ_RTN
+#undef LJ_RT
+}
+
 // the same reduce over NC arbitrary source arrays (the anti-entropy round reads the
 // rank's own copy in place in its state and the peers' copies from the receive buffer,
 // and writes the join back into the state: no staging copies)
@@ -346,36 +415,42 @@ struct Srcs {
     const u64x2* p[8];
 };
 
+// tiles of 4 cells per lane, one per block, sources read one at a time (as
+// k_reduce_chunks_tile)
 template <bool MAX, int NC>
 __global__ __launch_bounds__(kBlock) void k_reduce_ptrs(u64x2* dst, Srcs s, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + stride < n; i += 2 * stride) {
-        u64x2 v[2][NC];
+    constexpr int T = 4;
+    const uint64_t tile = (uint64_t)T * kBlock;
+    const uint64_t tiles = n / tile;
+    for (uint64_t b = blockIdx.x; b < tiles; b += gridDim.x) {
+        const uint64_t i0 = b * tile + threadIdx.x;
+        u64x2 acc[T];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int j = 0; j < NC; ++j) v[u][j] = ld2<true>(s.p[j] + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-#pragma unroll
-            for (int j = 1; j < NC; ++j) {
-                v[u][0].x = join_word<MAX>(v[u][0].x, v[u][j].x);
-                v[u][0].y = join_word<MAX>(v[u][0].y, v[u][j].y);
-            }
-            st2<true>(dst + i + u * stride, v[u][0]);
-        }
-    }
-    for (; i < n; i += stride) {
-        u64x2 v[NC];
-#pragma unroll
-        for (int j = 0; j < NC; ++j) v[j] = ld2<true>(s.p[j] + i);
+        for (int u = 0; u < T; ++u) acc[u] = ld2<true>(s.p[0] + i0 + u * kBlock);
 #pragma unroll
         for (int j = 1; j < NC; ++j) {
-            v[0].x = join_word<MAX>(v[0].x, v[j].x);
-            v[0].y = join_word<MAX>(v[0].y, v[j].y);
+            u64x2 v[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) v[u] = ld2<true>(s.p[j] + i0 + u * kBlock);
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                acc[u].x = join_word<MAX>(acc[u].x, v[u].x);
+                acc[u].y = join_word<MAX>(acc[u].y, v[u].y);
+            }
         }
-        st2<true>(dst + i, v[0]);
+#pragma unroll
+        for (int u = 0; u < T; ++u) st2<true>(dst + i0 + u * kBlock, acc[u]);
+    }
+    for (uint64_t i = tiles * tile + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        u64x2 a = ld2<true>(s.p[0] + i);
+#pragma unroll
+        for (int j = 1; j < NC; ++j) {
+            const u64x2 v = ld2<true>(s.p[j] + i);
+            a.x = join_word<MAX>(a.x, v.x);
+            a.y = join_word<MAX>(a.y, v.y);
+        }
+        st2<true>(dst + i, a);
     }
 }
 
@@ -386,15 +461,15 @@ hipError_t launch_reduce_ptrs(laspj_ctx* ctx, uint64_t* dst, const uint64_t* con
     for (uint32_t j = 0; j < 8; ++j)
         s.p[j] = reinterpret_cast<const u64x2*>(srcs[j < nsrc ? j : 0]);
     const uint64_t n = words / 2;
-    StreamTune t = stream_tune(ctx, n);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n / (4 * kBlock), 1u << 30));
     auto* d = reinterpret_cast<u64x2*>(dst);
 #define LJ_RP(NC)                                                                              \
     case NC:                                                                                   \
         if (max_join)                                                                          \
-            hipLaunchKernelGGL((k_reduce_ptrs<true, NC>), dim3(t.grid), dim3(kBlock), 0,      \
+            hipLaunchKernelGGL((k_reduce_ptrs<true, NC>), dim3(grid), dim3(kBlock), 0,        \
                                ctx->stream, d, s, n);                                          \
         else                                                                                   \
-            hipLaunchKernelGGL((k_reduce_ptrs<false, NC>), dim3(t.grid), dim3(kBlock), 0,     \
+            hipLaunchKernelGGL((k_reduce_ptrs<false, NC>), dim3(grid), dim3(kBlock), 0,       \
                                ctx->stream, d, s, n);                                          \
         break
     switch (nsrc) {
@@ -441,6 +516,11 @@ static void launch_reduce_chunks_t(laspj_ctx* ctx, uint64_t* dst, const uint64_t
             hipLaunchKernelGGL((k_reduce_chunks_n<MAX, NC, 1, false>), dim3(t.grid),       \
                                dim3(kBlock), 0, ctx->stream, d2, s2, n);                    \
         break
+        if (ctx->tune_reduce != 2 && ctx->tune_reduce != 3 && nchunks >= 2 && nchunks <= 8) {
+            launch_reduce_tiles<MAX>(ctx, d2, s2, n, nchunks);
+            return;
+        }
+        // knob 3: the grid-stride sweep with NC compile-time loads per cell
         switch (ctx->tune_reduce == 2 ? 0u : nchunks) {
             LJ_RCN(2); LJ_RCN(3); LJ_RCN(4); LJ_RCN(5); LJ_RCN(6); LJ_RCN(7); LJ_RCN(8);
             default:

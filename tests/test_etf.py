@@ -390,7 +390,9 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 @contextlib.contextmanager
 def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
-    <= 8 token slots), 1 = serial scan, 2 = batched records only."""
+    <= 8 token slots), 1 = serial scan, 2 = batched records only, 4 = every payload
+    longer than 256 bytes split between waves (segment mode: header search, chain
+    check, redo of failed replicas)."""
     from lasp_amd import _lib
     ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
     try:
@@ -425,7 +427,7 @@ def _upload_payloads(ctx, blobs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1])
+@pytest.mark.parametrize("knob", [0, 1, 4])
 @pytest.mark.parametrize("tagged", [False, True])
 def test_gpu_from_binary_round_trip(tagged, knob):
     """Device from_binary/1 of oracle payloads (term_to_binary of random orddicts with
@@ -455,7 +457,7 @@ def test_gpu_from_binary_round_trip(tagged, knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
@@ -511,7 +513,7 @@ def test_gpu_from_binary_errors_and_atom_forms(knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1])
+@pytest.mark.parametrize("knob", [0, 1, 4])
 def test_gpu_from_binary_large_round_trip(knob):
     """4096 replicas x 512 slots x 64 token slots: device to_binary then from_binary
     restores every cell."""
@@ -578,6 +580,11 @@ def test_gpu_from_binary_fuzz():
     assert np.array_equal(st, st_serial), np.nonzero(st != st_serial)[0][:10]
     ok0 = st == 0
     assert np.array_equal(bt.download()[ok0], bs.download()[ok0])
+    bg = ctx.orset_batch(len(blobs), E)
+    with _read_kernel(ctx, 4):               # segment mode: same statuses and cells
+        st_seg = bg.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert np.array_equal(st_seg, st_serial), np.nonzero(st_seg != st_serial)[0][:10]
+    assert np.array_equal(bg.download()[ok0], bs.download()[ok0])
     ok = np.nonzero(st == 0)[0]
     if len(ok):
         again = bt.to_binaries(d, tag=T, vers=1)
@@ -604,7 +611,7 @@ def _small_orsets(rng, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4])
 def test_gpu_from_binary_small_tokens_round_trip(knob):
     """Elements with <= 3 token slots (element batches under knob 0): oracle payloads
     with every flag atom form decode to the host encoder's cells, and device to_binary ->
@@ -718,3 +725,37 @@ def test_gpu_from_binary_small_tokens_large():
             st = b2.etf_decode(d, out, offs, tag=etf.DT_ORSET_TAG, vers=1)
         assert (st == 0).all(), knob
         assert np.array_equal(b2.download(), h), knob
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", [0, 4])
+def test_gpu_from_binary_segments(knob):
+    """Long payloads split between waves (automatic for a few long payloads, knob 0;
+    every payload in 256-byte segments, knob 4): one 10k-element orddict, a few 2k-element
+    ones and short ones decode to the host encoder's cells.  Tokens that embed a real
+    element header (106 104 2 <elem image> 108) plant false segment starts: those
+    replicas fail the chain check and are decoded again serially, with the same result.
+    A LIST_EXT of 0 elements with its nil tail is [] (binary_to_term/1 accepts it), one
+    without the tail is malformed."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    rng = random.Random(11)
+    trap = lambda e, k: bytes([106, 104, 2, 97, e, 108]) + bytes([k]) * 14   # noqa: E731
+    big = [(e, [(bytes([e % 251, k]) * 10, rng.random() < 0.5) for k in range(2)])
+           for e in range(10_000)]
+    mids = [[(e, sorted([(trap((e + 7) % 200, k) if e % 5 == 0 else
+                          bytes([k, e % 256]) * 10, rng.random() < 0.3) for k in range(3)]))
+             for e in range(i, 2000 + i)] for i in range(3)]
+    states = [big] + mids + [[], [(1, [(bytes([1, 1]) * 10, True)])]]
+    ctx, dom, E, d = _decode_setup(states)
+    T = etf.DT_ORSET_TAG
+    blobs = [oetf.to_binary(T, 1, s) for s in states]
+    blobs += [bytes([T, 1, 131, 108, 0, 0, 0, 0, 106]), bytes([T, 1, 131, 108, 0, 0, 0, 0])]
+    pay, offs = _upload_payloads(ctx, blobs)
+    b = ctx.orset_batch(len(blobs), E)
+    with _read_kernel(ctx, knob):
+        st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert list(st) == [_lib.DEC_OK] * (len(states) + 1) + [_lib.DEC_MALFORMED]
+    want = dom.encode_orset(states + [[]], E)
+    assert np.array_equal(b.download()[:len(states) + 1], want)
+    assert etf.binary_to_term(bytes([131, 108, 0, 0, 0, 0, 106])) == []

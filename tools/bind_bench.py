@@ -82,6 +82,38 @@ def main():
     for _ in range(it):
         nd.encode(_lib.KIND_ORSET, [pa, pb], E, out=host)
     out["config1_native_encode_2x10k_us"] = (time.perf_counter() - t0) / it * 1e6
+    # where the rest goes: upload, kernel, device to_binary (size pass, write pass), download
+    stages = {"upload": 0.0, "join": 0.0, "etf_size_write": 0.0, "download": 0.0}
+    for _ in range(it):
+        t0 = time.perf_counter()
+        NA.upload(host[0])
+        NB.upload(host[1])
+        t1 = time.perf_counter()
+        NC.join(NA, NB)
+        ctx.synchronize()
+        t2 = time.perf_counter()
+        offs, buf, total = NC.etf_encode(d)
+        ctx.synchronize()
+        t3 = time.perf_counter()
+        o = offs.download(np.uint64)
+        buf.download(np.uint8, count=total)
+        t4 = time.perf_counter()
+        for k, v in zip(stages, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            stages[k] += v
+    for k, v in stages.items():
+        out["config1_native_%s_us" % k] = v / it * 1e6
+    out["config1_native_payload_bytes"] = int(total)
+    # from_binary/1 of the merged payload on the device (laspj_orset_etf_read), one replica
+    pay = ctx.buffer(len(got))
+    pay.upload(np.frombuffer(got, np.uint8))
+    po = ctx.buffer(16)
+    po.upload(np.array([0, len(got)], np.uint64))
+    st_ = NA.etf_decode(d, pay, po)
+    assert st_[0] == 0 and np.array_equal(NA.download_words(), NC.download_words())
+    t0 = time.perf_counter()
+    for _ in range(it):
+        NA.etf_decode(d, pay, po)
+    out["config1_device_from_binary_us"] = (time.perf_counter() - t0) / it * 1e6
 
     n = 1000
     st = core.Store(capacity=256)

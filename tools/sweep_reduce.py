@@ -17,6 +17,21 @@ E, q = 4096, 98304
 src, dst = ctx.orset_batch(8 * q, E), ctx.orset_batch(q, E)
 src.fill_synthetic(4)
 nbytes = 16 * 9 * q * E
+if len(sys.argv) > 1 and sys.argv[1] == "ab":
+    # interleaved repeats: the default sweep against tiles of 4 cells (64 per CU / all)
+    cfgs = {"sweep": (3, 0, 0), "tile4": (0, 0, 0), "tile2": (0, 2, 0), "tile8": (0, 8, 0)}
+    res = {k: [] for k in cfgs}
+    for _ in range(4):
+        for k, (kn, un, gr) in cfgs.items():
+            ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, kn)
+            ctx.set_tuning(_lib.TUNE_STREAM_UNROLL, un)
+            ctx.set_tuning(_lib.TUNE_STREAM_GRID, gr)
+            res[k].append(timed(ctx, lambda: dst.reduce_chunks(src, 8), 5))
+    for k, v in res.items():
+        print(json.dumps({"kernel": k, "ms": [round(x, 3) for x in v],
+                          "frac_hbm_best": round(nbytes / (min(v) / 1e3) / 8e12, 4)}), flush=True)
+    sys.exit(0)
+ctx.set_tuning(_lib.TUNE_REDUCE_KERNEL, 3)          # the grid-stride sweep's shapes
 for grid_per_cu in (0, 8, 16, 32, 128):
     for unroll in (1, 2):
         for nt in (1, 0):
