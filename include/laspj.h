@@ -127,9 +127,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         staging, 2 / 3 = record kernel, lanes, 16 / 20 KiB,
                                         4 = record kernel, lanes, 24 KiB, 5 = record
                                         kernel, per element thread, 24 KiB               */
-#define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = flat sweep when
-                                        the replica length is a power of two and
-                                        2 <= group <= 4, 1 = per-replica segments with a
+#define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = tiles of 4
+                                        cells per lane, one per block, when the replica
+                                        length is a power of two and 2 <= group <= 4
+                                        (4 = the same as a grid-stride sweep), 1 =
+                                        per-replica segments with a
                                         compile-time group, 2 = generic segments (also
                                         the runtime-count loop of reduce_chunks);
                                         reduce_chunks at 2..8 chunks: tiles read one

@@ -199,7 +199,8 @@ __device__ __forceinline__ u64 join_word(u64 x, u64 y) {
 }
 
 // power-of-two replica length: one flat grid-stride sweep over the destination (all
-// blocks move through HBM together, as the join does), 2 cells x G loads per lane;
+// blocks move through HBM together, as the join does), 2 cells x G loads per lane (knob
+// 4; the default is k_reduce_or_tile below);
 // MAX: the same sweep for the G-Counter reduce (per-actor max)
 template <int G, bool MAX = false>
 __global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64x2* src,
@@ -239,9 +240,65 @@ __global__ __launch_bounds__(kBlock) void k_reduce_or_flat(u64x2* dst, const u64
     }
 }
 
+// the same reduce as tiles of T x 256 destination cells, one per block, sources read
+// one at a time (as k_reduce_chunks_tile)
+template <int G, bool MAX, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_or_tile(u64x2* dst, const u64x2* src,
+                                                           uint64_t n, uint32_t lg) {
+    const uint64_t mask = (1ull << lg) - 1ull;
+    const uint64_t tile = (uint64_t)T * kBlock;
+    const uint64_t tiles = n / tile;
+    for (uint64_t b = blockIdx.x; b < tiles; b += gridDim.x) {
+        const uint64_t i0 = b * tile + threadIdx.x;
+        const u64x2* sp[T];
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+            const uint64_t i = i0 + u * kBlock;
+            sp[u] = src + (((i >> lg) * G) << lg) + (i & mask);
+        }
+        u64x2 acc[T];
+#pragma unroll
+        for (int u = 0; u < T; ++u) acc[u] = ld2<true>(sp[u]);
+#pragma unroll
+        for (int j = 1; j < G; ++j) {
+            u64x2 v[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) v[u] = ld2<true>(sp[u] + ((uint64_t)j << lg));
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                acc[u].x = join_word<MAX>(acc[u].x, v[u].x);
+                acc[u].y = join_word<MAX>(acc[u].y, v[u].y);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < T; ++u) st2<true>(dst + i0 + u * kBlock, acc[u]);
+    }
+    for (uint64_t i = tiles * tile + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const u64x2* s = src + (((i >> lg) * G) << lg) + (i & mask);
+        u64x2 a = ld2<true>(s);
+#pragma unroll
+        for (int j = 1; j < G; ++j) {
+            const u64x2 v = ld2<true>(s + ((uint64_t)j << lg));
+            a.x = join_word<MAX>(a.x, v.x);
+            a.y = join_word<MAX>(a.y, v.y);
+        }
+        st2<true>(dst + i, a);
+    }
+}
+
 template <int G, bool MAX = false>
 static void launch_reduce_flat(laspj_ctx* ctx, u64x2* d, const u64x2* s, uint64_t n,
                                uint32_t lg) {
+    // tiles by default (N = 3 OR-Set 12.6 -> 11.6 ms, N = 4 G-Counter 2.20 -> 1.81 ms,
+    // profiles/r02_sweep_reduce_groups.log); knob 4: the grid-stride sweep
+    if (ctx->tune_reduce != 4) {
+        const uint64_t tiles = n / (4ull * kBlock);
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1u << 30));
+        hipLaunchKernelGGL((k_reduce_or_tile<G, MAX, 4>), dim3(grid), dim3(kBlock), 0,
+                           ctx->stream, d, s, n, lg);
+        return;
+    }
     StreamTune t = stream_tune(ctx, n);
     hipLaunchKernelGGL((k_reduce_or_flat<G, MAX>), dim3(t.grid), dim3(kBlock), 0, ctx->stream,
                        d, s, n, lg);
@@ -249,7 +306,7 @@ static void launch_reduce_flat(laspj_ctx* ctx, u64x2* d, const u64x2* s, uint64_
 
 hipError_t launch_reduce_or(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                             uint64_t groups, uint32_t group, uint64_t wr) {
-    if ((wr % 2) == 0 && ctx->tune_reduce == 0) {
+    if ((wr % 2) == 0 && (ctx->tune_reduce == 0 || ctx->tune_reduce == 4)) {
         const uint64_t per = wr / 2;
         if ((per & (per - 1)) == 0 && group >= 2 && group <= 4) {
             const uint32_t lg = (uint32_t)__builtin_ctzll(per);
@@ -1203,7 +1260,9 @@ hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj
                                    uint8_t* res) {
     const uint32_t ns = (dst->elements + kFSeg - 1) / kFSeg;
     const uint64_t items = (dst->replicas + kFRun - 1) / kFRun * ns;
-    const uint64_t cap = (uint64_t)ctx->cus * 32;
+    // one (run, segment) item per block, no grid stride: 21.5 ms against 22.5 ms with 32
+    // blocks per CU striding (profiles/r02_sweep_c4_grid.log)
+    const uint64_t cap = ctx->tune_grid > 0 ? (uint64_t)ctx->tune_grid : (1ull << 30);
     const uint64_t g = items < cap ? items : cap;
     const bool bc = prev->replicas == 1 && dst->replicas != 1;
     u64* part = nullptr;
@@ -1378,7 +1437,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_max(u64* dst, const u64* src,
 
 hipError_t launch_reduce_max(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src,
                              uint64_t groups, uint32_t group, uint64_t wr) {
-    if ((wr % 2) == 0 && ctx->tune_reduce == 0) {     // the flat sweep, as the OR reduce
+    if ((wr % 2) == 0 && (ctx->tune_reduce == 0 || ctx->tune_reduce == 4)) {   // as the OR reduce
         const uint64_t per = wr / 2;
         if ((per & (per - 1)) == 0 && group >= 2 && group <= 4) {
             const uint32_t lg = (uint32_t)__builtin_ctzll(per);

@@ -234,8 +234,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_product_cols = value;
             return LASPJ_OK;
         case LASPJ_TUNE_REDUCE_KERNEL:
-            if (value < 0 || value > 3)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: reduce kernel must be 0..3");
+            if (value < 0 || value > 4)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: reduce kernel must be 0..4");
             ctx->tune_reduce = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_KERNEL:
