@@ -1287,6 +1287,7 @@ struct ReadLds {
     uint8_t win[kBWin + 64];     // 64 bytes of slack: rec_words reads 52 past a start
     uint8_t tab[kBuckets];       // bucket -> token rank of the current element
     uint8_t pres[64];            // token rank -> 1 present | 2 true
+    uint16_t rst[64];            // record starts found by locate_records (from the element's first)
 };
 
 // The batched decode's view of one payload: a 4 KiB LDS window over it, with every
@@ -1563,6 +1564,121 @@ __device__ __forceinline__ Cases lane_cases(uint32_t lane) {
     return Cases{lj, lane - lj * (lj + 1) / 2, lane < 55};
 }
 
+// Records of an element found without the scalar chain walk.  Every record after the
+// first starts right after a flag atom, so its first bytes are 101 104 2 (the `e` of
+// true / false, then 104 2): the lanes look for that byte triple over the element's
+// span, 4 positions per dword (a zero-byte test on the XOR with the pattern), and record
+// j is taken at the j-th match.  The element is committed only if every record
+// validates as in the chain path and each one ends exactly where the next begins (the
+// last one at the element's closing 106) — then the starts are the chain's.  Otherwise
+// nothing is touched and the caller walks the chain (a token image may hold those bytes,
+// and the chain gives the exact status of a malformed element).  Returns whether the
+// element's records were committed (into L.pres; pc left on the closing 106).
+__device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m_tok,
+                                               const RankPre& cur, uint32_t e, uint32_t kw,
+                                               uint32_t ksh, ReadLds& L, const DictView& d,
+                                               uint32_t lane) {
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    const uint32_t x0 = pc;
+    const uint32_t lim = min(w.hi, w.end);
+    if (x0 >= lim) return false;
+    const uint32_t span = min(m_tok * (RL + 8u) + 1u, lim - x0);   // [x0, x0 + span)
+    uint32_t total = 0;
+    if (m_tok > 1) {
+        const uint32_t a0 = x0 & ~3u;
+        const uint32_t K = (((span + (x0 - a0) + 63u) >> 6) + 3u) & ~3u;   // bytes per lane
+        const uint32_t b0 = a0 + lane * K;                                   // this lane's first
+        const uint32_t* w32 = reinterpret_cast<const uint32_t*>(w.buf);
+        const uint32_t top = (kBWin + 60u) >> 2;                            // last dword index
+        u64 mask = 0;
+        uint32_t dm1 = b0 >= 4u ? w32[min((b0 >> 2) - 1u, top)] : 0u;
+        uint32_t d0 = w32[min(b0 >> 2, top)];
+        for (uint32_t g = 0; g < (K >> 2); ++g) {
+            const uint32_t d1 = w32[min((b0 >> 2) + g + 1u, top)];
+            const uint32_t A = __builtin_amdgcn_alignbyte(d0, dm1, 3);       // b[q - 1 + k]
+            const uint32_t B = __builtin_amdgcn_alignbyte(d1, d0, 1);        // b[q + 1 + k]
+            const uint32_t T = (A ^ 0x65656565u) | (d0 ^ 0x68686868u) | (B ^ 0x02020202u);
+            const uint32_t z = ~(((T & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | T) & 0x80808080u;
+            mask |= (u64)((((z >> 7) * 0x204081u) >> 21) & 0xFu) << (4u * g);
+            dm1 = d0;
+            d0 = d1;
+        }
+        // positions q = b0 + i with x0 < q < x0 + span only
+        const int64_t lo = (int64_t)x0 + 1 - (int64_t)b0;                  // first allowed i
+        const int64_t hi = (int64_t)x0 + (int64_t)span - (int64_t)b0;      // first excluded i
+        if (hi <= 0) mask = 0;
+        else if (hi < 64) mask &= (1ull << hi) - 1ull;
+        if (lo >= 64) mask = 0;
+        else if (lo > 0) mask &= ~((1ull << lo) - 1ull);
+        // starts in stream order: a wave prefix sum of the counts
+        const uint32_t cnt = (uint32_t)__popcll(mask);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        total = rdlane(incl, 63);
+        if (total + 1u < m_tok) return false;
+        uint32_t k = incl - cnt;
+        while (mask && k < 63u) {
+            const uint32_t i = (uint32_t)__ffsll((long long)mask) - 1u;
+            mask &= mask - 1ull;
+            L.rst[k++] = (uint16_t)(b0 + i - x0);
+        }
+        wave_sync();
+    }
+    const bool mine = lane < m_tok;
+    uint32_t myx = x0, rank = 0xFFu, fl = 0, fend = 0;
+    bool ok = true;
+    if (mine) {
+        if (lane) myx = x0 + L.rst[lane - 1];
+        rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
+        ok = rank < cur.cnt;
+        if (ok) {                                               // exact compare
+            uint32_t rw[12], t[12];
+            rec_words(w.buf, myx, RL, rw);
+            load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) ok &= t[i] == rw[i];
+        }
+        const uint32_t fo = myx + RL;
+        const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
+        const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
+        const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
+        const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
+        uint32_t gh = 0, len = 0, word = 0, c4 = 0;
+        if ((a0 == 100 || a0 == 118) && a1 == 0) {
+            gh = 3;
+            len = (v0 >> 16) & 0xFFu;
+            word = __builtin_amdgcn_alignbyte(v1, v0, 3);
+            c4 = v1 >> 24;
+        } else if (a0 == 119) {
+            gh = 2;
+            len = a1;
+            word = __builtin_amdgcn_alignbyte(v1, v0, 2);
+            c4 = (v1 >> 16) & 0xFFu;
+        }
+        fend = fo + gh + len;
+        const bool tr = gh && len == 4 && word == 0x65757274u;
+        const bool fa = gh && len == 5 && word == 0x736C6166u && c4 == 'e';
+        ok &= (tr || fa) && fend < lim;
+        fl = tr;
+    }
+    // term order, and each record ends where the next one starts
+    const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+    const uint32_t nx = __shfl(myx, (lane + 1u) & 63u, 64);
+    if (mine) {
+        if (lane && rank <= pr) ok = false;
+        if (lane + 1u < m_tok) ok &= fend == nx;
+        else ok &= w.buf[min(fend, kBWin + 63u)] == 106;
+    }
+    if (__ballot(mine && !ok)) return false;
+    if (mine) L.pres[rank] = (uint8_t)(1u | (fl << 1));
+    pc = rdlane(fend, m_tok - 1u);
+    return true;
+}
+
 // Decode elements at the cursor into cells c: at most n of them (count mode), or with
 // n = ~0u every element that starts before the absolute payload position `stop`, up to
 // the list's closing 106 (segment mode: *tail is set when the cursor stops on it).
@@ -1659,7 +1775,15 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
         L.pres[lane] = 0;
         wave_sync();
         int32_t tprev = -1;
-        for (uint32_t done = 0; done < m_tok;) {
+        uint32_t done = 0;
+        if (d.tok_max > 8) {
+            // many records per element: locate them byte-parallel (the chain below only
+            // when that does not validate)
+            const uint32_t want = min(m_tok * (RL + 8u) + 8u, w.end - pc);
+            if (pc + want > w.hi && w.hi < w.end) pc = refill(w, pc);
+            if (locate_records(w, pc, m_tok, cur, e, kw, ksh, L, d, lane)) done = m_tok;
+        }
+        while (done < m_tok) {
             // room for the batch in the window
             {
                 const uint32_t want = min((m_tok - done) * (RL + 8u) + 8u, w.end - pc);

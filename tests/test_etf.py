@@ -759,3 +759,68 @@ def test_gpu_from_binary_segments(knob):
     want = dom.encode_orset(states + [[]], E)
     assert np.array_equal(b.download()[:len(states) + 1], want)
     assert etf.binary_to_term(bytes([131, 108, 0, 0, 0, 0, 106])) == []
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_record_locator_fuzz():
+    """Elements with 20-40 records (the byte-parallel record locator's case), tokens that
+    embed its `101 104 2` marker at every offset, flags in all three atom forms, and
+    1500 corrupted copies: the batched decode (locator + chain fallback) and the serial
+    scan agree on every status and cell, and clean payloads decode to the encoder's
+    cells."""
+    import numpy as np
+    from lasp_amd import etf
+    rng = random.Random(404)
+    marker = bytes([101, 104, 2])
+
+    def tok(i, k):
+        b = bytearray(rng.randrange(256) for _ in range(20))
+        if k % 3 == 0:
+            at = (i + k) % 18
+            b[at:at + 3] = marker
+        return bytes(b)
+    pools = {e: sorted({tok(e, k) for k in range(48)}) for e in range(40)}
+    states = []
+    for _ in range(30):
+        es = sorted(rng.sample(range(40), rng.randint(1, 12)))
+        states.append([(e, sorted((t, rng.random() < 0.5)
+                                  for t in rng.sample(pools[e], rng.randint(20, 40))))
+                       for e in es])
+    ctx, dom, E, d = _decode_setup(states)
+    T = etf.DT_ORSET_TAG
+    base = []
+    for i, s in enumerate(states):
+        p = oetf.to_binary(T, 1, s)
+        if i % 3 == 1:
+            p = p.replace(bytes([100, 0, 4]) + b"true", bytes([119, 4]) + b"true") \
+                 .replace(bytes([100, 0, 5]) + b"false", bytes([119, 5]) + b"false")
+        elif i % 3 == 2:
+            p = p.replace(bytes([100, 0, 5]) + b"false", bytes([118, 0, 5]) + b"false")
+        base.append(p)
+    blobs = list(base)
+    for _ in range(1500):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(4)
+        if kind == 0:
+            for _ in range(rng.randint(1, 2)):
+                b[rng.randrange(len(b))] = rng.choice([101, 104, 2, 106, 5, 4, rng.randrange(256)])
+        elif kind == 1:
+            del b[rng.randrange(len(b)):]
+        elif kind == 2:
+            pos = rng.randrange(len(b) + 1)
+            b[pos:pos] = rng.choice([marker, bytes([101]), bytes([104, 2]), b"\0"])
+        else:
+            pos = rng.randrange(len(b))
+            del b[pos:pos + rng.randint(1, 3)]
+        blobs.append(bytes(b))
+    pay, offs = _upload_payloads(ctx, blobs)
+    bt = ctx.orset_batch(len(blobs), E)
+    st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+    bs = ctx.orset_batch(len(blobs), E)
+    with _read_kernel(ctx, 1):
+        st_serial = bs.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert np.array_equal(st, st_serial), np.nonzero(st != st_serial)[0][:10]
+    ok = st == 0
+    assert np.array_equal(bt.download()[ok], bs.download()[ok])
+    assert (st[:len(base)] == 0).all()
+    assert np.array_equal(bt.download()[:len(base)], dom.encode_orset(states, E))
