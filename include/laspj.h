@@ -150,7 +150,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         1 = serial record scan, 2 = batched records
                                         without element batches, 3 = never split,
                                         4 = always split (256-byte segments),
-                                        5 = always split (sized segments)                */
+                                        5 = always split (sized segments), 6 = element
+                                        batches walked by the scalar unit (the lanes
+                                        find element starts by default)                 */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

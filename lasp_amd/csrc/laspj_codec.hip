@@ -1220,9 +1220,18 @@ inline uint64_t rd_bytes(uint64_t E, uint64_t RK) { return E * (16 + 64 + 2 * RK
 __device__ __forceinline__ void rec_words(const uint8_t* buf, uint32_t o, uint32_t L,
                                           uint32_t (&w)[12]) {
     const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf + (o & ~3u));
+    // 8 dwords cover L <= 28 (Lasp's 20-byte binary tokens: L = 27), else 13; one
+    // wave-uniform branch, the loads of each side issued together
     uint32_t q[13];
+    if (L <= 28u) {
 #pragma unroll
-    for (int i = 0; i < 13; ++i) q[i] = b32[i];
+        for (int i = 0; i < 8; ++i) q[i] = b32[i];
+#pragma unroll
+        for (int i = 8; i < 13; ++i) q[i] = 0u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 13; ++i) q[i] = b32[i];
+    }
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
         const uint32_t v = __builtin_amdgcn_alignbyte(q[i + 1], q[i], o & 3u);
@@ -1341,6 +1350,19 @@ __device__ __forceinline__ bool eq48(const uint8_t* q, const uint8_t* t16, uint3
     for (uint32_t i = 0; i < 48; ++i)
         if (i < L) eq &= q[i] == ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
     return eq;
+}
+
+struct HdrHash {
+    const uint32_t* tab;   // open addressing: rank + 1, 0 empty
+    uint32_t mask;
+    u64 lens;              // bit hl - 1: some header template is hl bytes (hl <= 64)
+};
+
+// the header-template hash (host and device agree): 16 words, bytes >= hl zero
+__host__ __device__ inline uint32_t hdr_mix(uint32_t h, uint32_t v) {
+    h ^= v;
+    h *= 0x9E3779B1u;
+    return h ^ (h >> 16);
 }
 
 // Element batches, for dictionaries with few token slots per element (tok_max <= 8,
@@ -1564,6 +1586,59 @@ __device__ __forceinline__ Cases lane_cases(uint32_t lane) {
     return Cases{lj, lane - lj * (lj + 1) / 2, lane < 55};
 }
 
+// Byte-parallel search of window bytes (x0, x0 + span) for the triple `first 104 2`
+// (first = 101, the `e` ending a flag atom, before a record; 106, a closing nil, before
+// an element): lanes take K bytes each (a multiple of 4 with an odd dword count, so
+// their dword reads hit distinct LDS banks) and test 4 positions per dword with a
+// zero-byte test on the XOR with the pattern.  The offsets (from x0) of the first 63
+// matches in stream order go to L.rst; returns the number of matches.
+__device__ __forceinline__ uint32_t find_marks(const PWin& w, uint32_t x0, uint32_t span,
+                                               uint32_t first, ReadLds& L, uint32_t lane) {
+    const uint32_t a0 = x0 & ~3u;
+    uint32_t K = (((span + (x0 - a0) + 63u) >> 6) + 3u) & ~3u;
+    if (!(K & 4u)) K += 4u;
+    const uint32_t b0 = a0 + lane * K;                                   // this lane's first
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(w.buf);
+    const uint32_t top = (kBWin + 60u) >> 2;                            // last dword index
+    const uint32_t pa = first * 0x01010101u;
+    u64 mask = 0;
+    uint32_t dm1 = b0 >= 4u ? w32[min((b0 >> 2) - 1u, top)] : 0u;
+    uint32_t d0 = w32[min(b0 >> 2, top)];
+    for (uint32_t g = 0; g < (K >> 2); ++g) {
+        const uint32_t d1 = w32[min((b0 >> 2) + g + 1u, top)];
+        const uint32_t A = __builtin_amdgcn_alignbyte(d0, dm1, 3);       // b[q - 1 + k]
+        const uint32_t B = __builtin_amdgcn_alignbyte(d1, d0, 1);        // b[q + 1 + k]
+        const uint32_t T = (A ^ pa) | (d0 ^ 0x68686868u) | (B ^ 0x02020202u);
+        const uint32_t z = ~(((T & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | T) & 0x80808080u;
+        mask |= (u64)((((z >> 7) * 0x204081u) >> 21) & 0xFu) << (4u * g);
+        dm1 = d0;
+        d0 = d1;
+    }
+    // positions q = b0 + i with x0 < q < x0 + span only
+    const int64_t lo = (int64_t)x0 + 1 - (int64_t)b0;
+    const int64_t hi = (int64_t)x0 + (int64_t)span - (int64_t)b0;
+    if (hi <= 0) mask = 0;
+    else if (hi < 64) mask &= (1ull << hi) - 1ull;
+    if (lo >= 64) mask = 0;
+    else if (lo > 0) mask &= ~((1ull << lo) - 1ull);
+    const uint32_t cnt = (uint32_t)__popcll(mask);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    const uint32_t total = rdlane(incl, 63);
+    uint32_t k = incl - cnt;
+    while (mask && k < 63u) {
+        const uint32_t i = (uint32_t)__ffsll((long long)mask) - 1u;
+        mask &= mask - 1ull;
+        L.rst[k++] = (uint16_t)(b0 + i - x0);
+    }
+    wave_sync();
+    return total;
+}
+
 // Records of an element found without the scalar chain walk.  Every record after the
 // first starts right after a flag atom, so its first bytes are 101 104 2 (the `e` of
 // true / false, then 104 2): the lanes look for that byte triple over the element's
@@ -1583,50 +1658,9 @@ __device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m
     const uint32_t lim = min(w.hi, w.end);
     if (x0 >= lim) return false;
     const uint32_t span = min(m_tok * (RL + 8u) + 1u, lim - x0);   // [x0, x0 + span)
-    uint32_t total = 0;
     if (m_tok > 1) {
-        const uint32_t a0 = x0 & ~3u;
-        const uint32_t K = (((span + (x0 - a0) + 63u) >> 6) + 3u) & ~3u;   // bytes per lane
-        const uint32_t b0 = a0 + lane * K;                                   // this lane's first
-        const uint32_t* w32 = reinterpret_cast<const uint32_t*>(w.buf);
-        const uint32_t top = (kBWin + 60u) >> 2;                            // last dword index
-        u64 mask = 0;
-        uint32_t dm1 = b0 >= 4u ? w32[min((b0 >> 2) - 1u, top)] : 0u;
-        uint32_t d0 = w32[min(b0 >> 2, top)];
-        for (uint32_t g = 0; g < (K >> 2); ++g) {
-            const uint32_t d1 = w32[min((b0 >> 2) + g + 1u, top)];
-            const uint32_t A = __builtin_amdgcn_alignbyte(d0, dm1, 3);       // b[q - 1 + k]
-            const uint32_t B = __builtin_amdgcn_alignbyte(d1, d0, 1);        // b[q + 1 + k]
-            const uint32_t T = (A ^ 0x65656565u) | (d0 ^ 0x68686868u) | (B ^ 0x02020202u);
-            const uint32_t z = ~(((T & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | T) & 0x80808080u;
-            mask |= (u64)((((z >> 7) * 0x204081u) >> 21) & 0xFu) << (4u * g);
-            dm1 = d0;
-            d0 = d1;
-        }
-        // positions q = b0 + i with x0 < q < x0 + span only
-        const int64_t lo = (int64_t)x0 + 1 - (int64_t)b0;                  // first allowed i
-        const int64_t hi = (int64_t)x0 + (int64_t)span - (int64_t)b0;      // first excluded i
-        if (hi <= 0) mask = 0;
-        else if (hi < 64) mask &= (1ull << hi) - 1ull;
-        if (lo >= 64) mask = 0;
-        else if (lo > 0) mask &= ~((1ull << lo) - 1ull);
-        // starts in stream order: a wave prefix sum of the counts
-        const uint32_t cnt = (uint32_t)__popcll(mask);
-        uint32_t incl = cnt;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        total = rdlane(incl, 63);
+        const uint32_t total = find_marks(w, x0, span, 0x65u, L, lane);
         if (total + 1u < m_tok) return false;
-        uint32_t k = incl - cnt;
-        while (mask && k < 63u) {
-            const uint32_t i = (uint32_t)__ffsll((long long)mask) - 1u;
-            mask &= mask - 1ull;
-            L.rst[k++] = (uint16_t)(b0 + i - x0);
-        }
-        wave_sync();
     }
     const bool mine = lane < m_tok;
     uint32_t myx = x0, rank = 0xFFu, fl = 0, fend = 0;
@@ -1679,6 +1713,141 @@ __device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m
     return true;
 }
 
+// Element batches without the scalar walk (few token slots per element, the ad
+// counter's 3-replica tokens): every element after the first at the cursor starts right
+// after the previous element's closing 106, so `106 104 2` marks element starts; lane i
+// takes the element at the i-th mark, finds its rank by the hash of its header bytes
+// (one probe per header length the dictionary has, exact 64-byte compare), and walks its
+// own <= 8 records: token bucket -> term rank among the element's, exact template
+// compare, flag atom, ascending ranks, the closing 106 — which must sit right before the
+// next lane's element.  Elements before the first lane that fails any of this are
+// committed (the cells the element-at-a-time path would write); that path decodes from
+// the failing one and gives its status.
+__device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_t left, u64 stop,
+                                   const ReadTabs& t, const DictView& d, const HdrHash& hh,
+                                   uint32_t E, ReadLds& L, u64x2* c, uint32_t lane) {
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    if (w.hi < w.end && pc + kBWin / 2 > w.hi) pc = refill(w, pc);
+    const uint32_t lim = min(w.hi, w.end);
+    const uint32_t srel = stop <= w.lo ? 0u : (uint32_t)min(stop - w.lo, (u64)0xFFFFFFFFu);
+    const uint32_t x0 = pc;
+    if (x0 >= lim || x0 >= srel) return 0;
+    const uint32_t total = find_marks(w, x0, lim - x0, 106u, L, lane);
+    const uint32_t N = min(min(64u, total + 1u), left);
+    const bool mine = lane < N;
+    const uint32_t s = x0 + (lane && mine ? L.rst[lane - 1] : 0u);
+    bool ok = mine && s < srel;
+    // the element's rank: its header 104 2 <elem image> 108 by hash
+    int64_t rk = -1;
+    uint32_t hl = 0;
+    if (ok) {
+        u64 lens = hh.lens;
+        while (lens && rk < 0) {
+            const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
+            lens &= lens - 1ull;
+            if (s + L2 > lim) break;
+            uint32_t q[16];
+            uint32_t h = L2 * 0x85EBCA6Bu;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int rem = (int)L2 - 4 * i;          // L2 is wave-uniform
+                const uint32_t v = rem > 0 ? word_at(w.buf, min(s + 4u * i, kBWin + 56u)) : 0u;
+                q[i] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+                h = hdr_mix(h, q[i]);
+            }
+            for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
+                const uint32_t v = hh.tab[i];
+                if (!v || v > E) break;
+                const uint32_t r = v - 1u;
+                // (no length check: images are self-delimiting, so an L2-byte template
+                // ending in 108 matches only its own element's header)
+                const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * r);
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if ((uint32_t)(16 * j) >= L2) break;   // the rest is zero on both sides
+                    const u32x4 a = tp[j];
+                    eq &= a.x == q[4 * j] && a.y == q[4 * j + 1] && a.z == q[4 * j + 2] &&
+                          a.w == q[4 * j + 3];
+                }
+                if (eq) { rk = r; hl = L2; break; }
+            }
+        }
+        ok = rk >= 0;
+    }
+    // ranks ascend: after the previous lane's element (lane 0: after prev)
+    const int64_t prk = (int64_t)(int32_t)__shfl((int32_t)rk, (lane + 63u) & 63u, 64);
+    if (ok) ok = rk > (lane ? prk : prev);
+    u64 pb = 0, rb = 0;
+    uint32_t e = 0, y = s;
+    if (ok) {
+        const uint4 ds = t.desc[rk];
+        e = ds.x;
+        const uint32_t cnt = ds.w, kw = 4u * (ds.z & 0xFFu), ksh = ds.z >> 8;
+        y = s + hl;
+        ok = y + 4u <= lim;
+        const uint32_t m = ok ? __builtin_bswap32(word_at(w.buf, y)) : 0u;
+        ok = ok && m >= 1u && m <= cnt && cnt <= kSmallTok;
+        y += 4u;
+        // the element's token buckets (by term rank) and rank -> slot
+        uint32_t tb[kSmallTok];
+#pragma unroll
+        for (uint32_t j = 0; j < kSmallTok; ++j) tb[j] = ok && j < cnt ? t.tb[(u64)rk * RK + j] : 0xFFFFFFFFu;
+        const u64 ord = ok ? *reinterpret_cast<const u64*>(d.tok_order + 64ull * e) : 0ull;
+        int32_t kprev = -1;
+        for (uint32_t j = 0; ok && j < m; ++j) {
+            if (y + RL + 8u > lim) { ok = false; break; }
+            const uint32_t bk = (word_at(w.buf, y + kw) >> ksh) & (kBuckets - 1u);
+            uint32_t k = 0xFFu;
+#pragma unroll
+            for (uint32_t jj = 0; jj < kSmallTok; ++jj)
+                if (tb[jj] == bk) k = jj;
+            if (k == 0xFFu || (int32_t)k <= kprev) { ok = false; break; }
+            uint32_t rw[12], tw[12];
+            rec_words(w.buf, y, RL, rw);
+            load48(tw, d.rec_pad + ((u64)e * RK + k) * RS, RL);
+            bool eq = true;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) eq &= tw[i] == rw[i];
+            const uint32_t fo = y + RL;
+            const uint32_t v0 = word_at(w.buf, fo), v1 = word_at(w.buf, fo + 4u);
+            const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
+            uint32_t gh = 0, len = 0, word = 0, c4 = 0;
+            if ((a0 == 100 || a0 == 118) && a1 == 0) {
+                gh = 3;
+                len = (v0 >> 16) & 0xFFu;
+                word = __builtin_amdgcn_alignbyte(v1, v0, 3);
+                c4 = v1 >> 24;
+            } else if (a0 == 119) {
+                gh = 2;
+                len = a1;
+                word = __builtin_amdgcn_alignbyte(v1, v0, 2);
+                c4 = (v1 >> 16) & 0xFFu;
+            }
+            const bool tr = gh && len == 4 && word == 0x65757274u;
+            const bool fa = gh && len == 5 && word == 0x736C6166u && c4 == 'e';
+            if (!eq || !(tr || fa)) { ok = false; break; }
+            const uint32_t slot = (uint32_t)(ord >> (8 * k)) & 0xFFu;
+            pb |= 1ull << slot;
+            if (tr) rb |= 1ull << slot;
+            kprev = (int32_t)k;
+            y += RL + gh + len;
+        }
+        ok = ok && y < lim && w.buf[y] == 106;
+        y += 1u;
+    }
+    // each element ends where the next lane's begins
+    const uint32_t nxs = __shfl(s, (lane + 1u) & 63u, 64);
+    if (ok && lane + 1u < N) ok = y == nxs;
+    const u64 bad = __ballot(mine && !ok);
+    const uint32_t commit = bad ? (uint32_t)__ffsll((long long)bad) - 1u : N;
+    if (commit == 0) return 0;
+    if (lane < commit) c[e] = u64x2{pb, rb};
+    prev = (int64_t)(int32_t)rdlane((uint32_t)rk, commit - 1u);
+    pc = rdlane(y, commit - 1u);
+    return commit;
+}
+
 // Decode elements at the cursor into cells c: at most n of them (count mode), or with
 // n = ~0u every element that starts before the absolute payload position `stop`, up to
 // the list's closing 106 (segment mode: *tail is set when the cursor stops on it).
@@ -1688,8 +1857,9 @@ template <bool SMALL>
 __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t& prev,
                                                  RankPre& nx, uint32_t n, u64 stop, bool& tail,
                                                  int32_t& st, const ReadTabs& tabs,
-                                                 const DictView& d, uint32_t E, ReadLds& L,
-                                                 u64x2* c, uint32_t lane, Cases cs) {
+                                                 const DictView& d, const HdrHash& hh,
+                                                 uint32_t E, ReadLds& L, u64x2* c,
+                                                 uint32_t lane, Cases cs) {
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
     const uint32_t hmax = min(d.ehdr_max + 4u, kBWin - 16u);
     const bool seg = n == 0xFFFFFFFFu;
@@ -1704,8 +1874,9 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
             if (ub(w, pc) == 106) { tail = true; break; }
         }
         if (SMALL) {
-            const uint32_t got = read_batch(w, pc, prev, n - k, stop, tabs, d, E, RL, RS, L, c,
-                                            lane);
+            const uint32_t got =
+                hh.tab ? read_batch_par(w, pc, prev, n - k, stop, tabs, d, hh, E, L, c, lane)
+                       : read_batch(w, pc, prev, n - k, stop, tabs, d, E, RL, RS, L, c, lane);
             if (got) {
                 k += got;
                 if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
@@ -1919,8 +2090,9 @@ template <bool SMALL>
 __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
-                                                           ReadTabs tabs, int tag, int vers,
-                                                           u64x2* cells, int32_t* status,
+                                                           ReadTabs tabs, HdrHash hh, int tag,
+                                                           int vers, u64x2* cells,
+                                                           int32_t* status,
                                                            const uint32_t* redo) {
     __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
     // the wave index as a scalar: everything per replica then stays wave-uniform
@@ -1944,7 +2116,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* pay
             int64_t prev = -1;                    // term rank of the previous element
             RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
             bool tail = false;
-            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, E, L, c, lane, cs);
+            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, hh, E, L, c, lane,
+                                cs);
         }
         if (st == LASPJ_DEC_OK && list) {
             if (pc + 1 > w.end) st = LASPJ_DEC_MALFORMED;
@@ -1980,19 +2153,6 @@ struct SegRes {
 };
 constexpr uint32_t kSegNone = 0xFFFFFFFFu;
 constexpr uint32_t kSegEmptyList = 1u;
-
-struct HdrHash {
-    const uint32_t* tab;   // open addressing: rank + 1, 0 empty
-    uint32_t mask;
-    u64 lens;              // bit hl - 1: some header template is hl bytes (hl <= 64)
-};
-
-// the header-template hash (host and device agree): 16 words, bytes >= hl zero
-__host__ __device__ inline uint32_t hdr_mix(uint32_t h, uint32_t v) {
-    h ^= v;
-    h *= 0x9E3779B1u;
-    return h ^ (h >> 16);
-}
 
 // the rank of the element whose header template is at window offset x, or -1
 __device__ int64_t resolve_hdr(const PWin& w, uint32_t x, const HdrHash& hh,
@@ -2111,8 +2271,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
         if (go) {
             bool tail = false;
             int32_t st = LASPJ_DEC_OK;
-            out.cnt = decode_elems<SMALL>(w, pc, prev, nx, 0xFFFFFFFFu, stop, tail, st, tabs, d, E,
-                                          L, c, lane, cs);
+            out.cnt = decode_elems<SMALL>(w, pc, prev, nx, 0xFFFFFFFFu, stop, tail, st, tabs, d,
+                                          hh, E, L, c, lane, cs);
             out.st = st;
             out.end = (uint32_t)(w.lo + pc - base);
             out.rlast = (int32_t)prev;
@@ -2333,9 +2493,14 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
-    auto kread = d->tok_max <= kSmallTok && ctx->tune_etf_read == 0 ? k_orset_etf_read<true>
-                                                                    : k_orset_etf_read<false>;
+    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6)
+                     ? k_orset_etf_read<true> : k_orset_etf_read<false>;
     const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+    // the header hash (segment search; element batches without the scalar walk — knob 6
+    // keeps the walking element batches)
+    const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
+    const HdrHash hh_small{ctx->tune_etf_read == 6 ? nullptr : d->rd_htab, d->rd_hmask,
+                           d->rd_hlens};
     // Segment mode when there are too few payloads to fill the chip with one wave each
     // (fewer than 8 per CU) and they are long: segments of S bytes, S sized for ~48 waves
     // per CU (6 resident per SIMD, the rest queued behind them for balance), at least
@@ -2374,7 +2539,6 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         LJ_HIP(ctx, hipMemcpyAsync(dsegbase, segbase.data(), 4ull * (R + 1), hipMemcpyHostToDevice,
                                    ctx->stream));
         LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
-        const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
         const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
         hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
                                ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
@@ -2394,7 +2558,7 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
                            ctx->stream, static_cast<const uint8_t*>(payload->dev),
                            (u64)payload->bytes, static_cast<const u64*>(offsets->dev), R,
-                           b->elements, view(d), tabs, tag, vers,
+                           b->elements, view(d), tabs, hh_small, tag, vers,
                            reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev),
                            (const uint32_t*)redo);
         LJ_LAUNCHED(ctx);
@@ -2409,7 +2573,7 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         hipLaunchKernelGGL(kread, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
                            static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tabs,
-                           tag, vers, reinterpret_cast<u64x2*>(b->dev),
+                           hh_small, tag, vers, reinterpret_cast<u64x2*>(b->dev),
                            static_cast<int32_t*>(status->dev), (const uint32_t*)nullptr);
     else
         hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,

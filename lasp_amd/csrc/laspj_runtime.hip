@@ -244,8 +244,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_etf = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_READ:
-            if (value < 0 || value > 5)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..5");
+            if (value < 0 || value > 6)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..6");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
         default:

@@ -457,7 +457,7 @@ def test_gpu_from_binary_round_trip(tagged, knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2, 4])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
@@ -611,7 +611,7 @@ def _small_orsets(rng, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2, 4])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6])
 def test_gpu_from_binary_small_tokens_round_trip(knob):
     """Elements with <= 3 token slots (element batches under knob 0): oracle payloads
     with every flag atom form decode to the host encoder's cells, and device to_binary ->
@@ -824,3 +824,61 @@ def test_gpu_from_binary_record_locator_fuzz():
     assert np.array_equal(bt.download()[ok], bs.download()[ok])
     assert (st[:len(base)] == 0).all()
     assert np.array_equal(bt.download()[:len(base)], dom.encode_orset(states, E))
+
+
+@pytest.mark.gpu
+def test_gpu_from_binary_small_tokens_fuzz():
+    """Elements with <= 3 token slots (the lane-parallel element batches): tokens that
+    embed the element-start marker `106 104 2` followed by a real element header, and
+    1500 corrupted payloads; the default decode, the scalar-walk element batches (knob 6)
+    and the serial scan agree on every status and cell."""
+    import numpy as np
+    from lasp_amd import etf
+    rng = random.Random(606)
+    states = _small_orsets(rng, 200)
+    hdrs = [bytes([106, 104, 2, 97, x, 108]) for x in range(0, 60, 3)]
+    memo = {}
+
+    def plant(t):
+        # the same rewrite every time a token appears: elements keep their <= 3 tokens
+        if t not in memo:
+            h = rng.choice(hdrs)
+            at = rng.randrange(0, 20 - len(h) + 1)
+            memo[t] = t[:at] + h + t[at + len(h):] if rng.random() < 0.4 else t
+        return memo[t]
+    planted = [[(e, sorted(dict((plant(t), f) for t, f in toks).items())) for e, toks in s_]
+               for s_ in states]
+    ctx, dom, E, d = _decode_setup(planted)
+    T = etf.DT_ORSET_TAG
+    base = [oetf.to_binary(T, 1, s_) for s_ in planted]
+    blobs = list(base)
+    for _ in range(1500):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(4)
+        if kind == 0 and b:
+            for _ in range(rng.randint(1, 2)):
+                b[rng.randrange(len(b))] = rng.choice([106, 104, 2, 108, 97, rng.randrange(256)])
+        elif kind == 1 and b:
+            del b[rng.randrange(len(b)):]
+        elif kind == 2:
+            pos = rng.randrange(len(b) + 1)
+            b[pos:pos] = rng.choice([bytes([106, 104, 2]), bytes([106]), b"\0"])
+        elif b:
+            pos = rng.randrange(len(b))
+            del b[pos:pos + rng.randint(1, 3)]
+        blobs.append(bytes(b))
+    pay, offs = _upload_payloads(ctx, blobs)
+    res = {}
+    for knob in (0, 6, 1):
+        bt = ctx.orset_batch(len(blobs), E)
+        with _read_kernel(ctx, knob):
+            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+        res[knob] = (st, bt.download())
+    st1, c1 = res[1]
+    for knob in (0, 6):
+        st, cl = res[knob]
+        assert np.array_equal(st, st1), (knob, np.nonzero(st != st1)[0][:10])
+        ok = st1 == 0
+        assert np.array_equal(cl[ok], c1[ok]), knob
+    assert (st1[:len(base)] == 0).all()
+    assert np.array_equal(res[0][1][:len(base)], dom.encode_orset(planted, E))
