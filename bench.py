@@ -229,6 +229,35 @@ def config1_gpu(ctx):
         ctx.synchronize()
         out["us_" + name] = (time.perf_counter() - t0) * 1e6 / iters
     out["workload"] = "1 replica pair x 20k element slots, inputs resident in HBM"
+    # the same merge as the NIF pays it: two term_to_binary/1 payloads of 10k-element
+    # orddicts (built untimed) -> native dictionary encode (laspj_dict_encode) -> upload ->
+    # k_or16 -> device to_binary -> download of the merged payload
+    from lasp_amd import _lib, etf
+    from lasp_amd.engine import ETFDict
+    from lasp_amd.hostdict import NativeDict
+    ta = [(e, [(b"A" + e.to_bytes(19, "big"), False)]) for e in range(n)]
+    tb = [(e, [(b"B" + e.to_bytes(19, "big"), e % 10 == 0)]) for e in range(n)]
+    pa, pb = etf.term_to_binary(ta), etf.term_to_binary(tb)
+    nd = NativeDict()
+    nd.add(_lib.KIND_ORSET, [pa, pb])
+    E = nd.info()[0]
+    d = ETFDict(ctx, E, *nd.export(E))
+    na, nb, nc = ctx.orset_batch(1, E), ctx.orset_batch(1, E), ctx.orset_batch(1, E)
+    host = np.zeros((2, 2 * E), np.uint64)
+
+    def e2e():
+        cells, st = nd.encode(_lib.KIND_ORSET, [pa, pb], E, out=host)
+        na.upload(cells[0])
+        nb.upload(cells[1])
+        nc.join(na, nb)
+        return nc.to_binaries(d)[0]
+    e2e()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        e2e()
+    out["us_merge_native_end_to_end"] = (time.perf_counter() - t0) * 1e6 / 5
+    out["end_to_end"] = ("2 x 10k-element term_to_binary payloads: native encode + upload + "
+                         "join + device to_binary + download")
     return out
 
 
