@@ -474,39 +474,83 @@ int payload_term(const uint8_t* p, size_t n, int tag, int vers, const uint8_t** 
     return LASPJ_DEC_OK;
 }
 
-// walk [{Elem, [{Tok, Bool}]}]; fn(elem image, tok image, flag) per token, and
-// on_elem(elem image, ntoks) per element; returns a LASPJ_DEC_* status
+// walk [{Elem, [{Tok, Bool}]}] in one pass (each byte read once, extents found as it
+// goes): on_elem(elem image) per element, on_tok(elem image, tok image, flag) per token;
+// *used = the term's length.  Returns a LASPJ_DEC_* status: the first problem in stream
+// order (callers that need "not a term at all" to win re-check with term_len).
 template <class OnElem, class OnTok>
-int walk_orset(const uint8_t* t, size_t tn, OnElem on_elem, OnTok on_tok) {
-    if (t[0] == kNil) return LASPJ_DEC_OK;
-    if (t[0] != kList) return LASPJ_DEC_MALFORMED;
-    ListIt it(t, tn);
-    size_t el;
-    while (const uint8_t* e = it.next(&el)) {
-        if (e[0] != kSmallTuple || e[1] != 2) return LASPJ_DEC_MALFORMED;
-        const uint8_t* k = e + 2;
-        size_t kl = term_len(k, el - 2);
-        const uint8_t* v = k + kl;
-        size_t vl = el - 2 - kl;
-        if (v[0] == kNil) return LASPJ_DEC_UNREPRESENTABLE;     // an element without tokens
-        if (v[0] != kList) return LASPJ_DEC_MALFORMED;
-        ListIt ti(v, vl);
-        size_t tl;
-        int st = on_elem(k, kl);
-        if (st) return st;
-        while (const uint8_t* te = ti.next(&tl)) {
-            if (te[0] != kSmallTuple || te[1] != 2) return LASPJ_DEC_MALFORMED;
-            const uint8_t* tk = te + 2;
-            size_t tkl = term_len(tk, tl - 2);
-            const uint8_t* f = tk + tkl;
-            const int flag = bool_atom(f);
-            if (flag < 0) return LASPJ_DEC_MALFORMED;
-            if ((st = on_tok(k, kl, tk, tkl, flag == 1))) return st;
-        }
-        if (ti.tail() && ti.tail()[0] != kNil) return LASPJ_DEC_MALFORMED;
+int walk_orset(const uint8_t* t, size_t tn, size_t* used, OnElem on_elem, OnTok on_tok) {
+    if (tn < 1) return LASPJ_DEC_MALFORMED;
+    if (t[0] == kNil) {
+        *used = 1;
+        return LASPJ_DEC_OK;
     }
-    if (it.tail() && it.tail()[0] != kNil) return LASPJ_DEC_MALFORMED;
+    if (t[0] != kList || tn < 5) return LASPJ_DEC_MALFORMED;
+    const uint32_t cnt = be32(t + 1);
+    size_t off = 5;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        if (off + 2 > tn || t[off] != kSmallTuple || t[off + 1] != 2) return LASPJ_DEC_MALFORMED;
+        off += 2;
+        const uint8_t* k = t + off;
+        const size_t kl = term_len(k, tn - off);
+        if (!kl) return LASPJ_DEC_MALFORMED;
+        off += kl;
+        if (off >= tn) return LASPJ_DEC_MALFORMED;
+        if (t[off] == kNil) return LASPJ_DEC_UNREPRESENTABLE;      // an element without tokens
+        if (t[off] != kList || off + 5 > tn) return LASPJ_DEC_MALFORMED;
+        const uint32_t m = be32(t + off + 1);
+        off += 5;
+        if (int st = on_elem(k, kl)) return st;
+        for (uint32_t j = 0; j < m; ++j) {
+            if (off + 2 > tn || t[off] != kSmallTuple || t[off + 1] != 2)
+                return LASPJ_DEC_MALFORMED;
+            off += 2;
+            const uint8_t* tk = t + off;
+            const size_t tkl = term_len(tk, tn - off);
+            if (!tkl) return LASPJ_DEC_MALFORMED;
+            off += tkl;
+            const size_t fl = off < tn ? term_len(t + off, tn - off) : 0;
+            if (!fl) return LASPJ_DEC_MALFORMED;
+            const int flag = bool_atom(t + off);
+            off += fl;
+            if (flag < 0) return LASPJ_DEC_MALFORMED;
+            if (int st = on_tok(k, kl, tk, tkl, flag == 1)) return st;
+        }
+        if (off >= tn || t[off] != kNil) return LASPJ_DEC_MALFORMED;   // proper token list
+        off += 1;
+    }
+    if (off >= tn || t[off] != kNil) return LASPJ_DEC_MALFORMED;       // proper outer list
+    *used = off + 1;
     return LASPJ_DEC_OK;
+}
+
+// the payload's term for the one-pass walker: after an optional <<Tag, Vers>> prefix and
+// the version byte 131 (its extent is checked by the walk)
+int payload_start(const uint8_t* p, size_t n, int tag, const uint8_t** t, size_t* tn) {
+    if (tag >= 0) {
+        if (n < 2 || p[0] != (uint8_t)tag) return LASPJ_DEC_INVALID_BINARY;
+        p += 2;
+        n -= 2;
+    }
+    if (n < 2 || p[0] != 131) return LASPJ_DEC_MALFORMED;
+    *t = p + 1;
+    *tn = n - 1;
+    return LASPJ_DEC_OK;
+}
+
+// an OR-Set payload walked once; a term that is not well-formed ETF reports MALFORMED
+// even when an earlier element already failed for another reason (binary_to_term/1
+// rejects the whole payload first)
+template <class OnElem, class OnTok>
+int walk_orset_payload(const uint8_t* p, size_t n, int tag, OnElem on_elem, OnTok on_tok) {
+    const uint8_t* t;
+    size_t tn, used = 0;
+    int st = payload_start(p, n, tag, &t, &tn);
+    if (st) return st;
+    st = walk_orset(t, tn, &used, on_elem, on_tok);
+    if (st == LASPJ_DEC_OK) return used == tn ? LASPJ_DEC_OK : LASPJ_DEC_MALFORMED;
+    if (st != LASPJ_DEC_MALFORMED && term_len(t, tn) != tn) return LASPJ_DEC_MALFORMED;
+    return st;
 }
 
 template <class OnElem>
@@ -608,24 +652,26 @@ int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const ui
     try {
         for (uint64_t i = 0; i < n; ++i) {
             if (offsets[i + 1] < offsets[i]) return LASPJ_E_INVAL;
-            const uint8_t* t;
-            size_t tn;
-            int st = payload_term(blob + offsets[i], offsets[i + 1] - offsets[i], tag, -1, &t, &tn);
-            if (st == LASPJ_DEC_OK) {
-                if (kind == LASPJ_KIND_ORSET) {
-                    uint32_t cur = 0;
-                    st = walk_orset(
-                        t, tn, [&](const uint8_t* k, size_t kl) { return reg_elem(d, k, kl, &cur); },
-                        [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl, bool) {
-                            uint8_t s;
-                            return reg_tok(d, cur, tk, tkl, &s);
-                        });
-                } else {
+            const uint8_t* pp = blob + offsets[i];
+            const size_t pn = offsets[i + 1] - offsets[i];
+            int st;
+            if (kind == LASPJ_KIND_ORSET) {
+                uint32_t cur = 0;
+                st = walk_orset_payload(
+                    pp, pn, tag, [&](const uint8_t* k, size_t kl) { return reg_elem(d, k, kl, &cur); },
+                    [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl, bool) {
+                        uint8_t s;
+                        return reg_tok(d, cur, tk, tkl, &s);
+                    });
+            } else {
+                const uint8_t* t;
+                size_t tn;
+                st = payload_term(pp, pn, tag, -1, &t, &tn);
+                if (st == LASPJ_DEC_OK)
                     st = walk_gset(t, tn, [&](const uint8_t* e, size_t el) {
                         uint32_t s;
                         return reg_elem(d, e, el, &s);
                     });
-                }
             }
             status[i] = st;
         }
@@ -717,48 +763,58 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
         for (uint64_t i = 0; i < n; ++i) {
             uint64_t* cells = out + i * wpr;
             memset(cells, 0, wpr * 8);
-            const uint8_t* t;
-            size_t tn;
-            int st = payload_term(blob + offsets[i], offsets[i + 1] - offsets[i], tag, -1, &t, &tn);
-            if (st == LASPJ_DEC_OK) {
-                // keys must ascend strictly (an orddict / ordset), tokens likewise
-                std::string_view prev_e, prev_t;
+            const uint8_t* pp = blob + offsets[i];
+            const size_t pn = offsets[i + 1] - offsets[i];
+            int st;
+            // keys must ascend strictly (an orddict / ordset), tokens likewise
+            std::string_view prev_e, prev_t;
+            bool have_e = false, have_t = false;
+            uint32_t cur = 0;
+            if (kind == LASPJ_KIND_ORSET) {
+                st = walk_orset_payload(
+                    pp, pn, tag,
+                    [&](const uint8_t* k, size_t kl) -> int {
+                        // k points into the payload: the view stays valid
+                        std::string_view key((const char*)k, kl);
+                        const int64_t f = d.elem(k, kl);
+                        if (f < 0 || f >= (int64_t)E) return LASPJ_DEC_UNKNOWN_TERM;
+                        if (have_e && cmp_view(prev_e, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
+                        prev_e = key;
+                        have_e = true;
+                        have_t = false;
+                        cur = (uint32_t)f;
+                        return LASPJ_DEC_OK;
+                    },
+                    [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl, bool flag) -> int {
+                        std::string_view key((const char*)tk, tkl);
+                        const int f = d.tok(cur, tk, tkl);
+                        if (f < 0) return LASPJ_DEC_UNKNOWN_TERM;
+                        if (have_t && cmp_view(prev_t, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
+                        prev_t = key;
+                        have_t = true;
+                        cells[2ull * cur] |= 1ull << f;
+                        if (flag) cells[2ull * cur + 1] |= 1ull << f;
+                        return LASPJ_DEC_OK;
+                    });
+            } else {
+                const uint8_t* t;
+                size_t tn;
                 std::string prev_buf;
-                bool have_e = false, have_t = false;
-                uint32_t cur = 0;
-                auto on_elem = [&](const uint8_t* k, size_t kl) -> int {
-                    std::string_view key((const char*)k, kl);
-                    const int64_t f = d.elem(k, kl);
-                    if (f < 0 || f >= (int64_t)E) return LASPJ_DEC_UNKNOWN_TERM;
-                    if (have_e && cmp_view(prev_e, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
-                    // a STRING_EXT element's image lives in the iterator's scratch: copy it
-                    // (the buffer keeps its capacity, so this does not allocate per element)
-                    prev_buf.assign(key.data(), key.size());
-                    prev_e = prev_buf;
-                    have_e = true;
-                    have_t = false;
-                    cur = (uint32_t)f;
-                    if (kind == LASPJ_KIND_GSET) cells[cur >> 6] |= 1ull << (cur & 63);
-                    return LASPJ_DEC_OK;
-                };
-                if (kind == LASPJ_KIND_ORSET) {
-                    st = walk_orset(t, tn, on_elem,
-                                    [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl,
-                                        bool flag) -> int {
-                                        std::string_view key((const char*)tk, tkl);
-                                        const int f = d.tok(cur, tk, tkl);
-                                        if (f < 0) return LASPJ_DEC_UNKNOWN_TERM;
-                                        if (have_t && cmp_view(prev_t, key) >= 0)
-                                            return LASPJ_DEC_UNKNOWN_TERM;
-                                        prev_t = key;
-                                        have_t = true;
-                                        cells[2ull * cur] |= 1ull << f;
-                                        if (flag) cells[2ull * cur + 1] |= 1ull << f;
-                                        return LASPJ_DEC_OK;
-                                    });
-                } else {
-                    st = walk_gset(t, tn, on_elem);
-                }
+                st = payload_term(pp, pn, tag, -1, &t, &tn);
+                if (st == LASPJ_DEC_OK)
+                    st = walk_gset(t, tn, [&](const uint8_t* k, size_t kl) -> int {
+                        std::string_view key((const char*)k, kl);
+                        const int64_t f = d.elem(k, kl);
+                        if (f < 0 || f >= (int64_t)E) return LASPJ_DEC_UNKNOWN_TERM;
+                        if (have_e && cmp_view(prev_e, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
+                        // a STRING_EXT element's image lives in the iterator's scratch: copy
+                        // it (the buffer keeps its capacity, so this does not allocate)
+                        prev_buf.assign(key.data(), key.size());
+                        prev_e = prev_buf;
+                        have_e = true;
+                        cells[f >> 6] |= 1ull << (f & 63);
+                        return LASPJ_DEC_OK;
+                    });
             }
             if (st != LASPJ_DEC_OK) memset(cells, 0, wpr * 8);
             status[i] = st;
