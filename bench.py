@@ -188,11 +188,19 @@ def cpu_baseline(elements: int, budget: float):
     cores = host_cores()
     eps, merges, secs = orc.bench_orset_merge(elements, 2, cores, 2, budget)
     m, u, f, v, infl = orc.bench_config1_ext(10_000, 200, 5)
+    # a second column: the device's own cell layout OR-ed on the same cores (bounded by
+    # host DRAM bandwidth, not by the orddict walk)
+    per_thread = 1 << 22                 # 4M cells = 64 MiB per array per thread
+    col = orc.bench_cells_join(per_thread, cores, min(3.0, budget / 4))
     return {
         "value": eps, "unit": "merged elements/s", "cores": cores, "kind": "port",
         "sample": (f"C restatement of lasp_orset:merge/2 (nested orddict two-finger merge, "
                    f"20-byte tokens) on {cores} threads x 2 synthetic replica pairs "
                    f"(E={elements}, T<=64), {merges} merges in {secs:.1f} s"),
+        "columnar": {"value": col, "unit": "merged elements/s", "cores": cores,
+                     "sample": (f"the GPU's {{p, r}} cell layout joined d = a | b on {cores} "
+                                f"threads, {per_thread} cells (3 x 64 MiB) per thread, "
+                                f"~{min(3.0, budget / 4):.0f} s")},
         "config1": {"workload": "2 replicas x 10k elements (BASELINE configs[0]), 1 thread",
                     "us_merge": m, "us_union": u, "us_filter": f, "us_value": v,
                     "us_inflation": infl},

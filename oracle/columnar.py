@@ -242,3 +242,14 @@ def bench_config1_ext(n: int = 10_000, iters: int = 200, slow_iters: int = 5):
     if lib().orc_bench_config1_ext(n, iters, slow_iters, out) != 0:
         raise RuntimeError("orc_bench_config1_ext failed")
     return tuple(out)
+
+
+def bench_cells_join(cells_per_thread: int, threads: int, budget_s: float) -> float:
+    """The device's cell layout joined (d = a | b) on host threads: cells per second
+    (a second CPU column for the headline; the reference's algorithm is bench_orset_merge)."""
+    out = C.c_double()
+    f = lib().orc_bench_cells_join
+    f.argtypes = [C.c_uint64, C.c_int, C.c_double, C.POINTER(C.c_double)]
+    if f(cells_per_thread, threads, budget_s, C.byref(out)) != 0:
+        raise RuntimeError("orc_bench_cells_join failed")
+    return out.value

@@ -629,3 +629,68 @@ int orc_bench_orset_merge(uint32_t E, u64 seed, int threads, uint32_t pairs, dou
     return orc_bench_orset_op(ORC_OP_MERGE, E, seed, threads, pairs, budget_s, elem_per_s,
                               merges_out, seconds_out);
 }
+
+/* ---- the columnar join on the host: the device's cell layout OR-ed on CPU threads ----
+ * Not the reference's algorithm (that is orc_orset_merge above): a second CPU column
+ * for the headline, the same {p, r} cells the GPU joins, d = a | b over replicas of E
+ * slots, each thread owning its own arrays (cells_per_thread u64x2 each, larger than
+ * the caches), timed for ~budget_s.  Returns joined cells (element slots) per second. */
+typedef struct {
+    uint64_t n;          /* u64 words per array */
+    double budget_s;
+    uint64_t passes;
+    double seconds;
+    int err;
+} cells_arg;
+
+static void* cells_thread(void* p) {
+    cells_arg* a = (cells_arg*)p;
+    u64* x = (u64*)malloc(a->n * 8);
+    u64* y = (u64*)malloc(a->n * 8);
+    u64* z = (u64*)malloc(a->n * 8);
+    if (!x || !y || !z) {
+        a->err = 1;
+        free(x); free(y); free(z);
+        return NULL;
+    }
+    for (uint64_t i = 0; i < a->n; ++i) {
+        x[i] = sm64(i);
+        y[i] = sm64(i ^ 0x5A5A5A5AULL);
+        z[i] = 0;
+    }
+    double t0 = now_s(), t = t0;
+    uint64_t passes = 0;
+    while (t - t0 < a->budget_s) {
+        for (uint64_t i = 0; i < a->n; ++i) z[i] = x[i] | y[i];
+        ++passes;
+        t = now_s();
+    }
+    a->passes = passes;
+    a->seconds = t - t0;
+    free(x); free(y); free(z);
+    return NULL;
+}
+
+int orc_bench_cells_join(uint64_t cells_per_thread, int threads, double budget_s,
+                         double* cells_per_s) {
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    cells_arg* args = (cells_arg*)calloc((size_t)threads, sizeof(cells_arg));
+    if (!th || !args) return -1;
+    for (int i = 0; i < threads; ++i) {
+        args[i] = (cells_arg){2 * cells_per_thread, budget_s, 0, 0, 0};
+        pthread_create(&th[i], NULL, cells_thread, &args[i]);
+    }
+    double cells = 0, secs = 0;
+    int err = 0;
+    for (int i = 0; i < threads; ++i) {
+        pthread_join(th[i], NULL);
+        cells += (double)args[i].passes * (double)cells_per_thread;
+        if (args[i].seconds > secs) secs = args[i].seconds;
+        err |= args[i].err;
+    }
+    free(th);
+    free(args);
+    if (err || secs <= 0) return -1;
+    *cells_per_s = cells / secs;
+    return 0;
+}
