@@ -308,6 +308,14 @@ int laspj_orset_product_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uin
                                           uint32_t er, laspj_batch** out);
 int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                         const laspj_batch* r);
+/* product followed by filter(fun({X, Y}) -> X =:= Y) (lasp_core.erl:499-533 then
+ * :681-712; BASELINE config 5's fused variant), over ONE element dictionary shared by l
+ * and r (slot e is the same term on both sides, so X =:= Y iff the slots agree): dst is
+ * a PRODUCT batch with EL = E and ER = 1 whose cell (e, 0) is the product cell of l[e]
+ * and r[e] ({{X, X}, orset_causal_product(Cx, Cy)}, kept tombstoned like any filter
+ * output), 0 when e is absent on either side.  Token slots must be < 8 (LASPJ_E_RANGE). */
+int laspj_orset_product_diag(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                             const laspj_batch* r);
 /* map / fold bodies — lasp_core.erl:641-667, :460-486: output slot o takes the cell of
  * input slot index[o] (uint32 per dst slot; 0xFFFFFFFF = empty).  The host builds the
  * index from F over the element dictionary (a map is one slot per input slot, a fold

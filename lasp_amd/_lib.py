@@ -125,6 +125,7 @@ SIGNATURES = {
     "laspj_orset_intersection": (i, [vp, vp, vp, vp]),
     "laspj_orset_product_batch_create": (i, [vp, u64, u32, u32, vpp]),
     "laspj_orset_product": (i, [vp, vp, vp, vp]),
+    "laspj_orset_product_diag": (i, [vp, vp, vp, vp]),
     "laspj_orset_product_wide_batch_create": (i, [vp, u64, u32, u32, vpp]),
     "laspj_orset_gather": (i, [vp, vp, vp, vp]),
     "laspj_gset_union": (i, [vp, vp, vp, vp]),

@@ -283,6 +283,28 @@ def decode_product(dl: Domain, dr: Domain, cells: np.ndarray) -> list:
     return out
 
 
+def decode_product_diag(dom: Domain, cells: np.ndarray) -> list:
+    """laspj_orset_product_diag cells (E, 1) uint32 over one dictionary -> the list
+    filter(fun({X, Y}) -> X =:= Y) leaves of the product body: {{X, X}, causal product}
+    in X order (the product's X-major order restricted to its diagonal)."""
+    out = []
+    for x in dom.elements.order():
+        x = int(x)
+        if x >= cells.shape[0]:
+            continue
+        c = int(cells[x, 0])
+        if not c:
+            continue
+        px, rx, py, ry = c & 0xFF, (c >> 8) & 0xFF, (c >> 16) & 0xFF, (c >> 24) & 0xFF
+        td = dom.tokens[x]
+        tx = [(td.terms[k], bool((rx >> int(k)) & 1)) for k in td.order() if (px >> int(k)) & 1]
+        ty = [(td.terms[k], bool((ry >> int(k)) & 1)) for k in td.order() if (py >> int(k)) & 1]
+        toks = [([a, b], da or db) for a, da in reversed(tx) for b, db in reversed(ty)]
+        xt = dom.elements.terms[x]
+        out.append(((xt, xt), toks))
+    return out
+
+
 def decode_gset_product(dl: Domain, dr: Domain, rows: np.ndarray) -> list:
     """G-Set product rows (EL, ceil(ER/64)) -> [{X, Y}] X-major (lasp_core.erl:518-520)."""
     out = []

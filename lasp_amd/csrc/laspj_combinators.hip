@@ -173,6 +173,45 @@ __global__ __launch_bounds__(kB) void k_orset_product_wide(u64x2* out, const u64
     }
 }
 
+// product followed by filter(fun({X, Y}) -> X =:= Y), fused (BASELINE config 5's
+// variant): over one element dictionary the pairs that pass are the slots present on
+// both sides, so cell e of the output (an EL = E, ER = 1 PRODUCT batch) is the product
+// cell of l[e] and r[e] — 32 B read and 4 B written per slot instead of EL x ER cells.
+// Grid-stride with 4 slots per lane a stride apart (each load instruction is 1 KiB of
+// consecutive cells, each store 256 B).
+__global__ __launch_bounds__(kB) void k_orset_product_diag(uint32_t* out, const u64x2* L,
+                                                           const u64x2* R, uint64_t n,
+                                                           uint32_t* flag) {
+    const uint64_t stride = (uint64_t)gridDim.x * kB;
+    uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        u64x2 a[4], b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = ldnt(L + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = ldnt(R + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = pack8(a[k], flag), y = pack8(b[k], flag) << 16;
+            __builtin_nontemporal_store((x && y) ? x | y : 0u, out + i + k * stride);
+        }
+    }
+    for (; i < n; i += stride) {
+        const uint32_t x = pack8(ldnt(L + i), flag), y = pack8(ldnt(R + i), flag) << 16;
+        out[i] = (x && y) ? x | y : 0u;
+    }
+}
+
+hipError_t launch_orset_product_diag(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                     const laspj_batch* r, uint32_t* flag) {
+    const uint64_t n = l->replicas * l->elements;
+    hipLaunchKernelGGL(k_orset_product_diag, dim3(grid_for(ctx, n)), dim3(kB), 0,
+                       ctx->stream, reinterpret_cast<uint32_t*>(dst->dev),
+                       reinterpret_cast<const u64x2*>(l->dev),
+                       reinterpret_cast<const u64x2*>(r->dev), n, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                 const laspj_batch* r, uint32_t* flag) {
     if (dst->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE) {

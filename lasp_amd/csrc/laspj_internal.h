@@ -145,6 +145,8 @@ hipError_t launch_orset_intersection(laspj_ctx* ctx, laspj_batch* dst, const las
                                      const laspj_batch* r);
 hipError_t launch_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                                 const laspj_batch* r, uint32_t* flag);
+hipError_t launch_orset_product_diag(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                     const laspj_batch* r, uint32_t* flag);
 hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                const uint32_t* index);
 hipError_t launch_and(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,

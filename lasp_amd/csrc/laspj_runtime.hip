@@ -856,6 +856,30 @@ int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
     return LASPJ_OK;
 }
 
+int laspj_orset_product_diag(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                             const laspj_batch* r) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, l) || !same_ctx(ctx, r))
+        return fail(ctx, LASPJ_E_INVAL, "orset_product_diag: bad batch");
+    if (l->kind != LASPJ_KIND_ORSET || r->kind != LASPJ_KIND_ORSET ||
+        dst->kind != LASPJ_KIND_ORSET_PRODUCT)
+        return fail(ctx, LASPJ_E_KIND,
+                    "orset_product_diag: OR-Set inputs and a PRODUCT (4-byte cell) output");
+    if (l->replicas != r->replicas || l->elements != r->elements ||
+        dst->replicas != l->replicas || dst->elements != l->elements || dst->elements_r != 1)
+        return fail(ctx, LASPJ_E_SHAPE,
+                    "orset_product_diag: inputs of one shape, output EL = E and ER = 1");
+    Guard g(ctx);
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
+    LJ_HIP(ctx, laspj::launch_orset_product_diag(ctx, dst, l, r, ctx->flag));
+    uint32_t flag = 0;
+    LJ_HIP(ctx, hipMemcpyAsync(&flag, ctx->flag, 4, hipMemcpyDeviceToHost, ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (flag)
+        return fail(ctx, LASPJ_E_RANGE,
+                    "orset_product_diag: an input element uses token slot >= 8 (4-byte cells)");
+    return LASPJ_OK;
+}
+
 int laspj_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                        const laspj_buf* index) {
     if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))

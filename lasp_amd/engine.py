@@ -428,6 +428,15 @@ class ORSetBatch(_Batch):
         check(self.ctx.L.laspj_orset_product(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
         return out
 
+    def product_diag(self, r: "ORSetBatch", out=None) -> "ORSetProductBatch":
+        """product then filter({X, Y} -> X =:= Y), fused (laspj_orset_product_diag): an
+        EL = E, ER = 1 PRODUCT batch whose cell (e, 0) pairs slot e of both sides (one
+        element dictionary shared by self and r)."""
+        if out is None:
+            out = ORSetProductBatch(self.ctx, self.replicas, self.elements, 1)
+        check(self.ctx.L.laspj_orset_product_diag(self.ctx.h, out.h, self.h, r.h), self.ctx.h)
+        return out
+
     # a gather whose output is threshold-checked in the same pass (config 4 fused)
     def gather_inflation(self, src: "ORSetBatch", index, prev: "ORSetBatch",
                          strict: bool = True) -> np.ndarray:

@@ -836,3 +836,48 @@ def test_concurrent_callers_one_context(ctx):
         th.join(timeout=120)
     assert not any(th.is_alive() for th in threads)
     assert not errors, errors[:5]
+
+
+def test_orset_product_diag_matches_product_then_filter(ctx):
+    """laspj_orset_product_diag = the product body followed by the filter body with
+    fun({X, Y}) -> X =:= Y (lasp_core.erl:499-533, 681-712) on the oracle: random
+    OR-Sets over one dictionary (<= 3 token slots per element, tombstones kept), several
+    replica pairs; the host decode of each replica's diagonal equals the oracle list."""
+    import random
+    from lasp_amd.codec import Domain, decode_product_diag
+    from lasp_amd.terms import Atom
+    from oracle import core, orset
+    rng = random.Random(91)
+    elems = list(range(0, 60, 3)) + [Atom("a"), Atom("zz"), 1 << 40]
+    pool = {i: [bytes([i % 251, k]) * 10 for k in range(3)] for i in range(len(elems))}
+
+    def rand_set(seed):
+        toks = iter([t for i in range(len(elems)) for t in pool[i]])
+        s = orset.new()
+        for i in rng.sample(range(len(elems)), rng.randint(0, len(elems))):
+            for t in rng.sample(pool[i], rng.randint(1, 3)):
+                s = orset.update(("add_by_token", t, elems[i]), None, s)[1]
+            if rng.random() < 0.3:
+                s = orset.update(("remove", elems[i]), None, s)[1]
+        return s
+    pairs = [(rand_set(2 * k), rand_set(2 * k + 1)) for k in range(6)]
+    dom = Domain()
+    for a, b in pairs:
+        dom.register_orset(a)
+        dom.register_orset(b)
+    E = dom.size + 3
+    L, Rb = ctx.orset_batch(len(pairs), E), ctx.orset_batch(len(pairs), E)
+    L.upload(dom.encode_orset([a for a, _ in pairs], E))
+    Rb.upload(dom.encode_orset([b for _, b in pairs], E))
+    D = L.product_diag(Rb)
+    cells = D.download().reshape(len(pairs), E, 1)
+    same = lambda xy: xy[0] == xy[1] and type(xy[0]) is type(xy[1])   # noqa: E731  (=:=)
+    for k, (a, b) in enumerate(pairs):
+        want = core.filter_body("lasp_orset", same, core.product_body("lasp_orset", a, b))
+        assert decode_product_diag(dom, cells[k]) == want, k
+    # shape / kind checks
+    from lasp_amd import LaspjError
+    from lasp_amd._lib import E_SHAPE
+    with pytest.raises(LaspjError) as ei:
+        L.product_diag(ctx.orset_batch(len(pairs), E + 1))
+    assert ei.value.status == E_SHAPE

@@ -275,7 +275,14 @@ def config5(ctx, steps):
     report("config5_intersection", timed(ctx, lambda: _lib.check(
         L.laspj_orset_intersection(ctx.h, x.h, l.h, r.h), ctx.h), steps),
         64 * P * E, P * E, "slots_per_s", pairs=P, slots=E)
-    del x, l, r
+    del x
+    # the fused product + filter({X, Y} -> X =:= Y) variant over the same pairs: 32 B
+    # read + 4 B written per slot instead of 1e10 product cells per pair
+    dg = engine.ORSetProductBatch(ctx, P, E, 1)
+    report("config5_product_diag", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_product_diag(ctx.h, dg.h, l.h, r.h), ctx.h), steps),
+        36 * P * E, P * E, "slots_per_s", pairs=P, slots=E)
+    del dg, l, r
     # product: 100k x 100k, T = 3 token slots
     n = 100_000
     pl, pr = ctx.orset_batch(1, n), ctx.orset_batch(1, n)
