@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--knob", type=int, default=0)
     ap.add_argument("--only", default="t64,t3")
+    ap.add_argument("--op", default="read", choices=["read", "write"])
     a = ap.parse_args()
     ctx = context()
     L = ctx.L
@@ -52,8 +53,23 @@ def main():
         _lib.check(L.laspj_orset_etf_write(ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h)
         back = ctx.orset_batch(R, E)
         stb = ctx.buffer(4 * R)
-        ctx.set_tuning(_lib.TUNE_ETF_READ, a.knob)
         ev0, ev1 = ctx.event(), ctx.event()
+        if a.op == "write":
+            ctx.set_tuning(_lib.TUNE_ETF_KERNEL, a.knob)
+            for _ in range(a.reps):
+                ev0.record()
+                _lib.check(L.laspj_orset_etf_write(ctx.h, b.h, d.h, 76, 1, offs.h, out.h), ctx.h)
+                ev1.record()
+                ctx.synchronize()
+            ctx.set_tuning(_lib.TUNE_ETF_KERNEL, 0)
+            _lib.check(L.laspj_orset_etf_read(ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h),
+                       ctx.h)
+            ok = np.array_equal(back.download(), b.download())
+            print(f"{tag} write knob={a.knob} ms={ev0.elapsed_ms(ev1):.3f} payload={total.value} "
+                  f"ok={ok}", flush=True)
+            del back, stb, out, offs, d, b
+            continue
+        ctx.set_tuning(_lib.TUNE_ETF_READ, a.knob)
         for _ in range(a.reps):
             ev0.record()
             _lib.check(L.laspj_orset_etf_read(ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h),

@@ -6,11 +6,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ONLY=${ONLY:-t64}
+OP=${OP:-read}
 i=0
 for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/read_pmc$i -o run -- \
-      python3 tools/etf_read_probe.py --only $ONLY --reps 1 > gpurun_out/read_pmc$i.log 2>&1 || exit $?
+      python3 tools/etf_read_probe.py --only $ONLY --op $OP --reps 1 > gpurun_out/read_pmc$i.log 2>&1 || exit $?
 done
 echo read profile ok
