@@ -34,6 +34,26 @@ def value(s):
     return list(s)
 
 
+def value2(_query, s):
+    """value/2 — lasp_gset.erl:78-81: not implemented in the reference, same as value/1."""
+    return value(s)
+
+
+def update4(op, actor, s, _ctx=None):
+    """update/4 — lasp_gset.erl:90-93 (context ignored)."""
+    return update(op, actor, s)
+
+
+def parent_clock(_clock, s):
+    """parent_clock/2 — lasp_gset.erl:95-97 (identity)."""
+    return s
+
+
+def to_version(_version, s):
+    """to_version/2 — lasp_gset.erl:144-146 (identity)."""
+    return s
+
+
 def update(op, _actor, s):
     """update/3 — lasp_gset.erl:84-88: {add, E} | {add_all, Es} (device set-bit ops)."""
     dom = Domain()

@@ -126,6 +126,16 @@ def update4(op, actor, s, _ctx=None):
     return update(op, actor, s)
 
 
+def parent_clock(_clock, s):
+    """parent_clock/2 — lasp_orset.erl:124-126 (identity)."""
+    return s
+
+
+def to_version(_version, s):
+    """to_version/2 — lasp_orset.erl:216-218 (identity)."""
+    return s
+
+
 def _unique(_actor) -> bytes:
     """unique/1 — lasp_orset.erl:261-262: 20 random bytes."""
     return os.urandom(20)
