@@ -153,6 +153,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         5 = always split (sized segments), 6 = element
                                         batches walked by the scalar unit (the lanes
                                         find element starts by default)                 */
+#define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
+                                        the launch (see LASPJ_TUNE_ETF_READ), else split
+                                        every payload longer than this (>= 256, a
+                                        multiple of 256)                               */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

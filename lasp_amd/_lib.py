@@ -36,6 +36,7 @@ TUNE_REDUCE_KERNEL = 5
 TUNE_PRODUCT_ROWS = 6
 TUNE_PRODUCT_COLS = 7
 TUNE_ETF_READ = 8
+TUNE_ETF_SEG = 9
 
 
 class LaspjUnavailable(RuntimeError):

@@ -2514,7 +2514,9 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         for (uint64_t i = 0; i < R; ++i) longest = std::max<uint64_t>(longest, off[i + 1] - off[i]);
         S = std::max<uint64_t>(2048, ((bytes_in / want) + 255) & ~255ull);
         if (ctx->tune_etf_read == 4) S = 256;
-        const bool split = ctx->tune_etf_read >= 4 || R < (uint64_t)ctx->cus * 8;
+        if (ctx->tune_etf_seg) S = (uint64_t)ctx->tune_etf_seg;
+        const bool split = ctx->tune_etf_read >= 4 || ctx->tune_etf_seg ||
+                           R < (uint64_t)ctx->cus * 8;
         if (longest < (1ull << 31) && split && longest > S) {
             for (uint64_t i = 0; i < R; ++i)
                 nseg += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);

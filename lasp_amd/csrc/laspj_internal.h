@@ -22,6 +22,7 @@ struct laspj_ctx {
     int64_t tune_nt = -1;
     int64_t tune_etf = 0;
     int64_t tune_etf_read = 0;
+    int64_t tune_etf_seg = 0;
     int64_t tune_reduce = 0;
     int64_t tune_product_rows = 0;
     int64_t tune_product_cols = 0;

@@ -248,6 +248,12 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
                 return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..6");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_ETF_SEG:
+            if (value < 0 || value > (1ll << 30) || (value % 256) != 0)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf segment bytes must be 0 or a "
+                            "multiple of 256");
+            ctx->tune_etf_seg = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

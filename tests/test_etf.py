@@ -392,13 +392,18 @@ def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
     <= 8 token slots), 1 = serial scan, 2 = batched records only, 4 = every payload
     longer than 256 bytes split between waves (segment mode: header search, chain
-    check, redo of failed replicas)."""
+    check, redo of failed replicas); "seg512": the default kernels with every payload
+    longer than 512 bytes split (LASPJ_TUNE_ETF_SEG)."""
     from lasp_amd import _lib
-    ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
+    if knob == "seg512":
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 512)
+    else:
+        ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
     try:
         yield
     finally:
         ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 0)
 
 
 def _decode_setup(states, rng_seed=0):
@@ -427,7 +432,7 @@ def _upload_payloads(ctx, blobs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 4])
+@pytest.mark.parametrize("knob", [0, 1, 4, "seg512"])
 @pytest.mark.parametrize("tagged", [False, True])
 def test_gpu_from_binary_round_trip(tagged, knob):
     """Device from_binary/1 of oracle payloads (term_to_binary of random orddicts with
@@ -457,7 +462,7 @@ def test_gpu_from_binary_round_trip(tagged, knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6, "seg512"])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
@@ -611,7 +616,7 @@ def _small_orsets(rng, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6, "seg512"])
 def test_gpu_from_binary_small_tokens_round_trip(knob):
     """Elements with <= 3 token slots (element batches under knob 0): oracle payloads
     with every flag atom form decode to the host encoder's cells, and device to_binary ->

@@ -5,6 +5,8 @@ pairs — the values lasp_core's combinator bodies bind and then merge on every 
 lasp_lattice.erl:137-161, 212-253, 277-312).  Each case encodes the oracle's list,
 runs one entry point, decodes and compares as terms (exact_eq)."""
 
+import os
+
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
 
@@ -18,7 +20,7 @@ KEY = st.integers(min_value=-3, max_value=9)
 ENTRY = st.tuples(KEY, st.lists(st.tuples(TOK, st.booleans()), max_size=5))
 OLIST = st.lists(ENTRY, max_size=10)
 GLIST = st.lists(KEY, max_size=12)
-SETTINGS = settings(max_examples=60, deadline=None,
+SETTINGS = settings(max_examples=60 * int(os.environ.get("LASPJ_SOAK", "1")), deadline=None,
                     suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 
 

@@ -3,6 +3,8 @@ the one-variable kernels, and the Store's batched bind path (bind_many, the batc
 {strict, Last} re-checks of the process loop) against sequential binds on the oracle
 store (lasp_core.erl:291-312, lasp_process.erl:61-95)."""
 
+import os
+
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
@@ -75,7 +77,7 @@ def test_inflation_many_matches_single_kernels(ctx):
 SET = st.lists(st.tuples(st.sampled_from(["add", "remove"]), st.integers(0, 9)), max_size=10)
 
 
-@settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=20 * int(os.environ.get("LASPJ_SOAK", "1")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(st.tuples(st.integers(0, 3), SET), min_size=1, max_size=6))
 def test_store_bind_many_vs_sequential_oracle(batch):
     """Store.bind_many ends where the oracle ends when it applies the same binds with the

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--knob", type=int, default=0)
     ap.add_argument("--only", default="t64,t3")
     ap.add_argument("--op", default="read", choices=["read", "write"])
+    ap.add_argument("--seg", default="0", help="comma list of LASPJ_TUNE_ETF_SEG values")
     a = ap.parse_args()
     ctx = context()
     L = ctx.L
@@ -70,16 +71,19 @@ def main():
             del back, stb, out, offs, d, b
             continue
         ctx.set_tuning(_lib.TUNE_ETF_READ, a.knob)
-        for _ in range(a.reps):
-            ev0.record()
-            _lib.check(L.laspj_orset_etf_read(ctx.h, back.h, d.h, 76, 1, out.h, offs.h, stb.h),
-                       ctx.h)
-            ev1.record()
-            ctx.synchronize()
-        ok = np.array_equal(back.download(), b.download())
-        print(f"{tag} knob={a.knob} ms={ev0.elapsed_ms(ev1):.3f} payload={total.value} ok={ok}",
-              flush=True)
+        for seg in [int(x) for x in a.seg.split(",")]:
+            ctx.set_tuning(_lib.TUNE_ETF_SEG, seg)
+            for _ in range(a.reps):
+                ev0.record()
+                _lib.check(L.laspj_orset_etf_read(ctx.h, back.h, d.h, 76, 1, out.h, offs.h,
+                                                  stb.h), ctx.h)
+                ev1.record()
+                ctx.synchronize()
+            ok = np.array_equal(back.download(), b.download())
+            print(f"{tag} knob={a.knob} seg={seg} ms={ev0.elapsed_ms(ev1):.3f} "
+                  f"payload={total.value} ok={ok}", flush=True)
         ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 0)
         del back, stb, out, offs, d, b
 
 
