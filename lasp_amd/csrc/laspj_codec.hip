@@ -1595,6 +1595,11 @@ __device__ __forceinline__ Cases lane_cases(uint32_t lane) {
 __device__ __forceinline__ uint32_t find_marks(const PWin& w, uint32_t x0, uint32_t span,
                                                uint32_t first, ReadLds& L, uint32_t lane) {
     const uint32_t a0 = x0 & ~3u;
+    // a lane's mask holds 64 positions: at most K = 60 bytes per lane, i.e. 3840 bytes
+    // from a0 (marks past that are not reported; callers treat a missing mark as "not
+    // validated").  Without the clamp a fresh 4 KiB window gave K = 68 and every lane's
+    // last 4 positions wrapped into its first 4: batches stopped at the first mark there.
+    span = min(span, 3840u - (x0 - a0));
     uint32_t K = (((span + (x0 - a0) + 63u) >> 6) + 3u) & ~3u;
     if (!(K & 4u)) K += 4u;
     const uint32_t b0 = a0 + lane * K;                                   // this lane's first
