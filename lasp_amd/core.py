@@ -196,43 +196,50 @@ class Store:
         return ("ok", (id_, v.type, value))
 
     def bind_many(self, pairs):
-        """Many binds as one device launch (laspj_batch_bind_many): every pair
+        """Many binds as few device launches (laspj_batch_bind_many): every pair
         (id, term) whose variable and value are canonical is encoded, then ONE kernel
         does `Value0 =:= Value` + merge + write for all of them and ONE status download
         says which variables were written (lasp_core.erl:291-312 for each); other pairs
-        bind one by one.  The writes land first and the dataflow then runs once over all
-        of them — one of the interleavings the reference's asynchronous processes allow
-        (its lasp_process readers race with binds).  Schedules are observable (the
-        union body keeps the left side's tokens, and re-runs merge into the output), so
-        this is that interleaving, not the one-bind-at-a-time one."""
-        pend, rest = [], []
-        for id_, term in pairs:
-            v = self.vars[id_]
-            if v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter") and \
-                    v.rep == "canonical" and not v.empty and id_ not in (p[0] for p in pend):
-                try:
-                    dv = self._encode(v.type, term, v.pairs)
-                except (NonCanonical, CapacityError, ValueError, TypeError):
-                    continue                     # merge would throw: bind swallows it
-                if dv.rep == "canonical":
-                    pend.append((id_, v, dv))
-                    continue
-            rest.append((id_, term))
-        if pend:
-            dsts = [_new_like(self.ctx, v.val) for _i, v, _d in pend]
-            st = self.ctx.bind_many(dsts, [v.val for _i, v, _d in pend],
-                                    [d.batch for _i, _v, d in pend])
-            self._depth += 1                      # one propagation after all writes
-            try:
-                for (id_, v, _d), dst, s_ in zip(pend, dsts, st):
-                    if s_:
-                        v.val = dst
-                        self._written(id_, v)
-            finally:
-                self._depth -= 1
-            self._propagate()
-        for id_, term in rest:
-            self.bind(id_, term)
+        bind one by one.  A variable named more than once takes its pairs in order, one
+        per launch.  Every write lands first and the dataflow then runs once over all of
+        them — one of the interleavings the reference's asynchronous processes allow
+        (its lasp_process readers race with binds).  Schedules are observable (the union
+        body keeps the left side's tokens, and re-runs merge into the output), so this is
+        that interleaving: the binds in pair order with propagation deferred to the end,
+        not the one-bind-at-a-time one."""
+        self._depth += 1                          # one propagation after all writes
+        try:
+            todo = list(pairs)
+            while todo:
+                pend, seen, later = [], set(), []
+                for id_, term in todo:
+                    if id_ in seen:               # this variable's next pair: next launch
+                        later.append((id_, term))
+                        continue
+                    seen.add(id_)
+                    v = self.vars[id_]
+                    if v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter") and \
+                            v.rep == "canonical" and not v.empty:
+                        try:
+                            dv = self._encode(v.type, term, v.pairs)
+                        except (NonCanonical, CapacityError, ValueError, TypeError):
+                            continue              # merge would throw: bind swallows it
+                        if dv.rep == "canonical":
+                            pend.append((id_, v, dv))
+                            continue
+                    self.bind(id_, term)          # written now, propagated at the end
+                if pend:
+                    dsts = [_new_like(self.ctx, v.val) for _i, v, _d in pend]
+                    st = self.ctx.bind_many(dsts, [v.val for _i, v, _d in pend],
+                                            [d.batch for _i, _v, d in pend])
+                    for (id_, v, _d), dst, s_ in zip(pend, dsts, st):
+                        if s_:
+                            v.val = dst
+                            self._written(id_, v)
+                todo = later
+        finally:
+            self._depth -= 1
+        self._propagate()
         return [("ok", (i, self.vars[i].type, t)) for i, t in pairs]
 
     def _bind_device(self, id_, v: _Var, dv: _Value):

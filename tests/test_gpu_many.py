@@ -7,7 +7,7 @@ import os
 
 import numpy as np
 import pytest
-from hypothesis import HealthCheck, given, settings, strategies as st
+from hypothesis import HealthCheck, example, given, settings, strategies as st
 
 from oracle import core as ocore
 from oracle import orset as oorset
@@ -79,6 +79,9 @@ SET = st.lists(st.tuples(st.sampled_from(["add", "remove"]), st.integers(0, 9)),
 
 @settings(max_examples=20 * int(os.environ.get("LASPJ_SOAK", "1")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(st.tuples(st.integers(0, 3), SET), min_size=1, max_size=6))
+# a variable named twice ahead of the union's right input: its second pair must land
+# before the dataflow runs (a soak found bind_many propagating between the two)
+@example([(0, []), (0, [("add", 0)]), (1, [("add", 0)])])
 def test_store_bind_many_vs_sequential_oracle(batch):
     """Store.bind_many ends where the oracle ends when it applies the same binds with the
     dataflow deferred until all of them have landed (the interleaving bind_many runs;
