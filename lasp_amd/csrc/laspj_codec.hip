@@ -1358,7 +1358,7 @@ struct HdrHash {
     u64 lens;              // bit hl - 1: some header template is hl bytes (hl <= 64)
 };
 
-// the header-template hash (host and device agree): 16 words, bytes >= hl zero
+// the header-template hash (host and device agree): ceil(hl / 4) words, bytes >= hl zero
 __host__ __device__ inline uint32_t hdr_mix(uint32_t h, uint32_t v) {
     h ^= v;
     h *= 0x9E3779B1u;
@@ -1751,13 +1751,14 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
             const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
             lens &= lens - 1ull;
             if (s + L2 > lim) break;
-            uint32_t q[16];
+            uint32_t q[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
             uint32_t h = L2 * 0x85EBCA6Bu;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int rem = (int)L2 - 4 * i;          // L2 is wave-uniform
-                const uint32_t v = rem > 0 ? word_at(w.buf, min(s + 4u * i, kBWin + 56u)) : 0u;
-                q[i] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+                if (rem <= 0) break;                      // the hash covers ceil(L2 / 4) words
+                const uint32_t v = word_at(w.buf, min(s + 4u * i, kBWin + 56u));
+                q[i] = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);
                 h = hdr_mix(h, q[i]);
             }
             for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
@@ -2172,7 +2173,7 @@ __device__ int64_t resolve_hdr(const PWin& w, uint32_t x, const HdrHash& hh,
         const int rem = (int)hl - 4 * i;
         const uint32_t v = word_at(w.buf, min(x + 4u * i, kBWin + 56u));
         q[i] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
-        h = hdr_mix(h, q[i]);
+        if (rem > 0) h = hdr_mix(h, q[i]);            // ceil(hl / 4) words
     }
     int64_t rank = -1;
     if (on) {
@@ -2774,7 +2775,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
             const uint32_t hl = desc[4 * r + 1];
             if (hl < 4 || hl > 64) continue;
             uint32_t h = hl * 0x85EBCA6Bu;
-            for (int i = 0; i < 16; ++i) {
+            for (uint32_t i = 0; 4 * i < hl; ++i) {         // ceil(hl / 4) words
                 uint32_t v;
                 std::memcpy(&v, hdr + 64 * r + 4 * i, 4);   // zero past hl
                 h = laspj::hdr_mix(h, v);
