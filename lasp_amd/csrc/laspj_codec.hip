@@ -1246,6 +1246,39 @@ __device__ __forceinline__ uint32_t word_at(const uint8_t* buf, uint32_t o) {
     return __builtin_amdgcn_alignbyte(b32[1], b32[0], o & 3u);
 }
 
+// staged bytes [o, o + L) equal the 16-byte-aligned, zero-padded template t16 (L <= 48).
+// L is wave-uniform: records of up to 28 bytes (Lasp's 20-byte binary tokens make
+// 104 2 109 <len:4> <20 bytes> = 27) compare 7 words read from 8 staged dwords and two
+// template loads; longer ones go through rec_words / load48.
+__device__ __forceinline__ bool rec_match(const uint8_t* buf, uint32_t o, uint32_t L,
+                                          const uint8_t* t16) {
+    if (L <= 28u) {
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf + (o & ~3u));
+        const u32x4* t = reinterpret_cast<const u32x4*>(t16);
+        const u32x4 z = {0, 0, 0, 0};
+        const u32x4 a = t[0], b = L > 16u ? t[1] : z;   // a 16-byte stride holds no t[1]
+        const uint32_t tw[7] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z};
+        uint32_t q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = b32[i];
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            const int rem = (int)L - 4 * i;
+            const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+            eq &= (__builtin_amdgcn_alignbyte(q[i + 1], q[i], o & 3u) & m) == tw[i];
+        }
+        return eq;
+    }
+    uint32_t rw[12], tw[12];
+    rec_words(buf, o, L, rw);
+    load48(tw, t16, L);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) eq &= tw[i] == rw[i];
+    return eq;
+}
+
 // what the wave holds about one element rank (lane-distributed where per lane)
 struct RankPre {
     uint32_t e, hl, key, cnt;   // slot, header length with the 108, word | shift << 8, tokens
@@ -1476,11 +1509,7 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
             if (t.tb[r * RK + j] == bk) k = j;
         ok = k < rcnt;
         if (ok) {                                   // exact compare
-            uint32_t rw[12], tw[12];
-            rec_words(w.buf, ry, RL, rw);
-            load48(tw, d.rec_pad + ((u64)re * RK + k) * RS, RL);
-#pragma unroll
-            for (int i = 0; i < 12; ++i) ok &= tw[i] == rw[i];
+            ok = rec_match(w.buf, ry, RL, d.rec_pad + ((u64)re * RK + k) * RS);
         }
         // "true" / "false" after the atom header the walk read
         const uint32_t fo = ry + RL + rh;
@@ -1675,11 +1704,7 @@ __device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m
         rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
         ok = rank < cur.cnt;
         if (ok) {                                               // exact compare
-            uint32_t rw[12], t[12];
-            rec_words(w.buf, myx, RL, rw);
-            load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
-#pragma unroll
-            for (int i = 0; i < 12; ++i) ok &= t[i] == rw[i];
+            ok = rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + rank) * RS);
         }
         const uint32_t fo = myx + RL;
         const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
@@ -1809,12 +1834,7 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
             for (uint32_t jj = 0; jj < kSmallTok; ++jj)
                 if (tb[jj] == bk) k = jj;
             if (k == 0xFFu || (int32_t)k <= kprev) { ok = false; break; }
-            uint32_t rw[12], tw[12];
-            rec_words(w.buf, y, RL, rw);
-            load48(tw, d.rec_pad + ((u64)e * RK + k) * RS, RL);
-            bool eq = true;
-#pragma unroll
-            for (int i = 0; i < 12; ++i) eq &= tw[i] == rw[i];
+            const bool eq = rec_match(w.buf, y, RL, d.rec_pad + ((u64)e * RK + k) * RS);
             const uint32_t fo = y + RL;
             const uint32_t v0 = word_at(w.buf, fo), v1 = word_at(w.buf, fo + 4u);
             const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
@@ -2028,11 +2048,7 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                 rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
                 bool eq = rank < cur.cnt;
                 if (eq) {                           // exact compare
-                    uint32_t rw[12], t[12];
-                    rec_words(w.buf, myx, RL, rw);
-                    load48(t, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
-#pragma unroll
-                    for (int i = 0; i < 12; ++i) eq &= t[i] == rw[i];
+                    eq = rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + rank) * RS);
                 }
                 // ATOM_EXT / ATOM_UTF8_EXT (2-byte length), SMALL_ATOM_UTF8_EXT
                 // (1-byte length), then "true" / "false"

@@ -462,6 +462,41 @@ def test_gpu_from_binary_round_trip(tagged, knob):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tok_len", [1, 9, 10, 20, 21, 22, 41])
+@pytest.mark.parametrize("pool_n", [3, 40])
+def test_gpu_from_binary_record_lengths(tok_len, pool_n):
+    """Records 104 2 <binary> of 8 .. 48 bytes (token binaries of 1 .. 41 bytes) on both
+    sides of the decoder's compare paths (<= 16, <= 28 and longer record templates),
+    with few token slots per element (element batches) and many (record locator):
+    from_binary of the oracle's payloads gives the encoder's cells."""
+    import numpy as np
+    from lasp_amd import _lib
+    from oracle.otp import lists_sort
+    rng = random.Random(tok_len * 13 + pool_n)
+    elems = list(range(0, 400, 3))
+    pool = {i: list({bytes(rng.randrange(256) for _ in range(tok_len)) for _ in range(pool_n)})
+            for i in range(len(elems))}
+    if tok_len == 1:
+        pool = {i: [bytes([x]) for x in rng.sample(range(256), pool_n)] for i in range(len(elems))}
+    states = [[]]
+    for _ in range(60):
+        d = {}
+        for i in rng.sample(range(len(elems)), rng.choice([1, 5, 60, len(elems)])):
+            d[elems[i]] = {t: rng.random() < 0.3 for t in rng.sample(pool[i], rng.randint(1, len(pool[i])))}
+        states.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in lists_sort(list(d))])
+    ctx, dom, E, d = _decode_setup(states)
+    blobs = [oetf.term_to_binary(s) for s in states]
+    pay, offs = _upload_payloads(ctx, blobs)
+    want = dom.encode_orset(states, E)
+    for knob in (0, "seg512"):
+        b = ctx.orset_batch(len(states), E)
+        with _read_kernel(ctx, knob):
+            st = b.etf_decode(d, pay, offs, tag=-1, vers=1)
+        assert (st == _lib.DEC_OK).all(), (knob, np.nonzero(st)[0][:10])
+        assert np.array_equal(b.download(), want), knob
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("knob", [0, 1, 2, 4, 6, "seg512"])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
