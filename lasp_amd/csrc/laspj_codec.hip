@@ -1655,6 +1655,18 @@ __device__ __forceinline__ uint32_t find_marks(const PWin& w, uint32_t x0, uint3
     else if (hi < 64) mask &= (1ull << hi) - 1ull;
     if (lo >= 64) mask = 0;
     else if (lo > 0) mask &= ~((1ull << lo) - 1ull);
+    if (!__ballot((mask & (mask - 1ull)) != 0)) {
+        // at most one match per lane (the usual case when records or elements are longer
+        // than K bytes): a match's index is the number of lanes below with one
+        const u64 has = __ballot(mask != 0);
+        if (mask) {
+            const uint32_t k = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
+            if (k < 63u) L.rst[k] = (uint16_t)(b0 + (uint32_t)__ffsll((long long)mask) - 1u - x0);
+        }
+        wave_sync();
+        return (uint32_t)__popcll(has);
+    }
     const uint32_t cnt = (uint32_t)__popcll(mask);
     uint32_t incl = cnt;
 #pragma unroll
