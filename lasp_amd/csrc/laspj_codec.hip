@@ -1279,6 +1279,32 @@ __device__ __forceinline__ bool rec_match(const uint8_t* buf, uint32_t o, uint32
     return eq;
 }
 
+// The flag atom whose first 8 bytes are v0, v1 (little-endian): 1 = true, 2 = false,
+// 0 = neither; n = its bytes.  ATOM_EXT 100 0 4 "true" / 100 0 5 "false" (what
+// term_to_binary writes) is two compares; ATOM_UTF8_EXT (118, 2-byte length) and
+// SMALL_ATOM_UTF8_EXT (119, 1-byte length) take the general parse.
+__device__ __forceinline__ uint32_t flag_atom(uint32_t v0, uint32_t v1, uint32_t& n) {
+    if (v0 == 0x74040064u && (v1 & 0xFFFFFFu) == 0x00657572u) { n = 7u; return 1u; }
+    if (v0 == 0x66050064u && v1 == 0x65736C61u) { n = 8u; return 2u; }
+    const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
+    uint32_t gh = 0, len = 0, word = 0, c4 = 0;
+    if ((a0 == 100 || a0 == 118) && a1 == 0) {
+        gh = 3;
+        len = (v0 >> 16) & 0xFFu;
+        word = __builtin_amdgcn_alignbyte(v1, v0, 3);
+        c4 = v1 >> 24;
+    } else if (a0 == 119) {
+        gh = 2;
+        len = a1;
+        word = __builtin_amdgcn_alignbyte(v1, v0, 2);
+        c4 = (v1 >> 16) & 0xFFu;
+    }
+    n = gh + len;
+    if (gh && len == 4 && word == 0x65757274u) return 1u;
+    if (gh && len == 5 && word == 0x736C6166u && c4 == 'e') return 2u;
+    return 0u;
+}
+
 // what the wave holds about one element rank (lane-distributed where per lane)
 struct RankPre {
     uint32_t e, hl, key, cnt;   // slot, header length with the 108, word | shift << 8, tokens
@@ -1722,24 +1748,11 @@ __device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m
         const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
         const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
         const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
-        const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
-        uint32_t gh = 0, len = 0, word = 0, c4 = 0;
-        if ((a0 == 100 || a0 == 118) && a1 == 0) {
-            gh = 3;
-            len = (v0 >> 16) & 0xFFu;
-            word = __builtin_amdgcn_alignbyte(v1, v0, 3);
-            c4 = v1 >> 24;
-        } else if (a0 == 119) {
-            gh = 2;
-            len = a1;
-            word = __builtin_amdgcn_alignbyte(v1, v0, 2);
-            c4 = (v1 >> 16) & 0xFFu;
-        }
-        fend = fo + gh + len;
-        const bool tr = gh && len == 4 && word == 0x65757274u;
-        const bool fa = gh && len == 5 && word == 0x736C6166u && c4 == 'e';
-        ok &= (tr || fa) && fend < lim;
-        fl = tr;
+        uint32_t fn;
+        const uint32_t fk = flag_atom(v0, v1, fn);
+        fend = fo + fn;
+        ok &= fk != 0u && fend < lim;
+        fl = fk == 1u;
     }
     // term order, and each record ends where the next one starts
     const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
@@ -1849,27 +1862,15 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
             const bool eq = rec_match(w.buf, y, RL, d.rec_pad + ((u64)e * RK + k) * RS);
             const uint32_t fo = y + RL;
             const uint32_t v0 = word_at(w.buf, fo), v1 = word_at(w.buf, fo + 4u);
-            const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
-            uint32_t gh = 0, len = 0, word = 0, c4 = 0;
-            if ((a0 == 100 || a0 == 118) && a1 == 0) {
-                gh = 3;
-                len = (v0 >> 16) & 0xFFu;
-                word = __builtin_amdgcn_alignbyte(v1, v0, 3);
-                c4 = v1 >> 24;
-            } else if (a0 == 119) {
-                gh = 2;
-                len = a1;
-                word = __builtin_amdgcn_alignbyte(v1, v0, 2);
-                c4 = (v1 >> 16) & 0xFFu;
-            }
-            const bool tr = gh && len == 4 && word == 0x65757274u;
-            const bool fa = gh && len == 5 && word == 0x736C6166u && c4 == 'e';
-            if (!eq || !(tr || fa)) { ok = false; break; }
+            uint32_t fn;
+            const uint32_t fk = flag_atom(v0, v1, fn);
+            const bool tr = fk == 1u;
+            if (!eq || !fk) { ok = false; break; }
             const uint32_t slot = (uint32_t)(ord >> (8 * k)) & 0xFFu;
             pb |= 1ull << slot;
             if (tr) rb |= 1ull << slot;
             kprev = (int32_t)k;
-            y += RL + gh + len;
+            y += RL + fn;
         }
         ok = ok && y < lim && w.buf[y] == 106;
         y += 1u;
@@ -2068,22 +2069,11 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                 const uint32_t* f32 = reinterpret_cast<const uint32_t*>(w.buf + (fo & ~3u));
                 const uint32_t v0 = __builtin_amdgcn_alignbyte(f32[1], f32[0], fo & 3u);
                 const uint32_t v1 = __builtin_amdgcn_alignbyte(f32[2], f32[1], fo & 3u);
-                const uint32_t a0 = v0 & 0xFFu, a1 = (v0 >> 8) & 0xFFu;
-                uint32_t gh = 0, len = 0, word = 0, c4 = 0;
-                if ((a0 == 100 || a0 == 118) && a1 == 0) {
-                    gh = 3;
-                    len = (v0 >> 16) & 0xFFu;
-                    word = __builtin_amdgcn_alignbyte(v1, v0, 3);
-                    c4 = v1 >> 24;
-                } else if (a0 == 119) {
-                    gh = 2;
-                    len = a1;
-                    word = __builtin_amdgcn_alignbyte(v1, v0, 2);
-                    c4 = (v1 >> 16) & 0xFFu;
-                }
-                const uint32_t fend = fo + gh + len;      // one past the flag
-                const bool tr = gh && len == 4 && fend <= w.end && word == 0x65757274u;
-                const bool fa = gh && len == 5 && fend <= w.end && word == 0x736C6166u && c4 == 'e';
+                uint32_t fn;
+                const uint32_t fk = flag_atom(v0, v1, fn);
+                const uint32_t fend = fo + fn;            // one past the flag
+                const bool tr = fk == 1u && fend <= w.end;
+                const bool fa = fk == 2u && fend <= w.end;
                 fl = tr;
                 // term order: after the previous record's rank
                 const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
