@@ -241,6 +241,15 @@ int laspj_batch_inflation_many(laspj_ctx* ctx, uint32_t n, const laspj_batch* co
 int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                               uint32_t nchunks);
 
+/* foldl(Type:merge, new(), Replies) over n separately held batches — the coordinator's
+ * N-way merge of the replies it received (lasp_update_fsm.erl:189-192,
+ * lasp_bind_fsm.erl:185-188) and the anti-entropy round's reduce, which reads the
+ * rank's own copy in place: dst = srcs[0] ⊔ ... ⊔ srcs[n-1], 1 <= n <= 8, batches of one
+ * kind and shape (any non-list kind; ⊔ as laspj_batch_join).  dst may alias any
+ * source. */
+int laspj_batch_join_n(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* const* srcs,
+                       uint32_t n);
+
 /* ------------------------------------------------------------------ lasp_orset */
 /* merge/2 — lasp_orset.erl:128-134: dst[i] = a[i] ⊔ b[i]  (p|p', r|r').
  * dst may alias a or b (the bind path merges in place, lasp_core.erl:300-303). */

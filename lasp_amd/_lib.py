@@ -98,6 +98,7 @@ SIGNATURES = {
     "laspj_batch_destroy": (i, [vp]),
     "laspj_batch_wrap": (i, [vp, C.c_int32, vp, u64, u64, u32, vpp]),
     "laspj_batch_reduce_chunks": (i, [vp, vp, vp, u32]),
+    "laspj_batch_join_n": (i, [vp, vp, vp, u32]),
     "laspj_batch_bind_many": (i, [vp, u32, vp, vp, vp, vp]),
     "laspj_batch_inflation_many": (i, [vp, u32, vp, vp, i, vp]),
     "laspj_batch_info_get": (i, [vp, C.POINTER(BatchInfo)]),

@@ -511,9 +511,30 @@ __global__ __launch_bounds__(kBlock) void k_reduce_ptrs(u64x2* dst, Srcs s, uint
     }
 }
 
+// the last word of an odd word count (a G-Set batch can have one)
+template <bool MAX>
+__global__ void k_reduce_ptrs_last(u64* dst, Srcs s, uint32_t nsrc, uint64_t w) {
+    if (threadIdx.x != 0) return;
+    u64 a = reinterpret_cast<const u64*>(s.p[0])[w];
+    for (uint32_t j = 1; j < nsrc; ++j) a = join_word<MAX>(a, reinterpret_cast<const u64*>(s.p[j])[w]);
+    dst[w] = a;
+}
+
 hipError_t launch_reduce_ptrs(laspj_ctx* ctx, uint64_t* dst, const uint64_t* const* srcs,
                               uint32_t nsrc, uint64_t words, bool max_join) {
-    if (nsrc < 1 || nsrc > 8 || (words & 1)) return hipErrorInvalidValue;
+    if (nsrc < 1 || nsrc > 8) return hipErrorInvalidValue;
+    if (words & 1) {
+        Srcs t;
+        for (uint32_t j = 0; j < 8; ++j)
+            t.p[j] = reinterpret_cast<const u64x2*>(srcs[j < nsrc ? j : 0]);
+        if (max_join)
+            hipLaunchKernelGGL(k_reduce_ptrs_last<true>, dim3(1), dim3(64), 0, ctx->stream,
+                               reinterpret_cast<u64*>(dst), t, nsrc, words - 1);
+        else
+            hipLaunchKernelGGL(k_reduce_ptrs_last<false>, dim3(1), dim3(64), 0, ctx->stream,
+                               reinterpret_cast<u64*>(dst), t, nsrc, words - 1);
+        if (--words == 0) return hipGetLastError();
+    }
     Srcs s;
     for (uint32_t j = 0; j < 8; ++j)
         s.p[j] = reinterpret_cast<const u64x2*>(srcs[j < nsrc ? j : 0]);

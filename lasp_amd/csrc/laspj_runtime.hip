@@ -404,6 +404,28 @@ int laspj_batch_reduce_chunks(laspj_ctx* ctx, laspj_batch* dst, const laspj_batc
     return LASPJ_OK;
 }
 
+int laspj_batch_join_n(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* const* srcs,
+                       uint32_t n) {
+    if (!same_ctx(ctx, dst) || !srcs || n < 1 || n > 8)
+        return fail(ctx, LASPJ_E_INVAL, "join_n: bad batch or n not in 1..8");
+    if (laspj_is_list(dst->kind)) return fail(ctx, LASPJ_E_KIND, "join_n: list batch");
+    const uint64_t* p[8];
+    for (uint32_t j = 0; j < n; ++j) {
+        const laspj_batch* s = srcs[j];
+        if (!same_ctx(ctx, s)) return fail(ctx, LASPJ_E_INVAL, "join_n: bad source %u", j);
+        if (s->kind != dst->kind) return fail(ctx, LASPJ_E_KIND, "join_n: kinds differ");
+        if (s->replicas != dst->replicas || s->elements != dst->elements ||
+            s->words_per_replica != dst->words_per_replica)
+            return fail(ctx, LASPJ_E_SHAPE, "join_n: shapes differ");
+        p[j] = s->dev;
+    }
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, dst->dev, p, n,
+                                          dst->replicas * dst->words_per_replica,
+                                          dst->kind == LASPJ_KIND_GCOUNTER));
+    return LASPJ_OK;
+}
+
 int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
     if (!b || !out) return LASPJ_E_INVAL;
     out->kind = b->kind;

@@ -288,6 +288,12 @@ class _Batch:
         check(self.ctx.L.laspj_batch_fill_synthetic(self.ctx.h, self.h, seed, replica_base),
               self.ctx.h)
 
+    def join_n(self, srcs):
+        """self = srcs[0] ⊔ ... ⊔ srcs[n-1] (laspj_batch_join_n; self may be one of them)."""
+        arr = (C.c_void_p * len(srcs))(*[b.h for b in srcs])
+        check(self.ctx.L.laspj_batch_join_n(self.ctx.h, self.h, arr, len(srcs)), self.ctx.h)
+        return self
+
     def reduce_chunks(self, src: "_Batch", nchunks: int):
         """self[i] = join over j of src[j*R + i] (laspj_batch_reduce_chunks)."""
         check(self.ctx.L.laspj_batch_reduce_chunks(self.ctx.h, self.h, src.h, nchunks),

@@ -227,6 +227,65 @@ def test_reduce_chunks_every_kind(ctx, nchunks):
             ctx.set_tuning(TUNE_REDUCE_KERNEL, 0)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+def test_join_n_every_kind(ctx, n):
+    """laspj_batch_join_n (foldl(merge, new(), Replies) over separately held batches —
+    the FSM's N-way merge, and the kernel the anti-entropy round reduces with, reading
+    the rank's own copy in place) is the kind's join over n sources, with dst a fresh
+    batch or aliasing any source; G-Set batches of an odd word count included.  Compared
+    with numpy's OR / max, and for OR-Sets with the C orddict merge fold."""
+    rng = np.random.default_rng(300 + n)
+    R_ = 37
+    cases = ((ctx.orset_batch, 100, "or"), (ctx.gset_batch, 100, "or"),
+             (ctx.gset_batch, 64, "or"),                                   # 37 words: odd
+             (ctx.gcounter_batch, 7, "max"))
+    for make, e_n, op in cases:
+        srcs = [make(R_, e_n) for _ in range(n)]
+        w = srcs[0].words_per_replica
+        hs = []
+        for b in srcs:
+            if op == "max":
+                h = rng.integers(0, 5, size=(R_, w), dtype=np.uint64)
+            else:
+                h = rng.integers(0, 2**63, size=(R_, w), dtype=np.uint64) * np.uint64(2) \
+                    + rng.integers(0, 2, size=(R_, w), dtype=np.uint64)
+                if make is ctx.orset_batch:
+                    h[:, 1::2] &= h[:, 0::2]                  # r within p
+                if make is ctx.gset_batch and e_n % 64:
+                    h[:, -1] &= np.uint64((1 << (e_n % 64)) - 1)
+            b.upload(h)
+            hs.append(h)
+        red = np.maximum.reduce if op == "max" else np.bitwise_or.reduce
+        want = red(np.stack(hs), axis=0)
+        dst = make(R_, e_n)
+        dst.join_n(srcs)
+        assert np.array_equal(dst.download_words(), want), (make.__name__, e_n)
+        k = n // 2                                   # in place into one of the sources
+        srcs[k].join_n(srcs)
+        assert np.array_equal(srcs[k].download_words(), want), (make.__name__, e_n, "alias")
+    # OR-Set: the fold of the reference merge over the n replies, token for token
+    tokens = orc.synth_tokens(64)
+    bs = [ctx.orset_batch(9, 64) for _ in range(n)]
+    for j, b in enumerate(bs):
+        b.fill_synthetic(40 + j)
+    dst = ctx.orset_batch(9, 64).join_n(bs)
+    got = dst.download()
+    for i in range(9):
+        acc = orc.ORDict.from_cells(np.zeros((64, 2), np.uint64), tokens)
+        for j in range(n):
+            acc = acc.merge(orc.ORDict.from_cells(orc.synth_orset(40 + j, i, 64), tokens))
+        assert orc.ORDict.from_cells(got[i], tokens).equal(acc), i
+
+
+def test_join_n_errors(ctx):
+    from lasp_amd._lib import LaspjError
+    a, b = ctx.orset_batch(4, 64), ctx.orset_batch(4, 65)
+    g = ctx.gset_batch(4, 64)
+    for bad in ([a, b], [a, g], [], [a] * 9):
+        with pytest.raises(LaspjError):
+            ctx.orset_batch(4, 64).join_n(bad)
+
+
 def test_batch_join_gcounter_is_max(ctx):
     """laspj_batch_join on G-Counter batches is riak_dt_gcounter's merge (per-actor max,
     the same as laspj_gcounter_join), not a bitwise OR of the counts."""
