@@ -21,6 +21,8 @@ from oracle import etf as oetf
 from lasp_amd.terms import Atom as PAtom
 from oracle.terms import Atom, exact_eq
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 # (term, term_to_binary(term)) from the external term format specification
@@ -71,7 +73,7 @@ _terms = st.recursive(_leaf, lambda ch: st.one_of(st.lists(ch, max_size=5),
                       max_leaves=12)
 
 
-@settings(max_examples=400, deadline=None)
+@settings(max_examples=400 * SOAK, deadline=None)
 @given(_terms)
 def test_host_encoder_matches_oracle(t):
     from lasp_amd import etf
@@ -595,7 +597,7 @@ def test_gpu_from_binary_fuzz():
     T = etf.DT_ORSET_TAG
     base = [oetf.to_binary(T, 1, s) for s in states]
     blobs = []
-    for _ in range(2000):
+    for _ in range(2000 * SOAK):
         b = bytearray(rng.choice(base))
         kind = rng.randrange(4)
         if kind == 0 and b:

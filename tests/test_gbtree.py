@@ -12,6 +12,8 @@ from hypothesis import HealthCheck, given, settings, strategies as st
 from oracle import gbtrees as ogb, lattice as olat, orset as oors, orset_gbtree as ogt
 from oracle.terms import exact_eq
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 
 def _tok(k: int) -> bytes:
     return bytes([(k * 37 + 11) & 0xFF]) * 19 + bytes([k & 0xFF])
@@ -157,7 +159,7 @@ def _dedupe(ops):
     return out
 
 
-@settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=120 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(_ops, _ops)
 def test_gbtree_contents_equal_orset(ops_a, ops_b):
     """With distinct tokens the two containers hold the same contents after the same

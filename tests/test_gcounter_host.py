@@ -11,13 +11,15 @@ from lasp_amd import gcounter as dg
 from oracle import core as ocore, lattice as olat
 from oracle.terms import Atom
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 THRESH = st.one_of(
     st.integers(min_value=-(1 << 70), max_value=1 << 70),
     st.floats(allow_nan=False, allow_infinity=True, width=64),
     st.just([]), st.just(Atom("undefined")), st.just(True), st.just(b"x"), st.just((1, 2)))
 
 
-@settings(max_examples=400, deadline=None)
+@settings(max_examples=400 * SOAK, deadline=None)
 @given(THRESH, st.integers(min_value=0, max_value=(1 << 64) - 1), st.booleans())
 def test_threshold_plan_matches_term_order(t, v, strict):
     """The plan (a constant, or a uint64 `t =< sum` run on the device) agrees with the

@@ -15,6 +15,8 @@ from lasp_amd import _lib, etf
 from lasp_amd.codec import Domain
 from lasp_amd.terms import Atom, term_cmp
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 ATOMS = st.sampled_from([Atom(a) for a in ("a", "b", "abc", "zz", "é", "ünïcode", "true", "false")])
 NUM = st.one_of(st.integers(-(1 << 70), 1 << 70), st.integers(-300, 300),
                 st.floats(allow_nan=False, allow_infinity=False, width=64),
@@ -40,7 +42,7 @@ def compare(lib, a, b):
     return out.value
 
 
-@settings(max_examples=600, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=600 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(TERM, TERM)
 def test_term_compare_matches_erlang_order(lib, a, b):
     assert compare(lib, a, b) == term_cmp(a, b), (a, b)
@@ -96,7 +98,7 @@ ELEMS = st.one_of(st.integers(-5, 300), ATOMS, st.tuples(st.integers(0, 3), ATOM
 OPS = st.lists(st.tuples(st.sampled_from(["add", "add", "remove"]), ELEMS), max_size=20)
 
 
-@settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=120 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(OPS, min_size=1, max_size=4))
 def test_dict_export_and_encode_match_python_codec(lib, opss):
     values = [orsets(ops, 10 + i) for i, ops in enumerate(opss)]
@@ -118,7 +120,7 @@ def test_dict_export_and_encode_match_python_codec(lib, opss):
     assert np.array_equal(cells, want)
 
 
-@settings(max_examples=80, deadline=None)
+@settings(max_examples=80 * SOAK, deadline=None)
 @given(st.lists(st.lists(ELEMS, max_size=12), min_size=1, max_size=4))
 def test_gset_dict_and_encode(lib, sets):
     from oracle import otp

@@ -18,6 +18,8 @@ from hypothesis import HealthCheck, given, settings, strategies as st
 from oracle import gset as ogset, orset as oorset
 from oracle.terms import Key
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 ELEM = st.integers(min_value=-3, max_value=6)
 GEN_UPDATE = st.one_of(
     st.tuples(st.just("add"), ELEM), st.tuples(st.just("remove"), ELEM),
@@ -169,7 +171,7 @@ def run(cmds, mod, model, equal, merge, update, new, value):
     assert got == model.value()
 
 
-SETTINGS = settings(max_examples=300, deadline=None,
+SETTINGS = settings(max_examples=300 * SOAK, deadline=None,
                     suppress_health_check=[HealthCheck.too_slow])
 
 

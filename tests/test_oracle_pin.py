@@ -18,6 +18,8 @@ import numpy as np
 import pytest
 from hypothesis import given, settings, strategies as st
 
+SOAK = int(__import__("os").environ.get("LASPJ_SOAK", "1"))   # x examples for a soak run
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 E = 12          # element ids 0..11 (the C restatement keys are the element ints)
 T = 8           # token pool per test: 20-byte binaries
@@ -106,7 +108,7 @@ OP = st.tuples(st.sampled_from(["add", "add", "remove"]), st.integers(0, E - 1),
                st.integers(0, T - 1))
 
 
-@settings(max_examples=300, deadline=None)
+@settings(max_examples=300 * SOAK, deadline=None)
 @given(st.lists(OP, max_size=24), st.lists(OP, max_size=24), st.integers(0, 3))
 def test_c_restatement_matches_python_oracle(aops, bops, seed):
     pool = _tokens(seed)
