@@ -531,7 +531,9 @@ def test_orset_intersection_concat(ctx):
 
 
 def test_gset_combinators(ctx):
-    """G-Set union / intersection / filter / product / gather bodies vs oracle lists."""
+    """G-Set intersection / filter / product / gather bodies vs oracle lists.  (The G-Set
+    union body is `L ++ R`, a list value: tests/test_gpu_lists.py compares it with
+    union_body on unsorted and overlapping lists, test_store_random re-binds it.)"""
     from oracle import core
     n, e_n = 4, 150
     a = np.stack([orc.synth_gset(91, i, e_n) for i in range(n)])
