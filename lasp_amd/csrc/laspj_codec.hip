@@ -805,30 +805,55 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     }
                     const uint32_t r_lo = jlo < kBlock ? s_rec[jlo] : nrec;
                     const uint32_t r_hi = s_rec[jhi];
-                    for (uint32_t ri = r_lo + tid; ri < r_hi; ri += kBlock) {
+                    // each thread takes a run of consecutive records: the element of the
+                    // run's first record by binary search and its token by rank select,
+                    // then the next record is the next present token (one find-first-set)
+                    // or the next element's first, its position the previous end
+                    const uint32_t per = (r_hi - r_lo + kBlock - 1) / kBlock;
+                    uint32_t ri = r_lo + tid * per;
+                    const uint32_t re = min(ri + per, r_hi);
+                    if (ri < re) {
                         uint32_t lo = jlo, hi = jhi;            // last j with s_rec[j] <= ri
                         while (hi - lo > 1) {
                             const uint32_t m = (lo + hi) >> 1;
                             if (s_rec[m] <= ri) lo = m;
                             else hi = m;
                         }
-                        const uint32_t j = lo, rho = ri - s_rec[j];
-                        const u64 pj = s_p[j], rj = s_r[j];
-                        const uint32_t rank = select64(pj, rho);
-                        const bool rm = (rj >> rank) & 1ull;
+                        uint32_t j = lo;
+                        const uint32_t rho = ri - s_rec[j];
+                        u64 pj = s_p[j], rj = s_r[j];
+                        uint32_t jend = s_rec[j + 1], e = s_e[j];
+                        uint32_t rank = select64(pj, rho);
                         const u64 below = rank ? (~0ull >> (64u - rank)) : 0ull;
-                        const int32_t rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u +
-                                                                rho * (RL + 8u) -
-                                                                (uint32_t)__popcll(rj & below));
-                        if (overlaps<WIN>(rel, RL)) {
-                            uint32_t w[12];
-                            load_piece48(w, d.rec_pad + ((u64)s_e[j] * RK + rank) * RS, RL);
-                            or_piece<12>(win, rel, w, RL);
+                        int32_t rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u +
+                                                          rho * (RL + 8u) -
+                                                          (uint32_t)__popcll(rj & below));
+                        for (;;) {
+                            const bool rm = (rj >> rank) & 1ull;
+                            if (overlaps<WIN>(rel, RL)) {
+                                uint32_t w[12];
+                                load_piece48(w, d.rec_pad + ((u64)e * RK + rank) * RS, RL);
+                                or_piece<12>(win, rel, w, RL);
+                            }
+                            // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
+                            const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
+                                                    rm ? 0x00657572u : 0x65736c61u};
+                            if (overlaps<WIN>(rel + (int32_t)RL, 8))
+                                or_piece<2>(win, rel + (int32_t)RL, wa, 8);
+                            if (++ri >= re) break;
+                            if (ri < jend) {                     // the element's next token
+                                rel += (int32_t)(RL + (rm ? 7u : 8u));
+                                rank = (uint32_t)__ffsll((long long)(pj & (~1ull << rank))) - 1u;
+                            } else {                             // the next element's first
+                                do ++j; while (s_rec[j + 1] <= ri);
+                                pj = s_p[j];
+                                rj = s_r[j];
+                                jend = s_rec[j + 1];
+                                e = s_e[j];
+                                rank = (uint32_t)__ffsll((long long)pj) - 1u;
+                                rel = cur_rel + (int32_t)(s_pos[j] + s_hl[j] + 4u);
+                            }
                         }
-                        // ATOM_EXT true = 100 0 4 "true", false = 100 0 5 "false"
-                        const uint32_t wa[2] = {rm ? 0x74040064u : 0x66050064u,
-                                                rm ? 0x00657572u : 0x65736c61u};
-                        if (overlaps<WIN>(rel + (int32_t)RL, 8)) or_piece<2>(win, rel + (int32_t)RL, wa, 8);
                     }
                 }
                 __syncthreads();
