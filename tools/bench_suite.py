@@ -147,6 +147,15 @@ def kernels(ctx, R, E, steps):
     gb.fill_synthetic(6)
     report("gset_join", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * R * W, R * E, "elements_per_s")
     del ga, gb, gc
+    # the same join at 16x the replicas (8 GiB per operand): the 0.3 ms launch above is
+    # short enough for launch and tail to show; this one is the steady-state rate
+    RL_ = 16 * R
+    ga, gb, gc = (ctx.gset_batch(RL_, E) for _ in range(3))
+    ga.fill_synthetic(5)
+    gb.fill_synthetic(6)
+    report("gset_join_16x", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * RL_ * W, RL_ * E,
+           "elements_per_s")
+    del ga, gb, gc
     # riak_dt_gcounter (the ad counter's threshold counter): 2^20 replicas x 1024 actors
     RG, A = 1 << 20, 1024
     ka, kb, kc = (ctx.gcounter_batch(RG, A) for _ in range(3))

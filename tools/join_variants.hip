@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 typedef unsigned long long u64;
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
@@ -125,9 +126,51 @@ struct Variant {
     bool inplace;
 };
 
+// skew mode: tools/join_variants <lg> <steps> skew <bytes>...: the current kernel with
+// b offset by `bytes` and d by 2 x `bytes` from their allocations (HBM placement of the
+// three streams relative to each other)
+static int skew_mode(int lg, int steps, int argc, char** argv) {
+    uint64_t n = 1ull << lg;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    const uint64_t pad = 64ull << 20;
+    char *ra, *rb, *rd;
+    CK(hipMalloc(&ra, n * 16 + pad));
+    CK(hipMalloc(&rb, n * 16 + pad));
+    CK(hipMalloc(&rd, n * 16 + 2 * pad));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int k = 4; k < argc; ++k) {
+        const uint64_t sk = strtoull(argv[k], nullptr, 0);
+        u64x2* a = (u64x2*)ra;
+        u64x2* b = (u64x2*)(rb + sk);
+        u64x2* d = (u64x2*)(rd + 2 * sk);
+        hipLaunchKernelGGL(k_fill, dim3(cus * 16), dim3(256), 0, 0, a, n, 1ull);
+        hipLaunchKernelGGL(k_fill, dim3(cus * 16), dim3(256), 0, 0, b, n, 2ull);
+        auto kern = k_gs<2, true, true, false, 256>;
+        hipLaunchKernelGGL(kern, dim3(cus * 64), dim3(256), 0, 0, d, a, b, n);
+        CK(hipEventRecord(e0, 0));
+        for (int s = 0; s < steps; ++s)
+            hipLaunchKernelGGL(kern, dim3(cus * 64), dim3(256), 0, 0, d, a, b, n);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= steps;
+        const double gbs = 48.0 * n / (ms * 1e-3) / 1e9;
+        printf("skew %-10llu a=%p b=%p d=%p %8.3f ms %7.1f GB/s %.1f%%\n", (unsigned long long)sk,
+               (void*)a, (void*)b, (void*)d, ms, gbs, gbs / 80.0);
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     int lg = argc > 1 ? atoi(argv[1]) : 32;
     int steps = argc > 2 ? atoi(argv[2]) : 6;
+    if (argc > 3 && !strcmp(argv[3], "skew")) return skew_mode(lg, steps, argc, argv);
     uint64_t n = 1ull << lg;
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
