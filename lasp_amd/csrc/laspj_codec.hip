@@ -1822,6 +1822,21 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     uint32_t hl = 0;
     if (ok) {
         u64 lens = hh.lens;
+        // the element image's length from its tag where the tag gives it (integers,
+        // binaries, atoms, small bignums): one probe at that header length; other terms
+        // try every length the dictionary has
+        {
+            const uint32_t b2 = w.buf[min(s + 2u, kBWin + 63u)];
+            const uint32_t h0 = word_at(w.buf, min(s + 3u, kBWin + 56u));
+            uint32_t il = 0;
+            if (b2 == 97) il = 2;                                        // SMALL_INTEGER_EXT
+            else if (b2 == 98) il = 5;                                   // INTEGER_EXT
+            else if (b2 == 109) il = 5u + __builtin_bswap32(h0);         // BINARY_EXT
+            else if (b2 == 100 || b2 == 118)                             // ATOM(_UTF8)_EXT
+                il = 3u + (((h0 & 0xFFu) << 8) | ((h0 >> 8) & 0xFFu));
+            else if (b2 == 115 || b2 == 119 || b2 == 110) il = 2u + (h0 & 0xFFu) + (b2 == 110);
+            if (il) lens = il <= 61u ? lens & (1ull << (il + 2u)) : 0ull;   // hl = il + 3
+        }
         while (lens && rk < 0) {
             const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
             lens &= lens - 1ull;
