@@ -103,7 +103,9 @@ def antientropy_leg(ctx, args, rank, world, barrier):
     from lasp_amd.engine import Comm
     comm = Comm(ctx, world, _uid(rank), rank)
     O, E = args.ae_objects, args.elements
-    st, rv = ctx.orset_batch(O, E), ctx.orset_batch(O, E)
+    st = ctx.orset_batch(O, E)
+    # the peers' copies of this rank's chunk: (n-1)/n of the state (none at n = 1)
+    rv = ctx.orset_batch(O // world * (world - 1), E) if world > 1 else None
     st.fill_synthetic(10 + rank)
     ctx.synchronize()
     comm.antientropy(st, rv)                     # warm-up round (RCCL connection setup)
@@ -125,8 +127,9 @@ def antientropy_leg(ctx, args, rank, world, barrier):
     out = {
         "workload": "gossip anti-entropy (BASELINE configs[2]) via laspj_antientropy: "
                     "RCCL all-to-all + HIP OR (own chunk joined in place) + RCCL "
-                    "all-gather, all on the engine stream",
-        "hbm_bytes_per_round": S + S // world,
+                    "all-gather, all on the engine stream (laspj_antientropy_plan's "
+                    "steps; a one-rank round has no step)",
+        "hbm_bytes_per_round": (S + S // world) if world > 1 else 0,
         "objects_per_gpu": O, "elements": E, "state_bytes_per_gpu": S,
         "rounds": args.ae_rounds, "ms_per_round": per_round * 1e3,
         "merged_elements_per_s": (world - 1) * O * E / per_round,

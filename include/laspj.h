@@ -346,6 +346,21 @@ int laspj_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
 int laspj_orset_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                  const laspj_buf* index, const laspj_batch* prev, int strict,
                                  laspj_buf* out);
+/* laspj_orset_gather_inflation compares prev and dst slot by slot, which is the
+ * reference's lists:keyfind when the output keys are distinct, or when every slot
+ * sharing a key takes the same src slot (fold X -> [X, X, X]).  When keys repeat across
+ * src slots (a collapsing map such as X div 3, a fold whose F(X) lists overlap), keyfind
+ * pairs each Prev entry with the FIRST Cur entry of its key: the keyed form takes, per
+ * dst slot o (uint32 each), head[o] = the first dst slot with o's key and next[o] = the
+ * next one in list order (0xFFFFFFFF after the last), and compares every present prev
+ * slot with the first present dst slot of its key chain.  Tokens of different src slots
+ * are taken to be different terms (Lasp mints a fresh token per add, lasp_orset.erl:
+ * 261-262); a host whose dictionary shares a token term between elements of one key
+ * uses list values instead. */
+int laspj_orset_gather_inflation_keyed(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                       const laspj_buf* index, const laspj_buf* head,
+                                       const laspj_buf* next, const laspj_batch* prev,
+                                       int strict, laspj_buf* out);
 
 /* ------------------------------------------------------------------ lasp_gset */
 /* merge/2 — lasp_gset.erl:99-101 (ordsets:union on canonical sets = OR) */
@@ -506,17 +521,53 @@ int laspj_comm_init_rank(laspj_ctx* ctx, int nranks, const uint8_t* id, int rank
 int laspj_comm_init_all(laspj_ctx* const* ctxs, int n, laspj_comm** out);
 int laspj_comm_destroy(laspj_comm* comm);
 int laspj_comm_info(const laspj_comm* comm, int* rank, int* nranks);
-/* one round on this rank: state (R objects, R % nranks == 0, nranks <= 8) and recv (R
- * objects of state's kind: the peers' copies land there).  The rank's own chunk is
+/* one round on this rank: state (R objects, R % nranks == 0, nranks <= 8) and recv (at
+ * least (nranks-1) * R / nranks objects of state's kind: the peers' copies of this
+ * rank's chunk land there, peer p's in slot p - (p > rank)).  The rank's own chunk is
  * joined in place in state and sent from there; `chunk` is not needed (may be NULL; when
- * given it must hold R / nranks objects and is left untouched).  For G-Counters recv
- * may be NULL too. */
+ * given it must hold R / nranks objects and is left untouched).  recv may be NULL for
+ * G-Counters and when nranks == 1.  The round runs laspj_antientropy_plan's steps. */
 int laspj_antientropy(laspj_comm* comm, laspj_batch* state, laspj_batch* recv,
                       laspj_batch* chunk);
-/* the same for n communicators of one process (laspj_comm_init_all), as one RCCL group
- * per phase */
+/* the same for n communicators of one process (laspj_comm_init_all): step g of every
+ * communicator's plan goes into one RCCL group */
 int laspj_antientropy_group(laspj_comm* const* comms, laspj_batch* const* state,
                             laspj_batch* const* recv, laspj_batch* const* chunk, int n);
+
+/* The schedule of one rank's round — pure host code, no GPU or RCCL needed — which
+ * laspj_antientropy executes step for step (and a test can execute over any transport).
+ * Word offsets into two buffers: STATE (state_words = R objects, chunk-major: rank j owns
+ * words [j*cw, (j+1)*cw), cw = state_words / nranks) and RECV ((nranks-1) slots of cw).
+ * Steps carry a group number: groups run in order; the SEND / RECV steps of one group are
+ * one RCCL group (at most 2 (nranks-1) point-to-point calls, each of at most piece_words
+ * words; 0 = 2^27 = 1 GiB, as one RCCL p2p call moves at most 4 GiB); a REDUCE or
+ * ALLREDUCE_MAX group holds that one step.  A SEND and the peer's matching RECV carry the
+ * same tag (the piece number within the phase).  kind: LASPJ_KIND_ORSET / GSET (all-to-all
+ * -> reduce -> all-gather) or LASPJ_KIND_GCOUNTER (all-reduce(max) in pieces).  *nsteps
+ * receives the step count; steps may be NULL (count only); LASPJ_E_RANGE when cap is
+ * smaller than the count. */
+#define LASPJ_AE_SEND          1  /* send words [offset, +words) of buf to peer          */
+#define LASPJ_AE_RECV          2  /* receive words from peer into [offset, +words) of buf */
+#define LASPJ_AE_REDUCE        3  /* STATE[offset, +words) := itself ⊔ RECV[src + j*words,
+                                     +words) for j < nsrc (the kind's join)              */
+#define LASPJ_AE_ALLREDUCE_MAX 4  /* STATE[offset, +words) := the unsigned max of every
+                                     rank's words (G-Counters)                           */
+#define LASPJ_AE_BUF_STATE 0
+#define LASPJ_AE_BUF_RECV  1
+typedef struct laspj_ae_step {
+    uint32_t group;
+    int32_t  op;                 /* LASPJ_AE_*                                          */
+    int32_t  peer;               /* SEND / RECV: the peer rank; else -1                 */
+    int32_t  buf;                /* SEND: the buffer read; RECV: the buffer written     */
+    uint64_t offset;             /* words                                               */
+    uint64_t words;
+    uint64_t src;                /* REDUCE: first source word in RECV                   */
+    uint32_t nsrc;               /* REDUCE: source runs                                 */
+    uint32_t tag;                /* SEND / RECV: piece number                           */
+} laspj_ae_step;
+int laspj_antientropy_plan(int32_t kind, int rank, int nranks, uint64_t state_words,
+                           uint64_t piece_words, laspj_ae_step* steps, uint64_t cap,
+                           uint64_t* nsteps);
 
 /* ------------------------------------------------------------------ list values */
 /* List-faithful values.  The combinator bodies of lasp_core bind lists that are not
@@ -641,7 +692,8 @@ int laspj_term_compare(const uint8_t* a, size_t na, const uint8_t* b, size_t nb,
 int laspj_dict_create(laspj_dict** out);
 int laspj_dict_destroy(laspj_dict* dict);
 /* register every element and token term the payloads hold (append-only slots; an
- * element keeps at most 64 token slots: LASPJ_DEC_UNREPRESENTABLE past that) */
+ * element keeps at most 64 token slots: LASPJ_DEC_UNREPRESENTABLE past that).  A payload
+ * whose status is not LASPJ_DEC_OK registers nothing (binary_to_term/1 rejects it whole). */
 int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const uint64_t* offsets,
                    uint64_t n, int tag, int32_t* status);
 int laspj_dict_info(const laspj_dict* dict, uint32_t* elements, uint64_t* elem_bytes,
@@ -652,7 +704,8 @@ int laspj_dict_info(const laspj_dict* dict, uint32_t* elements, uint64_t* elem_b
 int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, uint32_t* elem_off,
                       uint32_t* elem_order, uint8_t* tok_blob, uint32_t* tok_off,
                       uint8_t* tok_order);
-/* payloads -> cells over the dictionary: out holds n replicas of the batch layout
+/* payloads -> cells over the dictionary (offsets must not descend: LASPJ_E_INVAL): out
+ * holds n replicas of the batch layout
  * (OR-Set 2E words, G-Set ceil(E/64) words).  A value that is not an orddict / ordset
  * (keys or tokens not strictly ascending in term order) or holds a term outside the
  * dictionary gets LASPJ_DEC_UNKNOWN_TERM and an empty replica — such lists take the

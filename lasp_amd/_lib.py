@@ -66,6 +66,17 @@ class ListOrder(C.Structure):
                 ("grank", C.c_void_p)]
 
 
+class AEStep(C.Structure):
+    """laspj_ae_step: one step of an anti-entropy round's plan."""
+    _fields_ = [("group", C.c_uint32), ("op", C.c_int32), ("peer", C.c_int32),
+                ("buf", C.c_int32), ("offset", C.c_uint64), ("words", C.c_uint64),
+                ("src", C.c_uint64), ("nsrc", C.c_uint32), ("tag", C.c_uint32)]
+
+
+AE_SEND, AE_RECV, AE_REDUCE, AE_ALLREDUCE_MAX = 1, 2, 3, 4
+AE_BUF_STATE, AE_BUF_RECV = 0, 1
+
+
 class Incr(C.Structure):
     _fields_ = [("replica", C.c_uint64), ("actor", C.c_uint32), ("reserved", C.c_uint32),
                 ("amount", C.c_uint64)]
@@ -112,6 +123,7 @@ SIGNATURES = {
     "laspj_orset_fragment": (i, [vp, vp, u32, vp]),
     "laspj_orset_precondition_context": (i, [vp, vp, vp]),
     "laspj_orset_gather_inflation": (i, [vp, vp, vp, vp, vp, i, vp]),
+    "laspj_orset_gather_inflation_keyed": (i, [vp, vp, vp, vp, vp, vp, vp, i, vp]),
     "laspj_batch_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_join": (i, [vp, vp, vp, vp]),
     "laspj_orset_reduce": (i, [vp, vp, vp, u32]),
@@ -164,6 +176,8 @@ SIGNATURES = {
     "laspj_comm_info": (i, [vp, C.POINTER(i), C.POINTER(i)]),
     "laspj_antientropy": (i, [vp, vp, vp, vp]),
     "laspj_antientropy_group": (i, [vp, vp, vp, vp, i]),
+    "laspj_antientropy_plan": (i, [C.c_int32, i, i, u64, u64, C.POINTER(AEStep), u64,
+                                   C.POINTER(u64)]),
     "laspj_list_batch_create": (i, [vp, C.c_int32, u64, u32, u32, vpp]),
     "laspj_list_counts": (i, [vp, vp, vp]),
     "laspj_list_upload": (i, [vp, vp, u64, u32, vp, vp, vp]),

@@ -207,9 +207,11 @@ class Store:
         body keeps the left side's tokens, and re-runs merge into the output), so this is
         that interleaving: the binds in pair order with propagation deferred to the end,
         not the one-bind-at-a-time one."""
+        allp = list(pairs)                        # (a generator is read once)
         self._depth += 1                          # one propagation after all writes
+        done = False
         try:
-            todo = list(pairs)
+            todo = allp
             while todo:
                 pend, seen, later = [], set(), []
                 for id_, term in todo:
@@ -237,10 +239,18 @@ class Store:
                             v.val = dst
                             self._written(id_, v)
                 todo = later
+            done = True
         finally:
             self._depth -= 1
-        self._propagate()
-        return [("ok", (i, self.vars[i].type, t)) for i, t in pairs]
+            # the writes that landed before a failure still reach their processes
+            if done:
+                self._propagate()
+            else:
+                try:
+                    self._propagate()
+                except Exception:                 # the original error is the one raised
+                    pass
+        return [("ok", (i, self.vars[i].type, t)) for i, t in allp]
 
     def _bind_device(self, id_, v: _Var, dv: _Value):
         t = v.type

@@ -107,7 +107,8 @@ bool set_kind(int32_t k) {
     return k == LASPJ_KIND_ORSET || k == LASPJ_KIND_GSET || k == LASPJ_KIND_GCOUNTER;
 }
 
-// shapes of one rank's round: state R objects (R % n == 0), recv R, chunk R / n
+// shapes of one rank's round: state R objects (R % n == 0), recv >= (n-1) R / n objects
+// (may be NULL when n == 1), chunk (optional, unused) R / n objects
 int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batch* recv,
                  const laspj_batch* chunk, const char* what) {
     laspj_ctx* ctx = c->ctx;
@@ -115,20 +116,25 @@ int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batc
         return fail(ctx, LASPJ_E_INVAL, "%s: state must be an OR-Set, G-Set or G-Counter batch of "
                     "the communicator's context", what);
     if (state->kind == LASPJ_KIND_GCOUNTER) return LASPJ_OK;   // in place, no scratch
-    if (!recv || recv->ctx != ctx)
-        return fail(ctx, LASPJ_E_INVAL, "%s: recv batch missing", what);
-    if (recv->kind != state->kind || (chunk && chunk->kind != state->kind))
-        return fail(ctx, LASPJ_E_KIND, "%s: kinds differ", what);
     const uint64_t n = (uint64_t)c->nranks;
     if (n > 8)
         return fail(ctx, LASPJ_E_UNSUPPORTED, "%s: more than 8 ranks (one node's GPUs)", what);
-    if (state->replicas % n || recv->replicas != state->replicas ||
-        recv->elements != state->elements ||
+    if (!recv && n > 1) return fail(ctx, LASPJ_E_INVAL, "%s: recv batch missing", what);
+    if (recv && recv->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "%s: recv of another context", what);
+    if ((recv && recv->kind != state->kind) || (chunk && chunk->kind != state->kind))
+        return fail(ctx, LASPJ_E_KIND, "%s: kinds differ", what);
+    if (state->replicas % n ||
+        (recv && (recv->replicas < state->replicas / n * (n - 1) ||
+                  recv->elements != state->elements)) ||
         (chunk && (chunk->replicas * n != state->replicas || chunk->elements != state->elements)))
-        return fail(ctx, LASPJ_E_SHAPE, "%s: need objects %% ranks == 0, recv = state "
-                    "(chunk, when given = objects / ranks)", what);
-    if (recv->dev == state->dev)
-        return fail(ctx, LASPJ_E_INVAL, "%s: state and recv must not alias", what);
+        return fail(ctx, LASPJ_E_SHAPE, "%s: need objects %% ranks == 0, recv >= (ranks-1) / "
+                    "ranks x objects (chunk, when given = objects / ranks)", what);
+    if (recv) {
+        const uint64_t sb = laspj::bytes_of(state), rb = laspj::bytes_of(recv);
+        const uintptr_t s0 = (uintptr_t)state->dev, r0 = (uintptr_t)recv->dev;
+        if (s0 < r0 + rb && r0 < s0 + sb)
+            return fail(ctx, LASPJ_E_INVAL, "%s: state and recv must not overlap", what);
+    }
     if ((state->words_per_replica * (state->replicas / n)) & 1)
         return fail(ctx, LASPJ_E_SHAPE, "%s: a chunk must hold an even word count", what);
     return LASPJ_OK;
@@ -136,68 +142,93 @@ int round_checks(const laspj_comm* c, const laspj_batch* state, const laspj_batc
 
 // RCCL point-to-point calls move at most 4 GiB each (measured: a 64 GiB ncclSend/Recv
 // pair delivered only the first 2^32 bytes, tools/ae_probe.py), so every transfer goes
-// in pieces of 2^27 words (1 GiB), all inside the caller's group.
+// in pieces of 2^27 words (1 GiB).
 constexpr uint64_t kPiece = 1ull << 27;
 
-int p2p(const Rccl* R, laspj_comm* c, const uint64_t* src, uint64_t* dst, uint64_t words,
-        int peer) {
+// The schedule (laspj_antientropy_plan).  Bitmap kinds:
+//   all-to-all: piece k of every peer's chunk is one group -- SEND this rank's copy of
+//     chunk p (state words [p cw + k P, ...)) to p, RECV p's copy of this rank's chunk into
+//     recv slot p - (p > rank);
+//   reduce: the rank's own chunk joined in place with the n-1 received copies;
+//   all-gather: piece k of the joined chunk to every peer, and every peer's joined chunk
+//     into its place in state.
+// Per round this rank moves (n-1)/n S over xGMI each way and reads S + writes S/n of HBM
+// for the join.  G-Counters: all-reduce(max) of each piece of the state.
+struct Plan {
+    laspj_ae_step* out;
+    uint64_t cap, n = 0;
+    void put(const laspj_ae_step& s) {
+        if (out && n < cap) out[n] = s;
+        ++n;
+    }
+};
+
+void plan_steps(Plan& P, int32_t kind, int rank, int nranks, uint64_t words, uint64_t piece) {
+    uint32_t group = 0;
+    if (kind == LASPJ_KIND_GCOUNTER) {
+        if (nranks == 1) return;
+        for (uint64_t off = 0; off < words; off += piece)
+            P.put({group++, LASPJ_AE_ALLREDUCE_MAX, -1, LASPJ_AE_BUF_STATE, off,
+                   words - off < piece ? words - off : piece, 0, 0, 0});
+        return;
+    }
+    if (nranks == 1) return;                       // the join of one copy: nothing to do
+    const uint64_t cw = words / (uint64_t)nranks;
+    const uint64_t pieces = (cw + piece - 1) / piece;
+    auto slot = [&](int p) { return (uint64_t)(p - (p > rank ? 1 : 0)); };
+    for (uint64_t k = 0; k < pieces; ++k, ++group) {
+        const uint64_t off = k * piece, len = cw - off < piece ? cw - off : piece;
+        for (int d = 1; d < nranks; ++d) {
+            const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+            P.put({group, LASPJ_AE_SEND, to, LASPJ_AE_BUF_STATE, (uint64_t)to * cw + off, len,
+                   0, 0, (uint32_t)k});
+            P.put({group, LASPJ_AE_RECV, from, LASPJ_AE_BUF_RECV, slot(from) * cw + off, len,
+                   0, 0, (uint32_t)k});
+        }
+    }
+    P.put({group++, LASPJ_AE_REDUCE, -1, LASPJ_AE_BUF_STATE, (uint64_t)rank * cw, cw, 0,
+           (uint32_t)(nranks - 1), 0});
+    for (uint64_t k = 0; k < pieces; ++k, ++group) {
+        const uint64_t off = k * piece, len = cw - off < piece ? cw - off : piece;
+        for (int d = 1; d < nranks; ++d) {
+            const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+            P.put({group, LASPJ_AE_SEND, to, LASPJ_AE_BUF_STATE, (uint64_t)rank * cw + off, len,
+                   0, 0, (uint32_t)k});
+            P.put({group, LASPJ_AE_RECV, from, LASPJ_AE_BUF_STATE, (uint64_t)from * cw + off,
+                   len, 0, 0, (uint32_t)k});
+        }
+    }
+}
+
+// one step of a plan on the context's stream
+int run_step(const Rccl* R, laspj_comm* c, const laspj_ae_step& s, laspj_batch* state,
+             laspj_batch* recv) {
     laspj_ctx* ctx = c->ctx;
-    for (uint64_t off = 0; off < words; off += kPiece) {
-        const uint64_t len = words - off < kPiece ? words - off : kPiece;
-        LJ_NCCL(ctx, R, R->Send(src + off, len, ncclUint64, peer, c->comm, ctx->stream));
-        LJ_NCCL(ctx, R, R->Recv(dst + off, len, ncclUint64, peer, c->comm, ctx->stream));
+    uint64_t* bufs[2] = {state->dev, recv ? recv->dev : nullptr};
+    switch (s.op) {
+    case LASPJ_AE_SEND:
+        LJ_NCCL(ctx, R, R->Send(bufs[s.buf] + s.offset, s.words, ncclUint64, s.peer, c->comm,
+                                ctx->stream));
+        return LASPJ_OK;
+    case LASPJ_AE_RECV:
+        LJ_NCCL(ctx, R, R->Recv(bufs[s.buf] + s.offset, s.words, ncclUint64, s.peer, c->comm,
+                                ctx->stream));
+        return LASPJ_OK;
+    case LASPJ_AE_REDUCE: {
+        uint64_t* own = state->dev + s.offset;
+        const uint64_t* srcs[8];
+        srcs[0] = own;
+        for (uint32_t j = 0; j < s.nsrc; ++j) srcs[1 + j] = recv->dev + s.src + j * s.words;
+        LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, own, srcs, s.nsrc + 1, s.words,
+                                              state->kind == LASPJ_KIND_GCOUNTER));
+        return LASPJ_OK;
     }
-    return LASPJ_OK;
-}
-
-// the phases of one bitmap round, enqueued on the context's stream (the caller groups
-// the RCCL calls).  The rank's own chunk never moves: the reduce reads it in place in
-// the state, joins the peers' copies from the receive buffer into it, and the all-gather
-// sends it from there.  Per round this rank moves (n-1)/n S over xGMI each way and reads
-// S + writes S/n of HBM for the join.
-int phase_all_to_all(const Rccl* R, laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
-    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
-    for (int p = 0; p < c->nranks; ++p) {
-        // this rank's copy of chunk p goes to rank p; rank p's copy of chunk `rank`
-        // arrives at slot p of recv
-        if (p == c->rank) continue;
-        if (int s = p2p(R, c, state->dev + (uint64_t)p * cw, recv->dev + (uint64_t)p * cw, cw, p))
-            return s;
+    case LASPJ_AE_ALLREDUCE_MAX:
+        LJ_NCCL(ctx, R, R->AllReduce(state->dev + s.offset, state->dev + s.offset, s.words,
+                                     ncclUint64, ncclMax, c->comm, ctx->stream));
+        return LASPJ_OK;
     }
-    return LASPJ_OK;
-}
-
-int phase_reduce(laspj_comm* c, laspj_batch* state, laspj_batch* recv) {
-    laspj_ctx* ctx = c->ctx;
-    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
-    uint64_t* own = state->dev + (uint64_t)c->rank * cw;
-    const uint64_t* srcs[8];
-    for (int p = 0; p < c->nranks; ++p)
-        srcs[p] = p == c->rank ? own : recv->dev + (uint64_t)p * cw;
-    LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, own, srcs, (uint32_t)c->nranks, cw, false));
-    return LASPJ_OK;
-}
-
-// all-gather as point-to-point pieces: the joined chunk goes to every peer's slot `rank`
-int phase_all_gather(const Rccl* R, laspj_comm* c, laspj_batch* state) {
-    const uint64_t cw = (state->replicas / (uint64_t)c->nranks) * state->words_per_replica;
-    const uint64_t* own = state->dev + (uint64_t)c->rank * cw;
-    for (int p = 0; p < c->nranks; ++p) {
-        if (p == c->rank) continue;
-        if (int s = p2p(R, c, own, state->dev + (uint64_t)p * cw, cw, p)) return s;
-    }
-    return LASPJ_OK;
-}
-
-int phase_max(const Rccl* R, laspj_comm* c, laspj_batch* state) {
-    laspj_ctx* ctx = c->ctx;
-    const uint64_t words = state->replicas * state->words_per_replica;
-    for (uint64_t off = 0; off < words; off += kPiece) {
-        const uint64_t len = words - off < kPiece ? words - off : kPiece;
-        LJ_NCCL(ctx, R, R->AllReduce(state->dev + off, state->dev + off, len, ncclUint64,
-                                     ncclMax, c->comm, ctx->stream));
-    }
-    return LASPJ_OK;
+    return fail(ctx, LASPJ_E_INVAL, "antientropy: bad plan step");
 }
 
 }  // namespace
@@ -312,52 +343,62 @@ int laspj_antientropy_group(laspj_comm* const* cs, laspj_batch* const* state,
             return s;
     const bool max_join = state[0]->kind == LASPJ_KIND_GCOUNTER;
     for (int i = 1; i < n; ++i)
-        if ((state[i]->kind == LASPJ_KIND_GCOUNTER) != max_join)
-            return fail(cs[0]->ctx, LASPJ_E_KIND, "antientropy: mixed kinds in one group");
-    // one process may drive several GPUs: every RCCL phase is one group over all of them
-    // (the device is set per call; the contexts' mutexes serialise other callers)
-    std::vector<std::unique_ptr<CGuard>> guards;
+        if ((state[i]->kind == LASPJ_KIND_GCOUNTER) != max_join ||
+            cs[i]->nranks != cs[0]->nranks || laspj::bytes_of(state[i]) != laspj::bytes_of(state[0]))
+            return fail(cs[0]->ctx, LASPJ_E_KIND, "antientropy: one group needs one kind, "
+                        "world and state size");
+    // one process may drive several GPUs: group g of every communicator's plan is one RCCL
+    // group over all of them (the device is set per call; the contexts' mutexes serialise
+    // other callers)
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i; ++j)
+            if (cs[j]->ctx == cs[i]->ctx)
+                return fail(cs[0]->ctx, LASPJ_E_INVAL, "antientropy: one context twice");
+    std::vector<std::vector<laspj_ae_step>> plans(n);
     for (int i = 0; i < n; ++i) {
-        bool dup = false;
-        for (int j = 0; j < i; ++j) dup |= cs[j]->ctx == cs[i]->ctx;
-        if (dup) return fail(cs[0]->ctx, LASPJ_E_INVAL, "antientropy: one context twice");
+        const uint64_t words = state[i]->replicas * state[i]->words_per_replica;
+        Plan P{nullptr, 0};
+        plan_steps(P, state[i]->kind, cs[i]->rank, cs[i]->nranks, words, kPiece);
+        plans[i].resize(P.n);
+        Plan Q{plans[i].data(), P.n};
+        plan_steps(Q, state[i]->kind, cs[i]->rank, cs[i]->nranks, words, kPiece);
     }
+    std::vector<std::unique_ptr<CGuard>> guards;
     for (int i = 0; i < n; ++i) guards.emplace_back(new CGuard(cs[i]->ctx));
-    if (max_join) {
-        LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
+    std::vector<size_t> at(n, 0);
+    for (uint32_t g = 0;; ++g) {
+        bool any = false, comm = false;
+        for (int i = 0; i < n; ++i)
+            if (at[i] < plans[i].size() && plans[i][at[i]].group == g) {
+                any = true;
+                const int32_t op = plans[i][at[i]].op;
+                comm |= op == LASPJ_AE_SEND || op == LASPJ_AE_RECV || op == LASPJ_AE_ALLREDUCE_MAX;
+            }
+        if (!any) break;
+        if (comm) LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
         for (int i = 0; i < n; ++i) {
             hipSetDevice(cs[i]->ctx->device);
-            if (int s = phase_max(R, cs[i], state[i])) {
-                R->GroupEnd();
-                return s;
-            }
+            for (; at[i] < plans[i].size() && plans[i][at[i]].group == g; ++at[i])
+                if (int s = run_step(R, cs[i], plans[i][at[i]], state[i], recv ? recv[i] : nullptr)) {
+                    if (comm) R->GroupEnd();
+                    return s;
+                }
         }
-        LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
-        return LASPJ_OK;
+        if (comm) LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
     }
-    LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
-    for (int i = 0; i < n; ++i) {
-        hipSetDevice(cs[i]->ctx->device);
-        if (int s = phase_all_to_all(R, cs[i], state[i], recv[i])) {
-            R->GroupEnd();
-            return s;
-        }
-    }
-    LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
-    for (int i = 0; i < n; ++i) {
-        hipSetDevice(cs[i]->ctx->device);
-        if (int s = phase_reduce(cs[i], state[i], recv[i])) return s;
-    }
-    LJ_NCCL(cs[0]->ctx, R, R->GroupStart());
-    for (int i = 0; i < n; ++i) {
-        hipSetDevice(cs[i]->ctx->device);
-        if (int s = phase_all_gather(R, cs[i], state[i])) {
-            R->GroupEnd();
-            return s;
-        }
-    }
-    LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
     return LASPJ_OK;
+}
+
+int laspj_antientropy_plan(int32_t kind, int rank, int nranks, uint64_t state_words,
+                           uint64_t piece_words, laspj_ae_step* steps, uint64_t cap,
+                           uint64_t* nsteps) {
+    if (!nsteps || !set_kind(kind) || nranks < 1 || nranks > 8 || rank < 0 || rank >= nranks ||
+        (kind != LASPJ_KIND_GCOUNTER && state_words % (uint64_t)nranks))
+        return LASPJ_E_INVAL;
+    Plan P{steps, steps ? cap : 0};
+    plan_steps(P, kind, rank, nranks, state_words, piece_words ? piece_words : kPiece);
+    *nsteps = P.n;
+    return steps && P.n > cap ? LASPJ_E_RANGE : LASPJ_OK;
 }
 
 }  // extern "C"

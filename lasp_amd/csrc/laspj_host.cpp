@@ -427,6 +427,15 @@ struct Table {
         while (idx[i]) i = (i + 1) & mask;
         idx[i] = (uint32_t)ents.size();
     }
+    // undo the most recent insert.  Exact under linear probing when undone in LIFO order:
+    // every later entry is gone already, and no earlier one probed past this slot.
+    void pop_last() {
+        const uint32_t k = (uint32_t)ents.size();
+        uint64_t i = ents.back().h & mask;
+        while (idx[i] != k) i = (i + 1) & mask;
+        idx[i] = 0;
+        ents.pop_back();
+    }
 };
 
 constexpr uint64_t kElemSeed = 0x4C415350ull;
@@ -440,6 +449,25 @@ struct Dict {
     std::vector<std::string_view> elems;
     std::vector<std::vector<std::string_view>> toks;
     Table elem_slot, tok_slot;
+    // registrations of the payload being added (-1: an element, else the element slot of
+    // a token), undone in reverse when the payload fails: binary_to_term/1 would have
+    // rejected it whole, so none of its terms may take a slot
+    std::vector<int64_t> journal;
+
+    void rollback() {
+        for (size_t j = journal.size(); j-- > 0;) {
+            if (journal[j] < 0) {
+                elem_slot.pop_last();
+                elems.pop_back();
+                toks.pop_back();
+            } else {
+                tok_slot.pop_last();
+                toks[(size_t)journal[j]].pop_back();
+            }
+            store.pop_back();
+        }
+        journal.clear();
+    }
 
     std::string_view keep(const uint8_t* p, size_t n) {
         store.emplace_back((const char*)p, n);
@@ -582,6 +610,7 @@ int reg_elem(Dict* d, const uint8_t* k, size_t kl, uint32_t* slot) {
     d->elem_slot.insert(hash_bytes(k, kl, kElemSeed), 0, v, *slot);
     d->elems.push_back(v);
     d->toks.emplace_back();
+    d->journal.push_back(-1);
     return LASPJ_DEC_OK;
 }
 
@@ -599,6 +628,7 @@ int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
     std::string_view v = d->keep(t, tl);
     d->tok_slot.insert(tok_hash(es, t, tl), es, v, *slot);
     d->toks[es].push_back(v);
+    d->journal.push_back((int64_t)es);
     return LASPJ_DEC_OK;
 }
 
@@ -655,6 +685,7 @@ int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const ui
             const uint8_t* pp = blob + offsets[i];
             const size_t pn = offsets[i + 1] - offsets[i];
             int st;
+            d->journal.clear();
             if (kind == LASPJ_KIND_ORSET) {
                 uint32_t cur = 0;
                 st = walk_orset_payload(
@@ -673,9 +704,12 @@ int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const ui
                         return reg_elem(d, e, el, &s);
                     });
             }
+            if (st != LASPJ_DEC_OK) d->rollback();
+            d->journal.clear();
             status[i] = st;
         }
     } catch (const std::bad_alloc&) {
+        d->rollback();
         return LASPJ_E_NOMEM;
     }
     return LASPJ_OK;
@@ -761,6 +795,7 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
     const uint64_t wpr = kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
     try {
         for (uint64_t i = 0; i < n; ++i) {
+            if (offsets[i + 1] < offsets[i]) return LASPJ_E_INVAL;
             uint64_t* cells = out + i * wpr;
             memset(cells, 0, wpr * 8);
             const uint8_t* pp = blob + offsets[i];

@@ -123,8 +123,10 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                  uint64_t replica_base, uint64_t tmask = ~0ull);
 hipError_t launch_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t e, void* out);
 hipError_t launch_orset_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
+// head / next: the key chains of the KEYED form (laspj_orset_gather_inflation_keyed), or null
 hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
-                                   const uint32_t* index, const laspj_batch* prev, bool strict,
+                                   const uint32_t* index, const uint32_t* head,
+                                   const uint32_t* next, const laspj_batch* prev, bool strict,
                                    uint8_t* res);
 hipError_t launch_orset_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out,
                               bool removed);

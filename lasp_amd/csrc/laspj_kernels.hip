@@ -1206,12 +1206,24 @@ __global__ __launch_bounds__(kBlock) void k_orset_inflation(const u64x2* prev,
 // 235-253 — over the cells just written.  A block owns a 4096-slot segment of the output
 // and a run of 8 replicas (its 16 index entries per lane stay in registers); the block's
 // 4 waves combine their ballots in LDS and emit one partial per (replica, segment).
-constexpr uint32_t kFSeg = 4096, kFPer = kFSeg / kBlock, kFRun = 8;
+//
+// KEYED: output keys may repeat across source slots (a collapsing map such as X div 3, a
+// fold whose F(X) lists overlap).  The reference finds each Prev entry's key in Cur with
+// lists:keyfind — the FIRST entry of Cur carrying that key — so an entry is compared with
+// whatever entry of its key comes first in Cur, not with its own position.  head[o] is
+// the first output slot with o's key, next[o] the following one (list order, kNone after
+// the last); the walk takes the first present Cur slot of the chain.  Tokens of distinct
+// source elements are distinct terms (every token Lasp mints is fresh, unique/1), so a
+// match with another source slot is never ids_inflated and always `=/=`.  The walk only
+// moves forward inside [0, E_out), so a malformed chain cannot loop.
+constexpr uint32_t kFSeg = 4096, kFPer = kFSeg / kBlock, kFRun = 8, kNone = 0xFFFFFFFFu;
 
-template <bool STRICT, bool SEG>
+template <bool STRICT, bool SEG, bool KEYED>
 __global__ __launch_bounds__(kBlock) void k_gather_inflation(u64x2* out, const u64x2* src,
                                                              const u64x2* prev,
                                                              const uint32_t* index,
+                                                             const uint32_t* head,
+                                                             const uint32_t* next,
                                                              uint8_t* res, u64* part,
                                                              uint64_t reps, uint32_t E_out,
                                                              uint32_t E_in, uint32_t nseg,
@@ -1222,11 +1234,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_inflation(u64x2* out, const u
     for (uint64_t it = blockIdx.x; it < runs * nseg; it += gridDim.x) {
         const uint64_t run = it / nseg;
         const uint32_t o0 = (uint32_t)(it - run * nseg) * kFSeg;
-        uint32_t si[kFPer];
+        uint32_t si[kFPer], hd[KEYED ? kFPer : 1];
 #pragma unroll
         for (uint32_t k = 0; k < kFPer; ++k) {
             const uint32_t o = o0 + k * kBlock + threadIdx.x;
-            si[k] = o < E_out ? index[o] : 0xFFFFFFFFu;
+            si[k] = o < E_out ? index[o] : kNone;
+            if constexpr (KEYED) hd[k] = o < E_out ? head[o] : kNone;
         }
         const uint64_t r1 = min(reps, (run + 1) * kFRun);
         for (uint64_t rep = run * kFRun; rep < r1; ++rep) {
@@ -1245,9 +1258,31 @@ __global__ __launch_bounds__(kBlock) void k_gather_inflation(u64x2* out, const u
                 if (o < E_out) {
                     __builtin_nontemporal_store(v[k], d + o);
                     const u64x2 p = __builtin_nontemporal_load(P + o);
-                    viol |= (p.x & ~v[k].x) != 0;
+                    u64x2 c = v[k];
+                    bool other = false;             // keyfind matched another source slot
+                    if constexpr (KEYED) {
+                        if (p.x != 0 && (hd[k] != o || c.x == 0)) {
+                            // lists:keyfind(Key, 1, Cur): first present slot of the chain
+                            c = u64x2{0, 0};
+                            uint32_t j = hd[k] < E_out ? hd[k] : o;
+                            for (;;) {
+                                const uint32_t sj = j == o ? si[k] : index[j];
+                                const u64x2 cj = j == o ? v[k] : (sj < E_in ? s[sj] : u64x2{0, 0});
+                                if (cj.x != 0) {
+                                    c = cj;
+                                    other = sj != si[k];
+                                    break;
+                                }
+                                const uint32_t nj = next[j];
+                                if (nj == kNone || nj <= j || nj >= E_out) break;
+                                j = nj;
+                            }
+                        }
+                    }
+                    viol |= (p.x != 0) & ((c.x == 0) | other | ((p.x & ~c.x) != 0));
                     if constexpr (STRICT) {
-                        changed |= (p.x != 0) & (v[k].x != 0) & ((p.x != v[k].x) | (p.y != v[k].y));
+                        changed |= (p.x != 0) & (c.x != 0) &
+                                   (other | (p.x != c.x) | (p.y != c.y));
                         np += p.x != 0;
                         nc += v[k].x != 0;
                     }
@@ -1277,7 +1312,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_inflation(u64x2* out, const u
 }
 
 hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
-                                   const uint32_t* index, const laspj_batch* prev, bool strict,
+                                   const uint32_t* index, const uint32_t* head,
+                                   const uint32_t* next, const laspj_batch* prev, bool strict,
                                    uint8_t* res) {
     const uint32_t ns = (dst->elements + kFSeg - 1) / kFSeg;
     const uint64_t items = (dst->replicas + kFRun - 1) / kFRun * ns;
@@ -1292,18 +1328,28 @@ hipError_t launch_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj
         if (e != hipSuccess) return e;
     }
     const uint32_t fin = ns > 1 ? fin_for(dst->replicas * ns, ns) : 0u;
-#define LJ_GI(ST, SG)                                                                        \
-    hipLaunchKernelGGL((k_gather_inflation<ST, SG>), dim3((unsigned)(g ? g : 1)), dim3(kBlock), \
-                       0, ctx->stream, reinterpret_cast<u64x2*>(dst->dev),                   \
+    const bool keyed = head != nullptr;
+#define LJ_GI(ST, SG, KY)                                                                    \
+    hipLaunchKernelGGL((k_gather_inflation<ST, SG, KY>), dim3((unsigned)(g ? g : 1)),        \
+                       dim3(kBlock), 0, ctx->stream, reinterpret_cast<u64x2*>(dst->dev),     \
                        reinterpret_cast<const u64x2*>(src->dev),                             \
-                       reinterpret_cast<const u64x2*>(prev->dev), index, res, part,          \
-                       dst->replicas, dst->elements, src->elements, ns, fin, bc)
+                       reinterpret_cast<const u64x2*>(prev->dev), index, head, next, res,    \
+                       part, dst->replicas, dst->elements, src->elements, ns, fin, bc)
+#define LJ_GI2(SG)                                                                           \
+    do {                                                                                     \
+        if (keyed) {                                                                         \
+            if (strict) LJ_GI(true, SG, true); else LJ_GI(false, SG, true);                 \
+        } else {                                                                             \
+            if (strict) LJ_GI(true, SG, false); else LJ_GI(false, SG, false);               \
+        }                                                                                    \
+    } while (0)
     if (ns > 1) {
-        if (strict) LJ_GI(true, true); else LJ_GI(false, true);
+        LJ_GI2(true);
         if (!fin) return finalize(ctx, part, res, dst->replicas, strict ? 2 : 1);
         return hipGetLastError();
     }
-    if (strict) LJ_GI(true, false); else LJ_GI(false, false);
+    LJ_GI2(false);
+#undef LJ_GI2
 #undef LJ_GI
     return hipGetLastError();
 }

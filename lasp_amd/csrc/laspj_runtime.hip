@@ -546,26 +546,50 @@ int laspj_orset_precondition_context(laspj_ctx* ctx, laspj_batch* dst, const las
     return LASPJ_OK;
 }
 
+static int gather_inflation_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                 const laspj_buf* index, const laspj_buf* head,
+                                 const laspj_buf* next, const laspj_batch* prev, int strict,
+                                 laspj_buf* out, const char* what) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src) || !same_ctx(ctx, prev))
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    if (dst->kind != LASPJ_KIND_ORSET || src->kind != LASPJ_KIND_ORSET ||
+        prev->kind != LASPJ_KIND_ORSET)
+        return fail(ctx, LASPJ_E_KIND, "%s: OR-Set batches only", what);
+    if (dst->replicas != src->replicas || prev->elements != dst->elements ||
+        (prev->replicas != dst->replicas && prev->replicas != 1))
+        return fail(ctx, LASPJ_E_SHAPE, "%s: shapes", what);
+    if (dst->dev == src->dev || dst->dev == prev->dev)
+        return fail(ctx, LASPJ_E_INVAL, "%s: dst aliases an input", what);
+    if (int s = check_buf(ctx, index, 4ull * dst->elements, what)) return s;
+    if (head || next) {
+        if (!head || !next) return fail(ctx, LASPJ_E_INVAL, "%s: head and next go together", what);
+        if (int s = check_buf(ctx, head, 4ull * dst->elements, what)) return s;
+        if (int s = check_buf(ctx, next, 4ull * dst->elements, what)) return s;
+    }
+    if (int s = check_buf(ctx, out, dst->replicas, what)) return s;
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_gather_inflation(
+                    ctx, dst, src, static_cast<const uint32_t*>(index->dev),
+                    head ? static_cast<const uint32_t*>(head->dev) : nullptr,
+                    next ? static_cast<const uint32_t*>(next->dev) : nullptr, prev, strict != 0,
+                    static_cast<uint8_t*>(out->dev)));
+    return LASPJ_OK;
+}
+
 int laspj_orset_gather_inflation(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                                  const laspj_buf* index, const laspj_batch* prev, int strict,
                                  laspj_buf* out) {
-    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src) || !same_ctx(ctx, prev))
-        return fail(ctx, LASPJ_E_INVAL, "gather_inflation: bad batch");
-    if (dst->kind != LASPJ_KIND_ORSET || src->kind != LASPJ_KIND_ORSET ||
-        prev->kind != LASPJ_KIND_ORSET)
-        return fail(ctx, LASPJ_E_KIND, "gather_inflation: OR-Set batches only");
-    if (dst->replicas != src->replicas || prev->elements != dst->elements ||
-        (prev->replicas != dst->replicas && prev->replicas != 1))
-        return fail(ctx, LASPJ_E_SHAPE, "gather_inflation: shapes");
-    if (dst->dev == src->dev || dst->dev == prev->dev)
-        return fail(ctx, LASPJ_E_INVAL, "gather_inflation: dst aliases an input");
-    if (int s = check_buf(ctx, index, 4ull * dst->elements, "gather_inflation")) return s;
-    if (int s = check_buf(ctx, out, dst->replicas, "gather_inflation")) return s;
-    Guard g(ctx);
-    LJ_HIP(ctx, laspj::launch_gather_inflation(ctx, dst, src,
-                                               static_cast<const uint32_t*>(index->dev), prev,
-                                               strict != 0, static_cast<uint8_t*>(out->dev)));
-    return LASPJ_OK;
+    return gather_inflation_impl(ctx, dst, src, index, nullptr, nullptr, prev, strict, out,
+                                 "gather_inflation");
+}
+
+int laspj_orset_gather_inflation_keyed(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
+                                       const laspj_buf* index, const laspj_buf* head,
+                                       const laspj_buf* next, const laspj_batch* prev, int strict,
+                                       laspj_buf* out) {
+    if (!head || !next) return fail(ctx, LASPJ_E_INVAL, "gather_inflation_keyed: head / next");
+    return gather_inflation_impl(ctx, dst, src, index, head, next, prev, strict, out,
+                                 "gather_inflation_keyed");
 }
 
 // ------------------------------------------------------------------------- joins

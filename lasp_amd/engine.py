@@ -445,16 +445,28 @@ class ORSetBatch(_Batch):
 
     # a gather whose output is threshold-checked in the same pass (config 4 fused)
     def gather_inflation(self, src: "ORSetBatch", index, prev: "ORSetBatch",
-                         strict: bool = True) -> np.ndarray:
+                         strict: bool = True, chains=None) -> np.ndarray:
         """self <- src through index; returns is_(strict_)inflation(prev, self) per
-        replica (laspj_orset_gather_inflation).  `index` is a uint32 array or Buffer."""
-        idx = index if isinstance(index, Buffer) else None
-        if idx is None:
-            idx = self.ctx.buffer(4 * self.elements)
-            idx.upload(np.ascontiguousarray(index, dtype=np.uint32))
+        replica (laspj_orset_gather_inflation).  `index` is a uint32 array or Buffer.
+        `chains` = (head, next) from key_chains(): the keyed form, for outputs whose keys
+        repeat across src slots (laspj_orset_gather_inflation_keyed)."""
+        def dev(a):
+            if isinstance(a, Buffer):
+                return a
+            b = self.ctx.buffer(4 * self.elements)
+            b.upload(np.ascontiguousarray(a, dtype=np.uint32))
+            return b
+        idx = dev(index)
         out = self.ctx.buffer(self.replicas)
-        check(self.ctx.L.laspj_orset_gather_inflation(self.ctx.h, self.h, src.h, idx.h, prev.h,
-                                                      int(strict), out.h), self.ctx.h)
+        if chains is None:
+            check(self.ctx.L.laspj_orset_gather_inflation(self.ctx.h, self.h, src.h, idx.h,
+                                                          prev.h, int(strict), out.h),
+                  self.ctx.h)
+        else:
+            hd, nx = (dev(c) for c in chains)
+            check(self.ctx.L.laspj_orset_gather_inflation_keyed(
+                self.ctx.h, self.h, src.h, idx.h, hd.h, nx.h, prev.h, int(strict), out.h),
+                self.ctx.h)
         return out.download(np.uint8).astype(bool)
 
     # map / fold bodies: self <- src gathered through index (one u32 per slot of self)
@@ -808,6 +820,40 @@ class ListBatch:
         check(self.ctx.L.laspj_list_fold(self.ctx.h, out.h, self.h, ob.h, kb.h, len(off) - 1,
                                          int(per_entry)), self.ctx.h)
         return out
+
+
+def key_chains(keys: np.ndarray):
+    """The key chains of laspj_orset_gather_inflation_keyed for output slots whose key
+    ids (any integers; equal ids = equal key terms) are `keys`, in list order:
+    head[o] = first slot with o's key, next[o] = the next one (0xFFFFFFFF after the last)."""
+    keys = np.asarray(keys)
+    n = len(keys)
+    order = np.argsort(keys, kind="stable")          # slots grouped by key, list order kept
+    ks = keys[order]
+    start = np.ones(n, dtype=bool)
+    start[1:] = ks[1:] != ks[:-1]
+    first = order[np.maximum.accumulate(np.where(start, np.arange(n), 0))]
+    head = np.empty(n, dtype=np.uint32)
+    head[order] = first
+    nxt = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+    cont = ~start[1:]
+    nxt[order[:-1][cont]] = order[1:][cont]
+    return head, nxt
+
+
+def antientropy_plan(kind: int, rank: int, nranks: int, state_words: int,
+                     piece_words: int = 0) -> list:
+    """The steps one rank's anti-entropy round runs (laspj_antientropy_plan; host only, no
+    GPU): a list of dicts with the laspj_ae_step fields, in order."""
+    from ._lib import AEStep
+    L = load()
+    n = C.c_uint64()
+    check(L.laspj_antientropy_plan(kind, rank, nranks, state_words, piece_words, None, 0,
+                                   C.byref(n)))
+    arr = (AEStep * max(1, n.value))()
+    check(L.laspj_antientropy_plan(kind, rank, nranks, state_words, piece_words, arr,
+                                   n.value, C.byref(n)))
+    return [{f: getattr(arr[k], f) for f, _ in AEStep._fields_} for k in range(n.value)]
 
 
 class Comm:

@@ -114,7 +114,7 @@ class ORDict:
             raise MemoryError
 
     def __del__(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and lib is not None:   # (module torn down at exit)
             lib().orc_orset_free(self.h)
             self.h = None
 

@@ -1,5 +1,16 @@
-"""World-size-2 CPU coverage of the multi-GPU paths (gloo): the anti-entropy
-orchestration (lasp_amd.gossip.anti_entropy_round) and the bench's shard layout."""
+"""CPU coverage of the multi-GPU paths (gloo, world sizes 2 and 4).
+
+The anti-entropy round bench.py runs at N > 1 is `laspj_antientropy` (laspj_comm.hip),
+which executes the steps of `laspj_antientropy_plan` on RCCL.  Here every rank asks the
+same library for the same plan and executes exactly those steps with gloo point-to-point
+calls over host buffers: SEND / RECV steps of one group posted together (an RCCL group),
+REDUCE as the kind's join over the received copies, ALLREDUCE_MAX as an unsigned max.
+Small piece sizes force many pieces per chunk, as 1 GiB pieces do at BASELINE config 3
+(64 GiB per GPU).  After one round every rank must hold the join of every rank's
+replica of every object (the reference's fan-out -> foldl(merge) -> repair,
+lasp_update_fsm.erl:174-216), checked against numpy and, on sampled objects, against the
+C restatement's orddict merge fold.
+"""
 
 import os
 import socket
@@ -16,32 +27,94 @@ WORKER = textwrap.dedent("""
     sys.path.insert(0, %(root)r)
     import numpy as np
     import torch, torch.distributed as dist
-    from lasp_amd.gossip import anti_entropy_round
+    from lasp_amd import _lib
+    from lasp_amd.engine import antientropy_plan
     from oracle import columnar as orc
 
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    objects, E = 6, 33            # chunk = 3 objects per rank; odd E
-    # this rank's replica of every object: synthetic stream 100 + rank
+    SIGN = np.uint64(1 << 63)
+
+    def run_round(kind, state, recv, piece):
+        '''Execute this rank's plan: state / recv are uint64 numpy arrays.'''
+        plan = antientropy_plan(kind, rank, world, state.size, piece)
+        ts = torch.from_numpy(state.view(np.int64))
+        tr = torch.from_numpy(recv.view(np.int64)) if recv is not None else None
+        groups = {}
+        for s in plan:
+            groups.setdefault(s["group"], []).append(s)
+        assert sorted(groups) == list(range(len(groups)))
+        for g in range(len(groups)):
+            reqs = []
+            for s in groups[g]:
+                o, w = s["offset"], s["words"]
+                if s["op"] in (_lib.AE_SEND, _lib.AE_RECV):
+                    buf = ts if s["buf"] == _lib.AE_BUF_STATE else tr
+                    view = buf[o:o + w]
+                    if s["op"] == _lib.AE_SEND:
+                        reqs.append(dist.isend(view, s["peer"], tag=s["tag"]))
+                    else:
+                        reqs.append(dist.irecv(view, s["peer"], tag=s["tag"]))
+                elif s["op"] == _lib.AE_REDUCE:
+                    assert len(groups[g]) == 1
+                    runs = [recv[s["src"] + j * w:s["src"] + (j + 1) * w] for j in range(s["nsrc"])]
+                    state[o:o + w] = np.bitwise_or.reduce([state[o:o + w]] + runs)
+                elif s["op"] == _lib.AE_ALLREDUCE_MAX:
+                    # riak_dt_gcounter's join is the per-actor max of uint64 counts: the
+                    # sign flip makes gloo's signed max the unsigned one
+                    state[o:o + w] ^= SIGN
+                    dist.all_reduce(ts[o:o + w], op=dist.ReduceOp.MAX)
+                    state[o:o + w] ^= SIGN
+                else:
+                    raise AssertionError(s)
+            for r in reqs:
+                r.wait()
+        return plan
+
+    # ---- OR-Set: objects x E cells {p, r}; this rank's replica = synthetic stream 100 + rank
+    objects, E = 4 * world, 33
     mine = np.stack([orc.synth_orset(100 + rank, o, E) for o in range(objects)])
-    state = torch.from_numpy(mine.reshape(-1).view(np.int64).copy())
-    recv = torch.empty_like(state)
-    chunk = torch.empty(state.numel() // world, dtype=torch.int64)
-
-    def reduce_fn():     # CPU stand-in for laspj_batch_reduce_chunks (tested on GPU)
-        r = recv.numpy().view(np.uint64).reshape(world, -1)
-        chunk.numpy().view(np.uint64)[:] = np.bitwise_or.reduce(r, axis=0)
-
-    anti_entropy_round(state, recv, chunk, reduce_fn)
-    got = state.numpy().view(np.uint64).reshape(objects, E, 2)
+    state = mine.reshape(-1).copy()
+    recv = np.full(state.size // world * (world - 1), 0xDEAD, np.uint64)
     want = np.zeros_like(mine)
     for r in range(world):
         want |= np.stack([orc.synth_orset(100 + r, o, E) for o in range(objects)])
-    assert np.array_equal(got, want), "anti-entropy did not converge to the join"
+    for piece in (0, 7, 66):
+        state[:] = mine.reshape(-1)
+        plan = run_round(_lib.KIND_ORSET, state, recv, piece)
+        assert np.array_equal(state.reshape(mine.shape), want), ("not the join", piece)
+    assert any(s["op"] == _lib.AE_REDUCE for s in plan)
+    tokens = orc.synth_tokens(E)
+    for o in (0, objects - 1):
+        acc = orc.ORDict.from_cells(orc.synth_orset(100, o, E), tokens)
+        for r in range(1, world):
+            acc = acc.merge(orc.ORDict.from_cells(orc.synth_orset(100 + r, o, E), tokens))
+        assert orc.ORDict.from_cells(state.reshape(mine.shape)[o], tokens).equal(acc), o
     # a second round is idempotent (the join is already everywhere)
-    anti_entropy_round(state, recv, chunk, reduce_fn)
-    assert np.array_equal(state.numpy().view(np.uint64).reshape(objects, E, 2), want)
-    # bench shard layout: rank r's join shard is synthetic replicas [r*R, (r+1)*R)
+    run_round(_lib.KIND_ORSET, state, recv, 7)
+    assert np.array_equal(state.reshape(mine.shape), want)
+
+    # ---- G-Set: objects x ceil(E/64) words
+    gw = 3
+    gmine = np.stack([np.random.default_rng(300 + rank).integers(0, 1 << 63, (gw,), dtype=np.uint64)
+                      for _ in range(2 * world)])
+    gstate = gmine.reshape(-1).copy()
+    grecv = np.zeros(gstate.size // world * (world - 1), np.uint64)
+    gwant = np.bitwise_or.reduce([np.stack([np.random.default_rng(300 + r).integers(
+        0, 1 << 63, (gw,), dtype=np.uint64) for _ in range(2 * world)]) for r in range(world)])
+    run_round(_lib.KIND_GSET, gstate, grecv, 4)
+    assert np.array_equal(gstate.reshape(gmine.shape), gwant)
+
+    # ---- G-Counter: all-reduce(max) in pieces, counts at and above 2^63 included
+    objs, actors = 5, 7
+    big = [np.random.default_rng(70 + r).integers(0, 1 << 64, (objs, actors), dtype=np.uint64)
+           for r in range(world)]
+    big[0][0, 0], big[-1][0, 0] = np.uint64(1 << 63), np.uint64(5)
+    counts = big[rank].reshape(-1).copy()
+    run_round(_lib.KIND_GCOUNTER, counts, None, 6)
+    assert np.array_equal(counts.reshape(objs, actors), np.maximum.reduce(big))
+
+    # ---- bench shard layout: rank r's join shard is synthetic replicas [r*R, (r+1)*R)
     R = 4
     bases = [None] * world
     dist.all_gather_object(bases, rank * R)
@@ -49,25 +122,6 @@ WORKER = textwrap.dedent("""
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)        # bench takes the max wall time
     assert t.item() == float(world)
-    # G-Counter anti-entropy: one all_reduce(MAX) = riak_dt_gcounter's per-actor max
-    from lasp_amd.gossip import gcounter_anti_entropy_round
-    objs, actors = 5, 7
-    rng = [np.random.default_rng(40 + r) for r in range(world)]
-    views = [g.integers(0, 1 << 40, (objs, actors)).astype(np.int64) for g in rng]
-    counts = torch.from_numpy(views[rank].copy())
-    gcounter_anti_entropy_round(counts)
-    want = np.maximum.reduce(views)
-    assert np.array_equal(counts.numpy(), want)
-    gcounter_anti_entropy_round(counts)             # idempotent
-    assert np.array_equal(counts.numpy(), want)
-    # counts at and above 2^63 (uint64 in int64 words): the join is the UNSIGNED max,
-    # as the device join / reduces compute it
-    big = [g.integers(0, 1 << 64, (objs, actors), dtype=np.uint64) for g in
-           [np.random.default_rng(70 + r) for r in range(world)]]
-    big[0][0, 0], big[1][0, 0] = np.uint64(1 << 63), np.uint64(5)
-    counts = torch.from_numpy(big[rank].view(np.int64).copy())
-    gcounter_anti_entropy_round(counts)
-    assert np.array_equal(counts.numpy().view(np.uint64), np.maximum.reduce(big))
     print("ok", rank)
 """)
 
@@ -80,17 +134,73 @@ def _free_port():
     return p
 
 
-def test_anti_entropy_gloo_world2(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_antientropy_plan_over_gloo(tmp_path, world):
+    from lasp_amd import build
     from oracle import columnar
+    build.build()
     columnar.lib()
     script = tmp_path / "worker.py"
     script.write_text(WORKER % {"root": ROOT})
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", str(script)]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    assert res.stdout.count("ok") == 2
+    assert res.stdout.count("ok") == world
+
+
+def test_antientropy_plan_shape():
+    """Host-only properties of the plan for every world size 1..8: every SEND is matched
+    by one RECV on its peer (same group, tag and length), groups hold at most 2(n-1)
+    point-to-point steps, every word of recv is written exactly once before the REDUCE,
+    and every non-owned chunk of state is overwritten exactly once by the all-gather."""
+    from lasp_amd import _lib, build
+    from lasp_amd.engine import antientropy_plan
+    build.build()
+    for n in range(1, 9):
+        cw, piece = 2 * 37, 10
+        plans = [antientropy_plan(_lib.KIND_ORSET, r, n, n * cw, piece) for r in range(n)]
+        if n == 1:
+            assert plans == [[]]
+            continue
+        for r, plan in enumerate(plans):
+            per_group = {}
+            for s in plan:
+                per_group.setdefault(s["group"], []).append(s)
+            red = [s for s in plan if s["op"] == _lib.AE_REDUCE]
+            assert len(red) == 1 and red[0]["offset"] == r * cw and red[0]["nsrc"] == n - 1
+            for g, steps in per_group.items():
+                p2p = [s for s in steps if s["op"] in (_lib.AE_SEND, _lib.AE_RECV)]
+                assert len(p2p) <= 2 * (n - 1)
+                assert all(s["words"] <= piece for s in p2p)
+            seen_recv = [0] * ((n - 1) * cw)
+            seen_state = [0] * (n * cw)
+            for s in plan:
+                if s["op"] == _lib.AE_SEND:
+                    match = [t for t in plans[s["peer"]] if t["op"] == _lib.AE_RECV and
+                             t["peer"] == r and t["group"] == s["group"] and t["tag"] == s["tag"]]
+                    assert len(match) == 1 and match[0]["words"] == s["words"]
+                if s["op"] == _lib.AE_RECV:
+                    tgt = seen_recv if s["buf"] == _lib.AE_BUF_RECV else seen_state
+                    for w in range(s["offset"], s["offset"] + s["words"]):
+                        tgt[w] += 1
+                    if s["buf"] == _lib.AE_BUF_RECV:
+                        assert s["group"] < red[0]["group"]
+                    else:
+                        assert s["group"] > red[0]["group"]
+            assert seen_recv == [1] * ((n - 1) * cw)
+            assert seen_state == [0 if w // cw == r else 1 for w in range(n * cw)]
+    L = _lib.load()
+    import ctypes as C
+    cnt = C.c_uint64()
+    assert L.laspj_antientropy_plan(_lib.KIND_ORSET, 0, 3, 10, 0, None, 0, C.byref(cnt)) == \
+        _lib.E_INVAL                                    # 10 words do not split 3 ways
+    arr = (_lib.AEStep * 1)()
+    assert L.laspj_antientropy_plan(_lib.KIND_ORSET, 0, 2, 8, 1, arr, 1, C.byref(cnt)) == \
+        _lib.E_RANGE and cnt.value > 1
+    assert C.sizeof(_lib.AEStep) == 48
 
 
 def test_bench_self_launches_ranks():

@@ -4,8 +4,9 @@ A one-GPU box can only form one-rank communicators (RCCL refuses one device twic
 communicator), so these tests pin what a round must do at n = 1 — a round leaves the
 join of the single copy, i.e. the state unchanged, through the full all-to-all ->
 reduce_chunks -> all-gather path and the G-Counter all-reduce(max) — plus the argument
-checks; the n > 1 exchange runs in bench.py on the driver's 8-GPU node, and its
-orchestration is covered by the gloo world-2 test (tests/test_dist_gloo.py).
+checks; the n > 1 exchange runs in bench.py on the driver's 8-GPU node, and the plan it
+executes (laspj_antientropy_plan) is executed over gloo at world 2 and 4 by
+tests/test_dist_gloo.py.
 Reference: lasp_update_fsm.erl:174-216 (N-way merge + repair)."""
 
 import numpy as np
@@ -63,9 +64,7 @@ def test_round_argument_checks(ctx):
     from lasp_amd import _lib
     c = _comm(ctx)
     st = ctx.orset_batch(8, 16)
-    with pytest.raises(_lib.LaspjError) as e:
-        c.antientropy(st)                                     # recv missing
-    assert e.value.status == _lib.E_INVAL
+    c.antientropy(st)                       # one rank: no copies to receive, recv optional
     with pytest.raises(_lib.LaspjError) as e:
         c.antientropy(st, ctx.orset_batch(8, 16), ctx.orset_batch(4, 16))   # chunk != R/n
     assert e.value.status == _lib.E_SHAPE
@@ -74,5 +73,8 @@ def test_round_argument_checks(ctx):
     assert e.value.status == _lib.E_KIND
     with pytest.raises(_lib.LaspjError) as e:
         c.antientropy(st, st)                                  # aliasing
+    assert e.value.status == _lib.E_INVAL
+    with pytest.raises(_lib.LaspjError) as e:
+        c.antientropy(st, st.view(2, 4))                       # overlapping recv
     assert e.value.status == _lib.E_INVAL
     c.close()

@@ -1,4 +1,4 @@
-"""GPU parity at BASELINE.json's configs 3, 4 and 5 (their full workload sizes).
+"""GPU parity at BASELINE.json's configs 1, 3, 4 and 5 (their full workload sizes).
 
 Whole objects at these sizes are far beyond what the list-walking oracle finishes
 (its keyfind / `Acc ++` loops are quadratic), so each test combines
@@ -43,6 +43,93 @@ def window_orddict(cells, e0, key=lambda e: e):
             out.append((key(e), [(tok(e, k), bool((r >> k) & 1)) for k in range(64) if (p >> k) & 1]))
     return out
 
+
+
+# ----------------------------------------------------------------------------- config 1
+
+def _cfg1_terms():
+    """BASELINE configs[0] / SURVEY.md §8d cfg 1: replica A adds 0..9999 with token tA(e);
+    replica B adds them with tB(e) and removes a 10 % subset (seed 1); a second set C of
+    10k ints overlaps the first in 5k."""
+    n = 10_000
+    rng = np.random.default_rng(1)
+    removed = set(int(x) for x in rng.choice(n, n // 10, replace=False))
+    tA = lambda e: b"A" + e.to_bytes(19, "big")     # noqa: E731
+    tB = lambda e: b"B" + e.to_bytes(19, "big")     # noqa: E731
+    tC = lambda e: b"C" + e.to_bytes(19, "big")     # noqa: E731
+    A = [(e, [(tA(e), False)]) for e in range(n)]
+    B = [(e, [(tB(e), e in removed)]) for e in range(n)]
+    C = [(e, [(tC(e), False)]) for e in range(n // 2, n // 2 + n)]
+    return A, B, C
+
+
+def test_config1_terms_merge_union_filter():
+    """BASELINE configs[0] term for term: lasp_orset:merge/2 of the two 10k-element
+    replicas (lasp_orset.erl:128-134) through the drop-in mirror, then the lasp_core
+    union (keep-left orddict:merge, lasp_core.erl:602-627) with the second set and
+    filter(X rem 2 == 0) (lasp_core.erl:681-712, fun from lasp_filter_test.erl:70) run as
+    dataflow processes on the device store and re-run when B is bound; every value is
+    compared with the oracle's merge and bodies."""
+    from lasp_amd import core as dcore, orset as dorset
+    from oracle import orset as oorset, lattice as olat
+    A, B, C = _cfg1_terms()
+    M = oorset.merge(A, B)
+    assert exact_eq(dorset.merge(A, B), M)
+    assert exact_eq(dorset.value(M), oorset.value(M))
+    from lasp_amd import lattice as dlat
+    assert dlat.is_inflation("lasp_orset", A, M) == olat.is_inflation("lasp_orset", A, M)
+    assert dlat.is_strict_inflation("lasp_orset", A, M) is True
+    even = lambda x: x % 2 == 0                    # noqa: E731
+    U = ocore.union_body("lasp_orset", M, C)
+    F = ocore.filter_body("lasp_orset", even, U)
+    # (the oracle Store's quadratic keyfind inflation takes ~400 s at this size, so the
+    # device store is compared with the oracle bodies directly)
+    st = dcore.Store(capacity=64)
+    _, a = st.declare("lasp_orset")
+    _, c = st.declare("lasp_orset")
+    _, u = st.declare("lasp_orset")
+    _, f = st.declare("lasp_orset")
+    st.union(a, c, u)
+    st.filter(u, even, f)
+    st.bind(a, A)
+    st.bind(c, C)
+    st.bind(a, B)                                  # bind = merge(A, B): the config's merge
+    assert exact_eq(st.value(a), M)
+    assert exact_eq(st.value(u), U)
+    assert exact_eq(st.value(f), F)
+    assert len(U) == 15_000 and len(F) == 7_500
+
+
+def test_config1_bench_kernels():
+    """The calls bench.py's config1_gpu times (one 20k-slot replica pair: join, union,
+    filter with the even-slot mask, value/1, is_inflation) against the C orddict
+    restatement on the same synthetic replicas (element e = slot e)."""
+    n = 20_000
+    a, b = ctx_orset(n, 2), ctx_orset(n, 3)
+    ctx = a.ctx
+    tokens = orc.synth_tokens(n)
+    oa = orc.ORDict.from_cells(orc.synth_orset(2, 0, n), tokens)
+    ob = orc.ORDict.from_cells(orc.synth_orset(3, 0, n), tokens)
+    m = ctx.orset_batch(1, n).join(a, b)
+    om = oa.merge(ob)
+    assert orc.ORDict.from_cells(m.download()[0], tokens).equal(om)
+    u = ctx.orset_batch(1, n).union(a, b)
+    assert orc.ORDict.from_cells(u.download()[0], tokens).equal(oa.union(ob))
+    keep = np.full(((n + 63) // 64,), 0x5555555555555555, np.uint64)
+    f = ctx.orset_batch(1, n).filter(m, keep)
+    assert orc.ORDict.from_cells(f.download()[0], tokens).equal(om.filter_even())
+    bits = np.unpackbits(m.value_bits()[0].view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(np.nonzero(bits)[0], om.value())
+    assert bool(m.is_inflation_of(a)[0]) == om.is_inflation_of(oa) is True
+    assert bool(m.is_inflation_of(a, strict=True)[0]) == om.is_strict_inflation_of(oa)
+    assert bool(a.is_inflation_of(m)[0]) == oa.is_inflation_of(om)
+
+
+def ctx_orset(n, seed):
+    from lasp_amd.orset import context
+    b = context().orset_batch(1, n)
+    b.fill_synthetic(seed)
+    return b
 
 # ----------------------------------------------------------------------------- config 4
 
@@ -110,6 +197,100 @@ def test_config4_dataflow_full_size(ctx):
     # the kernel refuses aliasing / bad shapes before launching
     with pytest.raises(_lib.LaspjError):
         foldB.gather_inflation(B, comp, foldB)
+
+
+def keyfind_threshold(prev, cur, src, keys, strict):
+    """is_(strict_)inflation(Prev, Cur) (lasp_lattice.erl:153-161, 235-253) of two lists
+    held as cells over the same output slots (list order = slot order, present = p != 0),
+    slot o carrying key keys[o] and the tokens of source slot src[o]: lists:keyfind's
+    first match is the first present Cur slot of each key (np.unique's first index).
+    Tokens of different source slots are different terms (fresh tokens)."""
+    pp, cp = np.nonzero(prev[:, 0])[0], np.nonzero(cur[:, 0])[0]
+    if strict and len(pp) == 0:
+        return len(cp) > 0
+    uk, fi = np.unique(keys[cp], return_index=True)
+    first = cp[fi]
+    pos = np.minimum(np.searchsorted(uk, keys[pp]), max(len(uk) - 1, 0))
+    found = (uk[pos] == keys[pp]) if len(uk) else np.zeros(len(pp), bool)
+    j = first[pos] if len(uk) else np.zeros(len(pp), np.int64)
+    same = src[j] == src[pp]
+    pc, cc = prev[pp], cur[j]
+    ok = found & same & ((pc[:, 0] & ~cc[:, 0]) == 0)
+    infl = bool(ok.all())
+    if not strict:
+        return infl
+    changed = bool((found & (~same | (pc[:, 0] != cc[:, 0]) | (pc[:, 1] != cc[:, 1]))).any())
+    return infl and (changed or len(pp) < len(cp))
+
+
+def test_config4_collapsing_pipeline_full_size(ctx):
+    """BASELINE configs[3]'s shape with a pipeline whose output keys repeat across source
+    elements: map X -> X div 3 (collapsing), filter X rem 3 =/= 0 (drops whole keys), fold
+    X -> [X || _ <- lists:seq(1, X rem 4)] (fan-out 0..3), then the {strict, Prev} read —
+    through the keyed fused kernel (laspj_orset_gather_inflation_keyed, whose composed
+    index has the filter's empty slots).  Checked: cells == the staged gather -> filter ->
+    gather pipeline; thresholds == the keyfind restatement above on sampled replicas
+    (pinned to the oracle lattice in tests/test_gpu_keyed.py); windows == the oracle
+    map / filter / fold bodies."""
+    from lasp_amd.engine import key_chains
+    R, E, T = 1024, 1 << 20, 3
+    e = np.arange(E, dtype=np.int64)
+    key1 = e // 3                                    # map: slot e keeps position, key e div 3
+    keep1 = key1 % 3 != 0                            # filter on the mapped key
+    fan = key1 % 4                                   # fold fan-out per mapped slot
+    f = np.repeat(e, fan).astype(np.uint32)          # fold slot -> mapped slot (list order)
+    okeys = key1[f]
+    comp = np.where(keep1[f], f, 0xFFFFFFFF).astype(np.uint32)
+    chains = key_chains(okeys)
+    n_out = len(f)
+    keepbits = np.packbits(keep1.astype(np.uint8), bitorder="little").view(np.uint64)
+    A, B = ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+    A.fill_synthetic(42, token_slots=T)
+    B.fill_synthetic(43, token_slots=T)
+    B.join(A, B)
+    empty = ctx.orset_batch(1, n_out)
+    foldA = ctx.orset_batch(R, n_out)
+    first = foldA.gather_inflation(A, comp, empty, strict=True, chains=chains)
+    foldB = ctx.orset_batch(R, n_out)
+    flags = foldB.gather_inflation(B, comp, foldA, strict=True, chains=chains)
+    flags_ns = ctx.orset_batch(R, n_out).gather_inflation(B, comp, foldA, strict=False,
+                                                          chains=chains)
+    mapped = ctx.orset_batch(R, E).gather(B, e.astype(np.uint32))
+    filt = ctx.orset_batch(R, E).filter(mapped, keepbits)
+    del mapped
+    ref = ctx.orset_batch(R, n_out).gather(filt, f)
+    del filt
+    assert ref.equal(foldB).all(), "keyed fused output differs from the staged pipeline"
+    del ref
+    for rep in (0, 1, 2, 3, 517, R - 1):
+        pa, pb = foldA.download(rep, 1)[0], foldB.download(rep, 1)[0]
+        assert first[rep] == keyfind_threshold(np.zeros_like(pa), pa, comp, okeys, True)
+        assert flags[rep] == keyfind_threshold(pa, pb, comp, okeys, True), rep
+        assert flags_ns[rep] == keyfind_threshold(pa, pb, comp, okeys, False), rep
+    # a collapsing map makes keyfind compare entries of different source elements, so
+    # B over A is rarely an inflation here, unlike the slot-wise reading
+    assert not flags_ns.all()
+    div3 = lambda x: x // 3                          # noqa: E731
+    drop3 = lambda x: x % 3 != 0                     # noqa: E731
+    fanf = lambda x: [x] * (x % 4)                   # noqa: E731
+    K = 48
+    for rep in (0, 517, R - 1):
+        for e0 in (0, 333_333, E - K):
+            src = orc.synth_orset_t(43, rep, e0, K, T)
+            srcA = orc.synth_orset_t(42, rep, e0, K, T)
+            merged = [(int(x) | int(y), int(z) | int(w)) for (x, z), (y, w) in zip(src, srcA)]
+            want = ocore.fold_body("lasp_orset", fanf, ocore.filter_body(
+                "lasp_orset", drop3, ocore.map_body("lasp_orset", div3, window_orddict(merged, e0))))
+            lo, hi = np.searchsorted(f, e0), np.searchsorted(f, e0 + K)
+            cells = foldB.download(rep, 1)[0, lo:hi]
+            got = []
+            for o, (p, r) in enumerate(cells):
+                p, r = int(p), int(r)
+                if p:
+                    se = int(f[lo + o])
+                    got.append((se // 3, [(tok(se, k), bool((r >> k) & 1))
+                                          for k in range(64) if (p >> k) & 1]))
+            assert exact_eq(got, want), (rep, e0)
 
 
 # ----------------------------------------------------------------------------- config 5

@@ -195,7 +195,7 @@ def test_orset_reduce_all_kernels(ctx, e_n):
 @pytest.mark.parametrize("nchunks", [1, 2, 3, 5, 8])
 def test_reduce_chunks_every_kind(ctx, nchunks):
     """laspj_batch_reduce_chunks (the anti-entropy reduce of an all-to-all receive
-    buffer, gossip.DeviceAntiEntropy) is the kind's join over the chunk-major copies:
+    buffer) is the kind's join over the chunk-major copies:
     OR for OR-Set cells and G-Set words (odd word counts take the 8-byte kernel), the
     per-actor max for riak_dt_gcounter counts."""
     from lasp_amd._lib import TUNE_REDUCE_KERNEL

@@ -122,3 +122,25 @@ def test_store_bind_many_vs_sequential_oracle(batch):
     for a, b in zip(idd, ido):
         assert exact_eq(ds.value(a), os_.value(b))
     assert ds.ctx.pool_hits > 0
+
+
+def test_bind_many_generator_and_failure_propagation():
+    """bind_many reads a generator of pairs once and still answers every pair; writes
+    that landed before a failing pair reach their processes."""
+    from lasp_amd import core as dcore
+    t1, t2, t3 = (bytes([k]) * 20 for k in (1, 2, 3))
+    st_ = dcore.Store(capacity=64)
+    _, a = st_.declare("lasp_orset")
+    _, m = st_.declare("lasp_orset")
+    st_.update(a, ("add_by_token", t1, 1), None)
+    st_.map(a, lambda x: x * 2, m)
+    res = st_.bind_many(p for p in [(a, [(2, [(t2, False)])])])
+    assert [r[1][0] for r in res] == [a]
+    assert st_.type_value(m) == [2, 4]
+    _, b = st_.declare("lasp_orset")                # empty: bound through bind/3 at once
+    _, mb = st_.declare("lasp_orset")
+    st_.map(b, lambda x: x + 100, mb)
+    with pytest.raises(KeyError):
+        st_.bind_many([(b, [(5, [(t3, False)])]), (b"undeclared", [])])
+    assert st_.type_value(b) == [5]
+    assert st_.type_value(mb) == [105]

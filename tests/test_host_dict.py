@@ -165,3 +165,58 @@ def test_dict_statuses(lib):
     st2 = np.zeros((1,), np.int32)
     assert lib.laspj_dict_add(d.h, _lib.KIND_GCOUNTER, good, np.array([0, len(good)],
                               np.uint64).ctypes.data, 1, -1, st2.ctypes.data) == _lib.E_KIND
+
+
+def test_dict_encode_rejects_descending_offsets(lib):
+    """laspj_dict_encode checks offsets like laspj_dict_add: a descending pair is
+    LASPJ_E_INVAL, never a read past the blob."""
+    from lasp_amd.hostdict import NativeDict
+    d = NativeDict()
+    p = etf.term_to_binary([(1, [(b"t" * 20, False)])])
+    assert list(d.add(_lib.KIND_ORSET, [p])) == [_lib.DEC_OK]
+    blob = C.create_string_buffer(p, len(p))
+    offs = np.array([len(p), 0], np.uint64)            # offsets[1] < offsets[0]
+    out = np.zeros((1, 2), np.uint64)
+    st_ = np.zeros((1,), np.int32)
+    assert lib.laspj_dict_encode(d.h, _lib.KIND_ORSET, blob, offs.ctypes.data, 1, -1, 1,
+                                 out.ctypes.data, st_.ctypes.data) == _lib.E_INVAL
+    with pytest.raises(_lib.LaspjError):
+        lib_add = lib.laspj_dict_add(d.h, _lib.KIND_ORSET, blob, offs.ctypes.data, 1, -1,
+                                     st_.ctypes.data)
+        _lib.check(lib_add)
+
+
+def test_dict_add_failed_payload_registers_nothing(lib):
+    """A payload that fails (truncated, or an element past 64 tokens) leaves the
+    dictionary exactly as it was: binary_to_term/1 rejects the whole payload, so none of
+    its terms may take an element or token slot."""
+    from lasp_amd.hostdict import NativeDict
+    d = NativeDict()
+    good = etf.term_to_binary([(1, [(b"a" * 20, False)]), (2, [(b"b" * 20, True)])])
+    assert list(d.add(_lib.KIND_ORSET, [good])) == [_lib.DEC_OK]
+    before = d.info()
+    exp_before = d.export(4)
+    # new elements 3, 4 and a new token of 1, then the payload is cut short
+    bad = etf.term_to_binary([(1, [(b"a" * 20, False), (b"c" * 20, False)]),
+                              (3, [(b"d" * 20, False)]), (4, [(b"e" * 20, False)])])
+    for cut in (len(bad) - 1, len(bad) - 9, len(bad) // 2):
+        st_ = d.add(_lib.KIND_ORSET, [bad[:cut]])
+        assert st_[0] == _lib.DEC_MALFORMED
+        assert d.info() == before
+    # 65 distinct tokens for one new element: UNREPRESENTABLE, nothing kept
+    many = etf.term_to_binary([(9, [(bytes([k]) * 20, False) for k in range(65)])])
+    assert d.add(_lib.KIND_ORSET, [many])[0] == _lib.DEC_UNREPRESENTABLE
+    assert d.info() == before
+    exp_after = d.export(4)
+    for x, y in zip(exp_before, exp_after):
+        assert (x == y) if isinstance(x, bytes) else np.array_equal(x, y)
+    # the same terms register normally once the payload is whole, in first-seen order
+    assert d.add(_lib.KIND_ORSET, [bad])[0] == _lib.DEC_OK
+    assert d.info()[0] == 4
+    cells, st2 = d.encode(_lib.KIND_ORSET, [bad], 4)
+    assert st2[0] == _lib.DEC_OK
+    assert int(cells[0, 0]) == 0b11 and int(cells[0, 4]) == 1 and int(cells[0, 6]) == 1
+    # G-Set payloads too
+    g = etf.term_to_binary([100, 200, 300])
+    assert d.add(_lib.KIND_GSET, [g[:-2]])[0] == _lib.DEC_MALFORMED
+    assert d.info()[0] == 4
