@@ -241,8 +241,8 @@ def config1_gpu(ctx):
         out["us_" + name] = (time.perf_counter() - t0) * 1e6 / iters
     out["workload"] = "1 replica pair x 20k element slots, inputs resident in HBM"
     # the same merge as the NIF pays it: two term_to_binary/1 payloads of 10k-element
-    # orddicts (built untimed) -> native dictionary encode (laspj_dict_encode) -> upload ->
-    # k_or16 -> device to_binary -> download of the merged payload
+    # orddicts (built untimed, their terms registered untimed) -> upload -> device
+    # from_binary -> k_or16 -> device to_binary -> download of the merged payload
     from lasp_amd import _lib, etf
     from lasp_amd.engine import ETFDict
     from lasp_amd.hostdict import NativeDict
@@ -256,19 +256,76 @@ def config1_gpu(ctx):
     na, nb, nc = ctx.orset_batch(1, E), ctx.orset_batch(1, E), ctx.orset_batch(1, E)
     host = np.zeros((2, 2 * E), np.uint64)
 
-    def e2e():
+    def e2e_host_encode():
         cells, st = nd.encode(_lib.KIND_ORSET, [pa, pb], E, out=host)
         na.upload(cells[0])
         nb.upload(cells[1])
         nc.join(na, nb)
         return nc.to_binaries(d)[0]
-    e2e()
+
+    # the NIF's path when the dictionary already holds every term:
+    # the two payloads go to the device as they are and are decoded there
+    # (laspj_orset_etf_read); only a payload with a term the dictionary lacks
+    # (LASPJ_DEC_UNKNOWN_TERM) would take laspj_dict_add + laspj_dict_encode.  Buffers
+    # are the NIF's, allocated once.
+    import ctypes as C
+    blob = np.frombuffer(pa + pb, np.uint8)
+    offs = np.array([0, len(pa), len(pa) + len(pb)], np.uint64)
+    pay, poff = ctx.buffer(len(blob)), ctx.buffer(24)
+    ab = ctx.orset_batch(2, E)
+    a0, b0 = ab.view(0, 1), ab.view(1, 1)
+    stb, oo = ctx.buffer(8), ctx.buffer(16)
+    ob = ctx.buffer(len(blob) + 64)            # a merge is never longer than both inputs
+    total = C.c_uint64()
+
+    def e2e():
+        pay.upload(blob)
+        poff.upload(offs)
+        check(L.laspj_orset_etf_read(ctx.h, ab.h, d.h, -1, 1, pay.h, poff.h, stb.h), ctx.h)
+        check(L.laspj_orset_join(ctx.h, nc.h, a0.h, b0.h), ctx.h)
+        check(L.laspj_orset_etf_size(ctx.h, nc.h, d.h, -1, oo.h, C.byref(total)), ctx.h)
+        check(L.laspj_orset_etf_write(ctx.h, nc.h, d.h, -1, 1, oo.h, ob.h), ctx.h)
+        if stb.download(np.int32, count=2).any():
+            raise RuntimeError("config1 e2e: a payload did not decode")
+        return ob.download(np.uint8, count=total.value).tobytes()
+
+    ref = e2e_host_encode()
+    if e2e() != ref:
+        raise RuntimeError("config1 e2e: device-decode path differs from the host encoder")
+    for name, fn in (("us_merge_native_end_to_end", e2e),
+                     ("us_merge_native_host_encode", e2e_host_encode)):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            fn()
+        out[name] = (time.perf_counter() - t0) * 1e6 / 20
+    # where the device-decode path's time goes (one call, synchronised per stage)
+    stages = {}
     t0 = time.perf_counter()
-    for _ in range(5):
-        e2e()
-    out["us_merge_native_end_to_end"] = (time.perf_counter() - t0) * 1e6 / 5
-    out["end_to_end"] = ("2 x 10k-element term_to_binary payloads: native encode + upload + "
-                         "join + device to_binary + download")
+    pay.upload(blob)
+    poff.upload(offs)
+    t1 = time.perf_counter()
+    check(L.laspj_orset_etf_read(ctx.h, ab.h, d.h, -1, 1, pay.h, poff.h, stb.h), ctx.h)
+    ctx.synchronize()
+    t2 = time.perf_counter()
+    check(L.laspj_orset_join(ctx.h, nc.h, a0.h, b0.h), ctx.h)
+    ctx.synchronize()
+    t3 = time.perf_counter()
+    check(L.laspj_orset_etf_size(ctx.h, nc.h, d.h, -1, oo.h, C.byref(total)), ctx.h)
+    check(L.laspj_orset_etf_write(ctx.h, nc.h, d.h, -1, 1, oo.h, ob.h), ctx.h)
+    ctx.synchronize()
+    t4 = time.perf_counter()
+    stb.download(np.int32, count=2)
+    ob.download(np.uint8, count=total.value)
+    t5 = time.perf_counter()
+    for k, (u, v) in zip(("upload", "from_binary", "join", "to_binary", "download"),
+                         ((t0, t1), (t1, t2), (t2, t3), (t3, t4), (t4, t5))):
+        stages[k] = (v - u) * 1e6
+    out["end_to_end_stages_us"] = stages
+    out["end_to_end"] = ("2 x 10k-element term_to_binary payloads (%d B): upload + device "
+                         "from_binary + join + device to_binary + download of the %d-byte "
+                         "merged payload; us_merge_native_host_encode: host dictionary encode "
+                         "instead of the device decoder" % (len(blob), total.value))
     return out
 
 

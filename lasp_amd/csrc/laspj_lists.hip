@@ -21,6 +21,7 @@
 // slot), so a comparison is one integer compare and `==` is rank equality.
 
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "laspj_internal.h"
@@ -258,23 +259,282 @@ __global__ __launch_bounds__(64) void k_list_from_set(const u64* src, uint64_t w
     finish(out, r, n, nt, WRITE, need, flag);
 }
 
+// ---------------------------------------------------------------- merges
 // lasp_orset:merge/2 (MODE 0), the OR-Set union body = orddict:merge keeping the left
-// value (MODE 1), lasp_gset:merge/2 = OTP 17 ordsets:union (MODE 2)
-template <int MODE, bool WRITE>
-__global__ __launch_bounds__(64) void k_list_merge(LV a, LV b, LV out, RK rk, u64* sa, u64* sb,
-                                                   u64* plan, uint32_t* need) {
-    __shared__ uint32_t s_nout;
-    const u64 r = blockIdx.x;
-    const uint32_t na = a.n(r), nb = b.n(r);
-    sa += r * a.ce;
-    sb += r * b.ce;
-    plan += r * ((u64)a.ce + b.ce);
-    const u64* KA = a.K(r);
-    const u64* KB = b.K(r);
-    for (uint32_t i = lane_id(); i < na; i += 64) sa[i] = key_ord(KA[i], rk);
-    for (uint32_t j = lane_id(); j < nb; j += 64) sb[j] = key_ord(KB[j], rk);
+// value (MODE 1), lasp_gset:merge/2 = OTP 17 ordsets:union (MODE 2).
+//
+// The reference runs a two-finger walk.  Its outer chain is sequential only when keys do
+// not ascend: on lists whose key ranks are non-decreasing (every canonical value, an
+// intersection output, a filter or monotone map of one) the walk passes through the
+// point (i(v), j(v)) = (first index of A with key >= v, same in B) for EVERY key v — all
+// keys below v are consumed before any key >= v.  So the walk splits at such points into
+// independent pieces: merge-path diagonals (A first on ties) moved back to the first
+// element equal to the smallest unconsumed key.  A block owns a tile of kMTile diagonal
+// steps (its window staged in LDS), each thread a sub-piece of it; counts go through
+// block scans and a per-replica scan of tile totals.  Within a key, the walk pairs the
+// k-th copy of A with the k-th copy of B and emits the longer side's surplus alone, as
+// the clauses do.  ordsets:union's argument switch only decides which side's item a
+// pair emits: after a single-side step the walk's first argument is that side (a
+// smaller head of the second argument makes it switch; a smaller head of the first
+// keeps it), so the item of a pair is the side of the last single step before it (A
+// at the start) — carried across threads and tiles by "last non-none" scans.
+// Replicas whose ranks descend anywhere take the lane-0 walk (k_merge_serial).
+// Token runs of the planned entries (inner orddict:merge with `or`, or a copy) are then
+// counted, scanned and written one entry per thread over the whole grid.
+
+constexpr uint32_t kMT = 256;           // threads per block of the merge kernels
+constexpr uint32_t kMTile = 2048;       // diagonal steps per tile
+constexpr uint32_t kMWin = 4096;        // LDS window (u64) for a tile's A and B keys
+
+struct MS {
+    u64* sa;           // [R][ce_a] key ranks of A
+    u64* sb;           // [R][ce_b]
+    u64* plan;         // [R][ce_a + ce_b] output entries: ia | jb << 32 (MODE 0/1),
+                       //                 idx | side << 32 (MODE 2)
+    uint32_t* tcnt;    // [R][ce_a + ce_b] tokens per output entry
+    uint32_t* tile;    // [R][ntiles] entries per tile -> exclusive offsets
+    uint32_t* tside;   // [R][ntiles] MODE 2: last single side in the tile -> side at its start
+    uint32_t* chunk;   // [R][nchunks] tokens per chunk of kMT entries -> exclusive offsets
+    uint32_t* nout;    // [R] output entries
+    uint32_t* ntok;    // [R] output tokens
+    uint32_t* unsorted;// [R] 1: a side's ranks descend somewhere (lane-0 walk)
+    uint32_t ce_a, ce_b, ntiles, nchunks;
+};
+
+// exclusive prefix sum / running max over a block of kMT threads (s_w: kMT/64 words)
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* total, uint32_t* s_w) {
+    uint32_t wt;
+    const uint32_t x = wave_excl(v, &wt), w = threadIdx.x >> 6;
     __syncthreads();
-    if (lane_id() == 0) {
+    if (lane_id() == 0) s_w[w] = wt;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMT / 64; ++k) {
+        base += k < w ? s_w[k] : 0u;
+        tot += s_w[k];
+    }
+    *total = tot;
+    return base + x;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_max(uint32_t v, uint32_t* all) {
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane_id() >= off) x = x > y ? x : y;
+    }
+    *all = __shfl(x, 63, 64);
+    const uint32_t e = __shfl_up(x, 1, 64);
+    return lane_id() ? e : 0u;
+}
+
+__device__ __forceinline__ uint32_t block_excl_max(uint32_t v, uint32_t* all, uint32_t* s_w) {
+    uint32_t wa;
+    const uint32_t x = wave_excl_max(v, &wa), w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane_id() == 0) s_w[w] = wa;
+    __syncthreads();
+    uint32_t base = 0, mx = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMT / 64; ++k) {
+        if (k < w) base = base > s_w[k] ? base : s_w[k];
+        mx = mx > s_w[k] ? mx : s_w[k];
+    }
+    *all = mx;
+    return base > x ? base : x;
+}
+
+// first index in X[lo, hi) whose key is >= v (hi when none)
+__device__ __forceinline__ uint32_t lower_bound(const u64* X, uint32_t lo, uint32_t hi, u64 v) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (X[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// the merge-path point on diagonal d of non-decreasing X[0, nx), Y[0, ny) (A first on
+// ties), moved back to (i(v), j(v)) for the smallest unconsumed key v: a point the
+// two-finger walk passes through
+__device__ void mp_split(const u64* X, uint32_t nx, const u64* Y, uint32_t ny, uint32_t d,
+                         uint32_t* pi, uint32_t* pj) {
+    uint32_t lo = d > ny ? d - ny : 0, hi = d < nx ? d : nx;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (X[mid] <= Y[d - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint32_t i = lo, j = d - lo;
+    if (i >= nx && j >= ny) {
+        *pi = nx;
+        *pj = ny;
+        return;
+    }
+    const u64 v = i >= nx ? Y[j] : (j >= ny ? X[i] : (X[i] < Y[j] ? X[i] : Y[j]));
+    *pi = lower_bound(X, 0, i, v);
+    *pj = lower_bound(Y, 0, j, v);
+}
+
+// key ranks of both sides, and whether either descends
+__global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, uint64_t R) {
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t na = a.n(r), nb = b.n(r);
+        const uint32_t i = blockIdx.x * kMT + threadIdx.x;
+        bool desc = false;
+        if (i < na) {
+            const u64 x = key_ord(a.K(r)[i], rk);
+            m.sa[r * m.ce_a + i] = x;
+            desc |= i > 0 && key_ord(a.K(r)[i - 1], rk) > x;
+        }
+        if (i < nb) {
+            const u64 y = key_ord(b.K(r)[i], rk);
+            m.sb[r * m.ce_b + i] = y;
+            desc |= i > 0 && key_ord(b.K(r)[i - 1], rk) > y;
+        }
+        if (__syncthreads_or(desc) && threadIdx.x == 0) atomicOr(m.unsorted + r, 1u);
+    }
+}
+
+// one tile of the merge path per block: WRITE = false counts the tile's entries (and,
+// MODE 2, its last single side); WRITE = true writes its plan entries
+template <int MODE, bool WRITE>
+__global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t R) {
+    __shared__ u64 s_win[kMWin];
+    __shared__ uint32_t s_si[kMT + 1], s_sj[kMT + 1], s_last[kMT], s_w[kMT / 64], s_b[4];
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t na = a.n(r), nb = b.n(r), n = na + nb;
+        const uint32_t d0 = blockIdx.x * kMTile;
+        if (m.unsorted[r] || d0 >= n) continue;              // uniform over the block
+        const u64* X = m.sa + r * m.ce_a;
+        const u64* Y = m.sb + r * m.ce_b;
+        if (threadIdx.x == 0) {
+            mp_split(X, na, Y, nb, d0, s_b, s_b + 1);
+            mp_split(X, na, Y, nb, d0 + kMTile < n ? d0 + kMTile : n, s_b + 2, s_b + 3);
+        }
+        __syncthreads();
+        const uint32_t i0 = s_b[0], j0 = s_b[1];
+        const uint32_t wa = s_b[2] - i0, wb = s_b[3] - j0, w = wa + wb;
+        const u64* WX = X + i0;
+        const u64* WY = Y + j0;
+        if (w <= kMWin) {                                    // stage the window in LDS
+            for (uint32_t k = threadIdx.x; k < wa; k += kMT) s_win[k] = WX[k];
+            for (uint32_t k = threadIdx.x; k < wb; k += kMT) s_win[wa + k] = WY[k];
+            WX = s_win;
+            WY = s_win + wa;
+        }
+        __syncthreads();
+        {
+            uint32_t si, sj;
+            mp_split(WX, wa, WY, wb, (uint32_t)((u64)threadIdx.x * w / kMT), &si, &sj);
+            s_si[threadIdx.x] = si;
+            s_sj[threadIdx.x] = sj;
+            if (threadIdx.x == 0) {
+                s_si[kMT] = wa;
+                s_sj[kMT] = wb;
+            }
+        }
+        __syncthreads();
+        const uint32_t ei = s_si[threadIdx.x + 1], ej = s_sj[threadIdx.x + 1];
+        // pass 1: count and the last single-event side (1 = A, 2 = B)
+        uint32_t i = s_si[threadIdx.x], j = s_sj[threadIdx.x], c = 0, last = 0;
+        while (i < ei || j < ej) {
+            if (i < ei && j < ej) {
+                const u64 x = WX[i], y = WY[j];
+                if (x < y) ++i, last = 1;
+                else if (x > y) ++j, last = 2;
+                else ++i, ++j;
+            } else if (i < ei) {
+                ++i, last = 1;
+            } else {
+                ++j, last = 2;
+            }
+            ++c;
+        }
+        uint32_t total;
+        const uint32_t base = block_excl(c, &total, s_w);
+        uint32_t* tile = m.tile + r * m.ntiles + blockIdx.x;
+        uint32_t* tside = m.tside + r * m.ntiles + blockIdx.x;
+        if (MODE == 2) s_last[threadIdx.x] = last;
+        uint32_t lastidx;
+        const uint32_t prev = MODE == 2 ? block_excl_max(last ? threadIdx.x + 1 : 0u, &lastidx, s_w)
+                                        : 0u;
+        if (!WRITE) {
+            if (threadIdx.x == 0) {
+                *tile = total;
+                if (MODE == 2) *tside = lastidx ? s_last[lastidx - 1] : 0u;
+            }
+            __syncthreads();
+            continue;
+        }
+        // pass 2: the plan entries, at the tile's offset
+        u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b) + *tile + base;
+        uint32_t side = MODE == 2 ? (prev ? s_last[prev - 1] : *tside) : 0u;
+        i = s_si[threadIdx.x], j = s_sj[threadIdx.x];
+        for (uint32_t k = 0; k < c; ++k) {
+            u64 e;
+            if (i < ei && j < ej && WX[i] == WY[j]) {
+                if (MODE == 2) e = side == 2 ? (u64)(j0 + j) | (1ull << 32) : (u64)(i0 + i);
+                else e = (u64)(i0 + i) | ((u64)(j0 + j) << 32);
+                ++i, ++j;
+            } else if (i < ei && (j >= ej || WX[i] < WY[j])) {
+                e = MODE == 2 ? (u64)(i0 + i) : (u64)(i0 + i) | ((u64)kNone << 32);
+                ++i, side = 1;
+            } else {
+                e = MODE == 2 ? (u64)(j0 + j) | (1ull << 32) : (u64)kNone | ((u64)(j0 + j) << 32);
+                ++j, side = 2;
+            }
+            plan[k] = e;
+        }
+        __syncthreads();
+    }
+}
+
+// per replica: exclusive offsets of the tile counts, the output entry count, and (MODE 2)
+// the pair side at every tile's start (the last single side before it, A at the start)
+template <int MODE>
+__global__ __launch_bounds__(kMT) void k_merge_tile_scan(LV a, LV b, MS m, uint64_t R) {
+    __shared__ uint32_t s_w[kMT / 64], s_sd[kMT];
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
+        if (m.unsorted[r]) continue;
+        const uint32_t n = a.n(r) + b.n(r), nt = (n + kMTile - 1) / kMTile;
+        uint32_t* tile = m.tile + r * m.ntiles;
+        uint32_t* tside = m.tside + r * m.ntiles;
+        uint32_t carry = 0, side = 1;
+        for (uint32_t c0 = 0; c0 < nt; c0 += kMT) {
+            const uint32_t k = c0 + threadIdx.x;
+            const uint32_t v = k < nt ? tile[k] : 0u;
+            uint32_t tot;
+            const uint32_t off = carry + block_excl(v, &tot, s_w);
+            uint32_t mx = 0, pv = 0;
+            if (MODE == 2) {
+                const uint32_t sd = k < nt ? tside[k] : 0u;
+                s_sd[threadIdx.x] = sd;                      // the tiles' own last sides
+                pv = block_excl_max(sd ? threadIdx.x + 1 : 0u, &mx, s_w);
+            }
+            if (k < nt) {
+                tile[k] = off;
+                if (MODE == 2) tside[k] = pv ? s_sd[pv - 1] : side;
+            }
+            if (MODE == 2 && mx) side = s_sd[mx - 1];
+            carry += tot;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) m.nout[r] = carry;
+    }
+}
+
+// replicas whose keys do not ascend: the clauses' walk on lane 0 (over precomputed ranks)
+template <int MODE>
+__global__ __launch_bounds__(64) void k_merge_serial(LV a, LV b, MS m, uint64_t R) {
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
+        if (!m.unsorted[r] || lane_id() != 0) continue;
+        const uint32_t na = a.n(r), nb = b.n(r);
+        const u64* sa = m.sa + r * m.ce_a;
+        const u64* sb = m.sb + r * m.ce_b;
+        u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
         uint32_t o = 0, i = 0, j = 0;
         if (MODE != 2) {
             // merge(F,[{K1,_}=E1|D1],[{K2,_}=E2|D2]) when K1 < K2 -> [E1|merge(F,D1,[E2|D2])];
@@ -316,61 +576,117 @@ __global__ __launch_bounds__(64) void k_list_merge(LV a, LV b, LV out, RK rk, u6
             for (; i < nx; ++i) plan[o++] = (u64)i | ((u64)sx << 32);
             for (; j < ny; ++j) plan[o++] = (u64)j | ((u64)sy << 32);
         }
-        s_nout = o;
+        m.nout[r] = o;
     }
-    __syncthreads();
-    const uint32_t nout = s_nout;
-    const u64* TA = a.T(r);
-    const u64* TB = b.T(r);
+}
+
+// the token count of planned entry o (inner orddict:merge, or the run it copies)
+template <int MODE>
+__device__ __forceinline__ uint32_t entry_tokens(const LV& a, const LV& b, u64 r, u64 p,
+                                                 const RK& rk, uint32_t* ia, uint32_t* jb) {
+    *ia = kNone, *jb = kNone;
+    if (MODE == 2) {
+        if (p >> 32) *jb = (uint32_t)p;
+        else *ia = (uint32_t)p;
+        return 0;
+    }
+    *ia = (uint32_t)p;
+    *jb = (uint32_t)(p >> 32);
     const uint32_t* OA = a.O(r);
     const uint32_t* OB = b.O(r);
-    uint32_t nt = 0;
-    for (uint32_t c = 0; c < nout; c += 64) {
-        const uint32_t o = c + lane_id();
-        uint32_t ia = kNone, jb = kNone, cnt = 0;
+    if (*ia != kNone && *jb != kNone)
+        return MODE == 0 ? inner_merge<false>(a.T(r) + OA[*ia], OA[*ia + 1] - OA[*ia],
+                                              b.T(r) + OB[*jb], OB[*jb + 1] - OB[*jb], nullptr, rk)
+                         : OA[*ia + 1] - OA[*ia];
+    if (*ia != kNone) return OA[*ia + 1] - OA[*ia];
+    return OB[*jb + 1] - OB[*jb];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kMT) void k_merge_tok_count(LV a, LV b, RK rk, MS m, uint64_t R) {
+    __shared__ uint32_t s_w[kMT / 64];
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t nout = m.nout[r], o0 = blockIdx.x * kMT;
+        if (o0 >= nout) continue;
+        const uint32_t o = o0 + threadIdx.x;
+        uint32_t cnt = 0, ia, jb;
         if (o < nout) {
-            const u64 p = plan[o];
-            if (MODE == 2) {
-                if (p >> 32) jb = (uint32_t)p;
-                else ia = (uint32_t)p;
-            } else {
-                ia = (uint32_t)p;
-                jb = (uint32_t)(p >> 32);
-                if (ia != kNone && jb != kNone) {
-                    cnt = MODE == 0 ? inner_merge<false>(TA + OA[ia], OA[ia + 1] - OA[ia],
-                                                         TB + OB[jb], OB[jb + 1] - OB[jb],
-                                                         nullptr, rk)
-                                    : OA[ia + 1] - OA[ia];
-                } else if (ia != kNone) {
-                    cnt = OA[ia + 1] - OA[ia];
-                } else {
-                    cnt = OB[jb + 1] - OB[jb];
-                }
-            }
+            cnt = entry_tokens<MODE>(a, b, r, m.plan[r * ((u64)m.ce_a + m.ce_b) + o], rk, &ia, &jb);
+            m.tcnt[r * ((u64)m.ce_a + m.ce_b) + o] = cnt;
         }
-        uint32_t tt;
-        const uint32_t tpos = nt + wave_excl(cnt, &tt);
-        if (WRITE && o < nout) {
-            if (o >= out.ce || tpos + cnt > out.ct) {
+        uint32_t tot;
+        block_excl(cnt, &tot, s_w);
+        if (threadIdx.x == 0) m.chunk[r * m.nchunks + blockIdx.x] = tot;
+    }
+}
+
+// per replica: exclusive offsets of the chunk token counts; need = {entries, tokens}
+__global__ __launch_bounds__(kMT) void k_merge_chunk_scan(MS m, uint64_t R, uint32_t* need) {
+    __shared__ uint32_t s_w[kMT / 64];
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
+        const uint32_t nc = (m.nout[r] + kMT - 1) / kMT;
+        uint32_t* ch = m.chunk + r * m.nchunks;
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < nc; c0 += kMT) {
+            const uint32_t k = c0 + threadIdx.x;
+            uint32_t tot;
+            const uint32_t off = carry + block_excl(k < nc ? ch[k] : 0u, &tot, s_w);
+            if (k < nc) ch[k] = off;
+            carry += tot;
+        }
+        if (threadIdx.x == 0) {
+            m.ntok[r] = carry;
+            need[2 * r] = m.nout[r];
+            need[2 * r + 1] = carry;
+        }
+    }
+}
+
+// the write pass: one planned entry per thread
+template <int MODE>
+__global__ __launch_bounds__(kMT) void k_merge_write(LV a, LV b, LV out, RK rk, MS m, uint64_t R) {
+    __shared__ uint32_t s_w[kMT / 64];
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t nout = m.nout[r], nt = m.ntok[r], o0 = blockIdx.x * kMT;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (nout > out.ce || nt > out.ct) {
                 lraise(rk.flag, kErrRange);
             } else {
-                out.K(r)[o] = ia != kNone ? KA[ia] : KB[jb];
-                if (MODE != 2) {
-                    out.O(r)[o] = tpos;
-                    u64* to = out.T(r) + tpos;
-                    if (MODE == 0 && ia != kNone && jb != kNone) {
-                        inner_merge<true>(TA + OA[ia], OA[ia + 1] - OA[ia], TB + OB[jb],
-                                          OB[jb + 1] - OB[jb], to, rk);
-                    } else {
-                        const u64* from = ia != kNone ? TA + OA[ia] : TB + OB[jb];
-                        for (uint32_t k = 0; k < cnt; ++k) to[k] = from[k];
-                    }
-                }
+                out.hdr[2 * r] = nout;
+                out.hdr[2 * r + 1] = nt;
+                if (MODE != 2) out.O(r)[nout] = nt;
             }
         }
-        nt += tt;
+        if (o0 >= nout || nout > out.ce || nt > out.ct) continue;
+        const uint32_t o = o0 + threadIdx.x;
+        const u64 row = r * ((u64)m.ce_a + m.ce_b);
+        const uint32_t cnt = o < nout ? m.tcnt[row + o] : 0u;
+        uint32_t tot;
+        const uint32_t tpos = m.chunk[r * m.nchunks + blockIdx.x] + block_excl(cnt, &tot, s_w);
+        if (o >= nout) continue;
+        uint32_t ia, jb;
+        const u64 p = m.plan[row + o];
+        if (MODE == 2) {
+            if (p >> 32) jb = (uint32_t)p, ia = kNone;
+            else ia = (uint32_t)p, jb = kNone;
+        } else {
+            ia = (uint32_t)p;
+            jb = (uint32_t)(p >> 32);
+        }
+        out.K(r)[o] = ia != kNone ? a.K(r)[ia] : b.K(r)[jb];
+        if (MODE == 2) continue;
+        out.O(r)[o] = tpos;
+        u64* to = out.T(r) + tpos;
+        const uint32_t* OA = a.O(r);
+        const uint32_t* OB = b.O(r);
+        if (MODE == 0 && ia != kNone && jb != kNone) {
+            inner_merge<true>(a.T(r) + OA[ia], OA[ia + 1] - OA[ia], b.T(r) + OB[jb],
+                              OB[jb + 1] - OB[jb], to, rk);
+        } else {
+            const u64* from = ia != kNone ? a.T(r) + OA[ia] : b.T(r) + OB[jb];
+            for (uint32_t k = 0; k < cnt; ++k) to[k] = from[k];
+        }
     }
-    finish(out, r, nout, nt, WRITE, need, rk.flag);
 }
 
 // `case Value0 of Value` (=:=): same entries, keys, token runs and flags
@@ -1081,27 +1397,74 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     if (int s = ranks(ctx, ord, !gs, &rk, what)) return s;
     LGuard g(ctx);
     const uint64_t R = a->replicas;
-    const uint64_t sa_b = R * 8ull * a->cap_e, sb_b = R * 8ull * b->cap_e;
-    const uint64_t pl_b = R * 8ull * ((uint64_t)a->cap_e + b->cap_e);
-    char* base = static_cast<char*>(lscratch(ctx, sa_b + sb_b + pl_b + 8ull * R));
+    const uint64_t ce = (uint64_t)a->cap_e + b->cap_e;
+    if (ce > 0xFFFFFFF0ull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
+    MS m;
+    m.ce_a = a->cap_e;
+    m.ce_b = b->cap_e;
+    m.ntiles = (uint32_t)((ce + kMTile - 1) / kMTile);
+    m.nchunks = (uint32_t)((ce + kMT - 1) / kMT);
+    // scratch: ranks, plan, token counts, tile / chunk scans, per-replica words
+    const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
+                   sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
+                   sz_r = R * 4ull;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 2 * sz_t + sz_c + 4 * sz_r + 8ull * R + 64;
+    char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
-    u64* sa = reinterpret_cast<u64*>(base);
-    u64* sb = reinterpret_cast<u64*>(base + sa_b);
-    u64* plan = reinterpret_cast<u64*>(base + sa_b + sb_b);
-    auto* need = reinterpret_cast<uint32_t*>(base + sa_b + sb_b + pl_b);
-    const LV A = view(a), B = view(b), nil = view(dst);
-#define LJ_MERGE(MODE, W, OUT)                                                              \
-    hipLaunchKernelGGL((k_list_merge<MODE, W>), dim3(R), dim3(64), 0, ctx->stream, A, B, OUT, \
-                       rk, sa, sb, plan, need)
+    char* q = base;
+    auto take = [&](uint64_t bytes) {
+        char* p = q;
+        q += (bytes + 7) & ~7ull;
+        return p;
+    };
+    m.sa = reinterpret_cast<u64*>(take(sz_sa));
+    m.sb = reinterpret_cast<u64*>(take(sz_sb));
+    m.plan = reinterpret_cast<u64*>(take(sz_pl));
+    m.tcnt = reinterpret_cast<uint32_t*>(take(sz_tc));
+    m.tile = reinterpret_cast<uint32_t*>(take(sz_t));
+    m.tside = reinterpret_cast<uint32_t*>(take(sz_t));
+    m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
+    m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
+    m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
+    m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r));
+    auto* need = reinterpret_cast<uint32_t*>(take(8ull * R));
+    const LV A = view(a), B = view(b);
+    const unsigned ry = (unsigned)(R < 65535 ? R : 65535);
+    const unsigned rx = (unsigned)(R < (1u << 20) ? R : (1u << 20));
+    const uint32_t cmax = m.ce_a > m.ce_b ? m.ce_a : m.ce_b;
+    const unsigned gr = cmax ? (cmax + kMT - 1) / kMT : 1u;
+    auto size_pass = [&](auto mode) {
+        constexpr int MODE = decltype(mode)::value;
+        hipMemsetAsync(m.unsorted, 0, sz_r, ctx->stream);
+        hipLaunchKernelGGL(k_merge_ranks, dim3(gr, ry), dim3(kMT), 0, ctx->stream, A, B,
+                           rk, m, R);
+        hipLaunchKernelGGL((k_merge_tiles<MODE, false>), dim3(m.ntiles ? m.ntiles : 1, ry),
+                           dim3(kMT), 0, ctx->stream, A, B, m, R);
+        hipLaunchKernelGGL((k_merge_tile_scan<MODE>), dim3(rx), dim3(kMT), 0, ctx->stream, A, B,
+                           m, R);
+        hipLaunchKernelGGL((k_merge_serial<MODE>), dim3(rx), dim3(64), 0, ctx->stream, A, B, m, R);
+        hipLaunchKernelGGL((k_merge_tiles<MODE, true>), dim3(m.ntiles ? m.ntiles : 1, ry),
+                           dim3(kMT), 0, ctx->stream, A, B, m, R);
+        hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),
+                           dim3(kMT), 0, ctx->stream, A, B, rk, m, R);
+        hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R, need);
+    };
+    auto write_pass = [&](auto mode, LV out) {
+        constexpr int MODE = decltype(mode)::value;
+        hipLaunchKernelGGL((k_merge_write<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry), dim3(kMT),
+                           0, ctx->stream, A, B, out, rk, m, R);
+    };
+    using M0 = std::integral_constant<int, 0>;
+    using M1 = std::integral_constant<int, 1>;
+    using M2 = std::integral_constant<int, 2>;
     if (gs)
-        return sized(ctx, dst, need, [&] { LJ_MERGE(2, false, nil); },
-                     [&](LV out) { LJ_MERGE(2, true, out); }, what);
+        return sized(ctx, dst, need, [&] { size_pass(M2{}); },
+                     [&](LV out) { write_pass(M2{}, out); }, what);
     if (keep_left)
-        return sized(ctx, dst, need, [&] { LJ_MERGE(1, false, nil); },
-                     [&](LV out) { LJ_MERGE(1, true, out); }, what);
-    return sized(ctx, dst, need, [&] { LJ_MERGE(0, false, nil); },
-                 [&](LV out) { LJ_MERGE(0, true, out); }, what);
-#undef LJ_MERGE
+        return sized(ctx, dst, need, [&] { size_pass(M1{}); },
+                     [&](LV out) { write_pass(M1{}, out); }, what);
+    return sized(ctx, dst, need, [&] { size_pass(M0{}); },
+                 [&](LV out) { write_pass(M0{}, out); }, what);
 }
 
 int laspj_list_merge(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,

@@ -84,7 +84,7 @@ def test_config1_terms_merge_union_filter():
     F = ocore.filter_body("lasp_orset", even, U)
     # (the oracle Store's quadratic keyfind inflation takes ~400 s at this size, so the
     # device store is compared with the oracle bodies directly)
-    st = dcore.Store(capacity=64)
+    st = dcore.Store(capacity=1 << 15)             # element slots per variable
     _, a = st.declare("lasp_orset")
     _, c = st.declare("lasp_orset")
     _, u = st.declare("lasp_orset")
