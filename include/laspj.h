@@ -494,6 +494,17 @@ int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_e
 int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict* d,
                          int tag, int vers, const laspj_buf* payload,
                          const laspj_buf* offsets, laspj_buf* status);
+/* from_binary/1 — lasp_gset.erl:122-128 — for a G-Set batch: the payload is <<Tag, Vers>>
+ * (tag >= 0) ++ the external term image of an ordset whose elements are in the dictionary:
+ * [] (NIL_EXT), a LIST_EXT of element images with a [] tail, or STRING_EXT (every element
+ * an integer 0..255, as term_to_binary/1 writes it).  Statuses as for OR-Sets: MALFORMED
+ * when binary_to_term/1 would fail or the term is not a proper list, UNKNOWN_TERM for an
+ * element outside the dictionary or out of strict term order (not an ordset) or a term
+ * kind no dictionary holds (pids, refs, funs, maps, bit strings: the NIF hands such
+ * payloads to binary_to_term/1). */
+int laspj_gset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict* d,
+                        int tag, int vers, const laspj_buf* payload,
+                        const laspj_buf* offsets, laspj_buf* status);
 
 /* ------------------------------------------------------------------ anti-entropy */
 /* Gossip anti-entropy across GPUs over RCCL (xGMI) — the reference's N-way merge and

@@ -169,6 +169,7 @@ SIGNATURES = {
     "laspj_gset_etf_size": (i, [vp, vp, vp, i, vp, C.POINTER(u64)]),
     "laspj_gset_etf_write": (i, [vp, vp, vp, i, i, vp, vp]),
     "laspj_orset_etf_read": (i, [vp, vp, vp, i, i, vp, vp, vp]),
+    "laspj_gset_etf_read": (i, [vp, vp, vp, i, i, vp, vp, vp]),
     "laspj_comm_unique_id": (i, [vp]),
     "laspj_comm_init_rank": (i, [vp, i, vp, i, vpp]),
     "laspj_comm_init_all": (i, [vp, i, vp]),

@@ -75,6 +75,12 @@ struct laspj_etf_dict {
     const uint32_t* rd_htab = nullptr;
     uint32_t rd_hmask = 0;
     uint64_t rd_hlens = 0;                 // bit hl - 1: a header template of hl <= 64 bytes
+    // G-Set from_binary: element image hash (FNV-1a) -> slot + 1; term rank per slot
+    // (equal terms share one); slot + 1 of the SMALL_INTEGER_EXT image of each byte value
+    const uint32_t* gs_htab = nullptr;
+    uint32_t gs_hmask = 0;
+    const uint32_t* gs_rank = nullptr;     // E
+    const uint32_t* gs_byte = nullptr;     // 256
 };
 
 namespace laspj {
@@ -2413,6 +2419,255 @@ int reserve_scratch(laspj_ctx* ctx, uint64_t need) {
     return LASPJ_OK;
 }
 
+// ------------------------------------------------------------------ G-Set from_binary/1
+// lasp_gset:from_binary/1 (lasp_gset.erl:122-128; riak_dt:from_binary = binary_to_term):
+// <<Tag, Vers>> ++ the external term image of an ordset — [] (NIL_EXT), a LIST_EXT of
+// element images with a NIL tail, or STRING_EXT when every element is an integer 0..255
+// (term_to_binary's own choice).  One wave per payload: lane 0 checks the whole term is
+// well-formed (binary_to_term fails first: MALFORMED wins over every later status) and
+// lists element extents into LDS a chunk at a time; lanes then find each element's slot
+// through the image hash, check ranks strictly ascend (an ordset) and set its bit.
+
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+    return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+__device__ __host__ __forceinline__ uint32_t fnv1a(const uint8_t* p, uint32_t n) {
+    uint32_t h = 2166136261u;
+    for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 16777619u;
+    return h;
+}
+
+// extent of the external term at p within n bytes: its length; 0 when it runs past n or
+// is not well-formed; kTermOther when it holds a tag no dictionary term has (pids, refs,
+// funs, maps, bit strings, ...).  Terms are prefix-ordered, so one counter of pending
+// sub-terms replaces a stack.
+constexpr u64 kTermOther = ~0ull;
+
+// well-formed UTF-8 (RFC 3629: no overlong forms, surrogates or code points past
+// U+10FFFF) — binary_to_term/1 rejects ATOM_UTF8_EXT / SMALL_ATOM_UTF8_EXT names that
+// are not
+__device__ bool utf8_ok(const uint8_t* p, u64 n) {
+    u64 i = 0;
+    while (i < n) {
+        const uint8_t c = p[i];
+        if (c < 0x80) {
+            ++i;
+            continue;
+        }
+        uint32_t k;
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) k = 1;
+        else if (c >= 0xE0 && c <= 0xEF) {
+            k = 2;
+            if (c == 0xE0) lo = 0xA0;
+            if (c == 0xED) hi = 0x9F;
+        } else if (c >= 0xF0 && c <= 0xF4) {
+            k = 3;
+            if (c == 0xF0) lo = 0x90;
+            if (c == 0xF4) hi = 0x8F;
+        } else {
+            return false;
+        }
+        if (i + k >= n) return false;                 // continuation bytes run past n
+        if (p[i + 1] < lo || p[i + 1] > hi) return false;
+        for (uint32_t j = 2; j <= k; ++j)
+            if (p[i + j] < 0x80 || p[i + j] > 0xBF) return false;
+        i += 1 + k;
+    }
+    return true;
+}
+
+__device__ u64 etf_term_len(const uint8_t* p, u64 n) {
+    u64 off = 0, pending = 1;
+    while (pending) {
+        if (off >= n) return 0;
+        const uint8_t t = p[off];
+        --pending;
+        switch (t) {
+        case 97: off += 2; break;                                   // SMALL_INTEGER
+        case 98: off += 5; break;                                   // INTEGER
+        case 70: off += 9; break;                                   // NEW_FLOAT
+        case 99: off += 32; break;                                  // FLOAT
+        case 106: off += 1; break;                                  // NIL
+        case 100: case 118: case 107: {                             // ATOM(_UTF8), STRING
+            if (off + 3 > n) return 0;
+            const u64 len = (u64)p[off + 1] << 8 | p[off + 2];
+            if (t == 118 && (off + 3 + len > n || !utf8_ok(p + off + 3, len))) return 0;
+            off += 3 + len;
+            break;
+        }
+        case 115: case 119: {                                       // SMALL_ATOM(_UTF8)
+            if (off + 2 > n) return 0;
+            const u64 len = p[off + 1];
+            if (t == 119 && (off + 2 + len > n || !utf8_ok(p + off + 2, len))) return 0;
+            off += 2 + len;
+            break;
+        }
+        case 110:                                                   // SMALL_BIG
+            if (off + 2 > n) return 0;
+            off += 3 + (u64)p[off + 1];
+            break;
+        case 104:                                                   // SMALL_TUPLE
+            if (off + 2 > n) return 0;
+            pending += p[off + 1];
+            off += 2;
+            break;
+        case 105:                                                   // LARGE_TUPLE
+            if (off + 5 > n) return 0;
+            pending += be32(p + off + 1);
+            off += 5;
+            break;
+        case 108:                                                   // LIST: elements + tail
+            if (off + 5 > n) return 0;
+            pending += (u64)be32(p + off + 1) + 1;
+            off += 5;
+            break;
+        case 109:                                                   // BINARY
+            if (off + 5 > n) return 0;
+            off += 5 + (u64)be32(p + off + 1);
+            break;
+        case 111:                                                   // LARGE_BIG
+            if (off + 6 > n) return 0;
+            off += 6 + (u64)be32(p + off + 1);
+            break;
+        default:
+            return kTermOther;
+        }
+    }
+    return off <= n ? off : 0;
+}
+
+struct GsTabs {
+    const uint8_t* blob;
+    const uint32_t* off;
+    const uint32_t* htab;
+    uint32_t hmask;
+    const uint32_t* rank;
+    const uint32_t* byte_slot;
+    uint32_t E;
+};
+
+// the slot whose image is p[0, n), or kNoSlot
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t gs_slot(const GsTabs& g, const uint8_t* p, uint32_t n) {
+    for (uint32_t i = fnv1a(p, n) & g.hmask;; i = (i + 1) & g.hmask) {
+        const uint32_t v = g.htab[i];
+        if (!v) return kNoSlot;
+        const uint32_t e = v - 1, o = g.off[e];
+        if (g.off[e + 1] - o != n) continue;
+        bool same = true;
+        for (uint32_t k = 0; k < n && same; ++k) same = g.blob[o + k] == p[k];
+        if (same) return e;
+    }
+}
+
+constexpr uint32_t kGChunk = 256;
+
+__global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, const u64* offs,
+                                                      uint64_t R, GsTabs g, int tag, int vers,
+                                                      u64* words, uint64_t W, int32_t* status) {
+    __shared__ uint32_t s_o[kGChunk], s_l[kGChunk];
+    __shared__ u64 s_h[4];
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const uint8_t* p = payload + offs[rep];
+        const u64 n = offs[rep + 1] - offs[rep];
+        u64* w = words + rep * W;
+        if (lane == 0) {
+            // s_h: {status, list tag, element count, first element offset}
+            int st = LASPJ_DEC_OK;
+            u64 h = 0;
+            if (tag >= 0) {
+                if (n < 2 || p[0] != (uint8_t)tag) st = LASPJ_DEC_INVALID_BINARY;
+                else if (p[1] != (uint8_t)vers) st = LASPJ_DEC_UNSUPPORTED_VERSION;
+                h = 2;
+            }
+            if (st == LASPJ_DEC_OK && (n < h + 2 || p[h] != 131)) st = LASPJ_DEC_MALFORMED;
+            u64 lt = 0, cnt = 0, first = 0;
+            if (st == LASPJ_DEC_OK) {
+                const u64 L = etf_term_len(p + h + 1, n - h - 1);
+                if (L == kTermOther) st = LASPJ_DEC_UNKNOWN_TERM;
+                else if (L == 0 || L != n - h - 1) st = LASPJ_DEC_MALFORMED;
+            }
+            if (st == LASPJ_DEC_OK) {
+                lt = p[h + 1];
+                if (lt == 107) cnt = (u64)p[h + 2] << 8 | p[h + 3], first = h + 4;
+                else if (lt == 108) cnt = be32(p + h + 2), first = h + 6;
+                else if (lt != 106) st = LASPJ_DEC_MALFORMED;          // not a list
+            }
+            s_h[0] = (u64)st;
+            s_h[1] = lt;
+            s_h[2] = cnt;
+            s_h[3] = first;
+        }
+        __syncthreads();
+        int st = (int)s_h[0];
+        const uint32_t lt = (uint32_t)s_h[1];
+        const u64 cnt = s_h[2];
+        u64 pos = s_h[3];
+        bool unknown = false;
+        uint32_t prev_rank = 0;
+        bool have_prev = false;
+        if (st == LASPJ_DEC_OK && lt == 107) {
+            // STRING_EXT: every byte is the integer element of that value
+            for (u64 c0 = 0; c0 < cnt; c0 += 64) {
+                const u64 i = c0 + lane;
+                uint32_t slot = kNoSlot, rk = 0;
+                if (i < cnt) {
+                    const uint32_t v = g.byte_slot[p[pos + i]];
+                    slot = v ? v - 1 : kNoSlot;
+                    rk = slot != kNoSlot ? g.rank[slot] : 0;
+                }
+                const uint32_t before = __shfl_up(rk, 1, 64);
+                bool bad = i < cnt && (slot == kNoSlot ||
+                                       (lane ? rk <= before : (have_prev && rk <= prev_rank)));
+                if (i < cnt && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                unknown |= __ballot(bad) != 0;
+                const uint32_t last = (uint32_t)((cnt - c0 < 64 ? cnt - c0 : 64) - 1);
+                prev_rank = __shfl(rk, last, 64);
+                have_prev = true;
+            }
+        } else if (st == LASPJ_DEC_OK && lt == 108) {
+            for (u64 c0 = 0; c0 < cnt; c0 += kGChunk) {
+                const uint32_t m = (uint32_t)(cnt - c0 < kGChunk ? cnt - c0 : kGChunk);
+                if (lane == 0) {                    // element extents (the term is well-formed)
+                    for (uint32_t k = 0; k < m; ++k) {
+                        const u64 L = etf_term_len(p + pos, n - pos);
+                        s_o[k] = (uint32_t)pos;
+                        s_l[k] = (uint32_t)L;
+                        pos += L;
+                    }
+                    s_h[3] = pos;
+                }
+                __syncthreads();
+                pos = s_h[3];
+                for (uint32_t k0 = 0; k0 < m; k0 += 64) {
+                    const uint32_t k = k0 + lane;
+                    uint32_t slot = kNoSlot, rk = 0;
+                    if (k < m) {
+                        slot = s_l[k] <= 0xFFFFFFu ? gs_slot(g, p + s_o[k], s_l[k]) : kNoSlot;
+                        rk = slot != kNoSlot ? g.rank[slot] : 0;
+                    }
+                    const uint32_t before = __shfl_up(rk, 1, 64);
+                    bool bad = k < m && (slot == kNoSlot ||
+                                         (lane ? rk <= before : (have_prev && rk <= prev_rank)));
+                    if (k < m && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                    unknown |= __ballot(bad) != 0;
+                    const uint32_t last = (m - k0 < 64 ? m - k0 : 64) - 1;
+                    prev_rank = __shfl(rk, last, 64);
+                    have_prev = true;
+                }
+                __syncthreads();
+            }
+            if (p[pos] != 106) st = LASPJ_DEC_MALFORMED;       // improper list tail
+        }
+        if (st == LASPJ_DEC_OK && unknown) st = LASPJ_DEC_UNKNOWN_TERM;
+        if (lane == 0) status[rep] = st;
+        __syncthreads();
+    }
+}
+
 int check_args(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
                const char* what) {
     if (!ctx || !b || b->ctx != ctx || !d || d->ctx != ctx)
@@ -2651,6 +2906,42 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     return LASPJ_OK;
 }
 
+int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+                  const laspj_buf* payload, const laspj_buf* offsets, laspj_buf* status) {
+    const char* what = "gset_etf_read";
+    if (int s = check_args(ctx, b, d, LASPJ_KIND_GSET, what)) return s;
+    if (!payload || payload->ctx != ctx || !offsets || offsets->ctx != ctx || !status ||
+        status->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "%s: bad buffer", what);
+    if (offsets->bytes < 8ull * (b->replicas + 1) || status->bytes < 4ull * b->replicas)
+        return fail(ctx, LASPJ_E_RANGE, "%s: offsets must hold R + 1 uint64, status R int32",
+                    what);
+    if (tag > 255 || vers < 0 || vers > 255)
+        return fail(ctx, LASPJ_E_INVAL, "%s: tag and version are bytes", what);
+    Guard g(ctx);
+    const uint64_t R = b->replicas;
+    std::vector<u64> off(R + 1);
+    LJ_HIP(ctx, hipMemcpyAsync(off.data(), offsets->dev, 8ull * (R + 1), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint64_t i = 0; i < R; ++i)
+        if (off[i] > off[i + 1])
+            return fail(ctx, LASPJ_E_RANGE, "%s: offsets decrease at replica %llu", what,
+                        (unsigned long long)i);
+    if (off[R] > payload->bytes)
+        return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
+    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
+    const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
+                      d->elements};
+    const uint64_t cap = (uint64_t)ctx->cus * 16;
+    hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, cap))),
+                       dim3(64), 0, ctx->stream, static_cast<const uint8_t*>(payload->dev),
+                       static_cast<const u64*>(offsets->dev), R, tabs, tag, vers, reinterpret_cast<u64*>(b->dev),
+                       b->words_per_replica, static_cast<int32_t*>(status->dev));
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 }  // namespace
 }  // namespace laspj
 
@@ -2846,6 +3137,8 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     }
     for (uint64_t t = 0; t < tpoff.size(); ++t)
         std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
+    uint64_t gs_cap = 64;
+    while (gs_cap < 2ull * E) gs_cap <<= 1;
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
     const uint64_t o_eoff = 0, o_eord = o_eoff + al(4ull * (E + 1)), o_eb = o_eord + al(4ull * E),
                    o_mask = o_eb + al(E), o_toff = o_mask + al(8ull * E),
@@ -2856,7 +3149,47 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
                    o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
-                   o_htab = o_rd + al(rd.size() + 8), bytes = o_htab + al(4ull * htab.size() + 4);
+                   o_htab = o_rd + al(rd.size() + 8), o_gsh = o_htab + al(4ull * htab.size() + 4),
+                   o_gsr = o_gsh + al(4ull * gs_cap), o_gsb = o_gsr + al(4ull * E),
+                   bytes = o_gsb + al(4ull * 256);
+    // G-Set from_binary tables: ranks (equal terms share one), image hash, byte values
+    std::vector<uint32_t> gs_rank(E, 0), gs_byte(256, 0), gs_htab;
+    {
+        uint32_t rk = 0;
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint32_t e = elem_order[k];
+            if (k) {
+                const uint32_t p = elem_order[k - 1];
+                int c = 1;
+                const bool both = elem_off[e + 1] > elem_off[e] && elem_off[p + 1] > elem_off[p];
+                if (!both || laspj_term_compare(elem_blob + elem_off[p], elem_off[p + 1] - elem_off[p],
+                                                elem_blob + elem_off[e], elem_off[e + 1] - elem_off[e],
+                                                &c) != LASPJ_OK)
+                    c = 1;
+                if (c != 0) ++rk;
+            }
+            gs_rank[e] = rk;
+        }
+        const uint64_t cap = gs_cap;
+        gs_htab.assign(cap, 0);
+        for (uint32_t e = 0; e < E; ++e) {
+            const uint32_t n = elem_off[e + 1] - elem_off[e];
+            if (!n) continue;
+            const uint8_t* img = elem_blob + elem_off[e];
+            if (n == 2 && img[0] == 97 && !gs_byte[img[1]]) gs_byte[img[1]] = e + 1;
+            uint64_t i = laspj::fnv1a(img, n) & (cap - 1);
+            bool dup = false;
+            while (gs_htab[i]) {
+                const uint32_t o = gs_htab[i] - 1;
+                if (elem_off[o + 1] - elem_off[o] == n &&
+                    std::memcmp(elem_blob + elem_off[o], img, n) == 0)
+                    dup = true;                  // an image twice: the first slot keeps it
+                if (dup) break;
+                i = (i + 1) & (cap - 1);
+            }
+            if (!dup) gs_htab[i] = e + 1;
+        }
+    }
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -2889,6 +3222,9 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
     if (e == hipSuccess && hashed) e = up(o_rd, rd.data(), rd.size());
     if (e == hipSuccess && hashed) e = up(o_htab, htab.data(), 4ull * htab.size());
+    if (e == hipSuccess) e = up(o_gsh, gs_htab.data(), 4ull * gs_htab.size());
+    if (e == hipSuccess) e = up(o_gsr, gs_rank.data(), 4ull * E);
+    if (e == hipSuccess) e = up(o_gsb, gs_byte.data(), 4ull * 256);
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -2915,6 +3251,10 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         d->rd_hmask = (uint32_t)(htab.size() - 1);
         d->rd_hlens = hlens;
     }
+    d->gs_htab = reinterpret_cast<const uint32_t*>(base + o_gsh);
+    d->gs_hmask = (uint32_t)(gs_cap - 1);
+    d->gs_rank = reinterpret_cast<const uint32_t*>(base + o_gsr);
+    d->gs_byte = reinterpret_cast<const uint32_t*>(base + o_gsb);
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);
@@ -2970,6 +3310,12 @@ int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d
                          int vers, const laspj_buf* payload, const laspj_buf* offsets,
                          laspj_buf* status) {
     return laspj::etf_read(ctx, b, d, tag, vers, payload, offsets, status);
+}
+
+int laspj_gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag,
+                        int vers, const laspj_buf* payload, const laspj_buf* offsets,
+                        laspj_buf* status) {
+    return laspj::gset_etf_read(ctx, b, d, tag, vers, payload, offsets, status);
 }
 
 }  // extern "C"

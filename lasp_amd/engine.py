@@ -315,12 +315,14 @@ class _Batch:
 
     def etf_decode(self, d: ETFDict, payload: "Buffer", offsets: "Buffer", tag: int = -1,
                    vers: int = 1) -> np.ndarray:
-        """from_binary/1 of every replica on the device (laspj_orset_etf_read): payload
+        """from_binary/1 of every replica on the device (laspj_orset_etf_read /
+        laspj_gset_etf_read): payload
         bytes [offsets[i], offsets[i+1]) into replica i; returns the LASPJ_DEC_* status
         per replica (replicas with a non-zero status are undefined)."""
         st = self.ctx.buffer(4 * max(1, self.replicas))
-        check(self.ctx.L.laspj_orset_etf_read(self.ctx.h, self.h, d.h, tag, vers, payload.h,
-                                              offsets.h, st.h), self.ctx.h)
+        fn = self.ctx.L.laspj_gset_etf_read if self.kind == _lib.KIND_GSET else \
+            self.ctx.L.laspj_orset_etf_read
+        check(fn(self.ctx.h, self.h, d.h, tag, vers, payload.h, offsets.h, st.h), self.ctx.h)
         return st.download(np.int32, count=self.replicas)
 
     def to_binaries(self, d: ETFDict, tag: int = -1, vers: int = 1) -> list:

@@ -130,3 +130,139 @@ def build_sorted(pairs) -> tuple:
                     spine[depth - 1][3] = sub
                 break
     return (n, _freeze(root))
+
+
+# --------------------------------------------------------------------------- any order
+# OTP 17 gb_trees:insert/3, update/3, enter/3 and lookup/2 on the same terms, for the
+# shapes the reference's update path builds: add_elem inserts a token into the element's
+# existing token tree and enters the element into the set (src/lasp_orset_gbtree.erl:
+# 231-240), so a tree built by updates keeps the shape of its insertion history.  The
+# engine computes contents on the device; these functions only place keys (values are
+# filled in afterwards, in order, from the device's result).
+
+def _cmp(a, b) -> int:
+    from .terms import term_cmp
+    return term_cmp(a, b)
+
+
+def _count(n):
+    """count/1: (H, S) of an immutable subtree."""
+    if n == NIL:
+        return 1, 0
+    if n[2] == NIL and n[3] == NIL:
+        return 1, 1
+    h1, s1 = _count(n[2])
+    h2, s2 = _count(n[3])
+    return 2 * max(h1, h2), s1 + s2 + 1
+
+
+def _balance(n, s):
+    """balance/2: the perfectly balanced tree of n's S nodes."""
+    nodes = []
+    _inorder_t(n, nodes)
+    lst = [[k, v, None, None] for k, v in nodes]
+    sub, _ = _perfect(lst, 0, s)
+    return _freeze(sub)
+
+
+def _inorder_t(n, out):
+    stack = []
+    while stack or n != NIL:
+        while n != NIL:
+            stack.append(n)
+            n = n[2]
+        n = stack.pop()
+        out.append((n[0], n[1]))
+        n = n[3]
+
+
+class KeyExists(Exception):
+    """erlang:error({key_exists, Key}) from gb_trees:insert/3."""
+
+
+class _Measured:
+    """{T, H, S}: a subtree whose height is being measured on the way up."""
+    __slots__ = ("t", "h", "s")
+
+    def __init__(self, t, h, s):
+        self.t, self.h, self.s = t, h, s
+
+
+def _insert_1(key, val, n, s):
+    """insert_1/4: a node, or _Measured while the height is being measured."""
+    if n == NIL:
+        return _Measured((key, val, NIL, NIL), 1, 1) if s == 0 else (key, val, NIL, NIL)
+    c = _cmp(key, n[0])
+    if c == 0:
+        raise KeyExists(key)
+    r = _insert_1(key, val, n[2] if c < 0 else n[3], s >> 1)
+    if isinstance(r, _Measured):
+        t = (n[0], n[1], r.t, n[3]) if c < 0 else (n[0], n[1], n[2], r.t)
+        h2, s2 = _count(n[3] if c < 0 else n[2])
+        h = 2 * max(r.h, h2)
+        ss = r.s + s2 + 1
+        if h > ss * ss:
+            return _balance(t, ss)
+        return _Measured(t, h, ss)
+    return (n[0], n[1], r, n[3]) if c < 0 else (n[0], n[1], n[2], r)
+
+
+def insert(key, val, t):
+    s1 = t[0] + 1
+    r = _insert_1(key, val, t[1], s1 * s1)
+    return (s1, r.t if isinstance(r, _Measured) else r)
+
+
+def lookup(key, t):
+    n = t[1]
+    while n != NIL:
+        c = _cmp(key, n[0])
+        if c == 0:
+            return n[1]
+        n = n[2] if c < 0 else n[3]
+    return None
+
+
+def _update_1(key, val, n):
+    c = _cmp(key, n[0])
+    if c < 0:
+        return (n[0], n[1], _update_1(key, val, n[2]), n[3])
+    if c > 0:
+        return (n[0], n[1], n[2], _update_1(key, val, n[3]))
+    return (n[0], val, n[2], n[3])
+
+
+def update(key, val, t):
+    return (t[0], _update_1(key, val, t[1]))
+
+
+def enter(key, val, t):
+    return update(key, val, t) if lookup(key, t) is not None else insert(key, val, t)
+
+
+def keys(t) -> list:
+    return [k for k, _v in walk(t)]
+
+
+def shape(t):
+    """The tree with its values dropped: two trees of equal contents are the same term
+    exactly when their shapes are equal."""
+    def strip(n):
+        return NIL if n == NIL else (n[0], strip(n[2]), strip(n[3]))
+    return (t[0], strip(t[1]))
+
+
+def fill(t, values) -> tuple:
+    """t with its in-order values replaced by `values` (same length, in order)."""
+    it = iter(values)
+
+    def go(n):
+        if n == NIL:
+            return NIL
+        left = go(n[2])
+        v = next(it)
+        return (n[0], v, left, go(n[3]))
+    out = (t[0], go(t[1]))
+    if next(it, None) is not None:
+        raise ValueError("more values than keys")
+    return out

@@ -5,7 +5,8 @@ lasp_orset, lasp_orset_gbtree and lasp_gset clauses (src/lasp_lattice.erl:62-75,
 The lasp_orset_gbtree clauses run the lasp_orset kernels on the same cells: inflation
 is the same containment test; strict inflation has no `Prev == []` clause
 (:217-233), but there an empty Prev makes `NewElements` (size 0 < size Cur) carry the
-same answer, so the kernel's special case is immaterial."""
+same answer, so the kernel's special case is immaterial; its `Ids =/= Ids1` also sees
+token-tree shapes, which the host adds (orset_gbtree.shapes_differ)."""
 
 from __future__ import annotations
 
@@ -50,9 +51,16 @@ def is_inflation(type_, prev, cur) -> bool:
 
 
 def is_strict_inflation(type_, prev, cur) -> bool:
-    """is_strict_inflation/3 — lasp_lattice.erl:105-106."""
+    """is_strict_inflation/3 — lasp_lattice.erl:105-106.  lasp_orset_gbtree's `Ids =/=
+    Ids1` (:217-233) compares token TREES: an element whose tree changed shape is
+    changed too (the shapes are host terms; the device compares the contents)."""
     P, C = _pair(type_, prev, cur)
-    return bool(C.is_inflation_of(P, strict=True)[0])
+    if bool(C.is_inflation_of(P, strict=True)[0]):
+        return True
+    if type_ == "lasp_orset_gbtree":
+        from .orset_gbtree import shapes_differ
+        return shapes_differ(prev, cur) and bool(C.is_inflation_of(P)[0])
+    return False
 
 
 def threshold_met(type_, value, threshold) -> bool:

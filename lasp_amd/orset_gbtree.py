@@ -9,7 +9,11 @@ same HIP kernels as lasp_orset; only the host-side term walk differs:
 * operands are walked in order (gb_trees:to_list/1) into the shared Domain;
 * results are built as the trees OTP builds for them — `gb_trees_ext:merge/3`
   inserts keys in ascending order into `empty()` at both levels, and so does
-  remove_elem's rebuild, which `lasp_amd.gbtrees.build_sorted` reproduces.
+  remove_elem's rebuild, which `lasp_amd.gbtrees.build_sorted` reproduces; update/3
+  replays its gb_trees:insert / enter calls on the operand's own trees
+  (lasp_amd.gbtrees.insert / enter), so an update-built tree keeps the shape its
+  insertion history gives it.  Only keys are placed on the host: the values come, in
+  order, from the device's result.
 
 Semantics kept from the reference:
 * add / add_by_token insert the token with gb_trees:insert/3 (:232-240): a token that
@@ -17,9 +21,10 @@ Semantics kept from the reference:
   (LASPJ_OP_INSERT / LASPJ_OPST_KEY_EXISTS) with the call left unapplied;
 * remove of an absent element -> {error, {precondition, {not_present, E}}};
 * value/1 and value(removed) are in-order folds (:67-76, :93-101).
-Divergence: equal/2 is gb_trees_ext:equal, which also compares the
-SHAPE of inner token trees; the device compares contents.  The two agree whenever both
-trees were built the way merge builds them (every value a lasp_core store holds).
+* equal/2 is gb_trees_ext:equal: in-order {Key, Value} matches, where Value is the
+  inner token TREE, so inner shapes count — the device compares contents, the host the
+  inner trees' shapes; strict inflation (lasp_lattice.erl:217-233) likewise counts an
+  element whose token tree changed shape as changed (lasp_amd.lattice).
 """
 
 from __future__ import annotations
@@ -100,17 +105,21 @@ def value2(query, s):
     never the list `[]`, `{fragment, E}` is always the one-entry tree {E, Tokens}."""
     if isinstance(query, tuple) and len(query) == 2 and query[0] == "fragment":
         toks = value2(("tokens", query[1]), s)
-        return gbt.build_sorted([(query[1], toks)])
+        return gbt.insert(query[1], toks, gbt.empty())      # enter into empty()
     if isinstance(query, tuple) and len(query) == 2 and query[0] == "tokens":
+        # gb_trees:get(Elem, ORSet): the element's own token tree — its shape from the
+        # operand, its flags from the device's cell
         dom = Domain()
         b, _ = _batch(dom, [to_orddict(s)])
         es = dom.element_slot(query[1], create=False)
-        if es < 0:
+        tree = gbt.lookup(query[1], s)
+        if es < 0 or tree is None:
             return gbt.empty()
-        for elem, toks in dom.decode_orset(b.download()[0]):
-            if dom.element_slot(elem, create=False) == es:
-                return gbt.build_sorted(toks)
-        return gbt.empty()
+        cell = b.fragment(es)[0]
+        p, r = int(cell[0]), int(cell[1])
+        td = dom.tokens[es]
+        flags = [bool((r >> int(k)) & 1) for k in td.order() if (p >> int(k)) & 1]
+        return gbt.fill(tree, flags)
     if query == "removed":
         dom = Domain()
         b, _ = _batch(dom, [to_orddict(s)])
@@ -123,7 +132,9 @@ def _unique(_actor) -> bytes:
     return os.urandom(20)
 
 
-def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
+def _compile(op, dom: Domain, ops: list, new_call: bool, script: list) -> None:
+    """ops for the device; script = the (add | remove, elem, token) calls in order, for
+    the shape replay"""
     kind = op[0]
     flag = _lib.OP_FLAG_NEW_CALL if new_call else 0
     if kind in ("add", "add_by_token"):
@@ -131,21 +142,25 @@ def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
         tok = _unique(None) if kind == "add" else op[1]
         es = dom.element_slot(elem)
         ops.append((0, es, _lib.OP_INSERT, dom.token_slot(es, tok), flag))
+        script.append(("add", elem, tok))
     elif kind == "add_all":
         # foldl of `{ok, _} = update({add, E})` (:112-117): one call, fresh tokens
         for k, e in enumerate(op[1]):
             es = dom.element_slot(e)
-            ops.append((0, es, _lib.OP_INSERT, dom.token_slot(es, _unique(None)),
-                        flag if k == 0 else 0))
+            tok = _unique(None)
+            ops.append((0, es, _lib.OP_INSERT, dom.token_slot(es, tok), flag if k == 0 else 0))
+            script.append(("add", e, tok))
     elif kind == "remove":
         ops.append((0, dom.element_slot(op[1]), _lib.OP_REMOVE, 0, flag))
+        script.append(("remove", op[1], None))
     elif kind == "remove_all":
         for k, e in enumerate(op[1]):           # remove_elems/2 (:255-263)
             ops.append((0, dom.element_slot(e), _lib.OP_REMOVE, 0, flag if k == 0 else 0))
+            script.append(("remove", e, None))
     elif kind == "update":
         first = len(ops)                        # apply_ops/3 (:266-274)
         for sub in op[1]:
-            _compile(sub, dom, ops, new_call=False)
+            _compile(sub, dom, ops, new_call=False, script=script)
         for j in range(first, len(ops)):
             r, e, k, sl, _f = ops[j]
             ops[j] = (r, e, k, sl, flag if j == first else 0)
@@ -153,14 +168,42 @@ def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
         raise ValueError(f"function_clause: {op!r}")
 
 
+def _replay(script, s):
+    """The keys of the tree the reference's update calls build from s: add_elem inserts
+    the token into the element's token tree and enters the element (:231-240),
+    remove_elem re-enters every token into empty() in order (:242-253).  Values are
+    placeholders (filled from the device)."""
+    t = s
+    for kind, elem, tok in script:
+        inner = gbt.lookup(elem, t)
+        if kind == "add":
+            t = gbt.enter(elem, gbt.insert(tok, None, inner if inner is not None
+                                           else gbt.empty()), t)
+        else:
+            t = gbt.update(elem, gbt.build_sorted([(k, None) for k in gbt.keys(inner)]), t)
+    return t
+
+
+def _with_values(t, od) -> tuple:
+    """t's keys at both levels, its values from the orddict od (same keys, in order)."""
+    if len(gbt.keys(t)) != len(od):
+        raise ValueError("device contents and tree keys disagree")
+    inner = []
+    for (elem, toks), (_e, tree) in zip(od, gbt.walk(t)):
+        inner.append(gbt.fill(tree, [f for _t, f in toks]))
+    return gbt.fill(t, inner)
+
+
 def update(op, actor, s):
     """update/3 — :106-124.  ("ok", S1) | ("error", ("precondition", ("not_present",
-    E))); raises KeyExists where the reference's gb_trees:insert/3 crashes."""
+    E))); raises KeyExists where the reference's gb_trees:insert/3 crashes.  Contents
+    and preconditions on the device; the returned trees have the shapes the
+    reference's insert / enter sequence gives them."""
     od = to_orddict(s)
     dom = Domain()
     dom.register_orset(od)
-    ops = []
-    _compile(op, dom, ops, new_call=True)
+    ops, script = [], []
+    _compile(op, dom, ops, new_call=True, script=script)
     E = max(1, dom.size)
     b = context().orset_batch(1, E)
     b.upload(dom.encode_orset([od], E))
@@ -171,7 +214,7 @@ def update(op, actor, s):
         if st[bad[0]] == _lib.OPST_KEY_EXISTS:
             raise KeyExists(dom.tokens[es].terms[slot])
         return ("error", ("precondition", ("not_present", dom.elements.terms[es])))
-    return ("ok", from_orddict(dom.decode_orset(b.download()[0])))
+    return ("ok", _with_values(_replay(script, s), dom.decode_orset(b.download()[0])))
 
 
 def update4(op, actor, s, _ctx=None):
@@ -180,7 +223,9 @@ def update4(op, actor, s, _ctx=None):
 
 
 def equal(a, b) -> bool:
-    """equal/2 — :142-144, on contents (see the module note on shapes)."""
+    """equal/2 — :142-144, gb_trees_ext:equal (src/gb_trees_ext.erl:59-68): in-order
+    {Key, Value} pairs match, Value being the inner token tree — contents compared on
+    the device, the inner trees' shapes on the host."""
     dom = Domain()
     oa, ob = to_orddict(a), to_orddict(b)
     dom.register_orset(oa)
@@ -190,7 +235,31 @@ def equal(a, b) -> bool:
     B = context().orset_batch(1, E)
     A.upload(dom.encode_orset([oa], E))
     B.upload(dom.encode_orset([ob], E))
-    return bool(A.equal(B)[0])
+    if not bool(A.equal(B)[0]):
+        return False
+    return all(gbt.shape(x) == gbt.shape(y)
+               for (_e, x), (_f, y) in zip(gbt.walk(a), gbt.walk(b)))
+
+
+def shapes_differ(prev, cur) -> bool:
+    """Some element of prev found in cur (gb_trees:lookup) has a token tree of another
+    shape — one half of `Ids =/= Ids1` in the strict-inflation clause
+    (lasp_lattice.erl:217-233); the device compares the contents."""
+    for elem, toks in gbt.walk(prev):
+        other = gbt.lookup(elem, cur)
+        if other is not None and gbt.shape(other) != gbt.shape(toks):
+            return True
+    return False
+
+
+def precondition_context(s):
+    """precondition_context/1 — :153-162 with minimum_tokens (:279-287): the device
+    keeps the tokens flagged false; as in the reference, each element's value is the
+    LIST [{Token, false}] minimum_tokens returns, entered in order into empty()."""
+    dom = Domain()
+    b, E = _batch(dom, [to_orddict(s)])
+    out = context().orset_batch(1, E).precondition_context(b)
+    return gbt.build_sorted(dom.decode_orset(out.download()[0]))
 
 
 def stats(s):

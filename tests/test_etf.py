@@ -928,3 +928,175 @@ def test_gpu_from_binary_small_tokens_fuzz():
         assert np.array_equal(cl[ok], c1[ok]), knob
     assert (st1[:len(base)] == 0).all()
     assert np.array_equal(res[0][1][:len(base)], dom.encode_orset(planted, E))
+
+
+# ------------------------------------------------------------------ G-Set from_binary
+
+def _random_gsets(rng, n):
+    from oracle.otp import lists_usort
+    pool = ([0, 1, 7, 255, 256, 1000, -3, 1 << 40, -(1 << 70), 2.5] +
+            [PAtom(a) for a in ("a", "b", "zz")] + [(1, 2), (PAtom("k"), b"v")] +
+            [bytes(rng.randrange(256) for _ in range(rng.randint(0, 30))) for _ in range(20)] +
+            list(range(300, 340)))
+    out = [[], [0, 1, 255], list(range(0, 256, 3)), list(range(300)), [PAtom("a"), (1, 2), b"x"]]
+    for _ in range(n):
+        out.append(lists_usort(rng.sample(pool, rng.randint(0, len(pool)))))
+    return out
+
+
+def _gset_decode_setup(states):
+    from lasp_amd import engine
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    dom = Domain()
+    dom.encode_gset(states, 1 << 12)
+    E = dom.size + 3
+    ctx = context()
+    return ctx, dom, E, engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tagged", [False, True])
+def test_gpu_gset_from_binary_round_trip(tagged):
+    """lasp_gset:from_binary/1 on the device (laspj_gset_etf_read): term_to_binary
+    payloads of random ordsets — STRING_EXT (every element 0..255), LIST_EXT of mixed
+    terms, [] — give the host encoder's words, and device to_binary -> from_binary is the
+    identity."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    states = _random_gsets(random.Random(5 + tagged), 150)
+    ctx, dom, E, d = _gset_decode_setup(states)
+    tag = etf.DT_GSET_TAG if tagged else -1
+    blobs = [oetf.to_binary(tag, 1, s) if tagged else oetf.term_to_binary(s) for s in states]
+    assert blobs[2][2 if tagged else 0:][:2] == bytes([131, 107])      # a STRING_EXT case
+    pay, offs = _upload_payloads(ctx, blobs)
+    b = ctx.gset_batch(len(states), E)
+    st = b.etf_decode(d, pay, offs, tag=tag, vers=1)
+    assert (st == _lib.DEC_OK).all(), np.nonzero(st)[0][:10]
+    want = dom.encode_gset(states, E)
+    assert np.array_equal(b.download(), want)
+    offs2, out2, _ = b.etf_encode(d, tag=tag, vers=1)
+    b2 = ctx.gset_batch(len(states), E)
+    assert (b2.etf_decode(d, out2, offs2, tag=tag, vers=1) == 0).all()
+    assert np.array_equal(b2.download(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_gset_from_binary_errors():
+    """Statuses as the OR-Set decoder's: ?INVALID_BINARY, ?UNSUPPORTED_VERSION, malformed
+    (no 131, truncated, trailing byte, improper tail, not a list), elements outside the
+    dictionary, not strictly ascending (out of order, repeated, 1 next to 1.0), and
+    terms no dictionary holds (a pid)."""
+    from lasp_amd import _lib, etf
+    T = etf.DT_GSET_TAG
+    s0 = [1, 5, PAtom("a"), b"xy"]
+    ctx, dom, E, d = _gset_decode_setup([s0, [2, 300], [1.0]])
+    good = oetf.to_binary(T, 1, s0)
+    improper = good[:-1] + bytes([97, 3])                 # [1, 5, a, <<"xy">> | 3]
+    pid = bytes([T, 1, 131, 108, 0, 0, 0, 1, 88]) + bytes([100, 0, 1]) + b"n" + bytes(12) + bytes([106])
+    cases = [
+        (good, _lib.DEC_OK),
+        (oetf.to_binary(T, 1, []), _lib.DEC_OK),
+        (oetf.to_binary(T, 1, [2]), _lib.DEC_OK),                      # STRING_EXT [2]
+        (oetf.to_binary(T, 1, [1, 2, 5]), _lib.DEC_OK),
+        (bytes([T + 1]) + good[1:], _lib.DEC_INVALID_BINARY),
+        (b"", _lib.DEC_INVALID_BINARY),
+        (bytes([T, 2]) + good[2:], _lib.DEC_UNSUPPORTED_VERSION),
+        (bytes([T, 1, 130]) + good[3:], _lib.DEC_MALFORMED),
+        (good[:-1], _lib.DEC_MALFORMED), (good + b"\0", _lib.DEC_MALFORMED),
+        (good[:len(good) // 2], _lib.DEC_MALFORMED), (improper, _lib.DEC_MALFORMED),
+        (oetf.to_binary(T, 1, PAtom("a")), _lib.DEC_MALFORMED),         # not a list
+        (oetf.to_binary(T, 1, [7]), _lib.DEC_UNKNOWN_TERM),             # not in the dictionary
+        (oetf.to_binary(T, 1, [PAtom("zz")]), _lib.DEC_UNKNOWN_TERM),
+        (oetf.to_binary(T, 1, [5, 1]), _lib.DEC_UNKNOWN_TERM),          # out of order
+        (oetf.to_binary(T, 1, [1, 1]), _lib.DEC_UNKNOWN_TERM),          # repeated
+        (oetf.to_binary(T, 1, [1, 1.0]), _lib.DEC_UNKNOWN_TERM),        # 1 == 1.0
+        (oetf.to_binary(T, 1, [2, 2]), _lib.DEC_UNKNOWN_TERM),          # STRING_EXT repeated
+        (pid, _lib.DEC_UNKNOWN_TERM),                                   # a pid: binary_to_term
+    ]
+    pay, offs = _upload_payloads(ctx, [c[0] for c in cases])
+    b = ctx.gset_batch(len(cases), E)
+    st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert list(st) == [c[1] for c in cases]
+    assert list(b.download()[0]) == list(dom.encode_gset([s0], E)[0])
+
+
+@pytest.mark.gpu
+def test_gpu_gset_from_binary_fuzz():
+    """2000 corrupted G-Set payloads against the oracle's binary_to_term: payloads it
+    decodes to an ordset of dictionary terms decode OK to the host encoder's words; other
+    lists give UNKNOWN_TERM, non-lists and structural failures MALFORMED (a tag the oracle
+    decoder lacks may also read as UNKNOWN_TERM, which the NIF hands to binary_to_term);
+    nothing faults."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    from oracle.otp import lists_usort
+    from oracle.terms import exact_eq as eq
+    rng = random.Random(91)
+    states = _random_gsets(rng, 60)
+    ctx, dom, E, d = _gset_decode_setup(states)
+    T = etf.DT_GSET_TAG
+    base = [oetf.to_binary(T, 1, s) for s in states]
+    blobs = list(base)                     # the intact payloads decode too
+    for _ in range(2000 * SOAK):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(4)
+        if kind == 0 and len(b) > 2:
+            for _ in range(rng.randint(1, 3)):
+                b[rng.randrange(2, len(b))] = rng.randrange(256)
+        elif kind == 1:
+            del b[rng.randrange(2, len(b) + 1):]
+        elif kind == 2:
+            pos = rng.randrange(2, len(b) + 1)
+            b[pos:pos] = bytes(rng.randrange(256) for _ in range(rng.randint(1, 9)))
+        else:
+            other = rng.choice(base)
+            b = b[:rng.randrange(2, len(b) + 1)] + other[rng.randrange(2, len(other) + 1):]
+        blobs.append(bytes(b))
+    pay, offs = _upload_payloads(ctx, blobs)
+    bt = ctx.gset_batch(len(blobs), E)
+    st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+    words = bt.download()
+    eb, eo, _o, *_ = dom.etf_arrays(E, tokens=False)
+    images = {bytes(eb[eo[k]:eo[k + 1]]): k for k in range(dom.size)}
+
+    def raw_elements(b):
+        """the element images as they stand in a well-formed list payload"""
+        if b[1] == 106:
+            return []
+        if b[1] == 107:
+            n = int.from_bytes(b[2:4], "big")
+            return [bytes([97, v]) for v in b[4:4 + n]]
+        n, i, out = int.from_bytes(b[2:6], "big"), 6, []
+        for _ in range(n):
+            j = oetf._dec(b, i)[1]
+            out.append(bytes(b[i:j]))
+            i = j
+        return out
+    n_ok = 0
+    for i, blob in enumerate(blobs):
+        try:
+            term = oetf.binary_to_term(blob[2:])
+            why = None
+        except Exception as e:            # binary_to_term raises badarg
+            term, why = None, str(e)
+        if term is None:
+            lax = "external tag" in why or (len(blob) > 3 and blob[3] == 80)
+            assert st[i] in ((_lib.DEC_MALFORMED, _lib.DEC_UNKNOWN_TERM) if lax
+                             else (_lib.DEC_MALFORMED,)), (i, why, st[i])
+            continue
+        if not isinstance(term, list):
+            assert st[i] == _lib.DEC_MALFORMED, i
+            continue
+        is_set = eq(lists_usort(term), term) and all(r in images for r in raw_elements(blob[2:]))
+        if not is_set:
+            assert st[i] == _lib.DEC_UNKNOWN_TERM, (i, term)
+            continue
+        assert st[i] == _lib.DEC_OK, (i, term)
+        n_ok += 1
+        want = np.zeros_like(words[i])
+        for r in raw_elements(blob[2:]):
+            k = images[r]
+            want[k >> 6] |= np.uint64(1 << (k & 63))
+        assert np.array_equal(words[i], want), i
+    assert n_ok >= len(base)

@@ -270,7 +270,7 @@ def test_gpu_gbtree_update_errors():
     assert r == ("error", ("precondition", ("not_present", 77)))
     _, s2 = dg.update(("update", [("add_by_token", _tok(3), 8), ("remove", 8)]), 1, s)
     want2 = ogt.update(("update", [("add_by_token", _tok(3), 8), ("remove", 8)]), 1, want)[1]
-    assert exact_eq(s2, dg.from_orddict(ogt.to_orddict(want2)))
+    assert exact_eq(s2, want2)                  # the reference's tree, shapes included
     assert dg.value(s2) == ogt.value(want2) == [5]
 
 
@@ -334,3 +334,57 @@ def test_gpu_gbtree_store_matches_oracle_store():
         assert exact_eq(x, y), k
     assert ds.read(dv, ("strict", None))[0] == "ok"
     assert ds.read(dv, ("strict", ds.value(dv))) is None
+
+
+@pytest.mark.gpu
+def test_gpu_gbtree_update_shapes_match_reference():
+    """Trees built by update sequences keep the shape their insertion history gives them
+    (gb_trees:insert / enter in add_elem, the ordered rebuild in remove_elem,
+    src/lasp_orset_gbtree.erl:231-253): after every update the device mirror's state is
+    the oracle's state as a whole term; equal/2 (gb_trees_ext:equal compares the inner
+    token TREES) and strict inflation (lasp_lattice.erl:217-233, `Ids =/= Ids1` on trees)
+    against the state's merge agree with the reference, as do value({tokens, E}),
+    value({fragment, E}) and precondition_context/1."""
+    from lasp_amd import lattice as dl, orset_gbtree as dg
+    T = "lasp_orset_gbtree"
+    rng = random.Random(5)
+    for trial in range(6):
+        d, o, used = dg.new(), ogt.new(), set()
+        for _ in range(40):
+            e = rng.randint(0, 12)
+            if rng.random() < 0.8:
+                t = rng.randint(0, 200)
+                if (e, t) in used:
+                    continue
+                used.add((e, t))
+                op = ("add_by_token", _tok(t), e)
+            else:
+                op = ("remove", e)
+            rd, ro = dg.update(op, 1, d), ogt.update(op, 1, o)
+            assert rd[0] == ro[0]
+            if rd[0] == "ok":
+                d, o = rd[1], ro[1]
+            assert exact_eq(d, o), (trial, op)
+        m = ogt.merge(o, ogt.new())
+        assert dg.equal(d, m) is ogt.equal(o, m)
+        assert dg.equal(d, d) is True
+        assert dl.is_strict_inflation(T, d, m) is olat.is_strict_inflation(T, o, m)
+        assert dl.is_strict_inflation(T, m, d) is olat.is_strict_inflation(T, m, o)
+        for e in range(14):
+            assert exact_eq(dg.value2(("tokens", e), d), ogt.value2(("tokens", e), o)), e
+            assert exact_eq(dg.value2(("fragment", e), d), ogt.value2(("fragment", e), o)), e
+        assert exact_eq(dg.precondition_context(d), ogt.precondition_context(o))
+    # test_gbtree_quirks' case: tokens added in descending order vs their merge — same
+    # contents, different token-tree shapes: not equal, and a strict inflation
+    d = dg.new()
+    for k in (3, 2, 1):
+        d = dg.update(("add_by_token", _tok(k), 7), 1, d)[1]
+    m = dg.merge(d, dg.new())
+    assert dg.equal(d, m) is False
+    assert dl.is_strict_inflation(T, d, m) is True
+    assert dl.is_inflation(T, d, m) is True
+    o = ogt.new()
+    for k in (3, 2, 1):
+        o = ogt.update(("add_by_token", _tok(k), 7), 1, o)[1]
+    assert exact_eq(d, o)
+    assert ogt.equal(o, ogt.merge(o, ogt.new())) is False

@@ -159,7 +159,7 @@ def main():
     # the Store end to end: update R -> intersection re-run -> re-bind 50k entries
     from lasp_amd import core
     from lasp_amd.terms import Atom
-    st = core.Store(capacity=64)
+    st = core.Store(capacity=1 << 18)
     l, r, x = (st.declare("lasp_orset")[1] for _ in range(3))
     tk = lambda c, e: bytes([c]) + int(e).to_bytes(19, "big")    # noqa: E731
     st.bind(l, [(e, [(tk(1, e), False)]) for e in range(N)])
