@@ -225,7 +225,8 @@ int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
  * bind_many: status[i] = 0 when cur[i] =:= val[i] (bind is a no-op, :294-296); else
  *   dst[i] := merge(cur[i], val[i]) and status[i] = 1 (a canonical merge always
  *   inflates cur, and the reference writes whenever it does, :301-303).  dst[i] may be
- *   cur[i].  inflation_many: out[i] = is_inflation (strict = 0) / is_strict_inflation
+ *   cur[i] exactly; otherwise no dst may overlap any cur / val or another dst
+ *   (LASPJ_E_INVAL).  inflation_many: out[i] = is_inflation (strict = 0) / is_strict_inflation
  *   (strict = 1) of prev[i] -> cur[i] per kind (lasp_lattice.erl:137-161, 169-179,
  *   212-253, 273-275).  Both return after the work has completed. */
 int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,

@@ -15,6 +15,7 @@
 //                   (lasp_lattice.erl:137-161, 169-179, 212-253, 273-275), per kind.
 
 #include <new>
+#include <algorithm>
 #include <vector>
 
 #include "laspj_internal.h"
@@ -178,8 +179,6 @@ int describe(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst, const laspj_ba
             x->words_per_replica != y->words_per_replica ||
             (d && d->words_per_replica != x->words_per_replica) || x->elements != y->elements)
             return fail(ctx, LASPJ_E_SHAPE, "%s: item %u: one replica of one shape each", what, i);
-        if (d && d != x && (d->dev == y->dev))
-            return fail(ctx, LASPJ_E_INVAL, "%s: item %u: dst aliases val", what, i);
         MItem& m = (*items)[i];
         m.dst = d ? reinterpret_cast<u64*>(d->dev) : nullptr;
         m.a = reinterpret_cast<const u64*>(x->dev);
@@ -191,6 +190,40 @@ int describe(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst, const laspj_ba
         seg += (m.words + kMSeg - 1) / kMSeg;
     }
     *nseg = seg;
+    if (!dst) return LASPJ_OK;
+    // every dst is written while every cur / val is read by other waves: a dst may
+    // overlap nothing but its own cur exactly (the in-place bind), and no other dst
+    struct Iv {
+        uintptr_t lo, hi;
+        uint32_t item;
+    };
+    std::vector<Iv> ds(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uintptr_t lo = (uintptr_t)dst[i]->dev;
+        ds[i] = {lo, lo + 8 * (uintptr_t)dst[i]->words_per_replica, i};
+    }
+    std::sort(ds.begin(), ds.end(), [](const Iv& x, const Iv& y) { return x.lo < y.lo; });
+    for (uint32_t k = 1; k < n; ++k)
+        if (ds[k].lo < ds[k - 1].hi)
+            return fail(ctx, LASPJ_E_INVAL, "%s: items %u and %u: dst ranges overlap", what,
+                        ds[k - 1].item, ds[k].item);
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int side = 0; side < 2; ++side) {
+            const laspj_batch* r = side ? b[i] : a[i];
+            const uintptr_t lo = (uintptr_t)r->dev, hi = lo + 8 * (uintptr_t)r->words_per_replica;
+            // dst ranges starting below hi, walked down while they still reach past lo
+            auto it = std::lower_bound(ds.begin(), ds.end(), hi,
+                                       [](const Iv& x, uintptr_t v) { return x.lo < v; });
+            while (it != ds.begin()) {
+                --it;
+                if (it->hi <= lo) break;
+                const bool own_cur = side == 0 && it->item == i && it->lo == lo && it->hi == hi;
+                if (!own_cur)
+                    return fail(ctx, LASPJ_E_INVAL, "%s: item %u's dst overlaps item %u's %s",
+                                what, it->item, i, side ? "val" : "cur");
+            }
+        }
+    }
     return LASPJ_OK;
 }
 

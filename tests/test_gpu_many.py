@@ -144,3 +144,25 @@ def test_bind_many_generator_and_failure_propagation():
         st_.bind_many([(b, [(5, [(t3, False)])]), (b"undeclared", [])])
     assert st_.type_value(b) == [5]
     assert st_.type_value(mb) == [105]
+
+
+def test_bind_many_rejects_overlapping_dsts(ctx):
+    """dst[i] may be cur[i] exactly; a dst over another item's cur or val, over its own
+    val, or over another dst is refused before any launch (k_bind_many
+    would read and write the same words from different waves)."""
+    from lasp_amd import _lib
+    big = ctx.orset_batch(6, 64)
+    big.fill_synthetic(3)
+    v = [big.view(k, 1) for k in range(6)]
+    before = big.download()
+    st = ctx.bind_many([v[0], v[1]], [v[0], v[1]], [v[2], v[3]])      # in place: fine
+    assert list(st) == [1, 1]
+    for dsts, curs, vals in (([v[1], v[4]], [v[0], v[1]], [v[2], v[3]]),   # dst0 = cur1
+                             ([v[3], v[4]], [v[0], v[1]], [v[2], v[3]]),   # dst0 = val1
+                             ([v[2], v[4]], [v[0], v[1]], [v[2], v[3]]),   # dst0 = own val
+                             ([v[4], v[4]], [v[0], v[1]], [v[2], v[3]])):  # dst0 = dst1
+        with pytest.raises(_lib.LaspjError) as e:
+            ctx.bind_many(dsts, curs, vals)
+        assert e.value.status == _lib.E_INVAL
+    after = big.download()
+    assert np.array_equal(after[2:], before[2:])          # the refused calls wrote nothing

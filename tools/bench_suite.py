@@ -384,6 +384,63 @@ def etf(ctx, steps):
         del out, offs, d, b
 
 
+def weak(ctx, steps):
+    """The kernels VERDICT r2 found at 0.60-0.70 of the HBM roofline, alone, for PMC
+    passes (tools/gpu_pmc_weak.sh): config 4 fused, config 5 intersection and product
+    diag, the N = 8 anti-entropy reduce, and the G-Set join at 8 GiB operands."""
+    L = ctx.L
+    # config 4 fused (as config4(): composed index o -> o // 3, strict threshold)
+    objects, E = 1024, 1 << 20
+    src = ctx.orset_batch(objects, E)
+    src.fill_synthetic(40, token_slots=3)
+    fold, prev = ctx.orset_batch(objects, 3 * E), ctx.orset_batch(objects, 3 * E)
+    prev.fill_synthetic(41, token_slots=3)
+    fidx = ctx.buffer(4 * 3 * E)
+    fidx.upload(np.repeat(np.arange(E, dtype=np.uint32), 3))
+    out = ctx.buffer(objects)
+    report("config4_dataflow_fused", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_gather_inflation(ctx.h, fold.h, src.h, fidx.h, prev.h, 1, out.h), ctx.h),
+        steps), 112 * objects * E, objects * E, "input_elements_per_s")
+    del src, fold, prev
+    # config 5 intersection and product diag (as config5())
+    P, E5, N = 1024, 150_000, 100_000
+    bl, br = ctx.orset_batch(P, E5), ctx.orset_batch(P, E5)
+    bl.fill_synthetic(5, token_slots=3)
+    br.fill_synthetic(6, token_slots=3)
+    ids = np.arange(E5)
+
+    def bits(mask):
+        b = np.packbits(mask.astype(np.uint8), bitorder="little")
+        return np.concatenate([b, np.zeros((8 * ((E5 + 63) // 64) - len(b),), np.uint8)]).view(np.uint64)
+    l = ctx.orset_batch(P, E5).filter(bl, bits(ids < N))
+    r = ctx.orset_batch(P, E5).filter(br, bits(ids >= E5 - N))
+    del bl, br
+    x = l.intersection(r)
+    report("config5_intersection", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_intersection(ctx.h, x.h, l.h, r.h), ctx.h), steps),
+        64 * P * E5, P * E5, "slots_per_s")
+    del x
+    dg = engine.ORSetProductBatch(ctx, P, E5, 1)
+    report("config5_product_diag", timed(ctx, lambda: _lib.check(
+        L.laspj_orset_product_diag(ctx.h, dg.h, l.h, r.h), ctx.h), steps),
+        36 * P * E5, P * E5, "slots_per_s")
+    del dg, l, r
+    # anti-entropy reduce at N = 8
+    E8, q = 4096, (3 * (1 << 18)) // 8
+    src8, dst8 = ctx.orset_batch(8 * q, E8), ctx.orset_batch(q, E8)
+    report("orset_reduce_chunks_n8", timed(ctx, lambda: dst8.reduce_chunks(src8, 8), steps),
+           16 * 9 * q * E8, q * E8, "dst_cells_per_s")
+    del src8, dst8
+    # G-Set join, 8 GiB per operand
+    RL_, EG = 16 << 20, 4096
+    ga, gb, gc = (ctx.gset_batch(RL_, EG) for _ in range(3))
+    ga.fill_synthetic(5)
+    gb.fill_synthetic(6)
+    W = (EG + 63) // 64
+    report("gset_join_16x", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * RL_ * W, RL_ * EG,
+           "elements_per_s")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--replicas", type=int, default=1 << 20)
@@ -403,6 +460,8 @@ def main():
         config5(ctx, a.steps)
     if "etf" in todo:
         etf(ctx, a.steps)
+    if "weak" in todo:
+        weak(ctx, a.steps)
 
 
 if __name__ == "__main__":

@@ -6,8 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
-    timeout -k 10 ${TLIMIT:-400} python -u -m pytest $TESTS -m gpu -x -v --timeout 150 \
-        --timeout-method thread > gpurun_out/tests.log 2>&1
+    timeout -k 10 ${TLIMIT:-400} python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -x -v \
+        --timeout 150 --timeout-method thread > gpurun_out/tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|error" gpurun_out/tests.log | tail -3
     [ $rc -eq 0 ] || exit $rc
 fi
