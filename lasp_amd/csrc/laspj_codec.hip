@@ -1851,7 +1851,7 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
             uint32_t h = L2 * 0x85EBCA6Bu;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int rem = (int)L2 - 4 * i;          // L2 is wave-uniform
+                const int rem = (int)L2 - 4 * i;          // per lane: L2 follows the lane's tag
                 if (rem <= 0) break;                      // the hash covers ceil(L2 / 4) words
                 const uint32_t v = word_at(w.buf, min(s + 4u * i, kBWin + 56u));
                 q[i] = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);

@@ -431,6 +431,17 @@ def weak(ctx, steps):
     report("orset_reduce_chunks_n8", timed(ctx, lambda: dst8.reduce_chunks(src8, 8), steps),
            16 * 9 * q * E8, q * E8, "dst_cells_per_s")
     del src8, dst8
+    # the REDUCE step of an 8-GPU anti-entropy round at config 3 (laspj_antientropy_plan):
+    # the rank's own 2^17-object chunk (8 GiB) joined in place with the 7 received copies
+    # (recv: 56 GiB) — k_reduce_ptrs<8>, 8 x 16 B read + 16 B written per dst cell
+    Q = 1 << 17
+    own, recv = ctx.orset_batch(Q, E8), ctx.orset_batch(7 * Q, E8)
+    own.fill_synthetic(10)
+    recv.fill_synthetic(11)
+    srcs = [own] + [recv.view(j * Q, 1 * Q) for j in range(7)]
+    report("ae_reduce_in_place_n8", timed(ctx, lambda: own.join_n(srcs), steps),
+           16 * 9 * Q * E8, Q * E8, "dst_cells_per_s")
+    del own, recv, srcs
     # G-Set join, 8 GiB per operand
     RL_, EG = 16 << 20, 4096
     ga, gb, gc = (ctx.gset_batch(RL_, EG) for _ in range(3))
@@ -439,6 +450,31 @@ def weak(ctx, steps):
     W = (EG + 63) // 64
     report("gset_join_16x", timed(ctx, lambda: gc.join(ga, gb), steps), 24 * RL_ * W, RL_ * EG,
            "elements_per_s")
+
+
+def ceilings(ctx, steps):
+    """What plain streams of a given read:write mix reach at a given size on this box:
+    the yardstick for kernels whose operands are a few GiB.  join =
+    2 reads : 1 write (k_or16), copy = 1 : 1 (precondition_context: p & ~r, r = 0), read =
+    value/1 (a bitmap written), each at total traffic ~6, 12, 24, 48, 96 GB."""
+    L = ctx.L
+    E = 4096
+    for gib in (2, 4, 8, 16, 32):
+        R = gib << 30 >> 16                        # replicas of 64 KiB: `gib` GiB per operand
+        a, b, c = ctx.orset_batch(R, E), ctx.orset_batch(R, E), ctx.orset_batch(R, E)
+        a.fill_synthetic(2)
+        b.fill_synthetic(3)
+        cells = R * E
+        report(f"ceiling_join_{gib}g", timed(ctx, lambda: c.join(a, b), steps), 48 * cells, cells,
+               "cells_per_s", operand_gib=gib, mix="2R:1W")
+        report(f"ceiling_copy_{gib}g", timed(ctx, lambda: _lib.check(
+            L.laspj_orset_precondition_context(ctx.h, c.h, a.h), ctx.h), steps), 32 * cells,
+            cells, "cells_per_s", operand_gib=gib, mix="1R:1W")
+        bits = ctx.buffer(R * (E // 64) * 8)
+        report(f"ceiling_read_{gib}g", timed(ctx, lambda: _lib.check(
+            L.laspj_orset_value(ctx.h, a.h, bits.h), ctx.h), steps), 16 * cells + R * E // 8,
+            cells, "cells_per_s", operand_gib=gib, mix="1R")
+        del a, b, c, bits
 
 
 def main():
@@ -462,6 +498,8 @@ def main():
         etf(ctx, a.steps)
     if "weak" in todo:
         weak(ctx, a.steps)
+    if "ceilings" in todo:
+        ceilings(ctx, a.steps)
 
 
 if __name__ == "__main__":

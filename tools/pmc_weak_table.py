@@ -50,7 +50,7 @@ for i in range(1, 5):
         for c, v in cs.items():
             merged[k][c].append(v)
 order = ["config4_dataflow_fused", "config5_intersection", "config5_product_diag",
-         "orset_reduce_chunks_n8", "gset_join_16x"]
+         "orset_reduce_chunks_n8", "ae_reduce_in_place_n8", "gset_join_16x"]
 print("# suite rows (HIP events)")
 for n in order:
     if n in algo:
