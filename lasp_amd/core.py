@@ -51,7 +51,7 @@ class BodyCrash(Exception):
 
 
 class _Var:
-    __slots__ = ("type", "rep", "val", "empty", "waiting", "pairs", "as_list")
+    __slots__ = ("type", "rep", "val", "empty", "waiting", "pairs", "as_list", "gshape")
 
     def __init__(self, type_, val):
         self.type = type_
@@ -61,14 +61,19 @@ class _Var:
         self.waiting: List = []
         self.pairs = False        # list keys are product pairs {X, Y}
         self.as_list = None       # (value object, its list form) cache
+        # lasp_orset_gbtree: {hkey(elem): token tree} of the elements whose token tree
+        # is not ascending-insert shaped (gb_trees_ext:merge keeps a one-sided element's
+        # tree as it is); the device holds the contents
+        self.gshape: Dict = {}
 
 
 class _Value:
     """A device value about to be bound, or last read by a process."""
-    __slots__ = ("rep", "batch", "pairs", "empty")
+    __slots__ = ("rep", "batch", "pairs", "empty", "gb")
 
-    def __init__(self, rep, batch, pairs=False, empty=None):
+    def __init__(self, rep, batch, pairs=False, empty=None, gb=None):
         self.rep, self.batch, self.pairs, self.empty = rep, batch, pairs, empty
+        self.gb = gb              # lasp_orset_gbtree: orset_gbtree.shape_info of the term
 
 
 class Store:
@@ -113,10 +118,11 @@ class Store:
             b.upload(host)
             return _Value("canonical", b, empty=not term)
         if type_ == "lasp_orset_gbtree":
-            from .orset_gbtree import to_orddict
+            from .orset_gbtree import shape_info, to_orddict
             b = self._new_batch(type_)
-            b.upload(self.odom.encode_orset([to_orddict(term)], self.cap))
-            return _Value("canonical", b)
+            od = to_orddict(term)
+            b.upload(self.odom.encode_orset([od], self.cap))
+            return _Value("canonical", b, empty=not od, gb=shape_info(term))
         if not pairs:
             try:
                 if type_ == "lasp_orset":
@@ -261,16 +267,33 @@ class Store:
                 return
             v.rep, v.val, v.pairs = dv.rep, dv.batch, dv.pairs
             v.empty = False
+            if t == "lasp_orset_gbtree" and dv.gb is not None:
+                v.gshape = dict(dv.gb[1])            # merge(empty(), V) keeps V's trees
             self._written(id_, v)
             return
         if v.rep == "canonical" and dv.rep == "canonical":
             new = dv.batch
-            if bool(v.val.equal(new)[0]):                        # lasp_core.erl:294-296
+            same = bool(v.val.equal(new)[0])
+            if t == "lasp_orset_gbtree" and dv.gb is not None:
+                # `case Value0 of Value` matches whole terms: the stored value's outer
+                # tree is ascending-insert shaped (a merge output), so Value must be too,
+                # with the same token-tree shapes
+                outer, odd, _keys = dv.gb
+                same = same and outer and _same_shapes(v.gshape, odd)
+            if same:                                             # lasp_core.erl:294-296
                 return
             merged = _new_like(self.ctx, v.val)
             _or_into(self.ctx, merged, v.val, new)
             if not bool(merged.is_inflation_of(v.val)[0]):       # lasp_core.erl:301
                 return
+            if t == "lasp_orset_gbtree" and dv.gb is not None:
+                # gb_trees_ext:merge/3: an element of both operands gets an ascending
+                # token tree, one of one operand keeps that operand's tree
+                from .terms import hkey
+                old_keys = {hkey(e) for e, _ts in self.odom.decode_orset(v.val.download()[0])}
+                _outer, odd, new_keys = dv.gb
+                v.gshape = {k: tr for k, tr in v.gshape.items() if k not in new_keys}
+                v.gshape.update({k: tr for k, tr in odd.items() if k not in old_keys})
             v.val = merged
             self._written(id_, v)
             return
@@ -308,12 +331,12 @@ class Store:
             n = increment_amount(op)
             cur.increment([(0, self.cdom.element_slot(actor), n)])
         elif v.type in ("lasp_orset", "lasp_orset_gbtree"):
-            ops = []
+            ops, script = [], []
             if v.type == "lasp_orset":
                 _o._compile(op, self.odom, ops, new_call=True)
             else:
                 from . import orset_gbtree as _og
-                _og._compile(op, self.odom, ops, new_call=True)
+                _og._compile(op, self.odom, ops, new_call=True, script=script)
             st = cur.apply_ops(ops)
             if (st == _lib.OPST_KEY_EXISTS).any():
                 j = int(np.nonzero(st == _lib.OPST_KEY_EXISTS)[0][0])
@@ -326,7 +349,13 @@ class Store:
         else:
             elems = [op[1]] if op[0] == "add" else list(op[1])
             cur.apply_ops([(0, self.gdom.element_slot(e), _lib.OP_ADD, 0, 1) for e in elems])
-        self._bind_device(id_, v, _Value("canonical", cur, empty=False))
+        gb = None
+        if v.type == "lasp_orset_gbtree":
+            # Type:update's tree (its insert / enter calls replayed on the stored tree),
+            # then bind/3 merges it into the stored value
+            from .orset_gbtree import _replay, shape_info
+            gb = shape_info(_replay(script, self.value(id_)))
+        self._bind_device(id_, v, _Value("canonical", cur, empty=False, gb=gb))
         return ("ok", (id_, v.type, None))
 
     def read(self, id_, threshold=("strict", None)):
@@ -361,7 +390,21 @@ class Store:
     def _inflates(self, v: _Var, prev: _Value, strict: bool) -> bool:
         """is_inflation(prev, V) / is_strict_inflation(prev, V) for V = v's value."""
         if v.rep == "canonical" and prev.rep == "canonical":
-            return bool(v.val.is_inflation_of(prev.batch, strict=strict)[0])
+            if bool(v.val.is_inflation_of(prev.batch, strict=strict)[0]):
+                return True
+            if strict and v.type == "lasp_orset_gbtree" and prev.gb is not None:
+                # `Ids =/= Ids1` (lasp_lattice.erl:217-233) compares token TREES: a
+                # common element whose tree has another shape is changed too
+                from .gbtrees import shape
+                from .terms import hkey
+                _outer, odd, keys = prev.gb
+                common = keys & {hkey(e) for e, _t in
+                                 self.odom.decode_orset(v.val.download()[0])}
+                differs = any((k in odd) != (k in v.gshape) or
+                              (k in odd and shape(odd[k]) != shape(v.gshape[k]))
+                              for k in common)
+                return differs and bool(v.val.is_inflation_of(prev.batch)[0])
+            return False
         if v.type not in ("lasp_orset", "lasp_gset"):
             raise Unsupported(f"list values of {v.type}")
         cur = self._var_list(v)
@@ -379,8 +422,8 @@ class Store:
             return [(self.cdom.elements.terms[int(a)], int(cells[int(a)]))
                     for a in self.cdom.elements.order() if int(cells[int(a)])]
         if v.type == "lasp_orset_gbtree":
-            from .orset_gbtree import from_orddict
-            return from_orddict(self.odom.decode_orset(cells))
+            from .orset_gbtree import with_shapes
+            return with_shapes(self.odom.decode_orset(cells), v.gshape)
         return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
             self.gdom.decode_gset(cells)
 
@@ -588,6 +631,12 @@ class Store:
 def _pairs_guard(a: _Value, b: _Value):
     if a.pairs != b.pairs:
         raise Unsupported("a product output and plain keys in one combinator")
+
+
+def _same_shapes(a: Dict, b: Dict) -> bool:
+    """Two {hkey: token tree} maps name the same elements with trees of one shape."""
+    from .gbtrees import shape
+    return a.keys() == b.keys() and all(shape(a[k]) == shape(b[k]) for k in a)
 
 
 def _type_new(type_):

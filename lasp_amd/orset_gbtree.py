@@ -8,8 +8,10 @@ same HIP kernels as lasp_orset; only the host-side term walk differs:
 
 * operands are walked in order (gb_trees:to_list/1) into the shared Domain;
 * results are built as the trees OTP builds for them — `gb_trees_ext:merge/3`
-  inserts keys in ascending order into `empty()` at both levels, and so does
-  remove_elem's rebuild, which `lasp_amd.gbtrees.build_sorted` reproduces; update/3
+  inserts keys in ascending order into `empty()` (the outer tree, and the token tree of
+  an element both operands hold; an element of one operand keeps its token tree as it
+  is), and so does remove_elem's rebuild, which `lasp_amd.gbtrees.build_sorted`
+  reproduces; update/3
   replays its gb_trees:insert / enter calls on the operand's own trees
   (lasp_amd.gbtrees.insert / enter), so an update-built tree keeps the shape its
   insertion history gives it.  Only keys are placed on the host: the values come, in
@@ -90,7 +92,23 @@ def merge_many(pairs: Sequence[Tuple[tuple, tuple]]) -> List[tuple]:
     C = context().orset_batch(len(pairs), E)
     C.join(A, B)
     out = C.download()
-    return [from_orddict(dom.decode_orset(out[i])) for i in range(len(pairs))]
+    return [_merge_shape(a, b, dom.decode_orset(out[i])) for i, (a, b) in enumerate(pairs)]
+
+
+def _merge_shape(a, b, od) -> tuple:
+    """The tree gb_trees_ext:merge/3 builds (src/gb_trees_ext.erl:28-57) for the merged
+    contents od: the outer tree by ascending inserts into empty(); an element in both
+    operands gets its merged token tree (ascending inserts again); an element of one
+    operand keeps that operand's token tree as it is (do_merge inserts Val1 / Val2
+    itself) — its shape from the operand, its values from the device."""
+    inner = []
+    for elem, toks in od:
+        ta, tb = gbt.lookup(elem, a), gbt.lookup(elem, b)
+        if ta is not None and tb is not None:
+            inner.append((elem, gbt.build_sorted(toks)))
+        else:
+            inner.append((elem, gbt.fill(ta if ta is not None else tb, [f for _t, f in toks])))
+    return gbt.build_sorted(inner)
 
 
 def value(s):
@@ -132,9 +150,11 @@ def _unique(_actor) -> bytes:
     return os.urandom(20)
 
 
-def _compile(op, dom: Domain, ops: list, new_call: bool, script: list) -> None:
+def _compile(op, dom: Domain, ops: list, new_call: bool, script: list = None) -> None:
     """ops for the device; script = the (add | remove, elem, token) calls in order, for
     the shape replay"""
+    if script is None:
+        script = []
     kind = op[0]
     flag = _lib.OP_FLAG_NEW_CALL if new_call else 0
     if kind in ("add", "add_by_token"):
@@ -182,6 +202,33 @@ def _replay(script, s):
         else:
             t = gbt.update(elem, gbt.build_sorted([(k, None) for k in gbt.keys(inner)]), t)
     return t
+
+
+def shape_info(t):
+    """(outer canonical, {hkey(elem): token tree} for the elements whose token tree is
+    not the ascending-insert shape, {hkey(elem)}) — what a store keeps of a value's
+    shape besides its contents."""
+    from .terms import hkey
+    pairs = gbt.walk(t)
+    outer = gbt.shape(t) == gbt.shape(gbt.build_sorted([(k, None) for k, _v in pairs]))
+    odd = {}
+    for e, inner in pairs:
+        ks = gbt.keys(inner)
+        if gbt.shape(inner) != gbt.shape(gbt.build_sorted([(k, None) for k in ks])):
+            odd[hkey(e)] = inner
+    return outer, odd, {hkey(e) for e, _v in pairs}
+
+
+def with_shapes(od, odd) -> tuple:
+    """The tree of the orddict od whose outer tree is ascending-insert shaped and whose
+    token trees are too, except those named in odd (hkey -> a tree of the same keys)."""
+    from .terms import hkey
+    inner = []
+    for e, toks in od:
+        t = odd.get(hkey(e))
+        inner.append((e, gbt.fill(t, [f for _t, f in toks]) if t is not None
+                      else gbt.build_sorted(toks)))
+    return gbt.build_sorted(inner)
 
 
 def _with_values(t, od) -> tuple:

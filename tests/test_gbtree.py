@@ -232,8 +232,9 @@ def test_gpu_gbtree_merge_value_stats():
     got = dg.merge_many(pairs)
     for (a, b), g in zip(pairs, got):
         want = ogt.merge(a, b)
-        # contents always; whole term whenever the inputs are merge-shaped
-        assert exact_eq(ogt.to_orddict(g), ogt.to_orddict(want))
+        # the whole term, shapes included: an element of one operand keeps its token
+        # tree as it is (gb_trees_ext:merge/3 inserts Val1 / Val2 itself)
+        assert exact_eq(g, want)
         ca, cb = dg.from_orddict(ogt.to_orddict(a)), dg.from_orddict(ogt.to_orddict(b))
         assert exact_eq(dg.merge(ca, cb), ogt.merge(ca, cb))
         assert dg.value(g) == ogt.value(want)
@@ -388,3 +389,54 @@ def test_gpu_gbtree_update_shapes_match_reference():
         o = ogt.update(("add_by_token", _tok(k), 7), 1, o)[1]
     assert exact_eq(d, o)
     assert ogt.equal(o, ogt.merge(o, ogt.new())) is False
+
+
+@pytest.mark.gpu
+def test_gpu_gbtree_store_shapes_with_update_built_binds():
+    """Binding update-built trees (token trees of any shape) and updating in place: the
+    device store's variable equals the oracle store's as a whole term after every step
+    (gb_trees_ext:merge keeps a one-sided element's tree, rebuilds a shared one), and
+    {strict, T} reads agree, shape changes included (lasp_lattice.erl:217-233)."""
+    from lasp_amd import core as dcore
+    from oracle import core as ocore
+    rng = random.Random(17)
+    script = []
+    used = set()
+    for _ in range(70):
+        e = rng.randint(0, 15)
+        x = rng.random()
+        if x < 0.55:
+            t = rng.randint(0, 90)
+            if (e, t) in used:
+                continue
+            used.add((e, t))
+            script.append(("update", ("add_by_token", _tok(t), e)))
+        elif x < 0.7:
+            script.append(("update", ("remove", e)))
+        else:
+            tree = _random_tree(rng, 10)
+            for e2, toks in ogt.to_orddict(tree):
+                used.update((e2, tt) for tt in range(256)
+                            if any(tok == _tok(tt) for tok, _f in toks))
+            script.append(("bind", tree))
+
+    def run(store):
+        _, v = store.declare("lasp_orset_gbtree")
+        vals, reads = [], []
+        for kind, arg in script:
+            if kind == "update":
+                try:
+                    store.update(v, arg, 1)
+                except Exception:       # not_present / key_exists -> crash in both stores
+                    pass
+            else:
+                store.bind(v, arg)
+                reads.append(store.read(v, ("strict", arg)) is not None)
+            vals.append(store.value(v))
+        return vals, reads
+
+    dvals, dreads = run(dcore.Store(capacity=256))
+    ovals, oreads = run(ocore.Store())
+    for k, (x, y) in enumerate(zip(dvals, ovals)):
+        assert exact_eq(x, y), k
+    assert dreads == oreads
