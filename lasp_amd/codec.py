@@ -72,6 +72,9 @@ class Domain:
     def __init__(self, element_capacity: int = 1 << 30):
         self.elements = _Dict(element_capacity)
         self.tokens: List[_Dict] = []
+        # element slots in the order their token dictionaries gained a slot (one entry
+        # per new token): readers keep a position in it to update what they derived
+        self.tok_log: List[int] = []
 
     def element_slot(self, elem, create: bool = True) -> int:
         s = self.elements.slot(elem, create)
@@ -81,7 +84,12 @@ class Domain:
 
     def token_slot(self, eslot: int, tok, create: bool = True) -> int:
         try:
-            return self.tokens[eslot].slot(tok, create)
+            td = self.tokens[eslot]
+            n = len(td.terms)
+            s = td.slot(tok, create)
+            if len(td.terms) != n:
+                self.tok_log.append(eslot)
+            return s
         except CapacityError as e:
             raise CapacityError(
                 f"element {self.elements.terms[eslot]!r} has more than {TOKEN_SLOTS} tokens") from e

@@ -708,76 +708,94 @@ __global__ __launch_bounds__(64) void k_list_equal(LV a, LV b, RK rk, uint8_t* o
 }
 
 // is_lattice_inflation / is_lattice_strict_inflation (lasp_lattice.erl:137-161,
-// 212-215, 235-253, 277-285)
+// 212-215, 235-253, 277-285), spread over the grid (a 50k-entry list is 200 blocks, not
+// one wave): k_linf_insert builds, per replica, an open-addressing table of Cur's key
+// ranks -> first index (= lists:keyfind's first match; G-Set strict also Prev's keys),
+// k_linf_probe checks one Prev (and, G-Set strict, one Cur) entry per thread and ORs
+// violation / change bits into a per-replica word, k_linf_final turns them into the
+// answer.  The tables start as all-ones (kEmpty / kNone) from one memset.
+constexpr uint32_t kViolBit = 1, kChangedBit = 2;
+
 template <bool GSET, bool STRICT>
-__global__ __launch_bounds__(64) void k_list_inflation(LV prev, LV cur, RK rk, u64* hk,
-                                                       uint32_t* hi, uint32_t hsize,
-                                                       bool bcast, uint8_t* out) {
-    const u64 r = blockIdx.x, pr = bcast ? 0 : r;
-    const uint32_t np = prev.n(pr), nc = cur.n(r);
+__global__ __launch_bounds__(256) void k_linf_insert(LV prev, LV cur, RK rk, u64* hk,
+                                                     uint32_t* hi, uint32_t hsize, bool bcast,
+                                                     uint64_t R) {
     const uint32_t mask = hsize - 1;
-    u64* hk0 = hk + r * 2ull * hsize;
-    uint32_t* hi0 = hi + r * 2ull * hsize;
-    u64* hk1 = hk0 + hsize;      // G-Set strict: the set of Prev keys
-    uint32_t* hi1 = hi0 + hsize;
-    h_clear(hk0, hi0, hsize);
-    if (GSET && STRICT) h_clear(hk1, hi1, hsize);
-    __syncthreads();
-    const u64* KP = prev.K(pr);
-    const u64* KC = cur.K(r);
-    for (uint32_t j = lane_id(); j < nc; j += 64) h_insert(hk0, hi0, mask, key_ord(KC[j], rk), j);
-    if (GSET && STRICT)
-        for (uint32_t i = lane_id(); i < np; i += 64)
-            h_insert(hk1, hi1, mask, key_ord(KP[i], rk), i);
-    __syncthreads();
-    bool viol = false, changed = false;
-    if (GSET) {
-        // sets:is_subset(from_list(Prev), from_list(Cur))
-        for (uint32_t i = lane_id(); i < np; i += 64)
-            viol |= h_find(hk0, hi0, mask, key_ord(KP[i], rk)) == kNone;
-        // usort(Prev) =/= usort(Cur): with Prev ⊆ Cur, some Cur key is not in Prev
-        if (STRICT)
-            for (uint32_t j = lane_id(); j < nc; j += 64)
-                changed |= h_find(hk1, hi1, mask, key_ord(KC[j], rk)) == kNone;
-    } else {
-        const u64* TP = prev.T(pr);
-        const u64* TC = cur.T(r);
-        const uint32_t* OP = prev.O(pr);
-        const uint32_t* OC = cur.O(r);
-        for (uint32_t i = lane_id(); i < np; i += 64) {
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const u64 pr = bcast ? 0 : r;
+        const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+        u64* hk0 = hk + r * 2ull * hsize;
+        uint32_t* hi0 = hi + r * 2ull * hsize;
+        if (i < cur.n(r)) h_insert(hk0, hi0, mask, key_ord(cur.K(r)[i], rk), i);
+        if (GSET && STRICT && i < prev.n(pr))
+            h_insert(hk0 + hsize, hi0 + hsize, mask, key_ord(prev.K(pr)[i], rk), i);
+    }
+}
+
+template <bool GSET, bool STRICT>
+__global__ __launch_bounds__(256) void k_linf_probe(LV prev, LV cur, RK rk, const u64* hk,
+                                                    const uint32_t* hi, uint32_t hsize,
+                                                    bool bcast, uint64_t R, uint32_t* flags) {
+    const uint32_t mask = hsize - 1;
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const u64 pr = bcast ? 0 : r;
+        const uint32_t np = prev.n(pr), nc = cur.n(r);
+        const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+        const u64* hk0 = hk + r * 2ull * hsize;
+        const uint32_t* hi0 = hi + r * 2ull * hsize;
+        bool viol = false, changed = false;
+        if (GSET) {
+            // sets:is_subset(from_list(Prev), from_list(Cur))
+            if (i < np) viol = h_find(hk0, hi0, mask, key_ord(prev.K(pr)[i], rk)) == kNone;
+            // usort(Prev) =/= usort(Cur): with Prev ⊆ Cur, some Cur key is not in Prev
+            if (STRICT && i < nc)
+                changed = h_find(hk0 + hsize, hi0 + hsize, mask, key_ord(cur.K(r)[i], rk)) == kNone;
+        } else if (i < np) {
             // lists:keyfind(Element, 1, Current): the first entry with an equal key
-            const uint32_t j = h_find(hk0, hi0, mask, key_ord(KP[i], rk));
+            const uint32_t j = h_find(hk0, hi0, mask, key_ord(prev.K(pr)[i], rk));
             if (j == kNone) {
                 viol = true;
-                continue;
-            }
-            const u64* tp = TP + OP[i];
-            const u64* tc = TC + OC[j];
-            const uint32_t lp = OP[i + 1] - OP[i], lc = OC[j + 1] - OC[j];
-            // ids_inflated: every Prev token keyfind-s among Cur's (flags ignored)
-            for (uint32_t x = 0; x < lp && !viol; ++x) {
-                const u64 ox = tok_ord(tp[x], rk);
-                bool found = false;
-                for (uint32_t y = 0; y < lc && !found; ++y) found = tok_ord(tc[y], rk) == ox;
-                viol = !found;
-            }
-            // DeletedElements: Ids =/= Ids1 (order- and flag-sensitive)
-            if (STRICT && !changed) {
-                if (lp != lc) {
-                    changed = true;
-                } else {
-                    for (uint32_t x = 0; x < lp && !changed; ++x)
-                        changed = tok_ord(tp[x], rk) != tok_ord(tc[x], rk) ||
-                                  ((tp[x] ^ tc[x]) & kRemoved) != 0;
+            } else {
+                const uint32_t* OP = prev.O(pr);
+                const uint32_t* OC = cur.O(r);
+                const u64* tp = prev.T(pr) + OP[i];
+                const u64* tc = cur.T(r) + OC[j];
+                const uint32_t lp = OP[i + 1] - OP[i], lc = OC[j + 1] - OC[j];
+                // ids_inflated: every Prev token keyfind-s among Cur's (flags ignored)
+                for (uint32_t x = 0; x < lp && !viol; ++x) {
+                    const u64 ox = tok_ord(tp[x], rk);
+                    bool found = false;
+                    for (uint32_t y = 0; y < lc && !found; ++y) found = tok_ord(tc[y], rk) == ox;
+                    viol = !found;
+                }
+                // DeletedElements: Ids =/= Ids1 (order- and flag-sensitive)
+                if (STRICT) {
+                    if (lp != lc) {
+                        changed = true;
+                    } else {
+                        for (uint32_t x = 0; x < lp && !changed; ++x)
+                            changed = tok_ord(tp[x], rk) != tok_ord(tc[x], rk) ||
+                                      ((tp[x] ^ tc[x]) & kRemoved) != 0;
+                    }
                 }
             }
         }
+        const uint32_t f = (viol ? kViolBit : 0u) | (changed ? kChangedBit : 0u);
+        const u64 any = __ballot(f != 0);
+        uint32_t wf = f;
+        for (int off = 32; off > 0; off >>= 1) wf |= __shfl_xor(wf, off, 64);
+        if (any && lane_id() == 0) atomicOr(flags + r, wf);
     }
-    viol = __ballot(viol) != 0;
-    changed = __ballot(changed) != 0;
-    if (lane_id() == 0) {
-        bool res = !viol;
+}
+
+template <bool GSET, bool STRICT>
+__global__ void k_linf_final(LV prev, LV cur, bool bcast, uint64_t R, const uint32_t* flags,
+                             uint8_t* out) {
+    for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (u64)gridDim.x * blockDim.x) {
+        const uint32_t np = prev.n(bcast ? 0 : r), nc = cur.n(r), f = flags[r];
+        bool res = !(f & kViolBit);
         if (STRICT) {
+            const bool changed = (f & kChangedBit) != 0;
             if (GSET) res = res && changed;
             else if (np == 0 && nc != 0) res = true;       // ([], Current) when Current =/= []
             else res = res && (changed || np < nc);        // NewElements: length/1
@@ -1530,18 +1548,30 @@ int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
     if (int s = ranks(ctx, ord, !gs, &rk, "list_inflation")) return s;
     LGuard g(ctx);
     const uint64_t R = cur->replicas;
-    const uint32_t hsize = pow2_at_least(2ull * (cur->cap_e > prev->cap_e ? cur->cap_e
-                                                                          : prev->cap_e));
-    char* base = static_cast<char*>(lscratch(ctx, R * 2ull * hsize * 12ull));
+    const uint32_t cmax = cur->cap_e > prev->cap_e ? cur->cap_e : prev->cap_e;
+    const uint32_t hsize = pow2_at_least(2ull * cmax);
+    const uint64_t tbytes = R * 2ull * hsize * 12ull;
+    char* base = static_cast<char*>(lscratch(ctx, tbytes + 4ull * R));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "list_inflation: scratch");
     u64* hk = reinterpret_cast<u64*>(base);
     auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
+    auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    LJ_HIP(ctx, hipMemsetAsync(base, 0xFF, tbytes, ctx->stream));    // kEmpty / kNone
+    LJ_HIP(ctx, hipMemsetAsync(flags, 0, 4ull * R, ctx->stream));
     auto* o = static_cast<uint8_t*>(out->dev);
     const LV P = view(prev), C = view(cur);
+    const dim3 grid(cmax ? (cmax + 255) / 256 : 1, (unsigned)(R < 65535 ? R : 65535));
+    const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
 #define LJ_INFL(G, S)                                                                         \
-    hipLaunchKernelGGL((k_list_inflation<G, S>), dim3(R), dim3(64), 0, ctx->stream, P, C, rk, hk, \
-                       hi, hsize, bcast, o)
+    do {                                                                                      \
+        hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,   \
+                           hk, hi, hsize, bcast, R);                                          \
+        hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
+                           hk, hi, hsize, bcast, R, flags);                                   \
+        hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P, C,    \
+                           bcast, R, flags, o);                                               \
+    } while (0)
     if (gs) {
         if (strict) LJ_INFL(true, true); else LJ_INFL(true, false);
     } else {

@@ -34,15 +34,27 @@ class FunFailed(RuntimeError):
 
 
 class ListSpace:
-    """Rank tables of one Domain on one device context."""
+    """Rank tables of one Domain on one device context, kept up to date incrementally:
+    a dictionary that grew by a few terms (every update/3 mints a token) costs a few
+    ordered inserts and one upload, not a re-sort of every term."""
 
     def __init__(self, ctx, dom: Domain, tokens: bool = True):
         self.ctx, self.dom, self.tokens = ctx, dom, tokens
         self._sig = None
         self._order = _lib.ListOrder()
         self._bufs = ()
-        self._eorder = None
-        self._torder = None
+        # token ranks: the distinct token terms in term order (keys for bisect) and
+        # every token id g = 64 e + k already placed
+        self._tkeys: list = []            # term_key of each distinct token term, ascending
+        self._tids: list = []             # token ids per distinct term (same order)
+        self._seen: dict = {}             # element slot -> tokens placed
+        self._log_rank = 0                # position in dom.tok_log the ranks have seen
+        self._log_tord = 0                # ... and the token-order rows
+        # laspj_list_from_set's per-element token order rows, refreshed per element
+        self._tord = np.zeros((0, 64), dtype=np.uint8)
+        self._tord_seen = np.zeros((0,), dtype=np.int64)
+        self._tord_buf = None
+        self._eorder = None               # (elements order array, its device buffer)
 
     def _signature(self):
         d = self.dom
@@ -57,6 +69,7 @@ class ListSpace:
         return self._order
 
     def _refresh(self):
+        import bisect
         d = self.dom
         K = max(1, d.size)
         krank = np.zeros((K,), dtype=np.uint32)
@@ -68,16 +81,29 @@ class ListSpace:
         self._order.nkeys = K
         bufs = [kb]
         if self.tokens:
+            # place the tokens minted since the last refresh (ordered inserts)
+            log = d.tok_log
+            grown = sorted(set(log[self._log_rank:]))
+            self._log_rank = len(log)
+            for e in grown:
+                terms = d.tokens[e].terms
+                for k in range(self._seen.get(e, 0), len(terms)):
+                    key = term_key(terms[k])
+                    i = bisect.bisect_left(self._tkeys, key)
+                    if i < len(self._tkeys) and not (key < self._tkeys[i]) and \
+                            not (self._tkeys[i] < key):
+                        self._tids[i].append(64 * e + k)      # an equal term: same rank
+                    else:
+                        self._tkeys.insert(i, key)
+                        self._tids.insert(i, [64 * e + k])
+                self._seen[e] = len(terms)
             grank = np.zeros((64 * K,), dtype=np.uint32)
-            toks = [(t, 64 * e + k) for e, td in enumerate(d.tokens[:d.size])
-                    for k, t in enumerate(td.terms)]
-            toks.sort(key=lambda x: term_key(x[0]))
-            rank, prev = -1, None
-            for t, g in toks:
-                if prev is None or term_cmp(prev[0], t) != 0:
-                    rank += 1
-                    prev = (t,)
-                grank[g] = rank
+            if self._tids:
+                lens = np.fromiter((len(x) for x in self._tids), dtype=np.int64,
+                                   count=len(self._tids))
+                ids = np.fromiter((g for x in self._tids for g in x), dtype=np.int64,
+                                  count=int(lens.sum()))
+                grank[ids] = np.repeat(np.arange(len(self._tids), dtype=np.uint32), lens)
             gb = self.ctx.buffer(grank.nbytes)
             gb.upload(grank)
             self._order.grank = gb.h.value
@@ -90,20 +116,37 @@ class ListSpace:
 
     def set_orders(self, E: int):
         """(elem_order buffer, nslots, tok_order buffer) for laspj_list_from_set over a
-        dense batch of E element slots."""
+        dense batch of E element slots; only the rows of elements whose token dictionary
+        grew are rebuilt and re-uploaded."""
         d = self.dom
-        order = d.elements.order().astype(np.uint32)
-        eb = self.ctx.buffer(max(4, order.nbytes))
-        if len(order):
-            eb.upload(order)
+        order = d.elements.order()
+        if self._eorder is None or self._eorder[0] is not order:
+            o32 = order.astype(np.uint32)
+            eb = self.ctx.buffer(max(4, o32.nbytes))
+            if len(o32):
+                eb.upload(o32)
+            self._eorder = (order, eb)
+        eb = self._eorder[1]
         tb = None
         if self.tokens:
-            tord = np.full((E, 64), 0xFF, dtype=np.uint8)
-            for e, td in enumerate(d.tokens[:min(d.size, E)]):
-                o = td.order()
-                tord[e, :len(o)] = o
-            tb = self.ctx.buffer(tord.nbytes)
-            tb.upload(tord.reshape(-1))
+            log = d.tok_log
+            if self._tord.shape[0] != E:
+                self._tord = np.full((E, 64), 0xFF, dtype=np.uint8)
+                self._tord_buf = self.ctx.buffer(self._tord.nbytes)
+                todo, whole = range(min(d.size, E)), True
+            else:
+                todo, whole = sorted(set(e for e in log[self._log_tord:] if e < E)), False
+            self._log_tord = len(log)
+            for e in todo:
+                o = d.tokens[e].order()
+                self._tord[e, :] = 0xFF
+                self._tord[e, :len(o)] = o
+            if whole:
+                self._tord_buf.upload(self._tord.reshape(-1))
+            else:
+                for e in todo:
+                    self._tord_buf.upload(self._tord[e], offset=64 * e)
+            tb = self._tord_buf
         return eb, len(order), tb
 
 

@@ -375,20 +375,27 @@ def test_gpu_gbtree_update_shapes_match_reference():
             assert exact_eq(dg.value2(("tokens", e), d), ogt.value2(("tokens", e), o)), e
             assert exact_eq(dg.value2(("fragment", e), d), ogt.value2(("fragment", e), o)), e
         assert exact_eq(dg.precondition_context(d), ogt.precondition_context(o))
-    # test_gbtree_quirks' case: tokens added in descending order vs their merge — same
-    # contents, different token-tree shapes: not equal, and a strict inflation
-    d = dg.new()
+    # tokens added in descending order: merged with new() the element is one-sided and
+    # keeps its tree (equal, not strictly inflated); merged with a replica that also
+    # holds the element, its tree is rebuilt in ascending order — same contents, another
+    # shape: not equal, and a strict inflation (as the reference answers)
+    d, o = dg.new(), ogt.new()
     for k in (3, 2, 1):
         d = dg.update(("add_by_token", _tok(k), 7), 1, d)[1]
-    m = dg.merge(d, dg.new())
-    assert dg.equal(d, m) is False
-    assert dl.is_strict_inflation(T, d, m) is True
-    assert dl.is_inflation(T, d, m) is True
-    o = ogt.new()
-    for k in (3, 2, 1):
         o = ogt.update(("add_by_token", _tok(k), 7), 1, o)[1]
     assert exact_eq(d, o)
-    assert ogt.equal(o, ogt.merge(o, ogt.new())) is False
+    m0 = dg.merge(d, dg.new())
+    assert exact_eq(m0, ogt.merge(o, ogt.new()))
+    assert dg.equal(d, m0) is True and ogt.equal(o, ogt.merge(o, ogt.new())) is True
+    assert dl.is_strict_inflation(T, d, m0) is False
+    d1 = dg.update(("add_by_token", _tok(1), 7), 1, dg.new())[1]
+    o1 = ogt.update(("add_by_token", _tok(1), 7), 1, ogt.new())[1]
+    m = dg.merge(d, d1)
+    assert exact_eq(m, ogt.merge(o, o1))
+    assert dg.equal(d, m) is False and ogt.equal(o, ogt.merge(o, o1)) is False
+    assert dl.is_strict_inflation(T, d, m) is True
+    assert olat.is_strict_inflation(T, o, ogt.merge(o, o1)) is True
+    assert dl.is_inflation(T, d, m) is True
 
 
 @pytest.mark.gpu

@@ -167,10 +167,19 @@ def main():
     st.intersection(l, r, x)
     assert len(st.value(x)) == N - (D - N)
     k = 5
+    prof = None
+    if os.environ.get("PROFILE_STORE"):
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for i in range(k):
         st.update(r, ("add_by_token", tk(3, i), D - N + 17 * i), Atom("a"))
     res["store_update_rerun_rebind_50k_ms"] = (time.perf_counter() - t0) / k * 1e3
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
     print(json.dumps(res), flush=True)
 
 
