@@ -17,7 +17,7 @@ rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
 [ $rc -eq 0 ] || exit $rc
 
 if [ "${PROFILE:-0}" = 1 ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
       python3 bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   find gpurun_out/prof -name '*stats*' | head
