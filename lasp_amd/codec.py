@@ -40,6 +40,7 @@ class _Dict:
         self.terms: List = []
         self.index: Dict = {}
         self._order = None
+        self._skeys: List = []        # term_key of the placed slots, ascending
 
     def __len__(self):
         return len(self.terms)
@@ -55,14 +56,29 @@ class _Dict:
             s = len(self.terms)
             self.terms.append(term)
             self.index[k] = s
-            self._order = None
         return s
 
     def order(self) -> np.ndarray:
-        """Slots in ascending term order."""
-        if self._order is None or len(self._order) != len(self.terms):
-            idx = sorted(range(len(self.terms)), key=lambda i: term_key(self.terms[i]))
+        """Slots in ascending term order (ties — `==`-equal terms — in slot order).  A
+        dictionary that grew by a few terms places them by binary search (one new array
+        per change, so callers may test it by identity); a large growth re-sorts."""
+        n0 = 0 if self._order is None else len(self._order)
+        n = len(self.terms)
+        if n0 == n and self._order is not None:
+            return self._order
+        if n - n0 > 1024 or self._order is None:
+            idx = sorted(range(n), key=lambda i: term_key(self.terms[i]))
+            self._skeys = [term_key(self.terms[i]) for i in idx]
             self._order = np.asarray(idx, dtype=np.int64)
+            return self._order
+        import bisect
+        # each new slot's place among the OLD keys (after its equals: ties stay in slot
+        # order), then inserted together, last place first
+        new = sorted((bisect.bisect_right(self._skeys, term_key(self.terms[i])),
+                      term_key(self.terms[i]), i) for i in range(n0, n))
+        for p, key, _i in reversed(new):
+            self._skeys.insert(p, key)
+        self._order = np.insert(self._order, [p for p, _k, _i in new], [i for _p, _k, i in new])
         return self._order
 
 

@@ -34,85 +34,144 @@ class FunFailed(RuntimeError):
 
 
 class ListSpace:
-    """Rank tables of one Domain on one device context, kept up to date incrementally:
-    a dictionary that grew by a few terms (every update/3 mints a token) costs a few
-    ordered inserts and one upload, not a re-sort of every term."""
+    """Rank tables of one Domain on one device context, kept up to date incrementally.
+
+    krank (element slots) is dense: rank = position in the element order, rebuilt with
+    one vectorised pass when the element dictionary grew.  grank (token ids g = 64 e + k)
+    holds order LABELS, not dense ranks: the kernels only compare ranks and test them
+    for equality (include/laspj.h "list values"), so a label strictly between its
+    neighbours' labels serves as well as a rank.  A new token term takes the midpoint of
+    the gap its neighbours leave (a term equal to a placed one takes that one's label),
+    and only its grank entry is re-uploaded; when a gap is used up every distinct term
+    is relabelled evenly over [1, 2^31) and the table re-uploaded whole.  An update/3
+    that mints one token so costs a binary search and a 4-byte upload, not a rebuild of
+    64 x (element slots) entries."""
+
+    LABEL_END = 1 << 31              # labels are 31-bit (pairs pack two, laspj.h)
+    LABEL_STEP = 1 << 16             # gap left after the last / before the first term
 
     def __init__(self, ctx, dom: Domain, tokens: bool = True):
         self.ctx, self.dom, self.tokens = ctx, dom, tokens
-        self._sig = None
         self._order = _lib.ListOrder()
-        self._bufs = ()
-        # token ranks: the distinct token terms in term order (keys for bisect) and
-        # every token id g = 64 e + k already placed
-        self._tkeys: list = []            # term_key of each distinct token term, ascending
-        self._tids: list = []             # token ids per distinct term (same order)
+        self._kbuf = None
+        self._kfor = None                 # the element order array krank was built from
+        # token labels: the distinct token terms in term order (keys for bisect), their
+        # labels, and the token ids g = 64 e + k carrying each
+        self._tkeys: list = []
+        self._tlab: list = []
+        self._tids: list = []
         self._seen: dict = {}             # element slot -> tokens placed
-        self._log_rank = 0                # position in dom.tok_log the ranks have seen
-        self._log_tord = 0                # ... and the token-order rows
+        self._log_rank = 0                # position in dom.tok_log the labels have seen
+        self._grank = np.zeros((0,), dtype=np.uint32)
+        self._gbuf = None
+        self._relabels = 0
+        self._log_tord = 0                # position in dom.tok_log the token-order rows have seen
         # laspj_list_from_set's per-element token order rows, refreshed per element
         self._tord = np.zeros((0, 64), dtype=np.uint8)
-        self._tord_seen = np.zeros((0,), dtype=np.int64)
         self._tord_buf = None
         self._eorder = None               # (elements order array, its device buffer)
 
-    def _signature(self):
-        d = self.dom
-        return (d.size, sum(len(t) for t in d.tokens[:d.size]) if self.tokens else 0)
-
     def order(self) -> _lib.ListOrder:
-        """laspj_list_order over the current dictionary (refreshed when it grew)."""
-        sig = self._signature()
-        if sig != self._sig:
-            self._refresh()
-            self._sig = sig
-        return self._order
-
-    def _refresh(self):
-        import bisect
+        """laspj_list_order over the current dictionary (brought up to date first)."""
         d = self.dom
         K = max(1, d.size)
-        krank = np.zeros((K,), dtype=np.uint32)
-        order = d.elements.order()
-        krank[order] = np.arange(len(order), dtype=np.uint32)
-        kb = self.ctx.buffer(krank.nbytes)
-        kb.upload(krank)
-        self._order.krank = kb.h.value
-        self._order.nkeys = K
-        bufs = [kb]
+        eord = d.elements.order()
+        if self._kfor is not eord or self._order.nkeys != K:
+            krank = np.zeros((K,), dtype=np.uint32)
+            krank[eord] = np.arange(len(eord), dtype=np.uint32)
+            if self._kbuf is None or self._kbuf.nbytes < krank.nbytes:
+                self._kbuf = self.ctx.buffer(max(4, 2 * krank.nbytes))
+            self._kbuf.upload(krank)
+            self._order.krank = self._kbuf.h.value
+            self._order.nkeys = K
+            self._kfor = eord
         if self.tokens:
-            # place the tokens minted since the last refresh (ordered inserts)
-            log = d.tok_log
+            self._place_tokens(K)
+        else:
+            self._order.grank = None
+            self._order.ntokens = 0
+        return self._order
+
+    def _place_tokens(self, K: int):
+        import bisect
+        d = self.dom
+        grow = 64 * K > len(self._grank)
+        if grow:                                  # room for 64 x (twice the slots)
+            g2 = np.zeros((64 * max(2 * K, 64),), dtype=np.uint32)
+            g2[:len(self._grank)] = self._grank
+            self._grank = g2
+            self._gbuf = self.ctx.buffer(self._grank.nbytes)
+        log = d.tok_log
+        changed, relabel = [], False
+        if len(log) - self._log_rank > max(4096, len(self._tkeys) // 8):
+            # many new tokens (a first bind of a large value): one sort of every token
+            grown = sorted(set(log[self._log_rank:]))
+            self._log_rank = len(log)
+            for e in grown:
+                self._seen[e] = len(d.tokens[e].terms)
+            allg = sorted(((term_key(t), 64 * e + k) for e in self._seen
+                           for k, t in enumerate(d.tokens[e].terms[:self._seen[e]])),
+                          key=lambda x: x[0])
+            self._tkeys, self._tids = [], []
+            for key, g in allg:
+                if self._tkeys and not (self._tkeys[-1] < key):
+                    self._tids[-1].append(g)
+                else:
+                    self._tkeys.append(key)
+                    self._tids.append([g])
+            relabel = True
+        elif self._log_rank < len(log):
             grown = sorted(set(log[self._log_rank:]))
             self._log_rank = len(log)
             for e in grown:
                 terms = d.tokens[e].terms
                 for k in range(self._seen.get(e, 0), len(terms)):
                     key = term_key(terms[k])
+                    g = 64 * e + k
                     i = bisect.bisect_left(self._tkeys, key)
                     if i < len(self._tkeys) and not (key < self._tkeys[i]) and \
                             not (self._tkeys[i] < key):
-                        self._tids[i].append(64 * e + k)      # an equal term: same rank
+                        self._tids[i].append(g)        # an equal term: its label
+                        self._grank[g] = self._tlab[i]
+                        changed.append(g)
+                        continue
+                    lo = self._tlab[i - 1] if i > 0 else 0
+                    hi = self._tlab[i] if i < len(self._tlab) else self.LABEL_END
+                    if i == len(self._tlab):
+                        lab = lo + min(self.LABEL_STEP, (hi - lo) // 2)
+                    elif i == 0:
+                        lab = hi - min(self.LABEL_STEP, (hi - lo) // 2)
                     else:
-                        self._tkeys.insert(i, key)
-                        self._tids.insert(i, [64 * e + k])
+                        lab = (lo + hi) // 2
+                    self._tkeys.insert(i, key)
+                    self._tids.insert(i, [g])
+                    if lo < lab < hi:
+                        self._tlab.insert(i, lab)
+                        self._grank[g] = lab
+                        changed.append(g)
+                    else:                              # the gap is used up
+                        self._tlab.insert(i, lo)
+                        relabel = True
                 self._seen[e] = len(terms)
-            grank = np.zeros((64 * K,), dtype=np.uint32)
-            if self._tids:
-                lens = np.fromiter((len(x) for x in self._tids), dtype=np.int64,
-                                   count=len(self._tids))
-                ids = np.fromiter((g for x in self._tids for g in x), dtype=np.int64,
-                                  count=int(lens.sum()))
-                grank[ids] = np.repeat(np.arange(len(self._tids), dtype=np.uint32), lens)
-            gb = self.ctx.buffer(grank.nbytes)
-            gb.upload(grank)
-            self._order.grank = gb.h.value
-            self._order.ntokens = 64 * K
-            bufs.append(gb)
+        if relabel:
+            # evenly over the lower half, leaving the upper half for appended terms
+            n = len(self._tkeys)
+            step = (self.LABEL_END - 1) // (2 * n + 2)
+            if step < 1:
+                raise OverflowError("more than 2^31 distinct token terms")
+            self._tlab = [step * (j + 1) for j in range(n)]
+            lens = np.fromiter((len(x) for x in self._tids), dtype=np.int64, count=n)
+            ids = np.fromiter((g for x in self._tids for g in x), dtype=np.int64,
+                              count=int(lens.sum()))
+            self._grank[ids] = np.repeat(np.asarray(self._tlab, dtype=np.uint32), lens)
+            self._relabels += 1
+        if grow or relabel or len(changed) > 4096:
+            self._gbuf.upload(self._grank)
         else:
-            self._order.grank = None
-            self._order.ntokens = 0
-        self._bufs = tuple(bufs)         # keep the buffers alive with the order
+            for g in changed:
+                self._gbuf.upload(self._grank[g:g + 1], offset=4 * g)
+        self._order.grank = self._gbuf.h.value
+        self._order.ntokens = 64 * K
 
     def set_orders(self, E: int):
         """(elem_order buffer, nslots, tok_order buffer) for laspj_list_from_set over a
