@@ -209,56 +209,6 @@ __device__ __forceinline__ void finish(LV out, u64 r, uint32_t n, uint32_t nt, b
 
 // ================================================================ kernels
 
-// canonical dense batch -> list: elements ascending in term order, tokens likewise
-template <bool GSET, bool WRITE>
-__global__ __launch_bounds__(64) void k_list_from_set(const u64* src, uint64_t wpr,
-                                                      const uint32_t* order, uint32_t nord,
-                                                      const uint8_t* tord, LV out,
-                                                      uint32_t* need, uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const u64* s = src + r * wpr;
-    uint32_t n = 0, nt = 0;
-    for (uint32_t c = 0; c < nord; c += 64) {
-        const uint32_t idx = c + lane_id();
-        uint32_t e = 0;
-        u64 p = 0, rm = 0;
-        if (idx < nord) {
-            e = order[idx];
-            if (GSET) {
-                p = (s[e >> 6] >> (e & 63)) & 1ull;
-            } else {
-                p = s[2ull * e];
-                rm = s[2ull * e + 1];
-            }
-        }
-        const uint32_t pres = p != 0, cnt = GSET ? 0u : (uint32_t)__popcll(p);
-        uint32_t tp, tt;
-        const uint32_t pos = n + wave_excl(pres, &tp);
-        uint32_t tpos = nt + wave_excl(pres ? cnt : 0u, &tt);
-        if (WRITE && pres) {
-            if (pos >= out.ce || tpos + cnt > out.ct) {
-                lraise(flag, kErrRange);
-            } else {
-                out.K(r)[pos] = e;
-                if (!GSET) {
-                    out.O(r)[pos] = tpos;
-                    u64* T = out.T(r);
-                    const uint8_t* to = tord + 64ull * e;
-                    for (int j = 0; j < 64; ++j) {
-                        const uint32_t k = to[j];
-                        if (k >= 64) break;
-                        if ((p >> k) & 1ull)
-                            T[tpos++] = (64ull * e + k) | (((rm >> k) & 1ull) << 63);
-                    }
-                }
-            }
-        }
-        n += tp;
-        nt += tt;
-    }
-    finish(out, r, n, nt, WRITE, need, flag);
-}
-
 // ---------------------------------------------------------------- merges
 // lasp_orset:merge/2 (MODE 0), the OR-Set union body = orddict:merge keeping the left
 // value (MODE 1), lasp_gset:merge/2 = OTP 17 ordsets:union (MODE 2).
@@ -804,264 +754,403 @@ __global__ void k_linf_final(LV prev, LV cur, bool bcast, uint64_t R, const uint
     }
 }
 
-// value/1: keys of entries with a {_, false} token, in list order
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_list_value(LV src, LV out, uint32_t* need,
-                                                   uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t n = src.n(r);
-    const u64* K = src.K(r);
-    const u64* T = src.T(r);
-    const uint32_t* O = src.O(r);
-    uint32_t m = 0;
-    for (uint32_t c = 0; c < n; c += 64) {
-        const uint32_t i = c + lane_id();
-        uint32_t live = 0;
-        if (i < n)
-            for (uint32_t t = O[i]; t < O[i + 1] && !live; ++t) live = (T[t] & kRemoved) == 0;
-        uint32_t tot;
-        const uint32_t pos = m + wave_excl(live, &tot);
-        if (WRITE && live) {
-            if (pos >= out.ce) lraise(flag, kErrRange);
-            else out.K(r)[pos] = K[i];
-        }
-        m += tot;
+// ---------------------------------------------------------------- tiled producers
+// Every producer below emits, per replica, a compaction of one input sequence in order:
+// item i of replica r emits ne_i entries and nt_i tokens at the exclusive prefix sums of
+// the items before it.  A pass runs over a (tile, replica) grid of kPTile items per
+// block, so a single long replica (the bind path's one variable) spreads over the chip
+// instead of one wave:
+//   k_tp_count  per tile {ne, nt} sums -> tc[r][t]
+//   k_tp_scan   per replica, the exclusive scan of its tile sums in place; totals -> need
+//   k_tp_write  (write pass) each tile re-counts its items, one block scan gives every
+//               item's positions after the tile's offset, the functor writes; tile 0
+//               writes the header and the token-offset sentinel.
+// The functors restate the reference bodies item by item:
+//   PFromSet      canonical cells -> list (elements ascending in term order, tokens likewise)
+//   PValue        value/1: keys of entries with a {_, false} token (lasp_orset.erl:67-73)
+//   PConcat       G-Set union body L ++ R (lasp_core.erl:602-627)
+//   PIsect        intersection body: per entry of L in order, keyfind (OR-Set) / member
+//                 (G-Set) in R, tokens Cx ++ Cy (lasp_core.erl:546-589,
+//                 lasp_lattice.erl:311-312)
+//   PProduct      product body: entry (x, y) x-major, tokens orset_causal_product(Cx, Cy)
+//                 (lasp_core.erl:499-533, lasp_lattice.erl:303-308)
+//   PMap / PFilter / PFold   map / filter / fold bodies over host-evaluated fun tables
+//                 (lasp_core.erl:641-667, 681-712, 460-486)
+constexpr uint32_t kPT = 256;             // threads per tile block
+constexpr uint32_t kPI = 4;               // items per thread
+constexpr uint32_t kPTile = kPT * kPI;
+
+__device__ __forceinline__ u64 pk2(uint32_t ne, uint32_t nt) { return (u64)ne | ((u64)nt << 32); }
+
+// exclusive block scan of packed {ne, nt} (each half summed separately: no carries)
+__device__ __forceinline__ u64 block_scan_pk(u64 v, u64* lds, u64* total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    u64 x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u64 y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
     }
-    finish(out, r, m, 0, WRITE, need, flag);
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    u64 before = 0, all = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kPT / 64; ++i) {
+        const u64 t = lds[i];
+        if (i < w) before += t;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
 }
 
-// G-Set union body: L ++ R
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_list_concat(LV l, LV rr, LV out, uint32_t* need,
-                                                    uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t nl = l.n(r), nr = rr.n(r);
-    if (WRITE && nl + nr <= out.ce) {
-        for (uint32_t i = lane_id(); i < nl; i += 64) out.K(r)[i] = l.K(r)[i];
-        for (uint32_t j = lane_id(); j < nr; j += 64) out.K(r)[nl + j] = rr.K(r)[j];
-    }
-    finish(out, r, nl + nr, 0, WRITE, need, flag);
-}
-
-// intersection body: per entry of L in order, keyfind (OR-Set) / member (G-Set) in R
-template <bool GSET, bool WRITE>
-__global__ __launch_bounds__(64) void k_list_intersection(LV l, LV rr, LV out, RK rk, u64* hk,
-                                                          uint32_t* hi, uint32_t hsize,
-                                                          uint32_t* need) {
-    const u64 r = blockIdx.x;
-    const uint32_t nl = l.n(r), nr = rr.n(r), mask = hsize - 1;
-    hk += r * (u64)hsize;
-    hi += r * (u64)hsize;
-    h_clear(hk, hi, hsize);
-    __syncthreads();
-    const u64* KL = l.K(r);
-    const u64* KR = rr.K(r);
-    for (uint32_t j = lane_id(); j < nr; j += 64) h_insert(hk, hi, mask, key_ord(KR[j], rk), j);
-    __syncthreads();
-    const uint32_t* OL = l.O(r);
-    const uint32_t* OR = rr.O(r);
-    uint32_t m = 0, nt = 0;
-    for (uint32_t c = 0; c < nl; c += 64) {
-        const uint32_t i = c + lane_id();
-        uint32_t j = kNone, cnt = 0;
-        if (i < nl) {
-            j = h_find(hk, hi, mask, key_ord(KL[i], rk));
-            if (!GSET && j != kNone) cnt = (OL[i + 1] - OL[i]) + (OR[j + 1] - OR[j]);
-        }
-        const uint32_t hit = j != kNone;
-        uint32_t th, tt;
-        const uint32_t pos = m + wave_excl(hit, &th);
-        const uint32_t tpos = nt + wave_excl(cnt, &tt);
-        if (WRITE && hit) {
-            if (pos >= out.ce || tpos + cnt > out.ct) {
-                lraise(rk.flag, kErrRange);
-            } else {
-                out.K(r)[pos] = KL[i];
-                if (!GSET) {
-                    // orset_causal_union(Cx, Cy) = Cx ++ Cy
-                    out.O(r)[pos] = tpos;
-                    u64* to = out.T(r) + tpos;
-                    const u64* tl = l.T(r) + OL[i];
-                    const uint32_t ll = OL[i + 1] - OL[i];
-                    for (uint32_t k = 0; k < ll; ++k) to[k] = tl[k];
-                    const u64* tr = rr.T(r) + OR[j];
-                    for (uint32_t k = 0; k < cnt - ll; ++k) to[ll + k] = tr[k];
-                }
+template <class P>
+__global__ __launch_bounds__(kPT) void k_tp_count(P p, u64* tc, uint32_t ntile, uint64_t R) {
+    __shared__ u64 lds[kPT / 64];
+    const uint32_t t = blockIdx.x;
+    for (uint64_t r = blockIdx.y; r < R; r += gridDim.y) {
+        const u64 n = p.items(r), i0 = (u64)t * kPTile;
+        u64 sum = 0;
+        if (i0 < n) {
+#pragma unroll
+            for (uint32_t k = 0; k < kPI; ++k) {
+                const u64 i = i0 + k * kPT + threadIdx.x;
+                if (i < n) sum += p.count(r, i);
             }
         }
-        m += th;
-        nt += tt;
+        u64 tot;
+        block_scan_pk(sum, lds, &tot);
+        if (threadIdx.x == 0) tc[r * ntile + t] = tot;
     }
-    finish(out, r, m, nt, WRITE, need, rk.flag);
 }
 
-// product body: entry (x, y), x-major; tokens of (x, y): orset_causal_product(Cx, Cy)
-template <bool GSET, bool WRITE>
-__global__ __launch_bounds__(64) void k_list_product(LV l, LV rr, LV out, uint32_t* need,
-                                                     uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t nl = l.n(r), nr = rr.n(r);
-    const uint32_t ntl = GSET ? 0 : l.nt(r), ntr = GSET ? 0 : rr.nt(r);
-    const u64 n64 = (u64)nl * nr, nt64 = (u64)ntl * ntr;
-    if (n64 > 0xFFFFFFFFull || nt64 > 0xFFFFFFFFull) {
-        if (lane_id() == 0) lraise(flag, kErrRange);
-        return;
+__global__ __launch_bounds__(kPT) void k_tp_scan(u64* tc, uint32_t ntile, uint64_t R,
+                                                 uint32_t* need, uint32_t* flag) {
+    __shared__ u64 lds[kPT / 64];
+    for (uint64_t r = blockIdx.x; r < R; r += gridDim.x) {
+        u64* c = tc + r * ntile;
+        u64 carry = 0;
+        for (uint32_t t0 = 0; t0 < ntile; t0 += kPT) {
+            const uint32_t t = t0 + threadIdx.x;
+            const u64 v = t < ntile ? c[t] : 0;
+            u64 tot;
+            const u64 ex = block_scan_pk(v, lds, &tot);
+            if (t < ntile) c[t] = carry + ex;
+            carry += tot;
+        }
+        if (threadIdx.x == 0) {
+            need[2 * r] = (uint32_t)carry;
+            need[2 * r + 1] = (uint32_t)(carry >> 32);
+        }
     }
-    if (WRITE && n64 <= out.ce && nt64 <= out.ct) {
-        const u64* KL = l.K(r);
-        const u64* KR = rr.K(r);
+}
+
+template <class P>
+__global__ __launch_bounds__(kPT) void k_tp_write(P p, LV out, const u64* tc, uint32_t ntile,
+                                                  uint64_t R, const uint32_t* need,
+                                                  uint32_t* flag) {
+    __shared__ u64 lds[kPT / 64];
+    const uint32_t t = blockIdx.x;
+    for (uint64_t r = blockIdx.y; r < R; r += gridDim.y) {
+        const u64 n = p.items(r), i0 = (u64)t * kPTile + (u64)threadIdx.x * kPI;
+        if (t == 0 && threadIdx.x == 0) {
+            const uint32_t ne = need[2 * r], nt = need[2 * r + 1];
+            if (ne > out.ce || nt > out.ct) {
+                lraise(flag, kErrRange);
+            } else {
+                out.hdr[2 * r] = ne;
+                out.hdr[2 * r + 1] = nt;
+                out.O(r)[ne] = nt;
+            }
+        }
+        if ((u64)t * kPTile >= n) continue;        // block-uniform: no barrier skipped
+        u64 c[kPI], mine = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPI; ++k) {
+            c[k] = i0 + k < n ? p.count(r, i0 + k) : 0;
+            mine += c[k];
+        }
+        u64 tot;
+        u64 at = tc[r * ntile + t] + block_scan_pk(mine, lds, &tot);
+#pragma unroll
+        for (uint32_t k = 0; k < kPI; ++k) {
+            if (c[k]) {
+                const uint32_t pos = (uint32_t)at, tpos = (uint32_t)(at >> 32);
+                const uint32_t ne = (uint32_t)c[k], nt = (uint32_t)(c[k] >> 32);
+                if ((u64)pos + ne > out.ce || (u64)tpos + nt > out.ct) lraise(flag, kErrRange);
+                else p.write(r, i0 + k, pos, tpos, out);
+            }
+            at += c[k];
+        }
+    }
+}
+
+template <bool GSET>
+struct PFromSet {
+    const u64* src;
+    uint64_t wpr;
+    const uint32_t* order;
+    uint32_t nord, E;
+    const uint8_t* tord;
+    uint32_t* flag;
+    __device__ u64 items(u64) const { return nord; }
+    __device__ void cell(u64 r, u64 i, uint32_t& e, u64& p, u64& rm) const {
+        e = order[i];
+        p = rm = 0;
+        if (e >= E) {
+            lraise(flag, kErrId);
+            return;
+        }
+        const u64* s = src + r * wpr;
+        if (GSET) {
+            p = (s[e >> 6] >> (e & 63)) & 1ull;
+        } else {
+            p = s[2ull * e];
+            rm = s[2ull * e + 1];
+        }
+    }
+    __device__ u64 count(u64 r, u64 i) const {
+        uint32_t e;
+        u64 p, rm;
+        cell(r, i, e, p, rm);
+        return p ? pk2(1, GSET ? 0u : (uint32_t)__popcll(p)) : 0;
+    }
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        uint32_t e;
+        u64 p, rm;
+        cell(r, i, e, p, rm);
+        out.K(r)[pos] = e;
+        if (GSET) return;
+        out.O(r)[pos] = tpos;
+        u64* T = out.T(r);
+        const uint8_t* to = tord + 64ull * e;
+        for (int j = 0; j < 64; ++j) {
+            const uint32_t k = to[j];
+            if (k >= 64) break;
+            if ((p >> k) & 1ull) T[tpos++] = (64ull * e + k) | (((rm >> k) & 1ull) << 63);
+        }
+    }
+};
+
+struct PValue {
+    LV src;
+    __device__ u64 items(u64 r) const { return src.n(r); }
+    __device__ u64 count(u64 r, u64 i) const {
+        const uint32_t* O = src.O(r);
+        const u64* T = src.T(r);
+        for (uint32_t t = O[i]; t < O[i + 1]; ++t)
+            if (!(T[t] & kRemoved)) return pk2(1, 0);
+        return 0;
+    }
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t, LV out) const {
+        out.K(r)[pos] = src.K(r)[i];
+    }
+};
+
+struct PConcat {
+    LV l, rr;
+    __device__ u64 items(u64 r) const { return (u64)l.n(r) + rr.n(r); }
+    __device__ u64 count(u64, u64) const { return pk2(1, 0); }
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t, LV out) const {
+        const uint32_t nl = l.n(r);
+        out.K(r)[pos] = i < nl ? l.K(r)[i] : rr.K(r)[i - nl];
+    }
+};
+
+// R's keys -> first index, built before the count pass (k_isect_hash)
+template <bool GSET>
+struct PIsect {
+    LV l, rr;
+    RK rk;
+    const u64* hk;
+    const uint32_t* hi;
+    uint32_t hsize;
+    __device__ uint32_t find(u64 r, u64 i) const {
+        return h_find(hk + r * (u64)hsize, hi + r * (u64)hsize, hsize - 1,
+                      key_ord(l.K(r)[i], rk));
+    }
+    __device__ u64 items(u64 r) const { return l.n(r); }
+    __device__ u64 count(u64 r, u64 i) const {
+        const uint32_t j = find(r, i);
+        if (j == kNone) return 0;
+        if (GSET) return pk2(1, 0);
         const uint32_t* OL = l.O(r);
         const uint32_t* OR = rr.O(r);
-        for (u64 o = lane_id(); o < n64; o += 64) {
-            const uint32_t xi = (uint32_t)(o / nr), yi = (uint32_t)(o % nr);
-            const u64 kx = KL[xi], ky = KR[yi];
-            if ((kx & kPair) || (ky & kPair)) {
-                lraise(flag, kErrNested);
-                continue;
-            }
-            out.K(r)[o] = kPair | ((kx & kIdMask) << 31) | (ky & kIdMask);
-            if (GSET) continue;
-            const uint32_t lx = OL[xi + 1] - OL[xi], ly = OR[yi + 1] - OR[yi];
-            // tokens before (xi, yi): all of rows < xi, then |Cx| x tokens of columns < yi
-            const uint32_t tpos = OL[xi] * ntr + lx * OR[yi];
-            out.O(r)[o] = tpos;
-            u64* to = out.T(r) + tpos;
-            const u64* tx = l.T(r) + OL[xi];
-            const u64* ty = rr.T(r) + OR[yi];
-            uint32_t k = 0;
-            for (uint32_t a = lx; a-- > 0;) {           // reversed foldl: Xs backwards
-                const u64 X = tx[a];
-                for (uint32_t b = ly; b-- > 0;) {       // ... and Ys backwards
-                    const u64 Y = ty[b];
-                    if ((X & kCompound) || (Y & kCompound)) {
-                        lraise(flag, kErrNested);
-                        continue;
-                    }
-                    to[k++] = kCompound | ((X & kIdMask) << 31) | (Y & kIdMask) |
-                              ((X | Y) & kRemoved);     // XDeleted orelse YDeleted
+        return pk2(1, (OL[i + 1] - OL[i]) + (OR[j + 1] - OR[j]));
+    }
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        out.K(r)[pos] = l.K(r)[i];
+        if (GSET) return;
+        const uint32_t j = find(r, i);
+        const uint32_t* OL = l.O(r);
+        const uint32_t* OR = rr.O(r);
+        out.O(r)[pos] = tpos;
+        u64* to = out.T(r) + tpos;
+        const u64* tl = l.T(r) + OL[i];
+        const uint32_t ll = OL[i + 1] - OL[i], lr = OR[j + 1] - OR[j];
+        for (uint32_t k = 0; k < ll; ++k) to[k] = tl[k];        // Cx ++ Cy
+        const u64* tr = rr.T(r) + OR[j];
+        for (uint32_t k = 0; k < lr; ++k) to[ll + k] = tr[k];
+    }
+};
+
+template <bool GSET>
+__global__ __launch_bounds__(256) void k_isect_hash(LV rr, RK rk, u64* hk, uint32_t* hi,
+                                                    uint32_t hsize, uint64_t R) {
+    for (uint64_t r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t nr = rr.n(r);
+        const u64* KR = rr.K(r);
+        for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nr; j += gridDim.x * 256)
+            h_insert(hk + r * (u64)hsize, hi + r * (u64)hsize, hsize - 1, key_ord(KR[j], rk), j);
+    }
+}
+
+template <bool GSET>
+struct PProduct {
+    LV l, rr;
+    uint32_t* flag;
+    __device__ u64 items(u64 r) const { return (u64)l.n(r) * rr.n(r); }
+    __device__ u64 count(u64 r, u64 o) const {
+        // entries and tokens of the whole output must fit the list's 32-bit counts
+        if (items(r) > 0xFFFFFFFFull || (!GSET && (u64)l.nt(r) * rr.nt(r) > 0xFFFFFFFFull)) {
+            lraise(flag, kErrRange);
+            return 0;
+        }
+        if (GSET) return pk2(1, 0);
+        const uint32_t nr = rr.n(r);
+        const uint32_t xi = (uint32_t)(o / nr), yi = (uint32_t)(o - (u64)xi * nr);
+        const uint32_t lx = l.O(r)[xi + 1] - l.O(r)[xi], ly = rr.O(r)[yi + 1] - rr.O(r)[yi];
+        return pk2(1, lx * ly);
+    }
+    __device__ void write(u64 r, u64 o, uint32_t pos, uint32_t tpos, LV out) const {
+        const uint32_t nr = rr.n(r);
+        const uint32_t xi = (uint32_t)(o / nr), yi = (uint32_t)(o - (u64)xi * nr);
+        const u64 kx = l.K(r)[xi], ky = rr.K(r)[yi];
+        if ((kx & kPair) || (ky & kPair)) {
+            lraise(flag, kErrNested);
+            return;
+        }
+        out.K(r)[pos] = kPair | ((kx & kIdMask) << 31) | (ky & kIdMask);
+        if (GSET) return;
+        const uint32_t* OL = l.O(r);
+        const uint32_t* OR = rr.O(r);
+        const uint32_t lx = OL[xi + 1] - OL[xi], ly = OR[yi + 1] - OR[yi];
+        out.O(r)[pos] = tpos;
+        u64* to = out.T(r) + tpos;
+        const u64* tx = l.T(r) + OL[xi];
+        const u64* ty = rr.T(r) + OR[yi];
+        uint32_t k = 0;
+        for (uint32_t a = lx; a-- > 0;) {           // reversed foldl: Xs backwards
+            const u64 X = tx[a];
+            for (uint32_t b = ly; b-- > 0;) {       // ... and Ys backwards
+                const u64 Y = ty[b];
+                if ((X & kCompound) || (Y & kCompound)) {
+                    lraise(flag, kErrNested);
+                    ++k;
+                    continue;
                 }
+                to[k++] = kCompound | ((X & kIdMask) << 31) | (Y & kIdMask) |
+                          ((X | Y) & kRemoved);     // XDeleted orelse YDeleted
             }
         }
     }
-    finish(out, r, (uint32_t)n64, (uint32_t)nt64, WRITE, need, flag);
-}
+};
 
-__device__ __forceinline__ uint32_t tab_index(u64 key, uint32_t i, int per_entry, uint32_t ntab,
+__device__ __forceinline__ uint32_t tab_index(u64 key, uint64_t i, int per_entry, uint32_t ntab,
                                               uint32_t* flag) {
     if (!per_entry && (key & kPair)) {
         lraise(flag, kErrTable);
         return kNone;
     }
-    const uint32_t idx = per_entry ? i : (uint32_t)(key & kIdMask);
+    const u64 idx = per_entry ? i : (key & kIdMask);
     if (idx >= ntab) {
         lraise(flag, kErrTable);
         return kNone;
     }
-    return idx;
+    return (uint32_t)idx;
 }
 
 // map body: {F(X), C} / F(X) in list order — keys replaced, tokens kept
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_list_map(LV src, LV out, const u64* tab, uint32_t ntab,
-                                                 int per_entry, uint32_t* need,
-                                                 uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t n = src.n(r), nt = src.nt(r);
-    if (WRITE && n <= out.ce && nt <= out.ct) {
-        const u64* K = src.K(r);
-        for (uint32_t i = lane_id(); i < n; i += 64) {
-            const uint32_t idx = tab_index(K[i], i, per_entry, ntab, flag);
-            const u64 k = idx == kNone ? 0 : tab[idx];
-            if (k == kEmpty) lraise(flag, kErrFun);     // Function(X) raised
-            out.K(r)[i] = k;
-            out.O(r)[i] = src.O(r)[i];
-        }
-        for (uint32_t t = lane_id(); t < nt; t += 64) out.T(r)[t] = src.T(r)[t];
+struct PMap {
+    LV src;
+    const u64* tab;
+    uint32_t ntab;
+    int per_entry;
+    uint32_t* flag;
+    __device__ u64 items(u64 r) const { return src.n(r); }
+    __device__ u64 count(u64 r, u64 i) const {
+        return pk2(1, src.O(r)[i + 1] - src.O(r)[i]);
     }
-    finish(out, r, n, nt, WRITE, need, flag);
-}
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
+        const u64 k = idx == kNone ? 0 : tab[idx];
+        if (k == kEmpty) lraise(flag, kErrFun);     // Function(X) raised
+        out.K(r)[pos] = k;
+        out.O(r)[pos] = tpos;
+        const uint32_t* O = src.O(r);
+        const u64* from = src.T(r) + O[i];
+        for (uint32_t t = 0; t < O[i + 1] - O[i]; ++t) out.T(r)[tpos + t] = from[t];
+    }
+};
 
 // filter body: keep {X, C} / X when F(X) =:= true (tombstoned entries included)
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_list_filter(LV src, LV out, const uint8_t* keep,
-                                                    uint32_t ntab, int per_entry,
-                                                    uint32_t* need, uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t n = src.n(r);
-    const u64* K = src.K(r);
-    const uint32_t* O = src.O(r);
-    uint32_t m = 0, nt = 0;
-    for (uint32_t c = 0; c < n; c += 64) {
-        const uint32_t i = c + lane_id();
-        uint32_t k = 0, cnt = 0;
-        if (i < n) {
-            const uint32_t idx = tab_index(K[i], i, per_entry, ntab, flag);
-            if (idx != kNone && keep[idx] == 2) lraise(flag, kErrFun);   // Function(V) raised
-            k = idx != kNone && keep[idx] == 1;
-            cnt = k ? O[i + 1] - O[i] : 0;
-        }
-        uint32_t tk, tt;
-        const uint32_t pos = m + wave_excl(k, &tk);
-        const uint32_t tpos = nt + wave_excl(cnt, &tt);
-        if (WRITE && k) {
-            if (pos >= out.ce || tpos + cnt > out.ct) {
-                lraise(flag, kErrRange);
-            } else {
-                out.K(r)[pos] = K[i];
-                out.O(r)[pos] = tpos;
-                const u64* from = src.T(r) + O[i];
-                for (uint32_t t = 0; t < cnt; ++t) out.T(r)[tpos + t] = from[t];
-            }
-        }
-        m += tk;
-        nt += tt;
+struct PFilter {
+    LV src;
+    const uint8_t* keep;
+    uint32_t ntab;
+    int per_entry;
+    uint32_t* flag;
+    __device__ u64 items(u64 r) const { return src.n(r); }
+    __device__ u64 count(u64 r, u64 i) const {
+        const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
+        if (idx == kNone) return 0;
+        if (keep[idx] == 2) lraise(flag, kErrFun);   // Function(V) raised
+        if (keep[idx] != 1) return 0;
+        return pk2(1, src.O(r)[i + 1] - src.O(r)[i]);
     }
-    finish(out, r, m, nt, WRITE, need, flag);
-}
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        const uint32_t* O = src.O(r);
+        out.K(r)[pos] = src.K(r)[i];
+        out.O(r)[pos] = tpos;
+        const u64* from = src.T(r) + O[i];
+        for (uint32_t t = 0; t < O[i + 1] - O[i]; ++t) out.T(r)[tpos + t] = from[t];
+    }
+};
 
 // fold body: [{V, C} || V <- F(X)] / F(X), concatenated in list order
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_list_fold(LV src, LV out, const uint32_t* off,
-                                                  const u64* keys, uint32_t ntab,
-                                                  int per_entry, uint32_t* need,
-                                                  uint32_t* flag) {
-    const u64 r = blockIdx.x;
-    const uint32_t n = src.n(r);
-    const u64* K = src.K(r);
-    const uint32_t* O = src.O(r);
-    uint32_t m = 0, nt = 0;
-    for (uint32_t c = 0; c < n; c += 64) {
-        const uint32_t i = c + lane_id();
-        uint32_t idx = kNone, k = 0, len = 0;
-        if (i < n) {
-            idx = tab_index(K[i], i, per_entry, ntab, flag);
-            if (idx != kNone) {
-                k = off[idx + 1] - off[idx];
-                len = O[i + 1] - O[i];
-                for (uint32_t v = 0; v < k; ++v)
-                    if (keys[off[idx] + v] == kEmpty) lraise(flag, kErrFun);
-            }
+struct PFold {
+    LV src;
+    const uint32_t* off;
+    const u64* keys;
+    uint32_t ntab;
+    int per_entry;
+    uint32_t* flag;
+    __device__ u64 items(u64 r) const { return src.n(r); }
+    __device__ u64 count(u64 r, u64 i) const {
+        const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
+        if (idx == kNone) return 0;
+        const uint32_t k = off[idx + 1] - off[idx], len = src.O(r)[i + 1] - src.O(r)[i];
+        for (uint32_t v = 0; v < k; ++v)
+            if (keys[off[idx] + v] == kEmpty) lraise(flag, kErrFun);
+        if ((u64)k * len > 0xFFFFFFFFull) {
+            lraise(flag, kErrRange);
+            return 0;
         }
-        uint32_t tk, tt;
-        const uint32_t pos = m + wave_excl(k, &tk);
-        const uint32_t tpos = nt + wave_excl(k * len, &tt);
-        if (WRITE && k) {
-            if (pos + k > out.ce || tpos + k * len > out.ct) {
-                lraise(flag, kErrRange);
-            } else {
-                const u64* from = src.T(r) + O[i];
-                for (uint32_t v = 0; v < k; ++v) {
-                    out.K(r)[pos + v] = keys[off[idx] + v];
-                    out.O(r)[pos + v] = tpos + v * len;
-                    for (uint32_t t = 0; t < len; ++t) out.T(r)[tpos + v * len + t] = from[t];
-                }
-            }
-        }
-        m += tk;
-        nt += tt;
+        return pk2(k, k * len);
     }
-    finish(out, r, m, nt, WRITE, need, flag);
-}
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
+        const uint32_t* O = src.O(r);
+        const uint32_t k = off[idx + 1] - off[idx], len = O[i + 1] - O[i];
+        const u64* from = src.T(r) + O[i];
+        for (uint32_t v = 0; v < k; ++v) {
+            out.K(r)[pos + v] = keys[off[idx] + v];
+            out.O(r)[pos + v] = tpos + v * len;
+            for (uint32_t t = 0; t < len; ++t) out.T(r)[tpos + v * len + t] = from[t];
+        }
+    }
+};
 
 }  // namespace
 
@@ -1206,7 +1295,6 @@ template <class SizeFn, class WriteFn>
 int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, WriteFn write_pass,
           const char* what) {
     const uint64_t R = dst->replicas;
-    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
     size_pass();
     LJ_LAUNCHED(ctx);
     std::vector<uint32_t> h(2 * R);
@@ -1225,6 +1313,39 @@ int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, Wr
     write_pass(view(dst));
     LJ_LAUNCHED(ctx);
     return read_flag(ctx, what);
+}
+
+// a tiled producer (k_tp_*): `pre` carves its own scratch from the front of the block
+// (pre_bytes), enqueues whatever must run first and returns the functor
+template <class P, class Pre>
+int tiled(laspj_ctx* ctx, laspj_batch* dst, uint64_t max_items, uint64_t pre_bytes, Pre pre,
+          const char* what) {
+    const uint64_t R = dst->replicas;
+    const uint64_t nt64 = max_items ? (max_items + kPTile - 1) / kPTile : 1;
+    if (nt64 > 0x7FFFFFFFull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
+    const uint32_t ntile = (uint32_t)nt64;
+    const uint64_t pb = (pre_bytes + 63) & ~63ull;
+    char* base = static_cast<char*>(lscratch(ctx, pb + 8ull * R * ntile + 8ull * R));
+    if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
+    u64* tc = reinterpret_cast<u64*>(base + pb);
+    auto* need = reinterpret_cast<uint32_t*>(base + pb + 8ull * R * ntile);
+    uint32_t* flag = ctx->flag + 1;
+    LJ_HIP(ctx, hipMemsetAsync(flag, 0, 4, ctx->stream));
+    const P p = pre(base);
+    const dim3 grid(ntile, (unsigned)(R < 65535 ? R : 65535));
+    const unsigned sg = (unsigned)(R < 65535 ? R : 65535);
+    return sized(
+        ctx, dst, need,
+        [&] {
+            hipLaunchKernelGGL((k_tp_count<P>), grid, dim3(kPT), 0, ctx->stream, p, tc, ntile, R);
+            hipLaunchKernelGGL(k_tp_scan, dim3(sg), dim3(kPT), 0, ctx->stream, tc, ntile, R, need,
+                               flag);
+        },
+        [&](LV out) {
+            hipLaunchKernelGGL((k_tp_write<P>), grid, dim3(kPT), 0, ctx->stream, p, out, tc, ntile,
+                               R, need, flag);
+        },
+        what);
 }
 
 }  // namespace
@@ -1347,50 +1468,22 @@ int laspj_list_from_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src
         return fail(ctx, LASPJ_E_RANGE, "list_from_set: token order (64 bytes per slot)");
     if ((uint64_t)src->elements * 64ull > kIdMask)
         return fail(ctx, LASPJ_E_RANGE, "list_from_set: too many element slots for token ids");
-    // element slots in elem_order must be < E: checked on the host copy would need a
-    // download; the kernel reads cells of slot order[i] — validate by bound instead
+    // element slots in elem_order must be < E: the kernels raise kErrId (E_RANGE) on one
+    // that is not, so no copy of the order comes back to the host
     LGuard g(ctx);
-    {
-        std::vector<uint32_t> ord(nslots);
-        if (nslots) {
-            LJ_HIP(ctx, hipMemcpyAsync(ord.data(), elem_order->dev, 4ull * nslots,
-                                       hipMemcpyDeviceToHost, ctx->stream));
-            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        }
-        for (uint32_t v : ord)
-            if (v >= src->elements)
-                return fail(ctx, LASPJ_E_RANGE, "list_from_set: slot %u >= %u", v, src->elements);
-    }
-    const uint64_t R = src->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_from_set: scratch");
     const auto* ordp = static_cast<const uint32_t*>(elem_order->dev);
     const auto* tordp = gs ? nullptr : static_cast<const uint8_t*>(tok_order->dev);
+    const auto* sp = reinterpret_cast<const u64*>(src->dev);
+    const uint64_t wpr = src->words_per_replica;
+    const uint32_t E = src->elements;
     uint32_t* flag = ctx->flag + 1;
-    LV nil = view(dst);
-    return sized(
-        ctx, dst, need,
-        [&] {
-            if (gs)
-                hipLaunchKernelGGL((k_list_from_set<true, false>), dim3(R), dim3(64), 0, ctx->stream,
-                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
-                                   tordp, nil, need, flag);
-            else
-                hipLaunchKernelGGL((k_list_from_set<false, false>), dim3(R), dim3(64), 0,
-                                   ctx->stream, (const u64*)src->dev, src->words_per_replica,
-                                   ordp, nslots, tordp, nil, need, flag);
-        },
-        [&](LV out) {
-            if (gs)
-                hipLaunchKernelGGL((k_list_from_set<true, true>), dim3(R), dim3(64), 0, ctx->stream,
-                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
-                                   tordp, out, need, flag);
-            else
-                hipLaunchKernelGGL((k_list_from_set<false, true>), dim3(R), dim3(64), 0, ctx->stream,
-                                   (const u64*)src->dev, src->words_per_replica, ordp, nslots,
-                                   tordp, out, need, flag);
-        },
-        "list_from_set");
+    if (gs)
+        return tiled<PFromSet<true>>(ctx, dst, nslots, 0, [&](char*) {
+            return PFromSet<true>{sp, wpr, ordp, nslots, E, tordp, flag};
+        }, "list_from_set");
+    return tiled<PFromSet<false>>(ctx, dst, nslots, 0, [&](char*) {
+        return PFromSet<false>{sp, wpr, ordp, nslots, E, tordp, flag};
+    }, "list_from_set");
 }
 
 static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch* a,
@@ -1451,6 +1544,7 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const unsigned rx = (unsigned)(R < (1u << 20) ? R : (1u << 20));
     const uint32_t cmax = m.ce_a > m.ce_b ? m.ce_a : m.ce_b;
     const unsigned gr = cmax ? (cmax + kMT - 1) / kMT : 1u;
+    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
     auto size_pass = [&](auto mode) {
         constexpr int MODE = decltype(mode)::value;
         hipMemsetAsync(m.unsorted, 0, sz_r, ctx->stream);
@@ -1495,22 +1589,9 @@ int laspj_list_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
     if (l && l->kind == LASPJ_KIND_GSET_LIST) {
         if (int s = pair_checks(ctx, dst, l, r, "list_union")) return s;
         LGuard g(ctx);
-        const uint64_t R = l->replicas;
-        auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-        if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_union: scratch");
-        const LV L = view(l), Rr = view(r), nil = view(dst);
-        uint32_t* flag = ctx->flag + 1;
-        return sized(
-            ctx, dst, need,
-            [&] {
-                hipLaunchKernelGGL((k_list_concat<false>), dim3(R), dim3(64), 0, ctx->stream, L,
-                                   Rr, nil, need, flag);
-            },
-            [&](LV out) {
-                hipLaunchKernelGGL((k_list_concat<true>), dim3(R), dim3(64), 0, ctx->stream, L,
-                                   Rr, out, need, flag);
-            },
-            "list_union");
+        const LV L = view(l), Rr = view(r);
+        return tiled<PConcat>(ctx, dst, (uint64_t)l->cap_e + r->cap_e, 0,
+                              [&](char*) { return PConcat{L, Rr}; }, "list_union");
     }
     return merge_impl(ctx, dst, l, r, ord, true, "list_union");
 }
@@ -1589,22 +1670,9 @@ int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
         return fail(ctx, LASPJ_E_KIND, "list_value: OR-Set list -> G-Set list");
     if (dst->replicas != src->replicas) return fail(ctx, LASPJ_E_SHAPE, "list_value: replicas");
     LGuard g(ctx);
-    const uint64_t R = src->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_value: scratch");
-    const LV S = view(src), nil = view(dst);
-    uint32_t* flag = ctx->flag + 1;
-    return sized(
-        ctx, dst, need,
-        [&] {
-            hipLaunchKernelGGL((k_list_value<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
-                               need, flag);
-        },
-        [&](LV out) {
-            hipLaunchKernelGGL((k_list_value<true>), dim3(R), dim3(64), 0, ctx->stream, S, out,
-                               need, flag);
-        },
-        "list_value");
+    const LV S = view(src);
+    return tiled<PValue>(ctx, dst, src->cap_e, 0, [&](char*) { return PValue{S}; },
+                         "list_value");
 }
 
 int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
@@ -1616,21 +1684,26 @@ int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch*
     LGuard g(ctx);
     const uint64_t R = l->replicas;
     const uint32_t hsize = pow2_at_least(2ull * r->cap_e);
-    char* base = static_cast<char*>(lscratch(ctx, R * hsize * 12ull + 8ull * R));
-    if (!base) return fail(ctx, LASPJ_E_NOMEM, "list_intersection: scratch");
-    u64* hk = reinterpret_cast<u64*>(base);
-    auto* hi = reinterpret_cast<uint32_t*>(base + R * hsize * 8ull);
-    auto* need = reinterpret_cast<uint32_t*>(base + R * hsize * 12ull);
-    const LV L = view(l), Rr = view(r), nil = view(dst);
-#define LJ_ISECT(G, W, OUT)                                                                    \
-    hipLaunchKernelGGL((k_list_intersection<G, W>), dim3(R), dim3(64), 0, ctx->stream, L, Rr, OUT, \
-                       rk, hk, hi, hsize, need)
+    const uint64_t hbytes = R * hsize * 12ull;
+    const LV L = view(l), Rr = view(r);
+    const dim3 hg((r->cap_e + 255) / 256 ? (r->cap_e + 255) / 256 : 1,
+                  (unsigned)(R < 65535 ? R : 65535));
+    auto pre = [&](auto gtag) {
+        constexpr bool G = decltype(gtag)::value;
+        return [&, hg](char* base) {
+            u64* hk = reinterpret_cast<u64*>(base);
+            auto* hi = reinterpret_cast<uint32_t*>(base + R * hsize * 8ull);
+            hipMemsetAsync(base, 0xFF, hbytes, ctx->stream);        // kEmpty / kNone
+            hipLaunchKernelGGL((k_isect_hash<G>), hg, dim3(256), 0, ctx->stream, Rr, rk, hk, hi,
+                               hsize, R);
+            return PIsect<G>{L, Rr, rk, hk, hi, hsize};
+        };
+    };
     if (gs)
-        return sized(ctx, dst, need, [&] { LJ_ISECT(true, false, nil); },
-                     [&](LV out) { LJ_ISECT(true, true, out); }, "list_intersection");
-    return sized(ctx, dst, need, [&] { LJ_ISECT(false, false, nil); },
-                 [&](LV out) { LJ_ISECT(false, true, out); }, "list_intersection");
-#undef LJ_ISECT
+        return tiled<PIsect<true>>(ctx, dst, l->cap_e, hbytes, pre(std::true_type{}),
+                                   "list_intersection");
+    return tiled<PIsect<false>>(ctx, dst, l->cap_e, hbytes, pre(std::false_type{}),
+                                "list_intersection");
 }
 
 int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
@@ -1638,20 +1711,16 @@ int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
     if (int s = pair_checks(ctx, dst, l, r, "list_product")) return s;
     const bool gs = l->kind == LASPJ_KIND_GSET_LIST;
     LGuard g(ctx);
-    const uint64_t R = l->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_product: scratch");
-    const LV L = view(l), Rr = view(r), nil = view(dst);
+    const LV L = view(l), Rr = view(r);
     uint32_t* flag = ctx->flag + 1;
-#define LJ_PROD(G, W, OUT)                                                                     \
-    hipLaunchKernelGGL((k_list_product<G, W>), dim3(R), dim3(64), 0, ctx->stream, L, Rr, OUT,   \
-                       need, flag)
+    const uint64_t mx = (uint64_t)l->cap_e * r->cap_e;
     if (gs)
-        return sized(ctx, dst, need, [&] { LJ_PROD(true, false, nil); },
-                     [&](LV out) { LJ_PROD(true, true, out); }, "list_product");
-    return sized(ctx, dst, need, [&] { LJ_PROD(false, false, nil); },
-                 [&](LV out) { LJ_PROD(false, true, out); }, "list_product");
-#undef LJ_PROD
+        return tiled<PProduct<true>>(ctx, dst, mx, 0,
+                                     [&](char*) { return PProduct<true>{L, Rr, flag}; },
+                                     "list_product");
+    return tiled<PProduct<false>>(ctx, dst, mx, 0,
+                                  [&](char*) { return PProduct<false>{L, Rr, flag}; },
+                                  "list_product");
 }
 
 static int unary_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch* src,
@@ -1670,46 +1739,23 @@ int laspj_list_map(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                    const laspj_buf* keys, uint32_t nidx, int per_entry) {
     if (int s = unary_checks(ctx, dst, src, keys, 8ull * nidx, "list_map")) return s;
     LGuard g(ctx);
-    const uint64_t R = src->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_map: scratch");
-    const LV S = view(src), nil = view(dst);
+    const LV S = view(src);
     const auto* tab = static_cast<const u64*>(keys->dev);
     uint32_t* flag = ctx->flag + 1;
-    return sized(
-        ctx, dst, need,
-        [&] {
-            hipLaunchKernelGGL((k_list_map<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
-                               tab, nidx, per_entry, need, flag);
-        },
-        [&](LV out) {
-            hipLaunchKernelGGL((k_list_map<true>), dim3(R), dim3(64), 0, ctx->stream, S, out, tab,
-                               nidx, per_entry, need, flag);
-        },
-        "list_map");
+    return tiled<PMap>(ctx, dst, src->cap_e, 0,
+                       [&](char*) { return PMap{S, tab, nidx, per_entry, flag}; }, "list_map");
 }
 
 int laspj_list_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                       const laspj_buf* keep, uint32_t nidx, int per_entry) {
     if (int s = unary_checks(ctx, dst, src, keep, nidx, "list_filter")) return s;
     LGuard g(ctx);
-    const uint64_t R = src->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_filter: scratch");
-    const LV S = view(src), nil = view(dst);
+    const LV S = view(src);
     const auto* tab = static_cast<const uint8_t*>(keep->dev);
     uint32_t* flag = ctx->flag + 1;
-    return sized(
-        ctx, dst, need,
-        [&] {
-            hipLaunchKernelGGL((k_list_filter<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
-                               tab, nidx, per_entry, need, flag);
-        },
-        [&](LV out) {
-            hipLaunchKernelGGL((k_list_filter<true>), dim3(R), dim3(64), 0, ctx->stream, S, out,
-                               tab, nidx, per_entry, need, flag);
-        },
-        "list_filter");
+    return tiled<PFilter>(ctx, dst, src->cap_e, 0,
+                          [&](char*) { return PFilter{S, tab, nidx, per_entry, flag}; },
+                          "list_filter");
 }
 
 int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
@@ -1727,24 +1773,13 @@ int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
         if (h[i + 1] < h[i]) return fail(ctx, LASPJ_E_INVAL, "list_fold: offsets not ascending");
     if (8ull * h[nidx] > keys->bytes)
         return fail(ctx, LASPJ_E_RANGE, "list_fold: keys buffer too small");
-    const uint64_t R = src->replicas;
-    auto* need = static_cast<uint32_t*>(lscratch(ctx, 8ull * R));
-    if (!need) return fail(ctx, LASPJ_E_NOMEM, "list_fold: scratch");
-    const LV S = view(src), nil = view(dst);
+    const LV S = view(src);
     const auto* po = static_cast<const uint32_t*>(off->dev);
     const auto* pk = static_cast<const u64*>(keys->dev);
     uint32_t* flag = ctx->flag + 1;
-    return sized(
-        ctx, dst, need,
-        [&] {
-            hipLaunchKernelGGL((k_list_fold<false>), dim3(R), dim3(64), 0, ctx->stream, S, nil,
-                               po, pk, nidx, per_entry, need, flag);
-        },
-        [&](LV out) {
-            hipLaunchKernelGGL((k_list_fold<true>), dim3(R), dim3(64), 0, ctx->stream, S, out, po,
-                               pk, nidx, per_entry, need, flag);
-        },
-        "list_fold");
+    return tiled<PFold>(ctx, dst, src->cap_e, 0,
+                        [&](char*) { return PFold{S, po, pk, nidx, per_entry, flag}; },
+                        "list_fold");
 }
 
 }  // extern "C"
