@@ -602,13 +602,80 @@ __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* lds4, u64* total) {
     return before + x - v;
 }
 
+// Split mode (few long payloads, e.g. the NIF's one merged 10k-element value): the
+// chunks of 256 term-order elements of a payload are written by different blocks.
+// k_etf_chunk_sizes gives every chunk its byte size and present-element count (packed
+// size | count << 40, the same per-element sizes as orset_elem_size), k_etf_chunk_scan
+// turns them into per-payload exclusive offsets (entry nch = the payload's totals), and
+// each block of the writer then starts at its chunk's byte offset with a fresh window:
+// bytes below its first byte belong to the previous chunk's block and are left alone
+// (byte stores at both ends of a block's range, as at payload ends).
+constexpr u64 kChunkCnt = 1ull << 40;
+
+__global__ __launch_bounds__(kBlock) void k_etf_chunk_sizes(const u64x2* cells, uint64_t R,
+                                                            uint32_t E, DictView d, uint32_t nch,
+                                                            u64* coff, uint32_t* flag) {
+    __shared__ u64 lds4[kBlock / 64];
+    for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
+        const uint64_t rep = it / nch;
+        const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
+        u64 v = 0;
+        if (i < E) {
+            const uint32_t e = d.elem_order[i];
+            const u64x2 x = cells[rep * E + e];
+            if (x.x) {
+                // as k_orset_etf_size: a present slot without an image is an error
+                if (d.elem_off[e + 1] == d.elem_off[e] || (x.x & ~d.tok_mask[e]) != 0) {
+                    if (flag) atomicOr(flag, 1u);
+                } else {
+                    v = orset_elem_size(d, e, x.x, x.y) + kChunkCnt;
+                }
+            }
+        }
+        u64 tot;
+        block_excl_scan64(v, lds4, &tot);
+        if (threadIdx.x == 0) coff[rep * (nch + 1ull) + c] = tot;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_etf_chunk_scan(u64* coff, uint64_t R, uint32_t nch) {
+    __shared__ u64 lds4[kBlock / 64];
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        u64* c = coff + rep * (nch + 1ull);
+        u64 carry = 0;
+        for (uint32_t t0 = 0; t0 <= nch; t0 += kBlock) {
+            const uint32_t t = t0 + threadIdx.x;
+            const u64 v = t < nch ? c[t] : 0;
+            u64 tot;
+            const u64 ex = block_excl_scan64(v, lds4, &tot);
+            if (t <= nch) c[t] = carry + ex;
+            carry += tot;
+        }
+    }
+}
+
+// payload sizes from the chunk totals (etf_size for few long payloads): as
+// k_orset_etf_size, 131 108 <n:32> elements 106 or 131 106, plus the tag bytes
+__global__ void k_etf_sizes_from_chunks(const u64* coff, uint64_t R, uint32_t nch, uint32_t hdr,
+                                        u64* sizes) {
+    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
+         rep += (uint64_t)gridDim.x * blockDim.x) {
+        const u64 t = coff[rep * (nch + 1ull) + nch];
+        const u64 n = t / kChunkCnt, sum = t & (kChunkCnt - 1);
+        sizes[rep] = hdr + 1u + (n ? 5u + sum + 1u : 1u);
+    }
+}
+
 // EPAR (few token slots per element): each element's thread also stages its own records
-// (no record -> element search, no rank select); otherwise records are spread over lanes
+// (no record -> element search, no rank select); otherwise records are spread over lanes.
+// coff != nullptr: split mode (above), block b writes chunks [g cper, (g + 1) cper) of
+// payload b / ngroups.
 template <uint32_t WIN, bool EPAR>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cells, uint64_t R,
                                                                 uint32_t E, DictView d, int tag,
                                                                 int vers, const u64* offs,
-                                                                uint8_t* out) {
+                                                                uint8_t* out, const u64* coff,
+                                                                uint32_t cper) {
     __shared__ __attribute__((aligned(16))) uint32_t winbuf[(WIN + 2 * kGuard) / 4];
     __shared__ uint32_t s_e[kBlock], s_pos[kBlock + 1], s_rec[kBlock + 1], s_hl[kBlock];
     __shared__ u64 s_p[kBlock], s_r[kBlock], lds4[kBlock / 64];
@@ -619,9 +686,21 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
     // a block owns a contiguous run of replicas, whose payloads are contiguous too: the
     // carry flows from one payload into the next and only the run's two ends need
     // byte stores
-    const uint64_t per_blk = (R + gridDim.x - 1) / gridDim.x;
-    const uint64_t r_begin = (uint64_t)blockIdx.x * per_blk;
-    const uint64_t r_end = r_begin + per_blk < R ? r_begin + per_blk : R;
+    const uint32_t nch = (E + kBlock - 1) / kBlock;
+    const uint32_t ngroups = coff ? (nch + cper - 1) / cper : 1u;
+    uint64_t r_begin, r_end;
+    uint32_t c_begin = 0, c_end = E;             // element positions [c_begin, c_end)
+    if (coff) {
+        r_begin = blockIdx.x / ngroups;
+        r_end = r_begin + 1;
+        const uint32_t g = blockIdx.x - (uint32_t)(r_begin * ngroups);
+        c_begin = g * cper * kBlock;
+        c_end = min(E, (g + 1) * cper * kBlock);
+    } else {
+        const uint64_t per_blk = (R + gridDim.x - 1) / gridDim.x;
+        r_begin = (uint64_t)blockIdx.x * per_blk;
+        r_end = r_begin + per_blk < R ? r_begin + per_blk : R;
+    }
     if (r_begin >= R) return;
     for (uint32_t x = tid; x < (WIN + 2 * kGuard) / 16; x += kBlock)
         reinterpret_cast<u32x4*>(winbuf)[x] = u32x4{0, 0, 0, 0};
@@ -641,11 +720,20 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
         v_next = cells[r_begin * E + e_c];
     }
     u64 mask_lo = offs[r_begin];    // output bytes below this belong to another block
+    uint32_t n_split = 0;
+    u64 cur_split = 0;
+    if (coff) {
+        // this block's first byte: the payload's header for chunk 0, else its chunk's
+        const u64* co = coff + r_begin * (nch + 1ull);
+        n_split = (uint32_t)(co[nch] / kChunkCnt);
+        cur_split = mask_lo + hdr + (n_split ? 6u : 2u) + (co[c_begin / kBlock] & (kChunkCnt - 1));
+        if (c_begin) mask_lo = cur_split;
+    }
     u64 seg_lo = mask_lo;           // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
     for (uint64_t rep = r_begin; rep < r_end; ++rep) {
         const u64x2* c = cells + rep * E;
         const u64 base = offs[rep], end = offs[rep + 1];
-        if (seg_lo != base) {
+        if (!coff && seg_lo != base) {
             // the previous payload broke off (sizes disagreed): flush, restart at base
             if (tid < 16) {
                 const u64 g = (seg_lo & ~15ull) + tid;
@@ -659,16 +747,16 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
         }
         // present elements (the list header's length field): counted up front when the
         // replica spans several chunks, else taken from the one chunk's scan
-        uint32_t n = 0;
-        if (E > kBlock) {
+        uint32_t n = n_split;
+        if (!coff && E > kBlock) {
             u64 cnt = 0;
             for (uint32_t e = tid; e < E; e += kBlock) cnt += cw[2ull * (rep * E + e)] != 0;
             u64 n64;
             block_excl_scan64(cnt, lds4, &n64);
             n = (uint32_t)n64;
         }
-        u64 cursor = 0;                             // next element byte
-        for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
+        u64 cursor = cur_split;                     // next element byte
+        for (uint32_t c0 = c_begin; c0 < c_end; c0 += kBlock) {
             const bool last = c0 + kBlock >= E;
             // ---- A: element sizes, term-order token masks, record numbering
             const uint32_t i = c0 + tid;
@@ -2692,7 +2780,14 @@ int etf_size(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int 
     LJ_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const u64*)nullptr,
                                                  (u64*)nullptr, n, ctx->stream));
     const uint64_t sizes_bytes = (8ull * n + 255ull) & ~255ull;
-    if (int s = reserve_scratch(ctx, sizes_bytes + temp)) return s;
+    const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+    // few long OR-Set payloads: sizes from per-chunk sums spread over the chip (as the
+    // writer's split mode) instead of one wave walking each payload
+    const bool split = kind == LASPJ_KIND_ORSET && R <= (uint64_t)ctx->cus && nch >= 4;
+    const uint64_t temp_bytes = (temp + 255ull) & ~255ull;
+    if (int s = reserve_scratch(ctx, sizes_bytes + temp_bytes +
+                                (split ? 8ull * R * (nch + 1ull) : 0ull)))
+        return s;
     u64* sizes = static_cast<u64*>(ctx->scratch);
     void* tmp = static_cast<char*>(ctx->scratch) + sizes_bytes;
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
@@ -2700,7 +2795,18 @@ int etf_size(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int 
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
     uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     int grid = (int)(blocks < cap ? blocks : cap);
-    if (kind == LASPJ_KIND_ORSET)
+    if (split) {
+        u64* co = reinterpret_cast<u64*>(static_cast<char*>(ctx->scratch) + sizes_bytes +
+                                         temp_bytes);
+        const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+        hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), nch,
+                           co, ctx->flag);
+        hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                           dim3(kBlock), 0, ctx->stream, co, R, nch);
+        hipLaunchKernelGGL(k_etf_sizes_from_chunks, dim3((unsigned)((R + 255) / 256)), dim3(256),
+                           0, ctx->stream, co, R, nch, hdr, sizes);
+    } else if (kind == LASPJ_KIND_ORSET)
         hipLaunchKernelGGL(k_orset_etf_size, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), hdr,
                            sizes, ctx->flag);
@@ -2760,10 +2866,28 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
         }
         const uint64_t resident = (uint64_t)ctx->cus * (uint64_t)occ;
         grid = (int)(R < resident ? R : resident);
+        const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+        const u64* coff = nullptr;
+        uint32_t cper = 0;
+        if (4 * R <= resident && nch >= 4) {
+            // split mode: few long payloads, their chunks spread over blocks
+            cper = (uint32_t)std::max<uint64_t>(1, (R * nch + resident - 1) / resident);
+            const uint64_t groups = (nch + cper - 1) / cper;
+            if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
+            u64* co = static_cast<u64*>(ctx->scratch);
+            const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+            hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+                               reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d),
+                               nch, co, (uint32_t*)nullptr);
+            hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                               dim3(kBlock), 0, ctx->stream, co, R, nch);
+            coff = co;
+            grid = (int)(R * groups);
+        }
         hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, static_cast<const u64*>(offsets->dev),
-                           static_cast<uint8_t*>(out->dev));
+                           static_cast<uint8_t*>(out->dev), coff, cper);
     } else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
         hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,

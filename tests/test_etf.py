@@ -321,6 +321,77 @@ def test_gpu_orset_record_kernel_edges(tok_len, long_elems, pool_n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R,nelem,pool_n,density", [
+    (1, 3000, 64, 0.9), (3, 2600, 6, 0.5), (2, 5000, 40, 0.02), (200, 3000, 3, 0.08)])
+def test_gpu_record_kernel_split_payloads(R, nelem, pool_n, density):
+    """Few long payloads (the NIF's one merged value): the writer's split mode gives each
+    block a run of 256-element chunks of one payload at its chunk's byte offset — one to
+    200 payloads of up to 5000 elements, dense and sparse (whole chunks empty), 64 and
+    <= 8 token slots per element, element images across chunk edges: every payload equals
+    the oracle's term_to_binary byte for byte, bare and tagged, under every writer."""
+    from lasp_amd import engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle.otp import lists_sort
+    rng = random.Random(R * 131 + nelem)
+    elems = list(range(nelem))
+    pool = [bytes(rng.randrange(256) for _ in range(20)) for _ in range(97)]
+    states = []
+    for i in range(R):
+        d = {}
+        for e in elems:
+            if rng.random() < density:
+                d[e] = {pool[(e * 7 + j) % 97]: rng.random() < 0.3
+                        for j in rng.sample(range(pool_n), rng.randint(1, min(pool_n, 6)))}
+        states.append([(k, [(t, d[k][t]) for t in sorted(d[k])]) for k in lists_sort(list(d))])
+    dom = Domain()
+    for e in elems:                                   # every element registered, in order
+        es = dom.element_slot(e)
+        for j in range(pool_n):
+            dom.token_slot(es, pool[(e * 7 + j) % 97])
+    E = dom.size
+    ctx = context()
+    b = ctx.orset_batch(R, E)
+    b.upload(dom.encode_orset(states, E))
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E))
+    want = [oetf.term_to_binary(s) for s in states]
+    for bare, tagged in _etf_variants(ctx, lambda: (b.to_binaries(d),
+                                                    b.to_binaries(d, tag=etf.DT_ORSET_TAG))):
+        assert bare == want
+        assert tagged == [bytes([etf.DT_ORSET_TAG, 1]) + w for w in want]
+
+
+@pytest.mark.gpu
+def test_gpu_etf_split_sizes_reject_unregistered_slots():
+    """The chunked size pass (few long payloads) flags a present slot without an image
+    like the per-payload one, and agrees with it on valid payloads."""
+    import numpy as np
+    from lasp_amd import _lib, engine
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    n = 3000
+    s = [(e, [(b"t" + e.to_bytes(19, "big"), e % 3 == 0)]) for e in range(n)]
+    dom = Domain()
+    dom.register_orset(s)
+    ctx = context()
+    b = ctx.orset_batch(1, n + 5)
+    cells = dom.encode_orset([s], n + 5)
+    b.upload(cells)
+    d = engine.ETFDict(ctx, n + 5, *dom.etf_arrays(n + 5))
+    offs, out, total = b.etf_encode(d)
+    assert int(offs.download(np.uint64)[1]) == total == len(oetf.term_to_binary(s))
+    cells[0, n + 2, 0] = 1                               # slot n + 2 has no image
+    b.upload(cells)
+    with pytest.raises(_lib.LaspjError):
+        b.etf_encode(d)
+    cells[0, n + 2, 0] = 0
+    cells[0, 17, 0] = 0b100                              # token slot 2 of element 17
+    b.upload(cells)
+    with pytest.raises(_lib.LaspjError):
+        b.etf_encode(d)
+
+
+@pytest.mark.gpu
 def test_gpu_record_kernel_whole_buffer_equals_staging():
     """2048 replicas x 512 slots x 64 token slots (~1.1 GB of payloads): the record and
     the staging kernels write identical buffers, every byte of every replica."""

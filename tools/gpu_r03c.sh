@@ -11,4 +11,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/tests.log
 [ $rc -eq 0 ] || exit $rc
 PROFILE_STORE=1 timeout -k 10 300 python -u tools/list_bench.py > gpurun_out/list_bench.log 2> gpurun_out/list_bench_prof.txt
 rc=$?; echo "list_bench rc=$rc"; tail -c 1500 gpurun_out/list_bench.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -c 1500 gpurun_out/bench.log
 exit $rc
