@@ -2441,47 +2441,80 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
 
 // per replica: is the segment chain one well-formed orddict?  Yes: status OK.  No:
 // onto the redo list (decoded again serially, which gives the reference's status).
-__global__ void k_etf_read_chain(const uint8_t* payload, const u64* offs, uint64_t R,
-                                 const uint32_t* segbase, uint32_t S, const SegRes* res,
-                                 int32_t* status, uint32_t* redo) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    const u64 base = offs[r];
-    const u64 len = offs[r + 1] - base;
-    const uint32_t g0 = segbase[r], ns = segbase[r + 1] - g0;
-    const SegRes a = res[g0];
-    bool ok = a.st == LASPJ_DEC_OK;
-    if (ok && (a.flags & kSegEmptyList)) {
-        ok = a.end == len;
-    } else if (ok) {
-        u64 q = a.end;
-        uint32_t cnt = a.cnt;
-        int64_t rl = a.rlast;
-        for (uint32_t s = 1; s < ns && ok; ++s) {
-            const SegRes b = res[g0 + s];
-            const u64 send = (u64)(s + 1) * S;
-            if (b.start == kSegNone) {
-                // no header found: fine only if none starts here (q past the segment, or
-                // q on the list's closing 106)
-                if (q < send && q < len && payload[base + q] != 106) ok = false;
-                continue;
+// One wave per replica, lanes over its segments 64 at a time: segment s's predecessor
+// is the latest earlier segment that found an element start (a max-scan of indices
+// over the lanes, carried between groups of 64), and every segment checks itself
+// against it — a start that found nothing is fine only where no element starts, a
+// found one must begin exactly at its predecessor's end with a higher first rank —
+// then one ballot and one sum of element counts decide (the chain's checks, evaluated
+// in parallel: the answer is whether any of them fails).
+__global__ __launch_bounds__(64) void k_etf_read_chain(const uint8_t* payload, const u64* offs,
+                                                       uint64_t R, const uint32_t* segbase,
+                                                       uint32_t S, const SegRes* res,
+                                                       int32_t* status, uint32_t* redo) {
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t r = blockIdx.x; r < R; r += gridDim.x) {
+        const u64 base = offs[r];
+        const u64 len = offs[r + 1] - base;
+        const uint32_t g0 = segbase[r], ns = segbase[r + 1] - g0;
+        const SegRes a = res[g0];
+        bool ok = a.st == LASPJ_DEC_OK;
+        if (ok && (a.flags & kSegEmptyList)) {
+            ok = a.end == len;
+        } else if (ok) {
+            uint32_t q = a.end, cnt = 0;
+            int32_t rl = a.rlast;
+            bool bad = false;
+            for (uint32_t s0 = 1; s0 < ns; s0 += 64) {
+                const uint32_t s = s0 + lane;
+                SegRes b{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
+                if (s < ns) b = res[g0 + s];
+                const bool valid = s < ns && b.start != kSegNone;
+                int32_t li = valid ? (int32_t)lane : -1;      // latest valid lane <= this one
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int32_t v = __shfl_up(li, off, 64);
+                    if ((int)lane >= off) li = max(li, v);
+                }
+                int32_t lp = __shfl_up(li, 1, 64);             // ... strictly before it
+                if (lane == 0) lp = -1;
+                const uint32_t e_at = __shfl(b.end, lp < 0 ? 0 : lp, 64);
+                const int32_t r_at = __shfl(b.rlast, lp < 0 ? 0 : lp, 64);
+                const uint32_t pq = lp >= 0 ? e_at : q;
+                const int32_t prl = lp >= 0 ? r_at : rl;
+                if (s < ns) {
+                    if (!valid) {
+                        // no header found: fine only if none starts here (the predecessor's
+                        // end past the segment, or on the list's closing 106)
+                        const u64 send = (u64)(s + 1) * S;
+                        if (pq < send && pq < len && payload[base + pq] != 106) bad = true;
+                    } else if (b.start != pq || b.st != LASPJ_DEC_OK || b.rfirst <= prl) {
+                        bad = true;
+                    } else {
+                        cnt += b.cnt;
+                    }
+                }
+                const int32_t last = __shfl(li, 63, 64);
+                if (last >= 0) {
+                    q = __shfl(b.end, last, 64);
+                    rl = __shfl(b.rlast, last, 64);
+                }
             }
-            if (b.start != q || b.st != LASPJ_DEC_OK || b.rfirst <= rl) {
-                ok = false;
-                break;
-            }
-            q = b.end;
-            cnt += b.cnt;
-            rl = b.rlast;
+            uint32_t tot = cnt;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+            ok = !__ballot(bad) && a.cnt + tot == a.n && (u64)q + 1 == len &&
+                 payload[base + q] == 106;
         }
-        ok = ok && cnt == a.n && q + 1 == len && payload[base + q] == 106;
-    }
-    if (ok) {
-        status[r] = LASPJ_DEC_OK;
-    } else {
-        status[r] = LASPJ_DEC_MALFORMED;       // rewritten by the redo pass
-        const uint32_t i = atomicAdd(redo, 1u);
-        redo[1 + i] = (uint32_t)r;
+        if (lane == 0) {
+            if (ok) {
+                status[r] = LASPJ_DEC_OK;
+            } else {
+                status[r] = LASPJ_DEC_MALFORMED;       // rewritten by the redo pass
+                const uint32_t i = atomicAdd(redo, 1u);
+                redo[1 + i] = (uint32_t)r;
+            }
+        }
     }
 }
 
@@ -2993,7 +3026,8 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
                            tag, vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
                            (uint32_t)S, hh, dres);
         LJ_LAUNCHED(ctx);
-        hipLaunchKernelGGL(k_etf_read_chain, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,
+        hipLaunchKernelGGL(k_etf_read_chain,
+                           dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)), dim3(64), 0,
                            ctx->stream, static_cast<const uint8_t*>(payload->dev),
                            static_cast<const u64*>(offsets->dev), R, dsegbase, (uint32_t)S, dres,
                            static_cast<int32_t*>(status->dev), redo);
