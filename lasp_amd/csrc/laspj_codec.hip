@@ -2851,10 +2851,9 @@ int etf_size(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int 
     LJ_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, temp, sizes, static_cast<u64*>(offsets->dev),
                                                  n, ctx->stream));
     uint32_t flag = 0;
-    LJ_HIP(ctx, hipMemcpyAsync(&flag, ctx->flag, 4, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipMemcpyAsync(total, static_cast<u64*>(offsets->dev) + R, 8,
-                               hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const laspj::ReadPiece rp[2] = {{&flag, ctx->flag, 4},
+                                    {total, static_cast<u64*>(offsets->dev) + R, 8}};
+    LJ_HIP(ctx, laspj::readback(ctx, rp, 2));
     if (flag)
         return fail(ctx, LASPJ_E_RANGE, "%s: a present element or token slot has no image in "
                     "the dictionary", what);
@@ -2872,9 +2871,7 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
     Guard g(ctx);
     const uint64_t R = b->replicas;
     uint64_t total = 0;
-    LJ_HIP(ctx, hipMemcpyAsync(&total, static_cast<u64*>(offsets->dev) + R, 8,
-                               hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, &total, static_cast<u64*>(offsets->dev) + R, 8));
     if (out->bytes < total)
         return fail(ctx, LASPJ_E_RANGE, "%s: output holds %llu bytes, payloads need %llu", what,
                     (unsigned long long)out->bytes, (unsigned long long)total);
@@ -2958,9 +2955,7 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     Guard g(ctx);
     const uint64_t R = b->replicas;
     std::vector<u64> off(R + 1);
-    LJ_HIP(ctx, hipMemcpyAsync(off.data(), offsets->dev, 8ull * (R + 1), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, off.data(), offsets->dev, 8ull * (R + 1)));
     for (uint64_t i = 0; i < R; ++i)
         if (off[i] > off[i + 1])
             return fail(ctx, LASPJ_E_RANGE, "%s: offsets decrease at replica %llu", what,
@@ -3079,9 +3074,7 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     Guard g(ctx);
     const uint64_t R = b->replicas;
     std::vector<u64> off(R + 1);
-    LJ_HIP(ctx, hipMemcpyAsync(off.data(), offsets->dev, 8ull * (R + 1), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, off.data(), offsets->dev, 8ull * (R + 1)));
     for (uint64_t i = 0; i < R; ++i)
         if (off[i] > off[i + 1])
             return fail(ctx, LASPJ_E_RANGE, "%s: offsets decrease at replica %llu", what,

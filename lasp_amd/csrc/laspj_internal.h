@@ -37,6 +37,10 @@ struct laspj_ctx {
     // list kernels' scratch (merge plans, key-order arrays, hash tables, sizes)
     void* lscratch = nullptr;
     uint64_t lscratch_bytes = 0;
+    // pinned host staging for the small readbacks (sizes, statuses, flags): a round trip
+    // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
+    void* pinned = nullptr;
+    static constexpr uint64_t kPinned = 64 * 1024;
 };
 
 struct laspj_buf {
@@ -74,6 +78,19 @@ namespace laspj {
 int fail(laspj_ctx* ctx, int code, const char* fmt, ...);
 
 inline uint64_t bytes_of(const laspj_batch* b) { return b->replicas * b->words_per_replica * 8ull; }
+
+// Device -> host copies of up to a few pieces in one synchronisation, staged through the
+// context's pinned buffer when they fit (laspj_runtime.hip).  Returns a hipError_t.
+struct ReadPiece {
+    void* host;
+    const void* dev;
+    uint64_t bytes;
+};
+hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n);
+inline hipError_t readback(laspj_ctx* ctx, void* host, const void* dev, uint64_t bytes) {
+    const ReadPiece p{host, dev, bytes};
+    return readback(ctx, &p, 1);
+}
 
 #define LJ_HIP(ctx, call)                                                              \
     do {                                                                               \

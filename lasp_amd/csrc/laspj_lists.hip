@@ -1275,10 +1275,7 @@ uint32_t pow2_at_least(uint64_t n) {
     return (uint32_t)h;
 }
 
-int read_flag(laspj_ctx* ctx, const char* what) {
-    uint32_t f = 0;
-    LJ_HIP(ctx, hipMemcpyAsync(&f, ctx->flag + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+int flag_status(laspj_ctx* ctx, uint32_t f, const char* what) {
     if (f & kErrFun)
         return fail(ctx, LASPJ_E_FUN, "%s: the fun failed on a key of the list", what);
     if (f & kErrNested)
@@ -1290,6 +1287,12 @@ int read_flag(laspj_ctx* ctx, const char* what) {
     return LASPJ_OK;
 }
 
+int read_flag(laspj_ctx* ctx, const char* what) {
+    uint32_t f = 0;
+    LJ_HIP(ctx, laspj::readback(ctx, &f, ctx->flag + 1, 4));
+    return flag_status(ctx, f, what);
+}
+
 // run a size pass, size dst from the per-replica maxima, then the write pass
 template <class SizeFn, class WriteFn>
 int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, WriteFn write_pass,
@@ -1298,9 +1301,10 @@ int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, Wr
     size_pass();
     LJ_LAUNCHED(ctx);
     std::vector<uint32_t> h(2 * R);
-    LJ_HIP(ctx, hipMemcpyAsync(h.data(), need, 8ull * R, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (int s = read_flag(ctx, what)) return s;
+    uint32_t f = 0;
+    const laspj::ReadPiece rp[2] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
+    LJ_HIP(ctx, laspj::readback(ctx, rp, 2));
+    if (int s = flag_status(ctx, f, what)) return s;
     uint32_t ce = 0, ct = 0;
     for (uint64_t i = 0; i < R; ++i) {
         ce = h[2 * i] > ce ? h[2 * i] : ce;
@@ -1378,9 +1382,7 @@ int laspj_list_counts(laspj_ctx* ctx, const laspj_batch* b, uint32_t* out) {
     if (int s = check_list(ctx, b, "list_counts")) return s;
     if (!out) return fail(ctx, LASPJ_E_INVAL, "list_counts: null output");
     LGuard g(ctx);
-    LJ_HIP(ctx, hipMemcpyAsync(out, b->dev, 8ull * b->replicas, hipMemcpyDeviceToHost,
-                               ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, out, b->dev, 8ull * b->replicas));
     return LASPJ_OK;
 }
 
@@ -1433,8 +1435,7 @@ int laspj_list_download(laspj_ctx* ctx, const laspj_batch* b, uint64_t replica, 
     LGuard g(ctx);
     LV v = view(b);
     uint32_t hdr[2];
-    LJ_HIP(ctx, hipMemcpyAsync(hdr, v.hdr + 2 * replica, 8, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, hdr, v.hdr + 2 * replica, 8));
     if ((hdr[0] && !keys) || (!gs && (!toff || (hdr[1] && !toks))))
         return fail(ctx, LASPJ_E_INVAL, "list_download: null arrays");
     if (hdr[0])
@@ -1766,9 +1767,7 @@ int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
     LGuard g(ctx);
     // the CSR offsets must stay inside the keys buffer
     std::vector<uint32_t> h((uint64_t)nidx + 1);
-    LJ_HIP(ctx, hipMemcpyAsync(h.data(), off->dev, 4ull * h.size(), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, h.data(), off->dev, 4ull * h.size()));
     for (uint32_t i = 0; i < nidx; ++i)
         if (h[i + 1] < h[i]) return fail(ctx, LASPJ_E_INVAL, "list_fold: offsets not ascending");
     if (8ull * h[nidx] > keys->bytes)

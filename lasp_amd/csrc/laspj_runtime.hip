@@ -8,6 +8,7 @@
 // LASPJ_E_NOMEM via the nothrow paths below.
 
 #include <cstdarg>
+#include <cstring>
 #include <new>
 #include <vector>
 
@@ -123,6 +124,34 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
 
 }  // namespace
 
+namespace laspj {
+
+hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n) {
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) total += (pieces[i].bytes + 15) & ~15ull;
+    const bool stage = ctx->pinned && total <= laspj_ctx::kPinned;
+    uint64_t at = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!pieces[i].bytes) continue;
+        void* to = stage ? static_cast<char*>(ctx->pinned) + at : pieces[i].host;
+        hipError_t e = hipMemcpyAsync(to, pieces[i].dev, pieces[i].bytes, hipMemcpyDeviceToHost,
+                                      ctx->stream);
+        if (e != hipSuccess) return e;
+        at += (pieces[i].bytes + 15) & ~15ull;
+    }
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess || !stage) return e;
+    at = 0;
+    for (int i = 0; i < n; ++i) {
+        if (pieces[i].bytes)
+            memcpy(pieces[i].host, static_cast<const char*>(ctx->pinned) + at, pieces[i].bytes);
+        at += (pieces[i].bytes + 15) & ~15ull;
+    }
+    return hipSuccess;
+}
+
+}  // namespace laspj
+
 extern "C" {
 
 int laspj_abi_version(void) { return LASPJ_ABI_VERSION; }
@@ -178,6 +207,10 @@ int laspj_ctx_create(int device, laspj_ctx** out) {
         delete ctx;
         return LASPJ_E_NOMEM;
     }
+    if (hipHostMalloc(&ctx->pinned, laspj_ctx::kPinned, hipHostMallocDefault) != hipSuccess) {
+        hipGetLastError();
+        ctx->pinned = nullptr;            // readbacks then go to pageable memory directly
+    }
     *out = ctx;
     return LASPJ_OK;
 }
@@ -191,6 +224,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->flag) hipFree(ctx->flag);
         if (ctx->partials) hipFree(ctx->partials);
         if (ctx->lscratch) hipFree(ctx->lscratch);
+        if (ctx->pinned) hipHostFree(ctx->pinned);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -329,9 +363,7 @@ int laspj_buf_download(laspj_ctx* ctx, const laspj_buf* b, uint64_t off, void* d
         return fail(ctx, LASPJ_E_RANGE, "buf_download: range out of bounds");
     Guard g(ctx);
     if (!bytes) return LASPJ_OK;
-    LJ_HIP(ctx, hipMemcpyAsync(dst, static_cast<const char*>(b->dev) + off, bytes,
-                               hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, dst, static_cast<const char*>(b->dev) + off, bytes));
     return LASPJ_OK;
 }
 
@@ -457,9 +489,7 @@ int laspj_batch_download_range(laspj_ctx* ctx, const laspj_batch* b, uint64_t of
         return fail(ctx, LASPJ_E_RANGE, "batch_download_range: range out of bounds");
     Guard g(ctx);
     if (!bytes) return LASPJ_OK;
-    LJ_HIP(ctx, hipMemcpyAsync(host, reinterpret_cast<const char*>(b->dev) + offset, bytes,
-                               hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, host, reinterpret_cast<const char*>(b->dev) + offset, bytes));
     return LASPJ_OK;
 }
 
@@ -491,9 +521,7 @@ int laspj_batch_download(laspj_ctx* ctx, const laspj_batch* b, uint64_t first,
         return fail(ctx, LASPJ_E_RANGE, "batch_download: replicas out of range");
     Guard g(ctx);
     uint64_t rb = b->words_per_replica * 8ull;
-    LJ_HIP(ctx, hipMemcpyAsync(host, reinterpret_cast<const char*>(b->dev) + first * rb,
-                               count * rb, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, host, reinterpret_cast<const char*>(b->dev) + first * rb, count * rb));
     return LASPJ_OK;
 }
 
@@ -802,9 +830,7 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
     LJ_HIP(ctx, hipMemcpyAsync(dops, ops, nops * sizeof(laspj_op), hipMemcpyHostToDevice,
                                ctx->stream));
     LJ_HIP(ctx, laspj::launch_apply_ops(ctx, b, dops, nops, dst));
-    LJ_HIP(ctx, hipMemcpyAsync(status, dst, nops * sizeof(int32_t), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, status, dst, nops * sizeof(int32_t)));
     return LASPJ_OK;
 }
 
@@ -900,8 +926,7 @@ int laspj_orset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
     LJ_HIP(ctx, laspj::launch_orset_product(ctx, dst, l, r, ctx->flag));
     uint32_t flag = 0;
-    LJ_HIP(ctx, hipMemcpyAsync(&flag, ctx->flag, 4, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, &flag, ctx->flag, 4));
     if (flag)
         return fail(ctx, LASPJ_E_RANGE,
                     "orset_product: an input element uses token slot >= 8 (4-byte cells)");
@@ -924,8 +949,7 @@ int laspj_orset_product_diag(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
     LJ_HIP(ctx, laspj::launch_orset_product_diag(ctx, dst, l, r, ctx->flag));
     uint32_t flag = 0;
-    LJ_HIP(ctx, hipMemcpyAsync(&flag, ctx->flag, 4, hipMemcpyDeviceToHost, ctx->stream));
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LJ_HIP(ctx, laspj::readback(ctx, &flag, ctx->flag, 4));
     if (flag)
         return fail(ctx, LASPJ_E_RANGE,
                     "orset_product_diag: an input element uses token slot >= 8 (4-byte cells)");
