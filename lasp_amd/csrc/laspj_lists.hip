@@ -780,38 +780,50 @@ constexpr uint32_t kPT = 256;             // threads per tile block
 constexpr uint32_t kPI = 4;               // items per thread
 constexpr uint32_t kPTile = kPT * kPI;
 
-__device__ __forceinline__ u64 pk2(uint32_t ne, uint32_t nt) { return (u64)ne | ((u64)nt << 32); }
+// {entries, tokens} of an item, a tile or a replica prefix (64-bit sums: a total past
+// the list's 32-bit counts is caught by the scan, never wrapped)
+struct C2 {
+    u64 e, t;
+    __device__ C2& operator+=(const C2& o) {
+        e += o.e;
+        t += o.t;
+        return *this;
+    }
+    __device__ bool any() const { return (e | t) != 0; }
+};
+__device__ __forceinline__ C2 operator+(C2 a, const C2& b) { return a += b; }
+__device__ __forceinline__ C2 pk2(uint32_t ne, uint32_t nt) { return C2{ne, nt}; }
 
-// exclusive block scan of packed {ne, nt} (each half summed separately: no carries)
-__device__ __forceinline__ u64 block_scan_pk(u64 v, u64* lds, u64* total) {
+// exclusive block scan of {ne, nt}
+__device__ __forceinline__ C2 block_scan_pk(C2 v, C2* lds, C2* total) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    u64 x = v;
+    C2 x = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const u64 y = __shfl_up(x, off, 64);
+        const C2 y{__shfl_up(x.e, off, 64), __shfl_up(x.t, off, 64)};
         if ((int)lane >= off) x += y;
     }
     if (lane == 63) lds[w] = x;
     __syncthreads();
-    u64 before = 0, all = 0;
+    C2 before{0, 0}, all{0, 0};
 #pragma unroll
     for (uint32_t i = 0; i < kPT / 64; ++i) {
-        const u64 t = lds[i];
+        const C2 t = lds[i];
         if (i < w) before += t;
         all += t;
     }
     __syncthreads();
     *total = all;
-    return before + x - v;
+    return C2{before.e + x.e - v.e, before.t + x.t - v.t};
 }
 
 template <class P>
-__global__ __launch_bounds__(kPT) void k_tp_count(P p, u64* tc, uint32_t ntile, uint64_t R) {
-    __shared__ u64 lds[kPT / 64];
+__global__ __launch_bounds__(kPT) void k_tp_count(P p, C2* tc, uint32_t ntile, uint64_t R) {
+    __shared__ C2 lds[kPT / 64];
     const uint32_t t = blockIdx.x;
     for (uint64_t r = blockIdx.y; r < R; r += gridDim.y) {
         const u64 n = p.items(r), i0 = (u64)t * kPTile;
-        u64 sum = 0;
+        C2 sum{0, 0};
         if (i0 < n) {
 #pragma unroll
             for (uint32_t k = 0; k < kPI; ++k) {
@@ -819,38 +831,40 @@ __global__ __launch_bounds__(kPT) void k_tp_count(P p, u64* tc, uint32_t ntile, 
                 if (i < n) sum += p.count(r, i);
             }
         }
-        u64 tot;
+        C2 tot;
         block_scan_pk(sum, lds, &tot);
         if (threadIdx.x == 0) tc[r * ntile + t] = tot;
     }
 }
 
-__global__ __launch_bounds__(kPT) void k_tp_scan(u64* tc, uint32_t ntile, uint64_t R,
+__global__ __launch_bounds__(kPT) void k_tp_scan(C2* tc, uint32_t ntile, uint64_t R,
                                                  uint32_t* need, uint32_t* flag) {
-    __shared__ u64 lds[kPT / 64];
+    __shared__ C2 lds[kPT / 64];
     for (uint64_t r = blockIdx.x; r < R; r += gridDim.x) {
-        u64* c = tc + r * ntile;
-        u64 carry = 0;
+        C2* c = tc + r * ntile;
+        C2 carry{0, 0};
         for (uint32_t t0 = 0; t0 < ntile; t0 += kPT) {
             const uint32_t t = t0 + threadIdx.x;
-            const u64 v = t < ntile ? c[t] : 0;
-            u64 tot;
-            const u64 ex = block_scan_pk(v, lds, &tot);
+            const C2 v = t < ntile ? c[t] : C2{0, 0};
+            C2 tot;
+            const C2 ex = block_scan_pk(v, lds, &tot);
             if (t < ntile) c[t] = carry + ex;
             carry += tot;
         }
         if (threadIdx.x == 0) {
-            need[2 * r] = (uint32_t)carry;
-            need[2 * r + 1] = (uint32_t)(carry >> 32);
+            // a list counts entries and tokens in 32 bits
+            if (carry.e > 0xFFFFFFFFull || carry.t > 0xFFFFFFFFull) lraise(flag, kErrRange);
+            need[2 * r] = (uint32_t)min(carry.e, 0xFFFFFFFFull);
+            need[2 * r + 1] = (uint32_t)min(carry.t, 0xFFFFFFFFull);
         }
     }
 }
 
 template <class P>
-__global__ __launch_bounds__(kPT) void k_tp_write(P p, LV out, const u64* tc, uint32_t ntile,
+__global__ __launch_bounds__(kPT) void k_tp_write(P p, LV out, const C2* tc, uint32_t ntile,
                                                   uint64_t R, const uint32_t* need,
                                                   uint32_t* flag) {
-    __shared__ u64 lds[kPT / 64];
+    __shared__ C2 lds[kPT / 64];
     const uint32_t t = blockIdx.x;
     for (uint64_t r = blockIdx.y; r < R; r += gridDim.y) {
         const u64 n = p.items(r), i0 = (u64)t * kPTile + (u64)threadIdx.x * kPI;
@@ -865,21 +879,21 @@ __global__ __launch_bounds__(kPT) void k_tp_write(P p, LV out, const u64* tc, ui
             }
         }
         if ((u64)t * kPTile >= n) continue;        // block-uniform: no barrier skipped
-        u64 c[kPI], mine = 0;
+        C2 c[kPI], mine{0, 0};
 #pragma unroll
         for (uint32_t k = 0; k < kPI; ++k) {
-            c[k] = i0 + k < n ? p.count(r, i0 + k) : 0;
+            c[k] = i0 + k < n ? p.count(r, i0 + k) : C2{0, 0};
             mine += c[k];
         }
-        u64 tot;
-        u64 at = tc[r * ntile + t] + block_scan_pk(mine, lds, &tot);
+        C2 tot;
+        C2 at = tc[r * ntile + t] + block_scan_pk(mine, lds, &tot);
 #pragma unroll
         for (uint32_t k = 0; k < kPI; ++k) {
-            if (c[k]) {
-                const uint32_t pos = (uint32_t)at, tpos = (uint32_t)(at >> 32);
-                const uint32_t ne = (uint32_t)c[k], nt = (uint32_t)(c[k] >> 32);
-                if ((u64)pos + ne > out.ce || (u64)tpos + nt > out.ct) lraise(flag, kErrRange);
-                else p.write(r, i0 + k, pos, tpos, out);
+            if (c[k].any()) {
+                if (at.e + c[k].e > out.ce || at.t + c[k].t > out.ct)
+                    lraise(flag, kErrRange);
+                else
+                    p.write(r, i0 + k, (uint32_t)at.e, (uint32_t)at.t, out);
             }
             at += c[k];
         }
@@ -910,11 +924,11 @@ struct PFromSet {
             rm = s[2ull * e + 1];
         }
     }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         uint32_t e;
         u64 p, rm;
         cell(r, i, e, p, rm);
-        return p ? pk2(1, GSET ? 0u : (uint32_t)__popcll(p)) : 0;
+        return p ? pk2(1, GSET ? 0u : (uint32_t)__popcll(p)) : C2{0, 0};
     }
     __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
         uint32_t e;
@@ -936,12 +950,12 @@ struct PFromSet {
 struct PValue {
     LV src;
     __device__ u64 items(u64 r) const { return src.n(r); }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         const uint32_t* O = src.O(r);
         const u64* T = src.T(r);
         for (uint32_t t = O[i]; t < O[i + 1]; ++t)
             if (!(T[t] & kRemoved)) return pk2(1, 0);
-        return 0;
+        return C2{0, 0};
     }
     __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t, LV out) const {
         out.K(r)[pos] = src.K(r)[i];
@@ -951,7 +965,7 @@ struct PValue {
 struct PConcat {
     LV l, rr;
     __device__ u64 items(u64 r) const { return (u64)l.n(r) + rr.n(r); }
-    __device__ u64 count(u64, u64) const { return pk2(1, 0); }
+    __device__ C2 count(u64, u64) const { return pk2(1, 0); }
     __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t, LV out) const {
         const uint32_t nl = l.n(r);
         out.K(r)[pos] = i < nl ? l.K(r)[i] : rr.K(r)[i - nl];
@@ -971,9 +985,9 @@ struct PIsect {
                       key_ord(l.K(r)[i], rk));
     }
     __device__ u64 items(u64 r) const { return l.n(r); }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         const uint32_t j = find(r, i);
-        if (j == kNone) return 0;
+        if (j == kNone) return C2{0, 0};
         if (GSET) return pk2(1, 0);
         const uint32_t* OL = l.O(r);
         const uint32_t* OR = rr.O(r);
@@ -1011,11 +1025,11 @@ struct PProduct {
     LV l, rr;
     uint32_t* flag;
     __device__ u64 items(u64 r) const { return (u64)l.n(r) * rr.n(r); }
-    __device__ u64 count(u64 r, u64 o) const {
+    __device__ C2 count(u64 r, u64 o) const {
         // entries and tokens of the whole output must fit the list's 32-bit counts
         if (items(r) > 0xFFFFFFFFull || (!GSET && (u64)l.nt(r) * rr.nt(r) > 0xFFFFFFFFull)) {
             lraise(flag, kErrRange);
-            return 0;
+            return C2{0, 0};
         }
         if (GSET) return pk2(1, 0);
         const uint32_t nr = rr.n(r);
@@ -1079,7 +1093,7 @@ struct PMap {
     int per_entry;
     uint32_t* flag;
     __device__ u64 items(u64 r) const { return src.n(r); }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         return pk2(1, src.O(r)[i + 1] - src.O(r)[i]);
     }
     __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
@@ -1102,11 +1116,11 @@ struct PFilter {
     int per_entry;
     uint32_t* flag;
     __device__ u64 items(u64 r) const { return src.n(r); }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
-        if (idx == kNone) return 0;
+        if (idx == kNone) return C2{0, 0};
         if (keep[idx] == 2) lraise(flag, kErrFun);   // Function(V) raised
-        if (keep[idx] != 1) return 0;
+        if (keep[idx] != 1) return C2{0, 0};
         return pk2(1, src.O(r)[i + 1] - src.O(r)[i]);
     }
     __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
@@ -1127,15 +1141,15 @@ struct PFold {
     int per_entry;
     uint32_t* flag;
     __device__ u64 items(u64 r) const { return src.n(r); }
-    __device__ u64 count(u64 r, u64 i) const {
+    __device__ C2 count(u64 r, u64 i) const {
         const uint32_t idx = tab_index(src.K(r)[i], i, per_entry, ntab, flag);
-        if (idx == kNone) return 0;
+        if (idx == kNone) return C2{0, 0};
         const uint32_t k = off[idx + 1] - off[idx], len = src.O(r)[i + 1] - src.O(r)[i];
         for (uint32_t v = 0; v < k; ++v)
             if (keys[off[idx] + v] == kEmpty) lraise(flag, kErrFun);
         if ((u64)k * len > 0xFFFFFFFFull) {
             lraise(flag, kErrRange);
-            return 0;
+            return C2{0, 0};
         }
         return pk2(k, k * len);
     }
@@ -1329,10 +1343,10 @@ int tiled(laspj_ctx* ctx, laspj_batch* dst, uint64_t max_items, uint64_t pre_byt
     if (nt64 > 0x7FFFFFFFull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
     const uint32_t ntile = (uint32_t)nt64;
     const uint64_t pb = (pre_bytes + 63) & ~63ull;
-    char* base = static_cast<char*>(lscratch(ctx, pb + 8ull * R * ntile + 8ull * R));
+    char* base = static_cast<char*>(lscratch(ctx, pb + sizeof(C2) * R * ntile + 8ull * R));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
-    u64* tc = reinterpret_cast<u64*>(base + pb);
-    auto* need = reinterpret_cast<uint32_t*>(base + pb + 8ull * R * ntile);
+    C2* tc = reinterpret_cast<C2*>(base + pb);
+    auto* need = reinterpret_cast<uint32_t*>(base + pb + sizeof(C2) * R * ntile);
     uint32_t* flag = ctx->flag + 1;
     LJ_HIP(ctx, hipMemsetAsync(flag, 0, 4, ctx->stream));
     const P p = pre(base);
