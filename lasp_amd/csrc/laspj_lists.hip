@@ -477,56 +477,112 @@ __global__ __launch_bounds__(kMT) void k_merge_tile_scan(LV a, LV b, MS m, uint6
 }
 
 // replicas whose keys do not ascend: the clauses' walk on lane 0 (over precomputed ranks)
+// The clauses' walk for replicas whose ranks descend somewhere (no merge-path split).
+// One wave walks a replica: the next 64 ranks of each side sit one per lane in
+// registers and are read at the cursor with v_readlane (no memory round trip per step),
+// and plan entries are gathered one per lane and leave 64 at a time — the walk is the
+// same sequence of decisions, each step now ~a dozen instructions instead of two
+// dependent L2 loads.
+__device__ __forceinline__ u64 rd64(u64 v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 wr64(u64 old, u64 v, uint32_t l) {
+    return lane_id() == l ? v : old;
+}
+
+struct Win64 {
+    const u64* src;
+    uint32_t n, base;   // lanes hold src[base + lane] (base: a multiple of 64)
+    u64 v;
+    __device__ void load(uint32_t at) {
+        base = at & ~63u;
+        const uint32_t k = base + lane_id();
+        v = k < n ? src[k] : 0;
+    }
+    __device__ u64 get(uint32_t at) {
+        if (at - base >= 64u) load(at);
+        return rd64(v, at - base);
+    }
+};
+
+struct PlanOut {
+    u64* plan;
+    uint32_t o = 0;
+    u64 buf = 0;
+    __device__ void put(u64 e) {
+        buf = wr64(buf, e, o & 63u);
+        if ((++o & 63u) == 0) plan[o - 64 + lane_id()] = buf;
+    }
+    __device__ void flush() {
+        const uint32_t k = o & 63u;
+        if (lane_id() < k) plan[o - k + lane_id()] = buf;
+    }
+};
+
 template <int MODE>
 __global__ __launch_bounds__(64) void k_merge_serial(LV a, LV b, MS m, uint64_t R) {
     for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
-        if (!m.unsorted[r] || lane_id() != 0) continue;
+        if (!m.unsorted[r]) continue;
         const uint32_t na = a.n(r), nb = b.n(r);
-        const u64* sa = m.sa + r * m.ce_a;
-        const u64* sb = m.sb + r * m.ce_b;
-        u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
-        uint32_t o = 0, i = 0, j = 0;
+        Win64 A{m.sa + r * m.ce_a, na, 0, 0}, B{m.sb + r * m.ce_b, nb, 0, 0};
+        A.load(0);
+        B.load(0);
+        PlanOut P{m.plan + r * ((u64)m.ce_a + m.ce_b)};
+        uint32_t i = 0, j = 0;
         if (MODE != 2) {
             // merge(F,[{K1,_}=E1|D1],[{K2,_}=E2|D2]) when K1 < K2 -> [E1|merge(F,D1,[E2|D2])];
             //   ... when K1 > K2 -> [E2|merge(F,[E1|D1],D2)];  equal -> F on both;
             // merge(F,[],D2) -> D2;  merge(F,D1,[]) -> D1.
             while (i < na && j < nb) {
-                const u64 x = sa[i], y = sb[j];
-                if (x < y) plan[o++] = (u64)i++ | ((u64)kNone << 32);
-                else if (x > y) plan[o++] = (u64)kNone | ((u64)j++ << 32);
-                else plan[o++] = (u64)i++ | ((u64)j++ << 32);
+                const u64 x = A.get(i), y = B.get(j);
+                if (x < y) P.put((u64)i++ | ((u64)kNone << 32));
+                else if (x > y) P.put((u64)kNone | ((u64)j++ << 32));
+                else P.put((u64)i++ | ((u64)j++ << 32));
             }
-            for (; i < na; ++i) plan[o++] = (u64)i | ((u64)kNone << 32);
-            for (; j < nb; ++j) plan[o++] = (u64)kNone | ((u64)j << 32);
+            P.flush();
+            // the tails, lane-parallel
+            for (uint32_t k = lane_id(); k < na - i; k += 64)
+                P.plan[P.o + k] = (u64)(i + k) | ((u64)kNone << 32);
+            P.o += na - i;
+            for (uint32_t k = lane_id(); k < nb - j; k += 64)
+                P.plan[P.o + k] = (u64)kNone | ((u64)(j + k) << 32);
+            P.o += nb - j;
         } else {
             // union([E1|Es1],[E2|_]=S2) when E1 < E2 -> [E1|union(Es1,S2)];
             // union([E1|_]=S1,[E2|Es2]) when E1 > E2 -> [E2|union(Es2,S1)];  (switch)
             // union([E1|Es1],[_|Es2]) -> [E1|union(Es1,Es2)];  tails as they are.
-            const u64* X = sa;
-            const u64* Y = sb;
-            uint32_t nx = na, ny = nb, sx = 0, sy = 1;
-            while (i < nx && j < ny) {
-                const u64 x = X[i], y = Y[j];
+            // i / j index A / B; sx says which of them is the walk's first argument X.
+            uint32_t sx = 0;
+            while (i < na && j < nb) {
+                const u64 va = A.get(i), vb = B.get(j);
+                const u64 x = sx ? vb : va, y = sx ? va : vb;
+                const uint32_t ix = sx ? j : i, iy = sx ? i : j;
                 if (x < y) {
-                    plan[o++] = (u64)i++ | ((u64)sx << 32);
+                    P.put((u64)ix | ((u64)sx << 32));
+                    if (sx) ++j; else ++i;
                 } else if (x > y) {
-                    plan[o++] = (u64)j | ((u64)sy << 32);
-                    const u64* T = X;
-                    X = Y, Y = T;
-                    uint32_t t = nx;
-                    nx = ny, ny = t;
-                    t = sx, sx = sy, sy = t;
-                    const uint32_t ni = j + 1;
-                    j = i, i = ni;
+                    P.put((u64)iy | ((u64)(sx ^ 1u) << 32));
+                    if (sx) ++i; else ++j;             // Y's head taken, then Y becomes X
+                    sx ^= 1u;
                 } else {
-                    plan[o++] = (u64)i++ | ((u64)sx << 32);
-                    ++j;
+                    P.put((u64)ix | ((u64)sx << 32));
+                    ++i, ++j;
                 }
             }
-            for (; i < nx; ++i) plan[o++] = (u64)i | ((u64)sx << 32);
-            for (; j < ny; ++j) plan[o++] = (u64)j | ((u64)sy << 32);
+            P.flush();
+            // tails: the rest of X, then the rest of Y (one of them is empty)
+            const uint32_t nx = sx ? nb - j : na - i, x0 = sx ? j : i;
+            for (uint32_t k = lane_id(); k < nx; k += 64)
+                P.plan[P.o + k] = (u64)(x0 + k) | ((u64)sx << 32);
+            P.o += nx;
+            const uint32_t ny = sx ? na - i : nb - j, y0 = sx ? i : j;
+            for (uint32_t k = lane_id(); k < ny; k += 64)
+                P.plan[P.o + k] = (u64)(y0 + k) | ((u64)(sx ^ 1u) << 32);
+            P.o += ny;
         }
-        m.nout[r] = o;
+        if (lane_id() == 0) m.nout[r] = P.o;
     }
 }
 
