@@ -2684,12 +2684,43 @@ __device__ __forceinline__ uint32_t gs_slot(const GsTabs& g, const uint8_t* p, u
 }
 
 constexpr uint32_t kGChunk = 256;
+constexpr uint32_t kGWin = 4096;          // LDS window over the payload (LIST_EXT walk)
 
+// extent of the element term at buf[o] within the window's bytes [0, lim) when its
+// tag gives it directly (etf_term_len's rules for those tags); 0: not decidable here
+__device__ __forceinline__ u64 gs_elem_len(const uint8_t* buf, uint32_t o, uint32_t lim) {
+    const uint32_t t = buf[o];
+    switch (t) {
+    case 97: return 2;                                            // SMALL_INTEGER
+    case 98: return 5;                                            // INTEGER
+    case 70: return 9;                                            // NEW_FLOAT
+    case 100:                                                     // ATOM_EXT (latin-1)
+        return o + 3 <= lim ? 3u + ((uint32_t)buf[o + 1] << 8 | buf[o + 2]) : 0;
+    case 115:                                                     // SMALL_ATOM_EXT
+        return o + 2 <= lim ? 2u + buf[o + 1] : 0;
+    case 110:                                                     // SMALL_BIG
+        return o + 2 <= lim ? 3u + buf[o + 1] : 0;
+    case 109:                                                     // BINARY
+        return o + 5 <= lim ? 5ull + be32(buf + o + 1) : 0;
+    default: return 0;                   // UTF-8 atoms, tuples, lists, ...: the general walk
+    }
+}
+
+// One wave per replica.  LIST_EXT payloads are walked once: the payload is staged into
+// LDS 4 KiB at a time, lane 0 finds the next <= 256 element extents in the window
+// (common tags by their headers, anything else by etf_term_len), then every lane takes
+// one element: dictionary slot by hash and exact compare, term order against the
+// element before it, the bit set.  The statuses are those of the upfront whole-term
+// validation this walk replaces: the first structural failure in stream order decides
+// (truncation -> MALFORMED, a tag no dictionary term has -> UNKNOWN_TERM), then an
+// improper tail or trailing bytes (MALFORMED), then an element outside the dictionary
+// or out of order (UNKNOWN_TERM).
 __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, const u64* offs,
                                                       uint64_t R, GsTabs g, int tag, int vers,
                                                       u64* words, uint64_t W, int32_t* status) {
     __shared__ uint32_t s_o[kGChunk], s_l[kGChunk];
     __shared__ u64 s_h[4];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kGWin + 16];
     const uint32_t lane = threadIdx.x;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const uint8_t* p = payload + offs[rep];
@@ -2707,15 +2738,18 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
             if (st == LASPJ_DEC_OK && (n < h + 2 || p[h] != 131)) st = LASPJ_DEC_MALFORMED;
             u64 lt = 0, cnt = 0, first = 0;
             if (st == LASPJ_DEC_OK) {
-                const u64 L = etf_term_len(p + h + 1, n - h - 1);
-                if (L == kTermOther) st = LASPJ_DEC_UNKNOWN_TERM;
-                else if (L == 0 || L != n - h - 1) st = LASPJ_DEC_MALFORMED;
-            }
-            if (st == LASPJ_DEC_OK) {
                 lt = p[h + 1];
-                if (lt == 107) cnt = (u64)p[h + 2] << 8 | p[h + 3], first = h + 4;
-                else if (lt == 108) cnt = be32(p + h + 2), first = h + 6;
-                else if (lt != 106) st = LASPJ_DEC_MALFORMED;          // not a list
+                if (lt == 108) {
+                    // validated by the element walk below (one pass over the payload)
+                    if (n - h - 1 < 5) st = LASPJ_DEC_MALFORMED;
+                    else cnt = be32(p + h + 2), first = h + 6;
+                } else {
+                    const u64 L = etf_term_len(p + h + 1, n - h - 1);
+                    if (L == kTermOther) st = LASPJ_DEC_UNKNOWN_TERM;
+                    else if (L == 0 || L != n - h - 1) st = LASPJ_DEC_MALFORMED;
+                    else if (lt == 107) cnt = (u64)p[h + 2] << 8 | p[h + 3], first = h + 4;
+                    else if (lt != 106) st = LASPJ_DEC_MALFORMED;      // not a list
+                }
             }
             s_h[0] = (u64)st;
             s_h[1] = lt;
@@ -2750,24 +2784,66 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                 have_prev = true;
             }
         } else if (st == LASPJ_DEC_OK && lt == 108) {
-            for (u64 c0 = 0; c0 < cnt; c0 += kGChunk) {
-                const uint32_t m = (uint32_t)(cnt - c0 < kGChunk ? cnt - c0 : kGChunk);
-                if (lane == 0) {                    // element extents (the term is well-formed)
-                    for (uint32_t k = 0; k < m; ++k) {
-                        const u64 L = etf_term_len(p + pos, n - pos);
-                        s_o[k] = (uint32_t)pos;
-                        s_l[k] = (uint32_t)L;
-                        pos += L;
+            u64 left = cnt;
+            while (left > 0 && st == LASPJ_DEC_OK) {
+                // stage [pos & ~15, + 4 KiB) of the payload (absolute offsets stay 16-B
+                // aligned in the buffer: payload offsets are arbitrary, so bytes go one by
+                // one into place through 16-byte loads of the aligned span)
+                const u64 a0 = (offs[rep] + pos) & ~15ull;
+                const u64 aend = offs[rep] + n;
+                const uint32_t wl = (uint32_t)min((u64)kGWin, aend - a0);
+                for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
+                    const u64 at = a0 + 16ull * v;
+                    if (at + 16 <= aend) {
+                        *reinterpret_cast<u32x4*>(win + 16 * v) =
+                            *reinterpret_cast<const u32x4*>(payload + at);
+                    } else {
+                        for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
                     }
-                    s_h[3] = pos;
                 }
                 __syncthreads();
-                pos = s_h[3];
+                const uint32_t base = (uint32_t)(offs[rep] + pos - a0);     // pos in win
+                if (lane == 0) {
+                    // element extents inside the window; the general walk (global bytes)
+                    // for other tags and for an element the window does not hold
+                    const uint32_t mx = (uint32_t)min(left, (u64)kGChunk);
+                    uint32_t k = 0, o = base;
+                    int est = LASPJ_DEC_OK;
+                    while (k < mx) {
+                        const u64 rel = pos + (o - base);                  // payload offset
+                        if (rel >= n) { est = LASPJ_DEC_MALFORMED; break; }
+                        u64 L = o + 16 <= wl ? gs_elem_len(win, o, wl) : 0;
+                        if (L == 0 || o + L > wl) {
+                            if (o + 16 <= wl || k == 0) {
+                                L = etf_term_len(p + rel, n - rel);
+                                if (L == kTermOther) { est = LASPJ_DEC_UNKNOWN_TERM; break; }
+                                if (L == 0) { est = LASPJ_DEC_MALFORMED; break; }
+                            } else {
+                                break;                     // restage at this element
+                            }
+                        }
+                        if (rel + L > n) { est = LASPJ_DEC_MALFORMED; break; }
+                        s_o[k] = (uint32_t)rel;
+                        s_l[k] = L <= 0xFFFFFFull ? (uint32_t)L : 0xFFFFFFFFu;
+                        o += (uint32_t)min(L, (u64)0x7FFFFFFF);
+                        ++k;
+                        if (o > wl) break;                 // the next element starts past it
+                    }
+                    s_h[0] = (u64)est;
+                    s_h[2] = k;
+                    s_h[3] = pos + (o - base);
+                }
+                __syncthreads();
+                st = (int)s_h[0];
+                const uint32_t m = (uint32_t)s_h[2];
                 for (uint32_t k0 = 0; k0 < m; k0 += 64) {
                     const uint32_t k = k0 + lane;
                     uint32_t slot = kNoSlot, rk = 0;
                     if (k < m) {
-                        slot = s_l[k] <= 0xFFFFFFu ? gs_slot(g, p + s_o[k], s_l[k]) : kNoSlot;
+                        const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
+                        const bool in = s_l[k] <= 0xFFFFFFu && o + s_l[k] <= wl;
+                        slot = s_l[k] > 0xFFFFFFu ? kNoSlot
+                                                  : gs_slot(g, in ? win + o : p + s_o[k], s_l[k]);
                         rk = slot != kNoSlot ? g.rank[slot] : 0;
                     }
                     const uint32_t before = __shfl_up(rk, 1, 64);
@@ -2779,9 +2855,22 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                     prev_rank = __shfl(rk, last, 64);
                     have_prev = true;
                 }
+                left -= m;
+                pos = s_h[3];
                 __syncthreads();
             }
-            if (p[pos] != 106) st = LASPJ_DEC_MALFORMED;       // improper list tail
+            if (st == LASPJ_DEC_OK) {
+                // the tail: [] closing the list at the payload end (an improper tail, a
+                // tag no term has, or bytes after it are what the whole-term check saw)
+                if (pos >= n) {
+                    st = LASPJ_DEC_MALFORMED;
+                } else if (p[pos] != 106) {
+                    const u64 L = etf_term_len(p + pos, n - pos);
+                    st = L == kTermOther ? LASPJ_DEC_UNKNOWN_TERM : LASPJ_DEC_MALFORMED;
+                } else if (pos + 1 != n) {
+                    st = LASPJ_DEC_MALFORMED;
+                }
+            }
         }
         if (st == LASPJ_DEC_OK && unknown) st = LASPJ_DEC_UNKNOWN_TERM;
         if (lane == 0) status[rep] = st;

@@ -382,6 +382,37 @@ def etf(ctx, steps):
         ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
         del back, stb
         del out, offs, d, b
+    # G-Set to_binary / from_binary (lasp_gset.erl:111-113, 122-128): 65536 replicas x 1024
+    # integer elements (SMALL_INTEGER_EXT / INTEGER_EXT images), ~50 % present: LIST_EXT
+    R, E = 65536, 1024
+    g = ctx.gset_batch(R, E)
+    g.fill_synthetic(12)
+    dom = Domain()
+    for e in range(E):
+        dom.element_slot(e)
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+    offs = ctx.buffer(8 * (R + 1))
+    total = _lib.C.c_uint64()
+    size_ms = timed(ctx, lambda: _lib.check(L.laspj_gset_etf_size(
+        ctx.h, g.h, d.h, 82, offs.h, _lib.C.byref(total)), ctx.h), steps)
+    W = (E + 63) // 64
+    report("gset_etf_size", size_ms, 8 * W * R + 8 * R, R * E, "elements_per_s", replicas=R,
+           elements=E)
+    out = ctx.buffer(total.value)
+    ms = timed(ctx, lambda: _lib.check(L.laspj_gset_etf_write(
+        ctx.h, g.h, d.h, 82, 1, offs.h, out.h), ctx.h), steps)
+    report("gset_etf_write", ms, 8 * W * R + total.value, R * E, "elements_per_s", replicas=R,
+           elements=E, payload_bytes=total.value,
+           payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1))
+    back = ctx.gset_batch(R, E)
+    stb = ctx.buffer(4 * R)
+    ms = timed(ctx, lambda: _lib.check(L.laspj_gset_etf_read(
+        ctx.h, back.h, d.h, 82, 1, out.h, offs.h, stb.h), ctx.h), steps)
+    same = bool(np.array_equal(back.download(), g.download())) and \
+        not stb.download(np.int32, count=R).any()
+    report("gset_etf_read", ms, 8 * W * R + total.value, R * E, "elements_per_s", replicas=R,
+           elements=E, payload_bytes=total.value,
+           payload_GBps=round(total.value / (ms / 1e3) / 1e9, 1), round_trip_equal=same)
 
 
 def weak(ctx, steps):
