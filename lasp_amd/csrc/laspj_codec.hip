@@ -1080,6 +1080,75 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uin
     }
 }
 
+// One wave per G-Set payload (the payloads are short: a few bytes per element): lanes
+// take 64 element slots at a time in term order, a wave prefix sum of their image
+// lengths places them, and each lane stores its image bytes straight into the payload
+// (byte stores of consecutive lanes fill consecutive bytes of a line).  Same bytes as
+// k_gset_etf_write: 131 107 <n:16> <bytes> (STRING_EXT, every element a byte integer,
+// n < 65536), 131 108 <n:32> <images> 106, or 131 106.
+__global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words, uint64_t R,
+                                                                uint32_t E, uint32_t W,
+                                                                DictView d, int tag, int vers,
+                                                                const u64* offs, uint8_t* out) {
+    const uint32_t lane = threadIdx.x & 63u, hdr = tag >= 0 ? 2u : 0u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
+         rep += nwaves) {
+        const u64* w = words + rep * W;
+        const u64 base = offs[rep], end = offs[rep + 1];
+        uint32_t np = 0, nb = 0;
+        for (uint32_t wi = lane; wi < W; wi += 64) {
+            for (u64 m = w[wi]; m; m &= m - 1) {
+                const uint32_t e = 64u * wi + (uint32_t)__ffsll((long long)m) - 1u;
+                ++np;
+                nb += e >= E || d.elem_byte[e] == 0;
+            }
+        }
+        const uint32_t n = (uint32_t)wave_sum(np), nonbyte = (uint32_t)wave_sum(nb);
+        const bool str = n > 0 && nonbyte == 0 && n < 65536u;
+        u64 cursor = base + hdr + 1u + (str ? 3u : 5u);
+        bool fits = true;
+        for (uint32_t c0 = 0; c0 < E && n && fits; c0 += 64) {
+            const uint32_t i = c0 + lane;
+            const uint32_t e = i < E ? d.elem_order[i] : 0u;
+            const bool here = i < E && ((w[e >> 6] >> (e & 63u)) & 1ull);
+            const uint32_t el = here ? d.elem_off[e + 1] - d.elem_off[e] : 0u;
+            const uint32_t sz = here ? (str ? 1u : el) : 0u;
+            uint32_t x = sz;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, 64);
+                if ((int)lane >= off) x += y;
+            }
+            const uint32_t tot = __shfl(x, 63, 64), pos = x - sz;
+            if (cursor + tot + (str ? 0u : 1u) > end) {        // sizes disagree: never overrun
+                fits = false;
+                break;
+            }
+            if (here) {
+                uint8_t* o = out + cursor + pos;
+                const uint8_t* src = d.elem_blob + d.elem_off[e];
+                if (str) {
+                    o[0] = src[1];
+                } else if (el <= 16) {
+                    const u32x4 t = *reinterpret_cast<const u32x4*>(d.elem_pad + d.elem_poff[e]);
+                    const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                    for (uint32_t b = 0; b < 16; ++b)
+                        if (b < el) o[b] = (uint8_t)(tw[b >> 2] >> (8 * (b & 3)));
+                } else {
+                    for (uint32_t b = 0; b < el; ++b) o[b] = src[b];
+                }
+            }
+            cursor += tot;
+        }
+        if (lane == 0) {
+            write_list_header(out, base, hdr, tag, vers, n == 0 ? 106 : str ? 107 : 108, n);
+            if (fits && n && !str && cursor < end) out[cursor] = 106;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ from_binary/1
 // binary_to_term of OR-Set payloads into cells (lasp_orset.erl:202-214 decodes with
 // riak_dt:from_binary/1 = binary_to_term/1), for dictionaries with uniform token images.
@@ -3018,7 +3087,12 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
                            vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
     else
-        hipLaunchKernelGGL(k_gset_etf_write, dim3(grid), dim3(kBlock), 0, ctx->stream,
+        // LASPJ_TUNE_ETF_KERNEL 1: the block-per-payload staging writer
+        hipLaunchKernelGGL(ctx->tune_etf == 1 ? k_gset_etf_write : k_gset_etf_write_wave,
+                           dim3(ctx->tune_etf == 1 ? grid
+                                                   : (int)std::min<uint64_t>((R + 3) / 4,
+                                                                             (uint64_t)ctx->cus * 32)),
+                           dim3(kBlock), 0, ctx->stream,
                            (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
                            view(d), tag, vers, static_cast<const u64*>(offsets->dev),
                            static_cast<uint8_t*>(out->dev));
@@ -3173,7 +3247,9 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements};
-    const uint64_t cap = (uint64_t)ctx->cus * 16;
+    // one wave per replica and a latency-bound extent walk: as many waves as LDS allows
+    // (6 KiB each: ~25 per CU)
+    const uint64_t cap = (uint64_t)ctx->cus * 64;
     hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, cap))),
                        dim3(64), 0, ctx->stream, static_cast<const uint8_t*>(payload->dev),
                        static_cast<const u64*>(offsets->dev), R, tabs, tag, vers, reinterpret_cast<u64*>(b->dev),
