@@ -2754,6 +2754,7 @@ __device__ __forceinline__ uint32_t gs_slot(const GsTabs& g, const uint8_t* p, u
 
 constexpr uint32_t kGChunk = 256;
 constexpr uint32_t kGWin = 4096;          // LDS window over the payload (LIST_EXT walk)
+constexpr uint32_t kGWords = 256;         // replicas of <= 256 words collect their bits in LDS
 
 // extent of the element term at buf[o] within the window's bytes [0, lim) when its
 // tag gives it directly (etf_term_len's rules for those tags); 0: not decidable here
@@ -2790,11 +2791,18 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
     __shared__ uint32_t s_o[kGChunk], s_l[kGChunk];
     __shared__ u64 s_h[4];
     __shared__ __attribute__((aligned(16))) uint8_t win[kGWin + 16];
+    __shared__ u64 s_w[kGWords];
     const uint32_t lane = threadIdx.x;
+    // the element bits: OR-ed into LDS and stored once per replica when the replica's
+    // words fit (64 lanes setting bits of the same word would serialise on one global
+    // atomic), else straight into the batch with global atomics
+    const bool lw = W <= kGWords;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const uint8_t* p = payload + offs[rep];
         const u64 n = offs[rep + 1] - offs[rep];
         u64* w = words + rep * W;
+        if (lw)
+            for (uint32_t x = lane; x < W; x += 64) s_w[x] = 0;
         if (lane == 0) {
             // s_h: {status, list tag, element count, first element offset}
             int st = LASPJ_DEC_OK;
@@ -2846,7 +2854,10 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                 const uint32_t before = __shfl_up(rk, 1, 64);
                 bool bad = i < cnt && (slot == kNoSlot ||
                                        (lane ? rk <= before : (have_prev && rk <= prev_rank)));
-                if (i < cnt && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                if (i < cnt && !bad) {
+                    if (lw) atomicOr(s_w + (slot >> 6), 1ull << (slot & 63));
+                    else atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                }
                 unknown |= __ballot(bad) != 0;
                 const uint32_t last = (uint32_t)((cnt - c0 < 64 ? cnt - c0 : 64) - 1);
                 prev_rank = __shfl(rk, last, 64);
@@ -2872,16 +2883,40 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                 }
                 __syncthreads();
                 const uint32_t base = (uint32_t)(offs[rep] + pos - a0);     // pos in win
-                if (lane == 0) {
-                    // element extents inside the window; the general walk (global bytes)
-                    // for other tags and for an element the window does not hold
+                {
+                    // element extents inside the window, the whole wave walking together:
+                    // lanes test whether the next 64 elements all have the length L0 of the
+                    // one before (lane k: the element at o + k L0 has that length -- true
+                    // for all k below the first failure, element by element), a run of
+                    // equal-length images (small integers, then larger ones) at once;
+                    // otherwise one element from its header, or the general walk (global
+                    // bytes) for other tags and for an element the window does not hold
                     const uint32_t mx = (uint32_t)min(left, (u64)kGChunk);
-                    uint32_t k = 0, o = base;
+                    uint32_t k = 0, o = base, L0 = 0;
                     int est = LASPJ_DEC_OK;
                     while (k < mx) {
                         const u64 rel = pos + (o - base);                  // payload offset
                         if (rel >= n) { est = LASPJ_DEC_MALFORMED; break; }
+                        uint32_t run = 0;
+                        if (L0) {
+                            const uint32_t q = o + lane * L0;
+                            const bool ok = lane < mx - k && q + 16 <= wl &&
+                                            gs_elem_len(win, q, wl) == L0 &&
+                                            rel + (u64)(lane + 1) * L0 <= n;
+                            const u64 msk = __ballot(ok);
+                            run = ~msk ? (uint32_t)__ffsll((long long)~msk) - 1u : 64u;
+                        }
+                        if (run) {
+                            if (lane < run) {
+                                s_o[k + lane] = (uint32_t)(rel + (u64)lane * L0);
+                                s_l[k + lane] = L0;
+                            }
+                            o += run * L0;
+                            k += run;
+                            continue;
+                        }
                         u64 L = o + 16 <= wl ? gs_elem_len(win, o, wl) : 0;
+                        L0 = (L && o + L <= wl && L <= 64) ? (uint32_t)L : 0u;
                         if (L == 0 || o + L > wl) {
                             if (o + 16 <= wl || k == 0) {
                                 L = etf_term_len(p + rel, n - rel);
@@ -2892,15 +2927,19 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                             }
                         }
                         if (rel + L > n) { est = LASPJ_DEC_MALFORMED; break; }
-                        s_o[k] = (uint32_t)rel;
-                        s_l[k] = L <= 0xFFFFFFull ? (uint32_t)L : 0xFFFFFFFFu;
+                        if (lane == 0) {
+                            s_o[k] = (uint32_t)rel;
+                            s_l[k] = L <= 0xFFFFFFull ? (uint32_t)L : 0xFFFFFFFFu;
+                        }
                         o += (uint32_t)min(L, (u64)0x7FFFFFFF);
                         ++k;
                         if (o > wl) break;                 // the next element starts past it
                     }
-                    s_h[0] = (u64)est;
-                    s_h[2] = k;
-                    s_h[3] = pos + (o - base);
+                    if (lane == 0) {
+                        s_h[0] = (u64)est;
+                        s_h[2] = k;
+                        s_h[3] = pos + (o - base);
+                    }
                 }
                 __syncthreads();
                 st = (int)s_h[0];
@@ -2918,7 +2957,10 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                     const uint32_t before = __shfl_up(rk, 1, 64);
                     bool bad = k < m && (slot == kNoSlot ||
                                          (lane ? rk <= before : (have_prev && rk <= prev_rank)));
-                    if (k < m && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                    if (k < m && !bad) {
+                        if (lw) atomicOr(s_w + (slot >> 6), 1ull << (slot & 63));
+                        else atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                    }
                     unknown |= __ballot(bad) != 0;
                     const uint32_t last = (m - k0 < 64 ? m - k0 : 64) - 1;
                     prev_rank = __shfl(rk, last, 64);
@@ -2944,6 +2986,8 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
         if (st == LASPJ_DEC_OK && unknown) st = LASPJ_DEC_UNKNOWN_TERM;
         if (lane == 0) status[rep] = st;
         __syncthreads();
+        if (lw)
+            for (uint32_t x = lane; x < W; x += 64) w[x] = s_w[x];
     }
 }
 

@@ -1093,6 +1093,57 @@ def test_gpu_gset_from_binary_errors():
 
 
 @pytest.mark.gpu
+def test_gpu_gset_from_binary_long_payloads():
+    """Payloads longer than the decoder's 4 KiB window (the walk restages it): 10k
+    integers (2- and 5-byte images: runs of equal lengths taken 64 at a time), mixed
+    terms with atoms, binaries and tuples of many lengths, a binary longer than the
+    window, and elements straddling window edges; then the same payloads truncated at
+    and around window edges, with a trailing byte, an improper tail, an element outside
+    the dictionary, and two elements swapped deep inside — each with its status."""
+    import numpy as np
+    from lasp_amd import _lib, engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle.otp import lists_usort
+    rng = random.Random(17)
+    T = etf.DT_GSET_TAG
+    mixed = lists_usort([rng.randrange(70000) for _ in range(1500)] +
+                        [PAtom("a" * rng.randint(1, 40)) for _ in range(60)] +
+                        [bytes(rng.randrange(256) for _ in range(rng.randint(0, 100)))
+                         for _ in range(200)] +
+                        [(rng.randrange(9), b"t" * rng.randrange(30)) for _ in range(50)] +
+                        [b"L" * 6000])
+    states = [list(range(0, 70000, 7)), mixed, list(range(300)), list(range(256, 2256)),
+              lists_usort([b"x" * k for k in range(0, 300, 3)])]
+    dom = Domain(element_capacity=1 << 16)
+    dom.encode_gset(states, 1 << 16)
+    E = dom.size + 5
+    ctx = context()
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+    good = [oetf.to_binary(T, 1, s) for s in states]
+    assert all(len(g) > 4096 for g in good[:2])
+    cases = [(g, _lib.DEC_OK) for g in good]
+    L0 = good[0]
+    for cut in (4096, 4097, 4100, 8190, 8192, len(L0) - 1, len(L0) // 2 + 1):
+        cases.append((L0[:cut], _lib.DEC_MALFORMED))
+    cases.append((good[1][:4096 + 13], _lib.DEC_MALFORMED))
+    cases.append((L0 + b"\0", _lib.DEC_MALFORMED))
+    cases.append((L0[:-1] + bytes([97, 3]), _lib.DEC_MALFORMED))           # improper tail
+    # element 5000 of range(0, 70000, 7) is 35000 (INTEGER_EXT): make it 99999 (in no set)
+    i5000 = L0.index(bytes([98]) + (35000).to_bytes(4, "big"))
+    cases.append((L0[:i5000 + 1] + (99999).to_bytes(4, "big") + L0[i5000 + 5:],
+                  _lib.DEC_UNKNOWN_TERM))
+    j = L0.index(bytes([98]) + (49000).to_bytes(4, "big"))                # swap two
+    swapped = L0[:j] + L0[j + 5:j + 10] + L0[j:j + 5] + L0[j + 10:]
+    cases.append((swapped, _lib.DEC_UNKNOWN_TERM))
+    pay, offs = _upload_payloads(ctx, [c[0] for c in cases])
+    b = ctx.gset_batch(len(cases), E)
+    st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    assert list(st) == [c[1] for c in cases]
+    assert np.array_equal(b.download()[:len(states)], dom.encode_gset(states, E))
+
+
+@pytest.mark.gpu
 def test_gpu_gset_from_binary_fuzz():
     """2000 corrupted G-Set payloads against the oracle's binary_to_term: payloads it
     decodes to an ordset of dictionary terms decode OK to the host encoder's words; other
