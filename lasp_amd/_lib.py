@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblaspj.so")
+# LASPJ_LIB: another build of the library (A/B timing of kernel variants, tools/)
+LIB_PATH = os.environ.get("LASPJ_LIB") or os.path.join(HERE, "liblaspj.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "laspj.h")
 
 ABI_VERSION = 2
