@@ -5,8 +5,10 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/laspj.h"
 
@@ -41,6 +43,12 @@ struct laspj_ctx {
     // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
     void* pinned = nullptr;
     static constexpr uint64_t kPinned = 64 * 1024;
+    // released device blocks by size class (laspj::dev_alloc / dev_release): every kernel
+    // runs on `stream`, so a block released after its last enqueued use can serve the
+    // next allocation without waiting — no hipFree (a device-wide synchronisation) and
+    // no hipMalloc on the bind path's short-lived lists and buffers
+    std::map<uint64_t, std::vector<void*>> cache;
+    uint64_t cached_bytes = 0;
 };
 
 struct laspj_buf {
@@ -87,6 +95,15 @@ struct ReadPiece {
     uint64_t bytes;
 };
 hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n);
+
+// Device blocks through the context's cache (laspj_runtime.hip).  Blocks up to
+// kCacheMax are rounded to a power of two and reused in stream order; larger ones go to
+// hipMalloc / hipFree directly.  Call with the context's mutex held.
+constexpr uint64_t kCacheMax = 256ull << 20;      // largest cached block
+constexpr uint64_t kCacheCap = 2ull << 30;        // bytes a context keeps cached
+hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out);
+void dev_release(laspj_ctx* ctx, void* p, uint64_t bytes);
+void dev_cache_clear(laspj_ctx* ctx);
 inline hipError_t readback(laspj_ctx* ctx, void* host, const void* dev, uint64_t bytes) {
     const ReadPiece p{host, dev, bytes};
     return readback(ctx, &p, 1);

@@ -1267,7 +1267,7 @@ int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
         return fail(ctx, LASPJ_E_SHAPE, "list: size overflow");
     const uint64_t bytes = b->replicas * wpr * 8ull;
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes);
+    hipError_t e = laspj::dev_alloc(ctx, bytes, &p);
     if (e != hipSuccess) {
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "list: hipMalloc(%llu): %s", (unsigned long long)bytes,
@@ -1275,13 +1275,10 @@ int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
     }
     e = hipMemsetAsync(p, 0, bytes, ctx->stream);
     if (e != hipSuccess) {
-        hipFree(p);
+        laspj::dev_release(ctx, p, bytes);
         return fail(ctx, LASPJ_E_DEVICE, "list: memset: %s", hipGetErrorString(e));
     }
-    if (b->dev) {
-        hipStreamSynchronize(ctx->stream);
-        hipFree(b->dev);
-    }
+    if (b->dev) laspj::dev_release(ctx, b->dev, laspj::bytes_of(b));
     b->dev = static_cast<uint64_t*>(p);
     b->cap_e = ce;
     b->cap_t = ct;

@@ -105,16 +105,18 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
         delete b;
         return fail(ctx, LASPJ_E_SHAPE, "batch_create: size overflow");
     }
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&b->dev), bytes);
+    void* mem = nullptr;
+    hipError_t e = laspj::dev_alloc(ctx, bytes, &mem);
     if (e != hipSuccess) {
         delete b;
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "batch_create: hipMalloc(%llu) failed: %s",
                     (unsigned long long)bytes, hipGetErrorString(e));
     }
+    b->dev = static_cast<uint64_t*>(mem);
     e = hipMemsetAsync(b->dev, 0, bytes, ctx->stream);  // new/0 for every replica
     if (e != hipSuccess) {
-        hipFree(b->dev);
+        laspj::dev_release(ctx, b->dev, bytes);
         delete b;
         return fail(ctx, LASPJ_E_DEVICE, "batch_create: memset: %s", hipGetErrorString(e));
     }
@@ -125,6 +127,56 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
 }  // namespace
 
 namespace laspj {
+
+static uint64_t cache_class(uint64_t bytes) {
+    uint64_t c = 256;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out) {
+    if (bytes <= kCacheMax) {
+        const uint64_t c = cache_class(bytes);
+        auto it = ctx->cache.find(c);
+        if (it != ctx->cache.end() && !it->second.empty()) {
+            *out = it->second.back();
+            it->second.pop_back();
+            ctx->cached_bytes -= c;
+            return hipSuccess;
+        }
+        bytes = c;
+    }
+    hipError_t e = hipMalloc(out, bytes);
+    if (e != hipSuccess && !ctx->cache.empty()) {      // give the cached blocks back, retry
+        dev_cache_clear(ctx);
+        hipGetLastError();
+        e = hipMalloc(out, bytes);
+    }
+    return e;
+}
+
+void dev_release(laspj_ctx* ctx, void* p, uint64_t bytes) {
+    if (!p) return;
+    if (bytes <= kCacheMax) {
+        const uint64_t c = cache_class(bytes);
+        if (ctx->cached_bytes + c <= kCacheCap) {
+            ctx->cache[c].push_back(p);
+            ctx->cached_bytes += c;
+            return;
+        }
+    }
+    hipStreamSynchronize(ctx->stream);
+    hipFree(p);
+}
+
+void dev_cache_clear(laspj_ctx* ctx) {
+    if (ctx->cache.empty()) return;
+    hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->cache)
+        for (void* p : kv.second) hipFree(p);
+    ctx->cache.clear();
+    ctx->cached_bytes = 0;
+}
 
 hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n) {
     uint64_t total = 0;
@@ -224,6 +276,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->flag) hipFree(ctx->flag);
         if (ctx->partials) hipFree(ctx->partials);
         if (ctx->lscratch) hipFree(ctx->lscratch);
+        laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
         hipStreamDestroy(ctx->stream);
     }
@@ -304,7 +357,7 @@ int laspj_buf_create(laspj_ctx* ctx, uint64_t bytes, laspj_buf** out) {
     b->ctx = ctx;
     b->bytes = bytes;
     if (bytes) {
-        hipError_t e = hipMalloc(&b->dev, bytes);
+        hipError_t e = laspj::dev_alloc(ctx, bytes, &b->dev);
         if (e != hipSuccess) {
             delete b;
             hipGetLastError();
@@ -313,7 +366,7 @@ int laspj_buf_create(laspj_ctx* ctx, uint64_t bytes, laspj_buf** out) {
         }
         e = hipMemsetAsync(b->dev, 0, bytes, ctx->stream);
         if (e != hipSuccess) {
-            hipFree(b->dev);
+            laspj::dev_release(ctx, b->dev, bytes);
             delete b;
             return fail(ctx, LASPJ_E_DEVICE, "buf_create: memset: %s", hipGetErrorString(e));
         }
@@ -326,8 +379,7 @@ int laspj_buf_destroy(laspj_buf* b) {
     if (!b) return LASPJ_E_INVAL;
     {
         Guard g(b->ctx);
-        hipStreamSynchronize(b->ctx->stream);
-        if (b->dev) hipFree(b->dev);
+        laspj::dev_release(b->ctx, b->dev, b->bytes);
     }
     delete b;
     return LASPJ_OK;
@@ -383,8 +435,7 @@ int laspj_batch_destroy(laspj_batch* b) {
     if (!b) return LASPJ_E_INVAL;
     {
         Guard g(b->ctx);
-        hipStreamSynchronize(b->ctx->stream);
-        if (b->owns) hipFree(b->dev);
+        if (b->owns) laspj::dev_release(b->ctx, b->dev, laspj::bytes_of(b));
     }
     delete b;
     return LASPJ_OK;
