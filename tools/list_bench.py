@@ -166,7 +166,8 @@ def main():
     st.bind(r, [(e, [(tk(2, e), False)]) for e in range(D - N, D)])
     st.intersection(l, r, x)
     assert len(st.value(x)) == N - (D - N)
-    k = 5
+    st.update(r, ("add_by_token", tk(3, 999), D - N + 1), Atom("a"))     # first-use pools
+    k = 10
     prof = None
     if os.environ.get("PROFILE_STORE"):
         import cProfile
