@@ -1,4 +1,4 @@
-"""CPU coverage of the multi-GPU paths (gloo, world sizes 2 and 4).
+"""CPU coverage of the multi-GPU paths (gloo, world sizes 2, 4 and 8).
 
 The anti-entropy round bench.py runs at N > 1 is `laspj_antientropy` (laspj_comm.hip),
 which executes the steps of `laspj_antientropy_plan` on RCCL.  Here every rank asks the
@@ -134,7 +134,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_antientropy_plan_over_gloo(tmp_path, world):
     from lasp_amd import build
     from oracle import columnar
