@@ -152,7 +152,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         4 = always split (256-byte segments),
                                         5 = always split (sized segments), 6 = element
                                         batches walked by the scalar unit (the lanes
-                                        find element starts by default)                 */
+                                        find element starts by default), 7 = no element
+                                        batches for many-token dictionaries (one element
+                                        at a time)                                       */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

@@ -1603,6 +1603,7 @@ struct HdrHash {
     const uint32_t* tab;   // open addressing: rank + 1, 0 empty
     uint32_t mask;
     u64 lens;              // bit hl - 1: some header template is hl bytes (hl <= 64)
+    uint32_t many = 0;     // many-token dictionaries: element batches (read_batch_many)
 };
 
 // the header-template hash (host and device agree): ceil(hl / 4) words, bytes >= hl zero
@@ -1956,6 +1957,63 @@ __device__ __forceinline__ bool locate_records(PWin& w, uint32_t& pc, uint32_t m
     return true;
 }
 
+// The rank of the element whose header 104 2 <elem image> 108 starts at window offset s
+// (hl: the header's bytes), or -1: the image's length from its tag where the tag gives it
+// (integers, binaries, atoms, small bignums) -> one probe of the header hash at that
+// length; other terms try every header length the dictionary has.  Exact compare against
+// the rank's 64-byte header template.  Per lane (s differs between lanes).
+__device__ __forceinline__ int64_t hdr_rank(const PWin& w, uint32_t s, uint32_t lim,
+                                            const HdrHash& hh, const ReadTabs& t, uint32_t E,
+                                            uint32_t& hl) {
+    int64_t rk = -1;
+    u64 lens = hh.lens;
+    {
+        const uint32_t b2 = w.buf[min(s + 2u, kBWin + 63u)];
+        const uint32_t h0 = word_at(w.buf, min(s + 3u, kBWin + 56u));
+        uint32_t il = 0;
+        if (b2 == 97) il = 2;                                        // SMALL_INTEGER_EXT
+        else if (b2 == 98) il = 5;                                   // INTEGER_EXT
+        else if (b2 == 109) il = 5u + __builtin_bswap32(h0);         // BINARY_EXT
+        else if (b2 == 100 || b2 == 118)                             // ATOM(_UTF8)_EXT
+            il = 3u + (((h0 & 0xFFu) << 8) | ((h0 >> 8) & 0xFFu));
+        else if (b2 == 115 || b2 == 119 || b2 == 110) il = 2u + (h0 & 0xFFu) + (b2 == 110);
+        if (il) lens = il <= 61u ? lens & (1ull << (il + 2u)) : 0ull;   // hl = il + 3
+    }
+    while (lens && rk < 0) {
+        const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
+        lens &= lens - 1ull;
+        if (s + L2 > lim) break;
+        uint32_t q[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        uint32_t h = L2 * 0x85EBCA6Bu;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int rem = (int)L2 - 4 * i;          // per lane: L2 follows the lane's tag
+            if (rem <= 0) break;                      // the hash covers ceil(L2 / 4) words
+            const uint32_t v = word_at(w.buf, min(s + 4u * i, kBWin + 56u));
+            q[i] = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);
+            h = hdr_mix(h, q[i]);
+        }
+        for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
+            const uint32_t v = hh.tab[i];
+            if (!v || v > E) break;
+            const uint32_t r = v - 1u;
+            // (no length check: images are self-delimiting, so an L2-byte template
+            // ending in 108 matches only its own element's header)
+            const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * r);
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((uint32_t)(16 * j) >= L2) break;   // the rest is zero on both sides
+                const u32x4 a = tp[j];
+                eq &= a.x == q[4 * j] && a.y == q[4 * j + 1] && a.z == q[4 * j + 2] &&
+                      a.w == q[4 * j + 3];
+            }
+            if (eq) { rk = r; hl = L2; break; }
+        }
+    }
+    return rk;
+}
+
 // Element batches without the scalar walk (few token slots per element, the ad
 // counter's 3-replica tokens): every element after the first at the cursor starts right
 // after the previous element's closing 106, so `106 104 2` marks element starts; lane i
@@ -1981,59 +2039,9 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     const uint32_t s = x0 + (lane && mine ? L.rst[lane - 1] : 0u);
     bool ok = mine && s < srel;
     // the element's rank: its header 104 2 <elem image> 108 by hash
-    int64_t rk = -1;
     uint32_t hl = 0;
-    if (ok) {
-        u64 lens = hh.lens;
-        // the element image's length from its tag where the tag gives it (integers,
-        // binaries, atoms, small bignums): one probe at that header length; other terms
-        // try every length the dictionary has
-        {
-            const uint32_t b2 = w.buf[min(s + 2u, kBWin + 63u)];
-            const uint32_t h0 = word_at(w.buf, min(s + 3u, kBWin + 56u));
-            uint32_t il = 0;
-            if (b2 == 97) il = 2;                                        // SMALL_INTEGER_EXT
-            else if (b2 == 98) il = 5;                                   // INTEGER_EXT
-            else if (b2 == 109) il = 5u + __builtin_bswap32(h0);         // BINARY_EXT
-            else if (b2 == 100 || b2 == 118)                             // ATOM(_UTF8)_EXT
-                il = 3u + (((h0 & 0xFFu) << 8) | ((h0 >> 8) & 0xFFu));
-            else if (b2 == 115 || b2 == 119 || b2 == 110) il = 2u + (h0 & 0xFFu) + (b2 == 110);
-            if (il) lens = il <= 61u ? lens & (1ull << (il + 2u)) : 0ull;   // hl = il + 3
-        }
-        while (lens && rk < 0) {
-            const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
-            lens &= lens - 1ull;
-            if (s + L2 > lim) break;
-            uint32_t q[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-            uint32_t h = L2 * 0x85EBCA6Bu;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int rem = (int)L2 - 4 * i;          // per lane: L2 follows the lane's tag
-                if (rem <= 0) break;                      // the hash covers ceil(L2 / 4) words
-                const uint32_t v = word_at(w.buf, min(s + 4u * i, kBWin + 56u));
-                q[i] = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);
-                h = hdr_mix(h, q[i]);
-            }
-            for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
-                const uint32_t v = hh.tab[i];
-                if (!v || v > E) break;
-                const uint32_t r = v - 1u;
-                // (no length check: images are self-delimiting, so an L2-byte template
-                // ending in 108 matches only its own element's header)
-                const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * r);
-                bool eq = true;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if ((uint32_t)(16 * j) >= L2) break;   // the rest is zero on both sides
-                    const u32x4 a = tp[j];
-                    eq &= a.x == q[4 * j] && a.y == q[4 * j + 1] && a.z == q[4 * j + 2] &&
-                          a.w == q[4 * j + 3];
-                }
-                if (eq) { rk = r; hl = L2; break; }
-            }
-        }
-        ok = rk >= 0;
-    }
+    const int64_t rk = ok ? hdr_rank(w, s, lim, hh, t, E, hl) : -1;
+    ok = rk >= 0;
     // ranks ascend: after the previous lane's element (lane 0: after prev)
     const int64_t prk = (int64_t)(int32_t)__shfl((int32_t)rk, (lane + 63u) & 63u, 64);
     if (ok) ok = rk > (lane ? prk : prev);
@@ -2090,6 +2098,230 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     return commit;
 }
 
+// Element batches for many-token dictionaries (tok_max > 8, e.g. 64 token slots per
+// element): one element at a time pays the whole per-element sequence (header match,
+// bucket table, mark scan, one validation pass, presence ballot) for ~30 records, and at
+// t64 that sequence, not the records, is most of the time (tools/decoder_probe.py).  So
+// a batch takes up to kNT whole elements and up to kItems items at once.  Every element
+// and every record starts with 104 2 (a 2-tuple header), so one byte-parallel scan of
+// the window lists the items in stream order; an item whose previous byte is 106 (the
+// closing nil of the element before) starts an element, every other one a record (item
+// 0 is the element at the cursor).  Lanes resolve the elements' ranks by the header hash
+// (ascending after prev), read their counts and set up one bucket table each; then each
+// lane validates one record per half of the batch exactly as the per-element path does:
+// bucket -> token rank, exact template compare, flag atom, ranks ascending within the
+// element, the record ending where the next item starts (the next record, or the closing
+// 106 before the next element / at the element's end), the element's m-th record being
+// its last.  A token image may hold 104 2 or 106 104 2: a false item shifts the lanes
+// after it, and the elements it touches fail.  Elements before the first one that fails
+// anything (or is not wholly inside the batch) are committed with the cells the
+// per-element path writes; that path takes the failing one and gives its status.
+constexpr uint32_t kNT = 4;             // elements per batch (one bucket table each)
+constexpr uint32_t kItems = 128;        // element starts and records per batch
+
+struct ReadLdsX {
+    uint8_t tab[kNT - 1][kBuckets];     // bucket tables of elements 1 .. kNT-1 (0: ReadLds)
+    uint8_t pres[kNT - 1][64];
+    uint16_t pos[kItems];               // item starts, relative to the batch's first
+};
+
+// Positions q in [x0, x0 + span) of the bytes 104 2, in stream order, into X.pos
+// (relative to x0, the first kItems of them); returns how many the scanned span holds.
+// Lane l scans K bytes from a0 + l K (K / 4 odd: the lanes' dwords fall in distinct LDS
+// banks); span is clamped to 3840 bytes so that a lane's 64-bit mask holds its K <= 60
+// positions.
+__device__ __forceinline__ uint32_t scan_items(const PWin& w, uint32_t x0, uint32_t span,
+                                               ReadLdsX& X, uint32_t lane) {
+    const uint32_t a0 = x0 & ~3u;
+    span = min(span, 3840u - (x0 - a0));
+    uint32_t K = (((span + (x0 - a0) + 63u) >> 6) + 3u) & ~3u;
+    if (!(K & 4u)) K += 4u;
+    const uint32_t b0 = a0 + lane * K;
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(w.buf);
+    const uint32_t top = (kBWin + 60u) >> 2;                            // last dword index
+    u64 mask = 0;
+    uint32_t d0 = w32[min(b0 >> 2, top)];
+    for (uint32_t g = 0; g < (K >> 2); ++g) {
+        const uint32_t d1 = w32[min((b0 >> 2) + g + 1u, top)];
+        const uint32_t B = __builtin_amdgcn_alignbyte(d1, d0, 1);        // b[q + 1 + k]
+        const uint32_t T = (d0 ^ 0x68686868u) | (B ^ 0x02020202u);
+        const uint32_t z = ~(((T & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | T) & 0x80808080u;
+        mask |= (u64)((((z >> 7) * 0x204081u) >> 21) & 0xFu) << (4u * g);
+        d0 = d1;
+    }
+    const int32_t lo = (int32_t)x0 - (int32_t)b0, hi = lo + (int32_t)span;
+    if (hi <= 0) mask = 0;
+    else if (hi < 64) mask &= (1ull << hi) - 1ull;
+    if (lo >= 64) mask = 0;
+    else if (lo > 0) mask &= ~((1ull << lo) - 1ull);
+    // exclusive prefix of the per-lane counts, bit plane by bit plane (104 2 cannot
+    // overlap itself: at most 30 in a lane's 60 bytes)
+    const uint32_t cnt = (uint32_t)__popcll(mask);
+    uint32_t k = 0, total = 0;
+#pragma unroll
+    for (uint32_t bit = 0; bit < 5; ++bit) {
+        const u64 m = __ballot((cnt >> bit) & 1u);
+        k += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
+        total += (uint32_t)__popcll(m) << bit;
+    }
+    while (mask && k < kItems) {
+        const uint32_t i = (uint32_t)__ffsll((long long)mask) - 1u;
+        mask &= mask - 1ull;
+        X.pos[k++] = (uint16_t)(b0 + i - x0);
+    }
+    wave_sync();
+    return total;
+}
+
+__device__ uint32_t read_batch_many(PWin& w, uint32_t& pc, int64_t& prev, uint32_t left,
+                                    uint32_t hint, const ReadTabs& t, const DictView& d,
+                                    const HdrHash& hh, uint32_t E, ReadLds& L, ReadLdsX& X,
+                                    u64x2* c, uint32_t lane) {
+    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
+    if (w.hi < w.end && pc + hint > w.hi) pc = refill(w, pc);
+    const uint32_t lim = min(w.hi, w.end);
+    const uint32_t x0 = pc;
+    if (x0 + 8u > lim) return 0;
+    const uint32_t NI = min(scan_items(w, x0, min(lim - x0, hint), X, lane), kItems);
+    if (NI < 2u || ufl32(X.pos[0]) != 0u) return 0;
+    // items of the two halves: lane l holds items l and 64 + l
+    uint32_t q[2];
+    bool el[2];
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t i = 64u * h + lane;
+        q[h] = i < NI ? x0 + X.pos[i] : 0u;
+        el[h] = i < NI && (i == 0u || w.buf[q[h] - 1u] == 106);
+    }
+    const u64 em0 = __ballot(el[0]), em1 = __ballot(el[1]);
+    const uint32_t ne0 = (uint32_t)__popcll(em0);
+    const uint32_t nel = min(min(ne0 + (uint32_t)__popcll(em1), kNT), left);
+    // lane o < nel: element o of the batch (its item index it, rank, header, count)
+    uint32_t it = 0, e = 0, cnt = 0, key = 0, m = 0;
+    int32_t rk = -1;
+    bool eok = lane < nel;
+    if (eok) {
+        it = lane < ne0 ? select64(em0, lane) : 64u + select64(em1, lane - ne0);
+        const uint32_t s = x0 + X.pos[it];
+        uint32_t hl = 0;
+        rk = (int32_t)hdr_rank(w, s, lim, hh, t, E, hl);
+        eok = rk >= 0;
+        if (eok) {
+            const uint4 ds = t.desc[rk];
+            e = ds.x;
+            cnt = ds.w;
+            key = ds.z;
+            const uint32_t y = s + hl;
+            eok = y + 4u <= lim;
+            m = eok ? __builtin_bswap32(word_at(w.buf, y)) : 0u;
+            // its m records are items it + 1 .. it + m, all inside the batch, the first
+            // right after the count
+            eok = eok && m >= 1u && m <= cnt && it + m < NI && x0 + X.pos[it + 1u] == y + 4u;
+        }
+    }
+    // ranks ascend: after the previous element (element 0: after prev)
+    const int32_t prk = __shfl(rk, (lane + 63u) & 63u, 64);
+    if (eok) eok = (int64_t)rk > (lane ? (int64_t)prk : prev);
+    // the elements' bucket tables and empty presence tables; their rank -> slot maps
+    uint32_t ros[kNT];
+    wave_sync();
+#pragma unroll
+    for (uint32_t o = 0; o < kNT; ++o) {
+        ros[o] = 0xFFu;
+        if (o >= nel) continue;
+        const int32_t r = (int32_t)rdlane((uint32_t)rk, o);
+        if (r < 0) continue;
+        const uint32_t co = rdlane(cnt, o);
+        uint8_t* tab = o ? X.tab[o - 1] : L.tab;
+        uint8_t* pr = o ? X.pres[o - 1] : L.pres;
+        if (lane < co) tab[t.tb[(u64)r * RK + lane]] = (uint8_t)lane;
+        pr[lane] = 0;
+        ros[o] = t.ros[64ull * r + lane];
+    }
+    wave_sync();
+    // lane l: record 64 h + l of the batch
+    uint32_t fend[2] = {0u, 0u};
+    u64 bad[2];
+    int32_t obad[2] = {0x7FFFFFFF, 0x7FFFFFFF};
+    uint32_t last = 0xFFu;                       // rank of item 63 (the next half's lane 0)
+    bad[1] = 0;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        if (64u * h >= NI) break;
+        const uint32_t i = 64u * h + lane;
+        // the element the item belongs to: element items up to it, minus one
+        const u64 below = lane == 63u ? ~0ull : (2ull << lane) - 1ull;
+        const uint32_t oi = (h ? ne0 + (uint32_t)__popcll(em1 & below)
+                               : (uint32_t)__popcll(em0 & below)) - 1u;
+        const bool rec = i < NI && !el[h] && oi < nel;
+        const uint32_t src = rec ? oi : 0u;
+        const uint32_t it_o = (uint32_t)__shfl((int32_t)it, (int32_t)src, 64);
+        const uint32_t e_o = (uint32_t)__shfl((int32_t)e, (int32_t)src, 64);
+        const uint32_t key_o = (uint32_t)__shfl((int32_t)key, (int32_t)src, 64);
+        const uint32_t cnt_o = (uint32_t)__shfl((int32_t)cnt, (int32_t)src, 64);
+        const uint32_t m_o = (uint32_t)__shfl((int32_t)m, (int32_t)src, 64);
+        const uint32_t j = i - it_o;             // 1-based record index in the element
+        bool ok = rec && j <= m_o;
+        uint32_t rank = 0xFFu, fl = 0;
+        if (ok) {
+            const uint32_t x = q[h];
+            const uint8_t* tab = src ? X.tab[src - 1u] : L.tab;
+            const uint32_t kw = 4u * (key_o & 0xFFu), ksh = key_o >> 8;
+            rank = tab[(word_at(w.buf, x + kw) >> ksh) & (kBuckets - 1u)];
+            ok = rank < cnt_o;
+            if (ok) ok = rec_match(w.buf, x, RL, d.rec_pad + ((u64)e_o * RK + rank) * RS);
+            const uint32_t fo = x + RL;
+            uint32_t fn;
+            const uint32_t fk = flag_atom(word_at(w.buf, fo), word_at(w.buf, fo + 4u), fn);
+            fend[h] = fo + fn;
+            ok &= fk != 0u && fend[h] < lim;
+            fl = fk == 1u;
+        }
+        // term order: after the previous record of the same element
+        const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
+        const uint32_t prv = lane ? pr : last;
+        if (ok && j > 1u) ok = rank > prv;
+        last = rdlane(rank, 63u);
+        // the record ends where the next item starts: the next record (j < m), or the
+        // closing 106 of the element's token list (j = m) before the next element
+        if (ok) {
+            if (i + 1u < NI) {
+                const uint32_t qn = x0 + X.pos[i + 1u];
+                const bool nel_n = i + 1u < 64u ? ((em0 >> (i + 1u)) & 1ull) != 0
+                                                : ((em1 >> (i - 63u)) & 1ull) != 0;
+                ok = j < m_o ? !nel_n && fend[h] == qn : nel_n && fend[h] + 1u == qn;
+            } else {
+                ok = j == m_o && w.buf[min(fend[h], kBWin + 63u)] == 106;
+            }
+        }
+        bad[h] = __ballot(rec && !ok);
+        if (bad[h]) obad[h] = (int32_t)rdlane(oi, (uint32_t)__ffsll((long long)bad[h]) - 1u);
+        if (ok) {
+            uint8_t* prs = src ? X.pres[src - 1u] : L.pres;
+            prs[rank] = (uint8_t)(1u | (fl << 1));
+        }
+    }
+    // commit the elements before the first failure
+    const u64 ebad = __ballot(lane < nel && !eok);
+    uint32_t commit = ebad ? (uint32_t)__ffsll((long long)ebad) - 1u : nel;
+    commit = (uint32_t)min((int32_t)commit, min(obad[0], obad[1]));
+    if (commit == 0) return 0;
+    wave_sync();
+#pragma unroll
+    for (uint32_t o = 0; o < kNT; ++o) {
+        if (o >= commit) break;
+        const uint8_t* prs = o ? X.pres[o - 1] : L.pres;
+        const uint32_t v = ros[o] < 64u ? prs[ros[o]] : 0u;
+        const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
+        if (lane == 0) c[rdlane(e, o)] = u64x2{pb, rb};
+    }
+    prev = (int64_t)(int32_t)rdlane((uint32_t)rk, commit - 1u);
+    const uint32_t li = rdlane(it, commit - 1u) + rdlane(m, commit - 1u);   // its last record
+    pc = (li < 64u ? rdlane(fend[0], li) : rdlane(fend[1], li - 64u)) + 1u;
+    return commit;
+}
+
 // Decode elements at the cursor into cells c: at most n of them (count mode), or with
 // n = ~0u every element that starts before the absolute payload position `stop`, up to
 // the list's closing 106 (segment mode: *tail is set when the cursor stops on it).
@@ -2100,14 +2332,19 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                                                  RankPre& nx, uint32_t n, u64 stop, bool& tail,
                                                  int32_t& st, const ReadTabs& tabs,
                                                  const DictView& d, const HdrHash& hh,
-                                                 uint32_t E, ReadLds& L, u64x2* c,
-                                                 uint32_t lane, Cases cs) {
+                                                 uint32_t E, ReadLds& L, ReadLdsX* X,
+                                                 u64x2* c, uint32_t lane, Cases cs) {
     const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
     const uint32_t hmax = min(d.ehdr_max + 4u, kBWin - 16u);
     const bool seg = n == 0xFFFFFFFFu;
     const uint32_t lj = cs.lj, lf = cs.lf;
     const bool lcase = cs.on;
-    uint32_t k = 0;
+    const bool many = !SMALL && X && hh.tab && hh.many && !seg;
+    // Element batches pay off only when they fill up (kNT small elements): after one
+    // that does not, or after an element of more than 12 records, the next 16 elements
+    // go one at a time; an element of <= 12 records re-arms the batches.  hint: bytes
+    // the next batch scans (kNT elements at the last batch's bytes per element).
+    uint32_t k = 0, cool = 0, hint = 1024;
     while (k < n && st == LASPJ_DEC_OK) {
         if (seg) {
             if (w.lo + pc >= stop) break;
@@ -2123,6 +2360,23 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                 k += got;
                 if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
                 continue;
+            }
+        }
+        if (many) {
+            if (cool == 0) {
+                const u64 at = w.lo + pc;
+                const uint32_t got = read_batch_many(w, pc, prev, n - k, hint, tabs, d, hh, E,
+                                                     L, *X, c, lane);
+                if (got < kNT) cool = 16;
+                if (!got) hint = min(2u * hint, 3840u);
+                if (got) {
+                    hint = (uint32_t)min((w.lo + pc - at) / got * kNT + 256u, (u64)3840u);
+                    k += got;
+                    if (k < n) nx = load_rank(tabs, RK, prev + 1, E, lane);
+                    continue;
+                }
+            } else {
+                --cool;
             }
         }
         // 104 2 <elem image> 108 <count:32> of the next element in term order
@@ -2181,6 +2435,10 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
         }
         pc += 4;
         if (m_tok == 0 || m_tok > 64) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+        if (many) {
+            if (m_tok <= 12u) cool = 0;
+            else if (cool < 16u) cool = 16;
+        }
         // the element's bucket table and an empty presence table
         const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = cur.key >> 8;
         wave_sync();
@@ -2313,8 +2571,9 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
 
 // One wave per replica.  With `redo` (segment mode's fallback) the wave takes the
 // replicas listed there (redo[0] of them) and clears their cells first.
+// (many-token dictionaries: the element batches' LDS leaves 4 waves per SIMD)
 template <bool SMALL>
-__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* payload, u64 total,
+__global__ __launch_bounds__(kBlock, SMALL ? 6 : 4) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
                                                            ReadTabs tabs, HdrHash hh, int tag,
@@ -2322,10 +2581,12 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* pay
                                                            int32_t* status,
                                                            const uint32_t* redo) {
     __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) ReadLdsX ldx[SMALL ? 1 : kBlock / 64];
     // the wave index as a scalar: everything per replica then stays wave-uniform
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t RK = d.tok_max;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    ReadLdsX* X = SMALL ? nullptr : &ldx[wave];
     const Cases cs = lane_cases(lane);
     ReadLds& L = lds[wave];
     const uint64_t count = redo ? (uint64_t)ufl32(redo[0]) : R;
@@ -2343,8 +2604,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read(const uint8_t* pay
             int64_t prev = -1;                    // term rank of the previous element
             RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
             bool tail = false;
-            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, hh, E, L, c, lane,
-                                cs);
+            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, hh, E, L, X, c,
+                                lane, cs);
         }
         if (st == LASPJ_DEC_OK && list) {
             if (pc + 1 > w.end) st = LASPJ_DEC_MALFORMED;
@@ -2499,7 +2760,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
             bool tail = false;
             int32_t st = LASPJ_DEC_OK;
             out.cnt = decode_elems<SMALL>(w, pc, prev, nx, 0xFFFFFFFFu, stop, tail, st, tabs, d,
-                                          hh, E, L, c, lane, cs);
+                                          hh, E, L, nullptr, c, lane, cs);
             out.st = st;
             out.end = (uint32_t)(w.lo + pc - base);
             out.rlast = (int32_t)prev;
@@ -3177,8 +3438,9 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     // the header hash (segment search; element batches without the scalar walk — knob 6
     // keeps the walking element batches)
     const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
+    // (knob 7: many-token dictionaries decode one element at a time)
     const HdrHash hh_small{ctx->tune_etf_read == 6 ? nullptr : d->rd_htab, d->rd_hmask,
-                           d->rd_hlens};
+                           d->rd_hlens, ctx->tune_etf_read == 7 ? 0u : 1u};
     // Segment mode when there are too few payloads to fill the chip with one wave each
     // (fewer than 8 per CU) and they are long: segments of S bytes, S sized for ~48 waves
     // per CU (6 resident per SIMD, the rest queued behind them for balance), at least
@@ -3193,7 +3455,8 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
         S = std::max<uint64_t>(2048, ((bytes_in / want) + 255) & ~255ull);
         if (ctx->tune_etf_read == 4) S = 256;
         if (ctx->tune_etf_seg) S = (uint64_t)ctx->tune_etf_seg;
-        const bool split = ctx->tune_etf_read >= 4 || ctx->tune_etf_seg ||
+        const bool split = (ctx->tune_etf_read >= 4 && ctx->tune_etf_read <= 6) ||
+                           ctx->tune_etf_seg ||
                            R < (uint64_t)ctx->cus * 8;
         if (longest < (1ull << 31) && split && longest > S) {
             for (uint64_t i = 0; i < R; ++i)

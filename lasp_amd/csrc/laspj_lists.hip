@@ -129,13 +129,6 @@ __device__ __forceinline__ uint32_t hmix(u64 k) {
     return (uint32_t)k;
 }
 
-__device__ __forceinline__ void h_clear(u64* hk, uint32_t* hi, uint32_t hsize) {
-    for (uint32_t h = lane_id(); h < hsize; h += 64) {
-        hk[h] = kEmpty;
-        hi[h] = kNone;
-    }
-}
-
 __device__ __forceinline__ void h_insert(u64* hk, uint32_t* hi, uint32_t mask, u64 key,
                                          uint32_t idx) {
     uint32_t h = hmix(key) & mask;
@@ -188,23 +181,6 @@ __device__ uint32_t inner_merge(const u64* ta, uint32_t la, const u64* tb, uint3
     for (; y < lb; ++y, ++n)
         if (W) to[n] = tb[y];
     return n;
-}
-
-__device__ __forceinline__ void finish(LV out, u64 r, uint32_t n, uint32_t nt, bool write,
-                                       uint32_t* need, uint32_t* flag) {
-    if (lane_id() != 0) return;
-    if (!write) {
-        need[2 * r] = n;
-        need[2 * r + 1] = nt;
-        return;
-    }
-    if (n > out.ce || nt > out.ct) {
-        lraise(flag, kErrRange);
-        return;
-    }
-    out.hdr[2 * r] = n;
-    out.hdr[2 * r + 1] = nt;
-    out.O(r)[n] = nt;
 }
 
 // ================================================================ kernels

@@ -944,6 +944,92 @@ def test_gpu_from_binary_record_locator_fuzz():
 
 
 @pytest.mark.gpu
+def test_gpu_from_binary_many_token_batches_fuzz():
+    """Many-token dictionaries (up to 64 token slots per element), elements of 1 to 64
+    records, so a batch holds one to several whole elements or stops inside one; tokens
+    that embed the batch's item marker 104 2 and whole false element starts (106 104 2
+    <a real element header>), flags in all three atom forms, and 2500 corrupted copies:
+    element batches (knob 0), one element at a time (7) and the serial scan (1) agree on
+    every status and cell, and the clean payloads decode to the encoder's cells."""
+    import numpy as np
+    from lasp_amd import etf
+    rng = random.Random(4242)
+    T = etf.DT_ORSET_TAG
+    elems = list(range(0, 120, 2)) + [300, 1 << 33]
+
+    def hdr(x):
+        return bytes(oetf.term_to_binary([(x, [(b"", False)])])[6:])[:2 + (2 if x < 256 else 5)]
+
+    def tok(i, k):
+        b = bytearray(rng.randrange(256) for _ in range(20))
+        kind = k % 5
+        if kind == 0:
+            at = (i + k) % 19
+            b[at:at + 2] = bytes([104, 2])
+        elif kind == 1:
+            h = bytes([106]) + hdr(elems[(i + k) % len(elems)]) + bytes([108])
+            at = (i * 7 + k) % (21 - len(h))
+            b[at:at + len(h)] = h
+        return bytes(b)
+    pools = {e: sorted({tok(i, k) for k in range(64)}) for i, e in enumerate(elems)}
+    states = []
+    for n in range(60):
+        es = sorted(rng.sample(elems, rng.randint(1, 14)))
+        sizes = [1, 2, 5, 20, 33, 63, 64]
+        states.append([(e, sorted((t, rng.random() < 0.5) for t in
+                                  rng.sample(pools[e], rng.choice(sizes)))) for e in es])
+    ctx, dom, E, d = _decode_setup(states)
+    base = []
+    for i, s in enumerate(states):
+        p = oetf.to_binary(T, 1, s)
+        if i % 3 == 1:
+            p = p.replace(bytes([100, 0, 4]) + b"true", bytes([119, 4]) + b"true") \
+                 .replace(bytes([100, 0, 5]) + b"false", bytes([119, 5]) + b"false")
+        elif i % 3 == 2:
+            p = p.replace(bytes([100, 0, 5]) + b"false", bytes([118, 0, 5]) + b"false")
+        base.append(p)
+    blobs = list(base)
+    for _ in range(2500):
+        b = bytearray(rng.choice(base))
+        kind = rng.randrange(5)
+        if kind == 0:
+            for _ in range(rng.randint(1, 2)):
+                b[rng.randrange(len(b))] = rng.choice([101, 104, 2, 106, 108, 0, 5, 4,
+                                                       rng.randrange(256)])
+        elif kind == 1:
+            del b[rng.randrange(len(b)):]
+        elif kind == 2:
+            pos = rng.randrange(len(b) + 1)
+            b[pos:pos] = rng.choice([bytes([104, 2]), bytes([106, 104, 2]), bytes([106]),
+                                     b"\0"])
+        elif kind == 3:
+            pos = rng.randrange(len(b))
+            del b[pos:pos + rng.randint(1, 3)]
+        else:                                  # an element's count nudged by one
+            at = [i for i in range(len(b) - 4) if b[i] == 108 and b[i + 1:i + 3] == b"\0\0"]
+            if at:
+                i = rng.choice(at) + 4
+                b[i] = (b[i] + rng.choice([1, 255])) & 0xFF
+        blobs.append(bytes(b))
+    pay, offs = _upload_payloads(ctx, blobs)
+    res = {}
+    for knob in (0, 7, 1):
+        bt = ctx.orset_batch(len(blobs), E)
+        with _read_kernel(ctx, knob):
+            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+        res[knob] = (st, bt.download())
+    st0, c0 = res[0]
+    assert set(np.unique(st0)) <= {0, 1, 2, 3, 4, 5}
+    assert (st0[:len(base)] == 0).all(), np.nonzero(st0[:len(base)])[0][:10]
+    assert np.array_equal(c0[:len(base)], dom.encode_orset(states, E))
+    for knob in (7, 1):
+        st, c = res[knob]
+        assert np.array_equal(st0, st), (knob, np.nonzero(st0 != st)[0][:10])
+        ok = st0 == 0
+        assert np.array_equal(c0[ok], c[ok]), knob
+
+
+@pytest.mark.gpu
 def test_gpu_from_binary_small_tokens_fuzz():
     """Elements with <= 3 token slots (the lane-parallel element batches): tokens that
     embed the element-start marker `106 104 2` followed by a real element header, and
