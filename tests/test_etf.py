@@ -463,7 +463,8 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 @contextlib.contextmanager
 def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
-    <= 8 token slots), 1 = serial scan, 2 = batched records only, 4 = every payload
+    <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
+    scan, 2 = batched records only, 7 = no many-token element batches, 4 = every payload
     longer than 256 bytes split between waves (segment mode: header search, chain
     check, redo of failed replicas); "seg512": the default kernels with every payload
     longer than 512 bytes split (LASPJ_TUNE_ETF_SEG)."""
