@@ -46,6 +46,19 @@ def test_binding_covers_header():
     assert sorted(_lib.SIGNATURES) == declared()
 
 
+def test_integration_table_matches_header():
+    """INTEGRATION.md §4 lists every entry point with the reference function it serves,
+    as tools/abi_table.py generates it from the header (no entry point undocumented)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import abi_table
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    i = doc.index(abi_table.BEGIN) + len(abi_table.BEGIN)
+    assert doc[i:doc.index(abi_table.END)].strip() == abi_table.table().strip()
+    listed = set(re.findall(r"^\| `(laspj_\w+)`", doc, flags=re.M))
+    assert listed == set(declared())
+
+
 def test_abi_calls_without_gpu(lib):
     assert lib.laspj_abi_version() == 2
     assert lib.laspj_strerror(_lib.E_SHAPE) == b"shape mismatch"
