@@ -657,6 +657,15 @@ int laspj_list_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
  * G-Sets: sets:is_subset, usort =/=); prev has R replicas or 1 (broadcast) */
 int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                          int strict, const laspj_list_order* ord, laspj_buf* out);
+/* lasp_core:bind/3 on list values (lasp_core.erl:291-312) in one call, per replica:
+ * status[i] = 0 when cur[i] =:= val[i] (the no-op of :294-296); else dst[i] :=
+ * Type:merge(cur[i], val[i]) (as laspj_list_merge) and status[i] = 1 when
+ * is_inflation(cur[i], dst[i]) (:301, the bind writes dst[i]) or 2 when not (no write).
+ * status is host memory, R bytes.  Two synchronisations (sizes with the equalities,
+ * then the inflations with the error flag) instead of the separate calls' six; when
+ * every replica is equal, dst is left as it was. */
+int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
+                    const laspj_batch* val, const laspj_list_order* ord, uint8_t* status);
 /* value/1 of OR-Set lists (lasp_orset.erl:67-73): the keys of entries with a {_, false}
  * token, in list order, as a G-Set list dst */
 int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);

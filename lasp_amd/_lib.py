@@ -188,6 +188,7 @@ SIGNATURES = {
     "laspj_list_merge": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
     "laspj_list_equal": (i, [vp, vp, vp, C.POINTER(ListOrder), vp]),
     "laspj_list_inflation": (i, [vp, vp, vp, i, C.POINTER(ListOrder), vp]),
+    "laspj_list_bind": (i, [vp, vp, vp, vp, C.POINTER(ListOrder), vp]),
     "laspj_list_value": (i, [vp, vp, vp]),
     "laspj_list_union": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
     "laspj_list_intersection": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),

@@ -304,10 +304,10 @@ class Store:
             raise Unsupported("a product output and plain keys in one variable")
         old, new = self._var_list(v), self._value_list(t, dv)
         order = self._order(t)
-        if bool(old.equal(new, order)[0]):                       # Value0 =:= Value
-            return
-        merged = old.merge(new, order)                           # Type:merge(Value0, Value)
-        if not bool(merged.is_inflation_of(old, order)[0]):      # is_inflation(Value0, Merged)
+        # Value0 =:= Value -> no-op; Merged = Type:merge(Value0, Value); write when
+        # is_inflation(Value0, Merged) — one call (laspj_list_bind)
+        merged, st = old.bind(new, order)
+        if st[0] != 1:
             return
         v.rep, v.val = "list", merged
         self._written(id_, v)

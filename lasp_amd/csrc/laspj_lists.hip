@@ -1336,18 +1336,34 @@ int read_flag(laspj_ctx* ctx, const char* what) {
     return flag_status(ctx, f, what);
 }
 
+// What laspj_list_bind adds to a merge: the equality bytes of the inputs (computed
+// before the size pass, read back with the sizes into `eq_host`), the write pass
+// skipped when every replica is equal, and no flag read after the write pass (the
+// caller reads it with the inflation bytes).
+struct BindX {
+    uint8_t* eq_dev;      // R bytes: cur =:= val
+    uint8_t* eq_host;     // R bytes
+    bool skipped;         // out: every replica equal, dst untouched
+};
+
 // run a size pass, size dst from the per-replica maxima, then the write pass
 template <class SizeFn, class WriteFn>
 int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, WriteFn write_pass,
-          const char* what) {
+          const char* what, BindX* bx = nullptr) {
     const uint64_t R = dst->replicas;
     size_pass();
     LJ_LAUNCHED(ctx);
     std::vector<uint32_t> h(2 * R);
     uint32_t f = 0;
-    const laspj::ReadPiece rp[2] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
-    LJ_HIP(ctx, laspj::readback(ctx, rp, 2));
+    const laspj::ReadPiece rp[3] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4},
+                                    {bx ? bx->eq_host : nullptr, bx ? bx->eq_dev : nullptr, R}};
+    LJ_HIP(ctx, laspj::readback(ctx, rp, bx ? 3 : 2));
     if (int s = flag_status(ctx, f, what)) return s;
+    if (bx) {
+        bx->skipped = true;
+        for (uint64_t i = 0; i < R && bx->skipped; ++i) bx->skipped = bx->eq_host[i] != 0;
+        if (bx->skipped) return LASPJ_OK;
+    }
     uint32_t ce = 0, ct = 0;
     for (uint64_t i = 0; i < R; ++i) {
         ce = h[2 * i] > ce ? h[2 * i] : ce;
@@ -1359,7 +1375,7 @@ int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, Wr
             return s;
     write_pass(view(dst));
     LJ_LAUNCHED(ctx);
-    return read_flag(ctx, what);
+    return bx ? LASPJ_OK : read_flag(ctx, what);
 }
 
 // a tiled producer (k_tp_*): `pre` carves its own scratch from the front of the block
@@ -1543,14 +1559,11 @@ static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch
     return LASPJ_OK;
 }
 
-static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
-                      const laspj_batch* b, const laspj_list_order* ord, bool keep_left,
-                      const char* what) {
-    if (int s = pair_checks(ctx, dst, a, b, what)) return s;
+// the merge proper, with the context's lock held and the arguments checked
+static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                     const laspj_batch* b, const RK& rk, bool keep_left, const char* what,
+                     BindX* bx) {
     const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
-    RK rk;
-    if (int s = ranks(ctx, ord, !gs, &rk, what)) return s;
-    LGuard g(ctx);
     const uint64_t R = a->replicas;
     const uint64_t ce = (uint64_t)a->cap_e + b->cap_e;
     if (ce > 0xFFFFFFF0ull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
@@ -1589,6 +1602,8 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint32_t cmax = m.ce_a > m.ce_b ? m.ce_a : m.ce_b;
     const unsigned gr = cmax ? (cmax + kMT - 1) / kMT : 1u;
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    if (bx)
+        hipLaunchKernelGGL(k_list_equal, dim3(R), dim3(64), 0, ctx->stream, A, B, rk, bx->eq_dev);
     auto size_pass = [&](auto mode) {
         constexpr int MODE = decltype(mode)::value;
         hipMemsetAsync(m.unsorted, 0, sz_r, ctx->stream);
@@ -1615,12 +1630,63 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     using M2 = std::integral_constant<int, 2>;
     if (gs)
         return sized(ctx, dst, need, [&] { size_pass(M2{}); },
-                     [&](LV out) { write_pass(M2{}, out); }, what);
+                     [&](LV out) { write_pass(M2{}, out); }, what, bx);
     if (keep_left)
         return sized(ctx, dst, need, [&] { size_pass(M1{}); },
-                     [&](LV out) { write_pass(M1{}, out); }, what);
+                     [&](LV out) { write_pass(M1{}, out); }, what, bx);
     return sized(ctx, dst, need, [&] { size_pass(M0{}); },
-                 [&](LV out) { write_pass(M0{}, out); }, what);
+                 [&](LV out) { write_pass(M0{}, out); }, what, bx);
+}
+
+static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                      const laspj_batch* b, const laspj_list_order* ord, bool keep_left,
+                      const char* what) {
+    if (int s = pair_checks(ctx, dst, a, b, what)) return s;
+    RK rk;
+    if (int s = ranks(ctx, ord, a->kind != LASPJ_KIND_GSET_LIST, &rk, what)) return s;
+    LGuard g(ctx);
+    return merge_run(ctx, dst, a, b, rk, keep_left, what, nullptr);
+}
+
+// the inflation kernels of prev -> cur into o (R bytes); clear_flag: start from a clean
+// error flag (the fused bind keeps the merge's bits and reads them with o)
+static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                            int strict, const RK& rk, uint8_t* o, bool clear_flag,
+                            const char* what) {
+    const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
+    const bool bcast = prev->replicas == 1 && cur->replicas != 1;
+    const uint64_t R = cur->replicas;
+    const uint32_t cmax = cur->cap_e > prev->cap_e ? cur->cap_e : prev->cap_e;
+    const uint32_t hsize = pow2_at_least(2ull * cmax);
+    const uint64_t tbytes = R * 2ull * hsize * 12ull;
+    char* base = static_cast<char*>(lscratch(ctx, tbytes + 4ull * R));
+    if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
+    u64* hk = reinterpret_cast<u64*>(base);
+    auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
+    auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
+    if (clear_flag) LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    LJ_HIP(ctx, hipMemsetAsync(base, 0xFF, tbytes, ctx->stream));    // kEmpty / kNone
+    LJ_HIP(ctx, hipMemsetAsync(flags, 0, 4ull * R, ctx->stream));
+    const LV P = view(prev), C = view(cur);
+    const dim3 grid(cmax ? (cmax + 255) / 256 : 1, (unsigned)(R < 65535 ? R : 65535));
+    const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
+#define LJ_INFL(G, S)                                                                         \
+    do {                                                                                      \
+        hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,   \
+                           hk, hi, hsize, bcast, R);                                          \
+        hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
+                           hk, hi, hsize, bcast, R, flags);                                   \
+        hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P, C,    \
+                           bcast, R, flags, o);                                               \
+    } while (0)
+    if (gs) {
+        if (strict) LJ_INFL(true, true); else LJ_INFL(true, false);
+    } else {
+        if (strict) LJ_INFL(false, true); else LJ_INFL(false, false);
+    }
+#undef LJ_INFL
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
 }
 
 int laspj_list_merge(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
@@ -1668,43 +1734,53 @@ int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
         return fail(ctx, LASPJ_E_SHAPE, "list_inflation: replicas");
     if (!out || out->ctx != ctx || out->bytes < cur->replicas)
         return fail(ctx, LASPJ_E_RANGE, "list_inflation: output buffer");
-    const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
     RK rk;
-    if (int s = ranks(ctx, ord, !gs, &rk, "list_inflation")) return s;
+    if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_inflation"))
+        return s;
     LGuard g(ctx);
-    const uint64_t R = cur->replicas;
-    const uint32_t cmax = cur->cap_e > prev->cap_e ? cur->cap_e : prev->cap_e;
-    const uint32_t hsize = pow2_at_least(2ull * cmax);
-    const uint64_t tbytes = R * 2ull * hsize * 12ull;
-    char* base = static_cast<char*>(lscratch(ctx, tbytes + 4ull * R));
-    if (!base) return fail(ctx, LASPJ_E_NOMEM, "list_inflation: scratch");
-    u64* hk = reinterpret_cast<u64*>(base);
-    auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
-    auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
-    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
-    LJ_HIP(ctx, hipMemsetAsync(base, 0xFF, tbytes, ctx->stream));    // kEmpty / kNone
-    LJ_HIP(ctx, hipMemsetAsync(flags, 0, 4ull * R, ctx->stream));
-    auto* o = static_cast<uint8_t*>(out->dev);
-    const LV P = view(prev), C = view(cur);
-    const dim3 grid(cmax ? (cmax + 255) / 256 : 1, (unsigned)(R < 65535 ? R : 65535));
-    const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
-#define LJ_INFL(G, S)                                                                         \
-    do {                                                                                      \
-        hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,   \
-                           hk, hi, hsize, bcast, R);                                          \
-        hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
-                           hk, hi, hsize, bcast, R, flags);                                   \
-        hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P, C,    \
-                           bcast, R, flags, o);                                               \
-    } while (0)
-    if (gs) {
-        if (strict) LJ_INFL(true, true); else LJ_INFL(true, false);
-    } else {
-        if (strict) LJ_INFL(false, true); else LJ_INFL(false, false);
-    }
-#undef LJ_INFL
-    LJ_LAUNCHED(ctx);
+    if (int s = inflation_launch(ctx, prev, cur, strict, rk, static_cast<uint8_t*>(out->dev),
+                                 true, "list_inflation"))
+        return s;
     return read_flag(ctx, "list_inflation");
+}
+
+int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
+                    const laspj_batch* val, const laspj_list_order* ord, uint8_t* status) {
+    if (int s = check_list(ctx, dst, "list_bind")) return s;
+    if (int s = check_list(ctx, cur, "list_bind")) return s;
+    if (int s = check_list(ctx, val, "list_bind")) return s;
+    if (!status) return fail(ctx, LASPJ_E_INVAL, "list_bind: null status");
+    if (int s = pair_checks(ctx, dst, cur, val, "list_bind")) return s;
+    RK rk;
+    if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
+    const uint64_t R = cur->replicas;
+    LGuard g(ctx);
+    void* dev = nullptr;
+    if (laspj::dev_alloc(ctx, 2 * R, &dev) != hipSuccess) {
+        hipGetLastError();
+        return fail(ctx, LASPJ_E_NOMEM, "list_bind: status bytes");
+    }
+    uint8_t* eq = static_cast<uint8_t*>(dev);
+    std::vector<uint8_t> inf(R, 0);
+    BindX bx{eq, status, false};
+    int s = merge_run(ctx, dst, cur, val, rk, false, "list_bind", &bx);
+    if (s == LASPJ_OK && !bx.skipped) {
+        s = inflation_launch(ctx, cur, dst, 0, rk, eq + R, false, "list_bind");
+        if (s == LASPJ_OK) {
+            uint32_t f = 0;
+            const laspj::ReadPiece rp[2] = {{inf.data(), eq + R, R}, {&f, ctx->flag + 1, 4}};
+            const hipError_t e = laspj::readback(ctx, rp, 2);
+            if (e != hipSuccess)
+                s = fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s", hipGetErrorString(e));
+            else
+                s = flag_status(ctx, f, "list_bind");
+        }
+    }
+    laspj::dev_release(ctx, dev, 2 * R);
+    if (s != LASPJ_OK) return s;
+    // status: 0 = cur =:= val (no-op), 1 = the merge inflates cur (written), 2 = it does not
+    for (uint64_t i = 0; i < R; ++i) status[i] = status[i] ? 0 : (inf[i] ? 1 : 2);
+    return LASPJ_OK;
 }
 
 int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {

@@ -785,6 +785,17 @@ class ListBatch:
                                               C.byref(order), buf.h), self.ctx.h)
         return buf.download(np.uint8).astype(bool)
 
+    # lasp_core:bind/3 (lasp_core.erl:291-312) on list values, one call
+    def bind(self, val: "ListBatch", order):
+        """(merged, status) for Value0 = self, Value = val: status[i] = 0 when
+        self[i] =:= val[i] (no-op), 1 when merged[i] = Type:merge(self[i], val[i])
+        inflates self[i] (the bind writes it), 2 when it does not (no write)."""
+        out = self._like()
+        st = np.zeros((self.replicas,), dtype=np.uint8)
+        check(self.ctx.L.laspj_list_bind(self.ctx.h, out.h, self.h, val.h, C.byref(order),
+                                         st.ctypes.data), self.ctx.h)
+        return out, st
+
     def value(self) -> "ListBatch":
         out = self._like(_lib.KIND_GSET_LIST)
         check(self.ctx.L.laspj_list_value(self.ctx.h, out.h, self.h), self.ctx.h)

@@ -81,6 +81,44 @@ def test_gset_list_merge_equal_inflation(a, b):
         assert bool(P.equal(C, s.order)[0]) == exact_eq(p, c)
 
 
+def _bind_want(kind, mod, p, v):
+    """lasp_core:bind/3 (lasp_core.erl:291-312): 0 no-op, 1 written, 2 not an inflation."""
+    if exact_eq(p, v):
+        return 0, None
+    m = mod.merge(p, v)
+    return (1 if olat.is_inflation(kind, p, m) else 2), m
+
+
+@SETTINGS
+@given(OLIST, OLIST, st.booleans())
+def test_list_bind_matches_lasp_core(a, b, gs):
+    """laspj_list_bind (equal -> merge -> is_inflation in one call) over a 3-replica
+    batch (Value0, Value) = (a, b), (a, a), (b, a): statuses and merged lists as the
+    oracle's bind/3 gives them; G-Set lists from the keys."""
+    from lasp_amd import _lib
+    if gs:
+        a, b = [k for k, _ in a], [k for k, _ in b]
+    s = Space(gset=gs)
+    kind, mod = ("lasp_gset", ogset) if gs else ("lasp_orset", oorset)
+    lk = _lib.KIND_GSET_LIST if gs else _lib.KIND_ORSET_LIST
+    pairs = [(a, b), (a, a), (b, a)]
+    ce = 1 + max(len(x) for x in (a, b))
+    ct = 1 + (0 if gs else max(sum(len(ts) for _, ts in x) for x in (a, b)))
+    P, V = (s.engine.ListBatch(s.ctx, lk, replicas=3, cap_entries=ce, cap_tokens=ct)
+            for _ in range(2))
+    for i, (p, v) in enumerate(pairs):
+        P.upload(*s.L.encode(s.dom, p, gs, False), replica=i)
+        V.upload(*s.L.encode(s.dom, v, gs, False), replica=i)
+    merged, status = P.bind(V, s.order)
+    want = [_bind_want(kind, mod, p, v) for p, v in pairs]
+    assert list(status) == [w for w, _ in want], (pairs, list(status))
+    if any(status):
+        for i, (w, m) in enumerate(want):
+            if w:
+                keys, toff, toks = merged.download(replica=i)
+                assert exact_eq(s.L.decode(s.dom, keys, toff, toks, gs), m), (pairs[i], m)
+
+
 @SETTINGS
 @given(OLIST, OLIST)
 def test_orset_list_bodies(a, b):

@@ -102,6 +102,11 @@ def bench_pair(ctx, order, old, new, it=20, R=1):
         "us_merge": timed(lambda: a.merge(b, order), it),
         "us_equal": timed(lambda: a.equal(b, order), it),
         "us_inflation_strict": timed(lambda: m.is_inflation_of(a, order, strict=True), it),
+        # lasp_core:bind/3 on the pair: =:=, merge, is_inflation as three calls, and
+        # fused (laspj_list_bind: two synchronisations instead of six)
+        "us_bind_separate": timed(lambda: (a.equal(b, order), a.merge(b, order)
+                                           .is_inflation_of(a, order)), it),
+        "us_bind_fused": timed(lambda: a.bind(b, order), it),
     }
     out["operand_bytes"] = 8 * (2 * (out["entries_old"] + out["entries_new"]) +
                                 out["tokens_old"] + int(sum(len(o[2]) for o in new)))
