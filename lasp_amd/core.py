@@ -273,6 +273,15 @@ class Store:
             return
         if v.rep == "canonical" and dv.rep == "canonical":
             new = dv.batch
+            if t != "lasp_orset_gbtree":
+                # `Value0 =:= Value` + merge in one launch (laspj_batch_bind_many); a
+                # canonical merge always inflates Value0, so it is written (:301-303)
+                merged = _new_like(self.ctx, v.val)
+                if not self.ctx.bind_many([merged], [v.val], [new])[0]:
+                    return                                       # lasp_core.erl:294-296
+                v.val = merged
+                self._written(id_, v)
+                return
             same = bool(v.val.equal(new)[0])
             if t == "lasp_orset_gbtree" and dv.gb is not None:
                 # `case Value0 of Value` matches whole terms: the stored value's outer
