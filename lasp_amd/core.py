@@ -90,6 +90,10 @@ class Store:
         self._n = 0
         self._depth = 0
         self._bottoms: Dict = {}
+        # canonical batch -> its list form, for the bodies' operands: a stored batch is
+        # never written again (updates and binds make new ones), so the conversion of a
+        # value the bodies see again (the unchanged input of a re-run) is reused
+        self._lcache: Dict = {}
 
     # ---------------------------------------------------------------- helpers
     def _new_batch(self, type_):
@@ -159,7 +163,16 @@ class Store:
         return c[1]
 
     def _value_list(self, type_, dv: _Value):
-        return dv.batch if dv.rep == "list" else self._to_list(type_, dv.batch)
+        if dv.rep == "list":
+            return dv.batch
+        c = self._lcache.get(id(dv.batch))
+        if c is not None and c[0] is dv.batch:
+            return c[1]
+        lst = self._to_list(type_, dv.batch)
+        if len(self._lcache) >= 16:                     # oldest out (dicts keep order)
+            self._lcache.pop(next(iter(self._lcache)))
+        self._lcache[id(dv.batch)] = (dv.batch, lst)    # the entry keeps the batch alive
+        return lst
 
     def _order(self, type_):
         return self._space(type_).order()
