@@ -2341,10 +2341,11 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
     const bool lcase = cs.on;
     const bool many = !SMALL && X && hh.tab && hh.many && !seg;
     // Element batches pay off only when they fill up (kNT small elements): after one
-    // that does not, or after an element of more than 12 records, the next 16 elements
-    // go one at a time; an element of <= 12 records re-arms the batches.  hint: bytes
-    // the next batch scans (kNT elements at the last batch's bytes per element).
-    uint32_t k = 0, cool = 0, hint = 1024;
+    // that does not, the next 16 elements go one at a time (hold); after an element of
+    // more than 12 records, too (cool), until an element of <= 12 records re-arms them.
+    // hint: bytes the next batch scans (kNT elements at the last batch's bytes per
+    // element).
+    uint32_t k = 0, cool = 0, hold = 0, hint = 1024;
     while (k < n && st == LASPJ_DEC_OK) {
         if (seg) {
             if (w.lo + pc >= stop) break;
@@ -2363,11 +2364,11 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
             }
         }
         if (many) {
-            if (cool == 0) {
+            if (cool == 0 && hold == 0) {
                 const u64 at = w.lo + pc;
                 const uint32_t got = read_batch_many(w, pc, prev, n - k, hint, tabs, d, hh, E,
                                                      L, *X, c, lane);
-                if (got < kNT) cool = 16;
+                if (got < kNT) hold = 16;
                 if (!got) hint = min(2u * hint, 3840u);
                 if (got) {
                     hint = (uint32_t)min((w.lo + pc - at) / got * kNT + 256u, (u64)3840u);
@@ -2376,7 +2377,8 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                     continue;
                 }
             } else {
-                --cool;
+                if (cool) --cool;
+                if (hold) --hold;
             }
         }
         // 104 2 <elem image> 108 <count:32> of the next element in term order
