@@ -663,7 +663,8 @@ int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
  * is_inflation(cur[i], dst[i]) (:301, the bind writes dst[i]) or 2 when not (no write).
  * status is host memory, R bytes.  Two synchronisations (sizes with the equalities,
  * then the inflations with the error flag) instead of the separate calls' six; when
- * every replica is equal, dst is left as it was. */
+ * every replica is equal, dst is left as it was.  On an error status, status[] and
+ * dst hold no result. */
 int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
                     const laspj_batch* val, const laspj_list_order* ord, uint8_t* status);
 /* value/1 of OR-Set lists (lasp_orset.erl:67-73): the keys of entries with a {_, false}
