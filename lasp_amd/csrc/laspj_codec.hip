@@ -2573,9 +2573,11 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
 
 // One wave per replica.  With `redo` (segment mode's fallback) the wave takes the
 // replicas listed there (redo[0] of them) and clears their cells first.
-// (many-token dictionaries: the element batches' LDS leaves 4 waves per SIMD)
+// (element batches: 5 waves per SIMD give 96 VGPRs, 6 spilled instead of 20 at 6 waves,
+// t3 1.05-1.09 -> 1.03-1.04 ms, profiles/r03k_decoder_occ5_ab.log; many-token
+// dictionaries: the element batches' LDS leaves 4)
 template <bool SMALL>
-__global__ __launch_bounds__(kBlock, SMALL ? 6 : 4) void k_orset_etf_read(const uint8_t* payload, u64 total,
+__global__ __launch_bounds__(kBlock, SMALL ? 5 : 4) void k_orset_etf_read(const uint8_t* payload, u64 total,
                                                            const u64* offs, uint64_t R,
                                                            uint32_t E, DictView d,
                                                            ReadTabs tabs, HdrHash hh, int tag,
