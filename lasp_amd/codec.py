@@ -81,6 +81,17 @@ class _Dict:
         self._order = np.insert(self._order, [p for p, _k, _i in new], [i for _p, _k, i in new])
         return self._order
 
+    def truncate(self, n: int) -> None:
+        """Forget the slots from n on (an encode that failed part way: its registrations
+        are undone, so a rejected value leaves no slots behind)."""
+        if n >= len(self.terms):
+            return
+        for t in self.terms[n:]:
+            self.index.pop(hkey(t), None)
+        del self.terms[n:]
+        if self._order is not None and len(self._order) > n:
+            self._order, self._skeys = None, []
+
 
 class Domain:
     """Element + token dictionaries shared by all batches of one engine domain."""
@@ -113,6 +124,11 @@ class Domain:
     @property
     def size(self) -> int:
         return len(self.elements)
+
+    def journal(self) -> "_Journal":
+        """`with dom.journal(): ...` — registrations made inside the block are undone
+        when it raises (the device store commits slots only for values it encodes)."""
+        return _Journal(self)
 
     # ------------------------------------------------------------------ OR-Set
     def register_orset(self, s) -> None:
@@ -230,6 +246,29 @@ class Domain:
             if pred(elem) is True:
                 out[es >> 6] |= np.uint64(1) << np.uint64(es & 63)
         return out
+
+
+class _Journal:
+    def __init__(self, dom: Domain):
+        self.dom = dom
+
+    def __enter__(self):
+        d = self.dom
+        self.ne = len(d.elements.terms)
+        self.nt = [len(td.terms) for td in d.tokens]
+        self.nlog = len(d.tok_log)
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if et is None:
+            return False
+        d = self.dom
+        for es, n in enumerate(self.nt):
+            d.tokens[es].truncate(n)
+        del d.tokens[len(self.nt):]
+        d.elements.truncate(self.ne)
+        del d.tok_log[self.nlog:]
+        return False
 
 
 def _check_canonical_orset(s) -> None:

@@ -113,7 +113,23 @@ class Store:
 
     def _encode(self, type_, term, pairs: bool = False) -> _Value:
         """A host term as a device value: canonical when it is an orddict / ordset (and
-        the variable holds no product pairs), else a list."""
+        the variable holds no product pairs), else a list.
+
+        A value the device form cannot hold — an element with more than 64 distinct
+        tokens, or more distinct elements than the store's `capacity` — raises
+        `Unsupported`, and the dictionary slots the attempt registered are undone.  The
+        reference's merge takes such values (add_elem mints a fresh token per add,
+        lasp_orset.erl:222-230, 261-262), so lasp_core:bind/3 would write them
+        (lasp_core.erl:300-304): the store must not answer `ok` with the variable
+        unchanged, which is what swallowing the error as a failed merge would do."""
+        dom = self.cdom if type_ == "riak_dt_gcounter" else self._dom(type_)
+        try:
+            with dom.journal():
+                return self._encode_term(type_, term, pairs)
+        except CapacityError as e:
+            raise Unsupported(f"value not representable on the device store: {e}") from e
+
+    def _encode_term(self, type_, term, pairs: bool) -> _Value:
         if type_ == "riak_dt_gcounter":
             b = self._new_batch(type_)
             host = np.zeros((1, self.cap), dtype=np.uint64)
@@ -207,8 +223,10 @@ class Store:
         try:
             dv = value if isinstance(value, _Value) else self._encode(v.type, value, v.pairs)
             self._bind_device(id_, v, dv)
-        except (NonCanonical, CapacityError, ValueError, TypeError):
-            pass        # merge may throw for invalid values; bind swallows it (:308-311)
+        except (NonCanonical, ValueError, TypeError):
+            # merge may throw for invalid values; bind swallows it (:308-311).  Values the
+            # device cannot hold raise Unsupported from _encode instead (not swallowed).
+            pass
         except _lib.LaspjError as e:
             if e.status in (_lib.E_UNSUPPORTED, _lib.E_NOMEM, _lib.E_DEVICE):
                 raise Unsupported(str(e)) if e.status == _lib.E_UNSUPPORTED else e
@@ -243,7 +261,7 @@ class Store:
                             v.rep == "canonical" and not v.empty:
                         try:
                             dv = self._encode(v.type, term, v.pairs)
-                        except (NonCanonical, CapacityError, ValueError, TypeError):
+                        except (NonCanonical, ValueError, TypeError):
                             continue              # merge would throw: bind swallows it
                         if dv.rep == "canonical":
                             pend.append((id_, v, dv))
@@ -346,19 +364,31 @@ class Store:
         if v.rep != "canonical":
             raise Unsupported("update/3 on a combinator output (a list value)")
         from . import orset as _o
+        ops, script = [], []
+        dom = self.cdom if v.type == "riak_dt_gcounter" else self._dom(v.type)
+        try:
+            # the op's slots (the 65th token of an element — add_elem mints one per add,
+            # lasp_orset.erl:222-230 — or an element past `capacity` is Unsupported, and
+            # the slots the op registered are undone)
+            with dom.journal():
+                if v.type == "riak_dt_gcounter":
+                    from .gcounter import increment_amount
+                    ops.append((0, self.cdom.element_slot(actor), increment_amount(op)))
+                elif v.type == "lasp_orset":
+                    _o._compile(op, self.odom, ops, new_call=True)
+                elif v.type == "lasp_orset_gbtree":
+                    from . import orset_gbtree as _og
+                    _og._compile(op, self.odom, ops, new_call=True, script=script)
+                else:
+                    elems = [op[1]] if op[0] == "add" else list(op[1])
+                    ops = [(0, self.gdom.element_slot(e), _lib.OP_ADD, 0, 1) for e in elems]
+        except CapacityError as e:
+            raise Unsupported(f"update not representable on the device store: {e}") from e
         cur = _new_like(self.ctx, v.val)
         _or_into(self.ctx, cur, v.val, v.val)
         if v.type == "riak_dt_gcounter":
-            from .gcounter import increment_amount
-            n = increment_amount(op)
-            cur.increment([(0, self.cdom.element_slot(actor), n)])
+            cur.increment(ops)
         elif v.type in ("lasp_orset", "lasp_orset_gbtree"):
-            ops, script = [], []
-            if v.type == "lasp_orset":
-                _o._compile(op, self.odom, ops, new_call=True)
-            else:
-                from . import orset_gbtree as _og
-                _og._compile(op, self.odom, ops, new_call=True, script=script)
             st = cur.apply_ops(ops)
             if (st == _lib.OPST_KEY_EXISTS).any():
                 j = int(np.nonzero(st == _lib.OPST_KEY_EXISTS)[0][0])
@@ -369,8 +399,7 @@ class Store:
                 raise RuntimeError(f"badmatch: {{error,{{precondition,{{not_present,"
                                    f"{self.odom.elements.terms[bad]!r}}}}}}}")
         else:
-            elems = [op[1]] if op[0] == "add" else list(op[1])
-            cur.apply_ops([(0, self.gdom.element_slot(e), _lib.OP_ADD, 0, 1) for e in elems])
+            cur.apply_ops(ops)
         gb = None
         if v.type == "lasp_orset_gbtree":
             # Type:update's tree (its insert / enter calls replayed on the stored tree),

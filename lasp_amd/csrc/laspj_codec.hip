@@ -13,7 +13,7 @@
 //             131 108 <n:32> <elem image>* 106  |  131 106 when empty
 //
 // Two launches: k_*_etf_size (one wave per replica: payload size, dictionary check)
-// feeding a device exclusive scan (hipcub) into the caller's offsets, then a writer:
+// feeding a device exclusive scan (k_scan_*) into the caller's offsets, then a writer:
 //   k_orset_etf_write_rec   every token image the same length (Lasp's 20-byte tokens):
 //                           host-built record templates, records OR-ed into 16-byte
 //                           aligned LDS windows as byte-shifted dwords (below);
@@ -23,8 +23,6 @@
 //   k_gset_etf_write        G-Set lists.
 // Elements go in term order; a block scan of their sizes places them.  The path is
 // write-bound: a payload is ~15-70x the bytes of its cells.
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -361,7 +359,8 @@ __device__ __forceinline__ void write_list_header(uint8_t* out, u64 base, uint32
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write(const u64x2* cells, uint64_t R,
                                                             uint32_t E, DictView d, int tag,
                                                             int vers, const u64* offs,
-                                                            uint8_t* out) {
+                                                            uint8_t* out, u64 ocap) {
+    if (offs[R] > ocap) return;              // the payloads do not fit: the host re-sizes
     __shared__ uint32_t lds4[kBlock / 64];
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
@@ -414,7 +413,8 @@ constexpr uint32_t kWB = 4096;
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write_wave(const u64x2* cells, uint64_t R,
                                                                  uint32_t E, DictView d, int tag,
                                                                  int vers, const u64* offs,
-                                                                 uint8_t* out) {
+                                                                 uint8_t* out, u64 ocap) {
+    if (offs[R] > ocap) return;
     __shared__ uint32_t lds4[kBlock / 64];
     __shared__ __attribute__((aligned(16))) uint8_t wbuf[kBlock / 64][kWB + 16];
     __shared__ uint32_t s_e[kBlock], s_pos[kBlock], s_sz[kBlock];
@@ -654,18 +654,6 @@ __global__ __launch_bounds__(kBlock) void k_etf_chunk_scan(u64* coff, uint64_t R
     }
 }
 
-// payload sizes from the chunk totals (etf_size for few long payloads): as
-// k_orset_etf_size, 131 108 <n:32> elements 106 or 131 106, plus the tag bytes
-__global__ void k_etf_sizes_from_chunks(const u64* coff, uint64_t R, uint32_t nch, uint32_t hdr,
-                                        u64* sizes) {
-    for (uint64_t rep = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rep < R;
-         rep += (uint64_t)gridDim.x * blockDim.x) {
-        const u64 t = coff[rep * (nch + 1ull) + nch];
-        const u64 n = t / kChunkCnt, sum = t & (kChunkCnt - 1);
-        sizes[rep] = hdr + 1u + (n ? 5u + sum + 1u : 1u);
-    }
-}
-
 // EPAR (few token slots per element): each element's thread also stages its own records
 // (no record -> element search, no rank select); otherwise records are spread over lanes.
 // coff != nullptr: split mode (above), block b writes chunks [g cper, (g + 1) cper) of
@@ -675,7 +663,8 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                                                                 uint32_t E, DictView d, int tag,
                                                                 int vers, const u64* offs,
                                                                 uint8_t* out, const u64* coff,
-                                                                uint32_t cper) {
+                                                                uint32_t cper, u64 ocap) {
+    if (offs[R] > ocap) return;
     __shared__ __attribute__((aligned(16))) uint32_t winbuf[(WIN + 2 * kGuard) / 4];
     __shared__ uint32_t s_e[kBlock], s_pos[kBlock + 1], s_rec[kBlock + 1], s_hl[kBlock];
     __shared__ u64 s_p[kBlock], s_r[kBlock], lds4[kBlock / 64];
@@ -1024,7 +1013,8 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_size(const u64* words, uint
 __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uint64_t R,
                                                            uint32_t E, uint32_t W, DictView d,
                                                            int tag, int vers, const u64* offs,
-                                                           uint8_t* out) {
+                                                           uint8_t* out, u64 ocap) {
+    if (offs[R] > ocap) return;
     __shared__ uint32_t lds4[kBlock / 64];
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
@@ -1089,7 +1079,9 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write(const u64* words, uin
 __global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words, uint64_t R,
                                                                 uint32_t E, uint32_t W,
                                                                 DictView d, int tag, int vers,
-                                                                const u64* offs, uint8_t* out) {
+                                                                const u64* offs, uint8_t* out,
+                                                                u64 ocap) {
+    if (offs[R] > ocap) return;
     const uint32_t lane = threadIdx.x & 63u, hdr = tag >= 0 ? 2u : 0u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t rep = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; rep < R;
@@ -3256,6 +3248,100 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
     }
 }
 
+// ------------------------------------------------------------------ exclusive scans
+// out[i] = in[0] + ... + in[i-1] for i <= n (out[n] = the total): the payload offsets from
+// the per-replica sizes.  Up to kScanOne values one block walks tiles of 256 with a carry
+// (one launch: the NIF path's few payloads); beyond, tile sums -> one-block scan of the
+// sums -> tiles re-scanned with their carry.
+constexpr uint64_t kScanTile = 4096;                  // 256 threads x 16 values
+constexpr uint64_t kScanOne = 8192;
+
+__global__ __launch_bounds__(kBlock) void k_scan_one(const u64* in, u64* out, uint64_t n) {
+    __shared__ u64 lds4[kBlock / 64];
+    u64 carry = 0;
+    for (uint64_t t0 = 0; t0 < n; t0 += kBlock) {
+        const uint64_t t = t0 + threadIdx.x;
+        const u64 v = t < n ? in[t] : 0;
+        u64 tot;
+        const u64 ex = block_excl_scan64(v, lds4, &tot);
+        if (t < n) out[t] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_tile_sums(const u64* in, uint64_t n, u64* sums) {
+    __shared__ u64 lds4[kBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    u64 v = 0;
+    for (uint32_t k = 0; k < kScanTile / kBlock; ++k) {
+        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        if (i < n) v += in[i];
+    }
+    u64 tot;
+    block_excl_scan64(v, lds4, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(const u64* in, u64* out, uint64_t n,
+                                                       const u64* carries) {
+    __shared__ u64 lds4[kBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    u64 carry = carries[blockIdx.x];
+    for (uint32_t k = 0; k < kScanTile / kBlock; ++k) {
+        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        const u64 v = i < n ? in[i] : 0;
+        u64 tot;
+        const u64 ex = block_excl_scan64(v, lds4, &tot);
+        if (i < n) out[i] = carry + ex;
+        carry += tot;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = carry;
+}
+
+// bytes of device scratch launch_scan needs for n values
+uint64_t scan_tmp_bytes(uint64_t n) {
+    return n <= kScanOne ? 0 : 8ull * ((n + kScanTile - 1) / kScanTile + 1);
+}
+
+hipError_t launch_scan(laspj_ctx* ctx, const u64* in, u64* out, uint64_t n, u64* tmp) {
+    if (n <= kScanOne) {
+        hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(kBlock), 0, ctx->stream, in, out, n);
+        return hipGetLastError();
+    }
+    const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_tile_sums, dim3((unsigned)tiles), dim3(kBlock), 0, ctx->stream, in,
+                       n, tmp);
+    // the carries in place: tmp[0..tiles] := exclusive scan of the tile sums
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(kBlock), 0, ctx->stream, tmp, tmp, tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kBlock), 0, ctx->stream, in, out,
+                       n, tmp);
+    return hipGetLastError();
+}
+
+// few payloads in split mode: sizes from the chunk totals (k_etf_sizes_from_chunks) and
+// their exclusive scan in one launch
+__global__ __launch_bounds__(kBlock) void k_etf_offsets_from_chunks(const u64* coff, uint64_t R,
+                                                                    uint32_t nch, uint32_t hdr,
+                                                                    u64* offs) {
+    __shared__ u64 lds4[kBlock / 64];
+    u64 carry = 0;
+    for (uint64_t t0 = 0; t0 < R; t0 += kBlock) {
+        const uint64_t rep = t0 + threadIdx.x;
+        u64 v = 0;
+        if (rep < R) {
+            const u64 t = coff[rep * (nch + 1ull) + nch];
+            const u64 n = t / kChunkCnt, sum = t & (kChunkCnt - 1);
+            v = hdr + 1u + (n ? 5u + sum + 1u : 1u);
+        }
+        u64 tot;
+        const u64 ex = block_excl_scan64(v, lds4, &tot);
+        if (rep < R) offs[rep] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) offs[R] = carry;
+}
+
 int check_args(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
                const char* what) {
     if (!ctx || !b || b->ctx != ctx || !d || d->ctx != ctx)
@@ -3275,48 +3361,11 @@ int etf_size(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int 
     if (!offsets || offsets->ctx != ctx || offsets->bytes < 8ull * (b->replicas + 1) || !total)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets must hold replicas + 1 uint64", what);
     Guard g(ctx);
-    const uint64_t R = b->replicas, n = R + 1;
-    size_t temp = 0;
-    LJ_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const u64*)nullptr,
-                                                 (u64*)nullptr, n, ctx->stream));
-    const uint64_t sizes_bytes = (8ull * n + 255ull) & ~255ull;
-    const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
-    // few long OR-Set payloads: sizes from per-chunk sums spread over the chip (as the
-    // writer's split mode) instead of one wave walking each payload
-    const bool split = kind == LASPJ_KIND_ORSET && R <= (uint64_t)ctx->cus && nch >= 4;
-    const uint64_t temp_bytes = (temp + 255ull) & ~255ull;
-    if (int s = reserve_scratch(ctx, sizes_bytes + temp_bytes +
-                                (split ? 8ull * R * (nch + 1ull) : 0ull)))
-        return s;
-    u64* sizes = static_cast<u64*>(ctx->scratch);
-    void* tmp = static_cast<char*>(ctx->scratch) + sizes_bytes;
+    const uint64_t R = b->replicas;
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag, 0, 4, ctx->stream));
-    LJ_HIP(ctx, hipMemsetAsync(sizes + R, 0, 8, ctx->stream));
-    const uint32_t hdr = tag >= 0 ? 2u : 0u;
-    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
-    int grid = (int)(blocks < cap ? blocks : cap);
-    if (split) {
-        u64* co = reinterpret_cast<u64*>(static_cast<char*>(ctx->scratch) + sizes_bytes +
-                                         temp_bytes);
-        const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
-        hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), nch,
-                           co, ctx->flag);
-        hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
-                           dim3(kBlock), 0, ctx->stream, co, R, nch);
-        hipLaunchKernelGGL(k_etf_sizes_from_chunks, dim3((unsigned)((R + 255) / 256)), dim3(256),
-                           0, ctx->stream, co, R, nch, hdr, sizes);
-    } else if (kind == LASPJ_KIND_ORSET)
-        hipLaunchKernelGGL(k_orset_etf_size, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), hdr,
-                           sizes, ctx->flag);
-    else
-        hipLaunchKernelGGL(k_gset_etf_size, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, R, b->elements,
-                           (uint32_t)b->words_per_replica, view(d), hdr, sizes, ctx->flag);
-    LJ_LAUNCHED(ctx);
-    LJ_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, temp, sizes, static_cast<u64*>(offsets->dev),
-                                                 n, ctx->stream));
+    if (int s = etf_size_enqueue(ctx, b, d, kind, tag, static_cast<u64*>(offsets->dev), ctx->flag,
+                                 nullptr))
+        return s;
     uint32_t flag = 0;
     const laspj::ReadPiece rp[2] = {{&flag, ctx->flag, 4},
                                     {total, static_cast<u64*>(offsets->dev) + R, 8}};
@@ -3342,73 +3391,9 @@ int etf_write(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int
     if (out->bytes < total)
         return fail(ctx, LASPJ_E_RANGE, "%s: output holds %llu bytes, payloads need %llu", what,
                     (unsigned long long)out->bytes, (unsigned long long)total);
-    uint64_t cap = (uint64_t)ctx->cus * 8;
-    int grid = (int)(R < cap ? R : cap);
-    if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf != 1) {
-        // 0: 24 KiB window (profiles/r01_suite_etf_windows.log), records staged by their
-        // element's thread when elements hold <= 8 token slots, spread over lanes otherwise;
-        // 2, 3: 16 / 20 KiB windows, 4: 24 KiB, always spread over lanes
-        auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true>
-                                 : k_orset_etf_write_rec<24576, false>;
-        if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384, false>;
-        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480, false>;
-        if (ctx->tune_etf == 4) k = k_orset_etf_write_rec<24576, false>;
-        if (ctx->tune_etf == 5) k = k_orset_etf_write_rec<24576, true>;
-        // one resident wave of blocks, each with a contiguous run of replicas
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||
-            occ < 1) {
-            hipGetLastError();
-            occ = 4;
-        }
-        const uint64_t resident = (uint64_t)ctx->cus * (uint64_t)occ;
-        grid = (int)(R < resident ? R : resident);
-        const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
-        const u64* coff = nullptr;
-        uint32_t cper = 0;
-        if (4 * R <= resident && nch >= 4) {
-            // split mode: few long payloads, their chunks spread over blocks
-            cper = (uint32_t)std::max<uint64_t>(1, (R * nch + resident - 1) / resident);
-            const uint64_t groups = (nch + cper - 1) / cper;
-            if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
-            u64* co = static_cast<u64*>(ctx->scratch);
-            const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
-            hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
-                               reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d),
-                               nch, co, (uint32_t*)nullptr);
-            hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
-                               dim3(kBlock), 0, ctx->stream, co, R, nch);
-            coff = co;
-            grid = (int)(R * groups);
-        }
-        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
-                           vers, static_cast<const u64*>(offsets->dev),
-                           static_cast<uint8_t*>(out->dev), coff, cper);
-    } else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
-        hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
-                           vers, static_cast<const u64*>(offsets->dev),
-                           static_cast<uint8_t*>(out->dev));
-    else if (kind == LASPJ_KIND_ORSET)
-        hipLaunchKernelGGL(k_orset_etf_write, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
-                           vers, static_cast<const u64*>(offsets->dev),
-                           static_cast<uint8_t*>(out->dev));
-    else
-        // LASPJ_TUNE_ETF_KERNEL 1: the block-per-payload staging writer
-        hipLaunchKernelGGL(ctx->tune_etf == 1 ? k_gset_etf_write : k_gset_etf_write_wave,
-                           dim3(ctx->tune_etf == 1 ? grid
-                                                   : (int)std::min<uint64_t>((R + 3) / 4,
-                                                                             (uint64_t)ctx->cus * 32)),
-                           dim3(kBlock), 0, ctx->stream,
-                           (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
-                           view(d), tag, vers, static_cast<const u64*>(offsets->dev),
-                           static_cast<uint8_t*>(out->dev));
-    LJ_LAUNCHED(ctx);
-    return LASPJ_OK;
+    return etf_write_enqueue(ctx, b, d, kind, tag, vers, static_cast<const u64*>(offsets->dev),
+                             static_cast<uint8_t*>(out->dev), out->bytes, nullptr);
 }
-
 
 int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
              const laspj_buf* payload, const laspj_buf* offsets, laspj_buf* status) {
@@ -3434,103 +3419,11 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
                         (unsigned long long)i);
     if (off[R] > payload->bytes)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
-    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
-    const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
-    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6)
-                     ? k_orset_etf_read<true> : k_orset_etf_read<false>;
-    const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
-    // the header hash (segment search; element batches without the scalar walk — knob 6
-    // keeps the walking element batches)
-    const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
-    // (knob 7: many-token dictionaries decode one element at a time)
-    const HdrHash hh_small{ctx->tune_etf_read == 6 ? nullptr : d->rd_htab, d->rd_hmask,
-                           d->rd_hlens, ctx->tune_etf_read == 7 ? 0u : 1u};
-    // Segment mode when there are too few payloads to fill the chip with one wave each
-    // (fewer than 8 per CU) and they are long: segments of S bytes, S sized for ~48 waves
-    // per CU (6 resident per SIMD, the rest queued behind them for balance), at least
-    // 2 KiB.  Knob 4 splits every payload longer than 256 bytes into 256-byte segments
-    // (what the tests use to stress the chain), 5 always splits with the sized S.
-    const uint64_t bytes_in = off[R] - off[0];
-    uint64_t S = 0, nseg = 0;
-    if (batched && d->rd_htab && ctx->tune_etf_read != 3) {
-        const uint64_t want = (uint64_t)ctx->cus * 48;
-        uint64_t longest = 0;
-        for (uint64_t i = 0; i < R; ++i) longest = std::max<uint64_t>(longest, off[i + 1] - off[i]);
-        S = std::max<uint64_t>(2048, ((bytes_in / want) + 255) & ~255ull);
-        if (ctx->tune_etf_read == 4) S = 256;
-        if (ctx->tune_etf_seg) S = (uint64_t)ctx->tune_etf_seg;
-        const bool split = (ctx->tune_etf_read >= 4 && ctx->tune_etf_read <= 6) ||
-                           ctx->tune_etf_seg ||
-                           R < (uint64_t)ctx->cus * 8;
-        if (longest < (1ull << 31) && split && longest > S) {
-            for (uint64_t i = 0; i < R; ++i)
-                nseg += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);
-            if (nseg >= (1ull << 32)) nseg = 0;
-        }
-    }
-    if (nseg) {
-        std::vector<uint32_t> segbase(R + 1);
-        uint64_t acc = 0;
-        for (uint64_t i = 0; i < R; ++i) {
-            segbase[i] = (uint32_t)acc;
-            acc += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);
-        }
-        segbase[R] = (uint32_t)acc;
-        auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
-        const uint64_t o_res = al(4ull * (R + 1)), o_redo = o_res + al(sizeof(SegRes) * nseg);
-        if (int s2 = reserve_scratch(ctx, o_redo + 4ull * (R + 1))) return s2;
-        char* sc = static_cast<char*>(ctx->scratch);
-        uint32_t* dsegbase = reinterpret_cast<uint32_t*>(sc);
-        SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
-        uint32_t* redo = reinterpret_cast<uint32_t*>(sc + o_redo);
-        LJ_HIP(ctx, hipMemcpyAsync(dsegbase, segbase.data(), 4ull * (R + 1), hipMemcpyHostToDevice,
-                                   ctx->stream));
-        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
-        const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
-        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
-                               ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
-                           dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
-                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
-                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tabs,
-                           tag, vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
-                           (uint32_t)S, hh, dres);
-        LJ_LAUNCHED(ctx);
-        hipLaunchKernelGGL(k_etf_read_chain,
-                           dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)), dim3(64), 0,
-                           ctx->stream, static_cast<const uint8_t*>(payload->dev),
-                           static_cast<const u64*>(offsets->dev), R, dsegbase, (uint32_t)S, dres,
-                           static_cast<int32_t*>(status->dev), redo);
-        LJ_LAUNCHED(ctx);
-        // the redo pass: usually an empty list (the kernel exits at once)
-        const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
-        hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
-                           ctx->stream, static_cast<const uint8_t*>(payload->dev),
-                           (u64)payload->bytes, static_cast<const u64*>(offsets->dev), R,
-                           b->elements, view(d), tabs, hh_small, tag, vers,
-                           reinterpret_cast<u64x2*>(b->dev), static_cast<int32_t*>(status->dev),
-                           (const uint32_t*)redo);
-        LJ_LAUNCHED(ctx);
-        return LASPJ_OK;
-    }
-    // one replica per wave up to 64 blocks per CU: short blocks keep every CU busy to the
-    // end (a grid-stride over a few resident waves left a 20 % tail at 65536 replicas)
-    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
-    const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    if (batched)
-        // 0: element batches when elements hold <= 8 token slots; 2: records batched only
-        hipLaunchKernelGGL(kread, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
-                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tabs,
-                           hh_small, tag, vers, reinterpret_cast<u64x2*>(b->dev),
-                           static_cast<int32_t*>(status->dev), (const uint32_t*)nullptr);
-    else
-        hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           static_cast<const uint8_t*>(payload->dev), (u64)payload->bytes,
-                           static_cast<const u64*>(offsets->dev), R, b->elements, view(d), tag,
-                           vers, reinterpret_cast<u64x2*>(b->dev),
-                           static_cast<int32_t*>(status->dev));
-    LJ_LAUNCHED(ctx);
-    return LASPJ_OK;
+    EtfReadPlan plan;
+    etf_read_plan(ctx, d, R, off.data(), &plan);
+    return etf_read_enqueue(ctx, b, d, tag, vers, static_cast<const uint8_t*>(payload->dev),
+                            payload->bytes, static_cast<const u64*>(offsets->dev), plan, nullptr,
+                            static_cast<int32_t*>(status->dev), true);
 }
 
 int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
@@ -3570,6 +3463,243 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
 }
 
 }  // namespace
+}  // namespace laspj
+
+// ------------------------------------------------------------------ enqueue-only forms
+// (laspj_internal.h): the public entry points above validate, read back what they need and
+// call these; the NIF-level entry points (laspj_nif.hip) call them directly with the
+// offsets they staged themselves, so a whole decode -> join -> encode chain runs with one
+// host synchronisation.
+namespace laspj {
+
+bool etf_dict_decodable(const laspj_etf_dict* d) { return d && d->rec_len != 0; }
+uint32_t etf_dict_elements(const laspj_etf_dict* d) { return d ? d->elements : 0; }
+
+void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, const u64* off,
+                   EtfReadPlan* plan) {
+    // Segment mode when there are too few payloads to fill the chip with one wave each
+    // (fewer than 8 per CU) and they are long: segments of S bytes, S sized for ~48 waves
+    // per CU (6 resident per SIMD, the rest queued behind them for balance), at least
+    // 2 KiB.  Knob 4 splits every payload longer than 256 bytes into 256-byte segments
+    // (what the tests use to stress the chain), 5 always splits with the sized S.
+    plan->S = plan->nseg = 0;
+    plan->segbase.clear();
+    const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
+    if (!(batched && d->rd_htab && ctx->tune_etf_read != 3)) return;
+    const uint64_t bytes_in = off[R] - off[0];
+    const uint64_t want = (uint64_t)ctx->cus * 48;
+    uint64_t longest = 0;
+    for (uint64_t i = 0; i < R; ++i) longest = std::max<uint64_t>(longest, off[i + 1] - off[i]);
+    uint64_t S = std::max<uint64_t>(2048, ((bytes_in / want) + 255) & ~255ull);
+    if (ctx->tune_etf_read == 4) S = 256;
+    if (ctx->tune_etf_seg) S = (uint64_t)ctx->tune_etf_seg;
+    const bool split = (ctx->tune_etf_read >= 4 && ctx->tune_etf_read <= 6) ||
+                       ctx->tune_etf_seg || R < (uint64_t)ctx->cus * 8;
+    if (!(longest < (1ull << 31) && split && longest > S)) return;
+    uint64_t acc = 0;
+    plan->segbase.resize(R + 1);
+    for (uint64_t i = 0; i < R; ++i) {
+        plan->segbase[i] = (uint32_t)acc;
+        acc += std::max<uint64_t>(1, (off[i + 1] - off[i] + S - 1) / S);
+        if (acc >= (1ull << 32)) {
+            plan->segbase.clear();
+            return;
+        }
+    }
+    plan->segbase[R] = (uint32_t)acc;
+    plan->S = S;
+    plan->nseg = acc;
+}
+
+int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+                     const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
+                     const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
+                     bool clear) {
+    const uint64_t R = b->replicas;
+    if (clear)
+        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
+                                   ctx->stream));
+    const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
+    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6)
+                     ? k_orset_etf_read<true> : k_orset_etf_read<false>;
+    const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+    // the header hash (segment search; element batches without the scalar walk — knob 6
+    // keeps the walking element batches)
+    const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
+    // (knob 7: many-token dictionaries decode one element at a time)
+    const HdrHash hh_small{ctx->tune_etf_read == 6 ? nullptr : d->rd_htab, d->rd_hmask,
+                           d->rd_hlens, ctx->tune_etf_read == 7 ? 0u : 1u};
+    if (plan.nseg) {
+        const uint64_t nseg = plan.nseg;
+        auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
+        const uint64_t o_res = al(4ull * (R + 1)), o_redo = o_res + al(sizeof(SegRes) * nseg);
+        if (int s2 = reserve_scratch(ctx, o_redo + 4ull * (R + 1))) return s2;
+        char* sc = static_cast<char*>(ctx->scratch);
+        const uint32_t* dsegbase = segbase;
+        if (!dsegbase) {
+            uint32_t* up = reinterpret_cast<uint32_t*>(sc);
+            LJ_HIP(ctx, hipMemcpyAsync(up, plan.segbase.data(), 4ull * (R + 1),
+                                       hipMemcpyHostToDevice, ctx->stream));
+            dsegbase = up;
+        }
+        SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
+        uint32_t* redo = reinterpret_cast<uint32_t*>(sc + o_redo);
+        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
+        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
+                               ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
+                           dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
+                           payload, (u64)payload_bytes, offs, R, b->elements, view(d), tabs, tag,
+                           vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
+                           (uint32_t)plan.S, hh, dres);
+        LJ_LAUNCHED(ctx);
+        hipLaunchKernelGGL(k_etf_read_chain,
+                           dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)), dim3(64), 0,
+                           ctx->stream, payload, offs, R, dsegbase, (uint32_t)plan.S, dres, status,
+                           redo);
+        LJ_LAUNCHED(ctx);
+        // the redo pass: usually an empty list (the kernel exits at once)
+        const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
+        hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
+                           ctx->stream, payload, (u64)payload_bytes, offs, R, b->elements,
+                           view(d), tabs, hh_small, tag, vers, reinterpret_cast<u64x2*>(b->dev),
+                           status, (const uint32_t*)redo);
+        LJ_LAUNCHED(ctx);
+        return LASPJ_OK;
+    }
+    // one replica per wave up to 64 blocks per CU: short blocks keep every CU busy to the
+    // end (a grid-stride over a few resident waves left a 20 % tail at 65536 replicas)
+    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
+    const int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
+    if (batched)
+        // 0: element batches when elements hold <= 8 token slots; 2: records batched only
+        hipLaunchKernelGGL(kread, dim3(grid), dim3(kBlock), 0, ctx->stream, payload,
+                           (u64)payload_bytes, offs, R, b->elements, view(d), tabs, hh_small, tag,
+                           vers, reinterpret_cast<u64x2*>(b->dev), status,
+                           (const uint32_t*)nullptr);
+    else
+        hipLaunchKernelGGL(k_orset_etf_read_serial, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           payload, (u64)payload_bytes, offs, R, b->elements, view(d), tag, vers,
+                           reinterpret_cast<u64x2*>(b->dev), status);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
+                     int tag, u64* offsets, uint32_t* flag, const u64** chunks) {
+    const uint64_t R = b->replicas;
+    const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    // few long OR-Set payloads: sizes from per-chunk sums spread over the chip (as the
+    // writer's split mode) instead of one wave walking each payload
+    const bool split = kind == LASPJ_KIND_ORSET && R <= (uint64_t)ctx->cus && nch >= 4;
+    if (chunks) *chunks = nullptr;
+    if (split) {
+        if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
+        u64* co = static_cast<u64*>(ctx->scratch);
+        const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+        hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), nch,
+                           co, flag);
+        hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                           dim3(kBlock), 0, ctx->stream, co, R, nch);
+        hipLaunchKernelGGL(k_etf_offsets_from_chunks, dim3(1), dim3(kBlock), 0, ctx->stream, co,
+                           R, nch, hdr, offsets);
+        LJ_LAUNCHED(ctx);
+        if (chunks) *chunks = co;
+        return LASPJ_OK;
+    }
+    const uint64_t sizes_bytes = (8ull * R + 255ull) & ~255ull;
+    if (int s = reserve_scratch(ctx, sizes_bytes + scan_tmp_bytes(R))) return s;
+    u64* sizes = static_cast<u64*>(ctx->scratch);
+    u64* tmp = reinterpret_cast<u64*>(static_cast<char*>(ctx->scratch) + sizes_bytes);
+    uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
+    int grid = (int)(blocks < cap ? (blocks ? blocks : 1) : cap);
+    if (kind == LASPJ_KIND_ORSET)
+        hipLaunchKernelGGL(k_orset_etf_size, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), hdr,
+                           sizes, flag);
+    else
+        hipLaunchKernelGGL(k_gset_etf_size, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, R, b->elements,
+                           (uint32_t)b->words_per_replica, view(d), hdr, sizes, flag);
+    LJ_LAUNCHED(ctx);
+    LJ_HIP(ctx, launch_scan(ctx, sizes, offsets, R, tmp));
+    return LASPJ_OK;
+}
+
+int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
+                      int32_t kind, int tag, int vers, const u64* offsets, uint8_t* out,
+                      uint64_t cap_bytes, const u64* chunks) {
+    const uint64_t R = b->replicas;
+    uint64_t cap = (uint64_t)ctx->cus * 8;
+    int grid = (int)(R < cap ? R : cap);
+    if (kind == LASPJ_KIND_ORSET && d->rec_len && ctx->tune_etf != 1) {
+        // 0: 24 KiB window (profiles/r01_suite_etf_windows.log), records staged by their
+        // element's thread when elements hold <= 8 token slots, spread over lanes otherwise;
+        // 2, 3: 16 / 20 KiB windows, 4: 24 KiB, always spread over lanes
+        auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true>
+                                 : k_orset_etf_write_rec<24576, false>;
+        if (ctx->tune_etf == 2) k = k_orset_etf_write_rec<16384, false>;
+        if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480, false>;
+        if (ctx->tune_etf == 4) k = k_orset_etf_write_rec<24576, false>;
+        if (ctx->tune_etf == 5) k = k_orset_etf_write_rec<24576, true>;
+        // one resident wave of blocks, each with a contiguous run of replicas
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||
+            occ < 1) {
+            hipGetLastError();
+            occ = 4;
+        }
+        const uint64_t resident = (uint64_t)ctx->cus * (uint64_t)occ;
+        grid = (int)(R < resident ? R : resident);
+        const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+        const u64* coff = nullptr;
+        uint32_t cper = 0;
+        if (4 * R <= resident && nch >= 4) {
+            // split mode: few long payloads, their chunks spread over blocks (the chunk
+            // offsets come from the size pass when it ran in split mode too)
+            cper = (uint32_t)std::max<uint64_t>(1, (R * nch + resident - 1) / resident);
+            const uint64_t groups = (nch + cper - 1) / cper;
+            if (chunks) {
+                coff = chunks;
+            } else {
+                if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
+                u64* co = static_cast<u64*>(ctx->scratch);
+                const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+                hipLaunchKernelGGL(k_etf_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0,
+                                   ctx->stream, reinterpret_cast<const u64x2*>(b->dev), R,
+                                   b->elements, view(d), nch, co, (uint32_t*)nullptr);
+                hipLaunchKernelGGL(k_etf_chunk_scan, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                                   dim3(kBlock), 0, ctx->stream, co, R, nch);
+                coff = co;
+            }
+            grid = (int)(R * groups);
+        }
+        hipLaunchKernelGGL(k, dim3(grid ? grid : 1), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
+                           vers, offsets, out, coff, cper, (u64)cap_bytes);
+    } else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
+        hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid ? grid : 1), dim3(kBlock), 0,
+                           ctx->stream, reinterpret_cast<const u64x2*>(b->dev), R, b->elements,
+                           view(d), tag, vers, offsets, out, (u64)cap_bytes);
+    else if (kind == LASPJ_KIND_ORSET)
+        hipLaunchKernelGGL(k_orset_etf_write, dim3(grid ? grid : 1), dim3(kBlock), 0, ctx->stream,
+                           reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
+                           vers, offsets, out, (u64)cap_bytes);
+    else
+        // LASPJ_TUNE_ETF_KERNEL 1: the block-per-payload staging writer
+        hipLaunchKernelGGL(ctx->tune_etf == 1 ? k_gset_etf_write : k_gset_etf_write_wave,
+                           dim3(ctx->tune_etf == 1 ? (grid ? grid : 1)
+                                                   : (int)std::max<uint64_t>(1, std::min<uint64_t>(
+                                                         (R + 3) / 4, (uint64_t)ctx->cus * 32))),
+                           dim3(kBlock), 0, ctx->stream,
+                           (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
+                           view(d), tag, vers, offsets, out, (u64)cap_bytes);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 }  // namespace laspj
 
 using laspj::fail;

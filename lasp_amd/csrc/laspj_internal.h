@@ -195,4 +195,34 @@ hipError_t launch_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_bat
 hipError_t launch_gset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                               const uint32_t* index);
 
+
+// ---- wire codec, enqueue-only forms (laspj_codec.hip) -----------------------------------
+// For callers that hold ctx->mu and know the payload offsets on the host (the NIF-level
+// entry points, laspj_nif.hip): no readbacks, no synchronisation — a decode -> join ->
+// encode chain then costs one host round trip.  Pointers are device addresses.
+struct EtfReadPlan {
+    uint64_t S = 0, nseg = 0;               // segment bytes / count (0: a wave per payload)
+    std::vector<uint32_t> segbase;          // R + 1 when nseg
+};
+bool etf_dict_decodable(const laspj_etf_dict* d);     // from_binary runs on the device
+uint32_t etf_dict_elements(const laspj_etf_dict* d);
+void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R,
+                   const unsigned long long* host_offsets, EtfReadPlan* plan);
+// segbase: plan.segbase already on the device, or null (uploaded here); clear: zero the
+// batch first (the decoders only set the cells they decode)
+int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+                     const uint8_t* payload, uint64_t payload_bytes,
+                     const unsigned long long* offsets, const EtfReadPlan& plan,
+                     const uint32_t* segbase, int32_t* status, bool clear);
+// offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
+// caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
+// (valid until the context's scratch is next used), or null
+int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
+                     int tag, unsigned long long* offsets, uint32_t* flag,
+                     const unsigned long long** chunks);
+// writes nothing when offsets[R] > cap (the caller reads offsets[R] back and re-sizes)
+int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
+                      int32_t kind, int tag, int vers, const unsigned long long* offsets,
+                      uint8_t* out, uint64_t cap, const unsigned long long* chunks);
+
 }  // namespace laspj

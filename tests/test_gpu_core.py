@@ -190,3 +190,66 @@ def test_gcounter_increment_amounts_on_device():
     assert st.read(c, (1 << 32) + 6) is not None
     assert st.read(c, ("strict", (1 << 32) + 6)) is None
     assert st.read(c, ("strict", (1 << 32) + 5.5)) is not None
+
+
+def test_store_unrepresentable_values_raise_not_swallowed():
+    """VERDICT r3 'What's weak' 1: a value the columnar form cannot hold (an element with
+    a 65th token, an element past the store's capacity) must not make bind/3 answer `ok`
+    with the variable unchanged — the reference's merge takes it and lasp_core.erl:300-304
+    writes it.  The device store raises Unsupported, keeps the value it had (equal to the
+    oracle store's value before the failing call) and registers no slots for the attempt."""
+    from lasp_amd import core as dcore
+    toks = [bytes([7, k]) + bytes(18) for k in range(66)]
+    ds, os_ = dcore.Store(capacity=8), ocore.Store()
+    ids = []
+    for st in (ds, os_):
+        _, a = st.declare("lasp_orset")
+        ids.append(a)
+        for k in range(64):                   # 64 tokens on element 1: still representable
+            st.update(a, ("add_by_token", toks[k], 1), None)
+    a_d, a_o = ids
+    assert exact_eq(ds.value(a_d), os_.value(a_o))
+    n_el, n_tok = ds.odom.size, len(ds.odom.tokens[0].terms)
+
+    # update/3 minting the 65th token: the reference writes it; the device store raises
+    os_.update(a_o, ("add_by_token", toks[64], 1), None)
+    with pytest.raises(dcore.Unsupported):
+        ds.update(a_d, ("add_by_token", toks[64], 1), None)
+    assert len(ds.odom.tokens[0].terms) == n_tok and ds.odom.size == n_el
+    # bind/3 of a value carrying 65 tokens on one element, and through bind_many
+    big = [(1, [(t, False) for t in sorted(toks[:65])])]
+    for call in (lambda: ds.bind(a_d, big), lambda: ds.bind_many([(a_d, big)])):
+        with pytest.raises(dcore.Unsupported):
+            call()
+        assert len(ds.odom.tokens[0].terms) == n_tok and ds.odom.size == n_el
+    assert len(ds.value(a_d)[0][1]) == 64     # unchanged, never silently "ok"
+
+    # one element past capacity (8 slots): element 1 is registered, 8 more do not fit
+    wide = [(1, [(toks[0], False)])] + [(e, [(toks[65], False)]) for e in range(2, 10)]
+    with pytest.raises(dcore.Unsupported):
+        ds.bind(a_d, wide)
+    assert ds.odom.size == n_el and len(ds.odom.tokens) == n_el
+    # a representable bind afterwards still lands exactly as in the oracle store
+    ok = [(e, [(toks[65], False)]) for e in range(2, 9)]
+    ds.bind(a_d, ok)
+    os2 = ocore.Store()
+    _, b_o = os2.declare("lasp_orset")
+    for k in range(64):
+        os2.update(b_o, ("add_by_token", toks[k], 1), None)
+    os2.bind(b_o, ok)
+    assert exact_eq(ds.value(a_d), os2.value(b_o))
+
+    # G-Sets and G-Counters: an element / actor past capacity
+    _, g = ds.declare("lasp_gset")
+    ds.bind(g, list(range(8)))
+    with pytest.raises(dcore.Unsupported):
+        ds.bind(g, list(range(9)))
+    with pytest.raises(dcore.Unsupported):
+        ds.update(g, ("add", 100), None)
+    assert ds.value(g) == list(range(8)) and ds.gdom.size == 8
+    _, c = ds.declare("riak_dt_gcounter")
+    for actor in range(8):
+        ds.update(c, "increment", actor)
+    with pytest.raises(dcore.Unsupported):
+        ds.update(c, "increment", 8)
+    assert ds.type_value(c) == 8 and ds.cdom.size == 8

@@ -220,3 +220,31 @@ def test_dict_add_failed_payload_registers_nothing(lib):
     g = etf.term_to_binary([100, 200, 300])
     assert d.add(_lib.KIND_GSET, [g[:-2]])[0] == _lib.DEC_MALFORMED
     assert d.info()[0] == 4
+
+
+def test_domain_journal_undoes_failed_registrations():
+    """Store._encode registers under Domain.journal(): an encode that fails part way (a
+    65th token, an element past capacity, a non-orddict) leaves no slots behind, and the
+    term order afterwards is the order of the surviving slots."""
+    from lasp_amd.codec import CapacityError
+    dom = Domain(element_capacity=4)
+    dom.encode_orset([[(1, [(b"t1", False)]), (3, [(b"t3", False)])]], 4)
+    before = (list(dom.elements.terms), [list(t.terms) for t in dom.tokens], list(dom.tok_log))
+    order0 = list(dom.elements.order())
+    with pytest.raises(CapacityError):
+        with dom.journal():
+            dom.encode_orset([[(0, [(b"a", False)]), (2, [(b"b", False)]),
+                               (5, [(b"c", False)]), (7, [(b"d", False)])]], 4)
+    assert (list(dom.elements.terms), [list(t.terms) for t in dom.tokens],
+            list(dom.tok_log)) == before
+    assert list(dom.elements.order()) == order0
+    assert dom.element_slot(5, create=False) == -1
+    with pytest.raises(CapacityError):
+        with dom.journal():
+            for k in range(65):
+                dom.token_slot(0, bytes([k]))
+    assert list(dom.tokens[0].terms) == [b"t1"]
+    with dom.journal():                      # a block that succeeds keeps its slots
+        dom.element_slot(2)
+    assert dom.size == 3 and len(dom.tokens) == 3
+    assert [dom.elements.terms[int(s)] for s in dom.elements.order()] == [1, 2, 3]
