@@ -191,6 +191,7 @@ def cpu_baseline(elements: int, budget: float):
     cores = host_cores()
     eps, merges, secs = orc.bench_orset_merge(elements, 2, cores, 2, budget)
     m, u, f, v, infl = orc.bench_config1_ext(10_000, 200, 5)
+    m_threads = orc.bench_config1_merge_threads(10_000, cores, 2.0)
     # a second column: the device's own cell layout OR-ed on the same cores (bounded by
     # host DRAM bandwidth, not by the orddict walk)
     per_thread = 1 << 22                 # 4M cells = 64 MiB per array per thread
@@ -206,7 +207,9 @@ def cpu_baseline(elements: int, budget: float):
                                 f"~{min(3.0, budget / 4):.0f} s")},
         "config1": {"workload": "2 replicas x 10k elements (BASELINE configs[0]), 1 thread",
                     "us_merge": m, "us_union": u, "us_filter": f, "us_value": v,
-                    "us_inflation": infl},
+                    "us_inflation": infl,
+                    "us_merge_all_cores_per_merge": m_threads,
+                    "all_cores": cores},
     }
 
 
@@ -299,6 +302,48 @@ def config1_gpu(ctx):
         for _ in range(20):
             fn()
         out[name] = (time.perf_counter() - t0) * 1e6 / 20
+    # the NIF-level entry point (laspj_orset_etf_merge, laspj_nif.hip): the same two
+    # images in host memory -> the merged image in pinned host memory, one C call with one
+    # host synchronisation (the context's own dictionary, warmed by the first call); and
+    # n queued merges in one call (laspj_orset_etf_merge_many), per merge
+    op, on, vd = C.c_void_p(), C.c_uint64(), C.c_int32()
+
+    def nif():
+        check(L.laspj_orset_etf_merge(ctx.h, pa, len(pa), pb, len(pb), C.byref(op),
+                                      C.byref(on), C.byref(vd)), ctx.h)
+
+    nif()
+    if vd.value != 0 or C.string_at(op, on.value) != ref:
+        raise RuntimeError("config1: the NIF entry point's merge differs from the host encoder")
+    nif()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        nif()
+    out["us_merge_nif"] = (time.perf_counter() - t0) * 1e6 / 50
+    nm = 32
+    arr_a = (C.c_char_p * nm)(*([pa] * nm))
+    arr_b = (C.c_char_p * nm)(*([pb] * nm))
+    len_a = (C.c_uint64 * nm)(*([len(pa)] * nm))
+    len_b = (C.c_uint64 * nm)(*([len(pb)] * nm))
+    outs, olens, vds = (C.c_void_p * nm)(), (C.c_uint64 * nm)(), (C.c_int32 * nm)()
+
+    def nif_many():
+        check(L.laspj_orset_etf_merge_many(ctx.h, nm, arr_a, len_a, arr_b, len_b, outs, olens,
+                                           vds), ctx.h)
+
+    nif_many()
+    if any(vds[k] for k in range(nm)) or C.string_at(outs[nm - 1], olens[nm - 1]) != ref:
+        raise RuntimeError("config1: merge_many differs from the host encoder")
+    t0 = time.perf_counter()
+    for _ in range(5):
+        nif_many()
+    out["us_merge_nif_many_per_merge"] = (time.perf_counter() - t0) * 1e6 / (5 * nm)
+    out["nif_many_batch"] = nm
+    st = (C.c_uint64 * 8)()
+    check(L.laspj_nif_stats(ctx.h, st, 8), ctx.h)
+    out["nif_stats"] = dict(zip(("calls", "device_passes", "registrations", "dict_resets",
+                                 "image_rebuilds", "host_encoded_passes", "fallbacks",
+                                 "dict_elements"), (int(x) for x in st)))
     # where the device-decode path's time goes (one call, synchronised per stage)
     stages = {}
     t0 = time.perf_counter()

@@ -738,6 +738,56 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
                       const uint64_t* offsets, uint64_t n, int tag, uint32_t E, uint64_t* out,
                       int32_t* status);
 
+/* ------------------------------------------------------------------ NIF entry points */
+/* What a NIF function does between enif_term_to_binary/3 and enif_binary_to_term/4, as
+ * one call: the operands arrive as term_to_binary/1 images (131 + the orddict
+ * [{Elem, [{Token, true|false}]}], no tag bytes), are decoded on the device against the
+ * context's own dictionary, answered there and encoded back — one copy each way and one
+ * host synchronisation when every term is already in the dictionary; terms it has not
+ * seen are registered (laspj_dict_add) and the device pass runs again.  Each context keeps
+ * its own dictionary, device images, pinned staging and scratch (one context per BEAM
+ * scheduler; no process globals); a context serialises its calls.
+ *
+ * verdict LASPJ_NIF_OK: the answer is valid.  LASPJ_NIF_FALLBACK: an operand this path
+ * does not take — not a list of {Elem, [{Token, true|false}]} with keys and tokens
+ * strictly ascending in term order, an element with no tokens or more than 64, a term
+ * kind no dictionary holds — and the NIF runs the reference's own Erlang clause on the
+ * terms (so the caller gets the reference's answer, or its exception).  A non-zero return
+ * status is a library failure (E_NOMEM / E_DEVICE: raise).
+ *
+ * *out points into the context's pinned memory and stays valid until the next call on the
+ * same context: the NIF hands it to enif_binary_to_term at once. */
+#define LASPJ_NIF_OK       0
+#define LASPJ_NIF_FALLBACK 1
+/* merge/2 — lasp_orset.erl:128-134 (as lasp_core:bind/3 calls it, lasp_core.erl:298-311):
+ * *out = term_to_binary(merge(A, B)) */
+int laspj_orset_etf_merge(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                          uint64_t nb, const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* n merges in one pass (a vnode's queued binds, lasp_vnode.erl:213-237): out[i], out_len[i],
+ * verdict[i] per pair */
+int laspj_orset_etf_merge_many(laspj_ctx* ctx, uint32_t n, const uint8_t* const* a,
+                               const uint64_t* na, const uint8_t* const* b, const uint64_t* nb,
+                               const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* value/1 — lasp_orset.erl:67-73: *out = term_to_binary(value(S)) (the keys with a
+ * {_, false} token, in term order) */
+int laspj_orset_etf_value(laspj_ctx* ctx, const uint8_t* s, uint64_t ns, const uint8_t** out,
+                          uint64_t* out_len, int32_t* verdict);
+/* equal/2 — lasp_orset.erl:136-138 (ORDictA == ORDictB): *result 1 / 0 */
+int laspj_orset_etf_equal(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                          uint64_t nb, int32_t* result, int32_t* verdict);
+/* is_inflation (strict = 0) / is_strict_inflation (strict = 1) of prev -> cur —
+ * lasp_lattice.erl:97-98,153-161 / 105-106,235-253: *result 1 / 0 */
+int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
+                              const uint8_t* cur, uint64_t nc, int strict, int32_t* result,
+                              int32_t* verdict);
+/* counters of this context's NIF path: [0] calls, [1] device passes, [2] dictionary
+ * registrations, [3] dictionary resets, [4] device image rebuilds, [5] host-encoded passes
+ * (token images of mixed lengths), [6] FALLBACK verdicts, [7] dictionary elements */
+#define LASPJ_NIF_STATS 8
+int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
+/* drop the context's dictionary (its memory; the next call registers afresh) */
+int laspj_nif_reset(laspj_ctx* ctx);
+
 /* ------------------------------------------------------------------ timing */
 int laspj_event_create(laspj_ctx* ctx, laspj_event** out);
 int laspj_event_destroy(laspj_event* ev);

@@ -38,6 +38,8 @@ TUNE_PRODUCT_ROWS = 6
 TUNE_PRODUCT_COLS = 7
 TUNE_ETF_READ = 8
 TUNE_ETF_SEG = 9
+NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
+NIF_STATS = 8
 
 
 class LaspjUnavailable(RuntimeError):
@@ -203,6 +205,16 @@ SIGNATURES = {
     "laspj_dict_info": (i, [vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64)]),
     "laspj_dict_export": (i, [vp, u32, vp, vp, vp, vp, vp, vp]),
     "laspj_dict_encode": (i, [vp, C.c_int32, vp, vp, u64, i, u32, vp, vp]),
+    "laspj_orset_etf_merge": (i, [vp, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                  C.POINTER(C.c_int32)]),
+    "laspj_orset_etf_merge_many": (i, [vp, u32, vp, vp, vp, vp, vp, vp, vp]),
+    "laspj_orset_etf_value": (i, [vp, vp, u64, vpp, C.POINTER(u64), C.POINTER(C.c_int32)]),
+    "laspj_orset_etf_equal": (i, [vp, vp, u64, vp, u64, C.POINTER(C.c_int32),
+                                  C.POINTER(C.c_int32)]),
+    "laspj_orset_etf_inflation": (i, [vp, vp, u64, vp, u64, i, C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_int32)]),
+    "laspj_nif_stats": (i, [vp, vp, u32]),
+    "laspj_nif_reset": (i, [vp]),
     "laspj_event_create": (i, [vp, vpp]),
     "laspj_event_destroy": (i, [vp]),
     "laspj_event_record": (i, [vp, vp]),

@@ -12,6 +12,11 @@
 
 #include "../../include/laspj.h"
 
+namespace laspj {
+struct NifState;                       // laspj_nif.hip
+void nif_destroy(laspj_ctx* ctx);      // call without ctx->mu held
+}  // namespace laspj
+
 struct laspj_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -49,6 +54,8 @@ struct laspj_ctx {
     // no hipMalloc on the bind path's short-lived lists and buffers
     std::map<uint64_t, std::vector<void*>> cache;
     uint64_t cached_bytes = 0;
+    // the NIF-level entry points' dictionary, staging and scratch (laspj_nif.hip)
+    laspj::NifState* nif = nullptr;
 };
 
 struct laspj_buf {

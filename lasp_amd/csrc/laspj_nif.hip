@@ -1,0 +1,608 @@
+// NIF-level entry points (include/laspj.h "NIF entry points"): what a `laspj_nif` NIF
+// function does between `enif_term_to_binary` and `enif_binary_to_term`, inside liblaspj
+// so that it is compiled, tested and timed here rather than living as a listing.
+//
+// The reference's drop-in point is `Type:merge/2` and friends (lasp_orset.erl:32-36,
+// 67-73, 128-138), called from lasp_core:bind/3 (lasp_core.erl:291-312) on many BEAM
+// schedulers at once (lasp_vnode.erl:213-237).  A call here takes the operands as
+// `term_to_binary/1` images and
+//   1. stages them into the context's pinned ring and copies them to the device (one
+//      asynchronous copy; offsets and the decoder's segment table ride along),
+//   2. decodes them on the device against the context's dictionary (laspj_orset_etf_read's
+//      kernels), joins / tests / filters the cells, encodes the answer on the device
+//      (laspj_orset_etf_write's kernels) and copies it back — all enqueued on the
+//      context's stream with ONE host synchronisation,
+//   3. answers from pinned memory: the merged / value term's image (what the NIF hands to
+//      enif_binary_to_term) or the boolean.
+// A term the dictionary has not seen (a freshly minted token) makes the decoder answer
+// UNKNOWN_TERM: the call registers the operands' terms in the host dictionary
+// (laspj_dict_add), rebuilds the device images and runs the device pass again.  An
+// operand the columnar form does not take — not an orddict of {Elem, [{Token, Bool}]} in
+// term order, an element with no tokens or more than 64, a term kind no dictionary holds —
+// gets verdict LASPJ_NIF_FALLBACK: the NIF then runs the reference's own Erlang clause,
+// so the caller always gets the reference's answer (or its crash).  Scratch, dictionary
+// and staging are per context: one context per scheduler, no process globals.
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "laspj_internal.h"
+
+namespace laspj {
+
+struct NifState {
+    std::mutex mu;                  // one call at a time (ctx->mu is held per device phase)
+    laspj_dict* dict = nullptr;     // term images -> slots (host, append-only)
+    laspj_etf_dict* etf = nullptr;  // the device images of `dict` (rebuilt when it grows)
+    uint32_t E = 0;                 // element slots of `etf` and of the batches
+    bool stale = false;             // `dict` registered terms since `etf` was built
+    // device: [in region: offsets | segment table | payloads or cells][out region: statuses
+    // | answer bytes | payload offsets | payloads]; cells: the batches
+    void* dblk = nullptr;
+    uint64_t dblk_bytes = 0;
+    void* dcells = nullptr;
+    uint64_t dcells_bytes = 0;
+    // pinned host staging for the two copies
+    void* hin = nullptr;
+    uint64_t hin_bytes = 0;
+    void* hout = nullptr;
+    uint64_t hout_bytes = 0;
+    uint64_t ocap = 1 << 20;        // device bytes reserved for answer payloads
+    uint64_t stats[LASPJ_NIF_STATS] = {};
+};
+
+namespace {
+
+struct Guard {
+    std::lock_guard<std::mutex> lk;
+    explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
+};
+
+constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is reset
+constexpr uint64_t kStagePiece = 256ull << 10;    // host -> pinned staging granule
+
+uint64_t al(uint64_t x, uint64_t a) { return (x + a - 1) & ~(a - 1); }
+
+enum class Op { MERGE, VALUE, EQUAL, INFLATION };
+
+// one NIF-level call over m operand payloads giving n answers
+struct Call {
+    Op op = Op::MERGE;
+    int strict = 0;
+    uint32_t n = 0, m = 0;
+    std::vector<const uint8_t*> p;  // m payloads: MERGE / EQUAL / INFLATION: lhs[0..n) then rhs
+    std::vector<uint64_t> len;
+    std::vector<int32_t> st;        // m decode statuses
+    std::vector<uint8_t> res;       // n answer bytes (EQUAL / INFLATION)
+    std::vector<uint64_t> ooff;     // n + 1 answer payload offsets (MERGE / VALUE)
+    const uint8_t* obase = nullptr; // pinned answer payloads
+};
+
+laspj_batch view(laspj_ctx* ctx, int32_t kind, uint64_t R, uint32_t E, uint64_t* dev) {
+    laspj_batch b;
+    b.ctx = ctx;
+    b.kind = kind;
+    b.elements = E;
+    b.replicas = R;
+    b.words_per_replica = kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
+    b.cells = E;
+    b.dev = dev;
+    b.owns = false;
+    return b;
+}
+
+int grow_dev(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
+    if (*have >= need) return LASPJ_OK;
+    const uint64_t want = std::max<uint64_t>(need, *have + *have / 2);
+    if (*p) {
+        hipStreamSynchronize(ctx->stream);
+        hipFree(*p);
+        *p = nullptr;
+        *have = 0;
+    }
+    if (hipMalloc(p, want) != hipSuccess) {
+        hipGetLastError();
+        dev_cache_clear(ctx);                       // give the block cache back, retry
+        if (hipMalloc(p, want) != hipSuccess) {
+            hipGetLastError();
+            *p = nullptr;
+            return fail(ctx, LASPJ_E_NOMEM, "nif: device allocation of %llu bytes",
+                        (unsigned long long)want);
+        }
+    }
+    *have = want;
+    return LASPJ_OK;
+}
+
+int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
+    if (*have >= need) return LASPJ_OK;
+    const uint64_t want = std::max<uint64_t>(need, *have + *have / 2);
+    if (*p) {
+        hipStreamSynchronize(ctx->stream);
+        hipHostFree(*p);
+        *p = nullptr;
+        *have = 0;
+    }
+    if (hipHostMalloc(p, want, hipHostMallocDefault) != hipSuccess) {
+        hipGetLastError();
+        *p = nullptr;
+        return fail(ctx, LASPJ_E_NOMEM, "nif: pinned allocation of %llu bytes",
+                    (unsigned long long)want);
+    }
+    *have = want;
+    return LASPJ_OK;
+}
+
+void free_etf(NifState* S) {
+    if (S->etf) laspj_etf_dict_destroy(S->etf);
+    S->etf = nullptr;
+    S->E = 0;
+}
+
+int reset_dict(laspj_ctx* ctx, NifState* S) {
+    free_etf(S);
+    if (S->dict) laspj_dict_destroy(S->dict);
+    S->dict = nullptr;
+    if (laspj_dict_create(&S->dict) != LASPJ_OK)
+        return fail(ctx, LASPJ_E_NOMEM, "nif: dictionary allocation");
+    S->stale = false;
+    ++S->stats[3];
+    return LASPJ_OK;
+}
+
+// the device images of the dictionary (called without ctx->mu: etf_dict_create takes it)
+int rebuild_etf(laspj_ctx* ctx, NifState* S) {
+    uint32_t n = 0;
+    uint64_t eb = 0, tb = 0;
+    if (laspj_dict_info(S->dict, &n, &eb, &tb) != LASPJ_OK)
+        return fail(ctx, LASPJ_E_INVAL, "nif: dictionary info");
+    // head-room: registrations are append-only, so a larger E holds the next terms
+    uint32_t E = S->E;
+    if (!S->etf || n > E) E = n + n / 4 + 64;
+    std::vector<uint8_t> ebl(eb + 1), tbl(tb + 1), tord(64ull * E);
+    std::vector<uint32_t> eoff(E + 1ull), eord(E), toff(64ull * E + 1);
+    if (laspj_dict_export(S->dict, E, ebl.data(), eoff.data(), eord.data(), tbl.data(),
+                          toff.data(), tord.data()) != LASPJ_OK)
+        return fail(ctx, LASPJ_E_INVAL, "nif: dictionary export");
+    free_etf(S);
+    laspj_etf_dict* d = nullptr;
+    if (int s = laspj_etf_dict_create(ctx, E, ebl.data(), eoff.data(), eord.data(), tbl.data(),
+                                      toff.data(), tord.data(), &d))
+        return s;
+    S->etf = d;
+    S->E = E;
+    S->stale = false;
+    ++S->stats[4];
+    return LASPJ_OK;
+}
+
+// One device pass: stage, copy, decode (or upload host-encoded cells), answer, copy back,
+// one synchronisation.  Fills c.st / c.res / c.ooff / c.obase.
+int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
+    const uint32_t m = c.m, n = c.n, E = S->E;
+    const bool dec = etf_dict_decodable(S->etf);
+    std::vector<unsigned long long> hoffs(m + 1ull, 0);
+    for (uint32_t i = 0; i < m; ++i) hoffs[i + 1] = hoffs[i] + c.len[i];
+    const uint64_t pay = hoffs[m];
+    EtfReadPlan plan;
+    if (dec) etf_read_plan(ctx, S->etf, m, hoffs.data(), &plan);
+    const bool has_payload_out = c.op == Op::MERGE || c.op == Op::VALUE;
+    // in region (host -> device)
+    const uint64_t i_offs = 0, i_seg = al(8ull * (m + 1), 256),
+                   i_pay = i_seg + (plan.nseg ? al(4ull * (m + 1), 256) : 0);
+    const uint64_t cells_in = (uint64_t)m * E * 16ull;
+    const uint64_t in_bytes = i_pay + (dec ? al(pay + 64, 256) : al(cells_in, 256));
+    // out region (device -> host)
+    const uint64_t o_st = 0, o_res = al(4ull * m, 16), o_ooff = o_res + al(n, 16),
+                   o_pay = o_ooff + al(8ull * (n + 1), 16);
+    // answer payload bound: a merge's image is at most both operands' (flags may be
+    // re-encoded one byte longer than a SMALL_ATOM_UTF8 input: the slack, and a second
+    // copy when even that is short); value/1's at most its operand's
+    uint64_t bound = 64ull * n + 64;
+    for (uint32_t i = 0; i < m; ++i) bound += c.len[i];
+    if (has_payload_out) {
+        if (S->ocap < bound + bound / 8) S->ocap = al(bound + bound / 8, 1 << 16);
+    }
+    const uint64_t ocap = has_payload_out ? S->ocap : 0;
+    const uint64_t out_bytes = o_pay + ocap;
+    // cells: in batch m x E; MERGE: answers n x E; VALUE: value words n x ceil(E/64)
+    const uint64_t W = (E + 63ull) / 64ull;
+    const uint64_t cells_out = c.op == Op::MERGE ? (uint64_t)n * E * 16ull
+                               : c.op == Op::VALUE ? (uint64_t)n * W * 8ull : 0;
+    const uint64_t c_out = al(cells_in, 256);
+    std::vector<uint8_t> blob;      // the host-encode path's contiguous payloads
+    {
+        Guard g(ctx);
+        if (int s = grow_dev(ctx, &S->dblk, &S->dblk_bytes, al(in_bytes, 256) + out_bytes)) return s;
+        if (int s = grow_dev(ctx, &S->dcells, &S->dcells_bytes, c_out + cells_out + 256)) return s;
+        if (int s = grow_host(ctx, &S->hin, &S->hin_bytes, in_bytes)) return s;
+        if (int s = grow_host(ctx, &S->hout, &S->hout_bytes, out_bytes)) return s;
+    }
+    uint8_t* hin = static_cast<uint8_t*>(S->hin);
+    uint8_t* din = static_cast<uint8_t*>(S->dblk);
+    uint8_t* dout = din + al(in_bytes, 256);
+    uint64_t* cin = static_cast<uint64_t*>(S->dcells);
+    uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
+    std::memcpy(hin + i_offs, hoffs.data(), 8ull * (m + 1));
+    if (plan.nseg) std::memcpy(hin + i_seg, plan.segbase.data(), 4ull * (m + 1));
+    std::vector<int32_t> hst;
+    if (!dec) {
+        // token images of several lengths (or no tokens yet): the host dictionary encodes
+        // the cells (laspj_dict_encode), the device does the rest
+        blob.resize(pay);
+        for (uint32_t i = 0; i < m; ++i)
+            if (c.len[i]) std::memcpy(blob.data() + hoffs[i], c.p[i], c.len[i]);
+        hst.assign(m, 0);
+        if (int s = laspj_dict_encode(S->dict, LASPJ_KIND_ORSET, blob.data(),
+                                      reinterpret_cast<const uint64_t*>(hoffs.data()), m, -1, E,
+                                      reinterpret_cast<uint64_t*>(hin + i_pay), hst.data()))
+            return fail(ctx, s, "nif: host encode failed (%d)", s);
+        ++S->stats[5];
+    }
+    {
+        Guard g(ctx);
+        // the offsets (and segment table), then the payloads a piece at a time: each
+        // piece's copy starts while the next one is staged
+        if (dec) {
+            uint64_t at = 0;
+            uint32_t i = 0;
+            uint64_t io = 0;                     // offset inside payload i
+            uint64_t sent = 0;                   // region bytes already copied
+            const uint64_t head = i_pay;
+            while (i < m && c.len[i] == 0) ++i;
+            while (at < pay) {
+                const uint64_t piece = std::min(kStagePiece, pay - at);
+                uint64_t done = 0;
+                while (done < piece) {
+                    const uint64_t take = std::min(piece - done, c.len[i] - io);
+                    std::memcpy(hin + i_pay + at + done, c.p[i] + io, take);
+                    done += take;
+                    io += take;
+                    if (io == c.len[i]) {
+                        ++i;
+                        io = 0;
+                        while (i < m && c.len[i] == 0) ++i;
+                    }
+                }
+                at += piece;
+                const uint64_t upto = head + at;
+                LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, upto - sent,
+                                           hipMemcpyHostToDevice, ctx->stream));
+                sent = upto;
+            }
+            if (pay == 0)
+                LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, head - sent,
+                                           hipMemcpyHostToDevice, ctx->stream));
+        } else {
+            LJ_HIP(ctx, hipMemcpyAsync(cin, hin + i_pay, cells_in, hipMemcpyHostToDevice,
+                                       ctx->stream));
+        }
+        laspj_batch inb = view(ctx, LASPJ_KIND_ORSET, m, E, cin);
+        int32_t* dst = reinterpret_cast<int32_t*>(dout + o_st);
+        if (dec) {
+            if (int s = etf_read_enqueue(ctx, &inb, S->etf, -1, 1, din + i_pay, pay,
+                                         reinterpret_cast<const unsigned long long*>(din + i_offs),
+                                         plan,
+                                         plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg)
+                                                   : nullptr,
+                                         dst, true))
+                return s;
+        }
+        laspj_batch lhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin);
+        laspj_batch rhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin + (uint64_t)n * 2ull * E);
+        auto* dooff = reinterpret_cast<unsigned long long*>(dout + o_ooff);
+        uint8_t* dopay = dout + o_pay;
+        switch (c.op) {
+        case Op::MERGE: {
+            // lasp_orset:merge/2 (lasp_orset.erl:128-134): the nested orddict:merge of two
+            // canonical orddicts is the slot-wise OR of their cells
+            LJ_HIP(ctx, launch_or(ctx, cout, lhs.dev, rhs.dev, (uint64_t)n * 2ull * E));
+            laspj_batch ob = view(ctx, LASPJ_KIND_ORSET, n, E, cout);
+            const unsigned long long* chunks = nullptr;
+            if (int s = etf_size_enqueue(ctx, &ob, S->etf, LASPJ_KIND_ORSET, -1, dooff, ctx->flag,
+                                         &chunks))
+                return s;
+            if (int s = etf_write_enqueue(ctx, &ob, S->etf, LASPJ_KIND_ORSET, -1, 1, dooff, dopay,
+                                          ocap, chunks))
+                return s;
+            break;
+        }
+        case Op::VALUE: {
+            // value/1 (lasp_orset.erl:67-73): the elements with a {_, false} token, as the
+            // ordset image the G-Set writer gives a bit row (term_to_binary of the keys)
+            LJ_HIP(ctx, launch_orset_value(ctx, &inb, cout, false));
+            laspj_batch vb = view(ctx, LASPJ_KIND_GSET, n, E, cout);
+            if (int s = etf_size_enqueue(ctx, &vb, S->etf, LASPJ_KIND_GSET, -1, dooff, ctx->flag,
+                                         nullptr))
+                return s;
+            if (int s = etf_write_enqueue(ctx, &vb, S->etf, LASPJ_KIND_GSET, -1, 1, dooff, dopay,
+                                          ocap, nullptr))
+                return s;
+            break;
+        }
+        case Op::EQUAL:
+            // equal/2 (lasp_orset.erl:136-138): ORDictA == ORDictB
+            LJ_HIP(ctx, launch_equal(ctx, &lhs, &rhs, dout + o_res));
+            break;
+        case Op::INFLATION:
+            // is_inflation / is_strict_inflation (lasp_lattice.erl:153-161, 235-253)
+            LJ_HIP(ctx, launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, dout + o_res));
+            break;
+        }
+        const uint64_t first = o_pay + (has_payload_out ? std::min(ocap, bound) : 0);
+        LJ_HIP(ctx, hipMemcpyAsync(S->hout, dout, first, hipMemcpyDeviceToHost, ctx->stream));
+        LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        ++S->stats[1];
+        const uint8_t* hout = static_cast<const uint8_t*>(S->hout);
+        c.st.assign(m, 0);
+        if (dec) std::memcpy(c.st.data(), hout + o_st, 4ull * m);
+        else c.st = hst;
+        c.res.assign(hout + o_res, hout + o_res + n);
+        if (has_payload_out) {
+            c.ooff.resize(n + 1ull);
+            std::memcpy(c.ooff.data(), hout + o_ooff, 8ull * (n + 1));
+            const uint64_t total = c.ooff[n];
+            if (total > ocap) {
+                // the writer wrote nothing: a larger answer area, the encode again (the
+                // cells are still in place)
+                S->ocap = al(total + total / 4, 1 << 16);
+                return -1000;            // caller re-runs the pass (rare)
+            }
+            if (total > first - o_pay) {
+                LJ_HIP(ctx, hipMemcpyAsync(static_cast<uint8_t*>(S->hout) + first, dout + first,
+                                           o_pay + total - first, hipMemcpyDeviceToHost,
+                                           ctx->stream));
+                LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            }
+            c.obase = hout + o_pay;
+        }
+    }
+    return LASPJ_OK;
+}
+
+int register_payloads(laspj_ctx* ctx, NifState* S, const std::vector<const uint8_t*>& p,
+                      const std::vector<uint64_t>& len, std::vector<int32_t>* st) {
+    const uint64_t k = p.size();
+    std::vector<uint64_t> offs(k + 1, 0);
+    for (uint64_t i = 0; i < k; ++i) offs[i + 1] = offs[i] + len[i];
+    std::vector<uint8_t> blob(offs[k] + 1);
+    for (uint64_t i = 0; i < k; ++i)
+        if (len[i]) std::memcpy(blob.data() + offs[i], p[i], len[i]);
+    st->assign(k, 0);
+    if (int s = laspj_dict_add(S->dict, LASPJ_KIND_ORSET, blob.data(), offs.data(), k, -1,
+                               st->data()))
+        return fail(ctx, s, "nif: dictionary registration failed (%d)", s);
+    ++S->stats[2];
+    S->stale = true;
+    return LASPJ_OK;
+}
+
+// The call: device pass; operands with unknown terms registered and a second pass; every
+// other undecodable operand -> FALLBACK.  verdict[j] per answer.
+int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
+    ++S->stats[0];
+    if (!S->dict && reset_dict(ctx, S)) return LASPJ_E_NOMEM;
+    const uint32_t n = c.n, m = c.m;
+    auto answer_of = [&](uint32_t i) { return i % n; };
+    std::vector<uint8_t> fallback(n, 0);
+    bool registered = false;
+    for (int pass = 0; pass < 4; ++pass) {
+        if (!S->etf || S->stale) {
+            if (!S->etf) {
+                // nothing registered yet: register this call's operands first
+                std::vector<int32_t> rst;
+                if (int s = register_payloads(ctx, S, c.p, c.len, &rst)) return s;
+                registered = true;
+                for (uint32_t i = 0; i < m; ++i)
+                    if (rst[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+            }
+            if (int s = rebuild_etf(ctx, S)) return s;
+        }
+        int s = device_pass(ctx, S, c);
+        if (s == -1000) continue;                // answer area grown: once more
+        if (s) return s;
+        std::vector<uint32_t> unknown;
+        for (uint32_t i = 0; i < m; ++i) {
+            if (fallback[answer_of(i)]) continue;
+            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && !registered) unknown.push_back(i);
+            else if (c.st[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+        }
+        if (unknown.empty()) break;
+        // terms the dictionary has not seen (or operands that are not orddicts, which the
+        // second pass tells apart): register the operands of every answer concerned
+        std::vector<uint8_t> want(n, 0);
+        for (uint32_t i : unknown) want[answer_of(i)] = 1;
+        std::vector<const uint8_t*> rp;
+        std::vector<uint64_t> rl;
+        std::vector<uint32_t> ri;
+        for (uint32_t i = 0; i < m; ++i)
+            if (want[answer_of(i)]) {
+                rp.push_back(c.p[i]);
+                rl.push_back(c.len[i]);
+                ri.push_back(i);
+            }
+        uint32_t nd = 0;
+        uint64_t eb, tb;
+        laspj_dict_info(S->dict, &nd, &eb, &tb);
+        std::vector<int32_t> rst;
+        if (int s2 = register_payloads(ctx, S, rp, rl, &rst)) return s2;
+        bool full = false;
+        for (int32_t x : rst) full |= x == LASPJ_DEC_UNREPRESENTABLE;
+        laspj_dict_info(S->dict, &nd, &eb, &tb);
+        if ((full && nd) || nd > kMaxDictElements) {
+            // an element's 64 token slots used up by earlier calls (or a dictionary grown
+            // past its bound): start a fresh dictionary holding this call's terms only —
+            // calls are self-contained (images in, images out), so nothing else refers to
+            // the old slots
+            if (int s2 = reset_dict(ctx, S)) return s2;
+            if (int s2 = register_payloads(ctx, S, c.p, c.len, &rst)) return s2;
+            for (uint32_t i = 0; i < m; ++i)
+                if (rst[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+        } else {
+            for (size_t k = 0; k < ri.size(); ++k)
+                if (rst[k] != LASPJ_DEC_OK) fallback[answer_of(ri[k])] = 1;
+        }
+        registered = true;
+    }
+    verdict->assign(n, LASPJ_NIF_OK);
+    for (uint32_t j = 0; j < n; ++j)
+        if (fallback[j]) {
+            (*verdict)[j] = LASPJ_NIF_FALLBACK;
+            ++S->stats[6];
+        }
+    return LASPJ_OK;
+}
+
+NifState* state(laspj_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->nif) ctx->nif = new (std::nothrow) NifState;
+    return ctx->nif;
+}
+
+}  // namespace
+
+void nif_destroy(laspj_ctx* ctx) {
+    NifState* S = ctx->nif;
+    if (!S) return;
+    if (S->etf) laspj_etf_dict_destroy(S->etf);
+    if (S->dict) laspj_dict_destroy(S->dict);
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    if (S->dblk) hipFree(S->dblk);
+    if (S->dcells) hipFree(S->dcells);
+    if (S->hin) hipHostFree(S->hin);
+    if (S->hout) hipHostFree(S->hout);
+    delete S;
+    ctx->nif = nullptr;
+}
+
+}  // namespace laspj
+
+using laspj::fail;
+
+namespace {
+
+int pair_call(laspj_ctx* ctx, laspj::NifState* S, laspj::Op op, int strict, uint32_t n,
+              const uint8_t* const* a, const uint64_t* na, const uint8_t* const* b,
+              const uint64_t* nb, laspj::Call* c, std::vector<int32_t>* verdict) {
+    if (!n || !a || !na || (op != laspj::Op::VALUE && (!b || !nb)))
+        return fail(ctx, LASPJ_E_INVAL, "nif: null operand array");
+    const uint32_t per = op == laspj::Op::VALUE ? 1u : 2u;
+    if ((uint64_t)n * per > (1ull << 31))
+        return fail(ctx, LASPJ_E_RANGE, "nif: too many operands");
+    c->op = op;
+    c->strict = strict;
+    c->n = n;
+    c->m = n * per;
+    c->p.resize(c->m);
+    c->len.resize(c->m);
+    for (uint32_t i = 0; i < n; ++i) {
+        if ((!a[i] && na[i]) || (per == 2 && !b[i] && nb[i]))
+            return fail(ctx, LASPJ_E_INVAL, "nif: null payload");
+        c->p[i] = a[i];
+        c->len[i] = na[i];
+        if (per == 2) {
+            c->p[n + i] = b[i];
+            c->len[n + i] = nb[i];
+        }
+    }
+    return laspj::run(ctx, S, *c, verdict);
+}
+
+}  // namespace
+
+extern "C" {
+
+int laspj_orset_etf_merge_many(laspj_ctx* ctx, uint32_t n, const uint8_t* const* a,
+                               const uint64_t* na, const uint8_t* const* b, const uint64_t* nb,
+                               const uint8_t** out, uint64_t* out_len, int32_t* verdict) {
+    if (!ctx) return LASPJ_E_INVAL;
+    if (!out || !out_len || !verdict) return fail(ctx, LASPJ_E_INVAL, "nif: null output array");
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    std::lock_guard<std::mutex> lk(S->mu);
+    laspj::Call c;
+    std::vector<int32_t> v;
+    if (int s = pair_call(ctx, S, laspj::Op::MERGE, 0, n, a, na, b, nb, &c, &v)) return s;
+    for (uint32_t i = 0; i < n; ++i) {
+        verdict[i] = v[i];
+        out[i] = v[i] == LASPJ_NIF_OK ? c.obase + c.ooff[i] : nullptr;
+        out_len[i] = v[i] == LASPJ_NIF_OK ? c.ooff[i + 1] - c.ooff[i] : 0;
+    }
+    return LASPJ_OK;
+}
+
+int laspj_orset_etf_merge(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                          uint64_t nb, const uint8_t** out, uint64_t* out_len, int32_t* verdict) {
+    return laspj_orset_etf_merge_many(ctx, 1, &a, &na, &b, &nb, out, out_len, verdict);
+}
+
+int laspj_orset_etf_value(laspj_ctx* ctx, const uint8_t* s, uint64_t ns, const uint8_t** out,
+                          uint64_t* out_len, int32_t* verdict) {
+    if (!ctx) return LASPJ_E_INVAL;
+    if (!out || !out_len || !verdict) return fail(ctx, LASPJ_E_INVAL, "nif: null output");
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    std::lock_guard<std::mutex> lk(S->mu);
+    laspj::Call c;
+    std::vector<int32_t> v;
+    if (int st = pair_call(ctx, S, laspj::Op::VALUE, 0, 1, &s, &ns, nullptr, nullptr, &c, &v))
+        return st;
+    *verdict = v[0];
+    *out = v[0] == LASPJ_NIF_OK ? c.obase + c.ooff[0] : nullptr;
+    *out_len = v[0] == LASPJ_NIF_OK ? c.ooff[1] - c.ooff[0] : 0;
+    return LASPJ_OK;
+}
+
+static int bool_call(laspj_ctx* ctx, laspj::Op op, int strict, const uint8_t* a, uint64_t na,
+                     const uint8_t* b, uint64_t nb, int32_t* result, int32_t* verdict) {
+    if (!ctx) return LASPJ_E_INVAL;
+    if (!result || !verdict) return fail(ctx, LASPJ_E_INVAL, "nif: null output");
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    std::lock_guard<std::mutex> lk(S->mu);
+    laspj::Call c;
+    std::vector<int32_t> v;
+    if (int s = pair_call(ctx, S, op, strict, 1, &a, &na, &b, &nb, &c, &v)) return s;
+    *verdict = v[0];
+    *result = v[0] == LASPJ_NIF_OK ? (int32_t)(c.res[0] != 0) : 0;
+    return LASPJ_OK;
+}
+
+int laspj_orset_etf_equal(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                          uint64_t nb, int32_t* result, int32_t* verdict) {
+    return bool_call(ctx, laspj::Op::EQUAL, 0, a, na, b, nb, result, verdict);
+}
+
+int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
+                              const uint8_t* cur, uint64_t nc, int strict, int32_t* result,
+                              int32_t* verdict) {
+    return bool_call(ctx, laspj::Op::INFLATION, strict ? 1 : 0, prev, np, cur, nc, result,
+                     verdict);
+}
+
+int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n) {
+    if (!ctx || (n && !out)) return LASPJ_E_INVAL;
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    std::lock_guard<std::mutex> lk(S->mu);
+    for (uint32_t i = 0; i < n && i < LASPJ_NIF_STATS; ++i) out[i] = S->stats[i];
+    if (n > 7) {
+        uint32_t e = 0;
+        uint64_t eb, tb;
+        out[7] = S->dict && laspj_dict_info(S->dict, &e, &eb, &tb) == LASPJ_OK ? e : 0;
+    }
+    return LASPJ_OK;
+}
+
+int laspj_nif_reset(laspj_ctx* ctx) {
+    if (!ctx) return LASPJ_E_INVAL;
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    std::lock_guard<std::mutex> lk(S->mu);
+    return laspj::reset_dict(ctx, S);
+}
+
+}  // extern "C"

@@ -104,6 +104,64 @@ class Context:
               self.h)
         return st.download(np.uint8)
 
+    # ------------------------------------------------------------ NIF entry points
+    # laspj.h "NIF entry points": term_to_binary images in, images / booleans out, over
+    # this context's own dictionary.  Each returns (verdict, answer); answer is None on
+    # NIF_FALLBACK (the NIF would run the reference's Erlang clause).
+
+    def nif_merge_many(self, pairs):
+        """lasp_orset:merge/2 over many (A, B) image pairs: [(verdict, image)]."""
+        n = len(pairs)
+        if n == 0:
+            return []
+        keep = [(bytes(a), bytes(b)) for a, b in pairs]
+        pa = (C.c_char_p * n)(*[a for a, _ in keep])
+        pb = (C.c_char_p * n)(*[b for _, b in keep])
+        na = (C.c_uint64 * n)(*[len(a) for a, _ in keep])
+        nb = (C.c_uint64 * n)(*[len(b) for _, b in keep])
+        out = (C.c_void_p * n)()
+        olen = (C.c_uint64 * n)()
+        verd = (C.c_int32 * n)()
+        check(self.L.laspj_orset_etf_merge_many(self.h, n, pa, na, pb, nb, out, olen, verd),
+              self.h)
+        return [(int(verd[k]), C.string_at(out[k], olen[k]) if verd[k] == 0 else None)
+                for k in range(n)]
+
+    def nif_merge(self, a: bytes, b: bytes):
+        return self.nif_merge_many([(a, b)])[0]
+
+    def nif_value(self, s: bytes):
+        out, olen, verd = C.c_void_p(), C.c_uint64(), C.c_int32()
+        s = bytes(s)
+        check(self.L.laspj_orset_etf_value(self.h, s, len(s), C.byref(out), C.byref(olen),
+                                           C.byref(verd)), self.h)
+        return int(verd.value), (C.string_at(out, olen.value) if verd.value == 0 else None)
+
+    def nif_equal(self, a: bytes, b: bytes):
+        res, verd = C.c_int32(), C.c_int32()
+        a, b = bytes(a), bytes(b)
+        check(self.L.laspj_orset_etf_equal(self.h, a, len(a), b, len(b), C.byref(res),
+                                           C.byref(verd)), self.h)
+        return int(verd.value), (bool(res.value) if verd.value == 0 else None)
+
+    def nif_inflation(self, prev: bytes, cur: bytes, strict: bool = False):
+        res, verd = C.c_int32(), C.c_int32()
+        prev, cur = bytes(prev), bytes(cur)
+        check(self.L.laspj_orset_etf_inflation(self.h, prev, len(prev), cur, len(cur),
+                                               int(strict), C.byref(res), C.byref(verd)),
+              self.h)
+        return int(verd.value), (bool(res.value) if verd.value == 0 else None)
+
+    def nif_stats(self) -> dict:
+        out = (C.c_uint64 * 8)()
+        check(self.L.laspj_nif_stats(self.h, out, 8), self.h)
+        keys = ("calls", "device_passes", "registrations", "dict_resets", "image_rebuilds",
+                "host_encoded_passes", "fallbacks", "dict_elements")
+        return dict(zip(keys, (int(x) for x in out)))
+
+    def nif_reset(self):
+        check(self.L.laspj_nif_reset(self.h), self.h)
+
     def inflation_many(self, prevs, curs, strict: bool) -> np.ndarray:
         """laspj_batch_inflation_many: is_(strict_)inflation(prev[i], cur[i])."""
         n = len(curs)

@@ -244,6 +244,17 @@ def bench_config1_ext(n: int = 10_000, iters: int = 200, slow_iters: int = 5):
     return tuple(out)
 
 
+def bench_config1_merge_threads(n: int, threads: int, budget_s: float) -> float:
+    """BASELINE config 1's merge on `threads` host threads at once: wall microseconds per
+    merge over all threads (the node-wide rate the batched NIF merges are set against)."""
+    out = C.c_double()
+    f = lib().orc_bench_config1_merge_threads
+    f.argtypes = [C.c_uint32, C.c_int, C.c_double, C.POINTER(C.c_double)]
+    if f(n, threads, budget_s, C.byref(out)) != 0:
+        raise RuntimeError("orc_bench_config1_merge_threads failed")
+    return out.value
+
+
 def bench_cells_join(cells_per_thread: int, threads: int, budget_s: float) -> float:
     """The device's cell layout joined (d = a | b) on host threads: cells per second
     (a second CPU column for the headline; the reference's algorithm is bench_orset_merge)."""

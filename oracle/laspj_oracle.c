@@ -694,3 +694,80 @@ int orc_bench_cells_join(uint64_t cells_per_thread, int threads, double budget_s
     *cells_per_s = cells / secs;
     return 0;
 }
+
+/* BASELINE config 1's merge on many host threads: every thread builds the pair of
+ * orc_bench_config1_ext (n elements, one token each side) and merges it for budget_s;
+ * *us = wall seconds / merges done by all threads, in microseconds — the per-merge cost
+ * of a node whose schedulers all merge, next to the device's batched NIF merges. */
+typedef struct {
+    uint32_t n;
+    double budget_s, seconds;
+    u64 merges;
+    int err;
+} c1_arg;
+
+static void* c1_thread(void* p) {
+    c1_arg* a = (c1_arg*)p;
+    const uint32_t n = a->n, E = 2 * n;
+    orc_orset *x = orc_orset_alloc(E, E), *y = orc_orset_alloc(E, E);
+    orc_orset* m = orc_orset_alloc(2 * E, 2 * E);
+    if (!x || !y || !m) {
+        a->err = 1;
+        return NULL;
+    }
+    u64 s = 0x4C415350ull;
+    for (uint32_t e = 0; e < n; ++e) {
+        orc_elem* ea = &x->elems[x->nelem++];
+        orc_elem* eb = &y->elems[y->nelem++];
+        ea->key = eb->key = e;
+        ea->off = x->ntok;
+        eb->off = y->ntok;
+        ea->n = eb->n = 1;
+        orc_tok* ta = &x->toks[x->ntok++];
+        orc_tok* tb = &y->toks[y->ntok++];
+        for (int k = 0; k < 20; k += 8) {
+            s = sm64(s);
+            memcpy(ta->tok + k, &s, k + 8 <= 20 ? 8 : 20 - k);
+            s = sm64(s);
+            memcpy(tb->tok + k, &s, k + 8 <= 20 ? 8 : 20 - k);
+        }
+        ta->removed = 0;
+        tb->removed = (uint8_t)(sm64(e ^ 1ull) % 10 == 0);
+    }
+    const double t0 = now_s();
+    double t = t0;
+    u64 k = 0;
+    while (t - t0 < a->budget_s) {
+        for (int i = 0; i < 16; ++i) orc_orset_merge(x, y, m);
+        k += 16;
+        t = now_s();
+    }
+    a->merges = k;
+    a->seconds = t - t0;
+    orc_orset_free(x), orc_orset_free(y), orc_orset_free(m);
+    return NULL;
+}
+
+int orc_bench_config1_merge_threads(uint32_t n, int threads, double budget_s, double* us) {
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    c1_arg* args = (c1_arg*)calloc((size_t)threads, sizeof(c1_arg));
+    if (!th || !args) return -1;
+    for (int i = 0; i < threads; ++i) {
+        args[i] = (c1_arg){n, budget_s, 0, 0, 0};
+        pthread_create(&th[i], NULL, c1_thread, &args[i]);
+    }
+    double secs = 0;
+    u64 merges = 0;
+    int err = 0;
+    for (int i = 0; i < threads; ++i) {
+        pthread_join(th[i], NULL);
+        merges += args[i].merges;
+        if (args[i].seconds > secs) secs = args[i].seconds;
+        err |= args[i].err;
+    }
+    free(th);
+    free(args);
+    if (err || !merges) return -1;
+    *us = secs * 1e6 / (double)merges;
+    return 0;
+}
