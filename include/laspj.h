@@ -159,6 +159,8 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a
                                         multiple of 256)                               */
+#define LASPJ_TUNE_LIST_WALK    10   /* list merges whose keys descend somewhere: 0 = the
+                                        run-jumping walk, 1 = one step per element      */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -38,6 +38,7 @@ TUNE_PRODUCT_ROWS = 6
 TUNE_PRODUCT_COLS = 7
 TUNE_ETF_READ = 8
 TUNE_ETF_SEG = 9
+TUNE_LIST_WALK = 10
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
 NIF_STATS = 8
 

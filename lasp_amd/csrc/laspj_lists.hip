@@ -204,7 +204,7 @@ __device__ uint32_t inner_merge(const u64* ta, uint32_t la, const u64* tb, uint3
 // smaller head of the second argument makes it switch; a smaller head of the first
 // keeps it), so the item of a pair is the side of the last single step before it (A
 // at the start) — carried across threads and tiles by "last non-none" scans.
-// Replicas whose ranks descend anywhere take the lane-0 walk (k_merge_serial).
+// Replicas whose ranks descend anywhere take a one-wave walk (k_merge_runs).
 // Token runs of the planned entries (inner orddict:merge with `or`, or a copy) are then
 // counted, scanned and written one entry per thread over the whole grid.
 
@@ -559,6 +559,144 @@ __global__ __launch_bounds__(64) void k_merge_serial(LV a, LV b, MS m, uint64_t 
             P.o += ny;
         }
         if (lane_id() == 0) m.nout[r] = P.o;
+    }
+}
+
+// Run-jumping walk (round 4) for replicas whose ranks descend somewhere.  Every clause
+// emits the smaller head, or both heads on a tie (ordsets:union's switch only decides
+// which side a tie's item comes from: the side of the last single step, see above), and
+// step kinds come in runs: A's head while A[i] < B[j] (B's head fixed), B's while
+// B[j] < A[i], ties while A[i+k] == B[j+k].  The wave holds each side's next 256 ranks
+// in registers (a window based at its cursor, position base + 64 t + lane in v[t]) and
+// finds how far the current run extends with four ballots; a run that reaches the
+// window's end continues as a streaming scan over the precomputed ranks (1024 per wave
+// iteration, coalesced).  The run's plan entries are index ranges, written
+// lane-parallel.  So the reversed re-bind (one tie run, then one side's rest) costs
+// ~n/1024 iterations where the step walk took n dependent steps, and an interleaving of
+// short runs still costs one step per run.
+struct Win256 {
+    const u64* src;
+    uint32_t n, base;
+    u64 v[4];
+    __device__ void load(uint32_t at) {
+        base = at;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t k = at + 64u * t + lane_id();
+            v[t] = k < n ? src[k] : ~0ull;
+        }
+    }
+    // rank at position p, base <= p < base + 256 (wave-uniform)
+    __device__ u64 at(uint32_t p) const {
+        const uint32_t q = p - base, t = q >> 6;
+        return rd64(t == 0 ? v[0] : t == 1 ? v[1] : t == 2 ? v[2] : v[3], q & 63u);
+    }
+};
+
+// first failing position at or after window offset s: kind 0 = tie (A.v == B.v, windows
+// aligned), 1 = A.v < y, 2 = B.v < y; 256 when none in the window (positions >= n fail)
+template <int KIND>
+__device__ __forceinline__ uint32_t win_fail(const Win256& A, const Win256& B, uint32_t s, u64 y) {
+    const Win256& W = KIND == 2 ? B : A;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+        const uint32_t q = 64u * t + lane_id();
+        bool ok;
+        if (KIND == 0) ok = W.base + q < W.n && B.base + q < B.n && A.v[t] == B.v[t];
+        else ok = W.base + q < W.n && W.v[t] < y;
+        const u64 f = __ballot(q >= s && !ok);
+        if (f) return 64u * t + (uint32_t)__ffsll((long long)f) - 1u;
+    }
+    return 256u;
+}
+
+// the run's length from positions p (and q for ties) onwards over global ranks, to the
+// first failure or the end of a side
+template <int KIND>
+__device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64* Y, uint32_t ny,
+                               uint32_t q, u64 y) {
+    uint32_t L = 0;
+    for (;;) {
+        u64 vx[16], vy[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t k = L + 64u * t + lane_id();
+            vx[t] = p + k < nx ? X[p + k] : ~0ull;
+            if (KIND == 0) vy[t] = q + k < ny ? Y[q + k] : ~0ull;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t k = L + 64u * t + lane_id();
+            const bool ok = KIND == 0 ? (p + k < nx && q + k < ny && vx[t] == vy[t])
+                                      : (p + k < nx && vx[t] < y);
+            const u64 f = __ballot(!ok);
+            if (f) return L + 64u * t + (uint32_t)__ffsll((long long)f) - 1u;
+        }
+        L += 1024;
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_merge_runs(LV a, LV b, MS m, uint64_t R) {
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
+        if (!m.unsorted[r]) continue;
+        const uint32_t na = a.n(r), nb = b.n(r);
+        const u64* SA = m.sa + r * m.ce_a;
+        const u64* SB = m.sb + r * m.ce_b;
+        Win256 A{SA, na, 0, {}}, B{SB, nb, 0, {}};
+        A.load(0);
+        B.load(0);
+        u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
+        uint32_t i = 0, j = 0, o = 0, sx = 0;        // sx: the last single step was B's
+        while (i < na && j < nb) {
+            if (i - A.base >= 192u) A.load(i);
+            if (j - B.base >= 192u) B.load(j);
+            const u64 x = A.at(i), y = B.at(j);
+            uint32_t L;
+            if (x == y) {
+                if (i - A.base != j - B.base) {
+                    A.load(i);
+                    B.load(j);
+                }
+                const uint32_t s = i - A.base;
+                L = win_fail<0>(A, B, s, 0) - s;
+                if (L == 256u - s) L += stream_run<0>(SA, na, i + L, SB, nb, j + L, 0);
+                // merge(F, [{K1,V1}|D1], [{_,V2}|D2]) -> [{K1, F(K1,V1,V2)} | ...];
+                // union: the item of the walk's first argument
+                for (uint32_t k = lane_id(); k < L; k += 64)
+                    plan[o + k] = MODE == 2 ? (sx ? (u64)(j + k) | (1ull << 32) : (u64)(i + k))
+                                            : (u64)(i + k) | ((u64)(j + k) << 32);
+                i += L, j += L;
+            } else if (x < y) {
+                const uint32_t s = i - A.base;
+                L = win_fail<1>(A, B, s, y) - s;
+                if (L == 256u - s) L += stream_run<1>(SA, na, i + L, nullptr, 0, 0, y);
+                for (uint32_t k = lane_id(); k < L; k += 64)
+                    plan[o + k] = MODE == 2 ? (u64)(i + k) : (u64)(i + k) | ((u64)kNone << 32);
+                i += L;
+                sx = 0;
+            } else {
+                const uint32_t s = j - B.base;
+                L = win_fail<2>(A, B, s, x) - s;
+                if (L == 256u - s) L += stream_run<1>(SB, nb, j + L, nullptr, 0, 0, x);
+                for (uint32_t k = lane_id(); k < L; k += 64)
+                    plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
+                                            : (u64)kNone | ((u64)(j + k) << 32);
+                j += L;
+                sx = 1;
+            }
+            o += L;
+        }
+        // the rest of the side left over (merge(F,[],D2) -> D2; merge(F,D1,[]) -> D1;
+        // the union's tails as they are), tagged with its side
+        for (uint32_t k = lane_id(); k < na - i; k += 64)
+            plan[o + k] = MODE == 2 ? (u64)(i + k) : (u64)(i + k) | ((u64)kNone << 32);
+        o += na - i;
+        for (uint32_t k = lane_id(); k < nb - j; k += 64)
+            plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
+                                    : (u64)kNone | ((u64)(j + k) << 32);
+        o += nb - j;
+        if (lane_id() == 0) m.nout[r] = o;
     }
 }
 
@@ -1613,7 +1751,10 @@ static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                            dim3(kMT), 0, ctx->stream, A, B, m, R);
         hipLaunchKernelGGL((k_merge_tile_scan<MODE>), dim3(rx), dim3(kMT), 0, ctx->stream, A, B,
                            m, R);
-        hipLaunchKernelGGL((k_merge_serial<MODE>), dim3(rx), dim3(64), 0, ctx->stream, A, B, m, R);
+        // keys that descend somewhere: the run-jumping walk (LASPJ_TUNE_LIST_WALK 1: the
+        // step-by-step walk it replaced)
+        hipLaunchKernelGGL(ctx->tune_list_walk == 1 ? k_merge_serial<MODE> : k_merge_runs<MODE>,
+                           dim3(rx), dim3(64), 0, ctx->stream, A, B, m, R);
         hipLaunchKernelGGL((k_merge_tiles<MODE, true>), dim3(m.ntiles ? m.ntiles : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, m, R);
         hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),

@@ -342,6 +342,10 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
                             "multiple of 256");
             ctx->tune_etf_seg = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_LIST_WALK:
+            if (value < 0 || value > 1) return fail(ctx, LASPJ_E_INVAL, "tuning: list walk 0 or 1");
+            ctx->tune_list_walk = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

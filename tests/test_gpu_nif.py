@@ -45,7 +45,7 @@ def _orset(rng, elems, pool, p=0.7, pflag=0.3, tmax=None):
         if rng.random() < p:
             ts = pool[e]
             k = rng.randint(1, min(len(ts), tmax or len(ts)))
-            toks = sorted(rng.sample(ts, k))
+            toks = sorted(rng.sample(ts, k), key=_key)
             s.append((e, [(t, rng.random() < pflag) for t in toks]))
     return s
 

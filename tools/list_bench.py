@@ -115,6 +115,8 @@ def bench_pair(ctx, order, old, new, it=20, R=1):
 
 def main():
     ctx = engine.Context(0)
+    if os.environ.get("LASPJ_LIST_WALK"):          # 1: the step-by-step walk (A/B)
+        ctx.set_tuning(_lib.TUNE_LIST_WALK, int(os.environ["LASPJ_LIST_WALK"]))
     res = {}
     rng = np.random.default_rng(5)
     # config 5 intersection output: L = [0, 100k), R = [50k, 150k) -> common [50k, 100k)
@@ -138,6 +140,18 @@ def main():
                      np.concatenate([l[2][l[1][i]:l[1][i + 1]] for i in range(len(l[0]))][::-1]))
     res["config5_intersection_rebind_50k_unsorted_walk"], _ = bench_pair(
         ctx, order, [rev(old)], [rev(new)], it=5)
+    print(json.dumps(res), flush=True)
+    # the same entries in a random order shared by both sides (a hash-like map fun: all
+    # ties again), and each side in its own random order (short runs everywhere)
+    def perm(l, p):
+        runs = [l[2][l[1][i]:l[1][i + 1]] for i in range(len(l[0]))]
+        return (l[0][p].copy(), np.concatenate([[0], np.cumsum([len(runs[i]) for i in p])]).astype(np.uint32),
+                np.concatenate([runs[i] for i in p]))
+    p1, p2 = rng.permutation(len(common)), rng.permutation(len(common))
+    res["config5_intersection_rebind_50k_shuffled_same"], _ = bench_pair(
+        ctx, order, [perm(old, p1)], [perm(new, p1)], it=5)
+    res["config5_intersection_rebind_50k_shuffled_each"], _ = bench_pair(
+        ctx, order, [perm(old, p1)], [perm(new, p2)], it=3)
     print(json.dumps(res), flush=True)
     # product output 256 x 256
     nx = ny = 256
