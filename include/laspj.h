@@ -663,10 +663,11 @@ int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
  * status[i] = 0 when cur[i] =:= val[i] (the no-op of :294-296); else dst[i] :=
  * Type:merge(cur[i], val[i]) (as laspj_list_merge) and status[i] = 1 when
  * is_inflation(cur[i], dst[i]) (:301, the bind writes dst[i]) or 2 when not (no write).
- * status is host memory, R bytes.  Two synchronisations (sizes with the equalities,
- * then the inflations with the error flag) instead of the separate calls' six; when
- * every replica is equal, dst is left as it was.  On an error status, status[] and
- * dst hold no result. */
+ * status is host memory, R bytes.  One synchronisation (the equalities, the merge sized
+ * from the inputs' counts, the inflations, then sizes, bytes and the error flag read
+ * together) instead of the separate calls' six; dst holds the merge for every replica
+ * (what the bind writes where status is 1).  On an error status, status[] and dst hold
+ * no result. */
 int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
                     const laspj_batch* val, const laspj_list_order* ord, uint8_t* status);
 /* value/1 of OR-Set lists (lasp_orset.erl:67-73): the keys of entries with a {_, false}

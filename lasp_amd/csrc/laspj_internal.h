@@ -78,6 +78,11 @@ struct laspj_batch {
     // LASPJ_KIND_*_LIST: entry / token capacity per replica (laspj_lists.hip)
     uint32_t cap_e = 0;
     uint32_t cap_t = 0;
+    // list batches: every replica holds at most known_e entries and known_t tokens (kept
+    // on the host by the operations that write lists, so a merge can size its output
+    // without reading the inputs' counts back)
+    uint32_t known_e = 0;
+    uint32_t known_t = 0;
 };
 
 inline bool laspj_is_list(int32_t kind) {

@@ -1373,7 +1373,9 @@ LV view(const laspj_batch* b) {
 }
 
 // (re)allocate a list batch's device memory for caps (ce, ct); contents: empty lists
-int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
+// zero: clear the new block (empty lists); otherwise its contents are undefined until the
+// caller's write pass (known counts = the capacities until then)
+int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct, bool zero = true) {
     if (ce == 0) ce = 1;
     if (ct == 0) ct = 1;
     const uint64_t wpr = list_wpr(ce, ct);
@@ -1387,7 +1389,7 @@ int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
         return fail(ctx, LASPJ_E_NOMEM, "list: hipMalloc(%llu): %s", (unsigned long long)bytes,
                     hipGetErrorString(e));
     }
-    e = hipMemsetAsync(p, 0, bytes, ctx->stream);
+    if (zero) e = hipMemsetAsync(p, 0, bytes, ctx->stream);
     if (e != hipSuccess) {
         laspj::dev_release(ctx, p, bytes);
         return fail(ctx, LASPJ_E_DEVICE, "list: memset: %s", hipGetErrorString(e));
@@ -1396,6 +1398,8 @@ int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct) {
     b->dev = static_cast<uint64_t*>(p);
     b->cap_e = ce;
     b->cap_t = ct;
+    b->known_e = zero ? 0 : ce;
+    b->known_t = zero ? 0 : ct;
     b->words_per_replica = wpr;
     b->elements = ce;
     b->cells = ce;
@@ -1474,34 +1478,18 @@ int read_flag(laspj_ctx* ctx, const char* what) {
     return flag_status(ctx, f, what);
 }
 
-// What laspj_list_bind adds to a merge: the equality bytes of the inputs (computed
-// before the size pass, read back with the sizes into `eq_host`), the write pass
-// skipped when every replica is equal, and no flag read after the write pass (the
-// caller reads it with the inflation bytes).
-struct BindX {
-    uint8_t* eq_dev;      // R bytes: cur =:= val
-    uint8_t* eq_host;     // R bytes
-    bool skipped;         // out: every replica equal, dst untouched
-};
-
 // run a size pass, size dst from the per-replica maxima, then the write pass
 template <class SizeFn, class WriteFn>
 int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, WriteFn write_pass,
-          const char* what, BindX* bx = nullptr) {
+          const char* what) {
     const uint64_t R = dst->replicas;
     size_pass();
     LJ_LAUNCHED(ctx);
     std::vector<uint32_t> h(2 * R);
     uint32_t f = 0;
-    const laspj::ReadPiece rp[3] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4},
-                                    {bx ? bx->eq_host : nullptr, bx ? bx->eq_dev : nullptr, R}};
-    LJ_HIP(ctx, laspj::readback(ctx, rp, bx ? 3 : 2));
+    const laspj::ReadPiece rp[2] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
+    LJ_HIP(ctx, laspj::readback(ctx, rp, 2));
     if (int s = flag_status(ctx, f, what)) return s;
-    if (bx) {
-        bx->skipped = true;
-        for (uint64_t i = 0; i < R && bx->skipped; ++i) bx->skipped = bx->eq_host[i] != 0;
-        if (bx->skipped) return LASPJ_OK;
-    }
     uint32_t ce = 0, ct = 0;
     for (uint64_t i = 0; i < R; ++i) {
         ce = h[2 * i] > ce ? h[2 * i] : ce;
@@ -1513,7 +1501,9 @@ int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, Wr
             return s;
     write_pass(view(dst));
     LJ_LAUNCHED(ctx);
-    return bx ? LASPJ_OK : read_flag(ctx, what);
+    dst->known_e = ce;
+    dst->known_t = ct;
+    return read_flag(ctx, what);
 }
 
 // a tiled producer (k_tp_*): `pre` carves its own scratch from the front of the block
@@ -1607,6 +1597,13 @@ int laspj_list_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t replica, uint32_t
         if (int s = list_alloc(ctx, b, n > b->cap_e ? n : b->cap_e, nt > b->cap_t ? nt : b->cap_t))
             return s;
     }
+    if (b->replicas == 1) {
+        b->known_e = n;
+        b->known_t = nt;
+    } else {
+        b->known_e = n > b->known_e ? n : b->known_e;
+        b->known_t = nt > b->known_t ? nt : b->known_t;
+    }
     LV v = view(b);
     uint32_t hdr[2] = {n, nt};
     LJ_HIP(ctx, hipMemcpyAsync(v.hdr + 2 * replica, hdr, 8, hipMemcpyHostToDevice, ctx->stream));
@@ -1697,14 +1694,27 @@ static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch
     return LASPJ_OK;
 }
 
-// the merge proper, with the context's lock held and the arguments checked
-static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
-                     const laspj_batch* b, const RK& rk, bool keep_left, const char* what,
-                     BindX* bx) {
+// The merge proper, with the context's lock held and the arguments checked.  A merge has
+// at most the entries and the tokens of both inputs together, so dst is sized from the
+// inputs' known counts and the size pass and the write pass run back to back: the caller
+// synchronises once, reading `need` (per replica {entries, tokens}), the error flag and
+// whatever it enqueued after (the bind's equality and inflation bytes).  eq (R bytes, or
+// null): `cur =:= val` per replica, launched first.
+static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
+                         const laspj_batch* b, const RK& rk, bool keep_left, uint32_t* need,
+                         uint8_t* eq, const char* what) {
     const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
     const uint64_t R = a->replicas;
     const uint64_t ce = (uint64_t)a->cap_e + b->cap_e;
     if (ce > 0xFFFFFFF0ull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
+    const uint64_t be = (uint64_t)a->known_e + b->known_e;
+    const uint64_t bt = gs ? 1ull : (uint64_t)a->known_t + b->known_t;
+    if (be > 0xFFFFFFF0ull || bt > 0xFFFFFFF0ull)
+        return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
+    if (be > dst->cap_e || bt > dst->cap_t)
+        if (int s = list_alloc(ctx, dst, be > dst->cap_e ? (uint32_t)be : dst->cap_e,
+                               bt > dst->cap_t ? (uint32_t)bt : dst->cap_t, false))
+            return s;
     MS m;
     m.ce_a = a->cap_e;
     m.ce_b = b->cap_e;
@@ -1714,7 +1724,7 @@ static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
                    sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
                    sz_r = R * 4ull;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 2 * sz_t + sz_c + 4 * sz_r + 8ull * R + 64;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 2 * sz_t + sz_c + 4 * sz_r + 64;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -1733,16 +1743,15 @@ static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
     m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r));
-    auto* need = reinterpret_cast<uint32_t*>(take(8ull * R));
-    const LV A = view(a), B = view(b);
+    const LV A = view(a), B = view(b), OUT = view(dst);
     const unsigned ry = (unsigned)(R < 65535 ? R : 65535);
     const unsigned rx = (unsigned)(R < (1u << 20) ? R : (1u << 20));
     const uint32_t cmax = m.ce_a > m.ce_b ? m.ce_a : m.ce_b;
     const unsigned gr = cmax ? (cmax + kMT - 1) / kMT : 1u;
     LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
-    if (bx)
-        hipLaunchKernelGGL(k_list_equal, dim3(R), dim3(64), 0, ctx->stream, A, B, rk, bx->eq_dev);
-    auto size_pass = [&](auto mode) {
+    if (eq)
+        hipLaunchKernelGGL(k_list_equal, dim3(R), dim3(64), 0, ctx->stream, A, B, rk, eq);
+    auto passes = [&](auto mode) {
         constexpr int MODE = decltype(mode)::value;
         hipMemsetAsync(m.unsorted, 0, sz_r, ctx->stream);
         hipLaunchKernelGGL(k_merge_ranks, dim3(gr, ry), dim3(kMT), 0, ctx->stream, A, B,
@@ -1760,23 +1769,26 @@ static int merge_run(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, rk, m, R);
         hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R, need);
-    };
-    auto write_pass = [&](auto mode, LV out) {
-        constexpr int MODE = decltype(mode)::value;
+        // the write pass (it raises kErrRange rather than write past dst's capacity)
         hipLaunchKernelGGL((k_merge_write<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry), dim3(kMT),
-                           0, ctx->stream, A, B, out, rk, m, R);
+                           0, ctx->stream, A, B, OUT, rk, m, R);
     };
-    using M0 = std::integral_constant<int, 0>;
-    using M1 = std::integral_constant<int, 1>;
-    using M2 = std::integral_constant<int, 2>;
-    if (gs)
-        return sized(ctx, dst, need, [&] { size_pass(M2{}); },
-                     [&](LV out) { write_pass(M2{}, out); }, what, bx);
-    if (keep_left)
-        return sized(ctx, dst, need, [&] { size_pass(M1{}); },
-                     [&](LV out) { write_pass(M1{}, out); }, what, bx);
-    return sized(ctx, dst, need, [&] { size_pass(M0{}); },
-                 [&](LV out) { write_pass(M0{}, out); }, what, bx);
+    if (gs) passes(std::integral_constant<int, 2>{});
+    else if (keep_left) passes(std::integral_constant<int, 1>{});
+    else passes(std::integral_constant<int, 0>{});
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+// dst's known counts from the per-replica {entries, tokens} a merge read back
+static void set_known(laspj_batch* dst, const uint32_t* h, uint64_t R) {
+    uint32_t ce = 0, ct = 0;
+    for (uint64_t i = 0; i < R; ++i) {
+        ce = h[2 * i] > ce ? h[2 * i] : ce;
+        ct = h[2 * i + 1] > ct ? h[2 * i + 1] : ct;
+    }
+    dst->known_e = ce;
+    dst->known_t = ct;
 }
 
 static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
@@ -1786,7 +1798,30 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     RK rk;
     if (int s = ranks(ctx, ord, a->kind != LASPJ_KIND_GSET_LIST, &rk, what)) return s;
     LGuard g(ctx);
-    return merge_run(ctx, dst, a, b, rk, keep_left, what, nullptr);
+    const uint64_t R = a->replicas;
+    void* dev = nullptr;
+    if (laspj::dev_alloc(ctx, 8 * R, &dev) != hipSuccess) {
+        hipGetLastError();
+        return fail(ctx, LASPJ_E_NOMEM, "%s: sizes", what);
+    }
+    auto* need = static_cast<uint32_t*>(dev);
+    int s = merge_enqueue(ctx, dst, a, b, rk, keep_left, need, nullptr, what);
+    std::vector<uint32_t> h(2 * R);
+    if (s == LASPJ_OK) {
+        uint32_t f = 0;
+        const laspj::ReadPiece rp[2] = {{h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
+        const hipError_t e = laspj::readback(ctx, rp, 2);
+        s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "%s: readback: %s", what,
+                                   hipGetErrorString(e))
+                            : flag_status(ctx, f, what);
+    }
+    laspj::dev_release(ctx, dev, 8 * R);
+    if (s != LASPJ_OK) {
+        dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;     // contents undefined
+        return s;
+    }
+    set_known(dst, h.data(), R);
+    return LASPJ_OK;
 }
 
 // the inflation kernels of prev -> cur into o (R bytes); clear_flag: start from a clean
@@ -1896,29 +1931,36 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
     const uint64_t R = cur->replicas;
     LGuard g(ctx);
+    // one device block: equality bytes, inflation bytes, the merge's sizes
+    const uint64_t o_need = (2 * R + 7) & ~7ull, bytes = o_need + 8 * R;
     void* dev = nullptr;
-    if (laspj::dev_alloc(ctx, 2 * R, &dev) != hipSuccess) {
+    if (laspj::dev_alloc(ctx, bytes, &dev) != hipSuccess) {
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "list_bind: status bytes");
     }
     uint8_t* eq = static_cast<uint8_t*>(dev);
+    auto* need = reinterpret_cast<uint32_t*>(eq + o_need);
     std::vector<uint8_t> inf(R, 0);
-    BindX bx{eq, status, false};
-    int s = merge_run(ctx, dst, cur, val, rk, false, "list_bind", &bx);
-    if (s == LASPJ_OK && !bx.skipped) {
-        s = inflation_launch(ctx, cur, dst, 0, rk, eq + R, false, "list_bind");
-        if (s == LASPJ_OK) {
-            uint32_t f = 0;
-            const laspj::ReadPiece rp[2] = {{inf.data(), eq + R, R}, {&f, ctx->flag + 1, 4}};
-            const hipError_t e = laspj::readback(ctx, rp, 2);
-            if (e != hipSuccess)
-                s = fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s", hipGetErrorString(e));
-            else
-                s = flag_status(ctx, f, "list_bind");
-        }
+    std::vector<uint32_t> h(2 * R);
+    // `Value0 =:= Value`, Type:merge and is_inflation(Value0, Merged) enqueued back to back
+    // (the merge sized from the inputs' known counts), then ONE synchronisation
+    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, eq, "list_bind");
+    if (s == LASPJ_OK) s = inflation_launch(ctx, cur, dst, 0, rk, eq + R, false, "list_bind");
+    if (s == LASPJ_OK) {
+        uint32_t f = 0;
+        const laspj::ReadPiece rp[4] = {{status, eq, R}, {inf.data(), eq + R, R},
+                                        {h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
+        const hipError_t e = laspj::readback(ctx, rp, 4);
+        s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s",
+                                   hipGetErrorString(e))
+                            : flag_status(ctx, f, "list_bind");
     }
-    laspj::dev_release(ctx, dev, 2 * R);
-    if (s != LASPJ_OK) return s;
+    laspj::dev_release(ctx, dev, bytes);
+    if (s != LASPJ_OK) {
+        dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;
+        return s;
+    }
+    set_known(dst, h.data(), R);
     // status: 0 = cur =:= val (no-op), 1 = the merge inflates cur (written), 2 = it does not
     for (uint64_t i = 0; i < R; ++i) status[i] = status[i] ? 0 : (inf[i] ? 1 : 2);
     return LASPJ_OK;
