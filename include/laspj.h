@@ -171,7 +171,11 @@ int      laspj_buf_upload(laspj_ctx* ctx, laspj_buf* buf, uint64_t offset,
                           const void* src, uint64_t bytes);
 int      laspj_buf_download(laspj_ctx* ctx, const laspj_buf* buf, uint64_t offset,
                             void* dst, uint64_t bytes);
-/* device address of a buffer (to wrap sub-ranges as batches, or hand to a collective) */
+/* device address of a buffer (to wrap sub-ranges as batches, or hand to a collective).
+ * Destroying a buffer or batch is ordered with its context's stream only, and released
+ * blocks are reused by later allocations of the context; a buffer / batch whose address
+ * was handed out here therefore synchronises the whole device when it is destroyed, so
+ * work another stream still runs on it finishes first. */
 int      laspj_buf_device_ptr(const laspj_buf* buf, void** out);
 
 /* ------------------------------------------------------------------ batches */
@@ -190,7 +194,8 @@ int laspj_batch_wrap(laspj_ctx* ctx, int32_t kind, void* device_ptr, uint64_t by
                      uint64_t replicas, uint32_t elements, laspj_batch** out);
 int laspj_batch_info_get(const laspj_batch* batch, laspj_batch_info* out);
 /* device address of a batch's first word (to wrap replica ranges with laspj_batch_wrap
- * or hand them to a collective); list batches have no flat layout (LASPJ_E_KIND) */
+ * or hand them to a collective; its destroy then synchronises the device, as for
+ * laspj_buf_device_ptr); list batches have no flat layout (LASPJ_E_KIND) */
 int laspj_batch_device_ptr(const laspj_batch* batch, void** out);
 /* bytes [offset, offset + bytes) of a batch's device image (synchronous), e.g. one row
  * window of a product batch */
@@ -519,8 +524,9 @@ int laspj_gset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict
  * after a round every rank holds the join of all ranks' replicas of every object.
  *   OR-Set / G-Set: grouped ncclSend/ncclRecv all-to-all (rank j receives every rank's
  *     copy of object chunk j, objects chunk-major: rank j owns objects
- *     [j*R/n, (j+1)*R/n)), the reduce_chunks kernel (OR over the n copies), then
- *     ncclAllGather of the joined chunks — RCCL has no bitwise-OR reduction;
+ *     [j*R/n, (j+1)*R/n)), the reduce kernel (OR over the n copies, in place), then an
+ *     all-gather of the joined chunks made of grouped ncclSend/ncclRecv pieces — RCCL
+ *     has no bitwise-OR reduction;
  *   G-Counter: one ncclAllReduce(ncclMax) over the uint64 counts (in place).
  * Everything is enqueued on the contexts' streams (no host synchronisation); results
  * are valid after the next synchronising call.  LASPJ_E_UNSUPPORTED when RCCL cannot be
@@ -584,6 +590,14 @@ typedef struct laspj_ae_step {
 int laspj_antientropy_plan(int32_t kind, int rank, int nranks, uint64_t state_words,
                            uint64_t piece_words, laspj_ae_step* steps, uint64_t cap,
                            uint64_t* nsteps);
+/* Every rank's plan of one round executed on ONE context, rank i's buffers being state[i]
+ * / recv[i]: a SEND / RECV pair becomes a device copy between the two ranks' buffers,
+ * REDUCE is the round's reduce step (the same word arithmetic and kernel as
+ * laspj_antientropy), ALLREDUCE_MAX the unsigned max of every rank's piece.  The same
+ * argument checks as a round.  For testing the round's step arithmetic at nranks > 1 where
+ * one process has one GPU (RCCL refuses one device twice in a communicator). */
+int laspj_antientropy_loopback(laspj_ctx* ctx, int nranks, laspj_batch* const* state,
+                               laspj_batch* const* recv, uint64_t piece_words);
 
 /* ------------------------------------------------------------------ list values */
 /* List-faithful values.  The combinator bodies of lasp_core bind lists that are not

@@ -181,6 +181,7 @@ SIGNATURES = {
     "laspj_comm_info": (i, [vp, C.POINTER(i), C.POINTER(i)]),
     "laspj_antientropy": (i, [vp, vp, vp, vp]),
     "laspj_antientropy_group": (i, [vp, vp, vp, vp, i]),
+    "laspj_antientropy_loopback": (i, [vp, i, vp, vp, u64]),
     "laspj_antientropy_plan": (i, [C.c_int32, i, i, u64, u64, C.POINTER(AEStep), u64,
                                    C.POINTER(u64)]),
     "laspj_list_batch_create": (i, [vp, C.c_int32, u64, u32, u32, vpp]),

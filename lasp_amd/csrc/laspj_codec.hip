@@ -2857,7 +2857,7 @@ int reserve_scratch(laspj_ctx* ctx, uint64_t need) {
         ctx->scratch = nullptr;
         ctx->scratch_bytes = 0;
     }
-    if (hipMalloc(&ctx->scratch, need) != hipSuccess) {
+    if (laspj::dev_malloc(ctx, &ctx->scratch, need) != hipSuccess) {
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "etf: scratch allocation of %llu bytes",
                     (unsigned long long)need);
@@ -3951,7 +3951,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
-    if (hipMalloc(&d->block, bytes) != hipSuccess) {
+    if (laspj::dev_malloc(ctx, &d->block, bytes) != hipSuccess) {
         hipGetLastError();
         delete d;
         return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: hipMalloc(%llu)", (unsigned long long)bytes);

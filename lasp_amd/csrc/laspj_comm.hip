@@ -7,8 +7,9 @@
 //   * bitmap kinds (OR-Set, G-Set): RCCL has no bitwise-OR reduction and max on packed
 //     masks is not a join, so a round is a grouped ncclSend/ncclRecv all-to-all (rank j
 //     receives every rank's copy of object chunk j: the reduce-scatter layout, driving
-//     all n-1 xGMI links at once), the HIP reduce_chunks kernel (one OR over the n
-//     copies), and ncclAllGather of the joined chunks;
+//     all n-1 xGMI links at once), the HIP reduce kernel (one OR over the n copies, in
+//     place), and an all-gather of the joined chunks made of the same grouped
+//     ncclSend/ncclRecv pieces (1 GiB each: one p2p call moves at most 4 GiB);
 //   * G-Counters: the join IS the per-actor max, so a round is one ncclAllReduce(ncclMax)
 //     on ncclUint64 counts (the unsigned max the device join uses).
 // All phases are enqueued on the engine context's stream: RCCL, the reduce kernel and the
@@ -51,8 +52,6 @@ struct Rccl {
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
-    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
-                              hipStream_t) = nullptr;
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t,
                               ncclComm_t, hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
@@ -85,7 +84,7 @@ const Rccl* rccl() {
            sym(h, "ncclCommInitAll", &r.CommInitAll) && sym(h, "ncclCommDestroy", &r.CommDestroy) &&
            sym(h, "ncclGroupStart", &r.GroupStart) && sym(h, "ncclGroupEnd", &r.GroupEnd) &&
            sym(h, "ncclSend", &r.Send) && sym(h, "ncclRecv", &r.Recv) &&
-           sym(h, "ncclAllGather", &r.AllGather) && sym(h, "ncclAllReduce", &r.AllReduce) &&
+           sym(h, "ncclAllReduce", &r.AllReduce) &&
            sym(h, "ncclGetErrorString", &r.GetErrorString);
     if (!r.ok) r.why = "librccl lacks a required symbol";
     return r.ok ? &r : nullptr;
@@ -200,29 +199,38 @@ void plan_steps(Plan& P, int32_t kind, int rank, int nranks, uint64_t words, uin
     }
 }
 
+// the words a SEND / RECV step reads / writes
+uint64_t* step_words(const laspj_ae_step& s, laspj_batch* state, laspj_batch* recv) {
+    uint64_t* bufs[2] = {state->dev, recv ? recv->dev : nullptr};
+    return bufs[s.buf] + s.offset;
+}
+
+// a REDUCE step: the rank's own chunk joined in place with the received copies
+int reduce_step(laspj_ctx* ctx, const laspj_ae_step& s, laspj_batch* state, laspj_batch* recv) {
+    uint64_t* own = state->dev + s.offset;
+    const uint64_t* srcs[8];
+    srcs[0] = own;
+    for (uint32_t j = 0; j < s.nsrc; ++j) srcs[1 + j] = recv->dev + s.src + j * s.words;
+    LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, own, srcs, s.nsrc + 1, s.words,
+                                          state->kind == LASPJ_KIND_GCOUNTER));
+    return LASPJ_OK;
+}
+
 // one step of a plan on the context's stream
 int run_step(const Rccl* R, laspj_comm* c, const laspj_ae_step& s, laspj_batch* state,
              laspj_batch* recv) {
     laspj_ctx* ctx = c->ctx;
-    uint64_t* bufs[2] = {state->dev, recv ? recv->dev : nullptr};
     switch (s.op) {
     case LASPJ_AE_SEND:
-        LJ_NCCL(ctx, R, R->Send(bufs[s.buf] + s.offset, s.words, ncclUint64, s.peer, c->comm,
+        LJ_NCCL(ctx, R, R->Send(step_words(s, state, recv), s.words, ncclUint64, s.peer, c->comm,
                                 ctx->stream));
         return LASPJ_OK;
     case LASPJ_AE_RECV:
-        LJ_NCCL(ctx, R, R->Recv(bufs[s.buf] + s.offset, s.words, ncclUint64, s.peer, c->comm,
+        LJ_NCCL(ctx, R, R->Recv(step_words(s, state, recv), s.words, ncclUint64, s.peer, c->comm,
                                 ctx->stream));
         return LASPJ_OK;
-    case LASPJ_AE_REDUCE: {
-        uint64_t* own = state->dev + s.offset;
-        const uint64_t* srcs[8];
-        srcs[0] = own;
-        for (uint32_t j = 0; j < s.nsrc; ++j) srcs[1 + j] = recv->dev + s.src + j * s.words;
-        LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, own, srcs, s.nsrc + 1, s.words,
-                                              state->kind == LASPJ_KIND_GCOUNTER));
-        return LASPJ_OK;
-    }
+    case LASPJ_AE_REDUCE:
+        return reduce_step(ctx, s, state, recv);
     case LASPJ_AE_ALLREDUCE_MAX:
         LJ_NCCL(ctx, R, R->AllReduce(state->dev + s.offset, state->dev + s.offset, s.words,
                                      ncclUint64, ncclMax, c->comm, ctx->stream));
@@ -385,6 +393,74 @@ int laspj_antientropy_group(laspj_comm* const* cs, laspj_batch* const* state,
                 }
         }
         if (comm) LJ_NCCL(cs[0]->ctx, R, R->GroupEnd());
+    }
+    return LASPJ_OK;
+}
+
+int laspj_antientropy_loopback(laspj_ctx* ctx, int nranks, laspj_batch* const* state,
+                               laspj_batch* const* recv, uint64_t piece_words) {
+    if (!ctx || !state || nranks < 1 || nranks > 8)
+        return fail(ctx, LASPJ_E_INVAL, "antientropy_loopback: bad argument");
+    std::vector<laspj_comm> cs(nranks);
+    for (int i = 0; i < nranks; ++i) {
+        cs[i].ctx = ctx;
+        cs[i].rank = i;
+        cs[i].nranks = nranks;
+        if (!state[i]) return fail(ctx, LASPJ_E_INVAL, "antientropy_loopback: null state");
+        if (int s = round_checks(&cs[i], state[i], recv ? recv[i] : nullptr, nullptr,
+                                 "antientropy_loopback"))
+            return s;
+        if (state[i]->kind != state[0]->kind || laspj::bytes_of(state[i]) != laspj::bytes_of(state[0]))
+            return fail(ctx, LASPJ_E_KIND, "antientropy_loopback: one kind and size");
+        for (int j = 0; j < i; ++j)
+            if (state[j] == state[i] || (recv && recv[i] && recv[j] == recv[i]))
+                return fail(ctx, LASPJ_E_INVAL, "antientropy_loopback: a buffer twice");
+    }
+    const uint64_t words = state[0]->replicas * state[0]->words_per_replica;
+    const uint64_t piece = piece_words ? piece_words : kPiece;
+    std::vector<std::vector<laspj_ae_step>> plans(nranks);
+    for (int i = 0; i < nranks; ++i) {
+        Plan P{nullptr, 0};
+        plan_steps(P, state[0]->kind, i, nranks, words, piece);
+        plans[i].resize(P.n);
+        Plan Q{plans[i].data(), P.n};
+        plan_steps(Q, state[0]->kind, i, nranks, words, piece);
+    }
+    CGuard g(ctx);
+    std::vector<size_t> at(nranks, 0);
+    for (uint32_t grp = 0;; ++grp) {
+        // this group's steps of every rank (SENDs first: a RECV takes its peer's SEND)
+        std::vector<std::pair<int, const laspj_ae_step*>> steps;
+        for (int i = 0; i < nranks; ++i)
+            for (; at[i] < plans[i].size() && plans[i][at[i]].group == grp; ++at[i])
+                steps.push_back({i, &plans[i][at[i]]});
+        if (steps.empty()) break;
+        for (auto& [i, s] : steps) {
+            laspj_batch* rv = recv ? recv[i] : nullptr;
+            if (s->op == LASPJ_AE_RECV) {
+                const laspj_ae_step* snd = nullptr;
+                for (auto& [k, t] : steps)
+                    if (k == s->peer && t->op == LASPJ_AE_SEND && t->peer == i && t->tag == s->tag)
+                        snd = t;
+                if (!snd || snd->words != s->words)
+                    return fail(ctx, LASPJ_E_INVAL, "antientropy_loopback: unmatched RECV");
+                LJ_HIP(ctx, hipMemcpyAsync(step_words(*s, state[i], rv),
+                                           step_words(*snd, state[s->peer], recv ? recv[s->peer] : nullptr),
+                                           8ull * s->words, hipMemcpyDeviceToDevice, ctx->stream));
+            } else if (s->op == LASPJ_AE_REDUCE) {
+                if (int st = reduce_step(ctx, *s, state[i], rv)) return st;
+            } else if (s->op == LASPJ_AE_ALLREDUCE_MAX && i == 0) {
+                // every rank's piece -> their unsigned max in rank 0's, then copied out
+                const uint64_t* srcs[8];
+                for (int k = 0; k < nranks; ++k) srcs[k] = state[k]->dev + s->offset;
+                LJ_HIP(ctx, laspj::launch_reduce_ptrs(ctx, state[0]->dev + s->offset, srcs,
+                                                      (uint32_t)nranks, s->words, true));
+                for (int k = 1; k < nranks; ++k)
+                    LJ_HIP(ctx, hipMemcpyAsync(state[k]->dev + s->offset, state[0]->dev + s->offset,
+                                               8ull * s->words, hipMemcpyDeviceToDevice,
+                                               ctx->stream));
+            }
+        }
     }
     return LASPJ_OK;
 }

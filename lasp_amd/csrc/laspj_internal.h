@@ -63,6 +63,9 @@ struct laspj_buf {
     laspj_ctx* ctx = nullptr;
     void* dev = nullptr;
     uint64_t bytes = 0;
+    // the device address was handed out (laspj_buf_device_ptr): work on other streams may
+    // still use the block, so its release synchronises the device first
+    mutable bool exported = false;
 };
 
 struct laspj_batch {
@@ -75,6 +78,7 @@ struct laspj_batch {
     uint64_t cells = 0;         // cells per replica: E, or EL*ER for products
     uint64_t* dev = nullptr;
     bool owns = true;           // false for laspj_batch_wrap
+    mutable bool exported = false;  // laspj_batch_device_ptr handed out the address
     // LASPJ_KIND_*_LIST: entry / token capacity per replica (laspj_lists.hip)
     uint32_t cap_e = 0;
     uint32_t cap_t = 0;
@@ -115,6 +119,9 @@ hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n);
 constexpr uint64_t kCacheMax = 256ull << 20;      // largest cached block
 constexpr uint64_t kCacheCap = 2ull << 30;        // bytes a context keeps cached
 hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out);
+// hipMalloc that gives the context's cached blocks back and retries once when it fails
+// (every long-lived scratch allocation goes through it)
+hipError_t dev_malloc(laspj_ctx* ctx, void** out, uint64_t bytes);
 void dev_release(laspj_ctx* ctx, void* p, uint64_t bytes);
 void dev_cache_clear(laspj_ctx* ctx);
 inline hipError_t readback(laspj_ctx* ctx, void* host, const void* dev, uint64_t bytes) {

@@ -1029,7 +1029,7 @@ static hipError_t partials(laspj_ctx* ctx, uint64_t R, u64** out) {
             ctx->partials = nullptr;
             ctx->partials_bytes = 0;
         }
-        hipError_t e = hipMalloc(&ctx->partials, need);
+        hipError_t e = dev_malloc(ctx, &ctx->partials, need);
         if (e != hipSuccess) return e;
         ctx->partials_bytes = need;
         e = hipMemsetAsync(ctx->partials, 0, need, ctx->stream);

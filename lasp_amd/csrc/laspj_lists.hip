@@ -1415,7 +1415,7 @@ void* lscratch(laspj_ctx* ctx, uint64_t bytes) {
             ctx->lscratch = nullptr;
             ctx->lscratch_bytes = 0;
         }
-        if (hipMalloc(&ctx->lscratch, bytes) != hipSuccess) {
+        if (laspj::dev_malloc(ctx, &ctx->lscratch, bytes) != hipSuccess) {
             hipGetLastError();
             return nullptr;
         }

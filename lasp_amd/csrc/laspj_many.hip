@@ -242,7 +242,7 @@ void* mscratch(laspj_ctx* ctx, uint64_t bytes) {
             ctx->lscratch = nullptr;
             ctx->lscratch_bytes = 0;
         }
-        if (hipMalloc(&ctx->lscratch, bytes) != hipSuccess) {
+        if (laspj::dev_malloc(ctx, &ctx->lscratch, bytes) != hipSuccess) {
             hipGetLastError();
             return nullptr;
         }

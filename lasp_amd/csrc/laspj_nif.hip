@@ -102,15 +102,11 @@ int grow_dev(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
         *p = nullptr;
         *have = 0;
     }
-    if (hipMalloc(p, want) != hipSuccess) {
+    if (dev_malloc(ctx, p, want) != hipSuccess) {
         hipGetLastError();
-        dev_cache_clear(ctx);                       // give the block cache back, retry
-        if (hipMalloc(p, want) != hipSuccess) {
-            hipGetLastError();
-            *p = nullptr;
-            return fail(ctx, LASPJ_E_NOMEM, "nif: device allocation of %llu bytes",
-                        (unsigned long long)want);
-        }
+        *p = nullptr;
+        return fail(ctx, LASPJ_E_NOMEM, "nif: device allocation of %llu bytes",
+                    (unsigned long long)want);
     }
     *have = want;
     return LASPJ_OK;

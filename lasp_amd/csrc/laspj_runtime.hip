@@ -128,10 +128,24 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
 
 namespace laspj {
 
+// size classes: powers of two up to 4 MiB, then eighths of the next power of two (a
+// block just past a power of two no longer takes twice its size)
 static uint64_t cache_class(uint64_t bytes) {
     uint64_t c = 256;
     while (c < bytes) c <<= 1;
-    return c;
+    if (c <= (4ull << 20)) return c;
+    const uint64_t step = c >> 4;                       // c / 2 < bytes <= c
+    return (bytes + step - 1) / step * step;
+}
+
+hipError_t dev_malloc(laspj_ctx* ctx, void** out, uint64_t bytes) {
+    hipError_t e = hipMalloc(out, bytes);
+    if (e != hipSuccess && !ctx->cache.empty()) {      // give the cached blocks back, retry
+        hipGetLastError();
+        dev_cache_clear(ctx);
+        e = hipMalloc(out, bytes);
+    }
+    return e;
 }
 
 hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out) {
@@ -146,13 +160,7 @@ hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out) {
         }
         bytes = c;
     }
-    hipError_t e = hipMalloc(out, bytes);
-    if (e != hipSuccess && !ctx->cache.empty()) {      // give the cached blocks back, retry
-        dev_cache_clear(ctx);
-        hipGetLastError();
-        e = hipMalloc(out, bytes);
-    }
-    return e;
+    return dev_malloc(ctx, out, bytes);
 }
 
 void dev_release(laspj_ctx* ctx, void* p, uint64_t bytes) {
@@ -384,6 +392,9 @@ int laspj_buf_destroy(laspj_buf* b) {
     if (!b) return LASPJ_E_INVAL;
     {
         Guard g(b->ctx);
+        // an exported block may still be in use on another stream (a collective, a torch
+        // kernel): wait for the device before the block cache can hand it out again
+        if (b->exported) hipDeviceSynchronize();
         laspj::dev_release(b->ctx, b->dev, b->bytes);
     }
     delete b;
@@ -394,6 +405,7 @@ uint64_t laspj_buf_bytes(const laspj_buf* b) { return b ? b->bytes : 0; }
 
 int laspj_buf_device_ptr(const laspj_buf* b, void** out) {
     if (!b || !out) return LASPJ_E_INVAL;
+    b->exported = true;
     *out = b->dev;
     return LASPJ_OK;
 }
@@ -440,6 +452,7 @@ int laspj_batch_destroy(laspj_batch* b) {
     if (!b) return LASPJ_E_INVAL;
     {
         Guard g(b->ctx);
+        if (b->owns && b->exported) hipDeviceSynchronize();        // as laspj_buf_destroy
         if (b->owns) laspj::dev_release(b->ctx, b->dev, laspj::bytes_of(b));
     }
     delete b;
@@ -530,6 +543,7 @@ int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
 int laspj_batch_device_ptr(const laspj_batch* b, void** out) {
     if (!b || !out) return LASPJ_E_INVAL;
     if (laspj_is_list(b->kind)) return LASPJ_E_KIND;
+    b->exported = true;
     *out = b->dev;
     return LASPJ_OK;
 }
@@ -875,7 +889,7 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
             ctx->scratch = nullptr;
             ctx->scratch_bytes = 0;
         }
-        if (hipMalloc(&ctx->scratch, need) != hipSuccess) {
+        if (laspj::dev_malloc(ctx, &ctx->scratch, need) != hipSuccess) {
             hipGetLastError();
             return fail(ctx, LASPJ_E_NOMEM, "%s: scratch allocation", what);
         }
@@ -1156,7 +1170,7 @@ int laspj_gcounter_apply_increments(laspj_ctx* ctx, laspj_batch* b, const laspj_
             ctx->scratch = nullptr;
             ctx->scratch_bytes = 0;
         }
-        if (hipMalloc(&ctx->scratch, need) != hipSuccess) {
+        if (laspj::dev_malloc(ctx, &ctx->scratch, need) != hipSuccess) {
             hipGetLastError();
             return fail(ctx, LASPJ_E_NOMEM, "gcounter_apply_increments: scratch");
         }
