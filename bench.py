@@ -339,11 +339,15 @@ def config1_gpu(ctx):
         nif_many()
     out["us_merge_nif_many_per_merge"] = (time.perf_counter() - t0) * 1e6 / (5 * nm)
     out["nif_many_batch"] = nm
-    st = (C.c_uint64 * 8)()
-    check(L.laspj_nif_stats(ctx.h, st, 8), ctx.h)
-    out["nif_stats"] = dict(zip(("calls", "device_passes", "registrations", "dict_resets",
-                                 "image_rebuilds", "host_encoded_passes", "fallbacks",
-                                 "dict_elements"), (int(x) for x in st)))
+    st0 = ctx.nif_stats()
+    for _ in range(20):
+        nif()
+    st1 = ctx.nif_stats()
+    out["nif_stats"] = st1
+    # where one warm NIF merge's time goes (host clock, averaged over 20 calls)
+    out["nif_stages_us"] = {k: (st1[k] - st0[k]) / 20e3 for k in
+                            ("ns_stage_copy", "ns_stage_enqueue", "ns_device_wait",
+                             "ns_answers")}
     # where the device-decode path's time goes (one call, synchronised per stage)
     stages = {}
     t0 = time.perf_counter()

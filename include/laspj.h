@@ -799,8 +799,11 @@ int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
                               int32_t* verdict);
 /* counters of this context's NIF path: [0] calls, [1] device passes, [2] dictionary
  * registrations, [3] dictionary resets, [4] device image rebuilds, [5] host-encoded passes
- * (token images of mixed lengths), [6] FALLBACK verdicts, [7] dictionary elements */
-#define LASPJ_NIF_STATS 8
+ * (token images of mixed lengths), [6] FALLBACK verdicts, [7] dictionary elements; host
+ * nanoseconds summed over device passes: [8] staging + enqueueing, [9] waiting for the
+ * device, [10] reading the answers after it, [11] the part of [8] spent copying operands
+ * into pinned memory */
+#define LASPJ_NIF_STATS 12
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
 /* drop the context's dictionary (its memory; the next call registers afresh) */
 int laspj_nif_reset(laspj_ctx* ctx);

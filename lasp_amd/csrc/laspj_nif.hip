@@ -24,6 +24,7 @@
 // and staging are per context: one context per scheduler, no process globals.
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -176,7 +177,14 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S) {
 
 // One device pass: stage, copy, decode (or upload host-encoded cells), answer, copy back,
 // one synchronisation.  Fills c.st / c.res / c.ooff / c.obase.
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
+    const uint64_t t0 = now_ns();
+    uint64_t t_copy = 0;
     const uint32_t m = c.m, n = c.n, E = S->E;
     const bool dec = etf_dict_decodable(S->etf);
     std::vector<unsigned long long> hoffs(m + 1ull, 0);
@@ -251,6 +259,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             while (at < pay) {
                 const uint64_t piece = std::min(kStagePiece, pay - at);
                 uint64_t done = 0;
+                const uint64_t tc = now_ns();
                 while (done < piece) {
                     const uint64_t take = std::min(piece - done, c.len[i] - io);
                     std::memcpy(hin + i_pay + at + done, c.p[i] + io, take);
@@ -262,6 +271,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                         while (i < m && c.len[i] == 0) ++i;
                     }
                 }
+                t_copy += now_ns() - tc;
                 at += piece;
                 const uint64_t upto = head + at;
                 LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, upto - sent,
@@ -329,8 +339,13 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         }
         const uint64_t first = o_pay + (has_payload_out ? std::min(ocap, bound) : 0);
         LJ_HIP(ctx, hipMemcpyAsync(S->hout, dout, first, hipMemcpyDeviceToHost, ctx->stream));
+        const uint64_t t1 = now_ns();
         LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        const uint64_t t2 = now_ns();
         ++S->stats[1];
+        S->stats[8] += t1 - t0;
+        S->stats[9] += t2 - t1;
+        S->stats[11] += t_copy;
         const uint8_t* hout = static_cast<const uint8_t*>(S->hout);
         c.st.assign(m, 0);
         if (dec) std::memcpy(c.st.data(), hout + o_st, 4ull * m);
@@ -354,6 +369,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             }
             c.obase = hout + o_pay;
         }
+        S->stats[10] += now_ns() - t2;
     }
     return LASPJ_OK;
 }
@@ -586,7 +602,7 @@ int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n) {
     std::lock_guard<std::mutex> lk(S->mu);
     for (uint32_t i = 0; i < n && i < LASPJ_NIF_STATS; ++i) out[i] = S->stats[i];
     if (n > 7) {
-        uint32_t e = 0;
+        uint32_t e = 0;  // [7] is the dictionary's size, not a counter
         uint64_t eb, tb;
         out[7] = S->dict && laspj_dict_info(S->dict, &e, &eb, &tb) == LASPJ_OK ? e : 0;
     }

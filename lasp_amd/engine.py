@@ -153,10 +153,11 @@ class Context:
         return int(verd.value), (bool(res.value) if verd.value == 0 else None)
 
     def nif_stats(self) -> dict:
-        out = (C.c_uint64 * 8)()
-        check(self.L.laspj_nif_stats(self.h, out, 8), self.h)
+        out = (C.c_uint64 * _lib.NIF_STATS)()
+        check(self.L.laspj_nif_stats(self.h, out, _lib.NIF_STATS), self.h)
         keys = ("calls", "device_passes", "registrations", "dict_resets", "image_rebuilds",
-                "host_encoded_passes", "fallbacks", "dict_elements")
+                "host_encoded_passes", "fallbacks", "dict_elements", "ns_stage_enqueue",
+                "ns_device_wait", "ns_answers", "ns_stage_copy")
         return dict(zip(keys, (int(x) for x in out)))
 
     def nif_reset(self):
