@@ -1711,9 +1711,12 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t bt = gs ? 1ull : (uint64_t)a->known_t + b->known_t;
     if (be > 0xFFFFFFF0ull || bt > 0xFFFFFFF0ull)
         return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
+    // OR-Set lists: the write pass writes every word a reader looks at (header, keys,
+    // token offsets, tokens), so a fresh block is not cleared; G-Set lists keep zero token
+    // offsets, which the write pass does not write (k_list_equal compares them)
     if (be > dst->cap_e || bt > dst->cap_t)
         if (int s = list_alloc(ctx, dst, be > dst->cap_e ? (uint32_t)be : dst->cap_e,
-                               bt > dst->cap_t ? (uint32_t)bt : dst->cap_t, false))
+                               bt > dst->cap_t ? (uint32_t)bt : dst->cap_t, gs))
             return s;
     MS m;
     m.ce_a = a->cap_e;
