@@ -79,6 +79,13 @@ struct laspj_etf_dict {
     uint32_t gs_hmask = 0;
     const uint32_t* gs_rank = nullptr;     // E
     const uint32_t* gs_byte = nullptr;     // 256
+    // integer elements (minimal SMALL_INTEGER / INTEGER images) by value: entry v - gs_ilo
+    // = slot + 1 | rank << 32 (0: no element), so the decoder finds an integer element with
+    // one load instead of a hash probe and an image compare; null when no integer element
+    // or their values are too spread out
+    const uint64_t* gs_itab = nullptr;
+    int64_t gs_ilo = 0;
+    uint32_t gs_in = 0;
 };
 
 namespace laspj {
@@ -2993,7 +3000,11 @@ struct GsTabs {
     const uint32_t* rank;
     const uint32_t* byte_slot;
     uint32_t E;
+    const u64* itab;       // integer elements by value (see laspj_etf_dict::gs_itab)
+    int64_t ilo;
+    uint32_t in;
 };
+
 
 // the slot whose image is p[0, n), or kNoSlot
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -3007,6 +3018,33 @@ __device__ __forceinline__ uint32_t gs_slot(const GsTabs& g, const uint8_t* p, u
         for (uint32_t k = 0; k < n && same; ++k) same = g.blob[o + k] == p[k];
         if (same) return e;
     }
+}
+
+// slot and rank of the element image p[0, n): integers through the value table (an image
+// that is not the minimal encoding of its value is no dictionary image: not found, as in
+// the hash), every other term through the image hash
+__device__ __forceinline__ void gs_lookup(const GsTabs& g, const uint8_t* p, uint32_t n,
+                                          uint32_t* slot, uint32_t* rk) {
+    if (g.itab && (n == 2 || n == 5) && (p[0] == 97 || p[0] == 98)) {
+        bool ok = false;
+        int64_t v = 0;
+        if (n == 2 && p[0] == 97) {
+            v = p[1];
+            ok = true;
+        } else if (n == 5 && p[0] == 98) {
+            v = (int32_t)((uint32_t)p[1] << 24 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 8 | p[4]);
+            ok = v < 0 || v > 255;
+        }
+        if (ok) {
+            const int64_t x = v - g.ilo;
+            const u64 t = x >= 0 && x < (int64_t)g.in ? g.itab[x] : 0ull;
+            *slot = (uint32_t)t ? (uint32_t)t - 1u : kNoSlot;
+            *rk = (uint32_t)(t >> 32);
+            return;
+        }
+    }
+    *slot = gs_slot(g, p, n);
+    *rk = *slot != kNoSlot ? g.rank[*slot] : 0;
 }
 
 constexpr uint32_t kGChunk = 256;
@@ -3207,9 +3245,8 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                     if (k < m) {
                         const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
                         const bool in = s_l[k] <= 0xFFFFFFu && o + s_l[k] <= wl;
-                        slot = s_l[k] > 0xFFFFFFu ? kNoSlot
-                                                  : gs_slot(g, in ? win + o : p + s_o[k], s_l[k]);
-                        rk = slot != kNoSlot ? g.rank[slot] : 0;
+                        if (s_l[k] > 0xFFFFFFu) slot = kNoSlot;
+                        else gs_lookup(g, in ? win + o : p + s_o[k], s_l[k], &slot, &rk);
                     }
                     const uint32_t before = __shfl_up(rk, 1, 64);
                     bool bad = k < m && (slot == kNoSlot ||
@@ -3450,7 +3487,7 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
-                      d->elements};
+                      d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
     // one wave per replica and a latency-bound extent walk: as many waves as LDS allows
     // (6 KiB each: ~25 per CU)
     const uint64_t cap = (uint64_t)ctx->cus * 64;
@@ -3897,18 +3934,6 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     uint64_t gs_cap = 64;
     while (gs_cap < 2ull * E) gs_cap <<= 1;
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
-    const uint64_t o_eoff = 0, o_eord = o_eoff + al(4ull * (E + 1)), o_eb = o_eord + al(4ull * E),
-                   o_mask = o_eb + al(E), o_toff = o_mask + al(8ull * E),
-                   o_tord = o_toff + (toks ? al(4ull * (64ull * E + 1)) : 0),
-                   o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
-                   o_epoff = o_tblob + al(tblob + 1), o_tpoff = o_epoff + al(4ull * E),
-                   o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
-                   o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
-                   o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
-                   o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
-                   o_htab = o_rd + al(rd.size() + 8), o_gsh = o_htab + al(4ull * htab.size() + 4),
-                   o_gsr = o_gsh + al(4ull * gs_cap), o_gsb = o_gsr + al(4ull * E),
-                   bytes = o_gsb + al(4ull * 256);
     // G-Set from_binary tables: ranks (equal terms share one), image hash, byte values
     std::vector<uint32_t> gs_rank(E, 0), gs_byte(256, 0), gs_htab;
     {
@@ -3947,6 +3972,52 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
             if (!dup) gs_htab[i] = e + 1;
         }
     }
+    // integer elements by value (minimal images: SMALL_INTEGER for 0..255, INTEGER past it)
+    std::vector<uint64_t> gs_itab;
+    int64_t ilo = 0;
+    {
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        uint64_t cnt = 0;
+        auto int_of = [&](uint32_t e, int64_t* v) {
+            const uint32_t n = elem_off[e + 1] - elem_off[e];
+            const uint8_t* img = elem_blob + elem_off[e];
+            if (n == 2 && img[0] == 97) {
+                *v = img[1];
+                return true;
+            }
+            if (n == 5 && img[0] == 98) {
+                *v = (int32_t)((uint32_t)img[1] << 24 | (uint32_t)img[2] << 16 |
+                               (uint32_t)img[3] << 8 | img[4]);
+                return *v < 0 || *v > 255;
+            }
+            return false;
+        };
+        for (uint32_t e = 0; e < E; ++e) {
+            int64_t v;
+            if (int_of(e, &v)) lo = std::min(lo, v), hi = std::max(hi, v), ++cnt;
+        }
+        if (cnt && (uint64_t)(hi - lo) < std::max<uint64_t>(4 * cnt, 1ull << 16)) {
+            ilo = lo;
+            gs_itab.assign((uint64_t)(hi - lo) + 1, 0);
+            for (uint32_t e = 0; e < E; ++e) {
+                int64_t v;
+                if (int_of(e, &v) && !gs_itab[v - lo])      // one value twice: the first slot
+                    gs_itab[v - lo] = (e + 1ull) | ((uint64_t)gs_rank[e] << 32);
+            }
+        }
+    }
+    const uint64_t o_eoff = 0, o_eord = o_eoff + al(4ull * (E + 1)), o_eb = o_eord + al(4ull * E),
+                   o_mask = o_eb + al(E), o_toff = o_mask + al(8ull * E),
+                   o_tord = o_toff + (toks ? al(4ull * (64ull * E + 1)) : 0),
+                   o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
+                   o_epoff = o_tblob + al(tblob + 1), o_tpoff = o_epoff + al(4ull * E),
+                   o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
+                   o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
+                   o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
+                   o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
+                   o_htab = o_rd + al(rd.size() + 8), o_gsh = o_htab + al(4ull * htab.size() + 4),
+                   o_gsr = o_gsh + al(4ull * gs_cap), o_gsb = o_gsr + al(4ull * E),
+                   o_gsi = o_gsb + al(4ull * 256), bytes = o_gsi + al(8ull * gs_itab.size() + 8);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -3957,8 +4028,18 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
         return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: hipMalloc(%llu)", (unsigned long long)bytes);
     }
     char* base = static_cast<char*>(d->block);
+    // every array staged into one host image of the block, then one copy
+    std::vector<char> img;
+    try {
+        img.assign(bytes, 0);
+    } catch (const std::bad_alloc&) {
+        hipFree(d->block);
+        delete d;
+        return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host staging");
+    }
     auto up = [&](uint64_t off, const void* src, uint64_t n) {
-        return n ? hipMemcpy(base + off, src, n, hipMemcpyHostToDevice) : hipSuccess;
+        if (n) std::memcpy(img.data() + off, src, n);
+        return hipSuccess;
     };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = up(o_eoff, elem_off, 4ull * (E + 1));
@@ -3982,6 +4063,8 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess) e = up(o_gsh, gs_htab.data(), 4ull * gs_htab.size());
     if (e == hipSuccess) e = up(o_gsr, gs_rank.data(), 4ull * E);
     if (e == hipSuccess) e = up(o_gsb, gs_byte.data(), 4ull * 256);
+    if (e == hipSuccess && !gs_itab.empty()) e = up(o_gsi, gs_itab.data(), 8ull * gs_itab.size());
+    if (e == hipSuccess) e = hipMemcpy(base, img.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         hipFree(d->block);
         delete d;
@@ -4012,6 +4095,9 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->gs_hmask = (uint32_t)(gs_cap - 1);
     d->gs_rank = reinterpret_cast<const uint32_t*>(base + o_gsr);
     d->gs_byte = reinterpret_cast<const uint32_t*>(base + o_gsb);
+    d->gs_itab = gs_itab.empty() ? nullptr : reinterpret_cast<const uint64_t*>(base + o_gsi);
+    d->gs_ilo = ilo;
+    d->gs_in = (uint32_t)gs_itab.size();
     d->elem_off = reinterpret_cast<const uint32_t*>(base + o_eoff);
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);
