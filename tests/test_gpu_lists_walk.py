@@ -141,8 +141,8 @@ def test_unsorted_replicas_batched(env):
     rng = np.random.default_rng(4242)
     sh = shapes(rng)
     R = len(sh)
-    A = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, R, 9000, 40000)
-    B = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, R, 9000, 40000)
+    A = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, R, 12000, 40000)
+    B = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, R, 12000, 40000)
     want = []
     for r, (name, va, vb) in enumerate(sh):
         ta, *ia = _list(rng, va)
