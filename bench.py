@@ -339,6 +339,23 @@ def config1_gpu(ctx):
         nif_many()
     out["us_merge_nif_many_per_merge"] = (time.perf_counter() - t0) * 1e6 / (5 * nm)
     out["nif_many_batch"] = nm
+    # an update/3 between binds mints a token (lasp_orset.erl:222-230, 261-262): the
+    # merge then meets one term its dictionary lacks — registration, device images
+    # rebuilt, a second device pass
+    cold = []
+    for k in range(5):
+        tb2 = list(tb)
+        e = 17 * k + 3
+        tb2[e] = (e, sorted(tb[e][1] + [(b"N" + (k * 7919 + e).to_bytes(19, "big"), False)]))
+        pb2 = etf.term_to_binary(tb2)
+        t0 = time.perf_counter()
+        check(L.laspj_orset_etf_merge(ctx.h, pa, len(pa), pb2, len(pb2), C.byref(op),
+                                      C.byref(on), C.byref(vd)), ctx.h)
+        cold.append((time.perf_counter() - t0) * 1e6)
+        if vd.value != 0:
+            raise RuntimeError("config1: a merge with a new token fell back")
+    out["us_merge_nif_new_token"] = sorted(cold)[len(cold) // 2]
+    nif()
     st0 = ctx.nif_stats()
     for _ in range(20):
         nif()

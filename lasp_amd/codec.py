@@ -249,13 +249,16 @@ class Domain:
 
 
 class _Journal:
+    """O(1) to enter: the element count and the position in tok_log (every new token slot
+    logs its element slot), from which a rollback knows what each token dictionary
+    gained."""
+
     def __init__(self, dom: Domain):
         self.dom = dom
 
     def __enter__(self):
         d = self.dom
         self.ne = len(d.elements.terms)
-        self.nt = [len(td.terms) for td in d.tokens]
         self.nlog = len(d.tok_log)
         return self
 
@@ -263,9 +266,14 @@ class _Journal:
         if et is None:
             return False
         d = self.dom
-        for es, n in enumerate(self.nt):
-            d.tokens[es].truncate(n)
-        del d.tokens[len(self.nt):]
+        gained: Dict[int, int] = {}
+        for es in d.tok_log[self.nlog:]:
+            gained[es] = gained.get(es, 0) + 1
+        for es, k in gained.items():
+            if es < self.ne:
+                td = d.tokens[es]
+                td.truncate(len(td.terms) - k)
+        del d.tokens[self.ne:]
         d.elements.truncate(self.ne)
         del d.tok_log[self.nlog:]
         return False
