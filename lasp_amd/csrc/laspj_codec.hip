@@ -25,6 +25,7 @@
 // write-bound: a payload is ~15-70x the bytes of its cells.
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -3681,12 +3682,23 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
         if (ctx->tune_etf == 3) k = k_orset_etf_write_rec<20480, false>;
         if (ctx->tune_etf == 4) k = k_orset_etf_write_rec<24576, false>;
         if (ctx->tune_etf == 5) k = k_orset_etf_write_rec<24576, true>;
-        // one resident wave of blocks, each with a contiguous run of replicas
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||
-            occ < 1) {
-            hipGetLastError();
-            occ = 4;
+        // one resident wave of blocks, each with a contiguous run of replicas (the
+        // occupancy query is asked once per kernel variant: it costs host microseconds the
+        // NIF path's single-merge calls would pay every time)
+        static std::atomic<int> occ_cache[4];       // <24K, EPAR>, <24K>, <16K>, <20K>
+        int variant = d->tok_max <= 8 ? 0 : 1;
+        if (ctx->tune_etf == 2) variant = 2;
+        if (ctx->tune_etf == 3) variant = 3;
+        if (ctx->tune_etf == 4) variant = 1;
+        if (ctx->tune_etf == 5) variant = 0;
+        int occ = occ_cache[variant].load(std::memory_order_relaxed);
+        if (occ <= 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, 0) != hipSuccess ||
+                occ < 1) {
+                hipGetLastError();
+                occ = 4;
+            }
+            occ_cache[variant].store(occ, std::memory_order_relaxed);
         }
         const uint64_t resident = (uint64_t)ctx->cus * (uint64_t)occ;
         grid = (int)(R < resident ? R : resident);
