@@ -662,6 +662,88 @@ __global__ __launch_bounds__(kBlock) void k_etf_chunk_scan(u64* coff, uint64_t R
     }
 }
 
+// The NIF path's merge (laspj_nif.hip): lasp_orset:merge/2 of replica i of `a` and of `b`
+// (the slot-wise OR of canonical cells) written to `z`, fused with the split-mode size
+// pass over z, and the operands' cells cleared behind it (the next call's decoders then
+// start from new() without a memset).  Same chunk totals as k_etf_chunk_sizes.
+__global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2* b, u64x2* z,
+                                                                 uint64_t R, uint32_t E,
+                                                                 DictView d, uint32_t nch,
+                                                                 u64* coff, uint32_t* flag) {
+    __shared__ u64 lds4[kBlock / 64];
+    for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
+        const uint64_t rep = it / nch;
+        const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
+        u64 v = 0;
+        if (i < E) {
+            const uint32_t e = d.elem_order[i];
+            const uint64_t at = rep * E + e;
+            const u64x2 x = a[at] | b[at];
+            z[at] = x;
+            a[at] = u64x2{0, 0};
+            b[at] = u64x2{0, 0};
+            if (x.x) {
+                if (d.elem_off[e + 1] == d.elem_off[e] || (x.x & ~d.tok_mask[e]) != 0) {
+                    if (flag) atomicOr(flag, 1u);
+                } else {
+                    v = orset_elem_size(d, e, x.x, x.y) + kChunkCnt;
+                }
+            }
+        }
+        u64 tot;
+        block_excl_scan64(v, lds4, &tot);
+        if (threadIdx.x == 0) coff[rep * (nch + 1ull) + c] = tot;
+    }
+}
+
+// k_etf_chunk_scan, then (the block that finishes last, by an agent-scope ticket) the
+// payload offsets as k_etf_offsets_from_chunks: one launch instead of two.  ticket is zero
+// on entry and left zero.
+__global__ __launch_bounds__(kBlock) void k_etf_chunk_scan_offsets(u64* coff, uint64_t R,
+                                                                   uint32_t nch, uint32_t hdr,
+                                                                   u64* offs, uint32_t* ticket) {
+    __shared__ u64 lds4[kBlock / 64];
+    __shared__ uint32_t s_last;
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        u64* c = coff + rep * (nch + 1ull);
+        u64 carry = 0;
+        for (uint32_t t0 = 0; t0 <= nch; t0 += kBlock) {
+            const uint32_t t = t0 + threadIdx.x;
+            const u64 v = t < nch ? c[t] : 0;
+            u64 tot;
+            const u64 ex = block_excl_scan64(v, lds4, &tot);
+            if (t <= nch) c[t] = carry + ex;
+            carry += tot;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();                                   // this block's totals, visible
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();                                       // every block's totals, seen
+    u64 carry = 0;
+    for (uint64_t t0 = 0; t0 < R; t0 += kBlock) {
+        const uint64_t rep = t0 + threadIdx.x;
+        u64 v = 0;
+        if (rep < R) {
+            const u64 t = __atomic_load_n(coff + rep * (nch + 1ull) + nch, __ATOMIC_RELAXED);
+            const u64 n = t / kChunkCnt, sum = t & (kChunkCnt - 1);
+            v = hdr + 1u + (n ? 5u + sum + 1u : 1u);
+        }
+        u64 tot;
+        const u64 ex = block_excl_scan64(v, lds4, &tot);
+        if (rep < R) offs[rep] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        offs[R] = carry;
+        *ticket = 0;
+    }
+}
+
 // EPAR (few token slots per element): each element's thread also stages its own records
 // (no record -> element search, no rank select); otherwise records are spread over lanes.
 // coff != nullptr: split mode (above), block b writes chunks [g cper, (g + 1) cper) of
@@ -3461,7 +3543,7 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
     etf_read_plan(ctx, d, R, off.data(), &plan);
     return etf_read_enqueue(ctx, b, d, tag, vers, static_cast<const uint8_t*>(payload->dev),
                             payload->bytes, static_cast<const u64*>(offsets->dev), plan, nullptr,
-                            static_cast<int32_t*>(status->dev), true);
+                            static_cast<int32_t*>(status->dev), true, nullptr);
 }
 
 int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
@@ -3552,7 +3634,7 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, co
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
                      const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
-                     bool clear) {
+                     bool clear, uint32_t* redo_zeroed) {
     const uint64_t R = b->replicas;
     if (clear)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
@@ -3581,8 +3663,11 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
             dsegbase = up;
         }
         SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
-        uint32_t* redo = reinterpret_cast<uint32_t*>(sc + o_redo);
-        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        uint32_t* redo = redo_zeroed;
+        if (!redo) {
+            redo = reinterpret_cast<uint32_t*>(sc + o_redo);
+            LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        }
         const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
         hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
                                ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
@@ -3663,6 +3748,30 @@ int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict*
                            (uint32_t)b->words_per_replica, view(d), hdr, sizes, flag);
     LJ_LAUNCHED(ctx);
     LJ_HIP(ctx, launch_scan(ctx, sizes, offsets, R, tmp));
+    return LASPJ_OK;
+}
+
+bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
+    const uint32_t nch = (E + kBlock - 1) / kBlock;
+    return R <= (uint64_t)ctx->cus && nch >= 4;      // etf_size_enqueue's split mode
+}
+
+int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj_batch* z,
+                           const laspj_etf_dict* d, int tag, u64* offsets, uint32_t* flag,
+                           uint32_t* ticket, const u64** chunks) {
+    const uint64_t R = z->replicas;
+    const uint32_t nch = (z->elements + kBlock - 1) / kBlock;
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
+    u64* co = static_cast<u64*>(ctx->scratch);
+    const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+    hipLaunchKernelGGL(k_etf_join_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b),
+                       reinterpret_cast<u64x2*>(z->dev), R, z->elements, view(d), nch, co, flag);
+    hipLaunchKernelGGL(k_etf_chunk_scan_offsets, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                       dim3(kBlock), 0, ctx->stream, co, R, nch, hdr, offsets, ticket);
+    LJ_LAUNCHED(ctx);
+    *chunks = co;
     return LASPJ_OK;
 }
 

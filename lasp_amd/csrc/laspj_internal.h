@@ -230,10 +230,18 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R,
                    const unsigned long long* host_offsets, EtfReadPlan* plan);
 // segbase: plan.segbase already on the device, or null (uploaded here); clear: zero the
 // batch first (the decoders only set the cells they decode)
+// redo_zeroed: R + 1 words the caller has zeroed (segment mode's redo list), or null
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes,
                      const unsigned long long* offsets, const EtfReadPlan& plan,
-                     const uint32_t* segbase, int32_t* status, bool clear);
+                     const uint32_t* segbase, int32_t* status, bool clear,
+                     uint32_t* redo_zeroed);
+// merge/2 of a[i] and b[i] into z fused with z's size pass (and a, b cleared behind it),
+// when etf_merge_fused(ctx, R, E) holds; ticket: one zeroed word (left zero)
+bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E);
+int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj_batch* z,
+                           const laspj_etf_dict* d, int tag, unsigned long long* offsets,
+                           uint32_t* flag, uint32_t* ticket, const unsigned long long** chunks);
 // offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
 // caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
 // (valid until the context's scratch is next used), or null

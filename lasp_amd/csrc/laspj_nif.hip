@@ -51,6 +51,10 @@ struct NifState {
     void* hout = nullptr;
     uint64_t hout_bytes = 0;
     uint64_t ocap = 1 << 20;        // device bytes reserved for answer payloads
+    // the operand cells known to be new() (the fused merge clears them behind it), so the
+    // next call's decoders need no memset: words [0, clean_words) at element slots clean_E
+    uint64_t clean_words = 0;
+    uint32_t clean_E = 0;
     uint64_t stats[LASPJ_NIF_STATS] = {};
 };
 
@@ -194,8 +198,11 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     if (dec) etf_read_plan(ctx, S->etf, m, hoffs.data(), &plan);
     const bool has_payload_out = c.op == Op::MERGE || c.op == Op::VALUE;
     // in region (host -> device)
+    // [offsets | segment table | zeroed words: the size pass's ticket, the decoder's redo
+    //  list | payloads]
     const uint64_t i_offs = 0, i_seg = al(8ull * (m + 1), 256),
-                   i_pay = i_seg + (plan.nseg ? al(4ull * (m + 1), 256) : 0);
+                   i_zero = i_seg + (plan.nseg ? al(4ull * (m + 1), 256) : 0),
+                   i_pay = i_zero + al(4ull * (m + 2), 256);
     const uint64_t cells_in = (uint64_t)m * E * 16ull;
     const uint64_t in_bytes = i_pay + (dec ? al(pay + 64, 256) : al(cells_in, 256));
     // out region (device -> host)
@@ -220,7 +227,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     {
         Guard g(ctx);
         if (int s = grow_dev(ctx, &S->dblk, &S->dblk_bytes, al(in_bytes, 256) + out_bytes)) return s;
+        const uint64_t had = S->dcells_bytes;
         if (int s = grow_dev(ctx, &S->dcells, &S->dcells_bytes, c_out + cells_out + 256)) return s;
+        if (S->dcells_bytes != had) S->clean_words = 0;
         if (int s = grow_host(ctx, &S->hin, &S->hin_bytes, in_bytes)) return s;
         if (int s = grow_host(ctx, &S->hout, &S->hout_bytes, out_bytes)) return s;
     }
@@ -231,6 +240,10 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
     std::memcpy(hin + i_offs, hoffs.data(), 8ull * (m + 1));
     if (plan.nseg) std::memcpy(hin + i_seg, plan.segbase.data(), 4ull * (m + 1));
+    std::memset(hin + i_zero, 0, 4ull * (m + 2));
+    uint32_t* dticket = reinterpret_cast<uint32_t*>(din + i_zero);
+    const uint64_t in_words = (uint64_t)m * 2ull * E;
+    const bool clean = S->clean_E == E && S->clean_words >= in_words;
     std::vector<int32_t> hst;
     if (!dec) {
         // token images of several lengths (or no tokens yet): the host dictionary encodes
@@ -282,6 +295,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, head - sent,
                                            hipMemcpyHostToDevice, ctx->stream));
         } else {
+            LJ_HIP(ctx, hipMemcpyAsync(din, hin, i_pay, hipMemcpyHostToDevice, ctx->stream));
             LJ_HIP(ctx, hipMemcpyAsync(cin, hin + i_pay, cells_in, hipMemcpyHostToDevice,
                                        ctx->stream));
         }
@@ -293,7 +307,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                                          plan,
                                          plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg)
                                                    : nullptr,
-                                         dst, true))
+                                         dst, !clean, dticket + 1))
                 return s;
         }
         laspj_batch lhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin);
@@ -304,18 +318,29 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         case Op::MERGE: {
             // lasp_orset:merge/2 (lasp_orset.erl:128-134): the nested orddict:merge of two
             // canonical orddicts is the slot-wise OR of their cells
-            LJ_HIP(ctx, launch_or(ctx, cout, lhs.dev, rhs.dev, (uint64_t)n * 2ull * E));
             laspj_batch ob = view(ctx, LASPJ_KIND_ORSET, n, E, cout);
             const unsigned long long* chunks = nullptr;
-            if (int s = etf_size_enqueue(ctx, &ob, S->etf, LASPJ_KIND_ORSET, -1, dooff, ctx->flag,
-                                         &chunks))
-                return s;
+            if (etf_merge_fused(ctx, n, E)) {
+                // the OR fused with the answer's size pass, the operands cleared behind it
+                if (int s = etf_merge_size_enqueue(ctx, lhs.dev, rhs.dev, &ob, S->etf, -1, dooff,
+                                                   ctx->flag, dticket, &chunks))
+                    return s;
+                S->clean_words = in_words;
+                S->clean_E = E;
+            } else {
+                LJ_HIP(ctx, launch_or(ctx, cout, lhs.dev, rhs.dev, (uint64_t)n * 2ull * E));
+                if (int s = etf_size_enqueue(ctx, &ob, S->etf, LASPJ_KIND_ORSET, -1, dooff,
+                                             ctx->flag, &chunks))
+                    return s;
+                S->clean_words = 0;
+            }
             if (int s = etf_write_enqueue(ctx, &ob, S->etf, LASPJ_KIND_ORSET, -1, 1, dooff, dopay,
                                           ocap, chunks))
                 return s;
             break;
         }
         case Op::VALUE: {
+            S->clean_words = 0;
             // value/1 (lasp_orset.erl:67-73): the elements with a {_, false} token, as the
             // ordset image the G-Set writer gives a bit row (term_to_binary of the keys)
             LJ_HIP(ctx, launch_orset_value(ctx, &inb, cout, false));
@@ -329,10 +354,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             break;
         }
         case Op::EQUAL:
+            S->clean_words = 0;
             // equal/2 (lasp_orset.erl:136-138): ORDictA == ORDictB
             LJ_HIP(ctx, launch_equal(ctx, &lhs, &rhs, dout + o_res));
             break;
         case Op::INFLATION:
+            S->clean_words = 0;
             // is_inflation / is_strict_inflation (lasp_lattice.erl:153-161, 235-253)
             LJ_HIP(ctx, launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, dout + o_res));
             break;
