@@ -129,13 +129,17 @@ __device__ __forceinline__ uint32_t hmix(u64 k) {
     return (uint32_t)k;
 }
 
+// Slots hold ~key and ~first index, so a zeroed table is empty (one memset with the
+// kernels' other zeroed words): no real key is ~0, no index is 0xFFFFFFFF, and the first
+// index is the largest ~index (atomicMax).
 __device__ __forceinline__ void h_insert(u64* hk, uint32_t* hi, uint32_t mask, u64 key,
                                          uint32_t idx) {
     uint32_t h = hmix(key) & mask;
+    const u64 nk = ~key;
     for (;;) {
-        const u64 prev = atomicCAS(hk + h, kEmpty, key);
-        if (prev == kEmpty || prev == key) {
-            atomicMin(hi + h, idx);
+        const u64 prev = atomicCAS(hk + h, 0ull, nk);
+        if (prev == 0ull || prev == nk) {
+            atomicMax(hi + h, ~idx);
             return;
         }
         h = (h + 1) & mask;
@@ -145,13 +149,14 @@ __device__ __forceinline__ void h_insert(u64* hk, uint32_t* hi, uint32_t mask, u
 __device__ __forceinline__ uint32_t h_find(const u64* hk, const uint32_t* hi, uint32_t mask,
                                            u64 key) {
     uint32_t h = hmix(key) & mask;
+    const u64 nk = ~key;
     for (;;) {
         const u64 k = __hip_atomic_load(const_cast<u64*>(hk + h), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
-        if (k == key)
-            return __hip_atomic_load(const_cast<uint32_t*>(hi + h), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (k == kEmpty) return kNone;
+        if (k == nk)
+            return ~__hip_atomic_load(const_cast<uint32_t*>(hi + h), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0ull) return kNone;
         h = (h + 1) & mask;
     }
 }
@@ -827,13 +832,35 @@ __global__ __launch_bounds__(64) void k_list_equal(LV a, LV b, RK rk, uint8_t* o
     if (lane_id() == 0) out[r] = diff ? 0 : 1;
 }
 
+// the same spread over a (chunk, replica) grid for the bind path's few long replicas:
+// diff[r] (zeroed) gets a bit at the first difference any block sees
+__global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint32_t* diff,
+                                                         uint64_t R) {
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t n = a.n(r), nt = a.nt(r);
+        if (n != b.n(r) || nt != b.nt(r)) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(diff + r, 1u);
+            continue;
+        }
+        const u64 *KA = a.K(r), *KB = b.K(r), *TA = a.T(r), *TB = b.T(r);
+        const uint32_t *OA = a.O(r), *OB = b.O(r);
+        bool d = false;
+        const uint32_t stride = gridDim.x * 256u;
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n && !d; i += stride)
+            d = key_ord(KA[i], rk) != key_ord(KB[i], rk) || OA[i] != OB[i];
+        for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < nt && !d; t += stride)
+            d = tok_ord(TA[t], rk) != tok_ord(TB[t], rk) || ((TA[t] ^ TB[t]) & kRemoved) != 0;
+        if (__ballot(d) != 0 && lane_id() == 0) atomicOr(diff + r, 1u);
+    }
+}
+
 // is_lattice_inflation / is_lattice_strict_inflation (lasp_lattice.erl:137-161,
 // 212-215, 235-253, 277-285), spread over the grid (a 50k-entry list is 200 blocks, not
 // one wave): k_linf_insert builds, per replica, an open-addressing table of Cur's key
 // ranks -> first index (= lists:keyfind's first match; G-Set strict also Prev's keys),
 // k_linf_probe checks one Prev (and, G-Set strict, one Cur) entry per thread and ORs
 // violation / change bits into a per-replica word, k_linf_final turns them into the
-// answer.  The tables start as all-ones (kEmpty / kNone) from one memset.
+// answer.  The tables start zeroed (empty, see h_insert) by one memset with the flags.
 constexpr uint32_t kViolBit = 1, kChangedBit = 2;
 
 template <bool GSET, bool STRICT>
@@ -1831,21 +1858,24 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
 // error flag (the fused bind keeps the merge's bits and reads them with o)
 static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                             int strict, const RK& rk, uint8_t* o, bool clear_flag,
-                            const char* what) {
+                            const char* what, uint32_t** zeroed_words = nullptr) {
     const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
     const bool bcast = prev->replicas == 1 && cur->replicas != 1;
     const uint64_t R = cur->replicas;
     const uint32_t cmax = cur->cap_e > prev->cap_e ? cur->cap_e : prev->cap_e;
     const uint32_t hsize = pow2_at_least(2ull * cmax);
     const uint64_t tbytes = R * 2ull * hsize * 12ull;
-    char* base = static_cast<char*>(lscratch(ctx, tbytes + 4ull * R));
+    // [tables | flag words | R more zeroed words for the caller (zeroed_words)]
+    const uint64_t zbytes = tbytes + 4ull * R * (zeroed_words ? 2 : 1);
+    char* base = static_cast<char*>(lscratch(ctx, zbytes));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     u64* hk = reinterpret_cast<u64*>(base);
     auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
     auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
+    if (zeroed_words) *zeroed_words = flags + R;
     if (clear_flag) LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
-    LJ_HIP(ctx, hipMemsetAsync(base, 0xFF, tbytes, ctx->stream));    // kEmpty / kNone
-    LJ_HIP(ctx, hipMemsetAsync(flags, 0, 4ull * R, ctx->stream));
+    // the tables (empty = zero) and the per-replica flag words, one memset
+    LJ_HIP(ctx, hipMemsetAsync(base, 0, zbytes, ctx->stream));
     const LV P = view(prev), C = view(cur);
     const dim3 grid(cmax ? (cmax + 255) / 256 : 1, (unsigned)(R < 65535 ? R : 65535));
     const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
@@ -1934,24 +1964,37 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
     const uint64_t R = cur->replicas;
     LGuard g(ctx);
-    // one device block: equality bytes, inflation bytes, the merge's sizes
-    const uint64_t o_need = (2 * R + 7) & ~7ull, bytes = o_need + 8 * R;
+    // one device block: inflation bytes, the merge's sizes
+    const uint64_t o_need = (R + 7) & ~7ull, bytes = o_need + 8 * R;
     void* dev = nullptr;
     if (laspj::dev_alloc(ctx, bytes, &dev) != hipSuccess) {
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "list_bind: status bytes");
     }
-    uint8_t* eq = static_cast<uint8_t*>(dev);
-    auto* need = reinterpret_cast<uint32_t*>(eq + o_need);
+    uint8_t* infd = static_cast<uint8_t*>(dev);
+    auto* need = reinterpret_cast<uint32_t*>(infd + o_need);
     std::vector<uint8_t> inf(R, 0);
-    std::vector<uint32_t> h(2 * R);
-    // `Value0 =:= Value`, Type:merge and is_inflation(Value0, Merged) enqueued back to back
-    // (the merge sized from the inputs' known counts), then ONE synchronisation
-    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, eq, "list_bind");
-    if (s == LASPJ_OK) s = inflation_launch(ctx, cur, dst, 0, rk, eq + R, false, "list_bind");
+    std::vector<uint32_t> h(2 * R), diff(R, 0);
+    // Type:merge and is_inflation(Value0, Merged) enqueued back to back (the merge sized
+    // from the inputs' known counts), `Value0 =:= Value` over the grid into words the
+    // inflation's memset zeroed, then ONE synchronisation
+    uint32_t* dd = nullptr;
+    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind");
+    if (s == LASPJ_OK)
+        s = inflation_launch(ctx, cur, dst, 0, rk, infd, false, "list_bind", &dd);
+    if (s == LASPJ_OK) {
+        const uint32_t cmax = cur->cap_e > val->cap_e ? cur->cap_e : val->cap_e;
+        const uint32_t tmax = cur->cap_t > val->cap_t ? cur->cap_t : val->cap_t;
+        const uint32_t span = cmax > tmax ? cmax : tmax;
+        const unsigned gx = (unsigned)std::min<uint64_t>((span + 2047) / 2048 + 1, 1024);
+        hipLaunchKernelGGL(k_list_equal_grid, dim3(gx, (unsigned)(R < 65535 ? R : 65535)),
+                           dim3(256), 0, ctx->stream, view(cur), view(val), rk, dd, R);
+        s = hipGetLastError() == hipSuccess ? LASPJ_OK
+                                            : fail(ctx, LASPJ_E_DEVICE, "list_bind: launch");
+    }
     if (s == LASPJ_OK) {
         uint32_t f = 0;
-        const laspj::ReadPiece rp[4] = {{status, eq, R}, {inf.data(), eq + R, R},
+        const laspj::ReadPiece rp[4] = {{diff.data(), dd, 4ull * R}, {inf.data(), infd, R},
                                         {h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
         const hipError_t e = laspj::readback(ctx, rp, 4);
         s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s",
@@ -1965,7 +2008,7 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     }
     set_known(dst, h.data(), R);
     // status: 0 = cur =:= val (no-op), 1 = the merge inflates cur (written), 2 = it does not
-    for (uint64_t i = 0; i < R; ++i) status[i] = status[i] ? 0 : (inf[i] ? 1 : 2);
+    for (uint64_t i = 0; i < R; ++i) status[i] = !diff[i] ? 0 : (inf[i] ? 1 : 2);
     return LASPJ_OK;
 }
 
@@ -1999,7 +2042,7 @@ int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch*
         return [&, hg](char* base) {
             u64* hk = reinterpret_cast<u64*>(base);
             auto* hi = reinterpret_cast<uint32_t*>(base + R * hsize * 8ull);
-            hipMemsetAsync(base, 0xFF, hbytes, ctx->stream);        // kEmpty / kNone
+            hipMemsetAsync(base, 0, hbytes, ctx->stream);           // empty tables
             hipLaunchKernelGGL((k_isect_hash<G>), hg, dim3(256), 0, ctx->stream, Rr, rk, hk, hi,
                                hsize, R);
             return PIsect<G>{L, Rr, rk, hk, hi, hsize};
