@@ -154,7 +154,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         batches walked by the scalar unit (the lanes
                                         find element starts by default), 7 = no element
                                         batches for many-token dictionaries (one element
-                                        at a time)                                       */
+                                        at a time), 8 = never the item decoder (many-token
+                                        dictionaries, at least one payload per CU: one
+                                        block per payload, one thread per element or
+                                        record), 9 = the item decoder whatever the
+                                        number of payloads                               */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

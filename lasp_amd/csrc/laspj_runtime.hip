@@ -340,8 +340,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_etf = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_READ:
-            if (value < 0 || value > 7)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..7");
+            if (value < 0 || value > 9)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..9");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_SEG:
