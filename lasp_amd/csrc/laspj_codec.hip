@@ -3533,7 +3533,8 @@ __device__ __forceinline__ u64 gs_elem_len(const uint8_t* buf, uint32_t o, uint3
 // or out of order (UNKNOWN_TERM).
 __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, const u64* offs,
                                                       uint64_t R, GsTabs g, int tag, int vers,
-                                                      u64* words, uint64_t W, int32_t* status) {
+                                                      u64* words, uint64_t W, int32_t* status,
+                                                      const uint32_t* redo) {
     __shared__ uint32_t s_o[kGChunk], s_l[kGChunk];
     __shared__ u64 s_h[4];
     __shared__ __attribute__((aligned(16))) uint8_t win[kGWin + 16];
@@ -3543,7 +3544,11 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
     // words fit (64 lanes setting bits of the same word would serialise on one global
     // atomic), else straight into the batch with global atomics
     const bool lw = W <= kGWords;
-    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+    // with `redo` (the block parser's fallback, W <= kGWords): the replicas listed there,
+    // whose words are all rewritten below
+    const uint64_t count = redo ? (uint64_t)redo[0] : R;
+    for (uint64_t i = blockIdx.x; i < count; i += gridDim.x) {
+        const uint64_t rep = redo ? (uint64_t)redo[1 + i] : i;
         const uint8_t* p = payload + offs[rep];
         const u64 n = offs[rep + 1] - offs[rep];
         u64* w = words + rep * W;
@@ -3733,6 +3738,231 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
         __syncthreads();
         if (lw)
             for (uint32_t x = lane; x < W; x += 64) w[x] = s_w[x];
+    }
+}
+
+// ---- integer G-Set payloads, one block per payload (round 4)
+//
+// A G-Set of integers is `131 108 <n:4>` then n images SMALL_INTEGER_EXT (97 v, 2 bytes)
+// or INTEGER_EXT (98 <v:4>, 5 bytes), then 106.  Where an element starts depends on every
+// earlier tag, but only through an offset of 0..4 bytes: a block stages 4 KiB, thread t
+// takes bytes [16 t, 16 t + 16) and walks them from each of the 5 possible entry offsets
+// (97: +2, 98: +5, 106: the list's end, anything else: not this kernel's case), which gives
+// a map entry -> exit offset into the next thread's bytes; a block scan composes the maps
+// (thread 0 enters at the cursor, so every prefix is a constant) and hands each thread
+// its real entry.  Then every thread walks its bytes once more and takes its elements:
+// value -> slot and rank through the integer value table, ranks strictly ascending (across
+// threads through their first and last ranks), the bit ORed into the replica's LDS words.
+// The payload must end in 106 on its last byte after exactly n elements.  Anything else —
+// another tag, a value outside the table, a non-minimal image, a rank out of order,
+// truncation, STRING_EXT — puts the payload on the redo list, which the wave decoder
+// (k_gset_etf_read) takes, rewriting the words and giving the status; so both are the wave
+// decoder's by construction.
+constexpr uint32_t kGPW = 4096;                // window bytes (16 per thread)
+
+// exit of the walk over a thread's 16 bytes from entry offset p (0..15): 0..4 into the next
+// thread's bytes, 6: the list's closing 106, 7: a tag this kernel does not take (or past
+// the payload); masks: bit i = byte 16 t + i is that tag (i < 20)
+__device__ __forceinline__ uint32_t gs_walk16(uint32_t m97, uint32_t m98, uint32_t m106,
+                                              uint32_t p) {
+    while (p < 16u) {
+        if ((m97 >> p) & 1u) p += 2u;
+        else if ((m98 >> p) & 1u) p += 5u;
+        else return (m106 >> p) & 1u ? 6u : 7u;
+    }
+    return p - 16u;
+}
+
+// maps entry -> exit as 8 fields of 4 bits (entries 0..4, 6 and 7 stay); a then b
+__device__ __forceinline__ uint32_t gs_compose(uint32_t a, uint32_t b) {
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < 8; ++s) h |= ((b >> (4u * ((a >> (4u * s)) & 0xFu))) & 0xFu) << (4u * s);
+    return h;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* payload, u64 total,
+                                                              const u64* offs, uint64_t R,
+                                                              GsTabs g, int tag, int vers,
+                                                              u64* words, uint64_t W,
+                                                              int32_t* status, uint32_t* redo) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kGPW + 32];
+    __shared__ u64 s_w[kGWords];
+    __shared__ uint32_t firstrk[kBlock], lastrk[kBlock];
+    __shared__ uint32_t wt[kBlock / 64], sc[8];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (tid < 4) reinterpret_cast<uint32_t*>(buf + kGPW + 16)[tid] = 0u;
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64 base = offs[rep], aend = offs[rep + 1], len = aend - base;
+        for (uint32_t x = tid; x < W; x += kBlock) s_w[x] = 0ull;
+        bool ok = true, fin = false;
+        uint32_t x = 0, n = 0;
+        {
+            const uint8_t* p = payload + base;
+            if (tag >= 0) {
+                ok = len >= 2 && p[0] == (uint8_t)tag && p[1] == (uint8_t)vers;
+                x = 2;
+            }
+            if (ok && len == x + 2 && p[x] == 131 && p[x + 1] == 106) {
+                fin = true;                                        // []
+            } else if (ok && len >= x + 7 && p[x] == 131 && p[x + 1] == 108) {
+                n = ((uint32_t)p[x + 2] << 24) | ((uint32_t)p[x + 3] << 16) |
+                    ((uint32_t)p[x + 4] << 8) | p[x + 5];
+                x += 6;
+                ok = n >= 1;
+            } else {
+                ok = false;
+            }
+        }
+        uint32_t got = 0, prev_rank = 0;
+        bool have_prev = false;
+        while (ok && !fin) {
+            const u64 lo = (base + x) & ~15ull;
+            const uint32_t x0 = (uint32_t)(base + x - lo);
+            const uint32_t nst = (uint32_t)min((u64)(kGPW + 16), total - lo);
+            const uint32_t hi = (uint32_t)min((u64)nst, aend - lo);
+            __syncthreads();
+            for (uint32_t v = tid; v < (kGPW + 16) / 16; v += kBlock) {
+                u32x4 q = {0u, 0u, 0u, 0u};
+                if (16u * v + 16u <= nst) {
+                    q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(payload + lo) + v);
+                } else if (16u * v < nst) {
+                    uint32_t wv4[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t b = 16u * v; b < nst; ++b)
+                        wv4[(b >> 2) & 3u] |= (uint32_t)payload[lo + b] << (8u * (b & 3u));
+                    q = u32x4{wv4[0], wv4[1], wv4[2], wv4[3]};
+                }
+                reinterpret_cast<u32x4*>(buf)[v] = q;
+            }
+            if (tid == 0) sc[0] = sc[1] = sc[2] = 0u;
+            __syncthreads();
+            // tag masks over bytes [16 t, 16 t + 20), only bytes of this payload
+            const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+            uint32_t m97 = 0, m98 = 0, m106 = 0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const uint32_t v = b32[4 * tid + i];
+                m97 |= zbytes4(v ^ 0x61616161u) << (4 * i);
+                m98 |= zbytes4(v ^ 0x62626262u) << (4 * i);
+                m106 |= zbytes4(v ^ 0x6A6A6A6Au) << (4 * i);
+            }
+            {
+                const int32_t lim = (int32_t)hi - 16 * (int32_t)tid;
+                const uint32_t keep = lim <= 0 ? 0u : lim >= 20 ? 0xFFFFFu : (1u << lim) - 1u;
+                m97 &= keep;
+                m98 &= keep;
+                m106 &= keep;
+            }
+            // this thread's map; thread 0 enters at the cursor (a constant map)
+            uint32_t mp = 0x76700000u;                  // fields 5 -> 7, 6 -> 6, 7 -> 7
+            if (tid == 0) {
+                const uint32_t e = gs_walk16(m97, m98, m106, x0);
+                mp |= e * 0x11111u;
+            } else {
+#pragma unroll
+                for (uint32_t s = 0; s < 5; ++s) mp |= gs_walk16(m97, m98, m106, s) << (4u * s);
+            }
+            // inclusive composition scan, then the exclusive prefix = this thread's entry
+            uint32_t inc = mp;
+#pragma unroll
+            for (uint32_t off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if (lane >= off) inc = gs_compose(y, inc);
+            }
+            if (lane == 63) wt[wv] = inc;
+            __syncthreads();
+            uint32_t pre = 0x76543210u;                 // identity
+            for (uint32_t i = 0; i < wv; ++i) pre = gs_compose(pre, wt[i]);
+            uint32_t exc = __shfl_up(inc, 1, 64);
+            if (lane == 0) exc = pre;
+            else if (wv) exc = gs_compose(pre, exc);
+            const uint32_t fin_state = [&] {
+                uint32_t f = 0x76543210u;
+                for (uint32_t i = 0; i < kBlock / 64; ++i) f = gs_compose(f, wt[i]);
+                return f & 0xFu;
+            }();
+            uint32_t p = tid == 0 ? x0 : 16u * tid + (exc & 0xFu);
+            const bool walk = tid == 0 || (exc & 0xFu) <= 4u;
+            // take the elements
+            bool bad = false;
+            uint32_t cnt = 0, first = 0, last = 0;
+            if (walk) {
+                const uint32_t send = 16u * tid + 16u;
+                while (p < send) {
+                    const uint32_t tg = buf[p];
+                    if (tg == 106) {
+                        sc[1] = p + 1u;                   // one past the closing nil
+                        break;
+                    }
+                    int64_t v;
+                    if (tg == 97 && p + 2u <= hi) {
+                        v = buf[p + 1];
+                        p += 2u;
+                    } else if (tg == 98 && p + 5u <= hi) {
+                        v = (int32_t)(((uint32_t)buf[p + 1] << 24) | ((uint32_t)buf[p + 2] << 16) |
+                                      ((uint32_t)buf[p + 3] << 8) | buf[p + 4]);
+                        bad |= v >= 0 && v <= 255;        // not minimal: no dictionary image
+                        p += 5u;
+                    } else {
+                        bad = true;
+                        break;
+                    }
+                    const int64_t xv = v - g.ilo;
+                    const u64 t = xv >= 0 && xv < (int64_t)g.in ? g.itab[xv] : 0ull;
+                    if (!(uint32_t)t) {
+                        bad = true;
+                        break;
+                    }
+                    const uint32_t slot = (uint32_t)t - 1u, rk = (uint32_t)(t >> 32);
+                    if (cnt == 0) first = rk;
+                    else bad |= rk <= last;
+                    last = rk;
+                    ++cnt;
+                    atomicOr(&s_w[slot >> 6], 1ull << (slot & 63u));
+                }
+            }
+            firstrk[tid] = cnt ? first : 0xFFFFFFFFu;
+            lastrk[tid] = cnt ? last : 0xFFFFFFFFu;
+            atomicAdd(&sc[0], cnt);
+            if (cnt) atomicMax(&sc[2], tid);
+            __syncthreads();
+            if (cnt) {
+                if (tid == 0) bad |= have_prev && first <= prev_rank;
+                else bad |= lastrk[tid - 1] == 0xFFFFFFFFu && firstrk[tid - 1] == 0xFFFFFFFFu
+                                ? true : first <= lastrk[tid - 1];
+            }
+            const bool anybad = __syncthreads_or(bad);
+            const uint32_t wcnt = sc[0];
+            if (anybad || fin_state == 7u || got + wcnt > n) {
+                ok = false;
+                break;
+            }
+            got += wcnt;
+            if (wcnt) {
+                prev_rank = lastrk[sc[2]];
+                have_prev = true;
+            }
+            if (fin_state == 6u) {
+                ok = sc[1] == hi && lo + hi == aend && got == n;
+                fin = true;
+            } else {
+                if (lo + kGPW >= aend) { ok = false; break; }
+                x = (uint32_t)(lo + kGPW + fin_state - base);
+            }
+        }
+        __syncthreads();
+        u64* w = words + rep * W;
+        for (uint32_t i = tid; i < W; i += kBlock) w[i] = s_w[i];
+        if (tid == 0) {
+            if (ok) {
+                status[rep] = LASPJ_DEC_OK;
+            } else {
+                status[rep] = LASPJ_DEC_MALFORMED;      // rewritten by the redo pass
+                const uint32_t i = atomicAdd(redo, 1u);
+                redo[1 + i] = (uint32_t)rep;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -3936,16 +4166,38 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
                         (unsigned long long)i);
     if (off[R] > payload->bytes)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
-    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
+    const uint64_t cap = (uint64_t)ctx->cus * 64;
+    const uint8_t* pay = static_cast<const uint8_t*>(payload->dev);
+    const u64* offs = static_cast<const u64*>(offsets->dev);
+    // integer dictionaries: the block parser first (knob 8: never), the wave decoder over
+    // its redo list; every replica's words are written by one of them
+    if (d->gs_itab && b->words_per_replica <= kGWords && ctx->tune_etf_read != 8 &&
+        !((uintptr_t)pay & 15u)) {
+        if (int s = reserve_scratch(ctx, 4ull * (R + 1))) return s;
+        uint32_t* redo = static_cast<uint32_t*>(ctx->scratch);
+        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        hipLaunchKernelGGL(k_gset_etf_read_par,
+                           dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 16))),
+                           dim3(kBlock), 0, ctx->stream, pay, (u64)payload->bytes, offs, R, tabs,
+                           tag, vers, reinterpret_cast<u64*>(b->dev), b->words_per_replica,
+                           static_cast<int32_t*>(status->dev), redo);
+        LJ_LAUNCHED(ctx);
+        hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 4))),
+                           dim3(64), 0, ctx->stream, pay, offs, R, tabs, tag, vers,
+                           reinterpret_cast<u64*>(b->dev), b->words_per_replica,
+                           static_cast<int32_t*>(status->dev), (const uint32_t*)redo);
+        LJ_LAUNCHED(ctx);
+        return LASPJ_OK;
+    }
+    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     // one wave per replica and a latency-bound extent walk: as many waves as LDS allows
     // (6 KiB each: ~25 per CU)
-    const uint64_t cap = (uint64_t)ctx->cus * 64;
     hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, cap))),
-                       dim3(64), 0, ctx->stream, static_cast<const uint8_t*>(payload->dev),
-                       static_cast<const u64*>(offsets->dev), R, tabs, tag, vers, reinterpret_cast<u64*>(b->dev),
-                       b->words_per_replica, static_cast<int32_t*>(status->dev));
+                       dim3(64), 0, ctx->stream, pay, offs, R, tabs, tag, vers,
+                       reinterpret_cast<u64*>(b->dev), b->words_per_replica,
+                       static_cast<int32_t*>(status->dev), (const uint32_t*)nullptr);
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }

@@ -1235,6 +1235,90 @@ def test_gpu_gset_from_binary_long_payloads():
 
 
 @pytest.mark.gpu
+def test_gpu_gset_block_parser_matches_wave_decoder():
+    """Integer G-Sets (the block parser's case: SMALL_INTEGER_EXT / INTEGER_EXT images,
+    negative and large values, payloads from a few bytes to several 4 KiB windows) and
+    3000 corrupted copies — tags flipped between 97 / 98 / 106, values nudged, bytes cut or
+    inserted at and around window edges, two elements swapped, a duplicate, a
+    non-minimal INTEGER_EXT, a value outside the dictionary: the block parser (with the
+    wave decoder over its redo list, knob 0) and the wave decoder alone (knob 8) give the
+    same status and the same words for every payload, and the clean payloads decode to
+    the host encoder's words."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    rng = random.Random(2024)
+    T = etf.DT_GSET_TAG
+    # (a value span the dictionary's integer table covers: at most 65536)
+    pool = list(range(-40, 3000, 1)) + [30000, 60000]
+    states = [[], [0], [255], [256], [-1], list(range(256)), list(range(200, 2200)),
+              list(range(-40, 3000)), [-40, 60000]]
+    for _ in range(120):
+        states.append(sorted(rng.sample(pool, rng.choice([1, 3, 50, 400, 1500]))))
+    ctx, dom, E, d = _gset_decode_setup(states)
+    base = [oetf.to_binary(T, 1, s) if rng.random() < 0.5 else oetf.term_to_binary(s)
+            for s in states]
+    tags = [T if b[0] == T else -1 for b in base]
+    blobs = [b for b, t in zip(base, tags) if t == T]
+    for _ in range(3000):
+        b = bytearray(rng.choice(blobs))
+        kind = rng.randrange(7)
+        if kind == 0 and len(b) > 8:
+            b[rng.randrange(8, len(b))] = rng.choice([97, 98, 106, 0, 255])
+        elif kind == 1 and len(b) > 8:
+            i = rng.randrange(8, len(b))
+            b[i] = (b[i] + rng.choice([1, 255])) & 0xFF
+        elif kind == 2:
+            cut = rng.choice([4096, 4097, 4100, 8192, 8195, rng.randrange(len(b) + 1)])
+            del b[min(cut, len(b)):]
+        elif kind == 3:
+            pos = rng.choice([4094, 4095, 4096, rng.randrange(len(b) + 1)])
+            pos = min(pos, len(b))
+            b[pos:pos] = rng.choice([bytes([97, 5]), bytes([98, 0, 0, 0, 7]), b"\0", bytes([106])])
+        elif kind == 4 and len(b) > 40:
+            j = rng.randrange(8, len(b) - 20)
+            while j < len(b) and b[j] not in (97, 98):
+                j += 1
+            del b[j:j + rng.randint(1, 6)]
+        elif kind == 5:
+            b = bytearray(oetf.to_binary(T, 1, [])) if rng.random() < 0.1 else b
+            s = sorted(rng.sample(pool, rng.randint(2, 300)))
+            k = rng.randrange(len(s) - 1)
+            s[k], s[k + 1] = s[k + 1], s[k]
+            b = bytearray(oetf.to_binary(T, 1, s))
+        else:
+            v = rng.randrange(256)
+            s = sorted(set(rng.sample(pool, rng.randint(1, 200))) - {v})
+            b = bytearray(oetf.to_binary(T, 1, s))
+            at = b.index(bytes([108])) + 5
+            b[at:at] = bytes([98, 0, 0, 0, v])      # a non-minimal image
+            b[4:8] = (len(s) + 1).to_bytes(4, "big")
+        blobs.append(bytes(b))
+    res = {}
+    for knob in (0, 8):
+        pay, offs = _upload_payloads(ctx, blobs)
+        bt = ctx.gset_batch(len(blobs), E)
+        ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
+        try:
+            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+        finally:
+            ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
+        res[knob] = (st, bt.download())
+    assert np.array_equal(res[0][0], res[8][0]), np.nonzero(res[0][0] != res[8][0])[0][:10]
+    assert np.array_equal(res[0][1], res[8][1])
+    nb = sum(1 for t in tags if t == T)
+    assert (res[0][0][:nb] == 0).all()
+    clean = [s for s, t in zip(states, tags) if t == T]
+    assert np.array_equal(res[0][1][:nb], dom.encode_gset(clean, E))
+    # untagged payloads too
+    untag = [b for b, t in zip(base, tags) if t < 0]
+    if untag:
+        pay, offs = _upload_payloads(ctx, untag)
+        bt = ctx.gset_batch(len(untag), E)
+        assert (bt.etf_decode(d, pay, offs, tag=-1, vers=1) == 0).all()
+        assert np.array_equal(bt.download(), dom.encode_gset([s for s, t in zip(states, tags) if t < 0], E))
+
+
+@pytest.mark.gpu
 def test_gpu_gset_from_binary_fuzz():
     """2000 corrupted G-Set payloads against the oracle's binary_to_term: payloads it
     decodes to an ordset of dictionary terms decode OK to the host encoder's words; other
