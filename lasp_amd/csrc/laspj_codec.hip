@@ -2980,10 +2980,12 @@ struct ItemLds {
     uint8_t ik[kIT];           // 0 not an item, 1 element, 2 record (true), 3 record (false)
     uint8_t iown[kIT];         // owning element (window index), 0xFF none, 0xFE dropped
     uint8_t im[kIT];           // element: its count
+    uint32_t islot[kIT];       // element: its slot
+    uint32_t ikey[kIT];        // element: its bucket word | shift << 8
     uint16_t elist[kIE];       // element -> item
     uint16_t ecj[kIE];         // element -> compacted index
     int32_t erk[kIE];
-    uint32_t eslot[kIE], ekey[kIE], ecnt[kIE], em[kIE];
+    uint32_t eslot[kIE], ekey[kIE], em[kIE];
     u64 pm[kIE], tm[kIE];      // presence / true bits by token slot
     uint32_t sc[8];
 };
@@ -3170,12 +3172,14 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_items(
                 uint8_t kind = 0;
                 if (rk >= 0 && s + hl + 4u <= hi) {
                     const uint32_t m = __builtin_bswap32(word_at(S.buf, s + hl));
-                    const uint32_t cnt = tabs.desc[rk].w;
-                    if (m >= 1u && m <= cnt && cnt <= 64u) {
+                    const uint4 ds = tabs.desc[rk];
+                    if (m >= 1u && m <= ds.w && ds.w <= 64u) {
                         kind = 1;
                         S.irk[i] = (int32_t)rk;
                         S.im[i] = (uint8_t)m;
                         S.iend[i] = (uint16_t)(s + hl + 4u);
+                        S.islot[i] = ds.x;
+                        S.ikey[i] = ds.z;
                     }
                 }
                 S.ik[i] = kind;
@@ -3195,14 +3199,11 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_items(
                 const int32_t own = (int32_t)(eb + f0 + (h ? f1 : 0u)) - 1;
                 S.iown[i] = own < 0 ? 0xFF : own < (int32_t)kIE ? (uint8_t)own : 0xFE;
                 if ((h ? f1 : f0) && own < (int32_t)kIE) {
-                    const int32_t rk = S.irk[i];
-                    const uint4 ds = tabs.desc[rk];
                     S.elist[own] = (uint16_t)i;
-                    S.erk[own] = rk;
+                    S.erk[own] = S.irk[i];
                     S.em[own] = S.im[i];
-                    S.eslot[own] = ds.x;
-                    S.ekey[own] = ds.z;
-                    S.ecnt[own] = ds.w;
+                    S.eslot[own] = S.islot[i];
+                    S.ekey[own] = S.ikey[i];
                 }
             }
             __syncthreads();
@@ -3219,9 +3220,14 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_items(
                     const uint32_t key = S.ekey[l], e = S.eslot[l];
                     const uint32_t kw = 4u * (key & 0xFFu), ksh = key >> 8;
                     const uint32_t bk = (word_at(S.buf, q + kw) >> ksh) & (kIBuckets - 1u);
+                    // (btab holds term ranks below the element's token count only)
                     const uint32_t k = btab[(u64)S.erk[l] * kIBuckets + bk];
-                    bool v = k < S.ecnt[l] && q + RL + 7u <= hi;
-                    if (v) v = rec_match(S.buf, q, RL, d.rec_pad + ((u64)e * RK + k) * RS);
+                    bool v = k < 64u && q + RL + 7u <= hi;
+                    uint32_t slot = 0;
+                    if (v) {
+                        slot = d.tok_order[64ull * e + k];        // issued beside the template
+                        v = rec_match(S.buf, q, RL, d.rec_pad + ((u64)e * RK + k) * RS);
+                    }
                     if (v) {
                         const uint32_t fo = q + RL;
                         uint32_t fn;
@@ -3230,7 +3236,6 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_items(
                             kind = (uint8_t)(1u + fk);
                             S.irk[i] = (int32_t)k;
                             S.iend[i] = (uint16_t)(fo + fn);
-                            const uint32_t slot = d.tok_order[64ull * e + k];
                             atomicOr(&S.pm[l], 1ull << (slot & 63u));
                             if (fk == 1u) atomicOr(&S.tm[l], 1ull << (slot & 63u));
                         }
