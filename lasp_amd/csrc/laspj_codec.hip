@@ -3786,6 +3786,20 @@ __device__ __forceinline__ uint32_t gs_compose(uint32_t a, uint32_t b) {
     return h;
 }
 
+__device__ __forceinline__ u32x4 gs_piece(const uint8_t* payload, u64 lo, uint32_t nst,
+                                          uint32_t v) {
+    u32x4 q = {0u, 0u, 0u, 0u};
+    if (16u * v + 16u <= nst) {
+        q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(payload + lo) + v);
+    } else if (16u * v < nst) {
+        uint32_t w4[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t b = 16u * v; b < nst; ++b)
+            w4[(b >> 2) & 3u] |= (uint32_t)payload[lo + b] << (8u * (b & 3u));
+        q = u32x4{w4[0], w4[1], w4[2], w4[3]};
+    }
+    return q;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* payload, u64 total,
                                                               const u64* offs, uint64_t R,
                                                               GsTabs g, int tag, int vers,
@@ -3797,29 +3811,20 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
     __shared__ uint32_t wt[kBlock / 64], sc[8];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (tid < 4) reinterpret_cast<uint32_t*>(buf + kGPW + 16)[tid] = 0u;
+    // a payload's first window (its head on) comes from registers loaded while the
+    // previous payload decoded: 257 pieces of 16 bytes, thread 0 holds two
+    u32x4 pf0 = {0u, 0u, 0u, 0u}, pf1 = {0u, 0u, 0u, 0u};
+    if (blockIdx.x < R) {
+        const u64 l0 = offs[blockIdx.x] & ~15ull;
+        const uint32_t n0 = (uint32_t)min((u64)(kGPW + 16), total - l0);
+        pf0 = gs_piece(payload, l0, n0, tid);
+        if (tid == 0) pf1 = gs_piece(payload, l0, n0, kBlock);
+    }
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64 base = offs[rep], aend = offs[rep + 1], len = aend - base;
         for (uint32_t x = tid; x < W; x += kBlock) s_w[x] = 0ull;
-        bool ok = true, fin = false;
-        uint32_t x = 0, n = 0;
-        {
-            const uint8_t* p = payload + base;
-            if (tag >= 0) {
-                ok = len >= 2 && p[0] == (uint8_t)tag && p[1] == (uint8_t)vers;
-                x = 2;
-            }
-            if (ok && len == x + 2 && p[x] == 131 && p[x + 1] == 106) {
-                fin = true;                                        // []
-            } else if (ok && len >= x + 7 && p[x] == 131 && p[x + 1] == 108) {
-                n = ((uint32_t)p[x + 2] << 24) | ((uint32_t)p[x + 3] << 16) |
-                    ((uint32_t)p[x + 4] << 8) | p[x + 5];
-                x += 6;
-                ok = n >= 1;
-            } else {
-                ok = false;
-            }
-        }
-        uint32_t got = 0, prev_rank = 0;
+        bool ok = true, fin = false, head = true;
+        uint32_t x = 0, n = 0, got = 0, prev_rank = 0;
         bool have_prev = false;
         while (ok && !fin) {
             const u64 lo = (base + x) & ~15ull;
@@ -3827,20 +3832,48 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
             const uint32_t nst = (uint32_t)min((u64)(kGPW + 16), total - lo);
             const uint32_t hi = (uint32_t)min((u64)nst, aend - lo);
             __syncthreads();
-            for (uint32_t v = tid; v < (kGPW + 16) / 16; v += kBlock) {
-                u32x4 q = {0u, 0u, 0u, 0u};
-                if (16u * v + 16u <= nst) {
-                    q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(payload + lo) + v);
-                } else if (16u * v < nst) {
-                    uint32_t wv4[4] = {0u, 0u, 0u, 0u};
-                    for (uint32_t b = 16u * v; b < nst; ++b)
-                        wv4[(b >> 2) & 3u] |= (uint32_t)payload[lo + b] << (8u * (b & 3u));
-                    q = u32x4{wv4[0], wv4[1], wv4[2], wv4[3]};
+            if (head) {
+                reinterpret_cast<u32x4*>(buf)[tid] = pf0;
+                if (tid == 0) reinterpret_cast<u32x4*>(buf)[kBlock] = pf1;
+                const uint64_t nx = rep + gridDim.x;
+                if (nx < R) {
+                    const u64 l1 = offs[nx] & ~15ull;
+                    const uint32_t n1 = (uint32_t)min((u64)(kGPW + 16), total - l1);
+                    pf0 = gs_piece(payload, l1, n1, tid);
+                    if (tid == 0) pf1 = gs_piece(payload, l1, n1, kBlock);
                 }
-                reinterpret_cast<u32x4*>(buf)[v] = q;
+            } else {
+                for (uint32_t v = tid; v < (kGPW + 16) / 16; v += kBlock)
+                    reinterpret_cast<u32x4*>(buf)[v] = gs_piece(payload, lo, nst, v);
             }
             if (tid == 0) sc[0] = sc[1] = sc[2] = 0u;
             __syncthreads();
+            uint32_t p0 = x0;
+            if (head) {
+                // [tag vers] 131 108 <n:4> (131 106: []), read from the window
+                head = false;
+                uint32_t h = x0;
+                if (tag >= 0) {
+                    ok = len >= 2 && buf[h] == (uint8_t)tag && buf[h + 1] == (uint8_t)vers;
+                    h += 2;
+                }
+                const u64 hl = h - x0;
+                if (ok && len == hl + 2 && buf[h] == 131 && buf[h + 1] == 106) {
+                    fin = true;
+                    break;
+                }
+                if (!(ok && len >= hl + 7 && buf[h] == 131 && buf[h + 1] == 108)) {
+                    ok = false;
+                    break;
+                }
+                n = ((uint32_t)buf[h + 2] << 24) | ((uint32_t)buf[h + 3] << 16) |
+                    ((uint32_t)buf[h + 4] << 8) | buf[h + 5];
+                if (n == 0) {
+                    ok = false;
+                    break;
+                }
+                p0 = h + 6;
+            }
             // tag masks over bytes [16 t, 16 t + 20), only bytes of this payload
             const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
             uint32_t m97 = 0, m98 = 0, m106 = 0;
@@ -3858,16 +3891,19 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
                 m98 &= keep;
                 m106 &= keep;
             }
-            // this thread's map; thread 0 enters at the cursor (a constant map)
+            // this thread's map: before the cursor's thread t0 every entry goes to 5 (no
+            // element yet); t0 enters at the cursor (a constant map), so every prefix from
+            // t0 on is a constant
+            const uint32_t t0 = p0 >> 4;
             uint32_t mp = 0x76700000u;                  // fields 5 -> 7, 6 -> 6, 7 -> 7
-            if (tid == 0) {
-                const uint32_t e = gs_walk16(m97, m98, m106, x0);
-                mp |= e * 0x11111u;
+            if (tid < t0) {
+                mp = 0x55555555u;
+            } else if (tid == t0) {
+                mp |= gs_walk16(m97, m98, m106, p0 & 15u) * 0x11111u;
             } else {
 #pragma unroll
-                for (uint32_t s = 0; s < 5; ++s) mp |= gs_walk16(m97, m98, m106, s) << (4u * s);
+                for (uint32_t s2 = 0; s2 < 5; ++s2) mp |= gs_walk16(m97, m98, m106, s2) << (4u * s2);
             }
-            // inclusive composition scan, then the exclusive prefix = this thread's entry
             uint32_t inc = mp;
 #pragma unroll
             for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -3881,60 +3917,84 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
             uint32_t exc = __shfl_up(inc, 1, 64);
             if (lane == 0) exc = pre;
             else if (wv) exc = gs_compose(pre, exc);
-            const uint32_t fin_state = [&] {
-                uint32_t f = 0x76543210u;
-                for (uint32_t i = 0; i < kBlock / 64; ++i) f = gs_compose(f, wt[i]);
-                return f & 0xFu;
-            }();
-            uint32_t p = tid == 0 ? x0 : 16u * tid + (exc & 0xFu);
-            const bool walk = tid == 0 || (exc & 0xFu) <= 4u;
-            // take the elements
+            uint32_t fin_state = 0x76543210u;
+            for (uint32_t i = 0; i < kBlock / 64; ++i) fin_state = gs_compose(fin_state, wt[i]);
+            fin_state &= 0xFu;
+            // this thread's element starts (bit i: byte 16 t + i), from its entry
             bool bad = false;
-            uint32_t cnt = 0, first = 0, last = 0;
-            if (walk) {
-                const uint32_t send = 16u * tid + 16u;
-                while (p < send) {
-                    const uint32_t tg = buf[p];
-                    if (tg == 106) {
-                        sc[1] = p + 1u;                   // one past the closing nil
-                        break;
+            uint32_t sm = 0;
+            {
+                const bool walk = tid == t0 || (tid > t0 && (exc & 0xFu) <= 4u);
+                uint32_t q = tid == t0 ? (p0 & 15u) : (exc & 0xFu);
+                if (walk) {
+                    while (q < 16u) {
+                        if ((m97 >> q) & 1u) {
+                            sm |= 1u << q;
+                            q += 2u;
+                        } else if ((m98 >> q) & 1u) {
+                            sm |= 1u << q;
+                            q += 5u;
+                        } else {
+                            if ((m106 >> q) & 1u) sc[1] = 16u * tid + q + 1u;   // one past the nil
+                            else bad = true;
+                            break;
+                        }
                     }
+                }
+            }
+            // the elements: every value-table load issued before any is used
+            const uint32_t cnt = (uint32_t)__popc(sm);
+            u64 tv[8];
+            bool vok[8];
+            {
+                uint32_t m = sm;
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t q = m ? (uint32_t)__ffs(m) - 1u : 0u;
+                    m &= m - 1u;
+                    const uint32_t pp = 16u * tid + q;
                     int64_t v;
-                    if (tg == 97 && p + 2u <= hi) {
-                        v = buf[p + 1];
-                        p += 2u;
-                    } else if (tg == 98 && p + 5u <= hi) {
-                        v = (int32_t)(((uint32_t)buf[p + 1] << 24) | ((uint32_t)buf[p + 2] << 16) |
-                                      ((uint32_t)buf[p + 3] << 8) | buf[p + 4]);
-                        bad |= v >= 0 && v <= 255;        // not minimal: no dictionary image
-                        p += 5u;
+                    bool okk = k < cnt;
+                    if (buf[pp] == 97) {
+                        v = buf[pp + 1];
+                        okk &= pp + 2u <= hi;
                     } else {
-                        bad = true;
-                        break;
+                        v = (int32_t)(((uint32_t)buf[pp + 1] << 24) | ((uint32_t)buf[pp + 2] << 16) |
+                                      ((uint32_t)buf[pp + 3] << 8) | buf[pp + 4]);
+                        okk &= pp + 5u <= hi && (v < 0 || v > 255);   // minimal images only
                     }
                     const int64_t xv = v - g.ilo;
-                    const u64 t = xv >= 0 && xv < (int64_t)g.in ? g.itab[xv] : 0ull;
-                    if (!(uint32_t)t) {
-                        bad = true;
-                        break;
-                    }
-                    const uint32_t slot = (uint32_t)t - 1u, rk = (uint32_t)(t >> 32);
-                    if (cnt == 0) first = rk;
-                    else bad |= rk <= last;
-                    last = rk;
-                    ++cnt;
-                    atomicOr(&s_w[slot >> 6], 1ull << (slot & 63u));
+                    okk &= xv >= 0 && xv < (int64_t)g.in;
+                    tv[k] = g.itab[okk ? xv : 0];
+                    vok[k] = okk;
                 }
+            }
+            uint32_t first = 0, last = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                if (k >= cnt) break;
+                const u64 t = tv[k];
+                if (!vok[k] || !(uint32_t)t) {
+                    bad = true;
+                    break;
+                }
+                const uint32_t slot = (uint32_t)t - 1u, rk = (uint32_t)(t >> 32);
+                if (k == 0) first = rk;
+                else bad |= rk <= last;
+                last = rk;
+                atomicOr(&s_w[slot >> 6], 1ull << (slot & 63u));
             }
             firstrk[tid] = cnt ? first : 0xFFFFFFFFu;
             lastrk[tid] = cnt ? last : 0xFFFFFFFFu;
-            atomicAdd(&sc[0], cnt);
-            if (cnt) atomicMax(&sc[2], tid);
+            if (cnt) {
+                atomicAdd(&sc[0], cnt);
+                atomicMax(&sc[2], tid);
+            }
             __syncthreads();
             if (cnt) {
-                if (tid == 0) bad |= have_prev && first <= prev_rank;
-                else bad |= lastrk[tid - 1] == 0xFFFFFFFFu && firstrk[tid - 1] == 0xFFFFFFFFu
-                                ? true : first <= lastrk[tid - 1];
+                if (tid == t0) bad |= have_prev && first <= prev_rank;
+                else if (tid > t0)
+                    bad |= lastrk[tid - 1] == 0xFFFFFFFFu ? true : first <= lastrk[tid - 1];
             }
             const bool anybad = __syncthreads_or(bad);
             const uint32_t wcnt = sc[0];
@@ -3951,7 +4011,10 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
                 ok = sc[1] == hi && lo + hi == aend && got == n;
                 fin = true;
             } else {
-                if (lo + kGPW >= aend) { ok = false; break; }
+                if (lo + kGPW >= aend) {
+                    ok = false;
+                    break;
+                }
                 x = (uint32_t)(lo + kGPW + fin_state - base);
             }
         }
@@ -4257,22 +4320,23 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, co
 }
 
 // The item decoder's bucket tables, built once per dictionary, when the batch should take
-// that decoder: many-token dictionaries (> 8 token slots) whose records hash apart, at
-// most 65536 elements (64 MiB of tables), a 16-byte aligned payload buffer, and at least
-// one payload per CU (knob 9: any batch size; knob 8 or any other knob: never).  Null:
-// the wave decoder.
+// that decoder: knob 9 only (measured slower than the wave decoder at the t64 shape,
+// 6.1 vs 4.4 ms, profiles/r04f_dec_*: the per-window scans, compaction and barriers cost
+// as much per element as the wave decoder's per-element sequence), many-token
+// dictionaries (> 8 token slots) whose records hash apart, at most 65536 elements
+// (64 MiB of tables), a 16-byte aligned payload buffer.  Null: the wave decoder.
 uint8_t* items_btab(laspj_ctx* ctx, const laspj_etf_dict* dc, uint64_t R, const uint8_t* payload) {
     laspj_etf_dict* d = const_cast<laspj_etf_dict*>(dc);
     const int64_t kn = ctx->tune_etf_read;
-    if (!(kn == 0 || kn == 9) || !d->rd_desc || !d->rd_htab || d->tok_max <= kSmallTok ||
-        d->elements > 65536u || d->elements == 0 || ((uintptr_t)payload & 15u) ||
-        (kn == 0 && R < (uint64_t)ctx->cus))
+    (void)R;
+    if (kn != 9 || !d->rd_desc || !d->rd_htab || d->tok_max <= kSmallTok ||
+        d->elements > 65536u || d->elements == 0 || ((uintptr_t)payload & 15u))
         return nullptr;
     if (!d->btab_tried) {
         d->btab_tried = true;
         const uint64_t bytes = (uint64_t)d->elements * kIBuckets;
         void* p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) {
+        if (dev_malloc(ctx, &p, bytes) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }
@@ -4349,9 +4413,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
         LJ_LAUNCHED(ctx);
         return LASPJ_OK;
     }
-    // many-token dictionaries with enough payloads to fill the chip: the item decoder,
-    // one block per payload (knob 8: never, 9: whatever the batch size), then the wave
-    // decoder over whatever it sent to the redo list
+    // knob 9, many-token dictionaries: the item decoder, one block per payload, then the
+    // wave decoder over whatever it sent to the redo list
     if (uint8_t* bt = items_btab(ctx, d, R, payload)) {
         uint32_t* redo = redo_zeroed;
         if (!redo) {

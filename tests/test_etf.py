@@ -463,13 +463,12 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 @contextlib.contextmanager
 def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
-    <= 8 token slots, and for small elements of many-token dictionaries; the item
-    decoder for many-token dictionaries at >= 1 payload per CU), 1 = serial scan, 2 =
-    batched records only, 7 = no many-token element batches, 8 = never the item decoder,
-    9 = the item decoder at any batch size, 4 = every payload
-    longer than 256 bytes split between waves (segment mode: header search, chain
-    check, redo of failed replicas); "seg512": the default kernels with every payload
-    longer than 512 bytes split (LASPJ_TUNE_ETF_SEG)."""
+    <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
+    scan, 2 = batched records only, 7 = no many-token element batches, 8 = wave decoders
+    only, 9 = the item decoder for many-token dictionaries, 4 = every payload longer
+    than 256 bytes split between waves (segment mode: header search, chain check, redo
+    of failed replicas); "seg512": the default kernels with every payload longer than 512
+    bytes split (LASPJ_TUNE_ETF_SEG)."""
     from lasp_amd import _lib
     if knob == "seg512":
         ctx.set_tuning(_lib.TUNE_ETF_SEG, 512)
@@ -629,10 +628,10 @@ def test_gpu_from_binary_errors_and_atom_forms(knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 4, 8])
+@pytest.mark.parametrize("knob", [0, 1, 4, 9])
 def test_gpu_from_binary_large_round_trip(knob):
     """4096 replicas x 512 slots x 64 token slots: device to_binary then from_binary
-    restores every cell (knob 0: the item decoder, 8: the wave decoder)."""
+    restores every cell (knob 9: the item decoder)."""
     import numpy as np
     from lasp_amd import engine, etf
     from lasp_amd.codec import Domain
@@ -953,9 +952,9 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
     records, so a batch holds one to several whole elements or stops inside one; tokens
     that embed the batch's item marker 104 2 and whole false element starts (106 104 2
     <a real element header>), flags in all three atom forms, and 2500 corrupted copies:
-    the item decoder (knob 0: 2560 payloads), element batches (8), one element at a time
-    (7) and the serial scan (1) agree on every status and cell, and the clean payloads
-    decode to the encoder's cells."""
+    element batches (knob 0), the item decoder (9), one element at a time (7) and the
+    serial scan (1) agree on every status and cell, and the clean payloads decode to the
+    encoder's cells."""
     import numpy as np
     from lasp_amd import etf
     rng = random.Random(seed)
@@ -1018,7 +1017,7 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
         blobs.append(bytes(b))
     pay, offs = _upload_payloads(ctx, blobs)
     res = {}
-    for knob in (0, 7, 8, 1):
+    for knob in (0, 7, 9, 1):
         bt = ctx.orset_batch(len(blobs), E)
         with _read_kernel(ctx, knob):
             st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
@@ -1027,7 +1026,7 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
     assert set(np.unique(st0)) <= {0, 1, 2, 3, 4, 5}
     assert (st0[:len(base)] == 0).all(), np.nonzero(st0[:len(base)])[0][:10]
     assert np.array_equal(c0[:len(base)], dom.encode_orset(states, E))
-    for knob in (7, 8, 1):
+    for knob in (7, 9, 1):
         st, c = res[knob]
         assert np.array_equal(st0, st), (knob, np.nonzero(st0 != st)[0][:10])
         ok = st0 == 0
