@@ -154,11 +154,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         batches walked by the scalar unit (the lanes
                                         find element starts by default), 7 = no element
                                         batches for many-token dictionaries (one element
-                                        at a time), 8 = the wave decoders only (G-Set:
-                                        no block parser for integer payloads), 9 = the
-                                        item decoder for many-token dictionaries (one
-                                        block per payload, one thread per element or
-                                        record; slower than the default at t64)          */
+                                        at a time), 8 = the same as 0, 9 = block
+                                        decoders: OR-Set many-token dictionaries one
+                                        thread per element or record, G-Set integer
+                                        payloads by composed tag-length maps (both
+                                        slower than the default)           */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

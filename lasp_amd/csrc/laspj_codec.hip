@@ -3899,7 +3899,8 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* pay
             if (tid < t0) {
                 mp = 0x55555555u;
             } else if (tid == t0) {
-                mp |= gs_walk16(m97, m98, m106, p0 & 15u) * 0x11111u;
+                // every field: the threads before t0 hand it entry 5
+                mp = gs_walk16(m97, m98, m106, p0 & 15u) * 0x11111111u;
             } else {
 #pragma unroll
                 for (uint32_t s2 = 0; s2 < 5; ++s2) mp |= gs_walk16(m97, m98, m106, s2) << (4u * s2);
@@ -4239,9 +4240,12 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     const uint64_t cap = (uint64_t)ctx->cus * 64;
     const uint8_t* pay = static_cast<const uint8_t*>(payload->dev);
     const u64* offs = static_cast<const u64*>(offsets->dev);
-    // integer dictionaries: the block parser first (knob 8: never), the wave decoder over
-    // its redo list; every replica's words are written by one of them
-    if (d->gs_itab && b->words_per_replica <= kGWords && ctx->tune_etf_read != 8 &&
+    // knob 9, integer dictionaries: the block parser first, the wave decoder over its redo
+    // list; every replica's words are written by one of them.  Not the default: measured
+    // 0.84 ms of kernel time against the wave decoder's 0.46 at 65536 x 1024 (its per-thread
+    // maps and their composition scan cost ~7000 wave-instructions per 2 KiB payload,
+    // profiles/r04h_gs_*)
+    if (d->gs_itab && b->words_per_replica <= kGWords && ctx->tune_etf_read == 9 &&
         !((uintptr_t)pay & 15u)) {
         if (int s = reserve_scratch(ctx, 4ull * (R + 1))) return s;
         uint32_t* redo = static_cast<uint32_t*>(ctx->scratch);

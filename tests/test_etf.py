@@ -464,8 +464,8 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
     <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
-    scan, 2 = batched records only, 7 = no many-token element batches, 8 = wave decoders
-    only, 9 = the item decoder for many-token dictionaries, 4 = every payload longer
+    scan, 2 = batched records only, 7 = no many-token element batches, 8 = the same as 0
+    only, 9 = the block decoders (many-token OR-Sets, integer G-Sets), 4 = every payload longer
     than 256 bytes split between waves (segment mode: header search, chain check, redo
     of failed replicas); "seg512": the default kernels with every payload longer than 512
     bytes split (LASPJ_TUNE_ETF_SEG)."""
@@ -1240,7 +1240,7 @@ def test_gpu_gset_block_parser_matches_wave_decoder():
     3000 corrupted copies — tags flipped between 97 / 98 / 106, values nudged, bytes cut or
     inserted at and around window edges, two elements swapped, a duplicate, a
     non-minimal INTEGER_EXT, a value outside the dictionary: the block parser (with the
-    wave decoder over its redo list, knob 0) and the wave decoder alone (knob 8) give the
+    wave decoder over its redo list, knob 9) and the wave decoder alone (knob 0) give the
     same status and the same words for every payload, and the clean payloads decode to
     the host encoder's words."""
     import numpy as np
@@ -1293,7 +1293,7 @@ def test_gpu_gset_block_parser_matches_wave_decoder():
             b[4:8] = (len(s) + 1).to_bytes(4, "big")
         blobs.append(bytes(b))
     res = {}
-    for knob in (0, 8):
+    for knob in (9, 0):
         pay, offs = _upload_payloads(ctx, blobs)
         bt = ctx.gset_batch(len(blobs), E)
         ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
@@ -1302,12 +1302,12 @@ def test_gpu_gset_block_parser_matches_wave_decoder():
         finally:
             ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
         res[knob] = (st, bt.download())
-    assert np.array_equal(res[0][0], res[8][0]), np.nonzero(res[0][0] != res[8][0])[0][:10]
-    assert np.array_equal(res[0][1], res[8][1])
+    assert np.array_equal(res[9][0], res[0][0]), np.nonzero(res[9][0] != res[0][0])[0][:10]
+    assert np.array_equal(res[9][1], res[0][1])
     nb = sum(1 for t in tags if t == T)
-    assert (res[0][0][:nb] == 0).all()
+    assert (res[9][0][:nb] == 0).all()
     clean = [s for s, t in zip(states, tags) if t == T]
-    assert np.array_equal(res[0][1][:nb], dom.encode_gset(clean, E))
+    assert np.array_equal(res[9][1][:nb], dom.encode_gset(clean, E))
     # untagged payloads too
     untag = [b for b, t in zip(base, tags) if t < 0]
     if untag:

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """G-Set from_binary at the suite's shape (tools/bench_suite.py: 65536 replicas x 1024
-integer elements, ~50 % present, SMALL_INTEGER_EXT / INTEGER_EXT images): the block
-parser (LASPJ_TUNE_ETF_READ 0) against the wave decoder alone (8), interleaved, each
-checked against the batch it was encoded from."""
+integer elements, ~50 % present, SMALL_INTEGER_EXT / INTEGER_EXT images): the wave
+decoder (LASPJ_TUNE_ETF_READ 0) against the block parser (9), interleaved, each checked
+against the batch it was encoded from."""
 import json
 import os
 import sys
@@ -41,7 +41,7 @@ def run():
 
 
 for rep in range(2):
-    for knob in (0, 8):
+    for knob in (0, 9):
         ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
         back.clear()
         for _ in range(3):
