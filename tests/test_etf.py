@@ -464,9 +464,9 @@ def test_gpu_record_kernel_runs_with_tiny_payloads():
 def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
     <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
-    scan, 2 = batched records only, 7 = no many-token element batches, 8 = the same as 0
-    only, 9 = the block decoders (many-token OR-Sets, integer G-Sets), 4 = every payload longer
-    than 256 bytes split between waves (segment mode: header search, chain check, redo
+    scan, 2 = batched records only, 7 = no many-token element batches, 8 = the same as
+    0, 9 = the block decoders (many-token OR-Sets, integer G-Sets), 4 = every payload
+    longer than 256 bytes split between waves (segment mode: header search, chain check, redo
     of failed replicas); "seg512": the default kernels with every payload longer than 512
     bytes split (LASPJ_TUNE_ETF_SEG)."""
     from lasp_amd import _lib
