@@ -165,6 +165,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         multiple of 256)                               */
 #define LASPJ_TUNE_LIST_WALK    10   /* list merges whose keys descend somewhere: 0 = the
                                         run-jumping walk, 1 = one step per element      */
+#define LASPJ_TUNE_NIF_PIECE    11   /* NIF entry points: bytes staged into pinned memory
+                                        per host -> device copy (0 = 256 KiB; a multiple
+                                        of 4096)                                        */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -270,7 +270,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             const uint64_t head = i_pay;
             while (i < m && c.len[i] == 0) ++i;
             while (at < pay) {
-                const uint64_t piece = std::min(kStagePiece, pay - at);
+                const uint64_t piece = std::min(ctx->tune_nif_piece ? (uint64_t)ctx->tune_nif_piece
+                                                                    : kStagePiece, pay - at);
                 uint64_t done = 0;
                 const uint64_t tc = now_ns();
                 while (done < piece) {

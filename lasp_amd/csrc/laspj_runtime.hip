@@ -354,6 +354,12 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             if (value < 0 || value > 1) return fail(ctx, LASPJ_E_INVAL, "tuning: list walk 0 or 1");
             ctx->tune_list_walk = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_NIF_PIECE:
+            if (value < 0 || value > (1ll << 30) || (value % 4096) != 0)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: NIF staging piece must be 0 or a "
+                            "multiple of 4096");
+            ctx->tune_nif_piece = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

@@ -21,9 +21,11 @@ tb = [(e, [(b"B" + e.to_bytes(19, "big"), e % 10 == 0)]) for e in range(n)]
 pa, pb = etf.term_to_binary(ta), etf.term_to_binary(tb)
 ctx = engine.Context(0)
 L = ctx.L
+from lasp_amd import _lib  # noqa: E402
 if os.environ.get("NIF_SEG"):                  # from_binary segment bytes (A/B)
-    from lasp_amd import _lib
     ctx.set_tuning(_lib.TUNE_ETF_SEG, int(os.environ["NIF_SEG"]))
+if os.environ.get("NIF_PIECE"):                # pinned staging piece bytes (A/B)
+    ctx.set_tuning(_lib.TUNE_NIF_PIECE, int(os.environ["NIF_PIECE"]))
 op, on, vd = C.c_void_p(), C.c_uint64(), C.c_int32()
 
 
