@@ -343,6 +343,7 @@ def config1_gpu(ctx):
     # merge then meets one term its dictionary lacks — registration, device images
     # rebuilt, a second device pass
     cold = []
+    sc0 = ctx.nif_stats()
     for k in range(5):
         tb2 = list(tb)
         e = 17 * k + 3
@@ -355,6 +356,13 @@ def config1_gpu(ctx):
         if vd.value != 0:
             raise RuntimeError("config1: a merge with a new token fell back")
     out["us_merge_nif_new_token"] = sorted(cold)[len(cold) // 2]
+    sc1 = ctx.nif_stats()
+    # where a cold merge's time goes (host clock, averaged over the 5): the first device
+    # pass that meets the new term, registering both operands' terms, rebuilding the device
+    # images, the second pass
+    out["nif_new_token_stages_us"] = {k: (sc1[k] - sc0[k]) / 5e3 for k in
+                                      ("ns_stage_enqueue", "ns_device_wait", "ns_register",
+                                       "ns_rebuild")}
     nif()
     st0 = ctx.nif_stats()
     for _ in range(20):

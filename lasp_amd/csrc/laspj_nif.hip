@@ -66,7 +66,10 @@ struct Guard {
 };
 
 constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is reset
-constexpr uint64_t kStagePiece = 256ull << 10;    // host -> pinned staging granule
+// host -> pinned staging granule: one copy per call up to 64 MiB (a single ~1 MiB copy
+// beat 256 KiB pieces, 135 vs 154 us per config-1 merge, and 512 KiB pieces hit a slow
+// runtime path, 475 us: profiles/r04i_nif_ab.log)
+constexpr uint64_t kStagePiece = 64ull << 20;
 
 uint64_t al(uint64_t x, uint64_t a) { return (x + a - 1) & ~(a - 1); }
 
@@ -153,8 +156,14 @@ int reset_dict(laspj_ctx* ctx, NifState* S) {
     return LASPJ_OK;
 }
 
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // the device images of the dictionary (called without ctx->mu: etf_dict_create takes it)
 int rebuild_etf(laspj_ctx* ctx, NifState* S) {
+    const uint64_t t0 = now_ns();
     uint32_t n = 0;
     uint64_t eb = 0, tb = 0;
     if (laspj_dict_info(S->dict, &n, &eb, &tb) != LASPJ_OK)
@@ -176,15 +185,12 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S) {
     S->E = E;
     S->stale = false;
     ++S->stats[4];
+    S->stats[13] += now_ns() - t0;
     return LASPJ_OK;
 }
 
 // One device pass: stage, copy, decode (or upload host-encoded cells), answer, copy back,
 // one synchronisation.  Fills c.st / c.res / c.ooff / c.obase.
-uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const uint64_t t0 = now_ns();
@@ -404,6 +410,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
 
 int register_payloads(laspj_ctx* ctx, NifState* S, const std::vector<const uint8_t*>& p,
                       const std::vector<uint64_t>& len, std::vector<int32_t>* st) {
+    const uint64_t t0 = now_ns();
     const uint64_t k = p.size();
     std::vector<uint64_t> offs(k + 1, 0);
     for (uint64_t i = 0; i < k; ++i) offs[i + 1] = offs[i] + len[i];
@@ -415,6 +422,7 @@ int register_payloads(laspj_ctx* ctx, NifState* S, const std::vector<const uint8
                                st->data()))
         return fail(ctx, s, "nif: dictionary registration failed (%d)", s);
     ++S->stats[2];
+    S->stats[12] += now_ns() - t0;
     S->stale = true;
     return LASPJ_OK;
 }

@@ -34,13 +34,27 @@ def nif():
                                   C.byref(vd)), ctx.h)
 
 
+cold = os.environ.get("NIF_COLD") == "1"     # every call meets one new token
+colds = []
+for k in range(iters if cold else 0):
+    tb2 = list(tb)
+    e = 17 * k + 3
+    tb2[e] = (e, sorted(tb[e][1] + [(b"N" + (k * 7919 + e).to_bytes(19, "big"), False)]))
+    colds.append(etf.term_to_binary(tb2))
+
+
+def nif_cold(k):
+    check(L.laspj_orset_etf_merge(ctx.h, pa, len(pa), colds[k], len(colds[k]), C.byref(op),
+                                  C.byref(on), C.byref(vd)), ctx.h)
+
+
 for _ in range(5):
     nif()
 s0 = ctx.nif_stats()
 t0 = time.perf_counter()
-for _ in range(iters):
-    nif()
+for k in range(iters):
+    nif_cold(k) if cold else nif()
 us = (time.perf_counter() - t0) * 1e6 / iters
 s1 = ctx.nif_stats()
-print(json.dumps({"us_per_merge": us, "bytes_in": len(pa) + len(pb), "bytes_out": on.value,
+print(json.dumps({"cold": cold, "us_per_merge": us, "bytes_in": len(pa) + len(pb), "bytes_out": on.value,
                   "stages_us": {k: (s1[k] - s0[k]) / iters / 1e3 for k in s1 if k.startswith("ns_")}}))
