@@ -158,7 +158,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         decoders: OR-Set many-token dictionaries one
                                         thread per element or record, G-Set integer
                                         payloads by composed tag-length maps (both
-                                        slower than the default)           */
+                                        slower than the default), 10 = as
+                                        0, with segment mode's redo pass as a launch of
+                                        its own (by default the chain check's wave decodes
+                                        a payload that failed it again itself)          */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

@@ -39,6 +39,7 @@ struct laspj_etf_dict {
     uint32_t tok_uniform = 0;     // every used token image has this length (0: mixed)
     uint32_t tok_max = 0;         // most token slots any element uses
     void* block = nullptr;        // one device allocation holding the arrays below
+    uint64_t block_bytes = 0;     // (from the context's block cache: dev_alloc / dev_release)
     const uint8_t* elem_blob = nullptr;
     const uint32_t* elem_off = nullptr;    // E + 1
     const uint32_t* elem_order = nullptr;  // E
@@ -670,11 +671,17 @@ __global__ __launch_bounds__(kBlock) void k_etf_chunk_scan(u64* coff, uint64_t R
 // (the slot-wise OR of canonical cells) written to `z`, fused with the split-mode size
 // pass over z, and the operands' cells cleared behind it (the next call's decoders then
 // start from new() without a memset).  Same chunk totals as k_etf_chunk_sizes.
+// With `ticket` (few replicas: the NIF's single merges) the block that finishes last also
+// scans the chunk totals and writes the payload offsets (k_etf_chunk_scan_offsets' work),
+// so the whole size pass is one launch; ticket is zero on entry and left zero.
 __global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2* b, u64x2* z,
                                                                  uint64_t R, uint32_t E,
                                                                  DictView d, uint32_t nch,
-                                                                 u64* coff, uint32_t* flag) {
+                                                                 u64* coff, uint32_t* flag,
+                                                                 uint32_t* ticket, uint32_t hdr,
+                                                                 u64* offs) {
     __shared__ u64 lds4[kBlock / 64];
+    __shared__ uint32_t s_last;
     for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
         const uint64_t rep = it / nch;
         const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
@@ -697,6 +704,35 @@ __global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2
         u64 tot;
         block_excl_scan64(v, lds4, &tot);
         if (threadIdx.x == 0) coff[rep * (nch + 1ull) + c] = tot;
+    }
+    if (!ticket) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();                                   // this block's totals, visible
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();                                       // every block's totals, seen
+    u64 ocarry = 0;
+    for (uint64_t rep = 0; rep < R; ++rep) {
+        u64* cp = coff + rep * (nch + 1ull);
+        u64 carry = 0;
+        for (uint32_t t0 = 0; t0 <= nch; t0 += kBlock) {
+            const uint32_t t = t0 + threadIdx.x;
+            const u64 v = t < nch ? __atomic_load_n(cp + t, __ATOMIC_RELAXED) : 0;
+            u64 tot;
+            const u64 ex = block_excl_scan64(v, lds4, &tot);
+            if (t <= nch) cp[t] = carry + ex;
+            carry += tot;
+        }
+        const u64 n = carry / kChunkCnt, sum = carry & (kChunkCnt - 1);
+        if (threadIdx.x == 0) offs[rep] = ocarry;
+        ocarry += hdr + 1u + (n ? 5u + sum + 1u : 1u);
+    }
+    if (threadIdx.x == 0) {
+        offs[R] = ocarry;
+        *ticket = 0;
     }
 }
 
@@ -2657,6 +2693,42 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
     return k;
 }
 
+// One replica's payload decoded by one wave, from its head to its end (cells cleared
+// first when `clear`): the reference's status.
+template <bool SMALL>
+__device__ int32_t decode_replica(const uint8_t* payload, u64 total, const u64* offs,
+                                  uint64_t rep, uint32_t E, const DictView& d,
+                                  const ReadTabs& tabs, const HdrHash& hh, int tag, int vers,
+                                  u64x2* cells, bool clear, ReadLds& L, ReadLdsX* X,
+                                  uint32_t lane, Cases cs) {
+    const uint32_t RK = d.tok_max;
+    const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
+    u64x2* c = cells + rep * E;
+    if (clear)
+        for (uint32_t e = lane; e < E; e += 64) c[e] = u64x2{0, 0};
+    PWin w{L.win, payload, total, aend, base, 0, (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
+    uint32_t pc = 0, n = 0;
+    bool list = false;
+    int32_t st = parse_head(w, pc, tag, vers, n, list);
+    if (st == LASPJ_DEC_OK) {
+        int64_t prev = -1;                    // term rank of the previous element
+        RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
+        bool tail = false;
+        decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, hh, E, L, X, c, lane,
+                            cs);
+    }
+    if (st == LASPJ_DEC_OK && list) {
+        if (pc + 1 > w.end) st = LASPJ_DEC_MALFORMED;
+        else {
+            pc = need(w, pc, 1);
+            if (ub(w, pc) != 106) st = LASPJ_DEC_MALFORMED;
+            pc += 1;
+        }
+    }
+    if (st == LASPJ_DEC_OK && w.lo + pc != aend) st = LASPJ_DEC_MALFORMED;   // trailing bytes
+    return st;
+}
+
 // One wave per replica.  With `redo` (segment mode's fallback) the wave takes the
 // replicas listed there (redo[0] of them) and clears their cells first.
 // (element batches: 5 waves per SIMD give 96 VGPRs, 6 spilled instead of 20 at 6 waves,
@@ -2674,7 +2746,6 @@ __global__ __launch_bounds__(kBlock, SMALL ? 5 : 4) void k_orset_etf_read(const 
     __shared__ __attribute__((aligned(16))) ReadLdsX ldx[SMALL ? 1 : kBlock / 64];
     // the wave index as a scalar: everything per replica then stays wave-uniform
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t RK = d.tok_max;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     ReadLdsX* X = SMALL ? nullptr : &ldx[wave];
     const Cases cs = lane_cases(lane);
@@ -2682,30 +2753,8 @@ __global__ __launch_bounds__(kBlock, SMALL ? 5 : 4) void k_orset_etf_read(const 
     const uint64_t count = redo ? (uint64_t)ufl32(redo[0]) : R;
     for (uint64_t i = (uint64_t)blockIdx.x * (kBlock / 64) + wave; i < count; i += nwaves) {
         const uint64_t rep = redo ? (uint64_t)ufl32(redo[1 + i]) : i;
-        const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
-        u64x2* c = cells + rep * E;
-        if (redo)
-            for (uint32_t e = lane; e < E; e += 64) c[e] = u64x2{0, 0};
-        PWin w{L.win, payload, total, aend, base, 0, (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
-        uint32_t pc = 0, n = 0;
-        bool list = false;
-        int32_t st = parse_head(w, pc, tag, vers, n, list);
-        if (st == LASPJ_DEC_OK) {
-            int64_t prev = -1;                    // term rank of the previous element
-            RankPre nx = load_rank(tabs, RK, 0, E, lane);   // the predicted next rank
-            bool tail = false;
-            decode_elems<SMALL>(w, pc, prev, nx, n, ~0ull, tail, st, tabs, d, hh, E, L, X, c,
-                                lane, cs);
-        }
-        if (st == LASPJ_DEC_OK && list) {
-            if (pc + 1 > w.end) st = LASPJ_DEC_MALFORMED;
-            else {
-                pc = need(w, pc, 1);
-                if (ub(w, pc) != 106) st = LASPJ_DEC_MALFORMED;
-                pc += 1;
-            }
-        }
-        if (st == LASPJ_DEC_OK && w.lo + pc != aend) st = LASPJ_DEC_MALFORMED;   // trailing bytes
+        const int32_t st = decode_replica<SMALL>(payload, total, offs, rep, E, d, tabs, hh, tag,
+                                                 vers, cells, redo != nullptr, L, X, lane, cs);
         if (lane == 0) status[rep] = st;
     }
 }
@@ -2768,6 +2817,64 @@ __device__ int64_t resolve_hdr(const PWin& w, uint32_t x, const HdrHash& hh,
     const u64 m = __ballot(rank >= 0);
     // images are self-delimiting and distinct: at most one header length matches
     return m ? (int64_t)rdlane((uint32_t)rank, (uint32_t)__ffsll((long long)m) - 1u) : -1;
+}
+
+// Is replica's segment chain one well-formed orddict (segments g0 .. g0 + ns of res)?
+// One wave, lanes over the segments 64 at a time: segment s's predecessor is the latest
+// earlier segment that found an element start (a max-scan of indices over the lanes,
+// carried between groups of 64), and every segment checks itself against it — a start
+// that found nothing is fine only where no element starts, a found one must begin exactly
+// at its predecessor's end with a higher first rank — then one ballot and one sum of
+// element counts decide (the chain's checks, evaluated in parallel: the answer is whether
+// any of them fails).
+__device__ bool chain_ok(const uint8_t* payload, u64 base, u64 len, uint32_t g0, uint32_t ns,
+                         uint32_t S, const SegRes* res, uint32_t lane) {
+    const SegRes a = res[g0];
+    bool ok = a.st == LASPJ_DEC_OK;
+    if (ok && (a.flags & kSegEmptyList)) return a.end == len;
+    if (!ok) return false;
+    uint32_t q = a.end, cnt = 0;
+    int32_t rl = a.rlast;
+    bool bad = false;
+    for (uint32_t s0 = 1; s0 < ns; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        SegRes b{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
+        if (s < ns) b = res[g0 + s];
+        const bool valid = s < ns && b.start != kSegNone;
+        int32_t li = valid ? (int32_t)lane : -1;      // latest valid lane <= this one
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t v = __shfl_up(li, off, 64);
+            if ((int)lane >= off) li = max(li, v);
+        }
+        int32_t lp = __shfl_up(li, 1, 64);             // ... strictly before it
+        if (lane == 0) lp = -1;
+        const uint32_t e_at = __shfl(b.end, lp < 0 ? 0 : lp, 64);
+        const int32_t r_at = __shfl(b.rlast, lp < 0 ? 0 : lp, 64);
+        const uint32_t pq = lp >= 0 ? e_at : q;
+        const int32_t prl = lp >= 0 ? r_at : rl;
+        if (s < ns) {
+            if (!valid) {
+                // no header found: fine only if none starts here (the predecessor's end
+                // past the segment, or on the list's closing 106)
+                const u64 send = (u64)(s + 1) * S;
+                if (pq < send && pq < len && payload[base + pq] != 106) bad = true;
+            } else if (b.start != pq || b.st != LASPJ_DEC_OK || b.rfirst <= prl) {
+                bad = true;
+            } else {
+                cnt += b.cnt;
+            }
+        }
+        const int32_t last = __shfl(li, 63, 64);
+        if (last >= 0) {
+            q = __shfl(b.end, last, 64);
+            rl = __shfl(b.rlast, last, 64);
+        }
+    }
+    uint32_t tot = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+    return !__ballot(bad) && a.cnt + tot == a.n && (u64)q + 1 == len && payload[base + q] == 106;
 }
 
 template <bool SMALL>
@@ -2868,72 +2975,34 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
 // found one must begin exactly at its predecessor's end with a higher first rank —
 // then one ballot and one sum of element counts decide (the chain's checks, evaluated
 // in parallel: the answer is whether any of them fails).
-__global__ __launch_bounds__(64) void k_etf_read_chain(const uint8_t* payload, const u64* offs,
-                                                       uint64_t R, const uint32_t* segbase,
-                                                       uint32_t S, const SegRes* res,
-                                                       int32_t* status, uint32_t* redo) {
+// With `cells` (the default), a replica whose chain fails is decoded again right here by
+// this wave from its head, its cells cleared first (the redo pass's work, the reference's
+// status): one launch fewer.  Without, it goes onto the redo list for k_orset_etf_read.
+template <bool SMALL>
+__global__ __launch_bounds__(64) void k_etf_read_chain(const uint8_t* payload, u64 total,
+                                                       const u64* offs, uint64_t R,
+                                                       const uint32_t* segbase, uint32_t S,
+                                                       const SegRes* res, int32_t* status,
+                                                       uint32_t* redo, uint32_t E, DictView d,
+                                                       ReadTabs tabs, HdrHash hh, int tag,
+                                                       int vers, u64x2* cells) {
+    __shared__ __attribute__((aligned(16))) ReadLds L;
     const uint32_t lane = threadIdx.x;
+    const Cases cs = lane_cases(lane);
     for (uint64_t r = blockIdx.x; r < R; r += gridDim.x) {
         const u64 base = offs[r];
-        const u64 len = offs[r + 1] - base;
-        const uint32_t g0 = segbase[r], ns = segbase[r + 1] - g0;
-        const SegRes a = res[g0];
-        bool ok = a.st == LASPJ_DEC_OK;
-        if (ok && (a.flags & kSegEmptyList)) {
-            ok = a.end == len;
-        } else if (ok) {
-            uint32_t q = a.end, cnt = 0;
-            int32_t rl = a.rlast;
-            bool bad = false;
-            for (uint32_t s0 = 1; s0 < ns; s0 += 64) {
-                const uint32_t s = s0 + lane;
-                SegRes b{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
-                if (s < ns) b = res[g0 + s];
-                const bool valid = s < ns && b.start != kSegNone;
-                int32_t li = valid ? (int32_t)lane : -1;      // latest valid lane <= this one
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const int32_t v = __shfl_up(li, off, 64);
-                    if ((int)lane >= off) li = max(li, v);
-                }
-                int32_t lp = __shfl_up(li, 1, 64);             // ... strictly before it
-                if (lane == 0) lp = -1;
-                const uint32_t e_at = __shfl(b.end, lp < 0 ? 0 : lp, 64);
-                const int32_t r_at = __shfl(b.rlast, lp < 0 ? 0 : lp, 64);
-                const uint32_t pq = lp >= 0 ? e_at : q;
-                const int32_t prl = lp >= 0 ? r_at : rl;
-                if (s < ns) {
-                    if (!valid) {
-                        // no header found: fine only if none starts here (the predecessor's
-                        // end past the segment, or on the list's closing 106)
-                        const u64 send = (u64)(s + 1) * S;
-                        if (pq < send && pq < len && payload[base + pq] != 106) bad = true;
-                    } else if (b.start != pq || b.st != LASPJ_DEC_OK || b.rfirst <= prl) {
-                        bad = true;
-                    } else {
-                        cnt += b.cnt;
-                    }
-                }
-                const int32_t last = __shfl(li, 63, 64);
-                if (last >= 0) {
-                    q = __shfl(b.end, last, 64);
-                    rl = __shfl(b.rlast, last, 64);
-                }
-            }
-            uint32_t tot = cnt;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
-            ok = !__ballot(bad) && a.cnt + tot == a.n && (u64)q + 1 == len &&
-                 payload[base + q] == 106;
-        }
-        if (lane == 0) {
-            if (ok) {
-                status[r] = LASPJ_DEC_OK;
-            } else {
-                status[r] = LASPJ_DEC_MALFORMED;       // rewritten by the redo pass
-                const uint32_t i = atomicAdd(redo, 1u);
-                redo[1 + i] = (uint32_t)r;
-            }
+        const bool ok = chain_ok(payload, base, offs[r + 1] - base, segbase[r],
+                                 segbase[r + 1] - segbase[r], S, res, lane);
+        if (ok) {
+            if (lane == 0) status[r] = LASPJ_DEC_OK;
+        } else if (cells) {
+            const int32_t st = decode_replica<SMALL>(payload, total, offs, r, E, d, tabs, hh, tag,
+                                                     vers, cells, true, L, nullptr, lane, cs);
+            if (lane == 0) status[r] = st;
+        } else if (lane == 0) {
+            status[r] = LASPJ_DEC_MALFORMED;           // rewritten by the redo pass
+            const uint32_t i = atomicAdd(redo, 1u);
+            redo[1 + i] = (uint32_t)r;
         }
     }
 }
@@ -4390,24 +4459,32 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
             dsegbase = up;
         }
         SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
-        uint32_t* redo = redo_zeroed;
-        if (!redo) {
-            redo = reinterpret_cast<uint32_t*>(sc + o_redo);
-            LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
-        }
         const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
-        hipLaunchKernelGGL(d->tok_max <= kSmallTok && ctx->tune_etf_read != 2
-                               ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
+        const bool small = d->tok_max <= kSmallTok && ctx->tune_etf_read != 2;
+        hipLaunchKernelGGL(small ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
                            dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
                            payload, (u64)payload_bytes, offs, R, b->elements, view(d), tabs, tag,
                            vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
                            (uint32_t)plan.S, hh, dres);
         LJ_LAUNCHED(ctx);
-        hipLaunchKernelGGL(k_etf_read_chain,
+        // the chain check, whose wave decodes a failed replica again itself (knob 10: the
+        // redo list and a launch of the wave decoder over it, as before)
+        const bool inline_redo = ctx->tune_etf_read != 10;
+        uint32_t* redo = redo_zeroed;
+        if (!redo && !inline_redo) {
+            redo = reinterpret_cast<uint32_t*>(sc + o_redo);
+            LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
+        }
+        const bool csmall = d->tok_max <= kSmallTok &&
+                            (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6);
+        hipLaunchKernelGGL(csmall ? k_etf_read_chain<true> : k_etf_read_chain<false>,
                            dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)), dim3(64), 0,
-                           ctx->stream, payload, offs, R, dsegbase, (uint32_t)plan.S, dres, status,
-                           redo);
+                           ctx->stream, payload, (u64)payload_bytes, offs, R, dsegbase,
+                           (uint32_t)plan.S, dres, status, redo, b->elements, view(d), tabs,
+                           hh_small, tag, vers,
+                           inline_redo ? reinterpret_cast<u64x2*>(b->dev) : (u64x2*)nullptr);
         LJ_LAUNCHED(ctx);
+        if (inline_redo) return LASPJ_OK;
         // the redo pass: usually an empty list (the kernel exits at once)
         const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
         hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
@@ -4515,11 +4592,16 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
     if (int s = reserve_scratch(ctx, 8ull * R * (nch + 1ull))) return s;
     u64* co = static_cast<u64*>(ctx->scratch);
     const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+    // up to 4 replicas the last block scans them all (one launch); more go to the
+    // per-replica scan kernel
+    const bool one = R <= 4;
     hipLaunchKernelGGL(k_etf_join_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
                        reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b),
-                       reinterpret_cast<u64x2*>(z->dev), R, z->elements, view(d), nch, co, flag);
-    hipLaunchKernelGGL(k_etf_chunk_scan_offsets, dim3((unsigned)std::min<uint64_t>(R, 65535)),
-                       dim3(kBlock), 0, ctx->stream, co, R, nch, hdr, offsets, ticket);
+                       reinterpret_cast<u64x2*>(z->dev), R, z->elements, view(d), nch, co, flag,
+                       one ? ticket : nullptr, hdr, offsets);
+    if (!one)
+        hipLaunchKernelGGL(k_etf_chunk_scan_offsets, dim3((unsigned)std::min<uint64_t>(R, 65535)),
+                           dim3(kBlock), 0, ctx->stream, co, R, nch, hdr, offsets, ticket);
     LJ_LAUNCHED(ctx);
     *chunks = co;
     return LASPJ_OK;
@@ -4893,23 +4975,39 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
-    if (laspj::dev_malloc(ctx, &d->block, bytes) != hipSuccess) {
+    // a block from the context's cache (a rebuilt dictionary of the same size class takes
+    // the block its predecessor gave back: no hipMalloc / hipFree per rebuild)
+    if (laspj::dev_alloc(ctx, bytes, &d->block) != hipSuccess) {
         hipGetLastError();
         delete d;
         return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: hipMalloc(%llu)", (unsigned long long)bytes);
     }
+    d->block_bytes = bytes;
     char* base = static_cast<char*>(d->block);
-    // every array staged into one host image of the block, then one copy
-    std::vector<char> img;
-    try {
-        img.assign(bytes, 0);
-    } catch (const std::bad_alloc&) {
-        hipFree(d->block);
-        delete d;
-        return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host staging");
+    // every array staged into one pinned host image of the block (the context's, grow-only;
+    // the previous image's copy has finished before it is rewritten), then one async copy
+    hipStreamSynchronize(ctx->stream);
+    if (ctx->dstage_bytes < bytes) {
+        if (ctx->dstage) hipHostFree(ctx->dstage);
+        ctx->dstage = nullptr;
+        ctx->dstage_bytes = 0;
+        const uint64_t want = std::max<uint64_t>(bytes, 1ull << 20) + bytes / 4;
+        if (hipHostMalloc(&ctx->dstage, want, hipHostMallocDefault) != hipSuccess) {
+            hipGetLastError();
+            ctx->dstage = nullptr;
+            laspj::dev_release(ctx, d->block, bytes);
+            delete d;
+            return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: pinned staging");
+        }
+        ctx->dstage_bytes = want;
     }
+    char* img = static_cast<char*>(ctx->dstage);
+    // the arrays, then zeros in the alignment gaps between them (nothing reads them; kept
+    // deterministic) — no zero fill of the whole image first
+    std::vector<std::pair<uint64_t, uint64_t>> spans;
     auto up = [&](uint64_t off, const void* src, uint64_t n) {
-        if (n) std::memcpy(img.data() + off, src, n);
+        if (n) std::memcpy(img + off, src, n);
+        spans.emplace_back(off, n);
         return hipSuccess;
     };
     hipError_t e = hipSuccess;
@@ -4935,9 +5033,18 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess) e = up(o_gsr, gs_rank.data(), 4ull * E);
     if (e == hipSuccess) e = up(o_gsb, gs_byte.data(), 4ull * 256);
     if (e == hipSuccess && !gs_itab.empty()) e = up(o_gsi, gs_itab.data(), 8ull * gs_itab.size());
-    if (e == hipSuccess) e = hipMemcpy(base, img.data(), bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        std::sort(spans.begin(), spans.end());
+        uint64_t at = 0;
+        for (const auto& sp : spans) {
+            if (sp.first > at) std::memset(img + at, 0, sp.first - at);
+            at = std::max(at, sp.first + sp.second);
+        }
+        if (bytes > at) std::memset(img + at, 0, bytes - at);
+        e = hipMemcpyAsync(base, img, bytes, hipMemcpyHostToDevice, ctx->stream);
+    }
     if (e != hipSuccess) {
-        hipFree(d->block);
+        laspj::dev_release(ctx, d->block, bytes);
         delete d;
         return fail(ctx, LASPJ_E_DEVICE, "etf_dict_create: upload: %s", hipGetErrorString(e));
     }
@@ -4991,9 +5098,13 @@ int laspj_etf_dict_destroy(laspj_etf_dict* d) {
     {
         std::lock_guard<std::mutex> lk(d->ctx->mu);
         hipSetDevice(d->ctx->device);
-        hipStreamSynchronize(d->ctx->stream);
-        hipFree(d->block);
-        if (d->rd_btab) hipFree(d->rd_btab);
+        // back to the context's cache: its next user is ordered after every kernel that
+        // read this image (all on the context's stream)
+        laspj::dev_release(d->ctx, d->block, d->block_bytes);
+        if (d->rd_btab) {
+            hipStreamSynchronize(d->ctx->stream);
+            hipFree(d->rd_btab);
+        }
     }
     delete d;
     return LASPJ_OK;

@@ -49,6 +49,10 @@ struct laspj_ctx {
     // pinned host staging for the small readbacks (sizes, statuses, flags): a round trip
     // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
     void* pinned = nullptr;
+    // pinned staging for device dictionary images (laspj_etf_dict_create), grow-only: the
+    // NIF path rebuilds its image whenever a call registers new terms
+    void* dstage = nullptr;
+    uint64_t dstage_bytes = 0;
     static constexpr uint64_t kPinned = 64 * 1024;
     // released device blocks by size class (laspj::dev_alloc / dev_release): every kernel
     // runs on `stream`, so a block released after its last enqueued use can serve the

@@ -459,18 +459,16 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         }
         if (unknown.empty()) break;
         // terms the dictionary has not seen (or operands that are not orddicts, which the
-        // second pass tells apart): register the operands of every answer concerned
-        std::vector<uint8_t> want(n, 0);
-        for (uint32_t i : unknown) want[answer_of(i)] = 1;
+        // second pass tells apart): register the operands that met them (an operand that
+        // decoded holds only registered terms)
         std::vector<const uint8_t*> rp;
         std::vector<uint64_t> rl;
         std::vector<uint32_t> ri;
-        for (uint32_t i = 0; i < m; ++i)
-            if (want[answer_of(i)]) {
-                rp.push_back(c.p[i]);
-                rl.push_back(c.len[i]);
-                ri.push_back(i);
-            }
+        for (uint32_t i : unknown) {
+            rp.push_back(c.p[i]);
+            rl.push_back(c.len[i]);
+            ri.push_back(i);
+        }
         uint32_t nd = 0;
         uint64_t eb, tb;
         laspj_dict_info(S->dict, &nd, &eb, &tb);

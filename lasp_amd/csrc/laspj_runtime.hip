@@ -287,6 +287,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->lscratch) hipFree(ctx->lscratch);
         laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
+        if (ctx->dstage) hipHostFree(ctx->dstage);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -340,8 +341,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_etf = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_READ:
-            if (value < 0 || value > 9)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..9");
+            if (value < 0 || value > 10)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..10");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_SEG:

@@ -695,11 +695,12 @@ def test_gpu_from_binary_fuzz():
     assert np.array_equal(st, st_serial), np.nonzero(st != st_serial)[0][:10]
     ok0 = st == 0
     assert np.array_equal(bt.download()[ok0], bs.download()[ok0])
-    bg = ctx.orset_batch(len(blobs), E)
-    with _read_kernel(ctx, 4):               # segment mode: same statuses and cells
-        st_seg = bg.etf_decode(d, pay, offs, tag=T, vers=1)
-    assert np.array_equal(st_seg, st_serial), np.nonzero(st_seg != st_serial)[0][:10]
-    assert np.array_equal(bg.download()[ok0], bs.download()[ok0])
+    for knob in (4, 10):                     # segment mode: same statuses and cells
+        bg = ctx.orset_batch(len(blobs), E)
+        with _read_kernel(ctx, knob):
+            st_seg = bg.etf_decode(d, pay, offs, tag=T, vers=1)
+        assert np.array_equal(st_seg, st_serial), np.nonzero(st_seg != st_serial)[0][:10]
+        assert np.array_equal(bg.download()[ok0], bs.download()[ok0])
     ok = np.nonzero(st == 0)[0]
     if len(ok):
         again = bt.to_binaries(d, tag=T, vers=1)
@@ -847,7 +848,7 @@ def test_gpu_from_binary_small_tokens_large():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 4])
+@pytest.mark.parametrize("knob", [0, 4, 10])
 def test_gpu_from_binary_segments(knob):
     """Long payloads split between waves (automatic for a few long payloads, knob 0;
     every payload in 256-byte segments, knob 4): one 10k-element orddict, a few 2k-element
