@@ -44,15 +44,15 @@ struct laspj_etf_dict {
     const uint32_t* elem_off = nullptr;    // E + 1
     const uint32_t* elem_order = nullptr;  // E
     const uint8_t* elem_byte = nullptr;    // E: 1 = image is SMALL_INTEGER_EXT (97, v)
-    const uint8_t* tok_blob = nullptr;
-    const uint32_t* tok_off = nullptr;     // 64E + 1
+    const uint8_t* tok_blob = nullptr;     // null: not kept on the device
+    const uint32_t* tok_off = nullptr;     // 64E + 1 (mixed image lengths only)
     const uint8_t* tok_order = nullptr;    // 64E
     const uint64_t* tok_mask = nullptr;    // E: token slots with an image
     // the same images again, each starting on a 16-byte boundary (wide loads)
     const uint8_t* elem_pad = nullptr;
     const uint32_t* elem_poff = nullptr;   // E
     const uint8_t* tok_pad = nullptr;
-    const uint32_t* tok_poff = nullptr;    // 64E
+    const uint32_t* tok_poff = nullptr;    // 64E (null: not kept on the device)
     // per element, tokens in term order: k | image length << 8 | padded offset << 32
     // (k = 0xFF after the last one) — one load per (element, rank)
     const uint64_t* tok_desc = nullptr;    // 64E
@@ -4743,7 +4743,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                             "etf_dict_create: token order of element %u misses a slot", e);
         }
     }
-    const uint64_t eblob = elem_off[E], tblob = toks ? tok_off[64ull * E] : 0;
+    const uint64_t eblob = elem_off[E];
     // 16-byte-aligned copies of every image (the write kernels load them 16 B at a time)
     auto pad16 = [](uint64_t x) { return (x + 15ull) & ~15ull; };
     std::vector<uint32_t> epoff(E), tpoff(toks ? 64ull * E : 0);
@@ -4959,12 +4959,17 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
             }
         }
     }
+    // on the device: the token offsets only for mixed image lengths (the size pass reads
+    // them then); the token images themselves and their padded offsets never (the kernels
+    // read the padded copies through tok_desc) — 64 E-slot arrays the NIF path's rebuilds
+    // would otherwise stage and copy every time
+    const bool dev_toff = toks && mixed;
     const uint64_t o_eoff = 0, o_eord = o_eoff + al(4ull * (E + 1)), o_eb = o_eord + al(4ull * E),
                    o_mask = o_eb + al(E), o_toff = o_mask + al(8ull * E),
-                   o_tord = o_toff + (toks ? al(4ull * (64ull * E + 1)) : 0),
+                   o_tord = o_toff + (dev_toff ? al(4ull * (64ull * E + 1)) : 0),
                    o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
-                   o_epoff = o_tblob + al(tblob + 1), o_tpoff = o_epoff + al(4ull * E),
-                   o_epad = o_tpoff + al(4ull * tpoff.size() + 4), o_tpad = o_epad + al(epad_n),
+                   o_epoff = o_tblob, o_tpoff = o_epoff + al(4ull * E),
+                   o_epad = o_tpoff, o_tpad = o_epad + al(epad_n),
                    o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
                    o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
@@ -5015,12 +5020,12 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     if (e == hipSuccess) e = up(o_eord, elem_order, 4ull * E);
     if (e == hipSuccess) e = up(o_eb, ebyte.data(), E);
     if (e == hipSuccess) e = up(o_mask, tmask.data(), 8ull * E);
-    if (e == hipSuccess && toks) e = up(o_toff, tok_off, 4ull * (64ull * E + 1));
+    if (e == hipSuccess && dev_toff) e = up(o_toff, tok_off, 4ull * (64ull * E + 1));
     if (e == hipSuccess && toks) e = up(o_tord, tok_order, 64ull * E);
     if (e == hipSuccess) e = up(o_eblob, elem_blob, eblob);
-    if (e == hipSuccess && toks) e = up(o_tblob, tok_blob, tblob);
+
     if (e == hipSuccess) e = up(o_epoff, epoff.data(), 4ull * E);
-    if (e == hipSuccess && toks) e = up(o_tpoff, tpoff.data(), 4ull * tpoff.size());
+
     if (e == hipSuccess) e = up(o_epad, epad.data(), epad_n);
     if (e == hipSuccess && toks) e = up(o_tpad, tpad.data(), tpad_n);
     if (e == hipSuccess && toks) e = up(o_tdesc, tdesc.data(), 8ull * tdesc.size());
@@ -5080,12 +5085,12 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->elem_order = reinterpret_cast<const uint32_t*>(base + o_eord);
     d->elem_byte = reinterpret_cast<const uint8_t*>(base + o_eb);
     d->tok_mask = reinterpret_cast<const uint64_t*>(base + o_mask);
-    d->tok_off = toks ? reinterpret_cast<const uint32_t*>(base + o_toff) : nullptr;
+    d->tok_off = dev_toff ? reinterpret_cast<const uint32_t*>(base + o_toff) : nullptr;
     d->tok_order = toks ? reinterpret_cast<const uint8_t*>(base + o_tord) : nullptr;
     d->elem_blob = reinterpret_cast<const uint8_t*>(base + o_eblob);
-    d->tok_blob = toks ? reinterpret_cast<const uint8_t*>(base + o_tblob) : nullptr;
+    d->tok_blob = nullptr;                 // (host-side arrays only, see above)
     d->elem_poff = reinterpret_cast<const uint32_t*>(base + o_epoff);
-    d->tok_poff = toks ? reinterpret_cast<const uint32_t*>(base + o_tpoff) : nullptr;
+    d->tok_poff = nullptr;
     d->elem_pad = reinterpret_cast<const uint8_t*>(base + o_epad);
     d->tok_pad = toks ? reinterpret_cast<const uint8_t*>(base + o_tpad) : nullptr;
     d->tok_desc = toks ? reinterpret_cast<const uint64_t*>(base + o_tdesc) : nullptr;

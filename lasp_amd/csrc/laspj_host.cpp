@@ -453,8 +453,17 @@ struct Dict {
     // a token), undone in reverse when the payload fails: binary_to_term/1 would have
     // rejected it whole, so none of its terms may take a slot
     std::vector<int64_t> journal;
+    // laspj_dict_export's term orders, kept between exports (registrations only append):
+    // element slots sorted by term (the first ord_n slots), each element's token slots
+    // sorted by term (valid while its size matches the element's token count)
+    mutable std::vector<uint32_t> ord;
+    mutable uint32_t ord_n = 0;
+    mutable std::vector<std::vector<uint8_t>> tord;
 
     void rollback() {
+        ord.clear();
+        ord_n = 0;
+        tord.clear();
         for (size_t j = journal.size(); j-- > 0;) {
             if (journal[j] < 0) {
                 elem_slot.pop_last();
@@ -748,12 +757,26 @@ int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, ui
             if (off > 0xFFFFFFFFull) return LASPJ_E_RANGE;
             elem_off[e + 1] = (uint32_t)off;
         }
-        std::vector<uint32_t> ord(K);
-        for (uint32_t e = 0; e < K; ++e) ord[e] = e;
-        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-            return cmp_view(d.elems[x], d.elems[y]) < 0;
-        });
+        // the cached order of the first ord_n slots, the newer slots sorted and merged in
+        // (ties keep slot order: std::merge takes the earlier range's element first)
+        auto less = [&](uint32_t x, uint32_t y) { return cmp_view(d.elems[x], d.elems[y]) < 0; };
+        if (d.ord_n > K) {
+            d.ord.clear();
+            d.ord_n = 0;
+        }
+        if (d.ord_n < K) {
+            std::vector<uint32_t> add(K - d.ord_n);
+            for (uint32_t e = d.ord_n; e < K; ++e) add[e - d.ord_n] = e;
+            std::stable_sort(add.begin(), add.end(), less);
+            std::vector<uint32_t> merged(K);
+            std::merge(d.ord.begin(), d.ord.end(), add.begin(), add.end(), merged.begin(), less);
+            d.ord.swap(merged);
+            d.ord_n = K;
+        }
+        const std::vector<uint32_t>& ord = d.ord;
         for (uint32_t e = 0; e < E; ++e) elem_order[e] = e < K ? ord[e] : e;
+        if (d.tord.size() > K) d.tord.clear();
+        d.tord.resize(K);
         if (tok_off) {
             uint64_t to = 0;
             tok_off[0] = 0;
@@ -770,11 +793,14 @@ int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, ui
                     uint8_t* o = tok_order + 64ull * e;
                     memset(o, 0xFF, 64);
                     if (e < K) {
-                        std::vector<uint8_t> ts(d.toks[e].size());
-                        for (size_t k = 0; k < ts.size(); ++k) ts[k] = (uint8_t)k;
-                        std::stable_sort(ts.begin(), ts.end(), [&](uint8_t x, uint8_t y) {
-                            return cmp_view(d.toks[e][x], d.toks[e][y]) < 0;
-                        });
+                        std::vector<uint8_t>& ts = d.tord[e];
+                        if (ts.size() != d.toks[e].size()) {    // tokens added since
+                            ts.resize(d.toks[e].size());
+                            for (size_t k = 0; k < ts.size(); ++k) ts[k] = (uint8_t)k;
+                            std::stable_sort(ts.begin(), ts.end(), [&](uint8_t x, uint8_t y) {
+                                return cmp_view(d.toks[e][x], d.toks[e][y]) < 0;
+                            });
+                        }
                         memcpy(o, ts.data(), ts.size());
                     }
                 }
