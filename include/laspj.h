@@ -813,8 +813,9 @@ int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
  * nanoseconds summed over device passes: [8] staging + enqueueing, [9] waiting for the
  * device, [10] reading the answers after it, [11] the part of [8] spent copying operands
  * into pinned memory, [12] registering operands' terms in the host dictionary, [13]
- * rebuilding the device images */
-#define LASPJ_NIF_STATS 14
+ * rebuilding or patching the device images; [14] device image patches (registrations
+ * that only added tokens to known elements, rewritten in place instead of rebuilt) */
+#define LASPJ_NIF_STATS 15
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
 /* drop the context's dictionary (its memory; the next call registers afresh) */
 int laspj_nif_reset(laspj_ctx* ctx);

@@ -41,7 +41,7 @@ TUNE_ETF_SEG = 9
 TUNE_LIST_WALK = 10
 TUNE_NIF_PIECE = 11
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
-NIF_STATS = 14
+NIF_STATS = 15
 
 
 class LaspjUnavailable(RuntimeError):

@@ -92,6 +92,13 @@ struct laspj_etf_dict {
     // on the device the first time a batch needs them (k_build_btab); own allocation
     uint8_t* rd_btab = nullptr;
     bool btab_tried = false;
+    // host-side state for laspj::etf_dict_patch (dictionaries built with token headroom,
+    // the NIF path's): slot -> rank, each token slot's padded image offset (0xFFFFFFFF:
+    // none), where the patched arrays sit in the block, the padded-image area's use
+    bool patchable = false;
+    std::vector<uint32_t> h_rank, h_tpoff;
+    uint64_t o_mask = 0, o_tord = 0, o_tpad = 0, o_tdesc = 0, o_rpad = 0, o_rd = 0;
+    uint64_t tpad_used = 0, tpad_cap = 0;
 };
 
 namespace laspj {
@@ -4696,10 +4703,14 @@ using laspj::fail;
 
 extern "C" {
 
-int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
-                          const uint32_t* elem_off, const uint32_t* elem_order,
-                          const uint8_t* tok_blob, const uint32_t* tok_off,
-                          const uint8_t* tok_order, laspj_etf_dict** out) {
+// tok_headroom: build the per-element token tables for up to that many more tokens per
+// element than the widest element has (at most 8 while that stays <= 8, at most 64), keep
+// the host state etf_dict_patch needs and room for appended token images
+static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
+                                const uint32_t* elem_off, const uint32_t* elem_order,
+                                const uint8_t* tok_blob, const uint32_t* tok_off,
+                                const uint8_t* tok_order, uint32_t tok_headroom,
+                                laspj_etf_dict** out) {
     if (!ctx || !out || !elem_off || !elem_order || (!elem_blob && elem_off[E]))
         return fail(ctx, LASPJ_E_INVAL, "etf_dict_create: null argument");
     *out = nullptr;
@@ -4773,6 +4784,11 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     uint32_t tok_max = 0;
     for (uint32_t x = 0; x < E; ++x)
         tok_max = std::max(tok_max, (uint32_t)__builtin_popcountll(tmask[x]));
+    if (tok_headroom && toks)
+        tok_max = tok_max <= 8 ? std::min(8u, tok_max + tok_headroom)
+                               : std::min(64u, tok_max + tok_headroom);
+    // room for token images appended by etf_dict_patch
+    const uint64_t tpad_cap = tpad_n + (tok_headroom && toks ? std::max<uint64_t>(tpad_n / 4, 1ull << 16) : 0);
     // record templates (uniform token images only): 104 2 <image> per (element, term rank),
     // and 104 2 <elem image> 108 per element
     const uint32_t rec_len = (toks && !mixed && uniform && uniform + 2u <= 48u) ? uniform + 2u : 0u;
@@ -4970,7 +4986,7 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                    o_eblob = o_tord + (toks ? al(64ull * E) : 0), o_tblob = o_eblob + al(eblob + 1),
                    o_epoff = o_tblob, o_tpoff = o_epoff + al(4ull * E),
                    o_epad = o_tpoff, o_tpad = o_epad + al(epad_n),
-                   o_tdesc = o_tpad + al(tpad_n), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
+                   o_tdesc = o_tpad + al(tpad_cap), o_rpad = o_tdesc + al(8ull * tdesc.size() + 8),
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
                    o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
                    o_htab = o_rd + al(rd.size() + 8), o_gsh = o_htab + al(4ull * htab.size() + 4),
@@ -5094,8 +5110,32 @@ int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
     d->elem_pad = reinterpret_cast<const uint8_t*>(base + o_epad);
     d->tok_pad = toks ? reinterpret_cast<const uint8_t*>(base + o_tpad) : nullptr;
     d->tok_desc = toks ? reinterpret_cast<const uint64_t*>(base + o_tdesc) : nullptr;
+    if (tok_headroom && toks && rec_len && hashed) {
+        d->patchable = true;
+        d->h_rank.assign(E, 0);
+        for (uint32_t r = 0; r < E; ++r) d->h_rank[elem_order[r]] = r;
+        d->h_tpoff.assign(64ull * E, 0xFFFFFFFFu);
+        for (uint64_t t = 0; t < 64ull * E; ++t)
+            if (tok_off[t + 1] > tok_off[t]) d->h_tpoff[t] = tpoff[t];
+        d->o_mask = o_mask;
+        d->o_tord = o_tord;
+        d->o_tpad = o_tpad;
+        d->o_tdesc = o_tdesc;
+        d->o_rpad = o_rpad;
+        d->o_rd = o_rd;
+        d->tpad_used = tpad_n - 48;
+        d->tpad_cap = tpad_cap;
+    }
     *out = d;
     return LASPJ_OK;
+}
+
+int laspj_etf_dict_create(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
+                          const uint32_t* elem_off, const uint32_t* elem_order,
+                          const uint8_t* tok_blob, const uint32_t* tok_off,
+                          const uint8_t* tok_order, laspj_etf_dict** out) {
+    return etf_dict_create_body(ctx, E, elem_blob, elem_off, elem_order, tok_blob, tok_off,
+                                tok_order, 0, out);
 }
 
 int laspj_etf_dict_destroy(laspj_etf_dict* d) {
@@ -5150,3 +5190,175 @@ int laspj_gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ dictionary patches
+namespace laspj {
+
+namespace {
+
+struct PatchRec {
+    u64 dst;            // byte offset in the dictionary's block
+    uint32_t src, len;  // bytes [src, src + len) of the staged patch data
+};
+
+// one block per record, bytes copied as they stand (records are a few hundred bytes)
+__global__ __launch_bounds__(kBlock) void k_patch(const uint8_t* src, const PatchRec* recs,
+                                                  uint32_t n, uint8_t* base) {
+    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const PatchRec pr = recs[r];
+        for (uint32_t i = threadIdx.x; i < pr.len; i += kBlock) base[pr.dst + i] = src[pr.src + i];
+    }
+}
+
+}  // namespace
+
+int etf_dict_create_ex(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
+                       const uint32_t* elem_off, const uint32_t* elem_order,
+                       const uint8_t* tok_blob, const uint32_t* tok_off, const uint8_t* tok_order,
+                       uint32_t tok_headroom, laspj_etf_dict** out) {
+    return etf_dict_create_body(ctx, E, elem_blob, elem_off, elem_order, tok_blob, tok_off,
+                                tok_order, tok_headroom, out);
+}
+
+// The device rows of element slots `dirty` (each gained tokens in the host dictionary `hd`
+// since `d` was built or last patched) rewritten from the host dictionary, as a full
+// rebuild would write them: token mask, term order, writer descriptors (a new token's
+// padded image appended to the image area), record templates, the from_binary tables of
+// its rank (bucket word and shift chosen again, bucket per term rank, slot -> rank).  One
+// staged copy of the rows and one scatter launch, on the context's stream.  Returns
+// LASPJ_E_UNSUPPORTED (nothing written) when only a rebuild will do: a dictionary built
+// without headroom, an element past its token headroom, a token image of another length,
+// no bucket choice that separates the element's tokens, the image area full.
+int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
+                   const uint32_t* dirty, uint32_t n) {
+    if (!d || !d->patchable || d->rd_btab) return LASPJ_E_UNSUPPORTED;
+    if (n == 0) return LASPJ_OK;
+    const uint32_t E = d->elements, RK = d->tok_max, RL = d->rec_len;
+    const uint64_t RS = d->rec_stride;
+    const uint32_t TL = d->tok_uniform;
+    std::vector<uint8_t> data;
+    std::vector<PatchRec> recs;
+    auto put = [&](u64 dst, const void* p, uint32_t len) {
+        const uint32_t at = (uint32_t)data.size();
+        data.resize(data.size() + ((len + 15u) & ~15u), 0);
+        std::memcpy(data.data() + at, p, len);
+        recs.push_back(PatchRec{dst, at, len});
+    };
+    uint64_t tpad_used = d->tpad_used;
+    std::vector<std::pair<uint64_t, uint32_t>> new_tpoff;     // (slot index, offset)
+    std::vector<std::string_view> imgs;
+    std::vector<uint8_t> order;
+    const uint64_t o_desc = d->o_rd, o_tb = d->o_rd + 80ull * E,
+                   o_ros = o_tb + 2ull * E * RK;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t e = dirty[i];
+        if (e >= E || !dict_tokens(hd, e, &imgs, &order)) return LASPJ_E_UNSUPPORTED;
+        const uint32_t cnt = (uint32_t)imgs.size();
+        if (cnt > RK || cnt > 64 || cnt == 0) return LASPJ_E_UNSUPPORTED;
+        for (const auto& im : imgs)
+            if (im.size() != TL || TL + 2u != RL) return LASPJ_E_UNSUPPORTED;
+        // token mask and term order
+        const u64 mask = cnt == 64 ? ~0ull : (1ull << cnt) - 1ull;
+        put(d->o_mask + 8ull * e, &mask, 8);
+        uint8_t ord[64];
+        std::memset(ord, 0xFF, 64);
+        std::memcpy(ord, order.data(), cnt);
+        put(d->o_tord + 64ull * e, ord, 64);
+        // padded images of the new slots, appended
+        uint32_t tpo[64];
+        for (uint32_t k = 0; k < 64; ++k) {
+            uint32_t o = k < cnt ? d->h_tpoff[64ull * e + k] : 0xFFFFFFFFu;
+            for (const auto& nt : new_tpoff)
+                if (nt.first == 64ull * e + k) o = nt.second;
+            if (k < cnt && o == 0xFFFFFFFFu) {
+                const uint64_t need = (TL + 15u) & ~15u;
+                if (tpad_used + need + 48 > d->tpad_cap) return LASPJ_E_UNSUPPORTED;
+                o = (uint32_t)tpad_used;
+                tpad_used += need;
+                put(d->o_tpad + o, imgs[k].data(), TL);
+                new_tpoff.emplace_back(64ull * e + k, o);
+            }
+            tpo[k] = o;
+        }
+        // writer descriptors by term rank: slot | length << 8 | padded offset << 32
+        u64 td[64];
+        for (uint32_t j = 0; j < 64; ++j)
+            td[j] = j < cnt ? (u64)order[j] | ((u64)TL << 8) | ((u64)tpo[order[j]] << 32) : 0xFFull;
+        put(d->o_tdesc + 8ull * 64 * e, td, 8 * 64);
+        // record templates by term rank
+        std::vector<uint8_t> rows((size_t)RK * RS, 0);
+        for (uint32_t j = 0; j < cnt; ++j) {
+            uint8_t* r = rows.data() + j * RS;
+            r[0] = 104;
+            r[1] = 2;
+            std::memcpy(r + 2, imgs[order[j]].data(), TL);
+        }
+        put(d->o_rpad + (u64)e * RK * RS, rows.data(), (uint32_t)rows.size());
+        // from_binary tables of the element's rank
+        const uint32_t r = d->h_rank[e];
+        uint32_t key = 0;
+        std::vector<uint16_t> tb(RK, 0);
+        bool placed = false;
+        std::vector<uint32_t> keys(cnt);
+        for (uint32_t wi = RL / 4; wi-- > 0 && !placed;) {
+            for (uint32_t j = 0; j < cnt; ++j) std::memcpy(&keys[j], rows.data() + j * RS + 4 * wi, 4);
+            for (uint32_t sh = 0; sh + 10 <= 32 && !placed; ++sh) {
+                uint64_t seen[kBuckets / 64] = {};
+                bool ok = true;
+                for (uint32_t j = 0; j < cnt && ok; ++j) {
+                    const uint32_t bk = (keys[j] >> sh) & (kBuckets - 1u);
+                    ok = !((seen[bk / 64] >> (bk % 64)) & 1ull);
+                    seen[bk / 64] |= 1ull << (bk % 64);
+                }
+                if (!ok) continue;
+                placed = true;
+                key = wi | (sh << 8);
+                for (uint32_t j = 0; j < cnt; ++j) tb[j] = (uint16_t)((keys[j] >> sh) & (kBuckets - 1u));
+            }
+        }
+        if (!placed) return LASPJ_E_UNSUPPORTED;
+        // descriptor {slot, header length, key, tokens}: the first two do not change
+        const uint32_t kc[2] = {key, cnt};
+        put(o_desc + 16ull * r + 8, kc, 8);
+        put(o_tb + 2ull * r * RK, tb.data(), 2 * RK);
+        uint8_t ros[64];
+        std::memset(ros, 0xFF, 64);
+        for (uint32_t j = 0; j < cnt; ++j) ros[order[j]] = (uint8_t)j;
+        put(o_ros + 64ull * r, ros, 64);
+    }
+    // stage and scatter
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipSetDevice(ctx->device);
+    const uint64_t rec_bytes = recs.size() * sizeof(PatchRec);
+    const uint64_t total = data.size() + ((rec_bytes + 15) & ~15ull);
+    hipStreamSynchronize(ctx->stream);                // the pinned staging is free
+    if (ctx->dstage_bytes < total) {
+        if (ctx->dstage) hipHostFree(ctx->dstage);
+        ctx->dstage = nullptr;
+        ctx->dstage_bytes = 0;
+        if (hipHostMalloc(&ctx->dstage, std::max<uint64_t>(total, 1ull << 20), hipHostMallocDefault) != hipSuccess) {
+            hipGetLastError();
+            ctx->dstage = nullptr;
+            return LASPJ_E_NOMEM;
+        }
+        ctx->dstage_bytes = std::max<uint64_t>(total, 1ull << 20);
+    }
+    char* st = static_cast<char*>(ctx->dstage);
+    std::memcpy(st, data.data(), data.size());
+    std::memcpy(st + data.size(), recs.data(), rec_bytes);
+    if (int s = reserve_scratch(ctx, total)) return s;
+    char* dev = static_cast<char*>(ctx->scratch);
+    if (hipMemcpyAsync(dev, st, total, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        return LASPJ_E_DEVICE;
+    hipLaunchKernelGGL(k_patch, dim3((unsigned)std::min<uint64_t>(recs.size(), 4096)), dim3(kBlock),
+                       0, ctx->stream, reinterpret_cast<const uint8_t*>(dev),
+                       reinterpret_cast<const PatchRec*>(dev + data.size()), (uint32_t)recs.size(),
+                       static_cast<uint8_t*>(d->block));
+    if (hipGetLastError() != hipSuccess) return LASPJ_E_DEVICE;
+    for (const auto& nt : new_tpoff) d->h_tpoff[nt.first] = nt.second;
+    d->tpad_used = tpad_used;
+    return LASPJ_OK;
+}
+
+}  // namespace laspj
+

@@ -887,3 +887,41 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ internal accessors
+// (laspj_internal.h): what laspj::etf_dict_patch reads from the host dictionary when the
+// NIF path patches the device images of elements that gained tokens instead of
+// rebuilding them
+namespace laspj {
+
+uint32_t dict_elements(const laspj_dict* dict) {
+    return dict ? (uint32_t)dict->d.elems.size() : 0u;
+}
+
+uint32_t dict_token_count(const laspj_dict* dict, uint32_t e) {
+    if (!dict || e >= dict->d.toks.size()) return 0;
+    return (uint32_t)dict->d.toks[e].size();
+}
+
+// element slot e's token images by slot, and its slots in term order (order[j] = the slot
+// of the j-th smallest token): the same order laspj_dict_export writes (and caches)
+bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_view>* imgs,
+                 std::vector<uint8_t>* order) {
+    if (!dict || e >= dict->d.toks.size()) return false;
+    const Dict& d = dict->d;
+    const auto& tv = d.toks[e];
+    imgs->assign(tv.begin(), tv.end());
+    if (d.tord.size() < d.toks.size()) d.tord.resize(d.toks.size());
+    std::vector<uint8_t>& ts = d.tord[e];
+    if (ts.size() != tv.size()) {
+        ts.resize(tv.size());
+        for (size_t k = 0; k < ts.size(); ++k) ts[k] = (uint8_t)k;
+        std::stable_sort(ts.begin(), ts.end(), [&](uint8_t x, uint8_t y) {
+            return cmp_view(tv[x], tv[y]) < 0;
+        });
+    }
+    *order = ts;
+    return true;
+}
+
+}  // namespace laspj

@@ -8,6 +8,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "../../include/laspj.h"
@@ -257,5 +258,22 @@ int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict*
 int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                       int32_t kind, int tag, int vers, const unsigned long long* offsets,
                       uint8_t* out, uint64_t cap, const unsigned long long* chunks);
+
+// laspj_etf_dict_create with per-element token headroom (up to tok_headroom more tokens
+// per element than the widest has) and the host state etf_dict_patch needs
+int etf_dict_create_ex(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
+                       const uint32_t* elem_off, const uint32_t* elem_order,
+                       const uint8_t* tok_blob, const uint32_t* tok_off, const uint8_t* tok_order,
+                       uint32_t tok_headroom, laspj_etf_dict** out);
+// rewrite the device rows of element slots that gained tokens in the host dictionary
+// (call without ctx->mu held); LASPJ_E_UNSUPPORTED: rebuild instead (nothing written)
+int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
+                   const uint32_t* dirty, uint32_t n);
+// host dictionary (laspj_host.cpp): element slots, tokens of a slot, its images and their
+// term order (order[j] = slot of the j-th smallest)
+uint32_t dict_elements(const laspj_dict* dict);
+uint32_t dict_token_count(const laspj_dict* dict, uint32_t e);
+bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_view>* imgs,
+                 std::vector<uint8_t>* order);
 
 }  // namespace laspj

@@ -56,6 +56,11 @@ struct NifState {
     uint64_t clean_words = 0;
     uint32_t clean_E = 0;
     uint64_t stats[LASPJ_NIF_STATS] = {};
+    // what `etf` was built (or last patched) from: host dictionary elements and each
+    // one's token count, so registrations that only add tokens to known elements are
+    // patched into the device images (etf_dict_patch) instead of rebuilding them
+    uint32_t built_K = 0;
+    std::vector<uint32_t> built_cnt;
 };
 
 namespace {
@@ -178,15 +183,40 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S) {
         return fail(ctx, LASPJ_E_INVAL, "nif: dictionary export");
     free_etf(S);
     laspj_etf_dict* d = nullptr;
-    if (int s = laspj_etf_dict_create(ctx, E, ebl.data(), eoff.data(), eord.data(), tbl.data(),
-                                      toff.data(), tord.data(), &d))
+    // two tokens of headroom per element: a call that only adds tokens to known elements
+    // patches the images (patch_etf) instead of coming back here
+    if (int s = etf_dict_create_ex(ctx, E, ebl.data(), eoff.data(), eord.data(), tbl.data(),
+                                   toff.data(), tord.data(), 2, &d))
         return s;
     S->etf = d;
     S->E = E;
     S->stale = false;
+    S->built_K = n;
+    S->built_cnt.resize(n);
+    for (uint32_t e = 0; e < n; ++e) S->built_cnt[e] = dict_token_count(S->dict, e);
     ++S->stats[4];
     S->stats[13] += now_ns() - t0;
     return LASPJ_OK;
+}
+
+// Registrations that only added tokens to elements the images already hold: their rows
+// patched in place.  False: rebuild (new elements, an element past its headroom, ...).
+bool patch_etf(laspj_ctx* ctx, NifState* S) {
+    if (!S->etf) return false;
+    const uint64_t t0 = now_ns();
+    const uint32_t n = dict_elements(S->dict);
+    if (n != S->built_K || n > S->E) return false;
+    std::vector<uint32_t> dirty;
+    for (uint32_t e = 0; e < n; ++e)
+        if (dict_token_count(S->dict, e) != S->built_cnt[e]) dirty.push_back(e);
+    if (!dirty.empty() &&
+        etf_dict_patch(ctx, S->etf, S->dict, dirty.data(), (uint32_t)dirty.size()) != LASPJ_OK)
+        return false;
+    for (uint32_t e : dirty) S->built_cnt[e] = dict_token_count(S->dict, e);
+    S->stale = false;
+    ++S->stats[14];
+    S->stats[13] += now_ns() - t0;
+    return true;
 }
 
 // One device pass: stage, copy, decode (or upload host-encoded cells), answer, copy back,
@@ -446,7 +476,8 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 for (uint32_t i = 0; i < m; ++i)
                     if (rst[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
             }
-            if (int s = rebuild_etf(ctx, S)) return s;
+            if (!patch_etf(ctx, S))
+                if (int s = rebuild_etf(ctx, S)) return s;
         }
         int s = device_pass(ctx, S, c);
         if (s == -1000) continue;                // answer area grown: once more

@@ -157,7 +157,8 @@ class Context:
         check(self.L.laspj_nif_stats(self.h, out, _lib.NIF_STATS), self.h)
         keys = ("calls", "device_passes", "registrations", "dict_resets", "image_rebuilds",
                 "host_encoded_passes", "fallbacks", "dict_elements", "ns_stage_enqueue",
-                "ns_device_wait", "ns_answers", "ns_stage_copy", "ns_register", "ns_rebuild")
+                "ns_device_wait", "ns_answers", "ns_stage_copy", "ns_register", "ns_rebuild",
+                "image_patches")
         return dict(zip(keys, (int(x) for x in out)))
 
     def nif_reset(self):

@@ -240,6 +240,50 @@ def test_nif_unknown_terms_register_once_then_one_pass():
 
 
 @pytest.mark.gpu
+def test_nif_new_tokens_patch_the_device_images():
+    """Replicas exchanging state after updates: every merge meets tokens the dictionary
+    has not seen, on elements it holds.  Those registrations patch the device images in
+    place (etf_dict_patch: token mask, term order, writer descriptors, record templates,
+    bucket tables of the elements concerned) instead of rebuilding them; an element that
+    outgrows its token headroom, or a new element, rebuilds.  Every answer is the
+    oracle's, image for image, across 60 rounds in which the state keeps growing."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(77)
+        elems = list(range(0, 900, 3))
+        mk = lambda: bytes(rng.getrandbits(8) for _ in range(20))  # noqa: E731
+        a = [(e, [(mk(), rng.random() < 0.3)]) for e in elems]
+        b = [(e, [(mk(), rng.random() < 0.3)]) for e in elems if rng.random() < 0.8]
+        cur = oorset.merge(a, b)
+        assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(cur))
+        s0 = ctx.nif_stats()
+        for rnd in range(60):
+            # the other replica's update: new tokens on a few known elements (its own
+            # earlier tokens kept), now and then a new element, a removal flag set
+            other = dict((e, list(ts)) for e, ts in cur)
+            for e in rng.sample(elems, rng.randint(1, 6)):
+                other.setdefault(e, []).append((mk(), rng.random() < 0.2))
+            if rnd % 17 == 16:
+                other[901 + rnd] = [(mk(), False)]
+            for e in rng.sample(list(other), 3):
+                ts = other[e]
+                j = rng.randrange(len(ts))
+                ts[j] = (ts[j][0], True)
+            o = sorted(((e, sorted(ts, key=lambda x: _key(x[0]))) for e, ts in other.items()),
+                       key=lambda x: _key(x[0]))
+            want = oorset.merge(cur, o)
+            got = ctx.nif_merge(_tb(cur), _tb(o))
+            assert got == (OK, _tb(want)), rnd
+            cur = want
+        s1 = ctx.nif_stats()
+        assert s1["image_patches"] - s0["image_patches"] >= 30
+        assert s1["image_rebuilds"] - s0["image_rebuilds"] < 30
+        assert s1["fallbacks"] == s0["fallbacks"]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 def test_nif_dictionary_reset_when_an_element_runs_out_of_token_slots():
     """Calls are self-contained, so a context whose dictionary has given an element all 64
     token slots starts a fresh dictionary for a call that needs more (and answers it)."""
