@@ -225,6 +225,8 @@ struct MS {
     uint32_t* tcnt;    // [R][ce_a + ce_b] tokens per output entry
     uint32_t* tile;    // [R][ntiles] entries per tile -> exclusive offsets
     uint32_t* tside;   // [R][ntiles] MODE 2: last single side in the tile -> side at its start
+    uint32_t* tsplit;  // [R][ntiles][4] the tile's merge-path start and end (i, j), found by
+                       // the counting pass, read by the writing pass
     uint32_t* chunk;   // [R][nchunks] tokens per chunk of kMT entries -> exclusive offsets
     uint32_t* nout;    // [R] output entries
     uint32_t* ntok;    // [R] output tokens
@@ -309,6 +311,52 @@ __device__ void mp_split(const u64* X, uint32_t nx, const u64* Y, uint32_t ny, u
     *pj = lower_bound(Y, 0, j, v);
 }
 
+// The first k in [lo, hi) with pred(k) true (hi when none) for a predicate that is false
+// then true, with every thread of the block probing: 256 candidates per step, so a range
+// of 10^5 takes three steps of one load each instead of ~17 dependent loads on one
+// thread.  Block-uniform arguments; s: one word of LDS.
+template <class P>
+__device__ uint32_t block_first_true(uint32_t lo, uint32_t hi, P pred, uint32_t* s) {
+    while (hi > lo) {
+        const uint32_t step = (hi - lo + kMT - 1) / kMT;           // >= 1
+        const uint32_t c = lo + threadIdx.x * step;
+        const bool f = c < hi && pred(c);
+        if (threadIdx.x == 0) s[0] = kMT;
+        __syncthreads();
+        const u64 bal = __ballot(f);
+        if (bal && lane_id() == 0)
+            atomicMin(s, (threadIdx.x & ~63u) + (uint32_t)__ffsll((long long)bal) - 1u);
+        __syncthreads();
+        const uint32_t t = s[0];
+        __syncthreads();                                            // s read before reuse
+        if (t == kMT) {
+            // every probe below hi is false: the answer is past the last of them
+            lo = lo + ((hi - 1 - lo) / step) * step + 1;
+        } else {
+            hi = lo + t * step;                                     // pred(hi) holds
+            if (t) lo = lo + (t - 1) * step + 1;                    // pred(probe t-1) fails
+        }
+    }
+    return lo;
+}
+
+// mp_split with the whole block searching (block-uniform arguments, every thread gets the
+// result)
+__device__ void mp_split_block(const u64* X, uint32_t nx, const u64* Y, uint32_t ny, uint32_t d,
+                               uint32_t* pi, uint32_t* pj, uint32_t* s) {
+    const uint32_t lo = d > ny ? d - ny : 0, hi = d < nx ? d : nx;
+    const uint32_t i = block_first_true(lo, hi, [&](uint32_t k) { return X[k] > Y[d - 1 - k]; }, s);
+    const uint32_t j = d - i;
+    if (i >= nx && j >= ny) {
+        *pi = nx;
+        *pj = ny;
+        return;
+    }
+    const u64 v = i >= nx ? Y[j] : (j >= ny ? X[i] : (X[i] < Y[j] ? X[i] : Y[j]));
+    *pi = block_first_true(0, i, [&](uint32_t k) { return X[k] >= v; }, s);
+    *pj = block_first_true(0, j, [&](uint32_t k) { return Y[k] >= v; }, s);
+}
+
 // key ranks of both sides, and whether either descends
 __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, uint64_t R) {
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
@@ -334,20 +382,33 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
 template <int MODE, bool WRITE>
 __global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t R) {
     __shared__ u64 s_win[kMWin];
-    __shared__ uint32_t s_si[kMT + 1], s_sj[kMT + 1], s_last[kMT], s_w[kMT / 64], s_b[4];
+    __shared__ uint32_t s_si[kMT + 1], s_sj[kMT + 1], s_last[kMT], s_w[kMT / 64], s_s[1];
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
         const uint32_t na = a.n(r), nb = b.n(r), n = na + nb;
         const uint32_t d0 = blockIdx.x * kMTile;
         if (m.unsorted[r] || d0 >= n) continue;              // uniform over the block
         const u64* X = m.sa + r * m.ce_a;
         const u64* Y = m.sb + r * m.ce_b;
-        if (threadIdx.x == 0) {
-            mp_split(X, na, Y, nb, d0, s_b, s_b + 1);
-            mp_split(X, na, Y, nb, d0 + kMTile < n ? d0 + kMTile : n, s_b + 2, s_b + 3);
+        uint32_t* sp = m.tsplit + 4ull * (r * m.ntiles + blockIdx.x);
+        uint32_t i0, j0, i1, j1;
+        if (!WRITE) {
+            // the tile's start and end on the merge path, the whole block searching; kept
+            // for the writing pass
+            mp_split_block(X, na, Y, nb, d0, &i0, &j0, s_s);
+            mp_split_block(X, na, Y, nb, d0 + kMTile < n ? d0 + kMTile : n, &i1, &j1, s_s);
+            if (threadIdx.x == 0) {
+                sp[0] = i0;
+                sp[1] = j0;
+                sp[2] = i1;
+                sp[3] = j1;
+            }
+        } else {
+            i0 = sp[0];
+            j0 = sp[1];
+            i1 = sp[2];
+            j1 = sp[3];
         }
-        __syncthreads();
-        const uint32_t i0 = s_b[0], j0 = s_b[1];
-        const uint32_t wa = s_b[2] - i0, wb = s_b[3] - j0, w = wa + wb;
+        const uint32_t wa = i1 - i0, wb = j1 - j0, w = wa + wb;
         const u64* WX = X + i0;
         const u64* WY = Y + j0;
         if (w <= kMWin) {                                    // stage the window in LDS
@@ -1754,7 +1815,7 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
                    sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
                    sz_r = R * 4ull;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 2 * sz_t + sz_c + 4 * sz_r + 64;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 4 * sz_r + 64;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -1769,6 +1830,7 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.tcnt = reinterpret_cast<uint32_t*>(take(sz_tc));
     m.tile = reinterpret_cast<uint32_t*>(take(sz_t));
     m.tside = reinterpret_cast<uint32_t*>(take(sz_t));
+    m.tsplit = reinterpret_cast<uint32_t*>(take(4 * sz_t));
     m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
