@@ -20,6 +20,7 @@
 // Term order comes from host-built rank tables (krank per element slot, grank per token
 // slot), so a comparison is one integer compare and `==` is rank equality.
 
+#include <cstring>
 #include <new>
 #include <type_traits>
 #include <vector>
@@ -209,7 +210,7 @@ __device__ uint32_t inner_merge(const u64* ta, uint32_t la, const u64* tb, uint3
 // smaller head of the second argument makes it switch; a smaller head of the first
 // keeps it), so the item of a pair is the side of the last single step before it (A
 // at the start) — carried across threads and tiles by "last non-none" scans.
-// Replicas whose ranks descend anywhere take a one-wave walk (k_merge_runs).
+// Replicas whose ranks descend anywhere take a one-wave walk (merge_runs_replica, run by k_merge_tile_scan).
 // Token runs of the planned entries (inner orddict:merge with `or`, or a copy) are then
 // counted, scanned and written one entry per thread over the whole grid.
 
@@ -487,10 +488,18 @@ __global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t 
 // per replica: exclusive offsets of the tile counts, the output entry count, and (MODE 2)
 // the pair side at every tile's start (the last single side before it, A at the start)
 template <int MODE>
+__device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r);
+
+// WALK: a replica whose ranks descend takes the run-jumping walk on the block's first
+// wave instead (merge_runs_replica: the walk in this launch)
+template <int MODE, bool WALK>
 __global__ __launch_bounds__(kMT) void k_merge_tile_scan(LV a, LV b, MS m, uint64_t R) {
     __shared__ uint32_t s_w[kMT / 64], s_sd[kMT];
     for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
-        if (m.unsorted[r]) continue;
+        if (m.unsorted[r]) {
+            if (WALK && threadIdx.x < 64) merge_runs_replica<MODE>(a, b, m, r);
+            continue;
+        }
         const uint32_t n = a.n(r) + b.n(r), nt = (n + kMTile - 1) / kMTile;
         uint32_t* tile = m.tile + r * m.ntiles;
         uint32_t* tside = m.tside + r * m.ntiles;
@@ -702,10 +711,11 @@ __device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64*
     }
 }
 
+// one replica's walk by one wave (its lanes); k_merge_tile_scan runs it on its first wave
+// for a replica whose ranks descend, so the scan and the walk are one launch
 template <int MODE>
-__global__ __launch_bounds__(64) void k_merge_runs(LV a, LV b, MS m, uint64_t R) {
-    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
-        if (!m.unsorted[r]) continue;
+__device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r) {
+    {
         const uint32_t na = a.n(r), nb = b.n(r);
         const u64* SA = m.sa + r * m.ce_a;
         const u64* SB = m.sb + r * m.ce_b;
@@ -1010,6 +1020,19 @@ __global__ void k_linf_final(LV prev, LV cur, bool bcast, uint64_t R, const uint
         }
         out[r] = res ? 1 : 0;
     }
+}
+
+// bind/3's answer per replica, after the merge, is_inflation(Value0, Merged)'s probe and
+// `Value0 =:= Value`: 0 = equal (no-op), 1 = the merge inflates Value0 (written), 2 = it
+// does not (k_linf_final's non-strict rule folded in), and the merge's error flag copied
+// beside it, so one copy brings the whole answer back
+__global__ __launch_bounds__(256) void k_bind_final(uint64_t R, const uint32_t* flags,
+                                                    const uint32_t* diff, const uint32_t* err,
+                                                    uint8_t* status, uint32_t* err_out) {
+    for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < R;
+         r += (u64)gridDim.x * blockDim.x)
+        status[r] = !diff[r] ? 0 : ((flags[r] & kViolBit) ? 2 : 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *err_out = *err;
 }
 
 // ---------------------------------------------------------------- tiled producers
@@ -1850,12 +1873,17 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                            rk, m, R);
         hipLaunchKernelGGL((k_merge_tiles<MODE, false>), dim3(m.ntiles ? m.ntiles : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, m, R);
-        hipLaunchKernelGGL((k_merge_tile_scan<MODE>), dim3(rx), dim3(kMT), 0, ctx->stream, A, B,
-                           m, R);
-        // keys that descend somewhere: the run-jumping walk (LASPJ_TUNE_LIST_WALK 1: the
-        // step-by-step walk it replaced)
-        hipLaunchKernelGGL(ctx->tune_list_walk == 1 ? k_merge_serial<MODE> : k_merge_runs<MODE>,
-                           dim3(rx), dim3(64), 0, ctx->stream, A, B, m, R);
+        // keys that descend somewhere: the run-jumping walk, in the scan's launch
+        // (LASPJ_TUNE_LIST_WALK 1: the step-by-step walk it replaced, a launch of its own)
+        if (ctx->tune_list_walk == 1) {
+            hipLaunchKernelGGL((k_merge_tile_scan<MODE, false>), dim3(rx), dim3(kMT), 0,
+                               ctx->stream, A, B, m, R);
+            hipLaunchKernelGGL(k_merge_serial<MODE>, dim3(rx), dim3(64), 0, ctx->stream, A, B,
+                               m, R);
+        } else {
+            hipLaunchKernelGGL((k_merge_tile_scan<MODE, true>), dim3(rx), dim3(kMT), 0,
+                               ctx->stream, A, B, m, R);
+        }
         hipLaunchKernelGGL((k_merge_tiles<MODE, true>), dim3(m.ntiles ? m.ntiles : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, m, R);
         hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),
@@ -1918,9 +1946,12 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
 
 // the inflation kernels of prev -> cur into o (R bytes); clear_flag: start from a clean
 // error flag (the fused bind keeps the merge's bits and reads them with o)
+// final = false: the answer kernel is left to the caller, which gets the flag words
+// through *flag_words (list_bind's k_bind_final)
 static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                             int strict, const RK& rk, uint8_t* o, bool clear_flag,
-                            const char* what, uint32_t** zeroed_words = nullptr) {
+                            const char* what, uint32_t** zeroed_words = nullptr,
+                            bool final = true, const uint32_t** flag_words = nullptr) {
     const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
     const bool bcast = prev->replicas == 1 && cur->replicas != 1;
     const uint64_t R = cur->replicas;
@@ -1935,6 +1966,7 @@ static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj
     auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
     auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
     if (zeroed_words) *zeroed_words = flags + R;
+    if (flag_words) *flag_words = flags;
     if (clear_flag) LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
     // the tables (empty = zero) and the per-replica flag words, one memset
     LJ_HIP(ctx, hipMemsetAsync(base, 0, zbytes, ctx->stream));
@@ -1947,8 +1979,9 @@ static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj
                            hk, hi, hsize, bcast, R);                                          \
         hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
                            hk, hi, hsize, bcast, R, flags);                                   \
-        hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P, C,    \
-                           bcast, R, flags, o);                                               \
+        if (final)                                                                            \
+            hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P,   \
+                               C, bcast, R, flags, o);                                        \
     } while (0)
     if (gs) {
         if (strict) LJ_INFL(true, true); else LJ_INFL(true, false);
@@ -2026,24 +2059,26 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
     const uint64_t R = cur->replicas;
     LGuard g(ctx);
-    // one device block: inflation bytes, the merge's sizes
-    const uint64_t o_need = (R + 7) & ~7ull, bytes = o_need + 8 * R;
+    // one device block, read back in one copy: the merge's sizes {entries, tokens} per
+    // replica, the answer bytes, the error flag
+    const uint64_t o_st = 8 * R, o_flag = o_st + ((R + 7) & ~7ull), bytes = o_flag + 8;
     void* dev = nullptr;
     if (laspj::dev_alloc(ctx, bytes, &dev) != hipSuccess) {
         hipGetLastError();
         return fail(ctx, LASPJ_E_NOMEM, "list_bind: status bytes");
     }
-    uint8_t* infd = static_cast<uint8_t*>(dev);
-    auto* need = reinterpret_cast<uint32_t*>(infd + o_need);
-    std::vector<uint8_t> inf(R, 0);
-    std::vector<uint32_t> h(2 * R), diff(R, 0);
+    auto* need = static_cast<uint32_t*>(dev);
+    uint8_t* std_ = static_cast<uint8_t*>(dev) + o_st;
+    auto* errd = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(dev) + o_flag);
+    std::vector<uint8_t> hb(bytes);
     // Type:merge and is_inflation(Value0, Merged) enqueued back to back (the merge sized
     // from the inputs' known counts), `Value0 =:= Value` over the grid into words the
-    // inflation's memset zeroed, then ONE synchronisation
+    // inflation's memset zeroed, the answer bytes, then ONE copy and ONE synchronisation
     uint32_t* dd = nullptr;
+    const uint32_t* fw = nullptr;
     int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind");
     if (s == LASPJ_OK)
-        s = inflation_launch(ctx, cur, dst, 0, rk, infd, false, "list_bind", &dd);
+        s = inflation_launch(ctx, cur, dst, 0, rk, nullptr, false, "list_bind", &dd, false, &fw);
     if (s == LASPJ_OK) {
         const uint32_t cmax = cur->cap_e > val->cap_e ? cur->cap_e : val->cap_e;
         const uint32_t tmax = cur->cap_t > val->cap_t ? cur->cap_t : val->cap_t;
@@ -2051,14 +2086,16 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
         const unsigned gx = (unsigned)std::min<uint64_t>((span + 2047) / 2048 + 1, 1024);
         hipLaunchKernelGGL(k_list_equal_grid, dim3(gx, (unsigned)(R < 65535 ? R : 65535)),
                            dim3(256), 0, ctx->stream, view(cur), view(val), rk, dd, R);
+        hipLaunchKernelGGL(k_bind_final, dim3((unsigned)std::min<uint64_t>((R + 255) / 256, 4096)),
+                           dim3(256), 0, ctx->stream, R, fw, dd, rk.flag, std_, errd);
         s = hipGetLastError() == hipSuccess ? LASPJ_OK
                                             : fail(ctx, LASPJ_E_DEVICE, "list_bind: launch");
     }
     if (s == LASPJ_OK) {
+        const laspj::ReadPiece rp[1] = {{hb.data(), dev, bytes}};
+        const hipError_t e = laspj::readback(ctx, rp, 1);
         uint32_t f = 0;
-        const laspj::ReadPiece rp[4] = {{diff.data(), dd, 4ull * R}, {inf.data(), infd, R},
-                                        {h.data(), need, 8ull * R}, {&f, ctx->flag + 1, 4}};
-        const hipError_t e = laspj::readback(ctx, rp, 4);
+        if (e == hipSuccess) std::memcpy(&f, hb.data() + o_flag, 4);
         s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s",
                                    hipGetErrorString(e))
                             : flag_status(ctx, f, "list_bind");
@@ -2068,9 +2105,9 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
         dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;
         return s;
     }
-    set_known(dst, h.data(), R);
+    set_known(dst, reinterpret_cast<const uint32_t*>(hb.data()), R);
     // status: 0 = cur =:= val (no-op), 1 = the merge inflates cur (written), 2 = it does not
-    for (uint64_t i = 0; i < R; ++i) status[i] = !diff[i] ? 0 : (inf[i] ? 1 : 2);
+    std::memcpy(status, hb.data() + o_st, R);
     return LASPJ_OK;
 }
 

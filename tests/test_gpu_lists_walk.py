@@ -1,4 +1,4 @@
-"""The run-jumping list merge (k_merge_runs, laspj_lists.hip) on lists whose keys do NOT
+"""The run-jumping list merge (merge_runs_replica in k_merge_tile_scan, laspj_lists.hip) on lists whose keys do NOT
 ascend — a non-monotone map's output re-bound (lasp_core.erl:641-667 then :300, merged by
 lasp_orset.erl:128-134 / lasp_gset.erl:99-101 over OTP 17's two-finger clauses, SURVEY
 Appendix A) — against the oracle's clauses (oracle/otp.py via oracle/orset.py,
