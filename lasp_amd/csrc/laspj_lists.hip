@@ -354,8 +354,10 @@ __device__ void mp_split_block(const u64* X, uint32_t nx, const u64* Y, uint32_t
         return;
     }
     const u64 v = i >= nx ? Y[j] : (j >= ny ? X[i] : (X[i] < Y[j] ? X[i] : Y[j]));
-    *pi = block_first_true(0, i, [&](uint32_t k) { return X[k] >= v; }, s);
-    *pj = block_first_true(0, j, [&](uint32_t k) { return Y[k] >= v; }, s);
+    // moved back over keys equal to v: none there (the usual case: distinct keys) is one
+    // load, not a search
+    *pi = i == 0 || X[i - 1] < v ? i : block_first_true(0, i, [&](uint32_t k) { return X[k] >= v; }, s);
+    *pj = j == 0 || Y[j - 1] < v ? j : block_first_true(0, j, [&](uint32_t k) { return Y[k] >= v; }, s);
 }
 
 // key ranks of both sides, and whether either descends
@@ -378,12 +380,74 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
     }
 }
 
+template <int MODE>
+__device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r);
+
+// one replica's tile counts -> exclusive offsets, its output entry count, and (MODE 2) the
+// pair side at every tile's start (the last single side before it, A at the start); WALK:
+// a replica whose ranks descend takes the run-jumping walk on the block's first wave
+// instead.  Tile words are read with relaxed atomic loads: in the fused form (the
+// counting pass's last block) other blocks of the same launch wrote them.
+template <int MODE, bool WALK>
+__device__ void tile_scan_replica(const LV& a, const LV& b, const MS& m, u64 r, uint32_t* s_w,
+                                  uint32_t* s_sd) {
+    if (m.unsorted[r]) {
+        if (WALK && threadIdx.x < 64) merge_runs_replica<MODE>(a, b, m, r);
+        return;
+    }
+    const uint32_t n = a.n(r) + b.n(r), nt = (n + kMTile - 1) / kMTile;
+    uint32_t* tile = m.tile + r * m.ntiles;
+    uint32_t* tside = m.tside + r * m.ntiles;
+    uint32_t carry = 0, side = 1;
+    for (uint32_t c0 = 0; c0 < nt; c0 += kMT) {
+        const uint32_t k = c0 + threadIdx.x;
+        const uint32_t v = k < nt ? __atomic_load_n(tile + k, __ATOMIC_RELAXED) : 0u;
+        uint32_t tot;
+        const uint32_t off = carry + block_excl(v, &tot, s_w);
+        uint32_t mx = 0, pv = 0;
+        if (MODE == 2) {
+            const uint32_t sd = k < nt ? __atomic_load_n(tside + k, __ATOMIC_RELAXED) : 0u;
+            s_sd[threadIdx.x] = sd;                          // the tiles' own last sides
+            pv = block_excl_max(sd ? threadIdx.x + 1 : 0u, &mx, s_w);
+        }
+        if (k < nt) {
+            tile[k] = off;
+            if (MODE == 2) tside[k] = pv ? s_sd[pv - 1] : side;
+        }
+        if (MODE == 2 && mx) side = s_sd[mx - 1];
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) m.nout[r] = carry;
+}
+
+// the last block of a launch to finish (agent-scope ticket, zero on entry and left zero)
+__device__ __forceinline__ bool last_block(uint32_t* ticket, uint32_t* s_flag) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        *s_flag = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1u;
+    }
+    __syncthreads();
+    const bool last = *s_flag != 0;
+    if (last) {
+        __threadfence();
+        if (threadIdx.x == 0) *ticket = 0;
+    }
+    return last;
+}
+
 // one tile of the merge path per block: WRITE = false counts the tile's entries (and,
 // MODE 2, its last single side); WRITE = true writes its plan entries
+// ticket (the counting pass of a merge of few replicas): the last block to finish also
+// runs the tile scan (and the walk of replicas whose ranks descend) — k_merge_tile_scan's
+// work, one launch fewer
 template <int MODE, bool WRITE>
-__global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t R) {
+__global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t R,
+                                                     uint32_t* ticket) {
     __shared__ u64 s_win[kMWin];
     __shared__ uint32_t s_si[kMT + 1], s_sj[kMT + 1], s_last[kMT], s_w[kMT / 64], s_s[1];
+    __shared__ uint32_t s_sd[kMT];
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
         const uint32_t na = a.n(r), nb = b.n(r), n = na + nb;
         const uint32_t d0 = blockIdx.x * kMTile;
@@ -483,48 +547,19 @@ __global__ __launch_bounds__(kMT) void k_merge_tiles(LV a, LV b, MS m, uint64_t 
         }
         __syncthreads();
     }
+    if (!WRITE && ticket && last_block(ticket, s_s))
+        for (u64 r = 0; r < R; ++r) tile_scan_replica<MODE, true>(a, b, m, r, s_w, s_sd);
 }
 
 // per replica: exclusive offsets of the tile counts, the output entry count, and (MODE 2)
 // the pair side at every tile's start (the last single side before it, A at the start)
-template <int MODE>
-__device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r);
-
 // WALK: a replica whose ranks descend takes the run-jumping walk on the block's first
 // wave instead (merge_runs_replica: the walk in this launch)
 template <int MODE, bool WALK>
 __global__ __launch_bounds__(kMT) void k_merge_tile_scan(LV a, LV b, MS m, uint64_t R) {
     __shared__ uint32_t s_w[kMT / 64], s_sd[kMT];
-    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
-        if (m.unsorted[r]) {
-            if (WALK && threadIdx.x < 64) merge_runs_replica<MODE>(a, b, m, r);
-            continue;
-        }
-        const uint32_t n = a.n(r) + b.n(r), nt = (n + kMTile - 1) / kMTile;
-        uint32_t* tile = m.tile + r * m.ntiles;
-        uint32_t* tside = m.tside + r * m.ntiles;
-        uint32_t carry = 0, side = 1;
-        for (uint32_t c0 = 0; c0 < nt; c0 += kMT) {
-            const uint32_t k = c0 + threadIdx.x;
-            const uint32_t v = k < nt ? tile[k] : 0u;
-            uint32_t tot;
-            const uint32_t off = carry + block_excl(v, &tot, s_w);
-            uint32_t mx = 0, pv = 0;
-            if (MODE == 2) {
-                const uint32_t sd = k < nt ? tside[k] : 0u;
-                s_sd[threadIdx.x] = sd;                      // the tiles' own last sides
-                pv = block_excl_max(sd ? threadIdx.x + 1 : 0u, &mx, s_w);
-            }
-            if (k < nt) {
-                tile[k] = off;
-                if (MODE == 2) tside[k] = pv ? s_sd[pv - 1] : side;
-            }
-            if (MODE == 2 && mx) side = s_sd[mx - 1];
-            carry += tot;
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) m.nout[r] = carry;
-    }
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x)
+        tile_scan_replica<MODE, WALK>(a, b, m, r, s_w, s_sd);
 }
 
 // replicas whose keys do not ascend: the clauses' walk on lane 0 (over precomputed ranks)
@@ -798,9 +833,33 @@ __device__ __forceinline__ uint32_t entry_tokens(const LV& a, const LV& b, u64 r
     return OB[*jb + 1] - OB[*jb];
 }
 
+// one replica's chunk token counts -> exclusive offsets; need = {entries, tokens}
+// (relaxed loads: in the fused form other blocks of the same launch wrote the counts)
+__device__ void chunk_scan_replica(const MS& m, u64 r, uint32_t* need, uint32_t* s_w) {
+    const uint32_t nc = (m.nout[r] + kMT - 1) / kMT;
+    uint32_t* ch = m.chunk + r * m.nchunks;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nc; c0 += kMT) {
+        const uint32_t k = c0 + threadIdx.x;
+        uint32_t tot;
+        const uint32_t off =
+            carry + block_excl(k < nc ? __atomic_load_n(ch + k, __ATOMIC_RELAXED) : 0u, &tot, s_w);
+        if (k < nc) ch[k] = off;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        m.ntok[r] = carry;
+        need[2 * r] = m.nout[r];
+        need[2 * r + 1] = carry;
+    }
+}
+
+// ticket (few replicas): the last block to finish also scans the chunk counts
+// (k_merge_chunk_scan's work, one launch fewer)
 template <int MODE>
-__global__ __launch_bounds__(kMT) void k_merge_tok_count(LV a, LV b, RK rk, MS m, uint64_t R) {
-    __shared__ uint32_t s_w[kMT / 64];
+__global__ __launch_bounds__(kMT) void k_merge_tok_count(LV a, LV b, RK rk, MS m, uint64_t R,
+                                                         uint32_t* ticket, uint32_t* need) {
+    __shared__ uint32_t s_w[kMT / 64], s_s[1];
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
         const uint32_t nout = m.nout[r], o0 = blockIdx.x * kMT;
         if (o0 >= nout) continue;
@@ -814,28 +873,14 @@ __global__ __launch_bounds__(kMT) void k_merge_tok_count(LV a, LV b, RK rk, MS m
         block_excl(cnt, &tot, s_w);
         if (threadIdx.x == 0) m.chunk[r * m.nchunks + blockIdx.x] = tot;
     }
+    if (ticket && last_block(ticket, s_s))
+        for (u64 r = 0; r < R; ++r) chunk_scan_replica(m, r, need, s_w);
 }
 
 // per replica: exclusive offsets of the chunk token counts; need = {entries, tokens}
 __global__ __launch_bounds__(kMT) void k_merge_chunk_scan(MS m, uint64_t R, uint32_t* need) {
     __shared__ uint32_t s_w[kMT / 64];
-    for (u64 r = blockIdx.x; r < R; r += gridDim.x) {
-        const uint32_t nc = (m.nout[r] + kMT - 1) / kMT;
-        uint32_t* ch = m.chunk + r * m.nchunks;
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < nc; c0 += kMT) {
-            const uint32_t k = c0 + threadIdx.x;
-            uint32_t tot;
-            const uint32_t off = carry + block_excl(k < nc ? ch[k] : 0u, &tot, s_w);
-            if (k < nc) ch[k] = off;
-            carry += tot;
-        }
-        if (threadIdx.x == 0) {
-            m.ntok[r] = carry;
-            need[2 * r] = m.nout[r];
-            need[2 * r + 1] = carry;
-        }
-    }
+    for (u64 r = blockIdx.x; r < R; r += gridDim.x) chunk_scan_replica(m, r, need, s_w);
 }
 
 // the write pass: one planned entry per thread
@@ -1838,7 +1883,7 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
                    sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
                    sz_r = R * 4ull;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 4 * sz_r + 64;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 4 * sz_r + 72;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -1857,7 +1902,11 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
-    m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r));
+    m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r + 8));
+    uint32_t* tickets = m.unsorted + R;          // two words, zeroed with the flags
+    // few replicas: the scans ride in the last block of the pass before them (two launches
+    // fewer); many: their own launches, one block per replica
+    const bool fuse = R <= 4 && ctx->tune_list_walk != 1;
     const LV A = view(a), B = view(b), OUT = view(dst);
     const unsigned ry = (unsigned)(R < 65535 ? R : 65535);
     const unsigned rx = (unsigned)(R < (1u << 20) ? R : (1u << 20));
@@ -1868,11 +1917,12 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         hipLaunchKernelGGL(k_list_equal, dim3(R), dim3(64), 0, ctx->stream, A, B, rk, eq);
     auto passes = [&](auto mode) {
         constexpr int MODE = decltype(mode)::value;
-        hipMemsetAsync(m.unsorted, 0, sz_r, ctx->stream);
+        hipMemsetAsync(m.unsorted, 0, sz_r + 8, ctx->stream);
         hipLaunchKernelGGL(k_merge_ranks, dim3(gr, ry), dim3(kMT), 0, ctx->stream, A, B,
                            rk, m, R);
         hipLaunchKernelGGL((k_merge_tiles<MODE, false>), dim3(m.ntiles ? m.ntiles : 1, ry),
-                           dim3(kMT), 0, ctx->stream, A, B, m, R);
+                           dim3(kMT), 0, ctx->stream, A, B, m, R,
+                           fuse ? tickets : (uint32_t*)nullptr);
         // keys that descend somewhere: the run-jumping walk, in the scan's launch
         // (LASPJ_TUNE_LIST_WALK 1: the step-by-step walk it replaced, a launch of its own)
         if (ctx->tune_list_walk == 1) {
@@ -1880,15 +1930,18 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                                ctx->stream, A, B, m, R);
             hipLaunchKernelGGL(k_merge_serial<MODE>, dim3(rx), dim3(64), 0, ctx->stream, A, B,
                                m, R);
-        } else {
+        } else if (!fuse) {
             hipLaunchKernelGGL((k_merge_tile_scan<MODE, true>), dim3(rx), dim3(kMT), 0,
                                ctx->stream, A, B, m, R);
         }
         hipLaunchKernelGGL((k_merge_tiles<MODE, true>), dim3(m.ntiles ? m.ntiles : 1, ry),
-                           dim3(kMT), 0, ctx->stream, A, B, m, R);
+                           dim3(kMT), 0, ctx->stream, A, B, m, R, (uint32_t*)nullptr);
         hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),
-                           dim3(kMT), 0, ctx->stream, A, B, rk, m, R);
-        hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R, need);
+                           dim3(kMT), 0, ctx->stream, A, B, rk, m, R,
+                           fuse ? tickets + 1 : (uint32_t*)nullptr, need);
+        if (!fuse)
+            hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R,
+                               need);
         // the write pass (it raises kErrRange rather than write past dst's capacity)
         hipLaunchKernelGGL((k_merge_write<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry), dim3(kMT),
                            0, ctx->stream, A, B, OUT, rk, m, R);
