@@ -1904,8 +1904,8 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
     m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r + 8));
     uint32_t* tickets = m.unsorted + R;          // two words, zeroed with the flags
-    // few replicas: the scans ride in the last block of the pass before them (two launches
-    // fewer); many: their own launches, one block per replica
+    // few replicas: the tile scan rides in the counting pass's last block (one launch
+    // fewer); many: its own launch, one block per replica
     const bool fuse = R <= 4 && ctx->tune_list_walk != 1;
     const LV A = view(a), B = view(b), OUT = view(dst);
     const unsigned ry = (unsigned)(R < 65535 ? R : 65535);
@@ -1936,12 +1936,11 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         }
         hipLaunchKernelGGL((k_merge_tiles<MODE, true>), dim3(m.ntiles ? m.ntiles : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, m, R, (uint32_t*)nullptr);
+        // (the chunk scan in the token count's last block measured slower: every one of
+        // its ~400 blocks pays the ticket's agent-scope fence — profiles/r04t_*)
         hipLaunchKernelGGL((k_merge_tok_count<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry),
-                           dim3(kMT), 0, ctx->stream, A, B, rk, m, R,
-                           fuse ? tickets + 1 : (uint32_t*)nullptr, need);
-        if (!fuse)
-            hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R,
-                               need);
+                           dim3(kMT), 0, ctx->stream, A, B, rk, m, R, (uint32_t*)nullptr, need);
+        hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R, need);
         // the write pass (it raises kErrRange rather than write past dst's capacity)
         hipLaunchKernelGGL((k_merge_write<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry), dim3(kMT),
                            0, ctx->stream, A, B, OUT, rk, m, R);
