@@ -308,7 +308,9 @@ int laspj_orset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b
 int laspj_orset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                           int strict, laspj_buf* out);
 /* update/3 — lasp_orset.erl:99-117 (add_elem :222-230, remove_elem :232-241).
- * ops: host array sorted by replica (stable within a replica); status: nops int32 */
+ * ops: host array sorted by replica (stable within a replica); status: nops int32, or
+ * null when every op is an ADD (no precondition can fail: nothing is read back, the call
+ * returns without waiting for the device) */
 int laspj_orset_apply_ops(laspj_ctx* ctx, laspj_batch* batch, const laspj_op* ops,
                           uint64_t nops, int32_t* status);
 /* union body for lasp_orset — lasp_core.erl:616-618: orddict:merge keep-left:
@@ -395,7 +397,8 @@ int laspj_gset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
 /* is_inflation — lasp_lattice.erl:137-140; strict — :212-215 */
 int laspj_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                          int strict, laspj_buf* out);
-/* update/3 add / add_all — lasp_gset.erl:84-88 (LASPJ_OP_ADD only) */
+/* update/3 add / add_all — lasp_gset.erl:84-88 (LASPJ_OP_ADD only; status may be null:
+ * nothing read back, no wait) */
 int laspj_gset_apply_ops(laspj_ctx* ctx, laspj_batch* batch, const laspj_op* ops,
                          uint64_t nops, int32_t* status);
 

@@ -51,7 +51,8 @@ class BodyCrash(Exception):
 
 
 class _Var:
-    __slots__ = ("type", "rep", "val", "empty", "waiting", "pairs", "as_list", "gshape")
+    __slots__ = ("type", "rep", "val", "empty", "waiting", "pairs", "as_list", "gshape",
+                 "last_write")
 
     def __init__(self, type_, val):
         self.type = type_
@@ -65,6 +66,8 @@ class _Var:
         # is not ascending-insert shaped (gb_trees_ext:merge keeps a one-sided element's
         # tree as it is); the device holds the contents
         self.gshape: Dict = {}
+        # (value before, value after) of the latest canonical merge that changed the value
+        self.last_write = None
 
 
 class _Value:
@@ -310,6 +313,9 @@ class Store:
                 merged = _new_like(self.ctx, v.val)
                 if not self.ctx.bind_many([merged], [v.val], [new])[0]:
                     return                                       # lasp_core.erl:294-296
+                # merged came from v.val by a merge that changed it: a strict inflation
+                # of v.val, which _propagate then knows without asking the device
+                v.last_write = (v.val, merged)
                 v.val = merged
                 self._written(id_, v)
                 return
@@ -388,6 +394,10 @@ class Store:
         _or_into(self.ctx, cur, v.val, v.val)
         if v.type == "riak_dt_gcounter":
             cur.increment(ops)
+        elif v.type == "lasp_orset" and all(o[2] == _lib.OP_ADD for o in ops):
+            # add / add_by_token / add_all: no precondition can fail (lasp_orset.erl:
+            # 222-230), so no statuses are read back and nothing waits for the device
+            cur.apply_ops(ops, statuses=False)
         elif v.type in ("lasp_orset", "lasp_orset_gbtree"):
             st = cur.apply_ops(ops)
             if (st == _lib.OPST_KEY_EXISTS).any():
@@ -399,7 +409,7 @@ class Store:
                 raise RuntimeError(f"badmatch: {{error,{{precondition,{{not_present,"
                                    f"{self.odom.elements.terms[bad]!r}}}}}}}")
         else:
-            cur.apply_ops(ops)
+            cur.apply_ops(ops, statuses=False)             # G-Set adds: nothing can fail
         gb = None
         if v.type == "lasp_orset_gbtree":
             # Type:update's tree (its insert / enter calls replayed on the stored tree),
@@ -529,8 +539,12 @@ class Store:
                                 # DESIGN.md §2)
                                 continue
                             hit = pre.get((id(proc), i))
-                            fire = hit[1] if hit is not None and hit[0] is v.val and \
-                                hit[2] is last.batch else self._inflates(v, last, strict=True)
+                            if self._merged_from(v, last):
+                                fire = True
+                            elif hit is not None and hit[0] is v.val and hit[2] is last.batch:
+                                fire = hit[1]
+                            else:
+                                fire = self._inflates(v, last, strict=True)
                             if not fire:
                                 continue
                         proc["seen"][i] = _Value(v.rep, v.val, v.pairs, empty=False)
@@ -543,6 +557,17 @@ class Store:
         finally:
             self._depth -= 1
 
+    @staticmethod
+    def _merged_from(v: _Var, last) -> bool:
+        """v's value is a canonical merge that changed last's value: for lasp_orset,
+        lasp_gset and riak_dt_gcounter a strict inflation of it (changed cells of a merge
+        = a new element, a token or flag gained on a common element, a larger count:
+        lasp_lattice.erl:212-215, 235-253, 273-275), known without a device call."""
+        lw = getattr(v, "last_write", None)
+        return lw is not None and lw[1] is v.val and lw[0] is last.batch and \
+            v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter") and \
+            v.rep == "canonical" and last.rep == "canonical"
+
     def _strict_checks(self):
         """Every pending {strict, Last} re-check between canonical values, in ONE
         launch (laspj_batch_inflation_many): {(proc, input): (value, result, last)}."""
@@ -550,7 +575,7 @@ class Store:
         for proc in self.procs:
             for i in proc["inputs"]:
                 v, last = self.vars[i], proc["seen"][i]
-                if v.empty or last is None or last.batch is v.val:
+                if v.empty or last is None or last.batch is v.val or self._merged_from(v, last):
                     continue
                 if v.rep == "canonical" and last.rep == "canonical" and \
                         v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter"):

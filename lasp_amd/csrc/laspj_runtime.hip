@@ -863,7 +863,7 @@ int laspj_gset_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
 
 static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
                           int32_t* status, int32_t kind, const char* what) {
-    if (!same_ctx(ctx, b) || (!ops && nops) || (!status && nops))
+    if (!same_ctx(ctx, b) || (!ops && nops))
         return fail(ctx, LASPJ_E_INVAL, "%s: bad argument", what);
     if (b->kind != kind) return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
     // Host-side validation: every op addresses a real cell and the list is grouped by
@@ -885,6 +885,11 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
         if (i && ops[i - 1].replica > o.replica)
             return fail(ctx, LASPJ_E_INVAL, "%s: ops not sorted by replica at %llu", what,
                         (unsigned long long)i);
+        // no status array: only for ADDs, whose precondition cannot fail (every status
+        // would be APPLIED), so nothing is read back and nothing waits for the device
+        if (!status && o.kind != LASPJ_OP_ADD)
+            return fail(ctx, LASPJ_E_INVAL, "%s: a null status needs every op to be an ADD",
+                        what);
     }
     if (!nops) return LASPJ_OK;
     Guard g(ctx);
@@ -907,7 +912,7 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
     LJ_HIP(ctx, hipMemcpyAsync(dops, ops, nops * sizeof(laspj_op), hipMemcpyHostToDevice,
                                ctx->stream));
     LJ_HIP(ctx, laspj::launch_apply_ops(ctx, b, dops, nops, dst));
-    LJ_HIP(ctx, laspj::readback(ctx, status, dst, nops * sizeof(int32_t)));
+    if (status) LJ_HIP(ctx, laspj::readback(ctx, status, dst, nops * sizeof(int32_t)));
     return LASPJ_OK;
 }
 

@@ -397,12 +397,17 @@ class _Batch:
         check(fn(self.ctx.h, *args, buf.h), self.ctx.h)
         return buf.download(np.uint8).astype(bool)
 
-    def _apply_ops(self, fn, ops: Sequence[tuple]) -> np.ndarray:
+    def _apply_ops(self, fn, ops: Sequence[tuple], statuses: bool = True):
+        """statuses=False (every op an ADD, whose precondition cannot fail): no status
+        readback, the call does not wait for the device; returns None."""
         n = len(ops)
         arr = (_lib.Op * max(n, 1))()
         for k, (rep, elem, kind, slot, flags) in enumerate(ops):
             arr[k].replica, arr[k].element, arr[k].kind = rep, elem, kind
             arr[k].slot, arr[k].flags, arr[k].pad = slot, flags, 0
+        if not statuses:
+            check(fn(self.ctx.h, self.h, arr, n, None), self.ctx.h)
+            return None
         status = np.zeros((max(n, 1),), dtype=np.int32)
         check(fn(self.ctx.h, self.h, arr, n, status.ctypes.data_as(C.POINTER(C.c_int32))),
               self.ctx.h)
@@ -460,9 +465,9 @@ class ORSetBatch(_Batch):
     def is_inflation_of(self, prev: "ORSetBatch", strict: bool = False) -> np.ndarray:
         return self._bool_out(self.ctx.L.laspj_orset_inflation, prev.h, self.h, int(strict))
 
-    def apply_ops(self, ops: Sequence[tuple]) -> np.ndarray:
+    def apply_ops(self, ops: Sequence[tuple], statuses: bool = True):
         """ops: (replica, element_slot, OP_ADD|OP_REMOVE, token_slot, flags)."""
-        return self._apply_ops(self.ctx.L.laspj_orset_apply_ops, ops)
+        return self._apply_ops(self.ctx.L.laspj_orset_apply_ops, ops, statuses)
 
     def union(self, l: "ORSetBatch", r: "ORSetBatch"):
         check(self.ctx.L.laspj_orset_union(self.ctx.h, self.h, l.h, r.h), self.ctx.h)
@@ -667,8 +672,8 @@ class GSetBatch(_Batch):
     def is_inflation_of(self, prev: "GSetBatch", strict: bool = False) -> np.ndarray:
         return self._bool_out(self.ctx.L.laspj_gset_inflation, prev.h, self.h, int(strict))
 
-    def apply_ops(self, ops: Sequence[tuple]) -> np.ndarray:
-        return self._apply_ops(self.ctx.L.laspj_gset_apply_ops, ops)
+    def apply_ops(self, ops: Sequence[tuple], statuses: bool = True):
+        return self._apply_ops(self.ctx.L.laspj_gset_apply_ops, ops, statuses)
 
     def union(self, l: "GSetBatch", r: "GSetBatch"):
         check(self.ctx.L.laspj_gset_union(self.ctx.h, self.h, l.h, r.h), self.ctx.h)
