@@ -3776,55 +3776,14 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                 __syncthreads();
                 st = (int)s_h[0];
                 const uint32_t m = (uint32_t)s_h[2];
-                // minimal integer images in the window: every group's value-table load is
-                // issued before the first is used (one round trip for the chunk instead of
-                // one per 64 elements); anything else goes through gs_lookup as before
-                u64 pre[kGChunk / 64];
-                bool fast[kGChunk / 64];
-#pragma unroll
-                for (uint32_t q = 0; q < kGChunk / 64; ++q) {
-                    const uint32_t k = q * 64 + lane;
-                    fast[q] = false;
-                    pre[q] = 0;
-                    if (g.itab && k < m) {
-                        const uint32_t L = s_l[k];
-                        const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
-                        if ((L == 2u || L == 5u) && o + L <= wl) {
-                            const uint8_t* q8 = win + o;
-                            int64_t v = 0;
-                            bool ok = false;
-                            if (L == 2u && q8[0] == 97) {
-                                v = q8[1];
-                                ok = true;
-                            } else if (L == 5u && q8[0] == 98) {
-                                v = (int32_t)((uint32_t)q8[1] << 24 | (uint32_t)q8[2] << 16 |
-                                              (uint32_t)q8[3] << 8 | q8[4]);
-                                ok = v < 0 || v > 255;
-                            }
-                            if (ok) {
-                                const int64_t x = v - g.ilo;
-                                fast[q] = true;
-                                pre[q] = x >= 0 && x < (int64_t)g.in ? g.itab[x] : 0ull;
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (uint32_t q = 0; q < kGChunk / 64; ++q) {
-                    const uint32_t k0 = q * 64;
-                    if (k0 >= m) break;
+                for (uint32_t k0 = 0; k0 < m; k0 += 64) {
                     const uint32_t k = k0 + lane;
                     uint32_t slot = kNoSlot, rk = 0;
                     if (k < m) {
-                        if (fast[q]) {
-                            slot = (uint32_t)pre[q] ? (uint32_t)pre[q] - 1u : kNoSlot;
-                            rk = (uint32_t)(pre[q] >> 32);
-                        } else {
-                            const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
-                            const bool in = s_l[k] <= 0xFFFFFFu && o + s_l[k] <= wl;
-                            if (s_l[k] > 0xFFFFFFu) slot = kNoSlot;
-                            else gs_lookup(g, in ? win + o : p + s_o[k], s_l[k], &slot, &rk);
-                        }
+                        const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
+                        const bool in = s_l[k] <= 0xFFFFFFu && o + s_l[k] <= wl;
+                        if (s_l[k] > 0xFFFFFFu) slot = kNoSlot;
+                        else gs_lookup(g, in ? win + o : p + s_o[k], s_l[k], &slot, &rk);
                     }
                     const uint32_t before = __shfl_up(rk, 1, 64);
                     bool bad = k < m && (slot == kNoSlot ||
