@@ -134,7 +134,10 @@ int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
         *p = nullptr;
         *have = 0;
     }
-    if (hipHostMalloc(p, want, hipHostMallocDefault) != hipSuccess) {
+    const unsigned flags = ctx->tune_nif_host == 1   ? hipHostMallocNonCoherent
+                           : ctx->tune_nif_host == 2 ? hipHostMallocCoherent
+                                                     : hipHostMallocDefault;
+    if (hipHostMalloc(p, want, flags) != hipSuccess) {
         hipGetLastError();
         *p = nullptr;
         return fail(ctx, LASPJ_E_NOMEM, "nif: pinned allocation of %llu bytes",

@@ -361,6 +361,10 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
                             "multiple of 4096");
             ctx->tune_nif_piece = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_NIF_HOST:
+            if (value < 0 || value > 2) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF host 0..2");
+            ctx->tune_nif_host = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }
