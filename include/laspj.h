@@ -174,6 +174,15 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_NIF_HOST     12   /* NIF entry points' pinned staging (allocated from
                                         the next growth on): 0 = default, 1 =
                                         non-coherent, 2 = coherent                      */
+#define LASPJ_TUNE_NIF_DIRECT   13   /* NIF entry points' operand and answer traffic
+                                        (default 6): 0 =
+                                        copies to and from device memory, 1 = the decoder
+                                        reads the operands from pinned host memory, 2 = the
+                                        answer's kernels write it into pinned host memory,
+                                        3 = both; + 4: a kernel on the context's stream
+                                        pulls the operands to the device (in place of
+                                        the copy and of bit 1).  The staging is coherent
+                                        from the first call with any bit set            */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

@@ -41,6 +41,7 @@ TUNE_ETF_SEG = 9
 TUNE_LIST_WALK = 10
 TUNE_NIF_PIECE = 11
 TUNE_NIF_HOST = 12
+TUNE_NIF_DIRECT = 13
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
 NIF_STATS = 15
 

@@ -37,6 +37,7 @@ struct laspj_ctx {
     int64_t tune_list_walk = 0;
     int64_t tune_nif_piece = 0;
     int64_t tune_nif_host = 0;
+    int64_t tune_nif_direct = 6;     // pull kernel in, kernels write the answer out
     // device scratch for apply_ops (grown on demand)
     void* scratch = nullptr;
     uint64_t scratch_bytes = 0;

@@ -50,6 +50,7 @@ struct NifState {
     uint64_t hin_bytes = 0;
     void* hout = nullptr;
     uint64_t hout_bytes = 0;
+    bool h_coherent = false;        // both allocated coherent (LASPJ_TUNE_NIF_DIRECT)
     uint64_t ocap = 1 << 20;        // device bytes reserved for answer payloads
     // the operand cells known to be new() (the fused merge clears them behind it), so the
     // next call's decoders need no memset: words [0, clean_words) at element slots clean_E
@@ -64,6 +65,17 @@ struct NifState {
 };
 
 namespace {
+
+// The in region pulled from pinned host memory by a kernel on the context's stream
+// (LASPJ_TUNE_NIF_DIRECT bit 2): the decoder then starts right behind it instead of
+// waiting for a copy engine's completion signal.  16-byte lanes, grid-stride.
+typedef uint32_t pull16 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src,
+                                                  pull16* __restrict__ dst, uint64_t n16) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
+        dst[i] = __builtin_nontemporal_load(src + i);
+}
 
 struct Guard {
     std::lock_guard<std::mutex> lk;
@@ -125,7 +137,7 @@ int grow_dev(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
     return LASPJ_OK;
 }
 
-int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
+int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need, bool coherent) {
     if (*have >= need) return LASPJ_OK;
     const uint64_t want = std::max<uint64_t>(need, *have + *have / 2);
     if (*p) {
@@ -134,9 +146,11 @@ int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
         *p = nullptr;
         *have = 0;
     }
-    const unsigned flags = ctx->tune_nif_host == 1   ? hipHostMallocNonCoherent
-                           : ctx->tune_nif_host == 2 ? hipHostMallocCoherent
-                                                     : hipHostMallocDefault;
+    // kernels that read or write the staging themselves need it coherent: a device L2
+    // line of last call's operands must not outlive the host's rewrite
+    const unsigned flags = coherent || ctx->tune_nif_host == 2 ? hipHostMallocCoherent
+                           : ctx->tune_nif_host == 1           ? hipHostMallocNonCoherent
+                                                               : hipHostMallocDefault;
     if (hipHostMalloc(p, want, flags) != hipSuccess) {
         hipGetLastError();
         *p = nullptr;
@@ -269,12 +283,43 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         const uint64_t had = S->dcells_bytes;
         if (int s = grow_dev(ctx, &S->dcells, &S->dcells_bytes, c_out + cells_out + 256)) return s;
         if (S->dcells_bytes != had) S->clean_words = 0;
-        if (int s = grow_host(ctx, &S->hin, &S->hin_bytes, in_bytes)) return s;
-        if (int s = grow_host(ctx, &S->hout, &S->hout_bytes, out_bytes)) return s;
+        if (ctx->tune_nif_direct && !S->h_coherent) {
+            // the staging reallocated coherent (once: it stays so)
+            hipStreamSynchronize(ctx->stream);
+            if (S->hin) hipHostFree(S->hin);
+            if (S->hout) hipHostFree(S->hout);
+            S->hin = S->hout = nullptr;
+            S->hin_bytes = S->hout_bytes = 0;
+            S->h_coherent = true;
+        }
+        if (int s = grow_host(ctx, &S->hin, &S->hin_bytes, in_bytes, S->h_coherent)) return s;
+        if (int s = grow_host(ctx, &S->hout, &S->hout_bytes, out_bytes, S->h_coherent)) return s;
     }
     uint8_t* hin = static_cast<uint8_t*>(S->hin);
     uint8_t* din = static_cast<uint8_t*>(S->dblk);
     uint8_t* dout = din + al(in_bytes, 256);
+    // LASPJ_TUNE_NIF_DIRECT: the decoder reads the in region where the host staged it (the
+    // zeroed words stay on the device), the answer's kernels write the out region where
+    // the host reads it
+    // (bit 2: a kernel pulls the in region to the device instead)
+    const bool pull_in = dec && (ctx->tune_nif_direct & 4);
+    const bool direct_in = dec && (ctx->tune_nif_direct & 1) && !pull_in;
+    const bool direct_out = (ctx->tune_nif_direct & 2) != 0;
+    uint8_t* rin = din;                  // where the kernels read the in region
+    uint8_t* rout = dout;                // where they write the out region
+    const uint8_t* hin_d = nullptr;      // the staging as the device addresses it
+    if (direct_in || pull_in || direct_out) {
+        void* hd = nullptr;
+        if (direct_in || pull_in) {
+            LJ_HIP(ctx, hipHostGetDevicePointer(&hd, S->hin, 0));
+            hin_d = static_cast<const uint8_t*>(hd);
+            if (direct_in) rin = static_cast<uint8_t*>(hd);
+        }
+        if (direct_out) {
+            LJ_HIP(ctx, hipHostGetDevicePointer(&hd, S->hout, 0));
+            rout = static_cast<uint8_t*>(hd);
+        }
+    }
     uint64_t* cin = static_cast<uint64_t*>(S->dcells);
     uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
     std::memcpy(hin + i_offs, hoffs.data(), 8ull * (m + 1));
@@ -301,7 +346,28 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         Guard g(ctx);
         // the offsets (and segment table), then the payloads a piece at a time: each
         // piece's copy starts while the next one is staged
-        if (dec) {
+        if (direct_in || pull_in) {
+            // staged whole; then either only the zeroed words go to the device, or a kernel
+            // pulls the region (zeroed words included) over
+            uint64_t at = 0;
+            const uint64_t tc = now_ns();
+            for (uint32_t i = 0; i < m; ++i) {
+                if (c.len[i]) std::memcpy(hin + i_pay + at, c.p[i], c.len[i]);
+                at += c.len[i];
+            }
+            t_copy += now_ns() - tc;
+            if (direct_in) {
+                LJ_HIP(ctx, hipMemsetAsync(din + i_zero, 0, 4ull * (m + 2), ctx->stream));
+            } else {
+                // in_bytes is a multiple of 256 (the payload area rounded up): whole lanes
+                const uint64_t n16 = (i_pay + al(pay, 16)) / 16;
+                const uint64_t blocks = std::min<uint64_t>((n16 + 255) / 256, (uint64_t)ctx->cus * 4);
+                hipLaunchKernelGGL(k_nif_pull, dim3((unsigned)std::max<uint64_t>(blocks, 1)),
+                                   dim3(256), 0, ctx->stream, reinterpret_cast<const pull16*>(hin_d),
+                                   reinterpret_cast<pull16*>(din), n16);
+                LJ_LAUNCHED(ctx);
+            }
+        } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
             uint64_t io = 0;                     // offset inside payload i
@@ -340,20 +406,20 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                                        ctx->stream));
         }
         laspj_batch inb = view(ctx, LASPJ_KIND_ORSET, m, E, cin);
-        int32_t* dst = reinterpret_cast<int32_t*>(dout + o_st);
+        int32_t* dst = reinterpret_cast<int32_t*>(rout + o_st);
         if (dec) {
-            if (int s = etf_read_enqueue(ctx, &inb, S->etf, -1, 1, din + i_pay, pay,
-                                         reinterpret_cast<const unsigned long long*>(din + i_offs),
+            if (int s = etf_read_enqueue(ctx, &inb, S->etf, -1, 1, rin + i_pay, pay,
+                                         reinterpret_cast<const unsigned long long*>(rin + i_offs),
                                          plan,
-                                         plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg)
+                                         plan.nseg ? reinterpret_cast<const uint32_t*>(rin + i_seg)
                                                    : nullptr,
                                          dst, !clean, dticket + 1))
                 return s;
         }
         laspj_batch lhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin);
         laspj_batch rhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin + (uint64_t)n * 2ull * E);
-        auto* dooff = reinterpret_cast<unsigned long long*>(dout + o_ooff);
-        uint8_t* dopay = dout + o_pay;
+        auto* dooff = reinterpret_cast<unsigned long long*>(rout + o_ooff);
+        uint8_t* dopay = rout + o_pay;
         switch (c.op) {
         case Op::MERGE: {
             // lasp_orset:merge/2 (lasp_orset.erl:128-134): the nested orddict:merge of two
@@ -396,16 +462,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         case Op::EQUAL:
             S->clean_words = 0;
             // equal/2 (lasp_orset.erl:136-138): ORDictA == ORDictB
-            LJ_HIP(ctx, launch_equal(ctx, &lhs, &rhs, dout + o_res));
+            LJ_HIP(ctx, launch_equal(ctx, &lhs, &rhs, rout + o_res));
             break;
         case Op::INFLATION:
             S->clean_words = 0;
             // is_inflation / is_strict_inflation (lasp_lattice.erl:153-161, 235-253)
-            LJ_HIP(ctx, launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, dout + o_res));
+            LJ_HIP(ctx, launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, rout + o_res));
             break;
         }
         const uint64_t first = o_pay + (has_payload_out ? std::min(ocap, bound) : 0);
-        LJ_HIP(ctx, hipMemcpyAsync(S->hout, dout, first, hipMemcpyDeviceToHost, ctx->stream));
+        if (!direct_out)
+            LJ_HIP(ctx, hipMemcpyAsync(S->hout, dout, first, hipMemcpyDeviceToHost, ctx->stream));
         const uint64_t t1 = now_ns();
         LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
         const uint64_t t2 = now_ns();
@@ -428,7 +495,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 S->ocap = al(total + total / 4, 1 << 16);
                 return -1000;            // caller re-runs the pass (rare)
             }
-            if (total > first - o_pay) {
+            if (!direct_out && total > first - o_pay) {
                 LJ_HIP(ctx, hipMemcpyAsync(static_cast<uint8_t*>(S->hout) + first, dout + first,
                                            o_pay + total - first, hipMemcpyDeviceToHost,
                                            ctx->stream));

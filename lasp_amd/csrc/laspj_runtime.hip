@@ -365,6 +365,10 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             if (value < 0 || value > 2) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF host 0..2");
             ctx->tune_nif_host = value;
             return LASPJ_OK;
+        case LASPJ_TUNE_NIF_DIRECT:
+            if (value < 0 || value > 7) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF direct 0..7");
+            ctx->tune_nif_direct = value;
+            return LASPJ_OK;
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }

@@ -170,9 +170,14 @@ def test_nif_cases_are_the_oracles_answers(tmp_path):
 
 # ------------------------------------------------------------------ GPU side
 
-def _ctx():
-    from lasp_amd import engine
-    return engine.Context(0)
+def _ctx(direct=0):
+    from lasp_amd import _lib, engine
+    ctx = engine.Context(0)
+    if direct:
+        # LASPJ_TUNE_NIF_DIRECT: kernels read operands from / write answers into pinned
+        # host memory instead of the two copies
+        ctx.set_tuning(_lib.TUNE_NIF_DIRECT, direct)
+    return ctx
 
 
 def _run_case(ctx, case):
@@ -200,8 +205,9 @@ def _check(case, got):
 
 
 @pytest.mark.gpu
-def test_nif_answers_match_oracle():
-    ctx = _ctx()
+@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
+def test_nif_answers_match_oracle(direct):
+    ctx = _ctx(direct)
     try:
         for case in valid_cases(seed=11, n=30) + fallback_cases(seed=12):
             _check(case, _run_case(ctx, case))
@@ -303,8 +309,9 @@ def test_nif_dictionary_reset_when_an_element_runs_out_of_token_slots():
 
 
 @pytest.mark.gpu
-def test_nif_merge_many_mixed_verdicts():
-    ctx = _ctx()
+@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
+def test_nif_merge_many_mixed_verdicts(direct):
+    ctx = _ctx(direct)
     try:
         rng = random.Random(7)
         elems, pool = _universe(rng, 48)
@@ -325,10 +332,11 @@ def test_nif_merge_many_mixed_verdicts():
 
 
 @pytest.mark.gpu
-def test_nif_mixed_token_image_lengths_take_the_host_encoder():
+@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
+def test_nif_mixed_token_image_lengths_take_the_host_encoder(direct):
     """Token images of several lengths: the device decoder needs one length, so the
     context's host dictionary encodes the cells and the device does the rest."""
-    ctx = _ctx()
+    ctx = _ctx(direct)
     try:
         rng = random.Random(8)
         elems = list(range(30))
@@ -349,11 +357,12 @@ def test_nif_mixed_token_image_lengths_take_the_host_encoder():
 
 
 @pytest.mark.gpu
-def test_nif_flags_in_other_atom_encodings_and_second_copy():
+@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
+def test_nif_flags_in_other_atom_encodings_and_second_copy(direct):
     """Operands whose flags use SMALL_ATOM_UTF8_EXT (an OTP 26 node's term_to_binary):
     decoded alike; the answer is written with ATOM_EXT flags, one byte longer per token,
     so it outgrows the first copy's bound and takes the second copy."""
-    ctx = _ctx()
+    ctx = _ctx(direct)
     try:
         rng = random.Random(9)
         toks = sorted(_tokens(rng, 3000))

@@ -28,6 +28,8 @@ if os.environ.get("NIF_PIECE"):                # pinned staging piece bytes (A/B
     ctx.set_tuning(_lib.TUNE_NIF_PIECE, int(os.environ["NIF_PIECE"]))
 if os.environ.get("NIF_HOST"):                 # pinned staging kind (A/B)
     ctx.set_tuning(_lib.TUNE_NIF_HOST, int(os.environ["NIF_HOST"]))
+if os.environ.get("NIF_DIRECT"):               # kernels on pinned host memory (A/B)
+    ctx.set_tuning(_lib.TUNE_NIF_DIRECT, int(os.environ["NIF_DIRECT"]))
 op, on, vd = C.c_void_p(), C.c_uint64(), C.c_int32()
 
 
