@@ -829,8 +829,10 @@ int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
  * device, [10] reading the answers after it, [11] the part of [8] spent copying operands
  * into pinned memory, [12] registering operands' terms in the host dictionary, [13]
  * rebuilding or patching the device images; [14] device image patches (registrations
- * that only added tokens to known elements, rewritten in place instead of rebuilt) */
-#define LASPJ_NIF_STATS 15
+ * that only added tokens to known elements, rewritten in place instead of rebuilt); [15]
+ * merge passes run again because a segment chain checked beside the join broke before
+ * any failing segment (a false element-header match: only a serial decode can judge) */
+#define LASPJ_NIF_STATS 16
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
 /* drop the context's dictionary (its memory; the next call registers afresh) */
 int laspj_nif_reset(laspj_ctx* ctx);

@@ -43,7 +43,7 @@ TUNE_NIF_PIECE = 11
 TUNE_NIF_HOST = 12
 TUNE_NIF_DIRECT = 13
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
-NIF_STATS = 15
+NIF_STATS = 16
 
 
 class LaspjUnavailable(RuntimeError):

@@ -681,15 +681,42 @@ __global__ __launch_bounds__(kBlock) void k_etf_chunk_scan(u64* coff, uint64_t R
 // With `ticket` (few replicas: the NIF's single merges) the block that finishes last also
 // scans the chunk totals and writes the payload offsets (k_etf_chunk_scan_offsets' work),
 // so the whole size pass is one launch; ticket is zero on entry and left zero.
+// With `chain` (the segment decoder's chain check deferred, ChainJob): the last
+// (cj.nrep + 3) / 4 blocks check the decoded payloads' segment chains instead, one wave
+// per payload, beside the join (its answer is only used when every chain held: the caller
+// decodes serially and joins again when a status comes back kDecRedo).
+struct SegRes;
+__device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
+                                 uint32_t ns, uint32_t S, const SegRes* res, uint32_t lane);
+struct ChainArgs {
+    const uint8_t* payload;
+    const u64* offs;
+    const uint32_t* segbase;
+    const SegRes* res;
+    int32_t* status;
+    uint32_t nrep, S;
+};
 __global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2* b, u64x2* z,
                                                                  uint64_t R, uint32_t E,
                                                                  DictView d, uint32_t nch,
                                                                  u64* coff, uint32_t* flag,
                                                                  uint32_t* ticket, uint32_t hdr,
-                                                                 u64* offs) {
+                                                                 u64* offs, ChainArgs cj) {
     __shared__ u64 lds4[kBlock / 64];
     __shared__ uint32_t s_last;
-    for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
+    const uint32_t cblocks = cj.status ? (cj.nrep + 3u) / 4u : 0u;
+    const uint32_t jblocks = gridDim.x - cblocks;
+    if (blockIdx.x >= jblocks) {
+        const uint32_t r = (blockIdx.x - jblocks) * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+        if (r < cj.nrep) {
+            const u64 base = cj.offs[r];
+            const int32_t st = chain_verdict(cj.payload, base, cj.offs[r + 1] - base,
+                                             cj.segbase[r], cj.segbase[r + 1] - cj.segbase[r],
+                                             cj.S, cj.res, lane);
+            if (lane == 0) cj.status[r] = st;
+        }
+    }
+    for (uint64_t it = blockIdx.x; blockIdx.x < jblocks && it < R * nch; it += jblocks) {
         const uint64_t rep = it / nch;
         const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
         u64 v = 0;
@@ -2884,6 +2911,69 @@ __device__ bool chain_ok(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
     return !__ballot(bad) && a.cnt + tot == a.n && (u64)q + 1 == len && payload[base + q] == 106;
 }
 
+// The chain check as a status, for callers that cannot decode a failed payload again on
+// the spot (the NIF merge checks chains beside the join, laspj_nif.hip): OK; a failing
+// segment's own status when every segment before it chains (it then started where the
+// serial decoder would be, so the serial decoder stops at the same element with the same
+// status); kDecRedo when the chain breaks first (a false header match, a malformed
+// payload): only a serial decode tells.  The same per-segment checks as chain_ok, the
+// first offending segment in stream order deciding.
+__device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
+                                 uint32_t ns, uint32_t S, const SegRes* res, uint32_t lane) {
+    const SegRes a = res[g0];
+    if (a.st != LASPJ_DEC_OK) return a.st;                 // segment 0 starts at the head
+    if (a.flags & kSegEmptyList) return a.end == len ? LASPJ_DEC_OK : kDecRedo;
+    uint32_t q = a.end, cnt = 0;
+    int32_t rl = a.rlast;
+    for (uint32_t s0 = 1; s0 < ns; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        SegRes b{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
+        if (s < ns) b = res[g0 + s];
+        const bool valid = s < ns && b.start != kSegNone;
+        int32_t li = valid ? (int32_t)lane : -1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t v = __shfl_up(li, off, 64);
+            if ((int)lane >= off) li = max(li, v);
+        }
+        int32_t lp = __shfl_up(li, 1, 64);
+        if (lane == 0) lp = -1;
+        const uint32_t e_at = __shfl(b.end, lp < 0 ? 0 : lp, 64);
+        const int32_t r_at = __shfl(b.rlast, lp < 0 ? 0 : lp, 64);
+        const uint32_t pq = lp >= 0 ? e_at : q;
+        const int32_t prl = lp >= 0 ? r_at : rl;
+        bool brk = false, bad = false;
+        if (s < ns) {
+            if (!valid) {
+                const u64 send = (u64)(s + 1) * S;
+                brk = pq < send && pq < len && payload[base + pq] != 106;
+            } else if (b.start != pq || b.rfirst <= prl) {
+                brk = true;
+            } else if (b.st != LASPJ_DEC_OK) {
+                bad = true;
+            }
+        }
+        const u64 ev = __ballot(brk || bad);
+        if (ev) {
+            const uint32_t f = (uint32_t)__ffsll((long long)ev) - 1u;
+            const int32_t fst = __shfl(b.st, f, 64);
+            const bool fbrk = __shfl((int)brk, f, 64) != 0;
+            return fbrk ? kDecRedo : fst;
+        }
+        cnt += valid ? b.cnt : 0u;
+        const int32_t last = __shfl(li, 63, 64);
+        if (last >= 0) {
+            q = __shfl(b.end, last, 64);
+            rl = __shfl(b.rlast, last, 64);
+        }
+    }
+    uint32_t tot = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+    return a.cnt + tot == a.n && (u64)q + 1 == len && payload[base + q] == 106 ? LASPJ_DEC_OK
+                                                                              : kDecRedo;
+}
+
 template <bool SMALL>
 __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
     const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
@@ -4437,7 +4527,7 @@ uint8_t* items_btab(laspj_ctx* ctx, const laspj_etf_dict* dc, uint64_t R, const 
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
                      const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
-                     bool clear, uint32_t* redo_zeroed) {
+                     bool clear, uint32_t* redo_zeroed, ChainJob* defer) {
     const uint64_t R = b->replicas;
     if (clear)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
@@ -4465,7 +4555,10 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                                        hipMemcpyHostToDevice, ctx->stream));
             dsegbase = up;
         }
-        SegRes* dres = reinterpret_cast<SegRes*>(sc + o_res);
+        static_assert(sizeof(SegRes) == kSegResBytes, "ChainJob::res sizing");
+        const bool deferred = defer && defer->res;
+        SegRes* dres = deferred ? static_cast<SegRes*>(defer->res)
+                                : reinterpret_cast<SegRes*>(sc + o_res);
         const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
         const bool small = d->tok_max <= kSmallTok && ctx->tune_etf_read != 2;
         hipLaunchKernelGGL(small ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
@@ -4474,6 +4567,16 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                            vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
                            (uint32_t)plan.S, hh, dres);
         LJ_LAUNCHED(ctx);
+        if (deferred) {
+            defer->payload = payload;
+            defer->offs = offs;
+            defer->segbase = dsegbase;
+            defer->status = status;
+            defer->nrep = (uint32_t)R;
+            defer->S = (uint32_t)plan.S;
+            defer->armed = true;
+            return LASPJ_OK;
+        }
         // the chain check, whose wave decodes a failed replica again itself (knob 10: the
         // redo list and a launch of the wave decoder over it, as before)
         const bool inline_redo = ctx->tune_etf_read != 10;
@@ -4592,7 +4695,7 @@ bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
 
 int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj_batch* z,
                            const laspj_etf_dict* d, int tag, u64* offsets, uint32_t* flag,
-                           uint32_t* ticket, const u64** chunks) {
+                           uint32_t* ticket, const u64** chunks, const ChainJob* chain) {
     const uint64_t R = z->replicas;
     const uint32_t nch = (z->elements + kBlock - 1) / kBlock;
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
@@ -4602,10 +4705,16 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
     // up to 4 replicas the last block scans them all (one launch); more go to the
     // per-replica scan kernel
     const bool one = R <= 4;
-    hipLaunchKernelGGL(k_etf_join_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
-                       reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b),
+    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    if (chain && chain->armed)
+        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
+                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
+                       chain->S};
+    const uint64_t cblocks = cj.status ? (cj.nrep + 3u) / 4u : 0u;
+    hipLaunchKernelGGL(k_etf_join_chunk_sizes, dim3((unsigned)(sg + cblocks)), dim3(kBlock), 0,
+                       ctx->stream, reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b),
                        reinterpret_cast<u64x2*>(z->dev), R, z->elements, view(d), nch, co, flag,
-                       one ? ticket : nullptr, hdr, offsets);
+                       one ? ticket : nullptr, hdr, offsets, cj);
     if (!one)
         hipLaunchKernelGGL(k_etf_chunk_scan_offsets, dim3((unsigned)std::min<uint64_t>(R, 65535)),
                            dim3(kBlock), 0, ctx->stream, co, R, nch, hdr, offsets, ticket);

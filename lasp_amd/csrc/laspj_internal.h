@@ -236,6 +236,22 @@ bool etf_dict_decodable(const laspj_etf_dict* d);     // from_binary runs on the
 uint32_t etf_dict_elements(const laspj_etf_dict* d);
 void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R,
                    const unsigned long long* host_offsets, EtfReadPlan* plan);
+// A segment-mode decode whose chain check is left to the join (etf_merge_size_enqueue):
+// the caller gives `res` (device memory, kSegResBytes per segment: ctx->scratch is reused
+// by the join); etf_read_enqueue fills the rest and sets `armed` when it decoded in
+// segments.  The statuses then come from the join's launch; kDecRedo = the chain broke
+// before any failing segment: decode that call again without deferring.
+constexpr uint64_t kSegResBytes = 32;
+constexpr int32_t kDecRedo = 64;
+struct ChainJob {
+    void* res = nullptr;
+    const uint8_t* payload = nullptr;
+    const unsigned long long* offs = nullptr;
+    const uint32_t* segbase = nullptr;
+    int32_t* status = nullptr;
+    uint32_t nrep = 0, S = 0;
+    bool armed = false;
+};
 // segbase: plan.segbase already on the device, or null (uploaded here); clear: zero the
 // batch first (the decoders only set the cells they decode)
 // redo_zeroed: R + 1 words the caller has zeroed (segment mode's redo list), or null
@@ -243,13 +259,14 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                      const uint8_t* payload, uint64_t payload_bytes,
                      const unsigned long long* offsets, const EtfReadPlan& plan,
                      const uint32_t* segbase, int32_t* status, bool clear,
-                     uint32_t* redo_zeroed);
+                     uint32_t* redo_zeroed, ChainJob* defer = nullptr);
 // merge/2 of a[i] and b[i] into z fused with z's size pass (and a, b cleared behind it),
 // when etf_merge_fused(ctx, R, E) holds; ticket: one zeroed word (left zero)
 bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E);
 int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj_batch* z,
                            const laspj_etf_dict* d, int tag, unsigned long long* offsets,
-                           uint32_t* flag, uint32_t* ticket, const unsigned long long** chunks);
+                           uint32_t* flag, uint32_t* ticket, const unsigned long long** chunks,
+                           const ChainJob* chain = nullptr);
 // offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
 // caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
 // (valid until the context's scratch is next used), or null

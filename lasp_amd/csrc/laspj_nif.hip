@@ -103,6 +103,7 @@ struct Call {
     std::vector<uint8_t> res;       // n answer bytes (EQUAL / INFLATION)
     std::vector<uint64_t> ooff;     // n + 1 answer payload offsets (MERGE / VALUE)
     const uint8_t* obase = nullptr; // pinned answer payloads
+    bool no_defer = false;          // a deferred chain check came back kDecRedo: decode serially
 };
 
 laspj_batch view(laspj_ctx* ctx, int32_t kind, uint64_t R, uint32_t E, uint64_t* dev) {
@@ -271,6 +272,11 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     }
     const uint64_t ocap = has_payload_out ? S->ocap : 0;
     const uint64_t out_bytes = o_pay + ocap;
+    // MERGE: the segment decoder's chain check rides on the join's launch (ChainJob), its
+    // per-segment results in a device area of their own after the out region
+    const bool defer = dec && plan.nseg && c.op == Op::MERGE && !c.no_defer &&
+                       etf_merge_fused(ctx, n, E);
+    const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
     // cells: in batch m x E; MERGE: answers n x E; VALUE: value words n x ceil(E/64)
     const uint64_t W = (E + 63ull) / 64ull;
     const uint64_t cells_out = c.op == Op::MERGE ? (uint64_t)n * E * 16ull
@@ -279,7 +285,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     std::vector<uint8_t> blob;      // the host-encode path's contiguous payloads
     {
         Guard g(ctx);
-        if (int s = grow_dev(ctx, &S->dblk, &S->dblk_bytes, al(in_bytes, 256) + out_bytes)) return s;
+        if (int s = grow_dev(ctx, &S->dblk, &S->dblk_bytes,
+                             al(in_bytes, 256) + al(out_bytes, 256) + seg_bytes))
+            return s;
         const uint64_t had = S->dcells_bytes;
         if (int s = grow_dev(ctx, &S->dcells, &S->dcells_bytes, c_out + cells_out + 256)) return s;
         if (S->dcells_bytes != had) S->clean_words = 0;
@@ -407,13 +415,15 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         }
         laspj_batch inb = view(ctx, LASPJ_KIND_ORSET, m, E, cin);
         int32_t* dst = reinterpret_cast<int32_t*>(rout + o_st);
+        ChainJob cjob;
+        if (defer) cjob.res = din + al(in_bytes, 256) + al(out_bytes, 256);
         if (dec) {
             if (int s = etf_read_enqueue(ctx, &inb, S->etf, -1, 1, rin + i_pay, pay,
                                          reinterpret_cast<const unsigned long long*>(rin + i_offs),
                                          plan,
                                          plan.nseg ? reinterpret_cast<const uint32_t*>(rin + i_seg)
                                                    : nullptr,
-                                         dst, !clean, dticket + 1))
+                                         dst, !clean, dticket + 1, defer ? &cjob : nullptr))
                 return s;
         }
         laspj_batch lhs = view(ctx, LASPJ_KIND_ORSET, n, E, cin);
@@ -429,7 +439,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             if (etf_merge_fused(ctx, n, E)) {
                 // the OR fused with the answer's size pass, the operands cleared behind it
                 if (int s = etf_merge_size_enqueue(ctx, lhs.dev, rhs.dev, &ob, S->etf, -1, dooff,
-                                                   ctx->flag, dticket, &chunks))
+                                                   ctx->flag, dticket, &chunks, &cjob))
                     return s;
                 S->clean_words = in_words;
                 S->clean_E = E;
@@ -552,6 +562,15 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         int s = device_pass(ctx, S, c);
         if (s == -1000) continue;                // answer area grown: once more
         if (s) return s;
+        bool redo = false;
+        for (uint32_t i = 0; i < m; ++i) redo |= c.st[i] == kDecRedo;
+        if (redo) {
+            // a segment chain that only a serial decode can judge: once more, decoding
+            // serially (the join's answer of this pass is not used)
+            c.no_defer = true;
+            ++S->stats[15];
+            continue;
+        }
         std::vector<uint32_t> unknown;
         for (uint32_t i = 0; i < m; ++i) {
             if (fallback[answer_of(i)]) continue;

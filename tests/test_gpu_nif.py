@@ -285,6 +285,52 @@ def test_nif_new_tokens_patch_the_device_images():
         assert s1["image_patches"] - s0["image_patches"] >= 30
         assert s1["image_rebuilds"] - s0["image_rebuilds"] < 30
         assert s1["fallbacks"] == s0["fallbacks"]
+        # the chain checked beside the join gives a new token's UNKNOWN_TERM exactly (the
+        # failing segment started where the serial decoder would be): no serial pass for
+        # those; only a new element (its header resolves nowhere) may take one
+        assert s1["chain_redo_passes"] - s0["chain_redo_passes"] <= 3
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_nif_false_element_headers_in_tokens_take_the_serial_pass():
+    """Tokens that embed a real element header (106 104 2 97 e 108) plant false segment
+    starts in 256-byte segments: the chain checked beside the join breaks, the call decodes
+    again serially (chain_redo_passes) and answers the oracle's merge, image for image.
+    Then a new token deep in a 10k-element operand: its segment's UNKNOWN_TERM is exact
+    (no serial pass), the call registers it and answers the oracle's merge."""
+    from lasp_amd import _lib
+    ctx = _ctx()
+    try:
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 256)
+        rng = random.Random(31)
+        trap = lambda e, k: bytes([106, 104, 2, 97, e, 108]) + bytes([k]) * 14   # noqa: E731
+        tok = lambda e, k: (trap((e + 7) % 200, k) if e % 5 == 0  # noqa: E731
+                            else bytes([k, e % 256]) * 10)
+        # >= 1024 element slots: the merge is the fused join the chain check rides on
+        a = [(e, sorted([(tok(e, k), rng.random() < 0.3) for k in range(2)],
+                        key=lambda x: _key(x[0]))) for e in range(1200)]
+        b = [(e, sorted([(tok(e, k), rng.random() < 0.3) for k in range(1, 3)],
+                        key=lambda x: _key(x[0]))) for e in range(0, 1200, 2)]
+        want = _tb(oorset.merge(a, b))
+        assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, want)
+        s0 = ctx.nif_stats()
+        assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, want)          # warm
+        s1 = ctx.nif_stats()
+        assert s1["chain_redo_passes"] > s0["chain_redo_passes"]
+        assert s1["registrations"] == s0["registrations"]
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 0)
+        big = [(e, [(bytes([e % 251, e // 251]) * 10, False)]) for e in range(10_000)]
+        other = [(e, list(ts)) for e, ts in big]
+        assert ctx.nif_merge(_tb(big), _tb(other)) == (OK, _tb(big))
+        s2 = ctx.nif_stats()
+        other[7777] = (7777, sorted(other[7777][1] + [(b"\x05" * 20, True)],
+                                    key=lambda x: _key(x[0])))
+        assert ctx.nif_merge(_tb(big), _tb(other)) == (OK, _tb(oorset.merge(big, other)))
+        s3 = ctx.nif_stats()
+        assert s3["registrations"] == s2["registrations"] + 1
+        assert s3["chain_redo_passes"] == s2["chain_redo_passes"]
     finally:
         ctx.close()
 
