@@ -169,8 +169,9 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
 #define LASPJ_TUNE_LIST_WALK    10   /* list merges whose keys descend somewhere: 0 = the
                                         run-jumping walk, 1 = one step per element      */
 #define LASPJ_TUNE_NIF_PIECE    11   /* NIF entry points: bytes staged into pinned memory
-                                        per host -> device copy (0 = one copy per call up
-                                        to 64 MiB; a multiple of 4096)                  */
+                                        per host -> device copy or pull (0 = one copy per
+                                        call up to 64 MiB, or pulls of 512 KiB while the
+                                        host stages the next; a multiple of 4096)       */
 #define LASPJ_TUNE_NIF_HOST     12   /* NIF entry points' pinned staging (allocated from
                                         the next growth on): 0 = default, 1 =
                                         non-coherent, 2 = coherent                      */

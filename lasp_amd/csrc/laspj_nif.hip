@@ -51,6 +51,10 @@ struct NifState {
     void* hout = nullptr;
     uint64_t hout_bytes = 0;
     bool h_coherent = false;        // both allocated coherent (LASPJ_TUNE_NIF_DIRECT)
+    uint8_t* hin_d = nullptr;       // their device addresses, for the allocations hin_dkey /
+    uint8_t* hout_d = nullptr;      // hout_dkey
+    const void* hin_dkey = nullptr;
+    const void* hout_dkey = nullptr;
     uint64_t ocap = 1 << 20;        // device bytes reserved for answer payloads
     // the operand cells known to be new() (the fused merge clears them behind it), so the
     // next call's decoders need no memset: words [0, clean_words) at element slots clean_E
@@ -87,6 +91,9 @@ constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is rese
 // beat 256 KiB pieces, 135 vs 154 us per config-1 merge, and 512 KiB pieces hit a slow
 // runtime path, 475 us: profiles/r04i_nif_ab.log)
 constexpr uint64_t kStagePiece = 64ull << 20;
+// ... but pulled by kernels (LASPJ_TUNE_NIF_DIRECT bit 2) in pieces of this many bytes:
+// each piece's pull runs while the host stages the next
+constexpr uint64_t kPullPiece = 512ull << 10;
 
 uint64_t al(uint64_t x, uint64_t a) { return (x + a - 1) & ~(a - 1); }
 
@@ -317,16 +324,23 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     uint8_t* rout = dout;                // where they write the out region
     const uint8_t* hin_d = nullptr;      // the staging as the device addresses it
     if (direct_in || pull_in || direct_out) {
+        // (looked up once per allocation: the runtime's lookup costs host microseconds)
         void* hd = nullptr;
-        if (direct_in || pull_in) {
+        if (S->hin_dkey != S->hin) {
             LJ_HIP(ctx, hipHostGetDevicePointer(&hd, S->hin, 0));
-            hin_d = static_cast<const uint8_t*>(hd);
-            if (direct_in) rin = static_cast<uint8_t*>(hd);
+            S->hin_d = static_cast<uint8_t*>(hd);
+            S->hin_dkey = S->hin;
         }
-        if (direct_out) {
+        if (S->hout_dkey != S->hout) {
             LJ_HIP(ctx, hipHostGetDevicePointer(&hd, S->hout, 0));
-            rout = static_cast<uint8_t*>(hd);
+            S->hout_d = static_cast<uint8_t*>(hd);
+            S->hout_dkey = S->hout;
         }
+        if (direct_in || pull_in) {
+            hin_d = S->hin_d;
+            if (direct_in) rin = S->hin_d;
+        }
+        if (direct_out) rout = S->hout_d;
     }
     uint64_t* cin = static_cast<uint64_t*>(S->dcells);
     uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
@@ -354,9 +368,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         Guard g(ctx);
         // the offsets (and segment table), then the payloads a piece at a time: each
         // piece's copy starts while the next one is staged
-        if (direct_in || pull_in) {
-            // staged whole; then either only the zeroed words go to the device, or a kernel
-            // pulls the region (zeroed words included) over
+        if (direct_in) {
+            // staged whole; only the zeroed words go to the device
             uint64_t at = 0;
             const uint64_t tc = now_ns();
             for (uint32_t i = 0; i < m; ++i) {
@@ -364,17 +377,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 at += c.len[i];
             }
             t_copy += now_ns() - tc;
-            if (direct_in) {
-                LJ_HIP(ctx, hipMemsetAsync(din + i_zero, 0, 4ull * (m + 2), ctx->stream));
-            } else {
-                // in_bytes is a multiple of 256 (the payload area rounded up): whole lanes
-                const uint64_t n16 = (i_pay + al(pay, 16)) / 16;
-                const uint64_t blocks = std::min<uint64_t>((n16 + 255) / 256, (uint64_t)ctx->cus * 4);
-                hipLaunchKernelGGL(k_nif_pull, dim3((unsigned)std::max<uint64_t>(blocks, 1)),
-                                   dim3(256), 0, ctx->stream, reinterpret_cast<const pull16*>(hin_d),
-                                   reinterpret_cast<pull16*>(din), n16);
-                LJ_LAUNCHED(ctx);
-            }
+            LJ_HIP(ctx, hipMemsetAsync(din + i_zero, 0, 4ull * (m + 2), ctx->stream));
         } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
@@ -382,9 +385,29 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             uint64_t sent = 0;                   // region bytes already copied
             const uint64_t head = i_pay;
             while (i < m && c.len[i] == 0) ++i;
+            // (a kernel pulls each piece: while it runs the host stages the next)
+            const uint64_t dflt = pull_in ? kPullPiece : kStagePiece;
+            auto send = [&](uint64_t upto) -> int {
+                if (!pull_in) {
+                    LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, upto - sent,
+                                               hipMemcpyHostToDevice, ctx->stream));
+                    return LASPJ_OK;
+                }
+                // 16-byte lanes: sent is a multiple of 16 (the head is 256-aligned, pieces
+                // 4096-multiples), upto is rounded up inside the staged region
+                const uint64_t n16 = (al(upto, 16) - sent) / 16;
+                const uint64_t blocks = std::min<uint64_t>((n16 + 255) / 256,
+                                                           (uint64_t)ctx->cus * 4);
+                hipLaunchKernelGGL(k_nif_pull, dim3((unsigned)std::max<uint64_t>(blocks, 1)),
+                                   dim3(256), 0, ctx->stream,
+                                   reinterpret_cast<const pull16*>(hin_d + sent),
+                                   reinterpret_cast<pull16*>(din + sent), n16);
+                LJ_LAUNCHED(ctx);
+                return LASPJ_OK;
+            };
             while (at < pay) {
-                const uint64_t piece = std::min(ctx->tune_nif_piece ? (uint64_t)ctx->tune_nif_piece
-                                                                    : kStagePiece, pay - at);
+                uint64_t piece = ctx->tune_nif_piece ? (uint64_t)ctx->tune_nif_piece : dflt;
+                piece = std::min(piece, pay - at);
                 uint64_t done = 0;
                 const uint64_t tc = now_ns();
                 while (done < piece) {
@@ -401,13 +424,11 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 t_copy += now_ns() - tc;
                 at += piece;
                 const uint64_t upto = head + at;
-                LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, upto - sent,
-                                           hipMemcpyHostToDevice, ctx->stream));
+                if (int s = send(upto)) return s;
                 sent = upto;
             }
             if (pay == 0)
-                LJ_HIP(ctx, hipMemcpyAsync(din + sent, hin + sent, head - sent,
-                                           hipMemcpyHostToDevice, ctx->stream));
+                if (int s = send(head)) return s;
         } else {
             LJ_HIP(ctx, hipMemcpyAsync(din, hin, i_pay, hipMemcpyHostToDevice, ctx->stream));
             LJ_HIP(ctx, hipMemcpyAsync(cin, hin + i_pay, cells_in, hipMemcpyHostToDevice,

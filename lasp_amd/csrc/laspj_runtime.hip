@@ -369,6 +369,7 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             if (value < 0 || value > 7) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF direct 0..7");
             ctx->tune_nif_direct = value;
             return LASPJ_OK;
+
         default:
             return fail(ctx, LASPJ_E_INVAL, "tuning: unknown knob %d", knob);
     }
