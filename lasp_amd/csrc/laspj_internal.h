@@ -49,6 +49,19 @@ struct laspj_ctx {
     // list kernels' scratch (merge plans, key-order arrays, hash tables, sizes)
     void* lscratch = nullptr;
     uint64_t lscratch_bytes = 0;
+    // list_bind's keyfind tables, kept zeroed between calls (each call's last kernel zeroes
+    // what it used), so a bind needs no memset of them; dirty: a call may have left them used
+    void* ltab = nullptr;
+    uint64_t ltab_bytes = 0;
+    bool ltab_dirty = false;
+    // list_bind's per-call words (device, kept zeroed between calls by the call's last
+    // block, as ltab) and its answer (pinned, coherent: the last block writes it there)
+    void* lbind = nullptr;
+    uint64_t lbind_bytes = 0;
+    bool lbind_dirty = false;
+    void* lbind_h = nullptr;
+    void* lbind_hd = nullptr;       // its device address
+    uint64_t lbind_h_bytes = 0;
     // pinned host staging for the small readbacks (sizes, statuses, flags): a round trip
     // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
     void* pinned = nullptr;

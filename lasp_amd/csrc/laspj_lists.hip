@@ -232,6 +232,7 @@ struct MS {
     uint32_t* nout;    // [R] output entries
     uint32_t* ntok;    // [R] output tokens
     uint32_t* unsorted;// [R] 1: a side's ranks descend somewhere (lane-0 walk)
+    uint32_t* aweak;   // [R] 1: a's keys are not strictly ascending (a tie or a descent)
     uint32_t ce_a, ce_b, ntiles, nchunks;
 };
 
@@ -365,11 +366,13 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
         const uint32_t na = a.n(r), nb = b.n(r);
         const uint32_t i = blockIdx.x * kMT + threadIdx.x;
-        bool desc = false;
+        bool desc = false, weak = false;
         if (i < na) {
             const u64 x = key_ord(a.K(r)[i], rk);
             m.sa[r * m.ce_a + i] = x;
-            desc |= i > 0 && key_ord(a.K(r)[i - 1], rk) > x;
+            const u64 px = i > 0 ? key_ord(a.K(r)[i - 1], rk) : 0;
+            desc |= i > 0 && px > x;
+            weak = i > 0 && px >= x;
         }
         if (i < nb) {
             const u64 y = key_ord(b.K(r)[i], rk);
@@ -377,6 +380,7 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
             desc |= i > 0 && key_ord(b.K(r)[i - 1], rk) > y;
         }
         if (__syncthreads_or(desc) && threadIdx.x == 0) atomicOr(m.unsorted + r, 1u);
+        if (__syncthreads_or(weak) && threadIdx.x == 0) atomicOr(m.aweak + r, 1u);
     }
 }
 
@@ -950,9 +954,30 @@ __global__ __launch_bounds__(64) void k_list_equal(LV a, LV b, RK rk, uint8_t* o
 
 // the same spread over a (chunk, replica) grid for the bind path's few long replicas:
 // diff[r] (zeroed) gets a bit at the first difference any block sees
+// (list_bind: also zeroes the keyfind tables of the replicas whose inflation check used
+// them — used[r] != 0 — so the next bind finds them empty without a memset; and the block
+// that finishes last writes bind/3's answer into pinned host memory (BindFin))
+constexpr uint32_t kViolBit = 1, kChangedBit = 2;   // the inflation check's flag bits
+struct BindFin {
+    uint32_t* words;         // [flag | unsorted R | tickets 2 | aweak R | flags R | diff R |
+                             //  ticket], zero on entry, left zero
+    const uint32_t* need;    // [R][2] the merge's {entries, tokens}
+    uint32_t* hneed;         // host: need, then status R bytes, then the flag word
+    uint32_t R;
+};
 __global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint32_t* diff,
-                                                         uint64_t R) {
+                                                         uint64_t R, u64* hk, uint32_t* hi,
+                                                         uint32_t hsize, const uint32_t* used,
+                                                         BindFin fin) {
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        if (used && used[r]) {
+            u64* k0 = hk + r * hsize;
+            uint32_t* i0 = hi + r * hsize;
+            for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < hsize; x += gridDim.x * 256u) {
+                k0[x] = 0;
+                i0[x] = 0;
+            }
+        }
         const uint32_t n = a.n(r), nt = a.nt(r);
         if (n != b.n(r) || nt != b.nt(r)) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(diff + r, 1u);
@@ -968,6 +993,40 @@ __global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint
             d = tok_ord(TA[t], rk) != tok_ord(TB[t], rk) || ((TA[t] ^ TB[t]) & kRemoved) != 0;
         if (__ballot(d) != 0 && lane_id() == 0) atomicOr(diff + r, 1u);
     }
+    if (!fin.words) return;
+    // bind/3's answer per replica (k_bind_final's rule): 0 = equal (no-op), 1 = the merge
+    // inflates Value0 (written), 2 = it does not; then every word zeroed for the next call
+    __shared__ uint32_t s_last;
+    const uint32_t n = fin.R;
+    uint32_t* w = fin.words;
+    uint32_t* ticket = w + 4 * n + 3;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    uint8_t* hst = reinterpret_cast<uint8_t*>(fin.hneed + 2 * n);
+    for (uint32_t r = threadIdx.x; r < n; r += 256) {
+        const uint32_t dv = __atomic_load_n(w + 3 * n + 3 + r, __ATOMIC_RELAXED);
+        const uint32_t lf = __atomic_load_n(w + 2 * n + 3 + r, __ATOMIC_RELAXED);
+        hst[r] = !dv ? 0 : ((lf & kViolBit) ? 2 : 1);
+        fin.hneed[2 * r] = fin.need[2 * r];
+        fin.hneed[2 * r + 1] = fin.need[2 * r + 1];
+        w[1 + r] = 0;                                          // unsorted
+        w[n + 3 + r] = 0;                                      // aweak
+        w[2 * n + 3 + r] = 0;                                  // inflation flags
+        w[3 * n + 3 + r] = 0;                                  // diff
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        fin.hneed[2 * n + (n + 3) / 4] = __atomic_load_n(w, __ATOMIC_RELAXED);
+        w[0] = 0;
+        *ticket = 0;
+        __threadfence_system();
+    }
 }
 
 // is_lattice_inflation / is_lattice_strict_inflation (lasp_lattice.erl:137-161,
@@ -977,18 +1036,25 @@ __global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint
 // k_linf_probe checks one Prev (and, G-Set strict, one Cur) entry per thread and ORs
 // violation / change bits into a per-replica word, k_linf_final turns them into the
 // answer.  The tables start zeroed (empty, see h_insert) by one memset with the flags.
-constexpr uint32_t kViolBit = 1, kChangedBit = 2;
+// skip (list_bind's non-strict check of Value0 against merge(Value0, Value), or null): a
+// replica with skip[r] == 0 — Value0's keys strictly ascending — has nothing to check:
+// orddict:merge's two-finger walk emits every entry of its first list, alone or with the
+// other list's equal key, and before any later entry of that key (the first list ascends,
+// so no earlier emitted key equals it), so keyfind finds it; the inner merge emits every
+// token of the first list likewise (ids_inflated asks presence only); ordsets:union
+// keeps every element of its first set.  The inflation then holds by construction.
 
 template <bool GSET, bool STRICT>
 __global__ __launch_bounds__(256) void k_linf_insert(LV prev, LV cur, RK rk, u64* hk,
                                                      uint32_t* hi, uint32_t hsize, bool bcast,
-                                                     uint64_t R) {
+                                                     uint64_t R, const uint32_t* skip) {
     const uint32_t mask = hsize - 1;
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        if (skip && !skip[r]) continue;
         const u64 pr = bcast ? 0 : r;
         const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-        u64* hk0 = hk + r * 2ull * hsize;
-        uint32_t* hi0 = hi + r * 2ull * hsize;
+        u64* hk0 = hk + r * (GSET && STRICT ? 2ull : 1ull) * hsize;
+        uint32_t* hi0 = hi + r * (GSET && STRICT ? 2ull : 1ull) * hsize;
         if (i < cur.n(r)) h_insert(hk0, hi0, mask, key_ord(cur.K(r)[i], rk), i);
         if (GSET && STRICT && i < prev.n(pr))
             h_insert(hk0 + hsize, hi0 + hsize, mask, key_ord(prev.K(pr)[i], rk), i);
@@ -998,14 +1064,16 @@ __global__ __launch_bounds__(256) void k_linf_insert(LV prev, LV cur, RK rk, u64
 template <bool GSET, bool STRICT>
 __global__ __launch_bounds__(256) void k_linf_probe(LV prev, LV cur, RK rk, const u64* hk,
                                                     const uint32_t* hi, uint32_t hsize,
-                                                    bool bcast, uint64_t R, uint32_t* flags) {
+                                                    bool bcast, uint64_t R, uint32_t* flags,
+                                                    const uint32_t* skip) {
     const uint32_t mask = hsize - 1;
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        if (skip && !skip[r]) continue;
         const u64 pr = bcast ? 0 : r;
         const uint32_t np = prev.n(pr), nc = cur.n(r);
         const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-        const u64* hk0 = hk + r * 2ull * hsize;
-        const uint32_t* hi0 = hi + r * 2ull * hsize;
+        const u64* hk0 = hk + r * (GSET && STRICT ? 2ull : 1ull) * hsize;
+        const uint32_t* hi0 = hi + r * (GSET && STRICT ? 2ull : 1ull) * hsize;
         bool viol = false, changed = false;
         if (GSET) {
             // sets:is_subset(from_list(Prev), from_list(Cur))
@@ -1856,9 +1924,15 @@ static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch
 // synchronises once, reading `need` (per replica {entries, tokens}), the error flag and
 // whatever it enqueued after (the bind's equality and inflation bytes).  eq (R bytes, or
 // null): `cur =:= val` per replica, launched first.
+// words (or null: the scratch and ctx's error word): 2R + 3 words of the caller's,
+// zeroed here in one memset — [rk.flag (the caller points rk.flag at words[0]) |
+// unsorted R | tickets 2 | aweak R] — for a caller that reads them after other users of
+// the scratch (list_bind's inflation reads `aweak`: words + R + 3)
 static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                          const laspj_batch* b, const RK& rk, bool keep_left, uint32_t* need,
-                         uint8_t* eq, const char* what) {
+                         uint8_t* eq, const char* what, uint32_t* words = nullptr,
+                         uint64_t words_bytes = 0) {
+    // (words_bytes == 0 with words: they are known zero already, no memset)
     const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
     const uint64_t R = a->replicas;
     const uint64_t ce = (uint64_t)a->cap_e + b->cap_e;
@@ -1883,7 +1957,7 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
                    sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
                    sz_r = R * 4ull;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 4 * sz_r + 72;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -1902,8 +1976,10 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
-    m.unsorted = reinterpret_cast<uint32_t*>(take(sz_r + 8));
-    uint32_t* tickets = m.unsorted + R;          // two words, zeroed with the flags
+    // [unsorted R | tickets 2 | aweak R], zeroed together
+    m.unsorted = words ? words + 1 : reinterpret_cast<uint32_t*>(take(2 * sz_r + 8));
+    uint32_t* tickets = m.unsorted + R;
+    m.aweak = m.unsorted + R + 2;
     // few replicas: the tile scan rides in the counting pass's last block (one launch
     // fewer); many: its own launch, one block per replica
     const bool fuse = R <= 4 && ctx->tune_list_walk != 1;
@@ -1912,12 +1988,20 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const unsigned rx = (unsigned)(R < (1u << 20) ? R : (1u << 20));
     const uint32_t cmax = m.ce_a > m.ce_b ? m.ce_a : m.ce_b;
     const unsigned gr = cmax ? (cmax + kMT - 1) / kMT : 1u;
-    LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    if (words) {
+        if (rk.flag != words) return fail(ctx, LASPJ_E_INVAL, "%s: error word", what);
+        if (words_bytes) {
+            const uint64_t wb = std::max<uint64_t>(words_bytes, (4 + 2 * sz_r + 8 + 15) & ~15ull);
+            LJ_HIP(ctx, hipMemsetAsync(words, 0, wb, ctx->stream));
+        }
+    } else {
+        LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+    }
     if (eq)
         hipLaunchKernelGGL(k_list_equal, dim3(R), dim3(64), 0, ctx->stream, A, B, rk, eq);
     auto passes = [&](auto mode) {
         constexpr int MODE = decltype(mode)::value;
-        hipMemsetAsync(m.unsorted, 0, sz_r + 8, ctx->stream);
+        if (!words) hipMemsetAsync(m.unsorted, 0, 2 * sz_r + 8, ctx->stream);
         hipLaunchKernelGGL(k_merge_ranks, dim3(gr, ry), dim3(kMT), 0, ctx->stream, A, B,
                            rk, m, R);
         hipLaunchKernelGGL((k_merge_tiles<MODE, false>), dim3(m.ntiles ? m.ntiles : 1, ry),
@@ -2003,34 +2087,70 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
 static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                             int strict, const RK& rk, uint8_t* o, bool clear_flag,
                             const char* what, uint32_t** zeroed_words = nullptr,
-                            bool final = true, const uint32_t** flag_words = nullptr) {
+                            bool final = true, const uint32_t** flag_words = nullptr,
+                            const uint32_t* skip = nullptr, uint32_t* zeroed_flags = nullptr,
+                            u64** tab_k = nullptr, uint32_t** tab_i = nullptr,
+                            uint32_t* tab_size = nullptr) {
     const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
     const bool bcast = prev->replicas == 1 && cur->replicas != 1;
     const uint64_t R = cur->replicas;
     const uint32_t cmax = cur->cap_e > prev->cap_e ? cur->cap_e : prev->cap_e;
     const uint32_t hsize = pow2_at_least(2ull * cmax);
-    const uint64_t tbytes = R * 2ull * hsize * 12ull;
+    // (a second table only for the G-Set strict check's Prev keys)
+    const uint64_t ntab = gs && strict ? 2 : 1;
+    const uint64_t tbytes = R * ntab * hsize * 12ull;
     // [tables | flag words | R more zeroed words for the caller (zeroed_words)]
-    const uint64_t zbytes = tbytes + 4ull * R * (zeroed_words ? 2 : 1);
-    char* base = static_cast<char*>(lscratch(ctx, zbytes));
-    if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
+    // (a multiple of 256 bytes: the runtime fills an unaligned tail with a second kernel)
+    const uint64_t zbytes = (tbytes + 4ull * R * (zeroed_words ? 2 : 1) + 255) & ~255ull;
+    char* base = nullptr;
+    uint32_t* flags = nullptr;
+    if (zeroed_flags) {
+        // list_bind: the tables kept zeroed in ctx->ltab (the caller's last kernel zeroes
+        // what this check used), the flag words the caller's, zeroed with its own
+        if (ctx->ltab_bytes < tbytes || ctx->ltab_dirty) {
+            if (ctx->ltab_bytes < tbytes) {
+                if (ctx->ltab) {
+                    hipStreamSynchronize(ctx->stream);
+                    hipFree(ctx->ltab);
+                    ctx->ltab = nullptr;
+                    ctx->ltab_bytes = 0;
+                }
+                if (laspj::dev_malloc(ctx, &ctx->ltab, tbytes) != hipSuccess) {
+                    hipGetLastError();
+                    return fail(ctx, LASPJ_E_NOMEM, "%s: keyfind tables", what);
+                }
+                ctx->ltab_bytes = tbytes;
+            }
+            LJ_HIP(ctx, hipMemsetAsync(ctx->ltab, 0, ctx->ltab_bytes, ctx->stream));
+        }
+        ctx->ltab_dirty = true;              // until the caller's clean-up is enqueued
+        base = static_cast<char*>(ctx->ltab);
+        flags = zeroed_flags;
+        if (zeroed_words) *zeroed_words = flags + R;
+    } else {
+        base = static_cast<char*>(lscratch(ctx, zbytes));
+        if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
+        flags = reinterpret_cast<uint32_t*>(base + tbytes);
+        if (zeroed_words) *zeroed_words = flags + R;
+        if (clear_flag) LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
+        // the tables (empty = zero) and the per-replica flag words, one memset
+        LJ_HIP(ctx, hipMemsetAsync(base, 0, zbytes, ctx->stream));
+    }
     u64* hk = reinterpret_cast<u64*>(base);
-    auto* hi = reinterpret_cast<uint32_t*>(base + R * 2ull * hsize * 8ull);
-    auto* flags = reinterpret_cast<uint32_t*>(base + tbytes);
-    if (zeroed_words) *zeroed_words = flags + R;
+    auto* hi = reinterpret_cast<uint32_t*>(base + R * ntab * hsize * 8ull);
     if (flag_words) *flag_words = flags;
-    if (clear_flag) LJ_HIP(ctx, hipMemsetAsync(ctx->flag + 1, 0, 4, ctx->stream));
-    // the tables (empty = zero) and the per-replica flag words, one memset
-    LJ_HIP(ctx, hipMemsetAsync(base, 0, zbytes, ctx->stream));
+    if (tab_k) *tab_k = hk;
+    if (tab_i) *tab_i = hi;
+    if (tab_size) *tab_size = hsize;
     const LV P = view(prev), C = view(cur);
     const dim3 grid(cmax ? (cmax + 255) / 256 : 1, (unsigned)(R < 65535 ? R : 65535));
     const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
 #define LJ_INFL(G, S)                                                                         \
     do {                                                                                      \
         hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,   \
-                           hk, hi, hsize, bcast, R);                                          \
+                           hk, hi, hsize, bcast, R, skip);                                    \
         hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
-                           hk, hi, hsize, bcast, R, flags);                                   \
+                           hk, hi, hsize, bcast, R, flags, skip);                             \
         if (final)                                                                            \
             hipLaunchKernelGGL((k_linf_final<G, S>), dim3(fg), dim3(256), 0, ctx->stream, P,   \
                                C, bcast, R, flags, o);                                        \
@@ -2111,55 +2231,99 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
     const uint64_t R = cur->replicas;
     LGuard g(ctx);
-    // one device block, read back in one copy: the merge's sizes {entries, tokens} per
-    // replica, the answer bytes, the error flag
-    const uint64_t o_st = 8 * R, o_flag = o_st + ((R + 7) & ~7ull), bytes = o_flag + 8;
-    void* dev = nullptr;
-    if (laspj::dev_alloc(ctx, bytes, &dev) != hipSuccess) {
-        hipGetLastError();
-        return fail(ctx, LASPJ_E_NOMEM, "list_bind: status bytes");
+    // the context's bind block (device): [words 4R + 4 (BindFin): the error word the
+    // kernels raise into, the merge's per-replica flags and tickets, the inflation's flags,
+    // the equality's words, the final ticket | ... | need 8R at the block's end], the words
+    // kept zero between calls (at offset 0 and need at the end, so one call's need never
+    // lies where another call's words do, whatever their R) —
+    // and the answer, written by the last block into pinned host memory: [need 8R |
+    // status R (to a word) | flag]: no memset, no copy, one synchronisation
+    const uint64_t nwords = 4 * R + 4, bytes = 4 * nwords + 8 * R;
+    const uint64_t hbytes = 8 * R + 4 * ((R + 3) / 4) + 4;
+    bool fresh = false;
+    if (ctx->lbind_bytes < bytes) {
+        if (ctx->lbind) {
+            hipStreamSynchronize(ctx->stream);
+            hipFree(ctx->lbind);
+            ctx->lbind = nullptr;
+            ctx->lbind_bytes = 0;
+        }
+        if (laspj::dev_malloc(ctx, &ctx->lbind, bytes) != hipSuccess) {
+            hipGetLastError();
+            return fail(ctx, LASPJ_E_NOMEM, "list_bind: bind block");
+        }
+        ctx->lbind_bytes = bytes;
+        fresh = true;
     }
-    auto* need = static_cast<uint32_t*>(dev);
-    uint8_t* std_ = static_cast<uint8_t*>(dev) + o_st;
-    auto* errd = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(dev) + o_flag);
-    std::vector<uint8_t> hb(bytes);
+    if (ctx->lbind_h_bytes < hbytes) {
+        if (ctx->lbind_h) {
+            hipStreamSynchronize(ctx->stream);
+            hipHostFree(ctx->lbind_h);
+            ctx->lbind_h = nullptr;
+            ctx->lbind_h_bytes = 0;
+        }
+        if (hipHostMalloc(&ctx->lbind_h, hbytes, hipHostMallocCoherent) != hipSuccess) {
+            hipGetLastError();
+            ctx->lbind_h = nullptr;
+            return fail(ctx, LASPJ_E_NOMEM, "list_bind: pinned answer");
+        }
+        ctx->lbind_h_bytes = hbytes;
+        LJ_HIP(ctx, hipHostGetDevicePointer(&ctx->lbind_hd, ctx->lbind_h, 0));
+    }
+    void* hdev = ctx->lbind_hd;
+    auto* mw = static_cast<uint32_t*>(ctx->lbind);
+    auto* need = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->lbind) +
+                                             ctx->lbind_bytes - 8 * R);
+    // words not known zero (a fresh block, or a call that stopped before its last kernel
+    // was enqueued): the merge zeroes them (the whole block's words) first
+    const uint64_t wzero = fresh || ctx->lbind_dirty ? 4 * nwords : 0;
+    ctx->lbind_dirty = true;
     // Type:merge and is_inflation(Value0, Merged) enqueued back to back (the merge sized
-    // from the inputs' known counts), `Value0 =:= Value` over the grid into words the
-    // inflation's memset zeroed, the answer bytes, then ONE copy and ONE synchronisation
+    // from the inputs' known counts), `Value0 =:= Value` over the grid, whose last block
+    // writes the answer
     uint32_t* dd = nullptr;
     const uint32_t* fw = nullptr;
-    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind");
+    rk.flag = mw;
+    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind", mw, wzero);
+    // (Value0's replicas whose keys strictly ascend skip the check: see k_linf_insert)
+    u64* tk = nullptr;
+    uint32_t* ti = nullptr;
+    uint32_t tsz = 0;
     if (s == LASPJ_OK)
-        s = inflation_launch(ctx, cur, dst, 0, rk, nullptr, false, "list_bind", &dd, false, &fw);
+        s = inflation_launch(ctx, cur, dst, 0, rk, nullptr, false, "list_bind", &dd, false, &fw,
+                             mw + R + 3, mw + 2 * R + 3, &tk, &ti, &tsz);
     if (s == LASPJ_OK) {
         const uint32_t cmax = cur->cap_e > val->cap_e ? cur->cap_e : val->cap_e;
         const uint32_t tmax = cur->cap_t > val->cap_t ? cur->cap_t : val->cap_t;
         const uint32_t span = cmax > tmax ? cmax : tmax;
         const unsigned gx = (unsigned)std::min<uint64_t>((span + 2047) / 2048 + 1, 1024);
+        const BindFin fin{mw, need, static_cast<uint32_t*>(hdev), (uint32_t)R};
         hipLaunchKernelGGL(k_list_equal_grid, dim3(gx, (unsigned)(R < 65535 ? R : 65535)),
-                           dim3(256), 0, ctx->stream, view(cur), view(val), rk, dd, R);
-        hipLaunchKernelGGL(k_bind_final, dim3((unsigned)std::min<uint64_t>((R + 255) / 256, 4096)),
-                           dim3(256), 0, ctx->stream, R, fw, dd, rk.flag, std_, errd);
+                           dim3(256), 0, ctx->stream, view(cur), view(val), rk, dd, R, tk, ti,
+                           tsz, mw + R + 3, fin);
         s = hipGetLastError() == hipSuccess ? LASPJ_OK
                                             : fail(ctx, LASPJ_E_DEVICE, "list_bind: launch");
+        if (s == LASPJ_OK) {
+            ctx->ltab_dirty = false;          // the clean-ups are enqueued
+            ctx->lbind_dirty = false;
+        }
     }
+    const auto* hb = static_cast<const uint8_t*>(ctx->lbind_h);
     if (s == LASPJ_OK) {
-        const laspj::ReadPiece rp[1] = {{hb.data(), dev, bytes}};
-        const hipError_t e = laspj::readback(ctx, rp, 1);
+        const hipError_t e = hipStreamSynchronize(ctx->stream);
         uint32_t f = 0;
-        if (e == hipSuccess) std::memcpy(&f, hb.data() + o_flag, 4);
-        s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: readback: %s",
+        if (e == hipSuccess) std::memcpy(&f, hb + 8 * R + 4 * ((R + 3) / 4), 4);
+        s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: synchronise: %s",
                                    hipGetErrorString(e))
                             : flag_status(ctx, f, "list_bind");
     }
-    laspj::dev_release(ctx, dev, bytes);
     if (s != LASPJ_OK) {
         dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;
         return s;
     }
-    set_known(dst, reinterpret_cast<const uint32_t*>(hb.data()), R);
+    set_known(dst, reinterpret_cast<const uint32_t*>(hb), R);
     // status: 0 = cur =:= val (no-op), 1 = the merge inflates cur (written), 2 = it does not
-    std::memcpy(status, hb.data() + o_st, R);
+    std::memcpy(status, hb + 8 * R, R);
     return LASPJ_OK;
 }
 

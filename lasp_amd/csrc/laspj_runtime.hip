@@ -285,6 +285,9 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->flag) hipFree(ctx->flag);
         if (ctx->partials) hipFree(ctx->partials);
         if (ctx->lscratch) hipFree(ctx->lscratch);
+        if (ctx->ltab) hipFree(ctx->ltab);
+        if (ctx->lbind) hipFree(ctx->lbind);
+        if (ctx->lbind_h) hipHostFree(ctx->lbind_h);
         laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
         if (ctx->dstage) hipHostFree(ctx->dstage);

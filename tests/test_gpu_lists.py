@@ -90,6 +90,16 @@ def _bind_want(kind, mod, p, v):
 
 
 @SETTINGS
+@given(st.lists(ENTRY, max_size=10, unique_by=lambda e: e[0]), OLIST, st.booleans())
+def test_list_bind_ascending_value0_skips_the_probe(a, b, gs):
+    """Value0 with strictly ascending keys (its tokens in any order, repeats allowed):
+    list_bind answers without probing (the inflation holds by construction, see
+    k_linf_insert) against a Value with unsorted and repeated keys — still the oracle's
+    bind/3, status and merged list."""
+    test_list_bind_matches_lasp_core.hypothesis.inner_test(sorted(a, key=lambda e: e[0]), b, gs)
+
+
+@SETTINGS
 @given(OLIST, OLIST, st.booleans())
 def test_list_bind_matches_lasp_core(a, b, gs):
     """laspj_list_bind (equal -> merge -> is_inflation in one call) over a 3-replica
