@@ -1731,10 +1731,15 @@ int sized(laspj_ctx* ctx, laspj_batch* dst, uint32_t* need, SizeFn size_pass, Wr
 }
 
 // a tiled producer (k_tp_*): `pre` carves its own scratch from the front of the block
-// (pre_bytes), enqueues whatever must run first and returns the functor
+// (pre_bytes), enqueues whatever must run first and returns the functor.
+// ub_e / ub_t (0: none): upper bounds of the output's entries / tokens per replica the
+// host knows, true in the usual case: dst sized to them, the count, scan and write passes
+// run back to back and one readback brings the sizes and the flag.  When the write pass
+// finds dst short after all (kErrRange: the bound did not hold), dst is sized from the
+// counts, which are still in the scratch, and the write pass runs again.
 template <class P, class Pre>
 int tiled(laspj_ctx* ctx, laspj_batch* dst, uint64_t max_items, uint64_t pre_bytes, Pre pre,
-          const char* what) {
+          const char* what, uint64_t ub_e = 0, uint64_t ub_t = 0) {
     const uint64_t R = dst->replicas;
     const uint64_t nt64 = max_items ? (max_items + kPTile - 1) / kPTile : 1;
     if (nt64 > 0x7FFFFFFFull) return fail(ctx, LASPJ_E_RANGE, "%s: lists too long", what);
@@ -1749,6 +1754,47 @@ int tiled(laspj_ctx* ctx, laspj_batch* dst, uint64_t max_items, uint64_t pre_byt
     const P p = pre(base);
     const dim3 grid(ntile, (unsigned)(R < 65535 ? R : 65535));
     const unsigned sg = (unsigned)(R < 65535 ? R : 65535);
+    if (ub_e && ub_t && ub_e <= 0xFFFFFFF0ull && ub_t <= 0xFFFFFFF0ull) {
+        const bool gs = dst->kind == LASPJ_KIND_GSET_LIST;
+        if (ub_e > dst->cap_e || ub_t > dst->cap_t)
+            if (int s = list_alloc(ctx, dst, ub_e > dst->cap_e ? (uint32_t)ub_e : dst->cap_e,
+                                   ub_t > dst->cap_t ? (uint32_t)ub_t : dst->cap_t, gs))
+                return s;
+        hipLaunchKernelGGL((k_tp_count<P>), grid, dim3(kPT), 0, ctx->stream, p, tc, ntile, R);
+        hipLaunchKernelGGL(k_tp_scan, dim3(sg), dim3(kPT), 0, ctx->stream, tc, ntile, R, need,
+                           flag);
+        hipLaunchKernelGGL((k_tp_write<P>), grid, dim3(kPT), 0, ctx->stream, p, view(dst), tc,
+                           ntile, R, need, flag);
+        LJ_LAUNCHED(ctx);
+        std::vector<uint32_t> h(2 * R);
+        uint32_t f = 0;
+        const laspj::ReadPiece rp[2] = {{h.data(), need, 8ull * R}, {&f, flag, 4}};
+        LJ_HIP(ctx, laspj::readback(ctx, rp, 2));
+        uint32_t ce = 0, ct = 0;
+        for (uint64_t i = 0; i < R; ++i) {
+            ce = h[2 * i] > ce ? h[2 * i] : ce;
+            ct = h[2 * i + 1] > ct ? h[2 * i + 1] : ct;
+        }
+        if (f == kErrRange && ce < 0xFFFFFFFFu && ct < 0xFFFFFFFFu &&
+            (ce > dst->cap_e || ct > dst->cap_t)) {
+            // the bound did not hold: dst from the counts, the write pass again
+            if (int s = list_alloc(ctx, dst, ce > dst->cap_e ? ce : dst->cap_e,
+                                   ct > dst->cap_t ? ct : dst->cap_t, gs))
+                return s;
+            LJ_HIP(ctx, hipMemsetAsync(flag, 0, 4, ctx->stream));
+            hipLaunchKernelGGL((k_tp_write<P>), grid, dim3(kPT), 0, ctx->stream, p, view(dst),
+                               tc, ntile, R, need, flag);
+            LJ_LAUNCHED(ctx);
+            LJ_HIP(ctx, laspj::readback(ctx, &f, flag, 4));
+        }
+        if (int s = flag_status(ctx, f, what)) {
+            dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;      // contents undefined
+            return s;
+        }
+        dst->known_e = ce;
+        dst->known_t = ct;
+        return LASPJ_OK;
+    }
     return sized(
         ctx, dst, need,
         [&] {
@@ -2177,7 +2223,8 @@ int laspj_list_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
         LGuard g(ctx);
         const LV L = view(l), Rr = view(r);
         return tiled<PConcat>(ctx, dst, (uint64_t)l->cap_e + r->cap_e, 0,
-                              [&](char*) { return PConcat{L, Rr}; }, "list_union");
+                              [&](char*) { return PConcat{L, Rr}; }, "list_union",
+                              std::max<uint64_t>(1, (uint64_t)l->known_e + r->known_e), 1);
     }
     return merge_impl(ctx, dst, l, r, ord, true, "list_union");
 }
@@ -2336,7 +2383,7 @@ int laspj_list_value(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
     LGuard g(ctx);
     const LV S = view(src);
     return tiled<PValue>(ctx, dst, src->cap_e, 0, [&](char*) { return PValue{S}; },
-                         "list_value");
+                         "list_value", src->known_e ? src->known_e : 1, 1);
 }
 
 int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
@@ -2365,9 +2412,11 @@ int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch*
     };
     if (gs)
         return tiled<PIsect<true>>(ctx, dst, l->cap_e, hbytes, pre(std::true_type{}),
-                                   "list_intersection");
+                                   "list_intersection", std::max<uint32_t>(1, l->known_e), 1);
+    // (tokens Cx ++ Cy: within l's and r's together unless l repeats a key of r)
     return tiled<PIsect<false>>(ctx, dst, l->cap_e, hbytes, pre(std::false_type{}),
-                                "list_intersection");
+                                "list_intersection", std::max<uint32_t>(1, l->known_e),
+                                std::max<uint64_t>(1, (uint64_t)l->known_t + r->known_t));
 }
 
 int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,

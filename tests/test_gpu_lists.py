@@ -164,6 +164,21 @@ def test_orset_list_bodies(a, b):
         "lasp_orset", a, b)))
 
 
+def test_orset_list_intersection_past_the_host_bound():
+    """The intersection is sized from l's and r's token counts together and written in
+    one pass; l repeating a key of r whose entry holds many tokens outgrows that bound:
+    the write pass finds dst short and runs again at the counted size (lasp_core.erl:546-589
+    body, keyfind per entry of l, tokens Cx ++ Cy)."""
+    s = Space()
+    toks = [b"t%02d" % i + b"\x00" * 17 for i in range(7)]
+    a = [(3, [(toks[0], False)])] * 6 + [(5, [(toks[1], True)]), (3, [(toks[2], False)])]
+    b = [(3, [(t, i % 2 == 0) for i, t in enumerate(toks)]), (5, [(toks[3], False)])]
+    A, B = s.enc(a), s.enc(b)
+    assert exact_eq(s.dec(A.intersection(B, s.order)), ocore.intersection_body("lasp_orset", a, b))
+    # and again on the same context (the bound holds this time)
+    assert exact_eq(s.dec(B.intersection(A, s.order)), ocore.intersection_body("lasp_orset", b, a))
+
+
 @SETTINGS
 @given(GLIST, GLIST)
 def test_gset_list_bodies(a, b):
