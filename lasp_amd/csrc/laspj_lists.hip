@@ -1942,13 +1942,18 @@ int laspj_list_from_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src
     const uint64_t wpr = src->words_per_replica;
     const uint32_t E = src->elements;
     uint32_t* flag = ctx->flag + 1;
+    // one entry per slot at most, 64 tokens per entry at most: exact bounds, used for a
+    // single pass while the tokens' block stays small (256 MiB)
+    const uint64_t R = src->replicas, ub_e = nslots ? nslots : 1;
+    const uint64_t ub_t = gs ? 1 : 64ull * ub_e;
+    const bool one = R * ub_t * 8ull <= (256ull << 20);
     if (gs)
         return tiled<PFromSet<true>>(ctx, dst, nslots, 0, [&](char*) {
             return PFromSet<true>{sp, wpr, ordp, nslots, E, tordp, flag};
-        }, "list_from_set");
+        }, "list_from_set", one ? ub_e : 0, one ? ub_t : 0);
     return tiled<PFromSet<false>>(ctx, dst, nslots, 0, [&](char*) {
         return PFromSet<false>{sp, wpr, ordp, nslots, E, tordp, flag};
-    }, "list_from_set");
+    }, "list_from_set", one ? ub_e : 0, one ? ub_t : 0);
 }
 
 static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch* a,
