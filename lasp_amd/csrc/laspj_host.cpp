@@ -924,4 +924,63 @@ bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_vie
     return true;
 }
 
+// Register the terms of the OR-Set payload p[0, n) elements that start in [from, to)
+// (from: an element's first byte, its 104 2 tuple header, as the segment decoder found
+// it): the same per-element parse and registration as laspj_dict_add's walk, over a range
+// — the NIF registers only the segments whose decode met an unknown term.  Stops at the
+// outer list's closing nil.  On any failure the range's registrations are undone.
+int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, size_t to) {
+    if (!dict || !p) return LASPJ_E_INVAL;
+    Dict* d = &dict->d;
+    d->journal.clear();
+    int st = LASPJ_DEC_OK;
+    try {
+        size_t off = from;
+        while (st == LASPJ_DEC_OK && off < to && off < n && p[off] != kNil) {
+            if (off + 2 > n || p[off] != kSmallTuple || p[off + 1] != 2) {
+                st = LASPJ_DEC_MALFORMED;
+                break;
+            }
+            off += 2;
+            const uint8_t* k = p + off;
+            const size_t kl = term_len(k, n - off);
+            if (!kl) { st = LASPJ_DEC_MALFORMED; break; }
+            off += kl;
+            if (off >= n) { st = LASPJ_DEC_MALFORMED; break; }
+            if (p[off] == kNil) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+            if (p[off] != kList || off + 5 > n) { st = LASPJ_DEC_MALFORMED; break; }
+            const uint32_t m = be32(p + off + 1);
+            off += 5;
+            uint32_t cur = 0;
+            if ((st = reg_elem(d, k, kl, &cur))) break;
+            for (uint32_t j = 0; j < m && st == LASPJ_DEC_OK; ++j) {
+                if (off + 2 > n || p[off] != kSmallTuple || p[off + 1] != 2) {
+                    st = LASPJ_DEC_MALFORMED;
+                    break;
+                }
+                off += 2;
+                const uint8_t* tk = p + off;
+                const size_t tkl = term_len(tk, n - off);
+                if (!tkl) { st = LASPJ_DEC_MALFORMED; break; }
+                off += tkl;
+                const size_t fl = off < n ? term_len(p + off, n - off) : 0;
+                if (!fl || bool_atom(p + off) < 0) { st = LASPJ_DEC_MALFORMED; break; }
+                off += fl;
+                uint8_t s;
+                st = reg_tok(d, cur, tk, tkl, &s);
+            }
+            if (st) break;
+            if (off >= n || p[off] != kNil) { st = LASPJ_DEC_MALFORMED; break; }
+            off += 1;
+        }
+    } catch (const std::bad_alloc&) {
+        d->rollback();
+        d->journal.clear();
+        return LASPJ_E_NOMEM;
+    }
+    if (st != LASPJ_DEC_OK) d->rollback();
+    d->journal.clear();
+    return st;
+}
+
 }  // namespace laspj

@@ -307,5 +307,8 @@ uint32_t dict_elements(const laspj_dict* dict);
 uint32_t dict_token_count(const laspj_dict* dict, uint32_t e);
 bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_view>* imgs,
                  std::vector<uint8_t>* order);
+// register the terms of the OR-Set payload elements that start in [from, to) (from: an
+// element's first byte); a DEC status (the range's registrations undone on failure)
+int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, size_t to);
 
 }  // namespace laspj

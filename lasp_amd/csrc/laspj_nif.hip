@@ -111,6 +111,12 @@ struct Call {
     std::vector<uint64_t> ooff;     // n + 1 answer payload offsets (MERGE / VALUE)
     const uint8_t* obase = nullptr; // pinned answer payloads
     bool no_defer = false;          // a deferred chain check came back kDecRedo: decode serially
+    // a deferred pass that met unknown terms: its segment results (SegRes records, 32 bytes
+    // each: status, start, ...) and table, so only the failing segments are registered
+    bool has_seg = false;
+    std::vector<uint32_t> segres;   // 8 words per segment
+    std::vector<uint32_t> segbase;
+    uint64_t segS = 0;
 };
 
 laspj_batch view(laspj_ctx* ctx, int32_t kind, uint64_t R, uint32_t E, uint64_t* dev) {
@@ -515,6 +521,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         c.st.assign(m, 0);
         if (dec) std::memcpy(c.st.data(), hout + o_st, 4ull * m);
         else c.st = hst;
+        c.has_seg = false;
+        if (defer && cjob.armed &&
+            std::find(c.st.begin(), c.st.end(), (int32_t)LASPJ_DEC_UNKNOWN_TERM) != c.st.end()) {
+            c.segres.resize(8ull * plan.nseg);
+            LJ_HIP(ctx, hipMemcpyAsync(c.segres.data(), cjob.res, kSegResBytes * plan.nseg,
+                                       hipMemcpyDeviceToHost, ctx->stream));
+            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            c.segbase = plan.segbase;
+            c.segS = plan.S;
+            c.has_seg = true;
+        }
         c.res.assign(hout + o_res, hout + o_res + n);
         if (has_payload_out) {
             c.ooff.resize(n + 1ull);
@@ -558,6 +575,40 @@ int register_payloads(laspj_ctx* ctx, NifState* S, const std::vector<const uint8
     return LASPJ_OK;
 }
 
+// A deferred pass's unknown terms: each failing segment of those operands (a status and a
+// start: its first element, where the chain check found it) registers the elements that
+// start in it — what the segment's decoder could not take; the segments that decoded hold
+// known terms.  False: a range did not register (nothing is kept), the caller registers
+// whole operands.
+bool register_segments(laspj_ctx* ctx, NifState* S, const Call& c,
+                       const std::vector<uint32_t>& ops) {
+    const uint64_t t0 = now_ns();
+    struct Range {
+        uint32_t i;
+        uint64_t from, to;
+    };
+    std::vector<Range> rs;
+    for (uint32_t i : ops) {
+        if (i + 1 >= c.segbase.size()) return false;
+        for (uint32_t g = c.segbase[i]; g < c.segbase[i + 1]; ++g) {
+            const int32_t st = (int32_t)c.segres[8ull * g];
+            const uint32_t start = c.segres[8ull * g + 1];
+            if (st == LASPJ_DEC_OK) continue;
+            if (start == 0xFFFFFFFFu) return false;
+            const uint64_t s = g - c.segbase[i];
+            rs.push_back({i, start, std::min<uint64_t>((s + 1) * c.segS, c.len[i])});
+        }
+    }
+    if (rs.empty()) return false;
+    for (const Range& r : rs)
+        if (dict_add_elems(S->dict, c.p[r.i], c.len[r.i], r.from, r.to) != LASPJ_DEC_OK)
+            return false;       // (ranges already added stay: they hold well-formed terms)
+    ++S->stats[2];
+    S->stats[12] += now_ns() - t0;
+    S->stale = true;
+    return true;
+}
+
 // The call: device pass; operands with unknown terms registered and a second pass; every
 // other undecodable operand -> FALLBACK.  verdict[j] per answer.
 int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
@@ -567,6 +618,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
     auto answer_of = [&](uint32_t i) { return i % n; };
     std::vector<uint8_t> fallback(n, 0);
     bool registered = false;
+    bool partial = false;           // the last registration took the failing segments only
     for (int pass = 0; pass < 4; ++pass) {
         if (!S->etf || S->stale) {
             if (!S->etf) {
@@ -595,10 +647,18 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         std::vector<uint32_t> unknown;
         for (uint32_t i = 0; i < m; ++i) {
             if (fallback[answer_of(i)]) continue;
-            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && !registered) unknown.push_back(i);
+            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && (!registered || partial)) unknown.push_back(i);
             else if (c.st[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
         }
         if (unknown.empty()) break;
+        if (!registered && c.has_seg && register_segments(ctx, S, c, unknown)) {
+            // the failing segments' elements registered; if the next pass still meets an
+            // unknown term, the whole operands are registered after all
+            partial = true;
+            registered = true;
+            continue;
+        }
+        partial = false;
         // terms the dictionary has not seen (or operands that are not orddicts, which the
         // second pass tells apart): register the operands that met them (an operand that
         // decoded holds only registered terms)
