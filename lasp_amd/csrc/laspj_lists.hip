@@ -887,9 +887,20 @@ __global__ __launch_bounds__(kMT) void k_merge_chunk_scan(MS m, uint64_t R, uint
     for (u64 r = blockIdx.x; r < R; r += gridDim.x) chunk_scan_replica(m, r, need, s_w);
 }
 
+// list_bind: the merged list's keyfind table filled by the write pass itself (the keys it
+// writes, their ranks from the rank pass) for the replicas whose check runs (used[r]) —
+// k_linf_insert's work without its launch
+struct Ins {
+    u64* hk;
+    uint32_t* hi;
+    uint32_t hsize;
+    const uint32_t* used;
+};
+
 // the write pass: one planned entry per thread
 template <int MODE>
-__global__ __launch_bounds__(kMT) void k_merge_write(LV a, LV b, LV out, RK rk, MS m, uint64_t R) {
+__global__ __launch_bounds__(kMT) void k_merge_write(LV a, LV b, LV out, RK rk, MS m, uint64_t R,
+                                                     Ins ins) {
     __shared__ uint32_t s_w[kMT / 64];
     for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
         const uint32_t nout = m.nout[r], nt = m.ntok[r], o0 = blockIdx.x * kMT;
@@ -919,6 +930,9 @@ __global__ __launch_bounds__(kMT) void k_merge_write(LV a, LV b, LV out, RK rk, 
             jb = (uint32_t)(p >> 32);
         }
         out.K(r)[o] = ia != kNone ? a.K(r)[ia] : b.K(r)[jb];
+        if (ins.hk && ins.used[r])
+            h_insert(ins.hk + r * ins.hsize, ins.hi + r * ins.hsize, ins.hsize - 1,
+                     ia != kNone ? m.sa[r * m.ce_a + ia] : m.sb[r * m.ce_b + jb], o);
         if (MODE == 2) continue;
         out.O(r)[o] = tpos;
         u64* to = out.T(r) + tpos;
@@ -1982,7 +1996,7 @@ static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch
 static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                          const laspj_batch* b, const RK& rk, bool keep_left, uint32_t* need,
                          uint8_t* eq, const char* what, uint32_t* words = nullptr,
-                         uint64_t words_bytes = 0) {
+                         uint64_t words_bytes = 0, const Ins* ins = nullptr) {
     // (words_bytes == 0 with words: they are known zero already, no memset)
     const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
     const uint64_t R = a->replicas;
@@ -2078,7 +2092,8 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         hipLaunchKernelGGL(k_merge_chunk_scan, dim3(rx), dim3(kMT), 0, ctx->stream, m, R, need);
         // the write pass (it raises kErrRange rather than write past dst's capacity)
         hipLaunchKernelGGL((k_merge_write<MODE>), dim3(m.nchunks ? m.nchunks : 1, ry), dim3(kMT),
-                           0, ctx->stream, A, B, OUT, rk, m, R);
+                           0, ctx->stream, A, B, OUT, rk, m, R,
+                           ins ? *ins : Ins{nullptr, nullptr, 0, nullptr});
     };
     if (gs) passes(std::integral_constant<int, 2>{});
     else if (keep_left) passes(std::integral_constant<int, 1>{});
@@ -2131,6 +2146,34 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     return LASPJ_OK;
 }
 
+// list_bind's keyfind tables: ctx->ltab, at least `bytes`, all zero (zeroed here when new
+// or when a call may have left them used); marked in use until the caller's clean-up is
+// enqueued.  Null (and the context's error set) when it cannot be allocated.
+static char* bind_tables(laspj_ctx* ctx, uint64_t bytes, const char* what) {
+    if (ctx->ltab_bytes < bytes || ctx->ltab_dirty) {
+        if (ctx->ltab_bytes < bytes) {
+            if (ctx->ltab) {
+                hipStreamSynchronize(ctx->stream);
+                hipFree(ctx->ltab);
+                ctx->ltab = nullptr;
+                ctx->ltab_bytes = 0;
+            }
+            if (laspj::dev_malloc(ctx, &ctx->ltab, bytes) != hipSuccess) {
+                hipGetLastError();
+                fail(ctx, LASPJ_E_NOMEM, "%s: keyfind tables", what);
+                return nullptr;
+            }
+            ctx->ltab_bytes = bytes;
+        }
+        if (hipMemsetAsync(ctx->ltab, 0, ctx->ltab_bytes, ctx->stream) != hipSuccess) {
+            fail(ctx, LASPJ_E_DEVICE, "%s: keyfind tables memset", what);
+            return nullptr;
+        }
+    }
+    ctx->ltab_dirty = true;
+    return static_cast<char*>(ctx->ltab);
+}
+
 // the inflation kernels of prev -> cur into o (R bytes); clear_flag: start from a clean
 // error flag (the fused bind keeps the merge's bits and reads them with o)
 // final = false: the answer kernel is left to the caller, which gets the flag words
@@ -2157,25 +2200,16 @@ static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj
     uint32_t* flags = nullptr;
     if (zeroed_flags) {
         // list_bind: the tables kept zeroed in ctx->ltab (the caller's last kernel zeroes
-        // what this check used), the flag words the caller's, zeroed with its own
-        if (ctx->ltab_bytes < tbytes || ctx->ltab_dirty) {
-            if (ctx->ltab_bytes < tbytes) {
-                if (ctx->ltab) {
-                    hipStreamSynchronize(ctx->stream);
-                    hipFree(ctx->ltab);
-                    ctx->ltab = nullptr;
-                    ctx->ltab_bytes = 0;
-                }
-                if (laspj::dev_malloc(ctx, &ctx->ltab, tbytes) != hipSuccess) {
-                    hipGetLastError();
-                    return fail(ctx, LASPJ_E_NOMEM, "%s: keyfind tables", what);
-                }
-                ctx->ltab_bytes = tbytes;
-            }
-            LJ_HIP(ctx, hipMemsetAsync(ctx->ltab, 0, ctx->ltab_bytes, ctx->stream));
+        // what this check used) — acquired by the caller already when *tab_k is set (its
+        // merge's write pass filled them: no insert launch), the flag words the caller's,
+        // zeroed with its own
+        if (tab_k && *tab_k) {
+            base = reinterpret_cast<char*>(*tab_k);
+            if (*tab_size != hsize) return fail(ctx, LASPJ_E_INVAL, "%s: table size", what);
+        } else {
+            base = bind_tables(ctx, tbytes, what);
+            if (!base) return LASPJ_E_NOMEM;
         }
-        ctx->ltab_dirty = true;              // until the caller's clean-up is enqueued
-        base = static_cast<char*>(ctx->ltab);
         flags = zeroed_flags;
         if (zeroed_words) *zeroed_words = flags + R;
     } else {
@@ -2190,6 +2224,7 @@ static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj
     u64* hk = reinterpret_cast<u64*>(base);
     auto* hi = reinterpret_cast<uint32_t*>(base + R * ntab * hsize * 8ull);
     if (flag_words) *flag_words = flags;
+    const bool inserted = tab_k && *tab_k;
     if (tab_k) *tab_k = hk;
     if (tab_i) *tab_i = hi;
     if (tab_size) *tab_size = hsize;
@@ -2198,8 +2233,9 @@ static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj
     const unsigned fg = (unsigned)((R + 255) / 256 < 4096 ? (R + 255) / 256 : 4096);
 #define LJ_INFL(G, S)                                                                         \
     do {                                                                                      \
-        hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,   \
-                           hk, hi, hsize, bcast, R, skip);                                    \
+        if (!inserted)                                                                        \
+            hipLaunchKernelGGL((k_linf_insert<G, S>), grid, dim3(256), 0, ctx->stream, P, C,   \
+                               rk, hk, hi, hsize, bcast, R, skip);                            \
         hipLaunchKernelGGL((k_linf_probe<G, S>), grid, dim3(256), 0, ctx->stream, P, C, rk,    \
                            hk, hi, hsize, bcast, R, flags, skip);                             \
         if (final)                                                                            \
@@ -2336,11 +2372,21 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     uint32_t* dd = nullptr;
     const uint32_t* fw = nullptr;
     rk.flag = mw;
-    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind", mw, wzero);
+    // the merged list's keyfind table, filled by the merge's write pass (Ins): sized as
+    // inflation_launch sizes it, from the capacities the merge leaves dst with
+    const uint64_t be = (uint64_t)cur->known_e + val->known_e;
+    const uint32_t dce = be > dst->cap_e ? (uint32_t)std::min<uint64_t>(be, 0xFFFFFFFFull)
+                                         : dst->cap_e;
+    const uint32_t tsz0 = pow2_at_least(2ull * (dce > cur->cap_e ? dce : cur->cap_e));
+    char* tb = bind_tables(ctx, R * tsz0 * 12ull, "list_bind");
+    if (!tb) return LASPJ_E_NOMEM;
+    u64* tk = reinterpret_cast<u64*>(tb);
+    uint32_t* ti = reinterpret_cast<uint32_t*>(tb + R * tsz0 * 8ull);
+    uint32_t tsz = tsz0;
+    const Ins ins{tk, ti, tsz0, mw + R + 3};
+    int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind", mw, wzero,
+                          &ins);
     // (Value0's replicas whose keys strictly ascend skip the check: see k_linf_insert)
-    u64* tk = nullptr;
-    uint32_t* ti = nullptr;
-    uint32_t tsz = 0;
     if (s == LASPJ_OK)
         s = inflation_launch(ctx, cur, dst, 0, rk, nullptr, false, "list_bind", &dd, false, &fw,
                              mw + R + 3, mw + 2 * R + 3, &tk, &ti, &tsz);
