@@ -6,17 +6,20 @@
 // 67-73, 128-138), called from lasp_core:bind/3 (lasp_core.erl:291-312) on many BEAM
 // schedulers at once (lasp_vnode.erl:213-237).  A call here takes the operands as
 // `term_to_binary/1` images and
-//   1. stages them into the context's pinned ring and copies them to the device (one
-//      asynchronous copy; offsets and the decoder's segment table ride along),
+//   1. stages them into the context's pinned memory, and kernels on the context's stream
+//      pull them to the device in pieces while the host stages the next (offsets and the
+//      decoder's segment table ride along; LASPJ_TUNE_NIF_DIRECT 0: copy-engine copies),
 //   2. decodes them on the device against the context's dictionary (laspj_orset_etf_read's
 //      kernels), joins / tests / filters the cells, encodes the answer on the device
-//      (laspj_orset_etf_write's kernels) and copies it back — all enqueued on the
+//      (laspj_orset_etf_write's kernels) straight into pinned memory — all enqueued on the
 //      context's stream with ONE host synchronisation,
 //   3. answers from pinned memory: the merged / value term's image (what the NIF hands to
 //      enif_binary_to_term) or the boolean.
 // A term the dictionary has not seen (a freshly minted token) makes the decoder answer
-// UNKNOWN_TERM: the call registers the operands' terms in the host dictionary
-// (laspj_dict_add), rebuilds the device images and runs the device pass again.  An
+// UNKNOWN_TERM: the call registers the operands' terms in the host dictionary (only the
+// elements of the decoder segments that failed, when it decoded in segments; else the
+// whole operands, laspj_dict_add), patches or rebuilds the device images and runs the
+// device pass again.  An
 // operand the columnar form does not take — not an orddict of {Elem, [{Token, Bool}]} in
 // term order, an element with no tokens or more than 64, a term kind no dictionary holds —
 // gets verdict LASPJ_NIF_FALLBACK: the NIF then runs the reference's own Erlang clause,
