@@ -818,17 +818,68 @@ __global__ __launch_bounds__(kBlock) void k_etf_chunk_scan_offsets(u64* coff, ui
     }
 }
 
+// LB (the NIF's single merge, laspj_nif.hip): merge/2's join and the size pass folded into
+// the writer.  One block per 256-element chunk of the one answer: it ORs the operands'
+// cells (clearing them behind it), sizes its elements, publishes its chunk's {bytes,
+// elements} and looks back over its predecessors' (decoupled look-back: a word per chunk,
+// 1 = own totals, 2 = inclusive prefix) for its offset, then writes as split mode does.
+// The list header's element count is not known to chunk 0: it writes a placeholder and the
+// block that finishes last (ticket) writes the count (or the empty list 131 106), the
+// answer's offsets {0, total} and — extra blocks after the chunks' — the segment decoder's
+// chain checks (as k_etf_join_chunk_sizes does beside the join).  A total past ocap: the
+// chunks write nothing, the caller re-runs with room.
+struct LBJoin {
+    u64x2* a;          // the operands' cells (cleared behind)
+    u64x2* b;
+    u64* st;           // a look-back word per chunk, zero on entry
+    uint32_t* ticket;  // zero on entry, left zero
+    u64* offs_out;     // {0, total}
+    ChainArgs cj;      // chain checks (cj.status null: none)
+};
+constexpr u64 kLBCnt = 1ull << 40;              // look-back word: bytes | elements << 40
+constexpr u64 kLBVal = (1ull << 62) - 1;
+
+__device__ void lb_finish(const LBJoin& lb, uint32_t nch, uint32_t hdr, uint8_t* out) {
+    __shared__ uint32_t s_lb_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();            // this block's answer bytes (host memory) first
+        s_lb_last = atomicAdd(lb.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_lb_last || threadIdx.x != 0) return;
+    __threadfence_system();
+    const u64 w = __hip_atomic_load(lb.st + nch - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 bytes = w & (kLBCnt - 1), n = (w & kLBVal) >> 40;
+    u64 total;
+    if (n) {
+        out[hdr + 2] = (uint8_t)(n >> 24);
+        out[hdr + 3] = (uint8_t)(n >> 16);
+        out[hdr + 4] = (uint8_t)(n >> 8);
+        out[hdr + 5] = (uint8_t)n;
+        total = hdr + 6 + bytes + 1;
+    } else {
+        out[hdr + 1] = 106;                 // 131 106: []
+        total = hdr + 2;
+    }
+    lb.offs_out[0] = 0;
+    lb.offs_out[1] = total;
+    *lb.ticket = 0;
+    __threadfence_system();
+}
+
 // EPAR (few token slots per element): each element's thread also stages its own records
 // (no record -> element search, no rank select); otherwise records are spread over lanes.
 // coff != nullptr: split mode (above), block b writes chunks [g cper, (g + 1) cper) of
 // payload b / ngroups.
-template <uint32_t WIN, bool EPAR>
+template <uint32_t WIN, bool EPAR, bool LB = false>
 __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cells, uint64_t R,
                                                                 uint32_t E, DictView d, int tag,
                                                                 int vers, const u64* offs,
                                                                 uint8_t* out, const u64* coff,
-                                                                uint32_t cper, u64 ocap) {
-    if (offs[R] > ocap) return;
+                                                                uint32_t cper, u64 ocap,
+                                                                LBJoin lb) {
+    if (!LB && offs[R] > ocap) return;
     __shared__ __attribute__((aligned(16))) uint32_t winbuf[(WIN + 2 * kGuard) / 4];
     __shared__ uint32_t s_e[kBlock], s_pos[kBlock + 1], s_rec[kBlock + 1], s_hl[kBlock];
     __shared__ u64 s_p[kBlock], s_r[kBlock], lds4[kBlock / 64];
@@ -843,7 +894,25 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
     const uint32_t ngroups = coff ? (nch + cper - 1) / cper : 1u;
     uint64_t r_begin, r_end;
     uint32_t c_begin = 0, c_end = E;             // element positions [c_begin, c_end)
-    if (coff) {
+    if (LB && blockIdx.x >= nch) {
+        // the chain checks: a wave per decoded operand
+        const uint32_t r = (blockIdx.x - nch) * 4u + (tid >> 6), lane = tid & 63u;
+        if (r < lb.cj.nrep) {
+            const u64 base = lb.cj.offs[r];
+            const int32_t st = chain_verdict(lb.cj.payload, base, lb.cj.offs[r + 1] - base,
+                                             lb.cj.segbase[r], lb.cj.segbase[r + 1] - lb.cj.segbase[r],
+                                             lb.cj.S, lb.cj.res, lane);
+            if (lane == 0) lb.cj.status[r] = st;
+        }
+        lb_finish(lb, nch, hdr, out);
+        return;
+    }
+    if (LB) {
+        r_begin = 0;
+        r_end = 1;
+        c_begin = blockIdx.x * kBlock;
+        c_end = min(E, c_begin + kBlock);
+    } else if (coff) {
         r_begin = blockIdx.x / ngroups;
         r_end = r_begin + 1;
         const uint32_t g = blockIdx.x - (uint32_t)(r_begin * ngroups);
@@ -872,7 +941,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
         if (hl_c <= 16) h_c = *reinterpret_cast<const u32x4*>(d.ehdr_pad + d.ehdr_poff[e_c]);
         v_next = cells[r_begin * E + e_c];
     }
-    u64 mask_lo = offs[r_begin];    // output bytes below this belong to another block
+    u64 mask_lo = LB ? 0 : offs[r_begin];    // output bytes below this belong to another block
     uint32_t n_split = 0;
     u64 cur_split = 0;
     if (coff) {
@@ -885,8 +954,8 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
     u64 seg_lo = mask_lo;           // bytes [floor16(seg_lo), seg_lo) are the carry in win[0..4)
     for (uint64_t rep = r_begin; rep < r_end; ++rep) {
         const u64x2* c = cells + rep * E;
-        const u64 base = offs[rep], end = offs[rep + 1];
-        if (!coff && seg_lo != base) {
+        const u64 base = LB ? 0 : offs[rep], end = LB ? ocap : offs[rep + 1];
+        if (!coff && !LB && seg_lo != base) {
             // the previous payload broke off (sizes disagreed): flush, restart at base
             if (tid < 16) {
                 const u64 g = (seg_lo & ~15ull) + tid;
@@ -901,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
         // present elements (the list header's length field): counted up front when the
         // replica spans several chunks, else taken from the one chunk's scan
         uint32_t n = n_split;
-        if (!coff && E > kBlock) {
+        if (!coff && !LB && E > kBlock) {
             u64 cnt = 0;
             for (uint32_t e = tid; e < E; e += kBlock) cnt += cw[2ull * (rep * E + e)] != 0;
             u64 n64;
@@ -917,7 +986,16 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             u64 pt = 0, rt = 0;
             if (i < E) {
                 e = single ? e_c : d.elem_order[i];
-                const u64x2 v = single ? v_next : c[e];
+                u64x2 v;
+                if (LB) {
+                    // merge/2: the slot-wise OR of the operands' cells, cleared behind
+                    const u64 at = rep * E + e;
+                    v = lb.a[at] | lb.b[at];
+                    lb.a[at] = u64x2{0, 0};
+                    lb.b[at] = u64x2{0, 0};
+                } else {
+                    v = single ? v_next : c[e];
+                }
                 if (single && rep + 1 < r_end) v_next = c[E + e];       // next replica
                 if (v.x) {
                     const u32x4* ord = reinterpret_cast<const u32x4*>(d.tok_order + 64ull * e);
@@ -944,9 +1022,47 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             const u64 pr = block_excl_scan64((u64)sz | ((u64)nt << 32) | ((u64)(sz != 0) << 52),
                                              lds4, &tot2);
             const uint32_t pos = (uint32_t)pr, tot = (uint32_t)tot2;
-            if (c0 == 0) {
-                if (E <= kBlock) n = (uint32_t)(tot2 >> 52);
-                cursor = base + hdr + (n ? 6u : 2u);
+            bool closing;
+            if (LB) {
+                // this chunk's {bytes, elements} published, its offset looked back for
+                __shared__ u64 s_pre;
+                if (tid == 0) {
+                    const uint32_t ch = c0 / kBlock;
+                    const u64 own = (u64)tot + ((tot2 >> 52) & 0xFFFull) * kLBCnt;
+                    u64 acc = 0;
+                    if (ch == 0) {
+                        __hip_atomic_store(lb.st, (2ull << 62) | own, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        __hip_atomic_store(lb.st + ch, (1ull << 62) | own, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        for (int32_t j = (int32_t)ch - 1; j >= 0;) {
+                            const u64 w = __hip_atomic_load(lb.st + j, __ATOMIC_ACQUIRE,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                            if (!(w >> 62)) continue;             // not published yet
+                            acc += w & kLBVal;
+                            if ((w >> 62) == 2) break;
+                            --j;
+                        }
+                        __hip_atomic_store(lb.st + ch, (2ull << 62) | (acc + own),
+                                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    s_pre = acc;
+                }
+                __syncthreads();
+                const u64 pre = s_pre;
+                const u64 ic = ((pre & kLBVal) >> 40) + ((tot2 >> 52) & 0xFFFull);
+                n = 1;                              // (a placeholder: lb_finish writes it)
+                cursor = hdr + 6u + (pre & (kLBCnt - 1));
+                if (c0) mask_lo = cursor;
+                seg_lo = mask_lo;
+                closing = last && ic != 0;
+            } else {
+                if (c0 == 0) {
+                    if (E <= kBlock) n = (uint32_t)(tot2 >> 52);
+                    cursor = base + hdr + (n ? 6u : 2u);
+                }
+                closing = last && n;
             }
             s_e[tid] = e;
             s_p[tid] = pt;
@@ -958,7 +1074,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                 s_pos[kBlock] = tot;
                 s_rec[kBlock] = (uint32_t)(tot2 >> 32) & 0xFFFFFu;
             }
-            const u64 seg_hi = cursor + tot + (last && n ? 1u : 0u);
+            const u64 seg_hi = cursor + tot + (closing ? 1u : 0u);
             if (seg_hi > end) break;                      // sizes disagree: never overrun
             __syncthreads();
             const uint32_t nrec = s_rec[kBlock];
@@ -980,7 +1096,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     const int32_t rel = (int32_t)(int64_t)(base - A);
                     if (overlaps<WIN>(rel, nb)) or_piece<3>(win, rel, w, 8);
                 }
-                if (last && n && tid == 0) {
+                if (closing && tid == 0) {
                     const uint32_t w[1] = {106u};
                     const int32_t rel = cur_rel + (int32_t)tot;
                     if (overlaps<WIN>(rel, 1)) or_piece<1>(win, rel, w, 1);
@@ -1139,6 +1255,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
         const u64 g = (seg_lo & ~15ull) + tid;
         if (g >= mask_lo && g < seg_lo) out[g] = (uint8_t)(win[tid >> 2] >> (8 * (tid & 3)));
     }
+    if (LB) lb_finish(lb, nch, hdr, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gset_etf_size(const u64* words, uint64_t R,
@@ -4723,6 +4840,32 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
     return LASPJ_OK;
 }
 
+bool etf_merge_write_one(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, uint32_t E) {
+    return R == 1 && etf_merge_fused(ctx, R, E) && d->rec_len && ctx->tune_etf == 0 &&
+           E < (1u << 22);
+}
+
+int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E,
+                            const laspj_etf_dict* d, int tag, int vers, u64* offs_out,
+                            uint8_t* out, uint64_t cap_bytes, u64* lbst, uint32_t* ticket,
+                            const ChainJob* chain) {
+    const uint32_t nch = (E + kBlock - 1) / kBlock;
+    LBJoin lb{reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b), lbst, ticket, offs_out,
+              ChainArgs{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0}};
+    if (chain && chain->armed)
+        lb.cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
+                          static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
+                          chain->S};
+    const uint32_t cblocks = lb.cj.status ? (lb.cj.nrep + 3u) / 4u : 0u;
+    auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true, true>
+                             : k_orset_etf_write_rec<24576, false, true>;
+    hipLaunchKernelGGL(k, dim3(nch + cblocks), dim3(kBlock), 0, ctx->stream, (const u64x2*)nullptr,
+                       (uint64_t)1, E, view(d), tag, vers, (const u64*)nullptr, out,
+                       (const u64*)nullptr, 1u, (u64)cap_bytes, lb);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                       int32_t kind, int tag, int vers, const u64* offsets, uint8_t* out,
                       uint64_t cap_bytes, const u64* chunks) {
@@ -4784,7 +4927,7 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
         }
         hipLaunchKernelGGL(k, dim3(grid ? grid : 1), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
-                           vers, offsets, out, coff, cper, (u64)cap_bytes);
+                           vers, offsets, out, coff, cper, (u64)cap_bytes, LBJoin{});
     } else if (kind == LASPJ_KIND_ORSET && d->tok_max > 8)
         hipLaunchKernelGGL(k_orset_etf_write_wave, dim3(grid ? grid : 1), dim3(kBlock), 0,
                            ctx->stream, reinterpret_cast<const u64x2*>(b->dev), R, b->elements,

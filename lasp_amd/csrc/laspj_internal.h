@@ -280,6 +280,15 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
                            const laspj_etf_dict* d, int tag, unsigned long long* offsets,
                            uint32_t* flag, uint32_t* ticket, const unsigned long long** chunks,
                            const ChainJob* chain = nullptr);
+// the NIF's single merge (R == 1): join, size pass and writer in ONE launch
+// (k_orset_etf_write_rec's look-back form), when etf_merge_write_one holds; lbst: a zeroed
+// word per 256-element chunk, ticket: a zeroed word (left zero), offs_out: {0, total}
+// (total > cap: nothing written), chain: the deferred chain checks ride along
+bool etf_merge_write_one(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, uint32_t E);
+int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E,
+                            const laspj_etf_dict* d, int tag, int vers,
+                            unsigned long long* offs_out, uint8_t* out, uint64_t cap_bytes,
+                            unsigned long long* lbst, uint32_t* ticket, const ChainJob* chain);
 // offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
 // caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
 // (valid until the context's scratch is next used), or null

@@ -272,7 +272,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     //  list | payloads]
     const uint64_t i_offs = 0, i_seg = al(8ull * (m + 1), 256),
                    i_zero = i_seg + (plan.nseg ? al(4ull * (m + 1), 256) : 0),
-                   i_pay = i_zero + al(4ull * (m + 2), 256);
+                   // [ticket | redo list m + 1 | one-launch merge's look-back words]
+                   z_lb = al(4ull * (m + 2), 16), z_bytes = z_lb + 8ull * ((E + 255) / 256),
+                   i_pay = i_zero + al(z_bytes, 256);
     const uint64_t cells_in = (uint64_t)m * E * 16ull;
     const uint64_t in_bytes = i_pay + (dec ? al(pay + 64, 256) : al(cells_in, 256));
     // out region (device -> host)
@@ -355,8 +357,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
     std::memcpy(hin + i_offs, hoffs.data(), 8ull * (m + 1));
     if (plan.nseg) std::memcpy(hin + i_seg, plan.segbase.data(), 4ull * (m + 1));
-    std::memset(hin + i_zero, 0, 4ull * (m + 2));
+    std::memset(hin + i_zero, 0, z_bytes);
     uint32_t* dticket = reinterpret_cast<uint32_t*>(din + i_zero);
+    auto* dlb = reinterpret_cast<unsigned long long*>(din + i_zero + z_lb);
     const uint64_t in_words = (uint64_t)m * 2ull * E;
     const bool clean = S->clean_E == E && S->clean_words >= in_words;
     std::vector<int32_t> hst;
@@ -386,7 +389,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 at += c.len[i];
             }
             t_copy += now_ns() - tc;
-            LJ_HIP(ctx, hipMemsetAsync(din + i_zero, 0, 4ull * (m + 2), ctx->stream));
+            LJ_HIP(ctx, hipMemsetAsync(din + i_zero, 0, z_bytes, ctx->stream));
         } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
@@ -466,6 +469,16 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             // canonical orddicts is the slot-wise OR of their cells
             laspj_batch ob = view(ctx, LASPJ_KIND_ORSET, n, E, cout);
             const unsigned long long* chunks = nullptr;
+            if (etf_merge_write_one(ctx, S->etf, n, E)) {
+                // one answer: join, size pass and writer in one launch (look-back), the
+                // operands cleared behind it, the chain checks riding along
+                if (int s = etf_merge_write_enqueue(ctx, lhs.dev, rhs.dev, E, S->etf, -1, 1, dooff,
+                                                    dopay, ocap, dlb, dticket, &cjob))
+                    return s;
+                S->clean_words = in_words;
+                S->clean_E = E;
+                break;
+            }
             if (etf_merge_fused(ctx, n, E)) {
                 // the OR fused with the answer's size pass, the operands cleared behind it
                 if (int s = etf_merge_size_enqueue(ctx, lhs.dev, rhs.dev, &ob, S->etf, -1, dooff,
