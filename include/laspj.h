@@ -126,7 +126,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         slots, spread over lanes otherwise), 1 = element
                                         staging, 2 / 3 = record kernel, lanes, 16 / 20 KiB,
                                         4 = record kernel, lanes, 24 KiB, 5 = record
-                                        kernel, per element thread, 24 KiB               */
+                                        kernel, per element thread, 24 KiB.  0 also
+                                        writes a NIF entry point's single merge in one
+                                        launch with its join and size pass (look-back);
+                                        any other value keeps them separate              */
 #define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = tiles of 4
                                         cells per lane, one per block, when the replica
                                         length is a power of two and 2 <= group <= 4
