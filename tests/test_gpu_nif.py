@@ -336,6 +336,30 @@ def test_nif_false_element_headers_in_tokens_take_the_serial_pass():
 
 
 @pytest.mark.gpu
+def test_nif_one_launch_merge_edges():
+    """The single merge written in one launch (look-back over 256-element chunks) once the
+    context's dictionary holds >= 1024 element slots: an empty answer ([] with [] -> the
+    list header alone, 131 106), answers whose present elements sit in one chunk or at
+    the ends, and an operand of one element — each the oracle's image."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(41)
+        tok = lambda e, k: bytes([k, e % 251, e // 251]) + bytes(17)   # noqa: E731
+        big = [(e, [(tok(e, 0), False)]) for e in range(1500)]
+        assert ctx.nif_merge(_tb(big), _tb(big)) == (OK, _tb(big))
+        cases = [([], []),
+                 ([], big[:1]),
+                 (big[700:760], big[730:800]),
+                 (big[:3], big[-3:]),
+                 ([(e, [(tok(e, 0), True)]) for e in range(0, 1500, 97)], big[::250])]
+        for a, b in cases:
+            assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(oorset.merge(a, b))), (len(a), len(b))
+        assert ctx.nif_stats()["registrations"] >= 1
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 def test_nif_dictionary_reset_when_an_element_runs_out_of_token_slots():
     """Calls are self-contained, so a context whose dictionary has given an element all 64
     token slots starts a fresh dictionary for a call that needs more (and answers it)."""
