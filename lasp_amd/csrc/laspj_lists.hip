@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint
         if (__ballot(d) != 0 && lane_id() == 0) atomicOr(diff + r, 1u);
     }
     if (!fin.words) return;
-    // bind/3's answer per replica (k_bind_final's rule): 0 = equal (no-op), 1 = the merge
+    // bind/3's answer per replica (the non-strict rule: no violation): 0 = equal (no-op), 1 = the merge
     // inflates Value0 (written), 2 = it does not; then every word zeroed for the next call
     __shared__ uint32_t s_last;
     const uint32_t n = fin.R;
@@ -1147,19 +1147,6 @@ __global__ void k_linf_final(LV prev, LV cur, bool bcast, uint64_t R, const uint
         }
         out[r] = res ? 1 : 0;
     }
-}
-
-// bind/3's answer per replica, after the merge, is_inflation(Value0, Merged)'s probe and
-// `Value0 =:= Value`: 0 = equal (no-op), 1 = the merge inflates Value0 (written), 2 = it
-// does not (k_linf_final's non-strict rule folded in), and the merge's error flag copied
-// beside it, so one copy brings the whole answer back
-__global__ __launch_bounds__(256) void k_bind_final(uint64_t R, const uint32_t* flags,
-                                                    const uint32_t* diff, const uint32_t* err,
-                                                    uint8_t* status, uint32_t* err_out) {
-    for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < R;
-         r += (u64)gridDim.x * blockDim.x)
-        status[r] = !diff[r] ? 0 : ((flags[r] & kViolBit) ? 2 : 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *err_out = *err;
 }
 
 // ---------------------------------------------------------------- tiled producers
@@ -2176,8 +2163,8 @@ static char* bind_tables(laspj_ctx* ctx, uint64_t bytes, const char* what) {
 
 // the inflation kernels of prev -> cur into o (R bytes); clear_flag: start from a clean
 // error flag (the fused bind keeps the merge's bits and reads them with o)
-// final = false: the answer kernel is left to the caller, which gets the flag words
-// through *flag_words (list_bind's k_bind_final)
+// final = false: the answer is left to the caller, which gets the flag words through
+// *flag_words (list_bind: its equality pass's last block)
 static int inflation_launch(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
                             int strict, const RK& rk, uint8_t* o, bool clear_flag,
                             const char* what, uint32_t** zeroed_words = nullptr,
