@@ -193,6 +193,9 @@ int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 int      laspj_buf_create(laspj_ctx* ctx, uint64_t bytes, laspj_buf** out);
 int      laspj_buf_destroy(laspj_buf* buf);
 uint64_t laspj_buf_bytes(const laspj_buf* buf);
+/* the bytes are taken (src may be reused) on return; a small upload (<= 64 KiB) to a
+ * buffer whose device address was never handed out completes on the context's stream
+ * (before any later call's work), a larger one or one to an exported buffer before return */
 int      laspj_buf_upload(laspj_ctx* ctx, laspj_buf* buf, uint64_t offset,
                           const void* src, uint64_t bytes);
 int      laspj_buf_download(laspj_ctx* ctx, const laspj_buf* buf, uint64_t offset,

@@ -69,6 +69,12 @@ struct laspj_ctx {
     // NIF path rebuilds its image whenever a call registers new terms
     void* dstage = nullptr;
     uint64_t dstage_bytes = 0;
+    // pinned ring for small laspj_buf_upload calls: the bytes copied in and the copy
+    // enqueued without waiting (the stream orders every later use; the ring synchronises
+    // the stream when it wraps)
+    void* upring = nullptr;
+    uint64_t upring_at = 0;
+    static constexpr uint64_t kUpRing = 1 << 20, kUpSmall = 64 * 1024;
     static constexpr uint64_t kPinned = 64 * 1024;
     // released device blocks by size class (laspj::dev_alloc / dev_release): every kernel
     // runs on `stream`, so a block released after its last enqueued use can serve the

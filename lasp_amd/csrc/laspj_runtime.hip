@@ -291,6 +291,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
         if (ctx->dstage) hipHostFree(ctx->dstage);
+        if (ctx->upring) hipHostFree(ctx->upring);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -437,6 +438,32 @@ int laspj_buf_upload(laspj_ctx* ctx, laspj_buf* b, uint64_t off, const void* src
         return fail(ctx, LASPJ_E_RANGE, "buf_upload: range out of bounds");
     Guard g(ctx);
     if (!bytes) return LASPJ_OK;
+    if (bytes <= laspj_ctx::kUpSmall && !b->exported) {
+        // small and used on the context's stream only: staged in the pinned ring, the copy
+        // enqueued, no wait (every later kernel, copy or readback of the buffer is on the
+        // same stream, after it)
+        if (!ctx->upring) {
+            if (hipHostMalloc(&ctx->upring, laspj_ctx::kUpRing, hipHostMallocDefault) !=
+                hipSuccess) {
+                hipGetLastError();
+                ctx->upring = nullptr;
+            }
+        }
+        if (ctx->upring) {
+            const uint64_t need = (bytes + 255) & ~255ull;
+            if (ctx->upring_at + need > laspj_ctx::kUpRing) {
+                // the ring's earlier copies must be done before its bytes are rewritten
+                LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+                ctx->upring_at = 0;
+            }
+            char* slot = static_cast<char*>(ctx->upring) + ctx->upring_at;
+            std::memcpy(slot, src, bytes);
+            LJ_HIP(ctx, hipMemcpyAsync(static_cast<char*>(b->dev) + off, slot, bytes,
+                                       hipMemcpyHostToDevice, ctx->stream));
+            ctx->upring_at += need;
+            return LASPJ_OK;
+        }
+    }
     LJ_HIP(ctx, hipMemcpyAsync(static_cast<char*>(b->dev) + off, src, bytes,
                                hipMemcpyHostToDevice, ctx->stream));
     LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
