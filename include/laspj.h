@@ -266,7 +266,10 @@ int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
  *   cur[i] exactly; otherwise no dst may overlap any cur / val or another dst
  *   (LASPJ_E_INVAL).  inflation_many: out[i] = is_inflation (strict = 0) / is_strict_inflation
  *   (strict = 1) of prev[i] -> cur[i] per kind (lasp_lattice.erl:137-161, 169-179,
- *   212-253, 273-275).  Both return after the work has completed. */
+ *   212-253, 273-275).  inflation_many returns after the work has completed; bind_many
+ *   once it is enqueued on the context's stream (every later call of the context sees
+ *   its results; it waits for the work itself when a batch's or the status buffer's
+ *   device address was handed out, or when there are many items). */
 int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
                           const laspj_batch* const* cur, const laspj_batch* const* val,
                           laspj_buf* status);

@@ -146,6 +146,9 @@ hipError_t readback(laspj_ctx* ctx, const ReadPiece* pieces, int n);
 constexpr uint64_t kCacheMax = 256ull << 20;      // largest cached block
 constexpr uint64_t kCacheCap = 2ull << 30;        // bytes a context keeps cached
 hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out);
+// src copied into the context's pinned ring for a stream-ordered host -> device copy with
+// no wait (<= 64 KiB; null: not staged).  Call with ctx->mu held.
+const void* stage_small(laspj_ctx* ctx, const void* src, uint64_t bytes);
 // hipMalloc that gives the context's cached blocks back and retries once when it fails
 // (every long-lived scratch allocation goes through it)
 hipError_t dev_malloc(laspj_ctx* ctx, void** out, uint64_t bytes);

@@ -272,7 +272,12 @@ int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "bind_many: scratch");
     auto* dev_items = reinterpret_cast<MItem*>(base);
     auto* st = reinterpret_cast<uint32_t*>(base + db);
-    LJ_HIP(ctx, hipMemcpyAsync(dev_items, items.data(), db, hipMemcpyHostToDevice, ctx->stream));
+    // the descriptors staged in the pinned ring when they are few: then nothing here has to
+    // wait — every later use of the batches and of the status buffer is on the context's
+    // stream — unless a buffer's device address was handed out (other streams may read it)
+    const void* staged = laspj::stage_small(ctx, items.data(), db);
+    LJ_HIP(ctx, hipMemcpyAsync(dev_items, staged ? staged : items.data(), db,
+                               hipMemcpyHostToDevice, ctx->stream));
     LJ_HIP(ctx, hipMemsetAsync(st, 0, sb, ctx->stream));
     hipLaunchKernelGGL(k_bind_many, dim3(grid_of(ctx, nseg)), dim3(256), 0, ctx->stream,
                        dev_items, n, nseg, st);
@@ -281,8 +286,10 @@ int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
     hipLaunchKernelGGL(k_many_status, dim3(fg), dim3(256), 0, ctx->stream, st,
                        static_cast<uint8_t*>(status->dev), n);
     LJ_LAUNCHED(ctx);
-    // the descriptors live in shared scratch: finish before the next call may reuse it
-    LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    bool exported = !staged || status->exported;
+    for (uint32_t i = 0; i < n && !exported; ++i)
+        exported = dst[i]->exported || cur[i]->exported || val[i]->exported;
+    if (exported) LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return LASPJ_OK;
 }
 

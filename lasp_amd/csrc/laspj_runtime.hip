@@ -430,6 +430,36 @@ int laspj_buf_device_ptr(const laspj_buf* b, void** out) {
     return LASPJ_OK;
 }
 
+}  // extern "C"
+
+namespace laspj {
+// a copy of src[0, bytes) in the context's pinned ring, to be copied to the device on its
+// stream; null when it does not fit (bytes > kUpSmall) or the ring cannot be allocated.
+// Call with ctx->mu held.
+const void* stage_small(laspj_ctx* ctx, const void* src, uint64_t bytes) {
+    if (bytes > laspj_ctx::kUpSmall) return nullptr;
+    if (!ctx->upring) {
+        if (hipHostMalloc(&ctx->upring, laspj_ctx::kUpRing, hipHostMallocDefault) != hipSuccess) {
+            hipGetLastError();
+            ctx->upring = nullptr;
+            return nullptr;
+        }
+    }
+    const uint64_t need = (bytes + 255) & ~255ull;
+    if (ctx->upring_at + need > laspj_ctx::kUpRing) {
+        // the ring's earlier copies must be done before its bytes are rewritten
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+        ctx->upring_at = 0;
+    }
+    char* slot = static_cast<char*>(ctx->upring) + ctx->upring_at;
+    std::memcpy(slot, src, bytes);
+    ctx->upring_at += need;
+    return slot;
+}
+}  // namespace laspj
+
+extern "C" {
+
 int laspj_buf_upload(laspj_ctx* ctx, laspj_buf* b, uint64_t off, const void* src,
                      uint64_t bytes) {
     if (!ctx || !b || b->ctx != ctx || (!src && bytes))
@@ -442,25 +472,9 @@ int laspj_buf_upload(laspj_ctx* ctx, laspj_buf* b, uint64_t off, const void* src
         // small and used on the context's stream only: staged in the pinned ring, the copy
         // enqueued, no wait (every later kernel, copy or readback of the buffer is on the
         // same stream, after it)
-        if (!ctx->upring) {
-            if (hipHostMalloc(&ctx->upring, laspj_ctx::kUpRing, hipHostMallocDefault) !=
-                hipSuccess) {
-                hipGetLastError();
-                ctx->upring = nullptr;
-            }
-        }
-        if (ctx->upring) {
-            const uint64_t need = (bytes + 255) & ~255ull;
-            if (ctx->upring_at + need > laspj_ctx::kUpRing) {
-                // the ring's earlier copies must be done before its bytes are rewritten
-                LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
-                ctx->upring_at = 0;
-            }
-            char* slot = static_cast<char*>(ctx->upring) + ctx->upring_at;
-            std::memcpy(slot, src, bytes);
+        if (const void* slot = laspj::stage_small(ctx, src, bytes)) {
             LJ_HIP(ctx, hipMemcpyAsync(static_cast<char*>(b->dev) + off, slot, bytes,
                                        hipMemcpyHostToDevice, ctx->stream));
-            ctx->upring_at += need;
             return LASPJ_OK;
         }
     }
