@@ -171,22 +171,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         multiple of 256)                               */
 #define LASPJ_TUNE_LIST_WALK    10   /* list merges whose keys descend somewhere: 0 = the
                                         run-jumping walk, 1 = one step per element      */
-#define LASPJ_TUNE_NIF_PIECE    11   /* NIF entry points: bytes staged into pinned memory
-                                        per host -> device copy or pull (0 = one copy per
-                                        call up to 64 MiB, or pulls of 512 KiB while the
-                                        host stages the next; a multiple of 4096)       */
-#define LASPJ_TUNE_NIF_HOST     12   /* NIF entry points' pinned staging (allocated from
-                                        the next growth on): 0 = default, 1 =
-                                        non-coherent, 2 = coherent                      */
-#define LASPJ_TUNE_NIF_DIRECT   13   /* NIF entry points' operand and answer traffic
-                                        (default 6): 0 =
-                                        copies to and from device memory, 1 = the decoder
-                                        reads the operands from pinned host memory, 2 = the
-                                        answer's kernels write it into pinned host memory,
-                                        3 = both; + 4: a kernel on the context's stream
-                                        pulls the operands to the device (in place of
-                                        the copy and of bit 1).  The staging is coherent
-                                        from the first call with any bit set            */
+#define LASPJ_TUNE_NIF_PASSES   14   /* NIF entry points: device passes a call may take
+                                        (0 = default 6; registering unseen terms, a grown
+                                        answer area and a serial re-decode take one each).
+                                        A call still unresolved after them answers
+                                        LASPJ_NIF_FALLBACK — for tests of that guard      */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */
@@ -410,10 +399,13 @@ int laspj_orset_gather_inflation_keyed(laspj_ctx* ctx, laspj_batch* dst, const l
 /* merge/2 — lasp_gset.erl:99-101 (ordsets:union on canonical sets = OR) */
 int laspj_gset_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                     const laspj_batch* b);
+/* foldl(merge, new(), Replies) over groups of `group` consecutive replicas —
+ * lasp_update_fsm.erl:189-192 / lasp_bind_fsm.erl:185-188, as laspj_orset_reduce */
 int laspj_gset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                       uint32_t group);
 /* stat(element_count) — lasp_gset.erl:135-136: one uint64 per replica */
 int laspj_gset_stats(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_counts);
+/* equal/2 — lasp_gset.erl:103-105 (GSet1 == GSet2): out[i] = (a[i] == b[i]) as one byte */
 int laspj_gset_equal(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
                      laspj_buf* out);
 /* is_inflation — lasp_lattice.erl:137-140; strict — :212-215 */
@@ -536,6 +528,14 @@ int laspj_gset_etf_write(laspj_ctx* ctx, const laspj_batch* batch, const laspj_e
 #define LASPJ_DEC_UNKNOWN_TERM        4  /* an element or token outside the dictionary, or
                                             out of term order (not an orddict)           */
 #define LASPJ_DEC_UNREPRESENTABLE     5  /* an element with no tokens or more than 64     */
+#define LASPJ_DEC_EQUAL_TERMS         6  /* host dictionary only: a term `==` to one that
+                                            already holds a slot under another image (1 vs
+                                            1.0, {a, 1} vs {a, 1.0}, an atom in another
+                                            encoding) — orddict:merge / ordsets:union treat
+                                            them as one key, separate slots would not; the
+                                            NIF hands such operands to the reference's
+                                            clause (lasp_orset.erl:128-138, SURVEY.md
+                                            Appendix A)                                   */
 int laspj_orset_etf_read(laspj_ctx* ctx, laspj_batch* batch, const laspj_etf_dict* d,
                          int tag, int vers, const laspj_buf* payload,
                          const laspj_buf* offsets, laspj_buf* status);
@@ -832,19 +832,97 @@ int laspj_orset_etf_equal(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const u
 int laspj_orset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
                               const uint8_t* cur, uint64_t nc, int strict, int32_t* result,
                               int32_t* verdict);
+/* lasp_gset (lasp_gset.erl:39-43) at the same boundary, over the context's G-Set
+ * dictionary (payloads: 131 + an ordset, LIST_EXT / STRING_EXT / NIL_EXT; verdicts as
+ * above, FALLBACK for a list that is not an ordset in term order):
+ * merge/2 — lasp_gset.erl:99-101 (ordsets:union): *out = term_to_binary(merge(A, B)) */
+int laspj_gset_etf_merge(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                         uint64_t nb, const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+int laspj_gset_etf_merge_many(laspj_ctx* ctx, uint32_t n, const uint8_t* const* a,
+                              const uint64_t* na, const uint8_t* const* b, const uint64_t* nb,
+                              const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* value/1 — lasp_gset.erl:74-76 (ordsets:to_list/1, the identity): *out = s itself */
+int laspj_gset_etf_value(laspj_ctx* ctx, const uint8_t* s, uint64_t ns, const uint8_t** out,
+                         uint64_t* out_len, int32_t* verdict);
+/* equal/2 — lasp_gset.erl:103-105 (GSet1 == GSet2): *result 1 / 0 */
+int laspj_gset_etf_equal(laspj_ctx* ctx, const uint8_t* a, uint64_t na, const uint8_t* b,
+                         uint64_t nb, int32_t* result, int32_t* verdict);
+/* is_inflation (strict = 0) / is_strict_inflation (strict = 1) — lasp_lattice.erl:137-140
+ * (sets:is_subset) / 212-215 (and lists:usort =/=); threshold_met(lasp_gset, V, T) of
+ * lasp_lattice.erl:62-65 is inflation(T, V) */
+int laspj_gset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
+                             const uint8_t* cur, uint64_t nc, int strict, int32_t* result,
+                             int32_t* verdict);
+
+/* ------------------------------------------------------------------ resident variables */
+/* `#dv.value` (include/lasp.hrl:60-63) kept on the device between calls.  A variable is
+ * one OR-Set or G-Set value over its context's dictionary of that kind; lasp_core:bind/3
+ * (lasp_core.erl:291-312) then ships only the incoming `Value` — its image is decoded on
+ * the device, `Value0 =:= Value` and merge/2 decided against the resident cells by one
+ * kernel, and only the status comes back; the value is encoded when it is read.
+ *
+ * Ownership: the NIF wraps a laspj_var in an enif_alloc_resource
+ * whose destructor calls laspj_var_destroy; the resource keeps its context's resource
+ * alive (enif_keep_resource), since a variable belongs to one context (its dictionary and
+ * device memory) and every call on it is serialised by that context, from any scheduler.
+ *
+ * A value the columnar form does not hold (verdict FALLBACK of laspj_var_etf_write) is
+ * kept as its image on the host: laspj_var_etf_read answers that image, and bind /
+ * threshold / value answer FALLBACK — the NIF runs the reference's clause over the read
+ * term and stores the outcome with laspj_var_etf_write.  A dictionary reset (an element
+ * whose 64 token slots are used up) writes every resident variable of the context out to
+ * its image first; each is decoded again on its next call. */
+typedef struct laspj_var laspj_var;
+/* declare/3 (lasp_core.erl:208-218): a variable holding Type:new() = [] (kind
+ * LASPJ_KIND_ORSET or LASPJ_KIND_GSET) */
+int laspj_var_create(laspj_ctx* ctx, int32_t kind, laspj_var** out);
+int laspj_var_destroy(laspj_var* var);
+#define LASPJ_BIND_NOOP    0
+#define LASPJ_BIND_WRITTEN 1
+/* bind/3 (lasp_core.erl:291-312): status LASPJ_BIND_NOOP when `Value0 =:= Value`
+ * (:294-296), LASPJ_BIND_WRITTEN when Value0 := merge(Value0, Value) was written (a
+ * canonical merge always inflates Value0, :300-304).  verdict FALLBACK: the variable is
+ * unchanged and the NIF binds in Erlang (as above). */
+int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t* status,
+                       int32_t* verdict);
+/* n binds (lasp_core.erl:291-312) of distinct variables of one kind and context in one
+ * device pass (a vnode's queued binds, lasp_vnode.erl:213-237) */
+int laspj_var_etf_bind_many(laspj_ctx* ctx, uint32_t n, laspj_var* const* vars,
+                            const uint8_t* const* values, const uint64_t* lens, int32_t* status,
+                            int32_t* verdict);
+/* write/4 (lasp_core.erl:839-844): the variable := value (verdict FALLBACK: held as the
+ * image on the host) */
+int laspj_var_etf_write(laspj_var* var, const uint8_t* value, uint64_t n, int32_t* verdict);
+/* #dv.value as term_to_binary/1 (*out valid until the context's next call) */
+int laspj_var_etf_read(laspj_var* var, const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* Type:value(#dv.value) — lasp_orset.erl:67-73 / lasp_gset.erl:74-76 */
+int laspj_var_etf_value(laspj_var* var, const uint8_t** out, uint64_t* out_len,
+                        int32_t* verdict);
+/* threshold_met(Type, #dv.value, Threshold) — lasp_lattice.erl:62-75, as read/6 asks it
+ * (lasp_core.erl:331-364): is_inflation (strict = 0, Threshold) or is_strict_inflation
+ * (strict = 1, {strict, Threshold}) of Threshold -> the variable's value */
+int laspj_var_etf_threshold(laspj_var* var, const uint8_t* threshold, uint64_t n, int strict,
+                            int32_t* result, int32_t* verdict);
+/* 1 when the value (#dv.value, include/lasp.hrl:60-63) is on the device, 0 when it is
+ * held as an image */
+int laspj_var_resident(const laspj_var* var, int32_t* resident);
+
 /* counters of this context's NIF path: [0] calls, [1] device passes, [2] dictionary
  * registrations, [3] dictionary resets, [4] device image rebuilds, [5] host-encoded passes
- * (token images of mixed lengths), [6] FALLBACK verdicts, [7] dictionary elements; host
- * nanoseconds summed over device passes: [8] staging + enqueueing, [9] waiting for the
- * device, [10] reading the answers after it, [11] the part of [8] spent copying operands
- * into pinned memory, [12] registering operands' terms in the host dictionary, [13]
- * rebuilding or patching the device images; [14] device image patches (registrations
+ * (token images of mixed lengths), [6] FALLBACK verdicts, [7] dictionary elements (both
+ * kinds); host nanoseconds summed over device passes: [8] staging + enqueueing, [9] waiting
+ * for the device, [10] reading the answers after it, [11] the part of [8] spent copying
+ * operands into pinned memory, [12] registering operands' terms in the host dictionary,
+ * [13] rebuilding or patching the device images; [14] device image patches (registrations
  * that only added tokens to known elements, rewritten in place instead of rebuilt); [15]
  * merge passes run again because a segment chain checked beside the join broke before
- * any failing segment (a false element-header match: only a serial decode can judge) */
-#define LASPJ_NIF_STATS 16
+ * any failing segment (a false element-header match: only a serial decode can judge);
+ * [16] resident variables written out to their images by a dictionary reset; [17]
+ * variables decoded back onto the device after one */
+#define LASPJ_NIF_STATS 18
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
-/* drop the context's dictionary (its memory; the next call registers afresh) */
+/* drop the context's dictionaries (their memory; the next call registers afresh;
+ * resident variables are written out to their images and decoded again when used) */
 int laspj_nif_reset(laspj_ctx* ctx);
 
 /* ------------------------------------------------------------------ timing */

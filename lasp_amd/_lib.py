@@ -28,7 +28,7 @@ LIST_COMPOUND = 1 << 62      # token item: [Tx, Ty] of tokens (bits 31-61, 0-30)
 LIST_REMOVED = 1 << 63       # token item: the {Token, true} flag
 # from_binary statuses (laspj_orset_etf_read)
 DEC_OK, DEC_INVALID_BINARY, DEC_UNSUPPORTED_VERSION, DEC_MALFORMED, DEC_UNKNOWN_TERM, \
-    DEC_UNREPRESENTABLE = 0, 1, 2, 3, 4, 5
+    DEC_UNREPRESENTABLE, DEC_EQUAL_TERMS = 0, 1, 2, 3, 4, 5, 6
 OP_ADD, OP_REMOVE, OP_INSERT = 1, 2, 3
 OP_FLAG_NEW_CALL = 1
 OPST_APPLIED, OPST_NOT_PRESENT, OPST_ROLLED_BACK, OPST_KEY_EXISTS = 0, 1, 2, 3
@@ -39,11 +39,9 @@ TUNE_PRODUCT_COLS = 7
 TUNE_ETF_READ = 8
 TUNE_ETF_SEG = 9
 TUNE_LIST_WALK = 10
-TUNE_NIF_PIECE = 11
-TUNE_NIF_HOST = 12
-TUNE_NIF_DIRECT = 13
+TUNE_NIF_PASSES = 14
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
-NIF_STATS = 16
+NIF_STATS = 18
 
 
 class LaspjUnavailable(RuntimeError):
@@ -218,6 +216,24 @@ SIGNATURES = {
                                   C.POINTER(C.c_int32)]),
     "laspj_orset_etf_inflation": (i, [vp, vp, u64, vp, u64, i, C.POINTER(C.c_int32),
                                       C.POINTER(C.c_int32)]),
+    "laspj_gset_etf_merge": (i, [vp, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                 C.POINTER(C.c_int32)]),
+    "laspj_gset_etf_merge_many": (i, [vp, u32, vp, vp, vp, vp, vp, vp, vp]),
+    "laspj_gset_etf_value": (i, [vp, vp, u64, vpp, C.POINTER(u64), C.POINTER(C.c_int32)]),
+    "laspj_gset_etf_equal": (i, [vp, vp, u64, vp, u64, C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_int32)]),
+    "laspj_gset_etf_inflation": (i, [vp, vp, u64, vp, u64, i, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int32)]),
+    "laspj_var_create": (i, [vp, C.c_int32, vpp]),
+    "laspj_var_destroy": (i, [vp]),
+    "laspj_var_etf_bind": (i, [vp, vp, u64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "laspj_var_etf_bind_many": (i, [vp, u32, vp, vp, vp, vp, vp]),
+    "laspj_var_etf_write": (i, [vp, vp, u64, C.POINTER(C.c_int32)]),
+    "laspj_var_etf_read": (i, [vp, vpp, C.POINTER(u64), C.POINTER(C.c_int32)]),
+    "laspj_var_etf_value": (i, [vp, vpp, C.POINTER(u64), C.POINTER(C.c_int32)]),
+    "laspj_var_etf_threshold": (i, [vp, vp, u64, i, C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int32)]),
+    "laspj_var_resident": (i, [vp, C.POINTER(C.c_int32)]),
     "laspj_nif_stats": (i, [vp, vp, u32]),
     "laspj_nif_reset": (i, [vp]),
     "laspj_event_create": (i, [vp, vpp]),

@@ -21,7 +21,7 @@ from typing import Dict, Iterable, List, Sequence
 
 import numpy as np
 
-from .terms import hkey, term_cmp, term_key
+from .terms import hkey, same_term, term_cmp, term_key
 
 TOKEN_SLOTS = 64
 
@@ -32,6 +32,13 @@ class NonCanonical(ValueError):
 
 class CapacityError(ValueError):
     """An element needs more than 64 token slots, or the batch has too few slots."""
+
+
+class EqualTerms(CapacityError):
+    """A term `==` to one that holds a slot but not `=:=` to it (1 and 1.0, {a, 1} and
+    {a, 1.0}): orddict:merge / ordsets:union treat them as one key,
+    so neither "first seen wins" nor a second slot gives the reference's answers — the
+    value is not representable here (the store raises Unsupported)."""
 
 
 class _Dict:
@@ -48,6 +55,8 @@ class _Dict:
     def slot(self, term, create: bool = True) -> int:
         k = hkey(term)
         s = self.index.get(k)
+        if s is not None and not same_term(self.terms[s], term):
+            raise EqualTerms(f"{term!r} == {self.terms[s]!r} but is another term")
         if s is None:
             if not create:
                 return -1
@@ -117,6 +126,8 @@ class Domain:
             if len(td.terms) != n:
                 self.tok_log.append(eslot)
             return s
+        except EqualTerms:
+            raise
         except CapacityError as e:
             raise CapacityError(
                 f"element {self.elements.terms[eslot]!r} has more than {TOKEN_SLOTS} tokens") from e

@@ -4762,6 +4762,22 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
     return LASPJ_OK;
 }
 
+int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+                      const uint8_t* payload, const u64* offs, int32_t* status, bool clear) {
+    const uint64_t R = b->replicas;
+    if (clear)
+        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, R * b->words_per_replica * 8ull, ctx->stream));
+    const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
+                      d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
+    hipLaunchKernelGGL(k_gset_etf_read,
+                       dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 64))),
+                       dim3(64), 0, ctx->stream, payload, offs, R, tabs, tag, vers,
+                       reinterpret_cast<u64*>(b->dev), b->words_per_replica, status,
+                       (const uint32_t*)nullptr);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
                      int tag, u64* offsets, uint32_t* flag, const u64** chunks) {
     const uint64_t R = b->replicas;

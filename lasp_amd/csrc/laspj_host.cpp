@@ -369,6 +369,127 @@ int term_cmp(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, bool* ok)
     return 0;
 }
 
+// ------------------------------------------------------------------ `==` classes
+
+// A serialisation of the term at p in which two terms are byte-equal iff they compare
+// equal (term_cmp == 0, Erlang's `==`): numbers by value (an integral float as the
+// integer it equals, exactly as cmp_int_float compares them; -0.0 as 0), integers
+// without regard to their encoding (SMALL_INTEGER / INTEGER / SMALL_BIG / LARGE_BIG),
+// atoms by name whatever the encoding, STRING_EXT and LIST_EXT alike, [] however it is
+// written.  The dictionary keys slots by image bytes, so `1` and `1.0` (or {a, 1} and
+// {a, 1.0}) would take two slots where orddict:merge / ordsets:union see one key
+// (SURVEY.md Appendix A): it hashes this form to find such pairs and refuses the second
+// (LASPJ_DEC_EQUAL_TERMS).  False: a term outside this path.
+bool canon(const uint8_t* p, size_t n, std::string* out, int depth = 0) {
+    if (!n || depth > 64) return false;
+    auto put32 = [&](uint64_t v) {
+        for (int k = 3; k >= 0; --k) out->push_back((char)((v >> (8 * k)) & 0xFF));
+    };
+    auto put_int = [&](int sign, const uint8_t* mag, size_t len) {   // mag little-endian
+        while (len && mag[len - 1] == 0) --len;
+        out->push_back('I');
+        out->push_back(len == 0 ? 0 : (sign < 0 ? '-' : '+'));
+        put32(len);
+        out->append((const char*)mag, len);
+    };
+    switch (term_class(p[0])) {
+        case 0: {
+            if (p[0] == kSmallInt || p[0] == kInt) {
+                const int64_t v = p[0] == kSmallInt ? p[1] : (int32_t)be32(p + 1);
+                uint64_t m = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+                uint8_t mag[8];
+                for (int k = 0; k < 8; ++k) mag[k] = (uint8_t)(m >> (8 * k));
+                put_int(v < 0 ? -1 : 1, mag, 8);
+                return true;
+            }
+            Num x = read_num(p);
+            if (!x.is_float) {
+                put_int(x.sign, x.mag.data(), x.mag.size());
+                return true;
+            }
+            const double f = x.f;
+            if (!std::isfinite(f)) return false;
+            if (f != std::trunc(f)) {
+                uint64_t b;
+                memcpy(&b, &f, 8);
+                out->push_back('F');
+                for (int k = 7; k >= 0; --k) out->push_back((char)((b >> (8 * k)) & 0xFF));
+                return true;
+            }
+            // an integral double: |f| = mant 2^(ex-53), the integer's magnitude bytes
+            int ex = 0;
+            const double m = std::frexp(std::fabs(f), &ex);
+            std::vector<uint8_t> mag((size_t)std::max(ex, 0) / 8 + 9, 0);
+            if (ex > 0) {
+                const uint64_t mant = (uint64_t)std::ldexp(m, 53);
+                const int sh = ex - 53;
+                if (sh >= 0) {
+                    for (int k = 0; k < 8; ++k) {
+                        const unsigned v = (unsigned)((mant >> (8 * k)) & 0xFF) << (sh % 8);
+                        const size_t at = (size_t)(k + sh / 8);
+                        if (at < mag.size()) mag[at] |= (uint8_t)v;
+                        if (at + 1 < mag.size()) mag[at + 1] |= (uint8_t)(v >> 8);
+                    }
+                } else {
+                    const uint64_t iv = mant >> (-sh);
+                    for (int k = 0; k < 8; ++k) mag[k] = (uint8_t)(iv >> (8 * k));
+                }
+            }
+            put_int(f < 0 ? -1 : 1, mag.data(), mag.size());
+            return true;
+        }
+        case 1: {
+            const std::string a = atom_name(p);
+            out->push_back('A');
+            put32(a.size());
+            out->append(a);
+            return true;
+        }
+        case 6: {
+            const bool small = p[0] == kSmallTuple;
+            const uint64_t ar = small ? p[1] : be32(p + 1);
+            size_t off = small ? 2 : 5;
+            out->push_back('T');
+            put32(ar);
+            for (uint64_t k = 0; k < ar; ++k) {
+                const size_t l = term_len(p + off, n - off);
+                if (!l || !canon(p + off, l, out, depth + 1)) return false;
+                off += l;
+            }
+            return true;
+        }
+        case 8: out->push_back('N'); return true;
+        case 9: {
+            // [] written as an empty STRING_EXT / LIST_EXT is still []
+            ListIt it(p, n);
+            if (it.count == 0 && (it.str || (it.tail() && it.tail()[0] == kNil))) {
+                out->push_back('N');
+                return true;
+            }
+            out->push_back('L');
+            put32(it.count);
+            size_t el;
+            while (const uint8_t* e = it.next(&el))
+                if (!el || !canon(e, el, out, depth + 1)) return false;
+            const uint8_t* t = it.tail();
+            if (!t) {
+                out->push_back('N');
+                return true;
+            }
+            const size_t tl = term_len(t, n - (size_t)(t - p));
+            return tl && canon(t, tl, out, depth + 1);
+        }
+        case 10: {
+            const uint32_t l = be32(p + 1);
+            out->push_back('B');
+            put32(l);
+            out->append((const char*)p + 5, l);
+            return true;
+        }
+    }
+    return false;
+}
+
 // ------------------------------------------------------------------ dictionary
 
 // images are stored once (a deque keeps their addresses); lookups hash the payload's
@@ -410,6 +531,17 @@ struct Table {
             if (e.h == h && e.owner == owner && e.key == key) return &e;
         }
     }
+    // the first entry with this hash and owner for which same(key) holds
+    template <class Same>
+    const Ent* find_if(uint64_t h, uint32_t owner, Same same) const {
+        if (idx.empty()) return nullptr;
+        for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+            const uint32_t k = idx[i];
+            if (!k) return nullptr;
+            const Ent& e = ents[k - 1];
+            if (e.h == h && e.owner == owner && same(e.key)) return &e;
+        }
+    }
     void grow() {
         const uint64_t cap = idx.empty() ? 1024 : idx.size() * 2;
         idx.assign(cap, 0);
@@ -449,6 +581,11 @@ struct Dict {
     std::vector<std::string_view> elems;
     std::vector<std::vector<std::string_view>> toks;
     Table elem_slot, tok_slot;
+    // the `==` classes of the registered images (hash of canon(), owner as in the slot
+    // tables; the key is the registered image, re-compared with term_cmp on a hash hit):
+    // one image per class, so a slot never stands for half of an orddict key
+    Table elem_eq, tok_eq;
+    std::string scratch;
     // registrations of the payload being added (-1: an element, else the element slot of
     // a token), undone in reverse when the payload fails: binary_to_term/1 would have
     // rejected it whole, so none of its terms may take a slot
@@ -467,10 +604,12 @@ struct Dict {
         for (size_t j = journal.size(); j-- > 0;) {
             if (journal[j] < 0) {
                 elem_slot.pop_last();
+                elem_eq.pop_last();
                 elems.pop_back();
                 toks.pop_back();
             } else {
                 tok_slot.pop_last();
+                tok_eq.pop_last();
                 toks[(size_t)journal[j]].pop_back();
             }
             store.pop_back();
@@ -604,6 +743,14 @@ int walk_gset(const uint8_t* t, size_t tn, OnElem on_elem) {
     return LASPJ_DEC_OK;
 }
 
+// the `==` class hash of an image (canon), or false for a term outside this path
+bool eq_hash(Dict* d, const uint8_t* k, size_t kl, uint64_t seed, uint64_t* h) {
+    d->scratch.clear();
+    if (!canon(k, kl, &d->scratch)) return false;
+    *h = hash_bytes((const uint8_t*)d->scratch.data(), d->scratch.size(), seed);
+    return true;
+}
+
 int reg_elem(Dict* d, const uint8_t* k, size_t kl, uint32_t* slot) {
     const int64_t f = d->elem(k, kl);
     if (f >= 0) {
@@ -613,10 +760,19 @@ int reg_elem(Dict* d, const uint8_t* k, size_t kl, uint32_t* slot) {
     bool ok = true;
     term_cmp(k, kl, k, kl, &ok);              // the comparator must handle the term
     if (!ok) return LASPJ_DEC_MALFORMED;
+    uint64_t he = 0;
+    if (!eq_hash(d, k, kl, kElemSeed, &he)) return LASPJ_DEC_MALFORMED;
+    // another image of an `==`-equal term already holds a slot (1 vs 1.0)
+    if (d->elem_eq.find_if(he, 0, [&](std::string_view o) {
+            bool ok2 = true;
+            return term_cmp(k, kl, (const uint8_t*)o.data(), o.size(), &ok2) == 0 && ok2;
+        }))
+        return LASPJ_DEC_EQUAL_TERMS;
     if (d->elems.size() >= (1u << 24)) return LASPJ_DEC_UNREPRESENTABLE;
     *slot = (uint32_t)d->elems.size();
     std::string_view v = d->keep(k, kl);
     d->elem_slot.insert(hash_bytes(k, kl, kElemSeed), 0, v, *slot);
+    d->elem_eq.insert(he, 0, v, *slot);
     d->elems.push_back(v);
     d->toks.emplace_back();
     d->journal.push_back(-1);
@@ -632,10 +788,18 @@ int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
     bool ok = true;
     term_cmp(t, tl, t, tl, &ok);
     if (!ok) return LASPJ_DEC_MALFORMED;
+    uint64_t ht = 0;
+    if (!eq_hash(d, t, tl, 0x9E3779B97F4A7C15ull * (es + 1), &ht)) return LASPJ_DEC_MALFORMED;
+    if (d->tok_eq.find_if(ht, es, [&](std::string_view o) {
+            bool ok2 = true;
+            return term_cmp(t, tl, (const uint8_t*)o.data(), o.size(), &ok2) == 0 && ok2;
+        }))
+        return LASPJ_DEC_EQUAL_TERMS;
     if (d->toks[es].size() >= 64) return LASPJ_DEC_UNREPRESENTABLE;
     *slot = (uint8_t)d->toks[es].size();
     std::string_view v = d->keep(t, tl);
     d->tok_slot.insert(tok_hash(es, t, tl), es, v, *slot);
+    d->tok_eq.insert(ht, es, v, *slot);
     d->toks[es].push_back(v);
     d->journal.push_back((int64_t)es);
     return LASPJ_DEC_OK;

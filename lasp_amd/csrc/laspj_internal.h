@@ -35,9 +35,7 @@ struct laspj_ctx {
     int64_t tune_product_rows = 0;
     int64_t tune_product_cols = 0;
     int64_t tune_list_walk = 0;
-    int64_t tune_nif_piece = 0;
-    int64_t tune_nif_host = 0;
-    int64_t tune_nif_direct = 6;     // pull kernel in, kernels write the answer out
+    int64_t tune_nif_passes = 0;     // NIF device passes per call (0: the default)
     // device scratch for apply_ops (grown on demand)
     void* scratch = nullptr;
     uint64_t scratch_bytes = 0;
@@ -282,6 +280,11 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                      const unsigned long long* offsets, const EtfReadPlan& plan,
                      const uint32_t* segbase, int32_t* status, bool clear,
                      uint32_t* redo_zeroed, ChainJob* defer = nullptr);
+// lasp_gset:from_binary/1's decoder (k_gset_etf_read: one wave per payload), enqueue only;
+// offsets / status are device addresses; clear: zero the batch first
+int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
+                      const uint8_t* payload, const unsigned long long* offsets, int32_t* status,
+                      bool clear);
 // merge/2 of a[i] and b[i] into z fused with z's size pass (and a, b cleared behind it),
 // when etf_merge_fused(ctx, R, E) holds; ticket: one zeroed word (left zero)
 bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E);

@@ -359,19 +359,9 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             if (value < 0 || value > 1) return fail(ctx, LASPJ_E_INVAL, "tuning: list walk 0 or 1");
             ctx->tune_list_walk = value;
             return LASPJ_OK;
-        case LASPJ_TUNE_NIF_PIECE:
-            if (value < 0 || value > (1ll << 30) || (value % 4096) != 0)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: NIF staging piece must be 0 or a "
-                            "multiple of 4096");
-            ctx->tune_nif_piece = value;
-            return LASPJ_OK;
-        case LASPJ_TUNE_NIF_HOST:
-            if (value < 0 || value > 2) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF host 0..2");
-            ctx->tune_nif_host = value;
-            return LASPJ_OK;
-        case LASPJ_TUNE_NIF_DIRECT:
-            if (value < 0 || value > 7) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF direct 0..7");
-            ctx->tune_nif_direct = value;
+        case LASPJ_TUNE_NIF_PASSES:
+            if (value < 0 || value > 16) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF passes 0..16");
+            ctx->tune_nif_passes = value;
             return LASPJ_OK;
 
         default:

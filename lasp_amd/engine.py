@@ -109,8 +109,11 @@ class Context:
     # this context's own dictionary.  Each returns (verdict, answer); answer is None on
     # NIF_FALLBACK (the NIF would run the reference's Erlang clause).
 
-    def nif_merge_many(self, pairs):
-        """lasp_orset:merge/2 over many (A, B) image pairs: [(verdict, image)]."""
+    def nif_merge_many(self, pairs, kind: str = "orset"):
+        """lasp_orset:merge/2 (kind "gset": lasp_gset:merge/2) over many (A, B) image
+        pairs: [(verdict, image)]."""
+        fn = self.L.laspj_gset_etf_merge_many if kind == "gset" else \
+            self.L.laspj_orset_etf_merge_many
         n = len(pairs)
         if n == 0:
             return []
@@ -122,35 +125,53 @@ class Context:
         out = (C.c_void_p * n)()
         olen = (C.c_uint64 * n)()
         verd = (C.c_int32 * n)()
-        check(self.L.laspj_orset_etf_merge_many(self.h, n, pa, na, pb, nb, out, olen, verd),
-              self.h)
+        check(fn(self.h, n, pa, na, pb, nb, out, olen, verd), self.h)
         return [(int(verd[k]), C.string_at(out[k], olen[k]) if verd[k] == 0 else None)
                 for k in range(n)]
 
-    def nif_merge(self, a: bytes, b: bytes):
-        return self.nif_merge_many([(a, b)])[0]
+    def nif_merge(self, a: bytes, b: bytes, kind: str = "orset"):
+        return self.nif_merge_many([(a, b)], kind)[0]
 
-    def nif_value(self, s: bytes):
+    def nif_value(self, s: bytes, kind: str = "orset"):
+        fn = self.L.laspj_gset_etf_value if kind == "gset" else self.L.laspj_orset_etf_value
         out, olen, verd = C.c_void_p(), C.c_uint64(), C.c_int32()
         s = bytes(s)
-        check(self.L.laspj_orset_etf_value(self.h, s, len(s), C.byref(out), C.byref(olen),
-                                           C.byref(verd)), self.h)
+        check(fn(self.h, s, len(s), C.byref(out), C.byref(olen), C.byref(verd)), self.h)
         return int(verd.value), (C.string_at(out, olen.value) if verd.value == 0 else None)
 
-    def nif_equal(self, a: bytes, b: bytes):
+    def nif_equal(self, a: bytes, b: bytes, kind: str = "orset"):
+        fn = self.L.laspj_gset_etf_equal if kind == "gset" else self.L.laspj_orset_etf_equal
         res, verd = C.c_int32(), C.c_int32()
         a, b = bytes(a), bytes(b)
-        check(self.L.laspj_orset_etf_equal(self.h, a, len(a), b, len(b), C.byref(res),
-                                           C.byref(verd)), self.h)
+        check(fn(self.h, a, len(a), b, len(b), C.byref(res), C.byref(verd)), self.h)
         return int(verd.value), (bool(res.value) if verd.value == 0 else None)
 
-    def nif_inflation(self, prev: bytes, cur: bytes, strict: bool = False):
+    def nif_inflation(self, prev: bytes, cur: bytes, strict: bool = False, kind: str = "orset"):
+        fn = self.L.laspj_gset_etf_inflation if kind == "gset" else \
+            self.L.laspj_orset_etf_inflation
         res, verd = C.c_int32(), C.c_int32()
         prev, cur = bytes(prev), bytes(cur)
-        check(self.L.laspj_orset_etf_inflation(self.h, prev, len(prev), cur, len(cur),
-                                               int(strict), C.byref(res), C.byref(verd)),
-              self.h)
+        check(fn(self.h, prev, len(prev), cur, len(cur), int(strict), C.byref(res),
+                 C.byref(verd)), self.h)
         return int(verd.value), (bool(res.value) if verd.value == 0 else None)
+
+    def var(self, kind: str = "orset") -> "NifVar":
+        """A device-resident variable (laspj_var_create): #dv.value kept on the device."""
+        return NifVar(self, kind)
+
+    def var_bind_many(self, pairs):
+        """laspj_var_etf_bind_many over (NifVar, image) pairs: [(verdict, status)]."""
+        n = len(pairs)
+        if n == 0:
+            return []
+        keep = [bytes(img) for _v, img in pairs]
+        vs = (C.c_void_p * n)(*[v.h.value for v, _i in pairs])
+        pv = (C.c_char_p * n)(*keep)
+        nv = (C.c_uint64 * n)(*[len(x) for x in keep])
+        st = (C.c_int32 * n)()
+        verd = (C.c_int32 * n)()
+        check(self.L.laspj_var_etf_bind_many(self.h, n, vs, pv, nv, st, verd), self.h)
+        return [(int(verd[k]), int(st[k])) for k in range(n)]
 
     def nif_stats(self) -> dict:
         out = (C.c_uint64 * _lib.NIF_STATS)()
@@ -158,7 +179,7 @@ class Context:
         keys = ("calls", "device_passes", "registrations", "dict_resets", "image_rebuilds",
                 "host_encoded_passes", "fallbacks", "dict_elements", "ns_stage_enqueue",
                 "ns_device_wait", "ns_answers", "ns_stage_copy", "ns_register", "ns_rebuild",
-                "image_patches", "chain_redo_passes")
+                "image_patches", "chain_redo_passes", "vars_spilled", "vars_hydrated")
         return dict(zip(keys, (int(x) for x in out)))
 
     def nif_reset(self):
@@ -174,6 +195,67 @@ class Context:
         check(self.L.laspj_batch_inflation_many(self.h, n, arr(prevs), arr(curs), int(strict),
                                                 out.h), self.h)
         return out.download(np.uint8).astype(bool)
+
+
+class NifVar:
+    """laspj_var: one OR-Set / G-Set `#dv.value` resident on the device (laspj.h
+    "resident variables").  Every call returns (verdict, answer) like the NIF image calls;
+    answer is None on NIF_FALLBACK."""
+
+    def __init__(self, ctx: Context, kind: str = "orset"):
+        self.ctx, self.L, self.kind = ctx, ctx.L, kind
+        self.h = C.c_void_p()
+        k = _lib.KIND_GSET if kind == "gset" else _lib.KIND_ORSET
+        check(self.L.laspj_var_create(ctx.h, k, C.byref(self.h)), ctx.h)
+
+    def close(self):
+        if self.h:
+            self.L.laspj_var_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bind(self, img: bytes):
+        """bind/3: (verdict, status) — status 0 no-op (Value0 =:= Value), 1 written."""
+        st, verd = C.c_int32(), C.c_int32()
+        img = bytes(img)
+        check(self.L.laspj_var_etf_bind(self.h, img, len(img), C.byref(st), C.byref(verd)),
+              self.ctx.h)
+        return int(verd.value), int(st.value)
+
+    def write(self, img: bytes) -> int:
+        verd = C.c_int32()
+        img = bytes(img)
+        check(self.L.laspj_var_etf_write(self.h, img, len(img), C.byref(verd)), self.ctx.h)
+        return int(verd.value)
+
+    def _image(self, fn):
+        out, olen, verd = C.c_void_p(), C.c_uint64(), C.c_int32()
+        check(fn(self.h, C.byref(out), C.byref(olen), C.byref(verd)), self.ctx.h)
+        return int(verd.value), (C.string_at(out, olen.value) if verd.value == 0 else None)
+
+    def read(self):
+        return self._image(self.L.laspj_var_etf_read)
+
+    def value(self):
+        return self._image(self.L.laspj_var_etf_value)
+
+    def threshold(self, img: bytes, strict: bool = False):
+        res, verd = C.c_int32(), C.c_int32()
+        img = bytes(img)
+        check(self.L.laspj_var_etf_threshold(self.h, img, len(img), int(strict), C.byref(res),
+                                             C.byref(verd)), self.ctx.h)
+        return int(verd.value), (bool(res.value) if verd.value == 0 else None)
+
+    @property
+    def resident(self) -> bool:
+        r = C.c_int32()
+        check(self.L.laspj_var_resident(self.h, C.byref(r)), self.ctx.h)
+        return bool(r.value)
 
 
 def device_count() -> int:

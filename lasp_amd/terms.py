@@ -79,3 +79,27 @@ def hkey(t):
     if r == _RANK_TUPLE:
         return ("t",) + tuple(hkey(x) for x in t)
     return ("l",) + tuple(hkey(x) for x in t)
+
+
+def ekey(t):
+    """Hashable key with Erlang `=:=` semantics (1 and 1.0 differ)."""
+    r = _rank(t)
+    if r == _RANK_NUM:
+        return ("f" if isinstance(t, float) else "i", t)
+    if r == _RANK_ATOM:
+        return ("a", _name(t))
+    if r == _RANK_BIN:
+        return ("b", bytes(t))
+    if r == _RANK_TUPLE:
+        return ("t",) + tuple(ekey(x) for x in t)
+    return ("l",) + tuple(ekey(x) for x in t)
+
+
+def same_term(a, b) -> bool:
+    """a =:= b for two terms already known to be `==` (equal hkeys)."""
+    if a is b:
+        return True
+    ta = type(a)
+    if ta is type(b) and ta in (int, bytes, Atom, str, bool):
+        return True
+    return ekey(a) == ekey(b)

@@ -122,7 +122,11 @@ WORKER = textwrap.dedent("""
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)        # bench takes the max wall time
     assert t.item() == float(world)
-    print("ok", rank)
+    print("ok", rank, flush=True)
+    # every rank done before any closes its pairs (a peer's early exit aborted gloo's
+    # pair threads in another rank under load)
+    dist.barrier()
+    dist.destroy_process_group()
 """)
 
 

@@ -170,14 +170,9 @@ def test_nif_cases_are_the_oracles_answers(tmp_path):
 
 # ------------------------------------------------------------------ GPU side
 
-def _ctx(direct=0):
-    from lasp_amd import _lib, engine
-    ctx = engine.Context(0)
-    if direct:
-        # LASPJ_TUNE_NIF_DIRECT: kernels read operands from / write answers into pinned
-        # host memory instead of the two copies
-        ctx.set_tuning(_lib.TUNE_NIF_DIRECT, direct)
-    return ctx
+def _ctx():
+    from lasp_amd import engine
+    return engine.Context(0)
 
 
 def _run_case(ctx, case):
@@ -205,9 +200,8 @@ def _check(case, got):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
-def test_nif_answers_match_oracle(direct):
-    ctx = _ctx(direct)
+def test_nif_answers_match_oracle():
+    ctx = _ctx()
     try:
         for case in valid_cases(seed=11, n=30) + fallback_cases(seed=12):
             _check(case, _run_case(ctx, case))
@@ -379,9 +373,8 @@ def test_nif_dictionary_reset_when_an_element_runs_out_of_token_slots():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
-def test_nif_merge_many_mixed_verdicts(direct):
-    ctx = _ctx(direct)
+def test_nif_merge_many_mixed_verdicts():
+    ctx = _ctx()
     try:
         rng = random.Random(7)
         elems, pool = _universe(rng, 48)
@@ -402,11 +395,10 @@ def test_nif_merge_many_mixed_verdicts(direct):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
-def test_nif_mixed_token_image_lengths_take_the_host_encoder(direct):
+def test_nif_mixed_token_image_lengths_take_the_host_encoder():
     """Token images of several lengths: the device decoder needs one length, so the
     context's host dictionary encodes the cells and the device does the rest."""
-    ctx = _ctx(direct)
+    ctx = _ctx()
     try:
         rng = random.Random(8)
         elems = list(range(30))
@@ -427,12 +419,11 @@ def test_nif_mixed_token_image_lengths_take_the_host_encoder(direct):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", [0, 1, 2, 3, 6])
-def test_nif_flags_in_other_atom_encodings_and_second_copy(direct):
+def test_nif_flags_in_other_atom_encodings_and_second_copy():
     """Operands whose flags use SMALL_ATOM_UTF8_EXT (an OTP 26 node's term_to_binary):
     decoded alike; the answer is written with ATOM_EXT flags, one byte longer per token,
     so it outgrows the first copy's bound and takes the second copy."""
-    ctx = _ctx(direct)
+    ctx = _ctx()
     try:
         rng = random.Random(9)
         toks = sorted(_tokens(rng, 3000))
@@ -491,3 +482,96 @@ def test_nif_four_schedulers_plain_c(tmp_path):
     res = subprocess.run([exe, str(p), "4"], capture_output=True, text=True, timeout=240)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "laspj NIF threads OK" in res.stdout
+
+
+# ------------------------------------------------------------------ `==` classes
+
+def _oracle_answer(op, a, b):
+    """The reference's answer for (op, terms a, b) from the oracle."""
+    if op == MERGE:
+        return _tb(oorset.merge(a, b))
+    if op == VALUE:
+        return _tb(oorset.value(a))
+    if op == EQUAL:
+        return oorset.equal(a, b)
+    return olat.is_inflation("lasp_orset", a, b) if op == INFL else \
+        olat.is_strict_inflation("lasp_orset", a, b)
+
+
+def equal_term_cases(seed=3):
+    """Operands holding `==`-equal terms under other images (1 / 1.0 as elements, inside
+    tuples and lists, as tokens), in both orders and after the other image registered."""
+    rng = random.Random(seed)
+    t = _tokens(rng, 8)
+    pairs = [
+        ([(1, [(t[0], False)])], [(1.0, [(t[1], False)])]),
+        ([(1.0, [(t[0], True)])], [(1, [(t[0], False)])]),
+        ([((Atom("a"), 1), [(t[2], False)])], [((Atom("a"), 1.0), [(t[3], True)])]),
+        ([([1, 2], [(t[4], False)])], [([1.0, 2], [(t[4], False)])]),
+        ([(5, [(7, False)])], [(5, [(7.0, True)])]),
+        ([(2, [(t[5], False)]), (3, [(t[6], False)])], [(3.0, [(t[6], True)])]),
+    ]
+    out = []
+    for a, b in pairs:
+        for op in (MERGE, EQUAL, INFL, SINFL):
+            out.append((op, a, b))
+            out.append((op, b, a))
+        out.append((VALUE, b, None))
+    return out
+
+
+@pytest.mark.gpu
+def test_nif_equal_terms_answer_the_oracle_or_fallback():
+    """`1` and `1.0` (and terms holding them, and tokens) are
+    one orddict key for the reference (orddict:merge's equal clause keeps the left key,
+    lasp_orset.erl:128-134; equal/2 is ==, :136-138).  The dictionary refuses the second
+    image of a `==` class (LASPJ_DEC_EQUAL_TERMS), so every such call answers the oracle's
+    term or FALLBACK (the reference's own clause) — never a two-key answer with verdict OK.
+    The context keeps answering ordinary calls afterwards."""
+    ctx = _ctx()
+    try:
+        n_fb = 0
+        for op, a, b in equal_term_cases():
+            got = _run_case(ctx, (op, None, None, _tb(a), _tb(b) if b is not None else b"", b""))
+            v, ans = got
+            if v == FALLBACK:
+                n_fb += 1
+                assert ans is None
+                continue
+            assert v == OK
+            want = _oracle_answer(op, a, b)
+            assert ans == want, (op, a, b, ans, want)
+        assert n_fb >= 20
+        for case in valid_cases(seed=4, n=6):
+            _check(case, _run_case(ctx, case))
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_nif_unresolved_call_answers_fallback():
+    """run()'s post-condition: a call whose device passes run out
+    before its statuses are final answers FALLBACK, not the superseded pass's answer.  With
+    one pass allowed (LASPJ_TUNE_NIF_PASSES), a merge that meets a fresh token registers it
+    and has no pass left: FALLBACK; the same call with the default passes answers the
+    oracle's merge."""
+    from lasp_amd import _lib
+    ctx = _ctx()
+    try:
+        rng = random.Random(12)
+        elems, pool = _universe(rng, 40)
+        a, b = _orset(rng, elems, pool), _orset(rng, elems, pool)
+        assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(oorset.merge(a, b)))
+        ctx.set_tuning(_lib.TUNE_NIF_PASSES, 1)
+        e = [x for x, _ts in b][0]
+        b2 = oorset.merge(b, [(e, [(b"\x07" * 20, False)])])
+        assert ctx.nif_merge(_tb(a), _tb(b2)) == (FALLBACK, None)
+        # (now registered: one pass is enough)
+        assert ctx.nif_merge(_tb(a), _tb(b2)) == (OK, _tb(oorset.merge(a, b2)))
+        b3 = oorset.merge(b, [(e, [(b"\x08" * 20, True)])])
+        assert ctx.nif_merge(_tb(a), _tb(b3)) == (FALLBACK, None)
+        ctx.set_tuning(_lib.TUNE_NIF_PASSES, 0)
+        b4 = oorset.merge(b, [(e, [(b"\x09" * 20, True)])])
+        assert ctx.nif_merge(_tb(a), _tb(b4)) == (OK, _tb(oorset.merge(a, b4)))
+    finally:
+        ctx.close()

@@ -248,3 +248,97 @@ def test_domain_journal_undoes_failed_registrations():
         dom.element_slot(2)
     assert dom.size == 3 and len(dom.tokens) == 3
     assert [dom.elements.terms[int(s)] for s in dom.elements.order()] == [1, 2, 3]
+
+
+def _small_atom_utf8(name: str) -> bytes:
+    b = name.encode()
+    return bytes([119, len(b)]) + b
+
+
+def test_dict_refuses_equal_terms_under_other_images(lib):
+    """`==` classes: the dictionary keys slots by image bytes, so a term
+    `==` to a registered one under another image — 1 and 1.0, {a, 1} and {a, 1.0}, [1] and
+    [1.0], an atom in another encoding, 2^64 and 1.8446744073709552e19, -0.0 and 0 — would
+    take a second slot where orddict:merge / ordsets:union (lasp_orset.erl:128-134,
+    lasp_gset.erl:99-101) see one key.  Its payload gets
+    LASPJ_DEC_EQUAL_TERMS and registers nothing; terms that only look alike (2^64 + 1 and
+    that float, 0.5 and 1) register normally."""
+    from lasp_amd.hostdict import NativeDict
+    tok = b"t" * 20
+    od = lambda e, t=tok: etf.term_to_binary([(e, [(t, False)])])     # noqa: E731
+    pairs = [(1, 1.0), (-3, -3.0), ((Atom("a"), 1), (Atom("a"), 1.0)), ([1, 2], [1.0, 2]),
+             (2 ** 64, 1.8446744073709552e19), (0, -0.0), (2 ** 70, float(2 ** 70)),
+             (((1,), [2]), ((1.0,), [2.0]))]
+    for x, y in pairs:
+        d = NativeDict()
+        assert list(d.add(_lib.KIND_ORSET, [od(x)])) == [_lib.DEC_OK], x
+        n0 = d.info()
+        assert list(d.add(_lib.KIND_ORSET, [od(y)])) == [_lib.DEC_EQUAL_TERMS], (x, y)
+        assert d.info() == n0
+        # the registered image itself is still welcome
+        assert list(d.add(_lib.KIND_ORSET, [od(x)])) == [_lib.DEC_OK]
+        g = NativeDict()
+        assert list(g.add(_lib.KIND_GSET, [etf.term_to_binary([x])])) == [_lib.DEC_OK]
+        assert list(g.add(_lib.KIND_GSET, [etf.term_to_binary([y])])) == [_lib.DEC_EQUAL_TERMS]
+    # within one payload (not an orddict: 1 < 1.0 is false) and across tokens of an element
+    d = NativeDict()
+    assert list(d.add(_lib.KIND_ORSET, [etf.term_to_binary([(1, [(tok, False)]),
+                                                            (1.0, [(tok, False)])])])) == \
+        [_lib.DEC_EQUAL_TERMS]
+    assert d.info()[0] == 0
+    assert list(d.add(_lib.KIND_ORSET, [etf.term_to_binary([(5, [(7, False)])])])) == [0]
+    assert list(d.add(_lib.KIND_ORSET, [etf.term_to_binary([(5, [(7.0, True)])])])) == \
+        [_lib.DEC_EQUAL_TERMS]
+    # an atom in SMALL_ATOM_UTF8_EXT (an OTP 26 node's image) against ATOM_EXT
+    d = NativeDict()
+    plain = etf.term_to_binary([(Atom("zed"), [(tok, False)])])
+    assert list(d.add(_lib.KIND_ORSET, [plain])) == [0]
+    other = plain.replace(bytes([100, 0, 3]) + b"zed", _small_atom_utf8("zed"))
+    assert other != plain
+    assert list(d.add(_lib.KIND_ORSET, [other])) == [_lib.DEC_EQUAL_TERMS]
+    # look-alikes that are not `==` register as separate terms
+    for x, y in [(2 ** 64 + 1, 1.8446744073709552e19), (0.5, 1), (1, (1,)), ([1], [[1]]),
+                 (b"a", [97]), ([], b"")]:
+        d = NativeDict()
+        assert list(d.add(_lib.KIND_ORSET, [od(x), od(y)])) == [0, 0], (x, y)
+        assert d.info()[0] == 2
+
+
+@settings(max_examples=300 * SOAK, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(TERM, TERM)
+def test_dict_equal_terms_iff_compare_equal(lib, a, b):
+    """The `==` class check agrees with the comparator: b registers after a exactly when
+    the two are not `==` or have the same image."""
+    from lasp_amd.hostdict import NativeDict
+    d = NativeDict()
+    ia, ib = etf.encode(a), etf.encode(b)
+    pa = bytes([131, 108, 0, 0, 0, 1]) + ia + bytes([106])
+    pb = bytes([131, 108, 0, 0, 0, 1]) + ib + bytes([106])
+    assert list(d.add(_lib.KIND_GSET, [pa])) == [0]
+    st_ = d.add(_lib.KIND_GSET, [pb])[0]
+    same_class = compare(lib, a, b) == 0 and ia != ib
+    assert st_ == (_lib.DEC_EQUAL_TERMS if same_class else _lib.DEC_OK), (a, b)
+
+
+def test_domain_refuses_equal_terms():
+    """The Python Domain (the device store's dictionaries) refuses a second term of one
+    `==` class too, instead of letting the first-seen term stand for both: the store then
+    raises Unsupported."""
+    from lasp_amd.codec import CapacityError, EqualTerms
+    dom = Domain()
+    dom.element_slot(1)
+    assert dom.element_slot(1) == 0
+    with pytest.raises(EqualTerms):
+        dom.element_slot(1.0)
+    assert issubclass(EqualTerms, CapacityError)
+    es = dom.element_slot((Atom("a"), 2))
+    with pytest.raises(EqualTerms):
+        dom.element_slot((Atom("a"), 2.0))
+    dom.token_slot(es, 3)
+    with pytest.raises(EqualTerms):
+        dom.token_slot(es, 3.0)
+    # true / Atom("true") are one atom: no refusal
+    t = dom.element_slot(True)
+    assert dom.element_slot(Atom("true")) == t
+    with pytest.raises(EqualTerms):
+        dom.encode_orset([[(1.0, [(b"x" * 20, False)])]], 16)

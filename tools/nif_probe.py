@@ -24,12 +24,6 @@ L = ctx.L
 from lasp_amd import _lib  # noqa: E402
 if os.environ.get("NIF_SEG"):                  # from_binary segment bytes (A/B)
     ctx.set_tuning(_lib.TUNE_ETF_SEG, int(os.environ["NIF_SEG"]))
-if os.environ.get("NIF_PIECE"):                # pinned staging piece bytes (A/B)
-    ctx.set_tuning(_lib.TUNE_NIF_PIECE, int(os.environ["NIF_PIECE"]))
-if os.environ.get("NIF_HOST"):                 # pinned staging kind (A/B)
-    ctx.set_tuning(_lib.TUNE_NIF_HOST, int(os.environ["NIF_HOST"]))
-if os.environ.get("NIF_DIRECT"):               # kernels on pinned host memory (A/B)
-    ctx.set_tuning(_lib.TUNE_NIF_DIRECT, int(os.environ["NIF_DIRECT"]))
 if os.environ.get("NIF_ETF"):                  # writer variant (A/B; 5: the two-launch merge)
     ctx.set_tuning(_lib.TUNE_ETF_KERNEL, int(os.environ["NIF_ETF"]))
 op, on, vd = C.c_void_p(), C.c_uint64(), C.c_int32()
