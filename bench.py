@@ -400,6 +400,108 @@ def config1_gpu(ctx):
                          "from_binary + join + device to_binary + download of the %d-byte "
                          "merged payload; us_merge_native_host_encode: host dictionary encode "
                          "instead of the device decoder" % (len(blob), total.value))
+    out.update(config1_resident(ctx, pa, pb, ref))
+    return out
+
+
+def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
+    """bind/3 with `#dv.value` resident on the device (laspj_var_etf_bind, lasp_core.erl:
+    291-312): Value0 = A ⊔ B stays in HBM, each bind ships only the incoming 10k-element
+    image B, decodes it, decides `Value0 =:= Value` and merges in one kernel, and reads
+    back a status.  Single binds on one context, 32 binds per call, and 16 contexts (one
+    per BEAM scheduler) binding at once from 16 threads on the one GPU."""
+    import ctypes as C
+    import threading
+    from lasp_amd._lib import check
+    from lasp_amd import engine
+    L = ctx.L
+    out = {}
+    var = ctx.var("orset")
+    if var.write(pa) != 0 or var.bind(pb) != (0, 1) or var.read() != (0, ref):
+        raise RuntimeError("config1: the resident bind differs from the merge")
+    st, vd = C.c_int32(), C.c_int32()
+
+    def vbind(v=var):
+        check(L.laspj_var_etf_bind(v.h, pb, len(pb), C.byref(st), C.byref(vd)), ctx.h)
+
+    vbind()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        vbind()
+    out["us_bind_nif"] = (time.perf_counter() - t0) * 1e6 / 50
+    if (vd.value, st.value) != (0, 1) or var.read() != (0, ref):
+        raise RuntimeError("config1: resident bind answered wrongly")
+    t0 = time.perf_counter()
+    for _ in range(20):
+        var.read()
+    out["us_read_nif"] = (time.perf_counter() - t0) * 1e6 / 20
+    nm = 32
+    vs = [ctx.var("orset") for _ in range(nm)]
+    for v in vs:
+        v.write(ref)
+    arr_v = (C.c_void_p * nm)(*[v.h.value for v in vs])
+    arr_p = (C.c_char_p * nm)(*([pb] * nm))
+    arr_n = (C.c_uint64 * nm)(*([len(pb)] * nm))
+    sts, vds = (C.c_int32 * nm)(), (C.c_int32 * nm)()
+
+    def vbind_many():
+        check(L.laspj_var_etf_bind_many(ctx.h, nm, arr_v, arr_p, arr_n, sts, vds), ctx.h)
+
+    vbind_many()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        vbind_many()
+    out["us_bind_nif_many_per_bind"] = (time.perf_counter() - t0) * 1e6 / (5 * nm)
+    if any(vds[k] or sts[k] != 1 for k in range(nm)):
+        raise RuntimeError("config1: bind_many answered wrongly")
+    # 16 schedulers: a context and a variable each, binding B in a loop
+    nthreads, per = 16, 60
+    ready, errs, spans = threading.Barrier(nthreads + 1), [], []
+
+    def worker():
+        try:
+            c2 = engine.Context(ctx.device)
+            v2 = c2.var("orset")
+            v2.write(ref)
+            s2, d2 = C.c_int32(), C.c_int32()
+            check(L.laspj_var_etf_bind(v2.h, pb, len(pb), C.byref(s2), C.byref(d2)), c2.h)
+            ready.wait()
+            t = time.perf_counter()
+            for _ in range(per):
+                check(L.laspj_var_etf_bind(v2.h, pb, len(pb), C.byref(s2), C.byref(d2)), c2.h)
+            spans.append((t, time.perf_counter()))
+            if (d2.value, s2.value) != (0, 1):
+                errs.append("bad answer")
+            v2.close()
+            c2.close()
+        except Exception as e:       # noqa: BLE001 — reported below
+            errs.append(repr(e))
+            try:
+                ready.abort()
+            except Exception:
+                pass
+
+    ths = [threading.Thread(target=worker) for _ in range(nthreads)]
+    for t in ths:
+        t.start()
+    try:
+        ready.wait(timeout=120)
+    except threading.BrokenBarrierError:
+        pass
+    for t in ths:
+        t.join(timeout=300)
+    if errs or len(spans) != nthreads:
+        raise RuntimeError(f"config1: 16-context binds failed: {errs[:3]}")
+    wall = max(b for _a, b in spans) - min(a for a, _b in spans)
+    out["bind_16ctx"] = {"contexts": nthreads, "binds": nthreads * per,
+                         "us_per_bind": wall * 1e6 / (nthreads * per),
+                         "binds_per_s": nthreads * per / wall,
+                         "merged_elements_per_s": nthreads * per * 10_000 / wall}
+    out["resident"] = ("Value0 = A ⊔ B resident (laspj_var); per bind: the %d-byte image of B "
+                       "in, decode + `=:=` + merge on the device, the status out" % len(pb))
+    for v in vs:
+        v.close()
+    var.close()
     return out
 
 

@@ -4557,6 +4557,84 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     return LASPJ_OK;
 }
 
+// lasp_core:bind/3 (lasp_core.erl:291-312) for n resident variables at once (the NIF's
+// device-resident `#dv.value`, laspj_nif.hip): variable i's cells cur[i] and the decoded
+// incoming value in[i] (wpr words each).  `case Value0 of Value` is word equality (the
+// host dictionary holds one image per `==` class, so equal cells are equal terms);
+// otherwise cur := merge(cur, in) — the slot-wise OR of two canonical orddicts / ordsets,
+// which always inflates cur, so the reference writes it (:300-304).  WRITE (write/4,
+// :839-844) replaces the cells instead.  A value whose decode failed leaves its variable
+// untouched.  The decode status comes from dstat[i] or, with the chain check deferred
+// here (cj.status set: the segment decoder ran without its chain launch), from
+// chain_verdict, which every block of a variable evaluates for itself (deterministic, so
+// all agree without a grid-wide wait; block 0 of the variable stores it in dstat[i]).
+// in[] is left zero behind (the next call's decoders need clean cells).  The block that
+// finishes last publishes per variable the status byte (0 no-op, 1 written) and the
+// decode status into the pinned answer, and leaves the difference words and the ticket
+// zero.
+constexpr uint32_t kVarWords = 1024;     // words per block (4 per thread)
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ curs,
+                                                     u64* __restrict__ in, uint64_t wpr,
+                                                     uint32_t nch, uint32_t n,
+                                                     int32_t* __restrict__ dstat,
+                                                     uint32_t* __restrict__ diff,
+                                                     uint32_t* __restrict__ ticket,
+                                                     uint8_t* __restrict__ out_res,
+                                                     int32_t* __restrict__ out_st, ChainArgs cj) {
+    __shared__ int32_t s_st;
+    __shared__ bool s_last;
+    const uint32_t i = blockIdx.x / nch, ch = blockIdx.x % nch;
+    if (cj.status) {
+        if (threadIdx.x < 64) {
+            const u64 base = cj.offs[i];
+            const int32_t st = chain_verdict(cj.payload, base, cj.offs[i + 1] - base,
+                                             cj.segbase[i], cj.segbase[i + 1] - cj.segbase[i],
+                                             cj.S, cj.res, threadIdx.x);
+            if (threadIdx.x == 0) {
+                s_st = st;
+                if (ch == 0) dstat[i] = st;
+            }
+        }
+    } else if (threadIdx.x == 0) {
+        s_st = dstat[i];
+    }
+    __syncthreads();
+    const bool ok = s_st == LASPJ_DEC_OK;
+    u64* cur = curs[i];
+    u64* src = in + (uint64_t)i * wpr;
+    u64 d = 0;
+    const uint64_t w0 = (uint64_t)ch * kVarWords;
+    for (uint32_t k = threadIdx.x; k < kVarWords; k += kBlock) {
+        const uint64_t w = w0 + k;
+        if (w >= wpr) break;
+        const u64 b = src[w];
+        if (ok) {
+            const u64 a = cur[w];
+            d |= a ^ b;
+            const u64 v = WRITE ? b : (a | b);
+            if (v != a) cur[w] = v;
+        }
+        if (b) src[w] = 0;
+    }
+    const bool any = __syncthreads_or(d != 0);
+    if (threadIdx.x == 0) {
+        if (any) atomicOr(diff + i, 1u);
+        __threadfence();
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (uint32_t j = threadIdx.x; j < n; j += kBlock) {
+        const uint32_t dj = atomicExch(diff + j, 0u);
+        const int32_t st = __atomic_load_n(dstat + j, __ATOMIC_RELAXED);
+        out_res[j] = st == LASPJ_DEC_OK ? (uint8_t)(dj ? 1 : 0) : (uint8_t)0;
+        out_st[j] = st;
+    }
+    if (threadIdx.x == 0) *ticket = 0;
+}
+
 }  // namespace
 }  // namespace laspj
 
@@ -4878,6 +4956,23 @@ int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E
     hipLaunchKernelGGL(k, dim3(nch + cblocks), dim3(kBlock), 0, ctx->stream, (const u64x2*)nullptr,
                        (uint64_t)1, E, view(d), tag, vers, (const u64*)nullptr, out,
                        (const u64*)nullptr, 1u, (u64)cap_bytes, lb);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64_t wpr,
+                     uint32_t n, int32_t* dstat, uint32_t* diff, uint32_t* ticket,
+                     uint8_t* out_res, int32_t* out_st, bool write, const ChainJob* chain) {
+    const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (wpr + kVarWords - 1) / kVarWords);
+    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    if (chain && chain->armed)
+        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
+                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
+                       chain->S};
+    hipLaunchKernelGGL(write ? k_var_bind<true> : k_var_bind<false>, dim3(nch * n), dim3(kBlock),
+                       0, ctx->stream, reinterpret_cast<u64* const*>(curs),
+                       reinterpret_cast<u64*>(in), wpr, nch, n, dstat, diff, ticket, out_res,
+                       out_st, cj);
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }

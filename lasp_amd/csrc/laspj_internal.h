@@ -301,6 +301,14 @@ int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E
                             const laspj_etf_dict* d, int tag, int vers,
                             unsigned long long* offs_out, uint8_t* out, uint64_t cap_bytes,
                             unsigned long long* lbst, uint32_t* ticket, const ChainJob* chain);
+// lasp_core:bind/3 (write = false) / write/4 (write = true) of n resident variables: curs
+// (device array of n cell pointers), in (n x wpr decoded words, left zero), dstat (n
+// decode statuses: read, or — chain armed — written from the deferred chain check), diff
+// (n zeroed words) and ticket (a zeroed word) left zero; out_res / out_st (n bytes / n
+// int32, pinned) get the bind statuses and decode statuses
+int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64_t wpr,
+                     uint32_t n, int32_t* dstat, uint32_t* diff, uint32_t* ticket,
+                     uint8_t* out_res, int32_t* out_st, bool write, const ChainJob* chain);
 // offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
 // caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
 // (valid until the context's scratch is next used), or null

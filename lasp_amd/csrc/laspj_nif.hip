@@ -116,62 +116,6 @@ __global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src
         dst[i] = __builtin_nontemporal_load(src + i);
 }
 
-// lasp_core:bind/3 (lasp_core.erl:291-312) for n resident variables at once: variable i's
-// cells cur[i] and the decoded incoming value in[i] (wpr words each).  `case Value0 of
-// Value` is word equality (the dictionary holds one image per `==` class, so equal cells
-// are equal terms); otherwise cur := merge(cur, in) — the slot-wise OR of two canonical
-// orddicts / ordsets, which always inflates cur, so the reference writes it (:300-304).
-// A value whose decode failed (dstat[i] != 0) leaves its variable untouched.  WRITE
-// (write/4, :839-844) replaces the cells instead.  in[] is left zero behind it (the next
-// call's decoders need clean cells).  The last block publishes per variable the status
-// byte (0 no-op, 1 written) and the decode status into pinned host memory, and leaves the
-// difference words and the ticket zero.
-constexpr int kVarWords = 1024;     // words per block (4 per thread)
-template <bool WRITE>
-__global__ void __launch_bounds__(256) k_var_bind(uint64_t* const* __restrict__ curs,
-                                                  uint64_t* __restrict__ in, uint64_t wpr,
-                                                  uint32_t nch, uint32_t n,
-                                                  const int32_t* __restrict__ dstat,
-                                                  uint32_t* __restrict__ diff,
-                                                  uint32_t* __restrict__ ticket,
-                                                  uint8_t* __restrict__ out_res,
-                                                  int32_t* __restrict__ out_st) {
-    const uint32_t i = blockIdx.x / nch, ch = blockIdx.x % nch;
-    uint64_t* cur = curs[i];
-    uint64_t* src = in + (uint64_t)i * wpr;
-    const bool ok = dstat[i] == 0;
-    uint64_t d = 0;
-    const uint64_t w0 = (uint64_t)ch * kVarWords;
-    for (uint32_t k = threadIdx.x; k < (uint32_t)kVarWords; k += blockDim.x) {
-        const uint64_t w = w0 + k;
-        if (w >= wpr) break;
-        const uint64_t b = src[w];
-        if (ok) {
-            const uint64_t a = cur[w];
-            d |= a ^ b;
-            const uint64_t v = WRITE ? b : (a | b);
-            if (v != a) cur[w] = v;
-        }
-        if (b) src[w] = 0;
-    }
-    const bool any = __syncthreads_or(d != 0);
-    __shared__ bool last;
-    if (threadIdx.x == 0) {
-        if (any) atomicOr(diff + i, 1u);
-        __threadfence();
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint32_t dj = atomicExch(diff + j, 0u);
-        out_res[j] = dstat[j] == 0 ? (uint8_t)(dj ? 1 : 0) : (uint8_t)0;
-        out_st[j] = dstat[j];
-    }
-    if (threadIdx.x == 0) *ticket = 0;
-}
-
 struct Guard {
     std::lock_guard<std::mutex> lk;
     explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
@@ -417,8 +361,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
     const uint64_t out_bytes = o_pay + ocap;
     // MERGE: the segment decoder's chain check rides on the join's launch (ChainJob), its
     // per-segment results in a device area of their own after the in region
-    const bool defer = dec && orset && plan.nseg && c.op == Op::MERGE && !c.no_defer &&
-                       etf_merge_fused(ctx, n, E);
+    const bool defer = dec && orset && plan.nseg && !c.no_defer &&
+                       ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op);
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
     // device statuses of the variable calls (their kernel reads them)
     const uint64_t vst_bytes = var_op ? al(4ull * m, 256) : 0;
@@ -654,13 +598,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
         case Op::BIND:
         case Op::WRITE: {
             // bind/3 (lasp_core.erl:291-312) / write/4 (:839-844) into the resident cells
-            const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (W + kVarWords - 1) / kVarWords);
-            auto k = c.op == Op::BIND ? k_var_bind<false> : k_var_bind<true>;
-            hipLaunchKernelGGL(k, dim3(nch * n), dim3(256), 0, ctx->stream,
-                               reinterpret_cast<uint64_t* const*>(din + i_vptr), cin, W, nch, n,
-                               dvst, dvdiff, dvdiff + n, rout + o_res,
-                               reinterpret_cast<int32_t*>(rout + o_st));
-            LJ_LAUNCHED(ctx);
+            // (the segment decoder's chain check rides on this launch when deferred)
+            if (int s = var_bind_enqueue(ctx, reinterpret_cast<uint64_t* const*>(din + i_vptr),
+                                         cin, W, n, dvst, dvdiff, dvdiff + n, rout + o_res,
+                                         reinterpret_cast<int32_t*>(rout + o_st),
+                                         c.op == Op::WRITE, &cjob))
+                return s;
             S->clean_words = in_words;
             break;
         }
