@@ -754,6 +754,63 @@ int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                     const laspj_buf* off, const laspj_buf* keys, uint32_t nidx,
                     int per_entry);
 
+/* ------------------------------------------------------------------ list bodies from images */
+/* The combinator bodies (lasp_core.erl:460-712) and bind/3 (:291-312) on list values as a
+ * NIF holds them: term_to_binary/1 images in (131 + a list: OR-Set lists of
+ * {Key, [{Token, true|false}]}, G-Set lists of terms, in any order, keys / elements and
+ * tokens repeated or not), the answer's image out (*out valid until the context's next
+ * call), run on the device's list kernels above over a dictionary of the call's own terms
+ * (calls are self-contained).  kind: LASPJ_KIND_ORSET or LASPJ_KIND_GSET (the type of
+ * #dv).  verdict LASPJ_NIF_FALLBACK: a value this path does not take (not such a list, a
+ * key with more than 64 distinct tokens, two `==`-equal terms under different images, a
+ * G-Set intersection / product over 2-tuple elements) — the NIF runs the reference's
+ * body.  A fun is the caller's to evaluate: laspj_list_etf_args gives the distinct values
+ * the body passes it (the keys; a G-Set element, or the first component of a 2-tuple
+ * element, lasp_core.erl:648-655, 688-695) in first-appearance order as a list image, and
+ * the map / filter / fold entry points take the image of the list of its results in that
+ * order (LASPJ_E_INVAL when the counts differ; fold: each result a list). */
+/* the fun's distinct arguments (map/6, filter/6, fold/6 bodies) */
+int laspj_list_etf_args(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
+                        const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* map/6 body — lasp_core.erl:641-667: {F(X), Causality} / F(X) in list order */
+int laspj_list_etf_map(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
+                       const uint8_t* results, uint64_t nr, const uint8_t** out,
+                       uint64_t* out_len, int32_t* verdict);
+/* filter/6 body — lasp_core.erl:681-712: entries whose F(X) =:= true, tombstones kept */
+int laspj_list_etf_filter(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
+                          const uint8_t* results, uint64_t nr, const uint8_t** out,
+                          uint64_t* out_len, int32_t* verdict);
+/* fold/6 body — lasp_core.erl:460-486: [{V, Causality} || V <- F(X)] / F(X), appended */
+int laspj_list_etf_fold(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
+                        const uint8_t* results, uint64_t nr, const uint8_t** out,
+                        uint64_t* out_len, int32_t* verdict);
+/* union/7 body — lasp_core.erl:602-627: OR-Set orddict:merge keeping the left tokens,
+ * G-Set L ++ R */
+int laspj_list_etf_union(laspj_ctx* ctx, int32_t kind, const uint8_t* l, uint64_t nl,
+                         const uint8_t* r, uint64_t nr, const uint8_t** out, uint64_t* out_len,
+                         int32_t* verdict);
+/* intersection/7 body — lasp_core.erl:546-589: {X, Cx ++ Cy} for lists:keyfind hits /
+ * lists:member */
+int laspj_list_etf_intersection(laspj_ctx* ctx, int32_t kind, const uint8_t* l, uint64_t nl,
+                                const uint8_t* r, uint64_t nr, const uint8_t** out,
+                                uint64_t* out_len, int32_t* verdict);
+/* product/7 body — lasp_core.erl:499-533: X-major {{X, Y}, orset_causal_product(Cx, Cy)}
+ * (lasp_lattice.erl:303-308, descending token pairs) / {X, Y} */
+int laspj_list_etf_product(laspj_ctx* ctx, int32_t kind, const uint8_t* l, uint64_t nl,
+                           const uint8_t* r, uint64_t nr, const uint8_t** out, uint64_t* out_len,
+                           int32_t* verdict);
+/* Type:value/1 of a list value — lasp_orset.erl:67-73 (keys with a {_, false} token, list
+ * order) / lasp_gset.erl:74-76 (the identity) */
+int laspj_list_etf_value(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
+                         const uint8_t** out, uint64_t* out_len, int32_t* verdict);
+/* bind/3 on list values — lasp_core.erl:291-312: *status 0 when value0 =:= value (no-op),
+ * 1 when merge(value0, value) (orddict:merge / ordsets:union run as written) inflates
+ * value0 (lasp_lattice.erl:137-161, lists:keyfind first match: the bind writes *out), 2
+ * when it does not (no write, *out null) */
+int laspj_list_etf_bind(laspj_ctx* ctx, int32_t kind, const uint8_t* value0, uint64_t n0,
+                        const uint8_t* value, uint64_t n, const uint8_t** out, uint64_t* out_len,
+                        int32_t* status, int32_t* verdict);
+
 /* ------------------------------------------------------------------ host dictionary */
 /* The NIF side of the boundary, native (no GPU involved): element / token dictionaries
  * over external-term-format images (term_to_binary/1 of each term, no version byte),

@@ -234,6 +234,24 @@ SIGNATURES = {
     "laspj_var_etf_threshold": (i, [vp, vp, u64, i, C.POINTER(C.c_int32),
                                     C.POINTER(C.c_int32)]),
     "laspj_var_resident": (i, [vp, C.POINTER(C.c_int32)]),
+    "laspj_list_etf_args": (i, [vp, C.c_int32, vp, u64, vpp, C.POINTER(u64),
+                                C.POINTER(C.c_int32)]),
+    "laspj_list_etf_map": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                               C.POINTER(C.c_int32)]),
+    "laspj_list_etf_filter": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                  C.POINTER(C.c_int32)]),
+    "laspj_list_etf_fold": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                C.POINTER(C.c_int32)]),
+    "laspj_list_etf_union": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                 C.POINTER(C.c_int32)]),
+    "laspj_list_etf_intersection": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                        C.POINTER(C.c_int32)]),
+    "laspj_list_etf_product": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                   C.POINTER(C.c_int32)]),
+    "laspj_list_etf_value": (i, [vp, C.c_int32, vp, u64, vpp, C.POINTER(u64),
+                                 C.POINTER(C.c_int32)]),
+    "laspj_list_etf_bind": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
+                                C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "laspj_nif_stats": (i, [vp, vp, u32]),
     "laspj_nif_reset": (i, [vp]),
     "laspj_event_create": (i, [vp, vpp]),

@@ -30,7 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/laspj.h"
+#include "laspj_internal.h"
 
 namespace {
 
@@ -1146,5 +1146,281 @@ int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, si
     d->journal.clear();
     return st;
 }
+
+}  // namespace laspj
+
+// ------------------------------------------------------------------ list values as images
+// (laspj_list_etf.cpp): the combinator bodies and bind/3 on lists that are not orddicts /
+// ordsets (lasp_core.erl:460-712) take and give term_to_binary images; these walk an image
+// into list items over a host dictionary and write items back into an image.
+namespace laspj {
+
+namespace {
+
+constexpr uint64_t kPairBit = 1ull << 62;
+constexpr uint64_t kFlagBit = 1ull << 63;
+
+void put_be32(std::string* o, uint32_t v) {
+    for (int k = 3; k >= 0; --k) o->push_back((char)((v >> (8 * k)) & 0xFF));
+}
+
+bool small_int(std::string_view img, uint8_t* v) {
+    if (img.size() == 2 && (uint8_t)img[0] == kSmallInt) {
+        *v = (uint8_t)img[1];
+        return true;
+    }
+    return false;
+}
+
+}  // namespace
+
+int list_walk(laspj_dict* dict, int32_t kind, const uint8_t* p, size_t n, ListItems* it,
+              std::vector<uint32_t>* args) {
+    Dict* d = &dict->d;
+    it->keys.clear();
+    it->toff.assign(1, 0);
+    it->toks.clear();
+    d->journal.clear();
+    int st = LASPJ_DEC_OK;
+    try {
+        const uint8_t* t;
+        size_t tn;
+        st = payload_term(p, n, -1, -1, &t, &tn);
+        if (st == LASPJ_DEC_OK && t[0] != kNil && t[0] != kList && t[0] != kString)
+            st = LASPJ_DEC_MALFORMED;                    // not a list
+        if (st == LASPJ_DEC_OK && t[0] != kNil) {
+            ListIt li(t, tn);
+            size_t el;
+            while (st == LASPJ_DEC_OK) {
+                const uint8_t* e = li.next(&el);
+                if (!e) break;
+                if (kind == LASPJ_KIND_GSET) {
+                    // a G-Set element that is a 2-tuple takes the bodies' OR-Set branch
+                    // (lasp_core.erl:467-474, 648-655, 688-695): its first component is the
+                    // fun's argument
+                    uint32_t slot = 0;
+                    if ((st = reg_elem(d, e, el, &slot))) break;
+                    it->keys.push_back(slot);
+                    it->toff.push_back((uint32_t)it->toks.size());
+                    continue;
+                }
+                // {Key, [{Token, Bool}, ...]}
+                if (el < 2 || e[0] != kSmallTuple || e[1] != 2) { st = LASPJ_DEC_MALFORMED; break; }
+                const size_t kl = term_len(e + 2, el - 2);
+                if (!kl) { st = LASPJ_DEC_MALFORMED; break; }
+                uint32_t key = 0;
+                if ((st = reg_elem(d, e + 2, kl, &key))) break;
+                const uint8_t* c = e + 2 + kl;
+                const size_t cl = el - 2 - kl;
+                if (c[0] != kNil && c[0] != kList) { st = LASPJ_DEC_MALFORMED; break; }
+                if (c[0] == kList) {
+                    ListIt ci(c, cl);
+                    size_t rl;
+                    while (const uint8_t* r = ci.next(&rl)) {
+                        if (rl < 2 || r[0] != kSmallTuple || r[1] != 2) { st = LASPJ_DEC_MALFORMED; break; }
+                        const size_t tl = term_len(r + 2, rl - 2);
+                        if (!tl) { st = LASPJ_DEC_MALFORMED; break; }
+                        const int flag = bool_atom(r + 2 + tl);
+                        if (flag < 0 || term_len(r + 2 + tl, rl - 2 - tl) != rl - 2 - tl) {
+                            st = LASPJ_DEC_MALFORMED;
+                            break;
+                        }
+                        uint8_t ts = 0;
+                        if ((st = reg_tok(d, key, r + 2, tl, &ts))) break;
+                        it->toks.push_back((64ull * key + ts) | (flag ? kFlagBit : 0ull));
+                    }
+                    if (st == LASPJ_DEC_OK && ci.tail() && ci.tail()[0] != kNil) st = LASPJ_DEC_MALFORMED;
+                }
+                if (st) break;
+                it->keys.push_back(key);
+                it->toff.push_back((uint32_t)it->toks.size());
+            }
+            if (st == LASPJ_DEC_OK && li.tail() && li.tail()[0] != kNil) st = LASPJ_DEC_MALFORMED;
+        }
+        if (st == LASPJ_DEC_OK && args) {
+            // the fun's argument per entry: the key (OR-Set), the element or the first
+            // component of a 2-tuple element (G-Set), as slots of the dictionary
+            args->clear();
+            for (uint64_t k : it->keys) {
+                const uint32_t e = (uint32_t)k;
+                std::string_view img = d->elems[e];
+                uint32_t a = e;
+                if (kind == LASPJ_KIND_GSET && img.size() >= 2 && (uint8_t)img[0] == kSmallTuple &&
+                    (uint8_t)img[1] == 2) {
+                    const size_t l0 = term_len((const uint8_t*)img.data() + 2, img.size() - 2);
+                    if ((st = reg_elem(d, (const uint8_t*)img.data() + 2, l0, &a))) break;
+                }
+                args->push_back(a);
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        d->rollback();
+        d->journal.clear();
+        return LASPJ_E_NOMEM;
+    }
+    if (st != LASPJ_DEC_OK) d->rollback();
+    d->journal.clear();
+    return st;
+}
+
+int list_register(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot) {
+    Dict* d = &dict->d;
+    d->journal.clear();
+    int st;
+    try {
+        if (term_len(img, n) != n) return LASPJ_DEC_MALFORMED;
+        st = reg_elem(d, img, n, slot);
+    } catch (const std::bad_alloc&) {
+        d->rollback();
+        d->journal.clear();
+        return LASPJ_E_NOMEM;
+    }
+    if (st) d->rollback();
+    d->journal.clear();
+    return st;
+}
+
+std::string_view list_elem_image(const laspj_dict* dict, uint32_t e) {
+    return dict->d.elems[e];
+}
+
+std::string_view list_tok_image(const laspj_dict* dict, uint64_t g) {
+    return dict->d.toks[(size_t)(g >> 6)][(size_t)(g & 63)];
+}
+
+size_t list_term_len(const uint8_t* p, size_t n) { return term_len(p, n); }
+
+// dense ranks in term order: krank per element slot, grank per token g = 64 e + k (equal
+// terms share a rank; tokens of different elements are ordered together)
+int list_ranks(const laspj_dict* dict, std::vector<uint32_t>* krank, std::vector<uint32_t>* grank) {
+    const Dict& d = dict->d;
+    const uint32_t K = (uint32_t)d.elems.size();
+    try {
+        std::vector<uint32_t> o(K);
+        for (uint32_t e = 0; e < K; ++e) o[e] = e;
+        std::stable_sort(o.begin(), o.end(), [&](uint32_t x, uint32_t y) {
+            return cmp_view(d.elems[x], d.elems[y]) < 0;
+        });
+        krank->assign(K, 0);
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < K; ++i) {
+            if (i && cmp_view(d.elems[o[i - 1]], d.elems[o[i]]) != 0) ++r;
+            (*krank)[o[i]] = r;
+        }
+        std::vector<uint64_t> g;
+        for (uint32_t e = 0; e < K; ++e)
+            for (uint32_t k = 0; k < d.toks[e].size(); ++k) g.push_back(64ull * e + k);
+        auto img = [&](uint64_t x) { return d.toks[(size_t)(x >> 6)][(size_t)(x & 63)]; };
+        std::stable_sort(g.begin(), g.end(), [&](uint64_t x, uint64_t y) {
+            return cmp_view(img(x), img(y)) < 0;
+        });
+        grank->assign(64ull * std::max<uint32_t>(K, 1), 0);
+        r = 0;
+        for (size_t i = 0; i < g.size(); ++i) {
+            if (i && cmp_view(img(g[i - 1]), img(g[i])) != 0) ++r;
+            (*grank)[g[i]] = r;
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
+// items -> term_to_binary image (131 + the list), as term_to_binary/1 writes it: LIST_EXT
+// (STRING_EXT for a G-Set list of integers 0..255, NIL_EXT when empty), {Key, Tokens}
+// 2-tuples, pair keys {X, Y}, pair tokens [Tx, Ty], flags as ATOM_EXT
+int list_write(const laspj_dict* dict, int32_t kind, const ListItems& it, std::string* out) {
+    const Dict& d = dict->d;
+    try {
+        out->clear();
+        out->push_back((char)131);
+        const size_t n = it.keys.size();
+        if (n == 0) {
+            out->push_back((char)kNil);
+            return LASPJ_OK;
+        }
+        auto key_img = [&](uint64_t k, std::string* o) {
+            if (k & kPairBit) {
+                o->push_back((char)kSmallTuple);
+                o->push_back(2);
+                o->append(d.elems[(size_t)((k >> 31) & 0x7FFFFFFFull)]);
+                o->append(d.elems[(size_t)(k & 0x7FFFFFFFull)]);
+            } else {
+                o->append(d.elems[(size_t)(k & 0x7FFFFFFFull)]);
+            }
+        };
+        auto tok = [&](uint64_t g) { return d.toks[(size_t)(g >> 6)][(size_t)(g & 63)]; };
+        if (kind == LASPJ_KIND_GSET) {
+            bool bytes = n < 65536;
+            std::vector<uint8_t> b;
+            for (size_t i = 0; bytes && i < n; ++i) {
+                uint8_t v;
+                bytes = !(it.keys[i] & kPairBit) && small_int(d.elems[(size_t)it.keys[i]], &v);
+                b.push_back(v);
+            }
+            if (bytes) {
+                out->push_back((char)kString);
+                out->push_back((char)((n >> 8) & 0xFF));
+                out->push_back((char)(n & 0xFF));
+                out->append((const char*)b.data(), n);
+                return LASPJ_OK;
+            }
+            out->push_back((char)kList);
+            put_be32(out, (uint32_t)n);
+            for (size_t i = 0; i < n; ++i) key_img(it.keys[i], out);
+            out->push_back((char)kNil);
+            return LASPJ_OK;
+        }
+        out->push_back((char)kList);
+        put_be32(out, (uint32_t)n);
+        for (size_t i = 0; i < n; ++i) {
+            out->push_back((char)kSmallTuple);
+            out->push_back(2);
+            key_img(it.keys[i], out);
+            const uint32_t a = it.toff[i], b = it.toff[i + 1];
+            if (a == b) {
+                out->push_back((char)kNil);
+                continue;
+            }
+            out->push_back((char)kList);
+            put_be32(out, b - a);
+            for (uint32_t j = a; j < b; ++j) {
+                const uint64_t t = it.toks[j];
+                out->push_back((char)kSmallTuple);
+                out->push_back(2);
+                if (t & kPairBit) {
+                    std::string_view x = tok((t >> 31) & 0x7FFFFFFFull), y = tok(t & 0x7FFFFFFFull);
+                    uint8_t vx, vy;
+                    if (small_int(x, &vx) && small_int(y, &vy)) {
+                        out->push_back((char)kString);
+                        out->push_back(0);
+                        out->push_back(2);
+                        out->push_back((char)vx);
+                        out->push_back((char)vy);
+                    } else {
+                        out->push_back((char)kList);
+                        put_be32(out, 2);
+                        out->append(x);
+                        out->append(y);
+                        out->push_back((char)kNil);
+                    }
+                } else {
+                    out->append(tok(t & 0x7FFFFFFFull));
+                }
+                static const char kTrue[7] = {100, 0, 4, 't', 'r', 'u', 'e'};
+                static const char kFalse[8] = {100, 0, 5, 'f', 'a', 'l', 's', 'e'};
+                if (t & kFlagBit) out->append(kTrue, 7);
+                else out->append(kFalse, 8);
+            }
+            out->push_back((char)kNil);
+        }
+        out->push_back((char)kNil);
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
+uint32_t list_dict_elements(const laspj_dict* dict) { return (uint32_t)dict->d.elems.size(); }
 
 }  // namespace laspj

@@ -15,6 +15,7 @@
 
 namespace laspj {
 struct NifState;                       // laspj_nif.hip
+struct ListEtfState;                   // laspj_list_etf.cpp
 void nif_destroy(laspj_ctx* ctx);      // call without ctx->mu held
 }  // namespace laspj
 
@@ -82,6 +83,8 @@ struct laspj_ctx {
     uint64_t cached_bytes = 0;
     // the NIF-level entry points' dictionary, staging and scratch (laspj_nif.hip)
     laspj::NifState* nif = nullptr;
+    // the list-image entry points' dictionary and scratch (laspj_list_etf.cpp)
+    laspj::ListEtfState* listetf = nullptr;
 };
 
 struct laspj_buf {
@@ -339,5 +342,34 @@ bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_vie
 // register the terms of the OR-Set payload elements that start in [from, to) (from: an
 // element's first byte); a DEC status (the range's registrations undone on failure)
 int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, size_t to);
+
+
+// ---- list values as images (laspj_host.cpp; used by laspj_list_etf.cpp) ---------------
+// A list value as the list kernels take it (include/laspj.h "list values"): key items
+// (element slot, or a pair {X, Y}: bit 62, x << 31 | y), each entry's token run
+// toks[toff[i], toff[i+1]) (token g = 64 e + k, bit 63 the flag; bit 62: a pair [Tx, Ty])
+struct ListItems {
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> toff;      // keys.size() + 1
+    std::vector<uint64_t> toks;
+};
+// walk a term_to_binary image (131 + a list; OR-Set: of {Key, [{Token, Bool}]}, G-Set:
+// of elements, in any order, duplicates kept) into items, registering its terms (the
+// registrations undone when it fails); args (optional): per entry the slot of the fun's
+// argument (the key; a G-Set 2-tuple element's first component).  A LASPJ_DEC_* status,
+// or LASPJ_E_NOMEM
+int list_walk(laspj_dict* dict, int32_t kind, const uint8_t* p, size_t n, ListItems* it,
+              std::vector<uint32_t>* args);
+// register one term image (no version byte) as an element; a LASPJ_DEC_* status
+int list_register(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot);
+std::string_view list_elem_image(const laspj_dict* dict, uint32_t e);
+std::string_view list_tok_image(const laspj_dict* dict, uint64_t g);
+size_t list_term_len(const uint8_t* p, size_t n);
+uint32_t list_dict_elements(const laspj_dict* dict);
+// dense term-order ranks: krank per element slot, grank per token g (64 per slot)
+int list_ranks(const laspj_dict* dict, std::vector<uint32_t>* krank, std::vector<uint32_t>* grank);
+// items -> 131 + the list as term_to_binary/1 writes it
+int list_write(const laspj_dict* dict, int32_t kind, const ListItems& it, std::string* out);
+void list_etf_destroy(laspj_ctx* ctx);     // laspj_list_etf.cpp; call without ctx->mu held
 
 }  // namespace laspj

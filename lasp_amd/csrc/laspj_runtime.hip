@@ -278,6 +278,7 @@ int laspj_ctx_create(int device, laspj_ctx** out) {
 int laspj_ctx_destroy(laspj_ctx* ctx) {
     if (!ctx) return LASPJ_E_INVAL;
     laspj::nif_destroy(ctx);
+    laspj::list_etf_destroy(ctx);
     {
         Guard g(ctx);
         hipStreamSynchronize(ctx->stream);

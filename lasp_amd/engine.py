@@ -155,6 +155,32 @@ class Context:
                  C.byref(verd)), self.h)
         return int(verd.value), (bool(res.value) if verd.value == 0 else None)
 
+    def list_etf(self, body: str, kind: str, a: bytes, b: bytes = b""):
+        """laspj_list_etf_<body> (args, map, filter, fold, union, intersection, product,
+        value) on images: (verdict, image or None)."""
+        fn = getattr(self.L, "laspj_list_etf_" + body)
+        k = _lib.KIND_GSET if kind == "gset" else _lib.KIND_ORSET
+        out, olen, verd = C.c_void_p(), C.c_uint64(), C.c_int32()
+        a = bytes(a)
+        if body in ("args", "value"):
+            check(fn(self.h, k, a, len(a), C.byref(out), C.byref(olen), C.byref(verd)), self.h)
+        else:
+            b = bytes(b)
+            check(fn(self.h, k, a, len(a), b, len(b), C.byref(out), C.byref(olen),
+                     C.byref(verd)), self.h)
+        return int(verd.value), (C.string_at(out, olen.value) if verd.value == 0 else None)
+
+    def list_etf_bind(self, kind: str, value0: bytes, value: bytes):
+        """laspj_list_etf_bind: (verdict, status, written image or None)."""
+        k = _lib.KIND_GSET if kind == "gset" else _lib.KIND_ORSET
+        out, olen, st, verd = C.c_void_p(), C.c_uint64(), C.c_int32(), C.c_int32()
+        value0, value = bytes(value0), bytes(value)
+        check(self.L.laspj_list_etf_bind(self.h, k, value0, len(value0), value, len(value),
+                                         C.byref(out), C.byref(olen), C.byref(st),
+                                         C.byref(verd)), self.h)
+        img = C.string_at(out, olen.value) if verd.value == 0 and st.value == 1 else None
+        return int(verd.value), int(st.value), img
+
     def var(self, kind: str = "orset") -> "NifVar":
         """A device-resident variable (laspj_var_create): #dv.value kept on the device."""
         return NifVar(self, kind)

@@ -4,9 +4,13 @@
  * inflation on term_to_binary images at the same time.  Uses nothing but laspj.h.
  *
  * argv[1]: a case file written by tests/test_gpu_nif.py (the oracle's answers):
- *   u32 ncases, then per case: u32 op (0 merge, 1 value, 2 equal, 3 inflation,
- *   4 strict inflation), i32 verdict, i32 result, u64 la + bytes, u64 lb + bytes,
- *   u64 lexp + bytes (the expected image for merge / value).
+ *   u32 ncases, then per case: u32 op, i32 verdict, i32 result, u64 la + bytes, u64 lb +
+ *   bytes, u64 lexp + bytes (the expected image).  op: lasp_orset images 0 merge, 1 value,
+ *   2 equal, 3 inflation, 4 strict inflation; lasp_gset images 5..9 likewise; 10 / 11 an
+ *   OR-Set / G-Set resident variable (write a, bind b: result = the bind status, exp = the
+ *   value read back); 20 + k (OR-Set) / 120 + k (G-Set) a list body from images, k = 0
+ *   union, 1 intersection, 2 product, 3 map, 4 filter, 5 fold (b = the fun's results), 6
+ *   value, 7 bind (a = Value0, b = Value, result = status, exp = the written value).
  * argv[2]: threads (default 4).  Every thread creates its own context, runs every case
  * three times in its own rotation and compares verdicts, booleans and images byte for
  * byte.  Prints "laspj NIF threads OK" and the summed counters.
@@ -79,13 +83,52 @@ static void* run(void* arg) {
             uint64_t olen = 0;
             int32_t verdict = -1, result = -1;
             int st;
-            switch (c->op) {
-            case 0: st = laspj_orset_etf_merge(ctx, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
-            case 1: st = laspj_orset_etf_value(ctx, c->a, c->la, &out, &olen, &verdict); break;
-            case 2: st = laspj_orset_etf_equal(ctx, c->a, c->la, c->b, c->lb, &result, &verdict); break;
-            default:
-                st = laspj_orset_etf_inflation(ctx, c->a, c->la, c->b, c->lb, c->op == 4,
-                                               &result, &verdict);
+            int image = 0;                  /* the answer is an image (else a boolean) */
+            const uint32_t op = c->op;
+            if (op <= 9) {
+                const int g = op >= 5;
+                const uint32_t o = g ? op - 5 : op;
+                image = o <= 1;
+                if (o == 0)
+                    st = g ? laspj_gset_etf_merge(ctx, c->a, c->la, c->b, c->lb, &out, &olen, &verdict)
+                           : laspj_orset_etf_merge(ctx, c->a, c->la, c->b, c->lb, &out, &olen, &verdict);
+                else if (o == 1)
+                    st = g ? laspj_gset_etf_value(ctx, c->a, c->la, &out, &olen, &verdict)
+                           : laspj_orset_etf_value(ctx, c->a, c->la, &out, &olen, &verdict);
+                else if (o == 2)
+                    st = g ? laspj_gset_etf_equal(ctx, c->a, c->la, c->b, c->lb, &result, &verdict)
+                           : laspj_orset_etf_equal(ctx, c->a, c->la, c->b, c->lb, &result, &verdict);
+                else
+                    st = g ? laspj_gset_etf_inflation(ctx, c->a, c->la, c->b, c->lb, o == 4,
+                                                      &result, &verdict)
+                           : laspj_orset_etf_inflation(ctx, c->a, c->la, c->b, c->lb, o == 4,
+                                                       &result, &verdict);
+            } else if (op == 10 || op == 11) {
+                laspj_var* v = NULL;
+                int32_t wv = -1, rv = -1;
+                st = laspj_var_create(ctx, op == 10 ? LASPJ_KIND_ORSET : LASPJ_KIND_GSET, &v);
+                if (st == LASPJ_OK) st = laspj_var_etf_write(v, c->a, c->la, &wv);
+                if (st == LASPJ_OK) st = laspj_var_etf_bind(v, c->b, c->lb, &result, &verdict);
+                if (st == LASPJ_OK) st = laspj_var_etf_read(v, &out, &olen, &rv);
+                if (st == LASPJ_OK && (wv != LASPJ_NIF_OK || rv != LASPJ_NIF_OK)) verdict = -2;
+                image = 2;                  /* both: the status and the value */
+                if (v) laspj_var_destroy(v);
+            } else {
+                const int32_t kind = op >= 120 ? LASPJ_KIND_GSET : LASPJ_KIND_ORSET;
+                const uint32_t k = op >= 120 ? op - 120 : op - 20;
+                image = 1;
+                switch (k) {
+                case 0: st = laspj_list_etf_union(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 1: st = laspj_list_etf_intersection(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 2: st = laspj_list_etf_product(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 3: st = laspj_list_etf_map(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 4: st = laspj_list_etf_filter(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 5: st = laspj_list_etf_fold(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &verdict); break;
+                case 6: st = laspj_list_etf_value(ctx, kind, c->a, c->la, &out, &olen, &verdict); break;
+                default:
+                    st = laspj_list_etf_bind(ctx, kind, c->a, c->la, c->b, c->lb, &out, &olen, &result, &verdict);
+                    image = result == 1 ? 2 : 3;     /* status, and the image when written */
+                }
             }
             if (st != LASPJ_OK) {
                 snprintf(w->msg, sizeof w->msg, "thread %d case %u: status %d (%s)", w->tid, i, st,
@@ -95,12 +138,12 @@ static void* run(void* arg) {
                 snprintf(w->msg, sizeof w->msg, "thread %d case %u: verdict %d, want %d", w->tid,
                          i, verdict, c->verdict);
                 w->fails++;
-            } else if (verdict == LASPJ_NIF_OK && c->op <= 1 &&
+            } else if (verdict == LASPJ_NIF_OK && (image == 1 || image == 2) &&
                        (olen != c->lexp || memcmp(out, c->exp, olen) != 0)) {
-                snprintf(w->msg, sizeof w->msg, "thread %d case %u: image differs (%llu vs %llu B)",
-                         w->tid, i, (unsigned long long)olen, (unsigned long long)c->lexp);
+                snprintf(w->msg, sizeof w->msg, "thread %d case %u (op %u): image differs (%llu vs %llu B)",
+                         w->tid, i, c->op, (unsigned long long)olen, (unsigned long long)c->lexp);
                 w->fails++;
-            } else if (verdict == LASPJ_NIF_OK && c->op >= 2 && result != c->result) {
+            } else if (verdict == LASPJ_NIF_OK && image != 1 && result != c->result) {
                 snprintf(w->msg, sizeof w->msg, "thread %d case %u: result %d, want %d", w->tid,
                          i, result, c->result);
                 w->fails++;
