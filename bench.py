@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--replicas", type=int, default=1 << 20, help="replica pairs per GPU")
     ap.add_argument("--elements", type=int, default=4096)
+    ap.add_argument("--wide-replicas", type=int, default=1 << 19,
+                    help="replicas of the T = 128 join leg (0: skip it)")
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -505,6 +507,38 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     return out
 
 
+def wide_leg(ctx, args):
+    """The join when elements carry more than 64 tokens (LASPJ_KIND_ORSET_WIDE, T = 128:
+    two {p, r} pairs per cell; add_elem mints a token per add, lasp_orset.erl:222-241,
+    261-262): the same k_or16 over twice the words, timed with HIP events."""
+    R, E, k = args.wide_replicas, args.elements, 2
+    a, b, c = (ctx.orset_wide_batch(R, E, k) for _ in range(3))
+    a.fill_synthetic(2)
+    b.fill_synthetic(3)
+    for _ in range(2):
+        c.join(a, b)
+    ev0, ev1 = ctx.event(), ctx.event()
+    ctx.synchronize()
+    steps = 10
+    ev0.record()
+    for _ in range(steps):
+        c.join(a, b)
+    ev1.record()
+    ctx.synchronize()
+    ms = ev0.elapsed_ms(ev1) / steps
+    per_elem = BYTES_PER_JOIN * k
+    achieved = per_elem * R * E / (ms / 1e3) / 1e9
+    del a, b, c
+    ctx.synchronize()
+    return {"workload": "batched OR-Set join with 128 token slots per element "
+                        "(LASPJ_KIND_ORSET_WIDE, k = 2 {p, r} pairs per cell)",
+            "replicas": R, "elements": E, "token_slots": 64 * k, "kernel_ms": ms,
+            "merged_elements_per_s": R * E / (ms / 1e3),
+            "algorithmic_bytes_per_element": per_elem,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+
+
 def load_traffic(path: str, replicas: int, elements: int):
     try:
         with open(path) as f:
@@ -612,6 +646,9 @@ def main():
         wall = float(t.item())
 
     cfg1 = config1_gpu(ctx) if rank == 0 else None
+    del a, b, c                          # free the 192 GiB of join operands first
+    ctx.synchronize()
+    wide = wide_leg(ctx, args) if rank == 0 and world == 1 and args.wide_replicas else None
 
     out = None
     if rank == 0:
@@ -644,11 +681,10 @@ def main():
         }
         if cfg1 is not None:
             out["config1_gpu"] = cfg1
+        if wide is not None:
+            out["join_t128"] = wide
 
     if ae_on:
-        del a, b, c                      # free the 192 GiB of join operands first
-        ctx.synchronize()
-
         def abandon():
             # a collective that never completes must not cost the headline line: rank 0
             # prints it with the leg marked failed; every rank then exits with status 3

@@ -66,6 +66,9 @@ extern "C" {
                                             of 32 B {pX, rX, pY, rY}                  */
 #define LASPJ_KIND_GCOUNTER      6  /* riak_dt_gcounter: R x E actor slots, uint64 count
                                        per slot (0 = actor absent from the orddict)   */
+#define LASPJ_KIND_ORSET_WIDE   10  /* OR-Set with T = 64 k token slots per element: per
+                                       (replica, slot) k {p, r} pairs (16 k bytes), token
+                                       slot t in pair t / 64, bit t % 64              */
 
 typedef struct laspj_ctx   laspj_ctx;
 typedef struct laspj_buf   laspj_buf;
@@ -80,7 +83,7 @@ typedef struct laspj_batch_info {
     uint64_t bytes_per_replica;  /* 16*E (OR-Set) or 8*ceil(E/64) (G-Set) ...          */
     uint64_t bytes;              /* R * bytes_per_replica                              */
     uint32_t elements_r;         /* ER for product batches, else 0                     */
-    uint32_t reserved;
+    uint32_t token_words;        /* k {p, r} pairs per cell (LASPJ_KIND_ORSET_WIDE), else 1 */
     uint64_t cells_per_replica;  /* E, or EL*ER for products                           */
 } laspj_batch_info;
 
@@ -100,7 +103,7 @@ typedef struct laspj_op {
     uint8_t  kind;
     uint8_t  slot;               /* token slot 0..63 (ADD on an OR-Set)                */
     uint8_t  flags;
-    uint8_t  pad;
+    uint8_t  pad;                /* LASPJ_KIND_ORSET_WIDE: token slot bits 8..15 (0 else) */
 } laspj_op;
 /* per-op status written by apply_ops */
 #define LASPJ_OPST_APPLIED   0
@@ -200,6 +203,14 @@ int      laspj_buf_device_ptr(const laspj_buf* buf, void** out);
 /* lasp_orset:new/0 (lasp_orset.erl:63-65) for R replicas over E element slots */
 int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                              laspj_batch** out);
+/* lasp_orset:new/0 (lasp_orset.erl:63-65) with T = 64 * token_words token slots per
+ * element (token_words 1..16): an element re-added many times keeps its tokens
+ * (add_elem mints one per add and never collects them, lasp_orset.erl:222-241, 261-262).
+ * The OR-Set entry points join / reduce / equal / value / removed / stats / inflation /
+ * apply_ops and bind_many / inflation_many take these batches (both operands wide with the
+ * same token_words); the combinator bodies and the codec take narrow batches only. */
+int laspj_orset_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                                  uint32_t token_words, laspj_batch** out);
 /* lasp_gset:new/0 (lasp_gset.erl:70-72) */
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out);

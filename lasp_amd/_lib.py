@@ -22,6 +22,7 @@ E_INVAL, E_NOMEM, E_DEVICE, E_SHAPE, E_KIND, E_RANGE, E_COMM, E_UNSUPPORTED, E_F
 KIND_ORSET, KIND_GSET, KIND_ORSET_CONCAT, KIND_ORSET_PRODUCT, KIND_GSET_PRODUCT = 1, 2, 3, 4, 5
 KIND_GCOUNTER = 6
 KIND_ORSET_PRODUCT_WIDE = 7
+KIND_ORSET_WIDE = 10
 KIND_ORSET_LIST, KIND_GSET_LIST = 8, 9
 LIST_PAIR = 1 << 62          # key item: {X, Y} of element slots (bits 31-61, 0-30)
 LIST_COMPOUND = 1 << 62      # token item: [Tx, Ty] of tokens (bits 31-61, 0-30)
@@ -57,7 +58,7 @@ class LaspjError(RuntimeError):
 class BatchInfo(C.Structure):
     _fields_ = [("kind", C.c_int32), ("elements", C.c_uint32), ("replicas", C.c_uint64),
                 ("bytes_per_replica", C.c_uint64), ("bytes", C.c_uint64),
-                ("elements_r", C.c_uint32), ("reserved", C.c_uint32),
+                ("elements_r", C.c_uint32), ("token_words", C.c_uint32),
                 ("cells_per_replica", C.c_uint64)]
 
 
@@ -252,6 +253,7 @@ SIGNATURES = {
                                  C.POINTER(C.c_int32)]),
     "laspj_list_etf_bind": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "laspj_orset_wide_batch_create": (i, [vp, u64, u32, u32, vpp]),
     "laspj_nif_stats": (i, [vp, vp, u32]),
     "laspj_nif_reset": (i, [vp]),
     "laspj_event_create": (i, [vp, vpp]),

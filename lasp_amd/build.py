@@ -16,7 +16,7 @@ OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "liblaspj.so")
 SOURCES = ["laspj_runtime.hip", "laspj_kernels.hip", "laspj_combinators.hip",
            "laspj_codec.hip", "laspj_lists.hip", "laspj_comm.hip",
-           "laspj_many.hip", "laspj_nif.hip", "laspj_host.cpp", "laspj_list_etf.cpp"]
+           "laspj_many.hip", "laspj_wide.hip", "laspj_nif.hip", "laspj_host.cpp", "laspj_list_etf.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-Wall", "-Wno-unused-value", "-Wno-unused-result"]

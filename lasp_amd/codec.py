@@ -105,8 +105,9 @@ class _Dict:
 class Domain:
     """Element + token dictionaries shared by all batches of one engine domain."""
 
-    def __init__(self, element_capacity: int = 1 << 30):
+    def __init__(self, element_capacity: int = 1 << 30, token_capacity: int = TOKEN_SLOTS):
         self.elements = _Dict(element_capacity)
+        self.token_capacity = token_capacity      # token slots per element (64 k when wide)
         self.tokens: List[_Dict] = []
         # element slots in the order their token dictionaries gained a slot (one entry
         # per new token): readers keep a position in it to update what they derived
@@ -115,7 +116,7 @@ class Domain:
     def element_slot(self, elem, create: bool = True) -> int:
         s = self.elements.slot(elem, create)
         while create and len(self.tokens) < len(self.elements):
-            self.tokens.append(_Dict(TOKEN_SLOTS))
+            self.tokens.append(_Dict(self.token_capacity))
         return s
 
     def token_slot(self, eslot: int, tok, create: bool = True) -> int:
@@ -129,8 +130,8 @@ class Domain:
         except EqualTerms:
             raise
         except CapacityError as e:
-            raise CapacityError(
-                f"element {self.elements.terms[eslot]!r} has more than {TOKEN_SLOTS} tokens") from e
+            raise CapacityError(f"element {self.elements.terms[eslot]!r} has more than "
+                                f"{self.token_capacity} tokens") from e
 
     @property
     def size(self) -> int:
@@ -169,6 +170,52 @@ class Domain:
                         raise NonCanonical(f"token flag {rm!r} is not a boolean")
                 out[i, es, 0] = p
                 out[i, es, 1] = r
+        return out
+
+    def token_words(self) -> int:
+        """{p, r} pairs a cell needs for the widest element's token slots (1: narrow)."""
+        most = max((len(t) for t in self.tokens), default=0)
+        return max(1, (most + 63) // 64)
+
+    def encode_orset_wide(self, states: Sequence, E: int, k: int) -> np.ndarray:
+        """orddicts -> (len(states), E, k, 2) uint64 {p, r} pairs (LASPJ_KIND_ORSET_WIDE):
+        token slot t in pair t // 64, bit t % 64."""
+        for s in states:
+            self.register_orset(s)
+        if self.size > E:
+            raise CapacityError(f"{self.size} elements do not fit {E} slots")
+        if self.token_words() > k:
+            raise CapacityError(f"tokens need {self.token_words()} words, the batch has {k}")
+        out = np.zeros((len(states), E, k, 2), dtype=np.uint64)
+        for i, s in enumerate(states):
+            _check_canonical_orset(s)
+            for elem, toks in s:
+                es = self.element_slot(elem, create=False)
+                for tok, rm in toks:
+                    t = self.token_slot(es, tok, create=False)
+                    bit = np.uint64(1 << (t % 64))
+                    out[i, es, t // 64, 0] |= bit
+                    if rm is True:
+                        out[i, es, t // 64, 1] |= bit
+                    elif rm is not False:
+                        raise NonCanonical(f"token flag {rm!r} is not a boolean")
+        return out
+
+    def decode_orset_wide(self, cells: np.ndarray) -> list:
+        """(E, k, 2) pairs -> orddict (keys and tokens ascending in term order)."""
+        out = []
+        k = cells.shape[1]
+        for es in self.elements.order():
+            if es >= cells.shape[0]:
+                continue
+            ps = [int(cells[es, j, 0]) for j in range(k)]
+            if not any(ps):
+                continue
+            rs = [int(cells[es, j, 1]) for j in range(k)]
+            td = self.tokens[es]
+            toks = [(td.terms[t], bool((rs[t // 64] >> (t % 64)) & 1))
+                    for t in (int(x) for x in td.order()) if (ps[t // 64] >> (t % 64)) & 1]
+            out.append((self.elements.terms[es], toks))
         return out
 
     def decode_orset(self, cells: np.ndarray) -> list:
@@ -445,6 +492,52 @@ class SeqOutput:
 
     def index(self) -> np.ndarray:
         return np.asarray(self.src if self.src else [0xFFFFFFFF], dtype=np.uint32)
+
+    def token_words(self) -> int:
+        """{p, r} pairs a cell needs for the widest element's token slots (1: narrow)."""
+        most = max((len(t) for t in self.tokens), default=0)
+        return max(1, (most + 63) // 64)
+
+    def encode_orset_wide(self, states: Sequence, E: int, k: int) -> np.ndarray:
+        """orddicts -> (len(states), E, k, 2) uint64 {p, r} pairs (LASPJ_KIND_ORSET_WIDE):
+        token slot t in pair t // 64, bit t % 64."""
+        for s in states:
+            self.register_orset(s)
+        if self.size > E:
+            raise CapacityError(f"{self.size} elements do not fit {E} slots")
+        if self.token_words() > k:
+            raise CapacityError(f"tokens need {self.token_words()} words, the batch has {k}")
+        out = np.zeros((len(states), E, k, 2), dtype=np.uint64)
+        for i, s in enumerate(states):
+            _check_canonical_orset(s)
+            for elem, toks in s:
+                es = self.element_slot(elem, create=False)
+                for tok, rm in toks:
+                    t = self.token_slot(es, tok, create=False)
+                    bit = np.uint64(1 << (t % 64))
+                    out[i, es, t // 64, 0] |= bit
+                    if rm is True:
+                        out[i, es, t // 64, 1] |= bit
+                    elif rm is not False:
+                        raise NonCanonical(f"token flag {rm!r} is not a boolean")
+        return out
+
+    def decode_orset_wide(self, cells: np.ndarray) -> list:
+        """(E, k, 2) pairs -> orddict (keys and tokens ascending in term order)."""
+        out = []
+        k = cells.shape[1]
+        for es in self.elements.order():
+            if es >= cells.shape[0]:
+                continue
+            ps = [int(cells[es, j, 0]) for j in range(k)]
+            if not any(ps):
+                continue
+            rs = [int(cells[es, j, 1]) for j in range(k)]
+            td = self.tokens[es]
+            toks = [(td.terms[t], bool((rs[t // 64] >> (t % 64)) & 1))
+                    for t in (int(x) for x in td.order()) if (ps[t // 64] >> (t % 64)) & 1]
+            out.append((self.elements.terms[es], toks))
+        return out
 
     def decode_orset(self, cells: np.ndarray) -> list:
         out = []

@@ -104,6 +104,7 @@ struct laspj_batch {
     uint64_t words_per_replica = 0;  // u64 words: 2E (OR-Set) or ceil(E/64) (G-Set) ...
     uint32_t elements_r = 0;    // ER of product batches
     uint64_t cells = 0;         // cells per replica: E, or EL*ER for products
+    uint32_t tok_words = 1;     // {p, r} pairs per cell (LASPJ_KIND_ORSET_WIDE), else 1
     uint64_t* dev = nullptr;
     bool owns = true;           // false for laspj_batch_wrap
     mutable bool exported = false;  // laspj_batch_device_ptr handed out the address
@@ -239,6 +240,13 @@ hipError_t launch_orset_gather(laspj_ctx* ctx, laspj_batch* dst, const laspj_bat
                                const uint32_t* index);
 hipError_t launch_and(laspj_ctx* ctx, uint64_t* dst, const uint64_t* a, const uint64_t* b,
                       uint64_t words);
+// LASPJ_KIND_ORSET_WIDE (laspj_wide.hip)
+hipError_t launch_wide_value(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out, bool removed);
+hipError_t launch_wide_stats(laspj_ctx* ctx, const laspj_batch* b, uint64_t* out);
+hipError_t launch_wide_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_batch* cur,
+                                 bool strict, uint8_t* out);
+hipError_t launch_wide_apply(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
+                             int32_t* status);
 hipError_t launch_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                               const uint64_t* keep);
 hipError_t launch_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,

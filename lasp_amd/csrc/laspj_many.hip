@@ -97,6 +97,14 @@ __global__ __launch_bounds__(256) void k_inflation_many(const MItem* items, uint
                 np += pp != 0;
                 nc += cp != 0;
             }
+        } else if (it.kind == LASPJ_KIND_ORSET_WIDE) {
+            // {p, r} pairs, k per element: inflation = every Prev token in Cur; strict =
+            // and some pair differs (a common element's tokens or an element new in Cur)
+            for (uint64_t w = lo + 2 * lane; w + 1 < hi; w += 128) {
+                const u64 pp = it.a[w], pr = it.a[w + 1], cp = it.b[w], cr = it.b[w + 1];
+                viol |= (pp & ~cp) != 0;
+                changed |= (pp != cp) | (pr != cr);
+            }
         } else if (it.kind == LASPJ_KIND_GSET) {
             for (uint64_t w = lo + lane; w < hi; w += 64) {
                 const u64 p = it.a[w], c = it.b[w];
@@ -137,7 +145,7 @@ __global__ void k_inflation_many_finish(const MItem* items, uint32_t n, int stri
         if (strict) {
             const int32_t k = items[i].kind;
             if (k == LASPJ_KIND_ORSET) res = infl && ((f & 2) || np < nc);   // [] case: np < nc
-            else if (k == LASPJ_KIND_GSET) res = infl && (f & 2);
+            else if (k == LASPJ_KIND_GSET || k == LASPJ_KIND_ORSET_WIDE) res = infl && (f & 2);
             else res = np < nc;                                              // value(P) < value(C)
         }
         out[i] = res ? 1 : 0;
@@ -158,7 +166,8 @@ struct MGuard {
 };
 
 bool many_kind(int32_t k) {
-    return k == LASPJ_KIND_ORSET || k == LASPJ_KIND_GSET || k == LASPJ_KIND_GCOUNTER;
+    return k == LASPJ_KIND_ORSET || k == LASPJ_KIND_GSET || k == LASPJ_KIND_GCOUNTER ||
+           k == LASPJ_KIND_ORSET_WIDE;
 }
 
 // validate the triples / pairs and build the descriptors; returns the segment count

@@ -49,7 +49,8 @@ int check_pair(laspj_ctx* ctx, const laspj_batch* x, const laspj_batch* y, int32
     if (x->kind != kind || y->kind != kind)
         return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind (%d, %d; want %d)", what, x->kind,
                     y->kind, kind);
-    if (x->elements != y->elements || x->replicas != y->replicas)
+    if (x->elements != y->elements || x->replicas != y->replicas ||
+        x->words_per_replica != y->words_per_replica)
         return fail(ctx, LASPJ_E_SHAPE, "%s: shapes differ (%llu x %u vs %llu x %u)", what,
                     (unsigned long long)x->replicas, x->elements,
                     (unsigned long long)y->replicas, y->elements);
@@ -75,6 +76,7 @@ uint64_t words_per(int32_t kind, uint32_t elements, uint32_t er) {
         case LASPJ_KIND_GSET_PRODUCT: return (uint64_t)elements * ((er + 63ull) / 64ull);
         case LASPJ_KIND_GCOUNTER: return elements;
         case LASPJ_KIND_ORSET_PRODUCT_WIDE: return 4ull * elements * er;
+        case LASPJ_KIND_ORSET_WIDE: return 2ull * elements * er;        // er: token words
     }
     return 0;
 }
@@ -97,6 +99,7 @@ int batch_create(laspj_ctx* ctx, int32_t kind, uint64_t replicas, uint32_t eleme
     b->kind = kind;
     b->elements = elements;
     b->elements_r = is_product(kind) ? er : 0;
+    b->tok_words = kind == LASPJ_KIND_ORSET_WIDE ? er : 1;
     b->cells = is_product(kind) ? (uint64_t)elements * er : elements;
     b->replicas = replicas;
     b->words_per_replica = words_per(kind, elements, er);
@@ -494,6 +497,13 @@ int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t element
     return batch_create(ctx, LASPJ_KIND_ORSET, replicas, elements, out);
 }
 
+int laspj_orset_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
+                                  uint32_t token_words, laspj_batch** out) {
+    if (token_words < 1 || token_words > 16)
+        return fail(ctx, LASPJ_E_INVAL, "orset_wide_batch_create: token words must be 1..16");
+    return batch_create(ctx, LASPJ_KIND_ORSET_WIDE, replicas, elements, out, token_words);
+}
+
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out) {
     return batch_create(ctx, LASPJ_KIND_GSET, replicas, elements, out);
@@ -586,7 +596,7 @@ int laspj_batch_info_get(const laspj_batch* b, laspj_batch_info* out) {
     out->bytes_per_replica = b->words_per_replica * 8ull;
     out->bytes = laspj::bytes_of(b);
     out->elements_r = b->elements_r;
-    out->reserved = 0;
+    out->token_words = b->tok_words;
     out->cells_per_replica = b->cells;
     return LASPJ_OK;
 }
@@ -670,9 +680,20 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
                                uint64_t replica_base) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "fill_synthetic: bad argument");
     if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_GSET &&
-        b->kind != LASPJ_KIND_GCOUNTER)
+        b->kind != LASPJ_KIND_GCOUNTER && b->kind != LASPJ_KIND_ORSET_WIDE)
         return fail(ctx, LASPJ_E_KIND, "fill_synthetic: OR-Set, G-Set or G-Counter batches only");
     Guard g(ctx);
+    if (b->kind == LASPJ_KIND_ORSET_WIDE) {
+        // pair j of element e = the narrow stream's cell e k + j (bench data)
+        laspj_batch v = *b;
+        v.kind = LASPJ_KIND_ORSET;
+        v.elements = b->elements * b->tok_words;
+        v.cells = v.elements;
+        v.tok_words = 1;
+        v.owns = false;
+        LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, &v, seed, replica_base));
+        return LASPJ_OK;
+    }
     LJ_HIP(ctx, laspj::launch_fill_synthetic(ctx, b, seed, replica_base));
     return LASPJ_OK;
 }
@@ -743,8 +764,15 @@ int laspj_orset_gather_inflation_keyed(laspj_ctx* ctx, laspj_batch* dst, const l
 
 // ------------------------------------------------------------------------- joins
 
+// the OR-Set entry points take wide batches too (the same words, k pairs per cell)
+static int32_t orset_kind(const laspj_batch* a, int32_t kind) {
+    return kind == LASPJ_KIND_ORSET && a && a->kind == LASPJ_KIND_ORSET_WIDE
+               ? LASPJ_KIND_ORSET_WIDE : kind;
+}
+
 static int join_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b, int32_t kind, const char* what) {
+    kind = orset_kind(a, kind);
     if (int s = check_pair(ctx, a, b, kind, what)) return s;
     if (int s = check_pair(ctx, dst, a, kind, what)) return s;
     Guard g(ctx);
@@ -789,9 +817,11 @@ static int reduce_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                        uint32_t group, int32_t kind, const char* what) {
     if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
         return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    kind = orset_kind(src, kind);
     if (dst->kind != kind || src->kind != kind)
         return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
     if (group == 0 || dst->elements != src->elements ||
+        dst->words_per_replica != src->words_per_replica ||
         dst->replicas * (uint64_t)group != src->replicas)
         return fail(ctx, LASPJ_E_SHAPE, "%s: need src replicas = dst replicas * group", what);
     if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "%s: dst aliases src", what);
@@ -816,7 +846,7 @@ int laspj_gset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
 static int value_impl(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out, bool removed) {
     const char* what = removed ? "orset_removed" : "orset_value";
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
-    bool ok_kind = b->kind == LASPJ_KIND_ORSET ||
+    bool ok_kind = b->kind == LASPJ_KIND_ORSET || b->kind == LASPJ_KIND_ORSET_WIDE ||
                    (!removed && (b->kind == LASPJ_KIND_ORSET_CONCAT ||
                                  b->kind == LASPJ_KIND_ORSET_PRODUCT ||
                                  b->kind == LASPJ_KIND_ORSET_PRODUCT_WIDE));
@@ -824,7 +854,10 @@ static int value_impl(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out, bool
     uint64_t need = b->replicas * ((b->cells + 63ull) / 64ull) * 8ull;
     if (int s = check_buf(ctx, out, need, what)) return s;
     Guard g(ctx);
-    LJ_HIP(ctx, laspj::launch_orset_value(ctx, b, static_cast<uint64_t*>(out->dev), removed));
+    if (b->kind == LASPJ_KIND_ORSET_WIDE)
+        LJ_HIP(ctx, laspj::launch_wide_value(ctx, b, static_cast<uint64_t*>(out->dev), removed));
+    else
+        LJ_HIP(ctx, laspj::launch_orset_value(ctx, b, static_cast<uint64_t*>(out->dev), removed));
     return LASPJ_OK;
 }
 
@@ -838,10 +871,14 @@ int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
 
 int laspj_orset_stats(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "orset_stats: bad batch");
-    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "orset_stats: not an OR-Set");
+    if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_ORSET_WIDE)
+        return fail(ctx, LASPJ_E_KIND, "orset_stats: not an OR-Set");
     if (int s = check_buf(ctx, out, b->replicas * 24ull, "orset_stats")) return s;
     Guard g(ctx);
-    LJ_HIP(ctx, laspj::launch_orset_stats(ctx, b, static_cast<uint64_t*>(out->dev)));
+    if (b->kind == LASPJ_KIND_ORSET_WIDE)
+        LJ_HIP(ctx, laspj::launch_wide_stats(ctx, b, static_cast<uint64_t*>(out->dev)));
+    else
+        LJ_HIP(ctx, laspj::launch_orset_stats(ctx, b, static_cast<uint64_t*>(out->dev)));
     return LASPJ_OK;
 }
 
@@ -856,6 +893,7 @@ int laspj_gset_stats(laspj_ctx* ctx, const laspj_batch* b, laspj_buf* out) {
 
 static int equal_impl(laspj_ctx* ctx, const laspj_batch* a, const laspj_batch* b,
                       laspj_buf* out, int32_t kind, const char* what) {
+    kind = orset_kind(a, kind);
     if (int s = check_pair(ctx, a, b, kind, what)) return s;
     if (int s = check_buf(ctx, out, a->replicas, what)) return s;
     Guard g(ctx);
@@ -877,14 +915,18 @@ static int inflation_impl(laspj_ctx* ctx, const laspj_batch* prev, const laspj_b
                           int strict, laspj_buf* out, int32_t kind, const char* what) {
     if (!same_ctx(ctx, prev) || !same_ctx(ctx, cur))
         return fail(ctx, LASPJ_E_INVAL, "%s: bad batch", what);
+    kind = orset_kind(cur, kind);
     if (prev->kind != kind || cur->kind != kind)
         return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
-    if (prev->elements != cur->elements ||
+    if (prev->elements != cur->elements || prev->tok_words != cur->tok_words ||
         !(prev->replicas == cur->replicas || prev->replicas == 1))
         return fail(ctx, LASPJ_E_SHAPE, "%s: prev must have cur's replicas or 1", what);
     if (int s = check_buf(ctx, out, cur->replicas, what)) return s;
     Guard g(ctx);
-    if (kind == LASPJ_KIND_ORSET)
+    if (kind == LASPJ_KIND_ORSET_WIDE)
+        LJ_HIP(ctx, laspj::launch_wide_inflation(ctx, prev, cur, strict != 0,
+                                                 static_cast<uint8_t*>(out->dev)));
+    else if (kind == LASPJ_KIND_ORSET)
         LJ_HIP(ctx, laspj::launch_orset_inflation(ctx, prev, cur, strict != 0,
                                                   static_cast<uint8_t*>(out->dev)));
     else
@@ -909,7 +951,9 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
                           int32_t* status, int32_t kind, const char* what) {
     if (!same_ctx(ctx, b) || (!ops && nops))
         return fail(ctx, LASPJ_E_INVAL, "%s: bad argument", what);
+    kind = orset_kind(b, kind);
     if (b->kind != kind) return fail(ctx, LASPJ_E_KIND, "%s: wrong batch kind", what);
+    const uint32_t tslots = 64u * b->tok_words;
     // Host-side validation: every op addresses a real cell and the list is grouped by
     // replica, which is what the one-thread-per-replica-run kernel relies on.
     for (uint64_t i = 0; i < nops; ++i) {
@@ -918,9 +962,12 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
             return fail(ctx, LASPJ_E_RANGE, "%s: op %llu addresses (%llu, %u) outside %llu x %u",
                         what, (unsigned long long)i, (unsigned long long)o.replica, o.element,
                         (unsigned long long)b->replicas, b->elements);
-        if (o.slot >= 64) return fail(ctx, LASPJ_E_RANGE, "%s: op %llu token slot >= 64", what,
-                                      (unsigned long long)i);
-        bool ok_kind = kind == LASPJ_KIND_ORSET
+        const uint32_t tslot = kind == LASPJ_KIND_ORSET_WIDE ? (uint32_t)o.slot | ((uint32_t)o.pad << 8)
+                                                              : o.slot;
+        if (tslot >= tslots || (kind != LASPJ_KIND_ORSET_WIDE && o.pad))
+            return fail(ctx, LASPJ_E_RANGE, "%s: op %llu token slot %u >= %u", what,
+                        (unsigned long long)i, tslot, tslots);
+        bool ok_kind = kind == LASPJ_KIND_ORSET || kind == LASPJ_KIND_ORSET_WIDE
                            ? (o.kind == LASPJ_OP_ADD || o.kind == LASPJ_OP_REMOVE ||
                               o.kind == LASPJ_OP_INSERT)
                            : o.kind == LASPJ_OP_ADD;
@@ -955,7 +1002,10 @@ static int apply_ops_impl(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, u
     auto* dst = reinterpret_cast<int32_t*>(dops + nops);
     LJ_HIP(ctx, hipMemcpyAsync(dops, ops, nops * sizeof(laspj_op), hipMemcpyHostToDevice,
                                ctx->stream));
-    LJ_HIP(ctx, laspj::launch_apply_ops(ctx, b, dops, nops, dst));
+    if (kind == LASPJ_KIND_ORSET_WIDE)
+        LJ_HIP(ctx, laspj::launch_wide_apply(ctx, b, dops, nops, dst));
+    else
+        LJ_HIP(ctx, laspj::launch_apply_ops(ctx, b, dops, nops, dst));
     if (status) LJ_HIP(ctx, laspj::readback(ctx, status, dst, nops * sizeof(int32_t)));
     return LASPJ_OK;
 }

@@ -80,6 +80,10 @@ class Context:
     def orset_batch(self, replicas: int, elements: int) -> "ORSetBatch":
         return ORSetBatch(self, replicas, elements)
 
+    def orset_wide_batch(self, replicas: int, elements: int,
+                         token_words: int) -> "ORSetWideBatch":
+        return ORSetWideBatch(self, replicas, elements, token_words)
+
     def gset_batch(self, replicas: int, elements: int) -> "GSetBatch":
         return GSetBatch(self, replicas, elements)
 
@@ -664,6 +668,49 @@ def _wrap(self, ctx: Context, tensor, replicas: int, elements: int, bytes_per_re
     self.replicas, self.elements = replicas, elements
     self.bytes_per_replica = bytes_per_replica
     self.nbytes = nbytes
+
+
+class ORSetWideBatch(ORSetBatch):
+    """R replicas of an OR-Set with T = 64 k token slots per element
+    (LASPJ_KIND_ORSET_WIDE): k {p, r} pairs per cell, token slot t in pair t // 64.  Join,
+    reduce, equal, value/removed, stats, inflation and update/3 take it; the combinator
+    bodies and the codec take narrow batches only."""
+
+    kind = _lib.KIND_ORSET_WIDE
+
+    def __init__(self, ctx: Context, replicas: int, elements: int, token_words: int):
+        self.ctx = ctx
+        self.token_words = token_words
+        h = C.c_void_p()
+        check(ctx.L.laspj_orset_wide_batch_create(ctx.h, replicas, elements, token_words,
+                                                  C.byref(h)), ctx.h)
+        self.h = h
+        self._pool_key = None
+        self.replicas, self.elements = replicas, elements
+        info = _lib.BatchInfo()
+        check(ctx.L.laspj_batch_info_get(self.h, C.byref(info)))
+        self.bytes_per_replica, self.nbytes = info.bytes_per_replica, info.bytes
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """(count, E, k, 2) uint64 array of {p, r} pairs."""
+        w = self.download_words(first, count)
+        return w.reshape(w.shape[0], self.elements, self.token_words, 2)
+
+    def apply_ops(self, ops: Sequence[tuple], statuses: bool = True):
+        """ops: (replica, element_slot, OP_*, token_slot 0 .. 64 k - 1, flags)."""
+        n = len(ops)
+        arr = (_lib.Op * max(n, 1))()
+        for i, (rep, elem, kind, slot, flags) in enumerate(ops):
+            arr[i].replica, arr[i].element, arr[i].kind = rep, elem, kind
+            arr[i].slot, arr[i].flags, arr[i].pad = slot & 255, flags, slot >> 8
+        fn = self.ctx.L.laspj_orset_apply_ops
+        if not statuses:
+            check(fn(self.ctx.h, self.h, arr, n, None), self.ctx.h)
+            return None
+        status = np.zeros((max(n, 1),), dtype=np.int32)
+        check(fn(self.ctx.h, self.h, arr, n, status.ctypes.data_as(C.POINTER(C.c_int32))),
+              self.ctx.h)
+        return status[:n]
 
 
 class WrappedORSetBatch(ORSetBatch):
