@@ -160,14 +160,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         batches walked by the scalar unit (the lanes
                                         find element starts by default), 7 = no element
                                         batches for many-token dictionaries (one element
-                                        at a time), 8 = the same as 0, 9 = block
-                                        decoders: OR-Set many-token dictionaries one
-                                        thread per element or record, G-Set integer
-                                        payloads by composed tag-length maps (both
-                                        slower than the default), 10 = as
-                                        0, with segment mode's redo pass as a launch of
-                                        its own (by default the chain check's wave decodes
-                                        a payload that failed it again itself)          */
+                                        at a time), 8 = the same as 0, 10 = as 0, with
+                                        segment mode's redo pass as a launch of its own
+                                        (by default the chain check's wave decodes a
+                                        payload that failed it again itself)           */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

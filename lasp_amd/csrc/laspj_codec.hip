@@ -88,10 +88,6 @@ struct laspj_etf_dict {
     const uint64_t* gs_itab = nullptr;
     int64_t gs_ilo = 0;
     uint32_t gs_in = 0;
-    // the item decoder's per-rank bucket tables (E x 1024 bytes: bucket -> term rank), built
-    // on the device the first time a batch needs them (k_build_btab); own allocation
-    uint8_t* rd_btab = nullptr;
-    bool btab_tried = false;
     // host-side state for laspj::etf_dict_patch (dictionaries built with token headroom,
     // the NIF path's): slot -> rank, each token slot's padded image offset (0xFFFFFFFF:
     // none), where the patched arrays sit in the block, the padded-image area's use
@@ -3221,375 +3217,6 @@ __global__ __launch_bounds__(64) void k_etf_read_chain(const uint8_t* payload, u
     }
 }
 
-// ---- many-token payloads: one block per payload, one thread per item (round 4)
-//
-// The wave decoders above pay a fixed sequence per element (header match, bucket table,
-// mark scan, one validation pass, presence ballot): at ~32 tokens per element that
-// sequence, not the records, is most of the time (round 3, tools/decoder_probe.py).  Here
-// nothing is per element on the critical path.  A block stages an 8 KiB window of its
-// payload into LDS (coalesced) and lists every `104 2` in it — every element and every
-// record starts with that 2-tuple header — in stream order, one block-wide scan.  An item
-// right after a 106 (the previous element's closing nil), or at the cursor, is an element
-// candidate: its header 104 2 <elem image> 108 resolves to a dictionary rank by the
-// header hash (exact 64-byte compare), its count must be 1..64 and at most the rank's
-// tokens.  Every other item takes the latest valid element before it as its owner and is
-// validated as one of its records on its own thread: token bucket -> term rank through a
-// per-rank bucket table in global memory (btab), exact template compare, flag atom.  A
-// token image may hold `104 2` or `106 104 2`; such a false item almost never validates,
-// and is then simply not an item.  The chain is then checked on the compacted valid items
-// alone, every check between neighbours: the first is the element at the cursor; an
-// element's first record starts right after its count; each record ends where the next
-// begins, with a higher term rank; the last record of an element ends on a 106 right
-// before the next element; element ranks ascend (from the previous window's last); each
-// element has exactly its count of records.  The window's last element may be cut off:
-// it is decoded again as the first of the next window, unless the window holds the
-// payload's end, where the list must close (106) on the last byte and the element count
-// equal the header's.  Any failing check before that (a malformed payload, an unknown
-// term, a false item that validated) sends the whole payload to the redo list, which the
-// wave decoder takes with its cells cleared — so statuses and cells are the wave
-// decoder's by construction, and the fuzz tests compare both.
-constexpr uint32_t kIW = 8192;      // window bytes (32 per thread)
-constexpr uint32_t kIT = 512;       // items per window (two per thread)
-constexpr uint32_t kIE = 64;        // elements per window
-constexpr uint32_t kIBuckets = kBuckets;
-
-struct ItemLds {
-    uint8_t buf[kIW + 80];     // the window, then slack for reads past a start (zero)
-    uint16_t pos[kIT];         // item starts (window offsets), stream order
-    uint16_t iend[kIT];        // element: its first record's start; record: one past its flag
-    uint16_t vl[kIT];          // valid items, compacted
-    uint16_t ecl[kIT];         // element candidates (item indices)
-    int32_t irk[kIT];          // element: rank; record: term rank
-    uint8_t ik[kIT];           // 0 not an item, 1 element, 2 record (true), 3 record (false)
-    uint8_t iown[kIT];         // owning element (window index), 0xFF none, 0xFE dropped
-    uint8_t im[kIT];           // element: its count
-    uint32_t islot[kIT];       // element: its slot
-    uint32_t ikey[kIT];        // element: its bucket word | shift << 8
-    uint16_t elist[kIE];       // element -> item
-    uint16_t ecj[kIE];         // element -> compacted index
-    int32_t erk[kIE];
-    uint32_t eslot[kIE], ekey[kIE], em[kIE];
-    u64 pm[kIE], tm[kIE];      // presence / true bits by token slot
-    uint32_t sc[8];
-};
-
-// 4 bits: which bytes of T are zero
-__device__ __forceinline__ uint32_t zbytes4(uint32_t T) {
-    const uint32_t z = ~(((T & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | T) & 0x80808080u;
-    return (((z >> 7) * 0x204081u) >> 21) & 0xFu;
-}
-
-// hdr_rank over the item decoder's window (per thread)
-__device__ __forceinline__ int64_t hdr_rank_items(const uint8_t* buf, uint32_t s, uint32_t lim,
-                                                  const HdrHash& hh, const ReadTabs& t,
-                                                  uint32_t E, uint32_t& hl) {
-    int64_t rk = -1;
-    u64 lens = hh.lens;
-    {
-        const uint32_t b2 = buf[min(s + 2u, kIW + 63u)];
-        const uint32_t h0 = word_at(buf, min(s + 3u, kIW + 64u));
-        uint32_t il = 0;
-        if (b2 == 97) il = 2;                                        // SMALL_INTEGER_EXT
-        else if (b2 == 98) il = 5;                                   // INTEGER_EXT
-        else if (b2 == 109) il = 5u + __builtin_bswap32(h0);         // BINARY_EXT
-        else if (b2 == 100 || b2 == 118)                             // ATOM(_UTF8)_EXT
-            il = 3u + (((h0 & 0xFFu) << 8) | ((h0 >> 8) & 0xFFu));
-        else if (b2 == 115 || b2 == 119 || b2 == 110) il = 2u + (h0 & 0xFFu) + (b2 == 110);
-        if (il) lens = il <= 61u ? lens & (1ull << (il + 2u)) : 0ull;   // hl = il + 3
-    }
-    while (lens && rk < 0) {
-        const uint32_t L2 = (uint32_t)__ffsll((long long)lens);
-        lens &= lens - 1ull;
-        if (s + L2 > lim) break;
-        uint32_t q[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        uint32_t h = L2 * 0x85EBCA6Bu;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int rem = (int)L2 - 4 * i;
-            if (rem <= 0) break;
-            const uint32_t v = word_at(buf, min(s + 4u * i, kIW + 64u));
-            q[i] = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);
-            h = hdr_mix(h, q[i]);
-        }
-        for (uint32_t i = h & hh.mask;; i = (i + 1) & hh.mask) {
-            const uint32_t v = hh.tab[i];
-            if (!v || v > E) break;
-            const uint32_t r = v - 1u;
-            const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * r);
-            bool eq = true;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if ((uint32_t)(16 * j) >= L2) break;
-                const u32x4 a = tp[j];
-                eq &= a.x == q[4 * j] && a.y == q[4 * j + 1] && a.z == q[4 * j + 2] &&
-                      a.w == q[4 * j + 3];
-            }
-            if (eq) { rk = r; hl = L2; break; }
-        }
-    }
-    return rk;
-}
-
-// btab: by element rank r, 1024 bytes: bucket -> term rank (0xFF: none)
-__global__ __launch_bounds__(kBlock) void k_build_btab(const uint4* desc, const uint16_t* tb,
-                                                       uint32_t E, uint32_t RK, uint8_t* btab) {
-    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < (uint64_t)E * 64;
-         g += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t r = g >> 6;
-        const uint32_t j = (uint32_t)(g & 63u);
-        if (j < RK && j < desc[r].w) btab[r * kIBuckets + tb[r * RK + j]] = (uint8_t)j;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_orset_etf_read_items(
-    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
-    ReadTabs tabs, HdrHash hh, const uint8_t* btab, int tag, int vers, u64x2* cells,
-    int32_t* status, uint32_t* redo) {
-    __shared__ __attribute__((aligned(16))) ItemLds S;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t RL = d.rec_len, RS = d.rec_stride, RK = d.tok_max;
-    if (tid < 20) reinterpret_cast<uint32_t*>(S.buf + kIW)[tid] = 0u;
-    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
-        const u64 base = offs[rep], aend = offs[rep + 1];
-        const u64 len = aend - base;
-        u64x2* c = cells + rep * E;
-        // head: [tag vers] 131 108 <count:4>; 131 106 is the empty set; anything else
-        // goes to the wave decoder for its status
-        bool ok = true, fin = false;
-        uint32_t x = 0, n = 0;
-        {
-            const uint8_t* p = payload + base;
-            if (tag >= 0) {
-                ok = len >= 2 && p[0] == (uint8_t)tag && p[1] == (uint8_t)vers;
-                x = 2;
-            }
-            if (ok && len >= x + 2 && p[x] == 131 && p[x + 1] == 106 && len == x + 2) {
-                fin = true;
-            } else if (ok && len >= x + 6 && p[x] == 131 && p[x + 1] == 108) {
-                n = ((uint32_t)p[x + 2] << 24) | ((uint32_t)p[x + 3] << 16) |
-                    ((uint32_t)p[x + 4] << 8) | p[x + 5];
-                x += 6;
-                ok = n >= 1;
-            } else {
-                ok = false;
-            }
-        }
-        int64_t prev = -1;
-        uint32_t got = 0;
-        while (ok && !fin) {
-            const u64 lo = (base + x) & ~15ull;
-            const uint32_t x0 = (uint32_t)(base + x - lo);
-            const uint32_t nst = (uint32_t)min((u64)kIW, total - lo);
-            const uint32_t hi = (uint32_t)min((u64)nst, aend - lo);
-            __syncthreads();                       // the previous window's readers are done
-            for (uint32_t v = tid; v < kIW / 16; v += kBlock) {
-                u32x4 q = {0u, 0u, 0u, 0u};
-                if (16u * v + 16u <= nst) {
-                    q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(payload + lo) + v);
-                } else if (16u * v < nst) {
-                    uint32_t wv[4] = {0u, 0u, 0u, 0u};
-                    for (uint32_t b = 16u * v; b < nst; ++b)
-                        wv[(b >> 2) & 3u] |= (uint32_t)payload[lo + b] << (8u * (b & 3u));
-                    q = u32x4{wv[0], wv[1], wv[2], wv[3]};
-                }
-                reinterpret_cast<u32x4*>(S.buf)[v] = q;
-            }
-            if (tid < kIE) S.pm[tid] = S.tm[tid] = 0ull;
-            if (tid == 0) S.sc[7] = 0u;
-            __syncthreads();
-            // 1. items: positions q of `104 2` with x0 <= q, q + 1 < hi
-            const uint32_t* b32 = reinterpret_cast<const uint32_t*>(S.buf);
-            uint32_t mk = 0, emk = 0;
-            {
-                uint32_t dp = tid ? b32[8 * tid - 1] : 0u;
-                uint32_t d0 = b32[8 * tid];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t d1 = b32[8 * tid + i + 1];
-                    const uint32_t nx = __builtin_amdgcn_alignbyte(d1, d0, 1);   // b[q + 1]
-                    const uint32_t pv = __builtin_amdgcn_alignbyte(d0, dp, 3);   // b[q - 1]
-                    mk |= zbytes4((d0 ^ 0x68686868u) | (nx ^ 0x02020202u)) << (4 * i);
-                    emk |= zbytes4(pv ^ 0x6A6A6A6Au) << (4 * i);
-                    dp = d0;
-                    d0 = d1;
-                }
-            }
-            const int32_t q0 = 32 * (int32_t)tid;
-            {
-                const int32_t a = (int32_t)x0 - q0, bnd = (int32_t)hi - 1 - q0;
-                if (bnd <= 0) mk = 0u;
-                else if (bnd < 32) mk &= (1u << bnd) - 1u;
-                if (a >= 32) mk = 0u;
-                else if (a > 0) mk &= ~((1u << a) - 1u);
-                emk &= mk;
-                if (a >= 0 && a < 32) emk |= mk & (1u << a);            // the cursor
-            }
-            uint32_t tot;
-            const uint32_t before = block_excl_scan((uint32_t)__popc(mk) | ((uint32_t)__popc(emk) << 16),
-                                                    S.sc, &tot);
-            const uint32_t ni_all = tot & 0xFFFFu;
-            const uint32_t nit = min(ni_all, kIT);
-            {
-                uint32_t k = before & 0xFFFFu, ek = before >> 16, m = mk;
-                while (m && k < kIT) {
-                    const uint32_t b = (uint32_t)__ffs(m) - 1u;
-                    m &= m - 1u;
-                    const bool isE = (emk >> b) & 1u;
-                    S.pos[k] = (uint16_t)(q0 + (int32_t)b);
-                    S.ik[k] = isE ? 0x80 : 0;
-                    if (isE) {
-                        S.ecl[ek] = (uint16_t)k;
-                        atomicMax(&S.sc[7], ek + 1u);
-                        ++ek;
-                    }
-                    ++k;
-                }
-            }
-            __syncthreads();
-            // 2. element candidates: rank by the header hash, then the count
-            const uint32_t nec = S.sc[7];
-            for (uint32_t j = tid; j < nec; j += kBlock) {
-                const uint32_t i = S.ecl[j], s = S.pos[i];
-                uint32_t hl = 0;
-                const int64_t rk = hdr_rank_items(S.buf, s, hi, hh, tabs, E, hl);
-                uint8_t kind = 0;
-                if (rk >= 0 && s + hl + 4u <= hi) {
-                    const uint32_t m = __builtin_bswap32(word_at(S.buf, s + hl));
-                    const uint4 ds = tabs.desc[rk];
-                    if (m >= 1u && m <= ds.w && ds.w <= 64u) {
-                        kind = 1;
-                        S.irk[i] = (int32_t)rk;
-                        S.im[i] = (uint8_t)m;
-                        S.iend[i] = (uint16_t)(s + hl + 4u);
-                        S.islot[i] = ds.x;
-                        S.ikey[i] = ds.z;
-                    }
-                }
-                S.ik[i] = kind;
-            }
-            __syncthreads();
-            // 3. owners: the latest valid element at or before each item (pairs of items
-            // per thread keep stream order in the scan)
-            const uint32_t i0 = 2u * tid, i1 = i0 + 1u;
-            const uint32_t f0 = i0 < nit && S.ik[i0] == 1, f1 = i1 < nit && S.ik[i1] == 1;
-            uint32_t etot;
-            const uint32_t eb = block_excl_scan(f0 + f1, S.sc, &etot);
-            const uint32_t nE = min(etot, kIE);
-#pragma unroll
-            for (uint32_t h = 0; h < 2; ++h) {
-                const uint32_t i = i0 + h;
-                if (i >= nit) continue;
-                const int32_t own = (int32_t)(eb + f0 + (h ? f1 : 0u)) - 1;
-                S.iown[i] = own < 0 ? 0xFF : own < (int32_t)kIE ? (uint8_t)own : 0xFE;
-                if ((h ? f1 : f0) && own < (int32_t)kIE) {
-                    S.elist[own] = (uint16_t)i;
-                    S.erk[own] = S.irk[i];
-                    S.em[own] = S.im[i];
-                    S.eslot[own] = S.islot[i];
-                    S.ekey[own] = S.ikey[i];
-                }
-            }
-            __syncthreads();
-            // 4. records, each on its own thread
-            for (uint32_t i = tid; i < nit; i += kBlock) {
-                const uint32_t l = S.iown[i];
-                if (S.ik[i] == 1) {
-                    if (l >= kIE) S.ik[i] = 0;                          // dropped element
-                    continue;
-                }
-                uint8_t kind = 0;
-                if (l < kIE) {
-                    const uint32_t q = S.pos[i];
-                    const uint32_t key = S.ekey[l], e = S.eslot[l];
-                    const uint32_t kw = 4u * (key & 0xFFu), ksh = key >> 8;
-                    const uint32_t bk = (word_at(S.buf, q + kw) >> ksh) & (kIBuckets - 1u);
-                    // (btab holds term ranks below the element's token count only)
-                    const uint32_t k = btab[(u64)S.erk[l] * kIBuckets + bk];
-                    bool v = k < 64u && q + RL + 7u <= hi;
-                    uint32_t slot = 0;
-                    if (v) {
-                        slot = d.tok_order[64ull * e + k];        // issued beside the template
-                        v = rec_match(S.buf, q, RL, d.rec_pad + ((u64)e * RK + k) * RS);
-                    }
-                    if (v) {
-                        const uint32_t fo = q + RL;
-                        uint32_t fn;
-                        const uint32_t fk = flag_atom(word_at(S.buf, fo), word_at(S.buf, fo + 4u), fn);
-                        if (fk && fo + fn <= hi) {
-                            kind = (uint8_t)(1u + fk);
-                            S.irk[i] = (int32_t)k;
-                            S.iend[i] = (uint16_t)(fo + fn);
-                            atomicOr(&S.pm[l], 1ull << (slot & 63u));
-                            if (fk == 1u) atomicOr(&S.tm[l], 1ull << (slot & 63u));
-                        }
-                    }
-                }
-                S.ik[i] = kind;
-            }
-            __syncthreads();
-            // 5. compact the valid items
-            const uint32_t v0 = i0 < nit && S.ik[i0] != 0, v1 = i1 < nit && S.ik[i1] != 0;
-            uint32_t nv;
-            const uint32_t vb = block_excl_scan(v0 + v1, S.sc, &nv);
-            if (v0) {
-                S.vl[vb] = (uint16_t)i0;
-                if (S.ik[i0] == 1) S.ecj[S.iown[i0]] = (uint16_t)vb;
-            }
-            if (v1) {
-                S.vl[vb + v0] = (uint16_t)i1;
-                if (S.ik[i1] == 1) S.ecj[S.iown[i1]] = (uint16_t)(vb + v0);
-            }
-            __syncthreads();
-            // 6. the chain, between neighbours; the window's last element counts only when
-            // the window holds the payload's end
-            const bool atend = lo + hi == aend && ni_all <= kIT && etot <= kIE;
-            bool bad = false;
-            if (tid == 0)
-                bad = !(nv > 0 && S.vl[0] == 0 && S.ik[0] == 1 && S.pos[0] == x0);
-            for (uint32_t j = tid; j < nv; j += kBlock) {
-                const uint32_t i = S.vl[j], kd = S.ik[i], l = S.iown[i];
-                const bool has_next = j + 1u < nv;
-                const uint32_t i2 = has_next ? S.vl[j + 1u] : 0u;
-                const uint32_t k2 = has_next ? S.ik[i2] : 0u;
-                bool b = false;
-                if (kd == 1) {
-                    const int64_t pr = l ? (int64_t)S.erk[l - 1u] : prev;
-                    b |= (int64_t)S.erk[l] <= pr;
-                    b |= !has_next || k2 < 2u || S.pos[i2] != S.iend[i];
-                    const uint32_t nj = l + 1u < nE ? S.ecj[l + 1u] : nv;
-                    b |= nj - j - 1u != S.em[l];
-                } else {
-                    const uint32_t e_ = S.iend[i];
-                    if (k2 >= 2u) b |= e_ != S.pos[i2] || S.irk[i2] <= S.irk[i];
-                    else if (has_next) b |= S.buf[e_] != 106 || e_ + 1u != S.pos[i2];
-                    else b |= !(e_ + 2u == hi && S.buf[e_] == 106 && S.buf[e_ + 1u] == 106);
-                }
-                if (b && (l + 1u < nE || atend)) bad = true;
-            }
-            const bool fail = __syncthreads_or(bad);
-            const uint32_t ncommit = atend ? nE : nE - 1u;
-            if (fail || nE == 0 || ncommit == 0 || got + ncommit > n || (atend && got + ncommit != n)) {
-                ok = false;
-                break;
-            }
-            for (uint32_t l = tid; l < ncommit; l += kBlock) c[S.eslot[l]] = u64x2{S.pm[l], S.tm[l]};
-            got += ncommit;
-            prev = S.erk[ncommit - 1u];
-            if (atend) fin = true;
-            else x = (uint32_t)(lo + S.pos[S.elist[ncommit]] - base);
-        }
-        if (tid == 0) {
-            if (ok) {
-                status[rep] = LASPJ_DEC_OK;
-            } else {
-                status[rep] = LASPJ_DEC_MALFORMED;      // rewritten by the redo pass
-                const uint32_t i = atomicAdd(redo, 1u);
-                redo[1 + i] = (uint32_t)rep;
-            }
-        }
-    }
-}
-
 struct Guard {
     std::lock_guard<std::mutex> lk;
     explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
@@ -4029,295 +3656,6 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
     }
 }
 
-// ---- integer G-Set payloads, one block per payload (round 4)
-//
-// A G-Set of integers is `131 108 <n:4>` then n images SMALL_INTEGER_EXT (97 v, 2 bytes)
-// or INTEGER_EXT (98 <v:4>, 5 bytes), then 106.  Where an element starts depends on every
-// earlier tag, but only through an offset of 0..4 bytes: a block stages 4 KiB, thread t
-// takes bytes [16 t, 16 t + 16) and walks them from each of the 5 possible entry offsets
-// (97: +2, 98: +5, 106: the list's end, anything else: not this kernel's case), which gives
-// a map entry -> exit offset into the next thread's bytes; a block scan composes the maps
-// (thread 0 enters at the cursor, so every prefix is a constant) and hands each thread
-// its real entry.  Then every thread walks its bytes once more and takes its elements:
-// value -> slot and rank through the integer value table, ranks strictly ascending (across
-// threads through their first and last ranks), the bit ORed into the replica's LDS words.
-// The payload must end in 106 on its last byte after exactly n elements.  Anything else —
-// another tag, a value outside the table, a non-minimal image, a rank out of order,
-// truncation, STRING_EXT — puts the payload on the redo list, which the wave decoder
-// (k_gset_etf_read) takes, rewriting the words and giving the status; so both are the wave
-// decoder's by construction.
-constexpr uint32_t kGPW = 4096;                // window bytes (16 per thread)
-
-// exit of the walk over a thread's 16 bytes from entry offset p (0..15): 0..4 into the next
-// thread's bytes, 6: the list's closing 106, 7: a tag this kernel does not take (or past
-// the payload); masks: bit i = byte 16 t + i is that tag (i < 20)
-__device__ __forceinline__ uint32_t gs_walk16(uint32_t m97, uint32_t m98, uint32_t m106,
-                                              uint32_t p) {
-    while (p < 16u) {
-        if ((m97 >> p) & 1u) p += 2u;
-        else if ((m98 >> p) & 1u) p += 5u;
-        else return (m106 >> p) & 1u ? 6u : 7u;
-    }
-    return p - 16u;
-}
-
-// maps entry -> exit as 8 fields of 4 bits (entries 0..4, 6 and 7 stay); a then b
-__device__ __forceinline__ uint32_t gs_compose(uint32_t a, uint32_t b) {
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < 8; ++s) h |= ((b >> (4u * ((a >> (4u * s)) & 0xFu))) & 0xFu) << (4u * s);
-    return h;
-}
-
-__device__ __forceinline__ u32x4 gs_piece(const uint8_t* payload, u64 lo, uint32_t nst,
-                                          uint32_t v) {
-    u32x4 q = {0u, 0u, 0u, 0u};
-    if (16u * v + 16u <= nst) {
-        q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(payload + lo) + v);
-    } else if (16u * v < nst) {
-        uint32_t w4[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t b = 16u * v; b < nst; ++b)
-            w4[(b >> 2) & 3u] |= (uint32_t)payload[lo + b] << (8u * (b & 3u));
-        q = u32x4{w4[0], w4[1], w4[2], w4[3]};
-    }
-    return q;
-}
-
-__global__ __launch_bounds__(kBlock) void k_gset_etf_read_par(const uint8_t* payload, u64 total,
-                                                              const u64* offs, uint64_t R,
-                                                              GsTabs g, int tag, int vers,
-                                                              u64* words, uint64_t W,
-                                                              int32_t* status, uint32_t* redo) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kGPW + 32];
-    __shared__ u64 s_w[kGWords];
-    __shared__ uint32_t firstrk[kBlock], lastrk[kBlock];
-    __shared__ uint32_t wt[kBlock / 64], sc[8];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    if (tid < 4) reinterpret_cast<uint32_t*>(buf + kGPW + 16)[tid] = 0u;
-    // a payload's first window (its head on) comes from registers loaded while the
-    // previous payload decoded: 257 pieces of 16 bytes, thread 0 holds two
-    u32x4 pf0 = {0u, 0u, 0u, 0u}, pf1 = {0u, 0u, 0u, 0u};
-    if (blockIdx.x < R) {
-        const u64 l0 = offs[blockIdx.x] & ~15ull;
-        const uint32_t n0 = (uint32_t)min((u64)(kGPW + 16), total - l0);
-        pf0 = gs_piece(payload, l0, n0, tid);
-        if (tid == 0) pf1 = gs_piece(payload, l0, n0, kBlock);
-    }
-    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
-        const u64 base = offs[rep], aend = offs[rep + 1], len = aend - base;
-        for (uint32_t x = tid; x < W; x += kBlock) s_w[x] = 0ull;
-        bool ok = true, fin = false, head = true;
-        uint32_t x = 0, n = 0, got = 0, prev_rank = 0;
-        bool have_prev = false;
-        while (ok && !fin) {
-            const u64 lo = (base + x) & ~15ull;
-            const uint32_t x0 = (uint32_t)(base + x - lo);
-            const uint32_t nst = (uint32_t)min((u64)(kGPW + 16), total - lo);
-            const uint32_t hi = (uint32_t)min((u64)nst, aend - lo);
-            __syncthreads();
-            if (head) {
-                reinterpret_cast<u32x4*>(buf)[tid] = pf0;
-                if (tid == 0) reinterpret_cast<u32x4*>(buf)[kBlock] = pf1;
-                const uint64_t nx = rep + gridDim.x;
-                if (nx < R) {
-                    const u64 l1 = offs[nx] & ~15ull;
-                    const uint32_t n1 = (uint32_t)min((u64)(kGPW + 16), total - l1);
-                    pf0 = gs_piece(payload, l1, n1, tid);
-                    if (tid == 0) pf1 = gs_piece(payload, l1, n1, kBlock);
-                }
-            } else {
-                for (uint32_t v = tid; v < (kGPW + 16) / 16; v += kBlock)
-                    reinterpret_cast<u32x4*>(buf)[v] = gs_piece(payload, lo, nst, v);
-            }
-            if (tid == 0) sc[0] = sc[1] = sc[2] = 0u;
-            __syncthreads();
-            uint32_t p0 = x0;
-            if (head) {
-                // [tag vers] 131 108 <n:4> (131 106: []), read from the window
-                head = false;
-                uint32_t h = x0;
-                if (tag >= 0) {
-                    ok = len >= 2 && buf[h] == (uint8_t)tag && buf[h + 1] == (uint8_t)vers;
-                    h += 2;
-                }
-                const u64 hl = h - x0;
-                if (ok && len == hl + 2 && buf[h] == 131 && buf[h + 1] == 106) {
-                    fin = true;
-                    break;
-                }
-                if (!(ok && len >= hl + 7 && buf[h] == 131 && buf[h + 1] == 108)) {
-                    ok = false;
-                    break;
-                }
-                n = ((uint32_t)buf[h + 2] << 24) | ((uint32_t)buf[h + 3] << 16) |
-                    ((uint32_t)buf[h + 4] << 8) | buf[h + 5];
-                if (n == 0) {
-                    ok = false;
-                    break;
-                }
-                p0 = h + 6;
-            }
-            // tag masks over bytes [16 t, 16 t + 20), only bytes of this payload
-            const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-            uint32_t m97 = 0, m98 = 0, m106 = 0;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const uint32_t v = b32[4 * tid + i];
-                m97 |= zbytes4(v ^ 0x61616161u) << (4 * i);
-                m98 |= zbytes4(v ^ 0x62626262u) << (4 * i);
-                m106 |= zbytes4(v ^ 0x6A6A6A6Au) << (4 * i);
-            }
-            {
-                const int32_t lim = (int32_t)hi - 16 * (int32_t)tid;
-                const uint32_t keep = lim <= 0 ? 0u : lim >= 20 ? 0xFFFFFu : (1u << lim) - 1u;
-                m97 &= keep;
-                m98 &= keep;
-                m106 &= keep;
-            }
-            // this thread's map: before the cursor's thread t0 every entry goes to 5 (no
-            // element yet); t0 enters at the cursor (a constant map), so every prefix from
-            // t0 on is a constant
-            const uint32_t t0 = p0 >> 4;
-            uint32_t mp = 0x76700000u;                  // fields 5 -> 7, 6 -> 6, 7 -> 7
-            if (tid < t0) {
-                mp = 0x55555555u;
-            } else if (tid == t0) {
-                // every field: the threads before t0 hand it entry 5
-                mp = gs_walk16(m97, m98, m106, p0 & 15u) * 0x11111111u;
-            } else {
-#pragma unroll
-                for (uint32_t s2 = 0; s2 < 5; ++s2) mp |= gs_walk16(m97, m98, m106, s2) << (4u * s2);
-            }
-            uint32_t inc = mp;
-#pragma unroll
-            for (uint32_t off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(inc, off, 64);
-                if (lane >= off) inc = gs_compose(y, inc);
-            }
-            if (lane == 63) wt[wv] = inc;
-            __syncthreads();
-            uint32_t pre = 0x76543210u;                 // identity
-            for (uint32_t i = 0; i < wv; ++i) pre = gs_compose(pre, wt[i]);
-            uint32_t exc = __shfl_up(inc, 1, 64);
-            if (lane == 0) exc = pre;
-            else if (wv) exc = gs_compose(pre, exc);
-            uint32_t fin_state = 0x76543210u;
-            for (uint32_t i = 0; i < kBlock / 64; ++i) fin_state = gs_compose(fin_state, wt[i]);
-            fin_state &= 0xFu;
-            // this thread's element starts (bit i: byte 16 t + i), from its entry
-            bool bad = false;
-            uint32_t sm = 0;
-            {
-                const bool walk = tid == t0 || (tid > t0 && (exc & 0xFu) <= 4u);
-                uint32_t q = tid == t0 ? (p0 & 15u) : (exc & 0xFu);
-                if (walk) {
-                    while (q < 16u) {
-                        if ((m97 >> q) & 1u) {
-                            sm |= 1u << q;
-                            q += 2u;
-                        } else if ((m98 >> q) & 1u) {
-                            sm |= 1u << q;
-                            q += 5u;
-                        } else {
-                            if ((m106 >> q) & 1u) sc[1] = 16u * tid + q + 1u;   // one past the nil
-                            else bad = true;
-                            break;
-                        }
-                    }
-                }
-            }
-            // the elements: every value-table load issued before any is used
-            const uint32_t cnt = (uint32_t)__popc(sm);
-            u64 tv[8];
-            bool vok[8];
-            {
-                uint32_t m = sm;
-#pragma unroll
-                for (uint32_t k = 0; k < 8; ++k) {
-                    const uint32_t q = m ? (uint32_t)__ffs(m) - 1u : 0u;
-                    m &= m - 1u;
-                    const uint32_t pp = 16u * tid + q;
-                    int64_t v;
-                    bool okk = k < cnt;
-                    if (buf[pp] == 97) {
-                        v = buf[pp + 1];
-                        okk &= pp + 2u <= hi;
-                    } else {
-                        v = (int32_t)(((uint32_t)buf[pp + 1] << 24) | ((uint32_t)buf[pp + 2] << 16) |
-                                      ((uint32_t)buf[pp + 3] << 8) | buf[pp + 4]);
-                        okk &= pp + 5u <= hi && (v < 0 || v > 255);   // minimal images only
-                    }
-                    const int64_t xv = v - g.ilo;
-                    okk &= xv >= 0 && xv < (int64_t)g.in;
-                    tv[k] = g.itab[okk ? xv : 0];
-                    vok[k] = okk;
-                }
-            }
-            uint32_t first = 0, last = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                if (k >= cnt) break;
-                const u64 t = tv[k];
-                if (!vok[k] || !(uint32_t)t) {
-                    bad = true;
-                    break;
-                }
-                const uint32_t slot = (uint32_t)t - 1u, rk = (uint32_t)(t >> 32);
-                if (k == 0) first = rk;
-                else bad |= rk <= last;
-                last = rk;
-                atomicOr(&s_w[slot >> 6], 1ull << (slot & 63u));
-            }
-            firstrk[tid] = cnt ? first : 0xFFFFFFFFu;
-            lastrk[tid] = cnt ? last : 0xFFFFFFFFu;
-            if (cnt) {
-                atomicAdd(&sc[0], cnt);
-                atomicMax(&sc[2], tid);
-            }
-            __syncthreads();
-            if (cnt) {
-                if (tid == t0) bad |= have_prev && first <= prev_rank;
-                else if (tid > t0)
-                    bad |= lastrk[tid - 1] == 0xFFFFFFFFu ? true : first <= lastrk[tid - 1];
-            }
-            const bool anybad = __syncthreads_or(bad);
-            const uint32_t wcnt = sc[0];
-            if (anybad || fin_state == 7u || got + wcnt > n) {
-                ok = false;
-                break;
-            }
-            got += wcnt;
-            if (wcnt) {
-                prev_rank = lastrk[sc[2]];
-                have_prev = true;
-            }
-            if (fin_state == 6u) {
-                ok = sc[1] == hi && lo + hi == aend && got == n;
-                fin = true;
-            } else {
-                if (lo + kGPW >= aend) {
-                    ok = false;
-                    break;
-                }
-                x = (uint32_t)(lo + kGPW + fin_state - base);
-            }
-        }
-        __syncthreads();
-        u64* w = words + rep * W;
-        for (uint32_t i = tid; i < W; i += kBlock) w[i] = s_w[i];
-        if (tid == 0) {
-            if (ok) {
-                status[rep] = LASPJ_DEC_OK;
-            } else {
-                status[rep] = LASPJ_DEC_MALFORMED;      // rewritten by the redo pass
-                const uint32_t i = atomicAdd(redo, 1u);
-                redo[1 + i] = (uint32_t)rep;
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ------------------------------------------------------------------ exclusive scans
 // out[i] = in[0] + ... + in[i-1] for i <= n (out[n] = the total): the payload offsets from
 // the per-replica sizes.  Up to kScanOne values one block walks tiles of 256 with a carry
@@ -4523,29 +3861,6 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     const uint64_t cap = (uint64_t)ctx->cus * 64;
     const uint8_t* pay = static_cast<const uint8_t*>(payload->dev);
     const u64* offs = static_cast<const u64*>(offsets->dev);
-    // knob 9, integer dictionaries: the block parser first, the wave decoder over its redo
-    // list; every replica's words are written by one of them.  Not the default: measured
-    // 0.84 ms of kernel time against the wave decoder's 0.46 at 65536 x 1024 (its per-thread
-    // maps and their composition scan cost ~7000 wave-instructions per 2 KiB payload,
-    // profiles/r04h_gs_*)
-    if (d->gs_itab && b->words_per_replica <= kGWords && ctx->tune_etf_read == 9 &&
-        !((uintptr_t)pay & 15u)) {
-        if (int s = reserve_scratch(ctx, 4ull * (R + 1))) return s;
-        uint32_t* redo = static_cast<uint32_t*>(ctx->scratch);
-        LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
-        hipLaunchKernelGGL(k_gset_etf_read_par,
-                           dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 16))),
-                           dim3(kBlock), 0, ctx->stream, pay, (u64)payload->bytes, offs, R, tabs,
-                           tag, vers, reinterpret_cast<u64*>(b->dev), b->words_per_replica,
-                           static_cast<int32_t*>(status->dev), redo);
-        LJ_LAUNCHED(ctx);
-        hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 4))),
-                           dim3(64), 0, ctx->stream, pay, offs, R, tabs, tag, vers,
-                           reinterpret_cast<u64*>(b->dev), b->words_per_replica,
-                           static_cast<int32_t*>(status->dev), (const uint32_t*)redo);
-        LJ_LAUNCHED(ctx);
-        return LASPJ_OK;
-    }
     LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
     // one wave per replica and a latency-bound extent walk: as many waves as LDS allows
     // (6 KiB each: ~25 per CU)
@@ -4684,41 +3999,6 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, co
     plan->nseg = acc;
 }
 
-// The item decoder's bucket tables, built once per dictionary, when the batch should take
-// that decoder: knob 9 only (measured slower than the wave decoder at the t64 shape,
-// 6.1 vs 4.4 ms, profiles/r04f_dec_*: the per-window scans, compaction and barriers cost
-// as much per element as the wave decoder's per-element sequence), many-token
-// dictionaries (> 8 token slots) whose records hash apart, at most 65536 elements
-// (64 MiB of tables), a 16-byte aligned payload buffer.  Null: the wave decoder.
-uint8_t* items_btab(laspj_ctx* ctx, const laspj_etf_dict* dc, uint64_t R, const uint8_t* payload) {
-    laspj_etf_dict* d = const_cast<laspj_etf_dict*>(dc);
-    const int64_t kn = ctx->tune_etf_read;
-    (void)R;
-    if (kn != 9 || !d->rd_desc || !d->rd_htab || d->tok_max <= kSmallTok ||
-        d->elements > 65536u || d->elements == 0 || ((uintptr_t)payload & 15u))
-        return nullptr;
-    if (!d->btab_tried) {
-        d->btab_tried = true;
-        const uint64_t bytes = (uint64_t)d->elements * kIBuckets;
-        void* p = nullptr;
-        if (dev_malloc(ctx, &p, bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            return nullptr;
-        }
-        if (hipMemsetAsync(p, 0xFF, bytes, ctx->stream) != hipSuccess) {
-            hipFree(p);
-            return nullptr;
-        }
-        const uint64_t g = std::min<uint64_t>(((uint64_t)d->elements * 64 + kBlock - 1) / kBlock,
-                                              (uint64_t)ctx->cus * 16);
-        hipLaunchKernelGGL(k_build_btab, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream,
-                           static_cast<const uint4*>(d->rd_desc), d->rd_tb, d->elements,
-                           d->tok_max, static_cast<uint8_t*>(p));
-        d->rd_btab = static_cast<uint8_t*>(p);
-    }
-    return d->rd_btab;
-}
-
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
                      const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
@@ -4791,29 +4071,6 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
         LJ_LAUNCHED(ctx);
         if (inline_redo) return LASPJ_OK;
         // the redo pass: usually an empty list (the kernel exits at once)
-        const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
-        hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
-                           ctx->stream, payload, (u64)payload_bytes, offs, R, b->elements,
-                           view(d), tabs, hh_small, tag, vers, reinterpret_cast<u64x2*>(b->dev),
-                           status, (const uint32_t*)redo);
-        LJ_LAUNCHED(ctx);
-        return LASPJ_OK;
-    }
-    // knob 9, many-token dictionaries: the item decoder, one block per payload, then the
-    // wave decoder over whatever it sent to the redo list
-    if (uint8_t* bt = items_btab(ctx, d, R, payload)) {
-        uint32_t* redo = redo_zeroed;
-        if (!redo) {
-            if (int s2 = reserve_scratch(ctx, 4ull * (R + 1))) return s2;
-            redo = static_cast<uint32_t*>(ctx->scratch);
-            LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
-        }
-        hipLaunchKernelGGL(k_orset_etf_read_items,
-                           dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)),
-                           dim3(kBlock), 0, ctx->stream, payload, (u64)payload_bytes, offs, R,
-                           b->elements, view(d), tabs, hh, (const uint8_t*)bt, tag, vers,
-                           reinterpret_cast<u64x2*>(b->dev), status, redo);
-        LJ_LAUNCHED(ctx);
         const uint64_t rblocks = (R + 3) / 4, rcap = (uint64_t)ctx->cus * 4;
         hipLaunchKernelGGL(kread, dim3((unsigned)std::min(rblocks, rcap)), dim3(kBlock), 0,
                            ctx->stream, payload, (u64)payload_bytes, offs, R, b->elements,
@@ -5509,10 +4766,6 @@ int laspj_etf_dict_destroy(laspj_etf_dict* d) {
         // back to the context's cache: its next user is ordered after every kernel that
         // read this image (all on the context's stream)
         laspj::dev_release(d->ctx, d->block, d->block_bytes);
-        if (d->rd_btab) {
-            hipStreamSynchronize(d->ctx->stream);
-            hipFree(d->rd_btab);
-        }
     }
     delete d;
     return LASPJ_OK;
@@ -5594,7 +4847,7 @@ int etf_dict_create_ex(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
 // no bucket choice that separates the element's tokens, the image area full.
 int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
                    const uint32_t* dirty, uint32_t n) {
-    if (!d || !d->patchable || d->rd_btab) return LASPJ_E_UNSUPPORTED;
+    if (!d || !d->patchable) return LASPJ_E_UNSUPPORTED;
     if (n == 0) return LASPJ_OK;
     const uint32_t E = d->elements, RK = d->tok_max, RL = d->rec_len;
     const uint64_t RS = d->rec_stride;

@@ -507,7 +507,7 @@ def _upload_payloads(ctx, blobs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 4, 9, "seg512"])
+@pytest.mark.parametrize("knob", [0, 1, 4, "seg512"])
 @pytest.mark.parametrize("tagged", [False, True])
 def test_gpu_from_binary_round_trip(tagged, knob):
     """Device from_binary/1 of oracle payloads (term_to_binary of random orddicts with
@@ -563,7 +563,7 @@ def test_gpu_from_binary_record_lengths(tok_len, pool_n):
     blobs = [oetf.term_to_binary(s) for s in states]
     pay, offs = _upload_payloads(ctx, blobs)
     want = dom.encode_orset(states, E)
-    for knob in (0, 9, "seg512"):
+    for knob in (0, "seg512"):
         b = ctx.orset_batch(len(states), E)
         with _read_kernel(ctx, knob):
             st = b.etf_decode(d, pay, offs, tag=-1, vers=1)
@@ -572,7 +572,7 @@ def test_gpu_from_binary_record_lengths(tok_len, pool_n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6, 9, "seg512"])
+@pytest.mark.parametrize("knob", [0, 1, 2, 4, 6, "seg512"])
 def test_gpu_from_binary_errors_and_atom_forms(knob):
     """Statuses: ?INVALID_BINARY (wrong tag, no 131, empty), ?UNSUPPORTED_VERSION,
     malformed (truncated, trailing byte, bad flag atom, element without tokens), terms
@@ -628,10 +628,10 @@ def test_gpu_from_binary_errors_and_atom_forms(knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [0, 1, 4, 9])
+@pytest.mark.parametrize("knob", [0, 1, 4])
 def test_gpu_from_binary_large_round_trip(knob):
     """4096 replicas x 512 slots x 64 token slots: device to_binary then from_binary
-    restores every cell (knob 9: the item decoder)."""
+    restores every cell."""
     import numpy as np
     from lasp_amd import engine, etf
     from lasp_amd.codec import Domain
@@ -953,7 +953,7 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
     records, so a batch holds one to several whole elements or stops inside one; tokens
     that embed the batch's item marker 104 2 and whole false element starts (106 104 2
     <a real element header>), flags in all three atom forms, and 2500 corrupted copies:
-    element batches (knob 0), the item decoder (9), one element at a time (7) and the
+    element batches (knob 0), one element at a time (7) and the
     serial scan (1) agree on every status and cell, and the clean payloads decode to the
     encoder's cells."""
     import numpy as np
@@ -1018,7 +1018,7 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
         blobs.append(bytes(b))
     pay, offs = _upload_payloads(ctx, blobs)
     res = {}
-    for knob in (0, 7, 9, 1):
+    for knob in (0, 7, 1):
         bt = ctx.orset_batch(len(blobs), E)
         with _read_kernel(ctx, knob):
             st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
@@ -1027,7 +1027,7 @@ def test_gpu_from_binary_many_token_batches_fuzz(seed):
     assert set(np.unique(st0)) <= {0, 1, 2, 3, 4, 5}
     assert (st0[:len(base)] == 0).all(), np.nonzero(st0[:len(base)])[0][:10]
     assert np.array_equal(c0[:len(base)], dom.encode_orset(states, E))
-    for knob in (7, 9, 1):
+    for knob in (7, 1):
         st, c = res[knob]
         assert np.array_equal(st0, st), (knob, np.nonzero(st0 != st)[0][:10])
         ok = st0 == 0
@@ -1233,90 +1233,6 @@ def test_gpu_gset_from_binary_long_payloads():
     st = b.etf_decode(d, pay, offs, tag=T, vers=1)
     assert list(st) == [c[1] for c in cases]
     assert np.array_equal(b.download()[:len(states)], dom.encode_gset(states, E))
-
-
-@pytest.mark.gpu
-def test_gpu_gset_block_parser_matches_wave_decoder():
-    """Integer G-Sets (the block parser's case: SMALL_INTEGER_EXT / INTEGER_EXT images,
-    negative and large values, payloads from a few bytes to several 4 KiB windows) and
-    3000 corrupted copies — tags flipped between 97 / 98 / 106, values nudged, bytes cut or
-    inserted at and around window edges, two elements swapped, a duplicate, a
-    non-minimal INTEGER_EXT, a value outside the dictionary: the block parser (with the
-    wave decoder over its redo list, knob 9) and the wave decoder alone (knob 0) give the
-    same status and the same words for every payload, and the clean payloads decode to
-    the host encoder's words."""
-    import numpy as np
-    from lasp_amd import _lib, etf
-    rng = random.Random(2024)
-    T = etf.DT_GSET_TAG
-    # (a value span the dictionary's integer table covers: at most 65536)
-    pool = list(range(-40, 3000, 1)) + [30000, 60000]
-    states = [[], [0], [255], [256], [-1], list(range(256)), list(range(200, 2200)),
-              list(range(-40, 3000)), [-40, 60000]]
-    for _ in range(120):
-        states.append(sorted(rng.sample(pool, rng.choice([1, 3, 50, 400, 1500]))))
-    ctx, dom, E, d = _gset_decode_setup(states)
-    base = [oetf.to_binary(T, 1, s) if rng.random() < 0.5 else oetf.term_to_binary(s)
-            for s in states]
-    tags = [T if b[0] == T else -1 for b in base]
-    blobs = [b for b, t in zip(base, tags) if t == T]
-    for _ in range(3000):
-        b = bytearray(rng.choice(blobs))
-        kind = rng.randrange(7)
-        if kind == 0 and len(b) > 8:
-            b[rng.randrange(8, len(b))] = rng.choice([97, 98, 106, 0, 255])
-        elif kind == 1 and len(b) > 8:
-            i = rng.randrange(8, len(b))
-            b[i] = (b[i] + rng.choice([1, 255])) & 0xFF
-        elif kind == 2:
-            cut = rng.choice([4096, 4097, 4100, 8192, 8195, rng.randrange(len(b) + 1)])
-            del b[min(cut, len(b)):]
-        elif kind == 3:
-            pos = rng.choice([4094, 4095, 4096, rng.randrange(len(b) + 1)])
-            pos = min(pos, len(b))
-            b[pos:pos] = rng.choice([bytes([97, 5]), bytes([98, 0, 0, 0, 7]), b"\0", bytes([106])])
-        elif kind == 4 and len(b) > 40:
-            j = rng.randrange(8, len(b) - 20)
-            while j < len(b) and b[j] not in (97, 98):
-                j += 1
-            del b[j:j + rng.randint(1, 6)]
-        elif kind == 5:
-            b = bytearray(oetf.to_binary(T, 1, [])) if rng.random() < 0.1 else b
-            s = sorted(rng.sample(pool, rng.randint(2, 300)))
-            k = rng.randrange(len(s) - 1)
-            s[k], s[k + 1] = s[k + 1], s[k]
-            b = bytearray(oetf.to_binary(T, 1, s))
-        else:
-            v = rng.randrange(256)
-            s = sorted(set(rng.sample(pool, rng.randint(1, 200))) - {v})
-            b = bytearray(oetf.to_binary(T, 1, s))
-            at = b.index(bytes([108])) + 5
-            b[at:at] = bytes([98, 0, 0, 0, v])      # a non-minimal image
-            b[4:8] = (len(s) + 1).to_bytes(4, "big")
-        blobs.append(bytes(b))
-    res = {}
-    for knob in (9, 0):
-        pay, offs = _upload_payloads(ctx, blobs)
-        bt = ctx.gset_batch(len(blobs), E)
-        ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
-        try:
-            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
-        finally:
-            ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
-        res[knob] = (st, bt.download())
-    assert np.array_equal(res[9][0], res[0][0]), np.nonzero(res[9][0] != res[0][0])[0][:10]
-    assert np.array_equal(res[9][1], res[0][1])
-    nb = sum(1 for t in tags if t == T)
-    assert (res[9][0][:nb] == 0).all()
-    clean = [s for s, t in zip(states, tags) if t == T]
-    assert np.array_equal(res[9][1][:nb], dom.encode_gset(clean, E))
-    # untagged payloads too
-    untag = [b for b, t in zip(base, tags) if t < 0]
-    if untag:
-        pay, offs = _upload_payloads(ctx, untag)
-        bt = ctx.gset_batch(len(untag), E)
-        assert (bt.etf_decode(d, pay, offs, tag=-1, vers=1) == 0).all()
-        assert np.array_equal(bt.download(), dom.encode_gset([s for s, t in zip(states, tags) if t < 0], E))
 
 
 @pytest.mark.gpu
