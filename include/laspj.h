@@ -203,10 +203,15 @@ int laspj_orset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t element
  * element (token_words 1..16): an element re-added many times keeps its tokens
  * (add_elem mints one per add and never collects them, lasp_orset.erl:222-241, 261-262).
  * The OR-Set entry points join / reduce / equal / value / removed / stats / inflation /
- * apply_ops and bind_many / inflation_many take these batches (both operands wide with the
- * same token_words); the combinator bodies and the codec take narrow batches only. */
+ * apply_ops / fragment / precondition_context and bind_many / inflation_many take these
+ * batches (both operands wide with the same token_words); the combinator bodies and the
+ * codec take narrow batches only. */
 int laspj_orset_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                                   uint32_t token_words, laspj_batch** out);
+/* dst := src re-laid with dst's token_words (the same value: src's pairs first, the rest
+ * {0, 0}); src narrow or wide with at most dst's token_words, same replicas and element
+ * slots.  A variable whose value gains an element's 65th token moves to wide cells so. */
+int laspj_orset_widen(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
 /* lasp_gset:new/0 (lasp_gset.erl:70-72) */
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out);
@@ -303,13 +308,14 @@ int laspj_orset_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
  * flag, a PRODUCT cell (x, y) iff both x and y have one. */
 int laspj_orset_value(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);
 /* value({tokens, E}, S) / value({fragment, E}, S) — lasp_orset.erl:76-89: out receives
- * the 16-byte cell of element slot `element` of every replica (R cells): its tokens are
- * E's token orddict ([] when p = 0), the fragment is [{E, Tokens}] or [] */
+ * the 16-byte cell of element slot `element` of every replica (R cells; a wide batch's
+ * k pairs per replica, 16 k bytes): its tokens are E's token orddict ([] when p = 0), the
+ * fragment is [{E, Tokens}] or [] */
 int laspj_orset_fragment(laspj_ctx* ctx, const laspj_batch* batch, uint32_t element,
                          laspj_buf* out);
 /* precondition_context/1 — lasp_orset.erl:147-154 with minimum_tokens (:264-267): every
  * element keeps the tokens flagged false (p & ~r, r = 0) and drops out when none is
- * left; dst may alias src */
+ * left; dst may alias src; wide batches pair by pair */
 int laspj_orset_precondition_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
 /* value(removed, S) — lasp_orset.erl:90-95: elements with a token flagged true */
 int laspj_orset_removed(laspj_ctx* ctx, const laspj_batch* batch, laspj_buf* out_bits);

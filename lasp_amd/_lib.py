@@ -254,6 +254,7 @@ SIGNATURES = {
     "laspj_list_etf_bind": (i, [vp, C.c_int32, vp, u64, vp, u64, vpp, C.POINTER(u64),
                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "laspj_orset_wide_batch_create": (i, [vp, u64, u32, u32, vpp]),
+    "laspj_orset_widen": (i, [vp, vp, vp]),
     "laspj_nif_stats": (i, [vp, vp, u32]),
     "laspj_nif_reset": (i, [vp]),
     "laspj_event_create": (i, [vp, vpp]),

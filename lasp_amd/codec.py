@@ -162,7 +162,10 @@ class Domain:
                 es = self.element_slot(elem, create=False)
                 p = r = 0
                 for tok, rm in toks:
-                    bit = 1 << self.token_slot(es, tok, create=False)
+                    t = self.token_slot(es, tok, create=False)
+                    if t >= 64:
+                        raise CapacityError(f"element {elem!r}: token slot {t} needs wide cells")
+                    bit = 1 << t
                     p |= bit
                     if rm is True:
                         r |= bit
@@ -177,6 +180,17 @@ class Domain:
         most = max((len(t) for t in self.tokens), default=0)
         return max(1, (most + 63) // 64)
 
+    def orset_words(self, states: Sequence) -> int:
+        """{p, r} pairs per cell the states' own token slots need (registering them):
+        1 when every token slot they hold is < 64."""
+        most = -1
+        for s in states:
+            for elem, toks in s:
+                es = self.element_slot(elem)
+                for tok, _rm in toks:
+                    most = max(most, self.token_slot(es, tok))
+        return max(1, (most + 64) // 64)
+
     def encode_orset_wide(self, states: Sequence, E: int, k: int) -> np.ndarray:
         """orddicts -> (len(states), E, k, 2) uint64 {p, r} pairs (LASPJ_KIND_ORSET_WIDE):
         token slot t in pair t // 64, bit t % 64."""
@@ -184,8 +198,6 @@ class Domain:
             self.register_orset(s)
         if self.size > E:
             raise CapacityError(f"{self.size} elements do not fit {E} slots")
-        if self.token_words() > k:
-            raise CapacityError(f"tokens need {self.token_words()} words, the batch has {k}")
         out = np.zeros((len(states), E, k, 2), dtype=np.uint64)
         for i, s in enumerate(states):
             _check_canonical_orset(s)
@@ -193,6 +205,8 @@ class Domain:
                 es = self.element_slot(elem, create=False)
                 for tok, rm in toks:
                     t = self.token_slot(es, tok, create=False)
+                    if t // 64 >= k:
+                        raise CapacityError(f"token slot {t} needs more than {k} words")
                     bit = np.uint64(1 << (t % 64))
                     out[i, es, t // 64, 0] |= bit
                     if rm is True:
@@ -214,7 +228,8 @@ class Domain:
             rs = [int(cells[es, j, 1]) for j in range(k)]
             td = self.tokens[es]
             toks = [(td.terms[t], bool((rs[t // 64] >> (t % 64)) & 1))
-                    for t in (int(x) for x in td.order()) if (ps[t // 64] >> (t % 64)) & 1]
+                    for t in (int(x) for x in td.order())
+                    if t < 64 * k and (ps[t // 64] >> (t % 64)) & 1]
             out.append((self.elements.terms[es], toks))
         return out
 
@@ -266,11 +281,14 @@ class Domain:
         tparts = []
         tord = np.full((E, 64), 0xFF, dtype=np.uint8)
         for es, td in enumerate(self.tokens[:self.size]):
-            for k, term in enumerate(td.terms):
+            # narrow cells hold token slots 0..63 (a wide domain's later slots are not
+            # on this wire codec's cells)
+            for k, term in enumerate(td.terms[:64]):
                 img = etf.encode(term)
                 tparts.append((64 * es + k, img))
                 tlen[64 * es + k + 1] = len(img)
             o = td.order()
+            o = o[o < 64]
             tord[es, :len(o)] = o
         toff = np.cumsum(tlen).astype(np.uint32)
         tparts.sort(key=lambda x: x[0])
@@ -492,52 +510,6 @@ class SeqOutput:
 
     def index(self) -> np.ndarray:
         return np.asarray(self.src if self.src else [0xFFFFFFFF], dtype=np.uint32)
-
-    def token_words(self) -> int:
-        """{p, r} pairs a cell needs for the widest element's token slots (1: narrow)."""
-        most = max((len(t) for t in self.tokens), default=0)
-        return max(1, (most + 63) // 64)
-
-    def encode_orset_wide(self, states: Sequence, E: int, k: int) -> np.ndarray:
-        """orddicts -> (len(states), E, k, 2) uint64 {p, r} pairs (LASPJ_KIND_ORSET_WIDE):
-        token slot t in pair t // 64, bit t % 64."""
-        for s in states:
-            self.register_orset(s)
-        if self.size > E:
-            raise CapacityError(f"{self.size} elements do not fit {E} slots")
-        if self.token_words() > k:
-            raise CapacityError(f"tokens need {self.token_words()} words, the batch has {k}")
-        out = np.zeros((len(states), E, k, 2), dtype=np.uint64)
-        for i, s in enumerate(states):
-            _check_canonical_orset(s)
-            for elem, toks in s:
-                es = self.element_slot(elem, create=False)
-                for tok, rm in toks:
-                    t = self.token_slot(es, tok, create=False)
-                    bit = np.uint64(1 << (t % 64))
-                    out[i, es, t // 64, 0] |= bit
-                    if rm is True:
-                        out[i, es, t // 64, 1] |= bit
-                    elif rm is not False:
-                        raise NonCanonical(f"token flag {rm!r} is not a boolean")
-        return out
-
-    def decode_orset_wide(self, cells: np.ndarray) -> list:
-        """(E, k, 2) pairs -> orddict (keys and tokens ascending in term order)."""
-        out = []
-        k = cells.shape[1]
-        for es in self.elements.order():
-            if es >= cells.shape[0]:
-                continue
-            ps = [int(cells[es, j, 0]) for j in range(k)]
-            if not any(ps):
-                continue
-            rs = [int(cells[es, j, 1]) for j in range(k)]
-            td = self.tokens[es]
-            toks = [(td.terms[t], bool((rs[t // 64] >> (t % 64)) & 1))
-                    for t in (int(x) for x in td.order()) if (ps[t // 64] >> (t % 64)) & 1]
-            out.append((self.elements.terms[es], toks))
-        return out
 
     def decode_orset(self, cells: np.ndarray) -> list:
         out = []

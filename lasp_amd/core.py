@@ -80,10 +80,14 @@ class _Value:
 
 
 class Store:
-    def __init__(self, capacity: int = 4096, ctx: Optional[engine.Context] = None):
+    def __init__(self, capacity: int = 4096, ctx: Optional[engine.Context] = None,
+                 token_words: int = 16):
         self.ctx = ctx or context()
         self.cap = capacity
-        self.odom = Domain(element_capacity=capacity)
+        # an OR-Set element holds up to 64 * token_words tokens: a variable whose value
+        # names a token slot >= 64 moves to wide cells (LASPJ_KIND_ORSET_WIDE, k {p, r}
+        # pairs per element); the others keep 16-byte cells
+        self.odom = Domain(element_capacity=capacity, token_capacity=64 * token_words)
         self.gdom = Domain(element_capacity=capacity)
         self.cdom = Domain(element_capacity=capacity)      # G-Counter actors
         self.ospace = L.ListSpace(self.ctx, self.odom, tokens=True)
@@ -99,8 +103,10 @@ class Store:
         self._lcache: Dict = {}
 
     # ---------------------------------------------------------------- helpers
-    def _new_batch(self, type_):
+    def _new_batch(self, type_, k: int = 1):
         if type_ in ("lasp_orset", "lasp_orset_gbtree"):
+            if k > 1:
+                return self.ctx.orset_wide_batch(1, self.cap, k)
             return self.ctx.orset_batch(1, self.cap)
         if type_ == "lasp_gset":
             return self.ctx.gset_batch(1, self.cap)
@@ -118,8 +124,8 @@ class Store:
         """A host term as a device value: canonical when it is an orddict / ordset (and
         the variable holds no product pairs), else a list.
 
-        A value the device form cannot hold — an element with more than 64 distinct
-        tokens, or more distinct elements than the store's `capacity` — raises
+        A value the device form cannot hold — an element with more than 64 * token_words
+        distinct tokens, or more distinct elements than the store's `capacity` — raises
         `Unsupported`, and the dictionary slots the attempt registered are undone.  The
         reference's merge takes such values (add_elem mints a fresh token per add,
         lasp_orset.erl:222-230, 261-262), so lasp_core:bind/3 would write them
@@ -142,9 +148,8 @@ class Store:
             return _Value("canonical", b, empty=not term)
         if type_ == "lasp_orset_gbtree":
             from .orset_gbtree import shape_info, to_orddict
-            b = self._new_batch(type_)
             od = to_orddict(term)
-            b.upload(self.odom.encode_orset([od], self.cap))
+            b = self._orset_upload(type_, od)
             return _Value("canonical", b, empty=not od, gb=shape_info(term))
         if not pairs:
             try:
@@ -157,10 +162,10 @@ class Store:
             except (NonCanonical, TypeError, ValueError):
                 ok = False
             if ok:
-                b = self._new_batch(type_)
                 if type_ == "lasp_orset":
-                    b.upload(self.odom.encode_orset([term], self.cap))
+                    b = self._orset_upload(type_, term)
                 else:
+                    b = self._new_batch(type_)
                     b.upload(self.gdom.encode_gset([term], self.cap))
                 return _Value("canonical", b, empty=not term)
         keys, toff, toks = L.encode(self._dom(type_), term, type_ == "lasp_gset", pairs)
@@ -168,8 +173,37 @@ class Store:
         lb = engine.ListBatch(self.ctx, kind).upload(keys, toff, toks)
         return _Value("list", lb, pairs, empty=not term)
 
+    def _orset_upload(self, type_, od):
+        """An orddict in 16-byte cells, or in wide cells when it names a token slot >= 64."""
+        k = self.odom.orset_words([od])
+        b = self._new_batch(type_, k)
+        if k == 1:
+            b.upload(self.odom.encode_orset([od], self.cap))
+        else:
+            b.upload(self.odom.encode_orset_wide([od], self.cap, k))
+        return b
+
+    def _match(self, a, b):
+        """Two OR-Set batches with one cell width (the narrower widened on the device,
+        laspj_orset_widen: a new batch, the stored one untouched)."""
+        k = max(_width(a), _width(b))
+        return self._widen(a, k), self._widen(b, k)
+
+    def _widen(self, b, k: int):
+        if _width(b) >= k:
+            return b
+        return self.ctx.orset_wide_batch(b.replicas, b.elements, k).widen_from(b)
+
+    def _decode_orset(self, b) -> list:
+        cells = b.download()[0]
+        return self.odom.decode_orset_wide(cells) if _width(b) > 1 else \
+            self.odom.decode_orset(cells)
+
     def _to_list(self, type_, batch):
         """A canonical batch as a list (laspj_list_from_set)."""
+        if _width(batch) > 1:
+            raise Unsupported("a list form of an OR-Set value with more than 64 tokens "
+                              "on an element")
         eb, n, tb = self._space(type_).set_orders(batch.elements)
         return engine.ListBatch.from_set(batch, eb, n, tb)
 
@@ -201,12 +235,12 @@ class Store:
             return dv.empty
         if dv.rep == "list":
             return int(dv.batch.counts()[0][0]) == 0
-        return bool(dv.batch.equal(self._bottom(type_))[0])
+        return bool(dv.batch.equal(self._bottom(type_, _width(dv.batch)))[0])
 
-    def _bottom(self, type_):
-        b = self._bottoms.get(type_)
+    def _bottom(self, type_, k: int = 1):
+        b = self._bottoms.get((type_, k))
         if b is None:
-            b = self._bottoms[type_] = self._new_batch(type_)
+            b = self._bottoms[(type_, k)] = self._new_batch(type_, k)
         return b
 
     # ---------------------------------------------------------------- declare / bind
@@ -271,9 +305,9 @@ class Store:
                             continue
                     self.bind(id_, term)          # written now, propagated at the end
                 if pend:
-                    dsts = [_new_like(self.ctx, v.val) for _i, v, _d in pend]
-                    st = self.ctx.bind_many(dsts, [v.val for _i, v, _d in pend],
-                                            [d.batch for _i, _v, d in pend])
+                    ops = [self._match(v.val, d.batch) for _i, v, d in pend]
+                    dsts = [_new_like(self.ctx, c) for c, _n in ops]
+                    st = self.ctx.bind_many(dsts, [c for c, _n in ops], [n for _c, n in ops])
                     for (id_, v, _d), dst, s_ in zip(pend, dsts, st):
                         if s_:
                             v.val = dst
@@ -306,12 +340,12 @@ class Store:
             self._written(id_, v)
             return
         if v.rep == "canonical" and dv.rep == "canonical":
-            new = dv.batch
+            cur, new = self._match(v.val, dv.batch)
             if t != "lasp_orset_gbtree":
                 # `Value0 =:= Value` + merge in one launch (laspj_batch_bind_many); a
                 # canonical merge always inflates Value0, so it is written (:301-303)
-                merged = _new_like(self.ctx, v.val)
-                if not self.ctx.bind_many([merged], [v.val], [new])[0]:
+                merged = _new_like(self.ctx, cur)
+                if not self.ctx.bind_many([merged], [cur], [new])[0]:
                     return                                       # lasp_core.erl:294-296
                 # merged came from v.val by a merge that changed it: a strict inflation
                 # of v.val, which _propagate then knows without asking the device
@@ -319,7 +353,7 @@ class Store:
                 v.val = merged
                 self._written(id_, v)
                 return
-            same = bool(v.val.equal(new)[0])
+            same = bool(cur.equal(new)[0])
             if t == "lasp_orset_gbtree" and dv.gb is not None:
                 # `case Value0 of Value` matches whole terms: the stored value's outer
                 # tree is ascending-insert shaped (a merge output), so Value must be too,
@@ -328,15 +362,15 @@ class Store:
                 same = same and outer and _same_shapes(v.gshape, odd)
             if same:                                             # lasp_core.erl:294-296
                 return
-            merged = _new_like(self.ctx, v.val)
-            _or_into(self.ctx, merged, v.val, new)
-            if not bool(merged.is_inflation_of(v.val)[0]):       # lasp_core.erl:301
+            merged = _new_like(self.ctx, cur)
+            _or_into(self.ctx, merged, cur, new)
+            if not bool(merged.is_inflation_of(cur)[0]):         # lasp_core.erl:301
                 return
             if t == "lasp_orset_gbtree" and dv.gb is not None:
                 # gb_trees_ext:merge/3: an element of both operands gets an ascending
                 # token tree, one of one operand keeps that operand's tree
                 from .terms import hkey
-                old_keys = {hkey(e) for e, _ts in self.odom.decode_orset(v.val.download()[0])}
+                old_keys = {hkey(e) for e, _ts in self._decode_orset(cur)}
                 _outer, odd, new_keys = dv.gb
                 v.gshape = {k: tr for k, tr in v.gshape.items() if k not in new_keys}
                 v.gshape.update({k: tr for k, tr in odd.items() if k not in old_keys})
@@ -390,8 +424,14 @@ class Store:
                     ops = [(0, self.gdom.element_slot(e), _lib.OP_ADD, 0, 1) for e in elems]
         except CapacityError as e:
             raise Unsupported(f"update not representable on the device store: {e}") from e
-        cur = _new_like(self.ctx, v.val)
-        _or_into(self.ctx, cur, v.val, v.val)
+        k = 1
+        if v.type in ("lasp_orset", "lasp_orset_gbtree"):
+            k = max([_width(v.val)] + [(o[3] >> 6) + 1 for o in ops if o[2] != _lib.OP_REMOVE])
+        if k > _width(v.val):
+            cur = self._widen(v.val, k)       # the op mints token slot >= 64 * width
+        else:
+            cur = _new_like(self.ctx, v.val)
+            _or_into(self.ctx, cur, v.val, v.val)
         if v.type == "riak_dt_gcounter":
             cur.increment(ops)
         elif v.type == "lasp_orset" and all(o[2] == _lib.OP_ADD for o in ops):
@@ -451,7 +491,8 @@ class Store:
     def _inflates(self, v: _Var, prev: _Value, strict: bool) -> bool:
         """is_inflation(prev, V) / is_strict_inflation(prev, V) for V = v's value."""
         if v.rep == "canonical" and prev.rep == "canonical":
-            if bool(v.val.is_inflation_of(prev.batch, strict=strict)[0]):
+            cur, pb = self._match(v.val, prev.batch)
+            if bool(cur.is_inflation_of(pb, strict=strict)[0]):
                 return True
             if strict and v.type == "lasp_orset_gbtree" and prev.gb is not None:
                 # `Ids =/= Ids1` (lasp_lattice.erl:217-233) compares token TREES: a
@@ -459,12 +500,11 @@ class Store:
                 from .gbtrees import shape
                 from .terms import hkey
                 _outer, odd, keys = prev.gb
-                common = keys & {hkey(e) for e, _t in
-                                 self.odom.decode_orset(v.val.download()[0])}
+                common = keys & {hkey(e) for e, _t in self._decode_orset(v.val)}
                 differs = any((k in odd) != (k in v.gshape) or
                               (k in odd and shape(odd[k]) != shape(v.gshape[k]))
                               for k in common)
-                return differs and bool(v.val.is_inflation_of(prev.batch)[0])
+                return differs and bool(cur.is_inflation_of(pb)[0])
             return False
         if v.type not in ("lasp_orset", "lasp_gset"):
             raise Unsupported(f"list values of {v.type}")
@@ -478,15 +518,16 @@ class Store:
         if v.rep == "list":
             keys, toff, toks = v.val.download()
             return L.decode(self._dom(v.type), keys, toff, toks, v.type == "lasp_gset")
+        if v.type == "lasp_orset_gbtree":
+            from .orset_gbtree import with_shapes
+            return with_shapes(self._decode_orset(v.val), v.gshape)
+        if v.type == "lasp_orset":
+            return self._decode_orset(v.val)
         cells = v.val.download()[0]
         if v.type == "riak_dt_gcounter":
             return [(self.cdom.elements.terms[int(a)], int(cells[int(a)]))
                     for a in self.cdom.elements.order() if int(cells[int(a)])]
-        if v.type == "lasp_orset_gbtree":
-            from .orset_gbtree import with_shapes
-            return with_shapes(self.odom.decode_orset(cells), v.gshape)
-        return self.odom.decode_orset(cells) if v.type == "lasp_orset" else \
-            self.gdom.decode_gset(cells)
+        return self.gdom.decode_gset(cells)
 
     def type_value(self, id_):
         """Type:value(Value) of the variable (value/1 kernel + decode)."""
@@ -578,7 +619,8 @@ class Store:
                 if v.empty or last is None or last.batch is v.val or self._merged_from(v, last):
                     continue
                 if v.rep == "canonical" and last.rep == "canonical" and \
-                        v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter"):
+                        v.type in ("lasp_orset", "lasp_gset", "riak_dt_gcounter") and \
+                        _width(v.val) == _width(last.batch):
                     keys.append(((id(proc), i), v.val, last.batch))
                     prevs.append(last.batch)
                     curs.append(v.val)
@@ -611,6 +653,7 @@ class Store:
             if a is None or b is None:
                 return
             if t == "lasp_orset" and a.rep == b.rep == "canonical":
+                _narrow(a.batch, b.batch)
                 res = self._new_batch(t).union(a.batch, b.batch)       # keep-left merge
                 return self._bind_out(out, _Value("canonical", res))
             _pairs_guard(a, b)
@@ -660,6 +703,7 @@ class Store:
                     bits = np.zeros(((self.cap + 63) // 64,), dtype=np.uint64)
                     for e in np.nonzero(keep == 1)[0]:
                         bits[e >> 6] |= np.uint64(1) << np.uint64(e & 63)
+                    _narrow(a.batch)
                     res = self._new_batch(t).filter(a.batch, bits)
                     return self._bind_out(out, _Value("canonical", res))
             la = self._value_list(t, a)
@@ -723,8 +767,21 @@ def _type_new(type_):
     return []
 
 
+def _width(b) -> int:
+    """{p, r} pairs per cell of an OR-Set batch (1 for narrow cells and other kinds)."""
+    return getattr(b, "token_words", 1)
+
+
+def _narrow(*bs):
+    if any(_width(b) > 1 for b in bs):
+        raise Unsupported("combinator bodies over an OR-Set value with more than 64 tokens "
+                          "on an element")
+
+
 def _new_like(ctx, b):
     """An empty batch of b's kind and shape."""
+    if isinstance(b, engine.ORSetWideBatch):
+        return ctx.orset_wide_batch(b.replicas, b.elements, b.token_words)
     out = type(b).__new__(type(b))
     engine._Batch.__init__(out, ctx, b.replicas, b.elements)
     return out

@@ -247,6 +247,7 @@ hipError_t launch_wide_inflation(laspj_ctx* ctx, const laspj_batch* prev, const 
                                  bool strict, uint8_t* out);
 hipError_t launch_wide_apply(laspj_ctx* ctx, laspj_batch* b, const laspj_op* ops, uint64_t nops,
                              int32_t* status);
+hipError_t launch_wide_widen(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src);
 hipError_t launch_gset_filter(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
                               const uint64_t* keep);
 hipError_t launch_gset_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,

@@ -713,10 +713,14 @@ hipError_t launch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
 // every element keeps its tokens flagged false, and drops out when none is left.
 
 __global__ __launch_bounds__(kBlock) void k_orset_fragment(const u64x2* cells, u64x2* out,
-                                                           uint64_t R, uint32_t E, uint32_t e) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R;
-         i += (uint64_t)gridDim.x * kBlock)
-        out[i] = cells[i * E + e];
+                                                           uint64_t R, uint32_t E, uint32_t e,
+                                                           uint32_t k) {
+    // k {p, r} pairs per cell (wide batches): out holds replica i's pairs at i k ..
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R * k;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t rep = i / k;
+        out[i] = cells[(rep * E + e) * k + (i - rep * k)];
+    }
 }
 
 template <int U, bool NT>
@@ -737,16 +741,16 @@ __global__ __launch_bounds__(kBlock) void k_orset_context(u64x2* d, const u64x2*
 }
 
 hipError_t launch_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t e, void* out) {
-    uint64_t g = (b->replicas + kBlock - 1) / kBlock;
+    uint64_t g = (b->replicas * b->tok_words + kBlock - 1) / kBlock;
     if (g > (uint64_t)ctx->cus * 16) g = (uint64_t)ctx->cus * 16;
     hipLaunchKernelGGL(k_orset_fragment, dim3((unsigned)(g ? g : 1)), dim3(kBlock), 0, ctx->stream,
                        reinterpret_cast<const u64x2*>(b->dev), reinterpret_cast<u64x2*>(out),
-                       b->replicas, b->elements, e);
+                       b->replicas, b->elements, e, b->tok_words);
     return hipGetLastError();
 }
 
 hipError_t launch_orset_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
-    const uint64_t n = src->replicas * (uint64_t)src->elements;
+    const uint64_t n = src->replicas * (uint64_t)src->elements * src->tok_words;   // pairs
     StreamTune t = stream_tune(ctx, n);
     auto* d = reinterpret_cast<u64x2*>(dst->dev);
     auto* a = reinterpret_cast<const u64x2*>(src->dev);

@@ -504,6 +504,21 @@ int laspj_orset_wide_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t el
     return batch_create(ctx, LASPJ_KIND_ORSET_WIDE, replicas, elements, out, token_words);
 }
 
+int laspj_orset_widen(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
+    if (!same_ctx(ctx, dst) || !same_ctx(ctx, src))
+        return fail(ctx, LASPJ_E_INVAL, "orset_widen: bad batch");
+    if (dst->kind != LASPJ_KIND_ORSET_WIDE ||
+        (src->kind != LASPJ_KIND_ORSET && src->kind != LASPJ_KIND_ORSET_WIDE))
+        return fail(ctx, LASPJ_E_KIND, "orset_widen: OR-Set source, wide destination");
+    if (dst->replicas != src->replicas || dst->elements != src->elements ||
+        src->tok_words > dst->tok_words)
+        return fail(ctx, LASPJ_E_SHAPE, "orset_widen: shapes differ or the source is wider");
+    if (dst->dev == src->dev) return fail(ctx, LASPJ_E_INVAL, "orset_widen: dst aliases src");
+    Guard g(ctx);
+    LJ_HIP(ctx, laspj::launch_wide_widen(ctx, dst, src));
+    return LASPJ_OK;
+}
+
 int laspj_gset_batch_create(laspj_ctx* ctx, uint64_t replicas, uint32_t elements,
                             laspj_batch** out) {
     return batch_create(ctx, LASPJ_KIND_GSET, replicas, elements, out);
@@ -698,19 +713,28 @@ int laspj_batch_fill_synthetic(laspj_ctx* ctx, laspj_batch* b, uint64_t seed,
     return LASPJ_OK;
 }
 
+// the OR-Set entry points take wide batches too (the same words, k pairs per cell)
+static int32_t orset_kind(const laspj_batch* a, int32_t kind) {
+    return kind == LASPJ_KIND_ORSET && a && a->kind == LASPJ_KIND_ORSET_WIDE
+               ? LASPJ_KIND_ORSET_WIDE : kind;
+}
+
 int laspj_orset_fragment(laspj_ctx* ctx, const laspj_batch* b, uint32_t element,
                          laspj_buf* out) {
     if (!same_ctx(ctx, b)) return fail(ctx, LASPJ_E_INVAL, "orset_fragment: bad batch");
-    if (b->kind != LASPJ_KIND_ORSET) return fail(ctx, LASPJ_E_KIND, "orset_fragment: kind");
+    if (b->kind != LASPJ_KIND_ORSET && b->kind != LASPJ_KIND_ORSET_WIDE)
+        return fail(ctx, LASPJ_E_KIND, "orset_fragment: kind");
     if (element >= b->elements) return fail(ctx, LASPJ_E_RANGE, "orset_fragment: element slot");
-    if (int s = check_buf(ctx, out, 16ull * b->replicas, "orset_fragment")) return s;
+    if (int s = check_buf(ctx, out, 16ull * b->replicas * b->tok_words, "orset_fragment")) return s;
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_orset_fragment(ctx, b, element, out->dev));
     return LASPJ_OK;
 }
 
 int laspj_orset_precondition_context(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
-    if (int s = check_pair(ctx, dst, src, LASPJ_KIND_ORSET, "orset_precondition_context")) return s;
+    if (int s = check_pair(ctx, dst, src, orset_kind(src, LASPJ_KIND_ORSET),
+                           "orset_precondition_context"))
+        return s;
     Guard g(ctx);
     LJ_HIP(ctx, laspj::launch_orset_context(ctx, dst, src));
     return LASPJ_OK;
@@ -763,12 +787,6 @@ int laspj_orset_gather_inflation_keyed(laspj_ctx* ctx, laspj_batch* dst, const l
 }
 
 // ------------------------------------------------------------------------- joins
-
-// the OR-Set entry points take wide batches too (the same words, k pairs per cell)
-static int32_t orset_kind(const laspj_batch* a, int32_t kind) {
-    return kind == LASPJ_KIND_ORSET && a && a->kind == LASPJ_KIND_ORSET_WIDE
-               ? LASPJ_KIND_ORSET_WIDE : kind;
-}
 
 static int join_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                      const laspj_batch* b, int32_t kind, const char* what) {

@@ -201,6 +201,18 @@ __global__ __launch_bounds__(kB) void k_wide_apply(u64* state, uint64_t E, uint3
     }
 }
 
+// dst pair j of cell c = src pair j (j < k1) else {0, 0}: one lane per dst pair
+__global__ __launch_bounds__(kB) void k_wide_widen(u64x2* dst, const u64x2* src, uint64_t cells,
+                                                   uint32_t k1, uint32_t k2) {
+    const uint64_t n = cells * k2;
+    for (uint64_t q = (uint64_t)blockIdx.x * kB + threadIdx.x; q < n;
+         q += (uint64_t)gridDim.x * kB) {
+        const uint64_t c = q / k2;
+        const uint32_t j = (uint32_t)(q - c * k2);
+        dst[q] = j < k1 ? ld2(src + c * k1 + j) : u64x2{0, 0};
+    }
+}
+
 int grid_for(const laspj_ctx* ctx, uint64_t waves) {
     const uint64_t blocks = (waves + 3) / 4, cap = (uint64_t)ctx->cus * 16;
     return (int)std::max<uint64_t>(1, std::min(blocks, cap));
@@ -264,6 +276,15 @@ hipError_t launch_wide_inflation(laspj_ctx* ctx, const laspj_batch* prev, const 
     hipLaunchKernelGGL(k_wide_finish,
                        dim3((unsigned)std::min<uint64_t>((cur->replicas + 255) / 256, 4096)),
                        dim3(256), 0, ctx->stream, (uint32_t*)rec, out, cur->replicas, strict);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_widen(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src) {
+    const uint64_t cells = dst->replicas * (uint64_t)dst->elements;
+    const uint64_t n = cells * dst->tok_words;
+    hipLaunchKernelGGL(k_wide_widen, dim3(grid_for(ctx, (n + 63) / 64)), dim3(kB), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst->dev), reinterpret_cast<const u64x2*>(src->dev),
+                       cells, src->tok_words, dst->tok_words);
     return hipGetLastError();
 }
 

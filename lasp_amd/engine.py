@@ -691,6 +691,18 @@ class ORSetWideBatch(ORSetBatch):
         check(ctx.L.laspj_batch_info_get(self.h, C.byref(info)))
         self.bytes_per_replica, self.nbytes = info.bytes_per_replica, info.bytes
 
+    def fragment(self, element: int) -> np.ndarray:
+        """(R, k, 2) pairs of one element slot."""
+        k = self.token_words
+        buf = self.ctx.buffer(self.replicas * 16 * k)
+        check(self.ctx.L.laspj_orset_fragment(self.ctx.h, self.h, element, buf.h), self.ctx.h)
+        return buf.download(np.uint64).reshape(self.replicas, k, 2)
+
+    def widen_from(self, src: "ORSetBatch") -> "ORSetWideBatch":
+        """laspj_orset_widen: self := src (narrow, or wide with fewer token words)."""
+        check(self.ctx.L.laspj_orset_widen(self.ctx.h, self.h, src.h), self.ctx.h)
+        return self
+
     def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         """(count, E, k, 2) uint64 array of {p, r} pairs."""
         w = self.download_words(first, count)

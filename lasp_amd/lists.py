@@ -19,7 +19,7 @@ from typing import Callable, Optional
 import numpy as np
 
 from . import _lib
-from .codec import Domain, NonCanonical
+from .codec import CapacityError, Domain, NonCanonical
 from .terms import term_cmp, term_key
 
 PAIR = _lib.LIST_PAIR
@@ -110,7 +110,7 @@ class ListSpace:
             for e in grown:
                 self._seen[e] = len(d.tokens[e].terms)
             allg = sorted(((term_key(t), 64 * e + k) for e in self._seen
-                           for k, t in enumerate(d.tokens[e].terms[:self._seen[e]])),
+                           for k, t in enumerate(d.tokens[e].terms[:min(self._seen[e], 64)])),
                           key=lambda x: x[0])
             self._tkeys, self._tids = [], []
             for key, g in allg:
@@ -125,7 +125,7 @@ class ListSpace:
             self._log_rank = len(log)
             for e in grown:
                 terms = d.tokens[e].terms
-                for k in range(self._seen.get(e, 0), len(terms)):
+                for k in range(self._seen.get(e, 0), min(len(terms), 64)):
                     key = term_key(terms[k])
                     g = 64 * e + k
                     i = bisect.bisect_left(self._tkeys, key)
@@ -198,6 +198,7 @@ class ListSpace:
             self._log_tord = len(log)
             for e in todo:
                 o = d.tokens[e].order()
+                o = o[o < 64]
                 self._tord[e, :] = 0xFF
                 self._tord[e, :len(o)] = o
             if whole:
@@ -231,6 +232,16 @@ def _tok_term(dom: Domain, item: int):
     return dom.tokens[g >> 6].terms[g & 63]
 
 
+def _tslot(dom: Domain, e: int, tok) -> int:
+    """A token's slot as a list token id part: list values name 64 token slots per
+    element (g = 64 e + k); a wide domain's later slots are not representable here."""
+    k = dom.token_slot(e, tok)
+    if k >= 64:
+        raise CapacityError(f"element {dom.elements.terms[e]!r}: list values hold 64 "
+                            f"tokens per element")
+    return k
+
+
 def encode(dom: Domain, term, gset: bool, pairs: bool = False):
     """A Lasp value (any list: orddict-shaped or not) -> (keys, toff, toks) items.
     With `pairs`, 2-tuple keys become product key items and, under them, 2-list tokens
@@ -256,13 +267,13 @@ def encode(dom: Domain, term, gset: bool, pairs: bool = False):
             tok, flag = t
             if item & PAIR and isinstance(tok, list) and len(tok) == 2:
                 x, y = (item >> 31) & ID, item & ID
-                g = COMPOUND | ((64 * x + dom.token_slot(x, tok[0])) << 31) | \
-                    (64 * y + dom.token_slot(y, tok[1]))
+                g = COMPOUND | ((64 * x + _tslot(dom, x, tok[0])) << 31) | \
+                    (64 * y + _tslot(dom, y, tok[1]))
             else:
                 e = item & ID if not item & PAIR else None
                 if e is None:
                     raise NonCanonical("a product key's tokens are [Tx, Ty] pairs")
-                g = 64 * e + dom.token_slot(e, tok)
+                g = 64 * e + _tslot(dom, e, tok)
             toks.append(g | (REMOVED if flag else 0))
         toff[i + 1] = len(toks)
     return keys, toff, np.asarray(toks, dtype=np.uint64)

@@ -29,13 +29,29 @@ def context() -> engine.Context:
     return _CTX
 
 
-def _batch(dom: Domain, states: Sequence) -> Tuple[engine.ORSetBatch, int]:
-    for s in states:
-        dom.register_orset(s)
+# an element keeps up to 64 * TOKEN_WORDS tokens: values naming a token slot >= 64 go to
+# wide cells (LASPJ_KIND_ORSET_WIDE, k {p, r} pairs per element)
+TOKEN_WORDS = 16
+
+
+def _domain() -> Domain:
+    return Domain(token_capacity=64 * TOKEN_WORDS)
+
+
+def _new(R: int, E: int, k: int):
+    return context().orset_batch(R, E) if k == 1 else context().orset_wide_batch(R, E, k)
+
+
+def _batch(dom: Domain, states: Sequence, k: int = 1) -> Tuple[engine.ORSetBatch, int]:
+    k = max(k, dom.orset_words(states))
     E = max(1, dom.size)
-    b = context().orset_batch(len(states), E)
-    b.upload(dom.encode_orset(states, E))
+    b = _new(len(states), E, k)
+    b.upload(dom.encode_orset(states, E) if k == 1 else dom.encode_orset_wide(states, E, k))
     return b, E
+
+
+def _decode(dom: Domain, cells: np.ndarray) -> list:
+    return dom.decode_orset_wide(cells) if cells.ndim == 3 else dom.decode_orset(cells)
 
 
 # --------------------------------------------------------------------------- API
@@ -54,20 +70,19 @@ def merge_many(pairs: Sequence[Tuple[list, list]]) -> List[list]:
     """merge/2 over many independent pairs in one launch."""
     if not pairs:
         return []
-    dom = Domain()
-    A, E = _batch(dom, [p[0] for p in pairs])
-    B, _ = _batch(dom, [p[1] for p in pairs])
-    if B.elements != E:             # B registered more elements: re-encode A at B's size
-        A, E = _batch(dom, [p[0] for p in pairs])
-    C = context().orset_batch(len(pairs), E)
+    dom = _domain()
+    k = dom.orset_words([p[0] for p in pairs] + [p[1] for p in pairs])
+    A, E = _batch(dom, [p[0] for p in pairs], k)
+    B, _ = _batch(dom, [p[1] for p in pairs], k)
+    C = _new(len(pairs), E, k)
     C.join(A, B)
     out = C.download()
-    return [dom.decode_orset(out[i]) for i in range(len(pairs))]
+    return [_decode(dom, out[i]) for i in range(len(pairs))]
 
 
 def value(s):
     """value/1 — lasp_orset.erl:67-73 (device value bitmap)."""
-    dom = Domain()
+    dom = _domain()
     b, _ = _batch(dom, [s])
     return dom.decode_value_bits(b.value_bits()[0])
 
@@ -79,17 +94,18 @@ def value2(query, s):
         return [] if toks == [] else [(query[1], toks)]
     if isinstance(query, tuple) and len(query) == 2 and query[0] == "tokens":
         # orddict:find(Elem, ORSet): the element's cell, read on the device
-        dom = Domain()
+        dom = _domain()
         b, _ = _batch(dom, [s])
         es = dom.element_slot(query[1], create=False)
         if es < 0:
             return []
-        cell = b.fragment(es)[0]
-        p, r = int(cell[0]), int(cell[1])
+        pairs = b.fragment(es)[0].reshape(-1, 2)
+        p = sum(int(pairs[j, 0]) << (64 * j) for j in range(len(pairs)))
+        r = sum(int(pairs[j, 1]) << (64 * j) for j in range(len(pairs)))
         td = dom.tokens[es]
         return [(td.terms[k], bool((r >> int(k)) & 1)) for k in td.order() if (p >> int(k)) & 1]
     if query == "removed":
-        dom = Domain()
+        dom = _domain()
         b, _ = _batch(dom, [s])
         return dom.decode_value_bits(b.value_bits(removed=True)[0])
     return value(s)
@@ -98,27 +114,26 @@ def value2(query, s):
 def precondition_context(s):
     """precondition_context/1 — lasp_orset.erl:147-154: the adds observed (tokens
     flagged false), computed on the device."""
-    dom = Domain()
+    dom = _domain()
     b, E = _batch(dom, [s])
-    out = context().orset_batch(1, E).precondition_context(b)
-    return dom.decode_orset(out.download()[0])
+    out = _new(1, E, getattr(b, "token_words", 1)).precondition_context(b)
+    return _decode(dom, out.download()[0])
 
 
 def update(op, actor, s):
     """update/3 — lasp_orset.erl:99-117.  Returns ("ok", S1) or
     ("error", ("precondition", ("not_present", Elem)))."""
-    dom = Domain()
-    dom.register_orset(s)
+    dom = _domain()
+    k = dom.orset_words([s])
     ops = []
     _compile(op, dom, ops, new_call=True)
-    E = max(1, dom.size)
-    b = context().orset_batch(1, E)
-    b.upload(dom.encode_orset([s], E))
+    k = max([k] + [(o[3] >> 6) + 1 for o in ops if o[2] != _lib.OP_REMOVE])
+    b, _E = _batch(dom, [s], k)
     st = b.apply_ops(ops)
     bad = np.nonzero(st == _lib.OPST_NOT_PRESENT)[0]
     if len(bad):
         return ("error", ("precondition", ("not_present", dom.elements.terms[ops[bad[0]][1]])))
-    return ("ok", dom.decode_orset(b.download()[0]))
+    return ("ok", _decode(dom, b.download()[0]))
 
 
 def update4(op, actor, s, _ctx=None):
@@ -178,20 +193,16 @@ def _compile(op, dom: Domain, ops: list, new_call: bool) -> None:
 
 def equal(a, b) -> bool:
     """equal/2 — lasp_orset.erl:136-138."""
-    dom = Domain()
-    dom.register_orset(a)
-    dom.register_orset(b)
-    E = max(1, dom.size)
-    A = context().orset_batch(1, E)
-    B = context().orset_batch(1, E)
-    A.upload(dom.encode_orset([a], E))
-    B.upload(dom.encode_orset([b], E))
+    dom = _domain()
+    k = dom.orset_words([a, b])
+    A, _E = _batch(dom, [a], k)
+    B, _E = _batch(dom, [b], k)
     return bool(A.equal(B)[0])
 
 
 def stats(s):
     """stats/1 — lasp_orset.erl:156-161."""
-    dom = Domain()
+    dom = _domain()
     b, _ = _batch(dom, [s])
     elems, adds, rems = (int(x) for x in b.stats()[0])
     return [("element_count", elems), ("adds_count", adds), ("removes_count", rems),

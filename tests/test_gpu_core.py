@@ -197,10 +197,12 @@ def test_store_unrepresentable_values_raise_not_swallowed():
     a 65th token, an element past the store's capacity) must not make bind/3 answer `ok`
     with the variable unchanged — the reference's merge takes it and lasp_core.erl:300-304
     writes it.  The device store raises Unsupported, keeps the value it had (equal to the
-    oracle store's value before the failing call) and registers no slots for the attempt."""
+    oracle store's value before the failing call) and registers no slots for the attempt.
+    The token limit is 64 * token_words (16 words by default, test_gpu_wide.py); one word
+    here."""
     from lasp_amd import core as dcore
     toks = [bytes([7, k]) + bytes(18) for k in range(66)]
-    ds, os_ = dcore.Store(capacity=8), ocore.Store()
+    ds, os_ = dcore.Store(capacity=8, token_words=1), ocore.Store()
     ids = []
     for st in (ds, os_):
         _, a = st.declare("lasp_orset")

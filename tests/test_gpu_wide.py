@@ -167,3 +167,83 @@ def test_wide_bind_many_and_rejections():
             narrow.join(narrow, bs[0])
     finally:
         ctx.close()
+
+
+def test_store_wide_variables_match_oracle_store():
+    """lasp_core over the device with elements past 64 tokens (lasp_amd.core.Store): a
+    variable moves to wide cells when its value names token slot >= 64 (bind, bind_many,
+    update/3), a narrow variable binding a wide value is widened on the device
+    (laspj_orset_widen), threshold reads compare across widths, and every value decodes
+    to exactly the oracle store's term (oracle/core.py)."""
+    from lasp_amd import core as dcore
+    from oracle import core as ocore
+    from oracle.terms import exact_eq
+    reps = _replicas(seed=3, adds=100)
+    ds, os_ = dcore.Store(capacity=64), ocore.Store()
+    ids = []
+    for st in (ds, os_):
+        _, a = st.declare("lasp_orset")
+        _, b = st.declare("lasp_orset")
+        _, c = st.declare("lasp_orset")
+        st.bind(b, [(3, [(b"\x01" * 20, False)])])         # narrow cells first
+        st.bind(c, [(4, [(b"\x02" * 20, False)])])
+        ids.append((a, b, c))
+    (ad, bd, cd), (ao, bo, co) = ids
+    for s in reps:
+        ds.bind(ad, s)
+        os_.bind(ao, s)
+        assert exact_eq(ds.value(ad), os_.value(ao))
+    assert ds.vars[ad].val.token_words == 5
+    assert getattr(ds.vars[bd].val, "token_words", 1) == 1
+    ds.bind(bd, reps[0])                                   # narrow variable, wide value
+    os_.bind(bo, reps[0])
+    assert exact_eq(ds.value(bd), os_.value(bo))
+    assert ds.vars[bd].val.token_words > 1
+    # bind_many: a wide value into a narrow variable and a narrow one into a wide variable
+    small = [(3, [(b"\x05" * 20, False)])]
+    ds.bind_many([(cd, reps[1]), (ad, small)])
+    os_.bind(co, reps[1])
+    os_.bind(ao, small)
+    assert exact_eq(ds.value(cd), os_.value(co)) and exact_eq(ds.value(ad), os_.value(ao))
+    # update/3 on a wide variable, and one minting the 65th token of a narrow variable
+    _, nd = ds.declare("lasp_orset")
+    _, no = os_.declare("lasp_orset")
+    for k in range(70):
+        op = ("add_by_token", bytes([9, k]) + bytes(18), 1)
+        ds.update(nd, op, None)
+        os_.update(no, op, None)
+    assert exact_eq(ds.value(nd), os_.value(no))
+    assert ds.vars[nd].val.token_words == 2
+    for op in [("add_by_token", b"\x09" * 20, 7), ("remove", 7), ("add_by_token", b"\x0a" * 20, 11)]:
+        ds.update(ad, op, None)
+        os_.update(ao, op, None)
+    assert exact_eq(ds.value(ad), os_.value(ao))
+    assert ds.type_value(ad) == oorset.value(os_.value(ao))
+    # threshold reads across widths: a narrow threshold on a wide value and back
+    assert ds.read(ad, small) is not None and os_.read(ao, small) is not None
+    assert (ds.read(cd, ("strict", reps[0])) is None) == (os_.read(co, ("strict", reps[0])) is None)
+    assert ds.read(ad, ("strict", os_.value(ao))) is None
+    # combinator bodies take narrow values only: documented Unsupported
+    _, ud = ds.declare("lasp_orset")
+    with pytest.raises(dcore.Unsupported):
+        ds.union(ad, cd, ud)
+
+
+def test_module_api_wide_values_match_oracle():
+    """lasp_amd.orset (the lasp_orset mirror) on values past 64 tokens per element:
+    merge / value / value({tokens, E}) / precondition_context / update / equal / stats on
+    wide cells, against oracle/orset.py."""
+    from lasp_amd import orset as dorset
+    reps = _replicas(seed=4, adds=90)
+    m = oorset.merge(reps[0], reps[1])
+    assert dorset.merge(reps[0], reps[1]) == m
+    assert dorset.merge_many([(reps[0], reps[2]), (reps[1], [])]) == \
+        [oorset.merge(reps[0], reps[2]), oorset.merge(reps[1], [])]
+    assert dorset.value(m) == oorset.value(m)
+    assert dorset.value2(("tokens", 7), m) == oorset.value2(("tokens", 7), m)
+    assert dorset.value2("removed", m) == oorset.value2("removed", m)
+    assert dorset.precondition_context(m) == oorset.precondition_context(m)
+    assert dorset.equal(m, m) and not dorset.equal(m, reps[0])
+    assert [v for _k, v in dorset.stats(m)] == [v for _k, v in oorset.stats(m)]
+    for op in [("add_by_token", b"\x0b" * 20, 7), ("remove", 7), ("remove", 999)]:
+        assert dorset.update(op, None, m) == oorset.update(op, None, m)

@@ -103,3 +103,46 @@ def test_dict_order_incremental_matches_sort():
                     dd.slot(random.random())
         want = sorted(range(len(dd.terms)), key=lambda i: term_key(dd.terms[i]))
         assert list(dd.order()) == want
+
+
+def test_wide_domain_list_tables_hold_token_slots_below_64():
+    """A Store domain with more than 64 token slots per element (wide OR-Set cells): list
+    values name 64 token slots per element (g = 64 e + k), so the rank tables place slots
+    0..63 only — bulk and incremental paths — the from_set token-order rows list those,
+    and encoding a list value that names a later slot raises CapacityError (the store's
+    Unsupported) instead of aliasing another element's token id."""
+    from lasp_amd.codec import CapacityError
+    random.seed(11)
+    for bulk in (False, True):
+        d = Domain(element_capacity=1 << 12, token_capacity=64 * 4)
+        sp = L.ListSpace(_Ctx(), d, tokens=True)
+        nel = 80 if bulk else 2
+        for e in range(nel):
+            es = d.element_slot(e)
+            ks = list(range(100))
+            random.shuffle(ks)
+            for k in ks:
+                d.token_slot(es, (e, k))
+        o = sp.order()
+        assert o.ntokens == 64 * d.size
+        gr = sp._gbuf.mem.view(np.uint32)
+        for e in range(nel):
+            terms = d.tokens[e].terms[:64]
+            labs = [int(gr[64 * e + k]) for k in range(64)]
+            assert all(lab > 0 for lab in labs)
+            assert sorted(range(64), key=lambda k: labs[k]) == \
+                sorted(range(64), key=lambda k: term_key(terms[k]))
+        _eb, _n, tb = sp.set_orders(d.size)
+        row = tb.mem[64 * 0: 64 * 1]
+        want = [k for k in d.tokens[0].order() if k < 64]
+        assert [int(x) for x in row[:len(want)]] == want and len(want) == 64
+    late = next(t for k, t in enumerate(d.tokens[0].terms) if k >= 64)
+    with pytest.raises(CapacityError):
+        L.encode(d, [(0, [(late, False)])], False)
+    with pytest.raises(CapacityError):
+        d.encode_orset([[(0, [(late, False)])]], d.size)
+    assert d.orset_words([[(0, [(late, False)])]]) == 2
+    early = d.tokens[0].terms[3]
+    s = sorted([(early, False), (late, True)], key=lambda x: term_key(x[0]))
+    cells = d.encode_orset_wide([[(0, s)]], d.size, 2)
+    assert d.decode_orset_wide(cells[0]) == [(0, s)]
