@@ -169,12 +169,20 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         every payload longer than this (>= 256, a
                                         multiple of 256)                               */
 #define LASPJ_TUNE_LIST_WALK    10   /* list merges whose keys descend somewhere: 0 = the
-                                        run-jumping walk, 1 = one step per element      */
+                                        default (the chunked walk over the chip when an
+                                        input is known not to ascend, else the one-wave
+                                        run-jumping walk), 1 = one step per element,
+                                        3 = the chunked walk whenever few replicas merge;
+                                        2 = list_bind never takes its rank-indexed path
+                                        (both lists ascending); for A/B               */
 #define LASPJ_TUNE_NIF_PASSES   14   /* NIF entry points: device passes a call may take
                                         (0 = default 6; registering unseen terms, a grown
                                         answer area and a serial re-decode take one each).
                                         A call still unresolved after them answers
                                         LASPJ_NIF_FALLBACK — for tests of that guard      */
+#define LASPJ_TUNE_LIST_CHUNK   15   /* rows per chunk of the list merges' chunked walk
+                                        (0 = default: 1024, or more to keep <= 1024
+                                        chunks; 64 .. 2^20)                             */
 int         laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value);
 
 /* ------------------------------------------------------------------ device buffers */

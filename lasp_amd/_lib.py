@@ -41,6 +41,7 @@ TUNE_ETF_READ = 8
 TUNE_ETF_SEG = 9
 TUNE_LIST_WALK = 10
 TUNE_NIF_PASSES = 14
+TUNE_LIST_CHUNK = 15
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
 NIF_STATS = 18
 

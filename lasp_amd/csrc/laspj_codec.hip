@@ -839,13 +839,19 @@ __device__ void lb_finish(const LBJoin& lb, uint32_t nch, uint32_t hdr, uint8_t*
     __shared__ uint32_t s_lb_last;
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence_system();            // this block's answer bytes (host memory) first
+        // chunk 0's header bytes (host memory) land before the last block rewrites them;
+        // the other blocks' bytes are ordered by the kernel's end
+        if (blockIdx.x == 0) __threadfence_system();
         s_lb_last = atomicAdd(lb.ticket, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!s_lb_last || threadIdx.x != 0) return;
-    __threadfence_system();
-    const u64 w = __hip_atomic_load(lb.st + nch - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    u64 w;
+    for (;;) {                             // the last chunk's inclusive word (relaxed)
+        w = __hip_atomic_load(lb.st + nch - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w >> 62) == 2) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
     const u64 bytes = w & (kLBCnt - 1), n = (w & kLBVal) >> 40;
     u64 total;
     if (n) {
@@ -1026,22 +1032,27 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                     const uint32_t ch = c0 / kBlock;
                     const u64 own = (u64)tot + ((tot2 >> 52) & 0xFFFull) * kLBCnt;
                     u64 acc = 0;
+                    // (the words carry their whole payload: relaxed device-scope atomics,
+                    // no L2 write-back / invalidate per step as release / acquire would)
                     if (ch == 0) {
-                        __hip_atomic_store(lb.st, (2ull << 62) | own, __ATOMIC_RELEASE,
+                        __hip_atomic_store(lb.st, (2ull << 62) | own, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     } else {
-                        __hip_atomic_store(lb.st + ch, (1ull << 62) | own, __ATOMIC_RELEASE,
+                        __hip_atomic_store(lb.st + ch, (1ull << 62) | own, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                         for (int32_t j = (int32_t)ch - 1; j >= 0;) {
-                            const u64 w = __hip_atomic_load(lb.st + j, __ATOMIC_ACQUIRE,
+                            const u64 w = __hip_atomic_load(lb.st + j, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
-                            if (!(w >> 62)) continue;             // not published yet
+                            if (!(w >> 62)) {                     // not published yet
+                                __builtin_amdgcn_s_sleep(1);
+                                continue;
+                            }
                             acc += w & kLBVal;
                             if ((w >> 62) == 2) break;
                             --j;
                         }
                         __hip_atomic_store(lb.st + ch, (2ull << 62) | (acc + own),
-                                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     s_pre = acc;
                 }

@@ -37,6 +37,7 @@ struct laspj_ctx {
     int64_t tune_product_cols = 0;
     int64_t tune_list_walk = 0;
     int64_t tune_nif_passes = 0;     // NIF device passes per call (0: the default)
+    int64_t tune_list_chunk = 0;     // rows per chunk of the chunked list walk (0: default)
     // device scratch for apply_ops (grown on demand)
     void* scratch = nullptr;
     uint64_t scratch_bytes = 0;
@@ -61,6 +62,22 @@ struct laspj_ctx {
     void* lbind_h = nullptr;
     void* lbind_hd = nullptr;       // its device address
     uint64_t lbind_h_bytes = 0;
+    // list_bind's rank-indexed path (both lists strictly ascending): per-call words and
+    // look-back states (kept zeroed between calls as lbind), and the rank -> entry index
+    // maps, tagged with the call's epoch so they are never cleared (0 never valid)
+    void* lfz = nullptr;            // two halves: a call's words, the previous call's
+    uint64_t lfz_bytes = 0;
+    bool lfz_dirty = false;
+    uint32_t lf_parity = 0;         // the half the last call used
+    uint64_t lf_prev_use = 0;       // the bytes of it that call used (the next one zeroes them)
+    void* lfi = nullptr;
+    uint64_t lfi_bytes = 0;
+    uint32_t lf_epoch = 0;
+    // the list merges' chunked walk (k_merge_spec): per-replica round and chunk words,
+    // kept zeroed between calls by the kernel's last block per replica
+    void* lspec = nullptr;
+    uint64_t lspec_bytes = 0;
+    bool lspec_dirty = false;
     // pinned host staging for the small readbacks (sizes, statuses, flags): a round trip
     // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
     void* pinned = nullptr;
@@ -116,6 +133,13 @@ struct laspj_batch {
     // without reading the inputs' counts back)
     uint32_t known_e = 0;
     uint32_t known_t = 0;
+    // list batches, a hint only: list_bind found some replica's keys not strictly ascending
+    // (or product pairs) — its rank-indexed path is not tried again until the list is
+    // rewritten (upload, or a merge / bind writing it)
+    mutable bool not_asc = false;
+    // (a hint too) a merge of this list's keys with another's took the one-wave walk after
+    // the chunked walk's walks did not meet: the next merge goes to the one-wave walk
+    mutable bool no_spec = false;
 };
 
 inline bool laspj_is_list(int32_t kind) {

@@ -46,6 +46,7 @@ constexpr uint32_t kErrId = 2;       // an item's slot is outside the rank table
 constexpr uint32_t kErrNested = 4;   // product of product outputs (nested pairs)
 constexpr uint32_t kErrTable = 8;    // a map / filter / fold table index out of range
 constexpr uint32_t kErrFun = 16;     // the fun failed on a key present in the list
+constexpr uint32_t kInfoWalkFell = 256;  // (not an error) the chunked walk gave up
 
 struct LV {
     uint32_t* hdr;     // [R][2] {entries, tokens}
@@ -234,6 +235,7 @@ struct MS {
     uint32_t* unsorted;// [R] 1: a side's ranks descend somewhere (lane-0 walk)
     uint32_t* aweak;   // [R] 1: a's keys are not strictly ascending (a tie or a descent)
     uint32_t ce_a, ce_b, ntiles, nchunks;
+    uint32_t spec = 0; // 1: k_merge_spec walks the replicas whose ranks descend
 };
 
 // exclusive prefix sum / running max over a block of kMT threads (s_w: kMT/64 words)
@@ -396,7 +398,7 @@ template <int MODE, bool WALK>
 __device__ void tile_scan_replica(const LV& a, const LV& b, const MS& m, u64 r, uint32_t* s_w,
                                   uint32_t* s_sd) {
     if (m.unsorted[r]) {
-        if (WALK && threadIdx.x < 64) merge_runs_replica<MODE>(a, b, m, r);
+        if (WALK && !m.spec && threadIdx.x < 64) merge_runs_replica<MODE>(a, b, m, r);
         return;
     }
     const uint32_t n = a.n(r) + b.n(r), nt = (n + kMTile - 1) / kMTile;
@@ -815,6 +817,242 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
     }
 }
 
+// ---------------------------------------------------------------- chunked walk
+// The clauses' walk for replicas whose keys descend, spread over the chip (k_merge_spec).
+// Row i of A is emitted at the first column f >= j(i) with B[f] >= A[i] — B[j(i) .. f)
+// go first, alone; B[f] == A[i] pairs with it — and the next row starts at
+// j(i+1) = f + [pair].  So the walk is a chain of monotone maps j -> j' over rows, and
+// two walks of the same rows from different columns meet and then agree.  A wave takes
+// a chunk of L rows and walks it from a guessed column (round 0: proportional), then from
+// the previous chunk's exit of the round before, until no chunk's exit changes — that
+// round's walks are then one consistent walk from (0, 0), i.e. the clauses' own (chunk 0
+// always starts right, so round k has chunks 0 .. k right; reversed lists and lists
+// shuffled alike — tie runs — settle in 2).  Each round ends at a barrier over the replica's blocks (one u64 per
+// round: arrivals | blocks changed << 32, so every block reads the same decision).  Keys
+// shuffled independently on both sides do not meet (measured: 4 chunks of 16k rows took
+// 5 rounds, one chunk settling per round), so when most blocks still change after round
+// 1, or after kSpRounds rounds, the one-wave walk runs instead.
+// Chunk words (double-buffered by round) carry exit | pairs << 32 | last single side <<
+// 52 | round tag << 56.  Then every wave writes its chunk's plan entries at
+// i0 + entry - (pairs before the chunk), ordsets:union's item of a pair from the side of
+// the last single step (carried over chunks).
+constexpr uint32_t kSpW = 4;                // chunks (waves) per block
+constexpr uint32_t kSpRounds = 16;
+constexpr uint32_t kSpWords = kSpRounds + 2;  // per replica: round words, done ticket
+struct SP {
+    u64* w;            // [R][kSpWords] zero on entry, left zero
+    u64* cw;           // [R][2][C] chunk words, zero on entry, left zero
+    uint32_t* fr;      // [R][ce_a] per row: f | pair << 31
+    uint32_t L, C;     // rows per chunk, chunks per replica (gridDim.x * kSpW)
+    uint32_t* flag;    // the call's flag word (kInfoWalkFell)
+};
+
+__device__ __forceinline__ u64 sp_load(const u64* p) {
+    return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// chunk c's word of round `round` (waits for it)
+__device__ __forceinline__ u64 sp_word(const SP& sp, u64 r, uint32_t round, uint32_t c) {
+    const u64* p = sp.cw + (r * 2 + (round & 1)) * sp.C + c;
+    for (;;) {
+        const u64 v = sp_load(p);
+        if ((uint32_t)(v >> 56) == round + 1) return v;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64 * kSpW) void k_merge_spec(LV a, LV b, MS m, SP sp, uint64_t R) {
+    const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        if (!m.unsorted[r]) continue;                    // (uniform over the replica's grid)
+        const uint32_t na = a.n(r), nb = b.n(r);
+        const u64* SA = m.sa + r * m.ce_a;
+        const u64* SB = m.sb + r * m.ce_b;
+        const uint32_t c = blockIdx.x * kSpW + wv;
+        const uint32_t nc = (na + sp.L - 1) / sp.L;      // chunks with rows
+        const uint32_t i0 = c < nc ? c * sp.L : na, i1 = c < nc ? min(na, i0 + sp.L) : na;
+        u64* w = sp.w + r * kSpWords;
+        uint32_t* fr = sp.fr + r * m.ce_a;
+        uint32_t round = 0, entry = 0;
+        bool fallback = false;
+        for (;;) {
+            bool changed = false;
+            if (c < nc) {
+                if (c == 0) entry = 0;
+                else if (round == 0) entry = (uint32_t)((u64)i0 * nb / na);
+                else entry = (uint32_t)sp_word(sp, r, round - 1, c - 1);
+                // the walk of rows [i0, i1) from column `entry`, a run at a time (as
+                // merge_runs_replica): rows of an A run take f = j, a tie run f = j + k
+                // with the pair bit, a B run moves j
+                Win256 A{SA, i1, 0, {}}, B{SB, nb, 0, {}};
+                A.load(i0);
+                B.load(entry);
+                uint32_t i = i0, j = entry, pairs = 0, side = 0;
+                while (i < i1) {
+                    uint32_t L;
+                    if (j >= nb) {                                  // B is done: rows alone
+                        L = i1 - i;
+                        for (uint32_t k = lane; k < L; k += 64) fr[i + k] = nb;
+                        i = i1;
+                        side = 1;
+                        break;
+                    }
+                    if (i - A.base >= 192u) A.load(i);
+                    if (j - B.base >= 192u) B.load(j);
+                    const u64 x = A.at(i), y = B.at(j);
+                    if (x == y) {
+                        if (i - A.base != j - B.base) {
+                            A.load(i);
+                            B.load(j);
+                        }
+                        const uint32_t s0 = i - A.base;
+                        L = win_fail<0>(A, B, s0, 0) - s0;
+                        if (L == 256u - s0) L += stream_run<0>(SA, i1, i + L, SB, nb, j + L, 0);
+                        L = min(L, i1 - i);
+                        for (uint32_t k = lane; k < L; k += 64) fr[i + k] = (j + k) | 0x80000000u;
+                        pairs += L;
+                        i += L;
+                        j += L;
+                    } else if (x < y) {
+                        const uint32_t s0 = i - A.base;
+                        L = win_fail<1>(A, B, s0, y) - s0;
+                        if (L == 256u - s0) L += stream_run<1>(SA, i1, i + L, nullptr, 0, 0, y);
+                        L = min(L, i1 - i);
+                        for (uint32_t k = lane; k < L; k += 64) fr[i + k] = j;
+                        i += L;
+                        side = 1;
+                    } else {
+                        const uint32_t s0 = j - B.base;
+                        L = win_fail<2>(A, B, s0, x) - s0;
+                        if (L == 256u - s0) L += stream_run<1>(SB, nb, j + L, nullptr, 0, 0, x);
+                        j += L;
+                        side = 2;
+                    }
+                }
+                if (round > 0) changed = (uint32_t)sp_word(sp, r, round - 1, c) != j;
+                if (lane == 0)
+                    __hip_atomic_store(sp.cw + (r * 2 + (round & 1)) * sp.C + c,
+                                       (u64)j | ((u64)pairs << 32) | ((u64)side << 52) |
+                                           ((u64)(round + 1) << 56),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // the round's barrier over the replica's blocks, with its decision
+            __shared__ uint32_t s_ch;
+            if (threadIdx.x == 0) s_ch = 0;
+            __syncthreads();
+            if (lane == 0 && changed) atomicOr(&s_ch, 1u);
+            __syncthreads();
+            __shared__ u64 s_word;
+            if (threadIdx.x == 0) {
+                u64* rw = w + round;
+                __hip_atomic_fetch_add(rw, 1ull | ((u64)s_ch << 32), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                u64 v;
+                while ((uint32_t)(v = sp_load(rw)) < gridDim.x) __builtin_amdgcn_s_sleep(1);
+                s_word = v;
+            }
+            __syncthreads();
+            if (round > 0 && (uint32_t)(s_word >> 32) == 0) break;   // settled
+            // walks that do not meet (keys shuffled independently on both sides: the gap
+            // between two walks closes only when a row's key tops every B key in it) change
+            // most chunks every round: the one-wave walk then, without more rounds
+            if (++round == kSpRounds || (round > 1 && 2 * (uint32_t)(s_word >> 32) > gridDim.x)) {
+                fallback = true;
+                break;
+            }
+        }
+        if (fallback) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(sp.flag, kInfoWalkFell);
+            if (blockIdx.x == 0 && wv == 0) merge_runs_replica<MODE>(a, b, m, r);
+        } else if (c < nc || (c == 0 && nc == 0)) {
+            // the plan entries of this chunk (the final round's walk, from fr)
+            uint32_t before = 0, sidx = 0;                // pairs before; last sided chunk + 1
+            for (uint32_t k = lane; k < c; k += 64) {
+                const u64 v = sp_word(sp, r, round, k);
+                before += (uint32_t)(v >> 32) & 0xFFFFFu;
+                if ((v >> 52) & 3u) sidx = k + 1 > sidx ? k + 1 : sidx;
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                before += __shfl_xor(before, off, 64);
+                const uint32_t o2 = __shfl_xor(sidx, off, 64);
+                sidx = o2 > sidx ? o2 : sidx;
+            }
+            uint32_t side = 1;                                  // A at the start
+            if (MODE == 2 && sidx) side = (uint32_t)(sp_word(sp, r, round, sidx - 1) >> 52) & 3u;
+            u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
+            // 64 rows at a time, a row per lane: its entry column (the row before's f +
+            // pair), its place i + j - (pairs before), its B run, its own entry; ordsets:
+            // union's pair item from the last single side before it (a wave max-scan)
+            uint32_t j = entry, pbefore = before;
+            for (uint32_t g = i0; g < i1; g += 64) {
+                const uint32_t i = g + lane;
+                const bool live = i < i1;
+                const uint32_t e = live ? fr[i] : 0u;
+                const uint32_t f = e & 0x7FFFFFFFu;
+                const uint32_t pr = live ? e >> 31 : 0u;
+                uint32_t jn = __shfl_up(f + pr, 1, 64);          // the row before's exit
+                if (lane == 0) jn = j;
+                uint32_t ptot;
+                const uint32_t pex = wave_excl(pr, &ptot);
+                const uint32_t o = i + jn - (pbefore + pex);     // this row's B run starts here
+                const uint32_t run = live ? f - jn : 0u;
+                auto bent = [&](uint32_t k) {
+                    return MODE == 2 ? (u64)k | (1ull << 32) : (u64)kNone | ((u64)k << 32);
+                };
+                if (run <= 32)
+                    for (uint32_t k = 0; k < run; ++k) plan[o + k] = bent(jn + k);
+                for (u64 longs = __ballot(run > 32); longs; longs &= longs - 1) {
+                    const int l = __builtin_ctzll(longs);            // a long run: wave-wide
+                    const uint32_t lo = __shfl(o, l, 64), lj = __shfl(jn, l, 64),
+                                   lr = __shfl(run, l, 64);
+                    for (uint32_t k = lane; k < lr; k += 64) plan[lo + k] = bent(lj + k);
+                }
+                // ordsets:union's item of a pair: the side before this row's own entry —
+                // B when its run went first, else the last row before it that set one (A
+                // alone, or a B run), else the carried side
+                const uint32_t setter = live ? (!pr ? 1u : (run ? 2u : 0u)) : 0u;
+                uint32_t allmax;
+                const uint32_t prev_idx = wave_excl_max(setter ? lane + 1 : 0u, &allmax);
+                const uint32_t prev_side = __shfl(setter, prev_idx ? prev_idx - 1 : 0, 64);
+                if (live) {
+                    u64 ent;
+                    if (MODE == 2) {
+                        const uint32_t sd = run ? 2u : (prev_idx ? prev_side : side);
+                        ent = pr && sd == 2 ? (u64)f | (1ull << 32) : (u64)i;
+                    } else {
+                        ent = (u64)i | ((u64)(pr ? f : kNone) << 32);
+                    }
+                    plan[o + run] = ent;
+                }
+                // carry: the last live row's exit, pairs, and the side after the group
+                const uint32_t last = min(63u, i1 - 1 - g);
+                j = __shfl(f + pr, last, 64);
+                pbefore += ptot;
+                if (MODE == 2 && allmax) side = __shfl(setter, allmax - 1, 64);
+            }
+            uint32_t o = i1 + j - pbefore;
+            if (c + 1 >= nc) {                                   // the last chunk: B's tail
+                for (uint32_t k = lane; k < nb - j; k += 64)
+                    plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
+                                            : (u64)kNone | ((u64)(j + k) << 32);
+                if (lane == 0) m.nout[r] = o + (nb - j);
+            }
+        }
+        // the replica's words back to zero (the block that finishes last)
+        __syncthreads();
+        __shared__ uint32_t s_last;
+        if (threadIdx.x == 0)
+            s_last = __hip_atomic_fetch_add(w + kSpRounds + 1, 1ull, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        __syncthreads();
+        if (s_last) {
+            for (uint32_t k = threadIdx.x; k < 2 * sp.C; k += 64 * kSpW) sp.cw[r * 2 * sp.C + k] = 0;
+            for (uint32_t k = threadIdx.x; k < kSpWords; k += 64 * kSpW) w[k] = 0;
+        }
+    }
+}
+
 // the token count of planned entry o (inner orddict:merge, or the run it copies)
 template <int MODE>
 __device__ __forceinline__ uint32_t entry_tokens(const LV& a, const LV& b, u64 r, u64 p,
@@ -1040,6 +1278,238 @@ __global__ __launch_bounds__(256) void k_list_equal_grid(LV a, LV b, RK rk, uint
         w[0] = 0;
         *ticket = 0;
         __threadfence_system();
+    }
+}
+
+// ---------------------------------------------------------------- list_bind, ascending
+// When both lists' keys strictly ascend in term order (plain keys: every orddict and
+// ordset, an intersection / filter output of one, a merge of two), orddict:merge's and
+// ordsets:union's two-finger walk visits the keys in rank order and pairs equal keys:
+// the merged list has one entry per rank that either side holds — both sides: the inner
+// token merge (merge/2's F), ordsets:union's equal elements being one slot — in rank
+// order.  So this bind needs no merge path, no plan and no per-entry scans:
+//   k_lbf_prep   entry i of each side -> its rank's cell of a rank-indexed map (tagged
+//                with the call's epoch, so the maps are never cleared), the ascent
+//                checked against the lane below, every token id checked, and
+//                `Value0 =:= Value` over the grid
+//   k_lbf_write  256 ranks per block (one per thread): entry present?, token count (inner
+//                merge or run); offsets from a block scan and a decoupled look-back over
+//                the rank tiles; the merged list written; each replica's last tile writes
+//                its part of bind/3's answer
+// is_inflation(Value0, Merged) holds by construction when Value0 ascends (k_linf_probe's
+// skip, below), so the answer is equal ? 0 : 1.  A replica that does not ascend (or
+// carries product pairs, or an id outside the rank tables) answers 3 and the call runs
+// the merge path instead, which reports the errors.  No tickets, no fences: tiles are
+// block indices (dispatched in order), the look-back words carry their whole payload,
+// and the words a call uses are zeroed by the NEXT call (two parities), so nothing
+// waits for the whole grid to finish.
+constexpr uint32_t kLfT = 256;              // threads per block
+constexpr uint32_t kLfPer = 1;              // ranks per thread (4 measured slower: 42 vs 31 us;
+                                            // runs loaded into registers up front: 56 us)
+constexpr uint32_t kLfTile = kLfT * kLfPer; // ranks per tile
+struct LF {
+    u64* ia;          // [R][nk] epoch << 32 | index of the entry of A (Value0) with rank v
+    u64* ib;          // [R][nk] the same for B (Value)
+    uint32_t* w;      // this call's words [diff R | bad R], zero on entry
+    u64* st;          // this call's look-back words [R][ntiles]: state << 62 | entries << 32
+                      // | tokens, zero on entry
+    uint32_t* wz;     // the previous call's words and look-back words, zeroed here
+    uint64_t nwz;     //   (32-bit words)
+    uint32_t* hneed;  // host answer: need [R][2], then status R bytes
+    uint32_t epoch, nk, ntiles, R;
+};
+
+__device__ __forceinline__ bool tok_ok(u64 it, const RK& rk) {
+    if (it & kCompound)
+        return (uint32_t)((it >> 31) & kIdMask) < rk.ng && (uint32_t)(it & kIdMask) < rk.ng;
+    return (uint32_t)(it & kIdMask) < rk.ng;
+}
+
+// a side's entry i: its rank into the map when the keys ascend, else bad |= bit
+__device__ __forceinline__ uint32_t lbf_side(const LV& x, u64 r, uint32_t i, uint32_t n,
+                                             const RK& rk, const LF& f, u64* map,
+                                             uint32_t bit, u64* rank_out) {
+    u64 rank = ~0ull;
+    bool ok = true;
+    if (i < n) {
+        const u64 it = x.K(r)[i];
+        const uint32_t e = (uint32_t)(it & kIdMask);
+        if ((it & kPair) || e >= rk.nk) ok = false;         // (pairs: no rank universe)
+        else rank = rk.krank[e];
+        if (rank >= f.nk) ok = false;
+    }
+    u64 prev = __shfl_up(rank, 1, 64);                      // the previous entry's rank
+    if (lane_id() == 0 && i > 0 && i < n) {
+        const u64 it = x.K(r)[i - 1];
+        const uint32_t e = (uint32_t)(it & kIdMask);
+        prev = (it & kPair) || e >= rk.nk ? ~0ull : (u64)rk.krank[e];
+    }
+    if (i < n && i > 0 && !(prev < rank)) ok = false;
+    if (i < n && ok) map[r * f.nk + rank] = ((u64)f.epoch << 32) | i;
+    *rank_out = rank;
+    return i < n && !ok ? bit : 0u;
+}
+
+template <bool GSET>
+__global__ __launch_bounds__(256) void k_lbf_prep(LV a, LV b, RK rk, LF f, uint64_t R) {
+    for (u64 r = blockIdx.y; r < R; r += gridDim.y) {
+        const uint32_t na = a.n(r), nb = b.n(r), nta = a.nt(r), ntb = b.nt(r);
+        const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+        u64 ra, rb;
+        uint32_t bad = lbf_side(a, r, i, na, rk, f, f.ia, 1u, &ra);
+        bad |= lbf_side(b, r, i, nb, rk, f, f.ib, 2u, &rb);
+        // every token id inside the rank tables (the write pass reads ranks unchecked)
+        if (!GSET) {
+            if (i < nta && !tok_ok(a.T(r)[i], rk)) bad |= 1u;
+            if (i < ntb && !tok_ok(b.T(r)[i], rk)) bad |= 2u;
+        }
+        // `Value0 =:= Value` (k_list_equal_grid's comparisons)
+        bool d = false;
+        if (na != nb || nta != ntb) {
+            d = i == 0;
+        } else {
+            if (i < na) d = ra != rb || a.O(r)[i] != b.O(r)[i];
+            if (!GSET && i < nta) {
+                const u64 x = a.T(r)[i], y = b.T(r)[i];
+                if (tok_ok(x, rk) && tok_ok(y, rk))
+                    d = d || tok_ord(x, rk) != tok_ord(y, rk) || ((x ^ y) & kRemoved) != 0;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) bad |= __shfl_xor(bad, off, 64);
+        if (__ballot(d) && lane_id() == 0) atomicOr(f.w + r, 1u);
+        if (bad && lane_id() == 0) atomicOr(f.w + R + r, bad);
+    }
+}
+
+__device__ __forceinline__ u64 wave_excl64(u64 v, u64* total) {
+    u64 x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u64 y = __shfl_up(x, off, 64);
+        if ((int)lane_id() >= off) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kLfT) void k_lbf_write(LV a, LV b, LV out, RK rk, LF f) {
+    __shared__ u64 s_w[kLfT / 64];
+    __shared__ u64 s_base;
+    constexpr u64 kVal = (1ull << 62) - 1;
+    if (blockIdx.x == 0 && blockIdx.y == 0)                 // the previous call's words
+        for (u64 k = threadIdx.x; k < f.nwz; k += kLfT) f.wz[k] = 0;
+    const uint32_t t = blockIdx.x;
+    for (u64 r = blockIdx.y; r < f.R; r += gridDim.y) {
+        const uint32_t bad = f.w[f.R + r];                  // (the prep pass's, uniform)
+        uint8_t* hst = reinterpret_cast<uint8_t*>(f.hneed + 2 * f.R);
+        if (bad) {
+            if (t == f.ntiles - 1 && threadIdx.x == 0) hst[r] = (uint8_t)(3u | (bad << 2));
+            continue;
+        }
+        const uint32_t* OA = a.O(r);
+        const uint32_t* OB = b.O(r);
+        uint32_t ia[kLfPer], jb[kLfPer], cnt[kLfPer];
+        u64 mine = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kLfPer; ++k) {
+            const uint32_t v = t * kLfTile + threadIdx.x * kLfPer + k;   // (rank order = thread order)
+            ia[k] = kNone, jb[k] = kNone, cnt[k] = 0;
+            if (v < f.nk) {
+                const u64 xa = f.ia[r * f.nk + v], xb = f.ib[r * f.nk + v];
+                if ((uint32_t)(xa >> 32) == f.epoch) ia[k] = (uint32_t)xa;
+                if ((uint32_t)(xb >> 32) == f.epoch) jb[k] = (uint32_t)xb;
+            }
+            const bool has = ia[k] != kNone || jb[k] != kNone;
+            if (MODE == 2) {
+                // ordsets:union's pair of equal rank from two slots (1 and 1.0): its item
+                // is the side of the walk's last single step (the merge path's work).
+                // G-Set lists have no tokens: the count field carries these pairs through
+                // the look-back to the last tile
+                cnt[k] = ia[k] != kNone && jb[k] != kNone && a.K(r)[ia[k]] != b.K(r)[jb[k]];
+            } else if (has) {
+                if (ia[k] != kNone && jb[k] != kNone)
+                    cnt[k] = inner_merge<false>(a.T(r) + OA[ia[k]], OA[ia[k] + 1] - OA[ia[k]],
+                                                b.T(r) + OB[jb[k]], OB[jb[k] + 1] - OB[jb[k]],
+                                                nullptr, rk);
+                else if (ia[k] != kNone) cnt[k] = OA[ia[k] + 1] - OA[ia[k]];
+                else cnt[k] = OB[jb[k] + 1] - OB[jb[k]];
+            }
+            mine += ((u64)has << 32) | cnt[k];
+        }
+        // entries << 32 | tokens: one scan carries both (tokens stay below 2^32)
+        u64 wt;
+        const u64 x = wave_excl64(mine, &wt);
+        const uint32_t wv = threadIdx.x >> 6;
+        __syncthreads();
+        if (lane_id() == 0) s_w[wv] = wt;
+        __syncthreads();
+        u64 ex = x, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kLfT / 64; ++k) {
+            ex += k < wv ? s_w[k] : 0ull;
+            tot += s_w[k];
+        }
+        if (threadIdx.x == 0) {
+            // relaxed device-scope atomics: the words carry their whole payload (acquire /
+            // release would write back and invalidate the XCD's L2 at every step)
+            u64* st = f.st + r * f.ntiles;
+            u64 prefix = 0;
+            if (t == 0) {
+                __hip_atomic_store(st, (2ull << 62) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(st + t, (1ull << 62) | tot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                for (int64_t j = (int64_t)t - 1; j >= 0;) {
+                    const u64 sj = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!(sj >> 62)) {                              // not published yet
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    prefix += sj & kVal;
+                    if ((sj >> 62) == 2) break;
+                    --j;
+                }
+                __hip_atomic_store(st + t, (2ull << 62) | (prefix + tot), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_base = prefix;
+        }
+        __syncthreads();
+        u64 pos = s_base + ex;
+#pragma unroll
+        for (uint32_t k = 0; k < kLfPer; ++k) {
+            if (ia[k] == kNone && jb[k] == kNone) continue;
+            const uint32_t o = (uint32_t)(pos >> 32), tp = (uint32_t)pos;
+            out.K(r)[o] = ia[k] != kNone ? a.K(r)[ia[k]] : b.K(r)[jb[k]];
+            if (MODE != 2) {
+                out.O(r)[o] = tp;
+                u64* to = out.T(r) + tp;
+                if (ia[k] != kNone && jb[k] != kNone) {
+                    inner_merge<true>(a.T(r) + OA[ia[k]], OA[ia[k] + 1] - OA[ia[k]],
+                                      b.T(r) + OB[jb[k]], OB[jb[k] + 1] - OB[jb[k]], to, rk);
+                } else {
+                    const u64* from = ia[k] != kNone ? a.T(r) + OA[ia[k]] : b.T(r) + OB[jb[k]];
+                    for (uint32_t q = 0; q < cnt[k]; ++q) to[q] = from[q];
+                }
+            }
+            pos += (1ull << 32) | cnt[k];
+        }
+        if (t == f.ntiles - 1 && threadIdx.x == 0) {
+            // the last tile: the totals, and this replica's answer (0 = Value0 =:= Value,
+            // 1 = merged: the inflation holds, 3 | bad << 2 = retry on the merge path)
+            const u64 all = s_base + tot;
+            const uint32_t nout = (uint32_t)(all >> 32);
+            const uint32_t ntok = MODE == 2 ? 0u : (uint32_t)all;
+            const bool pairs2 = MODE == 2 && (uint32_t)all != 0;
+            out.hdr[2 * r] = nout;
+            out.hdr[2 * r + 1] = ntok;
+            if (MODE != 2) out.O(r)[nout] = ntok;
+            f.hneed[2 * r] = nout;
+            f.hneed[2 * r + 1] = ntok;
+            hst[r] = pairs2 ? (uint8_t)(3u | (16u << 2)) : (f.w[r] ? 1 : 0);
+        }
+        __syncthreads();
     }
 }
 
@@ -1625,6 +2095,8 @@ int list_alloc(laspj_ctx* ctx, laspj_batch* b, uint32_t ce, uint32_t ct, bool ze
     b->cap_t = ct;
     b->known_e = zero ? 0 : ce;
     b->known_t = zero ? 0 : ct;
+    b->not_asc = false;
+    b->no_spec = false;
     b->words_per_replica = wpr;
     b->elements = ce;
     b->cells = ce;
@@ -1868,6 +2340,8 @@ int laspj_list_upload(laspj_ctx* ctx, laspj_batch* b, uint64_t replica, uint32_t
         if (int s = list_alloc(ctx, b, n > b->cap_e ? n : b->cap_e, nt > b->cap_t ? nt : b->cap_t))
             return s;
     }
+    b->not_asc = false;                    // (hints: list_bind tries the ascending path,
+    b->no_spec = false;                    //  merges the chunked walk)
     if (b->replicas == 1) {
         b->known_e = n;
         b->known_t = nt;
@@ -1980,10 +2454,16 @@ static int pair_checks(laspj_ctx* ctx, const laspj_batch* dst, const laspj_batch
 // zeroed here in one memset — [rk.flag (the caller points rk.flag at words[0]) |
 // unsorted R | tickets 2 | aweak R] — for a caller that reads them after other users of
 // the scratch (list_bind's inflation reads `aweak`: words + R + 3)
+static int grow_block(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t bytes, bool zero,
+                      const char* what);
+
+// spec: replicas whose keys descend take the chunked walk (k_merge_spec) — asked for when
+// an input is known not to ascend (laspj_batch::not_asc), as it costs a launch otherwise
 static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
                          const laspj_batch* b, const RK& rk, bool keep_left, uint32_t* need,
                          uint8_t* eq, const char* what, uint32_t* words = nullptr,
-                         uint64_t words_bytes = 0, const Ins* ins = nullptr) {
+                         uint64_t words_bytes = 0, const Ins* ins = nullptr,
+                         bool spec = false) {
     // (words_bytes == 0 with words: they are known zero already, no memset)
     const bool gs = a->kind == LASPJ_KIND_GSET_LIST;
     const uint64_t R = a->replicas;
@@ -2009,7 +2489,18 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     const uint64_t sz_sa = R * 8ull * m.ce_a, sz_sb = R * 8ull * m.ce_b, sz_pl = R * 8ull * ce,
                    sz_tc = R * 4ull * ce, sz_t = R * 4ull * m.ntiles, sz_c = R * 4ull * m.nchunks,
                    sz_r = R * 4ull;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72;
+    // the chunked walk: L rows per chunk, C chunks (a multiple of kSpW, at most 1024)
+    const bool fuse0 = R <= 4 && ctx->tune_list_walk != 1;
+    uint32_t spL = 256, spC = 0;
+    if (((spec && !a->no_spec && !b->no_spec) || ctx->tune_list_walk == 3) && fuse0 &&
+        a->known_e) {
+        spL = (uint32_t)std::max<uint64_t>(ctx->tune_list_chunk ? ctx->tune_list_chunk : 1024,
+                                           (a->known_e + 1023) / 1024);
+        spC = (uint32_t)((((uint64_t)a->known_e + spL - 1) / spL + kSpW - 1) / kSpW * kSpW);
+        if (spL >= (1u << 20)) spC = 0;
+    }
+    const uint64_t sz_fr = spC ? R * 4ull * m.ce_a : 0;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72 + sz_fr + 8;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -2028,6 +2519,20 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
+    SP sp{};
+    if (spC) {
+        sp.fr = reinterpret_cast<uint32_t*>(take(sz_fr));
+        sp.L = spL;
+        sp.C = spC;
+        const uint64_t zb = R * 8ull * (kSpWords + 2ull * spC);
+        if (int s = grow_block(ctx, &ctx->lspec, &ctx->lspec_bytes, std::max<uint64_t>(zb, 1 << 16),
+                               ctx->lspec_dirty, what))
+            return s;
+        sp.w = static_cast<u64*>(ctx->lspec);
+        sp.flag = rk.flag;
+        sp.cw = sp.w + R * kSpWords;
+        m.spec = 1;
+    }
     // [unsorted R | tickets 2 | aweak R], zeroed together
     m.unsorted = words ? words + 1 : reinterpret_cast<uint32_t*>(take(2 * sz_r + 8));
     uint32_t* tickets = m.unsorted + R;
@@ -2056,6 +2561,11 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         if (!words) hipMemsetAsync(m.unsorted, 0, 2 * sz_r + 8, ctx->stream);
         hipLaunchKernelGGL(k_merge_ranks, dim3(gr, ry), dim3(kMT), 0, ctx->stream, A, B,
                            rk, m, R);
+        if (spC) {
+            // (its last block per replica zeroes the words again)
+            hipLaunchKernelGGL(k_merge_spec<MODE>, dim3(spC / kSpW, ry), dim3(64 * kSpW), 0,
+                               ctx->stream, A, B, m, sp, R);
+        }
         hipLaunchKernelGGL((k_merge_tiles<MODE, false>), dim3(m.ntiles ? m.ntiles : 1, ry),
                            dim3(kMT), 0, ctx->stream, A, B, m, R,
                            fuse ? tickets : (uint32_t*)nullptr);
@@ -2098,6 +2608,8 @@ static void set_known(laspj_batch* dst, const uint32_t* h, uint64_t R) {
     }
     dst->known_e = ce;
     dst->known_t = ct;
+    dst->not_asc = false;
+    dst->no_spec = false;
 }
 
 static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
@@ -2114,7 +2626,8 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         return fail(ctx, LASPJ_E_NOMEM, "%s: sizes", what);
     }
     auto* need = static_cast<uint32_t*>(dev);
-    int s = merge_enqueue(ctx, dst, a, b, rk, keep_left, need, nullptr, what);
+    int s = merge_enqueue(ctx, dst, a, b, rk, keep_left, need, nullptr, what, nullptr, 0, nullptr,
+                          a->not_asc || b->not_asc);
     std::vector<uint32_t> h(2 * R);
     if (s == LASPJ_OK) {
         uint32_t f = 0;
@@ -2123,6 +2636,7 @@ static int merge_impl(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "%s: readback: %s", what,
                                    hipGetErrorString(e))
                             : flag_status(ctx, f, what);
+        if (f & kInfoWalkFell) a->no_spec = b->no_spec = true;
     }
     laspj::dev_release(ctx, dev, 8 * R);
     if (s != LASPJ_OK) {
@@ -2295,6 +2809,133 @@ int laspj_list_inflation(laspj_ctx* ctx, const laspj_batch* prev, const laspj_ba
     return read_flag(ctx, "list_inflation");
 }
 
+// list_bind's answer block: pinned, coherent host memory the last block writes into
+static int bind_answer(laspj_ctx* ctx, uint64_t hbytes) {
+    if (ctx->lbind_h_bytes < hbytes) {
+        if (ctx->lbind_h) {
+            hipStreamSynchronize(ctx->stream);
+            hipHostFree(ctx->lbind_h);
+            ctx->lbind_h = nullptr;
+            ctx->lbind_h_bytes = 0;
+        }
+        if (hipHostMalloc(&ctx->lbind_h, hbytes, hipHostMallocCoherent) != hipSuccess) {
+            hipGetLastError();
+            ctx->lbind_h = nullptr;
+            return fail(ctx, LASPJ_E_NOMEM, "list_bind: pinned answer");
+        }
+        ctx->lbind_h_bytes = hbytes;
+        LJ_HIP(ctx, hipHostGetDevicePointer(&ctx->lbind_hd, ctx->lbind_h, 0));
+    }
+    return LASPJ_OK;
+}
+
+// a device block of at least `bytes` in *p (grown), zeroed when new or `zero`
+static int grow_block(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t bytes, bool zero,
+                      const char* what) {
+    if (*have < bytes) {
+        if (*p) {
+            hipStreamSynchronize(ctx->stream);
+            hipFree(*p);
+            *p = nullptr;
+            *have = 0;
+        }
+        if (laspj::dev_malloc(ctx, p, bytes) != hipSuccess) {
+            hipGetLastError();
+            *p = nullptr;
+            return fail(ctx, LASPJ_E_NOMEM, "%s: device block", what);
+        }
+        *have = bytes;
+        zero = true;
+    }
+    if (zero) LJ_HIP(ctx, hipMemsetAsync(*p, 0, *have, ctx->stream));
+    return LASPJ_OK;
+}
+
+constexpr int kLfRetry = 1;     // list_bind_ascending: take the merge path instead
+
+// list_bind over the rank universe when both lists' keys strictly ascend (k_lbf_*):
+// LASPJ_OK with status / dst set, kLfRetry when a replica does not ascend (the lists are
+// marked not_asc, so the next bind of them goes straight to the merge path), or an error
+static int list_bind_ascending(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
+                               const laspj_batch* val, const RK& rk, uint8_t* status) {
+    const bool gs = cur->kind == LASPJ_KIND_GSET_LIST;
+    const uint64_t R = cur->replicas, nk = rk.nk;
+    const uint64_t be = (uint64_t)cur->known_e + val->known_e;
+    const uint64_t bt = gs ? 1ull : (uint64_t)cur->known_t + val->known_t;
+    if (be > dst->cap_e || bt > dst->cap_t)
+        if (int s = list_alloc(ctx, dst, be > dst->cap_e ? (uint32_t)be : dst->cap_e,
+                               bt > dst->cap_t ? (uint32_t)bt : dst->cap_t, gs))
+            return s;
+    const uint32_t ntiles = (uint32_t)std::max<uint64_t>(1, (nk + kLfTile - 1) / kLfTile);
+    // this call's half of the zeroed block: [diff R | bad R] words, then the look-back words
+    const uint64_t wbytes = (8 * R + 7) & ~7ull;
+    const uint64_t use = wbytes + 8ull * R * ntiles;
+    if (ctx->lfz_bytes < 2 * use || ctx->lfz_dirty) {
+        const uint64_t want = std::max<uint64_t>({2 * use, ctx->lfz_bytes, 1 << 16});
+        if (int s = grow_block(ctx, &ctx->lfz, &ctx->lfz_bytes, want, true, "list_bind"))
+            return s;
+        ctx->lf_prev_use = 0;                               // all zero now
+    }
+    const uint64_t ibytes = 16ull * R * std::max<uint64_t>(nk, 1);
+    const bool grew = ctx->lfi_bytes < ibytes;
+    if (++ctx->lf_epoch == 0 || grew) ctx->lf_epoch = 1;   // (a new block is all zero: epoch 0)
+    if (int s = grow_block(ctx, &ctx->lfi, &ctx->lfi_bytes, ibytes, ctx->lf_epoch == 1 && !grew,
+                           "list_bind"))
+        return s;
+    const uint64_t hbytes = 8 * R + 4 * ((R + 3) / 4) + 4;
+    if (int s = bind_answer(ctx, hbytes)) return s;
+    const uint64_t half = (ctx->lfz_bytes / 2) & ~7ull;
+    const uint32_t par = ctx->lf_parity ^ 1u;
+    char* mine = static_cast<char*>(ctx->lfz) + par * half;
+    char* prev = static_cast<char*>(ctx->lfz) + (par ^ 1u) * half;
+    LF f;
+    f.ia = static_cast<u64*>(ctx->lfi);
+    f.ib = f.ia + R * nk;
+    f.w = reinterpret_cast<uint32_t*>(mine);
+    f.st = reinterpret_cast<u64*>(mine + wbytes);
+    f.wz = reinterpret_cast<uint32_t*>(prev);
+    f.nwz = ctx->lf_prev_use / 4;
+    f.hneed = static_cast<uint32_t*>(ctx->lbind_hd);
+    f.epoch = ctx->lf_epoch;
+    f.nk = (uint32_t)nk;
+    f.ntiles = ntiles;
+    f.R = (uint32_t)R;
+    const LV A = view(cur), B = view(val), OUT = view(dst);
+    const uint64_t span = std::max<uint64_t>(
+        {cur->known_e, val->known_e, gs ? 0 : cur->known_t, gs ? 0 : val->known_t, 1});
+    const unsigned ry = (unsigned)(R < 65535 ? R : 65535);
+    ctx->lfz_dirty = true;
+    const dim3 gp((unsigned)((span + 255) / 256), ry), gw(ntiles, ry);
+    if (gs) {
+        hipLaunchKernelGGL(k_lbf_prep<true>, gp, dim3(256), 0, ctx->stream, A, B, rk, f, R);
+        hipLaunchKernelGGL(k_lbf_write<2>, gw, dim3(kLfT), 0, ctx->stream, A, B, OUT, rk, f);
+    } else {
+        hipLaunchKernelGGL(k_lbf_prep<false>, gp, dim3(256), 0, ctx->stream, A, B, rk, f, R);
+        hipLaunchKernelGGL(k_lbf_write<0>, gw, dim3(kLfT), 0, ctx->stream, A, B, OUT, rk, f);
+    }
+    if (hipGetLastError() != hipSuccess) return fail(ctx, LASPJ_E_DEVICE, "list_bind: launch");
+    ctx->lf_parity = par;
+    ctx->lf_prev_use = use;
+    const hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess)
+        return fail(ctx, LASPJ_E_DEVICE, "list_bind: synchronise: %s", hipGetErrorString(e));
+    ctx->lfz_dirty = false;                 // the next call zeroes what this one used
+    const auto* hb = static_cast<const uint8_t*>(ctx->lbind_h);
+    bool retry = false;
+    for (uint64_t r = 0; r < R; ++r) {
+        const uint8_t st = hb[8 * R + r];
+        if ((st & 3u) == 3u) {
+            retry = true;
+            if (st & 4u) cur->not_asc = true;
+            if (st & 8u) val->not_asc = true;
+        }
+    }
+    if (retry) return kLfRetry;
+    set_known(dst, reinterpret_cast<const uint32_t*>(hb), R);
+    std::memcpy(status, hb + 8 * R, R);
+    return LASPJ_OK;
+}
+
 int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
                     const laspj_batch* val, const laspj_list_order* ord, uint8_t* status) {
     if (int s = check_list(ctx, dst, "list_bind")) return s;
@@ -2306,6 +2947,16 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     if (int s = ranks(ctx, ord, cur->kind != LASPJ_KIND_GSET_LIST, &rk, "list_bind")) return s;
     const uint64_t R = cur->replicas;
     LGuard g(ctx);
+    // both lists ascending (tried unless a list is known not to, and while the rank universe
+    // is not much larger than the lists): the rank-indexed bind, two launches
+    if (!cur->not_asc && !val->not_asc && ctx->tune_list_walk != 2 && R <= 1024 &&
+        R * (uint64_t)rk.nk <= (1ull << 22) &&
+        rk.nk <= 16ull * ((uint64_t)cur->known_e + val->known_e) + 65536 &&
+        (uint64_t)cur->known_e + val->known_e < (1ull << 30) &&
+        (uint64_t)cur->known_t + val->known_t <= 0xFFFFFFF0ull) {
+        const int s = list_bind_ascending(ctx, dst, cur, val, rk, status);
+        if (s != kLfRetry) return s;
+    }
     // the context's bind block (device): [words 4R + 4 (BindFin): the error word the
     // kernels raise into, the merge's per-replica flags and tickets, the inflation's flags,
     // the equality's words, the final ticket | ... | need 8R at the block's end], the words
@@ -2330,21 +2981,7 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
         ctx->lbind_bytes = bytes;
         fresh = true;
     }
-    if (ctx->lbind_h_bytes < hbytes) {
-        if (ctx->lbind_h) {
-            hipStreamSynchronize(ctx->stream);
-            hipHostFree(ctx->lbind_h);
-            ctx->lbind_h = nullptr;
-            ctx->lbind_h_bytes = 0;
-        }
-        if (hipHostMalloc(&ctx->lbind_h, hbytes, hipHostMallocCoherent) != hipSuccess) {
-            hipGetLastError();
-            ctx->lbind_h = nullptr;
-            return fail(ctx, LASPJ_E_NOMEM, "list_bind: pinned answer");
-        }
-        ctx->lbind_h_bytes = hbytes;
-        LJ_HIP(ctx, hipHostGetDevicePointer(&ctx->lbind_hd, ctx->lbind_h, 0));
-    }
+    if (int st = bind_answer(ctx, hbytes)) return st;
     void* hdev = ctx->lbind_hd;
     auto* mw = static_cast<uint32_t*>(ctx->lbind);
     auto* need = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->lbind) +
@@ -2372,7 +3009,7 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
     uint32_t tsz = tsz0;
     const Ins ins{tk, ti, tsz0, mw + R + 3};
     int s = merge_enqueue(ctx, dst, cur, val, rk, false, need, nullptr, "list_bind", mw, wzero,
-                          &ins);
+                          &ins, cur->not_asc || val->not_asc);
     // (Value0's replicas whose keys strictly ascend skip the check: see k_linf_insert)
     if (s == LASPJ_OK)
         s = inflation_launch(ctx, cur, dst, 0, rk, nullptr, false, "list_bind", &dd, false, &fw,
@@ -2401,6 +3038,7 @@ int laspj_list_bind(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* cur,
         s = e != hipSuccess ? fail(ctx, LASPJ_E_DEVICE, "list_bind: synchronise: %s",
                                    hipGetErrorString(e))
                             : flag_status(ctx, f, "list_bind");
+        if (f & kInfoWalkFell) cur->no_spec = val->no_spec = true;
     }
     if (s != LASPJ_OK) {
         dst->known_e = dst->cap_e, dst->known_t = dst->cap_t;

@@ -292,6 +292,9 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->ltab) hipFree(ctx->ltab);
         if (ctx->lbind) hipFree(ctx->lbind);
         if (ctx->lbind_h) hipHostFree(ctx->lbind_h);
+        if (ctx->lfz) hipFree(ctx->lfz);
+        if (ctx->lfi) hipFree(ctx->lfi);
+        if (ctx->lspec) hipFree(ctx->lspec);
         laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
         if (ctx->dstage) hipHostFree(ctx->dstage);
@@ -360,12 +363,17 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_etf_seg = value;
             return LASPJ_OK;
         case LASPJ_TUNE_LIST_WALK:
-            if (value < 0 || value > 1) return fail(ctx, LASPJ_E_INVAL, "tuning: list walk 0 or 1");
+            if (value < 0 || value > 3) return fail(ctx, LASPJ_E_INVAL, "tuning: list walk 0 .. 3");
             ctx->tune_list_walk = value;
             return LASPJ_OK;
         case LASPJ_TUNE_NIF_PASSES:
             if (value < 0 || value > 16) return fail(ctx, LASPJ_E_INVAL, "tuning: NIF passes 0..16");
             ctx->tune_nif_passes = value;
+            return LASPJ_OK;
+        case LASPJ_TUNE_LIST_CHUNK:
+            if (value != 0 && (value < 64 || value >= (1 << 20)))
+                return fail(ctx, LASPJ_E_INVAL, "tuning: list chunk 0 or 64 .. 2^20");
+            ctx->tune_list_chunk = value;
             return LASPJ_OK;
 
         default:

@@ -47,9 +47,10 @@ def key_term(slot):
     return float(v) if slot & 1 else v
 
 
-def gen(rng, n, runs=False, unsorted_tokens=False):
-    """A list with non-decreasing keys: (term list, keys, toff, toks)."""
-    vals = np.sort(rng.integers(0, V, n))
+def gen(rng, n, runs=False, unsorted_tokens=False, strict=False):
+    """A list with non-decreasing keys (strict: ascending ranks, n <= V): (term list,
+    keys, toff, toks)."""
+    vals = np.sort(rng.choice(V, n, replace=False) if strict else rng.integers(0, V, n))
     if runs and n:
         a = rng.integers(0, max(1, n - 1))
         vals[a:a + n // 2] = vals[a]             # one long run of a single key
@@ -150,3 +151,132 @@ def test_sorted_and_unsorted_replicas_in_one_batch(env):
                                    for t in toks[int(toff[i]):int(toff[i + 1])]])
                for i, k in enumerate(keys)]
         assert exact_eq(got, want[r]), r
+
+
+def _bind_want(mod, kind, p, v):
+    """lasp_core:bind/3 (lasp_core.erl:291-312): 0 no-op, 1 written, 2 not an inflation."""
+    from oracle import lattice as olat
+    if exact_eq(p, v):
+        return 0, None
+    m = mod.merge(p, v)
+    return (1 if olat.is_inflation(kind, p, m) else 2), m
+
+
+def _both_paths(ctx, A, B, order):
+    """laspj_list_bind on the rank-indexed path (tried first) and on the merge path
+    (LASPJ_TUNE_LIST_WALK 2): (status, downloaded merged list) of each."""
+    from lasp_amd import _lib
+    out = []
+    try:
+        for tune in (0, 2):
+            ctx.set_tuning(_lib.TUNE_LIST_WALK, tune)
+            M, st = A.bind(B, order)
+            out.append((int(st[0]), M.download() if st[0] else None))
+    finally:
+        ctx.set_tuning(_lib.TUNE_LIST_WALK, 0)
+    return out
+
+
+BIND_SIZES = [(0, 0), (0, 700), (5, 0), (1, 1), (300, 40), (2500, 2600), (2990, 2980), (7, 2990)]
+
+
+@pytest.mark.parametrize("na,nb", BIND_SIZES)
+@pytest.mark.parametrize("gs", [False, True])
+def test_list_bind_ascending_path(env, na, nb, gs):
+    """laspj_list_bind when both lists' keys strictly ascend (k_lbf_prep / k_lbf_write:
+    the rank-indexed bind, no merge path): status and merged list as the oracle's
+    bind/3, and bit-identical to the merge path's.  The int and the float of one value are
+    different slots of equal rank here: orddict:merge keeps the first list's key, and a
+    G-Set pair of different slots goes to the merge path (ordsets:union's argument switch
+    picks its item)."""
+    from lasp_amd import _lib, engine
+    ctx, order, _keep = env
+    rng = np.random.default_rng(4000 + na * 7 + nb + gs)
+    ta, *ia = gen(rng, na, strict=True, unsorted_tokens=True)
+    tb, *ib = gen(rng, nb, strict=True, unsorted_tokens=True)
+    kind, mod = ("lasp_gset", ogset) if gs else ("lasp_orset", oorset)
+    lk = _lib.KIND_GSET_LIST if gs else _lib.KIND_ORSET_LIST
+    if gs:
+        # G-Set statuses are compared with the oracle over int keys only: the list
+        # inflation check compares ranks (laspj.h: equal rank = the same term), which the
+        # Store's dictionaries guarantee (codec.EqualTerms); sets:is_subset is =:=
+        ints = lambda k: (2 * (k[0] // 2)).astype(np.uint64)             # noqa: E731
+        ia, ib = [ints(ia)], [ints(ib)]
+        ta = [key_term(int(x)) for x in ia[0]]
+        tb = [key_term(int(x)) for x in ib[0]]
+    for (p, P), (v, Q) in (((ta, ia), (tb, ib)), ((ta, ia), (ta, ia)), ((tb, ib), (ta, ia))):
+        A = engine.ListBatch(ctx, lk).upload(*P)
+        B = engine.ListBatch(ctx, lk).upload(*Q)
+        (s0, m0), (s2, m2) = _both_paths(ctx, A, B, order)
+        w, m = _bind_want(mod, kind, p, v)
+        assert s0 == s2 == w, (na, nb, s0, s2, w)
+        if w:
+            assert all(np.array_equal(x, y) for x, y in zip(m0, m2) if x is not None)
+            got = decode(engine.ListBatch(ctx, lk).upload(*m0), gs)
+            assert exact_eq(got, m)
+    if gs and na and nb:
+        # a pair of equal rank from two slots (int v, float v): the merge path's item
+        ka = ia[0].copy()
+        kb = np.unique(np.concatenate([ib[0], ka[:1] + np.uint64(1)]))
+        A = engine.ListBatch(ctx, lk).upload(ka)
+        B = engine.ListBatch(ctx, lk).upload(kb)
+        (s0, m0), (s2, m2) = _both_paths(ctx, A, B, order)
+        assert s0 == s2
+        assert all(np.array_equal(x, y) for x, y in zip(m0, m2))
+
+
+def test_list_bind_ascending_large_and_fallbacks():
+    """At the bench's scale (60k-80k-entry lists over 200k ranks, 1-3 tokens per entry
+    in any order): the rank-indexed bind equals the merge path bit for bit; a Value whose
+    keys descend somewhere, one with a repeated key, and a 3-replica batch with one such
+    replica fall back to the merge path (same answer as the merge path's)."""
+    from lasp_amd import _lib, engine
+    from lasp_amd.orset import context
+    ctx = context()
+    K = 200_000
+    kr = ctx.buffer(4 * K)
+    kr.upload(np.arange(K, dtype=np.uint32))
+    gr = ctx.buffer(4 * 64 * K)
+    gr.upload(np.tile(np.arange(64, dtype=np.uint32), K))
+    order = _lib.ListOrder()
+    order.krank, order.nkeys, order.grank, order.ntokens = kr.h.value, K, gr.h.value, 64 * K
+    rng = np.random.default_rng(9)
+
+    def lst(n, desc=False, dup=False):
+        keys = np.sort(rng.choice(K, n, replace=False)).astype(np.uint64)
+        if desc:
+            keys[n // 2], keys[n // 2 + 1] = keys[n // 2 + 1], keys[n // 2]
+        if dup:
+            keys[n // 3 + 1] = keys[n // 3]
+        cnt = rng.integers(1, 4, n)
+        toff = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
+        toks = np.concatenate([(64 * int(k) + rng.choice(6, c, replace=False)).astype(np.uint64)
+                               for k, c in zip(keys, cnt)])
+        toks |= (rng.random(len(toks)) < 0.2).astype(np.uint64) << np.uint64(63)
+        return keys, toff, toks
+
+    a, b = lst(60_000), lst(80_000)
+    for p, q in ((a, b), (a, a), (b, a), (a, lst(70_000, desc=True)), (a, lst(50_000, dup=True))):
+        A = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*p)
+        B = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*q)
+        (s0, m0), (s2, m2) = _both_paths(ctx, A, B, order)
+        assert s0 == s2
+        if s0:
+            assert all(np.array_equal(x, y) for x, y in zip(m0, m2))
+    # three replicas, the middle one descending
+    A = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, 3, 80_000, 240_000)
+    B = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST, 3, 80_000, 240_000)
+    for r, (p, q) in enumerate(((a, b), (lst(1000), lst(900, desc=True)), (b, a))):
+        A.upload(*p, replica=r)
+        B.upload(*q, replica=r)
+    outs = []
+    try:
+        for tune in (0, 2):
+            ctx.set_tuning(_lib.TUNE_LIST_WALK, tune)
+            M, st = A.bind(B, order)
+            outs.append((list(st), [M.download(r) for r in range(3)]))
+    finally:
+        ctx.set_tuning(_lib.TUNE_LIST_WALK, 0)
+    assert outs[0][0] == outs[1][0] == [1, 1, 1]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        assert all(np.array_equal(u, w) for u, w in zip(x, y))

@@ -1,4 +1,5 @@
-"""The run-jumping list merge (merge_runs_replica in k_merge_tile_scan, laspj_lists.hip) on lists whose keys do NOT
+"""The list merges for keys that do NOT ascend — the run-jumping walk (merge_runs_replica in
+k_merge_tile_scan, laspj_lists.hip) and the chunked walk over the chip (k_merge_spec) — on lists whose keys do NOT
 ascend — a non-monotone map's output re-bound (lasp_core.erl:641-667 then :300, merged by
 lasp_orset.erl:128-134 / lasp_gset.erl:99-101 over OTP 17's two-finger clauses, SURVEY
 Appendix A) — against the oracle's clauses (oracle/otp.py via oracle/orset.py,
@@ -83,13 +84,19 @@ def shapes_fix(out):
 
 
 def _walks(ctx, fn):
+    """fn() with the default walk, the step walk (LASPJ_TUNE_LIST_WALK 1) and the chunked
+    walk over the chip (3, k_merge_spec: chunks of 256 rows, so these shapes span up to
+    32 chunks); the chunked result must equal the default one."""
     from lasp_amd import _lib
     got = fn()
-    ctx.set_tuning(_lib.TUNE_LIST_WALK, 1)
     try:
+        ctx.set_tuning(_lib.TUNE_LIST_WALK, 3)
+        chunked = fn()
+        ctx.set_tuning(_lib.TUNE_LIST_WALK, 1)
         step = fn()
     finally:
         ctx.set_tuning(_lib.TUNE_LIST_WALK, 0)
+    assert exact_eq(chunked, got)
     return got, step
 
 
@@ -158,3 +165,38 @@ def test_unsorted_replicas_batched(env):
                                    for t in toks[int(toff[i]):int(toff[i + 1])]])
                for i, k in enumerate(keys)]
         assert exact_eq(got, want[r]), sh[r][0]
+
+
+def test_chunked_walk_bind_at_scale(env):
+    """laspj_list_bind of independently shuffled 20k-entry lists (the bench's
+    shuffled-each case at 2/5 size): the first bind finds the keys not ascending (the
+    rank-indexed path answers 3), marks the lists, and the merge path's chunked walk
+    runs; then each bind again.  Statuses and merged lists equal the step walk's, and the
+    merged list of one pair equals the oracle's merge."""
+    from lasp_amd import _lib, engine
+    ctx, order, _keep = env
+    rng = np.random.default_rng(77)
+    V = 3000
+    for name, va, vb in (("shuffled each", list(rng.integers(0, V, 20000)), list(rng.integers(0, V, 19000))),
+                         ("reversed", list(range(2999, 0, -1)) * 3, list(range(2999, 0, -1)) * 3),
+                         ("random vs sorted", list(rng.integers(0, V, 9000)), sorted(rng.integers(0, V, 9000)))):
+        ta, *ia = _list(rng, [int(x) for x in va])
+        tb, *ib = _list(rng, [int(x) for x in vb])
+        A = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*ia)
+        B = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*ib)
+        outs = []
+        for _ in range(2):                                  # first: the fallback; then hinted
+            M, st = A.bind(B, order)
+            outs.append((int(st[0]), M.download()))
+        try:
+            ctx.set_tuning(_lib.TUNE_LIST_WALK, 1)
+            M, st = A.bind(B, order)
+            step = (int(st[0]), M.download())
+        finally:
+            ctx.set_tuning(_lib.TUNE_LIST_WALK, 0)
+        for o in outs:
+            assert o[0] == step[0], name
+            assert all(np.array_equal(x, y) for x, y in zip(o[1], step[1])), name
+        if name == "random vs sorted":
+            assert exact_eq(decode(engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*outs[1][1]), False),
+                            oorset.merge(ta, tb))
