@@ -282,6 +282,12 @@ int laspj_batch_join(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
 int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
                           const laspj_batch* const* cur, const laspj_batch* const* val,
                           laspj_buf* status);
+/* bind_many with the statuses in host memory (n bytes): returns after the work has
+ * completed, with one synchronisation (the kernel writes them into the context's pinned
+ * memory) — what a bind/3 caller needs before it can answer */
+int laspj_batch_bind_many_host(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
+                               const laspj_batch* const* cur, const laspj_batch* const* val,
+                               uint8_t* status);
 int laspj_batch_inflation_many(laspj_ctx* ctx, uint32_t n, const laspj_batch* const* prev,
                                const laspj_batch* const* cur, int strict, laspj_buf* out);
 
@@ -751,6 +757,14 @@ int laspj_list_union(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
  * (first match) -> {X, Cx ++ Cy}; G-Set lists: lists:member -> X */
 int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
                             const laspj_batch* r, const laspj_list_order* ord);
+/* the intersection body with a canonical right side (lasp_core.erl:546-589): r is an
+ * OR-Set (G-Set) batch of l's replicas; keyfind / member of X in r's list form is r's cell
+ * of X's slot, whose tokens follow Cx in term order (tok_order: laspj_list_from_set's
+ * 64-byte rows) — what laspj_list_from_set(r) then laspj_list_intersection gives, without
+ * the conversion or its hash.  Distinct slots must be distinct terms (== apart), as the
+ * host dictionaries guarantee. */
+int laspj_list_intersection_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                const laspj_batch* r, const laspj_buf* tok_order);
 /* product body (lasp_core.erl:499-533): l-major pairs {X, Y}; OR-Set tokens
  * orset_causal_product(Cx, Cy) (both runs reversed, [Tx, Ty], Dx orelse Dy) */
 int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,

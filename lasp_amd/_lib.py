@@ -118,6 +118,7 @@ SIGNATURES = {
     "laspj_batch_reduce_chunks": (i, [vp, vp, vp, u32]),
     "laspj_batch_join_n": (i, [vp, vp, vp, u32]),
     "laspj_batch_bind_many": (i, [vp, u32, vp, vp, vp, vp]),
+    "laspj_batch_bind_many_host": (i, [vp, u32, vp, vp, vp, vp]),
     "laspj_batch_inflation_many": (i, [vp, u32, vp, vp, i, vp]),
     "laspj_batch_info_get": (i, [vp, C.POINTER(BatchInfo)]),
     "laspj_batch_device_ptr": (i, [vp, vpp]),
@@ -199,6 +200,7 @@ SIGNATURES = {
     "laspj_list_value": (i, [vp, vp, vp]),
     "laspj_list_union": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
     "laspj_list_intersection": (i, [vp, vp, vp, vp, C.POINTER(ListOrder)]),
+    "laspj_list_intersection_set": (i, [vp, vp, vp, vp, vp]),
     "laspj_list_product": (i, [vp, vp, vp, vp]),
     "laspj_list_map": (i, [vp, vp, vp, vp, u32, i]),
     "laspj_list_filter": (i, [vp, vp, vp, vp, u32, i]),

@@ -674,6 +674,14 @@ class Store:
                 res = self._new_batch(t).intersection(a.batch, b.batch)
                 return self._bind_out(out, _Value("canonical", res))
             _pairs_guard(a, b)
+            if b.rep == "canonical" and _width(b.batch) == 1:
+                # keyfind in R's list form = R's cell of the key's slot: R is read in place
+                # (laspj_list_intersection_set), not converted
+                la = self._value_list(t, a)
+                _eb, _n, tb = self._space(t).set_orders(b.batch.elements)
+                self._order(t)                    # (rank tables current for the bind)
+                return self._bind_out(out, _Value("list", la.intersection_set(b.batch, tb),
+                                                  a.pairs))
             la, lb = self._lists(t, a, b)
             self._bind_out(out, _Value("list", la.intersection(lb, self._order(t)), a.pairs))
         return self._start([l, r], body)

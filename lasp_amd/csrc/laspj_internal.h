@@ -78,6 +78,10 @@ struct laspj_ctx {
     void* lspec = nullptr;
     uint64_t lspec_bytes = 0;
     bool lspec_dirty = false;
+    // laspj_batch_bind_many_host's statuses (pinned, coherent: the kernel writes them there)
+    void* many_h = nullptr;
+    void* many_hd = nullptr;
+    uint64_t many_h_bytes = 0;
     // pinned host staging for the small readbacks (sizes, statuses, flags): a round trip
     // into pageable memory costs ~26 us, into pinned ~13 us (tools/readback_probe.py)
     void* pinned = nullptr;

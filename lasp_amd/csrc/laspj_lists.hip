@@ -1874,6 +1874,62 @@ struct PIsect {
     }
 };
 
+// the intersection body with a canonical right side (an OR-Set / G-Set batch): keyfind /
+// member of X in R's list form (one entry per present slot, tokens in term order) is R's
+// cell of X's slot — no conversion of R into a list, no hash.  (The Store's dictionaries
+// give distinct slots distinct ranks, codec.EqualTerms, so the slot is the only match.)
+template <bool GSET>
+struct PIsectSet {
+    LV l;
+    const u64* src;
+    uint64_t wpr;
+    uint32_t E;
+    const uint8_t* tord;
+    __device__ bool cell(u64 r, u64 i, uint32_t& e, u64& p, u64& rm) const {
+        const u64 it = l.K(r)[i];
+        p = rm = 0;
+        e = (uint32_t)(it & kIdMask);
+        if ((it & kPair) || e >= E) return false;      // not an element of the set
+        const u64* s = src + r * wpr;
+        if (GSET) {
+            p = (s[e >> 6] >> (e & 63)) & 1ull;
+        } else {
+            p = s[2ull * e];
+            rm = s[2ull * e + 1];
+        }
+        return p != 0;
+    }
+    __device__ u64 items(u64 r) const { return l.n(r); }
+    __device__ C2 count(u64 r, u64 i) const {
+        uint32_t e;
+        u64 p, rm;
+        if (!cell(r, i, e, p, rm)) return C2{0, 0};
+        if (GSET) return pk2(1, 0);
+        const uint32_t* OL = l.O(r);
+        return pk2(1, (OL[i + 1] - OL[i]) + (uint32_t)__popcll(p));
+    }
+    __device__ void write(u64 r, u64 i, uint32_t pos, uint32_t tpos, LV out) const {
+        uint32_t e;
+        u64 p, rm;
+        cell(r, i, e, p, rm);
+        out.K(r)[pos] = l.K(r)[i];
+        if (GSET) return;
+        const uint32_t* OL = l.O(r);
+        out.O(r)[pos] = tpos;
+        u64* to = out.T(r) + tpos;
+        const u64* tl = l.T(r) + OL[i];
+        const uint32_t ll = OL[i + 1] - OL[i];
+        for (uint32_t k = 0; k < ll; ++k) to[k] = tl[k];            // Cx ++ Cy
+        uint32_t n = ll;
+        const uint8_t* ot = tord + 64ull * e;
+        for (int j = 0; j < 64; ++j) {
+            const uint32_t k = ot[j];
+            if (k >= 64) break;
+            if ((p >> k) & 1ull) to[n++] = (64ull * e + k) | (((rm >> k) & 1ull) << 63);
+        }
+    }
+};
+
 template <bool GSET>
 __global__ __launch_bounds__(256) void k_isect_hash(LV rr, RK rk, u64* hk, uint32_t* hi,
                                                     uint32_t hsize, uint64_t R) {
@@ -3093,6 +3149,34 @@ int laspj_list_intersection(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch*
     return tiled<PIsect<false>>(ctx, dst, l->cap_e, hbytes, pre(std::false_type{}),
                                 "list_intersection", std::max<uint32_t>(1, l->known_e),
                                 std::max<uint64_t>(1, (uint64_t)l->known_t + r->known_t));
+}
+
+int laspj_list_intersection_set(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,
+                                const laspj_batch* r, const laspj_buf* tok_order) {
+    if (int s = check_list(ctx, dst, "list_intersection_set")) return s;
+    if (int s = check_list(ctx, l, "list_intersection_set")) return s;
+    if (!r || r->ctx != ctx) return fail(ctx, LASPJ_E_INVAL, "list_intersection_set: r");
+    const bool gs = l->kind == LASPJ_KIND_GSET_LIST;
+    if (r->kind != (gs ? LASPJ_KIND_GSET : LASPJ_KIND_ORSET) || dst->kind != l->kind)
+        return fail(ctx, LASPJ_E_KIND,
+                    "list_intersection_set: OR-Set list x OR-Set, G-Set list x G-Set");
+    if (r->replicas != l->replicas || dst->replicas != l->replicas)
+        return fail(ctx, LASPJ_E_SHAPE, "list_intersection_set: replicas");
+    if (!gs && (!tok_order || tok_order->ctx != ctx || tok_order->bytes < 64ull * r->elements))
+        return fail(ctx, LASPJ_E_RANGE, "list_intersection_set: token order (64 bytes per slot)");
+    LGuard g(ctx);
+    const LV L = view(l);
+    const auto* sp = reinterpret_cast<const u64*>(r->dev);
+    const auto* tordp = gs ? nullptr : static_cast<const uint8_t*>(tok_order->dev);
+    if (gs)
+        return tiled<PIsectSet<true>>(ctx, dst, l->cap_e, 0, [&](char*) {
+            return PIsectSet<true>{L, sp, r->words_per_replica, r->elements, tordp};
+        }, "list_intersection_set", std::max<uint32_t>(1, l->known_e), 1);
+    // (tokens Cx ++ Cy: l's run and at most 64 of the cell's)
+    return tiled<PIsectSet<false>>(ctx, dst, l->cap_e, 0, [&](char*) {
+        return PIsectSet<false>{L, sp, r->words_per_replica, r->elements, tordp};
+    }, "list_intersection_set", std::max<uint32_t>(1, l->known_e),
+       std::max<uint64_t>(1, (uint64_t)l->known_t + 64ull * l->known_e));
 }
 
 int laspj_list_product(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* l,

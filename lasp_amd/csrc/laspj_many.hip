@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <cstring>
+
 #include "laspj_internal.h"
 
 namespace laspj {
@@ -264,18 +266,36 @@ void* mscratch(laspj_ctx* ctx, uint64_t bytes) {
 
 extern "C" {
 
-int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
+// bind_many into a device buffer (status) or, host, into host memory through the
+// context's mapped answer block (one synchronisation, no separate download)
+static int bind_many_impl(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
                           const laspj_batch* const* cur, const laspj_batch* const* val,
-                          laspj_buf* status) {
+                          laspj_buf* status, uint8_t* host) {
     if (!ctx || (n && (!dst || !cur || !val)))
         return fail(ctx, LASPJ_E_INVAL, "bind_many: null argument");
-    if (!status || status->ctx != ctx || status->bytes < n)
+    if (!host && (!status || status->ctx != ctx || status->bytes < n))
         return fail(ctx, LASPJ_E_RANGE, "bind_many: status buffer (n bytes)");
     if (!n) return LASPJ_OK;
     std::vector<MItem> items;
     uint64_t nseg = 0;
     if (int s = describe(ctx, n, dst, cur, val, &items, &nseg, "bind_many")) return s;
     MGuard g(ctx);
+    if (host && ctx->many_h_bytes < n) {
+        if (ctx->many_h) {
+            hipStreamSynchronize(ctx->stream);
+            hipHostFree(ctx->many_h);
+            ctx->many_h = nullptr;
+            ctx->many_h_bytes = 0;
+        }
+        const uint64_t want = std::max<uint64_t>(n, 4096);
+        if (hipHostMalloc(&ctx->many_h, want, hipHostMallocCoherent) != hipSuccess) {
+            hipGetLastError();
+            ctx->many_h = nullptr;
+            return fail(ctx, LASPJ_E_NOMEM, "bind_many: pinned statuses");
+        }
+        ctx->many_h_bytes = want;
+        LJ_HIP(ctx, hipHostGetDevicePointer(&ctx->many_hd, ctx->many_h, 0));
+    }
     const uint64_t db = sizeof(MItem) * n, sb = 4ull * n;
     char* base = static_cast<char*>(mscratch(ctx, db + sb));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "bind_many: scratch");
@@ -293,13 +313,31 @@ int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
     LJ_LAUNCHED(ctx);
     const unsigned fg = (unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
     hipLaunchKernelGGL(k_many_status, dim3(fg), dim3(256), 0, ctx->stream, st,
-                       static_cast<uint8_t*>(status->dev), n);
+                       static_cast<uint8_t*>(host ? ctx->many_hd : status->dev), n);
     LJ_LAUNCHED(ctx);
+    if (host) {
+        LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        std::memcpy(host, ctx->many_h, n);
+        return LASPJ_OK;
+    }
     bool exported = !staged || status->exported;
     for (uint32_t i = 0; i < n && !exported; ++i)
         exported = dst[i]->exported || cur[i]->exported || val[i]->exported;
     if (exported) LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return LASPJ_OK;
+}
+
+int laspj_batch_bind_many(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
+                          const laspj_batch* const* cur, const laspj_batch* const* val,
+                          laspj_buf* status) {
+    return bind_many_impl(ctx, n, dst, cur, val, status, nullptr);
+}
+
+int laspj_batch_bind_many_host(laspj_ctx* ctx, uint32_t n, laspj_batch* const* dst,
+                               const laspj_batch* const* cur, const laspj_batch* const* val,
+                               uint8_t* status) {
+    if (n && !status) return fail(ctx, LASPJ_E_INVAL, "bind_many_host: null status");
+    return bind_many_impl(ctx, n, dst, cur, val, nullptr, status);
 }
 
 int laspj_batch_inflation_many(laspj_ctx* ctx, uint32_t n, const laspj_batch* const* prev,

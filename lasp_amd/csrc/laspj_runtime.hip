@@ -295,6 +295,7 @@ int laspj_ctx_destroy(laspj_ctx* ctx) {
         if (ctx->lfz) hipFree(ctx->lfz);
         if (ctx->lfi) hipFree(ctx->lfi);
         if (ctx->lspec) hipFree(ctx->lspec);
+        if (ctx->many_h) hipHostFree(ctx->many_h);
         laspj::dev_cache_clear(ctx);
         if (ctx->pinned) hipHostFree(ctx->pinned);
         if (ctx->dstage) hipHostFree(ctx->dstage);

@@ -98,15 +98,16 @@ class Context:
 
     # -- many one-replica batches per launch
     def bind_many(self, dsts, curs, vals) -> np.ndarray:
-        """laspj_batch_bind_many: status per item (0 = no-op, 1 = merged into dst)."""
+        """laspj_batch_bind_many_host: status per item (0 = no-op, 1 = merged into
+        dst), read back in the call's one synchronisation."""
         n = len(curs)
         if n == 0:
             return np.zeros((0,), dtype=np.uint8)
         arr = lambda xs: (C.c_void_p * n)(*[x.h.value for x in xs])  # noqa: E731
-        st = self.buffer(n)
-        check(self.L.laspj_batch_bind_many(self.h, n, arr(dsts), arr(curs), arr(vals), st.h),
-              self.h)
-        return st.download(np.uint8)
+        st = np.zeros((n,), dtype=np.uint8)
+        check(self.L.laspj_batch_bind_many_host(self.h, n, arr(dsts), arr(curs), arr(vals),
+                                                st.ctypes.data), self.h)
+        return st
 
     # ------------------------------------------------------------ NIF entry points
     # laspj.h "NIF entry points": term_to_binary images in, images / booleans out, over
@@ -1001,6 +1002,15 @@ class ListBatch:
 
     def intersection(self, other: "ListBatch", order) -> "ListBatch":
         return self._binary(self.ctx.L.laspj_list_intersection, other, order)
+
+    def intersection_set(self, other, tok_order: Optional["Buffer"]) -> "ListBatch":
+        """laspj_list_intersection_set: the body with a canonical right side (an OR-Set /
+        G-Set batch; tok_order: laspj_list_from_set's token-order rows)."""
+        out = self._like()
+        check(self.ctx.L.laspj_list_intersection_set(
+            self.ctx.h, out.h, self.h, other.h, tok_order.h if tok_order is not None else None),
+            self.ctx.h)
+        return out
 
     def product(self, other: "ListBatch") -> "ListBatch":
         return self._binary(self.ctx.L.laspj_list_product, other, None)

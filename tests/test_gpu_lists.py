@@ -237,3 +237,34 @@ def test_list_from_set_and_edges():
     with pytest.raises(_lib.LaspjError) as ei:
         P.product(lb)
     assert ei.value.status == _lib.E_UNSUPPORTED
+
+
+@SETTINGS
+@given(OLIST, OLIST, st.booleans())
+def test_list_intersection_with_set_operand(a, b, gs):
+    """laspj_list_intersection_set — the intersection body with a canonical right side,
+    read in place (the Store's re-run after an update of R) — against the oracle body over
+    R's orddict / ordset, and equal to the list body over R's list form."""
+    from lasp_amd.terms import term_key
+    s = Space(gset=gs)
+    if gs:
+        a = [k for k, _ in a]
+        b = sorted({k for k, _ in b})
+        kind = "lasp_gset"
+    else:
+        b = [(k, sorted(dict(ts).items(), key=lambda t: term_key(t[0])))
+             for k, ts in sorted(dict(b).items()) if ts]
+        kind = "lasp_orset"
+    A = s.enc(a)
+    E = 64
+    if gs:
+        Rb = s.ctx.gset_batch(1, E)
+        Rb.upload(s.dom.encode_gset([b], E))
+    else:
+        Rb = s.ctx.orset_batch(1, E)
+        Rb.upload(s.dom.encode_orset([b], E))
+    _eb, _n, tb = s.space.set_orders(E)
+    got = A.intersection_set(Rb, tb)
+    want = ocore.intersection_body(kind, a, b)
+    assert exact_eq(s.dec(got), want), (a, b)
+    assert exact_eq(s.dec(A.intersection(s.enc(b), s.order)), want)

@@ -45,8 +45,22 @@ def test_bind_many_matches_single_kernels(ctx):
         vals.append(b)
         dsts.append(d)
         want.append(0 if b is a else 1)
-    st = ctx.bind_many(dsts, curs, vals)
+    st = ctx.bind_many(dsts, curs, vals)          # laspj_batch_bind_many_host
     assert list(st) == want
+    # the device-buffer form (laspj_batch_bind_many) answers the same into a buffer
+    import ctypes as C
+    from lasp_amd import _lib
+    n = len(curs)
+    arr = lambda xs: (C.c_void_p * n)(*[x.h.value for x in xs])  # noqa: E731
+    dsts2 = [{"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
+             for k, E in shapes]
+    buf = ctx.buffer(n)
+    _lib.check(ctx.L.laspj_batch_bind_many(ctx.h, n, arr(dsts2), arr(curs), arr(vals), buf.h),
+               ctx.h)
+    assert list(buf.download(np.uint8)) == want
+    for d, d2, s in zip(dsts, dsts2, st):
+        if s:
+            assert np.array_equal(d.download_words(), d2.download_words())
     for (k, E), a, b, d, s in zip(shapes, curs, vals, dsts, st):
         if s:
             ref = {"o": ctx.orset_batch, "g": ctx.gset_batch, "c": ctx.gcounter_batch}[k](1, E)
