@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--elements", type=int, default=4096)
     ap.add_argument("--wide-replicas", type=int, default=1 << 19,
                     help="replicas of the T = 128 join leg (0: skip it)")
+    ap.add_argument("--list-leg", type=int, default=1,
+                    help="1: time config 5's list re-bind and the Store update (rank 0, N=1)")
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -539,6 +541,59 @@ def wide_leg(ctx, args):
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
 
 
+def list_leg(ctx):
+    """lasp_core:bind/3 of config 5's 50k-entry intersection output into the previous one
+    (laspj_list_bind: keys ascending -> the rank-indexed bind; reversed -> the chunked
+    walk) and the Store end to end (update R -> intersection re-run -> re-bind), as
+    tools/list_bench.py measures them."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from list_bench import cells, identity_order, intersection_list
+    from lasp_amd import _lib, core, engine
+    from lasp_amd.terms import Atom
+    rng = np.random.default_rng(5)
+    N, D = 100_000, 150_000
+    order, _keep = identity_order(ctx, D)
+    common = np.arange(D - N, N)
+    pl, rl = cells(rng, len(common))
+    pr, rr = cells(rng, len(common))
+    old = intersection_list(common, pl, rl, pr, rr)
+    pr2, rr2 = pr.copy(), rr.copy()
+    pr2[rng.random(len(common)) < 0.10] |= np.uint64(8)
+    rm = rng.random(len(common)) < 0.05
+    rr2[rm] = pr2[rm]
+    new = intersection_list(common, pl, rl, pr2, rr2)
+
+    def rev(lst):
+        runs = [lst[2][lst[1][i]:lst[1][i + 1]] for i in range(len(lst[0]))][::-1]
+        return (lst[0][::-1].copy(), np.concatenate([[0], np.cumsum([len(x) for x in runs])]).astype(np.uint32),
+                np.concatenate(runs))
+
+    out = {"workload": "config 5's intersection output (50k entries {X, Cx ++ Cy}) re-bound "
+                       "after R changed; the Store: update R -> intersection -> re-bind"}
+    for name, (o, n) in (("us_rebind_50k", (old, new)), ("us_rebind_50k_reversed", (rev(old), rev(new)))):
+        a = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*o)
+        b = engine.ListBatch(ctx, _lib.KIND_ORSET_LIST).upload(*n)
+        for _ in range(3):
+            a.bind(b, order)
+        t0 = time.perf_counter()
+        for _ in range(30):
+            a.bind(b, order)
+        out[name] = (time.perf_counter() - t0) * 1e6 / 30
+    st = core.Store(capacity=1 << 18, ctx=ctx)
+    lv, rv, xv = (st.declare("lasp_orset")[1] for _ in range(3))
+    tk = lambda c, e: bytes([c]) + int(e).to_bytes(19, "big")   # noqa: E731
+    st.bind(lv, [(e, [(tk(1, e), False)]) for e in range(N)])
+    st.bind(rv, [(e, [(tk(2, e), False)]) for e in range(D - N, D)])
+    st.intersection(lv, rv, xv)
+    st.update(rv, ("add_by_token", tk(3, 999), D - N + 1), Atom("a"))
+    t0 = time.perf_counter()
+    for i in range(10):
+        st.update(rv, ("add_by_token", tk(3, i), D - N + 17 * i), Atom("a"))
+    out["ms_store_update_rerun_rebind_50k"] = (time.perf_counter() - t0) / 10 * 1e3
+    return out
+
+
 def load_traffic(path: str, replicas: int, elements: int):
     try:
         with open(path) as f:
@@ -649,6 +704,7 @@ def main():
     del a, b, c                          # free the 192 GiB of join operands first
     ctx.synchronize()
     wide = wide_leg(ctx, args) if rank == 0 and world == 1 and args.wide_replicas else None
+    lists = list_leg(ctx) if rank == 0 and world == 1 and args.list_leg else None
 
     out = None
     if rank == 0:
@@ -683,6 +739,8 @@ def main():
             out["config1_gpu"] = cfg1
         if wide is not None:
             out["join_t128"] = wide
+        if lists is not None:
+            out["config5_list_bind"] = lists
 
     if ae_on:
         def abandon():
