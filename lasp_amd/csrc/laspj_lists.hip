@@ -236,6 +236,12 @@ struct MS {
     uint32_t* aweak;   // [R] 1: a's keys are not strictly ascending (a tie or a descent)
     uint32_t ce_a, ce_b, ntiles, nchunks;
     uint32_t spec = 0; // 1: k_merge_spec walks the replicas whose ranks descend
+    // [R][nca] / [R][ncb] the largest rank of each 1024-entry chunk of A / B (zeroed, then
+    // k_merge_ranks' atomicMax), or null: a walk's long run of one side skips the chunks
+    // that cannot end it
+    u64* amax = nullptr;
+    u64* bmax = nullptr;
+    uint32_t nca = 0, ncb = 0;
 };
 
 // exclusive prefix sum / running max over a block of kMT threads (s_w: kMT/64 words)
@@ -383,6 +389,31 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
         }
         if (__syncthreads_or(desc) && threadIdx.x == 0) atomicOr(m.unsorted + r, 1u);
         if (__syncthreads_or(weak) && threadIdx.x == 0) atomicOr(m.aweak + r, 1u);
+        if (m.amax) {
+            // this block's 256 ranks of each side -> their 1024-entry chunk's maximum
+            __shared__ u64 s_mx[2][kMT / 64];
+            u64 xa = i < na ? m.sa[r * m.ce_a + i] : 0ull, xb = i < nb ? m.sb[r * m.ce_b + i] : 0ull;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const u64 ya = __shfl_xor(xa, off, 64), yb = __shfl_xor(xb, off, 64);
+                xa = ya > xa ? ya : xa;
+                xb = yb > xb ? yb : xb;
+            }
+            if (lane_id() == 0) {
+                s_mx[0][threadIdx.x >> 6] = xa;
+                s_mx[1][threadIdx.x >> 6] = xb;
+            }
+            __syncthreads();
+            if (threadIdx.x < 2) {
+                u64 v = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < kMT / 64; ++k) v = s_mx[threadIdx.x][k] > v ? s_mx[threadIdx.x][k] : v;
+                const uint32_t c = blockIdx.x * kMT / 1024u;
+                if (threadIdx.x == 0 && blockIdx.x * kMT < na) atomicMax(m.amax + r * m.nca + c, v);
+                if (threadIdx.x == 1 && blockIdx.x * kMT < nb) atomicMax(m.bmax + r * m.ncb + c, v);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -728,18 +759,26 @@ __device__ __forceinline__ uint32_t win_fail(const Win256& A, const Win256& B, u
 
 // the run's length from positions p (and q for ties) onwards over global ranks, to the
 // first failure or the end of a side
+// (software-pipelined: the next 1024 ranks of each side are in flight while the current
+// ones are tested, so a long run costs one memory round trip per 1024, not two)
 template <int KIND>
 __device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64* Y, uint32_t ny,
                                uint32_t q, u64 y) {
     uint32_t L = 0;
-    for (;;) {
-        u64 vx[16], vy[16];
+    u64 vx[16], vy[16];
+    auto load = [&](uint32_t at, u64 (&ax)[16], u64 (&ay)[16]) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            const uint32_t k = L + 64u * t + lane_id();
-            vx[t] = p + k < nx ? X[p + k] : ~0ull;
-            if (KIND == 0) vy[t] = q + k < ny ? Y[q + k] : ~0ull;
+            const uint32_t k = at + 64u * t + lane_id();
+            ax[t] = p + k < nx ? X[p + k] : ~0ull;
+            if (KIND == 0) ay[t] = q + k < ny ? Y[q + k] : ~0ull;
         }
+    };
+    load(0, vx, vy);
+    for (;;) {
+        u64 nxv[16], nyv[16];
+        const bool more = p + L + 1024u < nx && (KIND != 0 || q + L + 1024u < ny);
+        if (more) load(L + 1024u, nxv, nyv);
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t k = L + 64u * t + lane_id();
@@ -749,7 +788,52 @@ __device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64*
             if (f) return L + 64u * t + (uint32_t)__ffsll((long long)f) - 1u;
         }
         L += 1024;
+        if (!more) load(L, nxv, nyv);          // (all past the end: the next test fails)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            vx[t] = nxv[t];
+            if (KIND == 0) vy[t] = nyv[t];
+        }
     }
+}
+
+// stream_run<1> (X[p ..] < y: the length of the run from p) with the chunk maxima of X:
+// the rest of p's 1024-entry chunk, then straight to the first later chunk whose maximum
+// reaches y (a ballot over 64 chunk maxima at a time), then that chunk — three memory
+// round trips for a run of any length instead of one per 1024 entries
+__device__ uint32_t stream_run_max(const u64* X, uint32_t nx, uint32_t p, u64 y, const u64* mx,
+                                   uint32_t nc) {
+    if (!mx) return stream_run<1>(X, nx, p, nullptr, 0, 0, y);
+    auto scan = [&](uint32_t from, uint32_t to) -> uint32_t {    // first q in [from, to): X >= y
+        for (uint32_t b0 = from; b0 < to; b0 += 1024u) {
+            u64 v[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t k = b0 + 64u * t + lane_id();
+                v[t] = k < to ? X[k] : ~0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const u64 f = __ballot(v[t] >= y);
+                if (f) return b0 + 64u * t + (uint32_t)__ffsll((long long)f) - 1u;
+            }
+        }
+        return to;
+    };
+    if (p >= nx) return 0;
+    const uint32_t ce = min(nx, ((p >> 10) + 1u) << 10);
+    uint32_t q = scan(p, ce);
+    if (q < ce) return q - p;
+    for (uint32_t c0 = ce >> 10; c0 < nc; c0 += 64u) {
+        const uint32_t c = c0 + lane_id();
+        const u64 f = __ballot(c < nc && mx[c] >= y);
+        if (f) {
+            const uint32_t cf = c0 + (uint32_t)__ffsll((long long)f) - 1u;
+            q = scan(cf << 10, min(nx, (cf + 1u) << 10));
+            return q - p;
+        }
+    }
+    return nx - p;
 }
 
 // one replica's walk by one wave (its lanes); k_merge_tile_scan runs it on its first wave
@@ -787,7 +871,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
             } else if (x < y) {
                 const uint32_t s = i - A.base;
                 L = win_fail<1>(A, B, s, y) - s;
-                if (L == 256u - s) L += stream_run<1>(SA, na, i + L, nullptr, 0, 0, y);
+                if (L == 256u - s)
+                    L += stream_run_max(SA, na, i + L, y, m.amax ? m.amax + r * m.nca : nullptr, m.nca);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(i + k) : (u64)(i + k) | ((u64)kNone << 32);
                 i += L;
@@ -795,7 +880,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
             } else {
                 const uint32_t s = j - B.base;
                 L = win_fail<2>(A, B, s, x) - s;
-                if (L == 256u - s) L += stream_run<1>(SB, nb, j + L, nullptr, 0, 0, x);
+                if (L == 256u - s)
+                    L += stream_run_max(SB, nb, j + L, x, m.bmax ? m.bmax + r * m.ncb : nullptr, m.ncb);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
                                             : (u64)kNone | ((u64)(j + k) << 32);
@@ -2556,7 +2642,12 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
         if (spL >= (1u << 20)) spC = 0;
     }
     const uint64_t sz_fr = spC ? R * 4ull * m.ce_a : 0;
-    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72 + sz_fr + 8;
+    // chunk maxima for the one-wave walk's long runs, when an input is known not to ascend
+    const bool maxima = (spec || ctx->tune_list_walk == 3) && ctx->tune_list_walk != 1;
+    const uint32_t nca = (m.ce_a + 1023u) / 1024u, ncb = (m.ce_b + 1023u) / 1024u;
+    const uint64_t sz_mx = maxima ? R * 8ull * ((uint64_t)nca + ncb) : 0;
+    const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72 + sz_fr +
+                           sz_mx + 16;
     char* base = static_cast<char*>(lscratch(ctx, total));
     if (!base) return fail(ctx, LASPJ_E_NOMEM, "%s: scratch", what);
     char* q = base;
@@ -2575,6 +2666,13 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.chunk = reinterpret_cast<uint32_t*>(take(sz_c));
     m.nout = reinterpret_cast<uint32_t*>(take(sz_r));
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
+    if (maxima) {
+        m.amax = reinterpret_cast<u64*>(take(sz_mx));
+        m.bmax = m.amax + R * nca;
+        m.nca = nca;
+        m.ncb = ncb;
+        LJ_HIP(ctx, hipMemsetAsync(m.amax, 0, sz_mx, ctx->stream));
+    }
     SP sp{};
     if (spC) {
         sp.fr = reinterpret_cast<uint32_t*>(take(sz_fr));

@@ -111,9 +111,23 @@ enum class Op { MERGE, VALUE, EQUAL, INFLATION, BIND, WRITE, THRESHOLD, READ, VV
 typedef uint32_t pull16 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src,
                                                   pull16* __restrict__ dst, uint64_t n16) {
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
-        dst[i] = __builtin_nontemporal_load(src + i);
+    // a wave moves 4 KiB per step: four 1 KiB loads in flight per instruction group
+    const uint64_t lane = threadIdx.x & 63u;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t c = wave; c * 256 < n16; c += nw) {
+        pull16 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t i = c * 256 + k * 64 + lane;
+            if (i < n16) v[k] = __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t i = c * 256 + k * 64 + lane;
+            if (i < n16) dst[i] = v[k];
+        }
+    }
 }
 
 struct Guard {
