@@ -802,7 +802,7 @@ __device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64*
 // reaches y (a ballot over 64 chunk maxima at a time), then that chunk — three memory
 // round trips for a run of any length instead of one per 1024 entries
 __device__ uint32_t stream_run_max(const u64* X, uint32_t nx, uint32_t p, u64 y, const u64* mx,
-                                   uint32_t nc) {
+                                   uint32_t nc, u64 mreg) {
     if (!mx) return stream_run<1>(X, nx, p, nullptr, 0, 0, y);
     auto scan = [&](uint32_t from, uint32_t to) -> uint32_t {    // first q in [from, to): X >= y
         for (uint32_t b0 = from; b0 < to; b0 += 1024u) {
@@ -824,9 +824,11 @@ __device__ uint32_t stream_run_max(const u64* X, uint32_t nx, uint32_t p, u64 y,
     const uint32_t ce = min(nx, ((p >> 10) + 1u) << 10);
     uint32_t q = scan(p, ce);
     if (q < ce) return q - p;
-    for (uint32_t c0 = ce >> 10; c0 < nc; c0 += 64u) {
+    for (uint32_t c0 = (ce >> 10) & ~63u; c0 < nc; c0 += 64u) {
+        // (chunks 0 .. 63: the maxima the walk holds in registers, mreg = chunk lane's)
         const uint32_t c = c0 + lane_id();
-        const u64 f = __ballot(c < nc && mx[c] >= y);
+        const u64 v = c0 == 0 ? mreg : (c < nc ? mx[c] : 0ull);
+        const u64 f = __ballot(c >= (ce >> 10) && c < nc && v >= y);
         if (f) {
             const uint32_t cf = c0 + (uint32_t)__ffsll((long long)f) - 1u;
             q = scan(cf << 10, min(nx, (cf + 1u) << 10));
@@ -847,6 +849,9 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
         Win256 A{SA, na, 0, {}}, B{SB, nb, 0, {}};
         A.load(0);
         B.load(0);
+        // the first 64 chunk maxima of each side, one per lane (stream_run_max)
+        const u64 mra = m.amax && lane_id() < m.nca ? m.amax[r * m.nca + lane_id()] : 0ull;
+        const u64 mrb = m.bmax && lane_id() < m.ncb ? m.bmax[r * m.ncb + lane_id()] : 0ull;
         u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
         uint32_t i = 0, j = 0, o = 0, sx = 0;        // sx: the last single step was B's
         while (i < na && j < nb) {
@@ -872,7 +877,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
                 const uint32_t s = i - A.base;
                 L = win_fail<1>(A, B, s, y) - s;
                 if (L == 256u - s)
-                    L += stream_run_max(SA, na, i + L, y, m.amax ? m.amax + r * m.nca : nullptr, m.nca);
+                    L += stream_run_max(SA, na, i + L, y, m.amax ? m.amax + r * m.nca : nullptr, m.nca,
+                                        mra);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(i + k) : (u64)(i + k) | ((u64)kNone << 32);
                 i += L;
@@ -881,7 +887,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
                 const uint32_t s = j - B.base;
                 L = win_fail<2>(A, B, s, x) - s;
                 if (L == 256u - s)
-                    L += stream_run_max(SB, nb, j + L, x, m.bmax ? m.bmax + r * m.ncb : nullptr, m.ncb);
+                    L += stream_run_max(SB, nb, j + L, x, m.bmax ? m.bmax + r * m.ncb : nullptr, m.ncb,
+                                        mrb);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
                                             : (u64)kNone | ((u64)(j + k) << 32);
