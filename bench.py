@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--nt", type=int, default=-1)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_pmc_join.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_pmc_join.json"),
                     help="PMC summary giving HBM traffic per join launch")
     ap.add_argument("--antientropy", choices=["auto", "on", "off"], default="auto",
                     help="config-3 gossip anti-entropy leg (auto: when N > 1)")

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS="--steps 5 --warmup 1 --no-cpu"
+ARGS="--steps 5 --warmup 1 --no-cpu --wide-replicas 0 --list-leg 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats -o run -- \
     python3 bench.py $ARGS > gpurun_out/prof_stats.log 2>&1 || exit $?
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- \
