@@ -2318,9 +2318,48 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     const bool mine = lane < N;
     const uint32_t s = x0 + (lane && mine ? L.rst[lane - 1] : 0u);
     bool ok = mine && s < srel;
-    // the element's rank: its header 104 2 <elem image> 108 by hash
+    // the element's rank.  First the prediction that the payload holds every element from
+    // prev on (the lane's element is rank prev + 1 + lane): that rank's descriptor, header
+    // template and token buckets are loaded together, and an exact match of the header
+    // bytes against the template (self-delimiting images: only its own element's header
+    // matches) settles it — one round of loads where the hash probe below takes three
+    // (bucket, template, then descriptor and buckets)
     uint32_t hl = 0;
-    const int64_t rk = ok ? hdr_rank(w, s, lim, hh, t, E, hl) : -1;
+    int64_t rk = -1;
+    const int64_t pr = prev + 1 + (int64_t)lane;
+    uint4 pds = {0u, 0u, 0u, 0u};
+    uint32_t ptb[kSmallTok];
+    bool predicted = false;
+    if (ok && pr < (int64_t)E) {
+        pds = t.desc[pr];
+        const u32x4* tp = reinterpret_cast<const u32x4*>(t.hdr + 64ull * pr);
+        u32x4 tw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tw[j] = tp[j];
+#pragma unroll
+        for (uint32_t j = 0; j < kSmallTok; ++j) ptb[j] = t.tb[(u64)pr * RK + min(j, RK - 1u)];
+        const uint32_t L2 = pds.y;
+        if (L2 > 3u && L2 <= 64u && s + L2 <= lim) {
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int rem = (int)L2 - 4 * j;
+                if (rem <= 0) break;
+                const uint32_t v = word_at(w.buf, min(s + 4u * j, kBWin + 56u));
+                const uint32_t q = rem >= 4 ? v : v & ((1u << (8 * rem)) - 1u);
+                const u32x4 a = tw[j >> 2];
+                const uint32_t tv = (j & 3) == 0 ? a.x : (j & 3) == 1 ? a.y : (j & 3) == 2 ? a.z : a.w;
+                eq &= q == tv;
+            }
+            if (eq) {
+                rk = pr;
+                hl = L2;
+                predicted = true;
+            }
+        }
+    }
+    // otherwise its header 104 2 <elem image> 108 by hash
+    if (ok && !predicted) rk = hdr_rank(w, s, lim, hh, t, E, hl);
     ok = rk >= 0;
     // ranks ascend: after the previous lane's element (lane 0: after prev)
     const int64_t prk = (int64_t)(int32_t)__shfl((int32_t)rk, (lane + 63u) & 63u, 64);
@@ -2328,7 +2367,7 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     u64 pb = 0, rb = 0;
     uint32_t e = 0, y = s;
     if (ok) {
-        const uint4 ds = t.desc[rk];
+        const uint4 ds = predicted ? pds : t.desc[rk];
         e = ds.x;
         const uint32_t cnt = ds.w, kw = 4u * (ds.z & 0xFFu), ksh = ds.z >> 8;
         y = s + hl;
@@ -2339,7 +2378,8 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
         // the element's token buckets (by term rank) and rank -> slot
         uint32_t tb[kSmallTok];
 #pragma unroll
-        for (uint32_t j = 0; j < kSmallTok; ++j) tb[j] = ok && j < cnt ? t.tb[(u64)rk * RK + j] : 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < kSmallTok; ++j)
+            tb[j] = ok && j < cnt ? (predicted ? ptb[j] : t.tb[(u64)rk * RK + j]) : 0xFFFFFFFFu;
         const u64 ord = ok ? *reinterpret_cast<const u64*>(d.tok_order + 64ull * e) : 0ull;
         int32_t kprev = -1;
         for (uint32_t j = 0; ok && j < m; ++j) {
