@@ -3084,6 +3084,15 @@ __device__ bool chain_ok(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
 // first offending segment in stream order deciding.
 __device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
                                  uint32_t ns, uint32_t S, const SegRes* res, uint32_t lane) {
+    // segment 0 and the first 256 segments' results loaded together (one memory round
+    // trip for a payload of up to 257 segments, instead of one per 64)
+    constexpr int kPre = 4;
+    SegRes pre[kPre];
+#pragma unroll
+    for (int t = 0; t < kPre; ++t) {
+        const uint32_t s = 1u + 64u * t + lane;
+        pre[t] = s < ns ? res[g0 + s] : SegRes{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
+    }
     const SegRes a = res[g0];
     if (a.st != LASPJ_DEC_OK) return a.st;                 // segment 0 starts at the head
     if (a.flags & kSegEmptyList) return a.end == len ? LASPJ_DEC_OK : kDecRedo;
@@ -3092,7 +3101,14 @@ __device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint
     for (uint32_t s0 = 1; s0 < ns; s0 += 64) {
         const uint32_t s = s0 + lane;
         SegRes b{LASPJ_DEC_OK, kSegNone, 0, 0, -1, -1, 0, 0};
-        if (s < ns) b = res[g0 + s];
+        const uint32_t grp = (s0 - 1u) / 64u;
+        if (grp < (uint32_t)kPre) {
+#pragma unroll
+            for (int t = 0; t < kPre; ++t)
+                if ((uint32_t)t == grp) b = pre[t];
+        } else if (s < ns) {
+            b = res[g0 + s];
+        }
         const bool valid = s < ns && b.start != kSegNone;
         int32_t li = valid ? (int32_t)lane : -1;
 #pragma unroll
