@@ -261,3 +261,71 @@ def test_list_cases_are_the_oracles_answers():
         oetf.binary_to_term(a)
         if exp:
             oetf.binary_to_term(exp)
+
+
+@pytest.mark.gpu
+def test_list_images_fuzz_answer_or_fall_back():
+    """Mutated images (truncated, a byte flipped, junk appended, a tag byte replaced) into
+    the list bodies and bind: every call answers FALLBACK, raises an error status, or
+    answers OK with the oracle body's answer on the terms the mutated images decode to —
+    never a crash (the NIF runs inside the BEAM) and never a wrong OK."""
+    from lasp_amd import _lib, engine
+    ctx = engine.Context(0)
+    rng = random.Random(99)
+    try:
+        A = _orddict(rng, rng.sample(range(40), 10))
+        B = _orddict(rng, rng.sample(range(40), 10))
+        bases = [("orset", "union", A, B), ("orset", "intersection", A, B),
+                 ("orset", "product", A[:4], B[:4]), ("orset", "bind", A, B),
+                 ("gset", "union", [1, 5, 9, Atom("x")], [5, 2, b"q"]),
+                 ("gset", "bind", [1, 5, 9], [2, 5])]
+
+        def mutate(img):
+            b = bytearray(img)
+            k = rng.randrange(4)
+            if k == 0 and len(b) > 2:
+                return bytes(b[:rng.randrange(1, len(b))])
+            if k == 1:
+                i = rng.randrange(len(b))
+                b[i] ^= 1 << rng.randrange(8)
+                return bytes(b)
+            if k == 2:
+                return bytes(b) + bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 6)))
+            i = rng.randrange(1, len(b))
+            b[i] = rng.choice([97, 98, 100, 104, 106, 107, 108, 109, 110, 115, 118, 119])
+            return bytes(b)
+
+        answered = 0
+        for n in range(3000):
+            kind, body, a, b = bases[n % len(bases)]
+            ia, ib = _tb(a), _tb(b)
+            if n % 2:
+                ia = mutate(ia)
+            else:
+                ib = mutate(ib)
+            try:
+                if body == "bind":
+                    verd, st, img = ctx.list_etf_bind(kind, ia, ib)
+                else:
+                    verd, img = ctx.list_etf(body, kind, ia, ib)
+            except _lib.LaspjError:
+                continue
+            assert verd in (OK, FALLBACK)
+            if verd != OK:
+                continue
+            # an OK answer: the mutated images are terms the body takes, and the answer is
+            # the oracle's
+            ta, tb_ = oetf.binary_to_term(ia), oetf.binary_to_term(ib)
+            t = "lasp_gset" if kind == "gset" else "lasp_orset"
+            if body == "bind":
+                want_st, m = _bind_oracle(kind, ta, tb_)
+                assert st == want_st, (ta, tb_)
+                if st == 1:
+                    assert exact_eq(oetf.binary_to_term(img), m)
+            else:
+                want = getattr(ocore, body + "_body")(t, ta, tb_)
+                assert exact_eq(oetf.binary_to_term(img), want), (body, ta, tb_)
+            answered += 1
+        assert answered > 0
+    finally:
+        ctx.close()
