@@ -340,3 +340,79 @@ def test_var_config1_bind():
         var.close()
     finally:
         ctx.close()
+
+
+def test_nif_and_var_fuzz_mutated_images():
+    """Mutated term_to_binary images (truncated, a bit flipped, junk appended, a tag byte
+    replaced) into merge / equal / value and into a resident variable's bind: each call
+    answers FALLBACK, raises an error status, or answers OK with the oracle's answer on the
+    terms the images decode to; a variable's value stays the oracle's after every bind that
+    answered (a failed decode leaves it untouched)."""
+    from lasp_amd import _lib
+    ctx = _ctx()
+    try:
+        rng = random.Random(57)
+        elems, pool = _universe(rng, 40)
+        A = _orset(rng, elems, pool)
+        B = _orset(rng, elems, pool)
+
+        def mutate(img):
+            b = bytearray(img)
+            k = rng.randrange(4)
+            if k == 0 and len(b) > 2:
+                return bytes(b[:rng.randrange(1, len(b))])
+            if k == 1:
+                i = rng.randrange(len(b))
+                b[i] ^= 1 << rng.randrange(8)
+                return bytes(b)
+            if k == 2:
+                return bytes(b) + bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 6)))
+            i = rng.randrange(1, len(b))
+            b[i] = rng.choice([97, 98, 100, 104, 106, 107, 108, 109, 110, 115, 118, 119])
+            return bytes(b)
+
+        def decoded(img):
+            try:
+                return True, oetf.binary_to_term(img)
+            except Exception:
+                return False, None
+
+        var = ctx.var("orset")
+        assert var.bind(_tb(A)) == (OK, 1)
+        cur = A
+        answered = 0
+        for n in range(1500):
+            ma = mutate(_tb(B))
+            op = n % 4
+            try:
+                if op == 0:
+                    verd, img = ctx.nif_merge(_tb(A), ma)
+                elif op == 1:
+                    verd, res = ctx.nif_equal(_tb(A), ma)
+                elif op == 2:
+                    verd, img = ctx.nif_value(ma)
+                else:
+                    verd, st = var.bind(ma)
+            except _lib.LaspjError:
+                continue
+            assert verd in (OK, FALLBACK)
+            if verd != OK:
+                continue
+            ok, tb_ = decoded(ma)
+            assert ok, (op, ma)
+            if op == 0:
+                assert exact_eq(oetf.binary_to_term(img), oorset.merge(A, tb_))
+            elif op == 1:
+                assert res == oorset.equal(A, tb_)
+            elif op == 2:
+                assert exact_eq(oetf.binary_to_term(img), oorset.value(tb_))
+            else:
+                want_st, cur2 = _bind_oracle("lasp_orset", cur, tb_)
+                assert st == want_st
+                cur = cur2
+            answered += 1
+        assert answered > 0
+        verd, img = var.read()
+        assert verd == OK and exact_eq(oetf.binary_to_term(img), cur)
+    finally:
+        ctx.close()
