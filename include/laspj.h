@@ -163,7 +163,13 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         at a time), 8 = the same as 0, 10 = as 0, with
                                         segment mode's redo pass as a launch of its own
                                         (by default the chain check's wave decodes a
-                                        payload that failed it again itself)           */
+                                        payload that failed it again itself).
+                                        G-Set from_binary forms (the OR-Set decoders as
+                                        with 0): 11 = round 4's (header by byte loads,
+                                        a window per 256 elements, a payload's last 16
+                                        bytes one element per window), 12 = 11 with the
+                                        tail taken from the window, 13 = 4 elements per
+                                        lane per round, 14 = 512-element chunks      */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

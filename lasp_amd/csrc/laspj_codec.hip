@@ -3480,7 +3480,6 @@ __device__ __forceinline__ void gs_lookup(const GsTabs& g, const uint8_t* p, uin
     *rk = *slot != kNoSlot ? g.rank[*slot] : 0;
 }
 
-constexpr uint32_t kGChunk = 256;
 constexpr uint32_t kGWin = 4096;          // LDS window over the payload (LIST_EXT walk)
 constexpr uint32_t kGWords = 256;         // replicas of <= 256 words collect their bits in LDS
 
@@ -3505,54 +3504,78 @@ __device__ __forceinline__ u64 gs_elem_len(const uint8_t* buf, uint32_t o, uint3
 }
 
 // One wave per replica.  LIST_EXT payloads are walked once: the payload is staged into
-// LDS 4 KiB at a time, lane 0 finds the next <= 256 element extents in the window
+// LDS 4 KiB at a time, lane 0 finds the next <= CH element extents in the window
 // (common tags by their headers, anything else by etf_term_len), then every lane takes
-// one element: dictionary slot by hash and exact compare, term order against the
-// element before it, the bit set.  The statuses are those of the upfront whole-term
-// validation this walk replaces: the first structural failure in stream order decides
-// (truncation -> MALFORMED, a tag no dictionary term has -> UNKNOWN_TERM), then an
-// improper tail or trailing bytes (MALFORMED), then an element outside the dictionary
-// or out of order (UNKNOWN_TERM).
+// ILP elements: dictionary slot by the integer table or by hash and exact compare (the
+// table loads of all ILP elements in flight together), term order against the element
+// before it, the bit set.  The statuses are those of the upfront whole-term validation
+// this walk replaces: the first structural failure in stream order decides (truncation
+// -> MALFORMED, a tag no dictionary term has -> UNKNOWN_TERM), then an improper tail or
+// trailing bytes (MALFORMED), then an element outside the dictionary or out of order
+// (UNKNOWN_TERM).
+template <uint32_t CH, uint32_t ILP, bool KEEP, bool TAIL>
 __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, const u64* offs,
                                                       uint64_t R, GsTabs g, int tag, int vers,
-                                                      u64* words, uint64_t W, int32_t* status,
-                                                      const uint32_t* redo) {
-    __shared__ uint32_t s_o[kGChunk], s_l[kGChunk];
+                                                      u64* words, uint64_t W, int32_t* status) {
+    __shared__ uint32_t s_o[CH], s_l[CH];
     __shared__ u64 s_h[4];
     __shared__ __attribute__((aligned(16))) uint8_t win[kGWin + 16];
     __shared__ u64 s_w[kGWords];
     const uint32_t lane = threadIdx.x;
     // the element bits: OR-ed into LDS and stored once per replica when the replica's
     // words fit (64 lanes setting bits of the same word would serialise on one global
-    // atomic), else straight into the batch with global atomics
+    // atomic; every word is stored, so the batch needs no clearing first), else straight
+    // into the (cleared) batch with global atomics
     const bool lw = W <= kGWords;
-    // with `redo` (the block parser's fallback, W <= kGWords): the replicas listed there,
-    // whose words are all rewritten below
-    const uint64_t count = redo ? (uint64_t)redo[0] : R;
-    for (uint64_t i = blockIdx.x; i < count; i += gridDim.x) {
-        const uint64_t rep = redo ? (uint64_t)redo[1 + i] : i;
-        const uint8_t* p = payload + offs[rep];
-        const u64 n = offs[rep + 1] - offs[rep];
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64 ob = offs[rep], aend = offs[rep + 1];
+        const uint8_t* p = payload + ob;
+        const u64 n = aend - ob;
         u64* w = words + rep * W;
         if (lw)
             for (uint32_t x = lane; x < W; x += 64) s_w[x] = 0;
+        // the LDS window [a0, a0 + wl) over the payload buffer: stage [at & ~15, + 4 KiB)
+        // (absolute offsets stay 16-B aligned in the buffer: payload offsets are
+        // arbitrary, so bytes go one by one into place through 16-byte loads of the
+        // aligned span)
+        u64 a0 = 0;
+        uint32_t wl = 0;
+        auto stage = [&](u64 at0) {
+            a0 = at0 & ~15ull;
+            wl = (uint32_t)min((u64)kGWin, aend - a0);
+            for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
+                const u64 at = a0 + 16ull * v;
+                if (at + 16 <= aend) {
+                    *reinterpret_cast<u32x4*>(win + 16 * v) =
+                        *reinterpret_cast<const u32x4*>(payload + at);
+                } else {
+                    for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
+                }
+            }
+            __syncthreads();
+        };
+        // KEEP: the first window is staged at once and the header read from it (one
+        // round trip instead of the header's dependent byte loads), and a window that
+        // still holds the rest of the payload (or 2 KiB of it) is walked on, not restaged
+        if (KEEP) stage(ob);
+        const uint8_t* hp = KEEP ? win + (ob - a0) : p;
         if (lane == 0) {
             // s_h: {status, list tag, element count, first element offset}
             int st = LASPJ_DEC_OK;
             u64 h = 0;
             if (tag >= 0) {
-                if (n < 2 || p[0] != (uint8_t)tag) st = LASPJ_DEC_INVALID_BINARY;
-                else if (p[1] != (uint8_t)vers) st = LASPJ_DEC_UNSUPPORTED_VERSION;
+                if (n < 2 || hp[0] != (uint8_t)tag) st = LASPJ_DEC_INVALID_BINARY;
+                else if (hp[1] != (uint8_t)vers) st = LASPJ_DEC_UNSUPPORTED_VERSION;
                 h = 2;
             }
-            if (st == LASPJ_DEC_OK && (n < h + 2 || p[h] != 131)) st = LASPJ_DEC_MALFORMED;
+            if (st == LASPJ_DEC_OK && (n < h + 2 || hp[h] != 131)) st = LASPJ_DEC_MALFORMED;
             u64 lt = 0, cnt = 0, first = 0;
             if (st == LASPJ_DEC_OK) {
-                lt = p[h + 1];
+                lt = hp[h + 1];
                 if (lt == 108) {
                     // validated by the element walk below (one pass over the payload)
                     if (n - h - 1 < 5) st = LASPJ_DEC_MALFORMED;
-                    else cnt = be32(p + h + 2), first = h + 6;
+                    else cnt = be32(hp + h + 2), first = h + 6;
                 } else {
                     const u64 L = etf_term_len(p + h + 1, n - h - 1);
                     if (L == kTermOther) st = LASPJ_DEC_UNKNOWN_TERM;
@@ -3599,23 +3622,11 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
         } else if (st == LASPJ_DEC_OK && lt == 108) {
             u64 left = cnt;
             while (left > 0 && st == LASPJ_DEC_OK) {
-                // stage [pos & ~15, + 4 KiB) of the payload (absolute offsets stay 16-B
-                // aligned in the buffer: payload offsets are arbitrary, so bytes go one by
-                // one into place through 16-byte loads of the aligned span)
-                const u64 a0 = (offs[rep] + pos) & ~15ull;
-                const u64 aend = offs[rep] + n;
-                const uint32_t wl = (uint32_t)min((u64)kGWin, aend - a0);
-                for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
-                    const u64 at = a0 + 16ull * v;
-                    if (at + 16 <= aend) {
-                        *reinterpret_cast<u32x4*>(win + 16 * v) =
-                            *reinterpret_cast<const u32x4*>(payload + at);
-                    } else {
-                        for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
-                    }
-                }
-                __syncthreads();
-                const uint32_t base = (uint32_t)(offs[rep] + pos - a0);     // pos in win
+                const u64 apos = ob + pos;
+                if (!KEEP || !(apos >= a0 && apos <= a0 + wl &&
+                               (aend <= a0 + wl || a0 + wl - apos >= 2048)))
+                    stage(apos);
+                const uint32_t base = (uint32_t)(apos - a0);                // pos in win
                 {
                     // element extents inside the window, the whole wave walking together:
                     // lanes test whether the next 64 elements all have the length L0 of the
@@ -3624,16 +3635,20 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                     // equal-length images (small integers, then larger ones) at once;
                     // otherwise one element from its header, or the general walk (global
                     // bytes) for other tags and for an element the window does not hold
-                    const uint32_t mx = (uint32_t)min(left, (u64)kGChunk);
+                    const uint32_t mx = (uint32_t)min(left, (u64)CH);
                     uint32_t k = 0, o = base, L0 = 0;
                     int est = LASPJ_DEC_OK;
                     while (k < mx) {
                         const u64 rel = pos + (o - base);                  // payload offset
                         if (rel >= n) { est = LASPJ_DEC_MALFORMED; break; }
                         uint32_t run = 0;
+                        // (gs_elem_len bounds its own reads: TAIL takes elements up to the
+                        // window's last byte, so a payload's last elements, which sit
+                        // within 16 bytes of its end, need no restage each)
                         if (L0) {
                             const uint32_t q = o + lane * L0;
-                            const bool ok = lane < mx - k && q + 16 <= wl &&
+                            const bool ok = lane < mx - k &&
+                                            (TAIL ? q + L0 <= wl : q + 16 <= wl) &&
                                             gs_elem_len(win, q, wl) == L0 &&
                                             rel + (u64)(lane + 1) * L0 <= n;
                             const u64 msk = __ballot(ok);
@@ -3648,10 +3663,12 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                             k += run;
                             continue;
                         }
-                        u64 L = o + 16 <= wl ? gs_elem_len(win, o, wl) : 0;
+                        u64 L = (TAIL ? o < wl : o + 16 <= wl) ? gs_elem_len(win, o, wl) : 0;
                         L0 = (L && o + L <= wl && L <= 64) ? (uint32_t)L : 0u;
                         if (L == 0 || o + L > wl) {
-                            if (o + 16 <= wl || k == 0) {
+                            // a tag the window cannot size (or a window that ends at the
+                            // payload's end): the general walk over global bytes
+                            if (o + 16 <= wl || k == 0 || (TAIL && a0 + wl >= aend)) {
                                 L = etf_term_len(p + rel, n - rel);
                                 if (L == kTermOther) { est = LASPJ_DEC_UNKNOWN_TERM; break; }
                                 if (L == 0) { est = LASPJ_DEC_MALFORMED; break; }
@@ -3677,26 +3694,71 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                 __syncthreads();
                 st = (int)s_h[0];
                 const uint32_t m = (uint32_t)s_h[2];
-                for (uint32_t k0 = 0; k0 < m; k0 += 64) {
-                    const uint32_t k = k0 + lane;
-                    uint32_t slot = kNoSlot, rk = 0;
-                    if (k < m) {
-                        const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0);
-                        const bool in = s_l[k] <= 0xFFFFFFu && o + s_l[k] <= wl;
-                        if (s_l[k] > 0xFFFFFFu) slot = kNoSlot;
-                        else gs_lookup(g, in ? win + o : p + s_o[k], s_l[k], &slot, &rk);
+                for (uint32_t k0 = 0; k0 < m; k0 += 64 * ILP) {
+                    // every element's integer-table load first (gs_lookup's integer case),
+                    // then the hash probes of the rest, then the order checks in sequence
+                    uint32_t slot[ILP], rk[ILP];
+                    u64 t[ILP];
+                    uint32_t how[ILP];             // 0 nothing, 1 integer table, 2 hash
+#pragma unroll
+                    for (uint32_t j = 0; j < ILP; ++j) {
+                        const uint32_t k = k0 + 64 * j + lane;
+                        how[j] = 0;
+                        t[j] = 0;
+                        if (k < m && s_l[k] <= 0xFFFFFFu) {
+                            const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0), L = s_l[k];
+                            const uint8_t* q = o + L <= wl ? win + o : p + s_o[k];
+                            how[j] = 2;
+                            if (g.itab && (L == 2 || L == 5) && (q[0] == 97 || q[0] == 98)) {
+                                bool ok = false;
+                                int64_t v = 0;
+                                if (L == 2 && q[0] == 97) {
+                                    v = q[1];
+                                    ok = true;
+                                } else if (L == 5 && q[0] == 98) {
+                                    v = (int32_t)((uint32_t)q[1] << 24 | (uint32_t)q[2] << 16 |
+                                                  (uint32_t)q[3] << 8 | q[4]);
+                                    ok = v < 0 || v > 255;
+                                }
+                                if (ok) {
+                                    how[j] = 1;
+                                    const int64_t x = v - g.ilo;
+                                    if (x >= 0 && x < (int64_t)g.in) t[j] = g.itab[x];
+                                }
+                            }
+                        }
                     }
-                    const uint32_t before = __shfl_up(rk, 1, 64);
-                    bool bad = k < m && (slot == kNoSlot ||
-                                         (lane ? rk <= before : (have_prev && rk <= prev_rank)));
-                    if (k < m && !bad) {
-                        if (lw) atomicOr(s_w + (slot >> 6), 1ull << (slot & 63));
-                        else atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+#pragma unroll
+                    for (uint32_t j = 0; j < ILP; ++j) {
+                        slot[j] = kNoSlot;
+                        rk[j] = 0;
+                        if (how[j] == 1) {
+                            slot[j] = (uint32_t)t[j] ? (uint32_t)t[j] - 1u : kNoSlot;
+                            rk[j] = (uint32_t)(t[j] >> 32);
+                        } else if (how[j] == 2) {
+                            const uint32_t k = k0 + 64 * j + lane;
+                            const uint32_t o = (uint32_t)(offs[rep] + s_o[k] - a0), L = s_l[k];
+                            gs_lookup(g, o + L <= wl ? win + o : p + s_o[k], L, &slot[j], &rk[j]);
+                        }
                     }
-                    unknown |= __ballot(bad) != 0;
-                    const uint32_t last = (m - k0 < 64 ? m - k0 : 64) - 1;
-                    prev_rank = __shfl(rk, last, 64);
-                    have_prev = true;
+#pragma unroll
+                    for (uint32_t j = 0; j < ILP; ++j) {
+                        const uint32_t c0 = k0 + 64 * j;
+                        if (c0 >= m) break;
+                        const bool valid = c0 + lane < m;
+                        const uint32_t before = __shfl_up(rk[j], 1, 64);
+                        const bool bad = valid && (slot[j] == kNoSlot ||
+                                                   (lane ? rk[j] <= before
+                                                         : (have_prev && rk[j] <= prev_rank)));
+                        if (valid && !bad) {
+                            if (lw) atomicOr(s_w + (slot[j] >> 6), 1ull << (slot[j] & 63));
+                            else atomicOr(w + (slot[j] >> 6), 1ull << (slot[j] & 63));
+                        }
+                        unknown |= __ballot(bad) != 0;
+                        const uint32_t last = (m - c0 < 64 ? m - c0 : 64) - 1;
+                        prev_rank = __shfl(rk[j], last, 64);
+                        have_prev = true;
+                    }
                 }
                 left -= m;
                 pos = s_h[3];
@@ -3720,6 +3782,24 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
         __syncthreads();
         if (lw)
             for (uint32_t x = lane; x < W; x += 64) w[x] = s_w[x];
+    }
+}
+
+// the G-Set decoder's form: 256-element chunks, one element per lane per round, the
+// header read from the first window and windows kept while they hold the rest, the
+// payload's tail taken from the window (LASPJ_TUNE_ETF_READ 11: the round-4 form, 12:
+// that with the tail from the window, 13: 4 elements per lane, 14: 512-element chunks;
+// profiles/r05_gset_read_forms.log.  Tried and dropped: the bits of a word run of lanes
+// OR-ed together before one atomic, 0.389 -> 0.42 ms)
+using GsRead = void (*)(const uint8_t*, const u64*, uint64_t, GsTabs, int, int, u64*, uint64_t,
+                        int32_t*);
+GsRead gset_reader(const laspj_ctx* ctx) {
+    switch (ctx->tune_etf_read) {
+    case 11: return k_gset_etf_read<256, 1, false, false>;
+    case 12: return k_gset_etf_read<256, 1, false, true>;
+    case 13: return k_gset_etf_read<256, 4, true, true>;
+    case 14: return k_gset_etf_read<512, 1, true, true>;
+    default: return k_gset_etf_read<256, 1, true, true>;
     }
 }
 
@@ -3928,13 +4008,14 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     const uint64_t cap = (uint64_t)ctx->cus * 64;
     const uint8_t* pay = static_cast<const uint8_t*>(payload->dev);
     const u64* offs = static_cast<const u64*>(offsets->dev);
-    LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull, ctx->stream));
+    if (b->words_per_replica > kGWords)
+        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
+                                   ctx->stream));
     // one wave per replica and a latency-bound extent walk: as many waves as LDS allows
-    // (6 KiB each: ~25 per CU)
-    hipLaunchKernelGGL(k_gset_etf_read, dim3((unsigned)std::max<uint64_t>(1, std::min(R, cap))),
+    hipLaunchKernelGGL(gset_reader(ctx), dim3((unsigned)std::max<uint64_t>(1, std::min(R, cap))),
                        dim3(64), 0, ctx->stream, pay, offs, R, tabs, tag, vers,
                        reinterpret_cast<u64*>(b->dev), b->words_per_replica,
-                       static_cast<int32_t*>(status->dev), (const uint32_t*)nullptr);
+                       static_cast<int32_t*>(status->dev));
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }
@@ -4075,7 +4156,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
                                    ctx->stream));
     const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
-    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6)
+    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
+                                              ctx->tune_etf_read >= 8)
                      ? k_orset_etf_read<true> : k_orset_etf_read<false>;
     const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
     // the header hash (segment search; element batches without the scalar walk — knob 6
@@ -4128,7 +4210,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
             LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
         }
         const bool csmall = d->tok_max <= kSmallTok &&
-                            (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6);
+                            (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
+                             ctx->tune_etf_read >= 8);
         hipLaunchKernelGGL(csmall ? k_etf_read_chain<true> : k_etf_read_chain<false>,
                            dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)), dim3(64), 0,
                            ctx->stream, payload, (u64)payload_bytes, offs, R, dsegbase,
@@ -4167,15 +4250,14 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                       const uint8_t* payload, const u64* offs, int32_t* status, bool clear) {
     const uint64_t R = b->replicas;
-    if (clear)
+    if (clear && b->words_per_replica > kGWords)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, R * b->words_per_replica * 8ull, ctx->stream));
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
-    hipLaunchKernelGGL(k_gset_etf_read,
+    hipLaunchKernelGGL(gset_reader(ctx),
                        dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 64))),
                        dim3(64), 0, ctx->stream, payload, offs, R, tabs, tag, vers,
-                       reinterpret_cast<u64*>(b->dev), b->words_per_replica, status,
-                       (const uint32_t*)nullptr);
+                       reinterpret_cast<u64*>(b->dev), b->words_per_replica, status);
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }

@@ -353,8 +353,8 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_etf = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_READ:
-            if (value < 0 || value > 10 || value == 9)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..8 or 10");
+            if (value < 0 || value > 14 || value == 9)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..8 or 10..14");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_SEG:

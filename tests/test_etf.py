@@ -465,7 +465,8 @@ def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
     <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
     scan, 2 = batched records only, 7 = no many-token element batches, 8 = the same as
-    0, 9 = the block decoders (many-token OR-Sets, integer G-Sets), 4 = every payload
+    0, 11..14 = the G-Set decoder's other forms (the OR-Set decoders as with 0), 4 = every
+    payload
     longer than 256 bytes split between waves (segment mode: header search, chain check, redo
     of failed replicas); "seg512": the default kernels with every payload longer than 512
     bytes split (LASPJ_TUNE_ETF_SEG)."""
@@ -1185,7 +1186,8 @@ def test_gpu_gset_from_binary_errors():
 
 
 @pytest.mark.gpu
-def test_gpu_gset_from_binary_long_payloads():
+@pytest.mark.parametrize("knob", [0, 11, 12, 13, 14])
+def test_gpu_gset_from_binary_long_payloads(knob):
     """Payloads longer than the decoder's 4 KiB window (the walk restages it): 10k
     integers (2- and 5-byte images: runs of equal lengths taken 64 at a time), mixed
     terms with atoms, binaries and tuples of many lengths, a binary longer than the
@@ -1230,13 +1232,15 @@ def test_gpu_gset_from_binary_long_payloads():
     cases.append((swapped, _lib.DEC_UNKNOWN_TERM))
     pay, offs = _upload_payloads(ctx, [c[0] for c in cases])
     b = ctx.gset_batch(len(cases), E)
-    st = b.etf_decode(d, pay, offs, tag=T, vers=1)
+    with _read_kernel(ctx, knob):
+        st = b.etf_decode(d, pay, offs, tag=T, vers=1)
     assert list(st) == [c[1] for c in cases]
     assert np.array_equal(b.download()[:len(states)], dom.encode_gset(states, E))
 
 
 @pytest.mark.gpu
-def test_gpu_gset_from_binary_fuzz():
+@pytest.mark.parametrize("knob", [0, 11, 13])
+def test_gpu_gset_from_binary_fuzz(knob):
     """2000 corrupted G-Set payloads against the oracle's binary_to_term: payloads it
     decodes to an ordset of dictionary terms decode OK to the host encoder's words; other
     lists give UNKNOWN_TERM, non-lists and structural failures MALFORMED (a tag the oracle
@@ -1269,7 +1273,8 @@ def test_gpu_gset_from_binary_fuzz():
         blobs.append(bytes(b))
     pay, offs = _upload_payloads(ctx, blobs)
     bt = ctx.gset_batch(len(blobs), E)
-    st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+    with _read_kernel(ctx, knob):
+        st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
     words = bt.download()
     eb, eo, _o, *_ = dom.etf_arrays(E, tokens=False)
     images = {bytes(eb[eo[k]:eo[k + 1]]): k for k in range(dom.size)}

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """G-Set from_binary at the suite's shape (tools/bench_suite.py: 65536 replicas x 1024
 integer elements, ~50 % present, SMALL_INTEGER_EXT / INTEGER_EXT images): the wave
-decoder (LASPJ_TUNE_ETF_READ 0) against the block parser (9), interleaved, each checked
-against the batch it was encoded from."""
+decoder's forms (LASPJ_TUNE_ETF_READ 0 = default, 11 = round 4's, 12 = 11 with the
+payload's tail taken from the window, 13 = 4 elements per lane, 14 = 512-element chunks),
+interleaved, each checked against the batch it was encoded from."""
 import json
 import os
 import sys
@@ -41,7 +42,7 @@ def run():
 
 
 for rep in range(2):
-    for knob in (0, 9):
+    for knob in (0, 11, 12, 13, 14):
         ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
         back.clear()
         for _ in range(3):
