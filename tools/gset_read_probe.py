@@ -18,6 +18,7 @@ from lasp_amd.codec import Domain  # noqa: E402
 R = int(os.environ.get("GS_R", "65536"))
 E = int(os.environ.get("GS_E", "1024"))
 STEPS = int(os.environ.get("STEPS", "10"))
+KNOBS = [int(k) for k in os.environ.get("KNOBS", "0,11,12,13,14").split(",")]
 
 ctx = engine.Context(0)
 L = ctx.L
@@ -42,7 +43,7 @@ def run():
 
 
 for rep in range(2):
-    for knob in (0, 11, 12, 13, 14):
+    for knob in KNOBS:
         ctx.set_tuning(_lib.TUNE_ETF_READ, knob)
         back.clear()
         for _ in range(3):
