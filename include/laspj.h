@@ -132,7 +132,10 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         kernel, per element thread, 24 KiB.  0 also
                                         writes a NIF entry point's single merge in one
                                         launch with its join and size pass (look-back);
-                                        any other value keeps them separate              */
+                                        any other value keeps them separate.  G-Set
+                                        writer: few long payloads in chunks of 256 slots
+                                        over the chip unless 6 (one wave per payload) or
+                                        1 (one block per payload)                        */
 #define LASPJ_TUNE_REDUCE_KERNEL 5   /* OR reduce over replica groups: 0 = tiles of 4
                                         cells per lane, one per block, when the replica
                                         length is a power of two and 2 <= group <= 4
@@ -169,7 +172,11 @@ int         laspj_ctx_synchronize(laspj_ctx* ctx);
                                         a window per 256 elements, a payload's last 16
                                         bytes one element per window), 12 = 11 with the
                                         tail taken from the window, 13 = 4 elements per
-                                        lane per round, 14 = 512-element chunks      */
+                                        lane per round, 14 = 512-element chunks, 15 =
+                                        the default form; 11..15 never take the split
+                                        decoder of few long payloads (the default's
+                                        element extents by one wave per payload, then
+                                        the elements resolved over the chip)          */
 #define LASPJ_TUNE_ETF_SEG       9   /* OR-Set from_binary segment bytes: 0 = sized by
                                         the launch (see LASPJ_TUNE_ETF_READ), else split
                                         every payload longer than this (>= 256, a

@@ -1429,6 +1429,125 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words
     }
 }
 
+// Split G-Set writer (few long payloads: the NIF's value/1 and merge answers, one 10k-
+// element ordset each, which one wave walking 64 elements at a time wrote in ~400 us): a
+// block takes a chunk of 256 slots in term order.  k_gset_chunk_sizes gives each chunk its
+// image bytes and element counts {bytes, elements | non-byte-integer elements << 32};
+// k_gset_chunk_scan (one block) turns them into per-payload exclusive prefixes (entry nch
+// = the payload's totals) and, with `offsets`, the payload offsets (k_gset_etf_size's
+// sizes, scanned); k_gset_write_chunks writes each chunk's images from its prefix (bytes,
+// or elements under STRING_EXT), chunk 0 the list header, the last chunk the tail.
+__global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, uint64_t R,
+                                                             uint32_t E, uint32_t W, DictView d,
+                                                             uint32_t nch, u64x2* co,
+                                                             uint32_t* flag) {
+    __shared__ u64 lds4[kBlock / 64];
+    for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
+        const uint64_t rep = it / nch;
+        const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
+        const u64* w = words + rep * W;
+        u64 by = 0, cn = 0;
+        if (i < E) {
+            const uint32_t e = d.elem_order[i];
+            if ((w[e >> 6] >> (e & 63u)) & 1ull) {
+                const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
+                // as k_gset_etf_size: a present slot without an image is an error
+                if (el == 0 && flag) atomicOr(flag, 1u);
+                by = el;
+                cn = 1ull + (d.elem_byte[e] == 0 ? (1ull << 32) : 0ull);
+            }
+        }
+        if (c == 0 && flag)                          // bits of no slot (past E): an error too
+            for (uint32_t wi = (E >> 6) + threadIdx.x; wi < W; wi += kBlock) {
+                u64 m = w[wi];
+                if (wi == (E >> 6)) m &= ~((1ull << (E & 63u)) - 1ull);
+                if (m) atomicOr(flag, 1u);
+            }
+        u64 tb, tc;
+        block_excl_scan64(by, lds4, &tb);
+        block_excl_scan64(cn, lds4, &tc);
+        if (threadIdx.x == 0) co[rep * (nch + 1ull) + c] = u64x2{tb, tc};
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gset_chunk_scan(u64x2* co, uint64_t R, uint32_t nch,
+                                                            uint32_t hdr, u64* offsets) {
+    __shared__ u64 lds4[kBlock / 64];
+    u64 run = 0;                                     // payload offset (one block: few payloads)
+    for (uint64_t rep = 0; rep < R; ++rep) {
+        u64x2* c = co + rep * (nch + 1ull);
+        u64 cb = 0, cc = 0;
+        for (uint32_t t0 = 0; t0 <= nch; t0 += kBlock) {
+            const uint32_t t = t0 + threadIdx.x;
+            const u64x2 v = t < nch ? c[t] : u64x2{0, 0};
+            u64 tb, tc;
+            const u64 eb = block_excl_scan64(v.x, lds4, &tb);
+            const u64 ec = block_excl_scan64(v.y, lds4, &tc);
+            if (t <= nch) c[t] = u64x2{cb + eb, cc + ec};
+            cb += tb;
+            cc += tc;
+        }
+        if (offsets) {
+            const uint32_t n = (uint32_t)cc, nb = (uint32_t)(cc >> 32);
+            const u64 body = n == 0 ? 1u : (nb == 0 && n < 65536u) ? 3u + n : 5u + cb + 1u;
+            if (threadIdx.x == 0) offsets[rep] = run;
+            run += hdr + 1u + body;
+        }
+    }
+    if (offsets && threadIdx.x == 0) offsets[R] = run;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, uint64_t R,
+                                                              uint32_t E, uint32_t W, DictView d,
+                                                              int tag, int vers, const u64* offs,
+                                                              uint8_t* out, u64 ocap,
+                                                              const u64x2* co, uint32_t nch) {
+    if (offs[R] > ocap) return;
+    __shared__ u64 lds4[kBlock / 64];
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
+        const uint64_t rep = it / nch;
+        const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
+        const u64* w = words + rep * W;
+        const u64x2 pre = co[rep * (nch + 1ull) + c], all = co[rep * (nch + 1ull) + nch];
+        const uint32_t n = (uint32_t)all.y, nb = (uint32_t)(all.y >> 32);
+        const bool str = n > 0 && nb == 0 && n < 65536u;
+        const u64 base = offs[rep], end = offs[rep + 1];
+        const u64 cursor = base + hdr + 1u + (str ? 3u : 5u) + (str ? (uint32_t)pre.y : pre.x);
+        uint32_t e = 0, el = 0;
+        bool here = false;
+        if (i < E) {
+            e = d.elem_order[i];
+            here = (w[e >> 6] >> (e & 63u)) & 1ull;
+            if (here) el = d.elem_off[e + 1] - d.elem_off[e];
+        }
+        const u64 sz = here ? (str ? 1u : el) : 0u;
+        u64 tot;
+        const u64 pos = block_excl_scan64(sz, lds4, &tot);
+        // sizes disagree with the offsets: never overrun the payload
+        const bool fits = cursor + tot + (str ? 0u : 1u) <= end;
+        if (fits && here) {
+            uint8_t* o = out + cursor + pos;
+            const uint8_t* src = d.elem_blob + d.elem_off[e];
+            if (str) {
+                o[0] = src[1];
+            } else if (el <= 16) {
+                const u32x4 t = *reinterpret_cast<const u32x4*>(d.elem_pad + d.elem_poff[e]);
+                const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b)
+                    if (b < el) o[b] = (uint8_t)(tw[b >> 2] >> (8 * (b & 3)));
+            } else {
+                for (uint32_t b = 0; b < el; ++b) o[b] = src[b];
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (c == 0) write_list_header(out, base, hdr, tag, vers, n == 0 ? 106 : str ? 107 : 108, n);
+            if (c == nch - 1 && fits && n && !str && cursor + tot < end) out[cursor + tot] = 106;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ from_binary/1
 // binary_to_term of OR-Set payloads into cells (lasp_orset.erl:202-214 decodes with
 // riak_dt:from_binary/1 = binary_to_term/1), for dictionaries with uniform token images.
@@ -3803,6 +3922,228 @@ GsRead gset_reader(const laspj_ctx* ctx) {
     }
 }
 
+// Split G-Set decoder (few long payloads: the NIF's merge operands, one 10k-element
+// ordset each, which one wave resolving 64 elements per round decoded in ~300 us).
+// Pass 1 (k_gset_read_walk): one wave per payload walks the element extents only -- the
+// header from the first window, runs of equal-length images 256 at a time in a 32 KiB LDS
+// window, the general walk for other tags, the tail -- and writes every element's offset
+// relative to its payload to eo[offs[r] + r + k] (entry n: the tail's), the element count
+// to en[r] and the walk's status to status[r] (the structural statuses of
+// k_gset_etf_read; a STRING_EXT payload, at most 65535 bytes, is decoded here whole).
+// Pass 2 (k_gset_read_lookup): waves over the chip take 64 elements each: slot and rank by
+// gs_lookup, strictly ascending ranks (lane 0 resolves the element before its chunk too),
+// the bit set with a global atomic (the words are zero on entry); a failure turns an OK
+// status into UNKNOWN_TERM.  Statuses and bits are k_gset_etf_read's.
+constexpr uint32_t kGWinL = 32768;
+
+__global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, const u64* offs,
+                                                       uint64_t R, GsTabs g, int tag, int vers,
+                                                       u64* words, uint64_t W, int32_t* status,
+                                                       uint32_t* eo, uint32_t* en) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kGWinL + 16];
+    __shared__ u64 s_h[4];
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64 ob = offs[rep], aend = offs[rep + 1];
+        const uint8_t* p = payload + ob;
+        const u64 n = aend - ob;
+        u64* w = words + rep * W;
+        uint32_t* e = eo + ob + rep;
+        u64 a0 = 0;
+        uint32_t wl = 0;
+        auto stage = [&](u64 at0) {
+            a0 = at0 & ~15ull;
+            wl = (uint32_t)min((u64)kGWinL, aend - a0);
+            for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
+                const u64 at = a0 + 16ull * v;
+                if (at + 16 <= aend) {
+                    *reinterpret_cast<u32x4*>(win + 16 * v) =
+                        *reinterpret_cast<const u32x4*>(payload + at);
+                } else {
+                    for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
+                }
+            }
+            __syncthreads();
+        };
+        stage(ob);
+        const uint8_t* hp = win + (ob - a0);
+        if (lane == 0) {
+            int st = LASPJ_DEC_OK;
+            u64 h = 0;
+            if (tag >= 0) {
+                if (n < 2 || hp[0] != (uint8_t)tag) st = LASPJ_DEC_INVALID_BINARY;
+                else if (hp[1] != (uint8_t)vers) st = LASPJ_DEC_UNSUPPORTED_VERSION;
+                h = 2;
+            }
+            if (st == LASPJ_DEC_OK && (n < h + 2 || hp[h] != 131)) st = LASPJ_DEC_MALFORMED;
+            u64 lt = 0, cnt = 0, first = 0;
+            if (st == LASPJ_DEC_OK) {
+                lt = hp[h + 1];
+                if (lt == 108) {
+                    if (n - h - 1 < 5) st = LASPJ_DEC_MALFORMED;
+                    else cnt = be32(hp + h + 2), first = h + 6;
+                } else {
+                    const u64 L = etf_term_len(p + h + 1, n - h - 1);
+                    if (L == kTermOther) st = LASPJ_DEC_UNKNOWN_TERM;
+                    else if (L == 0 || L != n - h - 1) st = LASPJ_DEC_MALFORMED;
+                    else if (lt == 107) cnt = (u64)p[h + 2] << 8 | p[h + 3], first = h + 4;
+                    else if (lt != 106) st = LASPJ_DEC_MALFORMED;
+                }
+            }
+            s_h[0] = (u64)st;
+            s_h[1] = lt;
+            s_h[2] = cnt;
+            s_h[3] = first;
+        }
+        __syncthreads();
+        int st = (int)s_h[0];
+        const uint32_t lt = (uint32_t)s_h[1];
+        const u64 cnt = s_h[2];
+        u64 pos = s_h[3];
+        __syncthreads();
+        u64 found = 0;
+        if (st == LASPJ_DEC_OK && lt == 107) {
+            // STRING_EXT: every byte is the integer element of that value
+            bool unknown = false, have_prev = false;
+            uint32_t prev_rank = 0;
+            for (u64 c0 = 0; c0 < cnt; c0 += 64) {
+                const u64 i = c0 + lane;
+                uint32_t slot = kNoSlot, rk = 0;
+                if (i < cnt) {
+                    const uint32_t v = g.byte_slot[p[pos + i]];
+                    slot = v ? v - 1 : kNoSlot;
+                    rk = slot != kNoSlot ? g.rank[slot] : 0;
+                }
+                const uint32_t before = __shfl_up(rk, 1, 64);
+                const bool bad = i < cnt && (slot == kNoSlot ||
+                                             (lane ? rk <= before : (have_prev && rk <= prev_rank)));
+                if (i < cnt && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                unknown |= __ballot(bad) != 0;
+                const uint32_t last = (uint32_t)((cnt - c0 < 64 ? cnt - c0 : 64) - 1);
+                prev_rank = __shfl(rk, last, 64);
+                have_prev = true;
+            }
+            if (unknown) st = LASPJ_DEC_UNKNOWN_TERM;
+        } else if (st == LASPJ_DEC_OK && lt == 108) {
+            u64 left = cnt;
+            while (left > 0 && st == LASPJ_DEC_OK) {
+                const u64 apos = ob + pos;
+                if (!(apos >= a0 && apos <= a0 + wl &&
+                      (aend <= a0 + wl || a0 + wl - apos >= kGWinL / 2)))
+                    stage(apos);
+                uint32_t o = (uint32_t)(apos - a0), L0 = 0;
+                u64 k = 0;
+                int est = LASPJ_DEC_OK;
+                while (k < left) {
+                    const u64 rel = a0 + o - ob;                   // payload offset
+                    if (rel >= n) { est = LASPJ_DEC_MALFORMED; break; }
+                    uint32_t run = 0;
+                    if (L0) {
+                        // candidate j * 64 + lane at o + (j * 64 + lane) L0: the run is the
+                        // first candidate whose image is not L0 long
+                        bool go = true;
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; ++j) {
+                            if (!go) break;
+                            const uint32_t idx = j * 64 + lane, q = o + idx * L0;
+                            const bool ok = idx < left - k && q + L0 <= wl &&
+                                            gs_elem_len(win, q, wl) == L0 &&
+                                            rel + (u64)(idx + 1) * L0 <= n;
+                            const u64 msk = __ballot(ok);
+                            const uint32_t r = ~msk ? (uint32_t)__ffsll((long long)~msk) - 1u : 64u;
+                            run += r;
+                            go = r == 64;
+                        }
+                    }
+                    if (run) {
+                        for (uint32_t idx = lane; idx < run; idx += 64)
+                            e[found + k + idx] = (uint32_t)(rel + (u64)idx * L0);
+                        o += run * L0;
+                        k += run;
+                        continue;
+                    }
+                    u64 L = o < wl ? gs_elem_len(win, o, wl) : 0;
+                    L0 = (L && o + L <= wl && L <= 64) ? (uint32_t)L : 0u;
+                    if (L == 0 || o + L > wl) {
+                        if (o + 16 <= wl || k == 0 || a0 + wl >= aend) {
+                            L = etf_term_len(p + rel, n - rel);
+                            if (L == kTermOther) { est = LASPJ_DEC_UNKNOWN_TERM; break; }
+                            if (L == 0) { est = LASPJ_DEC_MALFORMED; break; }
+                        } else {
+                            break;                     // restage at this element
+                        }
+                    }
+                    if (rel + L > n) { est = LASPJ_DEC_MALFORMED; break; }
+                    if (lane == 0) e[found + k] = (uint32_t)rel;
+                    o += (uint32_t)min(L, (u64)0x7FFFFFFF);
+                    ++k;
+                    if (o > wl) break;                 // the next element starts past it
+                }
+                found += k;
+                left -= k;
+                pos = a0 + o - ob;
+                st = est;
+            }
+            if (st == LASPJ_DEC_OK) {
+                if (pos >= n) {
+                    st = LASPJ_DEC_MALFORMED;
+                } else if (p[pos] != 106) {
+                    const u64 L = etf_term_len(p + pos, n - pos);
+                    st = L == kTermOther ? LASPJ_DEC_UNKNOWN_TERM : LASPJ_DEC_MALFORMED;
+                } else if (pos + 1 != n) {
+                    st = LASPJ_DEC_MALFORMED;
+                }
+            }
+        }
+        if (lane == 0) {
+            status[rep] = st;
+            const bool list = st == LASPJ_DEC_OK && lt == 108;
+            en[rep] = list ? (uint32_t)found : 0u;
+            if (list) e[found] = (uint32_t)pos;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gset_read_lookup(const uint8_t* payload,
+                                                             const u64* offs, uint64_t R, GsTabs g,
+                                                             u64* words, uint64_t W,
+                                                             int32_t* status, const uint32_t* eo,
+                                                             const uint32_t* en) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = 0; rep < R; ++rep) {
+        const uint32_t n = en[rep];                  // 0: nothing left to resolve
+        if (n == 0) continue;
+        const u64 ob = offs[rep];
+        const uint8_t* p = payload + ob;
+        const uint32_t* e = eo + ob + rep;
+        u64* w = words + rep * W;
+        for (uint64_t c = wave; c * 64 < n; c += nwaves) {
+            const uint64_t k = c * 64 + lane;
+            const bool valid = k < n;
+            uint32_t slot = kNoSlot, rk = 0, prk = 0;
+            if (valid) {
+                const uint32_t o = e[k], L = e[k + 1] - o;
+                if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &slot, &rk);
+            }
+            const bool have_prev = lane == 0 && k > 0;
+            if (have_prev) {
+                const uint32_t o = e[k - 1], L = e[k] - o;
+                uint32_t ps = kNoSlot;
+                if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &ps, &prk);
+            }
+            const uint32_t before = __shfl_up(rk, 1, 64);
+            const bool bad = valid && (slot == kNoSlot ||
+                                       (lane ? rk <= before : (have_prev && rk <= prk)));
+            if (valid && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+            if (__ballot(bad) && lane == 0)
+                atomicCAS(status + rep, (int32_t)LASPJ_DEC_OK, (int32_t)LASPJ_DEC_UNKNOWN_TERM);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ exclusive scans
 // out[i] = in[0] + ... + in[i-1] for i <= n (out[n] = the total): the payload offsets from
 // the per-replica sizes.  Up to kScanOne values one block walks tiles of 256 with a carry
@@ -3981,6 +4322,37 @@ int etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, i
                             static_cast<int32_t*>(status->dev), true, nullptr);
 }
 
+// few long G-Set payloads: the split decoder (knobs LASPJ_TUNE_ETF_READ 11..15: one wave
+// per payload always)
+static bool gset_read_split(const laspj_ctx* ctx, uint64_t R, const u64* off) {
+    if ((ctx->tune_etf_read >= 11 && ctx->tune_etf_read <= 15) || R > (uint64_t)ctx->cus ||
+        R == 0)
+        return false;
+    u64 longest = 0;
+    for (uint64_t i = 0; i < R; ++i) longest = std::max<u64>(longest, off[i + 1] - off[i]);
+    return longest >= 4096 && longest < (1ull << 31) && off[R] < (1ull << 40);
+}
+
+// pass 1 one wave per payload, pass 2 over the chip; the element offsets at the scratch's
+// start (4 bytes per payload byte and per payload, + 4); the words are zero on entry
+static int gset_read_split_enqueue(laspj_ctx* ctx, laspj_batch* b, const GsTabs& tabs, int tag,
+                                   int vers, const uint8_t* payload, const u64* offs,
+                                   u64 payload_end, int32_t* status) {
+    const uint64_t R = b->replicas;
+    const uint64_t eo_bytes = (4ull * (payload_end + R + 1) + 255ull) & ~255ull;
+    if (int s = reserve_scratch(ctx, eo_bytes + 4ull * R)) return s;
+    uint32_t* eo = static_cast<uint32_t*>(ctx->scratch);
+    uint32_t* en = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->scratch) + eo_bytes);
+    hipLaunchKernelGGL(k_gset_read_walk, dim3((unsigned)R), dim3(64), 0, ctx->stream, payload,
+                       offs, R, tabs, tag, vers, reinterpret_cast<u64*>(b->dev),
+                       b->words_per_replica, status, eo, en);
+    hipLaunchKernelGGL(k_gset_read_lookup, dim3((unsigned)ctx->cus * 2), dim3(kBlock), 0,
+                       ctx->stream, payload, offs, R, tabs, reinterpret_cast<u64*>(b->dev),
+                       b->words_per_replica, status, (const uint32_t*)eo, (const uint32_t*)en);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                   const laspj_buf* payload, const laspj_buf* offsets, laspj_buf* status) {
     const char* what = "gset_etf_read";
@@ -4008,6 +4380,12 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
     const uint64_t cap = (uint64_t)ctx->cus * 64;
     const uint8_t* pay = static_cast<const uint8_t*>(payload->dev);
     const u64* offs = static_cast<const u64*>(offsets->dev);
+    if (gset_read_split(ctx, R, off.data())) {
+        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
+                                   ctx->stream));
+        return gset_read_split_enqueue(ctx, b, tabs, tag, vers, pay, offs, off[R],
+                                       static_cast<int32_t*>(status->dev));
+    }
     if (b->words_per_replica > kGWords)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
                                    ctx->stream));
@@ -4248,12 +4626,18 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
 }
 
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
-                      const uint8_t* payload, const u64* offs, int32_t* status, bool clear) {
+                      const uint8_t* payload, const u64* offs, int32_t* status, bool clear,
+                      const u64* hoffs) {
     const uint64_t R = b->replicas;
-    if (clear && b->words_per_replica > kGWords)
-        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, R * b->words_per_replica * 8ull, ctx->stream));
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
+    if (hoffs && gset_read_split(ctx, R, hoffs)) {
+        if (clear)
+            LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, R * b->words_per_replica * 8ull, ctx->stream));
+        return gset_read_split_enqueue(ctx, b, tabs, tag, vers, payload, offs, hoffs[R], status);
+    }
+    if (clear && b->words_per_replica > kGWords)
+        LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, R * b->words_per_replica * 8ull, ctx->stream));
     hipLaunchKernelGGL(gset_reader(ctx),
                        dim3((unsigned)std::max<uint64_t>(1, std::min(R, (uint64_t)ctx->cus * 64))),
                        dim3(64), 0, ctx->stream, payload, offs, R, tabs, tag, vers,
@@ -4262,11 +4646,42 @@ int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, i
     return LASPJ_OK;
 }
 
+// few long G-Set payloads: chunks of 256 term-order slots spread over the chip for the
+// size pass and the writer (LASPJ_TUNE_ETF_KERNEL 6: one wave per payload always)
+static bool gset_split(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
+    return ctx->tune_etf != 6 && R <= (uint64_t)ctx->cus && (E + kBlock - 1) / kBlock >= 4;
+}
+
+// the split G-Set size pass: chunk sums and their scan (with `offsets`: the payload
+// offsets too); the chunk table at the scratch's start
+static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
+                               uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks) {
+    const uint64_t R = b->replicas;
+    const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+    if (int s = reserve_scratch(ctx, 16ull * R * (nch + 1ull))) return s;
+    u64x2* co = static_cast<u64x2*>(ctx->scratch);
+    const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
+    hipLaunchKernelGGL(k_gset_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+                       (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
+                       view(d), nch, co, flag);
+    hipLaunchKernelGGL(k_gset_chunk_scan, dim3(1), dim3(kBlock), 0, ctx->stream, co, R, nch, hdr,
+                       offsets);
+    LJ_LAUNCHED(ctx);
+    *chunks = reinterpret_cast<const u64*>(co);
+    return LASPJ_OK;
+}
+
 int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d, int32_t kind,
                      int tag, u64* offsets, uint32_t* flag, const u64** chunks) {
     const uint64_t R = b->replicas;
     const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    if (kind == LASPJ_KIND_GSET && gset_split(ctx, R, b->elements)) {
+        const u64* co = nullptr;
+        if (int s = gset_chunks_enqueue(ctx, b, d, hdr, offsets, flag, &co)) return s;
+        if (chunks) *chunks = co;
+        return LASPJ_OK;
+    }
     // few long OR-Set payloads: sizes from per-chunk sums spread over the chip (as the
     // writer's split mode) instead of one wave walking each payload
     const bool split = kind == LASPJ_KIND_ORSET && R <= (uint64_t)ctx->cus && nch >= 4;
@@ -4453,7 +4868,20 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
         hipLaunchKernelGGL(k_orset_etf_write, dim3(grid ? grid : 1), dim3(kBlock), 0, ctx->stream,
                            reinterpret_cast<const u64x2*>(b->dev), R, b->elements, view(d), tag,
                            vers, offsets, out, (u64)cap_bytes);
-    else
+    else if (gset_split(ctx, R, b->elements) && ctx->tune_etf != 1) {
+        // the chunk table from the size pass (or computed here when the caller's size
+        // pass ran apart: the public size / write pair)
+        const u64* co = chunks;
+        if (!co)
+            if (int s = gset_chunks_enqueue(ctx, b, d, tag >= 0 ? 2u : 0u, nullptr, nullptr, &co))
+                return s;
+        const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(k_gset_write_chunks,
+                           dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
+                           dim3(kBlock), 0, ctx->stream, (const u64*)b->dev, R, b->elements,
+                           (uint32_t)b->words_per_replica, view(d), tag, vers, offsets, out,
+                           (u64)cap_bytes, reinterpret_cast<const u64x2*>(co), nch);
+    } else
         // LASPJ_TUNE_ETF_KERNEL 1: the block-per-payload staging writer
         hipLaunchKernelGGL(ctx->tune_etf == 1 ? k_gset_etf_write : k_gset_etf_write_wave,
                            dim3(ctx->tune_etf == 1 ? (grid ? grid : 1)

@@ -324,7 +324,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
 // offsets / status are device addresses; clear: zero the batch first
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                       const uint8_t* payload, const unsigned long long* offsets, int32_t* status,
-                      bool clear);
+                      bool clear,
+                      const unsigned long long* hoffs = nullptr);
 // merge/2 of a[i] and b[i] into z fused with z's size pass (and a, b cleared behind it),
 // when etf_merge_fused(ctx, R, E) holds; ticket: one zeroed word (left zero)
 bool etf_merge_fused(const laspj_ctx* ctx, uint64_t R, uint32_t E);

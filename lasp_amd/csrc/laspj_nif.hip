@@ -516,7 +516,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
                     return s;
             } else if (int s = gset_read_enqueue(ctx, &inb, K.etf, -1, 1, din + i_pay,
                                                  reinterpret_cast<const unsigned long long*>(din + i_offs),
-                                                 dst, !clean)) {
+                                                 dst, !clean, hoffs.data())) {
                 return s;
             }
         } else if (m && var_op) {
@@ -570,11 +570,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
             laspj_batch src = c.op == Op::VALUE ? inb : view(ctx, c.kind, 1, E, c.vars[0]->cells);
             LJ_HIP(ctx, launch_orset_value(ctx, &src, cout, false));
             laspj_batch vb = view(ctx, LASPJ_KIND_GSET, n, E, cout);
+            const unsigned long long* chunks = nullptr;
             if (int s = etf_size_enqueue(ctx, &vb, K.etf, LASPJ_KIND_GSET, -1, dooff, ctx->flag,
-                                         nullptr))
+                                         &chunks))
                 return s;
             if (int s = etf_write_enqueue(ctx, &vb, K.etf, LASPJ_KIND_GSET, -1, 1, dooff, dopay,
-                                          ocap, nullptr))
+                                          ocap, chunks))
                 return s;
             break;
         }

@@ -348,13 +348,13 @@ int laspj_ctx_set_tuning(laspj_ctx* ctx, int knob, int64_t value) {
             ctx->tune_reduce = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_KERNEL:
-            if (value < 0 || value > 5)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..5");
+            if (value < 0 || value > 6)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf kernel must be 0..6");
             ctx->tune_etf = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_READ:
-            if (value < 0 || value > 14 || value == 9)
-                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..8 or 10..14");
+            if (value < 0 || value > 15 || value == 9)
+                return fail(ctx, LASPJ_E_INVAL, "tuning: etf read must be 0..8 or 10..15");
             ctx->tune_etf_read = value;
             return LASPJ_OK;
         case LASPJ_TUNE_ETF_SEG:

@@ -465,8 +465,8 @@ def _read_kernel(ctx, knob):
     """LASPJ_TUNE_ETF_READ for the duration: 0 = batched records (+ element batches at
     <= 8 token slots, and for small elements of many-token dictionaries), 1 = serial
     scan, 2 = batched records only, 7 = no many-token element batches, 8 = the same as
-    0, 11..14 = the G-Set decoder's other forms (the OR-Set decoders as with 0), 4 = every
-    payload
+    0, 11..15 = the G-Set decoder's one-wave forms, never split (the OR-Set decoders as
+    with 0), 4 = every payload
     longer than 256 bytes split between waves (segment mode: header search, chain check, redo
     of failed replicas); "seg512": the default kernels with every payload longer than 512
     bytes split (LASPJ_TUNE_ETF_SEG)."""
@@ -1119,6 +1119,58 @@ def _gset_decode_setup(states):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("knob", [0, 6, 1])
+def test_gpu_gset_to_binary_few_long_payloads(knob):
+    """Few long G-Set payloads (the NIF's value/1 and merge answers): the split writer
+    (chunks of 256 term-order slots over the chip, LASPJ_TUNE_ETF_KERNEL 0), the one-wave
+    writer (6) and the block writer (1) give the oracle's term_to_binary byte for byte:
+    10k integers (2- and 5-byte images), every byte integer (STRING_EXT), [], mixed terms
+    (atoms, binaries, tuples, big and negative integers), a set whose elements sit in the
+    last chunk only; the public size / write pair and bare / tagged payloads; a present slot
+    without an image, or a bit past the dictionary, is refused."""
+    import numpy as np
+    from lasp_amd import _lib, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from lasp_amd import engine
+    from oracle.otp import lists_usort
+    rng = random.Random(29)
+    mixed = lists_usort([rng.randrange(-500, 70000) for _ in range(900)] +
+                        [PAtom("k" * rng.randint(1, 30)) for _ in range(40)] +
+                        [bytes(rng.randrange(256) for _ in range(rng.randint(0, 40)))
+                         for _ in range(60)] + [(rng.randrange(5), PAtom("t")) for _ in range(9)] +
+                        [1 << 40, -(1 << 35)])
+    states = [list(range(0, 30000, 3)), list(range(256)), [], mixed, list(range(29990, 30000))]
+    dom = Domain(element_capacity=1 << 16)
+    dom.encode_gset(states, 1 << 16)
+    E = dom.size + 5
+    ctx = context()
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+    b = ctx.gset_batch(len(states), E)
+    b.upload(dom.encode_gset(states, E))
+    ctx.set_tuning(_lib.TUNE_ETF_KERNEL, knob)
+    try:
+        for tag in (-1, etf.DT_GSET_TAG):
+            got = b.to_binaries(d, tag=tag, vers=1)
+            for st, g in zip(states, got):
+                want = oetf.to_binary(tag, 1, st) if tag >= 0 else oetf.term_to_binary(st)
+                assert g == want, (len(st), len(g), len(want))
+        words = dom.encode_gset(states, E)
+        words[1, (E - 2) >> 6] |= np.uint64(1) << np.uint64((E - 2) & 63)    # no image
+        b.upload(words)
+        with pytest.raises(_lib.LaspjError):
+            b.etf_encode(d)
+        if E & 63:
+            words = dom.encode_gset(states, E)
+            words[3, E >> 6] |= np.uint64(1) << np.uint64(63)                  # past E
+            b.upload(words)
+            with pytest.raises(_lib.LaspjError):
+                b.etf_encode(d)
+    finally:
+        ctx.set_tuning(_lib.TUNE_ETF_KERNEL, 0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tagged", [False, True])
 def test_gpu_gset_from_binary_round_trip(tagged):
     """lasp_gset:from_binary/1 on the device (laspj_gset_etf_read): term_to_binary
@@ -1236,6 +1288,70 @@ def test_gpu_gset_from_binary_long_payloads(knob):
         st = b.etf_decode(d, pay, offs, tag=T, vers=1)
     assert list(st) == [c[1] for c in cases]
     assert np.array_equal(b.download()[:len(states)], dom.encode_gset(states, E))
+
+
+@pytest.mark.gpu
+def test_gpu_gset_from_binary_split_fuzz():
+    """The split decoder of few long payloads (element extents by one wave per payload,
+    the elements resolved over the chip; LASPJ_TUNE_ETF_READ 0) against the one-wave
+    decoder (15, which the oracle fuzz above pins): 6 x 120 long payloads (integers of
+    2- and 5-byte images, mixed terms, every byte integer) intact and corrupted (bytes
+    changed, truncated, bytes inserted, two payloads spliced, two elements swapped) give
+    the same statuses, and the same words where OK."""
+    import numpy as np
+    from lasp_amd import _lib, engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    from oracle.otp import lists_usort
+    rng = random.Random(53)
+    T = etf.DT_GSET_TAG
+    mixed = lists_usort([rng.randrange(-300, 90000) for _ in range(1500)] +
+                        [PAtom("m" * rng.randint(1, 20)) for _ in range(30)] +
+                        [bytes(rng.randrange(256) for _ in range(rng.randint(0, 30)))
+                         for _ in range(40)] + [(rng.randrange(4), PAtom("u")) for _ in range(6)])
+    pool = [list(range(0, 40000, 3)), mixed, list(range(256, 3000)), list(range(0, 90000, 7))]
+    dom = Domain(element_capacity=1 << 17)
+    dom.encode_gset(pool + [list(range(256))], 1 << 17)
+    E = dom.size + 3
+    ctx = context()
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+    for rnd in range(6 * SOAK):
+        base = []
+        for _ in range(8):
+            src = rng.choice(pool)
+            base.append(oetf.to_binary(T, 1, lists_usort(rng.sample(src, rng.randint(len(src) // 2, len(src))))))
+        base.append(oetf.to_binary(T, 1, list(range(256))))
+        blobs = list(base)
+        while len(blobs) < 120:
+            b = bytearray(rng.choice(base))
+            kind = rng.randrange(5)
+            if kind == 0:
+                for _ in range(rng.randint(1, 3)):
+                    b[rng.randrange(2, len(b))] = rng.randrange(256)
+            elif kind == 1:
+                del b[rng.randrange(2, len(b) + 1):]
+            elif kind == 2:
+                pos = rng.randrange(2, len(b) + 1)
+                b[pos:pos] = bytes(rng.randrange(256) for _ in range(rng.randint(1, 9)))
+            elif kind == 3:
+                other = rng.choice(base)
+                b = b[:rng.randrange(2, len(b) + 1)] + other[rng.randrange(2, len(other) + 1):]
+            else:
+                j = rng.randrange(7, max(8, len(b) - 12))
+                if b[j] == 98 and b[j + 5] == 98:
+                    b[j:j + 10] = b[j + 5:j + 10] + b[j:j + 5]
+            blobs.append(bytes(b))
+        pay, offs = _upload_payloads(ctx, blobs)
+        got = {}
+        for knob in (0, 15):
+            bt = ctx.gset_batch(len(blobs), E)
+            with _read_kernel(ctx, knob):
+                st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+            got[knob] = (st, bt.download())
+        assert list(got[0][0]) == list(got[15][0]), rnd
+        ok = got[0][0] == _lib.DEC_OK
+        assert ok[:len(base)].all()
+        assert np.array_equal(got[0][1][ok], got[15][1][ok]), rnd
 
 
 @pytest.mark.gpu

@@ -83,6 +83,13 @@ def test_gset_nif_answers_match_oracle():
         pairs = [(_gset(rng, pool), _gset(rng, pool)) for _ in range(24)]
         got = ctx.nif_merge_many([(_tb(a), _tb(b)) for a, b in pairs], kind="gset")
         assert got == [(OK, _tb(ogset.merge(a, b))) for a, b in pairs]
+        # long sets (the split writer: chunks of 256 term-order slots over the chip), and
+        # value/1 of a 10k-element OR-Set image (its answer is a G-Set image)
+        big_a, big_b = list(range(0, 20000, 2)), list(range(0, 30000, 3)) + [Atom("z")]
+        assert ctx.nif_merge(_tb(big_a), _tb(big_b), kind="gset") == \
+            (OK, _tb(ogset.merge(big_a, big_b)))
+        o = [(e, [(b"A" + e.to_bytes(19, "big"), e % 7 == 0)]) for e in range(10000)]
+        assert ctx.nif_value(_tb(o)) == (OK, _tb(oorset.value(o)))
     finally:
         ctx.close()
 
