@@ -324,6 +324,27 @@ def config1_gpu(ctx):
     for _ in range(50):
         nif()
     out["us_merge_nif"] = (time.perf_counter() - t0) * 1e6 / 50
+    # value/1 of B's image (lasp_orset.erl:67-73: its answer is a G-Set image) and the
+    # lasp_gset merge of config 1's two integer sets (10k each, 5k overlap:
+    # lasp_gset.erl:99-101) through the NIF entry points, warm
+    gva = [e for e, toks in tb if any(not f for _t, f in toks)]
+    ga, gb = list(range(n)), list(range(n // 2, n + n // 2))
+    qa, qb = etf.term_to_binary(ga), etf.term_to_binary(gb)
+    for name, fn, want in (
+            ("us_value_nif", lambda: L.laspj_orset_etf_value(ctx.h, pb, len(pb), C.byref(op),
+                                                             C.byref(on), C.byref(vd)),
+             etf.term_to_binary(gva)),
+            ("us_gset_merge_nif", lambda: L.laspj_gset_etf_merge(ctx.h, qa, len(qa), qb, len(qb),
+                                                                 C.byref(op), C.byref(on),
+                                                                 C.byref(vd)),
+             etf.term_to_binary(list(range(n + n // 2))))):
+        check(fn(), ctx.h)
+        if vd.value != 0 or C.string_at(op, on.value) != want:
+            raise RuntimeError("config1: %s answered wrongly" % name)
+        t0 = time.perf_counter()
+        for _ in range(50):
+            check(fn(), ctx.h)
+        out[name] = (time.perf_counter() - t0) * 1e6 / 50
     nm = 32
     arr_a = (C.c_char_p * nm)(*([pa] * nm))
     arr_b = (C.c_char_p * nm)(*([pb] * nm))
