@@ -1557,6 +1557,29 @@ __global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, 
 // by 64 lanes comparing `104 2 <token image>` of the element's next 64 token ranks,
 // then the flag atom (ATOM_EXT, ATOM_UTF8_EXT or SMALL_ATOM_UTF8_EXT).  Elements and
 // tokens must come in term order (an orddict), so every comparison is a forward scan.
+// One wave copies nv 16-byte vectors from global memory into LDS with NL loads in flight
+// per lane: a plain `for (v = lane; v < nv; v += 64) lds[v] = src[v]` loop waits for each
+// load before its LDS store (checked in the ISA), one memory round trip per KiB staged.
+template <uint32_t NL>
+__device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint32_t nv,
+                                            uint32_t lane) {
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    const u32x4* s = reinterpret_cast<const u32x4*>(src);
+    for (uint32_t v0 = 0; v0 < nv; v0 += 64 * NL) {
+        u32x4 t[NL];
+#pragma unroll
+        for (uint32_t j = 0; j < NL; ++j) {
+            const uint32_t v = v0 + 64 * j + lane;
+            if (v < nv) t[j] = s[v];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < NL; ++j) {
+            const uint32_t v = v0 + 64 * j + lane;
+            if (v < nv) d[v] = t[j];
+        }
+    }
+}
+
 constexpr uint32_t kDWin = 2048;
 
 struct Stage {
@@ -1576,8 +1599,7 @@ __device__ bool stage_span(Stage& s, u64 p, uint32_t n, u64 lim) {
     const uint32_t lane = threadIdx.x & 63u;
     wave_sync();
     const u64 nfull = (hi - lo) >> 4;
-    for (u64 v = lane; v < nfull; v += 64)
-        reinterpret_cast<u32x4*>(s.buf)[v] = *reinterpret_cast<const u32x4*>(s.src + lo + 16 * v);
+    wave_copy16<4>(s.buf, s.src + lo, (uint32_t)nfull, lane);
     for (u64 b = lo + 16 * nfull + lane; b < hi; b += 64) s.buf[b - lo] = s.src[b];
     wave_sync();
     s.lo = lo;
@@ -1965,8 +1987,7 @@ __device__ uint32_t refill(PWin& w, uint32_t pc) {
     const uint32_t lane = threadIdx.x & 63u;
     wave_sync();
     const uint32_t nfull = (uint32_t)((hi - lo) >> 4);
-    for (uint32_t v = lane; v < nfull; v += 64)
-        reinterpret_cast<u32x4*>(w.buf)[v] = *reinterpret_cast<const u32x4*>(w.src + lo + 16ull * v);
+    wave_copy16<4>(w.buf, w.src + lo, nfull, lane);
     for (u64 b = lo + 16ull * nfull + lane; b < hi; b += 64) w.buf[b - lo] = w.src[b];
     wave_sync();
     w.lo = lo;
@@ -3662,15 +3683,9 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
         auto stage = [&](u64 at0) {
             a0 = at0 & ~15ull;
             wl = (uint32_t)min((u64)kGWin, aend - a0);
-            for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
-                const u64 at = a0 + 16ull * v;
-                if (at + 16 <= aend) {
-                    *reinterpret_cast<u32x4*>(win + 16 * v) =
-                        *reinterpret_cast<const u32x4*>(payload + at);
-                } else {
-                    for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
-                }
-            }
+            const uint32_t nfull = wl >> 4;
+            wave_copy16<2>(win, payload + a0, nfull, lane);
+            for (uint32_t k = 16 * nfull + lane; k < wl; k += 64) win[k] = payload[a0 + k];
             __syncthreads();
         };
         // KEEP: the first window is staged at once and the header read from it (one
@@ -3954,15 +3969,9 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
         auto stage = [&](u64 at0) {
             a0 = at0 & ~15ull;
             wl = (uint32_t)min((u64)kGWinL, aend - a0);
-            for (uint32_t v = lane; v < (wl + 15) / 16; v += 64) {
-                const u64 at = a0 + 16ull * v;
-                if (at + 16 <= aend) {
-                    *reinterpret_cast<u32x4*>(win + 16 * v) =
-                        *reinterpret_cast<const u32x4*>(payload + at);
-                } else {
-                    for (uint32_t k = 0; k < 16 && at + k < aend; ++k) win[16 * v + k] = payload[at + k];
-                }
-            }
+            const uint32_t nfull = wl >> 4;
+            wave_copy16<8>(win, payload + a0, nfull, lane);
+            for (uint32_t k = 16 * nfull + lane; k < wl; k += 64) win[k] = payload[a0 + k];
             __syncthreads();
         };
         stage(ob);
