@@ -236,12 +236,12 @@ struct MS {
     uint32_t* aweak;   // [R] 1: a's keys are not strictly ascending (a tie or a descent)
     uint32_t ce_a, ce_b, ntiles, nchunks;
     uint32_t spec = 0; // 1: k_merge_spec walks the replicas whose ranks descend
-    // [R][nca] / [R][ncb] the largest rank of each 1024-entry chunk of A / B (zeroed, then
-    // k_merge_ranks' atomicMax), or null: a walk's long run of one side skips the chunks
-    // that cannot end it
+    // [R][nba] / [R][nbb] the largest rank of each 256-entry block of A / B (k_merge_ranks
+    // stores every one: no clearing), or null: a walk's long run of one side skips the
+    // 1024-entry chunks (nca / ncb, four blocks each) that cannot end it
     u64* amax = nullptr;
     u64* bmax = nullptr;
-    uint32_t nca = 0, ncb = 0;
+    uint32_t nca = 0, ncb = 0, nba = 0, nbb = 0;
 };
 
 // exclusive prefix sum / running max over a block of kMT threads (s_w: kMT/64 words)
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
         if (__syncthreads_or(desc) && threadIdx.x == 0) atomicOr(m.unsorted + r, 1u);
         if (__syncthreads_or(weak) && threadIdx.x == 0) atomicOr(m.aweak + r, 1u);
         if (m.amax) {
-            // this block's 256 ranks of each side -> their 1024-entry chunk's maximum
+            // this block's 256 ranks of each side -> their maximum (0 past a side's end)
             __shared__ u64 s_mx[2][kMT / 64];
             u64 xa = i < na ? m.sa[r * m.ce_a + i] : 0ull, xb = i < nb ? m.sb[r * m.ce_b + i] : 0ull;
 #pragma unroll
@@ -408,9 +408,8 @@ __global__ __launch_bounds__(kMT) void k_merge_ranks(LV a, LV b, RK rk, MS m, ui
                 u64 v = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < kMT / 64; ++k) v = s_mx[threadIdx.x][k] > v ? s_mx[threadIdx.x][k] : v;
-                const uint32_t c = blockIdx.x * kMT / 1024u;
-                if (threadIdx.x == 0 && blockIdx.x * kMT < na) atomicMax(m.amax + r * m.nca + c, v);
-                if (threadIdx.x == 1 && blockIdx.x * kMT < nb) atomicMax(m.bmax + r * m.ncb + c, v);
+                if (threadIdx.x == 0 && blockIdx.x < m.nba) m.amax[r * m.nba + blockIdx.x] = v;
+                if (threadIdx.x == 1 && blockIdx.x < m.nbb) m.bmax[r * m.nbb + blockIdx.x] = v;
             }
             __syncthreads();
         }
@@ -797,12 +796,24 @@ __device__ uint32_t stream_run(const u64* X, uint32_t nx, uint32_t p, const u64*
     }
 }
 
+// the largest rank of 1024-entry chunk c: the maximum of its four blocks' maxima
+__device__ __forceinline__ u64 chunk_max(const u64* bm, uint32_t nb, uint32_t c) {
+    u64 v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t q = 4u * c + k;
+        const u64 x = q < nb ? bm[q] : 0ull;
+        v = x > v ? x : v;
+    }
+    return v;
+}
+
 // stream_run<1> (X[p ..] < y: the length of the run from p) with the chunk maxima of X:
 // the rest of p's 1024-entry chunk, then straight to the first later chunk whose maximum
 // reaches y (a ballot over 64 chunk maxima at a time), then that chunk — three memory
 // round trips for a run of any length instead of one per 1024 entries
 __device__ uint32_t stream_run_max(const u64* X, uint32_t nx, uint32_t p, u64 y, const u64* mx,
-                                   uint32_t nc, u64 mreg) {
+                                   uint32_t nbk, uint32_t nc, u64 mreg) {
     if (!mx) return stream_run<1>(X, nx, p, nullptr, 0, 0, y);
     auto scan = [&](uint32_t from, uint32_t to) -> uint32_t {    // first q in [from, to): X >= y
         for (uint32_t b0 = from; b0 < to; b0 += 1024u) {
@@ -827,7 +838,7 @@ __device__ uint32_t stream_run_max(const u64* X, uint32_t nx, uint32_t p, u64 y,
     for (uint32_t c0 = (ce >> 10) & ~63u; c0 < nc; c0 += 64u) {
         // (chunks 0 .. 63: the maxima the walk holds in registers, mreg = chunk lane's)
         const uint32_t c = c0 + lane_id();
-        const u64 v = c0 == 0 ? mreg : (c < nc ? mx[c] : 0ull);
+        const u64 v = c0 == 0 ? mreg : (c < nc ? chunk_max(mx, nbk, c) : 0ull);
         const u64 f = __ballot(c >= (ce >> 10) && c < nc && v >= y);
         if (f) {
             const uint32_t cf = c0 + (uint32_t)__ffsll((long long)f) - 1u;
@@ -850,8 +861,10 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
         A.load(0);
         B.load(0);
         // the first 64 chunk maxima of each side, one per lane (stream_run_max)
-        const u64 mra = m.amax && lane_id() < m.nca ? m.amax[r * m.nca + lane_id()] : 0ull;
-        const u64 mrb = m.bmax && lane_id() < m.ncb ? m.bmax[r * m.ncb + lane_id()] : 0ull;
+        const u64 mra = m.amax && lane_id() < m.nca ? chunk_max(m.amax + r * m.nba, m.nba, lane_id())
+                                                    : 0ull;
+        const u64 mrb = m.bmax && lane_id() < m.ncb ? chunk_max(m.bmax + r * m.nbb, m.nbb, lane_id())
+                                                    : 0ull;
         u64* plan = m.plan + r * ((u64)m.ce_a + m.ce_b);
         uint32_t i = 0, j = 0, o = 0, sx = 0;        // sx: the last single step was B's
         while (i < na && j < nb) {
@@ -877,8 +890,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
                 const uint32_t s = i - A.base;
                 L = win_fail<1>(A, B, s, y) - s;
                 if (L == 256u - s)
-                    L += stream_run_max(SA, na, i + L, y, m.amax ? m.amax + r * m.nca : nullptr, m.nca,
-                                        mra);
+                    L += stream_run_max(SA, na, i + L, y, m.amax ? m.amax + r * m.nba : nullptr, m.nba,
+                                        m.nca, mra);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(i + k) : (u64)(i + k) | ((u64)kNone << 32);
                 i += L;
@@ -887,8 +900,8 @@ __device__ void merge_runs_replica(const LV& a, const LV& b, const MS& m, u64 r)
                 const uint32_t s = j - B.base;
                 L = win_fail<2>(A, B, s, x) - s;
                 if (L == 256u - s)
-                    L += stream_run_max(SB, nb, j + L, x, m.bmax ? m.bmax + r * m.ncb : nullptr, m.ncb,
-                                        mrb);
+                    L += stream_run_max(SB, nb, j + L, x, m.bmax ? m.bmax + r * m.nbb : nullptr, m.nbb,
+                                        m.ncb, mrb);
                 for (uint32_t k = lane_id(); k < L; k += 64)
                     plan[o + k] = MODE == 2 ? (u64)(j + k) | (1ull << 32)
                                             : (u64)kNone | ((u64)(j + k) << 32);
@@ -2652,7 +2665,8 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     // chunk maxima for the one-wave walk's long runs, when an input is known not to ascend
     const bool maxima = (spec || ctx->tune_list_walk == 3) && ctx->tune_list_walk != 1;
     const uint32_t nca = (m.ce_a + 1023u) / 1024u, ncb = (m.ce_b + 1023u) / 1024u;
-    const uint64_t sz_mx = maxima ? R * 8ull * ((uint64_t)nca + ncb) : 0;
+    const uint32_t nba = (m.ce_a + kMT - 1) / kMT, nbb = (m.ce_b + kMT - 1) / kMT;
+    const uint64_t sz_mx = maxima ? R * 8ull * ((uint64_t)nba + nbb) : 0;
     const uint64_t total = sz_sa + sz_sb + sz_pl + sz_tc + 6 * sz_t + sz_c + 5 * sz_r + 72 + sz_fr +
                            sz_mx + 16;
     char* base = static_cast<char*>(lscratch(ctx, total));
@@ -2675,10 +2689,11 @@ static int merge_enqueue(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* a,
     m.ntok = reinterpret_cast<uint32_t*>(take(sz_r));
     if (maxima) {
         m.amax = reinterpret_cast<u64*>(take(sz_mx));
-        m.bmax = m.amax + R * nca;
+        m.bmax = m.amax + R * nba;
         m.nca = nca;
         m.ncb = ncb;
-        LJ_HIP(ctx, hipMemsetAsync(m.amax, 0, sz_mx, ctx->stream));
+        m.nba = nba;
+        m.nbb = nbb;
     }
     SP sp{};
     if (spC) {
