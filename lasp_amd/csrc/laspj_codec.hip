@@ -1437,6 +1437,19 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words
 // = the payload's totals) and, with `offsets`, the payload offsets (k_gset_etf_size's
 // sizes, scanned); k_gset_write_chunks writes each chunk's images from its prefix (bytes,
 // or elements under STRING_EXT), chunk 0 the list header, the last chunk the tail.
+// CELLS: the source is an OR-Set batch's {p, r} cells and an element is present when it
+// has a {Token, false} — value/1's G-Set image written without the value bits in between
+template <bool CELLS>
+__device__ __forceinline__ bool gs_here(const u64* words, uint64_t rep, uint32_t W, uint32_t E,
+                                        uint32_t e) {
+    if (CELLS) {
+        const u64x2 x = reinterpret_cast<const u64x2*>(words)[rep * E + e];
+        return (x.x & ~x.y) != 0;
+    }
+    return (words[rep * W + (e >> 6)] >> (e & 63u)) & 1ull;
+}
+
+template <bool CELLS>
 __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, uint64_t R,
                                                              uint32_t E, uint32_t W, DictView d,
                                                              uint32_t nch, u64x2* co,
@@ -1449,7 +1462,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, u
         u64 by = 0, cn = 0;
         if (i < E) {
             const uint32_t e = d.elem_order[i];
-            if ((w[e >> 6] >> (e & 63u)) & 1ull) {
+            if (gs_here<CELLS>(words, rep, W, E, e)) {
                 const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
                 // as k_gset_etf_size: a present slot without an image is an error
                 if (el == 0 && flag) atomicOr(flag, 1u);
@@ -1457,7 +1470,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, u
                 cn = 1ull + (d.elem_byte[e] == 0 ? (1ull << 32) : 0ull);
             }
         }
-        if (c == 0 && flag)                          // bits of no slot (past E): an error too
+        if (!CELLS && c == 0 && flag)                // bits of no slot (past E): an error too
             for (uint32_t wi = (E >> 6) + threadIdx.x; wi < W; wi += kBlock) {
                 u64 m = w[wi];
                 if (wi == (E >> 6)) m &= ~((1ull << (E & 63u)) - 1ull);
@@ -1497,18 +1510,21 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_scan(u64x2* co, uint64_t 
     if (offsets && threadIdx.x == 0) offsets[R] = run;
 }
 
+// ZERO (CELLS only): the source cells are cleared behind the reads (the NIF's decoded
+// operand: the next call's decoder then needs no memset), whether or not the answer fits
+template <bool CELLS, bool ZERO>
 __global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, uint64_t R,
                                                               uint32_t E, uint32_t W, DictView d,
                                                               int tag, int vers, const u64* offs,
                                                               uint8_t* out, u64 ocap,
                                                               const u64x2* co, uint32_t nch) {
-    if (offs[R] > ocap) return;
+    const bool room = offs[R] <= ocap;
+    if (!ZERO && !room) return;
     __shared__ u64 lds4[kBlock / 64];
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
     for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
         const uint64_t rep = it / nch;
         const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
-        const u64* w = words + rep * W;
         const u64x2 pre = co[rep * (nch + 1ull) + c], all = co[rep * (nch + 1ull) + nch];
         const uint32_t n = (uint32_t)all.y, nb = (uint32_t)(all.y >> 32);
         const bool str = n > 0 && nb == 0 && n < 65536u;
@@ -1518,14 +1534,15 @@ __global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, 
         bool here = false;
         if (i < E) {
             e = d.elem_order[i];
-            here = (w[e >> 6] >> (e & 63u)) & 1ull;
+            here = gs_here<CELLS>(words, rep, W, E, e);
+            if (ZERO) reinterpret_cast<u64x2*>(const_cast<u64*>(words))[rep * E + e] = u64x2{0, 0};
             if (here) el = d.elem_off[e + 1] - d.elem_off[e];
         }
         const u64 sz = here ? (str ? 1u : el) : 0u;
         u64 tot;
         const u64 pos = block_excl_scan64(sz, lds4, &tot);
         // sizes disagree with the offsets: never overrun the payload
-        const bool fits = cursor + tot + (str ? 0u : 1u) <= end;
+        const bool fits = room && cursor + tot + (str ? 0u : 1u) <= end;
         if (fits && here) {
             uint8_t* o = out + cursor + pos;
             const uint8_t* src = d.elem_blob + d.elem_off[e];
@@ -1541,7 +1558,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, 
                 for (uint32_t b = 0; b < el; ++b) o[b] = src[b];
             }
         }
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && room) {
             if (c == 0) write_list_header(out, base, hdr, tag, vers, n == 0 ? 106 : str ? 107 : 108, n);
             if (c == nch - 1 && fits && n && !str && cursor + tot < end) out[cursor + tot] = 106;
         }
@@ -4664,13 +4681,15 @@ static bool gset_split(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
 // the split G-Set size pass: chunk sums and their scan (with `offsets`: the payload
 // offsets too); the chunk table at the scratch's start
 static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
-                               uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks) {
+                               uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks,
+                               bool cells = false) {
     const uint64_t R = b->replicas;
     const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
     if (int s = reserve_scratch(ctx, 16ull * R * (nch + 1ull))) return s;
     u64x2* co = static_cast<u64x2*>(ctx->scratch);
     const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
-    hipLaunchKernelGGL(k_gset_chunk_sizes, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
+    hipLaunchKernelGGL(cells ? k_gset_chunk_sizes<true> : k_gset_chunk_sizes<false>,
+                       dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
                        (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
                        view(d), nch, co, flag);
     hipLaunchKernelGGL(k_gset_chunk_scan, dim3(1), dim3(kBlock), 0, ctx->stream, co, R, nch, hdr,
@@ -4807,6 +4826,31 @@ int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64
     return LASPJ_OK;
 }
 
+bool etf_value_direct(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
+    return gset_split(ctx, R, E) && ctx->tune_etf != 1;
+}
+
+// value/1 of an OR-Set batch as G-Set images, straight from its cells (no value bits in
+// between): the split G-Set size pass and writer reading {p, r}; zero_cells: the cells are
+// cleared behind the writer's reads
+int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const laspj_etf_dict* d,
+                            int tag, int vers, u64* offsets, uint32_t* flag, uint8_t* out,
+                            uint64_t cap_bytes, bool zero_cells) {
+    const uint64_t R = cells->replicas;
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    const u64* co = nullptr;
+    if (int s = gset_chunks_enqueue(ctx, cells, d, hdr, offsets, flag, &co, true)) return s;
+    const uint32_t nch = (cells->elements + kBlock - 1) / kBlock;
+    auto kw = zero_cells ? k_gset_write_chunks<true, true> : k_gset_write_chunks<true, false>;
+    hipLaunchKernelGGL(kw,
+                       dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
+                       dim3(kBlock), 0, ctx->stream, (const u64*)cells->dev, R, cells->elements,
+                       (uint32_t)cells->words_per_replica, view(d), tag, vers, offsets, out,
+                       (u64)cap_bytes, reinterpret_cast<const u64x2*>(co), nch);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
 int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                       int32_t kind, int tag, int vers, const u64* offsets, uint8_t* out,
                       uint64_t cap_bytes, const u64* chunks) {
@@ -4885,7 +4929,7 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
             if (int s = gset_chunks_enqueue(ctx, b, d, tag >= 0 ? 2u : 0u, nullptr, nullptr, &co))
                 return s;
         const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_gset_write_chunks,
+        hipLaunchKernelGGL((k_gset_write_chunks<false, false>),
                            dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
                            dim3(kBlock), 0, ctx->stream, (const u64*)b->dev, R, b->elements,
                            (uint32_t)b->words_per_replica, view(d), tag, vers, offsets, out,

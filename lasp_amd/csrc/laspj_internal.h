@@ -360,6 +360,13 @@ int etf_size_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict*
 int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                       int32_t kind, int tag, int vers, const unsigned long long* offsets,
                       uint8_t* out, uint64_t cap, const unsigned long long* chunks);
+// value/1 of an OR-Set batch written as G-Set images straight from its cells (size pass,
+// offsets and writer; few long payloads: etf_value_direct); zero_cells clears the cells
+// behind the reads (even when the answer does not fit)
+bool etf_value_direct(const laspj_ctx* ctx, uint64_t R, uint32_t E);
+int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const laspj_etf_dict* d,
+                            int tag, int vers, unsigned long long* offsets, uint32_t* flag,
+                            uint8_t* out, uint64_t cap, bool zero_cells);
 
 // laspj_etf_dict_create with per-element token headroom (up to tok_headroom more tokens
 // per element than the widest has) and the host state etf_dict_patch needs

@@ -566,8 +566,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
             // value/1 (lasp_orset.erl:67-73): the elements with a {_, false} token, as the
             // ordset image the G-Set writer gives a bit row (term_to_binary of the keys)
             // (VVALUE has no operand cells: its value bits land where they would start)
-            S->clean_words = 0;
             laspj_batch src = c.op == Op::VALUE ? inb : view(ctx, c.kind, 1, E, c.vars[0]->cells);
+            if (c.kind == LASPJ_KIND_ORSET && etf_value_direct(ctx, n, E)) {
+                // few long answers: written from the cells (no value bits in between), a
+                // decoded operand's cells cleared behind the reads
+                if (int s = etf_value_write_enqueue(ctx, &src, K.etf, -1, 1, dooff, ctx->flag,
+                                                    dopay, ocap, c.op == Op::VALUE))
+                    return s;
+                S->clean_words = c.op == Op::VALUE ? in_words : S->clean_words;
+                break;
+            }
+            S->clean_words = 0;
             LJ_HIP(ctx, launch_orset_value(ctx, &src, cout, false));
             laspj_batch vb = view(ctx, LASPJ_KIND_GSET, n, E, cout);
             const unsigned long long* chunks = nullptr;

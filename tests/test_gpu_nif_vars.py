@@ -90,6 +90,18 @@ def test_gset_nif_answers_match_oracle():
             (OK, _tb(ogset.merge(big_a, big_b)))
         o = [(e, [(b"A" + e.to_bytes(19, "big"), e % 7 == 0)]) for e in range(10000)]
         assert ctx.nif_value(_tb(o)) == (OK, _tb(oorset.value(o)))
+        # (the value pass clears its decoded cells behind it: the next calls decode into
+        # them without a memset)
+        o2 = [(e, [(b"A" + e.to_bytes(19, "big"), e % 5 == 0)]) for e in range(0, 10000, 3)]
+        assert ctx.nif_value(_tb(o2)) == (OK, _tb(oorset.value(o2)))
+        assert ctx.nif_merge(_tb(o2), _tb(o)) == (OK, _tb(oorset.merge(o2, o)))
+        assert ctx.nif_value(_tb(o)) == (OK, _tb(oorset.value(o)))
+        # a resident variable's value/1 twice: its cells stay
+        v = ctx.var("orset")
+        v.write(_tb(o))
+        assert v.value() == (OK, _tb(oorset.value(o)))
+        assert v.value() == (OK, _tb(oorset.value(o)))
+        assert v.read() == (OK, _tb(o))
     finally:
         ctx.close()
 
