@@ -1437,22 +1437,26 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words
 // = the payload's totals) and, with `offsets`, the payload offsets (k_gset_etf_size's
 // sizes, scanned); k_gset_write_chunks writes each chunk's images from its prefix (bytes,
 // or elements under STRING_EXT), chunk 0 the list header, the last chunk the tail.
-// CELLS: the source is an OR-Set batch's {p, r} cells and an element is present when it
-// has a {Token, false} — value/1's G-Set image written without the value bits in between
-template <bool CELLS>
-__device__ __forceinline__ bool gs_here(const u64* words, uint64_t rep, uint32_t W, uint32_t E,
-                                        uint32_t e) {
-    if (CELLS) {
+// the source of the present elements: SRC 0 a G-Set batch's bits; 1 an OR-Set batch's
+// {p, r} cells, an element present when it has a {Token, false} (value/1's G-Set image
+// written without value bits in between); 2 the OR of two G-Set batches' bits (merge/2's
+// answer written without the merged bits in between)
+template <int SRC>
+__device__ __forceinline__ bool gs_here(const u64* words, const u64* words2, uint64_t rep,
+                                        uint32_t W, uint32_t E, uint32_t e) {
+    if (SRC == 1) {
         const u64x2 x = reinterpret_cast<const u64x2*>(words)[rep * E + e];
         return (x.x & ~x.y) != 0;
     }
-    return (words[rep * W + (e >> 6)] >> (e & 63u)) & 1ull;
+    const u64 w = SRC == 2 ? words[rep * W + (e >> 6)] | words2[rep * W + (e >> 6)]
+                           : words[rep * W + (e >> 6)];
+    return (w >> (e & 63u)) & 1ull;
 }
 
-template <bool CELLS>
-__global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, uint64_t R,
-                                                             uint32_t E, uint32_t W, DictView d,
-                                                             uint32_t nch, u64x2* co,
+template <int SRC>
+__global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, const u64* words2,
+                                                             uint64_t R, uint32_t E, uint32_t W,
+                                                             DictView d, uint32_t nch, u64x2* co,
                                                              uint32_t* flag) {
     __shared__ u64 lds4[kBlock / 64];
     for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
@@ -1462,7 +1466,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, u
         u64 by = 0, cn = 0;
         if (i < E) {
             const uint32_t e = d.elem_order[i];
-            if (gs_here<CELLS>(words, rep, W, E, e)) {
+            if (gs_here<SRC>(words, words2, rep, W, E, e)) {
                 const uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
                 // as k_gset_etf_size: a present slot without an image is an error
                 if (el == 0 && flag) atomicOr(flag, 1u);
@@ -1470,9 +1474,9 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, u
                 cn = 1ull + (d.elem_byte[e] == 0 ? (1ull << 32) : 0ull);
             }
         }
-        if (!CELLS && c == 0 && flag)                // bits of no slot (past E): an error too
+        if (SRC != 1 && c == 0 && flag)              // bits of no slot (past E): an error too
             for (uint32_t wi = (E >> 6) + threadIdx.x; wi < W; wi += kBlock) {
-                u64 m = w[wi];
+                u64 m = w[wi] | (SRC == 2 ? words2[rep * W + wi] : 0ull);
                 if (wi == (E >> 6)) m &= ~((1ull << (E & 63u)) - 1ull);
                 if (m) atomicOr(flag, 1u);
             }
@@ -1510,14 +1514,16 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_scan(u64x2* co, uint64_t 
     if (offsets && threadIdx.x == 0) offsets[R] = run;
 }
 
-// ZERO (CELLS only): the source cells are cleared behind the reads (the NIF's decoded
+// ZERO (SRC 1 only): the source cells are cleared behind the reads (the NIF's decoded
 // operand: the next call's decoder then needs no memset), whether or not the answer fits
-template <bool CELLS, bool ZERO>
-__global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, uint64_t R,
-                                                              uint32_t E, uint32_t W, DictView d,
-                                                              int tag, int vers, const u64* offs,
-                                                              uint8_t* out, u64 ocap,
-                                                              const u64x2* co, uint32_t nch) {
+template <int SRC, bool ZERO>
+__global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, const u64* words2,
+                                                              uint64_t R, uint32_t E, uint32_t W,
+                                                              DictView d, int tag, int vers,
+                                                              const u64* offs, uint8_t* out,
+                                                              u64 ocap, const u64x2* co,
+                                                              uint32_t nch) {
+    static_assert(!ZERO || SRC == 1, "only cells are cleared behind the reads");
     const bool room = offs[R] <= ocap;
     if (!ZERO && !room) return;
     __shared__ u64 lds4[kBlock / 64];
@@ -1534,7 +1540,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_write_chunks(const u64* words, 
         bool here = false;
         if (i < E) {
             e = d.elem_order[i];
-            here = gs_here<CELLS>(words, rep, W, E, e);
+            here = gs_here<SRC>(words, words2, rep, W, E, e);
             if (ZERO) reinterpret_cast<u64x2*>(const_cast<u64*>(words))[rep * E + e] = u64x2{0, 0};
             if (here) el = d.elem_off[e + 1] - d.elem_off[e];
         }
@@ -4682,16 +4688,17 @@ static bool gset_split(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
 // offsets too); the chunk table at the scratch's start
 static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                                uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks,
-                               bool cells = false) {
+                               int src = 0, const u64* words2 = nullptr) {
     const uint64_t R = b->replicas;
     const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
     if (int s = reserve_scratch(ctx, 16ull * R * (nch + 1ull))) return s;
     u64x2* co = static_cast<u64x2*>(ctx->scratch);
     const uint64_t sg = std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16);
-    hipLaunchKernelGGL(cells ? k_gset_chunk_sizes<true> : k_gset_chunk_sizes<false>,
-                       dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream,
-                       (const u64*)b->dev, R, b->elements, (uint32_t)b->words_per_replica,
-                       view(d), nch, co, flag);
+    auto ks = src == 1 ? k_gset_chunk_sizes<1> : src == 2 ? k_gset_chunk_sizes<2>
+                                                          : k_gset_chunk_sizes<0>;
+    hipLaunchKernelGGL(ks, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream, (const u64*)b->dev,
+                       words2, R, b->elements, (uint32_t)b->words_per_replica, view(d), nch, co,
+                       flag);
     hipLaunchKernelGGL(k_gset_chunk_scan, dim3(1), dim3(kBlock), 0, ctx->stream, co, R, nch, hdr,
                        offsets);
     LJ_LAUNCHED(ctx);
@@ -4839,14 +4846,36 @@ int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const lasp
     const uint64_t R = cells->replicas;
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
     const u64* co = nullptr;
-    if (int s = gset_chunks_enqueue(ctx, cells, d, hdr, offsets, flag, &co, true)) return s;
+    if (int s = gset_chunks_enqueue(ctx, cells, d, hdr, offsets, flag, &co, 1)) return s;
     const uint32_t nch = (cells->elements + kBlock - 1) / kBlock;
-    auto kw = zero_cells ? k_gset_write_chunks<true, true> : k_gset_write_chunks<true, false>;
+    auto kw = zero_cells ? k_gset_write_chunks<1, true> : k_gset_write_chunks<1, false>;
     hipLaunchKernelGGL(kw,
                        dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
-                       dim3(kBlock), 0, ctx->stream, (const u64*)cells->dev, R, cells->elements,
+                       dim3(kBlock), 0, ctx->stream, (const u64*)cells->dev, (const u64*)nullptr,
+                       R, cells->elements,
                        (uint32_t)cells->words_per_replica, view(d), tag, vers, offsets, out,
                        (u64)cap_bytes, reinterpret_cast<const u64x2*>(co), nch);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+// lasp_gset:merge/2 of few long operand pairs written as images straight from both
+// operands' bits (their OR, never stored): the split size pass and writer
+int etf_gset_merge_write_enqueue(laspj_ctx* ctx, const laspj_batch* lhs, const laspj_batch* rhs,
+                                 const laspj_etf_dict* d, int tag, int vers, u64* offsets,
+                                 uint32_t* flag, uint8_t* out, uint64_t cap_bytes) {
+    const uint64_t R = lhs->replicas;
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    const u64* co = nullptr;
+    if (int s = gset_chunks_enqueue(ctx, lhs, d, hdr, offsets, flag, &co, 2,
+                                    (const u64*)rhs->dev))
+        return s;
+    const uint32_t nch = (lhs->elements + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((k_gset_write_chunks<2, false>),
+                       dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
+                       dim3(kBlock), 0, ctx->stream, (const u64*)lhs->dev, (const u64*)rhs->dev,
+                       R, lhs->elements, (uint32_t)lhs->words_per_replica, view(d), tag, vers,
+                       offsets, out, (u64)cap_bytes, reinterpret_cast<const u64x2*>(co), nch);
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }
@@ -4929,9 +4958,10 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
             if (int s = gset_chunks_enqueue(ctx, b, d, tag >= 0 ? 2u : 0u, nullptr, nullptr, &co))
                 return s;
         const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL((k_gset_write_chunks<false, false>),
+        hipLaunchKernelGGL((k_gset_write_chunks<0, false>),
                            dim3((unsigned)std::min<uint64_t>(R * nch, (uint64_t)ctx->cus * 16)),
-                           dim3(kBlock), 0, ctx->stream, (const u64*)b->dev, R, b->elements,
+                           dim3(kBlock), 0, ctx->stream, (const u64*)b->dev, (const u64*)nullptr,
+                           R, b->elements,
                            (uint32_t)b->words_per_replica, view(d), tag, vers, offsets, out,
                            (u64)cap_bytes, reinterpret_cast<const u64x2*>(co), nch);
     } else

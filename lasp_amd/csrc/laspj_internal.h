@@ -364,6 +364,12 @@ int etf_write_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict
 // offsets and writer; few long payloads: etf_value_direct); zero_cells clears the cells
 // behind the reads (even when the answer does not fit)
 bool etf_value_direct(const laspj_ctx* ctx, uint64_t R, uint32_t E);
+// lasp_gset:merge/2 of few long pairs written from both operands' bits (their OR never
+// stored); the same condition as etf_value_direct
+int etf_gset_merge_write_enqueue(laspj_ctx* ctx, const laspj_batch* lhs, const laspj_batch* rhs,
+                                 const laspj_etf_dict* d, int tag, int vers,
+                                 unsigned long long* offsets, uint32_t* flag, uint8_t* out,
+                                 uint64_t cap);
 int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const laspj_etf_dict* d,
                             int tag, int vers, unsigned long long* offsets, uint32_t* flag,
                             uint8_t* out, uint64_t cap, bool zero_cells);

@@ -543,6 +543,14 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
                 S->clean_words = in_words;
                 break;
             }
+            if (!orset && etf_value_direct(ctx, n, E)) {
+                // few long G-Set answers: written from both operands' bits
+                if (int s = etf_gset_merge_write_enqueue(ctx, &lhs, &rhs, K.etf, -1, 1, dooff,
+                                                         ctx->flag, dopay, ocap))
+                    return s;
+                S->clean_words = 0;
+                break;
+            }
             if (orset && etf_merge_fused(ctx, n, E)) {
                 // the OR fused with the answer's size pass, the operands cleared behind it
                 if (int s = etf_merge_size_enqueue(ctx, lhs.dev, rhs.dev, &ob, K.etf, -1, dooff,

@@ -88,6 +88,9 @@ def test_gset_nif_answers_match_oracle():
         big_a, big_b = list(range(0, 20000, 2)), list(range(0, 30000, 3)) + [Atom("z")]
         assert ctx.nif_merge(_tb(big_a), _tb(big_b), kind="gset") == \
             (OK, _tb(ogset.merge(big_a, big_b)))
+        longs = [(big_a, big_b), (big_b[:3000], big_a[::7]), ([], big_a), (big_b, [])]
+        assert ctx.nif_merge_many([(_tb(x), _tb(y)) for x, y in longs], kind="gset") == \
+            [(OK, _tb(ogset.merge(x, y))) for x, y in longs]
         o = [(e, [(b"A" + e.to_bytes(19, "big"), e % 7 == 0)]) for e in range(10000)]
         assert ctx.nif_value(_tb(o)) == (OK, _tb(oorset.value(o)))
         # (the value pass clears its decoded cells behind it: the next calls decode into
