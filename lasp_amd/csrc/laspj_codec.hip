@@ -3962,9 +3962,10 @@ GsRead gset_reader(const laspj_ctx* ctx) {
 
 // Split G-Set decoder (few long payloads: the NIF's merge operands, one 10k-element
 // ordset each, which one wave resolving 64 elements per round decoded in ~300 us).
-// Pass 1 (k_gset_read_walk): one wave per payload walks the element extents only -- the
+// Pass 1 (k_gset_read_walk): one block per payload walks the element extents only -- the
 // header from the first window, runs of equal-length images 256 at a time in a 32 KiB LDS
-// window, the general walk for other tags, the tail -- and writes every element's offset
+// window (staged by the block's four waves at once), the general walk for other tags, the
+// tail -- and writes every element's offset
 // relative to its payload to eo[offs[r] + r + k] (entry n: the tail's), the element count
 // to en[r] and the walk's status to status[r] (the structural statuses of
 // k_gset_etf_read; a STRING_EXT payload, at most 65535 bytes, is decoded here whole).
@@ -3974,13 +3975,16 @@ GsRead gset_reader(const laspj_ctx* ctx) {
 // status into UNKNOWN_TERM.  Statuses and bits are k_gset_etf_read's.
 constexpr uint32_t kGWinL = 32768;
 
-__global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, const u64* offs,
+__global__ __launch_bounds__(kBlock) void k_gset_read_walk(const uint8_t* payload, const u64* offs,
                                                        uint64_t R, GsTabs g, int tag, int vers,
                                                        u64* words, uint64_t W, int32_t* status,
                                                        uint32_t* eo, uint32_t* en) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kGWinL + 16];
     __shared__ u64 s_h[4];
-    const uint32_t lane = threadIdx.x;
+    // the block's four waves stage each window together (32 KiB in one round of loads);
+    // all four then walk it alike (uniform control, the same ballots) and wave 0 stores
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool w0 = threadIdx.x < 64;
     for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
         const u64 ob = offs[rep], aend = offs[rep + 1];
         const uint8_t* p = payload + ob;
@@ -3993,13 +3997,30 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
             a0 = at0 & ~15ull;
             wl = (uint32_t)min((u64)kGWinL, aend - a0);
             const uint32_t nfull = wl >> 4;
-            wave_copy16<8>(win, payload + a0, nfull, lane);
-            for (uint32_t k = 16 * nfull + lane; k < wl; k += 64) win[k] = payload[a0 + k];
+            __syncthreads();                 // every wave is done with the last window
+            {
+                u32x4* dv = reinterpret_cast<u32x4*>(win);
+                const u32x4* sv = reinterpret_cast<const u32x4*>(payload + a0);
+                for (uint32_t v0 = 0; v0 < nfull; v0 += 8 * kBlock) {
+                    u32x4 t[8];
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) {
+                        const uint32_t v = v0 + j * kBlock + threadIdx.x;
+                        if (v < nfull) t[j] = sv[v];
+                    }
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) {
+                        const uint32_t v = v0 + j * kBlock + threadIdx.x;
+                        if (v < nfull) dv[v] = t[j];
+                    }
+                }
+            }
+            for (uint32_t k = 16 * nfull + threadIdx.x; k < wl; k += kBlock) win[k] = payload[a0 + k];
             __syncthreads();
         };
         stage(ob);
         const uint8_t* hp = win + (ob - a0);
-        if (lane == 0) {
+        if (threadIdx.x == 0) {
             int st = LASPJ_DEC_OK;
             u64 h = 0;
             if (tag >= 0) {
@@ -4049,7 +4070,7 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
                 const uint32_t before = __shfl_up(rk, 1, 64);
                 const bool bad = i < cnt && (slot == kNoSlot ||
                                              (lane ? rk <= before : (have_prev && rk <= prev_rank)));
-                if (i < cnt && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+                if (w0 && i < cnt && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
                 unknown |= __ballot(bad) != 0;
                 const uint32_t last = (uint32_t)((cnt - c0 < 64 ? cnt - c0 : 64) - 1);
                 prev_rank = __shfl(rk, last, 64);
@@ -4088,8 +4109,9 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
                         }
                     }
                     if (run) {
-                        for (uint32_t idx = lane; idx < run; idx += 64)
-                            e[found + k + idx] = (uint32_t)(rel + (u64)idx * L0);
+                        if (w0)
+                            for (uint32_t idx = lane; idx < run; idx += 64)
+                                e[found + k + idx] = (uint32_t)(rel + (u64)idx * L0);
                         o += run * L0;
                         k += run;
                         continue;
@@ -4106,7 +4128,7 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
                         }
                     }
                     if (rel + L > n) { est = LASPJ_DEC_MALFORMED; break; }
-                    if (lane == 0) e[found + k] = (uint32_t)rel;
+                    if (threadIdx.x == 0) e[found + k] = (uint32_t)rel;
                     o += (uint32_t)min(L, (u64)0x7FFFFFFF);
                     ++k;
                     if (o > wl) break;                 // the next element starts past it
@@ -4127,7 +4149,7 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
                 }
             }
         }
-        if (lane == 0) {
+        if (threadIdx.x == 0) {
             status[rep] = st;
             const bool list = st == LASPJ_DEC_OK && lt == 108;
             en[rep] = list ? (uint32_t)found : 0u;
@@ -4135,6 +4157,38 @@ __global__ __launch_bounds__(64) void k_gset_read_walk(const uint8_t* payload, c
         }
         __syncthreads();
     }
+}
+
+// one wave resolves elements [64 c, 64 c + 64) of payload rep (k_gset_read_lookup)
+__device__ __forceinline__ void gs_lookup_chunk(const uint8_t* payload, const u64* offs,
+                                                const GsTabs& g, u64* words, uint64_t W,
+                                                int32_t* status, const uint32_t* eo,
+                                                const uint32_t* en, uint64_t rep, uint64_t c,
+                                                uint32_t lane) {
+    const uint32_t n = en[rep];
+    const u64 ob = offs[rep];
+    const uint8_t* p = payload + ob;
+    const uint32_t* e = eo + ob + rep;
+    u64* w = words + rep * W;
+    const uint64_t k = c * 64 + lane;
+    const bool valid = k < n;
+    uint32_t slot = kNoSlot, rk = 0, prk = 0;
+    if (valid) {
+        const uint32_t o = e[k], L = e[k + 1] - o;
+        if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &slot, &rk);
+    }
+    const bool have_prev = lane == 0 && k > 0;
+    if (have_prev) {
+        const uint32_t o = e[k - 1], L = e[k] - o;
+        uint32_t ps = kNoSlot;
+        if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &ps, &prk);
+    }
+    const uint32_t before = __shfl_up(rk, 1, 64);
+    const bool bad = valid && (slot == kNoSlot ||
+                               (lane ? rk <= before : (have_prev && rk <= prk)));
+    if (valid && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
+    if (__ballot(bad) && lane == 0)
+        atomicCAS(status + rep, (int32_t)LASPJ_DEC_OK, (int32_t)LASPJ_DEC_UNKNOWN_TERM);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gset_read_lookup(const uint8_t* payload,
@@ -4145,34 +4199,28 @@ __global__ __launch_bounds__(kBlock) void k_gset_read_lookup(const uint8_t* payl
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = 0; rep < R; ++rep) {
-        const uint32_t n = en[rep];                  // 0: nothing left to resolve
-        if (n == 0) continue;
-        const u64 ob = offs[rep];
-        const uint8_t* p = payload + ob;
-        const uint32_t* e = eo + ob + rep;
-        u64* w = words + rep * W;
-        for (uint64_t c = wave; c * 64 < n; c += nwaves) {
-            const uint64_t k = c * 64 + lane;
-            const bool valid = k < n;
-            uint32_t slot = kNoSlot, rk = 0, prk = 0;
-            if (valid) {
-                const uint32_t o = e[k], L = e[k + 1] - o;
-                if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &slot, &rk);
-            }
-            const bool have_prev = lane == 0 && k > 0;
-            if (have_prev) {
-                const uint32_t o = e[k - 1], L = e[k] - o;
-                uint32_t ps = kNoSlot;
-                if (L <= 0xFFFFFFu) gs_lookup(g, p + o, L, &ps, &prk);
-            }
-            const uint32_t before = __shfl_up(rk, 1, 64);
-            const bool bad = valid && (slot == kNoSlot ||
-                                       (lane ? rk <= before : (have_prev && rk <= prk)));
-            if (valid && !bad) atomicOr(w + (slot >> 6), 1ull << (slot & 63));
-            if (__ballot(bad) && lane == 0)
-                atomicCAS(status + rep, (int32_t)LASPJ_DEC_OK, (int32_t)LASPJ_DEC_UNKNOWN_TERM);
+    // chunks of 64 elements numbered across the payloads, 64 payloads at a time (lane r's
+    // inclusive sum of their chunk counts), so no wave resolves payloads one after another
+    uint64_t cbase = 0;
+    for (uint64_t r0 = 0; r0 < R; r0 += 64) {
+        const uint64_t r = r0 + lane;
+        uint64_t x = r < R ? (en[r] + 63ull) / 64ull : 0ull;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t y = __shfl_up(x, off, 64);
+            if ((int)lane >= off) x += y;
         }
+        const uint64_t upto = cbase + __shfl(x, 63, 64);
+        // this wave's first chunk at or after cbase
+        uint64_t c = cbase + (wave + nwaves - cbase % nwaves) % nwaves;
+        for (; c < upto; c += nwaves) {
+            const uint64_t rel = c - cbase;
+            const uint32_t lr = (uint32_t)__ffsll((long long)__ballot(x > rel)) - 1u;
+            const uint64_t first = __shfl(x, lr ? lr - 1 : 0, 64);
+            gs_lookup_chunk(payload, offs, g, words, W, status, eo, en, r0 + lr,
+                            rel - (lr ? first : 0ull), lane);
+        }
+        cbase = upto;
     }
 }
 
@@ -4375,7 +4423,7 @@ static int gset_read_split_enqueue(laspj_ctx* ctx, laspj_batch* b, const GsTabs&
     if (int s = reserve_scratch(ctx, eo_bytes + 4ull * R)) return s;
     uint32_t* eo = static_cast<uint32_t*>(ctx->scratch);
     uint32_t* en = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->scratch) + eo_bytes);
-    hipLaunchKernelGGL(k_gset_read_walk, dim3((unsigned)R), dim3(64), 0, ctx->stream, payload,
+    hipLaunchKernelGGL(k_gset_read_walk, dim3((unsigned)R), dim3(kBlock), 0, ctx->stream, payload,
                        offs, R, tabs, tag, vers, reinterpret_cast<u64*>(b->dev),
                        b->words_per_replica, status, eo, en);
     hipLaunchKernelGGL(k_gset_read_lookup, dim3((unsigned)ctx->cus * 2), dim3(kBlock), 0,
