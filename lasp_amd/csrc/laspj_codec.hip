@@ -3666,6 +3666,19 @@ __device__ __forceinline__ u64 gs_elem_len(const uint8_t* buf, uint32_t o, uint3
     }
 }
 
+// a run's candidate test: with T0 (the run's tag when its images have a fixed length:
+// SMALL_INTEGER_EXT 2, INTEGER_EXT 5, NEW_FLOAT_EXT 9 bytes) one byte compare, else the
+// image sized by its header (gs_elem_len's branch tree costs ~100 instructions a lane; a
+// candidate of another tag just ends the run early, the walk's next step takes it)
+__device__ __forceinline__ bool gs_same_len(const uint8_t* buf, uint32_t q, uint32_t lim,
+                                            uint32_t L0, uint32_t T0) {
+    return T0 ? buf[q] == T0 : gs_elem_len(buf, q, lim) == L0;
+}
+
+__device__ __forceinline__ uint32_t gs_fixed_tag(uint32_t t) {
+    return t == 97 || t == 98 || t == 70 ? t : 0u;
+}
+
 // One wave per replica.  LIST_EXT payloads are walked once: the payload is staged into
 // LDS 4 KiB at a time, lane 0 finds the next <= CH element extents in the window
 // (common tags by their headers, anything else by etf_term_len), then every lane takes
@@ -3793,7 +3806,7 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                     // otherwise one element from its header, or the general walk (global
                     // bytes) for other tags and for an element the window does not hold
                     const uint32_t mx = (uint32_t)min(left, (u64)CH);
-                    uint32_t k = 0, o = base, L0 = 0;
+                    uint32_t k = 0, o = base, L0 = 0, T0 = 0;
                     int est = LASPJ_DEC_OK;
                     while (k < mx) {
                         const u64 rel = pos + (o - base);                  // payload offset
@@ -3806,7 +3819,7 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                             const uint32_t q = o + lane * L0;
                             const bool ok = lane < mx - k &&
                                             (TAIL ? q + L0 <= wl : q + 16 <= wl) &&
-                                            gs_elem_len(win, q, wl) == L0 &&
+                                            gs_same_len(win, q, wl, L0, T0) &&
                                             rel + (u64)(lane + 1) * L0 <= n;
                             const u64 msk = __ballot(ok);
                             run = ~msk ? (uint32_t)__ffsll((long long)~msk) - 1u : 64u;
@@ -3822,6 +3835,7 @@ __global__ __launch_bounds__(64) void k_gset_etf_read(const uint8_t* payload, co
                         }
                         u64 L = (TAIL ? o < wl : o + 16 <= wl) ? gs_elem_len(win, o, wl) : 0;
                         L0 = (L && o + L <= wl && L <= 64) ? (uint32_t)L : 0u;
+                        T0 = L0 ? gs_fixed_tag(win[o]) : 0u;
                         if (L == 0 || o + L > wl) {
                             // a tag the window cannot size (or a window that ends at the
                             // payload's end): the general walk over global bytes
@@ -4084,7 +4098,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_read_walk(const uint8_t* payloa
                 if (!(apos >= a0 && apos <= a0 + wl &&
                       (aend <= a0 + wl || a0 + wl - apos >= kGWinL / 2)))
                     stage(apos);
-                uint32_t o = (uint32_t)(apos - a0), L0 = 0;
+                uint32_t o = (uint32_t)(apos - a0), L0 = 0, T0 = 0;
                 u64 k = 0;
                 int est = LASPJ_DEC_OK;
                 while (k < left) {
@@ -4100,7 +4114,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_read_walk(const uint8_t* payloa
                             if (!go) break;
                             const uint32_t idx = j * 64 + lane, q = o + idx * L0;
                             const bool ok = idx < left - k && q + L0 <= wl &&
-                                            gs_elem_len(win, q, wl) == L0 &&
+                                            gs_same_len(win, q, wl, L0, T0) &&
                                             rel + (u64)(idx + 1) * L0 <= n;
                             const u64 msk = __ballot(ok);
                             const uint32_t r = ~msk ? (uint32_t)__ffsll((long long)~msk) - 1u : 64u;
@@ -4118,6 +4132,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_read_walk(const uint8_t* payloa
                     }
                     u64 L = o < wl ? gs_elem_len(win, o, wl) : 0;
                     L0 = (L && o + L <= wl && L <= 64) ? (uint32_t)L : 0u;
+                    T0 = L0 ? gs_fixed_tag(win[o]) : 0u;
                     if (L == 0 || o + L > wl) {
                         if (o + 16 <= wl || k == 0 || a0 + wl >= aend) {
                             L = etf_term_len(p + rel, n - rel);
