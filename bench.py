@@ -456,10 +456,15 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     out["us_bind_nif"] = (time.perf_counter() - t0) * 1e6 / 50
     if (vd.value, st.value) != (0, 1) or var.read() != (0, ref):
         raise RuntimeError("config1: resident bind answered wrongly")
+    # the C call alone, as us_merge_nif (the answer stays in pinned memory for
+    # enif_binary_to_term; var.read() above copied it into a Python bytes to check it)
+    rout, rlen, rvd = C.c_void_p(), C.c_uint64(), C.c_int32()
     t0 = time.perf_counter()
     for _ in range(20):
-        var.read()
+        check(L.laspj_var_etf_read(var.h, C.byref(rout), C.byref(rlen), C.byref(rvd)), ctx.h)
     out["us_read_nif"] = (time.perf_counter() - t0) * 1e6 / 20
+    if rvd.value != 0 or C.string_at(rout, rlen.value) != ref:
+        raise RuntimeError("config1: resident read answered wrongly")
     nm = 32
     vs = [ctx.var("orset") for _ in range(nm)]
     for v in vs:
