@@ -63,3 +63,18 @@ for rep in range(2):
                           "payload_GBps": round(total.value / (ms / 1e3) / 1e9, 1),
                           "exact": ok}), flush=True)
 ctx.set_tuning(_lib.TUNE_ETF_READ, 0)
+# the writer side: laspj_gset_etf_size + laspj_gset_etf_write of the same batch
+if os.environ.get("WRITE", "1") == "1":
+    def enc():
+        _lib.check(L.laspj_gset_etf_size(ctx.h, g.h, d.h, 82, offs.h, _lib.C.byref(total)), ctx.h)
+        _lib.check(L.laspj_gset_etf_write(ctx.h, g.h, d.h, 82, 1, offs.h, out.h), ctx.h)
+    for _ in range(3):
+        enc()
+    ctx.synchronize()
+    e0, e1 = ctx.event(), ctx.event()
+    e0.record()
+    for _ in range(STEPS):
+        enc()
+    e1.record()
+    print(json.dumps({"write_ms": round(e0.elapsed_ms(e1) / STEPS, 4),
+                      "payload_bytes": total.value}), flush=True)
