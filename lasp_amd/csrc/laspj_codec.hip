@@ -1265,33 +1265,74 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
     if (LB) lb_finish(lb, nch, hdr, out);
 }
 
+// One wave per G-Set payload: lanes over element slots, 64 per word, the payload's words
+// held in registers (lane j: word j of each group of 64) and four words' worth of
+// dictionary loads in flight at a time (a loop over each lane's set bits waited for one
+// load per element).  Per payload: element count, image bytes, whether every element is
+// a byte integer (STRING_EXT), and a present slot without an image or a bit past E (the
+// error flag).
+struct GsCount {
+    u64 sum = 0;               // image bytes of the present elements
+    uint32_t n = 0, nb = 0;    // present elements, of them not byte integers
+    bool bad = false;          // a present slot without an image, or a bit past E
+};
+
+template <bool SUM>
+__device__ __forceinline__ GsCount gs_count(const u64* w, uint32_t E, uint32_t W,
+                                            const DictView& d, uint32_t lane) {
+    GsCount r;
+    for (uint32_t g0 = 0; g0 < W; g0 += 64) {
+        const uint32_t wi = g0 + lane;
+        const u64 wv = wi < W ? w[wi] : 0ull;
+        if (wi >= (E >> 6) && wv) {
+            const u64 past = wi == (E >> 6) ? wv & ~((1ull << (E & 63u)) - 1ull) : wv;
+            r.bad |= past != 0;
+        }
+        const uint32_t nw = min(64u, W - g0);
+        for (uint32_t j0 = 0; j0 < nw; j0 += 4) {
+            uint32_t el[4], by[4];
+            bool hr[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t jj = j0 + j;
+                const u64 word = __shfl(wv, (int)min(jj, 63u), 64);
+                const uint32_t e = (g0 + jj) * 64u + lane;
+                hr[j] = jj < nw && e < E && ((word >> lane) & 1ull);
+                el[j] = 0;
+                by[j] = 1;
+                if (hr[j]) {
+                    if (SUM) el[j] = d.elem_off[e + 1] - d.elem_off[e];
+                    by[j] = d.elem_byte[e];
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (hr[j]) {
+                    if (SUM) {
+                        r.bad |= el[j] == 0;
+                        r.sum += el[j];
+                    }
+                    r.nb += by[j] == 0;
+                    ++r.n;
+                }
+        }
+    }
+    return r;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gset_etf_size(const u64* words, uint64_t R,
                                                           uint32_t E, uint32_t W, DictView d,
                                                           uint32_t hdr, u64* sizes,
                                                           uint32_t* flag) {
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64; rep < R;
          rep += waves) {
-        const u64* w = words + rep * W;
-        u64 sum = 0, n = 0;
-        bool bad = false, allbyte = true;
-        for (uint32_t wi = lane; wi < W; wi += 64) {
-            for (u64 m = w[wi]; m; m &= m - 1) {
-                uint32_t e = 64u * wi + (uint32_t)__ffsll((long long)m) - 1u;
-                if (e >= E) { bad = true; break; }
-                uint32_t el = d.elem_off[e + 1] - d.elem_off[e];
-                bad |= el == 0;
-                allbyte &= d.elem_byte[e] != 0;
-                sum += el;
-                ++n;
-            }
-        }
-        sum = wave_sum(sum);
-        n = wave_sum(n);
-        bool any_bad = __ballot(bad) != 0, every_byte = __ballot(!allbyte) == 0;
+        const GsCount c = gs_count<true>(words + rep * W, E, W, d, lane);
+        const u64 sum = wave_sum(c.sum), n = wave_sum((u64)c.n), nb = wave_sum((u64)c.nb);
+        const bool any_bad = __ballot(c.bad) != 0;
         if (lane == 0) {
-            u64 body = n == 0 ? 1u : (every_byte && n < 65536u) ? 3u + n : 5u + sum + 1u;
+            const u64 body = n == 0 ? 1u : (nb == 0 && n < 65536u) ? 3u + n : 5u + sum + 1u;
             sizes[rep] = hdr + 1u + body;
             if (any_bad) atomicOr(flag, 1u);
         }
@@ -1376,22 +1417,20 @@ __global__ __launch_bounds__(kBlock) void k_gset_etf_write_wave(const u64* words
          rep += nwaves) {
         const u64* w = words + rep * W;
         const u64 base = offs[rep], end = offs[rep + 1];
-        uint32_t np = 0, nb = 0;
-        for (uint32_t wi = lane; wi < W; wi += 64) {
-            for (u64 m = w[wi]; m; m &= m - 1) {
-                const uint32_t e = 64u * wi + (uint32_t)__ffsll((long long)m) - 1u;
-                ++np;
-                nb += e >= E || d.elem_byte[e] == 0;
-            }
-        }
-        const uint32_t n = (uint32_t)wave_sum(np), nonbyte = (uint32_t)wave_sum(nb);
+        // (a bit past E counts as not a byte integer, as the size pass refused it)
+        const GsCount cnt = gs_count<false>(w, E, W, d, lane);
+        const uint32_t n = (uint32_t)wave_sum((u64)cnt.n),
+                       nonbyte = (uint32_t)wave_sum((u64)cnt.nb + (cnt.bad ? 1u : 0u));
+        // the payload's words in registers (lane j: word j) when they fit one group
+        const u64 wreg = W <= 64 && lane < W ? w[lane] : 0ull;
         const bool str = n > 0 && nonbyte == 0 && n < 65536u;
         u64 cursor = base + hdr + 1u + (str ? 3u : 5u);
         bool fits = true;
         for (uint32_t c0 = 0; c0 < E && n && fits; c0 += 64) {
             const uint32_t i = c0 + lane;
             const uint32_t e = i < E ? d.elem_order[i] : 0u;
-            const bool here = i < E && ((w[e >> 6] >> (e & 63u)) & 1ull);
+            const u64 word = W <= 64 ? __shfl(wreg, (int)(e >> 6), 64) : w[e >> 6];
+            const bool here = i < E && ((word >> (e & 63u)) & 1ull);
             const uint32_t el = here ? d.elem_off[e + 1] - d.elem_off[e] : 0u;
             const uint32_t sz = here ? (str ? 1u : el) : 0u;
             uint32_t x = sz;
