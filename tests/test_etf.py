@@ -1355,6 +1355,44 @@ def test_gpu_gset_from_binary_split_fuzz():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tagged", [False, True])
+def test_gpu_gset_from_binary_split_edges(tagged):
+    """The split decoder's edges against the one-wave decoder and the host encoder: a batch
+    of few payloads mixing long ones (just past the 4 KiB split threshold, and 30k
+    elements: a walk over several 32 KiB windows) with [], one element, every byte integer
+    (STRING_EXT) and an empty payload; bare and tagged."""
+    import numpy as np
+    from lasp_amd import _lib, engine, etf
+    from lasp_amd.codec import Domain
+    from lasp_amd.orset import context
+    T = etf.DT_GSET_TAG if tagged else -1
+    long_ = list(range(0, 90000, 3))
+    states = [long_, [], [7], list(range(256)), list(range(300, 300 + 820)), long_[::2], []]
+    dom = Domain(element_capacity=1 << 17)
+    dom.encode_gset(states, 1 << 17)
+    E = dom.size + 3
+    ctx = context()
+    d = engine.ETFDict(ctx, E, *dom.etf_arrays(E, tokens=False))
+    enc = lambda st: oetf.to_binary(T, 1, st) if tagged else oetf.term_to_binary(st)  # noqa: E731
+    blobs = [enc(st) for st in states[:-1]] + [b""]
+    assert len(blobs[4]) > 4096 and len(blobs[0]) > 4 * 32768
+    pay, offs = _upload_payloads(ctx, blobs)
+    got = {}
+    for knob in (0, 15):
+        bt = ctx.gset_batch(len(blobs), E)
+        with _read_kernel(ctx, knob):
+            st = bt.etf_decode(d, pay, offs, tag=T, vers=1)
+        got[knob] = (list(st), bt.download())
+    assert got[0][0] == got[15][0]
+    want_st = [_lib.DEC_OK] * (len(blobs) - 1) + [_lib.DEC_INVALID_BINARY if tagged
+                                                  else _lib.DEC_MALFORMED]
+    assert got[0][0] == want_st
+    want = dom.encode_gset(states, E)
+    assert np.array_equal(got[0][1][:-1], want[:-1])
+    assert np.array_equal(got[15][1][:-1], want[:-1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("knob", [0, 11, 13])
 def test_gpu_gset_from_binary_fuzz(knob):
     """2000 corrupted G-Set payloads against the oracle's binary_to_term: payloads it
