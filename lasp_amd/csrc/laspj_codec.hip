@@ -1492,15 +1492,25 @@ __device__ __forceinline__ bool gs_here(const u64* words, const u64* words2, uin
     return (w >> (e & 63u)) & 1ull;
 }
 
+// cj.status (SRC 1: value/1 of decoded operands, the segment decoder's chain check
+// deferred here, ChainJob): the first chunk's block of each payload judges its segment
+// chain (chain_verdict) and stores the decode status
 template <int SRC>
 __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, const u64* words2,
                                                              uint64_t R, uint32_t E, uint32_t W,
                                                              DictView d, uint32_t nch, u64x2* co,
-                                                             uint32_t* flag) {
+                                                             uint32_t* flag, ChainArgs cj) {
     __shared__ u64 lds4[kBlock / 64];
     for (uint64_t it = blockIdx.x; it < R * nch; it += gridDim.x) {
         const uint64_t rep = it / nch;
         const uint32_t c = (uint32_t)(it - rep * nch), i = c * kBlock + threadIdx.x;
+        if (SRC == 1 && cj.status && c == 0 && threadIdx.x < 64) {
+            const u64 base = cj.offs[rep];
+            const int32_t st = chain_verdict(cj.payload, base, cj.offs[rep + 1] - base,
+                                             cj.segbase[rep], cj.segbase[rep + 1] - cj.segbase[rep],
+                                             cj.S, cj.res, threadIdx.x);
+            if (threadIdx.x == 0) cj.status[rep] = st;
+        }
         const u64* w = words + rep * W;
         u64 by = 0, cn = 0;
         if (i < E) {
@@ -4790,7 +4800,13 @@ static bool gset_split(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
 // offsets too); the chunk table at the scratch's start
 static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj_etf_dict* d,
                                uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks,
-                               int src = 0, const u64* words2 = nullptr) {
+                               int src = 0, const u64* words2 = nullptr,
+                               const ChainJob* chain = nullptr) {
+    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    if (chain && chain->armed)
+        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
+                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
+                       chain->S};
     const uint64_t R = b->replicas;
     const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
     if (int s = reserve_scratch(ctx, 16ull * R * (nch + 1ull))) return s;
@@ -4800,7 +4816,7 @@ static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj
                                                           : k_gset_chunk_sizes<0>;
     hipLaunchKernelGGL(ks, dim3((unsigned)sg), dim3(kBlock), 0, ctx->stream, (const u64*)b->dev,
                        words2, R, b->elements, (uint32_t)b->words_per_replica, view(d), nch, co,
-                       flag);
+                       flag, cj);
     hipLaunchKernelGGL(k_gset_chunk_scan, dim3(1), dim3(kBlock), 0, ctx->stream, co, R, nch, hdr,
                        offsets);
     LJ_LAUNCHED(ctx);
@@ -4944,11 +4960,12 @@ bool etf_value_direct(const laspj_ctx* ctx, uint64_t R, uint32_t E) {
 // cleared behind the writer's reads
 int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const laspj_etf_dict* d,
                             int tag, int vers, u64* offsets, uint32_t* flag, uint8_t* out,
-                            uint64_t cap_bytes, bool zero_cells) {
+                            uint64_t cap_bytes, bool zero_cells, const ChainJob* chain) {
     const uint64_t R = cells->replicas;
     const uint32_t hdr = tag >= 0 ? 2u : 0u;
     const u64* co = nullptr;
-    if (int s = gset_chunks_enqueue(ctx, cells, d, hdr, offsets, flag, &co, 1)) return s;
+    if (int s = gset_chunks_enqueue(ctx, cells, d, hdr, offsets, flag, &co, 1, nullptr, chain))
+        return s;
     const uint32_t nch = (cells->elements + kBlock - 1) / kBlock;
     auto kw = zero_cells ? k_gset_write_chunks<1, true> : k_gset_write_chunks<1, false>;
     hipLaunchKernelGGL(kw,

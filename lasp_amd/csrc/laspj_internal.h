@@ -370,9 +370,11 @@ int etf_gset_merge_write_enqueue(laspj_ctx* ctx, const laspj_batch* lhs, const l
                                  const laspj_etf_dict* d, int tag, int vers,
                                  unsigned long long* offsets, uint32_t* flag, uint8_t* out,
                                  uint64_t cap);
+// chain: the segment decoder's chain check deferred onto the size pass (as the merge's)
 int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const laspj_etf_dict* d,
                             int tag, int vers, unsigned long long* offsets, uint32_t* flag,
-                            uint8_t* out, uint64_t cap, bool zero_cells);
+                            uint8_t* out, uint64_t cap, bool zero_cells,
+                            const ChainJob* chain = nullptr);
 
 // laspj_etf_dict_create with per-element token headroom (up to tok_headroom more tokens
 // per element than the widest has) and the host state etf_dict_patch needs

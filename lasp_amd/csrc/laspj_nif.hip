@@ -376,7 +376,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
     // MERGE: the segment decoder's chain check rides on the join's launch (ChainJob), its
     // per-segment results in a device area of their own after the in region
     const bool defer = dec && orset && plan.nseg && !c.no_defer &&
-                       ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op);
+                       ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op ||
+                        (c.op == Op::VALUE && etf_value_direct(ctx, n, E)));
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
     // device statuses of the variable calls (their kernel reads them)
     const uint64_t vst_bytes = var_op ? al(4ull * m, 256) : 0;
@@ -579,7 +580,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
                 // few long answers: written from the cells (no value bits in between), a
                 // decoded operand's cells cleared behind the reads
                 if (int s = etf_value_write_enqueue(ctx, &src, K.etf, -1, 1, dooff, ctx->flag,
-                                                    dopay, ocap, c.op == Op::VALUE))
+                                                    dopay, ocap, c.op == Op::VALUE, &cjob))
                     return s;
                 S->clean_words = c.op == Op::VALUE ? in_words : S->clean_words;
                 break;

@@ -314,6 +314,11 @@ def test_nif_false_element_headers_in_tokens_take_the_serial_pass():
         s1 = ctx.nif_stats()
         assert s1["chain_redo_passes"] > s0["chain_redo_passes"]
         assert s1["registrations"] == s0["registrations"]
+        # value/1 of such an operand: its chain check rides on the answer's size pass, and
+        # breaks the same way
+        assert ctx.nif_value(_tb(a)) == (OK, _tb(oorset.value(a)))
+        s1v = ctx.nif_stats()
+        assert s1v["chain_redo_passes"] > s1["chain_redo_passes"]
         ctx.set_tuning(_lib.TUNE_ETF_SEG, 0)
         big = [(e, [(bytes([e % 251, e // 251]) * 10, False)]) for e in range(10_000)]
         other = [(e, list(ts)) for e, ts in big]
