@@ -484,8 +484,95 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     out["us_bind_nif_many_per_bind"] = (time.perf_counter() - t0) * 1e6 / (5 * nm)
     if any(vds[k] or sts[k] != 1 for k in range(nm)):
         raise RuntimeError("config1: bind_many answered wrongly")
-    # 16 schedulers: a context and a variable each, binding B in a loop
-    nthreads, per = 16, 60
+    # update/4 on the resident variable (laspj_var_etf_update, lasp_core.erl:283-287): {add, E}
+    # of a known element mints a token (unique/1), registers it in the variable's namespace,
+    # patches the device images and sets the token's bit — the update ships only the op
+    from oracle import etf as oetf             # (the op images are built untimed)
+    from oracle.terms import Atom
+    res, vd2, nmint = C.c_int32(), C.c_int32(), C.c_uint32()
+    eimg, elen, mint = C.c_void_p(), C.c_uint64(), C.c_void_p()
+    uv = ctx.var("orset")
+    uv.write(ref)
+    add_ops = [oetf.term_to_binary((Atom("add"), e)) for e in range(0, 10_000, 97)]
+    rm_ops = [oetf.term_to_binary((Atom("remove"), e)) for e in range(5, 10_000, 89)]
+
+    def vupdate(img):
+        check(L.laspj_var_etf_update(uv.h, img, len(img), C.byref(res), C.byref(eimg),
+                                     C.byref(elen), C.byref(mint), C.byref(nmint), C.byref(vd2)),
+              ctx.h)
+        if vd2.value != 0 or res.value != 0:
+            raise RuntimeError("config1: update/4 answered wrongly")
+
+    stage_keys = ("device_passes", "registrations", "image_rebuilds", "image_patches",
+                  "ns_register", "ns_rebuild", "ns_stage_enqueue", "ns_device_wait")
+
+    def stats_delta(a, b, k):
+        return {x: (b[x] - a[x]) / k if x.startswith("ns_") else b[x] - a[x] for x in stage_keys}
+
+    vupdate(add_ops[0])
+    ctx.synchronize()
+    su0 = ctx.nif_stats()
+    t0 = time.perf_counter()
+    for img in add_ops[1:51]:
+        vupdate(img)
+    ctx.synchronize()
+    out["us_update_nif"] = (time.perf_counter() - t0) * 1e6 / 50
+    out["update_stages"] = stats_delta(su0, ctx.nif_stats(), 50)
+    t0 = time.perf_counter()
+    for img in rm_ops[:50]:
+        vupdate(img)
+    out["us_update_nif_remove"] = (time.perf_counter() - t0) * 1e6 / 50
+    # the bind that meets a freshly minted token: a replica in the variable's namespace
+    # (laspj_var_create_replica) binds the updated state — the token is known, one device
+    # pass; a variable of its own namespace (another node's replica) binds it — a token its
+    # dictionary has not seen: registration and a second pass
+    rep = uv.replica()
+    far = ctx.var("orset")
+    _, img0 = uv.read()
+    rep.write(img0)
+    far.write(img0)
+    times_rep, times_far = [], []
+    sc0 = ctx.nif_stats()
+    for k in range(10):
+        vupdate(add_ops[60 + k])
+        _, img = uv.read()
+        for v, acc in ((rep, times_rep), (far, times_far)):
+            t0 = time.perf_counter()
+            check(L.laspj_var_etf_bind(v.h, img, len(img), C.byref(st), C.byref(vd)), ctx.h)
+            acc.append((time.perf_counter() - t0) * 1e6)
+            if (vd.value, st.value) != (0, 1):
+                raise RuntimeError("config1: the bind of an updated state answered wrongly")
+    sc1 = ctx.nif_stats()
+    out["new_token_stages"] = stats_delta(sc0, sc1, 10)
+    out["new_token_samples_us"] = {"replica": [round(x, 1) for x in times_rep],
+                                   "far": [round(x, 1) for x in times_far]}
+    if rep.read() != uv.read() or far.read() != uv.read():
+        raise RuntimeError("config1: replicas did not converge")
+    out["us_bind_nif_replica_update"] = sorted(times_rep)[len(times_rep) // 2]
+    out["us_bind_nif_new_token"] = sorted(times_far)[len(times_far) // 2]
+    out["bind_new_token_passes"] = (sc1["device_passes"] - sc0["device_passes"]) / 10
+    for v in (rep, far, uv):
+        v.close()
+    # schedulers: a context and a variable each, binding B in a loop (4 = the box's
+    # hardware queues per process, GPU_MAX_HW_QUEUES; 16 = one per BEAM scheduler)
+    for nthreads in (4, 16):
+        out[f"bind_{nthreads}ctx"] = _bind_threads(ctx, nthreads, 60, ref, pb)
+    out["resident"] = ("Value0 = A ⊔ B resident (laspj_var); per bind: the %d-byte image of B "
+                       "in, decode + `=:=` + merge on the device, the status out" % len(pb))
+    for v in vs:
+        v.close()
+    var.close()
+    return out
+
+
+def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes):
+    """nthreads BEAM schedulers, each with a context and a resident variable holding
+    A ⊔ B, binding B `per` times at once (lasp_vnode.erl:213-237: concurrent callers)."""
+    import ctypes as C
+    import threading
+    from lasp_amd._lib import check
+    from lasp_amd import engine
+    L = ctx.L
     ready, errs, spans = threading.Barrier(nthreads + 1), [], []
 
     def worker():
@@ -521,18 +608,107 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     for t in ths:
         t.join(timeout=300)
     if errs or len(spans) != nthreads:
-        raise RuntimeError(f"config1: 16-context binds failed: {errs[:3]}")
+        raise RuntimeError(f"config1: {nthreads}-context binds failed: {errs[:3]}")
     wall = max(b for _a, b in spans) - min(a for a, _b in spans)
-    out["bind_16ctx"] = {"contexts": nthreads, "binds": nthreads * per,
-                         "us_per_bind": wall * 1e6 / (nthreads * per),
-                         "binds_per_s": nthreads * per / wall,
-                         "merged_elements_per_s": nthreads * per * 10_000 / wall}
-    out["resident"] = ("Value0 = A ⊔ B resident (laspj_var); per bind: the %d-byte image of B "
-                       "in, decode + `=:=` + merge on the device, the status out" % len(pb))
-    for v in vs:
-        v.close()
-    var.close()
-    return out
+    return {"contexts": nthreads, "binds": nthreads * per,
+            "us_per_bind": wall * 1e6 / (nthreads * per),
+            "binds_per_s": nthreads * per / wall,
+            "merged_elements_per_s": nthreads * per * 10_000 / wall,
+            "pcie_GBps": nthreads * per * len(pb) / wall / 1e9}
+
+
+def steady_leg(ctx, nvars: int = 32, steps: int = 200):
+    """The drop-in's steady state (lasp_core.erl:283-312, lasp_update_fsm.erl:174-216): two
+    nodes, each a context holding `nvars` resident variables (a vnode's store), one replica
+    of every variable on each.  Each step picks a variable and a node: update/4 {add, E}
+    there (a token minted), the updated state read out (what gossip ships), bound into the
+    other node's replica (a token that node has not seen), then a threshold read there.
+    Every 10th step also removes an element (update {remove, E}).  Config 1's shape: 10k
+    elements, 1-2 tokens each.  Reported per op and per step, with the fallback / reset
+    counts and the bytes that crossed PCIe."""
+    import ctypes as C
+    import numpy as np
+    from lasp_amd._lib import check
+    from lasp_amd import engine, etf
+    from oracle import etf as oetf              # op images, built untimed
+    from oracle.terms import Atom
+    L = ctx.L
+    n = 10_000
+    nodes = [ctx, engine.Context(ctx.device)]
+    base = [(e, [(b"S" + e.to_bytes(19, "big"), e % 10 == 0)]) for e in range(n)]
+    img0 = etf.term_to_binary(base)
+    vs = [[c.var("orset") for _ in range(nvars)] for c in nodes]
+    for row in vs:
+        for v in row:
+            if v.write(img0) != 0:
+                raise RuntimeError("steady: write fell back")
+    rng = np.random.default_rng(11)
+    plan = [(int(rng.integers(nvars)), int(rng.integers(2)), int(rng.integers(n)), k % 10 == 9)
+            for k in range(steps)]
+    ops = {}
+    for _i, _nd, e, rm in plan:
+        ops[(e, rm)] = oetf.term_to_binary((Atom("remove" if rm else "add"), e))
+    th = etf.term_to_binary(base[:50])
+    res, vd, nm = C.c_int32(), C.c_int32(), C.c_uint32()
+    ei, el, mi = C.c_void_p(), C.c_uint64(), C.c_void_p()
+    rp, rl = C.c_void_p(), C.c_uint64()
+    st = C.c_int32()
+    t_upd = t_read = t_bind = t_th = 0.0
+    shipped = 0
+    s0 = [c.nif_stats() for c in nodes]
+    t_all = time.perf_counter()
+    for i, nd, e, rm in plan:
+        src, dst = vs[nd][i], vs[1 - nd][i]
+        op = ops[(e, rm)]
+        t0 = time.perf_counter()
+        check(L.laspj_var_etf_update(src.h, op, len(op), C.byref(res), C.byref(ei), C.byref(el),
+                                     C.byref(mi), C.byref(nm), C.byref(vd)), nodes[nd].h)
+        t1 = time.perf_counter()
+        if vd.value != 0:
+            raise RuntimeError("steady: update fell back")
+        check(L.laspj_var_etf_read(src.h, C.byref(rp), C.byref(rl), C.byref(vd)), nodes[nd].h)
+        img = C.string_at(rp, rl.value)          # (the gossip message: copied out)
+        t2 = time.perf_counter()
+        check(L.laspj_var_etf_bind(dst.h, img, len(img), C.byref(st), C.byref(vd)),
+              nodes[1 - nd].h)
+        t3 = time.perf_counter()
+        if vd.value != 0:
+            raise RuntimeError("steady: bind fell back")
+        check(L.laspj_var_etf_threshold(dst.h, th, len(th), 0, C.byref(res), C.byref(vd)),
+              nodes[1 - nd].h)
+        t4 = time.perf_counter()
+        if vd.value != 0 or res.value != 1:
+            raise RuntimeError("steady: threshold answered wrongly")
+        t_upd += t1 - t0
+        t_read += t2 - t1
+        t_bind += t3 - t2
+        t_th += t4 - t3
+        shipped += 2 * len(img) + len(op) + len(th)
+    wall = time.perf_counter() - t_all
+    s1 = [c.nif_stats() for c in nodes]
+    d = {k: sum(s1[j][k] - s0[j][k] for j in range(2))
+         for k in ("device_passes", "registrations", "dict_resets", "fallbacks", "vars_spilled",
+                   "image_rebuilds", "image_patches")}
+    # the replicas converge: every variable's two replicas read alike after a final exchange
+    for i in range(nvars):
+        _v, a = vs[0][i].read()
+        vs[1][i].bind(a)
+        _v, b = vs[1][i].read()
+        vs[0][i].bind(b)
+        if vs[0][i].read() != vs[1][i].read():
+            raise RuntimeError(f"steady: variable {i} did not converge")
+    for row in vs:
+        for v in row:
+            v.close()
+    nodes[1].close()
+    return {"workload": (f"2 nodes x {nvars} resident variables (10k elements each, config 1's "
+                         f"shape); {steps} steps of update/4 (a minted token; 1 in 10 a "
+                         f"remove) -> read (gossip) -> bind on the other node -> threshold"),
+            "us_per_step": wall * 1e6 / steps, "us_update": t_upd * 1e6 / steps,
+            "us_read": t_read * 1e6 / steps, "us_bind": t_bind * 1e6 / steps,
+            "us_threshold": t_th * 1e6 / steps,
+            "device_passes_per_step": d["device_passes"] / steps,
+            "pcie_GBps": shipped / wall / 1e9, "counts": d}
 
 
 def wide_leg(ctx, args):
@@ -726,7 +902,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
-    cfg1 = config1_gpu(ctx) if rank == 0 else None
+    # the per-call legs run at N = 1 only: with more ranks, rank 0's host-side legs would
+    # outlast the other ranks' anti-entropy guard (--ae-timeout) while they wait for it
+    cfg1 = config1_gpu(ctx) if rank == 0 and world == 1 else None
+    if cfg1 is not None:
+        cfg1["steady"] = steady_leg(ctx)
     del a, b, c                          # free the 192 GiB of join operands first
     ctx.synchronize()
     wide = wide_leg(ctx, args) if rank == 0 and world == 1 and args.wide_replicas else None

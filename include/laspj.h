@@ -816,7 +816,10 @@ int laspj_list_fold(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* src,
  * the body passes it (the keys; a G-Set element, or the first component of a 2-tuple
  * element, lasp_core.erl:648-655, 688-695) in first-appearance order as a list image, and
  * the map / filter / fold entry points take the image of the list of its results in that
- * order (LASPJ_E_INVAL when the counts differ; fold: each result a list). */
+ * order (LASPJ_E_INVAL when the counts differ; fold: each result a list).  The fun is
+ * taken to be pure: it is called once per distinct argument, where the reference's bodies
+ * call it once per entry (lasp_core.erl:466-476, 641-709) — the same results for a pure fun,
+ * fewer calls (and side effects) when keys repeat. */
 /* the fun's distinct arguments (map/6, filter/6, fold/6 bodies) */
 int laspj_list_etf_args(laspj_ctx* ctx, int32_t kind, const uint8_t* v, uint64_t nv,
                         const uint8_t** out, uint64_t* out_len, int32_t* verdict);
@@ -961,26 +964,39 @@ int laspj_gset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
 
 /* ------------------------------------------------------------------ resident variables */
 /* `#dv.value` (include/lasp.hrl:60-63) kept on the device between calls.  A variable is
- * one OR-Set or G-Set value over its context's dictionary of that kind; lasp_core:bind/3
- * (lasp_core.erl:291-312) then ships only the incoming `Value` — its image is decoded on
- * the device, `Value0 =:= Value` and merge/2 decided against the resident cells by one
- * kernel, and only the status comes back; the value is encoded when it is read.
+ * one OR-Set or G-Set value over the dictionary of its own token namespace;
+ * lasp_core:bind/3 (lasp_core.erl:291-312) then ships only the incoming `Value` — its
+ * image is decoded on the device, `Value0 =:= Value` and merge/2 decided against the
+ * resident cells by one kernel, and only the status comes back; update/4 (:283-287) runs on
+ * the cells without shipping anything but the operation; the value is encoded when it is
+ * read.
+ *
+ * Namespaces: each variable's dictionary holds the terms of its own value (as each
+ * #dv.value is independent), so variables never share an element's 64 token slots — a
+ * vnode's many variables holding the same element do not crowd one another out.  Replicas
+ * of one variable held in one context (laspj_var_create_replica) share a namespace: the
+ * tokens one mints are known to the others, so binding a replica's state decodes in one
+ * pass.
  *
  * Ownership: the NIF wraps a laspj_var in an enif_alloc_resource
  * whose destructor calls laspj_var_destroy; the resource keeps its context's resource
- * alive (enif_keep_resource), since a variable belongs to one context (its dictionary and
- * device memory) and every call on it is serialised by that context, from any scheduler.
+ * alive (enif_keep_resource), since a variable belongs to one context (its device memory)
+ * and every call on it is serialised by that context, from any scheduler.
  *
- * A value the columnar form does not hold (verdict FALLBACK of laspj_var_etf_write) is
- * kept as its image on the host: laspj_var_etf_read answers that image, and bind /
- * threshold / value answer FALLBACK — the NIF runs the reference's clause over the read
- * term and stores the outcome with laspj_var_etf_write.  A dictionary reset (an element
- * whose 64 token slots are used up) writes every resident variable of the context out to
- * its image first; each is decoded again on its next call. */
+ * A value the columnar form does not hold (verdict FALLBACK of laspj_var_etf_write: an
+ * element with more than 64 tokens, `==`-equal terms under two images) is kept as its
+ * image on the host: laspj_var_etf_read answers that image, and bind / update / threshold /
+ * value answer FALLBACK — the NIF runs the reference's clause over the read term and
+ * stores the outcome with laspj_var_etf_write.  A namespace whose element slots run out
+ * (a write of a value unlike the namespace's earlier ones) starts a fresh dictionary and
+ * writes its resident variables out to their images first; each is decoded again on its
+ * next call. */
 typedef struct laspj_var laspj_var;
 /* declare/3 (lasp_core.erl:208-218): a variable holding Type:new() = [] (kind
- * LASPJ_KIND_ORSET or LASPJ_KIND_GSET) */
+ * LASPJ_KIND_ORSET or LASPJ_KIND_GSET), in a namespace of its own */
 int laspj_var_create(laspj_ctx* ctx, int32_t kind, laspj_var** out);
+/* another replica of `peer`'s variable (its kind, context and namespace), holding new() */
+int laspj_var_create_replica(laspj_var* peer, laspj_var** out);
 int laspj_var_destroy(laspj_var* var);
 #define LASPJ_BIND_NOOP    0
 #define LASPJ_BIND_WRITTEN 1
@@ -1011,6 +1027,32 @@ int laspj_var_etf_threshold(laspj_var* var, const uint8_t* threshold, uint64_t n
 /* 1 when the value (#dv.value, include/lasp.hrl:60-63) is on the device, 0 when it is
  * held as an image */
 int laspj_var_resident(const laspj_var* var, int32_t* resident);
+/* lasp_core:update/4 (lasp_core.erl:283-287) on the variable: {ok, Value} =
+ * Type:update(Op, Actor, Value0) (lasp_orset.erl:99-117, 222-262; lasp_gset.erl:84-88)
+ * applied to the resident cells, then bind/3 of Value, which a successful update always
+ * inflates — the variable := Value.  op: term_to_binary/1 of Op — OR-Sets {add, E},
+ * {add_by_token, T, E}, {add_all, Es}, {remove, E}, {remove_all, Es}, {update, Ops};
+ * G-Sets {add, E}, {add_all, Es}.  Actor is not an argument: neither type's update reads it
+ * (unique/1 ignores it, lasp_orset.erl:261-262).  {add, E} / {add_all, Es} mint each
+ * token as unique/1 does (20 random bytes, crypto:strong_rand_bytes(20)) from the kernel's
+ * CSPRNG; *minted (optional) points at the nminted tokens' bytes, 20 each, in op order
+ * (valid until the context's next call).  The new terms join the variable's namespace and
+ * its device images at once (a token on a known element is patched in place).
+ * *result: LASPJ_UPDATE_OK, or LASPJ_UPDATE_NOT_PRESENT — the reference's
+ * {error, {precondition, {not_present, E}}} (:232-241: a remove of an absent element; the
+ * whole call is void, as remove_elems / apply_ops return the error and not a state), which
+ * lasp_core:update/4's `{ok, Value} =` turns into a badmatch — with *err_elem / *err_len
+ * (optional) the image of E (valid until the context's next call).  An update that only
+ * adds returns once its kernel is enqueued; one that removes waits for the statuses.
+ * verdict FALLBACK: an Op no clause of the reference's update/3 takes as written (it
+ * raises), a term `==` to one the namespace holds under another image, an element's 65th
+ * token, a host-held variable — the NIF runs the reference's update on the read value and
+ * writes the result. */
+#define LASPJ_UPDATE_OK          0
+#define LASPJ_UPDATE_NOT_PRESENT 1
+int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_t* result,
+                         const uint8_t** err_elem, uint64_t* err_len, const uint8_t** minted,
+                         uint32_t* nminted, int32_t* verdict);
 
 /* counters of this context's NIF path: [0] calls, [1] device passes, [2] dictionary
  * registrations, [3] dictionary resets, [4] device image rebuilds, [5] host-encoded passes

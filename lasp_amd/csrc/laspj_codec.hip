@@ -3109,11 +3109,10 @@ template <bool SMALL>
 __device__ int32_t decode_replica(const uint8_t* payload, u64 total, const u64* offs,
                                   uint64_t rep, uint32_t E, const DictView& d,
                                   const ReadTabs& tabs, const HdrHash& hh, int tag, int vers,
-                                  u64x2* cells, bool clear, ReadLds& L, ReadLdsX* X,
+                                  u64x2* c, bool clear, ReadLds& L, ReadLdsX* X,
                                   uint32_t lane, Cases cs) {
     const uint32_t RK = d.tok_max;
     const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
-    u64x2* c = cells + rep * E;
     if (clear)
         for (uint32_t e = lane; e < E; e += 64) c[e] = u64x2{0, 0};
     PWin w{L.win, payload, total, aend, base, 0, (uint32_t)min(aend - base, (u64)0x7FFFFFFF)};
@@ -3164,7 +3163,8 @@ __global__ __launch_bounds__(kBlock, SMALL ? 5 : 4) void k_orset_etf_read(const 
     for (uint64_t i = (uint64_t)blockIdx.x * (kBlock / 64) + wave; i < count; i += nwaves) {
         const uint64_t rep = redo ? (uint64_t)ufl32(redo[1 + i]) : i;
         const int32_t st = decode_replica<SMALL>(payload, total, offs, rep, E, d, tabs, hh, tag,
-                                                 vers, cells, redo != nullptr, L, X, lane, cs);
+                                                 vers, cells + rep * E, redo != nullptr, L, X,
+                                                 lane, cs);
         if (lane == 0) status[rep] = st;
     }
 }
@@ -3366,30 +3366,19 @@ __device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint
                                                                               : kDecRedo;
 }
 
+// segment s of replica rep's payload (cells c: the replica's) decoded by one wave: its
+// SegRes into *out
 template <bool SMALL>
-__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
-    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
-    ReadTabs tabs, int tag, int vers, u64x2* cells, const uint32_t* segbase, uint64_t nseg,
-    uint32_t S, HdrHash hh, SegRes* res) {
-    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+__device__ __forceinline__ void seg_decode(const uint8_t* payload, u64 total, const u64* offs,
+                                           uint64_t rep, uint32_t s, uint32_t E,
+                                           const DictView& d, const ReadTabs& tabs,
+                                           const HdrHash& hh, int tag, int vers, u64x2* c,
+                                           uint32_t S, SegRes* res_out, ReadLds& L,
+                                           uint32_t lane, const Cases& cs) {
     const uint32_t RK = d.tok_max;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    const Cases cs = lane_cases(lane);
-    ReadLds& L = lds[wave];
-    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
-        // the replica: the last r with segbase[r] <= g
-        uint64_t lo = 0, hi = R;
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (ufl32(segbase[mid]) <= g) lo = mid;
-            else hi = mid;
-        }
-        const uint64_t rep = lo;
-        const uint32_t s = (uint32_t)(g - ufl32(segbase[rep]));
+    {
         const u64 base = ufl(offs[rep]), aend = ufl(offs[rep + 1]);
         const uint32_t len = (uint32_t)min(aend - base, (u64)0x7FFFFFFF);
-        u64x2* c = cells + rep * E;
         PWin w{L.win, payload, total, aend, base, 0, len};
         SegRes out{LASPJ_DEC_OK, kSegNone, kSegNone, 0, -1, -1, 0, 0};
         const uint32_t send = (uint32_t)min((u64)(s + 1) * S, (u64)len);
@@ -3451,7 +3440,36 @@ __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
             out.end = (uint32_t)(w.lo + pc - base);
             out.rlast = (int32_t)prev;
         }
-        if (lane == 0) res[g] = out;
+        if (lane == 0) *res_out = out;
+    }
+}
+
+// the replica whose segments hold global segment g: the last r with segbase[r] <= g
+__device__ __forceinline__ uint64_t seg_replica(const uint32_t* segbase, uint64_t R, uint64_t g) {
+    uint64_t lo = 0, hi = R;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (ufl32(segbase[mid]) <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
+    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
+    ReadTabs tabs, int tag, int vers, u64x2* cells, const uint32_t* segbase, uint64_t nseg,
+    uint32_t S, HdrHash hh, SegRes* res) {
+    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const Cases cs = lane_cases(lane);
+    ReadLds& L = lds[wave];
+    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
+        const uint64_t rep = seg_replica(segbase, R, g);
+        const uint32_t s = (uint32_t)(g - ufl32(segbase[rep]));
+        seg_decode<SMALL>(payload, total, offs, rep, s, E, d, tabs, hh, tag, vers,
+                          cells + rep * E, S, res + g, L, lane, cs);
     }
 }
 
@@ -3486,13 +3504,105 @@ __global__ __launch_bounds__(64) void k_etf_read_chain(const uint8_t* payload, u
             if (lane == 0) status[r] = LASPJ_DEC_OK;
         } else if (cells) {
             const int32_t st = decode_replica<SMALL>(payload, total, offs, r, E, d, tabs, hh, tag,
-                                                     vers, cells, true, L, nullptr, lane, cs);
+                                                     vers, cells + r * E, true, L, nullptr, lane,
+                                                     cs);
             if (lane == 0) status[r] = st;
         } else if (lane == 0) {
             status[r] = LASPJ_DEC_MALFORMED;           // rewritten by the redo pass
             const uint32_t i = atomicAdd(redo, 1u);
             redo[1 + i] = (uint32_t)r;
         }
+    }
+}
+
+// ---- payloads over several dictionaries in one launch: the NIF binds many resident
+// variables per call (lasp_vnode.erl:213-237), each variable in a token namespace — a
+// dictionary — of its own.  A table holds every dictionary's decode views; a wave loads
+// the views of the payload it takes (the index is wave-uniform: scalar loads) and decodes
+// exactly as the one-dictionary kernels do.  Dictionaries with many tokens per element and
+// the SMALL ones take separate launches of the same grid (each skips the other's payloads).
+struct DecTabs {
+    DictView d;
+    ReadTabs tabs;
+    HdrHash hh;          // header search (segment starts)
+    HdrHash hh_small;    // element batches
+    u64x2* cells;        // the cells of the group's first payload
+    uint64_t rep0;       // the group's first payload
+    uint32_t E;
+    uint32_t small;      // d.tok_max <= kSmallTok
+};
+
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg_multi(
+    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, const DecTabs* dts,
+    const uint32_t* pay_dt, int tag, int vers, const uint32_t* segbase, uint64_t nseg,
+    uint32_t S, SegRes* res) {
+    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const Cases cs = lane_cases(lane);
+    ReadLds& L = lds[wave];
+    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
+        const uint64_t rep = seg_replica(segbase, R, g);
+        const uint32_t k = ufl32(pay_dt[rep]);
+        if ((dts[k].small != 0) != SMALL) continue;
+        const DecTabs D = dts[k];
+        const uint32_t s = (uint32_t)(g - ufl32(segbase[rep]));
+        seg_decode<SMALL>(payload, total, offs, rep, s, D.E, D.d, D.tabs, D.hh, tag, vers,
+                          D.cells + (rep - D.rep0) * D.E, S, res + g, L, lane, cs);
+    }
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(64) void k_etf_read_chain_multi(const uint8_t* payload, u64 total,
+                                                             const u64* offs, uint64_t R,
+                                                             const uint32_t* segbase, uint32_t S,
+                                                             const SegRes* res, int32_t* status,
+                                                             const DecTabs* dts,
+                                                             const uint32_t* pay_dt, int tag,
+                                                             int vers) {
+    __shared__ __attribute__((aligned(16))) ReadLds L;
+    const uint32_t lane = threadIdx.x;
+    const Cases cs = lane_cases(lane);
+    for (uint64_t r = blockIdx.x; r < R; r += gridDim.x) {
+        const uint32_t k = ufl32(pay_dt[r]);
+        if ((dts[k].small != 0) != SMALL) continue;
+        const u64 base = offs[r];
+        const bool ok = chain_ok(payload, base, offs[r + 1] - base, segbase[r],
+                                 segbase[r + 1] - segbase[r], S, res, lane);
+        if (ok) {
+            if (lane == 0) status[r] = LASPJ_DEC_OK;
+            continue;
+        }
+        const DecTabs D = dts[k];
+        const int32_t st = decode_replica<SMALL>(payload, total, offs, r, D.E, D.d, D.tabs,
+                                                 D.hh_small, tag, vers,
+                                                 D.cells + (r - D.rep0) * D.E, true, L, nullptr,
+                                                 lane, cs);
+        if (lane == 0) status[r] = st;
+    }
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock, SMALL ? 5 : 4) void k_orset_etf_read_multi(
+    const uint8_t* payload, u64 total, const u64* offs, uint64_t R, const DecTabs* dts,
+    const uint32_t* pay_dt, int tag, int vers, int32_t* status) {
+    __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) ReadLdsX ldx[SMALL ? 1 : kBlock / 64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    ReadLdsX* X = SMALL ? nullptr : &ldx[wave];
+    const Cases cs = lane_cases(lane);
+    ReadLds& L = lds[wave];
+    for (uint64_t i = (uint64_t)blockIdx.x * (kBlock / 64) + wave; i < R; i += nwaves) {
+        const uint32_t k = ufl32(pay_dt[i]);
+        if ((dts[k].small != 0) != SMALL) continue;
+        const DecTabs D = dts[k];
+        const int32_t st = decode_replica<SMALL>(payload, total, offs, i, D.E, D.d, D.tabs,
+                                                 D.hh_small, tag, vers,
+                                                 D.cells + (i - D.rep0) * D.E, false, L, X, lane,
+                                                 cs);
+        if (lane == 0) status[i] = st;
     }
 }
 
@@ -4560,7 +4670,8 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
 constexpr uint32_t kVarWords = 1024;     // words per block (4 per thread)
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ curs,
-                                                     u64* __restrict__ in, uint64_t wpr,
+                                                     u64* const* __restrict__ ins,
+                                                     const uint64_t* __restrict__ wprs,
                                                      uint32_t nch, uint32_t n,
                                                      int32_t* __restrict__ dstat,
                                                      uint32_t* __restrict__ diff,
@@ -4586,8 +4697,11 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
     }
     __syncthreads();
     const bool ok = s_st == LASPJ_DEC_OK;
+    // (variables of different namespaces have different widths: the blocks past a
+    // narrower one's words only take part in the ticket)
     u64* cur = curs[i];
-    u64* src = in + (uint64_t)i * wpr;
+    u64* src = ins[i];
+    const uint64_t wpr = wprs[i];
     u64 d = 0;
     const uint64_t w0 = (uint64_t)ch * kVarWords;
     for (uint32_t k = threadIdx.x; k < kVarWords; k += kBlock) {
@@ -4769,6 +4883,102 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
     return LASPJ_OK;
 }
 
+uint64_t etf_multi_bytes(uint32_t ngroups, uint32_t npay) {
+    return ((sizeof(DecTabs) * ngroups + 15ull) & ~15ull) + 4ull * npay;
+}
+
+bool etf_multi_fill(const laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups, uint32_t npay,
+                    void* host) {
+    // the default decoders only (knobs select one-dictionary forms), every dictionary with
+    // the batched tables and the header hash (what segment mode needs)
+    if (ctx->tune_etf_read != 0) return false;
+    for (uint32_t k = 0; k < ngroups; ++k) {
+        const laspj_etf_dict* d = g[k].d;
+        if (!d || !d->rd_desc || !d->rd_htab || !d->rec_len) return false;
+    }
+    if (!host) return true;                       // (the check alone)
+    auto* dt = static_cast<DecTabs*>(host);
+    auto* pd = reinterpret_cast<uint32_t*>(static_cast<char*>(host) +
+                                           ((sizeof(DecTabs) * ngroups + 15ull) & ~15ull));
+    for (uint32_t k = 0; k < ngroups; ++k) {
+        const laspj_etf_dict* d = g[k].d;
+        DecTabs t;
+        std::memset(&t, 0, sizeof(t));
+        t.d = view(d);
+        t.tabs = ReadTabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+        t.hh = HdrHash{d->rd_htab, d->rd_hmask, d->rd_hlens};
+        t.hh_small = HdrHash{d->rd_htab, d->rd_hmask, d->rd_hlens, 1u};
+        t.cells = reinterpret_cast<u64x2*>(g[k].cells);
+        t.rep0 = g[k].p0;
+        t.E = g[k].E;
+        t.small = d->tok_max <= kSmallTok ? 1u : 0u;
+        std::memcpy(dt + k, &t, sizeof(t));
+        for (uint32_t i = g[k].p0; i < g[k].p1 && i < npay; ++i) pd[i] = k;
+    }
+    return true;
+}
+
+int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
+                           const void* dev_tabs, uint32_t npay, const uint8_t* payload,
+                           uint64_t payload_bytes, const u64* offs, const EtfReadPlan& plan,
+                           const uint32_t* segbase, int32_t* status, ChainJob* defer) {
+    const DecTabs* dts = static_cast<const DecTabs*>(dev_tabs);
+    const uint32_t* pd = reinterpret_cast<const uint32_t*>(
+        static_cast<const char*>(dev_tabs) + ((sizeof(DecTabs) * ngroups + 15ull) & ~15ull));
+    bool any[2] = {false, false};                 // [SMALL]
+    for (uint32_t k = 0; k < ngroups; ++k) any[g[k].d->tok_max <= kSmallTok ? 1 : 0] = true;
+    const uint64_t R = npay;
+    if (plan.nseg) {
+        const uint64_t nseg = plan.nseg;
+        const bool deferred = defer && defer->res;
+        SegRes* dres;
+        if (deferred) {
+            dres = static_cast<SegRes*>(defer->res);
+        } else {
+            if (int s2 = reserve_scratch(ctx, sizeof(SegRes) * nseg)) return s2;
+            dres = static_cast<SegRes*>(ctx->scratch);
+        }
+        const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
+        for (int sm = 1; sm >= 0; --sm) {
+            if (!any[sm]) continue;
+            hipLaunchKernelGGL(sm ? k_orset_etf_read_seg_multi<true> : k_orset_etf_read_seg_multi<false>,
+                               dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
+                               payload, (u64)payload_bytes, offs, R, dts, pd, -1, 1, segbase, nseg,
+                               (uint32_t)plan.S, dres);
+            LJ_LAUNCHED(ctx);
+        }
+        if (deferred) {
+            defer->payload = payload;
+            defer->offs = offs;
+            defer->segbase = segbase;
+            defer->status = status;
+            defer->nrep = (uint32_t)R;
+            defer->S = (uint32_t)plan.S;
+            defer->armed = true;
+            return LASPJ_OK;
+        }
+        for (int sm = 1; sm >= 0; --sm) {
+            if (!any[sm]) continue;
+            hipLaunchKernelGGL(sm ? k_etf_read_chain_multi<true> : k_etf_read_chain_multi<false>,
+                               dim3((unsigned)std::min<uint64_t>(R, (uint64_t)ctx->cus * 32)),
+                               dim3(64), 0, ctx->stream, payload, (u64)payload_bytes, offs, R,
+                               segbase, (uint32_t)plan.S, dres, status, dts, pd, -1, 1);
+            LJ_LAUNCHED(ctx);
+        }
+        return LASPJ_OK;
+    }
+    const uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
+    for (int sm = 1; sm >= 0; --sm) {
+        if (!any[sm]) continue;
+        hipLaunchKernelGGL(sm ? k_orset_etf_read_multi<true> : k_orset_etf_read_multi<false>,
+                           dim3((unsigned)std::max<uint64_t>(1, std::min(blocks, cap))),
+                           dim3(kBlock), 0, ctx->stream, payload, (u64)payload_bytes, offs, R, dts,
+                           pd, -1, 1, status);
+        LJ_LAUNCHED(ctx);
+    }
+    return LASPJ_OK;
+}
+
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                       const uint8_t* payload, const u64* offs, int32_t* status, bool clear,
                       const u64* hoffs) {
@@ -4934,10 +5144,11 @@ int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E
     return LASPJ_OK;
 }
 
-int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64_t wpr,
-                     uint32_t n, int32_t* dstat, uint32_t* diff, uint32_t* ticket,
-                     uint8_t* out_res, int32_t* out_st, bool write, const ChainJob* chain) {
-    const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (wpr + kVarWords - 1) / kVarWords);
+int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* const* ins,
+                     const uint64_t* wprs, uint64_t maxw, uint32_t n, int32_t* dstat,
+                     uint32_t* diff, uint32_t* ticket, uint8_t* out_res, int32_t* out_st,
+                     bool write, const ChainJob* chain) {
+    const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (maxw + kVarWords - 1) / kVarWords);
     ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
     if (chain && chain->armed)
         cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
@@ -4945,8 +5156,8 @@ int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64
                        chain->S};
     hipLaunchKernelGGL(write ? k_var_bind<true> : k_var_bind<false>, dim3(nch * n), dim3(kBlock),
                        0, ctx->stream, reinterpret_cast<u64* const*>(curs),
-                       reinterpret_cast<u64*>(in), wpr, nch, n, dstat, diff, ticket, out_res,
-                       out_st, cj);
+                       reinterpret_cast<u64* const*>(ins), wprs, nch, n, dstat, diff, ticket,
+                       out_res, out_st, cj);
     LJ_LAUNCHED(ctx);
     return LASPJ_OK;
 }

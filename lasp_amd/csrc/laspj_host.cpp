@@ -1423,4 +1423,157 @@ int list_write(const laspj_dict* dict, int32_t kind, const ListItems& it, std::s
 
 uint32_t list_dict_elements(const laspj_dict* dict) { return (uint32_t)dict->d.elems.size(); }
 
+// ------------------------------------------------------------------ update/3 operations
+// (laspj_nif.hip's laspj_var_etf_update): the Op term of Type:update(Op, Actor, Value0)
+// read from its image, then its element / token terms registered one by one.
+
+namespace {
+
+// `a` is the atom image of `name` (any of the four atom encodings)
+bool is_atom(const uint8_t* a, size_t n, const char* name) {
+    if (!n || term_class(a[0]) != 1 || term_len(a, n) != n) return false;
+    return atom_name(a) == name;
+}
+
+struct OpParser {
+    int32_t kind;
+    std::vector<UpdateOp>* out;
+    int depth = 0;
+
+    // the elements of a proper list image (LIST_EXT / STRING_EXT / NIL_EXT) in order
+    template <class F>
+    bool each(const uint8_t* l, size_t n, F f) {
+        if (!n) return false;
+        if (l[0] == kNil) return n == 1;
+        if ((l[0] != kList && l[0] != kString) || term_len(l, n) != n) return false;
+        ListIt it(l, n);
+        size_t el;
+        while (const uint8_t* e = it.next(&el))
+            if (!el || !f(e, el)) return false;
+        return !it.tail() || it.tail()[0] == kNil;
+    }
+
+    void push(uint8_t k, const uint8_t* e, size_t el, const uint8_t* t, size_t tl) {
+        UpdateOp o;
+        o.kind = k;
+        o.elem.assign((const char*)e, el);
+        if (t) o.tok.assign((const char*)t, tl);
+        o.mint = k == LASPJ_OP_ADD && kind == LASPJ_KIND_ORSET && !t;
+        out->push_back(std::move(o));
+    }
+
+    // one operation (lasp_orset.erl:101-117 / lasp_gset.erl:84-88); false: no clause of
+    // the reference's update/3 takes it as written (function_clause, a badmatch inside
+    // add_all's fold, a crash in remove_elems / apply_ops over an improper list ...)
+    bool op(const uint8_t* p, size_t n) {
+        if (++depth > 64) return false;
+        if (n < 2 || (p[0] != kSmallTuple && p[0] != kLargeTuple) || term_len(p, n) != n)
+            return false;
+        const uint64_t ar = p[0] == kSmallTuple ? p[1] : be32(p + 1);
+        size_t off = p[0] == kSmallTuple ? 2 : 5;
+        const uint8_t* f[3];
+        size_t fl[3];
+        if (ar < 2 || ar > 3) return false;
+        for (uint64_t i = 0; i < ar; ++i) {
+            f[i] = p + off;
+            fl[i] = term_len(p + off, n - off);
+            if (!fl[i]) return false;
+            off += fl[i];
+        }
+        const bool orset = kind == LASPJ_KIND_ORSET;
+        if (ar == 3)
+            return orset && is_atom(f[0], fl[0], "add_by_token") &&
+                   (push(LASPJ_OP_ADD, f[2], fl[2], f[1], fl[1]), true);
+        if (is_atom(f[0], fl[0], "add")) {
+            push(LASPJ_OP_ADD, f[1], fl[1], nullptr, 0);
+            return true;
+        }
+        if (is_atom(f[0], fl[0], "add_all"))
+            return each(f[1], fl[1], [&](const uint8_t* e, size_t el) {
+                push(LASPJ_OP_ADD, e, el, nullptr, 0);
+                return true;
+            });
+        if (!orset) return false;
+        if (is_atom(f[0], fl[0], "remove")) {
+            push(LASPJ_OP_REMOVE, f[1], fl[1], nullptr, 0);
+            return true;
+        }
+        if (is_atom(f[0], fl[0], "remove_all"))
+            return each(f[1], fl[1], [&](const uint8_t* e, size_t el) {
+                push(LASPJ_OP_REMOVE, e, el, nullptr, 0);
+                return true;
+            });
+        if (is_atom(f[0], fl[0], "update"))
+            return each(f[1], fl[1], [&](const uint8_t* e, size_t el) { return op(e, el); });
+        return false;
+    }
+};
+
+}  // namespace
+
+int parse_update_op(int32_t kind, const uint8_t* img, size_t n, std::vector<UpdateOp>* ops) {
+    ops->clear();
+    try {
+        const uint8_t* t;
+        size_t tn;
+        if (payload_term(img, n, -1, -1, &t, &tn) != LASPJ_DEC_OK) return LASPJ_DEC_MALFORMED;
+        OpParser ps{kind, ops};
+        if (!ps.op(t, tn)) return LASPJ_DEC_MALFORMED;
+        // every term must be one the comparator handles (the dictionary's rule)
+        for (const UpdateOp& o : *ops) {
+            bool ok = true;
+            const auto* e = (const uint8_t*)o.elem.data();
+            term_cmp(e, o.elem.size(), e, o.elem.size(), &ok);
+            if (ok && !o.tok.empty()) {
+                const auto* k = (const uint8_t*)o.tok.data();
+                term_cmp(k, o.tok.size(), k, o.tok.size(), &ok);
+            }
+            if (!ok) return LASPJ_DEC_MALFORMED;
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_DEC_OK;
+}
+
+int64_t dict_find_elem(const laspj_dict* dict, const uint8_t* img, size_t n) {
+    const int64_t f = dict->d.elem(img, n);
+    if (f >= 0) return f;
+    // orddict:find/2 matches keys with `==`: another image of an equal term is not "absent"
+    Dict* d = const_cast<Dict*>(&dict->d);
+    uint64_t he = 0;
+    if (!eq_hash(d, img, n, kElemSeed, &he)) return -2;
+    const bool eq = d->elem_eq.find_if(he, 0, [&](std::string_view o) {
+        bool ok = true;
+        return term_cmp(img, n, (const uint8_t*)o.data(), o.size(), &ok) == 0 && ok;
+    }) != nullptr;
+    return eq ? -2 : -1;
+}
+
+void dict_begin(laspj_dict* dict) { dict->d.journal.clear(); }
+
+void dict_rollback(laspj_dict* dict) {
+    dict->d.rollback();
+    dict->d.journal.clear();
+}
+
+int dict_reg_elem(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot) {
+    try {
+        return reg_elem(&dict->d, img, n, slot);
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+}
+
+int dict_reg_tok(laspj_dict* dict, uint32_t e, const uint8_t* img, size_t n, uint32_t* slot) {
+    try {
+        uint8_t s = 0;
+        const int st = reg_tok(&dict->d, e, img, n, &s);
+        *slot = s;
+        return st;
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+}
+
 }  // namespace laspj

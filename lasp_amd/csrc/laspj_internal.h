@@ -320,6 +320,29 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                      const unsigned long long* offsets, const EtfReadPlan& plan,
                      const uint32_t* segbase, int32_t* status, bool clear,
                      uint32_t* redo_zeroed, ChainJob* defer = nullptr);
+// OR-Set payloads over several dictionaries decoded in one launch (the NIF's binds of many
+// variables, one token namespace each): group k's payloads [p0, p1) against dictionary d
+// into cells (its first payload's; E slots per replica, consecutive).  The caller stages
+// etf_multi_bytes of tables (etf_multi_fill: false when some dictionary cannot take the
+// shared launch — decode group by group then; host null: that check only) and hands their
+// device copy to
+// etf_read_multi_enqueue; offsets are every payload's (absolute), the plan and segbase
+// are over all payloads (etf_read_plan with any of the dictionaries); cells are not
+// cleared (the caller's are zero); defer as etf_read_enqueue's
+struct EtfGroup {
+    const laspj_etf_dict* d;
+    uint32_t p0, p1;
+    uint64_t* cells;
+    uint32_t E;
+};
+uint64_t etf_multi_bytes(uint32_t ngroups, uint32_t npay);
+bool etf_multi_fill(const laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups, uint32_t npay,
+                    void* host);
+int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
+                           const void* dev_tabs, uint32_t npay, const uint8_t* payload,
+                           uint64_t payload_bytes, const unsigned long long* offs,
+                           const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
+                           ChainJob* defer);
 // lasp_gset:from_binary/1's decoder (k_gset_etf_read: one wave per payload), enqueue only;
 // offsets / status are device addresses; clear: zero the batch first
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
@@ -342,14 +365,16 @@ int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E
                             const laspj_etf_dict* d, int tag, int vers,
                             unsigned long long* offs_out, uint8_t* out, uint64_t cap_bytes,
                             unsigned long long* lbst, uint32_t* ticket, const ChainJob* chain);
-// lasp_core:bind/3 (write = false) / write/4 (write = true) of n resident variables: curs
-// (device array of n cell pointers), in (n x wpr decoded words, left zero), dstat (n
-// decode statuses: read, or — chain armed — written from the deferred chain check), diff
-// (n zeroed words) and ticket (a zeroed word) left zero; out_res / out_st (n bytes / n
-// int32, pinned) get the bind statuses and decode statuses
-int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* in, uint64_t wpr,
-                     uint32_t n, int32_t* dstat, uint32_t* diff, uint32_t* ticket,
-                     uint8_t* out_res, int32_t* out_st, bool write, const ChainJob* chain);
+// lasp_core:bind/3 (write = false) / write/4 (write = true) of n resident variables: curs /
+// ins / wprs (device arrays of n: the variable's cells, its decoded operand's cells — left
+// zero — and their width in words; maxw the widest), dstat (n decode statuses: read, or —
+// chain armed — written from the deferred chain check), diff (n zeroed words) and ticket
+// (a zeroed word) left zero; out_res / out_st (n bytes / n int32, pinned) get the bind
+// statuses and decode statuses
+int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* const* ins,
+                     const uint64_t* wprs, uint64_t maxw, uint32_t n, int32_t* dstat,
+                     uint32_t* diff, uint32_t* ticket, uint8_t* out_res, int32_t* out_st,
+                     bool write, const ChainJob* chain);
 // offsets: R + 1 (offsets[R] = total); flag: set when a present slot has no image (the
 // caller zeroes it); *chunks: the split-mode chunk offsets etf_write_enqueue can reuse
 // (valid until the context's scratch is next used), or null
@@ -395,6 +420,26 @@ bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_vie
 // register the terms of the OR-Set payload elements that start in [from, to) (from: an
 // element's first byte); a DEC status (the range's registrations undone on failure)
 int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, size_t to);
+// update/3's Op (lasp_orset.erl:101-117, lasp_gset.erl:84-88) read from its image (131 +
+// the term), flattened in application order: {add, E} / {add_all, Es} (one ADD per element,
+// `mint` for an OR-Set: unique/1 mints its token), {add_by_token, T, E}, {remove, E},
+// {remove_all, Es}, {update, Ops}.  LASPJ_DEC_MALFORMED: no clause of the reference's update
+// takes it as written (the NIF runs the reference's, which raises)
+struct UpdateOp {
+    uint8_t kind = 0;            // LASPJ_OP_ADD / LASPJ_OP_REMOVE
+    bool mint = false;
+    std::string elem, tok;       // term images (no version byte); tok empty when minted
+};
+int parse_update_op(int32_t kind, const uint8_t* img, size_t n, std::vector<UpdateOp>* ops);
+// the element slot of an image, -1 when absent, -2 when a term `==` to it holds a slot
+// under another image (or the term is outside this path); single registrations inside a
+// journal that
+// dict_rollback undoes (LASPJ_DEC_* statuses as laspj_dict_add's)
+int64_t dict_find_elem(const laspj_dict* dict, const uint8_t* img, size_t n);
+void dict_begin(laspj_dict* dict);
+void dict_rollback(laspj_dict* dict);
+int dict_reg_elem(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot);
+int dict_reg_tok(laspj_dict* dict, uint32_t e, const uint8_t* img, size_t n, uint32_t* slot);
 
 
 // ---- list values as images (laspj_host.cpp; used by laspj_list_etf.cpp) ---------------

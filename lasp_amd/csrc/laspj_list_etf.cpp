@@ -262,11 +262,14 @@ int body(laspj_ctx* ctx, ListEtfState* S, LOp op, int32_t kind, const Args& in, 
         std::vector<uint32_t> off(nidx + 1ull, 0);
         std::vector<uint64_t> fk;
         std::vector<char> seen(nidx, 0);
+        // per slot, the position of its argument's result (the fold below reads it)
+        std::vector<int64_t> argpos(nidx, -1);
         for (size_t i = 0; i < x.keys.size(); ++i) {
             const uint32_t e = (uint32_t)x.keys[i];
             if (seen[e]) continue;
             seen[e] = 1;
             const int64_t p = pos[args[i]];
+            argpos[e] = p;
             std::string_view tail = tail_of(e);
             if (op == LOp::FILTER) {
                 keep[e] = is_true(res[(size_t)p]) ? 1 : 0;
@@ -282,10 +285,7 @@ int body(laspj_ctx* ctx, ListEtfState* S, LOp op, int32_t kind, const Args& in, 
             for (uint32_t e = 0; e < nidx; ++e) {
                 off[e] = (uint32_t)fk.size();
                 if (!seen[e]) continue;
-                // find the argument of slot e (any entry with this key)
-                int64_t p = -1;
-                for (size_t i = 0; i < x.keys.size() && p < 0; ++i)
-                    if ((uint32_t)x.keys[i] == e) p = pos[args[i]];
+                const int64_t p = argpos[e];
                 const std::string img = std::string(1, (char)131) + res[(size_t)p];
                 std::vector<std::string> vs;
                 if (!list_terms((const uint8_t*)img.data(), img.size(), &vs))
@@ -367,8 +367,8 @@ int entry(laspj_ctx* ctx, LOp op, int32_t kind, const Args& in, const uint8_t** 
     if (!ctx) return LASPJ_E_INVAL;
     if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET)
         return fail(ctx, LASPJ_E_KIND, "list_etf: OR-Set or G-Set lists");
-    if (!verdict || (!out && op != LOp::BIND) || (op == LOp::BIND && (!status || !out)) ||
-        (!in.a && in.na) || (!in.b && in.nb))
+    if (!verdict || !out || !out_len || (op == LOp::BIND && !status) || (!in.a && in.na) ||
+        (!in.b && in.nb))
         return fail(ctx, LASPJ_E_INVAL, "list_etf: null argument");
     ListEtfState* S = lstate(ctx);
     if (!S) return fail(ctx, LASPJ_E_NOMEM, "list_etf: state allocation");

@@ -34,32 +34,27 @@
 // Scratch, dictionaries and staging are per context: one context per scheduler (or per
 // vnode), no process globals.
 
+#include <sys/random.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <unordered_set>
 #include <vector>
 
 #include "laspj_internal.h"
 
-// A device-resident variable's value (the `#dv.value` of lasp_core's store): cells over the
-// dictionary of its kind in its context, or — when its value is not representable, or
-// between a dictionary reset and its next use — the value's image held on the host.
-struct laspj_var {
-    laspj_ctx* ctx = nullptr;        // null once the context is gone
-    int32_t kind = LASPJ_KIND_ORSET;
-    uint64_t* cells = nullptr;       // one replica over `E` element slots (null: new())
-    uint64_t cell_bytes = 0;         // the block's size (dev_alloc)
-    uint32_t E = 0;
-    uint64_t epoch = 0;              // the dictionary generation the cells refer to
-    bool resident = true;            // cells hold the value (else `image` does)
-    std::vector<uint8_t> image;      // host-held value (term_to_binary image)
-};
-
 namespace laspj {
 
-// one dictionary of one kind (OR-Set or G-Set) and its device images
+// One dictionary of one kind (OR-Set or G-Set) and its device images.  The image calls of a
+// context share one per kind; every resident variable has one of its own — its token
+// namespace — shared only with the replicas created beside it (laspj_var_create_replica),
+// so a variable's dictionary holds the terms of its own value (and its replicas') and
+// variables never compete for an element's token slots (include/lasp.hrl:60-63: each
+// #dv.value is independent).
 struct KindState {
     int32_t kind = LASPJ_KIND_ORSET;
     laspj_dict* dict = nullptr;     // term images -> slots (host, append-only)
@@ -72,11 +67,33 @@ struct KindState {
     // patched into the device images (etf_dict_patch) instead of rebuilding them
     uint32_t built_K = 0;
     std::vector<uint32_t> built_cnt;
+    // the variables whose cells refer to this dictionary (none for the image calls')
+    std::unordered_set<laspj_var*> vars;
 };
+
+}  // namespace laspj
+
+// A device-resident variable's value (the `#dv.value` of lasp_core's store): cells over its
+// namespace's dictionary, or — when its value is not representable, or between a dictionary
+// reset and its next use — the value's image held on the host.
+struct laspj_var {
+    laspj_ctx* ctx = nullptr;        // null once the context is gone
+    int32_t kind = LASPJ_KIND_ORSET;
+    std::shared_ptr<laspj::KindState> ns;   // the token namespace (dictionary) of the cells
+    uint64_t* cells = nullptr;       // one replica over `E` element slots (null: new())
+    uint64_t cell_bytes = 0;         // the block's size (dev_alloc)
+    uint32_t E = 0;
+    uint64_t epoch = 0;              // the dictionary generation the cells refer to
+    bool resident = true;            // cells hold the value (else `image` does)
+    bool held = false;               // `image` is a value write/4 could not represent
+    std::vector<uint8_t> image;      // host-held value (term_to_binary image)
+};
+
+namespace laspj {
 
 struct NifState {
     std::mutex mu;                  // one call at a time (ctx->mu is held per device phase)
-    KindState ks[2];                // [0] OR-Set, [1] G-Set
+    KindState ks[2];                // the image calls' dictionaries: [0] OR-Set, [1] G-Set
     // device: [in region: offsets | segment table | zeroed words | variable cell pointers
     // | payloads or cells][segment results][variable calls' statuses]; cells: the batches
     void* dblk = nullptr;
@@ -99,6 +116,10 @@ struct NifState {
     uint64_t clean_words = 0;
     uint64_t stats[LASPJ_NIF_STATS] = {};
     std::unordered_set<laspj_var*> vars;
+    // laspj_var_etf_update's answers (valid until the context's next call): the tokens it
+    // minted, the image of the element a failed precondition names
+    std::vector<uint8_t> minted;
+    std::string err_elem;
 };
 
 namespace {
@@ -130,6 +151,75 @@ __global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src
     }
 }
 
+// lasp_orset:update/3 / lasp_gset:update/3 (lasp_orset.erl:99-117, 222-259;
+// lasp_gset.erl:84-88) of one call on a resident variable's cells: the ops in order, all or
+// nothing.  A REMOVE whose element is absent — not in the cells and not added earlier in the
+// call — fails the call ({error, {precondition, {not_present, E}}}, remove_elems / apply_ops
+// stop there and the state is kept); element 0xFFFFFFFF is an element the dictionary has
+// never held.  Few ops travel as kernel arguments (no upload on the update path); one lane
+// walks them (a call is a handful of ops).
+constexpr uint32_t kUpdArgOps = 24;
+struct UpdArgs {
+    laspj_op op[kUpdArgOps];
+};
+constexpr uint32_t kNoElem = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(64) k_var_update(uint64_t* __restrict__ cells, int32_t kind,
+                                                   UpdArgs a, const laspj_op* __restrict__ dops,
+                                                   uint32_t nops, int32_t* __restrict__ status) {
+    if (threadIdx.x != 0) return;
+    auto op = [&](uint32_t k) -> laspj_op { return dops ? dops[k] : a.op[k]; };
+    uint32_t bad = nops;
+    if (kind == LASPJ_KIND_ORSET) {
+        for (uint32_t k = 0; k < nops && bad == nops; ++k) {
+            const laspj_op o = op(k);
+            if (o.kind != LASPJ_OP_REMOVE) continue;
+            bool present = o.element != kNoElem && cells[2ull * o.element] != 0;
+            for (uint32_t j = 0; j < k && !present; ++j) {
+                const laspj_op q = op(j);
+                present = q.kind == LASPJ_OP_ADD && q.element == o.element;
+            }
+            if (!present) bad = k;
+        }
+    }
+    for (uint32_t k = 0; k < nops; ++k) {
+        if (bad < nops) {
+            if (status) status[k] = k == bad ? LASPJ_OPST_NOT_PRESENT : LASPJ_OPST_ROLLED_BACK;
+            continue;
+        }
+        const laspj_op o = op(k);
+        if (kind == LASPJ_KIND_ORSET) {
+            uint64_t* c = cells + 2ull * o.element;
+            if (o.kind == LASPJ_OP_ADD) {
+                // orddict:store(Token, false, Tokens): present, flag false
+                c[0] |= 1ull << o.slot;
+                c[1] &= ~(1ull << o.slot);
+            } else {
+                c[1] = c[0];                           // every token of Elem := true
+            }
+        } else {
+            cells[o.element >> 6] |= 1ull << (o.element & 63u);
+        }
+        if (status) status[k] = LASPJ_OPST_APPLIED;
+    }
+}
+
+// the same for a call of ADDs only (add_all over many elements): commutative, one op per lane
+__global__ void __launch_bounds__(256) k_var_adds(uint64_t* __restrict__ cells, int32_t kind,
+                                                  const laspj_op* __restrict__ ops, uint32_t nops) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nops) return;
+    const laspj_op o = ops[k];
+    if (kind == LASPJ_KIND_ORSET) {
+        unsigned long long* c = reinterpret_cast<unsigned long long*>(cells + 2ull * o.element);
+        atomicOr(c, 1ull << o.slot);
+        atomicAnd(c + 1, ~(1ull << o.slot));
+    } else {
+        atomicOr(reinterpret_cast<unsigned long long*>(cells + (o.element >> 6)),
+                 1ull << (o.element & 63u));
+    }
+}
+
 struct Guard {
     std::lock_guard<std::mutex> lk;
     explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
@@ -151,12 +241,20 @@ uint64_t wpr_of(int32_t kind, uint32_t E) {
     return kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
 }
 
+// the payloads [p0, p1) of a call decoded against one dictionary (an image call: the
+// context's; a variable call: one per namespace of its variables)
+struct Group {
+    KindState* K = nullptr;
+    uint32_t p0 = 0, p1 = 0;
+};
+
 // one NIF-level call over m operand payloads giving n answers
 struct Call {
     Op op = Op::MERGE;
     int32_t kind = LASPJ_KIND_ORSET;
     int strict = 0;
     uint32_t n = 0, m = 0;
+    std::vector<Group> groups;      // >= 1; single-group ops (all but BIND / WRITE) use [0]
     std::vector<const uint8_t*> p;  // m payloads: MERGE / EQUAL / INFLATION: lhs[0..n) then rhs
     std::vector<uint64_t> len;
     std::vector<laspj_var*> vars;   // variable calls: n variables (payload i -> variable i)
@@ -333,33 +431,65 @@ int fit_var(laspj_ctx* ctx, laspj_var* v, uint32_t E) {
 // One device pass: stage, pull, decode (or upload host-encoded cells), answer, one
 // synchronisation.  Fills c.st / c.res / c.ooff / c.obase.
 
-int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
+int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const uint64_t t0 = now_ns();
     uint64_t t_copy = 0;
-    const uint32_t m = c.m, n = c.n, E = K.E;
+    const uint32_t m = c.m, n = c.n;
+    const size_t G = c.groups.size();
+    // single-group ops (every op but BIND / WRITE) answer over group 0's dictionary
+    KindState& K = *c.groups[0].K;
+    const uint32_t E = K.E;
     const bool orset = c.kind == LASPJ_KIND_ORSET;
-    const bool dec = m && (orset ? etf_dict_decodable(K.etf) : true);
+    bool dec = m != 0;
+    for (const Group& g : c.groups)
+        if (orset && g.p1 > g.p0 && !etf_dict_decodable(g.K->etf)) dec = false;
     const bool var_op = c.op == Op::BIND || c.op == Op::WRITE;
     const bool var_in = var_op || c.op == Op::THRESHOLD || c.op == Op::READ || c.op == Op::VVALUE;
     std::vector<unsigned long long> hoffs(m + 1ull, 0);
     for (uint32_t i = 0; i < m; ++i) hoffs[i + 1] = hoffs[i] + c.len[i];
     const uint64_t pay = hoffs[m];
-    EtfReadPlan plan;
-    if (dec && orset) etf_read_plan(ctx, K.etf, m, hoffs.data(), &plan);
+    // per group: its operand cells (words into the cell area: its payloads' replicas at its
+    // own width)
+    std::vector<uint64_t> gseg(G, 0), gcell(G, 0);
+    std::vector<EtfGroup> eg(G);
+    uint64_t seg_area = 0, in_words = 0;
+    for (size_t g = 0; g < G; ++g) {
+        const Group& gr = c.groups[g];
+        gcell[g] = in_words;
+        in_words += (uint64_t)(gr.p1 - gr.p0) * wpr_of(c.kind, gr.K->E);
+        eg[g] = EtfGroup{gr.K->etf, gr.p0, gr.p1, nullptr, gr.K->E};
+    }
+    // several namespaces' OR-Set payloads: one decode launch over all of them (a table of
+    // the dictionaries rides in the in region) with one plan, else group by group, each
+    // with its own plan and segment table
+    const bool multi = G > 1 && dec && orset &&
+                       etf_multi_fill(ctx, eg.data(), (uint32_t)G, m, nullptr);
+    std::vector<EtfReadPlan> plans(multi ? 1 : G);
+    for (size_t g = 0; g < plans.size(); ++g) {
+        const Group& gr = c.groups[g];
+        const uint32_t p0 = multi ? 0 : gr.p0, R = multi ? m : gr.p1 - gr.p0;
+        if (dec && orset && R) etf_read_plan(ctx, gr.K->etf, R, hoffs.data() + p0, &plans[g]);
+        gseg[g] = seg_area;
+        if (plans[g].nseg) seg_area += al(4ull * (R + 1), 16);
+    }
+    const EtfReadPlan& plan = plans[0];
+    const uint64_t mtab_bytes = multi ? al(etf_multi_bytes((uint32_t)G, m), 256) : 0;
     const bool has_payload_out = c.op == Op::MERGE || c.op == Op::VALUE || c.op == Op::READ ||
                                  c.op == Op::VVALUE;
-    const uint64_t W = wpr_of(c.kind, E);            // words per replica
+    const uint64_t W = wpr_of(c.kind, E);            // words per replica (single-group ops)
     // in region (host -> device)
-    // [offsets | segment table | zeroed words: the size pass's ticket, the decoder's redo
-    //  list, the one-launch merge's look-back words, the variable kernel's difference words
-    //  and ticket | variable cell pointers | payloads]
+    // [offsets | segment tables | zeroed words: the size pass's ticket, the decoders' redo
+    //  lists, the one-launch merge's look-back words, the variable kernel's difference words
+    //  and ticket | variable cell pointers, operand cell pointers, widths | the decode
+    //  table of several dictionaries | payloads]
     const uint64_t i_offs = 0, i_seg = al(8ull * (m + 1), 256),
-                   i_zero = i_seg + (plan.nseg ? al(4ull * (m + 1), 256) : 0),
-                   z_lb = al(4ull * (m + 2), 16), z_var = z_lb + 8ull * ((E + 255) / 256),
+                   i_zero = i_seg + al(seg_area, 256),
+                   z_lb = al(4ull * (m + G + 2), 16), z_var = z_lb + 8ull * ((E + 255) / 256),
                    z_bytes = z_var + 4ull * (n + 1),
                    i_vptr = i_zero + al(z_bytes, 256),
-                   i_pay = i_vptr + (var_op ? al(8ull * n, 256) : 0);
-    const uint64_t cells_in = (uint64_t)m * W * 8ull;
+                   i_mtab = i_vptr + (var_op ? al(24ull * n, 256) : 0),
+                   i_pay = i_mtab + mtab_bytes;
+    const uint64_t cells_in = in_words * 8ull;
     const uint64_t in_bytes = i_pay + (dec ? al(pay + 64, 256) : al(cells_in, 256));
     // out region: written by kernels into the pinned staging
     const uint64_t o_st = 0, o_res = al(4ull * m, 16), o_ooff = o_res + al(n, 16),
@@ -375,7 +505,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
     const uint64_t out_bytes = o_pay + ocap;
     // MERGE: the segment decoder's chain check rides on the join's launch (ChainJob), its
     // per-segment results in a device area of their own after the in region
-    const bool defer = dec && orset && plan.nseg && !c.no_defer &&
+    // (one plan only: the join / bind launch carries one chain check)
+    const bool defer = (G == 1 || multi) && dec && orset && plan.nseg && !c.no_defer &&
                        ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op ||
                         (c.op == Op::VALUE && etf_value_direct(ctx, n, E)));
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
@@ -387,7 +518,6 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
                                : (c.op == Op::VALUE || c.op == Op::VVALUE) ? (uint64_t)n * VW * 8ull
                                                                             : 0;
     const uint64_t c_out = al(cells_in, 256);
-    const uint64_t in_words = (uint64_t)m * W;
     {
         Guard g(ctx);
         if (int s = grow_dev(ctx, &S->dblk, &S->dblk_bytes,
@@ -413,7 +543,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
         }
         if (var_in)
             for (laspj_var* v : c.vars)
-                if (int s = fit_var(ctx, v, E)) return s;
+                if (int s = fit_var(ctx, v, v->ns->E)) return s;
     }
     uint8_t* hin = static_cast<uint8_t*>(S->hin);
     uint8_t* din = static_cast<uint8_t*>(S->dblk);
@@ -424,29 +554,54 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
     uint64_t* cin = static_cast<uint64_t*>(S->dcells);
     uint64_t* cout = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(S->dcells) + c_out);
     std::memcpy(hin + i_offs, hoffs.data(), 8ull * (m + 1));
-    if (plan.nseg) std::memcpy(hin + i_seg, plan.segbase.data(), 4ull * (m + 1));
+    for (size_t g = 0; g < plans.size(); ++g)
+        if (plans[g].nseg)
+            std::memcpy(hin + i_seg + gseg[g], plans[g].segbase.data(),
+                        4ull * plans[g].segbase.size());
+    if (multi) {
+        for (size_t g = 0; g < G; ++g) eg[g].cells = static_cast<uint64_t*>(S->dcells) + gcell[g];
+        etf_multi_fill(ctx, eg.data(), (uint32_t)G, m, hin + i_mtab);
+    }
     std::memset(hin + i_zero, 0, z_bytes);
-    if (var_op)
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint64_t p = reinterpret_cast<uint64_t>(c.vars[i]->cells);
-            std::memcpy(hin + i_vptr + 8ull * i, &p, 8);
+    uint64_t maxw = 0;                                // widest variable (the bind's chunks)
+    if (var_op) {
+        // per variable: its cells, its decoded operand's cells, their width
+        for (size_t g = 0; g < G; ++g) {
+            const Group& gr = c.groups[g];
+            const uint64_t w = wpr_of(c.kind, gr.K->E);
+            maxw = std::max(maxw, w);
+            for (uint32_t i = gr.p0; i < gr.p1; ++i) {
+                const uint64_t cur = reinterpret_cast<uint64_t>(c.vars[i]->cells);
+                const uint64_t in = reinterpret_cast<uint64_t>(
+                    static_cast<uint64_t*>(S->dcells) + gcell[g] + (uint64_t)(i - gr.p0) * w);
+                std::memcpy(hin + i_vptr + 8ull * i, &cur, 8);
+                std::memcpy(hin + i_vptr + 8ull * (n + i), &in, 8);
+                std::memcpy(hin + i_vptr + 8ull * (2ull * n + i), &w, 8);
+            }
         }
+    }
     uint32_t* dticket = reinterpret_cast<uint32_t*>(din + i_zero);
     auto* dlb = reinterpret_cast<unsigned long long*>(din + i_zero + z_lb);
     uint32_t* dvdiff = reinterpret_cast<uint32_t*>(din + i_zero + z_var);
     const bool clean = S->clean_words >= in_words;
     std::vector<int32_t> hst;
     if (m && !dec) {
-        // token images of several lengths (or no tokens yet): the host dictionary encodes
+        // token images of several lengths (or no tokens yet): the host dictionaries encode
         // the cells (laspj_dict_encode), the device does the rest
         std::vector<uint8_t> blob(pay);
         for (uint32_t i = 0; i < m; ++i)
             if (c.len[i]) std::memcpy(blob.data() + hoffs[i], c.p[i], c.len[i]);
         hst.assign(m, 0);
-        if (int s = laspj_dict_encode(K.dict, c.kind, blob.data(),
-                                      reinterpret_cast<const uint64_t*>(hoffs.data()), m, -1, E,
-                                      reinterpret_cast<uint64_t*>(hin + i_pay), hst.data()))
-            return fail(ctx, s, "nif: host encode failed (%d)", s);
+        for (size_t g = 0; g < G; ++g) {
+            const Group& gr = c.groups[g];
+            if (gr.p1 == gr.p0) continue;
+            if (int s = laspj_dict_encode(gr.K->dict, c.kind, blob.data(),
+                                          reinterpret_cast<const uint64_t*>(hoffs.data()) + gr.p0,
+                                          gr.p1 - gr.p0, -1, gr.K->E,
+                                          reinterpret_cast<uint64_t*>(hin + i_pay) + gcell[g],
+                                          hst.data() + gr.p0))
+                return fail(ctx, s, "nif: host encode failed (%d)", s);
+        }
         ++S->stats[5];
     }
     {
@@ -506,19 +661,37 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
         int32_t* dst = var_op ? dvst : reinterpret_cast<int32_t*>(rout + o_st);
         ChainJob cjob;
         if (defer) cjob.res = dseg;
-        if (dec) {
-            if (orset) {
-                if (int s = etf_read_enqueue(ctx, &inb, K.etf, -1, 1, din + i_pay, pay,
-                                             reinterpret_cast<const unsigned long long*>(din + i_offs),
-                                             plan,
-                                             plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg)
-                                                       : nullptr,
-                                             dst, !clean, dticket + 1, defer ? &cjob : nullptr))
-                    return s;
-            } else if (int s = gset_read_enqueue(ctx, &inb, K.etf, -1, 1, din + i_pay,
-                                                 reinterpret_cast<const unsigned long long*>(din + i_offs),
-                                                 dst, !clean, hoffs.data())) {
+        if (dec && multi) {
+            // every namespace's payloads in one launch (the cells zeroed first when the last
+            // call left them dirty: the decoders only set what they decode)
+            if (!clean) LJ_HIP(ctx, hipMemsetAsync(cin, 0, cells_in, ctx->stream));
+            if (int s = etf_read_multi_enqueue(
+                    ctx, eg.data(), (uint32_t)G, din + i_mtab, m, din + i_pay, pay,
+                    reinterpret_cast<const unsigned long long*>(din + i_offs), plan,
+                    plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg) : nullptr, dst,
+                    defer ? &cjob : nullptr))
                 return s;
+        } else if (dec) {
+            // each group's payloads against its own dictionary (offsets are absolute in the
+            // payload area, so a group reads its slice of them in place)
+            for (size_t g = 0; g < G; ++g) {
+                const Group& gr = c.groups[g];
+                const uint32_t R = gr.p1 - gr.p0;
+                if (!R) continue;
+                laspj_batch gb = view(ctx, c.kind, R, gr.K->E, cin + gcell[g]);
+                const auto* doffs = reinterpret_cast<const unsigned long long*>(din + i_offs) + gr.p0;
+                if (orset) {
+                    if (int s = etf_read_enqueue(
+                            ctx, &gb, gr.K->etf, -1, 1, din + i_pay, pay, doffs, plans[g],
+                            plans[g].nseg ? reinterpret_cast<const uint32_t*>(din + i_seg + gseg[g])
+                                          : nullptr,
+                            dst + gr.p0, !clean, dticket + 1 + gr.p0 + g,
+                            defer ? &cjob : nullptr))
+                        return s;
+                } else if (int s = gset_read_enqueue(ctx, &gb, gr.K->etf, -1, 1, din + i_pay, doffs,
+                                                     dst + gr.p0, !clean, hoffs.data() + gr.p0)) {
+                    return s;
+                }
             }
         } else if (m && var_op) {
             LJ_HIP(ctx, hipMemcpyAsync(dvst, hst.data(), 4ull * m, hipMemcpyHostToDevice,
@@ -633,7 +806,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, KindState& K, Call& c) {
             // bind/3 (lasp_core.erl:291-312) / write/4 (:839-844) into the resident cells
             // (the segment decoder's chain check rides on this launch when deferred)
             if (int s = var_bind_enqueue(ctx, reinterpret_cast<uint64_t* const*>(din + i_vptr),
-                                         cin, W, n, dvst, dvdiff, dvdiff + n, rout + o_res,
+                                         reinterpret_cast<uint64_t* const*>(din + i_vptr + 8ull * n),
+                                         reinterpret_cast<const uint64_t*>(din + i_vptr + 16ull * n),
+                                         maxw, n, dvst, dvdiff, dvdiff + n, rout + o_res,
                                          reinterpret_cast<int32_t*>(rout + o_st),
                                          c.op == Op::WRITE, &cjob))
                 return s;
@@ -704,7 +879,7 @@ int register_payloads(laspj_ctx* ctx, NifState* S, KindState& K,
 // start in it — what the segment's decoder could not take; the segments that decoded hold
 // known terms.  False: a range did not register (nothing is kept), the caller registers
 // whole operands.
-bool register_segments(NifState* S, KindState& K, const Call& c, const std::vector<uint32_t>& ops) {
+bool register_segments(NifState* S, const Call& c, const std::vector<uint32_t>& ops) {
     const uint64_t t0 = now_ns();
     struct Range {
         uint32_t i;
@@ -723,16 +898,24 @@ bool register_segments(NifState* S, KindState& K, const Call& c, const std::vect
         }
     }
     if (rs.empty()) return false;
-    for (const Range& r : rs)
+    for (const Range& r : rs) {
+        // (the payload's group: its namespace's dictionary)
+        size_t g = 0;
+        while (g + 1 < c.groups.size() && r.i >= c.groups[g].p1) ++g;
+        KindState& K = *c.groups[g].K;
         if (dict_add_elems(K.dict, c.p[r.i], c.len[r.i], r.from, r.to) != LASPJ_DEC_OK)
             return false;       // (ranges already added stay: they hold well-formed terms)
+        K.stale = true;
+    }
     ++S->stats[2];
     S->stats[12] += now_ns() - t0;
-    K.stale = true;
     return true;
 }
 
 int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict);
+
+// the call's payloads decoded against one dictionary
+void one_group(Call& c, KindState* K) { c.groups.assign(1, Group{K, 0, c.m}); }
 
 // the image of a resident variable (a READ pass; the caller holds S->mu)
 int read_var(laspj_ctx* ctx, NifState* S, laspj_var* v, std::vector<uint8_t>* img) {
@@ -742,6 +925,7 @@ int read_var(laspj_ctx* ctx, NifState* S, laspj_var* v, std::vector<uint8_t>* im
     c.n = 1;
     c.m = 0;
     c.vars.push_back(v);
+    one_group(c, v->ns.get());
     std::vector<int32_t> vd;
     if (int s = run(ctx, S, c, &vd)) return s;
     if (vd[0] != LASPJ_NIF_OK) return fail(ctx, LASPJ_E_DEVICE, "nif: variable encode failed");
@@ -753,8 +937,8 @@ int read_var(laspj_ctx* ctx, NifState* S, laspj_var* v, std::vector<uint8_t>* im
 // out to its image (encoded on the device with the dictionary its cells refer to) and its
 // cells released; the next call that uses it decodes the image again (hydrate)
 int spill_vars(laspj_ctx* ctx, NifState* S, KindState& K) {
-    for (laspj_var* v : S->vars) {
-        if (v->kind != K.kind || !v->resident || v->epoch != K.epoch) continue;
+    for (laspj_var* v : K.vars) {
+        if (!v->resident || v->epoch != K.epoch) continue;
         if (!v->cells) {
             v->image.assign({131, 106});              // new() = []
         } else if (int s = read_var(ctx, S, v, &v->image)) {
@@ -771,7 +955,8 @@ int spill_vars(laspj_ctx* ctx, NifState* S, KindState& K) {
 }
 
 int reset_dict(laspj_ctx* ctx, NifState* S, KindState& K) {
-    if (K.dict)
+    const bool had = K.dict != nullptr;       // (creating a namespace's first is no reset)
+    if (had)
         if (int s = spill_vars(ctx, S, K)) return s;
     free_etf(K);
     if (K.dict) laspj_dict_destroy(K.dict);
@@ -780,7 +965,7 @@ int reset_dict(laspj_ctx* ctx, NifState* S, KindState& K) {
         return fail(ctx, LASPJ_E_NOMEM, "nif: dictionary allocation");
     K.stale = false;
     ++K.epoch;
-    ++S->stats[3];
+    if (had) ++S->stats[3];
     return LASPJ_OK;
 }
 
@@ -788,34 +973,52 @@ int reset_dict(laspj_ctx* ctx, NifState* S, KindState& K) {
 // other undecodable operand -> FALLBACK.  verdict[j] per answer.
 int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
     ++S->stats[0];
-    KindState& K = kstate(S, c.kind);
-    if (!K.dict && reset_dict(ctx, S, K)) return LASPJ_E_NOMEM;
+    const size_t G = c.groups.size();
+    for (const Group& g : c.groups)
+        if (!g.K->dict && reset_dict(ctx, S, *g.K)) return LASPJ_E_NOMEM;
     const uint32_t n = c.n, m = c.m;
     auto answer_of = [&](uint32_t i) { return i % n; };
+    auto group_of = [&](uint32_t i) {
+        size_t g = 0;
+        while (g + 1 < G && i >= c.groups[g].p1) ++g;
+        return g;
+    };
+    auto slice = [&](uint32_t p0, uint32_t p1, std::vector<const uint8_t*>* p,
+                     std::vector<uint64_t>* l) {
+        p->assign(c.p.begin() + p0, c.p.begin() + p1);
+        l->assign(c.len.begin() + p0, c.len.begin() + p1);
+    };
     // a variable call's operands are its own (payload i belongs to variable i): one whose
-    // value needs a fresh dictionary (an element's 64 token slots used up) would write out
-    // every other variable's cells, so only write/4 resets; bind / threshold answer
-    // FALLBACK and the NIF runs the reference's clause over the variable's read image
+    // value needs a fresh dictionary (an element's 64 token slots used up in its namespace)
+    // would write out the namespace's other variables, so only write/4 resets; bind /
+    // threshold answer FALLBACK and the NIF runs the reference's clause over the variable's
+    // read image
     const bool may_reset = !(c.op == Op::BIND || c.op == Op::THRESHOLD);
     std::vector<uint8_t> fallback(n, 0);
-    bool registered = false;
+    std::vector<uint8_t> registered(G, 0);
     bool partial = false;           // the last registration took the failing segments only
     bool resolved = false;          // the last pass's answers stand (statuses all final)
     const int passes = ctx->tune_nif_passes ? (int)ctx->tune_nif_passes : kMaxPasses;
+    std::vector<const uint8_t*> rp;
+    std::vector<uint64_t> rl;
+    std::vector<int32_t> rst;
     for (int pass = 0; pass < passes && !resolved; ++pass) {
-        if (!K.etf || K.stale) {
-            if (!K.etf && m) {
-                // nothing registered yet: register this call's operands first
-                std::vector<int32_t> rst;
-                if (int s = register_payloads(ctx, S, K, c.p, c.len, &rst)) return s;
-                registered = true;
-                for (uint32_t i = 0; i < m; ++i)
-                    if (rst[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+        for (size_t g = 0; g < G; ++g) {
+            KindState& K = *c.groups[g].K;
+            if (K.etf && !K.stale) continue;
+            const uint32_t p0 = c.groups[g].p0, p1 = c.groups[g].p1;
+            if (!K.etf && p1 > p0) {
+                // nothing registered yet: register this group's operands first
+                slice(p0, p1, &rp, &rl);
+                if (int s = register_payloads(ctx, S, K, rp, rl, &rst)) return s;
+                registered[g] = 1;
+                for (uint32_t i = p0; i < p1; ++i)
+                    if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
             }
             if (!patch_etf(ctx, S, K))
                 if (int s = rebuild_etf(ctx, S, K)) return s;
         }
-        int s = device_pass(ctx, S, K, c);
+        int s = device_pass(ctx, S, c);
         if (s == -1000) continue;                // answer area grown: once more
         if (s) return s;
         bool redo = false;
@@ -830,57 +1033,68 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         std::vector<uint32_t> unknown;
         for (uint32_t i = 0; i < m; ++i) {
             if (fallback[answer_of(i)]) continue;
-            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && (!registered || partial)) unknown.push_back(i);
-            else if (c.st[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && (!registered[group_of(i)] || partial))
+                unknown.push_back(i);
+            else if (c.st[i] != LASPJ_DEC_OK)
+                fallback[answer_of(i)] = 1;
         }
         if (unknown.empty()) {
             resolved = true;
             break;
         }
-        if (!registered && c.has_seg && register_segments(S, K, c, unknown)) {
+        bool fresh = true;            // no group of an unknown operand registered yet
+        for (uint32_t i : unknown) fresh &= !registered[group_of(i)];
+        if (fresh && c.has_seg && register_segments(S, c, unknown)) {
             // the failing segments' elements registered; if the next pass still meets an
             // unknown term, the whole operands are registered after all
             partial = true;
-            registered = true;
+            for (uint32_t i : unknown) registered[group_of(i)] = 1;
             continue;
         }
         partial = false;
-        // terms the dictionary has not seen (or operands that are not orddicts, which the
-        // second pass tells apart): register the operands that met them (an operand that
-        // decoded holds only registered terms)
-        std::vector<const uint8_t*> rp;
-        std::vector<uint64_t> rl;
-        std::vector<uint32_t> ri;
-        for (uint32_t i : unknown) {
-            rp.push_back(c.p[i]);
-            rl.push_back(c.len[i]);
-            ri.push_back(i);
-        }
-        uint32_t nd = 0;
-        uint64_t eb, tb;
-        std::vector<int32_t> rst;
-        if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
-        bool full = false;
-        for (int32_t x : rst) full |= x == LASPJ_DEC_UNREPRESENTABLE;
-        laspj_dict_info(K.dict, &nd, &eb, &tb);
-        if (may_reset && ((full && nd) || nd > kMaxDictElements)) {
-            // an element's 64 token slots used up by earlier calls (or a dictionary grown
-            // past its bound): start a fresh dictionary holding this call's terms only —
-            // image calls are self-contained (images in, images out); resident variables
-            // are written out to their images first and decoded again when next used
-            if (int s2 = reset_dict(ctx, S, K)) return s2;
-            if (int s2 = register_payloads(ctx, S, K, c.p, c.len, &rst)) return s2;
-            for (uint32_t i = 0; i < m; ++i)
-                if (rst[i] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
-            for (laspj_var* v : c.vars) {             // write/4's own variable: new cells
-                v->epoch = K.epoch;
-                v->resident = true;
+        // terms a dictionary has not seen (or operands that are not orddicts, which the
+        // second pass tells apart): each group registers its operands that met them (an
+        // operand that decoded holds only registered terms)
+        for (size_t g = 0; g < G; ++g) {
+            KindState& K = *c.groups[g].K;
+            const uint32_t p0 = c.groups[g].p0, p1 = c.groups[g].p1;
+            std::vector<uint32_t> ri;
+            rp.clear();
+            rl.clear();
+            for (uint32_t i : unknown)
+                if (i >= p0 && i < p1) {
+                    rp.push_back(c.p[i]);
+                    rl.push_back(c.len[i]);
+                    ri.push_back(i);
+                }
+            if (ri.empty()) continue;
+            uint32_t nd = 0;
+            uint64_t eb, tb;
+            if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
+            bool full = false;
+            for (int32_t x : rst) full |= x == LASPJ_DEC_UNREPRESENTABLE;
+            laspj_dict_info(K.dict, &nd, &eb, &tb);
+            if (may_reset && ((full && nd) || nd > kMaxDictElements)) {
+                // an element's 64 token slots used up by earlier calls (or a dictionary grown
+                // past its bound): start a fresh dictionary holding this group's terms only —
+                // image calls are self-contained (images in, images out); the namespace's
+                // resident variables are written out to their images first and decoded again
+                // when next used
+                if (int s2 = reset_dict(ctx, S, K)) return s2;
+                slice(p0, p1, &rp, &rl);
+                if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
+                for (uint32_t i = p0; i < p1; ++i)
+                    if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
+                for (uint32_t i = p0; i < p1 && i < c.vars.size(); ++i) {
+                    c.vars[i]->epoch = K.epoch;           // write/4's own variable: new cells
+                    c.vars[i]->resident = true;
+                }
+            } else {
+                for (size_t k = 0; k < ri.size(); ++k)
+                    if (rst[k] != LASPJ_DEC_OK) fallback[answer_of(ri[k])] = 1;
             }
-        } else {
-            for (size_t k = 0; k < ri.size(); ++k)
-                if (rst[k] != LASPJ_DEC_OK) fallback[answer_of(ri[k])] = 1;
+            registered[g] = 1;
         }
-        registered = true;
     }
     // post-condition: an answer is OK only from a pass whose statuses were all final; a
     // call whose passes ran out (the answer area grown, a segment chain only a serial
@@ -908,9 +1122,10 @@ NifState* state(laspj_ctx* ctx) {
 // cells again: write/4 of that image.  *ok: the variable is resident over the current
 // dictionary (false: it stays host-held; its calls answer FALLBACK)
 int hydrate(laspj_ctx* ctx, NifState* S, laspj_var* v, bool* ok) {
-    KindState& K = kstate(S, v->kind);
+    KindState& K = *v->ns;
     *ok = v->resident && v->epoch == K.epoch;
-    if (*ok || v->image.empty()) return LASPJ_OK;
+    // (a value write/4 could not represent stays an image until the next write)
+    if (*ok || v->image.empty() || v->held) return LASPJ_OK;
     const std::vector<uint8_t> img = v->image;
     Call c;
     c.op = Op::WRITE;
@@ -919,6 +1134,7 @@ int hydrate(laspj_ctx* ctx, NifState* S, laspj_var* v, bool* ok) {
     c.p.push_back(img.data());
     c.len.push_back(img.size());
     c.vars.push_back(v);
+    one_group(c, &K);
     {
         Guard g(ctx);
         release_cells(ctx, v);
@@ -937,11 +1153,19 @@ int hydrate(laspj_ctx* ctx, NifState* S, laspj_var* v, bool* ok) {
     // (a reset inside the call may have written the empty cells out over the image)
     v->image = img;
     v->resident = false;
+    v->held = s == LASPJ_OK;
     {
         Guard g(ctx);
         release_cells(ctx, v);
     }
     return s;
+}
+
+// a namespace's dictionary and device images dropped (the context still alive)
+void free_ns(KindState& K) {
+    free_etf(K);
+    if (K.dict) laspj_dict_destroy(K.dict);
+    K.dict = nullptr;
 }
 
 }  // namespace
@@ -951,19 +1175,24 @@ void nif_destroy(laspj_ctx* ctx) {
     if (!S) return;
     {
         std::lock_guard<std::mutex> lk(S->mu);
-        Guard g(ctx);
+        {
+            Guard g(ctx);
+            for (laspj_var* v : S->vars) {
+                // the variables' cells go with the context (the cache it frees next)
+                release_cells(ctx, v);
+                v->ctx = nullptr;
+                v->resident = false;
+            }
+        }
+        // their namespaces' device images too (a variable outliving its context keeps only
+        // the host side, which its destroy frees)
         for (laspj_var* v : S->vars) {
-            // the variables' cells go with the context (the cache it frees next)
-            release_cells(ctx, v);
-            v->ctx = nullptr;
-            v->resident = false;
+            free_ns(*v->ns);
+            v->ns->vars.clear();
         }
         S->vars.clear();
     }
-    for (KindState& K : S->ks) {
-        if (K.etf) laspj_etf_dict_destroy(K.etf);
-        if (K.dict) laspj_dict_destroy(K.dict);
-    }
+    for (KindState& K : S->ks) free_ns(K);
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     if (S->dblk) hipFree(S->dblk);
@@ -1005,6 +1234,7 @@ int pair_call(laspj_ctx* ctx, laspj::NifState* S, int32_t kind, laspj::Op op, in
             c->len[n + i] = nb[i];
         }
     }
+    laspj::one_group(*c, &laspj::kstate(S, kind));
     return laspj::run(ctx, S, *c, verdict);
 }
 
@@ -1072,6 +1302,7 @@ int var_image_call(laspj_var* var, bool value, const uint8_t** out, uint64_t* ou
     c.n = 1;
     c.m = 0;
     c.vars.push_back(var);
+    laspj::one_group(c, var->ns.get());
     std::vector<int32_t> vd;
     if (int s = laspj::run(ctx, S, c, &vd)) return s;
     *verdict = vd[0];
@@ -1165,6 +1396,62 @@ int laspj_gset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
 
 // ---------------------------------------------------------------- resident variables
 
+}  // extern "C"
+
+namespace {
+
+// a variable in namespace `ns` (a fresh one when null); call with S->mu held
+int var_new(laspj_ctx* ctx, laspj::NifState* S, int32_t kind,
+            std::shared_ptr<laspj::KindState> ns, laspj_var** out) {
+    auto* v = new (std::nothrow) laspj_var;
+    if (!v) return fail(ctx, LASPJ_E_NOMEM, "var_create: host allocation");
+    v->ctx = ctx;
+    v->kind = kind;
+    try {
+        if (!ns) {
+            ns = std::make_shared<laspj::KindState>();
+            ns->kind = kind;
+        }
+        v->ns = ns;
+        if (!ns->dict && laspj::reset_dict(ctx, S, *ns)) {
+            delete v;
+            return LASPJ_E_NOMEM;
+        }
+        v->epoch = ns->epoch;         // new(): no cells until the first call sizes them
+        S->vars.insert(v);
+        try {
+            ns->vars.insert(v);
+        } catch (const std::bad_alloc&) {
+            S->vars.erase(v);
+            throw;
+        }
+    } catch (const std::bad_alloc&) {
+        delete v;
+        return fail(ctx, LASPJ_E_NOMEM, "var_create: registry");
+    }
+    *out = v;
+    return LASPJ_OK;
+}
+
+// the tokens unique/1 mints (lasp_orset.erl:261-262: crypto:strong_rand_bytes(20)), from the
+// kernel's CSPRNG
+bool strong_rand(uint8_t* p, size_t n) {
+    while (n) {
+        const ssize_t r = getrandom(p, n, 0);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        p += r;
+        n -= (size_t)r;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
 int laspj_var_create(laspj_ctx* ctx, int32_t kind, laspj_var** out) {
     if (!ctx || !out) return LASPJ_E_INVAL;
     *out = nullptr;
@@ -1172,25 +1459,18 @@ int laspj_var_create(laspj_ctx* ctx, int32_t kind, laspj_var** out) {
         return fail(ctx, LASPJ_E_KIND, "var_create: OR-Set or G-Set variables");
     laspj::NifState* S = laspj::state(ctx);
     if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
-    auto* v = new (std::nothrow) laspj_var;
-    if (!v) return fail(ctx, LASPJ_E_NOMEM, "var_create: host allocation");
-    v->ctx = ctx;
-    v->kind = kind;
     std::lock_guard<std::mutex> lk(S->mu);
-    laspj::KindState& K = laspj::kstate(S, kind);
-    if (!K.dict && laspj::reset_dict(ctx, S, K)) {
-        delete v;
-        return LASPJ_E_NOMEM;
-    }
-    v->epoch = K.epoch;               // new(): no cells until the first call sizes them
-    try {
-        S->vars.insert(v);
-    } catch (const std::bad_alloc&) {
-        delete v;
-        return fail(ctx, LASPJ_E_NOMEM, "var_create: registry");
-    }
-    *out = v;
-    return LASPJ_OK;
+    return var_new(ctx, S, kind, nullptr, out);
+}
+
+int laspj_var_create_replica(laspj_var* peer, laspj_var** out) {
+    laspj::NifState* S = var_state(peer);
+    if (!S || !out) return LASPJ_E_INVAL;
+    *out = nullptr;
+    laspj_ctx* ctx = peer->ctx;
+    std::lock_guard<std::mutex> lk(S->mu);
+    if (!S->vars.count(peer)) return fail(ctx, LASPJ_E_INVAL, "var_create_replica: unknown variable");
+    return var_new(ctx, S, peer->kind, peer->ns, out);
 }
 
 int laspj_var_destroy(laspj_var* v) {
@@ -1200,10 +1480,18 @@ int laspj_var_destroy(laspj_var* v) {
         if (S) {
             std::lock_guard<std::mutex> lk(S->mu);
             S->vars.erase(v);
-            std::lock_guard<std::mutex> lk2(v->ctx->mu);
-            hipSetDevice(v->ctx->device);
-            laspj::release_cells(v->ctx, v);
+            v->ns->vars.erase(v);
+            {
+                std::lock_guard<std::mutex> lk2(v->ctx->mu);
+                hipSetDevice(v->ctx->device);
+                laspj::release_cells(v->ctx, v);
+            }
+            // the namespace's last variable: its device images go too
+            if (v->ns.use_count() == 1) laspj::free_ns(*v->ns);
         }
+    } else if (v->ns && v->ns.use_count() == 1 && v->ns->dict) {
+        laspj_dict_destroy(v->ns->dict);         // (its device images went with the context)
+        v->ns->dict = nullptr;
     }
     delete v;
     return LASPJ_OK;
@@ -1241,19 +1529,27 @@ int laspj_var_etf_bind_many(laspj_ctx* ctx, uint32_t n, laspj_var* const* vars,
         verdict[i] = LASPJ_NIF_FALLBACK;
         status[i] = 0;
     }
-    const laspj::KindState& K = laspj::kstate(S, kind);
     std::vector<uint32_t> live;
     for (uint32_t i = 0; i < n; ++i)
-        if (vars[i]->resident && vars[i]->epoch == K.epoch) live.push_back(i);
+        if (vars[i]->resident && vars[i]->epoch == vars[i]->ns->epoch) live.push_back(i);
     if (live.empty()) return LASPJ_OK;
+    // one decode per namespace (its own dictionary): the payloads grouped by namespace
+    std::stable_sort(live.begin(), live.end(), [&](uint32_t x, uint32_t y) {
+        return std::less<const laspj::KindState*>()(vars[x]->ns.get(), vars[y]->ns.get());
+    });
     laspj::Call c;
     c.op = laspj::Op::BIND;
     c.kind = kind;
     c.n = c.m = (uint32_t)live.size();
-    for (uint32_t i : live) {
+    for (uint32_t k = 0; k < live.size(); ++k) {
+        const uint32_t i = live[k];
         c.p.push_back(values[i]);
         c.len.push_back(lens[i]);
         c.vars.push_back(vars[i]);
+        if (k == 0 || vars[live[k - 1]]->ns != vars[i]->ns)
+            c.groups.push_back(laspj::Group{vars[i]->ns.get(), k, k + 1});
+        else
+            c.groups.back().p1 = k + 1;
     }
     std::vector<int32_t> vd;
     if (int s = laspj::run(ctx, S, c, &vd)) return s;
@@ -1277,12 +1573,18 @@ int laspj_var_etf_write(laspj_var* var, const uint8_t* value, uint64_t n, int32_
     if ((!value && n) || !verdict) return fail(ctx, LASPJ_E_INVAL, "var_write: null argument");
     std::lock_guard<std::mutex> lk(S->mu);
     if (!S->vars.count(var)) return fail(ctx, LASPJ_E_INVAL, "var_write: unknown variable");
-    laspj::KindState& K = laspj::kstate(S, var->kind);
+    laspj::KindState& K = *var->ns;
     if (!K.dict && laspj::reset_dict(ctx, S, K)) return LASPJ_E_NOMEM;
-    // write/4 replaces the value: the old cells (or image) are not read
+    // write/4 replaces the value: the old cells (or image) are not read — but a write that
+    // fails with an error status (no memory, a device error) leaves the variable as it was
+    const bool was_resident = var->resident, was_held = var->held;
+    const uint64_t was_epoch = var->epoch;
+    std::vector<uint8_t> was_image;
+    was_image.swap(var->image);
+    const bool had_cells = was_resident && was_epoch == K.epoch;
     var->resident = true;
+    var->held = false;
     var->epoch = K.epoch;
-    var->image.clear();
     laspj::Call c;
     c.op = laspj::Op::WRITE;
     c.kind = var->kind;
@@ -1290,8 +1592,33 @@ int laspj_var_etf_write(laspj_var* var, const uint8_t* value, uint64_t n, int32_
     c.p.push_back(value);
     c.len.push_back(n);
     c.vars.push_back(var);
+    laspj::one_group(c, &K);
     std::vector<int32_t> vd;
-    if (int s = laspj::run(ctx, S, c, &vd)) return s;
+    const int s = laspj::run(ctx, S, c, &vd);
+    auto drop_cells = [&] {
+        std::lock_guard<std::mutex> lk2(ctx->mu);
+        hipSetDevice(ctx->device);
+        laspj::release_cells(ctx, var);
+    };
+    if (s) {
+        // the write never answered (no memory, a device error): the old value stands
+        if (!var->image.empty()) {
+            // a reset inside the call wrote the old cells out: the image is the old value
+            drop_cells();
+            var->resident = false;
+            var->held = false;
+        } else if (had_cells) {
+            var->epoch = was_epoch;   // the old cells (widened, perhaps): the old value
+            var->held = was_held;
+        } else {
+            drop_cells();             // host-held before: cells the call sized are dropped
+            var->resident = was_resident;
+            var->epoch = was_epoch;
+            var->held = was_held;
+            var->image.swap(was_image);
+        }
+        return s;
+    }
     *verdict = vd[0];
     if (vd[0] == LASPJ_NIF_OK) {
         var->image.clear();       // (a reset inside the call wrote the old cells out)
@@ -1305,9 +1632,8 @@ int laspj_var_etf_write(laspj_var* var, const uint8_t* value, uint64_t n, int32_
         return fail(ctx, LASPJ_E_NOMEM, "var_write: host image");
     }
     var->resident = false;
-    std::lock_guard<std::mutex> lk2(ctx->mu);
-    hipSetDevice(ctx->device);
-    laspj::release_cells(ctx, var);
+    var->held = true;
+    drop_cells();
     return LASPJ_OK;
 }
 
@@ -1342,6 +1668,7 @@ int laspj_var_etf_threshold(laspj_var* var, const uint8_t* threshold, uint64_t n
     c.p.push_back(threshold);
     c.len.push_back(n);
     c.vars.push_back(var);
+    laspj::one_group(c, var->ns.get());
     std::vector<int32_t> vd;
     if (int s = laspj::run(ctx, S, c, &vd)) return s;
     *verdict = vd[0];
@@ -1355,6 +1682,175 @@ int laspj_var_resident(const laspj_var* var, int32_t* resident) {
     return LASPJ_OK;
 }
 
+int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_t* result,
+                         const uint8_t** err_elem, uint64_t* err_len, const uint8_t** minted,
+                         uint32_t* nminted, int32_t* verdict) {
+    laspj::NifState* S = var_state(var);
+    if (!S) return LASPJ_E_INVAL;
+    laspj_ctx* ctx = var->ctx;
+    if (!op || !nop || !result || !verdict)
+        return fail(ctx, LASPJ_E_INVAL, "var_update: null argument");
+    std::lock_guard<std::mutex> lk(S->mu);
+    if (!S->vars.count(var)) return fail(ctx, LASPJ_E_INVAL, "var_update: unknown variable");
+    ++S->stats[0];
+    *result = LASPJ_UPDATE_OK;
+    *verdict = LASPJ_NIF_FALLBACK;
+    if (err_elem) *err_elem = nullptr;
+    if (err_len) *err_len = 0;
+    if (minted) *minted = nullptr;
+    if (nminted) *nminted = 0;
+    bool ok = false;
+    if (int s = laspj::hydrate(ctx, S, var, &ok)) return s;
+    auto fallback = [&] {
+        ++S->stats[6];
+        return LASPJ_OK;
+    };
+    if (!ok) return fallback();
+    // Type:update(Op, Actor, Value0) (lasp_core.erl:283-287): the op's terms
+    std::vector<laspj::UpdateOp> ops;
+    const int ps = laspj::parse_update_op(var->kind, op, nop, &ops);
+    if (ps == LASPJ_E_NOMEM) return fail(ctx, LASPJ_E_NOMEM, "var_update: host allocation");
+    if (ps != LASPJ_DEC_OK || ops.size() > (1u << 24)) return fallback();
+    if (ops.empty()) {
+        // {add_all, []}, {remove_all, []}, {update, []}: {ok, Value0}
+        *verdict = LASPJ_NIF_OK;
+        return LASPJ_OK;
+    }
+    const bool orset = var->kind == LASPJ_KIND_ORSET;
+    laspj::KindState& K = *var->ns;
+    if (!K.dict && laspj::reset_dict(ctx, S, K)) return LASPJ_E_NOMEM;
+    uint32_t nmint = 0;
+    for (const auto& o : ops) nmint += o.mint ? 1u : 0u;
+    S->minted.resize(20ull * nmint);
+    if (nmint && !strong_rand(S->minted.data(), S->minted.size()))
+        return fail(ctx, LASPJ_E_DEVICE, "var_update: getrandom failed (%d)", errno);
+    // the terms registered in the variable's namespace (element slots, token slots); the
+    // whole call's registrations undone when one is refused
+    const uint64_t t0 = laspj::now_ns();
+    const uint32_t nd0 = laspj::dict_elements(K.dict);
+    std::vector<laspj_op> dops(ops.size());
+    bool any_remove = false, registered = false;
+    uint8_t timg[25] = {109, 0, 0, 0, 20};       // BINARY_EXT of 20 bytes
+    laspj::dict_begin(K.dict);
+    uint32_t mi = 0;
+    for (size_t k = 0; k < ops.size(); ++k) {
+        const laspj::UpdateOp& o = ops[k];
+        laspj_op& d = dops[k];
+        d = laspj_op{};
+        d.kind = o.kind;
+        d.flags = k == 0 ? LASPJ_OP_FLAG_NEW_CALL : 0;
+        const auto* eimg = reinterpret_cast<const uint8_t*>(o.elem.data());
+        if (o.kind == LASPJ_OP_REMOVE) {
+            // orddict:find/2 (lasp_orset.erl:233): absent unless the namespace holds it
+            const int64_t e = laspj::dict_find_elem(K.dict, eimg, o.elem.size());
+            if (e == -2) {
+                laspj::dict_rollback(K.dict);
+                return fallback();            // an `==`-equal key under another image
+            }
+            d.element = e < 0 ? laspj::kNoElem : (uint32_t)e;
+            any_remove = true;
+            continue;
+        }
+        uint32_t e = 0, t = 0;
+        int st = laspj::dict_reg_elem(K.dict, eimg, o.elem.size(), &e);
+        if (st == LASPJ_DEC_OK && orset) {
+            const uint8_t* tp;
+            size_t tl;
+            if (o.mint) {
+                std::memcpy(timg + 5, S->minted.data() + 20ull * mi++, 20);
+                tp = timg;
+                tl = sizeof(timg);
+            } else {
+                tp = reinterpret_cast<const uint8_t*>(o.tok.data());
+                tl = o.tok.size();
+            }
+            const uint32_t had = laspj::dict_token_count(K.dict, e);
+            st = laspj::dict_reg_tok(K.dict, e, tp, tl, &t);
+            registered |= laspj::dict_token_count(K.dict, e) != had;
+        }
+        if (st == LASPJ_E_NOMEM) {
+            laspj::dict_rollback(K.dict);
+            return fail(ctx, LASPJ_E_NOMEM, "var_update: registration");
+        }
+        if (st != LASPJ_DEC_OK) {
+            // a 65th token on an element, an `==`-equal term under another image: the
+            // reference's clause on the NIF side
+            laspj::dict_rollback(K.dict);
+            return fallback();
+        }
+        d.element = e;
+        d.slot = (uint8_t)t;
+    }
+    laspj::dict_begin(K.dict);                    // (the journal kept nothing)
+    registered |= laspj::dict_elements(K.dict) != nd0;
+    if (registered) {
+        ++S->stats[2];
+        K.stale = true;
+    }
+    S->stats[12] += laspj::now_ns() - t0;
+    // the device images learn the new terms now (a token on a known element is patched in
+    // place), so the next bind of a state carrying them decodes in one pass
+    if (K.stale || !K.etf)
+        if (!laspj::patch_etf(ctx, S, K))
+            if (int s = laspj::rebuild_etf(ctx, S, K)) return s;
+    const uint32_t nops = (uint32_t)dops.size();
+    bool all_add = !any_remove;
+    int32_t* dstat = nullptr;
+    {
+        laspj::Guard g(ctx);
+        if (int s = laspj::fit_var(ctx, var, K.E)) return s;
+        laspj::UpdArgs args;
+        std::memset(&args, 0, sizeof(args));
+        const laspj_op* dev_ops = nullptr;
+        void* blk = nullptr;
+        const uint64_t stat_bytes = any_remove ? 4ull * nops : 0;
+        const uint64_t ops_bytes = nops > laspj::kUpdArgOps ? 16ull * nops : 0;
+        if (stat_bytes + ops_bytes) {
+            if (laspj::dev_alloc(ctx, ((stat_bytes + 255) & ~255ull) + ops_bytes, &blk) != hipSuccess) {
+                hipGetLastError();
+                return fail(ctx, LASPJ_E_NOMEM, "var_update: op buffer");
+            }
+            dstat = static_cast<int32_t*>(blk);
+            if (ops_bytes) {
+                auto* p = reinterpret_cast<laspj_op*>(static_cast<uint8_t*>(blk) +
+                                                      ((stat_bytes + 255) & ~255ull));
+                LJ_HIP(ctx, hipMemcpyAsync(p, dops.data(), ops_bytes, hipMemcpyHostToDevice,
+                                           ctx->stream));
+                dev_ops = p;
+            }
+        }
+        if (!dev_ops) std::memcpy(args.op, dops.data(), 16ull * nops);
+        if (all_add && dev_ops) {
+            hipLaunchKernelGGL(laspj::k_var_adds, dim3((nops + 255) / 256), dim3(256), 0,
+                               ctx->stream, var->cells, var->kind, dev_ops, nops);
+        } else {
+            hipLaunchKernelGGL(laspj::k_var_update, dim3(1), dim3(64), 0, ctx->stream, var->cells,
+                               var->kind, args, dev_ops, nops, any_remove ? dstat : nullptr);
+        }
+        LJ_LAUNCHED(ctx);
+        std::vector<int32_t> st;
+        if (any_remove) {
+            // a precondition may fail: its statuses back (one synchronisation)
+            st.resize(nops);
+            LJ_HIP(ctx, laspj::readback(ctx, st.data(), dstat, 4ull * nops));
+        }
+        if (blk) laspj::dev_release(ctx, blk, ((stat_bytes + 255) & ~255ull) + ops_bytes);
+        for (uint32_t k = 0; k < st.size(); ++k)
+            if (st[k] == LASPJ_OPST_NOT_PRESENT) {
+                // {error, {precondition, {not_present, Elem}}} (lasp_orset.erl:239-240)
+                *result = LASPJ_UPDATE_NOT_PRESENT;
+                S->err_elem = ops[k].elem;
+                if (err_elem) *err_elem = reinterpret_cast<const uint8_t*>(S->err_elem.data());
+                if (err_len) *err_len = S->err_elem.size();
+                break;
+            }
+    }
+    if (minted) *minted = S->minted.empty() ? nullptr : S->minted.data();
+    if (nminted) *nminted = nmint;
+    *verdict = LASPJ_NIF_OK;
+    return LASPJ_OK;
+}
+
 // ---------------------------------------------------------------- counters
 
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n) {
@@ -1364,11 +1860,21 @@ int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n) {
     std::lock_guard<std::mutex> lk(S->mu);
     for (uint32_t i = 0; i < n && i < LASPJ_NIF_STATS; ++i) out[i] = S->stats[i];
     if (n > 7) {
-        uint32_t e = 0, g = 0;  // [7] is the dictionaries' size, not a counter
-        uint64_t eb, tb;
-        if (S->ks[0].dict) laspj_dict_info(S->ks[0].dict, &e, &eb, &tb);
-        if (S->ks[1].dict) laspj_dict_info(S->ks[1].dict, &g, &eb, &tb);
-        out[7] = (uint64_t)e + g;
+        // [7] is the dictionaries' size, not a counter: the image calls' and every
+        // namespace's
+        uint64_t tot = 0;
+        std::unordered_set<const laspj::KindState*> seen;
+        auto add = [&](const laspj::KindState* K) {
+            uint32_t e = 0;
+            uint64_t eb, tb;
+            if (K->dict && seen.insert(K).second) {
+                laspj_dict_info(K->dict, &e, &eb, &tb);
+                tot += e;
+            }
+        };
+        for (const laspj::KindState& K : S->ks) add(&K);
+        for (const laspj_var* v : S->vars) add(v->ns.get());
+        out[7] = tot;
     }
     return LASPJ_OK;
 }
@@ -1380,6 +1886,12 @@ int laspj_nif_reset(laspj_ctx* ctx) {
     std::lock_guard<std::mutex> lk(S->mu);
     for (laspj::KindState& K : S->ks)
         if (int s = laspj::reset_dict(ctx, S, K)) return s;
+    std::unordered_set<laspj::KindState*> seen;
+    std::vector<std::shared_ptr<laspj::KindState>> nss;
+    for (laspj_var* v : S->vars)
+        if (seen.insert(v->ns.get()).second) nss.push_back(v->ns);
+    for (auto& ns : nss)
+        if (int s = laspj::reset_dict(ctx, S, *ns)) return s;
     return LASPJ_OK;
 }
 

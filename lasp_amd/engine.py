@@ -187,7 +187,8 @@ class Context:
         return int(verd.value), int(st.value), img
 
     def var(self, kind: str = "orset") -> "NifVar":
-        """A device-resident variable (laspj_var_create): #dv.value kept on the device."""
+        """A device-resident variable (laspj_var_create): #dv.value kept on the device, in a
+        token namespace of its own."""
         return NifVar(self, kind)
 
     def var_bind_many(self, pairs):
@@ -233,11 +234,34 @@ class NifVar:
     "resident variables").  Every call returns (verdict, answer) like the NIF image calls;
     answer is None on NIF_FALLBACK."""
 
-    def __init__(self, ctx: Context, kind: str = "orset"):
+    def __init__(self, ctx: Context, kind: str = "orset", peer: "NifVar" = None):
         self.ctx, self.L, self.kind = ctx, ctx.L, kind
         self.h = C.c_void_p()
+        if peer is not None:
+            self.kind = peer.kind
+            check(self.L.laspj_var_create_replica(peer.h, C.byref(self.h)), ctx.h)
+            return
         k = _lib.KIND_GSET if kind == "gset" else _lib.KIND_ORSET
         check(self.L.laspj_var_create(ctx.h, k, C.byref(self.h)), ctx.h)
+
+    def replica(self) -> "NifVar":
+        """laspj_var_create_replica: another replica in this variable's namespace."""
+        return NifVar(self.ctx, peer=self)
+
+    def update(self, op_img: bytes):
+        """lasp_core:update/4 (laspj_var_etf_update): (verdict, result, error element image
+        or None, [minted tokens]) — result 0 ok, 1 {error, {precondition, {not_present, E}}}."""
+        res, verd, n = C.c_int32(), C.c_int32(), C.c_uint32()
+        eimg, elen, mint = C.c_void_p(), C.c_uint64(), C.c_void_p()
+        op_img = bytes(op_img)
+        check(self.L.laspj_var_etf_update(self.h, op_img, len(op_img), C.byref(res),
+                                          C.byref(eimg), C.byref(elen), C.byref(mint),
+                                          C.byref(n), C.byref(verd)), self.ctx.h)
+        if verd.value != 0:
+            return int(verd.value), None, None, []
+        err = C.string_at(eimg, elen.value) if res.value == 1 else None
+        raw = C.string_at(mint, 20 * n.value) if n.value else b""
+        return 0, int(res.value), err, [raw[20 * k:20 * k + 20] for k in range(n.value)]
 
     def close(self):
         if self.h:

@@ -1,0 +1,282 @@
+"""lasp_core:update/4 on resident variables (laspj_var_etf_update) and per-variable token
+namespaces (include/laspj.h "resident variables"; lasp_amd/csrc/laspj_nif.hip), against the
+oracle.
+
+update/4 (lasp_core.erl:283-287) is Type:update(Op, Actor, Value0) then bind/3 of the result:
+OR-Set ops {add, E} (a token minted by unique/1, lasp_orset.erl:261-262), {add_by_token, T,
+E}, {add_all, Es}, {remove, E}, {remove_all, Es}, {update, Ops} (:99-117, 222-259) and G-Set
+{add, E}, {add_all, Es} (lasp_gset.erl:84-88) run on the device cells; a failed precondition
+answers {error, {precondition, {not_present, E}}} and voids the whole call.  Minted tokens
+come back from the call, so the oracle replays the same update with them.
+
+Namespaces: each variable's dictionary holds its own value's terms, so a hundred variables
+holding element 1 with their own tokens never exhaust its 64 slots (include/lasp.hrl:60-63);
+replicas created in one namespace know each other's tokens, so a bind of a replica's state
+after an update decodes in one device pass.
+"""
+
+import functools
+import random
+
+import pytest
+
+from oracle import etf as oetf
+from oracle import gset as ogset
+from oracle import lattice as olat
+from oracle import orset as oorset
+from oracle.terms import Atom, compare, exact_eq
+
+OK, FALLBACK = 0, 1
+UPD_OK, NOT_PRESENT = 0, 1
+A = Atom
+_key = functools.cmp_to_key(compare)
+
+pytestmark = pytest.mark.gpu
+
+
+def _tb(t) -> bytes:
+    return oetf.term_to_binary(t)
+
+
+def _ctx():
+    from lasp_amd import engine
+    return engine.Context(0)
+
+
+def _oracle_update(mod, op, state, minted):
+    """Type:update/3 on the oracle with the tokens the device minted, in op order."""
+    it = iter(minted)
+    if mod is ogset:
+        return ogset.update(op, A("a"), state)
+    return oorset.update(op, A("a"), state, tokens=lambda _actor: next(it))
+
+
+def _elements(rng):
+    return list(range(12)) + [A(f"e{k}") for k in range(6)] + [f"s{k}".encode() for k in range(4)] + \
+        [(k, A("t")) for k in range(3)]
+
+
+def _rand_op(rng, elems, toks, depth=0):
+    k = rng.randrange(9 if depth == 0 else 7)
+    e = rng.choice(elems)
+    if k in (0, 1):
+        return (A("add"), e)
+    if k == 2:
+        return (A("add_by_token"), rng.choice(toks), e)
+    if k == 3:
+        return (A("add_all"), [rng.choice(elems) for _ in range(rng.randint(0, 4))])
+    if k in (4, 5):
+        return (A("remove"), e)
+    if k == 6:
+        return (A("remove_all"), [rng.choice(elems) for _ in range(rng.randint(0, 3))])
+    return (A("update"), [_rand_op(rng, elems, toks, depth + 1) for _ in range(rng.randint(0, 4))])
+
+
+def test_var_update_random_ops_match_oracle():
+    """300 random update/4 calls on a resident OR-Set variable (every op form, nested
+    {update, Ops}, removes of absent elements, re-adds by a known token): the result, the
+    failing element and the value read back agree with lasp_orset:update/3 replayed on the
+    oracle with the minted tokens; value/1 and threshold_met agree along the way."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(61)
+        elems = _elements(rng)
+        toks = [bytes(rng.getrandbits(8) for _ in range(20)) for _ in range(6)] + [A("tk"), 7]
+        var = ctx.var("orset")
+        cur = []
+        history = [[]]
+        counts = {UPD_OK: 0, NOT_PRESENT: 0}
+        for k in range(300):
+            op = _rand_op(rng, elems, toks)
+            verd, res, err, minted = var.update(_tb(op))
+            assert verd == OK, (k, op)
+            assert all(len(t) == 20 for t in minted)
+            want = _oracle_update(oorset, op, cur, minted)
+            if want[0] == "ok":
+                assert res == UPD_OK, (k, op)
+                cur = want[1]
+            else:
+                assert res == NOT_PRESENT, (k, op)
+                assert exact_eq(oetf.binary_to_term(bytes([131]) + err), want[1][1][1]), (k, op)
+            counts[res] += 1
+            if k % 7 == 0 or res == NOT_PRESENT:
+                assert var.read() == (OK, _tb(cur)), (k, op)
+            if k % 25 == 0:
+                assert var.value() == (OK, _tb(oorset.value(cur)))
+                th = rng.choice(history)
+                assert var.threshold(_tb(th)) == (OK, olat.threshold_met("lasp_orset", cur, th))
+                history.append(cur)
+        assert counts[UPD_OK] > 100 and counts[NOT_PRESENT] >= 5
+        assert var.read() == (OK, _tb(cur))
+        # a bind after updates: the merge of a state with the variable's own tokens
+        other = oorset.merge(cur, [(A("zz"), [(b"\x07" * 20, False)])])
+        assert var.bind(_tb(other)) == (OK, 1)
+        assert var.read() == (OK, _tb(other))
+    finally:
+        ctx.close()
+
+
+def test_var_update_preconditions_void_the_call():
+    """remove_elems / apply_ops stop at the first absent element and the reference returns
+    the error, not a state (lasp_orset.erl:232-259): nothing of the call lands, including
+    adds before the failing remove; an element added earlier in the same call is present."""
+    ctx = _ctx()
+    try:
+        var = ctx.var("orset")
+        t1, t2 = b"\x01" * 20, b"\x02" * 20
+        assert var.update(_tb((A("add_by_token"), t1, 1)))[:2] == (OK, UPD_OK)
+        before = [(1, [(t1, False)])]
+        for op, bad in (((A("remove"), 2), 2),
+                        ((A("remove_all"), [1, 2, 3]), 2),
+                        ((A("update"), [(A("add_by_token"), t2, 5), (A("remove"), 9)]), 9),
+                        ((A("update"), [(A("add"), 4), (A("remove_all"), [1, 4, 6])]), 6)):
+            verd, res, err, _m = var.update(_tb(op))
+            assert (verd, res) == (OK, NOT_PRESENT), op
+            assert oetf.binary_to_term(bytes([131]) + err) == bad
+            assert var.read() == (OK, _tb(before)), op
+        # add then remove of a new element in one call: present by the add
+        verd, res, _e, _m = var.update(_tb((A("update"), [(A("add_by_token"), t2, 5),
+                                                          (A("remove"), 5)])))
+        assert (verd, res) == (OK, UPD_OK)
+        want = oorset.merge(before, [(5, [(t2, True)])])
+        assert var.read() == (OK, _tb(want))
+        # a re-add by a known token clears its removed flag (orddict:store(Token, false, ..))
+        assert var.update(_tb((A("add_by_token"), t2, 5)))[:2] == (OK, UPD_OK)
+        assert var.read() == (OK, _tb(oorset.merge(before, [(5, [(t2, False)])])))
+    finally:
+        ctx.close()
+
+
+def test_var_update_gset_and_fallbacks():
+    """G-Set add / add_all (ordsets:add_element / union with from_list) against the oracle;
+    ops no clause takes (an unknown atom, a G-Set remove, a non-list add_all, an improper
+    list), a term `==` to a held one under another image (1.0 after 1) and an element's
+    65th token answer FALLBACK and leave the value as it was."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(5)
+        g = ctx.var("gset")
+        cur = []
+        for k in range(60):
+            if k % 3 == 0:
+                op = (A("add_all"), [rng.randrange(300) for _ in range(rng.randint(0, 6))] +
+                      ([A(f"a{k}")] if k % 2 else []))
+            else:
+                op = (A("add"), rng.choice([rng.randrange(300), A(f"g{k % 5}"), (k % 4, b"x")]))
+            verd, res, err, minted = g.update(_tb(op))
+            assert (verd, res, minted) == (OK, UPD_OK, []), op
+            cur = ogset.update(op, A("a"), cur)[1]
+            assert g.read() == (OK, _tb(cur)), (k, op)
+        assert g.update(_tb((A("add"), 1)))[:2] == (OK, UPD_OK)
+        cur = ogset.update((A("add"), 1), A("a"), cur)[1]
+        for op in ((A("remove"), 1), (A("add_all"), A("x")), (A("nope"), 1), (A("add"), 1.0)):
+            assert g.update(_tb(op))[0] == FALLBACK, op
+            assert g.read() == (OK, _tb(cur))
+        v = ctx.var("orset")
+        assert v.update(_tb((A("add_by_token"), b"t" * 20, 1)))[:2] == (OK, UPD_OK)
+        state = v.read()[1]
+        improper = _tb((A("add_all"), [1, 2]))[:-1] + bytes([97, 3])
+        for img in (_tb((A("add"), 1.0)), _tb((A("bogus"), 1)), _tb((A("add_by_token"), 1)),
+                    _tb((A("update"), [(A("add"), 2), (A("frob"), 3)])), improper,
+                    _tb((A("remove"), 1.0))):
+            assert v.update(img)[0] == FALLBACK, img
+            assert v.read() == (OK, state)
+        # 63 more tokens on element 1 fit; the 65th answers FALLBACK
+        for k in range(63):
+            assert v.update(_tb((A("add"), 1)))[:2] == (OK, UPD_OK), k
+        assert v.update(_tb((A("add"), 1)))[0] == FALLBACK
+        verd, img = v.read()
+        assert verd == OK and len(oetf.binary_to_term(img)[0][1]) == 64
+    finally:
+        ctx.close()
+
+
+def test_namespaces_hundred_variables_share_an_element():
+    """A vnode's 100 variables each add element 1 three times (300 distinct tokens for one
+    element across the context): no dictionary reset, no FALLBACK, and each value is its
+    own oracle state; binds of states carrying other variables' tokens stay in their own
+    namespaces."""
+    ctx = _ctx()
+    try:
+        s0 = ctx.nif_stats()
+        vs = [ctx.var("orset") for _ in range(100)]
+        cur = [[] for _ in vs]
+        for rnd in range(3):
+            for i, v in enumerate(vs):
+                verd, res, _e, minted = v.update(_tb((A("add"), 1)))
+                assert (verd, res) == (OK, UPD_OK), (rnd, i)
+                cur[i] = _oracle_update(oorset, (A("add"), 1), cur[i], minted)[1]
+        for i in range(0, 100, 7):
+            assert vs[i].read() == (OK, _tb(cur[i])), i
+        # variable 0 binds variable 1's state: 6 tokens on element 1 in variable 0
+        st, cur[0] = 1, oorset.merge(cur[0], cur[1])
+        assert vs[0].bind(_tb(cur[1])) == (OK, st)
+        assert vs[0].read() == (OK, _tb(cur[0]))
+        s1 = ctx.nif_stats()
+        assert s1["dict_resets"] == s0["dict_resets"]
+        assert s1["fallbacks"] == s0["fallbacks"]
+        assert s1["vars_spilled"] == s0["vars_spilled"]
+        # binds of many variables of different namespaces in one call
+        vals = [oorset.merge(cur[i], cur[(i + 1) % 100]) for i in range(100)]
+        got = ctx.var_bind_many(list(zip(vs, [_tb(x) for x in vals])))
+        for i in range(100):
+            want_st = 0 if exact_eq(cur[i], vals[i]) else 1
+            assert got[i] == (OK, want_st), i
+            cur[i] = vals[i]
+        for i in range(0, 100, 9):
+            assert vs[i].read() == (OK, _tb(cur[i])), i
+        assert ctx.nif_stats()["dict_resets"] == s0["dict_resets"]
+        for v in vs:
+            v.close()
+    finally:
+        ctx.close()
+
+
+def test_replicas_bind_each_others_updates_in_one_pass():
+    """Three replicas of one variable in one namespace (laspj_var_create_replica): every
+    update mints a token the namespace then knows, so replica B binding replica A's state
+    takes one device pass and registers nothing; the converged replicas equal the oracle's
+    merge of the three."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(17)
+        a = ctx.var("orset")
+        reps = [a, a.replica(), a.replica()]
+        cur = [[] for _ in reps]
+        elems = list(range(40))
+        for r, v in enumerate(reps):
+            for e in rng.sample(elems, 20):
+                verd, res, _e, minted = v.update(_tb((A("add"), e)))
+                assert (verd, res) == (OK, UPD_OK)
+                cur[r] = _oracle_update(oorset, (A("add"), e), cur[r], minted)[1]
+        imgs = [v.read()[1] for v in reps]
+        assert imgs == [_tb(c) for c in cur]
+        s0 = ctx.nif_stats()
+        orig = list(cur)
+        for r, v in enumerate(reps):
+            for q in range(3):
+                if q == r:
+                    continue
+                want_st = 0 if exact_eq(cur[r], orig[q]) else 1
+                assert v.bind(imgs[q]) == (OK, want_st)
+                cur[r] = oorset.merge(cur[r], orig[q])
+        s1 = ctx.nif_stats()
+        assert s1["device_passes"] - s0["device_passes"] == 6
+        assert s1["registrations"] == s0["registrations"]
+        for v, c in zip(reps, cur):
+            assert v.read() == (OK, _tb(c))
+        assert exact_eq(cur[0], cur[1]) and exact_eq(cur[1], cur[2])
+        # an update on one replica, a remove on another, then a bind each way
+        verd, res, _e, minted = reps[0].update(_tb((A("add"), 99)))
+        cur[0] = _oracle_update(oorset, (A("add"), 99), cur[0], minted)[1]
+        gone = cur[1][0][0]
+        assert reps[1].update(_tb((A("remove"), gone)))[:2] == (OK, UPD_OK)
+        cur[1] = _oracle_update(oorset, (A("remove"), gone), cur[1], [])[1]
+        s2 = ctx.nif_stats()
+        assert reps[1].bind(_tb(cur[0])) == (OK, 1)
+        assert reps[0].bind(_tb(cur[1])) == (OK, 1)
+        assert ctx.nif_stats()["registrations"] == s2["registrations"]
+        both = oorset.merge(cur[0], cur[1])
+        assert reps[0].read() == (OK, _tb(both)) and reps[1].read() == (OK, _tb(both))
+    finally:
+        ctx.close()

@@ -304,8 +304,10 @@ def test_var_write_unrepresentable_is_held_as_its_image():
 
 
 def test_var_survives_a_dictionary_reset():
-    """An image call that needs a fresh dictionary (an element whose 64 token slots earlier
-    calls used up) writes every resident variable out to its image first; each is decoded
+    """The image calls' dictionary resets (an element whose 64 token slots earlier calls used
+    up) without touching the variables, whose namespaces are their own.  A namespace that
+    needs a fresh dictionary — replicas writing values whose tokens on one element add up
+    past 64 — writes its resident variables out to their images first; each is decoded
     again on its next call and keeps binding exactly as the oracle does."""
     ctx = _ctx()
     try:
@@ -325,15 +327,29 @@ def test_var_survives_a_dictionary_reset():
             assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(oorset.merge(a, b)))
         s1 = ctx.nif_stats()
         assert s1["dict_resets"] > s0["dict_resets"]
-        assert s1["vars_spilled"] >= 3
+        assert s1["vars_spilled"] == s0["vars_spilled"]
+        for i, v in enumerate(vs):
+            assert v.resident
+            assert v.read() == (OK, _tb(cur[i])), i
+        # replicas in one namespace: 40 + 40 tokens on element 1 do not fit one dictionary
+        r0 = vs[0]
+        r1 = r0.replica()
+        toks = sorted(_tokens(rng, 80))
+        w1 = [(1, [(t, False) for t in toks[:40]])]
+        w2 = [(1, [(t, True) for t in toks[40:]])]
+        assert r1.write(_tb(w1)) == OK
+        assert r0.write(_tb(w2)) == OK           # the namespace resets: r1 spilled first
+        s2 = ctx.nif_stats()
+        assert s2["vars_spilled"] > s1["vars_spilled"]
+        assert r1.read() == (OK, _tb(w1))        # hydrated again (a reset of its own)
+        assert ctx.nif_stats()["vars_hydrated"] > s1["vars_hydrated"]
+        cur[0] = w2
         for i, v in enumerate(vs):
             assert v.read() == (OK, _tb(cur[i])), i
-            assert v.resident
             val = _orset(rng, elems, pool)
             st, cur[i] = _bind_oracle("lasp_orset", cur[i], val)
             assert v.bind(_tb(val)) == (OK, st)
             assert v.read() == (OK, _tb(cur[i]))
-        assert ctx.nif_stats()["vars_hydrated"] >= 3
     finally:
         ctx.close()
 
