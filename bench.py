@@ -557,6 +557,8 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     # hardware queues per process, GPU_MAX_HW_QUEUES; 16 = one per BEAM scheduler)
     for nthreads in (4, 16):
         out[f"bind_{nthreads}ctx"] = _bind_threads(ctx, nthreads, 60, ref, pb)
+    # 16 schedulers through one context: the group commit batches them
+    out["bind_16thr_1ctx"] = _bind_threads(ctx, 16, 60, ref, pb, shared=True)
     out["resident"] = ("Value0 = A ⊔ B resident (laspj_var); per bind: the %d-byte image of B "
                        "in, decode + `=:=` + merge on the device, the status out" % len(pb))
     for v in vs:
@@ -565,9 +567,11 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     return out
 
 
-def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes):
-    """nthreads BEAM schedulers, each with a context and a resident variable holding
-    A ⊔ B, binding B `per` times at once (lasp_vnode.erl:213-237: concurrent callers)."""
+def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: bool = False):
+    """nthreads BEAM schedulers, each with a resident variable holding A ⊔ B, binding B
+    `per` times at once (lasp_vnode.erl:213-237: concurrent callers) — each on a context
+    of its own, or (shared) all on one context, whose group commit batches the binds
+    queued while a pass runs into the next pass."""
     import ctypes as C
     import threading
     from lasp_amd._lib import check
@@ -577,7 +581,7 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes):
 
     def worker():
         try:
-            c2 = engine.Context(ctx.device)
+            c2 = ctx if shared else engine.Context(ctx.device)
             v2 = c2.var("orset")
             v2.write(ref)
             s2, d2 = C.c_int32(), C.c_int32()
@@ -590,7 +594,8 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes):
             if (d2.value, s2.value) != (0, 1):
                 errs.append("bad answer")
             v2.close()
-            c2.close()
+            if not shared:
+                c2.close()
         except Exception as e:       # noqa: BLE001 — reported below
             errs.append(repr(e))
             try:
@@ -610,7 +615,8 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes):
     if errs or len(spans) != nthreads:
         raise RuntimeError(f"config1: {nthreads}-context binds failed: {errs[:3]}")
     wall = max(b for _a, b in spans) - min(a for a, _b in spans)
-    return {"contexts": nthreads, "binds": nthreads * per,
+    return {"contexts": 1 if shared else nthreads, "threads": nthreads,
+            "binds": nthreads * per,
             "us_per_bind": wall * 1e6 / (nthreads * per),
             "binds_per_s": nthreads * per / wall,
             "merged_elements_per_s": nthreads * per * 10_000 / wall,

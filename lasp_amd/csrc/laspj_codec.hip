@@ -3459,13 +3459,15 @@ template <bool SMALL>
 __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg(
     const uint8_t* payload, u64 total, const u64* offs, uint64_t R, uint32_t E, DictView d,
     ReadTabs tabs, int tag, int vers, u64x2* cells, const uint32_t* segbase, uint64_t nseg,
-    uint32_t S, HdrHash hh, SegRes* res) {
+    uint32_t S, HdrHash hh, SegRes* res, SegList only) {
     __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     const Cases cs = lane_cases(lane);
     ReadLds& L = lds[wave];
-    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
+    const uint64_t count = only.n ? only.n : nseg;
+    for (uint64_t j = (uint64_t)blockIdx.x * (kBlock / 64) + wave; j < count; j += nwaves) {
+        const uint64_t g = only.n ? only.g[j] : j;
         const uint64_t rep = seg_replica(segbase, R, g);
         const uint32_t s = (uint32_t)(g - ufl32(segbase[rep]));
         seg_decode<SMALL>(payload, total, offs, rep, s, E, d, tabs, hh, tag, vers,
@@ -3536,13 +3538,15 @@ template <bool SMALL>
 __global__ __launch_bounds__(kBlock, 6) void k_orset_etf_read_seg_multi(
     const uint8_t* payload, u64 total, const u64* offs, uint64_t R, const DecTabs* dts,
     const uint32_t* pay_dt, int tag, int vers, const uint32_t* segbase, uint64_t nseg,
-    uint32_t S, SegRes* res) {
+    uint32_t S, SegRes* res, SegList only) {
     __shared__ __attribute__((aligned(16))) ReadLds lds[kBlock / 64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     const Cases cs = lane_cases(lane);
     ReadLds& L = lds[wave];
-    for (uint64_t g = (uint64_t)blockIdx.x * (kBlock / 64) + wave; g < nseg; g += nwaves) {
+    const uint64_t count = only.n ? only.n : nseg;
+    for (uint64_t j = (uint64_t)blockIdx.x * (kBlock / 64) + wave; j < count; j += nwaves) {
+        const uint64_t g = only.n ? only.g[j] : j;
         const uint64_t rep = seg_replica(segbase, R, g);
         const uint32_t k = ufl32(pay_dt[rep]);
         if ((dts[k].small != 0) != SMALL) continue;
@@ -4714,7 +4718,9 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
             const u64 v = WRITE ? b : (a | b);
             if (v != a) cur[w] = v;
         }
-        if (b) src[w] = 0;
+        // (an operand that did not decode keeps its cells: a redo pass of its failed
+        // segments completes them, laspj_nif.hip)
+        if (b && ok) src[w] = 0;
     }
     const bool any = __syncthreads_or(d != 0);
     if (threadIdx.x == 0) {
@@ -4786,7 +4792,7 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, co
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
                      const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
-                     bool clear, uint32_t* redo_zeroed, ChainJob* defer) {
+                     bool clear, uint32_t* redo_zeroed, ChainJob* defer, const SegList* only) {
     const uint64_t R = b->replicas;
     if (clear)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
@@ -4825,7 +4831,7 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                            dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
                            payload, (u64)payload_bytes, offs, R, b->elements, view(d), tabs, tag,
                            vers, reinterpret_cast<u64x2*>(b->dev), dsegbase, nseg,
-                           (uint32_t)plan.S, hh, dres);
+                           (uint32_t)plan.S, hh, dres, only ? *only : SegList{});
         LJ_LAUNCHED(ctx);
         if (deferred) {
             defer->payload = payload;
@@ -4921,7 +4927,8 @@ bool etf_multi_fill(const laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups, u
 int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
                            const void* dev_tabs, uint32_t npay, const uint8_t* payload,
                            uint64_t payload_bytes, const u64* offs, const EtfReadPlan& plan,
-                           const uint32_t* segbase, int32_t* status, ChainJob* defer) {
+                           const uint32_t* segbase, int32_t* status, ChainJob* defer,
+                           const SegList* only) {
     const DecTabs* dts = static_cast<const DecTabs*>(dev_tabs);
     const uint32_t* pd = reinterpret_cast<const uint32_t*>(
         static_cast<const char*>(dev_tabs) + ((sizeof(DecTabs) * ngroups + 15ull) & ~15ull));
@@ -4944,7 +4951,7 @@ int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
             hipLaunchKernelGGL(sm ? k_orset_etf_read_seg_multi<true> : k_orset_etf_read_seg_multi<false>,
                                dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
                                payload, (u64)payload_bytes, offs, R, dts, pd, -1, 1, segbase, nseg,
-                               (uint32_t)plan.S, dres);
+                               (uint32_t)plan.S, dres, only ? *only : SegList{});
             LJ_LAUNCHED(ctx);
         }
         if (deferred) {
@@ -5937,6 +5944,29 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
     hipSetDevice(ctx->device);
     const uint64_t rec_bytes = recs.size() * sizeof(PatchRec);
     const uint64_t total = data.size() + ((rec_bytes + 15) & ~15ull);
+    if (total <= laspj_ctx::kUpSmall) {
+        // a few elements' rows (an update's token, a bind's new tokens): through the pinned
+        // upload ring, with no wait for the stream's earlier work
+        data.resize(total, 0);
+        std::memcpy(data.data() + (total - ((rec_bytes + 15) & ~15ull)), recs.data(), rec_bytes);
+        const uint64_t dlen = total - ((rec_bytes + 15) & ~15ull);
+        const void* staged = stage_small(ctx, data.data(), total);
+        if (staged) {
+            if (int s = reserve_scratch(ctx, total)) return s;
+            char* dev = static_cast<char*>(ctx->scratch);
+            if (hipMemcpyAsync(dev, staged, total, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+                return LASPJ_E_DEVICE;
+            hipLaunchKernelGGL(k_patch, dim3((unsigned)std::min<uint64_t>(recs.size(), 4096)),
+                               dim3(kBlock), 0, ctx->stream, reinterpret_cast<const uint8_t*>(dev),
+                               reinterpret_cast<const PatchRec*>(dev + dlen),
+                               (uint32_t)recs.size(), static_cast<uint8_t*>(d->block));
+            if (hipGetLastError() != hipSuccess) return LASPJ_E_DEVICE;
+            for (const auto& nt : new_tpoff) d->h_tpoff[nt.first] = nt.second;
+            d->tpad_used = tpad_used;
+            return LASPJ_OK;
+        }
+        data.resize(dlen);
+    }
     hipStreamSynchronize(ctx->stream);                // the pinned staging is free
     if (ctx->dstage_bytes < total) {
         if (ctx->dstage) hipHostFree(ctx->dstage);

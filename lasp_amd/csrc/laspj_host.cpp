@@ -590,6 +590,9 @@ struct Dict {
     // a token), undone in reverse when the payload fails: binary_to_term/1 would have
     // rejected it whole, so none of its terms may take a slot
     std::vector<int64_t> journal;
+    // element slots that gained a token since the last dict_take_dirty (the NIF patches
+    // their device rows; may repeat a slot or name one whose gain was rolled back)
+    std::vector<uint32_t> dirty;
     // laspj_dict_export's term orders, kept between exports (registrations only append):
     // element slots sorted by term (the first ord_n slots), each element's token slots
     // sorted by term (valid while its size matches the element's token count)
@@ -802,6 +805,7 @@ int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
     d->tok_eq.insert(ht, es, v, *slot);
     d->toks[es].push_back(v);
     d->journal.push_back((int64_t)es);
+    d->dirty.push_back(es);
     return LASPJ_DEC_OK;
 }
 
@@ -1060,6 +1064,11 @@ namespace laspj {
 
 uint32_t dict_elements(const laspj_dict* dict) {
     return dict ? (uint32_t)dict->d.elems.size() : 0u;
+}
+
+void dict_take_dirty(laspj_dict* dict, std::vector<uint32_t>* out) {
+    out->clear();
+    if (dict) out->swap(dict->d.dirty);
 }
 
 uint32_t dict_token_count(const laspj_dict* dict, uint32_t e) {

@@ -302,6 +302,12 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R,
 // segments.  The statuses then come from the join's launch; kDecRedo = the chain broke
 // before any failing segment: decode that call again without deferring.
 constexpr uint64_t kSegResBytes = 32;
+// a redo pass's segments (global segment numbers; n = 0: every segment): the segments of a
+// deferred pass that met terms since registered, decoded again over the cells they left
+struct SegList {
+    uint32_t n = 0;
+    uint32_t g[31] = {};
+};
 constexpr int32_t kDecRedo = 64;
 struct ChainJob {
     void* res = nullptr;
@@ -319,7 +325,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                      const uint8_t* payload, uint64_t payload_bytes,
                      const unsigned long long* offsets, const EtfReadPlan& plan,
                      const uint32_t* segbase, int32_t* status, bool clear,
-                     uint32_t* redo_zeroed, ChainJob* defer = nullptr);
+                     uint32_t* redo_zeroed, ChainJob* defer = nullptr,
+                     const SegList* only = nullptr);
 // OR-Set payloads over several dictionaries decoded in one launch (the NIF's binds of many
 // variables, one token namespace each): group k's payloads [p0, p1) against dictionary d
 // into cells (its first payload's; E slots per replica, consecutive).  The caller stages
@@ -342,7 +349,7 @@ int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
                            const void* dev_tabs, uint32_t npay, const uint8_t* payload,
                            uint64_t payload_bytes, const unsigned long long* offs,
                            const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
-                           ChainJob* defer);
+                           ChainJob* defer, const SegList* only = nullptr);
 // lasp_gset:from_binary/1's decoder (k_gset_etf_read: one wave per payload), enqueue only;
 // offsets / status are device addresses; clear: zero the batch first
 int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
@@ -415,6 +422,8 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
 // term order (order[j] = slot of the j-th smallest)
 uint32_t dict_elements(const laspj_dict* dict);
 uint32_t dict_token_count(const laspj_dict* dict, uint32_t e);
+// the element slots that gained tokens since the last call (repeats possible), cleared
+void dict_take_dirty(laspj_dict* dict, std::vector<uint32_t>* out);
 bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_view>* imgs,
                  std::vector<uint8_t>* order);
 // register the terms of the OR-Set payload elements that start in [from, to) (from: an

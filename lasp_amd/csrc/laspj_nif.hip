@@ -39,6 +39,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -91,8 +92,23 @@ struct laspj_var {
 
 namespace laspj {
 
+// a single bind waiting for a group-commit pass (laspj_var_etf_bind)
+struct BindReq {
+    laspj_var* var;
+    const uint8_t* p;
+    uint64_t n;
+    int32_t status = 0, verdict = LASPJ_NIF_FALLBACK;
+    int rc = LASPJ_OK;
+    bool done = false;
+};
+
 struct NifState {
     std::mutex mu;                  // one call at a time (ctx->mu is held per device phase)
+    // single binds queued for the next group-commit pass, and whether a caller leads one
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::vector<BindReq*> queue;
+    bool leading = false;
     KindState ks[2];                // the image calls' dictionaries: [0] OR-Set, [1] G-Set
     // device: [in region: offsets | segment table | zeroed words | variable cell pointers
     // | payloads or cells][segment results][variable calls' statuses]; cells: the batches
@@ -263,6 +279,9 @@ struct Call {
     std::vector<uint64_t> ooff;     // n + 1 answer payload offsets (MERGE / VALUE / READ)
     const uint8_t* obase = nullptr; // pinned answer payloads
     bool no_defer = false;          // a deferred chain check came back kDecRedo: decode serially
+    // a redo pass: the last pass's payloads and cells stay on the device and only these
+    // segments are decoded again (their terms registered since, patched into the images)
+    SegList redo;
     // a deferred pass that met unknown terms: its segment results (SegRes records, 32 bytes
     // each: status, start, ...) and table, so only the failing segments are registered
     bool has_seg = false;
@@ -369,6 +388,10 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
     K.E = E;
     K.stale = false;
     K.built_K = n;
+    {
+        std::vector<uint32_t> gone;
+        dict_take_dirty(K.dict, &gone);             // (the rebuild holds every token)
+    }
     K.built_cnt.resize(n);
     for (uint32_t e = 0; e < n; ++e) K.built_cnt[e] = toks ? dict_token_count(K.dict, e) : 0;
     ++S->stats[4];
@@ -383,9 +406,13 @@ bool patch_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
     const uint64_t t0 = now_ns();
     const uint32_t n = dict_elements(K.dict);
     if (n != K.built_K || n > K.E) return false;
-    std::vector<uint32_t> dirty;
-    for (uint32_t e = 0; e < n; ++e)
-        if (dict_token_count(K.dict, e) != K.built_cnt[e]) dirty.push_back(e);
+    // the slots the dictionary saw gain tokens (no scan over every element)
+    std::vector<uint32_t> seen, dirty;
+    dict_take_dirty(K.dict, &seen);
+    std::sort(seen.begin(), seen.end());
+    seen.erase(std::unique(seen.begin(), seen.end()), seen.end());
+    for (uint32_t e : seen)
+        if (e < n && dict_token_count(K.dict, e) != K.built_cnt[e]) dirty.push_back(e);
     if (!dirty.empty() &&
         etf_dict_patch(ctx, K.etf, K.dict, dirty.data(), (uint32_t)dirty.size()) != LASPJ_OK)
         return false;
@@ -623,7 +650,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             sent = al(upto, 16);
             return LASPJ_OK;
         };
-        if (dec) {
+        if (dec && c.redo.n) {
+            // (a redo pass: the head and payloads the last pass pulled are still there)
+        } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
             uint64_t io = 0;                     // offset inside payload i
@@ -664,12 +693,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         if (dec && multi) {
             // every namespace's payloads in one launch (the cells zeroed first when the last
             // call left them dirty: the decoders only set what they decode)
-            if (!clean) LJ_HIP(ctx, hipMemsetAsync(cin, 0, cells_in, ctx->stream));
+            if (!clean && !c.redo.n) LJ_HIP(ctx, hipMemsetAsync(cin, 0, cells_in, ctx->stream));
             if (int s = etf_read_multi_enqueue(
                     ctx, eg.data(), (uint32_t)G, din + i_mtab, m, din + i_pay, pay,
                     reinterpret_cast<const unsigned long long*>(din + i_offs), plan,
                     plan.nseg ? reinterpret_cast<const uint32_t*>(din + i_seg) : nullptr, dst,
-                    defer ? &cjob : nullptr))
+                    defer ? &cjob : nullptr, c.redo.n ? &c.redo : nullptr))
                 return s;
         } else if (dec) {
             // each group's payloads against its own dictionary (offsets are absolute in the
@@ -685,8 +714,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                             ctx, &gb, gr.K->etf, -1, 1, din + i_pay, pay, doffs, plans[g],
                             plans[g].nseg ? reinterpret_cast<const uint32_t*>(din + i_seg + gseg[g])
                                           : nullptr,
-                            dst + gr.p0, !clean, dticket + 1 + gr.p0 + g,
-                            defer ? &cjob : nullptr))
+                            dst + gr.p0, !clean && !c.redo.n, dticket + 1 + gr.p0 + g,
+                            defer ? &cjob : nullptr, c.redo.n ? &c.redo : nullptr))
                         return s;
                 } else if (int s = gset_read_enqueue(ctx, &gb, gr.K->etf, -1, 1, din + i_pay, doffs,
                                                      dst + gr.p0, !clean, hoffs.data() + gr.p0)) {
@@ -827,6 +856,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         c.st.assign(m, 0);
         if (dec || var_op) std::memcpy(c.st.data(), hout + o_st, 4ull * m);
         else c.st = hst;
+        if (var_op)
+            for (int32_t x : c.st)
+                if (x != LASPJ_DEC_OK) S->clean_words = 0;   // (its cells were kept)
         c.has_seg = false;
         if (defer && cjob.armed &&
             std::find(c.st.begin(), c.st.end(), (int32_t)LASPJ_DEC_UNKNOWN_TERM) != c.st.end()) {
@@ -1002,6 +1034,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
     std::vector<const uint8_t*> rp;
     std::vector<uint64_t> rl;
     std::vector<int32_t> rst;
+    std::vector<uint8_t> written;
     for (int pass = 0; pass < passes && !resolved; ++pass) {
         for (size_t g = 0; g < G; ++g) {
             KindState& K = *c.groups[g].K;
@@ -1015,12 +1048,22 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 for (uint32_t i = p0; i < p1; ++i)
                     if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
             }
-            if (!patch_etf(ctx, S, K))
+            if (!patch_etf(ctx, S, K)) {
                 if (int s = rebuild_etf(ctx, S, K)) return s;
+                c.redo.n = 0;         // (element ranks moved: the last pass's results stale)
+            }
         }
         int s = device_pass(ctx, S, c);
+        c.redo.n = 0;                 // (a redo pass is taken once)
         if (s == -1000) continue;                // answer area grown: once more
         if (s) return s;
+        // a bind that decoded in this pass was merged in it: WRITTEN if this pass (or an
+        // earlier one, for an operand whose call needed another pass) changed its value
+        if (c.op == Op::BIND) {
+            written.resize(n, 0);
+            for (uint32_t i = 0; i < m; ++i)
+                if (c.st[i] == LASPJ_DEC_OK) written[i] |= c.res[i];
+        }
         bool redo = false;
         for (uint32_t i = 0; i < m; ++i) redo |= c.st[i] == kDecRedo;
         if (redo) {
@@ -1049,6 +1092,18 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
             // unknown term, the whole operands are registered after all
             partial = true;
             for (uint32_t i : unknown) registered[group_of(i)] = 1;
+            // a single bind: the next pass decodes only those segments again, over the
+            // payload and cells this pass left (when the images are patched, not rebuilt)
+            if (c.op == Op::BIND && n == 1 && !c.no_defer) {
+                SegList sl;
+                for (uint32_t i : unknown)
+                    for (uint32_t g = c.segbase[i]; g < c.segbase[i + 1] && sl.n <= 31; ++g)
+                        if ((int32_t)c.segres[8ull * g] != LASPJ_DEC_OK) {
+                            if (sl.n < 31) sl.g[sl.n] = g;
+                            ++sl.n;
+                        }
+                if (sl.n <= 31) c.redo = sl;
+            }
             continue;
         }
         partial = false;
@@ -1100,6 +1155,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
     // call whose passes ran out (the answer area grown, a segment chain only a serial
     // decode judges, terms registered — each on the last pass) hands every operand to the
     // reference's clause rather than answer from a superseded pass
+    if (c.op == Op::BIND && written.size() == n) c.res = written;
     verdict->assign(n, LASPJ_NIF_OK);
     for (uint32_t j = 0; j < n; ++j)
         if (fallback[j] || !resolved) {
@@ -1448,7 +1504,110 @@ bool strong_rand(uint8_t* p, size_t n) {
     return true;
 }
 
+// bind_many with S->mu held (laspj_var_etf_bind_many's body)
+int bind_many_locked(laspj_ctx* ctx, laspj::NifState* S, uint32_t n, laspj_var* const* vars,
+                     const uint8_t* const* values, const uint64_t* lens, int32_t* status,
+                     int32_t* verdict) {
+    const int32_t kind = vars[0] ? vars[0]->kind : 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!vars[i] || vars[i]->ctx != ctx || !S->vars.count(vars[i]))
+            return fail(ctx, LASPJ_E_INVAL, "var_bind: variable %u is not this context's", i);
+        if (vars[i]->kind != kind)
+            return fail(ctx, LASPJ_E_KIND, "var_bind: variables of one kind per call");
+        if (!values[i] && lens[i]) return fail(ctx, LASPJ_E_INVAL, "var_bind: null payload");
+    }
+    {
+        std::unordered_set<laspj_var*> seen;
+        for (uint32_t i = 0; i < n; ++i)
+            if (!seen.insert(vars[i]).second)
+                return fail(ctx, LASPJ_E_INVAL, "var_bind: variable %u named twice", i);
+    }
+    // variables whose value sits in an image (after a dictionary reset) are decoded first;
+    // one that stays host-held answers FALLBACK (the NIF binds its read image in Erlang)
+    for (uint32_t i = 0; i < n; ++i) {
+        bool ok = false;
+        if (int s = laspj::hydrate(ctx, S, vars[i], &ok)) return s;
+        verdict[i] = LASPJ_NIF_FALLBACK;
+        status[i] = 0;
+    }
+    std::vector<uint32_t> live;
+    for (uint32_t i = 0; i < n; ++i)
+        if (vars[i]->resident && vars[i]->epoch == vars[i]->ns->epoch) live.push_back(i);
+    if (live.empty()) return LASPJ_OK;
+    // one decode per namespace (its own dictionary): the payloads grouped by namespace
+    std::stable_sort(live.begin(), live.end(), [&](uint32_t x, uint32_t y) {
+        return std::less<const laspj::KindState*>()(vars[x]->ns.get(), vars[y]->ns.get());
+    });
+    laspj::Call c;
+    c.op = laspj::Op::BIND;
+    c.kind = kind;
+    c.n = c.m = (uint32_t)live.size();
+    for (uint32_t k = 0; k < live.size(); ++k) {
+        const uint32_t i = live[k];
+        c.p.push_back(values[i]);
+        c.len.push_back(lens[i]);
+        c.vars.push_back(vars[i]);
+        if (k == 0 || vars[live[k - 1]]->ns != vars[i]->ns)
+            c.groups.push_back(laspj::Group{vars[i]->ns.get(), k, k + 1});
+        else
+            c.groups.back().p1 = k + 1;
+    }
+    std::vector<int32_t> vd;
+    if (int s = laspj::run(ctx, S, c, &vd)) return s;
+    for (size_t k = 0; k < live.size(); ++k) {
+        verdict[live[k]] = vd[k];
+        status[live[k]] = vd[k] == LASPJ_NIF_OK ? (int32_t)c.res[k] : 0;
+    }
+    return LASPJ_OK;
+}
+
 }  // namespace
+
+namespace laspj {
+namespace {
+
+// one batch of queued single binds (laspj_var_etf_bind's group commit), S->mu held: the
+// requests of each kind that name distinct variables go into one bind_many; a request
+// whose variable is not this context's answers LASPJ_E_INVAL on its own; a variable named
+// again waits for the next round of the same batch (the caller marks them done)
+void serve_binds(laspj_ctx* ctx, NifState* S, std::vector<BindReq*>& batch) {
+    std::vector<BindReq*> todo;
+    for (BindReq* r : batch) {
+        if (r->var->ctx != ctx || !S->vars.count(r->var)) {
+            r->rc = fail(ctx, LASPJ_E_INVAL, "var_bind: unknown variable");
+        } else {
+            todo.push_back(r);
+        }
+    }
+    while (!todo.empty()) {
+        std::vector<BindReq*> now, later;
+        std::unordered_set<laspj_var*> seen;
+        const int32_t kind = todo[0]->var->kind;
+        for (BindReq* r : todo)
+            (r->var->kind == kind && seen.insert(r->var).second ? now : later).push_back(r);
+        const uint32_t k = (uint32_t)now.size();
+        std::vector<laspj_var*> vs(k);
+        std::vector<const uint8_t*> ps(k);
+        std::vector<uint64_t> ls(k);
+        std::vector<int32_t> st(k, 0), vd(k, LASPJ_NIF_FALLBACK);
+        for (uint32_t i = 0; i < k; ++i) {
+            vs[i] = now[i]->var;
+            ps[i] = now[i]->p;
+            ls[i] = now[i]->n;
+        }
+        const int rc = bind_many_locked(ctx, S, k, vs.data(), ps.data(), ls.data(), st.data(),
+                                        vd.data());
+        for (uint32_t i = 0; i < k; ++i) {
+            now[i]->rc = rc;
+            now[i]->status = rc ? 0 : st[i];
+            now[i]->verdict = rc ? LASPJ_NIF_FALLBACK : vd[i];
+        }
+        todo.swap(later);
+    }
+}
+
+}  // namespace
+}  // namespace laspj
 
 extern "C" {
 
@@ -1507,63 +1666,48 @@ int laspj_var_etf_bind_many(laspj_ctx* ctx, uint32_t n, laspj_var* const* vars,
     laspj::NifState* S = laspj::state(ctx);
     if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
     std::lock_guard<std::mutex> lk(S->mu);
-    const int32_t kind = vars[0] ? vars[0]->kind : 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (!vars[i] || vars[i]->ctx != ctx || !S->vars.count(vars[i]))
-            return fail(ctx, LASPJ_E_INVAL, "var_bind: variable %u is not this context's", i);
-        if (vars[i]->kind != kind)
-            return fail(ctx, LASPJ_E_KIND, "var_bind: variables of one kind per call");
-        if (!values[i] && lens[i]) return fail(ctx, LASPJ_E_INVAL, "var_bind: null payload");
-    }
-    {
-        std::unordered_set<laspj_var*> seen;
-        for (uint32_t i = 0; i < n; ++i)
-            if (!seen.insert(vars[i]).second)
-                return fail(ctx, LASPJ_E_INVAL, "var_bind: variable %u named twice", i);
-    }
-    // variables whose value sits in an image (after a dictionary reset) are decoded first;
-    // one that stays host-held answers FALLBACK (the NIF binds its read image in Erlang)
-    for (uint32_t i = 0; i < n; ++i) {
-        bool ok = false;
-        if (int s = laspj::hydrate(ctx, S, vars[i], &ok)) return s;
-        verdict[i] = LASPJ_NIF_FALLBACK;
-        status[i] = 0;
-    }
-    std::vector<uint32_t> live;
-    for (uint32_t i = 0; i < n; ++i)
-        if (vars[i]->resident && vars[i]->epoch == vars[i]->ns->epoch) live.push_back(i);
-    if (live.empty()) return LASPJ_OK;
-    // one decode per namespace (its own dictionary): the payloads grouped by namespace
-    std::stable_sort(live.begin(), live.end(), [&](uint32_t x, uint32_t y) {
-        return std::less<const laspj::KindState*>()(vars[x]->ns.get(), vars[y]->ns.get());
-    });
-    laspj::Call c;
-    c.op = laspj::Op::BIND;
-    c.kind = kind;
-    c.n = c.m = (uint32_t)live.size();
-    for (uint32_t k = 0; k < live.size(); ++k) {
-        const uint32_t i = live[k];
-        c.p.push_back(values[i]);
-        c.len.push_back(lens[i]);
-        c.vars.push_back(vars[i]);
-        if (k == 0 || vars[live[k - 1]]->ns != vars[i]->ns)
-            c.groups.push_back(laspj::Group{vars[i]->ns.get(), k, k + 1});
-        else
-            c.groups.back().p1 = k + 1;
-    }
-    std::vector<int32_t> vd;
-    if (int s = laspj::run(ctx, S, c, &vd)) return s;
-    for (size_t k = 0; k < live.size(); ++k) {
-        verdict[live[k]] = vd[k];
-        status[live[k]] = vd[k] == LASPJ_NIF_OK ? (int32_t)c.res[k] : 0;
-    }
-    return LASPJ_OK;
+    return bind_many_locked(ctx, S, n, vars, values, lens, status, verdict);
 }
 
 int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t* status,
                        int32_t* verdict) {
     if (!var || !var->ctx) return LASPJ_E_INVAL;
-    return laspj_var_etf_bind_many(var->ctx, 1, &var, &value, &n, status, verdict);
+    laspj_ctx* ctx = var->ctx;
+    if ((!value && n) || !status || !verdict) return fail(ctx, LASPJ_E_INVAL, "var_bind: null argument");
+    laspj::NifState* S = laspj::state(ctx);
+    if (!S) return fail(ctx, LASPJ_E_NOMEM, "nif: state allocation");
+    // Group commit: schedulers binding through one context at once are served by one device
+    // pass.  The caller that finds no pass running leads: it takes every queued bind (its
+    // own first) and runs them as one bind_many, again while more arrive; the others wait
+    // for their answers.  One context per GPU then batches many schedulers' binds
+    // (lasp_vnode.erl:213-237) instead of one stream and pass per scheduler.
+    laspj::BindReq r{var, value, n};
+    std::unique_lock<std::mutex> q(S->qmu);
+    S->queue.push_back(&r);
+    while (!r.done && S->leading) S->qcv.wait(q);
+    if (r.done) {
+        *status = r.status;
+        *verdict = r.verdict;
+        return r.rc;
+    }
+    // (the leader serves one batch — its own request among them — and hands over: a waiter
+    // whose request came later leads the next)
+    S->leading = true;
+    std::vector<laspj::BindReq*> batch;
+    batch.swap(S->queue);
+    q.unlock();
+    {
+        std::lock_guard<std::mutex> lk(S->mu);
+        laspj::serve_binds(ctx, S, batch);
+    }
+    q.lock();
+    // (answers published under the queue's lock: a waiter reads them once it sees done)
+    for (laspj::BindReq* b : batch) b->done = true;
+    S->leading = false;
+    S->qcv.notify_all();
+    *status = r.status;
+    *verdict = r.verdict;
+    return r.rc;
 }
 
 int laspj_var_etf_write(laspj_var* var, const uint8_t* value, uint64_t n, int32_t* verdict) {

@@ -280,3 +280,117 @@ def test_replicas_bind_each_others_updates_in_one_pass():
         assert reps[0].read() == (OK, _tb(both)) and reps[1].read() == (OK, _tb(both))
     finally:
         ctx.close()
+
+
+def test_bind_of_unseen_tokens_redoes_only_failed_segments():
+    """A bind whose image carries tokens the variable's namespace has not seen (another
+    node's update, lasp_orset.erl:222-230) decodes, registers the failing segments' terms,
+    patches the images and decodes again only those segments over the cells the first pass
+    left: two device passes, one registration, the oracle's merge.  More failing segments
+    than a redo pass lists, or a new element (images rebuilt), take a full second pass —
+    the same answers."""
+    from lasp_amd import _lib
+    ctx = _ctx()
+    try:
+        rng = random.Random(23)
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 256)          # many segments per payload
+        tok = lambda c, e: bytes([c]) + e.to_bytes(4, "big") + bytes(15)   # noqa: E731
+        base = [(e, [(tok(1, e), e % 7 == 0)]) for e in range(3000)]
+        var = ctx.var("orset")
+        assert var.write(_tb(base)) == OK
+        cur = base
+        for case, nnew, new_elem in (("few", 5, False), ("many", 120, False),
+                                     ("element", 3, True)):
+            picks = sorted(rng.sample(range(3000), nnew))
+            add = {e: bytes(rng.getrandbits(8) for _ in range(20)) for e in picks}
+            val = [(e, sorted(ts + ([(add[e], False)] if e in add else []), key=_key))
+                   for e, ts in cur]
+            if new_elem:
+                val = sorted(val + [(5000, [(b"\x09" * 20, False)])], key=lambda x: _key(x[0]))
+            s0 = ctx.nif_stats()
+            assert var.bind(_tb(val)) == (OK, 1), case
+            s1 = ctx.nif_stats()
+            cur = oorset.merge(cur, val)
+            assert var.read() == (OK, _tb(cur)), case
+            assert s1["fallbacks"] == s0["fallbacks"]
+            if case == "few":
+                assert s1["device_passes"] - s0["device_passes"] == 2
+                assert s1["registrations"] - s0["registrations"] == 1
+            # binding the same state again: all known, one pass, a no-op
+            s2 = ctx.nif_stats()
+            assert var.bind(_tb(cur)) == (OK, 0), case
+            assert ctx.nif_stats()["device_passes"] - s2["device_passes"] == 1
+        ctx.set_tuning(_lib.TUNE_ETF_SEG, 0)
+    finally:
+        ctx.close()
+
+
+def test_group_commit_binds_from_many_threads():
+    """Sixteen threads binding their own variables through ONE context at once
+    (laspj_var_etf_bind's group commit: binds queued while a pass runs share the next
+    pass): every answer and every variable's value is the oracle's; the passes are fewer
+    than the binds."""
+    import threading
+    ctx = _ctx()
+    try:
+        rng = random.Random(31)
+        elems = list(range(200))
+        nthr, per = 16, 12
+        vs = [ctx.var("orset") for _ in range(nthr)]
+        vals = [[[(e, [(bytes([t, k]) + e.to_bytes(4, "big") + bytes(14), k % 3 == 0)])
+                  for e in sorted(rng.sample(elems, 50))] for k in range(per)]
+                for t in range(nthr)]
+        got = [[None] * per for _ in range(nthr)]
+        errs = []
+        go = threading.Barrier(nthr)
+
+        def work(t):
+            try:
+                go.wait()
+                for k in range(per):
+                    got[t][k] = vs[t].bind(_tb(vals[t][k]))
+            except Exception as e:       # noqa: BLE001
+                errs.append(repr(e))
+
+        s0 = ctx.nif_stats()
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert not errs, errs[:3]
+        passes = ctx.nif_stats()["device_passes"] - s0["device_passes"]
+        for t in range(nthr):
+            cur = []
+            for k in range(per):
+                want_st = 0 if exact_eq(cur, vals[t][k]) else 1
+                assert got[t][k] == (OK, want_st), (t, k)
+                cur = oorset.merge(cur, vals[t][k])
+            assert vs[t].read() == (OK, _tb(cur)), t
+        assert passes < nthr * per * 2            # (registration passes included)
+    finally:
+        ctx.close()
+
+
+def test_bind_many_fresh_namespaces():
+    """One bind_many over sixteen fresh variables (sixteen namespaces with no dictionary
+    yet, registered in the call, decoded in one launch), then again with new tokens and
+    repeats: statuses and values are the oracle's."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(32)
+        vs = [ctx.var("orset") for _ in range(16)]
+        cur = [[] for _ in vs]
+        for rnd in range(4):
+            vals = [[(e, [(bytes([t, rnd]) + e.to_bytes(4, "big") + bytes(14), rnd % 2 == 1)])
+                     for e in sorted(rng.sample(range(200), 50))] for t in range(16)]
+            if rnd == 3:
+                vals[4] = cur[4]
+            got = ctx.var_bind_many(list(zip(vs, [_tb(v) for v in vals])))
+            for t in range(16):
+                want = 0 if exact_eq(cur[t], vals[t]) else 1
+                assert got[t] == (OK, want), (rnd, t)
+                cur[t] = oorset.merge(cur[t], vals[t])
+                assert vs[t].read() == (OK, _tb(cur[t])), (rnd, t)
+    finally:
+        ctx.close()

@@ -28,7 +28,8 @@ def main():
     res, vd, nm = C.c_int32(), C.c_int32(), C.c_uint32()
     ei, el, mi = C.c_void_p(), C.c_uint64(), C.c_void_p()
     keys = ("device_passes", "registrations", "image_rebuilds", "image_patches", "ns_register",
-            "ns_rebuild", "dict_resets", "fallbacks")
+            "ns_rebuild", "ns_stage_enqueue", "ns_stage_copy", "ns_device_wait", "ns_answers",
+            "dict_resets", "fallbacks")
     rows = []
 
     def stats():
