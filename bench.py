@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--nt", type=int, default=-1)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_pmc_join.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06_pmc_join.json"),
                     help="PMC summary giving HBM traffic per join launch")
     ap.add_argument("--antientropy", choices=["auto", "on", "off"], default="auto",
                     help="config-3 gossip anti-entropy leg (auto: when N > 1)")
@@ -577,6 +577,7 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
     from lasp_amd._lib import check
     from lasp_amd import engine
     L = ctx.L
+    loop = _bind_loop_lib()
     ready, errs, spans = threading.Barrier(nthreads + 1), [], []
 
     def worker():
@@ -588,8 +589,9 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
             check(L.laspj_var_etf_bind(v2.h, pb, len(pb), C.byref(s2), C.byref(d2)), c2.h)
             ready.wait()
             t = time.perf_counter()
-            for _ in range(per):
-                check(L.laspj_var_etf_bind(v2.h, pb, len(pb), C.byref(s2), C.byref(d2)), c2.h)
+            # the loop in C (tests/c/bind_loop.c): the threads meet in the library, not on
+            # the interpreter lock
+            check(loop.bind_loop(v2.h, pb, len(pb), per, C.byref(s2), C.byref(d2)), c2.h)
             spans.append((t, time.perf_counter()))
             if (d2.value, s2.value) != (0, 1):
                 errs.append("bad answer")
@@ -621,6 +623,24 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
             "binds_per_s": nthreads * per / wall,
             "merged_elements_per_s": nthreads * per * 10_000 / wall,
             "pcie_GBps": nthreads * per * len(pb) / wall / 1e9}
+
+
+def _bind_loop_lib():
+    """tests/c/bind_loop.c built against include/laspj.h and liblaspj.so (gcc, in /tmp)."""
+    import ctypes as C
+    import subprocess
+    import tempfile
+    from lasp_amd import _lib
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    out = os.path.join(tempfile.gettempdir(), f"laspj_bind_loop_{os.getpid()}.so")
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", out,
+                    os.path.join(ROOT, "tests", "c", "bind_loop.c"), "-L", libdir, "-llaspj",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    lib = C.CDLL(out)
+    lib.bind_loop.restype = C.c_int
+    lib.bind_loop.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_int,
+                              C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    return lib
 
 
 def steady_leg(ctx, nvars: int = 32, steps: int = 200):
@@ -740,13 +760,22 @@ def wide_leg(ctx, args):
     achieved = per_elem * R * E / (ms / 1e3) / 1e9
     del a, b, c
     ctx.synchronize()
+    # HBM bytes per launch from the committed PMC passes of this join (tools/gpu_pmc_join.sh)
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r06_pmc_join_t128.json")) as f:
+            pm = json.load(f)
+        if pm.get("replicas") == R and pm.get("elements") == E and pm.get("pairs") == k:
+            traffic = pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
     return {"workload": "batched OR-Set join with 128 token slots per element "
                         "(LASPJ_KIND_ORSET_WIDE, k = 2 {p, r} pairs per cell)",
             "replicas": R, "elements": E, "token_slots": 64 * k, "kernel_ms": ms,
             "merged_elements_per_s": R * E / (ms / 1e3),
             "algorithmic_bytes_per_element": per_elem,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic}}
 
 
 def list_leg(ctx):

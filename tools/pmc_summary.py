@@ -42,18 +42,20 @@ def main():
     ap.add_argument("--kernel", default="k_or16<2")
     ap.add_argument("--replicas", type=int, default=1 << 20)
     ap.add_argument("--elements", type=int, default=4096)
+    ap.add_argument("--pairs", type=int, default=1,
+                    help="{p, r} pairs per cell (2: the T = 128 wide join)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     stats = [r for r in rows(os.path.join(a.stats_dir, "**", "*kernel_stats.csv"))
              if a.kernel in r.get("Name", "")]
     fetch = counter(a.fetch_dir, "FETCH_SIZE", a.kernel)
     write = counter(a.write_dir, "WRITE_SIZE", a.kernel)
-    algo = 48 * a.replicas * a.elements
+    algo = 48 * a.pairs * a.replicas * a.elements
     f_kib = statistics.median(fetch) if fetch else None
     w_kib = statistics.median(write) if write else None
     hbm = (2 * f_kib + w_kib) * 1024 if fetch and write else None
     out = {
-        "kernel": a.kernel, "replicas": a.replicas, "elements": a.elements,
+        "kernel": a.kernel, "replicas": a.replicas, "elements": a.elements, "pairs": a.pairs,
         "algorithmic_bytes_per_launch": algo,
         "fetch_size_kib_per_launch": f_kib, "write_size_kib_per_launch": w_kib,
         "fetch_launches": len(fetch), "write_launches": len(write),
