@@ -691,7 +691,16 @@ struct ChainArgs {
     const SegRes* res;
     int32_t* status;
     uint32_t nrep, S;
+    SegRes* hres;       // (or null) a failed payload's segment results copied here too
 };
+// the checking wave of payload r: its segment results into cj.hres when its verdict failed
+__device__ void chain_publish(const ChainArgs& cj, uint32_t r, int32_t st, uint32_t lane);
+ChainArgs chain_args(const ChainJob* chain) {
+    if (!chain || !chain->armed) return ChainArgs{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr};
+    return ChainArgs{chain->payload, chain->offs, chain->segbase,
+                     static_cast<const SegRes*>(chain->res), chain->status, chain->nrep, chain->S,
+                     static_cast<SegRes*>(chain->hres)};
+}
 __global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2* b, u64x2* z,
                                                                  uint64_t R, uint32_t E,
                                                                  DictView d, uint32_t nch,
@@ -710,6 +719,7 @@ __global__ __launch_bounds__(kBlock) void k_etf_join_chunk_sizes(u64x2* a, u64x2
                                              cj.segbase[r], cj.segbase[r + 1] - cj.segbase[r],
                                              cj.S, cj.res, lane);
             if (lane == 0) cj.status[r] = st;
+            chain_publish(cj, r, st, lane);
         }
     }
     for (uint64_t it = blockIdx.x; blockIdx.x < jblocks && it < R * nch; it += jblocks) {
@@ -905,6 +915,7 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
                                              lb.cj.segbase[r], lb.cj.segbase[r + 1] - lb.cj.segbase[r],
                                              lb.cj.S, lb.cj.res, lane);
             if (lane == 0) lb.cj.status[r] = st;
+            chain_publish(lb.cj, r, st, lane);
         }
         lb_finish(lb, nch, hdr, out);
         return;
@@ -1510,6 +1521,7 @@ __global__ __launch_bounds__(kBlock) void k_gset_chunk_sizes(const u64* words, c
                                              cj.segbase[rep], cj.segbase[rep + 1] - cj.segbase[rep],
                                              cj.S, cj.res, threadIdx.x);
             if (threadIdx.x == 0) cj.status[rep] = st;
+            chain_publish(cj, (uint32_t)rep, st, threadIdx.x);
         }
         const u64* w = words + rep * W;
         u64 by = 0, cn = 0;
@@ -3294,6 +3306,15 @@ __device__ bool chain_ok(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
 // status); kDecRedo when the chain breaks first (a false header match, a malformed
 // payload): only a serial decode tells.  The same per-segment checks as chain_ok, the
 // first offending segment in stream order deciding.
+__device__ void chain_publish(const ChainArgs& cj, uint32_t r, int32_t st, uint32_t lane) {
+    if (!cj.hres || st == LASPJ_DEC_OK) return;
+    static_assert(sizeof(SegRes) == 32, "four words a segment");
+    const uint32_t g0 = cj.segbase[r], n = 4u * (cj.segbase[r + 1] - g0);
+    const u64* src = reinterpret_cast<const u64*>(cj.res + g0);
+    u64* dst = reinterpret_cast<u64*>(cj.hres + g0);
+    for (uint32_t k = lane; k < n; k += 64) dst[k] = src[k];
+}
+
 __device__ int32_t chain_verdict(const uint8_t* payload, u64 base, u64 len, uint32_t g0,
                                  uint32_t ns, uint32_t S, const SegRes* res, uint32_t lane) {
     // segment 0 and the first 256 segments' results loaded together (one memory round
@@ -4695,6 +4716,7 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
                 s_st = st;
                 if (ch == 0) dstat[i] = st;
             }
+            if (ch == 0) chain_publish(cj, i, st, threadIdx.x);
         }
     } else if (threadIdx.x == 0) {
         s_st = dstat[i];
@@ -5019,11 +5041,7 @@ static int gset_chunks_enqueue(laspj_ctx* ctx, const laspj_batch* b, const laspj
                                uint32_t hdr, u64* offsets, uint32_t* flag, const u64** chunks,
                                int src = 0, const u64* words2 = nullptr,
                                const ChainJob* chain = nullptr) {
-    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-    if (chain && chain->armed)
-        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
-                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
-                       chain->S};
+    const ChainArgs cj = chain_args(chain);
     const uint64_t R = b->replicas;
     const uint32_t nch = (b->elements + kBlock - 1) / kBlock;
     if (int s = reserve_scratch(ctx, 16ull * R * (nch + 1ull))) return s;
@@ -5107,11 +5125,7 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
     // up to 4 replicas the last block scans them all (one launch); more go to the
     // per-replica scan kernel
     const bool one = R <= 4;
-    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-    if (chain && chain->armed)
-        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
-                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
-                       chain->S};
+    const ChainArgs cj = chain_args(chain);
     const uint64_t cblocks = cj.status ? (cj.nrep + 3u) / 4u : 0u;
     hipLaunchKernelGGL(k_etf_join_chunk_sizes, dim3((unsigned)(sg + cblocks)), dim3(kBlock), 0,
                        ctx->stream, reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b),
@@ -5136,11 +5150,7 @@ int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E
                             const ChainJob* chain) {
     const uint32_t nch = (E + kBlock - 1) / kBlock;
     LBJoin lb{reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b), lbst, ticket, offs_out,
-              ChainArgs{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0}};
-    if (chain && chain->armed)
-        lb.cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
-                          static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
-                          chain->S};
+              chain_args(chain)};
     const uint32_t cblocks = lb.cj.status ? (lb.cj.nrep + 3u) / 4u : 0u;
     auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true, true>
                              : k_orset_etf_write_rec<24576, false, true>;
@@ -5156,11 +5166,7 @@ int var_bind_enqueue(laspj_ctx* ctx, uint64_t* const* curs, uint64_t* const* ins
                      uint32_t* diff, uint32_t* ticket, uint8_t* out_res, int32_t* out_st,
                      bool write, const ChainJob* chain) {
     const uint32_t nch = (uint32_t)std::max<uint64_t>(1, (maxw + kVarWords - 1) / kVarWords);
-    ChainArgs cj{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-    if (chain && chain->armed)
-        cj = ChainArgs{chain->payload, chain->offs, chain->segbase,
-                       static_cast<const SegRes*>(chain->res), chain->status, chain->nrep,
-                       chain->S};
+    const ChainArgs cj = chain_args(chain);
     hipLaunchKernelGGL(write ? k_var_bind<true> : k_var_bind<false>, dim3(nch * n), dim3(kBlock),
                        0, ctx->stream, reinterpret_cast<u64* const*>(curs),
                        reinterpret_cast<u64* const*>(ins), wprs, nch, n, dstat, diff, ticket,
@@ -5998,3 +6004,457 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
 
 }  // namespace laspj
 
+
+// ------------------------------------------------------------------ wide namespaces
+// A resident variable whose element holds more than 64 tokens (add_elem mints a token per
+// add and never collects one, lasp_orset.erl:222-241, 261-262) lives in cells of k {p, r}
+// pairs per element (LASPJ_KIND_ORSET_WIDE's layout: token slot t in pair t / 64).  Its
+// namespace's device tables hold, per element slot, its tokens in term order as ranks of
+// a CSR array (slot of each rank, the record template 104 2 <token image> of each rank),
+// and the decoder / writer below read and write images of such values.  The decoder is
+// the serial one (one wave per payload, candidates ranked by lanes, LDS-staged payload
+// windows); the size pass and writer assemble elements one thread each.  Token images of
+// one length only (Lasp's 20-byte tokens), <= 46 bytes.
+namespace laspj {
+
+struct WideView {
+    DictView d;                 // the element tables (images, term order, templates)
+    const uint32_t* rb;         // E + 1: element slot e's ranks rb[e] .. rb[e + 1)
+    const uint16_t* rslot;      // by rank: the token slot
+    const uint8_t* rec;         // by rank: 104 2 <token image>, RS bytes each (RS = 16 k)
+    uint32_t RL, RS, E, tw;     // template bytes, stride, element slots, pairs per cell
+};
+
+struct WideDict {
+    laspj_ctx* ctx = nullptr;
+    void* block = nullptr;
+    uint64_t block_bytes = 0;
+    WideView v;
+    uint32_t max_cnt = 0;
+};
+
+namespace {
+
+__global__ __launch_bounds__(kBlock) void k_wide_read(const uint8_t* payload, u64 total,
+                                                      const u64* offs, uint64_t R, WideView W,
+                                                      u64x2* cells, int32_t* status) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin];
+    __shared__ u64 acc[kBlock / 64][64];       // an element's pairs (tw <= 32)
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const DictView& d = W.d;
+    const uint32_t E = W.E, tw = W.tw, RL = W.RL, RS = W.RS;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
+        Stage s{stage[wave], payload, total, 0, 0};
+        const u64 base = offs[rep], end = offs[rep + 1];
+        u64 p = base;
+        int32_t st = LASPJ_DEC_OK;
+        u64x2* c = cells + rep * (u64)E * tw;
+        do {
+            if (!stage_span(s, p, 2, end) || at(s, p) != 131) { st = LASPJ_DEC_MALFORMED; break; }
+            uint32_t n = 0;
+            bool list = false;
+            if (at(s, p + 1) == 106) {
+                p += 2;
+            } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
+                n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
+                p += 6;
+                list = true;
+            } else {
+                st = LASPJ_DEC_MALFORMED;
+                break;
+            }
+            int64_t prev = -1;
+            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
+                const uint32_t span = (uint32_t)min((u64)(kDWin - 16), end - p);
+                if (!stage_span(s, p, span, end)) { st = LASPJ_DEC_MALFORMED; break; }
+                int64_t found = -1;
+                uint32_t e = 0, hl = 0;
+                for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
+                    const int64_t r = c0 + lane;
+                    bool hit = false;
+                    uint32_t ec = 0, hlc = 0;
+                    if (r < (int64_t)E) {
+                        ec = d.elem_order[r];
+                        hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
+                        if (hlc > 3u && hlc <= span) {
+                            const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
+                            hit = hlc - 1u <= 48 ? same48(s, p, t, hlc - 1u)
+                                                 : same_long(s, p, t, hlc - 1u);
+                        }
+                    }
+                    const u64 m = __ballot(hit);
+                    if (m) {
+                        const uint32_t w = (uint32_t)__ffsll((long long)m) - 1u;
+                        found = c0 + w;
+                        e = __shfl(ec, w, 64);
+                        hl = __shfl(hlc, w, 64);
+                    }
+                }
+                if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                prev = found;
+                p += hl;
+                if (at(s, p - 1) != 108) {
+                    st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
+                    break;
+                }
+                if (!stage_span(s, p, 4, end)) { st = LASPJ_DEC_MALFORMED; break; }
+                const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
+                                       at(s, p + 3);
+                p += 4;
+                if (m_tok == 0 || m_tok > 64u * tw) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
+                const uint32_t r0 = W.rb[e], cnt = W.rb[e + 1] - r0;
+                if (lane < 2u * tw) acc[wave][lane] = 0;
+                wave_sync();
+                int32_t tprev = -1;
+                for (uint32_t j = 0; j < m_tok; ++j) {
+                    if (!stage_span(s, p, RL + 8u, end) && !stage_span(s, p, RL + 6u, end)) {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    int32_t rank = -1;
+                    for (int32_t q0 = tprev + 1; q0 < (int32_t)cnt && rank < 0; q0 += 64) {
+                        const int32_t q = q0 + (int32_t)lane;
+                        bool hit = false;
+                        if (q < (int32_t)cnt && p + RL <= s.hi)
+                            hit = same48(s, p, W.rec + (u64)(r0 + (uint32_t)q) * RS, RL);
+                        const u64 m = __ballot(hit);
+                        if (m) rank = q0 + (int32_t)__ffsll((long long)m) - 1;
+                    }
+                    if (rank < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
+                    tprev = rank;
+                    p += RL;
+                    const uint32_t t0 = p < s.hi ? at(s, p) : 0u;
+                    uint32_t len, h;
+                    if ((t0 == 100 || t0 == 118) && p + 3 <= s.hi && at(s, p + 1) == 0) {
+                        len = at(s, p + 2);
+                        h = 3;
+                    } else if (t0 == 119 && p + 2 <= s.hi) {
+                        len = at(s, p + 1);
+                        h = 2;
+                    } else {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    bool flag;
+                    if (len == 4 && p + h + 4 <= end && stage_span(s, p, h + 4, end) &&
+                        at(s, p + h) == 't' && at(s, p + h + 1) == 'r' && at(s, p + h + 2) == 'u' &&
+                        at(s, p + h + 3) == 'e') {
+                        flag = true;
+                    } else if (len == 5 && p + h + 5 <= end && stage_span(s, p, h + 5, end) &&
+                               at(s, p + h) == 'f' && at(s, p + h + 1) == 'a' &&
+                               at(s, p + h + 2) == 'l' && at(s, p + h + 3) == 's' &&
+                               at(s, p + h + 4) == 'e') {
+                        flag = false;
+                    } else {
+                        st = LASPJ_DEC_MALFORMED;
+                        break;
+                    }
+                    p += h + len;
+                    const uint32_t slot = W.rslot[r0 + (uint32_t)rank];
+                    if (lane == 0) {
+                        acc[wave][2u * (slot >> 6)] |= 1ull << (slot & 63u);
+                        if (flag) acc[wave][2u * (slot >> 6) + 1] |= 1ull << (slot & 63u);
+                    }
+                }
+                if (st != LASPJ_DEC_OK) break;
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+                wave_sync();
+                if (lane < tw) c[(u64)e * tw + lane] = u64x2{acc[wave][2 * lane], acc[wave][2 * lane + 1]};
+                wave_sync();
+            }
+            if (st != LASPJ_DEC_OK) break;
+            if (list) {
+                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
+                p += 1;
+            }
+            if (p != end) st = LASPJ_DEC_MALFORMED;
+        } while (false);
+        if (lane == 0) status[rep] = st;
+    }
+}
+
+// bytes of one present element: 104 2 <elem> 108 <n:32> records 106; a record is
+// 104 2 <token image> and the flag atom (false 8 bytes, true 7)
+__device__ __forceinline__ uint32_t wide_elem_size(const WideView& W, uint32_t e,
+                                                   const u64x2* c, uint32_t* npres, bool* bad) {
+    uint32_t n = 0, nt = 0;
+    const uint32_t cnt = W.rb[e + 1] - W.rb[e];
+    for (uint32_t j = 0; j < W.tw; ++j) {
+        const u64x2 v = c[j];
+        n += (uint32_t)__popcll(v.x);
+        nt += (uint32_t)__popcll(v.x & v.y);
+        const uint32_t lo = 64u * j;
+        const u64 valid = cnt >= lo + 64u ? ~0ull : (cnt > lo ? (1ull << (cnt - lo)) - 1ull : 0ull);
+        *bad |= (v.x & ~valid) != 0;
+    }
+    *npres = n;
+    const uint32_t el = W.d.elem_off[e + 1] - W.d.elem_off[e];
+    return n ? 7u + el + n * (W.RL + 8u) - nt + 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_wide_size(const u64x2* cells, uint64_t R, WideView W,
+                                                      uint32_t hdr, u64* sizes, uint32_t* flag) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64; rep < R;
+         rep += waves) {
+        const u64x2* c = cells + rep * (u64)W.E * W.tw;
+        u64 sum = 0, n = 0;
+        bool bad = false;
+        for (uint32_t e = lane; e < W.E; e += 64) {
+            uint32_t np = 0;
+            const uint32_t sz = wide_elem_size(W, e, c + (u64)e * W.tw, &np, &bad);
+            if (np) {
+                ++n;
+                bad |= W.d.elem_off[e + 1] == W.d.elem_off[e];
+                sum += sz;
+            }
+        }
+        sum = wave_sum(sum);
+        n = wave_sum(n);
+        const bool any_bad = __ballot(bad) != 0;
+        if (lane == 0) {
+            sizes[rep] = hdr + 1u + (n ? 5u + sum + 1u : 1u);
+            if (any_bad) atomicOr(flag, 1u);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wide_write(const u64x2* cells, uint64_t R, WideView W,
+                                                       int tag, int vers, const u64* offs,
+                                                       uint8_t* out, u64 ocap) {
+    if (offs[R] > ocap) return;              // the payloads do not fit: the host re-sizes
+    __shared__ uint32_t lds4[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 16];
+    const uint32_t hdr = tag >= 0 ? 2u : 0u;
+    const uint32_t E = W.E, tw = W.tw;
+    for (uint64_t rep = blockIdx.x; rep < R; rep += gridDim.x) {
+        const u64x2* c = cells + rep * (u64)E * tw;
+        const u64 base = offs[rep], end = offs[rep + 1];
+        u64 cursor = base + hdr + 6u;
+        uint32_t n = 0;
+        for (uint32_t c0 = 0; c0 < E; c0 += kBlock) {
+            const uint32_t i = c0 + threadIdx.x;
+            const uint32_t e = i < E ? W.d.elem_order[i] : 0u;
+            uint32_t np = 0;
+            bool bad = false;
+            const uint32_t sz = i < E ? wide_elem_size(W, e, c + (u64)e * tw, &np, &bad) : 0u;
+            uint32_t tot, cnt;
+            const uint32_t pos = block_excl_scan(sz, lds4, &tot);
+            block_excl_scan(np ? 1u : 0u, lds4, &cnt);
+            if (cursor + tot + 1u > end) break;          // sizes disagree: never overrun
+            for (uint32_t w0 = 0; w0 < tot; w0 += kWin) {
+                const uint32_t wl = min(kWin, tot - w0);
+                const u64 g = cursor + w0;
+                const uint32_t sh = (uint32_t)(g & 15u);
+                const Win win{buf + sh, w0, wl};
+                if (np && win.hits(pos, sz)) {
+                    stage_elem_header(win, W.d, e, np, pos);
+                    uint32_t q = pos + 7u + (W.d.elem_off[e + 1] - W.d.elem_off[e]);
+                    const uint32_t r0 = W.rb[e], rc = W.rb[e + 1] - r0;
+                    for (uint32_t r = 0; r < rc; ++r) {
+                        const uint32_t t = W.rslot[r0 + r];
+                        const u64x2 v = c[(u64)e * tw + (t >> 6)];
+                        if (!((v.x >> (t & 63u)) & 1ull)) continue;
+                        const bool rm = (v.y >> (t & 63u)) & 1ull;
+                        const uint32_t rl = W.RL + (rm ? 7u : 8u);
+                        if (win.hits(q, rl)) {
+                            win.span(q, W.rec + (u64)(r0 + r) * W.RS, W.RL);
+                            if (rm) win.span(q + W.RL, kAtomTrue, 7);
+                            else win.span(q + W.RL, kAtomFalse, 8);
+                        }
+                        q += rl;
+                    }
+                    win.put(q, 106);
+                }
+                __syncthreads();
+                copy_out(buf, sh, wl, out, g);
+                __syncthreads();
+            }
+            cursor += tot;
+            n += cnt;
+        }
+        if (threadIdx.x == 0) {
+            write_list_header(out, base, hdr, tag, vers, n ? 108 : 106, n);
+            if (n && cursor < end) out[cursor] = 106;
+        }
+        __syncthreads();
+    }
+}
+
+// cells re-laid: E_old x tw_old pairs -> E_new x tw_new (new element slots and pairs
+// {0, 0}); a variable's cells when its namespace grows or goes wide
+__global__ __launch_bounds__(kBlock) void k_relay(u64x2* dst, const u64x2* src, uint32_t eo,
+                                                  uint32_t to, uint32_t en, uint32_t tn) {
+    const u64 n = (u64)en * tn;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        const uint32_t e = (uint32_t)(i / tn), j = (uint32_t)(i % tn);
+        dst[i] = e < eo && j < to && src ? src[(u64)e * to + j] : u64x2{0, 0};
+    }
+}
+
+}  // namespace
+
+int wide_dict_create(laspj_ctx* ctx, const WideExport& x, uint32_t tw, WideDict** out) {
+    *out = nullptr;
+    const uint32_t K = (uint32_t)x.eorder.size();
+    if (K == 0) return LASPJ_E_SHAPE;
+    uint32_t TL = 0;
+    for (size_t r = 0; r + 1 < x.toff.size(); ++r) {
+        const uint32_t L = x.toff[r + 1] - x.toff[r];
+        if (!TL) TL = L;
+        else if (L != TL) return LASPJ_E_UNSUPPORTED;      // token images of several lengths
+    }
+    if (!TL) TL = 20;                                      // (no tokens yet)
+    const uint32_t RL = TL + 2u;
+    if (RL > 48) return LASPJ_E_UNSUPPORTED;
+    const uint64_t RS = (RL + 15u) & ~15u;
+    auto pad16 = [](uint64_t v) { return (v + 15ull) & ~15ull; };
+    const uint64_t nr = x.rslot.size();
+    // element tables as laspj_etf_dict_create lays them: images, offsets, order, padded
+    // images, header templates 104 2 <elem image> 108
+    std::vector<uint32_t> epoff(K), hpoff(K);
+    uint64_t epn = 0, hpn = 0;
+    for (uint32_t e = 0; e < K; ++e) {
+        epoff[e] = (uint32_t)epn;
+        epn += pad16(x.eoff[e + 1] - x.eoff[e]);
+        hpoff[e] = (uint32_t)hpn;
+        hpn += pad16(x.eoff[e + 1] - x.eoff[e] + 3ull);
+    }
+    epn += 48;
+    hpn += 48;
+    // the block: elem_blob | elem_off | elem_order | elem_pad | elem_poff | ehdr_pad |
+    // ehdr_poff | rb | rslot | rec
+    auto al = [](uint64_t v) { return (v + 255ull) & ~255ull; };
+    const uint64_t o_eb = 0, o_eo = o_eb + al(x.eblob.size() + 1), o_ord = o_eo + al(4ull * (K + 1)),
+                   o_ep = o_ord + al(4ull * K), o_epo = o_ep + al(epn), o_hp = o_epo + al(4ull * K),
+                   o_hpo = o_hp + al(hpn), o_rb = o_hpo + al(4ull * K),
+                   o_rs = o_rb + al(4ull * (K + 1)), o_rec = o_rs + al(2ull * nr + 2),
+                   total = o_rec + al(nr * RS + 48);
+    std::vector<uint8_t> h(total, 0);
+    std::memcpy(h.data() + o_eb, x.eblob.data(), x.eblob.size());
+    std::memcpy(h.data() + o_eo, x.eoff.data(), 4ull * (K + 1));
+    std::memcpy(h.data() + o_ord, x.eorder.data(), 4ull * K);
+    for (uint32_t e = 0; e < K; ++e) {
+        const uint32_t l = x.eoff[e + 1] - x.eoff[e];
+        std::memcpy(h.data() + o_ep + epoff[e], x.eblob.data() + x.eoff[e], l);
+        uint8_t* hp = h.data() + o_hp + hpoff[e];
+        hp[0] = 104;
+        hp[1] = 2;
+        std::memcpy(hp + 2, x.eblob.data() + x.eoff[e], l);
+        hp[2 + l] = 108;
+    }
+    std::memcpy(h.data() + o_epo, epoff.data(), 4ull * K);
+    std::memcpy(h.data() + o_hpo, hpoff.data(), 4ull * K);
+    std::memcpy(h.data() + o_rb, x.rb.data(), 4ull * (K + 1));
+    if (nr) std::memcpy(h.data() + o_rs, x.rslot.data(), 2ull * nr);
+    for (uint64_t r = 0; r < nr; ++r) {
+        uint8_t* t = h.data() + o_rec + r * RS;
+        t[0] = 104;
+        t[1] = 2;
+        std::memcpy(t + 2, x.tblob.data() + x.toff[r], TL);
+    }
+    auto* w = new (std::nothrow) WideDict;
+    if (!w) return LASPJ_E_NOMEM;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        hipSetDevice(ctx->device);
+        if (dev_alloc(ctx, total, &w->block) != hipSuccess) {
+            hipGetLastError();
+            delete w;
+            return LASPJ_E_NOMEM;
+        }
+        w->block_bytes = total;
+        if (hipMemcpyAsync(w->block, h.data(), total, hipMemcpyHostToDevice, ctx->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            dev_release(ctx, w->block, total);
+            delete w;
+            return LASPJ_E_DEVICE;
+        }
+    }
+    const uint8_t* b = static_cast<const uint8_t*>(w->block);
+    w->ctx = ctx;
+    std::memset(&w->v, 0, sizeof(w->v));
+    w->v.d.elem_blob = b + o_eb;
+    w->v.d.elem_off = reinterpret_cast<const uint32_t*>(b + o_eo);
+    w->v.d.elem_order = reinterpret_cast<const uint32_t*>(b + o_ord);
+    w->v.d.elem_pad = b + o_ep;
+    w->v.d.elem_poff = reinterpret_cast<const uint32_t*>(b + o_epo);
+    w->v.d.ehdr_pad = b + o_hp;
+    w->v.d.ehdr_poff = reinterpret_cast<const uint32_t*>(b + o_hpo);
+    w->v.rb = reinterpret_cast<const uint32_t*>(b + o_rb);
+    w->v.rslot = reinterpret_cast<const uint16_t*>(b + o_rs);
+    w->v.rec = b + o_rec;
+    w->v.RL = RL;
+    w->v.RS = (uint32_t)RS;
+    w->v.E = K;
+    w->v.tw = tw;
+    w->max_cnt = x.max_cnt;
+    *out = w;
+    return LASPJ_OK;
+}
+
+void wide_dict_destroy(WideDict* w) {
+    if (!w) return;
+    {
+        std::lock_guard<std::mutex> lk(w->ctx->mu);
+        hipSetDevice(w->ctx->device);
+        dev_release(w->ctx, w->block, w->block_bytes);
+    }
+    delete w;
+}
+
+uint32_t wide_elements(const WideDict* w) { return w ? w->v.E : 0; }
+
+int wide_read_enqueue(laspj_ctx* ctx, const WideDict* w, const uint8_t* payload, uint64_t total,
+                      const u64* offs, uint64_t R, uint64_t* cells, int32_t* status, bool clear) {
+    if (clear)
+        LJ_HIP(ctx, hipMemsetAsync(cells, 0, R * (u64)w->v.E * w->v.tw * 16ull, ctx->stream));
+    const uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
+    hipLaunchKernelGGL(k_wide_read, dim3((unsigned)std::max<uint64_t>(1, std::min(blocks, cap))),
+                       dim3(kBlock), 0, ctx->stream, payload, (u64)total, offs, R, w->v,
+                       reinterpret_cast<u64x2*>(cells), status);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+int wide_size_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
+                      int tag, u64* offsets, uint32_t* flag) {
+    const uint64_t sizes_bytes = (8ull * R + 255ull) & ~255ull;
+    if (int s = reserve_scratch(ctx, sizes_bytes + scan_tmp_bytes(R))) return s;
+    u64* sizes = static_cast<u64*>(ctx->scratch);
+    u64* tmp = reinterpret_cast<u64*>(static_cast<char*>(ctx->scratch) + sizes_bytes);
+    const uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 16;
+    hipLaunchKernelGGL(k_wide_size, dim3((unsigned)std::max<uint64_t>(1, std::min(blocks, cap))),
+                       dim3(kBlock), 0, ctx->stream, reinterpret_cast<const u64x2*>(cells), R, w->v,
+                       tag >= 0 ? 2u : 0u, sizes, flag);
+    LJ_LAUNCHED(ctx);
+    LJ_HIP(ctx, launch_scan(ctx, sizes, offsets, R, tmp));
+    return LASPJ_OK;
+}
+
+int wide_write_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
+                       int tag, int vers, const u64* offsets, uint8_t* out, uint64_t cap) {
+    const uint64_t g = std::min<uint64_t>(R, (uint64_t)ctx->cus * 8);
+    hipLaunchKernelGGL(k_wide_write, dim3((unsigned)std::max<uint64_t>(1, g)), dim3(kBlock), 0,
+                       ctx->stream, reinterpret_cast<const u64x2*>(cells), R, w->v, tag, vers,
+                       offsets, out, (u64)cap);
+    LJ_LAUNCHED(ctx);
+    return LASPJ_OK;
+}
+
+hipError_t launch_relay(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src, uint32_t eo,
+                        uint32_t to, uint32_t en, uint32_t tn) {
+    const uint64_t n = (uint64_t)en * tn;
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock,
+                                                                (uint64_t)ctx->cus * 8));
+    hipLaunchKernelGGL(k_relay, dim3((unsigned)g), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<u64x2*>(dst), reinterpret_cast<const u64x2*>(src), eo, to,
+                       en, tn);
+    return hipGetLastError();
+}
+
+}  // namespace laspj

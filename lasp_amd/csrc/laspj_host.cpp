@@ -590,6 +590,13 @@ struct Dict {
     // a token), undone in reverse when the payload fails: binary_to_term/1 would have
     // rejected it whole, so none of its terms may take a slot
     std::vector<int64_t> journal;
+    // token slots an element may hold: 64 (the columnar cells' {p, r} pair); a wide
+    // namespace's dictionary (the NIF's k-pair cells) raises it
+    uint32_t tok_cap = 64;
+    // a wide dictionary's token images all have one length (its device templates are
+    // fixed-width); 0: not wide, or no token yet
+    uint32_t tok_len = 0, tok_len_max = 0;
+    uint64_t ntok = 0;                      // tokens registered (all elements)
     // element slots that gained a token since the last dict_take_dirty (the NIF patches
     // their device rows; may repeat a slot or name one whose gain was rolled back)
     std::vector<uint32_t> dirty;
@@ -614,10 +621,12 @@ struct Dict {
                 tok_slot.pop_last();
                 tok_eq.pop_last();
                 toks[(size_t)journal[j]].pop_back();
+                --ntok;
             }
             store.pop_back();
         }
         journal.clear();
+        if (!ntok) tok_len = 0;             // (a length no registered token fixes)
     }
 
     std::string_view keep(const uint8_t* p, size_t n) {
@@ -782,10 +791,10 @@ int reg_elem(Dict* d, const uint8_t* k, size_t kl, uint32_t* slot) {
     return LASPJ_DEC_OK;
 }
 
-int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
+int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint16_t* slot) {
     const int f = d->tok(es, t, tl);
     if (f >= 0) {
-        *slot = (uint8_t)f;
+        *slot = (uint16_t)f;
         return LASPJ_DEC_OK;
     }
     bool ok = true;
@@ -798,12 +807,17 @@ int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint8_t* slot) {
             return term_cmp(t, tl, (const uint8_t*)o.data(), o.size(), &ok2) == 0 && ok2;
         }))
         return LASPJ_DEC_EQUAL_TERMS;
-    if (d->toks[es].size() >= 64) return LASPJ_DEC_UNREPRESENTABLE;
-    *slot = (uint8_t)d->toks[es].size();
+    if (d->toks[es].size() >= d->tok_cap) return LASPJ_DEC_UNREPRESENTABLE;
+    if (d->tok_len_max) {
+        if (d->tok_len ? tl != d->tok_len : tl > d->tok_len_max) return LASPJ_DEC_UNREPRESENTABLE;
+        d->tok_len = (uint32_t)tl;
+    }
+    *slot = (uint16_t)d->toks[es].size();
     std::string_view v = d->keep(t, tl);
     d->tok_slot.insert(tok_hash(es, t, tl), es, v, *slot);
     d->tok_eq.insert(ht, es, v, *slot);
     d->toks[es].push_back(v);
+    ++d->ntok;
     d->journal.push_back((int64_t)es);
     d->dirty.push_back(es);
     return LASPJ_DEC_OK;
@@ -868,7 +882,7 @@ int laspj_dict_add(laspj_dict* dict, int32_t kind, const uint8_t* blob, const ui
                 st = walk_orset_payload(
                     pp, pn, tag, [&](const uint8_t* k, size_t kl) { return reg_elem(d, k, kl, &cur); },
                     [&](const uint8_t*, size_t, const uint8_t* tk, size_t tkl, bool) {
-                        uint8_t s;
+                        uint16_t s;
                         return reg_tok(d, cur, tk, tkl, &s);
                     });
             } else {
@@ -1139,7 +1153,7 @@ int dict_add_elems(laspj_dict* dict, const uint8_t* p, size_t n, size_t from, si
                 const size_t fl = off < n ? term_len(p + off, n - off) : 0;
                 if (!fl || bool_atom(p + off) < 0) { st = LASPJ_DEC_MALFORMED; break; }
                 off += fl;
-                uint8_t s;
+                uint16_t s;
                 st = reg_tok(d, cur, tk, tkl, &s);
             }
             if (st) break;
@@ -1234,7 +1248,7 @@ int list_walk(laspj_dict* dict, int32_t kind, const uint8_t* p, size_t n, ListIt
                             st = LASPJ_DEC_MALFORMED;
                             break;
                         }
-                        uint8_t ts = 0;
+                        uint16_t ts = 0;
                         if ((st = reg_tok(d, key, r + 2, tl, &ts))) break;
                         it->toks.push_back((64ull * key + ts) | (flag ? kFlagBit : 0ull));
                     }
@@ -1574,9 +1588,70 @@ int dict_reg_elem(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot
     }
 }
 
+bool dict_set_tok_cap(laspj_dict* dict, uint32_t cap, uint32_t max_len) {
+    Dict& d = dict->d;
+    if (max_len) {
+        // every token registered so far of one length, at most max_len
+        uint32_t tl = 0;
+        for (const auto& tv : d.toks)
+            for (std::string_view t : tv) {
+                if (t.size() > max_len || (tl && t.size() != tl)) return false;
+                tl = (uint32_t)t.size();
+            }
+        d.tok_len = tl;
+    }
+    d.tok_len_max = max_len;
+    d.tok_cap = cap;
+    return true;
+}
+uint32_t dict_tok_cap(const laspj_dict* dict) { return dict->d.tok_cap; }
+
+int dict_export_wide(const laspj_dict* dict, WideExport* x) {
+    const Dict& d = dict->d;
+    const uint32_t K = (uint32_t)d.elems.size();
+    try {
+        x->eoff.assign(K + 1ull, 0);
+        x->eblob.clear();
+        for (uint32_t e = 0; e < K; ++e) {
+            x->eblob.insert(x->eblob.end(), d.elems[e].begin(), d.elems[e].end());
+            x->eoff[e + 1] = (uint32_t)x->eblob.size();
+        }
+        x->eorder.resize(K);
+        for (uint32_t e = 0; e < K; ++e) x->eorder[e] = e;
+        std::stable_sort(x->eorder.begin(), x->eorder.end(), [&](uint32_t a, uint32_t b) {
+            return cmp_view(d.elems[a], d.elems[b]) < 0;
+        });
+        // tokens by element slot, each element's in term order (rank), CSR
+        x->rb.assign(K + 1ull, 0);
+        x->rslot.clear();
+        x->tblob.clear();
+        x->toff.assign(1, 0);
+        x->max_cnt = 0;
+        std::vector<uint16_t> ord;
+        for (uint32_t e = 0; e < K; ++e) {
+            const auto& tv = d.toks[e];
+            ord.resize(tv.size());
+            for (size_t k = 0; k < ord.size(); ++k) ord[k] = (uint16_t)k;
+            std::stable_sort(ord.begin(), ord.end(), [&](uint16_t a, uint16_t b) {
+                return cmp_view(tv[a], tv[b]) < 0;
+            });
+            for (uint16_t k : ord) {
+                x->rslot.push_back(k);
+                x->tblob.insert(x->tblob.end(), tv[k].begin(), tv[k].end());
+                x->toff.push_back((uint32_t)x->tblob.size());
+            }
+            x->rb[e + 1] = (uint32_t)x->rslot.size();
+            x->max_cnt = std::max<uint32_t>(x->max_cnt, (uint32_t)tv.size());
+        }
+    } catch (const std::bad_alloc&) {
+        return LASPJ_E_NOMEM;
+    }
+    return LASPJ_OK;
+}
+
 int dict_reg_tok(laspj_dict* dict, uint32_t e, const uint8_t* img, size_t n, uint32_t* slot) {
     try {
-        uint8_t s = 0;
+        uint16_t s = 0;
         const int st = reg_tok(&dict->d, e, img, n, &s);
         *slot = s;
         return st;

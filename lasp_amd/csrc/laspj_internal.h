@@ -317,6 +317,7 @@ struct ChainJob {
     int32_t* status = nullptr;
     uint32_t nrep = 0, S = 0;
     bool armed = false;
+    void* hres = nullptr;      // (or null) host-visible copy of a failed payload's results
 };
 // segbase: plan.segbase already on the device, or null (uploaded here); clear: zero the
 // batch first (the decoders only set the cells they decode)
@@ -449,6 +450,42 @@ void dict_begin(laspj_dict* dict);
 void dict_rollback(laspj_dict* dict);
 int dict_reg_elem(laspj_dict* dict, const uint8_t* img, size_t n, uint32_t* slot);
 int dict_reg_tok(laspj_dict* dict, uint32_t e, const uint8_t* img, size_t n, uint32_t* slot);
+// token slots per element (64 by default; a wide namespace's 64 k)
+// token slots per element (64: the narrow cells); max_len > 0: from now on every token image
+// has the length of the first (at most max_len) — false when those registered already differ
+bool dict_set_tok_cap(laspj_dict* dict, uint32_t cap, uint32_t max_len = 0);
+uint32_t dict_tok_cap(const laspj_dict* dict);
+// a wide namespace's dictionary for its device tables: element images by slot (eblob /
+// eoff) and slots in term order (eorder); per element slot e the tokens in term order,
+// ranks rb[e] .. rb[e+1): rslot = the rank's token slot, its image tblob[toff[r] ..
+// toff[r+1]); max_cnt = the most tokens any element holds
+struct WideExport {
+    std::vector<uint8_t> eblob, tblob;
+    std::vector<uint32_t> eoff, eorder, rb, toff;
+    std::vector<uint16_t> rslot;
+    uint32_t max_cnt = 0;
+};
+int dict_export_wide(const laspj_dict* dict, WideExport* x);
+
+// ---- wide namespaces (laspj_codec.hip): device tables of a dictionary whose elements may
+// hold up to 64 tw tokens, cells of tw {p, r} pairs per element slot; LASPJ_E_UNSUPPORTED
+// for token images of several lengths (or longer than 46 bytes)
+struct WideDict;
+int wide_dict_create(laspj_ctx* ctx, const WideExport& x, uint32_t tw, WideDict** out);
+void wide_dict_destroy(WideDict* w);
+uint32_t wide_elements(const WideDict* w);
+// decode / size / write, enqueue only (offsets, status, out: device addresses)
+int wide_read_enqueue(laspj_ctx* ctx, const WideDict* w, const uint8_t* payload, uint64_t total,
+                      const unsigned long long* offs, uint64_t R, uint64_t* cells,
+                      int32_t* status, bool clear);
+int wide_size_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
+                      int tag, unsigned long long* offsets, uint32_t* flag);
+int wide_write_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
+                       int tag, int vers, const unsigned long long* offsets, uint8_t* out,
+                       uint64_t cap);
+// dst (en x tn pairs) := src (eo x to pairs) re-laid, the rest {0, 0}; src may be null
+hipError_t launch_relay(laspj_ctx* ctx, uint64_t* dst, const uint64_t* src, uint32_t eo,
+                        uint32_t to, uint32_t en, uint32_t tn);
 
 
 // ---- list values as images (laspj_host.cpp; used by laspj_list_etf.cpp) ---------------

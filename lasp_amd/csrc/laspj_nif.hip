@@ -70,6 +70,12 @@ struct KindState {
     std::vector<uint32_t> built_cnt;
     // the variables whose cells refer to this dictionary (none for the image calls')
     std::unordered_set<laspj_var*> vars;
+    // a wide namespace: an element holds more than 64 tokens (add_elem never collects one,
+    // lasp_orset.erl:222-241): cells of tw {p, r} pairs per element, the wide tables in wd
+    // (etf then holds the element images only, for value/1's G-Set answer)
+    bool wide = false;
+    uint32_t tw = 1;
+    WideDict* wd = nullptr;
 };
 
 }  // namespace laspj
@@ -84,6 +90,7 @@ struct laspj_var {
     uint64_t* cells = nullptr;       // one replica over `E` element slots (null: new())
     uint64_t cell_bytes = 0;         // the block's size (dev_alloc)
     uint32_t E = 0;
+    uint32_t tw = 1;                 // {p, r} pairs per element slot (a wide namespace's)
     uint64_t epoch = 0;              // the dictionary generation the cells refer to
     bool resident = true;            // cells hold the value (else `image` does)
     bool held = false;               // `image` is a value write/4 could not represent
@@ -173,15 +180,19 @@ __global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src
 // call — fails the call ({error, {precondition, {not_present, E}}}, remove_elems / apply_ops
 // stop there and the state is kept); element 0xFFFFFFFF is an element the dictionary has
 // never held.  Few ops travel as kernel arguments (no upload on the update path); one lane
-// walks them (a call is a handful of ops).
+// walks them (a call is a handful of ops).  tw {p, r} pairs per element (a wide namespace:
+// token slot t in pair t / 64, the slot's bits 8..15 in the op's pad byte).
 constexpr uint32_t kUpdArgOps = 24;
 struct UpdArgs {
     laspj_op op[kUpdArgOps];
 };
 constexpr uint32_t kNoElem = 0xFFFFFFFFu;
 
+__device__ inline uint32_t op_slot(const laspj_op& o) { return o.slot | (uint32_t)o.pad << 8; }
+
 __global__ void __launch_bounds__(64) k_var_update(uint64_t* __restrict__ cells, int32_t kind,
-                                                   UpdArgs a, const laspj_op* __restrict__ dops,
+                                                   uint32_t tw, UpdArgs a,
+                                                   const laspj_op* __restrict__ dops,
                                                    uint32_t nops, int32_t* __restrict__ status) {
     if (threadIdx.x != 0) return;
     auto op = [&](uint32_t k) -> laspj_op { return dops ? dops[k] : a.op[k]; };
@@ -190,7 +201,10 @@ __global__ void __launch_bounds__(64) k_var_update(uint64_t* __restrict__ cells,
         for (uint32_t k = 0; k < nops && bad == nops; ++k) {
             const laspj_op o = op(k);
             if (o.kind != LASPJ_OP_REMOVE) continue;
-            bool present = o.element != kNoElem && cells[2ull * o.element] != 0;
+            bool present = false;
+            if (o.element != kNoElem)
+                for (uint32_t j = 0; j < tw && !present; ++j)
+                    present = cells[2ull * ((uint64_t)o.element * tw + j)] != 0;
             for (uint32_t j = 0; j < k && !present; ++j) {
                 const laspj_op q = op(j);
                 present = q.kind == LASPJ_OP_ADD && q.element == o.element;
@@ -205,13 +219,15 @@ __global__ void __launch_bounds__(64) k_var_update(uint64_t* __restrict__ cells,
         }
         const laspj_op o = op(k);
         if (kind == LASPJ_KIND_ORSET) {
-            uint64_t* c = cells + 2ull * o.element;
+            uint64_t* c = cells + 2ull * (uint64_t)o.element * tw;
             if (o.kind == LASPJ_OP_ADD) {
                 // orddict:store(Token, false, Tokens): present, flag false
-                c[0] |= 1ull << o.slot;
-                c[1] &= ~(1ull << o.slot);
+                const uint32_t t = op_slot(o);
+                c[2 * (t >> 6)] |= 1ull << (t & 63u);
+                c[2 * (t >> 6) + 1] &= ~(1ull << (t & 63u));
             } else {
-                c[1] = c[0];                           // every token of Elem := true
+                for (uint32_t j = 0; j < tw; ++j)
+                    c[2 * j + 1] = c[2 * j];           // every token of Elem := true
             }
         } else {
             cells[o.element >> 6] |= 1ull << (o.element & 63u);
@@ -222,14 +238,17 @@ __global__ void __launch_bounds__(64) k_var_update(uint64_t* __restrict__ cells,
 
 // the same for a call of ADDs only (add_all over many elements): commutative, one op per lane
 __global__ void __launch_bounds__(256) k_var_adds(uint64_t* __restrict__ cells, int32_t kind,
-                                                  const laspj_op* __restrict__ ops, uint32_t nops) {
+                                                  uint32_t tw, const laspj_op* __restrict__ ops,
+                                                  uint32_t nops) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nops) return;
     const laspj_op o = ops[k];
     if (kind == LASPJ_KIND_ORSET) {
-        unsigned long long* c = reinterpret_cast<unsigned long long*>(cells + 2ull * o.element);
-        atomicOr(c, 1ull << o.slot);
-        atomicAnd(c + 1, ~(1ull << o.slot));
+        const uint32_t t = op_slot(o);
+        unsigned long long* c = reinterpret_cast<unsigned long long*>(
+            cells + 2ull * ((uint64_t)o.element * tw + (t >> 6)));
+        atomicOr(c, 1ull << (t & 63u));
+        atomicAnd(c + 1, ~(1ull << (t & 63u)));
     } else {
         atomicOr(reinterpret_cast<unsigned long long*>(cells + (o.element >> 6)),
                  1ull << (o.element & 63u));
@@ -242,6 +261,9 @@ struct Guard {
 };
 
 constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is reset
+// a wide namespace (an element past 64 tokens): token slots per element, and the token
+// image length its fixed-width templates hold
+constexpr uint32_t kWideTokens = 1024, kWideTokenLen = 46;
 // device passes per call: registration, a grown answer area and a serial re-decode each
 // take one; a call still unresolved after this many answers FALLBACK (run's post-condition)
 constexpr int kMaxPasses = 6;
@@ -253,9 +275,12 @@ constexpr uint64_t kPullPiece = 512ull << 10;
 
 uint64_t al(uint64_t x, uint64_t a) { return (x + a - 1) & ~(a - 1); }
 
-uint64_t wpr_of(int32_t kind, uint32_t E) {
-    return kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
+uint64_t wpr_of(int32_t kind, uint32_t E, uint32_t tw = 1) {
+    return kind == LASPJ_KIND_ORSET ? 2ull * E * tw : (E + 63ull) / 64ull;
 }
+
+// pairs per element slot of a namespace's cells
+uint32_t ktw(const KindState& K) { return K.wide ? K.tw : 1u; }
 
 // the payloads [p0, p1) of a call decoded against one dictionary (an image call: the
 // context's; a variable call: one per namespace of its variables)
@@ -294,14 +319,16 @@ KindState& kstate(NifState* S, int32_t kind) {
     return S->ks[kind == LASPJ_KIND_GSET ? 1 : 0];
 }
 
-laspj_batch view(laspj_ctx* ctx, int32_t kind, uint64_t R, uint32_t E, uint64_t* dev) {
+laspj_batch view(laspj_ctx* ctx, int32_t kind, uint64_t R, uint32_t E, uint64_t* dev,
+                 uint32_t tw = 1) {
     laspj_batch b;
     b.ctx = ctx;
-    b.kind = kind;
+    b.kind = kind == LASPJ_KIND_ORSET && tw > 1 ? LASPJ_KIND_ORSET_WIDE : kind;
     b.elements = E;
     b.replicas = R;
-    b.words_per_replica = wpr_of(kind, E);
+    b.words_per_replica = wpr_of(kind, E, tw);
     b.cells = E;
+    b.tok_words = kind == LASPJ_KIND_ORSET ? tw : 1;
     b.dev = dev;
     b.owns = false;
     return b;
@@ -350,6 +377,8 @@ int grow_host(laspj_ctx* ctx, void** p, uint64_t* have, uint64_t need) {
 void free_etf(KindState& K) {
     if (K.etf) laspj_etf_dict_destroy(K.etf);
     K.etf = nullptr;
+    if (K.wd) wide_dict_destroy(K.wd);
+    K.wd = nullptr;
     K.E = 0;
 }
 
@@ -359,7 +388,61 @@ uint64_t now_ns() {
 }
 
 // the device images of the dictionary (called without ctx->mu: etf_dict_create takes it)
+// a wide namespace's tables (called as rebuild_etf): every element exactly (no headroom:
+// any registration rebuilds — the wide path is the rare one), pairs per cell grown to hold
+// the widest element; LASPJ_E_UNSUPPORTED: token images of several lengths
+int rebuild_wide(laspj_ctx* ctx, NifState* S, KindState& K) {
+    const uint64_t t0 = now_ns();
+    WideExport x;
+    if (int s = dict_export_wide(K.dict, &x)) return fail(ctx, s, "nif: wide export");
+    const uint32_t n = (uint32_t)x.eorder.size();
+    if (!n) return LASPJ_E_UNSUPPORTED;
+    const uint32_t tw = std::max(K.tw, std::max(2u, (x.max_cnt + 63u) / 64u));
+    WideDict* wd = nullptr;
+    if (int s = wide_dict_create(ctx, x, tw, &wd)) return s;
+    laspj_etf_dict* g = nullptr;
+    if (int s = laspj_etf_dict_create(ctx, n, x.eblob.data(), x.eoff.data(), x.eorder.data(),
+                                      nullptr, nullptr, nullptr, &g)) {
+        wide_dict_destroy(wd);
+        return s;
+    }
+    free_etf(K);
+    K.wd = wd;
+    K.etf = g;
+    K.E = n;
+    K.tw = tw;
+    K.stale = false;
+    K.built_K = n;
+    {
+        std::vector<uint32_t> gone;
+        dict_take_dirty(K.dict, &gone);
+    }
+    ++S->stats[4];
+    S->stats[13] += now_ns() - t0;
+    return LASPJ_OK;
+}
+
+// the namespace takes elements of more than 64 tokens from now on (its cells widen on
+// their next use; slots are unchanged, so nothing is written out)
+// (false: the namespace stays narrow — its token images are not of one length, which the
+// wide templates need)
+bool go_wide(KindState& K) {
+    if (K.wide) return true;
+    if (K.kind != LASPJ_KIND_ORSET || !K.dict) return false;
+    if (!dict_set_tok_cap(K.dict, kWideTokens, kWideTokenLen)) return false;
+    K.wide = true;
+    K.stale = true;
+    return true;
+}
+
 int rebuild_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
+    if (K.wide && dict_elements(K.dict) == 0) {
+        // (every registration that widened it was refused: narrow again)
+        dict_set_tok_cap(K.dict, 64, 0);
+        K.wide = false;
+        K.tw = 1;
+    }
+    if (K.wide) return rebuild_wide(ctx, S, K);
     const uint64_t t0 = now_ns();
     uint32_t n = 0;
     uint64_t eb = 0, tb = 0;
@@ -402,7 +485,7 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
 // Registrations that only added tokens to elements the images already hold: their rows
 // patched in place.  False: rebuild (new elements, an element past its headroom, ...).
 bool patch_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
-    if (!K.etf || K.kind != LASPJ_KIND_ORSET) return false;
+    if (!K.etf || K.kind != LASPJ_KIND_ORSET || K.wide) return false;
     const uint64_t t0 = now_ns();
     const uint32_t n = dict_elements(K.dict);
     if (n != K.built_K || n > K.E) return false;
@@ -428,13 +511,14 @@ void release_cells(laspj_ctx* ctx, laspj_var* v) {
     v->cells = nullptr;
     v->cell_bytes = 0;
     v->E = 0;
+    v->tw = 1;
 }
 
 // a variable's cells widened to the dictionary's E (slots are append-only: the old cells
 // stay where they are, the new slots start absent); call with ctx->mu held
-int fit_var(laspj_ctx* ctx, laspj_var* v, uint32_t E) {
-    if (v->cells && v->E == E) return LASPJ_OK;
-    const uint64_t wnew = wpr_of(v->kind, E), wold = v->cells ? wpr_of(v->kind, v->E) : 0;
+int fit_var(laspj_ctx* ctx, laspj_var* v, uint32_t E, uint32_t tw = 1) {
+    if (v->cells && v->E == E && v->tw == tw) return LASPJ_OK;
+    const uint64_t wnew = wpr_of(v->kind, E, tw), wold = v->cells ? wpr_of(v->kind, v->E, v->tw) : 0;
     const uint64_t bytes = std::max<uint64_t>(8ull * wnew, 256);
     void* p = nullptr;
     if (dev_alloc(ctx, bytes, &p) != hipSuccess) {
@@ -443,15 +527,21 @@ int fit_var(laspj_ctx* ctx, laspj_var* v, uint32_t E) {
                     (unsigned long long)bytes);
     }
     uint64_t* c = static_cast<uint64_t*>(p);
-    const uint64_t keep = std::min(wold, wnew);
-    if (keep) LJ_HIP(ctx, hipMemcpyAsync(c, v->cells, 8ull * keep, hipMemcpyDeviceToDevice,
-                                         ctx->stream));
-    if (wnew > keep)
-        LJ_HIP(ctx, hipMemsetAsync(c + keep, 0, 8ull * (wnew - keep), ctx->stream));
+    if (v->kind == LASPJ_KIND_ORSET && (tw != 1 || (v->cells && v->tw != 1))) {
+        // pairs per element change (a namespace gone wide): re-laid, slot for slot
+        LJ_HIP(ctx, launch_relay(ctx, c, v->cells, v->cells ? v->E : 0, v->cells ? v->tw : 1, E, tw));
+    } else {
+        const uint64_t keep = std::min(wold, wnew);
+        if (keep) LJ_HIP(ctx, hipMemcpyAsync(c, v->cells, 8ull * keep, hipMemcpyDeviceToDevice,
+                                             ctx->stream));
+        if (wnew > keep)
+            LJ_HIP(ctx, hipMemsetAsync(c + keep, 0, 8ull * (wnew - keep), ctx->stream));
+    }
     release_cells(ctx, v);
     v->cells = c;
     v->cell_bytes = bytes;
     v->E = E;
+    v->tw = tw;
     return LASPJ_OK;
 }
 
@@ -465,11 +555,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const size_t G = c.groups.size();
     // single-group ops (every op but BIND / WRITE) answer over group 0's dictionary
     KindState& K = *c.groups[0].K;
-    const uint32_t E = K.E;
+    const uint32_t E = K.E, TW = ktw(K);
     const bool orset = c.kind == LASPJ_KIND_ORSET;
+    const bool wide = orset && K.wide;            // (single-group ops: answers by the wide codec)
     bool dec = m != 0;
     for (const Group& g : c.groups)
-        if (orset && g.p1 > g.p0 && !etf_dict_decodable(g.K->etf)) dec = false;
+        if (orset && g.p1 > g.p0 && !g.K->wide && !etf_dict_decodable(g.K->etf)) dec = false;
     const bool var_op = c.op == Op::BIND || c.op == Op::WRITE;
     const bool var_in = var_op || c.op == Op::THRESHOLD || c.op == Op::READ || c.op == Op::VVALUE;
     std::vector<unsigned long long> hoffs(m + 1ull, 0);
@@ -483,19 +574,22 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     for (size_t g = 0; g < G; ++g) {
         const Group& gr = c.groups[g];
         gcell[g] = in_words;
-        in_words += (uint64_t)(gr.p1 - gr.p0) * wpr_of(c.kind, gr.K->E);
+        in_words += (uint64_t)(gr.p1 - gr.p0) * wpr_of(c.kind, gr.K->E, ktw(*gr.K));
         eg[g] = EtfGroup{gr.K->etf, gr.p0, gr.p1, nullptr, gr.K->E};
     }
     // several namespaces' OR-Set payloads: one decode launch over all of them (a table of
     // the dictionaries rides in the in region) with one plan, else group by group, each
     // with its own plan and segment table
-    const bool multi = G > 1 && dec && orset &&
+    bool any_wide = false;
+    for (const Group& g : c.groups) any_wide |= orset && g.K->wide;
+    const bool multi = G > 1 && dec && orset && !any_wide &&
                        etf_multi_fill(ctx, eg.data(), (uint32_t)G, m, nullptr);
     std::vector<EtfReadPlan> plans(multi ? 1 : G);
     for (size_t g = 0; g < plans.size(); ++g) {
         const Group& gr = c.groups[g];
         const uint32_t p0 = multi ? 0 : gr.p0, R = multi ? m : gr.p1 - gr.p0;
-        if (dec && orset && R) etf_read_plan(ctx, gr.K->etf, R, hoffs.data() + p0, &plans[g]);
+        if (dec && orset && R && !gr.K->wide)
+            etf_read_plan(ctx, gr.K->etf, R, hoffs.data() + p0, &plans[g]);
         gseg[g] = seg_area;
         if (plans[g].nseg) seg_area += al(4ull * (R + 1), 16);
     }
@@ -503,7 +597,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const uint64_t mtab_bytes = multi ? al(etf_multi_bytes((uint32_t)G, m), 256) : 0;
     const bool has_payload_out = c.op == Op::MERGE || c.op == Op::VALUE || c.op == Op::READ ||
                                  c.op == Op::VVALUE;
-    const uint64_t W = wpr_of(c.kind, E);            // words per replica (single-group ops)
+    const uint64_t W = wpr_of(c.kind, E, TW);        // words per replica (single-group ops)
     // in region (host -> device)
     // [offsets | segment tables | zeroed words: the size pass's ticket, the decoders' redo
     //  lists, the one-launch merge's look-back words, the variable kernel's difference words
@@ -520,7 +614,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const uint64_t in_bytes = i_pay + (dec ? al(pay + 64, 256) : al(cells_in, 256));
     // out region: written by kernels into the pinned staging
     const uint64_t o_st = 0, o_res = al(4ull * m, 16), o_ooff = o_res + al(n, 16),
-                   o_pay = o_ooff + al(8ull * (n + 1), 16);
+                   o_seg = o_ooff + al(8ull * (n + 1), 16);
+    uint64_t o_pay = o_seg;          // (after the segment results of a deferred decode)
     // answer payload bound: a merge's image is at most both operands' (flags may be
     // re-encoded one byte longer than a SMALL_ATOM_UTF8 input: the slack, and a second
     // pass when even that is short); value/1's at most its operand's; a variable's image
@@ -529,7 +624,6 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     for (uint32_t i = 0; i < m; ++i) bound += c.len[i];
     if (has_payload_out && S->ocap < bound + bound / 8) S->ocap = al(bound + bound / 8, 1 << 16);
     const uint64_t ocap = has_payload_out ? S->ocap : 0;
-    const uint64_t out_bytes = o_pay + ocap;
     // MERGE: the segment decoder's chain check rides on the join's launch (ChainJob), its
     // per-segment results in a device area of their own after the in region
     // (one plan only: the join / bind launch carries one chain check)
@@ -537,6 +631,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                        ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op ||
                         (c.op == Op::VALUE && etf_value_direct(ctx, n, E)));
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
+    o_pay += seg_bytes;              // (a failed payload's results, written by its chain check)
+    const uint64_t out_bytes = o_pay + ocap;
     // device statuses of the variable calls (their kernel reads them)
     const uint64_t vst_bytes = var_op ? al(4ull * m, 256) : 0;
     // cells: in batch m x W words; MERGE: answers n x W; VALUE / VVALUE: value words
@@ -570,7 +666,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         }
         if (var_in)
             for (laspj_var* v : c.vars)
-                if (int s = fit_var(ctx, v, v->ns->E)) return s;
+                if (int s = fit_var(ctx, v, v->ns->E, v->ns->wide ? v->ns->tw : 1)) return s;
     }
     uint8_t* hin = static_cast<uint8_t*>(S->hin);
     uint8_t* din = static_cast<uint8_t*>(S->dblk);
@@ -595,7 +691,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         // per variable: its cells, its decoded operand's cells, their width
         for (size_t g = 0; g < G; ++g) {
             const Group& gr = c.groups[g];
-            const uint64_t w = wpr_of(c.kind, gr.K->E);
+            const uint64_t w = wpr_of(c.kind, gr.K->E, ktw(*gr.K));
             maxw = std::max(maxw, w);
             for (uint32_t i = gr.p0; i < gr.p1; ++i) {
                 const uint64_t cur = reinterpret_cast<uint64_t>(c.vars[i]->cells);
@@ -622,6 +718,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         for (size_t g = 0; g < G; ++g) {
             const Group& gr = c.groups[g];
             if (gr.p1 == gr.p0) continue;
+            if (orset && gr.K->wide) {
+                // (a wide namespace beside one the device cannot decode: the host encoder
+                // lays narrow cells only — those operands answer FALLBACK)
+                for (uint32_t i = gr.p0; i < gr.p1; ++i) hst[i] = LASPJ_DEC_UNREPRESENTABLE;
+                continue;
+            }
             if (int s = laspj_dict_encode(gr.K->dict, c.kind, blob.data(),
                                           reinterpret_cast<const uint64_t*>(hoffs.data()) + gr.p0,
                                           gr.p1 - gr.p0, -1, gr.K->E,
@@ -684,12 +786,15 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             if (m) LJ_HIP(ctx, hipMemcpyAsync(cin, hin + i_pay, cells_in, hipMemcpyHostToDevice,
                                               ctx->stream));
         }
-        laspj_batch inb = view(ctx, c.kind, m, E, cin);
+        laspj_batch inb = view(ctx, c.kind, m, E, cin, TW);
         // statuses: straight into the pinned answer, or (variable calls) device memory their
         // kernel reads and publishes
         int32_t* dst = var_op ? dvst : reinterpret_cast<int32_t*>(rout + o_st);
         ChainJob cjob;
-        if (defer) cjob.res = dseg;
+        if (defer) {
+            cjob.res = dseg;
+            cjob.hres = rout + o_seg;
+        }
         if (dec && multi) {
             // every namespace's payloads in one launch (the cells zeroed first when the last
             // call left them dirty: the decoders only set what they decode)
@@ -709,7 +814,11 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 if (!R) continue;
                 laspj_batch gb = view(ctx, c.kind, R, gr.K->E, cin + gcell[g]);
                 const auto* doffs = reinterpret_cast<const unsigned long long*>(din + i_offs) + gr.p0;
-                if (orset) {
+                if (orset && gr.K->wide) {
+                    if (int s = wide_read_enqueue(ctx, gr.K->wd, din + i_pay, pay, doffs, R,
+                                                  cin + gcell[g], dst + gr.p0, !clean && !c.redo.n))
+                        return s;
+                } else if (orset) {
                     if (int s = etf_read_enqueue(
                             ctx, &gb, gr.K->etf, -1, 1, din + i_pay, pay, doffs, plans[g],
                             plans[g].nseg ? reinterpret_cast<const uint32_t*>(din + i_seg + gseg[g])
@@ -726,8 +835,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             LJ_HIP(ctx, hipMemcpyAsync(dvst, hst.data(), 4ull * m, hipMemcpyHostToDevice,
                                        ctx->stream));
         }
-        laspj_batch lhs = view(ctx, c.kind, n, E, cin);
-        laspj_batch rhs = view(ctx, c.kind, n, E, cin + (uint64_t)n * W);
+        laspj_batch lhs = view(ctx, c.kind, n, E, cin, TW);
+        laspj_batch rhs = view(ctx, c.kind, n, E, cin + (uint64_t)n * W, TW);
         auto* dooff = reinterpret_cast<unsigned long long*>(rout + o_ooff);
         uint8_t* dopay = rout + o_pay;
         switch (c.op) {
@@ -735,8 +844,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             // lasp_orset:merge/2 (lasp_orset.erl:128-134): the nested orddict:merge of two
             // canonical orddicts is the slot-wise OR of their cells; lasp_gset:merge/2
             // (lasp_gset.erl:99-101): ordsets:union of two ordsets, the OR of their bits
-            laspj_batch ob = view(ctx, c.kind, n, E, cout);
+            laspj_batch ob = view(ctx, c.kind, n, E, cout, TW);
             const unsigned long long* chunks = nullptr;
+            if (wide) {
+                // elements past 64 tokens: the OR, then the wide size pass and writer
+                LJ_HIP(ctx, launch_or(ctx, cout, lhs.dev, rhs.dev, (uint64_t)n * W));
+                if (int s = wide_size_enqueue(ctx, K.wd, cout, n, -1, dooff, ctx->flag)) return s;
+                if (int s = wide_write_enqueue(ctx, K.wd, cout, n, -1, 1, dooff, dopay, ocap))
+                    return s;
+                S->clean_words = 0;
+                break;
+            }
             if (orset && etf_merge_write_one(ctx, K.etf, n, E)) {
                 // one answer: join, size pass and writer in one launch (look-back), the
                 // operands cleared behind it, the chain checks riding along
@@ -777,7 +895,21 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             // value/1 (lasp_orset.erl:67-73): the elements with a {_, false} token, as the
             // ordset image the G-Set writer gives a bit row (term_to_binary of the keys)
             // (VVALUE has no operand cells: its value bits land where they would start)
-            laspj_batch src = c.op == Op::VALUE ? inb : view(ctx, c.kind, 1, E, c.vars[0]->cells);
+            laspj_batch src = c.op == Op::VALUE ? inb : view(ctx, c.kind, 1, E, c.vars[0]->cells, TW);
+            if (wide) {
+                // the value bits of the wide cells, then the G-Set writer over the element images
+                S->clean_words = 0;
+                LJ_HIP(ctx, launch_wide_value(ctx, &src, cout, false));
+                laspj_batch vb = view(ctx, LASPJ_KIND_GSET, n, E, cout);
+                const unsigned long long* chunks = nullptr;
+                if (int s = etf_size_enqueue(ctx, &vb, K.etf, LASPJ_KIND_GSET, -1, dooff, ctx->flag,
+                                             &chunks))
+                    return s;
+                if (int s = etf_write_enqueue(ctx, &vb, K.etf, LASPJ_KIND_GSET, -1, 1, dooff, dopay,
+                                              ocap, chunks))
+                    return s;
+                break;
+            }
             if (c.kind == LASPJ_KIND_ORSET && etf_value_direct(ctx, n, E)) {
                 // few long answers: written from the cells (no value bits in between), a
                 // decoded operand's cells cleared behind the reads
@@ -801,7 +933,13 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         }
         case Op::READ: {
             // the variable's value as its term_to_binary image (#dv.value read back)
-            laspj_batch vb = view(ctx, c.kind, 1, E, c.vars[0]->cells);
+            laspj_batch vb = view(ctx, c.kind, 1, E, c.vars[0]->cells, TW);
+            if (wide) {
+                if (int s = wide_size_enqueue(ctx, K.wd, vb.dev, 1, -1, dooff, ctx->flag)) return s;
+                if (int s = wide_write_enqueue(ctx, K.wd, vb.dev, 1, -1, 1, dooff, dopay, ocap))
+                    return s;
+                break;
+            }
             const unsigned long long* chunks = nullptr;
             if (int s = etf_size_enqueue(ctx, &vb, K.etf, c.kind, -1, dooff, ctx->flag, &chunks))
                 return s;
@@ -818,15 +956,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         case Op::INFLATION:
             S->clean_words = 0;
             // is_inflation / is_strict_inflation (lasp_lattice.erl:137-161, 212-253)
-            LJ_HIP(ctx, orset ? launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, rout + o_res)
+            LJ_HIP(ctx, wide ? launch_wide_inflation(ctx, &lhs, &rhs, c.strict != 0, rout + o_res)
+                        : orset ? launch_orset_inflation(ctx, &lhs, &rhs, c.strict != 0, rout + o_res)
                               : launch_gset_inflation(ctx, &lhs, &rhs, c.strict != 0, rout + o_res));
             break;
         case Op::THRESHOLD: {
             // threshold_met(Type, Value, Threshold) (lasp_lattice.erl:62-75): is_(strict_)
             // inflation(Threshold, Value) with Value the resident cells
             S->clean_words = 0;
-            laspj_batch cur = view(ctx, c.kind, 1, E, c.vars[0]->cells);
-            LJ_HIP(ctx, orset ? launch_orset_inflation(ctx, &lhs, &cur, c.strict != 0, rout + o_res)
+            laspj_batch cur = view(ctx, c.kind, 1, E, c.vars[0]->cells, TW);
+            LJ_HIP(ctx, wide ? launch_wide_inflation(ctx, &lhs, &cur, c.strict != 0, rout + o_res)
+                        : orset ? launch_orset_inflation(ctx, &lhs, &cur, c.strict != 0, rout + o_res)
                               : launch_gset_inflation(ctx, &lhs, &cur, c.strict != 0, rout + o_res));
             break;
         }
@@ -862,10 +1002,10 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         c.has_seg = false;
         if (defer && cjob.armed &&
             std::find(c.st.begin(), c.st.end(), (int32_t)LASPJ_DEC_UNKNOWN_TERM) != c.st.end()) {
+            // (the chain checks copied the failed payloads' results into the answer area;
+            // those of payloads that decoded are not read)
             c.segres.resize(8ull * plan.nseg);
-            LJ_HIP(ctx, hipMemcpyAsync(c.segres.data(), cjob.res, kSegResBytes * plan.nseg,
-                                       hipMemcpyDeviceToHost, ctx->stream));
-            LJ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            std::memcpy(c.segres.data(), hout + o_seg, kSegResBytes * plan.nseg);
             c.segbase = plan.segbase;
             c.segS = plan.S;
             c.has_seg = true;
@@ -996,9 +1136,20 @@ int reset_dict(laspj_ctx* ctx, NifState* S, KindState& K) {
     if (laspj_dict_create(&K.dict) != LASPJ_OK)
         return fail(ctx, LASPJ_E_NOMEM, "nif: dictionary allocation");
     K.stale = false;
+    K.wide = false;                           // (a fresh dictionary starts narrow)
+    K.tw = 1;
     ++K.epoch;
     if (had) ++S->stats[3];
     return LASPJ_OK;
+}
+
+// an operand met an element's 64 token slots all taken: the namespace goes wide (true: the
+// caller registers the operands again)
+bool widen(KindState& K, const std::vector<int32_t>& st) {
+    if (K.wide || K.kind != LASPJ_KIND_ORSET) return false;
+    for (int32_t x : st)
+        if (x == LASPJ_DEC_UNREPRESENTABLE) return go_wide(K);
+    return false;
 }
 
 // The call: device pass; operands with unknown terms registered and a second pass; every
@@ -1020,11 +1171,11 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         p->assign(c.p.begin() + p0, c.p.begin() + p1);
         l->assign(c.len.begin() + p0, c.len.begin() + p1);
     };
-    // a variable call's operands are its own (payload i belongs to variable i): one whose
-    // value needs a fresh dictionary (an element's 64 token slots used up in its namespace)
-    // would write out the namespace's other variables, so only write/4 resets; bind /
-    // threshold answer FALLBACK and the NIF runs the reference's clause over the variable's
-    // read image
+    // a variable call's operands are its own (payload i belongs to variable i): an element
+    // past its 64 token slots widens the namespace's cells (k {p, r} pairs); only image
+    // calls start a fresh dictionary for it, and only write/4 resets a dictionary grown past
+    // its bound (bind / threshold answer FALLBACK there and the NIF runs the reference's
+    // clause over the variable's read image)
     const bool may_reset = !(c.op == Op::BIND || c.op == Op::THRESHOLD);
     std::vector<uint8_t> fallback(n, 0);
     std::vector<uint8_t> registered(G, 0);
@@ -1044,6 +1195,8 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 // nothing registered yet: register this group's operands first
                 slice(p0, p1, &rp, &rl);
                 if (int s = register_payloads(ctx, S, K, rp, rl, &rst)) return s;
+                if (widen(K, rst))
+                    if (int s = register_payloads(ctx, S, K, rp, rl, &rst)) return s;
                 registered[g] = 1;
                 for (uint32_t i = p0; i < p1; ++i)
                     if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
@@ -1076,7 +1229,13 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         std::vector<uint32_t> unknown;
         for (uint32_t i = 0; i < m; ++i) {
             if (fallback[answer_of(i)]) continue;
-            if (c.st[i] == LASPJ_DEC_UNKNOWN_TERM && (!registered[group_of(i)] || partial))
+            // (an element past a narrow namespace's 64 token slots: its registration widens
+            // the namespace)
+            const KindState& Ki = *c.groups[group_of(i)].K;
+            const bool grow = c.st[i] == LASPJ_DEC_UNREPRESENTABLE &&
+                              Ki.kind == LASPJ_KIND_ORSET && !Ki.wide;
+            if ((c.st[i] == LASPJ_DEC_UNKNOWN_TERM || grow) &&
+                (!registered[group_of(i)] || partial))
                 unknown.push_back(i);
             else if (c.st[i] != LASPJ_DEC_OK)
                 fallback[answer_of(i)] = 1;
@@ -1129,7 +1288,10 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
             bool full = false;
             for (int32_t x : rst) full |= x == LASPJ_DEC_UNREPRESENTABLE;
             laspj_dict_info(K.dict, &nd, &eb, &tb);
-            if (may_reset && ((full && nd) || nd > kMaxDictElements)) {
+            // image calls own their namespace's terms for the call only: a wide one starts
+            // over narrow when it meets new terms (the narrow codec is the fast one)
+            const bool image_call = c.vars.empty();
+            if (may_reset && ((image_call && ((full && nd) || K.wide)) || nd > kMaxDictElements)) {
                 // an element's 64 token slots used up by earlier calls (or a dictionary grown
                 // past its bound): start a fresh dictionary holding this group's terms only —
                 // image calls are self-contained (images in, images out); the namespace's
@@ -1138,6 +1300,9 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 if (int s2 = reset_dict(ctx, S, K)) return s2;
                 slice(p0, p1, &rp, &rl);
                 if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
+                // (an operand of more than 64 tokens on an element even so: wide)
+                if (widen(K, rst))
+                    if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
                 for (uint32_t i = p0; i < p1; ++i)
                     if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
                 for (uint32_t i = p0; i < p1 && i < c.vars.size(); ++i) {
@@ -1145,6 +1310,10 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                     c.vars[i]->resident = true;
                 }
             } else {
+                // a variable's namespace (its replicas' cells hold its slots) goes wide
+                // rather than start over
+                if (widen(K, rst))
+                    if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
                 for (size_t k = 0; k < ri.size(); ++k)
                     if (rst[k] != LASPJ_DEC_OK) fallback[answer_of(ri[k])] = 1;
             }
@@ -1878,6 +2047,10 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
     laspj::dict_begin(K.dict);
     uint32_t mi = 0;
     for (size_t k = 0; k < ops.size(); ++k) {
+        if (k == 0) {
+            any_remove = registered = false;
+            mi = 0;
+        }
         const laspj::UpdateOp& o = ops[k];
         laspj_op& d = dops[k];
         d = laspj_op{};
@@ -1916,14 +2089,26 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
             laspj::dict_rollback(K.dict);
             return fail(ctx, LASPJ_E_NOMEM, "var_update: registration");
         }
+        if (st == LASPJ_DEC_UNREPRESENTABLE && !K.wide) {
+            // a 65th token on an element: the namespace goes wide and the call's
+            // registrations start over
+            laspj::dict_rollback(K.dict);
+            if (laspj::go_wide(K)) {
+                laspj::dict_begin(K.dict);
+                k = (size_t)-1;
+                continue;
+            }
+            return fallback();
+        }
         if (st != LASPJ_DEC_OK) {
-            // a 65th token on an element, an `==`-equal term under another image: the
-            // reference's clause on the NIF side
+            // an `==`-equal term under another image, a token image a wide namespace cannot
+            // hold: the reference's clause on the NIF side
             laspj::dict_rollback(K.dict);
             return fallback();
         }
         d.element = e;
         d.slot = (uint8_t)t;
+        d.pad = (uint8_t)(t >> 8);
     }
     laspj::dict_begin(K.dict);                    // (the journal kept nothing)
     registered |= laspj::dict_elements(K.dict) != nd0;
@@ -1942,7 +2127,8 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
     int32_t* dstat = nullptr;
     {
         laspj::Guard g(ctx);
-        if (int s = laspj::fit_var(ctx, var, K.E)) return s;
+        const uint32_t tw = laspj::ktw(K);
+        if (int s = laspj::fit_var(ctx, var, K.E, tw)) return s;
         laspj::UpdArgs args;
         std::memset(&args, 0, sizeof(args));
         const laspj_op* dev_ops = nullptr;
@@ -1966,10 +2152,10 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
         if (!dev_ops) std::memcpy(args.op, dops.data(), 16ull * nops);
         if (all_add && dev_ops) {
             hipLaunchKernelGGL(laspj::k_var_adds, dim3((nops + 255) / 256), dim3(256), 0,
-                               ctx->stream, var->cells, var->kind, dev_ops, nops);
+                               ctx->stream, var->cells, var->kind, tw, dev_ops, nops);
         } else {
             hipLaunchKernelGGL(laspj::k_var_update, dim3(1), dim3(64), 0, ctx->stream, var->cells,
-                               var->kind, args, dev_ops, nops, any_remove ? dstat : nullptr);
+                               var->kind, tw, args, dev_ops, nops, any_remove ? dstat : nullptr);
         }
         LJ_LAUNCHED(ctx);
         std::vector<int32_t> st;

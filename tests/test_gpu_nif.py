@@ -95,7 +95,8 @@ def _pid_like_payload(tok: bytes) -> bytes:
 
 def fallback_cases(seed=2):
     """Operands the columnar path does not take: verdict FALLBACK (the NIF runs the
-    reference's Erlang clause, which answers or crashes as the reference does)."""
+    reference's Erlang clause, which answers or crashes as the reference does) — after
+    the answers of a wide element (65 tokens), so the wide decoder meets them too."""
     rng = random.Random(seed)
     t = _tokens(rng, 70)
     good = [(1, [(t[0], False)]), (2, [(t[1], True)])]
@@ -103,7 +104,8 @@ def fallback_cases(seed=2):
         "keys descend": [(2, [(t[0], False)]), (1, [(t[1], False)])],
         "key twice": [(1, [(t[0], False)]), (1, [(t[1], False)])],
         "tokens descend": [(1, sorted([(t[2], False), (t[3], False)], reverse=True))],
-        "65 tokens": [(1, [(x, False) for x in sorted(t[:65])])],
+        "65 tokens of two lengths": [(1, sorted([(x, False) for x in t[:64]] +
+                                                [(t[65] + b"x", False)], key=_key))],
         "no tokens": [(1, [])],
         "not a list": (1, 2),
         "flag not a boolean": [(1, [(t[4], Atom("maybe"))])],
@@ -119,6 +121,18 @@ def fallback_cases(seed=2):
     p = _pid_like_payload(t[6])
     out.append((MERGE, FALLBACK, 0, _tb(good), p, b""))
     out.append((VALUE, FALLBACK, 0, p, b"", b""))
+    # an element of 65 tokens (the reference mints one per add and never collects them,
+    # lasp_orset.erl:222-241): the namespace goes wide (k {p, r} pairs per cell) and
+    # answers; the operands after it still fall back as above
+    wide = [(1, [(x, k % 3 == 0) for k, x in enumerate(sorted(t[:65]))])]
+    out.insert(0, (MERGE, OK, 0, _tb(good), _tb(wide), _tb(oorset.merge(good, wide))))
+    out.insert(1, (MERGE, OK, 0, _tb(wide), _tb(good), _tb(oorset.merge(wide, good))))
+    out.insert(2, (VALUE, OK, 0, _tb(wide), b"", _tb(oorset.value(wide))))
+    out.insert(3, (EQUAL, OK, 0, _tb(wide), _tb(good), b""))
+    out.insert(4, (INFL, OK, int(olat.is_inflation("lasp_orset", good, wide)), _tb(good),
+                   _tb(wide), b""))
+    out.insert(5, (SINFL, OK, int(olat.is_strict_inflation("lasp_orset", wide, wide)),
+                   _tb(wide), _tb(wide), b""))
     return out
 
 

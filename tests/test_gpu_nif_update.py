@@ -150,8 +150,9 @@ def test_var_update_preconditions_void_the_call():
 def test_var_update_gset_and_fallbacks():
     """G-Set add / add_all (ordsets:add_element / union with from_list) against the oracle;
     ops no clause takes (an unknown atom, a G-Set remove, a non-list add_all, an improper
-    list), a term `==` to a held one under another image (1.0 after 1) and an element's
-    65th token answer FALLBACK and leave the value as it was."""
+    list), a term `==` to a held one under another image (1.0 after 1), and — once an
+    element's 65th token has made the namespace wide — a token image of another length
+    answer FALLBACK and leave the value as it was."""
     ctx = _ctx()
     try:
         rng = random.Random(5)
@@ -181,12 +182,14 @@ def test_var_update_gset_and_fallbacks():
                     _tb((A("remove"), 1.0))):
             assert v.update(img)[0] == FALLBACK, img
             assert v.read() == (OK, state)
-        # 63 more tokens on element 1 fit; the 65th answers FALLBACK
-        for k in range(63):
+        # 63 more tokens on element 1 fit; the 65th widens the namespace and fits too
+        for k in range(64):
             assert v.update(_tb((A("add"), 1)))[:2] == (OK, UPD_OK), k
-        assert v.update(_tb((A("add"), 1)))[0] == FALLBACK
         verd, img = v.read()
-        assert verd == OK and len(oetf.binary_to_term(img)[0][1]) == 64
+        assert verd == OK and len(oetf.binary_to_term(img)[0][1]) == 65
+        # a wide namespace's tokens are of one image length
+        assert v.update(_tb((A("add_by_token"), b"t" * 21, 1)))[0] == FALLBACK
+        assert v.read() == (OK, img)
     finally:
         ctx.close()
 
@@ -392,5 +395,73 @@ def test_bind_many_fresh_namespaces():
                 assert got[t] == (OK, want), (rnd, t)
                 cur[t] = oorset.merge(cur[t], vals[t])
                 assert vs[t].read() == (OK, _tb(cur[t])), (rnd, t)
+    finally:
+        ctx.close()
+
+
+def test_wide_namespace_element_past_64_tokens():
+    """The reference mints a token per add and never collects them (lasp_orset.erl:222-241,
+    261-262): an element past 64 tokens widens its namespace's cells to k {p, r} pairs
+    (token slot t in pair t / 64) instead of handing the variable back to Erlang.  Three
+    replicas add element 1 200 times between them, bind each other's states, remove it,
+    and answer value/1, threshold and read as the oracle does; write/4 and bind_many of wide
+    images, and image calls whose operands carry 100 tokens on an element, agree too."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(41)
+        a = ctx.var("orset")
+        reps = [a, a.replica(), a.replica()]
+        cur = [[] for _ in reps]
+        for k in range(240):
+            r = k % 3
+            op = (A("add"), 1) if k % 6 else (A("add"), rng.randrange(8))
+            verd, res, _e, minted = reps[r].update(_tb(op))
+            assert (verd, res) == (OK, UPD_OK), k
+            cur[r] = _oracle_update(oorset, op, cur[r], minted)[1]
+            if k % 40 == 39:
+                assert reps[r].read() == (OK, _tb(cur[r])), k
+        assert ctx.nif_stats()["fallbacks"] == 0
+        imgs = [v.read()[1] for v in reps]
+        assert imgs == [_tb(c) for c in cur]
+        orig = list(cur)
+        for r, v in enumerate(reps):
+            for q in range(3):
+                if q != r:
+                    assert v.bind(imgs[q]) == (OK, 0 if exact_eq(cur[r], orig[q]) else 1)
+                    cur[r] = oorset.merge(cur[r], orig[q])
+        assert all(v.read() == (OK, _tb(c)) for v, c in zip(reps, cur))
+        ones = [ts for e, ts in cur[0] if e == 1][0]
+        assert len(ones) > 150
+        th = orig[1]
+        assert reps[0].threshold(_tb(th)) == (OK, olat.threshold_met("lasp_orset", cur[0], th))
+        assert reps[0].value() == (OK, _tb(oorset.value(cur[0])))
+        assert reps[2].update(_tb((A("remove"), 1)))[:2] == (OK, UPD_OK)
+        cur[2] = _oracle_update(oorset, (A("remove"), 1), cur[2], [])[1]
+        assert reps[2].read() == (OK, _tb(cur[2]))
+        assert reps[2].value() == (OK, _tb(oorset.value(cur[2])))
+        assert reps[0].bind(_tb(cur[2])) == (OK, 1)
+        cur[0] = oorset.merge(cur[0], cur[2])
+        assert reps[0].read() == (OK, _tb(cur[0]))
+        # write/4 of a wide image into a fresh variable, bind_many beside a narrow one
+        w = ctx.var("orset")
+        assert w.write(_tb(cur[1])) == OK and w.resident
+        n = ctx.var("orset")
+        small = [(3, [(b"\x05" * 20, False)])]
+        got = ctx.var_bind_many([(w, _tb(cur[0])), (n, _tb(small))])
+        assert got == [(OK, 0 if exact_eq(cur[1], oorset.merge(cur[1], cur[0])) else 1), (OK, 1)]
+        assert w.read() == (OK, _tb(oorset.merge(cur[1], cur[0])))
+        assert n.read() == (OK, _tb(small))
+        # image calls: operands of 100 tokens on an element, then narrow ones again
+        toks = sorted(bytes(rng.getrandbits(8) for _ in range(20)) for _ in range(200))
+        x = [(1, [(t, i % 4 == 0) for i, t in enumerate(toks[:100])]), (2, [(toks[150], False)])]
+        y = [(1, [(t, i % 5 == 0) for i, t in enumerate(toks[50:150])])]
+        assert ctx.nif_merge(_tb(x), _tb(y)) == (OK, _tb(oorset.merge(x, y)))
+        assert ctx.nif_merge(_tb(y), _tb(x)) == (OK, _tb(oorset.merge(y, x)))
+        assert ctx.nif_value(_tb(x)) == (OK, _tb(oorset.value(x)))
+        assert ctx.nif_equal(_tb(x), _tb(x)) == (OK, True)
+        assert ctx.nif_inflation(_tb(y), _tb(oorset.merge(x, y))) == (OK, True)
+        z = [(1, [(toks[199], False)]), (4, [(toks[198], True)])]
+        assert ctx.nif_merge(_tb(z), _tb(small)) == (OK, _tb(oorset.merge(z, small)))
+        assert ctx.nif_stats()["fallbacks"] == 0
     finally:
         ctx.close()
