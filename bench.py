@@ -523,9 +523,10 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
         vupdate(img)
     out["us_update_nif_remove"] = (time.perf_counter() - t0) * 1e6 / 50
     # the bind that meets a freshly minted token: a replica in the variable's namespace
-    # (laspj_var_create_replica) binds the updated state — the token is known, one device
-    # pass; a variable of its own namespace (another node's replica) binds it — a token its
-    # dictionary has not seen: registration and a second pass
+    # (laspj_var_create_replica) binds the updated state — the token is known; a variable of
+    # its own namespace (another node's replica) binds it — a token its dictionary has not
+    # seen, taken by the decoder in the same pass (registered after it, the device images
+    # patched on the next call)
     rep = uv.replica()
     far = ctx.var("orset")
     _, img0 = uv.read()

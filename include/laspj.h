@@ -1065,8 +1065,10 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
  * merge passes run again because a segment chain checked beside the join broke before
  * any failing segment (a false element-header match: only a serial decode can judge);
  * [16] resident variables written out to their images by a dictionary reset; [17]
- * variables decoded back onto the device after one */
-#define LASPJ_NIF_STATS 18
+ * variables decoded back onto the device after one; [18] tokens a single bind's decoder
+ * took that its namespace had not seen (registered after the pass: no second pass); [19]
+ * namespaces widened (an element past 64 tokens: cells of k {p, r} pairs) */
+#define LASPJ_NIF_STATS 20
 int laspj_nif_stats(laspj_ctx* ctx, uint64_t* out, uint32_t n);
 /* drop the context's dictionaries (their memory; the next call registers afresh;
  * resident variables are written out to their images and decoded again when used) */

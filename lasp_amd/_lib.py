@@ -43,7 +43,7 @@ TUNE_LIST_WALK = 10
 TUNE_NIF_PASSES = 14
 TUNE_LIST_CHUNK = 15
 NIF_OK, NIF_FALLBACK = 0, 1           # verdicts of the NIF-level entry points
-NIF_STATS = 18
+NIF_STATS = 20
 
 
 class LaspjUnavailable(RuntimeError):

@@ -32,6 +32,12 @@
 
 #include "laspj_internal.h"
 
+// a token image that is BINARY_EXT of exactly the rest of its bytes
+static inline bool tok_is_binary(const uint8_t* p, uint32_t len) {
+    return len >= 5u && p[0] == 109 &&
+           (((uint32_t)p[1] << 24) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 8) | p[4]) == len - 5u;
+}
+
 struct laspj_etf_dict {
     laspj_ctx* ctx = nullptr;
     uint32_t elements = 0;
@@ -61,6 +67,7 @@ struct laspj_etf_dict {
     // 104 2 <token image>;  element e's header prefix 104 2 <elem image> 108 at
     // ehdr_pad + ehdr_poff[e]
     uint32_t rec_len = 0, rec_stride = 0;  // rec_len 0: no templates (mixed token lengths)
+    bool bin_tokens = false;               // every token a BINARY_EXT of rec_len - 7 bytes
     const uint8_t* rec_pad = nullptr;
     const uint8_t* ehdr_pad = nullptr;
     const uint32_t* ehdr_poff = nullptr;   // E
@@ -1904,6 +1911,7 @@ struct ReadTabs {
     const uint8_t* hdr;     // by rank: 64 bytes of 104 2 <elem image> 108, zero padded
     const uint16_t* tb;     // by rank r, token rank k: bucket at r * tok_max + k
     const uint8_t* ros;     // by rank r, token slot s: its token rank at 64 r + s (0xFF: none)
+    NewTokArgs nt;          // (out null: unseen tokens answer UNKNOWN_TERM)
 };
 
 // bytes of the ReadTabs tables: desc, hdr, tb, ros
@@ -1970,6 +1978,49 @@ __device__ __forceinline__ bool rec_match(const uint8_t* buf, uint32_t o, uint32
 #pragma unroll
     for (int i = 0; i < 12; ++i) eq &= tw[i] == rw[i];
     return eq;
+}
+
+// New tokens (NewTokArgs): the record at o is 104 2 <BINARY_EXT of RL - 7 bytes>, the form
+// of the dictionary's own token records (etf_dict_bin_tokens), so records compare bytewise
+// in term order
+__device__ __forceinline__ bool new_tok_image(const uint8_t* buf, uint32_t o, uint32_t RL) {
+    if (RL < 8u || buf[o] != 104 || buf[o + 1] != 2 || buf[o + 2] != 109) return false;
+    const uint32_t n = ((uint32_t)buf[o + 3] << 24) | ((uint32_t)buf[o + 4] << 16) |
+                       ((uint32_t)buf[o + 5] << 8) | buf[o + 6];
+    return n == RL - 7u;
+}
+
+// staged record at o against template t (global), bytewise: <0, 0, >0
+__device__ __forceinline__ int rec_cmp(const uint8_t* buf, uint32_t o, uint32_t RL,
+                                       const uint8_t* t) {
+    for (uint32_t i = 0; i < RL; ++i) {
+        const int a = buf[o + i], b = t[i];
+        if (a != b) return a - b;
+    }
+    return 0;
+}
+
+// how many of an element's cnt token templates (by rank, stride RS) sort below the record
+// at o; -1 when one equals it
+__device__ __forceinline__ int32_t new_tok_rank(const uint8_t* buf, uint32_t o, uint32_t RL,
+                                                const uint8_t* tpl, uint32_t RS, uint32_t cnt) {
+    uint32_t lo = 0, hi = cnt;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const int c = rec_cmp(buf, o, RL, tpl + (u64)mid * RS);
+        if (c == 0) return -1;
+        if (c > 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return (int32_t)lo;
+}
+
+// the staged record at a sorts after the one at b
+__device__ __forceinline__ bool img_after(const uint8_t* buf, uint32_t a, uint32_t b,
+                                          uint32_t RL) {
+    for (uint32_t i = 0; i < RL; ++i)
+        if (buf[a + i] != buf[b + i]) return buf[a + i] > buf[b + i];
+    return false;
 }
 
 // The flag atom whose first 8 bytes are v0, v1 (little-endian): 1 = true, 2 = false,
@@ -2991,8 +3042,9 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
         if (lane < cur.cnt) L.tab[cur.tb] = (uint8_t)lane;
         L.pres[lane] = 0;
         wave_sync();
-        int32_t tprev = -1;
-        uint32_t done = 0;
+        int32_t tprev = -1;             // the last record's order key (2 rank + 1; new: 2 below)
+        uint32_t done = 0, nnew = 0;    // new tokens of the element so far
+        u64 np = 0, nr = 0;             // their slot bits (present, removed)
         if (d.tok_max > 8) {
             // many records per element: locate them byte-parallel (the chain below only
             // when that does not validate)
@@ -3064,11 +3116,24 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
             const bool mine = lane < nb;
             int32_t lst = LASPJ_DEC_OK;
             uint32_t rank = 0xFFu, fl = 0;
+            bool unk = false, fok = false;
+            int32_t key = -1;
             if (mine) {
                 rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
                 bool eq = rank < cur.cnt;
                 if (eq) {                           // exact compare
                     eq = rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + rank) * RS);
+                }
+                if (eq) {
+                    key = 2 * (int32_t)rank + 1;
+                } else if (tabs.nt.out && new_tok_image(w.buf, myx, RL)) {
+                    // a token the element's images lack: its place among them
+                    const int32_t ip = new_tok_rank(w.buf, myx, RL,
+                                                    d.rec_pad + (u64)e * RK * RS, RS, cur.cnt);
+                    if (ip >= 0) {
+                        unk = true;
+                        key = 2 * ip;
+                    }
                 }
                 // ATOM_EXT / ATOM_UTF8_EXT (2-byte length), SMALL_ATOM_UTF8_EXT
                 // (1-byte length), then "true" / "false"
@@ -3082,21 +3147,61 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
                 const bool tr = fk == 1u && fend <= w.end;
                 const bool fa = fk == 2u && fend <= w.end;
                 fl = tr;
-                // term order: after the previous record's rank
-                const uint32_t pr = __shfl(rank, (lane + 63u) & 63u, 64);
-                const int32_t before = lane ? (int32_t)pr : tprev;
-                lst = !eq || (int32_t)rank <= before ? LASPJ_DEC_UNKNOWN_TERM
-                      : !(tr || fa)                  ? LASPJ_DEC_MALFORMED
-                                                     : LASPJ_DEC_OK;
+                fok = tr || fa;
             }
-            const u64 bad = __ballot(lst != LASPJ_DEC_OK);
+            // term order: after the previous record (two new tokens between the same two
+            // known ones: by their images)
+            const int32_t pk = __shfl(key, (lane + 63u) & 63u, 64);
+            const uint32_t px = __shfl(myx, (lane + 63u) & 63u, 64);
+            if (mine) {
+                const int32_t before = lane ? pk : tprev;
+                const bool asc = key > before ||
+                                 (unk && key == before && lane && img_after(w.buf, myx, px, RL));
+                lst = key < 0 || !asc ? LASPJ_DEC_UNKNOWN_TERM
+                      : !fok                       ? LASPJ_DEC_MALFORMED
+                                                   : LASPJ_DEC_OK;
+            }
+            u64 bad = __ballot(lst != LASPJ_DEC_OK);
+            const u64 um = __ballot(mine && unk);
+            if (!bad && um) {
+                // new tokens: the element's next free slots, in payload order; an entry each
+                const uint32_t nu = (uint32_t)__popcll(um);
+                if (cur.cnt + nnew + nu > 64u) {
+                    bad = 1;
+                    lst = LASPJ_DEC_UNKNOWN_TERM;
+                } else {
+                    const uint32_t slot =
+                        cur.cnt + nnew + (uint32_t)__popcll(um & ((1ull << lane) - 1ull));
+                    bool over = false;
+                    if (mine && unk) {
+                        const uint32_t idx = atomicAdd(tabs.nt.cnt, 1u);
+                        over = idx >= tabs.nt.cap;
+                        if (!over)
+                            tabs.nt.out[idx] = NewTok{tabs.nt.seq, e, slot,
+                                                      (uint32_t)(w.lo + myx + 2u)};
+                    }
+                    if (__ballot(over)) {
+                        bad = 1;
+                        lst = LASPJ_DEC_UNKNOWN_TERM;
+                    } else {
+                        const u64 tm = __ballot(mine && unk && fl);
+                        u64 mm = um;
+                        for (uint32_t k = 0; mm; ++k, mm &= mm - 1ull) {
+                            const uint32_t f = (uint32_t)__ffsll((long long)mm) - 1u;
+                            np |= 1ull << (cur.cnt + nnew + k);
+                            if ((tm >> f) & 1ull) nr |= 1ull << (cur.cnt + nnew + k);
+                        }
+                        nnew += nu;
+                    }
+                }
+            }
             if (bad) {
                 st = (int32_t)rdlane((uint32_t)lst, (uint32_t)__ffsll((long long)bad) - 1u);
                 break;
             }
             if (trunc) { st = LASPJ_DEC_MALFORMED; break; }
-            if (mine) L.pres[rank] = (uint8_t)(1u | (fl << 1));
-            tprev = (int32_t)rdlane(rank, nb - 1u);
+            if (mine && !unk) L.pres[rank] = (uint8_t)(1u | (fl << 1));
+            tprev = (int32_t)rdlane((uint32_t)key, nb - 1u);
             done += nb;
             pc = x;
         }
@@ -3109,7 +3214,7 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
         wave_sync();
         const uint32_t v = cur.ros < 64u ? L.pres[cur.ros] : 0u;
         const u64 pb = __ballot(v & 1u), rb = __ballot(v & 2u);
-        if (lane == 0) c[e] = u64x2{pb, rb};
+        if (lane == 0) c[e] = u64x2{pb | np, rb | nr};
         ++k;
     }
     return k;
@@ -4773,6 +4878,8 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
 namespace laspj {
 
 bool etf_dict_decodable(const laspj_etf_dict* d) { return d && d->rec_len != 0; }
+bool etf_dict_bin_tokens(const laspj_etf_dict* d) { return d && d->bin_tokens; }
+uint32_t etf_dict_tok_len(const laspj_etf_dict* d) { return d ? d->tok_uniform : 0; }
 uint32_t etf_dict_elements(const laspj_etf_dict* d) { return d ? d->elements : 0; }
 
 void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, const u64* off,
@@ -4814,7 +4921,8 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, co
 int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int tag, int vers,
                      const uint8_t* payload, uint64_t payload_bytes, const u64* offs,
                      const EtfReadPlan& plan, const uint32_t* segbase, int32_t* status,
-                     bool clear, uint32_t* redo_zeroed, ChainJob* defer, const SegList* only) {
+                     bool clear, uint32_t* redo_zeroed, ChainJob* defer, const SegList* only,
+                     const NewTokArgs* nt) {
     const uint64_t R = b->replicas;
     if (clear)
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
@@ -4823,7 +4931,8 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
     auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
                                               ctx->tune_etf_read >= 8)
                      ? k_orset_etf_read<true> : k_orset_etf_read<false>;
-    const ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+    ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
+    if (nt && nt->out && d->bin_tokens && b->replicas == 1) tabs.nt = *nt;
     // the header hash (segment search; element batches without the scalar walk — knob 6
     // keeps the walking element batches)
     const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
@@ -5377,6 +5486,11 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
                             "etf_dict_create: token order of element %u misses a slot", e);
         }
     }
+    bool bin = toks && !mixed && uniform >= 5u;
+    for (uint64_t t = 0; bin && t < 64ull * E; ++t) {
+        const uint32_t len = tok_off[t + 1] - tok_off[t];
+        if (len) bin = tok_is_binary(tok_blob + tok_off[t], len);
+    }
     const uint64_t eblob = elem_off[E];
     // 16-byte-aligned copies of every image (the write kernels load them 16 B at a time)
     auto pad16 = [](uint64_t x) { return (x + 15ull) & ~15ull; };
@@ -5698,6 +5812,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     d->tok_uniform = mixed ? 0u : uniform;
     d->tok_max = tok_max;
     d->rec_len = rec_len;
+    d->bin_tokens = bin && rec_len != 0;
     d->ehdr_max = (uint32_t)std::min<uint64_t>(ehdr_max, 0xFFFFFFFFull);
     d->rec_stride = (uint32_t)rec_stride;
     d->rec_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_rpad) : nullptr;
@@ -5876,6 +5991,8 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
         if (cnt > RK || cnt > 64 || cnt == 0) return LASPJ_E_UNSUPPORTED;
         for (const auto& im : imgs)
             if (im.size() != TL || TL + 2u != RL) return LASPJ_E_UNSUPPORTED;
+        for (const auto& im : imgs)
+            if (!tok_is_binary(reinterpret_cast<const uint8_t*>(im.data()), TL)) d->bin_tokens = false;
         // token mask and term order
         const u64 mask = cnt == 64 ? ~0ull : (1ull << cnt) - 1ull;
         put(d->o_mask + 8ull * e, &mask, 8);

@@ -304,6 +304,23 @@ void etf_read_plan(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R,
 constexpr uint64_t kSegResBytes = 32;
 // a redo pass's segments (global segment numbers; n = 0: every segment): the segments of a
 // deferred pass that met terms since registered, decoded again over the cells they left
+// A single payload's tokens its namespace has not seen, taken by the decoder on the spot
+// (binary tokens of the dictionary's token length on known elements): each gets the next
+// free slot of its element (the element's token count, then one up per new token in
+// payload order — one wave decodes an element, so no two waves hand out its slots) and
+// an entry {seq, element slot, token slot, image offset} in `out`, numbered by the device
+// counter `cnt`; the host registers them in slot order after the call (the dictionary's
+// own numbering: count, count + 1, ...).  An entry past `cap`, a slot past 63, or two new
+// tokens whose order the decoder cannot tell answer UNKNOWN_TERM as before.
+struct NewTok {
+    uint32_t seq, e, slot, off;
+};
+struct NewTokArgs {
+    uint32_t* cnt = nullptr;
+    NewTok* out = nullptr;
+    uint32_t cap = 0, seq = 0;
+};
+
 struct SegList {
     uint32_t n = 0;
     uint32_t g[31] = {};
@@ -327,7 +344,11 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                      const unsigned long long* offsets, const EtfReadPlan& plan,
                      const uint32_t* segbase, int32_t* status, bool clear,
                      uint32_t* redo_zeroed, ChainJob* defer = nullptr,
-                     const SegList* only = nullptr);
+                     const SegList* only = nullptr, const NewTokArgs* nt = nullptr);
+// every token template of the dictionary a BINARY_EXT of the record's length (the new-token
+// decode compares such images bytewise, which is their term order)
+bool etf_dict_bin_tokens(const laspj_etf_dict* d);
+uint32_t etf_dict_tok_len(const laspj_etf_dict* d);      // the uniform token image length
 // OR-Set payloads over several dictionaries decoded in one launch (the NIF's binds of many
 // variables, one token namespace each): group k's payloads [p0, p1) against dictionary d
 // into cells (its first payload's; E slots per replica, consecutive).  The caller stages

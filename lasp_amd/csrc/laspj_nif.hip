@@ -138,6 +138,7 @@ struct NifState {
     // them behind them), so the next call's decoders need no memset
     uint64_t clean_words = 0;
     uint64_t stats[LASPJ_NIF_STATS] = {};
+    uint32_t nt_seq = 0;            // device passes that took new tokens (their entries' tag)
     std::unordered_set<laspj_var*> vars;
     // laspj_var_etf_update's answers (valid until the context's next call): the tokens it
     // minted, the image of the element a failed precondition names
@@ -264,6 +265,8 @@ constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is rese
 // a wide namespace (an element past 64 tokens): token slots per element, and the token
 // image length its fixed-width templates hold
 constexpr uint32_t kWideTokens = 1024, kWideTokenLen = 46;
+// new tokens a single bind's decoder may take (NewTok entries; more: the two-pass path)
+constexpr uint32_t kNewTokCap = 512;
 // device passes per call: registration, a grown answer area and a serial re-decode each
 // take one; a call still unresolved after this many answers FALLBACK (run's post-condition)
 constexpr int kMaxPasses = 6;
@@ -313,6 +316,11 @@ struct Call {
     std::vector<uint32_t> segres;   // 8 words per segment
     std::vector<uint32_t> segbase;
     uint64_t segS = 0;
+    // a single bind / write whose decoder took tokens its namespace had not seen (NewTok):
+    // the entries of a pass that decoded, registered by run(); `nt_met`: the pass met some
+    // (its cells then hold slots nobody registered unless it decoded)
+    std::vector<NewTok> newtoks;
+    bool nt_met = false;
 };
 
 KindState& kstate(NifState* S, int32_t kind) {
@@ -426,12 +434,13 @@ int rebuild_wide(laspj_ctx* ctx, NifState* S, KindState& K) {
 // their next use; slots are unchanged, so nothing is written out)
 // (false: the namespace stays narrow — its token images are not of one length, which the
 // wide templates need)
-bool go_wide(KindState& K) {
+bool go_wide(NifState* S, KindState& K) {
     if (K.wide) return true;
     if (K.kind != LASPJ_KIND_ORSET || !K.dict) return false;
     if (!dict_set_tok_cap(K.dict, kWideTokens, kWideTokenLen)) return false;
     K.wide = true;
     K.stale = true;
+    ++S->stats[19];
     return true;
 }
 
@@ -606,7 +615,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const uint64_t i_offs = 0, i_seg = al(8ull * (m + 1), 256),
                    i_zero = i_seg + al(seg_area, 256),
                    z_lb = al(4ull * (m + G + 2), 16), z_var = z_lb + 8ull * ((E + 255) / 256),
-                   z_bytes = z_var + 4ull * (n + 1),
+                   z_nt = z_var + 4ull * (n + 1), z_bytes = z_nt + 4,
                    i_vptr = i_zero + al(z_bytes, 256),
                    i_mtab = i_vptr + (var_op ? al(24ull * n, 256) : 0),
                    i_pay = i_mtab + mtab_bytes;
@@ -632,6 +641,14 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                         (c.op == Op::VALUE && etf_value_direct(ctx, n, E)));
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
     o_pay += seg_bytes;              // (a failed payload's results, written by its chain check)
+    // one operand over binary tokens (a bind, write/4, a threshold, value/1 — no answer
+    // carries token images): tokens the namespace has not seen are taken by the decoder
+    // (NewTok entries into the answer area, registered by run())
+    const bool nt_on = (var_op || c.op == Op::THRESHOLD || c.op == Op::VALUE) && m == 1 &&
+                       G == 1 && orset && !K.wide && dec && !c.redo.n &&
+                       etf_dict_bin_tokens(K.etf);
+    const uint64_t o_nt = o_pay, nt_bytes = nt_on ? al(sizeof(NewTok) * kNewTokCap, 256) : 0;
+    o_pay += nt_bytes;
     const uint64_t out_bytes = o_pay + ocap;
     // device statuses of the variable calls (their kernel reads them)
     const uint64_t vst_bytes = var_op ? al(4ull * m, 256) : 0;
@@ -814,6 +831,13 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                 if (!R) continue;
                 laspj_batch gb = view(ctx, c.kind, R, gr.K->E, cin + gcell[g]);
                 const auto* doffs = reinterpret_cast<const unsigned long long*>(din + i_offs) + gr.p0;
+                NewTokArgs nta;
+                if (nt_on) {
+                    if (!++S->nt_seq) ++S->nt_seq;           // (0 never tags an entry)
+                    nta = NewTokArgs{reinterpret_cast<uint32_t*>(din + i_zero + z_nt),
+                                     reinterpret_cast<NewTok*>(rout + o_nt), kNewTokCap,
+                                     S->nt_seq};
+                }
                 if (orset && gr.K->wide) {
                     if (int s = wide_read_enqueue(ctx, gr.K->wd, din + i_pay, pay, doffs, R,
                                                   cin + gcell[g], dst + gr.p0, !clean && !c.redo.n))
@@ -824,7 +848,8 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                             plans[g].nseg ? reinterpret_cast<const uint32_t*>(din + i_seg + gseg[g])
                                           : nullptr,
                             dst + gr.p0, !clean && !c.redo.n, dticket + 1 + gr.p0 + g,
-                            defer ? &cjob : nullptr, c.redo.n ? &c.redo : nullptr))
+                            defer ? &cjob : nullptr, c.redo.n ? &c.redo : nullptr,
+                            nt_on ? &nta : nullptr))
                         return s;
                 } else if (int s = gset_read_enqueue(ctx, &gb, gr.K->etf, -1, 1, din + i_pay, doffs,
                                                      dst + gr.p0, !clean, hoffs.data() + gr.p0)) {
@@ -996,6 +1021,17 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         c.st.assign(m, 0);
         if (dec || var_op) std::memcpy(c.st.data(), hout + o_st, 4ull * m);
         else c.st = hst;
+        c.newtoks.clear();
+        c.nt_met = false;
+        if (nt_on) {
+            // the decoder's new tokens: the entries tagged with this pass, in the order the
+            // device numbered them
+            const NewTok* ents = reinterpret_cast<const NewTok*>(hout + o_nt);
+            uint32_t k = 0;
+            while (k < kNewTokCap && ents[k].seq == S->nt_seq) ++k;
+            c.nt_met = k != 0;
+            if (k && c.st[0] == LASPJ_DEC_OK) c.newtoks.assign(ents, ents + k);
+        }
         if (var_op)
             for (int32_t x : c.st)
                 if (x != LASPJ_DEC_OK) S->clean_words = 0;   // (its cells were kept)
@@ -1086,6 +1122,39 @@ bool register_segments(NifState* S, const Call& c, const std::vector<uint32_t>& 
 
 int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict);
 
+// The tokens a pass's decoder took (NewTok): registered in the host dictionary at the
+// slots the device gave them — each element's next free slots in payload order, which is
+// the order the dictionary numbers them in; the device images learn them on the next call
+// (patch_etf).  A slot the dictionary would number otherwise cannot happen by
+// construction; it fails the call loudly (the cells already hold the device's slots).
+int register_new_tokens(laspj_ctx* ctx, NifState* S, KindState& K, const Call& c) {
+    const uint64_t t0 = now_ns();
+    std::vector<NewTok> ts = c.newtoks;
+    std::sort(ts.begin(), ts.end(), [](const NewTok& a, const NewTok& b) {
+        return a.e != b.e ? a.e < b.e : a.slot < b.slot;
+    });
+    const uint32_t TL = etf_dict_tok_len(K.etf);
+    dict_begin(K.dict);
+    for (const NewTok& t : ts) {
+        uint32_t slot = 0;
+        const int st = (uint64_t)t.off + TL <= c.len[0]
+                           ? dict_reg_tok(K.dict, t.e, c.p[0] + t.off, TL, &slot)
+                           : LASPJ_DEC_MALFORMED;
+        if (st != LASPJ_DEC_OK || slot != t.slot) {
+            dict_rollback(K.dict);
+            return fail(ctx, LASPJ_E_DEVICE,
+                        "nif: new token of element %u at slot %u registered as %u (%d)", t.e,
+                        t.slot, slot, st);
+        }
+    }
+    dict_begin(K.dict);                           // (the journal kept nothing)
+    K.stale = true;                               // (patched on the next call)
+    ++S->stats[2];
+    S->stats[18] += ts.size();
+    S->stats[12] += now_ns() - t0;
+    return LASPJ_OK;
+}
+
 // the call's payloads decoded against one dictionary
 void one_group(Call& c, KindState* K) { c.groups.assign(1, Group{K, 0, c.m}); }
 
@@ -1145,10 +1214,10 @@ int reset_dict(laspj_ctx* ctx, NifState* S, KindState& K) {
 
 // an operand met an element's 64 token slots all taken: the namespace goes wide (true: the
 // caller registers the operands again)
-bool widen(KindState& K, const std::vector<int32_t>& st) {
+bool widen(NifState* S, KindState& K, const std::vector<int32_t>& st) {
     if (K.wide || K.kind != LASPJ_KIND_ORSET) return false;
     for (int32_t x : st)
-        if (x == LASPJ_DEC_UNREPRESENTABLE) return go_wide(K);
+        if (x == LASPJ_DEC_UNREPRESENTABLE) return go_wide(S, K);
     return false;
 }
 
@@ -1195,7 +1264,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 // nothing registered yet: register this group's operands first
                 slice(p0, p1, &rp, &rl);
                 if (int s = register_payloads(ctx, S, K, rp, rl, &rst)) return s;
-                if (widen(K, rst))
+                if (widen(S, K, rst))
                     if (int s = register_payloads(ctx, S, K, rp, rl, &rst)) return s;
                 registered[g] = 1;
                 for (uint32_t i = p0; i < p1; ++i)
@@ -1210,6 +1279,8 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         c.redo.n = 0;                 // (a redo pass is taken once)
         if (s == -1000) continue;                // answer area grown: once more
         if (s) return s;
+        if (!c.newtoks.empty())
+            if (int s2 = register_new_tokens(ctx, S, *c.groups[0].K, c)) return s2;
         // a bind that decoded in this pass was merged in it: WRITTEN if this pass (or an
         // earlier one, for an operand whose call needed another pass) changed its value
         if (c.op == Op::BIND) {
@@ -1253,7 +1324,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
             for (uint32_t i : unknown) registered[group_of(i)] = 1;
             // a single bind: the next pass decodes only those segments again, over the
             // payload and cells this pass left (when the images are patched, not rebuilt)
-            if (c.op == Op::BIND && n == 1 && !c.no_defer) {
+            if (c.op == Op::BIND && n == 1 && !c.no_defer && !c.nt_met) {
                 SegList sl;
                 for (uint32_t i : unknown)
                     for (uint32_t g = c.segbase[i]; g < c.segbase[i + 1] && sl.n <= 31; ++g)
@@ -1301,7 +1372,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 slice(p0, p1, &rp, &rl);
                 if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
                 // (an operand of more than 64 tokens on an element even so: wide)
-                if (widen(K, rst))
+                if (widen(S, K, rst))
                     if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
                 for (uint32_t i = p0; i < p1; ++i)
                     if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
@@ -1312,7 +1383,7 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
             } else {
                 // a variable's namespace (its replicas' cells hold its slots) goes wide
                 // rather than start over
-                if (widen(K, rst))
+                if (widen(S, K, rst))
                     if (int s2 = register_payloads(ctx, S, K, rp, rl, &rst)) return s2;
                 for (size_t k = 0; k < ri.size(); ++k)
                     if (rst[k] != LASPJ_DEC_OK) fallback[answer_of(ri[k])] = 1;
@@ -2093,7 +2164,7 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
             // a 65th token on an element: the namespace goes wide and the call's
             // registrations start over
             laspj::dict_rollback(K.dict);
-            if (laspj::go_wide(K)) {
+            if (laspj::go_wide(S, K)) {
                 laspj::dict_begin(K.dict);
                 k = (size_t)-1;
                 continue;

@@ -211,7 +211,8 @@ class Context:
         keys = ("calls", "device_passes", "registrations", "dict_resets", "image_rebuilds",
                 "host_encoded_passes", "fallbacks", "dict_elements", "ns_stage_enqueue",
                 "ns_device_wait", "ns_answers", "ns_stage_copy", "ns_register", "ns_rebuild",
-                "image_patches", "chain_redo_passes", "vars_spilled", "vars_hydrated")
+                "image_patches", "chain_redo_passes", "vars_spilled", "vars_hydrated",
+                "device_new_tokens", "namespaces_widened")
         return dict(zip(keys, (int(x) for x in out)))
 
     def nif_reset(self):

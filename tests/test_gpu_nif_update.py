@@ -286,18 +286,18 @@ def test_replicas_bind_each_others_updates_in_one_pass():
 
 
 def test_bind_of_unseen_tokens_redoes_only_failed_segments():
-    """A bind whose image carries tokens the variable's namespace has not seen (another
-    node's update, lasp_orset.erl:222-230) decodes, registers the failing segments' terms,
-    patches the images and decodes again only those segments over the cells the first pass
-    left: two device passes, one registration, the oracle's merge.  More failing segments
-    than a redo pass lists, or a new element (images rebuilt), take a full second pass —
-    the same answers."""
+    """A bind whose image carries tokens the variable's namespace has not seen, of a form the
+    decoder cannot take on the spot (tuple tokens here; binaries are taken in one pass, see
+    below), decodes, registers the failing segments' terms, patches the images and decodes
+    again only those segments over the cells the first pass left: two device passes, one
+    registration, the oracle's merge.  More failing segments than a redo pass lists, or a
+    new element (images rebuilt), take a full second pass — the same answers."""
     from lasp_amd import _lib
     ctx = _ctx()
     try:
         rng = random.Random(23)
         ctx.set_tuning(_lib.TUNE_ETF_SEG, 256)          # many segments per payload
-        tok = lambda c, e: bytes([c]) + e.to_bytes(4, "big") + bytes(15)   # noqa: E731
+        tok = lambda c, e: (bytes([c]) + e.to_bytes(4, "big") + bytes(15),)   # noqa: E731
         base = [(e, [(tok(1, e), e % 7 == 0)]) for e in range(3000)]
         var = ctx.var("orset")
         assert var.write(_tb(base)) == OK
@@ -305,11 +305,11 @@ def test_bind_of_unseen_tokens_redoes_only_failed_segments():
         for case, nnew, new_elem in (("few", 5, False), ("many", 120, False),
                                      ("element", 3, True)):
             picks = sorted(rng.sample(range(3000), nnew))
-            add = {e: bytes(rng.getrandbits(8) for _ in range(20)) for e in picks}
+            add = {e: (bytes(rng.getrandbits(8) for _ in range(20)),) for e in picks}
             val = [(e, sorted(ts + ([(add[e], False)] if e in add else []), key=_key))
                    for e, ts in cur]
             if new_elem:
-                val = sorted(val + [(5000, [(b"\x09" * 20, False)])], key=lambda x: _key(x[0]))
+                val = sorted(val + [(5000, [((b"\x09" * 20,), False)])], key=lambda x: _key(x[0]))
             s0 = ctx.nif_stats()
             assert var.bind(_tb(val)) == (OK, 1), case
             s1 = ctx.nif_stats()
@@ -465,3 +465,81 @@ def test_wide_namespace_element_past_64_tokens():
         assert ctx.nif_stats()["fallbacks"] == 0
     finally:
         ctx.close()
+
+
+def test_bind_takes_unseen_binary_tokens_in_one_pass():
+    """Another node's update mints a 20-byte binary token (lasp_orset.erl:222-230, 261-262):
+    a bind of its state decodes the unseen tokens of known elements on the device in one
+    pass (each gets its element's next free slot; the host dictionary registers them after
+    the call), whether they sort before, between or after the known ones, several on one
+    element, two between the same neighbours; the answers, the values read back, value/1
+    and threshold agree with the oracle, and binding the same state again is a one-pass
+    no-op.  An element pushed past 64 tokens this way takes the two-pass path and widens."""
+    from lasp_amd import _lib
+    for seg in (0, 256):
+        ctx = _ctx()
+        try:
+            rng = random.Random(29 + seg)
+            if seg:
+                ctx.set_tuning(_lib.TUNE_ETF_SEG, seg)
+            mid = lambda b: bytes([b]) + bytes(rng.getrandbits(8) for _ in range(19))  # noqa: E731
+            base = [(e, sorted([(mid(0x40 + 2 * k), k % 2 == 0) for k in range(3)], key=_key))
+                    for e in range(2000)]
+            var = ctx.var("orset")
+            assert var.write(_tb(base)) == OK
+            cur = base
+            for rnd in range(6):
+                val = []
+                picks = set(rng.sample(range(2000), 40))
+                for e, ts in cur:
+                    ts = list(ts)
+                    if e in picks:
+                        # before the first known, between two, after the last, two between
+                        # the same neighbours, several at once
+                        kind = rng.randrange(5)
+                        if kind == 0:
+                            new = [b"\x00" + bytes(rng.getrandbits(8) for _ in range(19))]
+                        elif kind == 1:
+                            new = [mid(0x41)]
+                        elif kind == 2:
+                            new = [b"\xff" + bytes(rng.getrandbits(8) for _ in range(19))]
+                        elif kind == 3:
+                            new = [mid(0x43), mid(0x43)]
+                        else:
+                            new = [mid(rng.randrange(256)) for _ in range(3)]
+                        ts += [(t, rng.random() < 0.3) for t in new]
+                    val.append((e, sorted(ts, key=_key)))
+                s0 = ctx.nif_stats()
+                assert var.bind(_tb(val)) == (OK, 1), (seg, rnd)
+                s1 = ctx.nif_stats()
+                cur = oorset.merge(cur, val)
+                assert s1["device_passes"] - s0["device_passes"] == 1, (seg, rnd)
+                assert s1["device_new_tokens"] - s0["device_new_tokens"] >= 40, (seg, rnd)
+                assert s1["fallbacks"] == s0["fallbacks"]
+                assert var.read() == (OK, _tb(cur)), (seg, rnd)
+                s2 = ctx.nif_stats()
+                assert var.bind(_tb(val)) == (OK, 0)
+                assert ctx.nif_stats()["device_passes"] - s2["device_passes"] == 1
+            assert var.value() == (OK, _tb(oorset.value(cur)))
+            assert var.threshold(_tb(base)) == (OK, olat.threshold_met("lasp_orset", cur, base))
+            # a threshold and a value/1 operand carrying unseen tokens: one pass each
+            th = oorset.merge(cur, [(3, [(b"\x01" * 20, False)]), (4, [(b"\xfe" * 20, True)])])
+            s0 = ctx.nif_stats()
+            assert var.threshold(_tb(th)) == (OK, olat.threshold_met("lasp_orset", cur, th))
+            assert var.threshold(_tb(cur)) == (OK, True)
+            vimg = oorset.merge(cur, [(5, [(b"\x02" * 20, False)]), (6, [(b"\xfd" * 20, True)])])
+            assert ctx.nif_value(_tb(vimg)) == (OK, _tb(oorset.value(vimg)))
+            s1 = ctx.nif_stats()
+            assert s1["device_passes"] - s0["device_passes"] <= 4
+            assert s1["device_new_tokens"] > s0["device_new_tokens"]
+            # element 7 past 64 tokens: two passes, the namespace widens, the oracle's answer
+            e7 = [ts for e, ts in cur if e == 7][0]
+            more = [(e, sorted(ts + ([(mid(rng.randrange(256)), False) for _ in range(70)]
+                                     if e == 7 else []), key=_key)) for e, ts in cur]
+            assert len(e7) + 70 > 64
+            assert var.bind(_tb(more)) == (OK, 1)
+            cur = oorset.merge(cur, more)
+            assert var.read() == (OK, _tb(cur))
+            assert ctx.nif_stats()["namespaces_widened"] == 1
+        finally:
+            ctx.close()

@@ -29,7 +29,7 @@ def main():
     ei, el, mi = C.c_void_p(), C.c_uint64(), C.c_void_p()
     keys = ("device_passes", "registrations", "image_rebuilds", "image_patches", "ns_register",
             "ns_rebuild", "ns_stage_enqueue", "ns_stage_copy", "ns_device_wait", "ns_answers",
-            "dict_resets", "fallbacks")
+            "dict_resets", "fallbacks", "chain_redo_passes", "device_new_tokens")
     rows = []
 
     def stats():
@@ -58,11 +58,16 @@ def main():
         check(L.laspj_var_etf_bind(far.h, img, len(img), C.byref(st), C.byref(vd)), ctx.h)
         t4 = time.perf_counter()
         s3 = stats()
+        check(L.laspj_var_etf_bind(far.h, img, len(img), C.byref(st), C.byref(vd)), ctx.h)
+        t5 = time.perf_counter()
+        s4 = stats()
         rows.append({"k": k, "us_update": (t1 - t0) * 1e6, "us_read": (t2 - t1) * 1e6,
                      "us_bind_replica": (t3 - t2) * 1e6, "us_bind_far": (t4 - t3) * 1e6,
+                     "us_bind_far_again": (t5 - t4) * 1e6,
                      "d_update": {x: s1[x] - s0[x] for x in keys},
                      "d_replica": {x: s2[x] - s1[x] for x in keys},
-                     "d_far": {x: s3[x] - s2[x] for x in keys}})
+                     "d_far": {x: s3[x] - s2[x] for x in keys},
+                     "d_far_again": {x: s4[x] - s3[x] for x in keys}})
     for r in rows:
         print(json.dumps(r))
 
