@@ -1905,6 +1905,10 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_read_serial(const uint8_t*
 
 constexpr uint32_t kBWin = 4096;         // batched decode window
 constexpr uint32_t kBuckets = 1024;      // token buckets per element
+// an element's key when no bucket window separates its tokens: the batch paths find no
+// bucket (its table entries are 0xFFFF) and leave it to decode_elems, which matches its
+// records against each template
+constexpr uint32_t kNoBuckets = 0x80000000u;
 
 struct ReadTabs {
     const uint4* desc;      // by rank: slot, header length, word | shift << 8, token ranks
@@ -2273,7 +2277,7 @@ __device__ uint32_t read_batch(PWin& w, uint32_t& pc, int64_t& prev, uint32_t le
     bool ok = false;
     if (mine) {
         const u64 r = (u64)(prev + 1) + myc;
-        const uint32_t kw = 4u * (rkey & 0xFFu), ksh = rkey >> 8;
+        const uint32_t kw = 4u * (rkey & 0xFFu), ksh = (rkey >> 8) & 31u;
         const uint32_t bk = (word_at(w.buf, ry + kw) >> ksh) & (kBuckets - 1u);
         for (uint32_t j = 0; j < rcnt && j < RK; ++j)
             if (t.tb[r * RK + j] == bk) k = j;
@@ -2644,7 +2648,7 @@ __device__ uint32_t read_batch_par(PWin& w, uint32_t& pc, int64_t& prev, uint32_
     if (ok) {
         const uint4 ds = predicted ? pds : t.desc[rk];
         e = ds.x;
-        const uint32_t cnt = ds.w, kw = 4u * (ds.z & 0xFFu), ksh = ds.z >> 8;
+        const uint32_t cnt = ds.w, kw = 4u * (ds.z & 0xFFu), ksh = (ds.z >> 8) & 31u;
         y = s + hl;
         ok = y + 4u <= lim;
         const uint32_t m = ok ? __builtin_bswap32(word_at(w.buf, y)) : 0u;
@@ -2830,7 +2834,10 @@ __device__ uint32_t read_batch_many(PWin& w, uint32_t& pc, int64_t& prev, uint32
         const uint32_t co = rdlane(cnt, o);
         uint8_t* tab = o ? X.tab[o - 1] : L.tab;
         uint8_t* pr = o ? X.pres[o - 1] : L.pres;
-        if (lane < co) tab[t.tb[(u64)r * RK + lane]] = (uint8_t)lane;
+        if (lane < co) {
+            const uint32_t b = t.tb[(u64)r * RK + lane];
+            if (b < kBuckets) tab[b] = (uint8_t)lane;
+        }
         pr[lane] = 0;
         ros[o] = t.ros[64ull * r + lane];
     }
@@ -2862,7 +2869,7 @@ __device__ uint32_t read_batch_many(PWin& w, uint32_t& pc, int64_t& prev, uint32
         if (ok) {
             const uint32_t x = q[h];
             const uint8_t* tab = src ? X.tab[src - 1u] : L.tab;
-            const uint32_t kw = 4u * (key_o & 0xFFu), ksh = key_o >> 8;
+            const uint32_t kw = 4u * (key_o & 0xFFu), ksh = (key_o >> 8) & 31u;
             rank = tab[(word_at(w.buf, x + kw) >> ksh) & (kBuckets - 1u)];
             ok = rank < cnt_o;
             if (ok) ok = rec_match(w.buf, x, RL, d.rec_pad + ((u64)e_o * RK + rank) * RS);
@@ -3037,15 +3044,16 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
             else if (cool < 16u) cool = 16;
         }
         // the element's bucket table and an empty presence table
-        const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = cur.key >> 8;
+        const uint32_t kw = 4u * (cur.key & 0xFFu), ksh = (cur.key >> 8) & 31u;
         wave_sync();
-        if (lane < cur.cnt) L.tab[cur.tb] = (uint8_t)lane;
+        const bool nobk = (cur.key & kNoBuckets) != 0;
+        if (lane < cur.cnt && !nobk) L.tab[cur.tb] = (uint8_t)lane;
         L.pres[lane] = 0;
         wave_sync();
         int32_t tprev = -1;             // the last record's order key (2 rank + 1; new: 2 below)
         uint32_t done = 0, nnew = 0;    // new tokens of the element so far
         u64 np = 0, nr = 0;             // their slot bits (present, removed)
-        if (d.tok_max > 8) {
+        if (d.tok_max > 8 && !nobk) {
             // many records per element: locate them byte-parallel (the chain below only
             // when that does not validate)
             const uint32_t want = min(m_tok * (RL + 8u) + 8u, w.end - pc);
@@ -3119,10 +3127,20 @@ __device__ __forceinline__ uint32_t decode_elems(PWin& w, uint32_t& pc, int64_t&
             bool unk = false, fok = false;
             int32_t key = -1;
             if (mine) {
-                rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
-                bool eq = rank < cur.cnt;
-                if (eq) {                           // exact compare
-                    eq = rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + rank) * RS);
+                bool eq = false;
+                if (nobk) {
+                    // template by template
+                    for (uint32_t j = 0; j < cur.cnt && !eq; ++j)
+                        if (rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + j) * RS)) {
+                            rank = j;
+                            eq = true;
+                        }
+                } else {
+                    rank = L.tab[(word_at(w.buf, myx + kw) >> ksh) & (kBuckets - 1u)];
+                    eq = rank < cur.cnt;
+                    if (eq) {                       // exact compare
+                        eq = rec_match(w.buf, myx, RL, d.rec_pad + ((u64)e * RK + rank) * RS);
+                    }
                 }
                 if (eq) {
                     key = 2 * (int32_t)rank + 1;
@@ -5607,7 +5625,13 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
                         tbk[r * tok_max + j] = (uint16_t)((keys[j] >> sh) & (laspj::kBuckets - 1u));
                 }
             }
-            hashed = placed;
+            if (!placed) {
+                // no one 10-bit window tells this element's tokens apart (tokens that agree
+                // everywhere but where others also agree): its records are matched against
+                // each of its templates instead (kNoBuckets; rare, and only this element)
+                desc[4 * r + 2] = laspj::kNoBuckets;
+                for (uint32_t j = 0; j < cnt; ++j) tbk[r * tok_max + j] = 0xFFFFu;
+            }
         }
         if (!hashed) rd.clear();
     }
@@ -6052,7 +6076,10 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
                 for (uint32_t j = 0; j < cnt; ++j) tb[j] = (uint16_t)((keys[j] >> sh) & (kBuckets - 1u));
             }
         }
-        if (!placed) return LASPJ_E_UNSUPPORTED;
+        if (!placed) {
+            key = kNoBuckets;                  // (matched template by template, see create)
+            for (uint32_t j = 0; j < cnt; ++j) tb[j] = 0xFFFFu;
+        }
         // descriptor {slot, header length, key, tokens}: the first two do not change
         const uint32_t kc[2] = {key, cnt};
         put(o_desc + 16ull * r + 8, kc, 8);

@@ -543,3 +543,44 @@ def test_bind_takes_unseen_binary_tokens_in_one_pass():
             assert ctx.nif_stats()["namespaces_widened"] == 1
         finally:
             ctx.close()
+
+
+def test_tokens_no_bucket_window_separates():
+    """Tokens of one element that no single 10-bit window of their records tells apart
+    (b"A" + x, b"B" + x, b"A" + y: the first pair differs in one byte, the last pair only
+    where the first pair agrees): that element is matched template by template while
+    every other element keeps its bucket table — the dictionary stays patchable, binds
+    decode in one pass and an update patches instead of rebuilding."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(43)
+        x, y = bytes(19), bytes([7]) * 19
+        bad = [(b"A" + x, False), (b"A" + y, True), (b"B" + x, False)]
+        base = [(e, [(bytes([0x30 + k]) + bytes(rng.getrandbits(8) for _ in range(19)),
+                      k == 1) for k in range(2)]) for e in range(3000)]
+        base[1234] = (1234, sorted(bad, key=_key))
+        var = ctx.var("orset")
+        assert var.write(_tb(base)) == OK
+        assert var.read() == (OK, _tb(base))
+        cur = base
+        s0 = ctx.nif_stats()
+        for k in range(6):
+            op = (A("add"), 1234 if k % 3 == 1 else rng.randrange(3000))
+            verd, res, _e, minted = var.update(_tb(op))
+            assert (verd, res) == (OK, UPD_OK)
+            cur = _oracle_update(oorset, op, cur, minted)[1]
+        s1 = ctx.nif_stats()
+        assert s1["image_rebuilds"] == s0["image_rebuilds"]
+        assert var.read() == (OK, _tb(cur))
+        other = [(e, sorted(ts + ([(b"Z" + bytes(rng.getrandbits(8) for _ in range(19)), False)]
+                                  if e % 30 == 4 or e == 1234 else []), key=_key))
+                 for e, ts in cur]
+        s2 = ctx.nif_stats()
+        assert var.bind(_tb(other)) == (OK, 1)
+        assert ctx.nif_stats()["device_passes"] - s2["device_passes"] == 1
+        cur = oorset.merge(cur, other)
+        assert var.read() == (OK, _tb(cur))
+        assert var.value() == (OK, _tb(oorset.value(cur)))
+        assert ctx.nif_merge(_tb(base), _tb(cur)) == (OK, _tb(oorset.merge(base, cur)))
+    finally:
+        ctx.close()
