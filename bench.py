@@ -613,12 +613,17 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
         ready.wait(timeout=120)
     except threading.BrokenBarrierError:
         pass
+    p0 = ctx.nif_stats()["device_passes"] if shared else 0
     for t in ths:
         t.join(timeout=300)
     if errs or len(spans) != nthreads:
         raise RuntimeError(f"config1: {nthreads}-context binds failed: {errs[:3]}")
     wall = max(b for _a, b in spans) - min(a for a, _b in spans)
-    return {"contexts": 1 if shared else nthreads, "threads": nthreads,
+    extra = {}
+    if shared:
+        # (binds per device pass: the group commit's batches)
+        extra["binds_per_pass"] = nthreads * per / max(1, ctx.nif_stats()["device_passes"] - p0)
+    return {**extra, "contexts": 1 if shared else nthreads, "threads": nthreads,
             "binds": nthreads * per,
             "us_per_bind": wall * 1e6 / (nthreads * per),
             "binds_per_s": nthreads * per / wall,

@@ -265,6 +265,8 @@ constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is rese
 // a wide namespace (an element past 64 tokens): token slots per element, and the token
 // image length its fixed-width templates hold
 constexpr uint32_t kWideTokens = 1024, kWideTokenLen = 46;
+// passes a group-commit leader runs back to back while binds keep queueing
+constexpr int kLeadRounds = 8;
 // new tokens a single bind's decoder may take (NewTok entries; more: the two-pass path)
 constexpr uint32_t kNewTokCap = 512;
 // device passes per call: registration, a grown answer area and a serial re-decode each
@@ -1406,10 +1408,14 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
 }
 
 NifState* state(laspj_ctx* ctx) {
+    // (without ctx->mu once it exists: a device phase holds that lock, and binds arriving
+    // meanwhile must reach the group-commit queue, not wait behind it)
+    if (NifState* s = __atomic_load_n(&ctx->nif, __ATOMIC_ACQUIRE)) return s;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->nif) {
-        ctx->nif = new (std::nothrow) NifState;
-        if (ctx->nif) ctx->nif->ks[1].kind = LASPJ_KIND_GSET;
+        NifState* s = new (std::nothrow) NifState;
+        if (s) s->ks[1].kind = LASPJ_KIND_GSET;
+        __atomic_store_n(&ctx->nif, s, __ATOMIC_RELEASE);
     }
     return ctx->nif;
 }
@@ -1930,19 +1936,23 @@ int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t
         *verdict = r.verdict;
         return r.rc;
     }
-    // (the leader serves one batch — its own request among them — and hands over: a waiter
-    // whose request came later leads the next)
+    // (the leader serves batches — its own request in the first — while binds keep
+    // arriving, up to kLeadRounds, then hands over: no waiter's wake-up between passes)
     S->leading = true;
     std::vector<laspj::BindReq*> batch;
-    batch.swap(S->queue);
-    q.unlock();
-    {
-        std::lock_guard<std::mutex> lk(S->mu);
-        laspj::serve_binds(ctx, S, batch);
+    for (int round = 0; round < laspj::kLeadRounds && !S->queue.empty(); ++round) {
+        batch.clear();
+        batch.swap(S->queue);
+        q.unlock();
+        {
+            std::lock_guard<std::mutex> lk(S->mu);
+            laspj::serve_binds(ctx, S, batch);
+        }
+        q.lock();
+        // (answers published under the queue's lock: a waiter reads them once it sees done)
+        for (laspj::BindReq* b : batch) b->done = true;
+        S->qcv.notify_all();
     }
-    q.lock();
-    // (answers published under the queue's lock: a waiter reads them once it sees done)
-    for (laspj::BindReq* b : batch) b->done = true;
     S->leading = false;
     S->qcv.notify_all();
     *status = r.status;

@@ -21,7 +21,7 @@ def main():
     ref = etf.term_to_binary(oorset.merge(ta, tb))
     out = bench.config1_resident(ctx, pa, pb, ref)
     keep = {k: v for k, v in out.items() if k.startswith("us_") or k.endswith("stages")
-            or k.endswith("samples_us")}
+            or k.endswith("samples_us") or k.startswith("bind_")}
     print(json.dumps(keep))
     print(json.dumps(ctx.nif_stats()))
 
