@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/laspj.h"
+#include "../../include/laspj_tune.h"
 
 namespace laspj {
 struct NifState;                       // laspj_nif.hip

@@ -1,4 +1,4 @@
-"""The C-ABI library loads and exports every entry point include/laspj.h declares, and
+"""The C-ABI library loads and exports every entry point include/*.h declares, and
 the ctypes binding (the NIF stand-in) binds each of them.  No compute without a GPU."""
 
 import ctypes
@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared():
-    src = open(os.path.join(ROOT, "include", "laspj.h")).read()
+    import glob
+    src = "".join(open(h).read() for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(laspj_[a-z0-9_]+)\s*\(", src)))
 

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""The C-ABI entry-point table of INTEGRATION.md §4, generated from include/laspj.h:
+"""The C-ABI entry-point table of INTEGRATION.md §4, generated from include/laspj.h (and the
+A/B knob header include/laspj_tune.h):
 every function the header declares, where (laspj.h:line), the reference function(s) its
 comment block cites (file.erl:lines), and the comment's first sentence.  Functions whose
 comment cites nothing are runtime plumbing (contexts, buffers, events, tuning).
@@ -12,7 +13,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDR = os.path.join(ROOT, "include", "laspj.h")
+HDRS = [os.path.join(ROOT, "include", h) for h in ("laspj.h", "laspj_tune.h")]
 DOC = os.path.join(ROOT, "INTEGRATION.md")
 BEGIN = "<!-- abi-table:begin (tools/abi_table.py --write) -->"
 END = "<!-- abi-table:end -->"
@@ -22,10 +23,19 @@ CITE = re.compile(r"\b[\w/]+\.(?:erl|hrl):\d+(?:-\d+)?(?:,\s*\d+(?:-\d+)?)*")
 
 
 def entries():
-    """(name, line, section, citations, first sentence) per declared function.  A comment
+    """(name, where, section, citations, first sentence) per declared function.  A comment
     block documents the declarations after it up to the next blank line or comment."""
-    lines = open(HDR).read().splitlines()
-    out, comment, section = [], [], ""
+    out = []
+    for hdr in HDRS:
+        out += _entries(hdr)
+    return out
+
+
+def _entries(hdr):
+    lines = open(hdr).read().splitlines()
+    base = os.path.basename(hdr)
+    out, comment = [], []
+    section = "" if base == "laspj.h" else "A/B knobs"
     in_c = prev_comment = False
     for no, line in enumerate(lines, 1):
         s = line.strip()
@@ -49,11 +59,12 @@ def entries():
             text = " ".join(c for c in comment if c)
             cites = sorted(set(CITE.findall(text)), key=text.index)
             first = re.split(r"(?<=[.;])\s", text, maxsplit=1)[0] if text else ""
-            out.append((m.group(1), no, section, cites, first))
+            out.append((m.group(1), no if base == "laspj.h" else f"{base}:{no}", section,
+                        cites, first))
     return out
 
 
-PLUMBING = ("library / context", "device buffers", "timing")
+PLUMBING = ("library / context", "device buffers", "timing", "A/B knobs")
 
 
 def table():
