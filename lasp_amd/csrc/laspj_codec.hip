@@ -1994,13 +1994,18 @@ __device__ __forceinline__ bool new_tok_image(const uint8_t* buf, uint32_t o, ui
     return n == RL - 7u;
 }
 
-// staged record at o against template t (global), bytewise: <0, 0, >0
+// staged record at o against the 16-byte-aligned, zero-padded template t (global),
+// bytewise: <0, 0, >0 — the template in three 16-byte loads issued together (a byte loop
+// would be a chain of dependent global loads), then word by word, big-endian
 __device__ __forceinline__ int rec_cmp(const uint8_t* buf, uint32_t o, uint32_t RL,
                                        const uint8_t* t) {
-    for (uint32_t i = 0; i < RL; ++i) {
-        const int a = buf[o + i], b = t[i];
-        if (a != b) return a - b;
-    }
+    uint32_t rw[12], tw[12];
+    rec_words(buf, o, RL, rw);
+    load48(tw, t, RL);
+#pragma unroll
+    for (int i = 0; i < 12; ++i)
+        if (rw[i] != tw[i])
+            return __builtin_bswap32(rw[i]) < __builtin_bswap32(tw[i]) ? -1 : 1;
     return 0;
 }
 
