@@ -848,6 +848,9 @@ struct LBJoin {
     uint32_t* ticket;  // zero on entry, left zero
     u64* offs_out;     // {0, total}
     ChainArgs cj;      // chain checks (cj.status null: none)
+    // (or null) nonzero: the decoders took tokens the images lack (NewTok) — nothing is
+    // written, the operands are kept for a second launch once the images know them
+    const uint32_t* skip;
 };
 constexpr u64 kLBCnt = 1ull << 40;              // look-back word: bytes | elements << 40
 constexpr u64 kLBVal = (1ull << 62) - 1;
@@ -863,6 +866,13 @@ __device__ void lb_finish(const LBJoin& lb, uint32_t nch, uint32_t hdr, uint8_t*
     }
     __syncthreads();
     if (!s_lb_last || threadIdx.x != 0) return;
+    if (lb.skip && *lb.skip) {
+        lb.offs_out[0] = 0;
+        lb.offs_out[1] = 0;
+        *lb.ticket = 0;
+        __threadfence_system();
+        return;
+    }
     u64 w;
     for (;;) {                             // the last chunk's inclusive word (relaxed)
         w = __hip_atomic_load(lb.st + nch - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -924,6 +934,10 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_rec(const u64x2* cel
             if (lane == 0) lb.cj.status[r] = st;
             chain_publish(lb.cj, r, st, lane);
         }
+        lb_finish(lb, nch, hdr, out);
+        return;
+    }
+    if (LB && lb.skip && *lb.skip) {
         lb_finish(lb, nch, hdr, out);
         return;
     }
@@ -4955,7 +4969,7 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
                                               ctx->tune_etf_read >= 8)
                      ? k_orset_etf_read<true> : k_orset_etf_read<false>;
     ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
-    if (nt && nt->out && d->bin_tokens && b->replicas == 1) tabs.nt = *nt;
+    if (nt && nt->out && d->bin_tokens) tabs.nt = *nt;
     // the header hash (segment search; element batches without the scalar walk — knob 6
     // keeps the walking element batches)
     const HdrHash hh{d->rd_htab, d->rd_hmask, d->rd_hlens};
@@ -5279,10 +5293,10 @@ bool etf_merge_write_one(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t
 int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E,
                             const laspj_etf_dict* d, int tag, int vers, u64* offs_out,
                             uint8_t* out, uint64_t cap_bytes, u64* lbst, uint32_t* ticket,
-                            const ChainJob* chain) {
+                            const ChainJob* chain, const uint32_t* skip) {
     const uint32_t nch = (E + kBlock - 1) / kBlock;
     LBJoin lb{reinterpret_cast<u64x2*>(a), reinterpret_cast<u64x2*>(b), lbst, ticket, offs_out,
-              chain_args(chain)};
+              chain_args(chain), skip};
     const uint32_t cblocks = lb.cj.status ? (lb.cj.nrep + 3u) / 4u : 0u;
     auto k = d->tok_max <= 8 ? k_orset_etf_write_rec<24576, true, true>
                              : k_orset_etf_write_rec<24576, false, true>;

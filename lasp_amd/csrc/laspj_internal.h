@@ -389,12 +389,15 @@ int etf_merge_size_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, const laspj
 // the NIF's single merge (R == 1): join, size pass and writer in ONE launch
 // (k_orset_etf_write_rec's look-back form), when etf_merge_write_one holds; lbst: a zeroed
 // word per 256-element chunk, ticket: a zeroed word (left zero), offs_out: {0, total}
-// (total > cap: nothing written), chain: the deferred chain checks ride along
+// (total > cap: nothing written), chain: the deferred chain checks ride along; skip (or
+// null): a device word the decoders set when they took unseen tokens (NewTok) — then
+// nothing is written, {0, 0} answered and the operands kept
 bool etf_merge_write_one(const laspj_ctx* ctx, const laspj_etf_dict* d, uint64_t R, uint32_t E);
 int etf_merge_write_enqueue(laspj_ctx* ctx, uint64_t* a, uint64_t* b, uint32_t E,
                             const laspj_etf_dict* d, int tag, int vers,
                             unsigned long long* offs_out, uint8_t* out, uint64_t cap_bytes,
-                            unsigned long long* lbst, uint32_t* ticket, const ChainJob* chain);
+                            unsigned long long* lbst, uint32_t* ticket, const ChainJob* chain,
+                            const uint32_t* skip = nullptr);
 // lasp_core:bind/3 (write = false) / write/4 (write = true) of n resident variables: curs /
 // ins / wprs (device arrays of n: the variable's cells, its decoded operand's cells — left
 // zero — and their width in words; maxw the widest), dstat (n decode statuses: read, or —

@@ -323,6 +323,10 @@ struct Call {
     // (its cells then hold slots nobody registered unless it decoded)
     std::vector<NewTok> newtoks;
     bool nt_met = false;
+    bool no_newtok = false;         // (two payloads gave one slot to different tokens)
+    // a merge whose decoders took new tokens: its operands' cells stay on the device and
+    // the next pass only joins and writes (the images patched with the tokens first)
+    bool write_only = false;
 };
 
 KindState& kstate(NifState* S, int32_t kind) {
@@ -639,6 +643,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     // per-segment results in a device area of their own after the in region
     // (one plan only: the join / bind launch carries one chain check)
     const bool defer = (G == 1 || multi) && dec && orset && plan.nseg && !c.no_defer &&
+                       !c.write_only &&
                        ((c.op == Op::MERGE && etf_merge_fused(ctx, n, E)) || var_op ||
                         (c.op == Op::VALUE && etf_value_direct(ctx, n, E)));
     const uint64_t seg_bytes = defer ? al(plan.nseg * kSegResBytes, 256) : 0;
@@ -646,9 +651,12 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     // one operand over binary tokens (a bind, write/4, a threshold, value/1 — no answer
     // carries token images): tokens the namespace has not seen are taken by the decoder
     // (NewTok entries into the answer area, registered by run())
-    const bool nt_on = (var_op || c.op == Op::THRESHOLD || c.op == Op::VALUE) && m == 1 &&
-                       G == 1 && orset && !K.wide && dec && !c.redo.n &&
-                       etf_dict_bin_tokens(K.etf);
+    const bool nt_merge = c.op == Op::MERGE && n == 1 && m == 2 &&
+                          etf_merge_write_one(ctx, K.etf, n, E);
+    const bool nt_on = ((var_op || c.op == Op::THRESHOLD || c.op == Op::VALUE) && m == 1 ||
+                        nt_merge) &&
+                       G == 1 && orset && !K.wide && dec && !c.redo.n && !c.write_only &&
+                       !c.no_newtok && etf_dict_bin_tokens(K.etf);
     const uint64_t o_nt = o_pay, nt_bytes = nt_on ? al(sizeof(NewTok) * kNewTokCap, 256) : 0;
     o_pay += nt_bytes;
     const uint64_t out_bytes = o_pay + ocap;
@@ -771,8 +779,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             sent = al(upto, 16);
             return LASPJ_OK;
         };
-        if (dec && c.redo.n) {
-            // (a redo pass: the head and payloads the last pass pulled are still there)
+        if (dec && (c.redo.n || c.write_only)) {
+            // (a redo or write-only pass: the head and payloads the last pass pulled are
+            // still there)
         } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
@@ -814,7 +823,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             cjob.res = dseg;
             cjob.hres = rout + o_seg;
         }
-        if (dec && multi) {
+        if (c.write_only) {
+            // (the operands' cells the last pass decoded are still there)
+        } else if (dec && multi) {
             // every namespace's payloads in one launch (the cells zeroed first when the last
             // call left them dirty: the decoders only set what they decode)
             if (!clean && !c.redo.n) LJ_HIP(ctx, hipMemsetAsync(cin, 0, cells_in, ctx->stream));
@@ -885,8 +896,10 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             if (orset && etf_merge_write_one(ctx, K.etf, n, E)) {
                 // one answer: join, size pass and writer in one launch (look-back), the
                 // operands cleared behind it, the chain checks riding along
-                if (int s = etf_merge_write_enqueue(ctx, lhs.dev, rhs.dev, E, K.etf, -1, 1, dooff,
-                                                    dopay, ocap, dlb, dticket, &cjob))
+                if (int s = etf_merge_write_enqueue(
+                        ctx, lhs.dev, rhs.dev, E, K.etf, -1, 1, dooff, dopay, ocap, dlb, dticket,
+                        &cjob,
+                        nt_on ? reinterpret_cast<const uint32_t*>(din + i_zero + z_nt) : nullptr))
                     return s;
                 S->clean_words = in_words;
                 break;
@@ -1032,7 +1045,11 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
             uint32_t k = 0;
             while (k < kNewTokCap && ents[k].seq == S->nt_seq) ++k;
             c.nt_met = k != 0;
-            if (k && c.st[0] == LASPJ_DEC_OK) c.newtoks.assign(ents, ents + k);
+            bool ok = true;
+            for (uint32_t i = 0; i < m; ++i) ok &= c.st[i] == LASPJ_DEC_OK;
+            if (k && ok) c.newtoks.assign(ents, ents + k);
+            // (a merge's writer then wrote nothing and left the operands' cells)
+            if (k && c.op == Op::MERGE) S->clean_words = 0;
         }
         if (var_op)
             for (int32_t x : c.st)
@@ -1129,19 +1146,43 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict);
 // the order the dictionary numbers them in; the device images learn them on the next call
 // (patch_etf).  A slot the dictionary would number otherwise cannot happen by
 // construction; it fails the call loudly (the cells already hold the device's slots).
-int register_new_tokens(laspj_ctx* ctx, NifState* S, KindState& K, const Call& c) {
+int register_new_tokens(laspj_ctx* ctx, NifState* S, KindState& K, const Call& c,
+                        bool* conflict) {
     const uint64_t t0 = now_ns();
+    *conflict = false;
     std::vector<NewTok> ts = c.newtoks;
     std::sort(ts.begin(), ts.end(), [](const NewTok& a, const NewTok& b) {
         return a.e != b.e ? a.e < b.e : a.slot < b.slot;
     });
     const uint32_t TL = etf_dict_tok_len(K.etf);
+    // an entry's image: offsets are into the call's payloads laid end to end
+    auto image = [&](const NewTok& t) -> const uint8_t* {
+        uint64_t at = 0;
+        for (uint32_t i = 0; i < c.m; ++i) {
+            if (t.off >= at && (uint64_t)t.off + TL <= at + c.len[i]) return c.p[i] + (t.off - at);
+            at += c.len[i];
+        }
+        return nullptr;
+    };
+    // two operands of a merge may each take a token for one element: the same slot is
+    // the same token (kept once) or a conflict (the caller decodes the usual way)
+    std::vector<NewTok> uniq;
+    for (size_t i = 0; i < ts.size(); ++i) {
+        if (!uniq.empty() && uniq.back().e == ts[i].e && uniq.back().slot == ts[i].slot) {
+            const uint8_t *x = image(uniq.back()), *y = image(ts[i]);
+            if (!x || !y || std::memcmp(x, y, TL) != 0) {
+                *conflict = true;
+                return LASPJ_OK;
+            }
+            continue;
+        }
+        uniq.push_back(ts[i]);
+    }
     dict_begin(K.dict);
-    for (const NewTok& t : ts) {
+    for (const NewTok& t : uniq) {
         uint32_t slot = 0;
-        const int st = (uint64_t)t.off + TL <= c.len[0]
-                           ? dict_reg_tok(K.dict, t.e, c.p[0] + t.off, TL, &slot)
-                           : LASPJ_DEC_MALFORMED;
+        const uint8_t* img = image(t);
+        const int st = img ? dict_reg_tok(K.dict, t.e, img, TL, &slot) : LASPJ_DEC_MALFORMED;
         if (st != LASPJ_DEC_OK || slot != t.slot) {
             dict_rollback(K.dict);
             return fail(ctx, LASPJ_E_DEVICE,
@@ -1152,7 +1193,7 @@ int register_new_tokens(laspj_ctx* ctx, NifState* S, KindState& K, const Call& c
     dict_begin(K.dict);                           // (the journal kept nothing)
     K.stale = true;                               // (patched on the next call)
     ++S->stats[2];
-    S->stats[18] += ts.size();
+    S->stats[18] += uniq.size();
     S->stats[12] += now_ns() - t0;
     return LASPJ_OK;
 }
@@ -1281,8 +1322,30 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         c.redo.n = 0;                 // (a redo pass is taken once)
         if (s == -1000) continue;                // answer area grown: once more
         if (s) return s;
-        if (!c.newtoks.empty())
-            if (int s2 = register_new_tokens(ctx, S, *c.groups[0].K, c)) return s2;
+        c.write_only = false;
+        if (!c.newtoks.empty()) {
+            KindState& K = *c.groups[0].K;
+            bool conflict = false;
+            if (int s2 = register_new_tokens(ctx, S, K, c, &conflict)) return s2;
+            if (conflict) {
+                // two operands gave one slot to different tokens: decode again the usual
+                // way (registration, then a pass over the known terms)
+                c.no_newtok = true;
+                S->clean_words = 0;
+                continue;
+            }
+            if (c.op == Op::MERGE) {
+                // the answer needs the tokens' images: patch them in, then join and write
+                // the cells the decoders left (a rebuild moves element slots: decode again)
+                if (patch_etf(ctx, S, K)) {
+                    c.write_only = true;
+                } else {
+                    if (int s2 = rebuild_etf(ctx, S, K)) return s2;
+                    S->clean_words = 0;
+                }
+                continue;
+            }
+        }
         // a bind that decoded in this pass was merged in it: WRITTEN if this pass (or an
         // earlier one, for an operand whose call needed another pass) changed its value
         if (c.op == Op::BIND) {

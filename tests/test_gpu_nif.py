@@ -594,3 +594,46 @@ def test_nif_unresolved_call_answers_fallback():
         assert ctx.nif_merge(_tb(a), _tb(b4)) == (OK, _tb(oorset.merge(a, b4)))
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_nif_merge_of_unseen_binary_tokens():
+    """merge/2 of a known state and one carrying tokens the context has not seen (another
+    node's updates, lasp_orset.erl:222-230): the decoders take them in the first pass, the
+    images are patched, and a second launch only joins and writes (no staging or decode
+    again); both operands carrying the same new token keep it once; two different new
+    tokens given one slot by the two operands decode the usual way.  Every answer is the
+    oracle's."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(71)
+        rb = lambda b: bytes([b]) + bytes(rng.getrandbits(8) for _ in range(19))  # noqa: E731
+        base = [(e, sorted([(rb(0x40 + 2 * k), k == 1) for k in range(2)], key=_key))
+                for e in range(3000)]
+        assert ctx.nif_merge(_tb(base), _tb(base)) == (OK, _tb(base))
+        for case in ("one side", "both sides alike", "both sides differ"):
+            picks = sorted(rng.sample(range(3000), 25))
+            new = {e: [rb(rng.choice((0x00, 0x41, 0xff)))] for e in picks}
+            b = [(e, sorted(ts + [(t, False) for t in new.get(e, [])], key=_key))
+                 for e, ts in base]
+            if case == "one side":
+                a = base
+            elif case == "both sides alike":
+                a = b
+            else:
+                other = {e: [rb(0x43)] for e in picks}
+                a = [(e, sorted(ts + [(t, True) for t in other.get(e, [])], key=_key))
+                     for e, ts in base]
+            s0 = ctx.nif_stats()
+            assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(oorset.merge(a, b))), case
+            s1 = ctx.nif_stats()
+            if case != "both sides differ":
+                assert s1["device_new_tokens"] - s0["device_new_tokens"] == 25, case
+                assert s1["device_passes"] - s0["device_passes"] == 2, case
+            assert s1["fallbacks"] == s0["fallbacks"]
+            # the same merge again: every token known, one pass
+            assert ctx.nif_merge(_tb(a), _tb(b)) == (OK, _tb(oorset.merge(a, b)))
+            assert ctx.nif_stats()["device_passes"] - s1["device_passes"] == 1
+            base = oorset.merge(a, b)
+    finally:
+        ctx.close()
