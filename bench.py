@@ -613,7 +613,7 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
         ready.wait(timeout=120)
     except threading.BrokenBarrierError:
         pass
-    p0 = ctx.nif_stats()["device_passes"] if shared else 0
+    st0 = ctx.nif_stats() if shared else None
     for t in ths:
         t.join(timeout=300)
     if errs or len(spans) != nthreads:
@@ -621,8 +621,13 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
     wall = max(b for _a, b in spans) - min(a for a, _b in spans)
     extra = {}
     if shared:
-        # (binds per device pass: the group commit's batches)
-        extra["binds_per_pass"] = nthreads * per / max(1, ctx.nif_stats()["device_passes"] - p0)
+        # binds per device pass (the group commit's batches) and where a pass's host time
+        # goes (µs per pass)
+        st1 = ctx.nif_stats()
+        passes = max(1, st1["device_passes"] - st0["device_passes"])
+        extra["binds_per_pass"] = nthreads * per / passes
+        extra["pass_stages_us"] = {k: round((st1[k] - st0[k]) / passes / 1e3, 1) for k in
+                                   ("ns_stage_enqueue", "ns_stage_copy", "ns_device_wait")}
     return {**extra, "contexts": 1 if shared else nthreads, "threads": nthreads,
             "binds": nthreads * per,
             "us_per_bind": wall * 1e6 / (nthreads * per),
