@@ -584,3 +584,56 @@ def test_tokens_no_bucket_window_separates():
         assert ctx.nif_merge(_tb(base), _tb(cur)) == (OK, _tb(oorset.merge(base, cur)))
     finally:
         ctx.close()
+
+
+def test_new_token_decode_fuzz():
+    """The one-pass new-token decode against the oracle on random binds: unseen binary
+    tokens anywhere in an element (several per element, runs of them), mixed with
+    non-canonical states — two tokens swapped (descending), a token twice, a token of
+    another length — which must answer FALLBACK and leave the variable as it was (the
+    reference's own clause then runs), exactly as the two-pass path would."""
+    ctx = _ctx()
+    try:
+        rng = random.Random(97)
+        tok = lambda: bytes(rng.getrandbits(8) for _ in range(20))  # noqa: E731
+        base = [(e, sorted([(tok(), rng.random() < 0.3) for _ in range(rng.randint(1, 3))],
+                           key=_key)) for e in range(600)]
+        var = ctx.var("orset")
+        assert var.write(_tb(base)) == OK
+        cur = base
+        kinds = {"ok": 0, "swap": 0, "twice": 0, "length": 0}
+        for it in range(80):
+            val = []
+            bad = rng.choice(["ok"] * 5 + ["swap", "twice", "length"])
+            victim = rng.randrange(600)
+            for e, ts in cur:
+                ts = list(ts)
+                if rng.random() < 0.08 or e == victim:
+                    ts += [(tok(), rng.random() < 0.3) for _ in range(rng.randint(1, 4))]
+                ts = sorted(ts, key=_key)
+                if e == victim and bad == "swap" and len(ts) >= 2:
+                    ts[0], ts[1] = ts[1], ts[0]
+                elif e == victim and bad == "twice":
+                    ts = sorted(ts + [ts[0]], key=_key)
+                elif e == victim and bad == "length":
+                    ts = sorted(ts + [(tok() + b"x", False)], key=_key)
+                if len(ts) > 60:
+                    ts = ts[:60]
+                val.append((e, ts))
+            kinds[bad] += 1
+            got = var.bind(_tb(val))
+            if bad in ("swap", "twice"):
+                assert got[0] == FALLBACK, (it, bad)
+                assert var.read() == (OK, _tb(cur)), (it, bad)
+                continue
+            assert got[0] == OK, (it, bad)
+            st, new = 0 if exact_eq(cur, oorset.merge(cur, val)) else 1, oorset.merge(cur, val)
+            assert got == (OK, st), (it, bad)
+            cur = new
+            if it % 5 == 0 or bad == "length":
+                assert var.read() == (OK, _tb(cur)), (it, bad)
+        assert var.read() == (OK, _tb(cur))
+        assert min(kinds.values()) > 0
+        assert ctx.nif_stats()["device_new_tokens"] > 100
+    finally:
+        ctx.close()
