@@ -212,6 +212,9 @@ def cpu_baseline(elements: int, budget: float):
         "config1": {"workload": "2 replicas x 10k elements (BASELINE configs[0]), 1 thread",
                     "us_merge": m, "us_union": u, "us_filter": f, "us_value": v,
                     "us_inflation": infl,
+                    # lasp_core:bind/3 (lasp_core.erl:298-304) does both: Merged = merge(Value0,
+                    # Value), then is_inflation(Value0, Merged) — the keyfind walk above
+                    "us_bind": m + infl,
                     "us_merge_all_cores_per_merge": m_threads,
                     "all_cores": cores},
     }
