@@ -1030,6 +1030,13 @@ def main():
 
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(E, args.cpu_budget)
+        steady = out.get("config1_gpu", {}).get("steady")
+        if isinstance(steady, dict):
+            # the same step on the reference's algorithm, one core (C restatement): bind/3
+            # is merge + is_inflation, read/6's threshold_met is is_inflation; update/3 and
+            # the read's term copy are left out (a lower bound)
+            c1 = out["cpu_baseline"]["config1"]
+            steady["cpu_reference_us_per_step_lower_bound"] = c1["us_bind"] + c1["us_inflation"]
     print(json.dumps(out), flush=True)
     if ae_failed:
         print("bench: anti-entropy leg failed (see antientropy.error)", file=sys.stderr)
