@@ -583,6 +583,7 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
     L = ctx.L
     loop = _bind_loop_lib()
     ready, errs, spans = threading.Barrier(nthreads + 1), [], []
+    done = threading.Barrier(nthreads)
 
     def worker():
         try:
@@ -599,15 +600,19 @@ def _bind_threads(ctx, nthreads: int, per: int, ref: bytes, pb: bytes, shared: b
             spans.append((t, time.perf_counter()))
             if (d2.value, s2.value) != (0, 1):
                 errs.append("bad answer")
+            # (teardown only once every scheduler is done: freeing device memory waits for
+            # the device and would stall the others' binds inside the timed span)
+            done.wait()
             v2.close()
             if not shared:
                 c2.close()
         except Exception as e:       # noqa: BLE001 — reported below
             errs.append(repr(e))
-            try:
-                ready.abort()
-            except Exception:
-                pass
+            for b in (ready, done):
+                try:
+                    b.abort()
+                except Exception:
+                    pass
 
     ths = [threading.Thread(target=worker) for _ in range(nthreads)]
     for t in ths:

@@ -106,14 +106,17 @@ struct BindReq {
     uint64_t n;
     int32_t status = 0, verdict = LASPJ_NIF_FALLBACK;
     int rc = LASPJ_OK;
-    bool done = false;
+    // its own wake-up (no herd of waiters on one condition and one lock): done — answered;
+    // lead — handed the leadership, its request still to serve
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, lead = false;
 };
 
 struct NifState {
     std::mutex mu;                  // one call at a time (ctx->mu is held per device phase)
     // single binds queued for the next group-commit pass, and whether a caller leads one
     std::mutex qmu;
-    std::condition_variable qcv;
     std::vector<BindReq*> queue;
     bool leading = false;
     KindState ks[2];                // the image calls' dictionaries: [0] OR-Set, [1] G-Set
@@ -1990,34 +1993,66 @@ int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t
     // own first) and runs them as one bind_many, again while more arrive; the others wait
     // for their answers.  One context per GPU then batches many schedulers' binds
     // (lasp_vnode.erl:213-237) instead of one stream and pass per scheduler.
-    laspj::BindReq r{var, value, n};
-    std::unique_lock<std::mutex> q(S->qmu);
-    S->queue.push_back(&r);
-    while (!r.done && S->leading) S->qcv.wait(q);
-    if (r.done) {
-        *status = r.status;
-        *verdict = r.verdict;
-        return r.rc;
+    laspj::BindReq r;
+    r.var = var;
+    r.p = value;
+    r.n = n;
+    {
+        std::lock_guard<std::mutex> q(S->qmu);
+        if (S->leading) {
+            S->queue.push_back(&r);
+        } else {
+            S->leading = true;
+            r.lead = true;
+        }
     }
-    // (the leader serves batches — its own request in the first — while binds keep
-    // arriving, up to kLeadRounds, then hands over: no waiter's wake-up between passes)
-    S->leading = true;
+    if (!r.lead) {
+        std::unique_lock<std::mutex> lk(r.m);
+        r.cv.wait(lk, [&] { return r.done || r.lead; });
+        if (r.done) {
+            *status = r.status;
+            *verdict = r.verdict;
+            return r.rc;
+        }
+    }
+    // the leader: its own request and every queued one per pass, again while binds keep
+    // arriving (up to kLeadRounds), then it hands the leadership to the oldest waiter
     std::vector<laspj::BindReq*> batch;
-    for (int round = 0; round < laspj::kLeadRounds && !S->queue.empty(); ++round) {
+    bool own = true;
+    for (int round = 0; round < laspj::kLeadRounds; ++round) {
         batch.clear();
-        batch.swap(S->queue);
-        q.unlock();
+        {
+            std::lock_guard<std::mutex> q(S->qmu);
+            batch.swap(S->queue);
+        }
+        if (own) batch.insert(batch.begin(), &r);
+        own = false;
+        if (batch.empty()) break;
         {
             std::lock_guard<std::mutex> lk(S->mu);
             laspj::serve_binds(ctx, S, batch);
         }
-        q.lock();
-        // (answers published under the queue's lock: a waiter reads them once it sees done)
-        for (laspj::BindReq* b : batch) b->done = true;
-        S->qcv.notify_all();
+        // (each answer published under its request's own lock; the waiter may return and
+        // drop the request as soon as that lock is released)
+        for (laspj::BindReq* b : batch) {
+            if (b == &r) continue;
+            std::lock_guard<std::mutex> lk(b->m);
+            b->done = true;
+            b->cv.notify_one();
+        }
     }
-    S->leading = false;
-    S->qcv.notify_all();
+    {
+        std::lock_guard<std::mutex> q(S->qmu);
+        if (S->queue.empty()) {
+            S->leading = false;
+        } else {
+            laspj::BindReq* nx = S->queue.front();
+            S->queue.erase(S->queue.begin());
+            std::lock_guard<std::mutex> lk(nx->m);
+            nx->lead = true;
+            nx->cv.notify_one();
+        }
+    }
     *status = r.status;
     *verdict = r.verdict;
     return r.rc;
