@@ -1323,7 +1323,15 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
         }
         int s = device_pass(ctx, S, c);
         c.redo.n = 0;                 // (a redo pass is taken once)
-        if (s == -1000) continue;                // answer area grown: once more
+        if (s == -1000) {
+            // answer area grown: once more (a write-only pass's writer may have cleared
+            // the operands: decode them again)
+            if (c.write_only) {
+                c.write_only = false;
+                S->clean_words = 0;
+            }
+            continue;
+        }
         if (s) return s;
         c.write_only = false;
         if (!c.newtoks.empty()) {
