@@ -557,6 +557,22 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     out["bind_new_token_passes"] = (sc1["device_passes"] - sc0["device_passes"]) / 10
     for v in (rep, far, uv):
         v.close()
+    # lasp_core:union/7's body re-run over resident variables of one namespace
+    # (laspj_var_union): l = A, r = B, out := merge(out, keep-left(l, r)) — nothing crosses
+    # PCIe but the status (the image route: var_read of both, the body, var_bind)
+    ul = ctx.var("orset")
+    ur, uo = ul.replica(), ul.replica()
+    if ul.write(pa) != 0 or ur.write(pb) != 0 or uo.union(ul, ur) != (0, 1):
+        raise RuntimeError("config1: var_union answered wrongly")
+    ust, uvd = C.c_int32(), C.c_int32()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        check(L.laspj_var_union(uo.h, ul.h, ur.h, C.byref(ust), C.byref(uvd)), ctx.h)
+    out["us_var_union"] = (time.perf_counter() - t0) * 1e6 / 50
+    if (uvd.value, ust.value) != (0, 0) or uo.read() != ul.read():     # out =:= keep-left = A
+        raise RuntimeError("config1: var_union answered wrongly")
+    for v in (ul, ur, uo):
+        v.close()
     # schedulers: a context and a variable each, binding B in a loop (4 = the box's
     # hardware queues per process, GPU_MAX_HW_QUEUES; 16 = one per BEAM scheduler)
     for nthreads in (4, 16):

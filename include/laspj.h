@@ -896,11 +896,16 @@ int laspj_gset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
  * read.
  *
  * Namespaces: each variable's dictionary holds the terms of its own value (as each
- * #dv.value is independent), so variables never share an element's 64 token slots — a
+ * #dv.value is independent), so variables never share an element's token slots — a
  * vnode's many variables holding the same element do not crowd one another out.  Replicas
  * of one variable held in one context (laspj_var_create_replica) share a namespace: the
- * tokens one mints are known to the others, so binding a replica's state decodes in one
- * pass.
+ * tokens one mints are known to the others, so binding a replica's state decodes with
+ * every token known; so may the variables of one dataflow (laspj_var_union takes its
+ * operands in one namespace).  An element past 64 tokens (add_elem never collects one)
+ * widens its namespace: cells of k {p, r} pairs, up to 1024 tokens of one image length.
+ * Tokens a namespace has not seen — binaries of its token length on known elements, as
+ * another node's unique/1 mints them — are taken by the decoder in the same device pass
+ * (laspj_nif_stats [18]).
  *
  * Ownership: the NIF wraps a laspj_var in an enif_alloc_resource
  * whose destructor calls laspj_var_destroy; the resource keeps its context's resource
@@ -908,13 +913,12 @@ int laspj_gset_etf_inflation(laspj_ctx* ctx, const uint8_t* prev, uint64_t np,
  * and every call on it is serialised by that context, from any scheduler.
  *
  * A value the columnar form does not hold (verdict FALLBACK of laspj_var_etf_write: an
- * element with more than 64 tokens, `==`-equal terms under two images) is kept as its
- * image on the host: laspj_var_etf_read answers that image, and bind / update / threshold /
- * value answer FALLBACK — the NIF runs the reference's clause over the read term and
- * stores the outcome with laspj_var_etf_write.  A namespace whose element slots run out
- * (a write of a value unlike the namespace's earlier ones) starts a fresh dictionary and
- * writes its resident variables out to their images first; each is decoded again on its
- * next call. */
+ * element past 64 tokens whose token images differ in length, `==`-equal terms under two
+ * images) is kept as its image on the host: laspj_var_etf_read answers that image, and
+ * bind / update / threshold / value answer FALLBACK — the NIF runs the reference's clause
+ * over the read term and stores the outcome with laspj_var_etf_write.  A namespace whose
+ * dictionary grows past 2^20 elements starts a fresh one on write/4 and writes its
+ * resident variables out to their images first; each is decoded again on its next call. */
 typedef struct laspj_var laspj_var;
 /* declare/3 (lasp_core.erl:208-218): a variable holding Type:new() = [] (kind
  * LASPJ_KIND_ORSET or LASPJ_KIND_GSET), in a namespace of its own */
@@ -951,6 +955,16 @@ int laspj_var_etf_threshold(laspj_var* var, const uint8_t* threshold, uint64_t n
 /* 1 when the value (#dv.value, include/lasp.hrl:60-63) is on the device, 0 when it is
  * held as an image */
 int laspj_var_resident(const laspj_var* var, int32_t* resident);
+/* lasp_core:union/7 (lasp_core.erl:602-627) re-run over resident variables: AccValue =
+ * orddict:merge(fun(_, L, _) -> L end, l, r) — per element l's tokens where l holds it,
+ * else r's — then bind/3 of AccValue into out (:291-312): status LASPJ_BIND_WRITTEN when
+ * out changed, LASPJ_BIND_NOOP when not.  Nothing crosses PCIe but the status.  OR-Sets
+ * of one namespace (laspj_var_create_replica); verdict FALLBACK otherwise (G-Sets — the
+ * body's `LValue ++ RValue` is a list value —, variables of different namespaces,
+ * host-held values): the NIF reads l and r and runs the body on their images
+ * (laspj_list_etf_union) as before.  out may be l or r. */
+int laspj_var_union(laspj_var* out, laspj_var* l, laspj_var* r, int32_t* status,
+                    int32_t* verdict);
 /* lasp_core:update/4 (lasp_core.erl:283-287) on the variable: {ok, Value} =
  * Type:update(Op, Actor, Value0) (lasp_orset.erl:99-117, 222-262; lasp_gset.erl:84-88)
  * applied to the resident cells, then bind/3 of Value, which a successful update always
@@ -969,9 +983,10 @@ int laspj_var_resident(const laspj_var* var, int32_t* resident);
  * (optional) the image of E (valid until the context's next call).  An update that only
  * adds returns once its kernel is enqueued; one that removes waits for the statuses.
  * verdict FALLBACK: an Op no clause of the reference's update/3 takes as written (it
- * raises), a term `==` to one the namespace holds under another image, an element's 65th
- * token, a host-held variable — the NIF runs the reference's update on the read value and
- * writes the result. */
+ * raises), a term `==` to one the namespace holds under another image, a token of another
+ * image length in a wide namespace, a host-held variable — the NIF runs the reference's
+ * update on the read value and writes the result (an element's 65th token widens the
+ * namespace instead). */
 #define LASPJ_UPDATE_OK          0
 #define LASPJ_UPDATE_NOT_PRESENT 1
 int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_t* result,

@@ -239,6 +239,7 @@ SIGNATURES = {
                                     C.POINTER(C.c_int32)]),
     "laspj_var_resident": (i, [vp, C.POINTER(C.c_int32)]),
     "laspj_var_create_replica": (i, [vp, vpp]),
+    "laspj_var_union": (i, [vp, vp, vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "laspj_var_etf_update": (i, [vp, vp, u64, C.POINTER(C.c_int32), vpp, C.POINTER(u64), vpp,
                                  C.POINTER(u32), C.POINTER(C.c_int32)]),
     "laspj_list_etf_args": (i, [vp, C.c_int32, vp, u64, vpp, C.POINTER(u64),

@@ -259,6 +259,37 @@ __global__ void __launch_bounds__(256) k_var_adds(uint64_t* __restrict__ cells, 
     }
 }
 
+// lasp_core:union/7's body for OR-Sets (lasp_core.erl:602-627: orddict:merge keeping the
+// left value of a key both hold) over resident l and r, bound into out (bind/3, :291-312:
+// out := merge(out, AccValue), the OR of the cells): per element slot, l's cell where l
+// holds the element (any pair's present word nonzero), else r's; *changed set when
+// `Value0 =:= AccValue` fails (the bind's no-op test: canonical values of one namespace
+// are equal exactly when their cells are; a wave's lanes agree on one atomic).  tw pairs
+// per element.
+// (out may be l or r: no restrict)
+__global__ void __launch_bounds__(256) k_var_union(uint64_t* out, const uint64_t* l,
+                                                   const uint64_t* r, uint32_t E, uint32_t tw,
+                                                   uint32_t* __restrict__ changed) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ch = false;
+    if (e < E) {
+        const uint64_t base = 2ull * e * tw;
+        bool inl = false;
+        for (uint32_t j = 0; j < tw; ++j) inl |= l[base + 2 * j] != 0;
+        const uint64_t* src = inl ? l : r;
+        for (uint32_t j = 0; j < tw; ++j) {
+            const uint64_t op = out[base + 2 * j], oq = out[base + 2 * j + 1];
+            const uint64_t ap = src[base + 2 * j], aq = src[base + 2 * j + 1];
+            ch |= op != ap || oq != aq;                    // Value0 =/= AccValue
+            if ((op | ap) != op || (oq | aq) != oq) {
+                out[base + 2 * j] = op | ap;
+                out[base + 2 * j + 1] = oq | aq;
+            }
+        }
+    }
+    if (__ballot(ch) && (threadIdx.x & 63u) == 0) atomicOr(changed, 1u);
+}
+
 struct Guard {
     std::lock_guard<std::mutex> lk;
     explicit Guard(laspj_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
@@ -2173,6 +2204,62 @@ int laspj_var_etf_threshold(laspj_var* var, const uint8_t* threshold, uint64_t n
     if (int s = laspj::run(ctx, S, c, &vd)) return s;
     *verdict = vd[0];
     *result = vd[0] == LASPJ_NIF_OK ? (int32_t)(c.res[0] != 0) : 0;
+    return LASPJ_OK;
+}
+
+int laspj_var_union(laspj_var* out, laspj_var* l, laspj_var* r, int32_t* status,
+                    int32_t* verdict) {
+    laspj::NifState* S = var_state(out);
+    if (!S || !l || !r) return LASPJ_E_INVAL;
+    laspj_ctx* ctx = out->ctx;
+    if (!status || !verdict) return fail(ctx, LASPJ_E_INVAL, "var_union: null argument");
+    if (l->ctx != ctx || r->ctx != ctx)
+        return fail(ctx, LASPJ_E_INVAL, "var_union: variables of different contexts");
+    std::lock_guard<std::mutex> lk(S->mu);
+    if (!S->vars.count(out) || !S->vars.count(l) || !S->vars.count(r))
+        return fail(ctx, LASPJ_E_INVAL, "var_union: unknown variable");
+    ++S->stats[0];
+    *status = LASPJ_BIND_NOOP;
+    *verdict = LASPJ_NIF_FALLBACK;
+    // OR-Sets of one namespace only: a G-Set's body is `LValue ++ RValue` (a list value),
+    // and cells of two namespaces name different terms by one slot
+    if (out->kind != LASPJ_KIND_ORSET || l->kind != LASPJ_KIND_ORSET ||
+        r->kind != LASPJ_KIND_ORSET || l->ns != out->ns || r->ns != out->ns) {
+        ++S->stats[6];
+        return LASPJ_OK;
+    }
+    for (laspj_var* v : {out, l, r}) {
+        bool ok = false;
+        if (int s = laspj::hydrate(ctx, S, v, &ok)) return s;
+        if (!ok) {
+            ++S->stats[6];
+            return LASPJ_OK;
+        }
+    }
+    laspj::KindState& K = *out->ns;
+    *verdict = LASPJ_NIF_OK;
+    if (!K.dict || K.E == 0) return LASPJ_OK;             // three new() values
+    laspj::Guard g(ctx);
+    const uint32_t tw = laspj::ktw(K);
+    for (laspj_var* v : {out, l, r})
+        if (int s = laspj::fit_var(ctx, v, K.E, tw)) return s;
+    void* word = nullptr;
+    if (laspj::dev_alloc(ctx, 256, &word) != hipSuccess) {
+        hipGetLastError();
+        return fail(ctx, LASPJ_E_NOMEM, "var_union: flag word");
+    }
+    uint32_t changed = 0;                                 // (Value0 =/= AccValue)
+    hipError_t e = hipMemsetAsync(word, 0, 4, ctx->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(laspj::k_var_union, dim3((K.E + 255) / 256), dim3(256), 0,
+                           ctx->stream, out->cells, l->cells, r->cells, K.E, tw,
+                           static_cast<uint32_t*>(word));
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = laspj::readback(ctx, &changed, word, 4);
+    laspj::dev_release(ctx, word, 256);
+    if (e != hipSuccess) return fail(ctx, LASPJ_E_DEVICE, "var_union: %s", hipGetErrorString(e));
+    *status = changed ? LASPJ_BIND_WRITTEN : LASPJ_BIND_NOOP;
     return LASPJ_OK;
 }
 

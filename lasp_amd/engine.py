@@ -264,6 +264,14 @@ class NifVar:
         raw = C.string_at(mint, 20 * n.value) if n.value else b""
         return 0, int(res.value), err, [raw[20 * k:20 * k + 20] for k in range(n.value)]
 
+    def union(self, left: "NifVar", right: "NifVar"):
+        """laspj_var_union: lasp_core:union/7's body over resident left / right (one
+        namespace) bound into this variable — (verdict, status)."""
+        st, verd = C.c_int32(), C.c_int32()
+        check(self.L.laspj_var_union(self.h, left.h, right.h, C.byref(st), C.byref(verd)),
+              self.ctx.h)
+        return int(verd.value), int(st.value)
+
     def close(self):
         if self.h:
             self.L.laspj_var_destroy(self.h)

@@ -637,3 +637,54 @@ def test_new_token_decode_fuzz():
         assert ctx.nif_stats()["device_new_tokens"] > 100
     finally:
         ctx.close()
+
+
+def test_var_union_matches_oracle():
+    """lasp_core:union/7's body re-run over resident variables of one namespace
+    (laspj_var_union): out := merge(out, orddict:merge(keep-left, l, r)), the status the
+    bind's `Value0 =:= AccValue` test gives — over random updates of l and r (adds,
+    removes, new elements), against the oracle's union body and bind; out may be l; a
+    wide namespace too; G-Sets and variables of two namespaces answer FALLBACK."""
+    from oracle import core as ocore
+    ctx = _ctx()
+    try:
+        rng = random.Random(53)
+        for wide in (False, True):
+            l = ctx.var("orset")
+            r, out = l.replica(), l.replica()
+            cur = {"l": [], "r": [], "out": []}
+            vs = {"l": l, "r": r}
+            for it in range(40):
+                name = rng.choice(("l", "r"))
+                e = rng.randrange(40)
+                if wide and it < 4:
+                    ops = [(A("add_all"), [e] * 1)] + [(A("add"), 7)] * 30
+                else:
+                    ops = [(A("add"), e) if rng.random() < 0.7 else (A("remove"), e)]
+                for op in ops:
+                    verd, res, _e, minted = vs[name].update(_tb(op))
+                    assert verd == OK
+                    want = _oracle_update(oorset, op, cur[name], minted)
+                    if want[0] == "ok":
+                        cur[name] = want[1]
+                acc = ocore.union_body("lasp_orset", cur["l"], cur["r"])
+                st = 0 if exact_eq(cur["out"], acc) else 1
+                assert out.union(l, r) == (OK, st), (wide, it)
+                if st:
+                    cur["out"] = oorset.merge(cur["out"], acc)
+                assert out.read() == (OK, _tb(cur["out"])), (wide, it)
+            # out may be one of its operands
+            acc = ocore.union_body("lasp_orset", cur["l"], cur["r"])
+            st = 0 if exact_eq(cur["l"], acc) else 1
+            assert l.union(l, r) == (OK, st)
+            cur["l"] = oorset.merge(cur["l"], acc) if st else cur["l"]
+            assert l.read() == (OK, _tb(cur["l"]))
+            if wide:
+                assert ctx.nif_stats()["namespaces_widened"] >= 1
+        other = ctx.var("orset")
+        assert other.union(l, r)[0] == FALLBACK
+        g1 = ctx.var("gset")
+        g2 = g1.replica()
+        assert g1.union(g1, g2)[0] == FALLBACK
+    finally:
+        ctx.close()
