@@ -22,17 +22,23 @@
 // `Value0 =:= Value`, joins it into the resident cells and answers the status; the value
 // is encoded only when it is read.
 //
-// A term the dictionary has not seen (a freshly minted token) makes the decoder answer
-// UNKNOWN_TERM: the call registers the operands' terms in the host dictionary (only the
-// elements of the decoder segments that failed, when it decoded in segments; else the
-// whole operands, laspj_dict_add), patches or rebuilds the device images and runs the
-// device pass again.  An operand the columnar form does not take — not an orddict of
-// {Elem, [{Token, Bool}]} (an ordset for G-Sets) in term order, an element with no tokens
-// or more than 64, a term `==` to a registered one under another image, a term kind no
-// dictionary holds — gets verdict LASPJ_NIF_FALLBACK: the NIF then runs the reference's
-// own Erlang clause, so the caller always gets the reference's answer (or its crash).
-// Scratch, dictionaries and staging are per context: one context per scheduler (or per
-// vnode), no process globals.
+// A token the dictionary has not seen (another node's unique/1) on a known element is
+// taken by the decoder in the same pass when it is a binary of the namespace's token
+// length (NewTok: the element's next free slot, registered after the pass; a merge's
+// answer is then written by a second, write-only launch once the images know it).  Any
+// other unseen term makes the decoder answer UNKNOWN_TERM: the call registers the
+// operands' terms in the host dictionary (only the elements of the decoder segments that
+// failed, when it decoded in segments; else the whole operands, laspj_dict_add), patches
+// or rebuilds the device images and decodes again (only the failed segments, when it can).
+// An element past 64 tokens widens its namespace (cells of k {p, r} pairs, the wide codec)
+// — image calls start a fresh dictionary first.  An operand the columnar form does not
+// take — not an orddict of {Elem, [{Token, Bool}]} (an ordset for G-Sets) in term order,
+// an element with no tokens, a term `==` to a registered one under another image, a term
+// kind no dictionary holds — gets verdict LASPJ_NIF_FALLBACK: the NIF then runs the
+// reference's own Erlang clause, so the caller always gets the reference's answer (or its
+// crash).  Scratch, dictionaries and staging are per context: one context per scheduler
+// (or per vnode), or one per GPU with the binds of many schedulers committed in groups;
+// no process globals.
 
 #include <sys/random.h>
 
