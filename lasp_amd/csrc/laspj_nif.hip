@@ -2397,9 +2397,12 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
         K.stale = true;
     }
     S->stats[12] += laspj::now_ns() - t0;
-    // the device images learn the new terms now (a token on a known element is patched in
-    // place), so the next bind of a state carrying them decodes in one pass
-    if (K.stale || !K.etf)
+    // the device images learn the new terms before the namespace's next device pass: a
+    // token on a known element is patched in by that pass (run() patches a stale namespace
+    // first — consecutive updates batch their patches); new elements or a new width need
+    // the images now (the cells' element slots and pairs come from them)
+    const bool lazy = orset && !K.wide && K.etf && laspj::dict_elements(K.dict) == K.built_K;
+    if ((K.stale || !K.etf) && !lazy)
         if (!laspj::patch_etf(ctx, S, K))
             if (int s = laspj::rebuild_etf(ctx, S, K)) return s;
     const uint32_t nops = (uint32_t)dops.size();
