@@ -5558,9 +5558,12 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     uint32_t tok_max = 0;
     for (uint32_t x = 0; x < E; ++x)
         tok_max = std::max(tok_max, (uint32_t)__builtin_popcountll(tmask[x]));
+    // (past 8 the head-room grows with the count: a hot element re-added again and again —
+    // add_elem never collects a token — then rebuilds the images every count / 2 adds, not
+    // every tok_headroom)
     if (tok_headroom && toks)
         tok_max = tok_max <= 8 ? std::min(8u, tok_max + tok_headroom)
-                               : std::min(64u, tok_max + tok_headroom);
+                               : std::min(64u, tok_max + std::max(tok_headroom, tok_max / 2));
     // room for token images appended by etf_dict_patch
     const uint64_t tpad_cap = tpad_n + (tok_headroom && toks ? std::max<uint64_t>(tpad_n / 4, 1ull << 16) : 0);
     // record templates (uniform token images only): 104 2 <image> per (element, term rank),
@@ -6198,145 +6201,6 @@ struct WideDict {
 
 namespace {
 
-__global__ __launch_bounds__(kBlock) void k_wide_read(const uint8_t* payload, u64 total,
-                                                      const u64* offs, uint64_t R, WideView W,
-                                                      u64x2* cells, int32_t* status) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock / 64][kDWin];
-    __shared__ u64 acc[kBlock / 64][64];       // an element's pairs (tw <= 32)
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const DictView& d = W.d;
-    const uint32_t E = W.E, tw = W.tw, RL = W.RL, RS = W.RS;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t rep = (uint64_t)blockIdx.x * (kBlock / 64) + wave; rep < R; rep += nwaves) {
-        Stage s{stage[wave], payload, total, 0, 0};
-        const u64 base = offs[rep], end = offs[rep + 1];
-        u64 p = base;
-        int32_t st = LASPJ_DEC_OK;
-        u64x2* c = cells + rep * (u64)E * tw;
-        do {
-            if (!stage_span(s, p, 2, end) || at(s, p) != 131) { st = LASPJ_DEC_MALFORMED; break; }
-            uint32_t n = 0;
-            bool list = false;
-            if (at(s, p + 1) == 106) {
-                p += 2;
-            } else if (at(s, p + 1) == 108 && stage_span(s, p, 6, end)) {
-                n = (at(s, p + 2) << 24) | (at(s, p + 3) << 16) | (at(s, p + 4) << 8) | at(s, p + 5);
-                p += 6;
-                list = true;
-            } else {
-                st = LASPJ_DEC_MALFORMED;
-                break;
-            }
-            int64_t prev = -1;
-            for (uint32_t k = 0; k < n && st == LASPJ_DEC_OK; ++k) {
-                const uint32_t span = (uint32_t)min((u64)(kDWin - 16), end - p);
-                if (!stage_span(s, p, span, end)) { st = LASPJ_DEC_MALFORMED; break; }
-                int64_t found = -1;
-                uint32_t e = 0, hl = 0;
-                for (int64_t c0 = prev + 1; c0 < (int64_t)E && found < 0; c0 += 64) {
-                    const int64_t r = c0 + lane;
-                    bool hit = false;
-                    uint32_t ec = 0, hlc = 0;
-                    if (r < (int64_t)E) {
-                        ec = d.elem_order[r];
-                        hlc = d.elem_off[ec + 1] - d.elem_off[ec] + 3u;
-                        if (hlc > 3u && hlc <= span) {
-                            const uint8_t* t = d.ehdr_pad + d.ehdr_poff[ec];
-                            hit = hlc - 1u <= 48 ? same48(s, p, t, hlc - 1u)
-                                                 : same_long(s, p, t, hlc - 1u);
-                        }
-                    }
-                    const u64 m = __ballot(hit);
-                    if (m) {
-                        const uint32_t w = (uint32_t)__ffsll((long long)m) - 1u;
-                        found = c0 + w;
-                        e = __shfl(ec, w, 64);
-                        hl = __shfl(hlc, w, 64);
-                    }
-                }
-                if (found < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
-                prev = found;
-                p += hl;
-                if (at(s, p - 1) != 108) {
-                    st = at(s, p - 1) == 106 ? LASPJ_DEC_UNREPRESENTABLE : LASPJ_DEC_MALFORMED;
-                    break;
-                }
-                if (!stage_span(s, p, 4, end)) { st = LASPJ_DEC_MALFORMED; break; }
-                const uint32_t m_tok = (at(s, p) << 24) | (at(s, p + 1) << 16) | (at(s, p + 2) << 8) |
-                                       at(s, p + 3);
-                p += 4;
-                if (m_tok == 0 || m_tok > 64u * tw) { st = LASPJ_DEC_UNREPRESENTABLE; break; }
-                const uint32_t r0 = W.rb[e], cnt = W.rb[e + 1] - r0;
-                if (lane < 2u * tw) acc[wave][lane] = 0;
-                wave_sync();
-                int32_t tprev = -1;
-                for (uint32_t j = 0; j < m_tok; ++j) {
-                    if (!stage_span(s, p, RL + 8u, end) && !stage_span(s, p, RL + 6u, end)) {
-                        st = LASPJ_DEC_MALFORMED;
-                        break;
-                    }
-                    int32_t rank = -1;
-                    for (int32_t q0 = tprev + 1; q0 < (int32_t)cnt && rank < 0; q0 += 64) {
-                        const int32_t q = q0 + (int32_t)lane;
-                        bool hit = false;
-                        if (q < (int32_t)cnt && p + RL <= s.hi)
-                            hit = same48(s, p, W.rec + (u64)(r0 + (uint32_t)q) * RS, RL);
-                        const u64 m = __ballot(hit);
-                        if (m) rank = q0 + (int32_t)__ffsll((long long)m) - 1;
-                    }
-                    if (rank < 0) { st = LASPJ_DEC_UNKNOWN_TERM; break; }
-                    tprev = rank;
-                    p += RL;
-                    const uint32_t t0 = p < s.hi ? at(s, p) : 0u;
-                    uint32_t len, h;
-                    if ((t0 == 100 || t0 == 118) && p + 3 <= s.hi && at(s, p + 1) == 0) {
-                        len = at(s, p + 2);
-                        h = 3;
-                    } else if (t0 == 119 && p + 2 <= s.hi) {
-                        len = at(s, p + 1);
-                        h = 2;
-                    } else {
-                        st = LASPJ_DEC_MALFORMED;
-                        break;
-                    }
-                    bool flag;
-                    if (len == 4 && p + h + 4 <= end && stage_span(s, p, h + 4, end) &&
-                        at(s, p + h) == 't' && at(s, p + h + 1) == 'r' && at(s, p + h + 2) == 'u' &&
-                        at(s, p + h + 3) == 'e') {
-                        flag = true;
-                    } else if (len == 5 && p + h + 5 <= end && stage_span(s, p, h + 5, end) &&
-                               at(s, p + h) == 'f' && at(s, p + h + 1) == 'a' &&
-                               at(s, p + h + 2) == 'l' && at(s, p + h + 3) == 's' &&
-                               at(s, p + h + 4) == 'e') {
-                        flag = false;
-                    } else {
-                        st = LASPJ_DEC_MALFORMED;
-                        break;
-                    }
-                    p += h + len;
-                    const uint32_t slot = W.rslot[r0 + (uint32_t)rank];
-                    if (lane == 0) {
-                        acc[wave][2u * (slot >> 6)] |= 1ull << (slot & 63u);
-                        if (flag) acc[wave][2u * (slot >> 6) + 1] |= 1ull << (slot & 63u);
-                    }
-                }
-                if (st != LASPJ_DEC_OK) break;
-                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
-                p += 1;
-                wave_sync();
-                if (lane < tw) c[(u64)e * tw + lane] = u64x2{acc[wave][2 * lane], acc[wave][2 * lane + 1]};
-                wave_sync();
-            }
-            if (st != LASPJ_DEC_OK) break;
-            if (list) {
-                if (!stage_span(s, p, 1, end) || at(s, p) != 106) { st = LASPJ_DEC_MALFORMED; break; }
-                p += 1;
-            }
-            if (p != end) st = LASPJ_DEC_MALFORMED;
-        } while (false);
-        if (lane == 0) status[rep] = st;
-    }
-}
 
 // bytes of one present element: 104 2 <elem> 108 <n:32> records 106; a record is
 // 104 2 <token image> and the flag atom (false 8 bytes, true 7)
@@ -6571,18 +6435,6 @@ void wide_dict_destroy(WideDict* w) {
 }
 
 uint32_t wide_elements(const WideDict* w) { return w ? w->v.E : 0; }
-
-int wide_read_enqueue(laspj_ctx* ctx, const WideDict* w, const uint8_t* payload, uint64_t total,
-                      const u64* offs, uint64_t R, uint64_t* cells, int32_t* status, bool clear) {
-    if (clear)
-        LJ_HIP(ctx, hipMemsetAsync(cells, 0, R * (u64)w->v.E * w->v.tw * 16ull, ctx->stream));
-    const uint64_t blocks = (R + 3) / 4, cap = (uint64_t)ctx->cus * 64;
-    hipLaunchKernelGGL(k_wide_read, dim3((unsigned)std::max<uint64_t>(1, std::min(blocks, cap))),
-                       dim3(kBlock), 0, ctx->stream, payload, (u64)total, offs, R, w->v,
-                       reinterpret_cast<u64x2*>(cells), status);
-    LJ_LAUNCHED(ctx);
-    return LASPJ_OK;
-}
 
 int wide_size_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
                       int tag, u64* offsets, uint32_t* flag) {

@@ -597,6 +597,7 @@ struct Dict {
     // fixed-width); 0: not wide, or no token yet
     uint32_t tok_len = 0, tok_len_max = 0;
     uint64_t ntok = 0;                      // tokens registered (all elements)
+    uint32_t max_toks = 0;                  // most tokens of one element (an upper bound)
     // element slots that gained a token since the last dict_take_dirty (the NIF patches
     // their device rows; may repeat a slot or name one whose gain was rolled back)
     std::vector<uint32_t> dirty;
@@ -818,6 +819,7 @@ int reg_tok(Dict* d, uint32_t es, const uint8_t* t, size_t tl, uint16_t* slot) {
     d->tok_eq.insert(ht, es, v, *slot);
     d->toks[es].push_back(v);
     ++d->ntok;
+    d->max_toks = std::max<uint32_t>(d->max_toks, (uint32_t)d->toks[es].size());
     d->journal.push_back((int64_t)es);
     d->dirty.push_back(es);
     return LASPJ_DEC_OK;
@@ -997,10 +999,19 @@ int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, ui
 int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
                       const uint64_t* offsets, uint64_t n, int tag, uint32_t E, uint64_t* out,
                       int32_t* status) {
-    if (!dict || (n && (!blob || !offsets || !status || !out))) return LASPJ_E_INVAL;
+    return laspj::dict_encode_cells(dict, kind, blob, offsets, n, tag, E, 1, out, status);
+}
+
+}  // extern "C"
+
+// (tw {p, r} pairs per OR-Set element: token slot f in pair f / 64 — a wide namespace)
+int laspj::dict_encode_cells(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
+                             const uint64_t* offsets, uint64_t n, int tag, uint32_t E,
+                             uint32_t tw, uint64_t* out, int32_t* status) {
+    if (!dict || (n && (!blob || !offsets || !status || !out)) || tw == 0) return LASPJ_E_INVAL;
     if (kind != LASPJ_KIND_ORSET && kind != LASPJ_KIND_GSET) return LASPJ_E_KIND;
     const Dict& d = dict->d;
-    const uint64_t wpr = kind == LASPJ_KIND_ORSET ? 2ull * E : (E + 63ull) / 64ull;
+    const uint64_t wpr = kind == LASPJ_KIND_ORSET ? 2ull * E * tw : (E + 63ull) / 64ull;
     try {
         for (uint64_t i = 0; i < n; ++i) {
             if (offsets[i + 1] < offsets[i]) return LASPJ_E_INVAL;
@@ -1032,11 +1043,13 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
                         std::string_view key((const char*)tk, tkl);
                         const int f = d.tok(cur, tk, tkl);
                         if (f < 0) return LASPJ_DEC_UNKNOWN_TERM;
+                        if ((uint32_t)f >= 64u * tw) return LASPJ_DEC_UNREPRESENTABLE;
                         if (have_t && cmp_view(prev_t, key) >= 0) return LASPJ_DEC_UNKNOWN_TERM;
                         prev_t = key;
                         have_t = true;
-                        cells[2ull * cur] |= 1ull << f;
-                        if (flag) cells[2ull * cur + 1] |= 1ull << f;
+                        uint64_t* pr = cells + 2ull * ((uint64_t)cur * tw + (uint32_t)f / 64u);
+                        pr[0] |= 1ull << (f & 63);
+                        if (flag) pr[1] |= 1ull << (f & 63);
                         return LASPJ_DEC_OK;
                     });
             } else {
@@ -1068,8 +1081,6 @@ int laspj_dict_encode(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
     return LASPJ_OK;
 }
 
-}  // extern "C"
-
 // ------------------------------------------------------------------ internal accessors
 // (laspj_internal.h): what laspj::etf_dict_patch reads from the host dictionary when the
 // NIF path patches the device images of elements that gained tokens instead of
@@ -1084,6 +1095,8 @@ void dict_take_dirty(laspj_dict* dict, std::vector<uint32_t>* out) {
     out->clear();
     if (dict) out->swap(dict->d.dirty);
 }
+
+uint32_t dict_max_tokens(const laspj_dict* dict) { return dict->d.max_toks; }
 
 uint32_t dict_token_count(const laspj_dict* dict, uint32_t e) {
     if (!dict || e >= dict->d.toks.size()) return 0;

@@ -448,6 +448,11 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
 // term order (order[j] = slot of the j-th smallest)
 uint32_t dict_elements(const laspj_dict* dict);
 uint32_t dict_token_count(const laspj_dict* dict, uint32_t e);
+uint32_t dict_max_tokens(const laspj_dict* dict);   // most tokens of one element (upper bound)
+// laspj_dict_encode with tw {p, r} pairs per OR-Set element (a wide namespace's cells)
+int dict_encode_cells(const laspj_dict* dict, int32_t kind, const uint8_t* blob,
+                      const uint64_t* offsets, uint64_t n, int tag, uint32_t E, uint32_t tw,
+                      uint64_t* out, int32_t* status);
 // the element slots that gained tokens since the last call (repeats possible), cleared
 void dict_take_dirty(laspj_dict* dict, std::vector<uint32_t>* out);
 bool dict_tokens(const laspj_dict* dict, uint32_t e, std::vector<std::string_view>* imgs,
@@ -499,10 +504,8 @@ struct WideDict;
 int wide_dict_create(laspj_ctx* ctx, const WideExport& x, uint32_t tw, WideDict** out);
 void wide_dict_destroy(WideDict* w);
 uint32_t wide_elements(const WideDict* w);
-// decode / size / write, enqueue only (offsets, status, out: device addresses)
-int wide_read_enqueue(laspj_ctx* ctx, const WideDict* w, const uint8_t* payload, uint64_t total,
-                      const unsigned long long* offs, uint64_t R, uint64_t* cells,
-                      int32_t* status, bool clear);
+// the answers' size pass and writer, enqueue only (offsets, out: device addresses); a wide
+// namespace's operands are encoded on the host (dict_encode_cells)
 int wide_size_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,
                       int tag, unsigned long long* offsets, uint32_t* flag);
 int wide_write_enqueue(laspj_ctx* ctx, const WideDict* w, const uint64_t* cells, uint64_t R,

@@ -614,8 +614,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     const bool orset = c.kind == LASPJ_KIND_ORSET;
     const bool wide = orset && K.wide;            // (single-group ops: answers by the wide codec)
     bool dec = m != 0;
+    // (a wide namespace's operands are encoded by the host dictionary: dict_encode_cells)
     for (const Group& g : c.groups)
-        if (orset && g.p1 > g.p0 && !g.K->wide && !etf_dict_decodable(g.K->etf)) dec = false;
+        if (orset && g.p1 > g.p0 && (g.K->wide || !etf_dict_decodable(g.K->etf))) dec = false;
     const bool var_op = c.op == Op::BIND || c.op == Op::WRITE;
     const bool var_in = var_op || c.op == Op::THRESHOLD || c.op == Op::READ || c.op == Op::VVALUE;
     std::vector<unsigned long long> hoffs(m + 1ull, 0);
@@ -785,15 +786,9 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         for (size_t g = 0; g < G; ++g) {
             const Group& gr = c.groups[g];
             if (gr.p1 == gr.p0) continue;
-            if (orset && gr.K->wide) {
-                // (a wide namespace beside one the device cannot decode: the host encoder
-                // lays narrow cells only — those operands answer FALLBACK)
-                for (uint32_t i = gr.p0; i < gr.p1; ++i) hst[i] = LASPJ_DEC_UNREPRESENTABLE;
-                continue;
-            }
-            if (int s = laspj_dict_encode(gr.K->dict, c.kind, blob.data(),
+            if (int s = dict_encode_cells(gr.K->dict, c.kind, blob.data(),
                                           reinterpret_cast<const uint64_t*>(hoffs.data()) + gr.p0,
-                                          gr.p1 - gr.p0, -1, gr.K->E,
+                                          gr.p1 - gr.p0, -1, gr.K->E, ktw(*gr.K),
                                           reinterpret_cast<uint64_t*>(hin + i_pay) + gcell[g],
                                           hst.data() + gr.p0))
                 return fail(ctx, s, "nif: host encode failed (%d)", s);
@@ -891,11 +886,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
                                      reinterpret_cast<NewTok*>(rout + o_nt), kNewTokCap,
                                      S->nt_seq};
                 }
-                if (orset && gr.K->wide) {
-                    if (int s = wide_read_enqueue(ctx, gr.K->wd, din + i_pay, pay, doffs, R,
-                                                  cin + gcell[g], dst + gr.p0, !clean && !c.redo.n))
-                        return s;
-                } else if (orset) {
+                if (orset) {
                     if (int s = etf_read_enqueue(
                             ctx, &gb, gr.K->etf, -1, 1, din + i_pay, pay, doffs, plans[g],
                             plans[g].nseg ? reinterpret_cast<const uint32_t*>(din + i_seg + gseg[g])
@@ -1353,6 +1344,13 @@ int run(laspj_ctx* ctx, NifState* S, Call& c, std::vector<int32_t>* verdict) {
                 for (uint32_t i = p0; i < p1; ++i)
                     if (rst[i - p0] != LASPJ_DEC_OK) fallback[answer_of(i)] = 1;
             }
+            // a wide namespace's operands are host-encoded: its device images serve the
+            // answers' writers only, so a call that writes none keeps the stale ones
+            // (while the cells' element slots and pairs still hold every term)
+            if (K.wide && K.etf && dict_elements(K.dict) <= K.E &&
+                dict_max_tokens(K.dict) <= 64u * K.tw && c.op != Op::MERGE &&
+                c.op != Op::VALUE && c.op != Op::VVALUE && c.op != Op::READ)
+                continue;
             if (!patch_etf(ctx, S, K)) {
                 if (int s = rebuild_etf(ctx, S, K)) return s;
                 c.redo.n = 0;         // (element ranks moved: the last pass's results stale)
@@ -2401,7 +2399,8 @@ int laspj_var_etf_update(laspj_var* var, const uint8_t* op, uint64_t nop, int32_
     // token on a known element is patched in by that pass (run() patches a stale namespace
     // first — consecutive updates batch their patches); new elements or a new width need
     // the images now (the cells' element slots and pairs come from them)
-    const bool lazy = orset && !K.wide && K.etf && laspj::dict_elements(K.dict) == K.built_K;
+    const bool lazy = orset && K.etf && laspj::dict_elements(K.dict) == K.built_K &&
+                      (!K.wide || laspj::dict_max_tokens(K.dict) <= 64u * K.tw);
     if ((K.stale || !K.etf) && !lazy)
         if (!laspj::patch_etf(ctx, S, K))
             if (int s = laspj::rebuild_etf(ctx, S, K)) return s;
