@@ -68,6 +68,7 @@ struct laspj_etf_dict {
     // ehdr_pad + ehdr_poff[e]
     uint32_t rec_len = 0, rec_stride = 0;  // rec_len 0: no templates (mixed token lengths)
     bool bin_tokens = false;               // every token a BINARY_EXT of rec_len - 7 bytes
+    uint32_t big_elems = 0;                // elements holding more than kSmallTok tokens
     const uint8_t* rec_pad = nullptr;
     const uint8_t* ehdr_pad = nullptr;
     const uint32_t* ehdr_poff = nullptr;   // E
@@ -2206,6 +2207,13 @@ __host__ __device__ inline uint32_t hdr_mix(uint32_t h, uint32_t v) {
 // is what that path would accept, with the same cells (element images are
 // self-delimiting and distinct, so the header match is the scan's first match).
 constexpr uint32_t kSmallTok = 8;
+// the element-batch decoders (SMALL) for a dictionary whose elements mostly hold at most
+// kSmallTok tokens: an element with more fails its batch and is decoded on its own by the
+// general path (a few hot elements — re-added again and again — no longer move every
+// element of the dictionary to the many-token decoders)
+inline bool small_dict(const laspj_etf_dict* d) {
+    return d->tok_max <= kSmallTok || 16ull * d->big_elems < d->elements;
+}
 
 __device__ __forceinline__ uint32_t ufl32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane(v);
@@ -4965,7 +4973,7 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
         LJ_HIP(ctx, hipMemsetAsync(b->dev, 0, b->replicas * b->words_per_replica * 8ull,
                                    ctx->stream));
     const bool batched = d->rd_desc && ctx->tune_etf_read != 1;
-    auto kread = d->tok_max <= kSmallTok && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
+    auto kread = small_dict(d) && (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
                                               ctx->tune_etf_read >= 8)
                      ? k_orset_etf_read<true> : k_orset_etf_read<false>;
     ReadTabs tabs{static_cast<const uint4*>(d->rd_desc), d->rd_hdr, d->rd_tb, d->rd_ros};
@@ -4994,7 +5002,7 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
         SegRes* dres = deferred ? static_cast<SegRes*>(defer->res)
                                 : reinterpret_cast<SegRes*>(sc + o_res);
         const uint64_t sblocks = (nseg + 3) / 4, scap = (uint64_t)ctx->cus * 64;
-        const bool small = d->tok_max <= kSmallTok && ctx->tune_etf_read != 2;
+        const bool small = small_dict(d) && ctx->tune_etf_read != 2;
         hipLaunchKernelGGL(small ? k_orset_etf_read_seg<true> : k_orset_etf_read_seg<false>,
                            dim3((unsigned)std::min(sblocks, scap)), dim3(kBlock), 0, ctx->stream,
                            payload, (u64)payload_bytes, offs, R, b->elements, view(d), tabs, tag,
@@ -5019,7 +5027,7 @@ int etf_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, in
             redo = reinterpret_cast<uint32_t*>(sc + o_redo);
             LJ_HIP(ctx, hipMemsetAsync(redo, 0, 4, ctx->stream));
         }
-        const bool csmall = d->tok_max <= kSmallTok &&
+        const bool csmall = small_dict(d) &&
                             (ctx->tune_etf_read == 0 || ctx->tune_etf_read == 6 ||
                              ctx->tune_etf_read >= 8);
         hipLaunchKernelGGL(csmall ? k_etf_read_chain<true> : k_etf_read_chain<false>,
@@ -5085,7 +5093,7 @@ bool etf_multi_fill(const laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups, u
         t.cells = reinterpret_cast<u64x2*>(g[k].cells);
         t.rep0 = g[k].p0;
         t.E = g[k].E;
-        t.small = d->tok_max <= kSmallTok ? 1u : 0u;
+        t.small = small_dict(d) ? 1u : 0u;
         std::memcpy(dt + k, &t, sizeof(t));
         for (uint32_t i = g[k].p0; i < g[k].p1 && i < npay; ++i) pd[i] = k;
     }
@@ -5101,7 +5109,7 @@ int etf_read_multi_enqueue(laspj_ctx* ctx, const EtfGroup* g, uint32_t ngroups,
     const uint32_t* pd = reinterpret_cast<const uint32_t*>(
         static_cast<const char*>(dev_tabs) + ((sizeof(DecTabs) * ngroups + 15ull) & ~15ull));
     bool any[2] = {false, false};                 // [SMALL]
-    for (uint32_t k = 0; k < ngroups; ++k) any[g[k].d->tok_max <= kSmallTok ? 1 : 0] = true;
+    for (uint32_t k = 0; k < ngroups; ++k) any[small_dict(g[k].d) ? 1 : 0] = true;
     const uint64_t R = npay;
     if (plan.nseg) {
         const uint64_t nseg = plan.nseg;
@@ -5523,6 +5531,8 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
                             "etf_dict_create: token order of element %u misses a slot", e);
         }
     }
+    uint32_t big = 0;
+    for (uint32_t e = 0; e < E; ++e) big += __builtin_popcountll(tmask[e]) > 8 ? 1u : 0u;
     bool bin = toks && !mixed && uniform >= 5u;
     for (uint64_t t = 0; bin && t < 64ull * E; ++t) {
         const uint32_t len = tok_off[t + 1] - tok_off[t];
@@ -5859,6 +5869,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     d->tok_max = tok_max;
     d->rec_len = rec_len;
     d->bin_tokens = bin && rec_len != 0;
+    d->big_elems = big;
     d->ehdr_max = (uint32_t)std::min<uint64_t>(ehdr_max, 0xFFFFFFFFull);
     d->rec_stride = (uint32_t)rec_stride;
     d->rec_pad = rec_len ? reinterpret_cast<const uint8_t*>(base + o_rpad) : nullptr;
@@ -6025,6 +6036,7 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
         recs.push_back(PatchRec{dst, at, len});
     };
     uint64_t tpad_used = d->tpad_used;
+    uint32_t big_add = 0;
     std::vector<std::pair<uint64_t, uint32_t>> new_tpoff;     // (slot index, offset)
     std::vector<std::string_view> imgs;
     std::vector<uint8_t> order;
@@ -6035,6 +6047,11 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
         if (e >= E || !dict_tokens(hd, e, &imgs, &order)) return LASPJ_E_UNSUPPORTED;
         const uint32_t cnt = (uint32_t)imgs.size();
         if (cnt > RK || cnt > 64 || cnt == 0) return LASPJ_E_UNSUPPORTED;
+        {
+            uint32_t had = 0;                  // (the element's count the images hold)
+            for (uint32_t k = 0; k < 64; ++k) had += d->h_tpoff[64ull * e + k] != 0xFFFFFFFFu;
+            if (had <= kSmallTok && cnt > kSmallTok) ++big_add;
+        }
         for (const auto& im : imgs)
             if (im.size() != TL || TL + 2u != RL) return LASPJ_E_UNSUPPORTED;
         for (const auto& im : imgs)
@@ -6135,6 +6152,7 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
             if (hipGetLastError() != hipSuccess) return LASPJ_E_DEVICE;
             for (const auto& nt : new_tpoff) d->h_tpoff[nt.first] = nt.second;
             d->tpad_used = tpad_used;
+            d->big_elems += big_add;
             return LASPJ_OK;
         }
         data.resize(dlen);
@@ -6165,6 +6183,7 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
     if (hipGetLastError() != hipSuccess) return LASPJ_E_DEVICE;
     for (const auto& nt : new_tpoff) d->h_tpoff[nt.first] = nt.second;
     d->tpad_used = tpad_used;
+    d->big_elems += big_add;
     return LASPJ_OK;
 }
 
