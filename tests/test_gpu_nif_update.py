@@ -688,3 +688,66 @@ def test_var_union_matches_oracle():
         assert g1.union(g1, g2)[0] == FALLBACK
     finally:
         ctx.close()
+
+
+def test_group_commit_wide_and_new_tokens_together():
+    """Eight threads binding through one context at once, each into its own variable, half
+    of them in a namespace widened by a hot element (host-encoded operands), every image
+    carrying tokens the namespace has not seen (another node's updates): the group commit
+    mixes wide and narrow namespaces, one-pass new tokens and two-pass registrations in
+    one batch — every answer and value is the oracle's."""
+    import threading
+    ctx = _ctx()
+    try:
+        rng = random.Random(59)
+        nthr, per = 8, 6
+        vs, cur = [], []
+        for t in range(nthr):
+            v = ctx.var("orset")
+            base = [(e, [(bytes([t, e]) + bytes(18), False)]) for e in range(200)]
+            assert v.write(_tb(base)) == OK
+            if t % 2:
+                for _ in range(70):                      # a hot element: the namespace widens
+                    verd, res, _e, minted = v.update(_tb((A("add"), 5)))
+                    assert (verd, res) == (OK, UPD_OK)
+                    base = _oracle_update(oorset, (A("add"), 5), base, minted)[1]
+            vs.append(v)
+            cur.append(base)
+        vals = [[None] * per for _ in range(nthr)]
+        for t in range(nthr):
+            c = cur[t]
+            for k in range(per):
+                c = [(e, sorted(ts + ([(bytes(rng.getrandbits(8) for _ in range(20)), False)]
+                                      if rng.random() < 0.1 else []), key=_key)) for e, ts in c]
+                if k == 3:
+                    c = sorted(c + [(1000 + t, [(bytes([9, t]) + bytes(18), True)])],
+                               key=lambda x: _key(x[0]))
+                vals[t][k] = c
+        got = [[None] * per for _ in range(nthr)]
+        errs = []
+        go = threading.Barrier(nthr)
+
+        def work(t):
+            try:
+                go.wait()
+                for k in range(per):
+                    got[t][k] = vs[t].bind(_tb(vals[t][k]))
+            except Exception as e:       # noqa: BLE001
+                errs.append(repr(e))
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert not errs, errs[:3]
+        for t in range(nthr):
+            c = cur[t]
+            for k in range(per):
+                want = 0 if exact_eq(c, vals[t][k]) else 1
+                assert got[t][k] == (OK, want), (t, k)
+                c = oorset.merge(c, vals[t][k])
+            assert vs[t].read() == (OK, _tb(c)), t
+        assert ctx.nif_stats()["namespaces_widened"] >= nthr // 2
+    finally:
+        ctx.close()
