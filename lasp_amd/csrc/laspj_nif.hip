@@ -694,7 +694,7 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     // (NewTok entries into the answer area, registered by run())
     const bool nt_merge = c.op == Op::MERGE && n == 1 && m == 2 &&
                           etf_merge_write_one(ctx, K.etf, n, E);
-    const bool nt_on = ((var_op || c.op == Op::THRESHOLD || c.op == Op::VALUE) && m == 1 ||
+    const bool nt_on = (((var_op || c.op == Op::THRESHOLD || c.op == Op::VALUE) && m == 1) ||
                         nt_merge) &&
                        G == 1 && orset && !K.wide && dec && !c.redo.n && !c.write_only &&
                        !c.no_newtok && etf_dict_bin_tokens(K.etf);
