@@ -335,8 +335,8 @@ __device__ void stage_elem_thread(const Win& w, const DictView& d, uint32_t e, u
     if (!w.hits(pos, sz)) return;
     stage_elem_header(w, d, e, (uint32_t)__popcll(p), pos);
     uint32_t q = pos + 7u + (d.elem_off[e + 1] - d.elem_off[e]);
-    const uint64_t* desc = d.tok_desc + 64u * e;
-    for (int j = 0; j < 64; ++j) {
+    const uint64_t* desc = d.tok_desc + (u64)d.tok_max * e;
+    for (uint32_t j = 0; j < d.tok_max; ++j) {
         const uint64_t ds = desc[j];
         const uint32_t k = (uint32_t)(ds & 0xFFu);
         if (k >= 64) break;
@@ -472,7 +472,8 @@ __global__ __launch_bounds__(kBlock) void k_orset_etf_write_wave(const u64x2* ce
                 const uint32_t je = s_e[j];
                 const u64 jp = s_p[j], jr = s_r[j];
                 const u64 g0 = cursor + s_pos[j];
-                const uint64_t ds = d.tok_desc[64u * je + lane];
+                const uint64_t ds = lane < d.tok_max ? d.tok_desc[(u64)d.tok_max * je + lane]
+                                                     : 0xFFull;
                 const uint32_t k = (uint32_t)(ds & 0xFFu);
                 const bool here = k < 64 && ((jp >> k) & 1ull);
                 const bool rm = here && ((jr >> k) & 1ull);
@@ -5556,13 +5557,6 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     if (epad_n >= (1ull << 32) || tpad_n >= (1ull << 32))
         return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: images exceed 4 GiB");
     std::vector<uint8_t> epad(epad_n, 0), tpad(tpad_n, 0);
-    std::vector<uint64_t> tdesc(toks ? 64ull * E : 0, 0xFFull);
-    for (uint64_t x = 0; x < tdesc.size(); ++x) {
-        const uint64_t k = tok_order[x];
-        if (k >= 64) continue;
-        const uint64_t t = (x / 64) * 64 + k, L = tok_off[t + 1] - tok_off[t];
-        tdesc[x] = k | (std::min<uint64_t>(L, 0xFFFFFFull) << 8) | ((uint64_t)tpoff[t] << 32);
-    }
     for (uint32_t e = 0; e < E; ++e)
         std::copy(elem_blob + elem_off[e], elem_blob + elem_off[e + 1], epad.begin() + epoff[e]);
     uint32_t tok_max = 0;
@@ -5574,6 +5568,17 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     if (tok_headroom && toks)
         tok_max = tok_max <= 8 ? std::min(8u, tok_max + tok_headroom)
                                : std::min(64u, tok_max + std::max(tok_headroom, tok_max / 2));
+    // the writer's descriptors by (element, term rank), tok_max per element (not 64: a
+    // rebuild then builds and uploads what the elements hold)
+    std::vector<uint64_t> tdesc(toks ? (uint64_t)tok_max * E : 0, 0xFFull);
+    for (uint64_t e = 0; toks && e < E; ++e)
+        for (uint32_t j = 0; j < tok_max; ++j) {
+            const uint64_t k = tok_order[64ull * e + j];
+            if (k >= 64) break;
+            const uint64_t t = 64ull * e + k, L = tok_off[t + 1] - tok_off[t];
+            tdesc[e * tok_max + j] =
+                k | (std::min<uint64_t>(L, 0xFFFFFFull) << 8) | ((uint64_t)tpoff[t] << 32);
+        }
     // room for token images appended by etf_dict_patch
     const uint64_t tpad_cap = tpad_n + (tok_headroom && toks ? std::max<uint64_t>(tpad_n / 4, 1ull << 16) : 0);
     // record templates (uniform token images only): 104 2 <image> per (element, term rank),
@@ -6081,9 +6086,9 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
         }
         // writer descriptors by term rank: slot | length << 8 | padded offset << 32
         u64 td[64];
-        for (uint32_t j = 0; j < 64; ++j)
+        for (uint32_t j = 0; j < RK; ++j)
             td[j] = j < cnt ? (u64)order[j] | ((u64)TL << 8) | ((u64)tpo[order[j]] << 32) : 0xFFull;
-        put(d->o_tdesc + 8ull * 64 * e, td, 8 * 64);
+        put(d->o_tdesc + 8ull * RK * e, td, 8 * RK);
         // record templates by term rank
         std::vector<uint8_t> rows((size_t)RK * RS, 0);
         for (uint32_t j = 0; j < cnt; ++j) {
