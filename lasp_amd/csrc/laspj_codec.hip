@@ -6146,10 +6146,17 @@ int etf_dict_patch(laspj_ctx* ctx, laspj_etf_dict* d, const laspj_dict* hd,
         const uint64_t dlen = total - ((rec_bytes + 15) & ~15ull);
         const void* staged = stage_small(ctx, data.data(), total);
         if (staged) {
-            if (int s = reserve_scratch(ctx, total)) return s;
-            char* dev = static_cast<char*>(ctx->scratch);
-            if (hipMemcpyAsync(dev, staged, total, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-                return LASPJ_E_DEVICE;
+            // k_patch reads the staged rows in place from pinned memory (a few KB: no copy
+            // to launch first)
+            const char* dev = static_cast<const char*>(staged_dev(ctx, staged));
+            if (!dev) {
+                if (int s = reserve_scratch(ctx, total)) return s;
+                char* sc = static_cast<char*>(ctx->scratch);
+                if (hipMemcpyAsync(sc, staged, total, hipMemcpyHostToDevice, ctx->stream) !=
+                    hipSuccess)
+                    return LASPJ_E_DEVICE;
+                dev = sc;
+            }
             hipLaunchKernelGGL(k_patch, dim3((unsigned)std::min<uint64_t>(recs.size(), 4096)),
                                dim3(kBlock), 0, ctx->stream, reinterpret_cast<const uint8_t*>(dev),
                                reinterpret_cast<const PatchRec*>(dev + dlen),

@@ -95,6 +95,7 @@ struct laspj_ctx {
     // the stream when it wraps)
     void* upring = nullptr;
     uint64_t upring_at = 0;
+    const uint8_t* upring_dev = nullptr;   // the ring's device address (kernels read it)
     static constexpr uint64_t kUpRing = 1 << 20, kUpSmall = 64 * 1024;
     static constexpr uint64_t kPinned = 64 * 1024;
     // released device blocks by size class (laspj::dev_alloc / dev_release): every kernel
@@ -180,6 +181,8 @@ hipError_t dev_alloc(laspj_ctx* ctx, uint64_t bytes, void** out);
 // src copied into the context's pinned ring for a stream-ordered host -> device copy with
 // no wait (<= 64 KiB; null: not staged).  Call with ctx->mu held.
 const void* stage_small(laspj_ctx* ctx, const void* src, uint64_t bytes);
+// the device address of a stage_small slot (kernels read staged bytes in place), or null
+const void* staged_dev(const laspj_ctx* ctx, const void* slot);
 // hipMalloc that gives the context's cached blocks back and retries once when it fails
 // (every long-lived scratch allocation goes through it)
 hipError_t dev_malloc(laspj_ctx* ctx, void** out, uint64_t bytes);

@@ -447,6 +447,12 @@ const void* stage_small(laspj_ctx* ctx, const void* src, uint64_t bytes) {
             ctx->upring = nullptr;
             return nullptr;
         }
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, ctx->upring, 0) != hipSuccess) {
+            hipGetLastError();
+            dp = nullptr;
+        }
+        ctx->upring_dev = static_cast<const uint8_t*>(dp);
     }
     const uint64_t need = (bytes + 255) & ~255ull;
     if (ctx->upring_at + need > laspj_ctx::kUpRing) {
@@ -458,6 +464,11 @@ const void* stage_small(laspj_ctx* ctx, const void* src, uint64_t bytes) {
     std::memcpy(slot, src, bytes);
     ctx->upring_at += need;
     return slot;
+}
+
+const void* staged_dev(const laspj_ctx* ctx, const void* slot) {
+    if (!ctx->upring_dev || !slot) return nullptr;
+    return ctx->upring_dev + (static_cast<const char*>(slot) - static_cast<const char*>(ctx->upring));
 }
 }  // namespace laspj
 
