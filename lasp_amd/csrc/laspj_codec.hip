@@ -5505,16 +5505,32 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
         ebyte[e] = elem_off[e + 1] - elem_off[e] == 2 && elem_blob[elem_off[e]] == 97;
     }
     uint32_t uniform = 0;
-    bool mixed = false;
+    bool mixed = false, binall = true;
+    // 16-byte-aligned copies of every image (the write kernels load them 16 B at a time);
+    // an empty token slot keeps offset ~0u (the patch's "no image" mark)
+    auto pad16 = [](uint64_t x) { return (x + 15ull) & ~15ull; };
+    std::vector<uint32_t> epoff(E), tpoff;
+    uint64_t epad_n = 0, tpad_n = 0;
     if (toks) {
-        for (uint64_t t = 0; t < 64ull * E; ++t) {
-            if (tok_off[t + 1] < tok_off[t])
-                return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: token offsets decrease");
-            uint32_t len = tok_off[t + 1] - tok_off[t];
-            if (!len) continue;
-            tmask[t / 64] |= 1ull << (t % 64);
-            if (!uniform) uniform = len;
-            else if (uniform != len) mixed = true;
+        uint32_t bad = 0;                             // (branch-free: it vectorises)
+        for (uint64_t t = 0; t < 64ull * E; ++t) bad |= tok_off[t + 1] < tok_off[t];
+        if (bad) return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: token offsets decrease");
+        tpoff.assign(64ull * E, 0xFFFFFFFFu);
+        for (uint32_t e = 0; e < E; ++e) {
+            const uint32_t* to = tok_off + 64ull * e;
+            if (to[64] == to[0]) continue;            // no tokens: the common case, one test
+            uint64_t m = 0;
+            for (uint32_t k = 0; k < 64 && to[k] != to[64]; ++k) {   // (to the last token)
+                const uint32_t len = to[k + 1] - to[k];
+                if (!len) continue;
+                m |= 1ull << k;
+                if (!uniform) uniform = len;
+                else if (uniform != len) mixed = true;
+                if (binall) binall = tok_is_binary(tok_blob + to[k], len);
+                tpoff[64ull * e + k] = (uint32_t)tpad_n;
+                tpad_n += pad16(len);
+            }
+            tmask[e] = m;
         }
         for (uint32_t e = 0; e < E; ++e) {
             uint64_t seen = 0;
@@ -5534,23 +5550,11 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     }
     uint32_t big = 0;
     for (uint32_t e = 0; e < E; ++e) big += __builtin_popcountll(tmask[e]) > 8 ? 1u : 0u;
-    bool bin = toks && !mixed && uniform >= 5u;
-    for (uint64_t t = 0; bin && t < 64ull * E; ++t) {
-        const uint32_t len = tok_off[t + 1] - tok_off[t];
-        if (len) bin = tok_is_binary(tok_blob + tok_off[t], len);
-    }
+    const bool bin = toks && !mixed && uniform >= 5u && binall;
     const uint64_t eblob = elem_off[E];
-    // 16-byte-aligned copies of every image (the write kernels load them 16 B at a time)
-    auto pad16 = [](uint64_t x) { return (x + 15ull) & ~15ull; };
-    std::vector<uint32_t> epoff(E), tpoff(toks ? 64ull * E : 0);
-    uint64_t epad_n = 0, tpad_n = 0;
     for (uint32_t e = 0; e < E; ++e) {
         epoff[e] = (uint32_t)epad_n;
         epad_n += pad16(elem_off[e + 1] - elem_off[e]);
-    }
-    for (uint64_t t = 0; t < tpoff.size(); ++t) {
-        tpoff[t] = (uint32_t)tpad_n;
-        tpad_n += pad16(tok_off[t + 1] - tok_off[t]);
     }
     epad_n += 48;                 // a 48-byte load past the last image stays inside
     tpad_n += 48;
@@ -5644,16 +5648,30 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
             bool placed = false;
             for (uint32_t wi = nwords; wi-- > 0 && !placed;) {
                 keys.resize(cnt);
-                for (uint32_t j = 0; j < cnt; ++j)
+                uint32_t diff = 0;                // the bits where some token differs
+                for (uint32_t j = 0; j < cnt; ++j) {
                     std::memcpy(&keys[j], rpad.data() + ((uint64_t)e * tok_max + j) * rec_stride +
                                                4 * wi, 4);
+                    diff |= keys[j] ^ keys[0];
+                }
+                if (cnt > 1 && !diff) continue;     // one word for all: no window parts them
                 for (uint32_t sh = 0; sh + 10 <= 32 && !placed; ++sh) {
-                    uint64_t seen[laspj::kBuckets / 64] = {};
+                    // (a window without a differing bit puts every token in one bucket)
+                    if (cnt > 1 && !((diff >> sh) & (laspj::kBuckets - 1u))) continue;
                     bool ok = true;
-                    for (uint32_t j = 0; j < cnt && ok; ++j) {
-                        const uint32_t bk = (keys[j] >> sh) & (laspj::kBuckets - 1u);
-                        ok = !((seen[bk / 64] >> (bk % 64)) & 1ull);
-                        seen[bk / 64] |= 1ull << (bk % 64);
+                    if (cnt <= 16) {
+                        for (uint32_t j = 1; j < cnt && ok; ++j) {
+                            const uint32_t bj = (keys[j] >> sh) & (laspj::kBuckets - 1u);
+                            for (uint32_t i = 0; i < j && ok; ++i)
+                                ok = ((keys[i] >> sh) & (laspj::kBuckets - 1u)) != bj;
+                        }
+                    } else {
+                        uint64_t seen[laspj::kBuckets / 64] = {};
+                        for (uint32_t j = 0; j < cnt && ok; ++j) {
+                            const uint32_t bk = (keys[j] >> sh) & (laspj::kBuckets - 1u);
+                            ok = !((seen[bk / 64] >> (bk % 64)) & 1ull);
+                            seen[bk / 64] |= 1ull << (bk % 64);
+                        }
                     }
                     if (!ok) continue;
                     placed = true;
@@ -5696,8 +5714,11 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
             hlens |= 1ull << (hl - 1);
         }
     }
-    for (uint64_t t = 0; t < tpoff.size(); ++t)
-        std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
+    for (uint64_t e = 0; toks && e < E; ++e)
+        for (uint64_t m = tmask[e]; m; m &= m - 1) {          // the slots holding a token
+            const uint64_t t = 64ull * e + __builtin_ctzll(m);
+            std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
+        }
     uint64_t gs_cap = 64;
     while (gs_cap < 2ull * E) gs_cap <<= 1;
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
@@ -5914,9 +5935,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
         d->patchable = true;
         d->h_rank.assign(E, 0);
         for (uint32_t r = 0; r < E; ++r) d->h_rank[elem_order[r]] = r;
-        d->h_tpoff.assign(64ull * E, 0xFFFFFFFFu);
-        for (uint64_t t = 0; t < 64ull * E; ++t)
-            if (tok_off[t + 1] > tok_off[t]) d->h_tpoff[t] = tpoff[t];
+        d->h_tpoff = std::move(tpoff);         // (~0u marks the empty slots already)
         d->o_mask = o_mask;
         d->o_tord = o_tord;
         d->o_tpad = o_tpad;

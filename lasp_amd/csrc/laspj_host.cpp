@@ -965,14 +965,17 @@ int laspj_dict_export(const laspj_dict* dict, uint32_t E, uint8_t* elem_blob, ui
             uint64_t to = 0;
             tok_off[0] = 0;
             for (uint32_t e = 0; e < E; ++e) {
-                for (uint32_t k = 0; k < 64; ++k) {
-                    if (e < K && k < d.toks[e].size()) {
-                        if (tok_blob) memcpy(tok_blob + to, d.toks[e][k].data(), d.toks[e][k].size());
-                        to += d.toks[e][k].size();
-                    }
+                // the element's tokens, then its empty slots at the running offset
+                uint32_t* te = tok_off + 64ull * e + 1;
+                const uint32_t cnt = e < K ? (uint32_t)std::min<size_t>(d.toks[e].size(), 64) : 0u;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const std::string_view t = d.toks[e][k];
+                    if (tok_blob) memcpy(tok_blob + to, t.data(), t.size());
+                    to += t.size();
                     if (to > 0xFFFFFFFFull) return LASPJ_E_RANGE;
-                    tok_off[64ull * e + k + 1] = (uint32_t)to;
+                    te[k] = (uint32_t)to;
                 }
+                std::fill(te + cnt, te + 64, (uint32_t)to);
                 if (tok_order) {
                     uint8_t* o = tok_order + 64ull * e;
                     memset(o, 0xFF, 64);

@@ -507,19 +507,23 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
     uint32_t E = K.E;
     if (!K.etf || n > E) E = n + n / 4 + 64;
     const bool toks = K.kind == LASPJ_KIND_ORSET;
-    std::vector<uint8_t> ebl(eb + 1), tbl(toks ? tb + 1 : 0), tord(toks ? 64ull * E : 0);
-    std::vector<uint32_t> eoff(E + 1ull), eord(E), toff(toks ? 64ull * E + 1 : 0);
-    if (laspj_dict_export(K.dict, E, ebl.data(), eoff.data(), eord.data(),
-                          toks ? tbl.data() : nullptr, toks ? toff.data() : nullptr,
-                          toks ? tord.data() : nullptr) != LASPJ_OK)
+    // (uninitialised: the export writes every entry, and zeroing 64 token slots per
+    // element cost as much as the export itself)
+    std::unique_ptr<uint8_t[]> ebl(new uint8_t[eb + 1]), tbl(new uint8_t[toks ? tb + 1 : 1]),
+        tord(new uint8_t[toks ? 64ull * E : 1]);
+    std::unique_ptr<uint32_t[]> eoff(new uint32_t[E + 1ull]), eord(new uint32_t[E]),
+        toff(new uint32_t[toks ? 64ull * E + 1 : 1]);
+    if (laspj_dict_export(K.dict, E, ebl.get(), eoff.get(), eord.get(),
+                          toks ? tbl.get() : nullptr, toks ? toff.get() : nullptr,
+                          toks ? tord.get() : nullptr) != LASPJ_OK)
         return fail(ctx, LASPJ_E_INVAL, "nif: dictionary export");
     free_etf(K);
     laspj_etf_dict* d = nullptr;
     // OR-Sets: two tokens of headroom per element, so a call that only adds tokens to
     // known elements patches the images (patch_etf) instead of coming back here
-    if (int s = toks ? etf_dict_create_ex(ctx, E, ebl.data(), eoff.data(), eord.data(),
-                                          tbl.data(), toff.data(), tord.data(), 2, &d)
-                     : laspj_etf_dict_create(ctx, E, ebl.data(), eoff.data(), eord.data(),
+    if (int s = toks ? etf_dict_create_ex(ctx, E, ebl.get(), eoff.get(), eord.get(),
+                                          tbl.get(), toff.get(), tord.get(), 2, &d)
+                     : laspj_etf_dict_create(ctx, E, ebl.get(), eoff.get(), eord.get(),
                                              nullptr, nullptr, nullptr, &d))
         return s;
     K.etf = d;

@@ -42,7 +42,9 @@ def main():
     far.write(img0)
     st = C.c_int32()
     for k in range(12):
-        op = oetf.term_to_binary((Atom("add"), 97 * k))
+        # (LASPJ_PROBE_NEW=1: each update adds a new element — the rebuild path)
+        el_ = n + k if os.environ.get("LASPJ_PROBE_NEW") == "1" else 97 * k
+        op = oetf.term_to_binary((Atom("add"), el_))
         s0 = stats()
         t0 = time.perf_counter()
         check(L.laspj_var_etf_update(uv.h, op, len(op), C.byref(res), C.byref(ei), C.byref(el),
