@@ -4857,6 +4857,25 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
     __shared__ int32_t s_st;
     __shared__ bool s_last;
     const uint32_t i = blockIdx.x / nch, ch = blockIdx.x % nch;
+    // (variables of different namespaces have different widths: the blocks past a
+    // narrower one's words only take part in the ticket)
+    u64* cur = curs[i];
+    u64* src = ins[i];
+    const uint64_t wpr = wprs[i];
+    const uint64_t w0 = (uint64_t)ch * kVarWords;
+    // both operands' words loaded first: they do not depend on the verdict, so their
+    // loads overlap its dependent chain of loads (wave 0's)
+    constexpr uint32_t kPer = kVarWords / kBlock;
+    u64 av[kPer], bv[kPer];
+#pragma unroll
+    for (uint32_t t = 0; t < kPer; ++t) {
+        const uint64_t w = w0 + threadIdx.x + t * kBlock;
+        av[t] = bv[t] = 0;
+        if (w < wpr) {
+            bv[t] = src[w];
+            av[t] = cur[w];
+        }
+    }
     if (cj.status) {
         if (threadIdx.x < 64) {
             const u64 base = cj.offs[i];
@@ -4874,26 +4893,18 @@ __global__ __launch_bounds__(kBlock) void k_var_bind(u64* const* __restrict__ cu
     }
     __syncthreads();
     const bool ok = s_st == LASPJ_DEC_OK;
-    // (variables of different namespaces have different widths: the blocks past a
-    // narrower one's words only take part in the ticket)
-    u64* cur = curs[i];
-    u64* src = ins[i];
-    const uint64_t wpr = wprs[i];
     u64 d = 0;
-    const uint64_t w0 = (uint64_t)ch * kVarWords;
-    for (uint32_t k = threadIdx.x; k < kVarWords; k += kBlock) {
-        const uint64_t w = w0 + k;
-        if (w >= wpr) break;
-        const u64 b = src[w];
-        if (ok) {
-            const u64 a = cur[w];
-            d |= a ^ b;
-            const u64 v = WRITE ? b : (a | b);
-            if (v != a) cur[w] = v;
-        }
+#pragma unroll
+    for (uint32_t t = 0; t < kPer; ++t) {
+        const uint64_t w = w0 + threadIdx.x + t * kBlock;
+        if (w >= wpr || !ok) continue;
         // (an operand that did not decode keeps its cells: a redo pass of its failed
         // segments completes them, laspj_nif.hip)
-        if (b && ok) src[w] = 0;
+        const u64 a = av[t], b = bv[t];
+        d |= a ^ b;
+        const u64 v = WRITE ? b : (a | b);
+        if (v != a) cur[w] = v;
+        if (b) src[w] = 0;
     }
     const bool any = __syncthreads_or(d != 0);
     if (threadIdx.x == 0) {
