@@ -452,6 +452,8 @@ int laspj_gcounter_reduce(laspj_ctx* ctx, laspj_batch* dst, const laspj_batch* s
  * which the host encodes once per distinct term:
  *   elem_blob[elem_off[e] .. elem_off[e+1])         element slot e   (empty: unused)
  *   elem_order[0 .. E)                              element slots in Erlang term order
+ *                                                   (a permutation of 0 .. E-1, else
+ *                                                   LASPJ_E_RANGE)
  *   tok_blob[tok_off[64e+k] .. tok_off[64e+k+1])    token slot k of element e (empty: unused)
  *   tok_order[64e + j], j < 64                      token slots of e in term order,
  *                                                   0xFF after the last used one

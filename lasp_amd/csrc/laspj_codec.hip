@@ -5510,10 +5510,13 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     // host-side validation and derived arrays
     std::vector<uint8_t> ebyte(E, 0);
     std::vector<uint64_t> tmask(E, 0);
-    for (uint32_t e = 0; e < E; ++e) {
-        if (elem_off[e + 1] < elem_off[e] || elem_order[e] >= E)
-            return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: element offsets / order invalid");
-        ebyte[e] = elem_off[e + 1] - elem_off[e] == 2 && elem_blob[elem_off[e]] == 97;
+    {
+        std::vector<uint8_t> ranked(E, 0);            // (the order must be a permutation)
+        for (uint32_t e = 0; e < E; ++e) {
+            if (elem_off[e + 1] < elem_off[e] || elem_order[e] >= E || ranked[elem_order[e]]++)
+                return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: element offsets / order invalid");
+            ebyte[e] = elem_off[e + 1] - elem_off[e] == 2 && elem_blob[elem_off[e]] == 97;
+        }
     }
     uint32_t uniform = 0;
     bool mixed = false, binall = true;
@@ -5644,8 +5647,11 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
         std::memset(ros, 0xFF, 64ull * E);
         const uint32_t nwords = rec_len / 4;     // whole words of the template
         std::vector<uint32_t> keys;
-        for (uint64_t r = 0; r < E && hashed; ++r) {
-            const uint32_t e = elem_order[r];
+        // (by slot, each slot's rank looked up: the slot-indexed sources read in order)
+        std::vector<uint32_t> rank_of(E);
+        for (uint32_t r = 0; r < E; ++r) rank_of[elem_order[r]] = r;
+        for (uint32_t e = 0; e < E && hashed; ++e) {
+            const uint64_t r = rank_of[e];
             const uint32_t hl = elem_off[e + 1] - elem_off[e] + 3u;
             uint32_t cnt = 0;
             while (cnt < tok_max && tok_order[64ull * e + cnt] < 64) ++cnt;
