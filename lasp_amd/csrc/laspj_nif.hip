@@ -43,6 +43,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
@@ -105,11 +106,22 @@ struct laspj_var {
 
 namespace laspj {
 
+// a pinned host block a group-commit waiter stages its payload into while it waits
+struct PinSlot {
+    uint8_t* h = nullptr;           // host address
+    const uint8_t* d = nullptr;     // its device address
+    uint64_t cap = 0;
+};
+
 // a single bind waiting for a group-commit pass (laspj_var_etf_bind)
 struct BindReq {
     laspj_var* var;
     const uint8_t* p;
     uint64_t n;
+    // the payload's pinned copy (device address), valid once `staged` is set: made by the
+    // waiter itself, so the leader's pass gathers it on the device instead of copying it
+    const uint8_t* pre = nullptr;
+    std::atomic<bool> staged{false};
     int32_t status = 0, verdict = LASPJ_NIF_FALLBACK;
     int rc = LASPJ_OK;
     // its own wake-up (no herd of waiters on one condition and one lock): done — answered;
@@ -125,6 +137,8 @@ struct NifState {
     std::mutex qmu;
     std::vector<BindReq*> queue;
     bool leading = false;
+    std::vector<PinSlot> pins;      // free waiters' staging blocks (qmu)
+    uint32_t pins_live = 0;         // blocks allocated (qmu)
     KindState ks[2];                // the image calls' dictionaries: [0] OR-Set, [1] G-Set
     // device: [in region: offsets | segment table | zeroed words | variable cell pointers
     // | payloads or cells][segment results][variable calls' statuses]; cells: the batches
@@ -180,6 +194,71 @@ __global__ void __launch_bounds__(256) k_nif_pull(const pull16* __restrict__ src
         for (int k = 0; k < 4; ++k) {
             const uint64_t i = c * 256 + k * 64 + lane;
             if (i < n16) dst[i] = v[k];
+        }
+    }
+}
+
+// Payloads gathered into the in region at their (byte) offsets from pinned blocks: those
+// group-commit waiters staged themselves, and the leader's own (copied into the staging
+// at its offset).  8-byte lanes, four loads in flight per lane (2 KiB per wave step), a
+// dst word composed of two source words (the neighbour lane's) when source and
+// destination differ in alignment, partial words at a payload's ends written byte by
+// byte (a neighbouring payload owns their other bytes).  blockIdx.y: the payload.
+struct GatherDesc {
+    const uint8_t* src;             // any alignment; readable 16 bytes past len
+    uint64_t dst, len;              // offset in the region, bytes
+};
+constexpr uint32_t kGatherMax = 16;
+constexpr uint32_t kGatherU = 4;
+struct GatherArgs {
+    GatherDesc d[kGatherMax];
+};
+__global__ void __launch_bounds__(256) k_nif_gather(GatherArgs g, uint8_t* __restrict__ dst) {
+    const GatherDesc ds = g.d[blockIdx.y];
+    const uint64_t d0 = ds.dst, d1 = ds.dst + ds.len;
+    if (d1 == d0) return;
+    const uint64_t w0 = d0 & ~7ull;
+    const uint32_t sh = (uint32_t)(d0 - w0);
+    const uint64_t nw = (d1 - w0 + 7) / 8;             // dst words touched
+    const uint64_t sa = reinterpret_cast<uint64_t>(ds.src);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(sa & ~7ull);
+    // dst byte w0 + 8j + b is source word j's byte b + delta (of the aligned source)
+    const int32_t delta = (int32_t)(sa & 7ull) - (int32_t)sh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwv = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t c = wave * 64 * kGatherU; c < nw; c += nwv * 64 * kGatherU) {
+        uint64_t cur[kGatherU], edge[kGatherU];
+#pragma unroll
+        for (uint32_t u = 0; u < kGatherU; ++u) {
+            const uint64_t j = c + 64 * u + lane;
+            cur[u] = j < nw ? __builtin_nontemporal_load(src + j) : 0ull;
+            // the one neighbour word no lane of this group loads
+            edge[u] = 0;
+            if (j < nw && delta < 0 && lane == 0 && j > 0) edge[u] = __builtin_nontemporal_load(src + j - 1);
+            if (j < nw && delta > 0 && (lane == 63 || j + 1 == nw))
+                edge[u] = __builtin_nontemporal_load(src + j + 1);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kGatherU; ++u) {
+            const uint64_t up = __shfl_up(cur[u], 1, 64), dn = __shfl_down(cur[u], 1, 64);
+            const uint64_t j = c + 64 * u + lane;
+            if (j >= nw) continue;
+            const uint64_t w = w0 + 8 * j;
+            if (w >= d0 && w + 8 <= d1) {
+                uint64_t v = cur[u];
+                if (delta < 0) {
+                    const uint64_t pv = lane ? up : edge[u];
+                    v = (pv >> (8 * (8 + delta))) | (cur[u] << (8 * -delta));
+                } else if (delta > 0) {
+                    const uint64_t nx = (lane == 63 || j + 1 == nw) ? edge[u] : dn;
+                    v = (cur[u] >> (8 * delta)) | (nx << (8 * (8 - delta)));
+                }
+                *reinterpret_cast<uint64_t*>(dst + w) = v;
+            } else {
+                for (uint32_t b = 0; b < 8; ++b)
+                    if (w + b >= d0 && w + b < d1) dst[w + b] = ds.src[w + b - d0];
+            }
         }
     }
 }
@@ -307,6 +386,30 @@ constexpr uint32_t kMaxDictElements = 1u << 20;   // a larger dictionary is rese
 constexpr uint32_t kWideTokens = 1024, kWideTokenLen = 46;
 // passes a group-commit leader runs back to back while binds keep queueing
 constexpr int kLeadRounds = 8;
+// waiters' staging blocks: payloads of at least kPinMin bytes, at most kPinSlots blocks
+constexpr uint64_t kPinMin = 64ull << 10;
+constexpr uint32_t kPinSlots = 64;
+
+// a waiter's pinned block grown to `need` bytes (false: no pinned memory; the leader then
+// copies that payload itself)
+bool pin_grow(PinSlot* s, uint64_t need) {
+    if (s->h) hipHostFree(s->h);
+    *s = PinSlot{};
+    const uint64_t cap = std::max<uint64_t>((need + (1ull << 20) - 1) & ~((1ull << 20) - 1), 1ull << 20);
+    void* h = nullptr;
+    if (hipHostMalloc(&h, cap, hipHostMallocCoherent) != hipSuccess) {
+        hipGetLastError();
+        return false;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        hipGetLastError();
+        hipHostFree(h);
+        return false;
+    }
+    *s = PinSlot{static_cast<uint8_t*>(h), static_cast<const uint8_t*>(d), cap};
+    return true;
+}
 // new tokens a single bind's decoder may take (NewTok entries; more: the two-pass path)
 constexpr uint32_t kNewTokCap = 512;
 // device passes per call: registration, a grown answer area and a serial re-decode each
@@ -343,6 +446,7 @@ struct Call {
     std::vector<Group> groups;      // >= 1; single-group ops (all but BIND / WRITE) use [0]
     std::vector<const uint8_t*> p;  // m payloads: MERGE / EQUAL / INFLATION: lhs[0..n) then rhs
     std::vector<uint64_t> len;
+    std::vector<const uint8_t*> pre;   // (binds) a payload's pinned copy on the device, or null
     std::vector<laspj_var*> vars;   // variable calls: n variables (payload i -> variable i)
     std::vector<int32_t> st;        // m decode statuses
     std::vector<uint8_t> res;       // n answer bytes (EQUAL / INFLATION / BIND / THRESHOLD)
@@ -742,6 +846,37 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
     }
     uint8_t* hin = static_cast<uint8_t*>(S->hin);
     uint8_t* din = static_cast<uint8_t*>(S->dblk);
+    // a group commit's waiters staged their payloads into pinned blocks of their own while
+    // they waited: gathered to their offsets by the device (k_nif_gather), launched before
+    // the host builds the rest of the pass
+    const bool gathered = dec && !c.redo.n && !c.write_only &&
+                          std::any_of(c.pre.begin(), c.pre.end(),
+                                      [](const uint8_t* x) { return x != nullptr; });
+    GatherArgs ga{};
+    uint32_t ng = 0;
+    uint64_t most = 0;
+    auto gather = [&]() -> int {
+        if (!ng) return LASPJ_OK;
+        // (one wave step of 2 KiB per wave, 8 KiB per block)
+        const uint64_t blocks = std::min<uint64_t>((most + 8191) / 8192, (uint64_t)ctx->cus);
+        hipLaunchKernelGGL(k_nif_gather, dim3((unsigned)std::max<uint64_t>(blocks, 1), ng),
+                           dim3(256), 0, ctx->stream, ga, din + i_pay);
+        LJ_LAUNCHED(ctx);
+        ng = 0;
+        most = 0;
+        return LASPJ_OK;
+    };
+    if (gathered) {
+        Guard g(ctx);
+        for (uint32_t i = 0; i < m; ++i) {
+            if (!c.len[i] || !c.pre[i]) continue;
+            ga.d[ng++] = GatherDesc{c.pre[i], hoffs[i], c.len[i]};
+            most = std::max(most, c.len[i]);
+            if (ng == kGatherMax)
+                if (int s = gather()) return s;
+        }
+        if (int s = gather()) return s;
+    }
     uint8_t* dseg = din + al(in_bytes, 256);          // deferred segment results
     int32_t* dvst = reinterpret_cast<int32_t*>(dseg + seg_bytes);   // variable calls' statuses
     uint8_t* rout = S->hout_d;                        // where kernels write the out region
@@ -821,6 +956,22 @@ int device_pass(laspj_ctx* ctx, NifState* S, Call& c) {
         if (dec && (c.redo.n || c.write_only)) {
             // (a redo or write-only pass: the head and payloads the last pass pulled are
             // still there)
+        } else if (gathered) {
+            // the head, then the payloads not staged by their callers (the leader's own)
+            // copied into the staging and gathered to their offsets (the staged ones are
+            // on their way since the region was allocated)
+            if (int s = send(i_pay)) return s;
+            for (uint32_t i = 0; i < m; ++i) {
+                if (!c.len[i] || c.pre[i]) continue;
+                const uint64_t tc = now_ns();
+                std::memcpy(hin + i_pay + hoffs[i], c.p[i], c.len[i]);
+                t_copy += now_ns() - tc;
+                ga.d[ng++] = GatherDesc{hin_d + i_pay + hoffs[i], hoffs[i], c.len[i]};
+                most = std::max(most, c.len[i]);
+                if (ng == kGatherMax)
+                    if (int s = gather()) return s;
+            }
+            if (int s = gather()) return s;
         } else if (dec) {
             uint64_t at = 0;
             uint32_t i = 0;
@@ -1614,6 +1765,7 @@ void nif_destroy(laspj_ctx* ctx) {
     if (S->dcells) hipFree(S->dcells);
     if (S->hin) hipHostFree(S->hin);
     if (S->hout) hipHostFree(S->hout);
+    for (const PinSlot& p : S->pins) hipHostFree(p.h);
     delete S;
     ctx->nif = nullptr;
 }
@@ -1866,7 +2018,7 @@ bool strong_rand(uint8_t* p, size_t n) {
 // bind_many with S->mu held (laspj_var_etf_bind_many's body)
 int bind_many_locked(laspj_ctx* ctx, laspj::NifState* S, uint32_t n, laspj_var* const* vars,
                      const uint8_t* const* values, const uint64_t* lens, int32_t* status,
-                     int32_t* verdict) {
+                     int32_t* verdict, const uint8_t* const* pre = nullptr) {
     const int32_t kind = vars[0] ? vars[0]->kind : 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (!vars[i] || vars[i]->ctx != ctx || !S->vars.count(vars[i]))
@@ -1905,6 +2057,7 @@ int bind_many_locked(laspj_ctx* ctx, laspj::NifState* S, uint32_t n, laspj_var* 
         const uint32_t i = live[k];
         c.p.push_back(values[i]);
         c.len.push_back(lens[i]);
+        c.pre.push_back(pre ? pre[i] : nullptr);
         c.vars.push_back(vars[i]);
         if (k == 0 || vars[live[k - 1]]->ns != vars[i]->ns)
             c.groups.push_back(laspj::Group{vars[i]->ns.get(), k, k + 1});
@@ -1946,16 +2099,18 @@ void serve_binds(laspj_ctx* ctx, NifState* S, std::vector<BindReq*>& batch) {
             (r->var->kind == kind && seen.insert(r->var).second ? now : later).push_back(r);
         const uint32_t k = (uint32_t)now.size();
         std::vector<laspj_var*> vs(k);
-        std::vector<const uint8_t*> ps(k);
+        std::vector<const uint8_t*> ps(k), pre(k);
         std::vector<uint64_t> ls(k);
         std::vector<int32_t> st(k, 0), vd(k, LASPJ_NIF_FALLBACK);
         for (uint32_t i = 0; i < k; ++i) {
             vs[i] = now[i]->var;
             ps[i] = now[i]->p;
             ls[i] = now[i]->n;
+            // (a waiter still copying: the leader copies the payload itself)
+            pre[i] = now[i]->staged.load(std::memory_order_acquire) ? now[i]->pre : nullptr;
         }
         const int rc = bind_many_locked(ctx, S, k, vs.data(), ps.data(), ls.data(), st.data(),
-                                        vd.data());
+                                        vd.data(), pre.data());
         for (uint32_t i = 0; i < k; ++i) {
             now[i]->rc = rc;
             now[i]->status = rc ? 0 : st[i];
@@ -2044,19 +2199,53 @@ int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t
     r.var = var;
     r.p = value;
     r.n = n;
+    laspj::PinSlot slot;
+    bool want_slot = false;
     {
         std::lock_guard<std::mutex> q(S->qmu);
         if (S->leading) {
             S->queue.push_back(&r);
+            // a waiter stages its own payload into a pinned block while the pass before
+            // it runs (the leader then only gathers it on the device)
+            if (n >= laspj::kPinMin) {
+                if (!S->pins.empty()) {
+                    slot = S->pins.back();
+                    S->pins.pop_back();
+                    want_slot = true;
+                } else if (S->pins_live < laspj::kPinSlots) {
+                    ++S->pins_live;
+                    want_slot = true;
+                }
+            }
         } else {
             S->leading = true;
             r.lead = true;
         }
     }
+    if (want_slot) {
+        if (slot.cap < n + 16 && !laspj::pin_grow(&slot, n + 16)) {
+            std::lock_guard<std::mutex> q(S->qmu);
+            --S->pins_live;
+            want_slot = false;
+        }
+        if (want_slot) {
+            std::memcpy(slot.h, value, n);
+            r.pre = slot.d;
+            r.staged.store(true, std::memory_order_release);
+        }
+    }
+    // (the block back to the pool once the pass that read it has answered)
+    auto give_back = [&]() {
+        if (!want_slot) return;
+        std::lock_guard<std::mutex> q(S->qmu);
+        S->pins.push_back(slot);
+    };
     if (!r.lead) {
         std::unique_lock<std::mutex> lk(r.m);
         r.cv.wait(lk, [&] { return r.done || r.lead; });
         if (r.done) {
+            lk.unlock();
+            give_back();
             *status = r.status;
             *verdict = r.verdict;
             return r.rc;
@@ -2100,6 +2289,7 @@ int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t
             nx->cv.notify_one();
         }
     }
+    give_back();
     *status = r.status;
     *verdict = r.verdict;
     return r.rc;

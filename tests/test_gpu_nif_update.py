@@ -376,6 +376,53 @@ def test_group_commit_binds_from_many_threads():
         ctx.close()
 
 
+def test_group_commit_waiters_stage_large_payloads():
+    """Group commit with payloads past the waiters' staging threshold (64 KiB): the waiting
+    threads copy their own payloads into pinned blocks and the leader's pass gathers them
+    on the device at byte offsets of every alignment (payload lengths vary by a few bytes)
+    — every answer and every value is the oracle's."""
+    import threading
+    ctx = _ctx()
+    try:
+        rng = random.Random(47)
+        elems = list(range(6000))
+        nthr, per = 8, 6
+        vs = [ctx.var("orset") for _ in range(nthr)]
+        # token images of one length (the device decoder's), element counts varied so the
+        # images' lengths (and so the gather's byte offsets) fall on every residue mod 16
+        vals = [[[(e, [(bytes([t, k]) + e.to_bytes(4, "big") + bytes(14), (e + k) % 3 == 0)])
+                  for e in sorted(rng.sample(elems, 2200 + 7 * t + k))] for k in range(per)]
+                for t in range(nthr)]
+        assert all(len(_tb(v)) >= 64 << 10 for row in vals for v in row)
+        got = [[None] * per for _ in range(nthr)]
+        errs = []
+        go = threading.Barrier(nthr)
+
+        def work(t):
+            try:
+                go.wait()
+                for k in range(per):
+                    got[t][k] = vs[t].bind(_tb(vals[t][k]))
+            except Exception as e:       # noqa: BLE001
+                errs.append(repr(e))
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert not errs, errs[:3]
+        for t in range(nthr):
+            cur = []
+            for k in range(per):
+                want_st = 0 if exact_eq(cur, vals[t][k]) else 1
+                assert got[t][k] == (OK, want_st), (t, k)
+                cur = oorset.merge(cur, vals[t][k])
+            assert vs[t].read() == (OK, _tb(cur)), t
+    finally:
+        ctx.close()
+
+
 def test_bind_many_fresh_namespaces():
     """One bind_many over sixteen fresh variables (sixteen namespaces with no dictionary
     yet, registered in the call, decoded in one launch), then again with new tokens and
