@@ -490,8 +490,8 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     # update/4 on the resident variable (laspj_var_etf_update, lasp_core.erl:283-287): {add, E}
     # of a known element mints a token (unique/1), registers it in the variable's namespace,
     # patches the device images and sets the token's bit — the update ships only the op
-    from oracle import etf as oetf             # (the op images are built untimed)
-    from oracle.terms import Atom
+    from lasp_amd import etf as oetf           # (the op images are built untimed)
+    from lasp_amd.terms import Atom
     res, vd2, nmint = C.c_int32(), C.c_int32(), C.c_uint32()
     eimg, elen, mint = C.c_void_p(), C.c_uint64(), C.c_void_p()
     uv = ctx.var("orset")
@@ -557,6 +557,24 @@ def config1_resident(ctx, pa: bytes, pb: bytes, ref: bytes):
     out["bind_new_token_passes"] = (sc1["device_passes"] - sc0["device_passes"]) / 10
     for v in (rep, far, uv):
         v.close()
+    # update/4 adding an element the namespace has never held: a new dictionary term, so
+    # the namespace's device images are rebuilt (the rank-indexed tables)
+    nv = ctx.var("orset")
+    if nv.write(pa) != 0:
+        raise RuntimeError("config1: write answered wrongly")
+    times_ne = []
+    for k in range(9):
+        op = oetf.term_to_binary((Atom("add"), 1_000_000 + k))
+        t0 = time.perf_counter()
+        check(L.laspj_var_etf_update(nv.h, op, len(op), C.byref(res), C.byref(eimg),
+                                     C.byref(elen), C.byref(mint), C.byref(nmint), C.byref(vd2)),
+              ctx.h)
+        ctx.synchronize()
+        times_ne.append((time.perf_counter() - t0) * 1e6)
+        if vd2.value != 0 or res.value != 0:
+            raise RuntimeError("config1: update/4 of a new element answered wrongly")
+    out["us_update_nif_new_element"] = sorted(times_ne)[len(times_ne) // 2]
+    nv.close()
     # lasp_core:union/7's body re-run over resident variables of one namespace
     # (laspj_var_union): l = A, r = B, out := merge(out, keep-left(l, r)) — nothing crosses
     # PCIe but the status (the image route: var_read of both, the body, var_bind)
@@ -691,8 +709,8 @@ def steady_leg(ctx, nvars: int = 32, steps: int = 200):
     import numpy as np
     from lasp_amd._lib import check
     from lasp_amd import engine, etf
-    from oracle import etf as oetf              # op images, built untimed
-    from oracle.terms import Atom
+    from lasp_amd import etf as oetf            # op images, built untimed
+    from lasp_amd.terms import Atom
     L = ctx.L
     n = 10_000
     nodes = [ctx, engine.Context(ctx.device)]
