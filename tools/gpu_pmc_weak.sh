@@ -16,5 +16,5 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 240 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/weak_pmc$i -o run -- \
       $CMD > gpurun_out/weak_pmc$i.log 2>&1 || exit $?
 done
-python3 tools/pmc_weak_table.py gpurun_out > gpurun_out/weak_table.txt
+python3 tools/pmc_bind_table.py gpurun_out weak_pmc > gpurun_out/weak_table.txt
 cat gpurun_out/weak_table.txt
