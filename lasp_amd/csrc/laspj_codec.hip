@@ -5499,7 +5499,10 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
                                 const uint32_t* elem_off, const uint32_t* elem_order,
                                 const uint8_t* tok_blob, const uint32_t* tok_off,
                                 const uint8_t* tok_order, uint32_t tok_headroom,
-                                laspj_etf_dict** out) {
+                                laspj_etf_dict** out, bool trusted = false) {
+    // (trusted: arrays the library exported itself from its host dictionary, where offsets
+    // ascend, the order is a permutation and token orders name exactly the used slots by
+    // construction — those checks, passes over every slot, are left out)
     if (!ctx || !out || !elem_off || !elem_order || (!elem_blob && elem_off[E]))
         return fail(ctx, LASPJ_E_INVAL, "etf_dict_create: null argument");
     *out = nullptr;
@@ -5511,9 +5514,10 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     std::vector<uint8_t> ebyte(E, 0);
     std::vector<uint64_t> tmask(E, 0);
     {
-        std::vector<uint8_t> ranked(E, 0);            // (the order must be a permutation)
+        std::vector<uint8_t> ranked(trusted ? 0 : E, 0);    // (the order must be a permutation)
         for (uint32_t e = 0; e < E; ++e) {
-            if (elem_off[e + 1] < elem_off[e] || elem_order[e] >= E || ranked[elem_order[e]]++)
+            if (!trusted &&
+                (elem_off[e + 1] < elem_off[e] || elem_order[e] >= E || ranked[elem_order[e]]++))
                 return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: element offsets / order invalid");
             ebyte[e] = elem_off[e + 1] - elem_off[e] == 2 && elem_blob[elem_off[e]] == 97;
         }
@@ -5527,7 +5531,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     uint64_t epad_n = 0, tpad_n = 0;
     if (toks) {
         uint32_t bad = 0;                             // (branch-free: it vectorises)
-        for (uint64_t t = 0; t < 64ull * E; ++t) bad |= tok_off[t + 1] < tok_off[t];
+        for (uint64_t t = 0; !trusted && t < 64ull * E; ++t) bad |= tok_off[t + 1] < tok_off[t];
         if (bad) return fail(ctx, LASPJ_E_RANGE, "etf_dict_create: token offsets decrease");
         tpoff.assign(64ull * E, 0xFFFFFFFFu);
         for (uint32_t e = 0; e < E; ++e) {
@@ -5546,7 +5550,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
             }
             tmask[e] = m;
         }
-        for (uint32_t e = 0; e < E; ++e) {
+        for (uint32_t e = 0; e < E && !trusted; ++e) {
             uint64_t seen = 0;
             for (int j = 0; j < 64; ++j) {
                 uint8_t k = tok_order[64ull * e + j];
@@ -6049,7 +6053,7 @@ int etf_dict_create_ex(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                        const uint8_t* tok_blob, const uint32_t* tok_off, const uint8_t* tok_order,
                        uint32_t tok_headroom, laspj_etf_dict** out) {
     return etf_dict_create_body(ctx, E, elem_blob, elem_off, elem_order, tok_blob, tok_off,
-                                tok_order, tok_headroom, out);
+                                tok_order, tok_headroom, out, true);
 }
 
 // The device rows of element slots `dirty` (each gained tokens in the host dictionary `hd`

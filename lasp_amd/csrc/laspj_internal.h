@@ -438,7 +438,8 @@ int etf_value_write_enqueue(laspj_ctx* ctx, const laspj_batch* cells, const lasp
                             const ChainJob* chain = nullptr);
 
 // laspj_etf_dict_create with per-element token headroom (up to tok_headroom more tokens
-// per element than the widest has) and the host state etf_dict_patch needs
+// per element than the widest has) and the host state etf_dict_patch needs, over arrays
+// laspj_dict_export wrote (consistent by construction: the per-slot checks are skipped)
 int etf_dict_create_ex(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_blob,
                        const uint32_t* elem_off, const uint32_t* elem_order,
                        const uint8_t* tok_blob, const uint32_t* tok_off, const uint8_t* tok_order,
