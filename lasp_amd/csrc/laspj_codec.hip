@@ -4805,6 +4805,8 @@ int gset_etf_read(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, int t
                         (unsigned long long)i);
     if (off[R] > payload->bytes)
         return fail(ctx, LASPJ_E_RANGE, "%s: offsets run past the payload buffer", what);
+    if (!d->gs_htab)
+        return fail(ctx, LASPJ_E_UNSUPPORTED, "gset read: a dictionary built without G-Set tables");
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
     const uint64_t cap = (uint64_t)ctx->cus * 64;
@@ -5178,6 +5180,8 @@ int gset_read_enqueue(laspj_ctx* ctx, laspj_batch* b, const laspj_etf_dict* d, i
                       const uint8_t* payload, const u64* offs, int32_t* status, bool clear,
                       const u64* hoffs) {
     const uint64_t R = b->replicas;
+    if (!d->gs_htab)
+        return fail(ctx, LASPJ_E_UNSUPPORTED, "gset read: a dictionary built without G-Set tables");
     const GsTabs tabs{d->elem_blob, d->elem_off, d->gs_htab, d->gs_hmask, d->gs_rank, d->gs_byte,
                       d->elements, reinterpret_cast<const u64*>(d->gs_itab), d->gs_ilo, d->gs_in};
     if (hoffs && gset_read_split(ctx, R, hoffs)) {
@@ -5740,12 +5744,15 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
             const uint64_t t = 64ull * e + __builtin_ctzll(m);
             std::copy(tok_blob + tok_off[t], tok_blob + tok_off[t + 1], tpad.begin() + tpoff[t]);
         }
+    // G-Set from_binary tables: ranks (equal terms share one), image hash, byte values.
+    // Not for the library's own OR-Set namespaces (trusted, with tokens): their payloads
+    // are OR-Set images only, and the tables cost a term comparison per slot per rebuild
+    const bool gs = !(trusted && toks);
     uint64_t gs_cap = 64;
-    while (gs_cap < 2ull * E) gs_cap <<= 1;
+    while (gs && gs_cap < 2ull * E) gs_cap <<= 1;
     auto al = [](uint64_t x) { return (x + 255ull) & ~255ull; };
-    // G-Set from_binary tables: ranks (equal terms share one), image hash, byte values
-    std::vector<uint32_t> gs_rank(E, 0), gs_byte(256, 0), gs_htab;
-    {
+    std::vector<uint32_t> gs_rank(gs ? E : 0, 0), gs_byte(256, 0), gs_htab;
+    if (gs) {
         uint32_t rk = 0;
         for (uint32_t k = 0; k < E; ++k) {
             const uint32_t e = elem_order[k];
@@ -5784,7 +5791,7 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     // integer elements by value (minimal images: SMALL_INTEGER for 0..255, INTEGER past it)
     std::vector<uint64_t> gs_itab;
     int64_t ilo = 0;
-    {
+    if (gs) {
         int64_t lo = INT64_MAX, hi = INT64_MIN;
         uint64_t cnt = 0;
         auto int_of = [&](uint32_t e, int64_t* v) {
@@ -5830,8 +5837,8 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
                    o_hpad = o_rpad + al(rpad.size()), o_hpoff = o_hpad + al(hpad.size()),
                    o_rd = o_hpoff + al(4ull * hpoff.size() + 4),
                    o_htab = o_rd + al(rd.size() + 8), o_gsh = o_htab + al(4ull * htab.size() + 4),
-                   o_gsr = o_gsh + al(4ull * gs_cap), o_gsb = o_gsr + al(4ull * E),
-                   o_gsi = o_gsb + al(4ull * 256), bytes = o_gsi + al(8ull * gs_itab.size() + 8);
+                   o_gsr = o_gsh + al(4ull * gs_cap), o_gsb = o_gsr + al(4ull * (gs ? E : 0)),
+                   o_gsi = o_gsb + al(4ull * (gs ? 256 : 0)), bytes = o_gsi + al(8ull * gs_itab.size() + 8);
     auto* d = new (std::nothrow) laspj_etf_dict;
     if (!d) return fail(ctx, LASPJ_E_NOMEM, "etf_dict_create: host allocation");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -5890,9 +5897,9 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
     if (e == hipSuccess && rec_len) e = up(o_hpoff, hpoff.data(), 4ull * hpoff.size());
     if (e == hipSuccess && hashed) e = up(o_rd, rd.data(), rd.size());
     if (e == hipSuccess && hashed) e = up(o_htab, htab.data(), 4ull * htab.size());
-    if (e == hipSuccess) e = up(o_gsh, gs_htab.data(), 4ull * gs_htab.size());
-    if (e == hipSuccess) e = up(o_gsr, gs_rank.data(), 4ull * E);
-    if (e == hipSuccess) e = up(o_gsb, gs_byte.data(), 4ull * 256);
+    if (e == hipSuccess && gs) e = up(o_gsh, gs_htab.data(), 4ull * gs_htab.size());
+    if (e == hipSuccess && gs) e = up(o_gsr, gs_rank.data(), 4ull * E);
+    if (e == hipSuccess && gs) e = up(o_gsb, gs_byte.data(), 4ull * 256);
     if (e == hipSuccess && !gs_itab.empty()) e = up(o_gsi, gs_itab.data(), 8ull * gs_itab.size());
     if (e == hipSuccess) {
         std::sort(spans.begin(), spans.end());
@@ -5932,10 +5939,10 @@ static int etf_dict_create_body(laspj_ctx* ctx, uint32_t E, const uint8_t* elem_
         d->rd_hmask = (uint32_t)(htab.size() - 1);
         d->rd_hlens = hlens;
     }
-    d->gs_htab = reinterpret_cast<const uint32_t*>(base + o_gsh);
+    d->gs_htab = gs ? reinterpret_cast<const uint32_t*>(base + o_gsh) : nullptr;
     d->gs_hmask = (uint32_t)(gs_cap - 1);
-    d->gs_rank = reinterpret_cast<const uint32_t*>(base + o_gsr);
-    d->gs_byte = reinterpret_cast<const uint32_t*>(base + o_gsb);
+    d->gs_rank = gs ? reinterpret_cast<const uint32_t*>(base + o_gsr) : nullptr;
+    d->gs_byte = gs ? reinterpret_cast<const uint32_t*>(base + o_gsb) : nullptr;
     d->gs_itab = gs_itab.empty() ? nullptr : reinterpret_cast<const uint64_t*>(base + o_gsi);
     d->gs_ilo = ilo;
     d->gs_in = (uint32_t)gs_itab.size();
