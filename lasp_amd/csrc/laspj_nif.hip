@@ -137,6 +137,10 @@ struct NifState {
     std::mutex qmu;
     std::vector<BindReq*> queue;
     bool leading = false;
+    // rebuild_etf's export arrays, kept between rebuilds (S->mu): fresh multi-MB blocks
+    // would be paged in again by every rebuild
+    std::vector<uint8_t> x_ebl, x_tbl, x_tord;
+    std::vector<uint32_t> x_eoff, x_eord, x_toff;
     std::vector<PinSlot> pins;      // free waiters' staging blocks (qmu)
     uint32_t pins_live = 0;         // blocks allocated (qmu)
     KindState ks[2];                // the image calls' dictionaries: [0] OR-Set, [1] G-Set
@@ -611,24 +615,27 @@ int rebuild_etf(laspj_ctx* ctx, NifState* S, KindState& K) {
     uint32_t E = K.E;
     if (!K.etf || n > E) E = n + n / 4 + 64;
     const bool toks = K.kind == LASPJ_KIND_ORSET;
-    // (uninitialised: the export writes every entry, and zeroing 64 token slots per
-    // element cost as much as the export itself)
-    std::unique_ptr<uint8_t[]> ebl(new uint8_t[eb + 1]), tbl(new uint8_t[toks ? tb + 1 : 1]),
-        tord(new uint8_t[toks ? 64ull * E : 1]);
-    std::unique_ptr<uint32_t[]> eoff(new uint32_t[E + 1ull]), eord(new uint32_t[E]),
-        toff(new uint32_t[toks ? 64ull * E + 1 : 1]);
-    if (laspj_dict_export(K.dict, E, ebl.get(), eoff.get(), eord.get(),
-                          toks ? tbl.get() : nullptr, toks ? toff.get() : nullptr,
-                          toks ? tord.get() : nullptr) != LASPJ_OK)
+    // (the context's arrays, grown only: the export writes every entry it hands on)
+    auto fit = [](auto& v, uint64_t n) {
+        if (v.size() < n) v.resize(n + n / 4);
+        return v.data();
+    };
+    uint8_t* ebl = fit(S->x_ebl, eb + 1);
+    uint8_t* tbl = fit(S->x_tbl, toks ? tb + 1 : 1);
+    uint8_t* tord = fit(S->x_tord, toks ? 64ull * E : 1);
+    uint32_t* eoff = fit(S->x_eoff, E + 1ull);
+    uint32_t* eord = fit(S->x_eord, E);
+    uint32_t* toff = fit(S->x_toff, toks ? 64ull * E + 1 : 1);
+    if (laspj_dict_export(K.dict, E, ebl, eoff, eord, toks ? tbl : nullptr,
+                          toks ? toff : nullptr, toks ? tord : nullptr) != LASPJ_OK)
         return fail(ctx, LASPJ_E_INVAL, "nif: dictionary export");
     free_etf(K);
     laspj_etf_dict* d = nullptr;
     // OR-Sets: two tokens of headroom per element, so a call that only adds tokens to
     // known elements patches the images (patch_etf) instead of coming back here
-    if (int s = toks ? etf_dict_create_ex(ctx, E, ebl.get(), eoff.get(), eord.get(),
-                                          tbl.get(), toff.get(), tord.get(), 2, &d)
-                     : laspj_etf_dict_create(ctx, E, ebl.get(), eoff.get(), eord.get(),
-                                             nullptr, nullptr, nullptr, &d))
+    if (int s = toks ? etf_dict_create_ex(ctx, E, ebl, eoff, eord, tbl, toff, tord, 2, &d)
+                     : laspj_etf_dict_create(ctx, E, ebl, eoff, eord, nullptr, nullptr,
+                                             nullptr, &d))
         return s;
     K.etf = d;
     K.E = E;
