@@ -933,7 +933,10 @@ int laspj_var_destroy(laspj_var* var);
 /* bind/3 (lasp_core.erl:291-312): status LASPJ_BIND_NOOP when `Value0 =:= Value`
  * (:294-296), LASPJ_BIND_WRITTEN when Value0 := merge(Value0, Value) was written (a
  * canonical merge always inflates Value0, :300-304).  verdict FALLBACK: the variable is
- * unchanged and the NIF binds in Erlang (as above). */
+ * unchanged and the NIF binds in Erlang (as above).  Calls arriving on one context while a
+ * device pass runs are served together by the next pass (group commit, as bind_many);
+ * while it waits, a caller copies its own image (64 KiB or more) into a pinned block the
+ * pass gathers from, so `value` must stay valid until the call returns, as always. */
 int laspj_var_etf_bind(laspj_var* var, const uint8_t* value, uint64_t n, int32_t* status,
                        int32_t* verdict);
 /* n binds (lasp_core.erl:291-312) of distinct variables of one kind and context in one
